@@ -1,0 +1,802 @@
+// ORB extraction kernels for gfx950 (CDNA4): the MI355X-native replacement of
+// ORB_SLAM2::ORBextractor::operator() (src/ORBextractor.cc:1043-1105).
+//
+// Pipeline per batch of frames (all kernels take the frame index from
+// blockIdx.y/z, so one launch covers the whole batch):
+//   k_pyr_level0 / k_pyr_level : ComputePyramid  (ORBextractor.cc:1107-1132)
+//   k_blur                     : GaussianBlur 7x7 s=2 per level (:1084-1086)
+//   k_fast_cells               : per-cell FAST(20) -> FAST(7) fallback (:789-827)
+//   k_octree                   : DistributeOctTree (:539-763) + border/octave (:837-847)
+//   k_orient_desc              : IC_Angle (:77-104) + computeOrbDescriptor (:108-147)
+//                                + level concatenation and pt *= scale (:1075-1104)
+// Bit-exactness against the CPU oracle relies on integer arithmetic for every
+// image stage and on orbpl_math.h for the two float stages.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "orb_geom.h"
+#include "orbpl_math.h"
+#include "orb_kernels.h"
+
+namespace orbpl {
+
+#include "orb_pattern.inc"
+__constant__ int c_pattern[1024];
+
+__device__ __forceinline__ int reflect101_dev(int p, int len) {
+  // BORDER_REFLECT_101 for |p| < 2*len (always true for the 19 px border on
+  // levels >= 20 px; smaller levels are rejected at create time).
+  if (p < 0) p = -p;
+  if (p >= len) p = 2 * len - 2 - p;
+  return p;
+}
+
+// ---------------------------------------------------------------------------
+// Pyramid level 0: copyMakeBorder(image, 19, REFLECT_101) (ORBextractor.cc:1127)
+// 4 padded pixels per thread, one u32 store.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_pyr_level0(const uint8_t* __restrict__ img, int stride,
+                                                    long long frame_pitch,
+                                                    uint8_t* __restrict__ pyr,
+                                                    const OrbGeom* __restrict__ g) {
+  const LevelGeom& L = g->lv[0];
+  const int f = blockIdx.z;
+  const int px0 = (blockIdx.x * 64 + threadIdx.x) * 4;
+  const int py = blockIdx.y * 4 + threadIdx.y;
+  if (px0 >= L.pw || py >= L.ph) return;
+  const uint8_t* src = img + (long long)f * frame_pitch;
+  const int sy = reflect101_dev(py - kEdge, L.h);
+  const uint8_t* row = src + (long long)sy * stride;
+  uint32_t packed = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    int px = px0 + k;
+    uint32_t v = 0;
+    if (px < L.pw) v = row[reflect101_dev(px - kEdge, L.w)];
+    packed |= v << (8 * k);
+  }
+  uint8_t* dst = pyr + (long long)f * g->pyr_bytes + L.pyr_off + (long long)py * L.pitch + px0;
+  *reinterpret_cast<uint32_t*>(dst) = packed;
+}
+
+// ---------------------------------------------------------------------------
+// Pyramid level l >= 1: resize(level l-1, INTER_LINEAR) in OpenCV's 8U
+// fixed-point form (11-bit coefficients, (S>>4)*beta>>16, +2>>2) followed by
+// copyMakeBorder(REFLECT_101 | ISOLATED): each padded pixel evaluates the
+// resize at its reflected content coordinate, so no separate border pass.
+// rs: xofs[w], alpha[w] (a0 | a1<<16), yofs[h], beta[h] for this level.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_pyr_level(uint8_t* __restrict__ pyr,
+                                                   const OrbGeom* __restrict__ g, int level,
+                                                   const int* __restrict__ rs_all) {
+  const LevelGeom& L = g->lv[level];
+  const LevelGeom& S = g->lv[level - 1];
+  const int f = blockIdx.z;
+  const int px0 = (blockIdx.x * 64 + threadIdx.x) * 4;
+  const int py = blockIdx.y * 4 + threadIdx.y;
+  if (px0 >= L.pw || py >= L.ph) return;
+  const int* rs = rs_all + L.rs_off;
+  const int* xofs = rs;
+  const int* alpha = rs + L.w;
+  const int* yofs = rs + 2 * L.w;
+  const int* beta = rs + 2 * L.w + L.h;
+  uint8_t* fp = pyr + (long long)f * g->pyr_bytes;
+  const uint8_t* sbase = fp + S.pyr_off + (long long)kEdge * S.pitch + kEdge;
+  const int cy = reflect101_dev(py - kEdge, L.h);
+  const int sy0 = yofs[cy];
+  const int ya = min(max(sy0, 0), S.h - 1);
+  const int yb = min(max(sy0 + 1, 0), S.h - 1);
+  const int bpk = beta[cy];
+  const int b0 = (int)(short)(bpk & 0xFFFF), b1 = (int)(short)(bpk >> 16);
+  const uint8_t* r0 = sbase + (long long)ya * S.pitch;
+  const uint8_t* r1 = sbase + (long long)yb * S.pitch;
+  uint32_t packed = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    int px = px0 + k;
+    uint32_t v = 0;
+    if (px < L.pw) {
+      int cx = reflect101_dev(px - kEdge, L.w);
+      int sx = xofs[cx];
+      int h0, h1;
+      if (cx < L.xmax) {
+        int apk = alpha[cx];
+        int a0 = (int)(short)(apk & 0xFFFF), a1 = (int)(short)(apk >> 16);
+        h0 = r0[sx] * a0 + r0[sx + 1] * a1;
+        h1 = r1[sx] * a0 + r1[sx + 1] * a1;
+      } else {
+        h0 = r0[sx] * 2048;
+        h1 = r1[sx] * 2048;
+      }
+      v = (uint32_t)((((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2);
+    }
+    packed |= v << (8 * k);
+  }
+  uint8_t* dst = fp + L.pyr_off + (long long)py * L.pitch + px0;
+  *reinterpret_cast<uint32_t*>(dst) = packed;
+}
+
+// ---------------------------------------------------------------------------
+// GaussianBlur(7x7, sigma 2, REFLECT_101), 8U fixed-point path (pinned P4):
+// out = (sum_v kv * sum_u ku * I + 2^15) >> 16 with k = {18,34,49,54,49,34,18}.
+// The padded pyramid already holds the REFLECT_101 border, so a 64x16 output
+// tile reads a 70x22 input tile straight from it. One launch covers every
+// level of every frame (tile list in the geometry).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_blur(const uint8_t* __restrict__ pyr,
+                                              uint8_t* __restrict__ blur,
+                                              const OrbGeom* __restrict__ g) {
+  __shared__ uint8_t tin[kBlurTileH + 6][kBlurTileW + 8];
+  __shared__ int tmid[kBlurTileH + 6][kBlurTileW];
+  const int f = blockIdx.y;
+  int tile = blockIdx.x;
+  int level = 0;
+  while (level + 1 < g->nlevels && tile >= g->lv[level + 1].blur_tile_base) level++;
+  const LevelGeom& L = g->lv[level];
+  tile -= L.blur_tile_base;
+  const int tx = tile % L.blur_tiles_x, ty = tile / L.blur_tiles_x;
+  const int ox = tx * kBlurTileW, oy = ty * kBlurTileH;  // content coords of tile origin
+  const uint8_t* src = pyr + (long long)f * g->pyr_bytes + L.pyr_off;
+  const int t = threadIdx.x;
+  // load (16+6) x (64+6) bytes starting at content (ox-3, oy-3) = padded (ox+16, oy+16)
+  for (int i = t; i < (kBlurTileH + 6) * (kBlurTileW + 6); i += 256) {
+    int r = i / (kBlurTileW + 6), c = i % (kBlurTileW + 6);
+    int px = ox + kEdge - 3 + c, py = oy + kEdge - 3 + r;
+    uint8_t v = 0;
+    if (px < L.pw && py < L.ph) v = src[(long long)py * L.pitch + px];
+    tin[r][c] = v;
+  }
+  __syncthreads();
+  const int k0 = 18, k1 = 34, k2 = 49, k3 = 54;
+  for (int i = t; i < (kBlurTileH + 6) * kBlurTileW; i += 256) {
+    int r = i / kBlurTileW, c = i % kBlurTileW;
+    const uint8_t* p = &tin[r][c];
+    tmid[r][c] = k0 * (p[0] + p[6]) + k1 * (p[1] + p[5]) + k2 * (p[2] + p[4]) + k3 * p[3];
+  }
+  __syncthreads();
+  uint8_t* dst = blur + (long long)f * g->pyr_bytes + L.pyr_off;
+  for (int i = t; i < kBlurTileH * kBlurTileW; i += 256) {
+    int r = i / kBlurTileW, c = i % kBlurTileW;
+    int x = ox + c, y = oy + r;
+    if (x >= L.w || y >= L.h) continue;
+    int acc = k0 * (tmid[r][c] + tmid[r + 6][c]) + k1 * (tmid[r + 1][c] + tmid[r + 5][c]) +
+              k2 * (tmid[r + 2][c] + tmid[r + 4][c]) + k3 * tmid[r + 3][c];
+    int v = (acc + (1 << 15)) >> 16;
+    dst[(long long)(y + kEdge) * L.pitch + (x + kEdge)] = (uint8_t)(v > 255 ? 255 : v);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// FAST-9/16 per cell window with per-window 3x3 NMS (cv::FAST semantics on a
+// ROI, features2d/fast.cpp FAST_t<16> + cornerScore<16>), threshold
+// iniThFAST then minThFAST if the window produced nothing.
+//
+// For every pixel the kernel computes m = max(A, -B), A/B = max/min over the
+// 16 circular 9-arcs of min/max(v - ring). Then, for any threshold t,
+//   is_corner_t  <=>  m >= t + 1,   cornerScore_t = m - 1,
+// which is exactly what FAST_t emits (see DESIGN.md for the derivation).
+// One wave per window, 4 windows per 256-thread block. Candidates are
+// written in the reference's row-major emission order into the window's slot.
+// ---------------------------------------------------------------------------
+constexpr int kFastMaxWin = 66;  // window edge <= wcell + 6 <= 65
+
+__device__ __forceinline__ int fast_m(const uint8_t* w, int ws, int x, int y) {
+  const uint8_t* c = w + y * ws + x;
+  const int v = c[0];
+  int d[16];
+  d[0] = v - c[3 * ws];
+  d[1] = v - c[3 * ws + 1];
+  d[2] = v - c[2 * ws + 2];
+  d[3] = v - c[ws + 3];
+  d[4] = v - c[3];
+  d[5] = v - c[-ws + 3];
+  d[6] = v - c[-2 * ws + 2];
+  d[7] = v - c[-3 * ws + 1];
+  d[8] = v - c[-3 * ws];
+  d[9] = v - c[-3 * ws - 1];
+  d[10] = v - c[-2 * ws - 2];
+  d[11] = v - c[-ws - 3];
+  d[12] = v - c[-3];
+  d[13] = v - c[ws - 3];
+  d[14] = v - c[2 * ws - 2];
+  d[15] = v - c[3 * ws - 1];
+  int mn2[16], mx2[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    mn2[k] = min(d[k], d[(k + 1) & 15]);
+    mx2[k] = max(d[k], d[(k + 1) & 15]);
+  }
+  int mn4[16], mx4[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    mn4[k] = min(mn2[k], mn2[(k + 2) & 15]);
+    mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
+  }
+  int A = -1024, B = 1024;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    int mn8 = min(mn4[k], mn4[(k + 4) & 15]);
+    int mx8 = max(mx4[k], mx4[(k + 4) & 15]);
+    A = max(A, min(mn8, d[(k + 8) & 15]));
+    B = min(B, max(mx8, d[(k + 8) & 15]));
+  }
+  return max(A, -B);
+}
+
+__global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ pyr,
+                                                    const OrbGeom* __restrict__ g,
+                                                    const CellGeom* __restrict__ cells,
+                                                    uint32_t* __restrict__ cell_cands,
+                                                    int* __restrict__ cell_counts, int ini_th,
+                                                    int min_th) {
+  __shared__ uint8_t s_img[4][kFastMaxWin * kFastMaxWin];
+  __shared__ uint8_t s_m[4][kFastMaxWin * kFastMaxWin];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int f = blockIdx.y;
+  const int cell = blockIdx.x * 4 + wave;
+  if (cell >= g->ncells_total) return;
+  const CellGeom cg = cells[cell];
+  const int slots = g->cell_slots;
+  int* cnt_out = cell_counts + (long long)f * g->ncells_total + cell;
+  if (cg.x1 == 0) {  // skipped cell (ORBextractor.cc:794-804)
+    if (lane == 0) *cnt_out = 0;
+    return;
+  }
+  const LevelGeom& L = g->lv[cg.level];
+  const int cols = cg.x1 - cg.x0, rows = cg.y1 - cg.y0;
+  const uint8_t* src = pyr + (long long)f * g->pyr_bytes + L.pyr_off +
+                       (long long)(cg.y0 + kEdge) * L.pitch + (cg.x0 + kEdge);
+  uint8_t* wimg = s_img[wave];
+  uint8_t* wm = s_m[wave];
+  const int ws = cols;  // LDS window stride
+  for (int i = lane; i < rows * cols; i += 64) {
+    int r = i / cols, c = i - r * cols;
+    wimg[i] = src[(long long)r * L.pitch + c];
+    wm[i] = 0;
+  }
+  __builtin_amdgcn_wave_barrier();
+  // detection region: rows [3, rows-4], cols [3, cols-4]
+  const int dr = rows - 6, dc = cols - 6;
+  const int ndet = (dr > 0 && dc > 0) ? dr * dc : 0;
+  for (int i = lane; i < ndet; i += 64) {
+    int r = i / dc, c = i - r * dc;
+    int m = fast_m(wimg, ws, c + 3, r + 3);
+    wm[(r + 3) * ws + (c + 3)] = (uint8_t)(m < 0 ? 0 : (m > 255 ? 255 : m));
+  }
+  __builtin_amdgcn_wave_barrier();
+  // NMS test at threshold t for detection pixel i (0 <= i < ndet)
+  auto nms_score = [&](int i, int t) -> int {
+    int r = i / dc, c = i - r * dc;
+    const uint8_t* p = wm + (r + 3) * ws + (c + 3);
+    int m = p[0];
+    if (m < t + 1) return -1;
+    int s = m - 1;
+    auto nb = [&](int mm) { return mm >= t + 1 ? mm - 1 : 0; };
+    // wm is zero outside the detection region, which nb() maps to 0
+    if (s > nb(p[1]) && s > nb(p[-1]) && s > nb(p[-ws - 1]) && s > nb(p[-ws]) &&
+        s > nb(p[-ws + 1]) && s > nb(p[ws - 1]) && s > nb(p[ws]) && s > nb(p[ws + 1]))
+      return s;
+    return -1;
+  };
+  int t = ini_th < 0 ? 0 : (ini_th > 255 ? 255 : ini_th);
+  int found = 0;
+  for (int base = 0; base < ndet && !found; base += 64) {
+    int i = base + lane;
+    bool is = i < ndet && nms_score(i, t) >= 0;
+    found = __ballot(is) != 0ull;
+  }
+  if (!found) t = min_th < 0 ? 0 : (min_th > 255 ? 255 : min_th);
+  uint32_t* out = cell_cands + ((long long)f * g->ncells_total + cell) * slots;
+  const int xoff = cg.x0 - kMinBorder, yoff = cg.y0 - kMinBorder;
+  int n = 0;
+  for (int base = 0; base < ndet; base += 64) {
+    int i = base + lane;
+    int s = i < ndet ? nms_score(i, t) : -1;
+    unsigned long long mask = __ballot(s >= 0);
+    if (s >= 0) {
+      int pos = n + __popcll(mask & ((1ull << lane) - 1ull));
+      int r = i / dc, c = i - r * dc;
+      if (pos < slots) out[pos] = pack_cand(xoff + c + 3, yoff + r + 3, s);
+    }
+    n += __popcll(mask);
+  }
+  if (lane == 0) *cnt_out = n < slots ? n : slots;
+}
+
+// ---------------------------------------------------------------------------
+// Block-wide helpers (256 threads = 4 waves)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int u = __shfl_up(v, o, 64);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+
+// Exclusive scan of vals[0..n) in place (n <= 256*kPer); returns the total.
+template <int kPer>
+__device__ int block_excl_scan(int* vals, int n, int* s_wsum) {
+  const int t = threadIdx.x;
+  int local[kPer];
+  int sum = 0;
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    int i = t * kPer + k;
+    local[k] = i < n ? vals[i] : 0;
+    sum += local[k];
+  }
+  int incl = wave_incl_scan(sum);
+  const int wave = t >> 6, lane = t & 63;
+  if (lane == 63) s_wsum[wave] = incl;
+  __syncthreads();
+  int wofs = 0, total = 0;
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    int s = s_wsum[w];
+    if (w < wave) wofs += s;
+    total += s;
+  }
+  int run = wofs + incl - sum;
+#pragma unroll
+  for (int k = 0; k < kPer; k++) {
+    int i = t * kPer + k;
+    if (i < n) vals[i] = run;
+    run += local[k];
+  }
+  __syncthreads();
+  return total;
+}
+
+// ---------------------------------------------------------------------------
+// DistributeOctTree (ORBextractor.cc:539-763) for one (frame, level).
+//
+// The reference keeps a std::list of nodes and pushes children to the front.
+// Here the list is an array in list order, rebuilt after every pass:
+//   new list = [children of the last processed node (n4..n1 nonempty)] ...
+//              [children of the first processed node] ++ [untouched nodes].
+// Keys (candidates) carry the index of their node; each pass is one sweep to
+// count children (LDS atomics) and one sweep to re-index keys. Phase-2 passes
+// divide nodes in descending (size, creation) order and stop at the first
+// node after which size >= N (prefix sums over the speculative child counts).
+// ---------------------------------------------------------------------------
+struct OctShared {
+  uint2 rect[2][kOctMaxList];       // (x0 | y0<<16, x1 | y1<<16)
+  int cnt[2][kOctMaxList];
+  int rank[kOctMaxList];            // processing rank of a list entry, -1 = untouched
+  int upos[kOctMaxList];            // new position of an untouched entry
+  int child[4 * kOctMaxList];       // child counts, then child positions
+  int exp_pos[kOctMaxList];         // expandable children (creation order): list position
+  int exp_cnt[kOctMaxList];
+  int proc[kOctMaxList];            // processing order -> list position (phase 2)
+  int scan[kOctMaxList];
+  int wsum[8];
+  int misc[8];
+};
+
+__device__ __forceinline__ uint2 mk_rect(int x0, int y0, int x1, int y1) {
+  return make_uint2((uint32_t)x0 | ((uint32_t)y0 << 16), (uint32_t)x1 | ((uint32_t)y1 << 16));
+}
+
+__device__ __forceinline__ int child_of(uint2 r, int x, int y) {
+  int x0 = r.x & 0xFFFF, y0 = r.x >> 16, x1 = r.y & 0xFFFF, y1 = r.y >> 16;
+  int mx = x0 + ((x1 - x0 + 1) >> 1), my = y0 + ((y1 - y0 + 1) >> 1);
+  return x < mx ? (y < my ? 0 : 2) : (y < my ? 1 : 3);
+}
+
+__device__ __forceinline__ uint2 child_rect(uint2 r, int c) {
+  int x0 = r.x & 0xFFFF, y0 = r.x >> 16, x1 = r.y & 0xFFFF, y1 = r.y >> 16;
+  int mx = x0 + ((x1 - x0 + 1) >> 1), my = y0 + ((y1 - y0 + 1) >> 1);
+  switch (c) {
+    case 0: return mk_rect(x0, y0, mx, my);
+    case 1: return mk_rect(mx, y0, x1, my);
+    case 2: return mk_rect(x0, my, mx, y1);
+    default: return mk_rect(mx, my, x1, y1);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
+                                                const uint32_t* __restrict__ cell_cands,
+                                                const int* __restrict__ cell_counts,
+                                                uint32_t* __restrict__ kcand,
+                                                int* __restrict__ knode,
+                                                uint32_t* __restrict__ kp_list,
+                                                int* __restrict__ kp_count,
+                                                int* __restrict__ err_flag) {
+  extern __shared__ char smem_raw[];
+  OctShared& S = *reinterpret_cast<OctShared*>(smem_raw);
+  const int level = blockIdx.x, f = blockIdx.y, t = threadIdx.x;
+  const LevelGeom& L = g->lv[level];
+  const int N = L.nfeat;
+  const int slots = g->cell_slots;
+  int* out_count = kp_count + (long long)f * g->nlevels + level;
+  uint32_t* out_list = kp_list + (long long)f * g->kp_cap_total + L.kp_base;
+  uint32_t* K = kcand + (long long)f * g->cand_cap_total + L.cand_base;
+  int* KN = knode + (long long)f * g->cand_cap_total + L.cand_base;
+
+  // ---- 1. gather candidates in cell order (vToDistributeKeys order) ----
+  const int ncells = L.ncells;
+  const int* ccnt = cell_counts + (long long)f * g->ncells_total + L.cell_base;
+  for (int i = t; i < ncells; i += 256) S.scan[i] = ccnt[i];
+  __syncthreads();
+  const int total = block_excl_scan<4>(S.scan, ncells, S.wsum);
+  if (total == 0) {
+    if (t == 0) *out_count = 0;
+    return;
+  }
+  {
+    const int wave = t >> 6, lane = t & 63;
+    const uint32_t* cc = cell_cands + ((long long)f * g->ncells_total + L.cell_base) * slots;
+    for (int c = wave; c < ncells; c += 4) {
+      int n = ccnt[c], o = S.scan[c];
+      for (int i = lane; i < n; i += 64) K[o + i] = cc[(long long)c * slots + i];
+    }
+  }
+  // ---- 2. initial nodes (ORBextractor.cc:543-585) ----
+  const int nIni = L.n_ini;
+  const float hX = L.hx;
+  const int H = L.max_border_y - kMinBorder;
+  for (int i = t; i < nIni; i += 256) S.child[i] = 0;
+  __syncthreads();
+  for (int k = t; k < total; k += 256) {
+    uint32_t c = K[k];
+    int idx = (int)((float)cand_x(c) / hX);
+    if (idx >= nIni) idx = nIni - 1;
+    KN[k] = idx;
+    atomicAdd(&S.child[idx], 1);
+  }
+  __syncthreads();
+  // list = nonempty initial nodes in order
+  for (int i = t; i < nIni; i += 256) S.scan[i] = S.child[i] > 0 ? 1 : 0;
+  __syncthreads();
+  int size = block_excl_scan<4>(S.scan, nIni, S.wsum);
+  int cur = 0;
+  for (int i = t; i < nIni; i += 256) {
+    if (S.child[i] > 0) {
+      int p = S.scan[i];
+      S.rect[0][p] = mk_rect((int)(hX * (float)i), 0, (int)(hX * (float)(i + 1)), H);
+      S.cnt[0][p] = S.child[i];
+      S.upos[i] = p;
+    }
+  }
+  __syncthreads();
+  for (int k = t; k < total; k += 256) KN[k] = S.upos[KN[k]];
+  // expandable list (for phase 2): empty until a pass creates children
+  int nexp = 0;
+  bool finish = false;
+  bool phase2 = false;
+  __syncthreads();
+
+  while (!finish) {
+    const int prevSize = size;
+    // ---- choose the nodes to divide and their processing rank ----
+    int nproc;  // number of candidate nodes (speculative in phase 2)
+    if (!phase2) {
+      for (int i = t; i < size; i += 256) S.scan[i] = S.cnt[cur][i] > 1 ? 1 : 0;
+      __syncthreads();
+      nproc = block_excl_scan<4>(S.scan, size, S.wsum);
+      for (int i = t; i < size; i += 256) {
+        bool d = S.cnt[cur][i] > 1;
+        S.rank[i] = d ? S.scan[i] : -1;
+        if (d) S.proc[S.scan[i]] = i;
+      }
+    } else {
+      // sort expandable nodes by (count, seq) descending; seq = creation index
+      nproc = nexp;
+      for (int i = t; i < size; i += 256) S.rank[i] = -1;
+      __syncthreads();
+      for (int i = t; i < nexp; i += 256) {
+        int ci = S.exp_cnt[i];
+        int r = 0;
+        for (int j = 0; j < nexp; j++) {
+          int cj = S.exp_cnt[j];
+          r += (cj > ci) || (cj == ci && j > i);
+        }
+        S.proc[r] = S.exp_pos[i];
+        S.rank[S.exp_pos[i]] = r;
+      }
+    }
+    __syncthreads();
+    if (nproc == 0) break;  // nothing divisible: size == prevSize -> finish
+    if (4 * nproc > 4 * kOctMaxList) {
+      if (t == 0) atomicOr(err_flag, 1);
+      break;
+    }
+    for (int i = t; i < 4 * nproc; i += 256) S.child[i] = 0;
+    __syncthreads();
+    // ---- sweep 1: child counts ----
+    for (int k = t; k < total; k += 256) {
+      int e = KN[k];
+      int r = S.rank[e];
+      if (r >= 0) {
+        uint32_t c = K[k];
+        atomicAdd(&S.child[4 * r + child_of(S.rect[cur][e], cand_x(c), cand_y(c))], 1);
+      }
+    }
+    __syncthreads();
+    // nonempty children per processed node
+    for (int r = t; r < nproc; r += 256) {
+      int ne = (S.child[4 * r] > 0) + (S.child[4 * r + 1] > 0) + (S.child[4 * r + 2] > 0) +
+               (S.child[4 * r + 3] > 0);
+      S.scan[r] = ne;
+    }
+    __syncthreads();
+    int nchild_all = block_excl_scan<4>(S.scan, nproc, S.wsum);  // S.scan = prefix (excl)
+    int kproc = nproc;
+    if (phase2) {
+      // first r with prevSize + sum_{q<=r}(ne_q - 1) >= N
+      if (t == 0) S.misc[0] = nproc;
+      __syncthreads();
+      for (int r = t; r < nproc; r += 256) {
+        int ne = (r + 1 < nproc ? S.scan[r + 1] : nchild_all) - S.scan[r];
+        int sz = prevSize + (S.scan[r] + ne) - (r + 1);
+        if (sz >= N) atomicMin(&S.misc[0], r + 1);
+      }
+      __syncthreads();
+      kproc = S.misc[0];
+      for (int i = t; i < size; i += 256)
+        if (S.rank[i] >= kproc) S.rank[i] = -1;
+      __syncthreads();
+    }
+    const int nchild = kproc < nproc ? S.scan[kproc] : nchild_all;
+    // ---- new positions: children blocks in reverse processing order ----
+    const int nxt = cur ^ 1;
+    for (int r = t; r < kproc; r += 256) {
+      const int pre = S.scan[r];
+      const int ne = (r + 1 < nproc ? S.scan[r + 1] : nchild_all) - pre;
+      const int off = nchild - pre - ne;
+      const int e = S.proc[r];
+      const uint2 pr = S.rect[cur][e];
+      int above = 0;  // nonempty children with larger index come first (n4..n1)
+      for (int c = 3; c >= 0; c--) {
+        int cc = S.child[4 * r + c];
+        if (cc > 0) {
+          int p = off + above;
+          above++;
+          S.rect[nxt][p] = child_rect(pr, c);
+          S.cnt[nxt][p] = cc;
+          S.child[4 * r + c] = p;  // now: position
+        } else {
+          S.child[4 * r + c] = -1;
+        }
+      }
+    }
+    // untouched entries keep relative order after the children
+    for (int i = t; i < size; i += 256) S.upos[i] = S.rank[i] < 0 ? 1 : 0;
+    __syncthreads();
+    const int nunt = block_excl_scan<4>(S.upos, size, S.wsum);
+    for (int i = t; i < size; i += 256) {
+      if (S.rank[i] < 0) {
+        int p = nchild + S.upos[i];
+        S.rect[nxt][p] = S.rect[cur][i];
+        S.cnt[nxt][p] = S.cnt[cur][i];
+        S.upos[i] = p;
+      }
+    }
+    const int newSize = nchild + nunt;
+    if (newSize > kOctMaxList) {
+      if (t == 0) atomicOr(err_flag, 2);
+      break;
+    }
+    __syncthreads();
+    // ---- sweep 2: re-index keys ----
+    for (int k = t; k < total; k += 256) {
+      int e = KN[k];
+      int r = S.rank[e];
+      int ne;
+      if (r >= 0) {
+        uint32_t c = K[k];
+        ne = S.child[4 * r + child_of(S.rect[cur][e], cand_x(c), cand_y(c))];
+      } else {
+        ne = S.upos[e];
+      }
+      KN[k] = ne;
+    }
+    // ---- expandable children in creation order (rank asc, child asc) ----
+    for (int r = t; r < kproc; r += 256) {
+      int ne = 0;
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        int p = S.child[4 * r + c];
+        ne += (p >= 0 && S.cnt[nxt][p] > 1) ? 1 : 0;
+      }
+      S.scan[r] = ne;
+    }
+    __syncthreads();
+    nexp = block_excl_scan<4>(S.scan, kproc, S.wsum);
+    for (int r = t; r < kproc; r += 256) {
+      int o = S.scan[r];
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        int p = S.child[4 * r + c];
+        if (p >= 0 && S.cnt[nxt][p] > 1) {
+          S.exp_pos[o] = p;
+          S.exp_cnt[o] = S.cnt[nxt][p];
+          o++;
+        }
+      }
+    }
+    __syncthreads();
+    cur = nxt;
+    size = newSize;
+    if (size >= N || size == prevSize) {
+      finish = true;
+    } else if (!phase2 && size + nexp * 3 > N) {
+      phase2 = true;
+    }
+  }
+  // ---- retain the best key per node (strict >, first in candidate order) ----
+  for (int i = t; i < size; i += 256) S.child[i] = 0;
+  __syncthreads();
+  for (int k = t; k < total; k += 256) {
+    uint32_t c = K[k];
+    int key = (cand_s(c) << 20) | (kMaxCandPerLevel - k);
+    atomicMax(&S.child[KN[k]], key);
+  }
+  __syncthreads();
+  const int cap = L.kp_cap;
+  for (int i = t; i < size && i < cap; i += 256) {
+    int k = kMaxCandPerLevel - (S.child[i] & kMaxCandPerLevel);
+    out_list[i] = K[k];
+  }
+  if (t == 0) {
+    if (size > cap) atomicOr(err_flag, 4);
+    *out_count = size < cap ? size : cap;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Orientation + descriptor + output, one wave per keypoint slot.
+// IC_Angle on the unblurred level, computeOrbDescriptor on the blurred level,
+// output rows ordered level by level (ORBextractor.cc:1075-1104).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__ pyr,
+                                                     const uint8_t* __restrict__ blur,
+                                                     const OrbGeom* __restrict__ g,
+                                                     const uint32_t* __restrict__ kp_list,
+                                                     const int* __restrict__ kp_count,
+                                                     orbpl_keypoint_dev* __restrict__ out_kps,
+                                                     uint8_t* __restrict__ out_desc,
+                                                     int kp_pitch, int* __restrict__ out_n) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int f = blockIdx.y;
+  const int slot = blockIdx.x * 4 + wave;
+  if (slot >= g->kp_cap_total) return;
+  int level = 0;
+  while (level + 1 < g->nlevels && slot >= g->lv[level + 1].kp_base) level++;
+  const LevelGeom& L = g->lv[level];
+  const int idx = slot - L.kp_base;
+  const int* cnts = kp_count + (long long)f * g->nlevels;
+  int offset = 0, total = 0;
+  for (int l = 0; l < g->nlevels; l++) {
+    int c = cnts[l];
+    if (l < level) offset += c;
+    total += c;
+  }
+  if (slot == 0 && lane == 0) out_n[f] = total < kp_pitch ? total : kp_pitch;
+  if (idx >= cnts[level]) return;
+  const int opos = offset + idx;
+  if (opos >= kp_pitch) return;
+  const uint32_t c = kp_list[(long long)f * g->kp_cap_total + slot];
+  const int kx = cand_x(c) + kMinBorder, ky = cand_y(c) + kMinBorder;
+  // --- IC_Angle: lane u+15 sums column u over the disc ---
+  const uint8_t* img = pyr + (long long)f * g->pyr_bytes + L.pyr_off +
+                       (long long)(ky + kEdge) * L.pitch + (kx + kEdge);
+  int m01 = 0, m10 = 0;
+  if (lane < 31) {
+    const int u = lane - 15;
+    const int au = u < 0 ? -u : u;
+    for (int v = -15; v <= 15; v++) {
+      const int av = v < 0 ? -v : v;
+      if (au <= g->umax[av]) {
+        int val = img[(long long)v * L.pitch + u];
+        m10 += u * val;
+        m01 += v * val;
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    m10 += __shfl_xor(m10, o, 64);
+    m01 += __shfl_xor(m01, o, 64);
+  }
+  const float angle = fast_atan2_deg((float)m01, (float)m10);
+  // --- steered BRIEF on the blurred level ---
+  const float factorPI = (float)(3.14159265358979323846 / 180.f);
+  float a, b;
+  cr_cos_sin(angle * factorPI, &a, &b);
+  const uint8_t* bimg = blur + (long long)f * g->pyr_bytes + L.pyr_off +
+                        (long long)(ky + kEdge) * L.pitch + (kx + kEdge);
+  const int step = L.pitch;
+  uint64_t words[4];
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int tst = r * 64 + lane;
+    const int* p = &c_pattern[4 * tst];
+    const float x1 = (float)p[0], y1 = (float)p[1], x2 = (float)p[2], y2 = (float)p[3];
+    const int v1 = bimg[cv_round(x1 * b + y1 * a) * step + cv_round(x1 * a - y1 * b)];
+    const int v2 = bimg[cv_round(x2 * b + y2 * a) * step + cv_round(x2 * a - y2 * b)];
+    words[r] = __ballot(v1 < v2);
+  }
+  uint8_t* d = out_desc + ((long long)f * kp_pitch + opos) * 32;
+  if (lane < 4) {
+    uint64_t w = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
+    reinterpret_cast<uint64_t*>(d)[lane] = w;
+  }
+  if (lane == 0) {
+    orbpl_keypoint_dev kp;
+    float sx = (float)kx, sy = (float)ky;
+    if (level != 0) {
+      sx = sx * L.scale;
+      sy = sy * L.scale;
+    }
+    kp.x = sx;
+    kp.y = sy;
+    kp.size = (float)L.scaled_patch;
+    kp.angle = angle;
+    kp.response = (float)cand_s(c);
+    kp.octave = level;
+    kp.class_id = -1;
+    out_kps[(long long)f * kp_pitch + opos] = kp;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Host-side launchers (called by the runtime in orbpl_runtime.cpp)
+// ---------------------------------------------------------------------------
+hipError_t upload_pattern(hipStream_t s) {
+  return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_pattern), bit_pattern_31_, sizeof(bit_pattern_31_), 0,
+                                hipMemcpyHostToDevice, s);
+}
+
+size_t octree_smem_bytes() { return sizeof(OctShared); }
+
+void launch_pyramid(const OrbGeom& hg, const OrbGeom* dg, const uint8_t* img, int stride,
+                    long long frame_pitch, uint8_t* pyr, const int* rs, int batch, hipStream_t s) {
+  for (int l = 0; l < hg.nlevels; l++) {
+    const LevelGeom& L = hg.lv[l];
+    dim3 block(64, 4);
+    dim3 grid((L.pw + 255) / 256, (L.ph + 3) / 4, batch);
+    if (l == 0)
+      hipLaunchKernelGGL(k_pyr_level0, grid, block, 0, s, img, stride, frame_pitch, pyr, dg);
+    else
+      hipLaunchKernelGGL(k_pyr_level, grid, block, 0, s, pyr, dg, l, rs);
+  }
+}
+
+void launch_blur(const OrbGeom& hg, const OrbGeom* dg, const uint8_t* pyr, uint8_t* blur, int batch,
+                 hipStream_t s) {
+  hipLaunchKernelGGL(k_blur, dim3(hg.blur_tiles_total, batch), dim3(256), 0, s, pyr, blur, dg);
+}
+
+void launch_fast(const OrbGeom& hg, const OrbGeom* dg, const CellGeom* cells, const uint8_t* pyr,
+                 uint32_t* cell_cands, int* cell_counts, int ini_th, int min_th, int batch,
+                 hipStream_t s) {
+  hipLaunchKernelGGL(k_fast_cells, dim3((hg.ncells_total + 3) / 4, batch), dim3(256), 0, s, pyr, dg,
+                     cells, cell_cands, cell_counts, ini_th, min_th);
+}
+
+void launch_octree(const OrbGeom& hg, const OrbGeom* dg, const uint32_t* cell_cands,
+                   const int* cell_counts, uint32_t* kcand, int* knode, uint32_t* kp_list,
+                   int* kp_count, int* err_flag, int batch, hipStream_t s) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)sizeof(OctShared));
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(k_octree, dim3(hg.nlevels, batch), dim3(256), sizeof(OctShared), s, dg,
+                     cell_cands, cell_counts, kcand, knode, kp_list, kp_count, err_flag);
+}
+
+void launch_orient_desc(const OrbGeom& hg, const OrbGeom* dg, const uint8_t* pyr,
+                        const uint8_t* blur, const uint32_t* kp_list, const int* kp_count,
+                        orbpl_keypoint_dev* out_kps, uint8_t* out_desc, int kp_pitch, int* out_n,
+                        int batch, hipStream_t s) {
+  hipLaunchKernelGGL(k_orient_desc, dim3((hg.kp_cap_total + 3) / 4, batch), dim3(256), 0, s, pyr,
+                     blur, dg, kp_list, kp_count, out_kps, out_desc, kp_pitch, out_n);
+}
+
+}  // namespace orbpl

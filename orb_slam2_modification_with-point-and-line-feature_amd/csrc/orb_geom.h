@@ -1,0 +1,73 @@
+// Geometry shared by the host runtime and the ORB kernels. Computed once per
+// extractor configuration on the host (orb_geom.cpp) with the reference's
+// formulas (ORBextractor.cc:410-470, 765-847, 1107-1132) and uploaded.
+#pragma once
+#include <stdint.h>
+
+namespace orbpl {
+
+constexpr int kMaxLevels = 16;
+constexpr int kEdge = 19;          // EDGE_THRESHOLD (ORBextractor.cc:74)
+constexpr int kMinBorder = 16;     // EDGE_THRESHOLD - 3 (ORBextractor.cc:773)
+constexpr int kOctMaxList = 1024;  // octree list capacity per (frame, level)
+constexpr int kMaxCandPerLevel = (1 << 20) - 1;
+
+struct LevelGeom {
+  int w, h;            // content size
+  int pw, ph;          // padded size (w + 38, h + 38)
+  int pitch;           // padded row pitch in bytes (multiple of 16)
+  int pad0;
+  long long pyr_off;   // byte offset of the padded level inside one frame's pyramid
+  float scale;         // mvScaleFactor[level]
+  int nfeat;           // mnFeaturesPerLevel[level]
+  int ncols, nrows;    // FAST cell grid (ORBextractor.cc:784-785)
+  int wcell, hcell;    // cell size (ORBextractor.cc:786-787)
+  int cell_base;       // first cell index of this level in the frame's cell array
+  int ncells;          // ncols * nrows
+  int max_border_x, max_border_y;  // cols-16, rows-16 (ORBextractor.cc:775-776)
+  int n_ini;           // DistributeOctTree initial nodes (ORBextractor.cc:543)
+  float hx;            // initial node width (ORBextractor.cc:545)
+  int kp_cap;          // keypoint list capacity for this level
+  int kp_base;         // offset of this level's list in the frame's list array
+  int cand_base;       // offset in the frame's compacted-candidate scratch
+  int cand_cap;        // ncells * cell_slots
+  int rs_off;          // offset of the resize tables (levels >= 1) in ints
+  int xmax;            // first dx whose sx + 1 >= src width (OpenCV resize)
+  int scaled_patch;    // (int)(PATCH_SIZE * scale)  (ORBextractor.cc:837)
+  int blur_tile_base;  // first blur tile of this level
+  int blur_tiles_x, blur_tiles_y;
+};
+
+// One FAST window (ORBextractor.cc:789-806): [x0,x1) x [y0,y1) in level
+// content coordinates; level index; x1 == 0 marks a skipped cell.
+struct CellGeom {
+  int16_t x0, y0, x1, y1;
+  int16_t level, pad;
+};
+
+struct OrbGeom {
+  int nlevels;
+  int W, H;
+  int ncells_total;
+  int kp_cap_total;    // sum of kp_cap (per-frame list array size)
+  int cand_cap_total;  // sum of cand_cap
+  int blur_tiles_total;
+  int cell_slots;      // max corners a FAST window can emit: ceil(dw/2)*ceil(dh/2)
+  long long pyr_bytes; // bytes of one frame's padded pyramid
+  int umax[16];        // IC_Angle circular patch row extents (ORBextractor.cc:454-469)
+  LevelGeom lv[kMaxLevels];
+};
+
+constexpr int kBlurTileW = 64;
+constexpr int kBlurTileH = 16;
+
+// Candidate packing: x (12 bits) | y (12 bits) << 12 | score (8 bits) << 24,
+// coordinates relative to minBorder (the reference's vToDistributeKeys frame).
+__host__ __device__ inline uint32_t pack_cand(int x, int y, int s) {
+  return (uint32_t)x | ((uint32_t)y << 12) | ((uint32_t)s << 24);
+}
+__host__ __device__ inline int cand_x(uint32_t c) { return (int)(c & 0xFFF); }
+__host__ __device__ inline int cand_y(uint32_t c) { return (int)((c >> 12) & 0xFFF); }
+__host__ __device__ inline int cand_s(uint32_t c) { return (int)(c >> 24); }
+
+}  // namespace orbpl

@@ -1,0 +1,47 @@
+// Kernel launchers of the ORB extraction pipeline (orb_extract.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "orb_geom.h"
+
+namespace orbpl {
+
+// Device-side mirror of orbpl_keypoint / cv::KeyPoint (28 bytes).
+struct orbpl_keypoint_dev {
+  float x, y, size, angle, response;
+  int octave, class_id;
+};
+
+hipError_t upload_pattern(hipStream_t s);
+size_t octree_smem_bytes();
+
+void launch_pyramid(const OrbGeom& hg, const OrbGeom* dg, const uint8_t* img, int stride,
+                    long long frame_pitch, uint8_t* pyr, const int* rs, int batch, hipStream_t s);
+void launch_blur(const OrbGeom& hg, const OrbGeom* dg, const uint8_t* pyr, uint8_t* blur, int batch,
+                 hipStream_t s);
+void launch_fast(const OrbGeom& hg, const OrbGeom* dg, const CellGeom* cells, const uint8_t* pyr,
+                 uint32_t* cell_cands, int* cell_counts, int ini_th, int min_th, int batch,
+                 hipStream_t s);
+void launch_octree(const OrbGeom& hg, const OrbGeom* dg, const uint32_t* cell_cands,
+                   const int* cell_counts, uint32_t* kcand, int* knode, uint32_t* kp_list,
+                   int* kp_count, int* err_flag, int batch, hipStream_t s);
+void launch_orient_desc(const OrbGeom& hg, const OrbGeom* dg, const uint8_t* pyr,
+                        const uint8_t* blur, const uint32_t* kp_list, const int* kp_count,
+                        orbpl_keypoint_dev* out_kps, uint8_t* out_desc, int kp_pitch, int* out_n,
+                        int batch, hipStream_t s);
+
+// Host geometry (orb_geom.cpp). Returns 0 or an ORBPL_ERR_* code with a
+// message in *err.
+struct OrbHostGeom {
+  OrbGeom g;
+  std::vector<CellGeom> cells;
+  std::vector<int> rs;           // resize tables for all levels >= 1
+  std::vector<float> scale, inv_scale, sigma2, inv_sigma2;
+};
+int build_orb_geometry(int nfeatures, float scale_factor, int nlevels, int W, int H,
+                       OrbHostGeom* out, const char** err);
+
+}  // namespace orbpl

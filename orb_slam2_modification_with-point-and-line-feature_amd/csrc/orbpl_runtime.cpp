@@ -1,0 +1,392 @@
+// Host runtime and C-ABI (include/orbpl.h) of the ORB extraction path.
+// One orbx_ctx = one device + one HIP stream + device buffers sized for
+// max_batch frames of one image geometry.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/orbpl.h"
+#include "orb_kernels.h"
+#include "orbpl_runtime.h"
+
+namespace orbpl {
+
+static thread_local std::string g_last_error;
+
+void set_error(const char* fmt, const char* a, int line) {
+  char buf[512];
+  snprintf(buf, sizeof(buf), fmt, a, line);
+  g_last_error = buf;
+}
+
+int hip_fail(hipError_t e, const char* what, int line) {
+  char buf[512];
+  snprintf(buf, sizeof(buf), "%s failed (line %d): %s", what, line, hipGetErrorString(e));
+  g_last_error = buf;
+  return ORBPL_ERR_HIP;
+}
+
+int arg_fail(const char* msg) {
+  g_last_error = msg;
+  return ORBPL_ERR_ARG;
+}
+
+}  // namespace orbpl
+
+using namespace orbpl;
+
+struct orbx_ctx {
+  orbpl_orb_params params{};
+  int device = 0;
+  int max_batch = 0;
+  OrbHostGeom hg;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[6] = {};
+  bool timed = false;
+  OrbGeom* d_geom = nullptr;
+  CellGeom* d_cells = nullptr;
+  int* d_rs = nullptr;
+  uint8_t* d_in = nullptr;
+  uint8_t* d_pyr = nullptr;
+  uint8_t* d_blur = nullptr;
+  uint32_t* d_cell_cands = nullptr;
+  int* d_cell_counts = nullptr;
+  uint32_t* d_kcand = nullptr;
+  int* d_knode = nullptr;
+  uint32_t* d_kp_list = nullptr;
+  int* d_kp_count = nullptr;
+  orbpl_keypoint_dev* d_out_kps = nullptr;
+  uint8_t* d_out_desc = nullptr;
+  int* d_out_n = nullptr;
+  int* d_err = nullptr;
+  int last_batch = 0;
+};
+
+#define HIP_CHECK(expr)                                              \
+  do {                                                               \
+    hipError_t _e = (expr);                                          \
+    if (_e != hipSuccess) return orbpl::hip_fail(_e, #expr, __LINE__); \
+  } while (0)
+
+extern "C" {
+
+const char* orbpl_last_error(void) { return orbpl::g_last_error.c_str(); }
+
+const char* orbpl_version(void) { return "orbpl gfx950 r1"; }
+
+int orbpl_device_count(int* n) {
+  if (!n) return arg_fail("n is NULL");
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) {
+    *n = 0;
+    hip_fail(e, "hipGetDeviceCount", __LINE__);
+    return ORBPL_ERR_NODEVICE;
+  }
+  *n = c;
+  return c > 0 ? ORBPL_OK : ORBPL_ERR_NODEVICE;
+}
+
+int orbpl_descriptor_distance(const uint8_t* a, const uint8_t* b) {
+  // ORBmatcher::DescriptorDistance (ORBmatcher.cc:2083-2103): popcount of XOR
+  int d = 0;
+  for (int i = 0; i < 4; i++) {
+    uint64_t x, y;
+    memcpy(&x, a + 8 * i, 8);
+    memcpy(&y, b + 8 * i, 8);
+    d += __builtin_popcountll(x ^ y);
+  }
+  return d;
+}
+
+static void free_ctx(orbx_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  void* ptrs[] = {c->d_geom, c->d_cells, c->d_rs, c->d_in, c->d_pyr, c->d_blur, c->d_cell_cands,
+                  c->d_cell_counts, c->d_kcand, c->d_knode, c->d_kp_list, c->d_kp_count,
+                  c->d_out_kps, c->d_out_desc, c->d_out_n, c->d_err};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  for (auto& e : c->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int orbx_create(const orbpl_orb_params* p, int width, int height, int max_batch, int device,
+                orbx_ctx** out) {
+  if (!p || !out) return arg_fail("NULL argument");
+  *out = nullptr;
+  if (width <= 0 || height <= 0 || max_batch <= 0) return arg_fail("bad size/batch");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    orbpl::g_last_error = "no HIP device visible";
+    return ORBPL_ERR_NODEVICE;
+  }
+  if (device < 0 || device >= ndev) return arg_fail("device index out of range");
+  orbx_ctx* c = new orbx_ctx();
+  c->params = *p;
+  c->device = device;
+  c->max_batch = max_batch;
+  const char* err = nullptr;
+  int rc = build_orb_geometry(p->nfeatures, p->scale_factor, p->nlevels, width, height, &c->hg, &err);
+  if (rc != ORBPL_OK) {
+    delete c;
+    return arg_fail(err ? err : "geometry");
+  }
+  const OrbGeom& g = c->hg.g;
+  auto fail = [&](hipError_t e, const char* what) {
+    int r = hip_fail(e, what, __LINE__);
+    free_ctx(c);
+    return r;
+  };
+#define CK(expr)                            \
+  do {                                      \
+    hipError_t _e = (expr);                 \
+    if (_e != hipSuccess) return fail(_e, #expr); \
+  } while (0)
+  CK(hipSetDevice(device));
+  CK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  for (auto& e : c->ev) CK(hipEventCreate(&e));
+  const size_t B = (size_t)max_batch;
+  CK(hipMalloc(&c->d_geom, sizeof(OrbGeom)));
+  CK(hipMalloc(&c->d_cells, sizeof(CellGeom) * std::max<size_t>(1, c->hg.cells.size())));
+  CK(hipMalloc(&c->d_rs, sizeof(int) * c->hg.rs.size()));
+  CK(hipMalloc(&c->d_in, B * (size_t)width * height));
+  CK(hipMalloc(&c->d_pyr, B * (size_t)g.pyr_bytes));
+  CK(hipMalloc(&c->d_blur, B * (size_t)g.pyr_bytes));
+  CK(hipMalloc(&c->d_cell_cands, B * (size_t)std::max(1, g.ncells_total) * g.cell_slots * 4));
+  CK(hipMalloc(&c->d_cell_counts, B * (size_t)std::max(1, g.ncells_total) * 4));
+  CK(hipMalloc(&c->d_kcand, B * (size_t)std::max(1, g.cand_cap_total) * 4));
+  CK(hipMalloc(&c->d_knode, B * (size_t)std::max(1, g.cand_cap_total) * 4));
+  CK(hipMalloc(&c->d_kp_list, B * (size_t)g.kp_cap_total * 4));
+  CK(hipMalloc(&c->d_kp_count, B * (size_t)g.nlevels * 4));
+  CK(hipMalloc(&c->d_out_kps, B * (size_t)g.kp_cap_total * sizeof(orbpl_keypoint_dev)));
+  CK(hipMalloc(&c->d_out_desc, B * (size_t)g.kp_cap_total * 32));
+  CK(hipMalloc(&c->d_out_n, B * 4));
+  CK(hipMalloc(&c->d_err, 4));
+  CK(hipMemsetAsync(c->d_err, 0, 4, c->stream));
+  CK(hipMemsetAsync(c->d_pyr, 0, B * (size_t)g.pyr_bytes, c->stream));
+  CK(hipMemsetAsync(c->d_blur, 0, B * (size_t)g.pyr_bytes, c->stream));
+  CK(hipMemcpyAsync(c->d_geom, &g, sizeof(OrbGeom), hipMemcpyHostToDevice, c->stream));
+  if (!c->hg.cells.empty())
+    CK(hipMemcpyAsync(c->d_cells, c->hg.cells.data(), sizeof(CellGeom) * c->hg.cells.size(),
+                      hipMemcpyHostToDevice, c->stream));
+  CK(hipMemcpyAsync(c->d_rs, c->hg.rs.data(), sizeof(int) * c->hg.rs.size(), hipMemcpyHostToDevice,
+                    c->stream));
+  CK(upload_pattern(c->stream));
+  CK(hipStreamSynchronize(c->stream));
+#undef CK
+  *out = c;
+  return ORBPL_OK;
+}
+
+int orbx_destroy(orbx_ctx* c) {
+  free_ctx(c);
+  return ORBPL_OK;
+}
+
+int orbx_get_scale_info(const orbx_ctx* c, int* nlevels, float* scale, float* inv_scale,
+                        float* sigma2, float* inv_sigma2) {
+  if (!c) return arg_fail("NULL ctx");
+  const int n = c->hg.g.nlevels;
+  if (nlevels) *nlevels = n;
+  for (int i = 0; i < n; i++) {
+    if (scale) scale[i] = c->hg.scale[i];
+    if (inv_scale) inv_scale[i] = c->hg.inv_scale[i];
+    if (sigma2) sigma2[i] = c->hg.sigma2[i];
+    if (inv_sigma2) inv_sigma2[i] = c->hg.inv_sigma2[i];
+  }
+  return ORBPL_OK;
+}
+
+int orbx_get_level_info(const orbx_ctx* c, int* w, int* h, int* nf) {
+  if (!c) return arg_fail("NULL ctx");
+  for (int i = 0; i < c->hg.g.nlevels; i++) {
+    if (w) w[i] = c->hg.g.lv[i].w;
+    if (h) h[i] = c->hg.g.lv[i].h;
+    if (nf) nf[i] = c->hg.g.lv[i].nfeat;
+  }
+  return ORBPL_OK;
+}
+
+int orbx_max_keypoints(const orbx_ctx* c) { return c ? c->hg.g.kp_cap_total : 0; }
+
+int orbx_describe(const orbpl_orb_params* p, int width, int height, int* lw, int* lh, int* nf,
+                  float* scale, int* max_kps) {
+  if (!p) return arg_fail("NULL params");
+  OrbHostGeom hg;
+  const char* err = nullptr;
+  int rc = build_orb_geometry(p->nfeatures, p->scale_factor, p->nlevels, width, height, &hg, &err);
+  if (rc != ORBPL_OK) return arg_fail(err ? err : "geometry");
+  for (int i = 0; i < hg.g.nlevels; i++) {
+    if (lw) lw[i] = hg.g.lv[i].w;
+    if (lh) lh[i] = hg.g.lv[i].h;
+    if (nf) nf[i] = hg.g.lv[i].nfeat;
+    if (scale) scale[i] = hg.scale[i];
+  }
+  if (max_kps) *max_kps = hg.g.kp_cap_total;
+  return ORBPL_OK;
+}
+
+}  // extern "C"
+
+namespace orbpl {
+// Whole extraction pipeline on the ctx stream; images already in device memory.
+int orbx_run(orbx_ctx* c, const uint8_t* d_imgs, int batch, int stride, long long frame_pitch,
+             orbpl_keypoint_dev* d_kps, uint8_t* d_desc, int kp_pitch, int* d_n) {
+  const OrbGeom& g = c->hg.g;
+  hipStream_t s = c->stream;
+  c->timed = true;
+  HIP_CHECK(hipEventRecord(c->ev[0], s));
+  launch_pyramid(g, c->d_geom, d_imgs, stride, frame_pitch, c->d_pyr, c->d_rs, batch, s);
+  HIP_CHECK(hipEventRecord(c->ev[1], s));
+  launch_blur(g, c->d_geom, c->d_pyr, c->d_blur, batch, s);
+  HIP_CHECK(hipEventRecord(c->ev[2], s));
+  launch_fast(g, c->d_geom, c->d_cells, c->d_pyr, c->d_cell_cands, c->d_cell_counts,
+              c->params.ini_th_fast, c->params.min_th_fast, batch, s);
+  HIP_CHECK(hipEventRecord(c->ev[3], s));
+  launch_octree(g, c->d_geom, c->d_cell_cands, c->d_cell_counts, c->d_kcand, c->d_knode,
+                c->d_kp_list, c->d_kp_count, c->d_err, batch, s);
+  HIP_CHECK(hipEventRecord(c->ev[4], s));
+  launch_orient_desc(g, c->d_geom, c->d_pyr, c->d_blur, c->d_kp_list, c->d_kp_count, d_kps, d_desc,
+                     kp_pitch, d_n, batch, s);
+  HIP_CHECK(hipEventRecord(c->ev[5], s));
+  HIP_CHECK(hipGetLastError());
+  c->last_batch = batch;
+  return ORBPL_OK;
+}
+}  // namespace orbpl
+
+extern "C" {
+
+int orbx_synchronize(orbx_ctx* c) {
+  if (!c) return arg_fail("NULL ctx");
+  HIP_CHECK(hipSetDevice(c->device));
+  HIP_CHECK(hipStreamSynchronize(c->stream));
+  int flag = 0;
+  HIP_CHECK(hipMemcpy(&flag, c->d_err, 4, hipMemcpyDeviceToHost));
+  if (flag) {
+    HIP_CHECK(hipMemset(c->d_err, 0, 4));
+    char buf[128];
+    snprintf(buf, sizeof(buf), "kernel capacity overflow (flags 0x%x)", flag);
+    orbpl::g_last_error = buf;
+    return ORBPL_ERR_OVERFLOW;
+  }
+  return ORBPL_OK;
+}
+
+int orbx_extract(orbx_ctx* c, const uint8_t* img, int width, int height, int stride,
+                 orbpl_keypoint* kps, uint8_t* desc, int cap, int* n) {
+  if (!c || !n) return arg_fail("NULL argument");
+  *n = 0;
+  if (!img || width <= 0 || height <= 0) return ORBPL_OK;  // _image.empty() -> return
+  if (width != c->hg.g.W || height != c->hg.g.H)
+    return arg_fail("image size differs from the size given to orbx_create");
+  if (stride < width) return arg_fail("stride < width");
+  HIP_CHECK(hipSetDevice(c->device));
+  const OrbGeom& g = c->hg.g;
+  HIP_CHECK(hipMemcpy2DAsync(c->d_in, width, img, stride, width, height, hipMemcpyHostToDevice,
+                             c->stream));
+  int rc = orbx_run(c, c->d_in, 1, width, (long long)width * height, c->d_out_kps, c->d_out_desc,
+                    g.kp_cap_total, c->d_out_n);
+  if (rc) return rc;
+  int cnt = 0;
+  HIP_CHECK(hipMemcpyAsync(&cnt, c->d_out_n, 4, hipMemcpyDeviceToHost, c->stream));
+  rc = orbx_synchronize(c);
+  if (rc) return rc;
+  if (cnt > cap) {
+    orbpl::g_last_error = "keypoint buffer too small";
+    *n = cnt;
+    return ORBPL_ERR_CAPACITY;
+  }
+  if (cnt > 0) {
+    if (kps)
+      HIP_CHECK(hipMemcpyAsync(kps, c->d_out_kps, (size_t)cnt * sizeof(orbpl_keypoint),
+                               hipMemcpyDeviceToHost, c->stream));
+    if (desc)
+      HIP_CHECK(hipMemcpyAsync(desc, c->d_out_desc, (size_t)cnt * 32, hipMemcpyDeviceToHost,
+                               c->stream));
+    HIP_CHECK(hipStreamSynchronize(c->stream));
+  }
+  *n = cnt;
+  return ORBPL_OK;
+}
+
+int orbx_extract_batch_device(orbx_ctx* c, const uint8_t* d_imgs, int batch, int stride,
+                              int64_t frame_pitch, orbpl_keypoint* d_kps, uint8_t* d_desc,
+                              int kp_pitch, int32_t* d_n) {
+  if (!c || !d_imgs || !d_kps || !d_desc || !d_n) return arg_fail("NULL argument");
+  if (batch <= 0 || batch > c->max_batch) return arg_fail("batch out of range");
+  if (stride < c->hg.g.W) return arg_fail("stride < width");
+  if (kp_pitch < 1) return arg_fail("kp_pitch < 1");
+  HIP_CHECK(hipSetDevice(c->device));
+  return orbx_run(c, d_imgs, batch, stride, (long long)frame_pitch,
+                  reinterpret_cast<orbpl_keypoint_dev*>(d_kps), d_desc, kp_pitch, d_n);
+}
+
+int orbx_get_pyramid(orbx_ctx* c, int frame, int level, int padded, int blurred, uint8_t* out,
+                     int out_cap, int* w, int* h) {
+  if (!c) return arg_fail("NULL ctx");
+  const OrbGeom& g = c->hg.g;
+  if (level < 0 || level >= g.nlevels || frame < 0 || frame >= c->max_batch)
+    return arg_fail("level/frame out of range");
+  const LevelGeom& L = g.lv[level];
+  const int ow = padded ? L.pw : L.w, oh = padded ? L.ph : L.h;
+  if (w) *w = ow;
+  if (h) *h = oh;
+  if (!out) return ORBPL_OK;
+  if (out_cap < ow * oh) return ORBPL_ERR_CAPACITY;
+  HIP_CHECK(hipSetDevice(c->device));
+  HIP_CHECK(hipStreamSynchronize(c->stream));
+  const uint8_t* base = (blurred ? c->d_blur : c->d_pyr) + (size_t)frame * g.pyr_bytes + L.pyr_off;
+  if (!padded) base += (size_t)kEdge * L.pitch + kEdge;
+  HIP_CHECK(hipMemcpy2D(out, ow, base, L.pitch, ow, oh, hipMemcpyDeviceToHost));
+  return ORBPL_OK;
+}
+
+int orbx_get_candidates(orbx_ctx* c, float* xyr, int cap, int* level_counts, int* total) {
+  if (!c || !total) return arg_fail("NULL argument");
+  const OrbGeom& g = c->hg.g;
+  HIP_CHECK(hipSetDevice(c->device));
+  HIP_CHECK(hipStreamSynchronize(c->stream));
+  std::vector<int> counts(std::max(1, g.ncells_total));
+  std::vector<uint32_t> cands((size_t)std::max(1, g.ncells_total) * g.cell_slots);
+  HIP_CHECK(hipMemcpy(counts.data(), c->d_cell_counts, 4 * (size_t)g.ncells_total, hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(cands.data(), c->d_cell_cands, 4 * cands.size(), hipMemcpyDeviceToHost));
+  int n = 0;
+  for (int l = 0; l < g.nlevels; l++) {
+    const LevelGeom& L = g.lv[l];
+    int lc = 0;
+    for (int ci = 0; ci < L.ncells; ci++) {
+      const int cell = L.cell_base + ci;
+      for (int k = 0; k < counts[cell]; k++) {
+        uint32_t v = cands[(size_t)cell * g.cell_slots + k];
+        if (n < cap && xyr) {
+          xyr[3 * n] = (float)cand_x(v);
+          xyr[3 * n + 1] = (float)cand_y(v);
+          xyr[3 * n + 2] = (float)cand_s(v);
+        }
+        n++;
+        lc++;
+      }
+    }
+    if (level_counts) level_counts[l] = lc;
+  }
+  *total = n;
+  return n > cap ? ORBPL_ERR_CAPACITY : ORBPL_OK;
+}
+
+int orbx_last_stage_ms(const orbx_ctx* c, float* ms5) {
+  if (!c || !ms5) return arg_fail("NULL argument");
+  if (!c->timed) return arg_fail("no extraction recorded yet");
+  HIP_CHECK(hipSetDevice(c->device));
+  HIP_CHECK(hipEventSynchronize(c->ev[5]));
+  for (int i = 0; i < 5; i++) HIP_CHECK(hipEventElapsedTime(&ms5[i], c->ev[i], c->ev[i + 1]));
+  return ORBPL_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,14 @@
+// Internal runtime helpers shared by the C-ABI translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "orb_kernels.h"
+
+struct orbx_ctx;
+
+namespace orbpl {
+int hip_fail(hipError_t e, const char* what, int line);
+int arg_fail(const char* msg);
+int orbx_run(orbx_ctx* c, const uint8_t* d_imgs, int batch, int stride, long long frame_pitch,
+             orbpl_keypoint_dev* d_kps, uint8_t* d_desc, int kp_pitch, int* d_n);
+}  // namespace orbpl

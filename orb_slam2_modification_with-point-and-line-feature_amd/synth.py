@@ -1,0 +1,222 @@
+"""Seeded synthetic RGB-D scenes for tests and the benchmark.
+
+There are no datasets on either box, so every frame is rendered here: a room of
+textured planes (value-noise texture at 4-64 px scales plus anti-aliased line
+segments, contrast 40-120 DN) seen by a pinhole camera moving on a smooth SE(3)
+trajectory. Depth comes exactly from the render (metres, float32) with ~5 %
+zero holes; Gaussian pixel noise sigma = 2 DN. Textures live in plane
+coordinates, so the same world point keeps its appearance across frames and
+FAST/ORB/LSD fire on consistent structure.
+
+Pure numpy; deterministic for a given seed.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+# TUM1.yaml intrinsics (Examples/RGB-D/TUM1.yaml:8-22)
+TUM1 = dict(fx=517.306408, fy=516.469215, cx=318.643040, cy=255.313989,
+            k1=0.262383, k2=-0.953104, p1=-0.005358, p2=0.002628, k3=1.163314,
+            width=640, height=480, bf=40.0, thdepth=40.0, depth_factor=5000.0)
+# TUM3.yaml (no distortion)
+TUM3 = dict(fx=535.4, fy=539.2, cx=320.1, cy=247.6, k1=0.0, k2=0.0, p1=0.0, p2=0.0, k3=0.0,
+            width=640, height=480, bf=40.0, thdepth=40.0, depth_factor=5000.0)
+# Upstream ORB-SLAM2 KITTI 00-02 values
+KITTI00 = dict(fx=718.856, fy=718.856, cx=607.1928, cy=185.2157, k1=0.0, k2=0.0, p1=0.0,
+               p2=0.0, k3=0.0, width=1241, height=376, bf=386.1448, thdepth=35.0,
+               depth_factor=1.0)
+
+
+def _hash2(ix, iy, seed):
+    """uint32 hash of integer lattice coordinates -> float in [0, 1)."""
+    h = (ix.astype(np.int64) * 374761393 + iy.astype(np.int64) * 668265263 +
+         np.int64(seed) * 2246822519) & 0xFFFFFFFF
+    h = h.astype(np.uint64)
+    h = (h ^ (h >> np.uint64(13))) * np.uint64(1274126177) & np.uint64(0xFFFFFFFF)
+    h = h ^ (h >> np.uint64(16))
+    return (h & np.uint64(0xFFFFFF)).astype(np.float64) / float(1 << 24)
+
+
+def _value_noise(u, v, freq, seed):
+    x = u * freq
+    y = v * freq
+    ix = np.floor(x)
+    iy = np.floor(y)
+    fx = x - ix
+    fy = y - iy
+    fx = fx * fx * (3 - 2 * fx)
+    fy = fy * fy * (3 - 2 * fy)
+    ix = ix.astype(np.int64)
+    iy = iy.astype(np.int64)
+    a = _hash2(ix, iy, seed)
+    b = _hash2(ix + 1, iy, seed)
+    c = _hash2(ix, iy + 1, seed)
+    d = _hash2(ix + 1, iy + 1, seed)
+    return (a * (1 - fx) + b * fx) * (1 - fy) + (c * (1 - fx) + d * fx) * fy
+
+
+def _segments_layer(u, v, cell, seed, width):
+    """Anti-aliased random segments: each `cell`-sized texture cell holds one
+    segment with random endpoints, contrast and polarity."""
+    cx = np.floor(u / cell).astype(np.int64)
+    cy = np.floor(v / cell).astype(np.int64)
+    out = np.zeros_like(u)
+    for dx in (-1, 0, 1):
+        for dy in (-1, 0, 1):
+            gx = cx + dx
+            gy = cy + dy
+            x0 = (gx + _hash2(gx, gy, seed + 11)) * cell
+            y0 = (gy + _hash2(gx, gy, seed + 12)) * cell
+            ang = _hash2(gx, gy, seed + 13) * np.pi
+            ln = (0.4 + 0.8 * _hash2(gx, gy, seed + 14)) * cell
+            con = (40 + 80 * _hash2(gx, gy, seed + 15)) * np.where(
+                _hash2(gx, gy, seed + 16) < 0.5, -1.0, 1.0)
+            ex = np.cos(ang)
+            ey = np.sin(ang)
+            px = u - x0
+            py = v - y0
+            t = np.clip(px * ex + py * ey, 0.0, ln)
+            dist = np.hypot(px - t * ex, py - t * ey)
+            cov = np.clip(1.0 - (dist - width * 0.5) / (width * 0.5 + 1e-12), 0.0, 1.0)
+            out += con * cov
+    return out
+
+
+def texture(u, v, seed):
+    """Intensity (float DN, unclipped) of plane texture coordinates (metres)."""
+    t = 128.0
+    for k, (freq, amp) in enumerate(((4.0, 60.0), (12.0, 40.0), (30.0, 30.0), (70.0, 18.0))):
+        t = t + amp * (_value_noise(u, v, freq, seed * 31 + k) - 0.5)
+    t = t + _segments_layer(u, v, 0.35, seed * 7 + 1, 0.008)
+    t = t + _segments_layer(u + 0.17, v + 0.05, 0.6, seed * 7 + 2, 0.012)
+    return t
+
+
+def default_room(seed=0):
+    """Planes as (point, normal, u_axis, v_axis, texture_seed)."""
+    rng = np.random.default_rng(seed)
+    planes = []
+    size = 4.0
+    specs = [((0, 0, size), (0, 0, -1), (1, 0, 0), (0, 1, 0)),     # front wall z=+4
+             ((0, 0, -size), (0, 0, 1), (-1, 0, 0), (0, 1, 0)),    # back wall
+             ((size, 0, 0), (-1, 0, 0), (0, 0, -1), (0, 1, 0)),    # right wall
+             ((-size, 0, 0), (1, 0, 0), (0, 0, 1), (0, 1, 0)),     # left wall
+             ((0, 1.2, 0), (0, -1, 0), (1, 0, 0), (0, 0, 1)),      # floor (y down)
+             ((0, -2.0, 0), (0, 1, 0), (1, 0, 0), (0, 0, -1))]     # ceiling
+    for p, n, ua, va in specs:
+        planes.append((np.array(p, float), np.array(n, float), np.array(ua, float),
+                       np.array(va, float), int(rng.integers(1, 1 << 20))))
+    # a few boxes' front faces for depth discontinuities
+    for k in range(3):
+        z = 2.0 + 1.2 * k
+        x = rng.uniform(-1.5, 1.5)
+        planes.append((np.array([x, 0, z]), np.array([0, 0, -1.0]), np.array([1.0, 0, 0]),
+                       np.array([0, 1.0, 0]), int(rng.integers(1, 1 << 20)), (x - 0.5, x + 0.5,
+                                                                                -0.8, 0.9)))
+    return planes
+
+
+def render(cam, Twc, planes, seed=0, noise_sigma=2.0, hole_frac=0.05):
+    """Render gray u8 (H, W) and depth float32 metres (H, W) for pose Twc (4x4,
+    camera-to-world). Rays are cast through the *distorted* pixel grid if the
+    camera has distortion, so keypoints need undistortion like a real TUM
+    frame."""
+    W, H = cam["width"], cam["height"]
+    fx, fy, cx, cy = cam["fx"], cam["fy"], cam["cx"], cam["cy"]
+    us, vs = np.meshgrid(np.arange(W, dtype=np.float64), np.arange(H, dtype=np.float64))
+    xn = (us - cx) / fx
+    yn = (vs - cy) / fy
+    k1, k2, p1, p2, k3 = cam["k1"], cam["k2"], cam["p1"], cam["p2"], cam["k3"]
+    if k1 != 0.0:
+        # invert the distortion model by fixed-point iteration (pixel -> ray)
+        x, y = xn.copy(), yn.copy()
+        for _ in range(8):
+            r2 = x * x + y * y
+            rad = 1 + k1 * r2 + k2 * r2 * r2 + k3 * r2 ** 3
+            dx = 2 * p1 * x * y + p2 * (r2 + 2 * x * x)
+            dy = p1 * (r2 + 2 * y * y) + 2 * p2 * x * y
+            x = (xn - dx) / rad
+            y = (yn - dy) / rad
+        xn, yn = x, y
+    R = Twc[:3, :3]
+    t = Twc[:3, 3]
+    dirs_c = np.stack([xn, yn, np.ones_like(xn)], -1)          # z = 1 in camera
+    dirs_w = dirs_c @ R.T
+    best = np.full((H, W), np.inf)
+    owner = np.full((H, W), -1, np.int32)
+    for k, pl in enumerate(planes):
+        p0, n = pl[0], pl[1]
+        denom = dirs_w @ n
+        with np.errstate(divide="ignore", invalid="ignore"):
+            lam = ((p0 - t) @ n) / denom
+        hit = (lam > 0.05) & np.isfinite(lam)
+        if len(pl) > 5:
+            P = t + dirs_w * lam[..., None]
+            x0, x1, y0, y1 = pl[5]
+            hit &= (P[..., 0] >= x0) & (P[..., 0] <= x1) & (P[..., 1] >= y0) & (P[..., 1] <= y1)
+        closer = hit & (lam < best)
+        best = np.where(closer, lam, best)
+        owner = np.where(closer, k, owner)
+    img = np.full((H, W), 128.0)
+    for k, pl in enumerate(planes):
+        sel = owner == k
+        if not sel.any():
+            continue
+        p0, ua, va, tseed = pl[0], pl[2], pl[3], pl[4]
+        P = t + dirs_w[sel] * best[sel][:, None]
+        img[sel] = texture((P - p0) @ ua, (P - p0) @ va, tseed)
+    depth = np.where(np.isfinite(best), best, 0.0)   # lam is z in camera (dir z = 1)
+    rng = np.random.default_rng(seed)
+    img = img + rng.normal(0.0, noise_sigma, img.shape)
+    gray = np.clip(np.rint(img), 0, 255).astype(np.uint8)
+    if hole_frac > 0:
+        holes = rng.random(depth.shape) < hole_frac
+        depth = np.where(holes, 0.0, depth)
+    return gray, depth.astype(np.float32)
+
+
+def se3(R, t):
+    T = np.eye(4)
+    T[:3, :3] = R
+    T[:3, 3] = t
+    return T
+
+
+def rot_xyz(rx, ry, rz):
+    cx, sx, cy, sy, cz, sz = np.cos(rx), np.sin(rx), np.cos(ry), np.sin(ry), np.cos(rz), np.sin(rz)
+    Rx = np.array([[1, 0, 0], [0, cx, -sx], [0, sx, cx]])
+    Ry = np.array([[cy, 0, sy], [0, 1, 0], [-sy, 0, cy]])
+    Rz = np.array([[cz, -sz, 0], [sz, cz, 0], [0, 0, 1]])
+    return Rz @ Ry @ Rx
+
+
+def trajectory(n, seed=0, step_t=0.01, step_r_deg=0.5, yaw0=0.0):
+    """Smooth camera-to-world poses: <= step_t metres and <= step_r_deg per
+    frame, starting near the room centre looking along +z."""
+    rng = np.random.default_rng(seed)
+    ph = rng.uniform(0, 2 * np.pi, 6)
+    fr = rng.uniform(0.3, 1.0, 6)
+    poses = []
+    for i in range(n):
+        s = i / 30.0
+        tx = 0.4 * np.sin(fr[0] * s + ph[0]) * step_t / 0.01
+        ty = 0.15 * np.sin(fr[1] * s + ph[1]) * step_t / 0.01
+        tz = 0.4 * np.sin(fr[2] * s + ph[2]) * step_t / 0.01 - 0.5
+        k = np.deg2rad(step_r_deg) * 30.0
+        rx = 0.2 * k * np.sin(fr[3] * s + ph[3])
+        ry = yaw0 + 0.6 * k * np.sin(fr[4] * s + ph[4])
+        rz = 0.15 * k * np.sin(fr[5] * s + ph[5])
+        poses.append(se3(rot_xyz(rx, ry, rz), np.array([tx, ty, tz])))
+    return poses
+
+
+def textured_image(width=640, height=480, seed=0, noise_sigma=2.0):
+    """One gray frame of the default room from a seeded pose (extraction tests)."""
+    rng = np.random.default_rng(seed)
+    cam = dict(TUM3)
+    cam.update(width=width, height=height, cx=width / 2.0 - 0.5, cy=height / 2.0 - 0.5,
+               fx=0.83 * width, fy=0.83 * width)
+    R = rot_xyz(rng.uniform(-0.2, 0.2), rng.uniform(-np.pi, np.pi), rng.uniform(-0.1, 0.1))
+    t = np.array([rng.uniform(-1, 1), rng.uniform(-0.3, 0.3), rng.uniform(-1, 1)])
+    gray, _ = render(cam, se3(R, t), default_room(seed), seed=seed, noise_sigma=noise_sigma)
+    return gray

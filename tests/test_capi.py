@@ -1,0 +1,55 @@
+"""CPU tests of the C-ABI boundary: the library loads, exports every symbol
+include/orbpl.h declares, and its device-free entry points agree with the
+oracle. No GPU calls."""
+import re
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _declared_functions():
+    src = (ROOT / "include" / "orbpl.h").read_text()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?[\w]+\s*\**\s+(\w+)\s*\(", src, flags=re.M)
+    return sorted(set(n for n in names if n not in ("if",)))
+
+
+def test_library_exports_every_declared_symbol(orbpl):
+    lib = orbpl.lib()
+    names = _declared_functions()
+    assert len(names) >= 15
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_describe_matches_oracle(orbpl, oracle):
+    for (w, h, nf) in ((640, 480, 1000), (1241, 376, 2000), (1280, 720, 2000), (320, 240, 500)):
+        d = orbpl.describe(nfeatures=nf, width=w, height=h)
+        lw, lh, nfl, sc, _ = oracle.level_sizes(oracle.params(nf), w, h)
+        assert np.array_equal(d["width"], lw)
+        assert np.array_equal(d["height"], lh)
+        assert np.array_equal(d["nfeatures"], nfl)
+        assert np.array_equal(d["scale"], sc)
+        assert d["max_keypoints"] >= nf + 3 * 8
+
+
+def test_describe_rejects_bad_geometry(orbpl):
+    import pytest
+    with pytest.raises(orbpl.OrbplError):
+        orbpl.describe(width=40, height=30)          # levels below 20 px
+    with pytest.raises(orbpl.OrbplError):
+        orbpl.describe(nfeatures=0)
+
+
+def test_descriptor_distance(orbpl):
+    rng = np.random.default_rng(0)
+    for _ in range(50):
+        a = rng.integers(0, 256, 32, dtype=np.uint8)
+        b = rng.integers(0, 256, 32, dtype=np.uint8)
+        ref = int(np.unpackbits(a ^ b).sum())
+        assert orbpl.DescriptorDistance(a, b) == ref
+    z = np.zeros(32, np.uint8)
+    assert orbpl.DescriptorDistance(z, z) == 0
+    assert orbpl.DescriptorDistance(z, np.full(32, 255, np.uint8)) == 256
