@@ -52,6 +52,15 @@ int orbpl_device_count(int* n);
 /* Library build tag (e.g. "orbpl gfx950 r1"). */
 const char* orbpl_version(void);
 
+/* Device memory plumbing for hosts without their own GPU allocator (the
+ * reference's C++ Tracking, ctypes tests, bench). Synchronous copies. */
+int orbpl_dev_malloc(int device, int64_t bytes, void** out);
+int orbpl_dev_free(int device, void* ptr);
+int orbpl_memcpy_htod(int device, void* dst, const void* src, int64_t bytes);
+int orbpl_memcpy_dtoh(int device, void* dst, const void* src, int64_t bytes);
+int orbpl_memset_d(int device, void* dst, int value, int64_t bytes);
+int orbpl_device_synchronize(int device);
+
 /* ------------------------------------------------------------------------
  * ORB extraction  — replaces ORB_SLAM2::ORBextractor (include/ORBextractor.h,
  * src/ORBextractor.cc:410-1132).

@@ -72,6 +72,12 @@ def _declare(L):
     L.orbx_synchronize.argtypes = [vp]
     L.orbx_last_stage_ms.argtypes = [vp, vp]
     L.orbpl_descriptor_distance.argtypes = [vp, vp]
+    L.orbpl_dev_malloc.argtypes = [i, C.c_int64, C.POINTER(vp)]
+    L.orbpl_dev_free.argtypes = [i, vp]
+    L.orbpl_memcpy_htod.argtypes = [i, vp, vp, C.c_int64]
+    L.orbpl_memcpy_dtoh.argtypes = [i, vp, vp, C.c_int64]
+    L.orbpl_memset_d.argtypes = [i, vp, i, C.c_int64]
+    L.orbpl_device_synchronize.argtypes = [i]
 
 
 def check(rc, what=""):
@@ -83,6 +89,51 @@ def check(rc, what=""):
 
 def _ptr(a):
     return a.ctypes.data_as(C.c_void_p)
+
+
+class DeviceBuffer:
+    """Owned device allocation (hipMalloc via the C-ABI)."""
+
+    def __init__(self, nbytes, device=0):
+        self.nbytes, self.device = int(nbytes), device
+        p = C.c_void_p()
+        check(lib().orbpl_dev_malloc(device, self.nbytes, C.byref(p)), "orbpl_dev_malloc")
+        self.ptr = p.value
+
+    @classmethod
+    def from_array(cls, arr, device=0):
+        arr = np.ascontiguousarray(arr)
+        b = cls(arr.nbytes, device)
+        b.upload(arr)
+        return b
+
+    def upload(self, arr):
+        arr = np.ascontiguousarray(arr)
+        assert arr.nbytes <= self.nbytes
+        check(lib().orbpl_memcpy_htod(self.device, C.c_void_p(self.ptr), _ptr(arr), arr.nbytes),
+              "orbpl_memcpy_htod")
+
+    def download(self, dtype, shape):
+        out = np.empty(shape, dtype)
+        assert out.nbytes <= self.nbytes
+        check(lib().orbpl_memcpy_dtoh(self.device, _ptr(out), C.c_void_p(self.ptr), out.nbytes),
+              "orbpl_memcpy_dtoh")
+        return out
+
+    def zero(self):
+        check(lib().orbpl_memset_d(self.device, C.c_void_p(self.ptr), 0, self.nbytes),
+              "orbpl_memset_d")
+
+    def free(self):
+        if self.ptr:
+            lib().orbpl_dev_free(self.device, C.c_void_p(self.ptr))
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 def device_count():

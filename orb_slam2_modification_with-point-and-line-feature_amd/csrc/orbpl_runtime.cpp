@@ -90,6 +90,43 @@ int orbpl_device_count(int* n) {
   return c > 0 ? ORBPL_OK : ORBPL_ERR_NODEVICE;
 }
 
+int orbpl_dev_malloc(int device, int64_t bytes, void** out) {
+  if (!out || bytes < 0) return arg_fail("bad argument");
+  HIP_CHECK(hipSetDevice(device));
+  HIP_CHECK(hipMalloc(out, (size_t)(bytes > 0 ? bytes : 1)));
+  return ORBPL_OK;
+}
+
+int orbpl_dev_free(int device, void* ptr) {
+  HIP_CHECK(hipSetDevice(device));
+  if (ptr) HIP_CHECK(hipFree(ptr));
+  return ORBPL_OK;
+}
+
+int orbpl_memcpy_htod(int device, void* dst, const void* src, int64_t bytes) {
+  HIP_CHECK(hipSetDevice(device));
+  if (bytes > 0) HIP_CHECK(hipMemcpy(dst, src, (size_t)bytes, hipMemcpyHostToDevice));
+  return ORBPL_OK;
+}
+
+int orbpl_memcpy_dtoh(int device, void* dst, const void* src, int64_t bytes) {
+  HIP_CHECK(hipSetDevice(device));
+  if (bytes > 0) HIP_CHECK(hipMemcpy(dst, src, (size_t)bytes, hipMemcpyDeviceToHost));
+  return ORBPL_OK;
+}
+
+int orbpl_memset_d(int device, void* dst, int value, int64_t bytes) {
+  HIP_CHECK(hipSetDevice(device));
+  if (bytes > 0) HIP_CHECK(hipMemset(dst, value, (size_t)bytes));
+  return ORBPL_OK;
+}
+
+int orbpl_device_synchronize(int device) {
+  HIP_CHECK(hipSetDevice(device));
+  HIP_CHECK(hipDeviceSynchronize());
+  return ORBPL_OK;
+}
+
 int orbpl_descriptor_distance(const uint8_t* a, const uint8_t* b) {
   // ORBmatcher::DescriptorDistance (ORBmatcher.cc:2083-2103): popcount of XOR
   int d = 0;

@@ -28,3 +28,11 @@ def oracle():
 def synth(orbpl):
     import orbpl.synth as s
     return s
+
+
+if os.environ.get("ORBPL_TEST_TORCH_FIRST"):
+    # Load torch's bundled HIP runtime before liborbpl.so (both carry the
+    # SONAME libamdhip64.so.7; the first one loaded serves the process).
+    import torch  # noqa: F401
+    if torch.cuda.is_available():
+        torch.zeros(1, device="cuda")

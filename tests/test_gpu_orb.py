@@ -95,24 +95,21 @@ def test_flat_and_empty(orbpl):
 
 
 def test_batch_device_matches_single(orbpl, synth):
-    import torch
     B = 4
     imgs = np.stack([synth.textured_image(640, 480, seed=30 + i) for i in range(B)])
     ex1 = _extractor(orbpl, (1000, 1.2, 8, 20, 7), 640, 480)
     singles = [ex1(imgs[i]) for i in range(B)]
     exb = _extractor(orbpl, (1000, 1.2, 8, 20, 7), 640, 480, batch=B)
     cap = exb.max_keypoints
-    d_img = torch.from_numpy(imgs).cuda()
-    d_kps = torch.zeros((B, cap, 7), dtype=torch.int32, device="cuda")
-    d_desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device="cuda")
-    d_n = torch.zeros(B, dtype=torch.int32, device="cuda")
-    exb.extract_batch_device(d_img.data_ptr(), B, 640, 640 * 480, d_kps.data_ptr(),
-                             d_desc.data_ptr(), cap, d_n.data_ptr())
+    d_img = orbpl.DeviceBuffer.from_array(imgs)
+    d_kps = orbpl.DeviceBuffer(B * cap * 28)
+    d_desc = orbpl.DeviceBuffer(B * cap * 32)
+    d_n = orbpl.DeviceBuffer(B * 4)
+    exb.extract_batch_device(d_img.ptr, B, 640, 640 * 480, d_kps.ptr, d_desc.ptr, cap, d_n.ptr)
     exb.synchronize()
-    n = d_n.cpu().numpy()
-    kraw = d_kps.cpu().numpy()
-    dd = d_desc.cpu().numpy()
+    n = d_n.download(np.int32, B)
+    kraw = d_kps.download(orbpl.KP_DTYPE, (B, cap))
+    dd = d_desc.download(np.uint8, (B, cap, 32))
     for i in range(B):
-        k = kraw[i, :n[i]].copy().view(orbpl.KP_DTYPE).reshape(-1)
-        assert _kp_equal(k, singles[i][0])
+        assert _kp_equal(kraw[i, :n[i]], singles[i][0])
         assert np.array_equal(dd[i, :n[i]], singles[i][1])

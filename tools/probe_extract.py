@@ -1,0 +1,34 @@
+"""Quick throughput probe of batched ORB extraction (dev tool)."""
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "tests"))
+from _pkg import load_pkg  # noqa: E402
+
+pkg = load_pkg()
+import orbpl.synth as synth  # noqa: E402
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+base = [synth.textured_image(640, 480, seed=100 + i) for i in range(8)]
+imgs = np.stack([base[i % 8] for i in range(B)])
+ex = pkg.ORBextractor(1000, 1.2, 8, 20, 7, width=640, height=480, max_batch=B)
+cap = ex.max_keypoints
+d_img = pkg.DeviceBuffer.from_array(imgs)
+d_kps = pkg.DeviceBuffer(B * cap * 28)
+d_desc = pkg.DeviceBuffer(B * cap * 32)
+d_n = pkg.DeviceBuffer(B * 4)
+for it in range(3):
+    ex.extract_batch_device(d_img.ptr, B, 640, 640 * 480, d_kps.ptr, d_desc.ptr, cap, d_n.ptr)
+    ex.synchronize()
+ms = ex.stage_ms()
+t = time.time()
+R = 10
+for it in range(R):
+    ex.extract_batch_device(d_img.ptr, B, 640, 640 * 480, d_kps.ptr, d_desc.ptr, cap, d_n.ptr)
+ex.synchronize()
+dt = (time.time() - t) / R
+n = d_n.download(np.int32, B)
+print(f"B={B} wall {dt*1e3:.2f} ms/batch -> {B/dt:.0f} fps; stages ms (pyr, blur, fast, octree, desc) = {np.round(ms, 3).tolist()} ; n[0:4]={n[:4].tolist()}")
