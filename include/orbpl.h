@@ -123,6 +123,134 @@ int orbx_synchronize(orbx_ctx* ctx);
  * stream. */
 int orbx_last_stage_ms(const orbx_ctx* ctx, float* ms5);
 
+
+/* ------------------------------------------------------------------------
+ * Camera / Frame glue — Frame constructors (Frame.cc:135-205): undistortion
+ * (UndistortKeyPoints :737-764, cv::undistortPoints 5 iterations), image
+ * bounds (ComputeImageBounds :847-885), RGB-D depth association
+ * (ComputeStereoFromRGBD :1065-1117) and the 64x48 grid (PosInGrid :527-538).
+ * ---------------------------------------------------------------------- */
+typedef struct orbpl_camera {
+  float fx, fy, cx, cy;        /* Camera.fx/fy/cx/cy                          */
+  float k1, k2, p1, p2, k3;    /* Camera.k1..k3 (OpenCV order)                */
+  float bf;                    /* mbf = Camera.bf                             */
+  float th_depth;              /* mThDepth = bf * ThDepth / fx (Tracking.cc:134-138) */
+  int32_t width, height;
+} orbpl_camera;
+
+#define ORBPL_GRID_COLS 64     /* FRAME_GRID_COLS (Frame.h:41) */
+#define ORBPL_GRID_ROWS 48     /* FRAME_GRID_ROWS (Frame.h:40) */
+
+/* Per-frame glue on the GPU. Inputs: raw keypoints kps[n] from orbx_extract,
+ * optional depth image (float metres, width x height, row stride = width;
+ * NULL for monocular: depth/uright = -1). Outputs (caller-owned, n entries):
+ * kps_un (mvKeysUn), depth (mvDepth), uright (mvuRight), grid_cell
+ * (gx + 64*gy, -1 if PosInGrid fails). bounds[4] = mnMinX, mnMaxX, mnMinY,
+ * mnMaxY. */
+int orbpl_frame_prepare(const orbpl_camera* cam, const orbpl_keypoint* kps, int n,
+                        const float* depth, orbpl_keypoint* kps_un, float* depth_out,
+                        float* uright_out, int32_t* grid_cell, float* bounds);
+
+/* ------------------------------------------------------------------------
+ * ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame,
+ * float th, bool bMono)  (ORBmatcher.cc:1710-1879), with ORBmatcher(0.9, true)
+ * as Tracking::TrackWithMotionModel builds it (Tracking.cc:1216).
+ * ---------------------------------------------------------------------- */
+typedef struct orbpl_match_current {
+  int32_t n;
+  const float* Tcw;            /* 4x4 row-major (mTcw, predicted pose)        */
+  const orbpl_keypoint* kps_un;/* mvKeysUn                                    */
+  const uint8_t* desc;         /* mDescriptors, n x 32                        */
+  const float* uright;         /* mvuRight                                    */
+} orbpl_match_current;
+
+typedef struct orbpl_match_last {
+  int32_t n;
+  const float* Tcw;            /* LastFrame.mTcw                              */
+  const orbpl_keypoint* kps_un;/* LastFrame.mvKeysUn (angle, octave used)     */
+  const uint8_t* has_mp;       /* LastFrame.mvpMapPoints[i] != NULL           */
+  const uint8_t* outlier;      /* LastFrame.mvbOutlier                        */
+  const float* mp_xyz;         /* pMP->GetWorldPos(), n x 3                   */
+  const uint8_t* mp_desc;      /* pMP->GetDescriptor(), n x 32                */
+  const int32_t* mp_nobs;      /* pMP->Observations()                         */
+} orbpl_match_last;
+
+/* match[i] = index j of the last-frame map point assigned to current keypoint
+ * i (CurrentFrame.mvpMapPoints[i] = LastFrame.mvpMapPoints[j]) or -1.
+ * *nmatches = the function's return value. */
+int orbm_search_by_projection_last(const orbpl_camera* cam, const float* scale_factors,
+                                   int nlevels, const orbpl_match_current* cur,
+                                   const orbpl_match_last* last, float th, int mono,
+                                   int check_orientation, int32_t* match, int* nmatches);
+
+/* ------------------------------------------------------------------------
+ * Optimizer::PoseOptimization / PoseOptimizationWithLines
+ * (Optimizer.cc:375-619, 2132-2486): 4 rounds x 10 Levenberg-Marquardt
+ * iterations on one SE3 vertex, Huber kernel in rounds 0-2, chi2 outlier
+ * re-labelling after each round. Point edge i exists if has_mp[i]; it is
+ * monocular if uright[i] < 0 else stereo. Line edge j exists if has_ml[j].
+ * ---------------------------------------------------------------------- */
+typedef struct orbpl_pose_problem {
+  int32_t n;                   /* points: N                                   */
+  const orbpl_keypoint* kps_un;
+  const float* uright;
+  const uint8_t* has_mp;
+  const float* mp_xyz;         /* n x 3                                       */
+  int32_t nl;                  /* lines: NL (0 for PoseOptimization)          */
+  const float* kl_obs;         /* nl x 4: startX, startY, endX, endY (mvKeyLinesUn) */
+  const int32_t* kl_octave;    /* nl                                          */
+  const uint8_t* has_ml;       /* nl                                          */
+  const float* ml_xyz;         /* nl x 6: world start, world end              */
+  const float* inv_sigma2;     /* mvInvLevelSigma2, nlevels                   */
+  int32_t nlevels;
+} orbpl_pose_problem;
+
+/* Tcw: in = pFrame->mTcw, out = optimised pose (4x4 row-major float).
+ * outlier[n] / line_outlier[nl]: in = pFrame->mvbOutlier / mvbLineOutlier,
+ * out = after the call. *n_inliers = return value of the reference
+ * (nInitialCorrespondences - nBad, 0 if < 3 correspondences). */
+int orbpl_pose_optimization(const orbpl_camera* cam, const orbpl_pose_problem* prob, float* Tcw,
+                            uint8_t* outlier, uint8_t* line_outlier, int* n_inliers);
+
+
+/* ------------------------------------------------------------------------
+ * Batched RGB-D tracker: the per-frame hot path of Tracking::Track for
+ * n_streams independent camera streams on one device, one
+ * TrackWithMotionModel step per call (Tracking.cc:1212-1330):
+ *   Frame(RGB-D) extraction + glue -> constant-velocity prediction ->
+ *   SearchByProjection(cur, last, th=15, retry 2*th if < 20) ->
+ *   PoseOptimization -> discard outliers -> velocity update.
+ * Every frame then acts as the keyframe of the next one: its keypoints with
+ * depth become map points (StereoInitialization-style, Tracking.cc:608-660);
+ * local mapping / loop closing are out of scope.
+ * ---------------------------------------------------------------------- */
+typedef struct orbpl_tracker orbpl_tracker;
+
+int orbpl_tracker_create(const orbpl_orb_params* orb, const orbpl_camera* cam, int n_streams,
+                         int device, orbpl_tracker** out);
+int orbpl_tracker_destroy(orbpl_tracker* tr);
+/* Forget all stream state; the next step initialises every stream with pose
+ * Tcw0 (n_streams x 16 floats row-major, NULL = identity). */
+int orbpl_tracker_reset(orbpl_tracker* tr, const float* Tcw0);
+/* One step for all streams. d_gray: n_streams frames of width*height u8;
+ * d_depth: n_streams frames of width*height float metres (device memory,
+ * contiguous). Asynchronous on the tracker's stream. */
+int orbpl_tracker_step(orbpl_tracker* tr, const uint8_t* d_gray, const float* d_depth);
+int orbpl_tracker_synchronize(orbpl_tracker* tr);
+/* Results of the last step, per stream (any pointer may be NULL):
+ * Tcw (16 floats), keypoints, SearchByProjection matches, PoseOptimization
+ * inliers, map matches after outlier removal. */
+int orbpl_tracker_get_state(orbpl_tracker* tr, float* Tcw, int* nkeypoints, int* nmatches,
+                            int* ninliers, int* nmatches_map);
+/* hipEvent times of the last step (ms): extract, glue, match, pose, finish. */
+int orbpl_tracker_stage_ms(orbpl_tracker* tr, float* ms5);
+/* Per-stream frame outputs of the last step (host copies, kp_cap entries per
+ * stream, see orbpl_tracker_kp_capacity): undistorted keypoints, descriptors,
+ * match (last-frame index per keypoint or -1), outlier flags. */
+int orbpl_tracker_kp_capacity(const orbpl_tracker* tr);
+int orbpl_tracker_get_frame(orbpl_tracker* tr, int stream, orbpl_keypoint* kps_un, uint8_t* desc,
+                            int32_t* match, uint8_t* outlier, int* n);
+
 /* ------------------------------------------------------------------------
  * Hamming distance — ORBmatcher::DescriptorDistance (ORBmatcher.cc:2083-2103)
  * ---------------------------------------------------------------------- */

@@ -117,3 +117,151 @@ def extract(p, img, cap=None):
                                   C.byref(n), _p(cnt))
     assert rc == 0, rc
     return kps[:n.value].copy(), desc[:n.value].copy(), cnt
+
+
+# ---------------------------------------------------------------------------
+# tracking half (track_oracle.cpp); argument conventions match the product's
+# Python mirror (orbpl.frame_prepare / ORBmatcher / pose_optimization)
+# ---------------------------------------------------------------------------
+class Camera(C.Structure):
+    _fields_ = [("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float),
+                ("k1", C.c_float), ("k2", C.c_float), ("p1", C.c_float), ("p2", C.c_float),
+                ("k3", C.c_float), ("bf", C.c_float), ("th_depth", C.c_float),
+                ("width", C.c_int32), ("height", C.c_int32)]
+
+
+class MatchCurrent(C.Structure):
+    _fields_ = [("n", C.c_int32), ("Tcw", C.c_void_p), ("kps_un", C.c_void_p),
+                ("desc", C.c_void_p), ("uright", C.c_void_p)]
+
+
+class MatchLast(C.Structure):
+    _fields_ = [("n", C.c_int32), ("Tcw", C.c_void_p), ("kps_un", C.c_void_p),
+                ("has_mp", C.c_void_p), ("outlier", C.c_void_p), ("mp_xyz", C.c_void_p),
+                ("mp_desc", C.c_void_p), ("mp_nobs", C.c_void_p)]
+
+
+class PoseProblem(C.Structure):
+    _fields_ = [("n", C.c_int32), ("kps_un", C.c_void_p), ("uright", C.c_void_p),
+                ("has_mp", C.c_void_p), ("mp_xyz", C.c_void_p), ("nl", C.c_int32),
+                ("kl_obs", C.c_void_p), ("kl_octave", C.c_void_p), ("has_ml", C.c_void_p),
+                ("ml_xyz", C.c_void_p), ("inv_sigma2", C.c_void_p), ("nlevels", C.c_int32)]
+
+
+def camera(cfg):
+    return Camera(cfg["fx"], cfg["fy"], cfg["cx"], cfg["cy"], cfg["k1"], cfg["k2"], cfg["p1"],
+                  cfg["p2"], cfg["k3"], cfg["bf"], cfg["bf"] * cfg["thdepth"] / cfg["fx"],
+                  cfg["width"], cfg["height"])
+
+
+def _c(a, dt):
+    return np.ascontiguousarray(a, dtype=dt)
+
+
+def _setup_track(L):
+    vp, i, ip = C.c_void_p, C.c_int, C.POINTER(C.c_int)
+    L.oracle_frame_prepare.argtypes = [vp, vp, i, vp, vp, vp, vp, vp, vp]
+    L.oracle_search_by_projection_last.argtypes = [vp, vp, i, vp, vp, C.c_float, i, i, vp, ip]
+    L.oracle_pose_optimization.argtypes = [vp, vp, vp, vp, vp, ip]
+    L.oracle_vo_create.argtypes = [vp, vp, i]
+    L.oracle_vo_create.restype = vp
+    L.oracle_vo_destroy.argtypes = [vp]
+    L.oracle_vo_reset.argtypes = [vp, vp]
+    L.oracle_vo_step.argtypes = [vp, i, vp, vp, vp, vp]
+
+
+_setup_orb = _setup
+
+
+def _setup(L):  # noqa: F811
+    _setup_orb(L)
+    _setup_track(L)
+
+
+def frame_prepare(cam, kps, depth=None):
+    kps = _c(kps, KP_DTYPE)
+    n = len(kps)
+    ku = np.zeros(n, KP_DTYPE)
+    d = np.zeros(n, np.float32)
+    ur = np.zeros(n, np.float32)
+    gc = np.zeros(n, np.int32)
+    b = np.zeros(4, np.float32)
+    dp = None if depth is None else _c(depth, np.float32)
+    lib().oracle_frame_prepare(C.byref(cam), _p(kps), n, None if dp is None else _p(dp), _p(ku),
+                               _p(d), _p(ur), _p(gc), _p(b))
+    return ku, d, ur, gc, b
+
+
+def search_by_projection_last(cam, scale_factors, cur, last, th, mono=False, check_ori=True):
+    keep = []
+
+    def arr(a, dt):
+        a = _c(a, dt)
+        keep.append(a)
+        return _p(a)
+
+    sf = _c(scale_factors, np.float32)
+    mc = MatchCurrent(len(cur["kps_un"]), arr(cur["Tcw"], np.float32), arr(cur["kps_un"], KP_DTYPE),
+                      arr(cur["desc"], np.uint8), arr(cur["uright"], np.float32))
+    ml = MatchLast(len(last["kps_un"]), arr(last["Tcw"], np.float32), arr(last["kps_un"], KP_DTYPE),
+                   arr(last["has_mp"], np.uint8), arr(last["outlier"], np.uint8),
+                   arr(last["mp_xyz"], np.float32), arr(last["mp_desc"], np.uint8),
+                   arr(last["mp_nobs"], np.int32))
+    match = np.zeros(max(1, mc.n), np.int32)
+    nm = C.c_int(0)
+    lib().oracle_search_by_projection_last(C.byref(cam), _p(sf), len(sf), C.byref(mc), C.byref(ml),
+                                           float(th), int(mono), int(check_ori), _p(match),
+                                           C.byref(nm))
+    return match[:mc.n].copy(), nm.value
+
+
+def pose_optimization(cam, prob, Tcw, outlier, line_outlier=None):
+    keep = []
+
+    def arr(a, dt):
+        a = _c(a, dt)
+        keep.append(a)
+        return _p(a)
+
+    n = len(prob["kps_un"])
+    nl = len(prob.get("kl_obs", ()))
+    isg = _c(prob["inv_sigma2"], np.float32)
+    P = PoseProblem(n, arr(prob["kps_un"], KP_DTYPE), arr(prob["uright"], np.float32),
+                    arr(prob["has_mp"], np.uint8), arr(prob["mp_xyz"], np.float32), nl,
+                    arr(prob.get("kl_obs", np.zeros((0, 4))), np.float32),
+                    arr(prob.get("kl_octave", np.zeros(0)), np.int32),
+                    arr(prob.get("has_ml", np.zeros(0)), np.uint8),
+                    arr(prob.get("ml_xyz", np.zeros((0, 6))), np.float32), _p(isg), len(isg))
+    T = _c(Tcw, np.float32).copy()
+    out = _c(outlier, np.uint8).copy()
+    lout = _c(line_outlier if line_outlier is not None else np.zeros(nl), np.uint8).copy()
+    nin = C.c_int(0)
+    lib().oracle_pose_optimization(C.byref(cam), C.byref(P), _p(T), _p(out), _p(lout), C.byref(nin))
+    return T, out, lout, nin.value
+
+
+class VO:
+    """CPU oracle of the batched tracker (one stream at a time)."""
+
+    def __init__(self, orb_params, cam, n_streams):
+        self.h = lib().oracle_vo_create(C.byref(orb_params), C.byref(cam), n_streams)
+
+    def reset(self, Tcw0=None):
+        T = None if Tcw0 is None else _c(Tcw0, np.float32)
+        lib().oracle_vo_reset(self.h, None if T is None else _p(T))
+
+    def step(self, stream, gray, depth):
+        g = _c(gray, np.uint8)
+        d = _c(depth, np.float32)
+        T = np.zeros(16, np.float32)
+        o = np.zeros(5, np.int32)
+        rc = lib().oracle_vo_step(self.h, stream, _p(g), _p(d), _p(T), _p(o))
+        assert rc == 0
+        return T.reshape(4, 4), dict(nkeypoints=int(o[0]), nmatches=int(o[1]), ninliers=int(o[2]),
+                                     nmatches_map=int(o[3]), ok=int(o[4]))
+
+    def __del__(self):
+        try:
+            lib().oracle_vo_destroy(self.h)
+        except Exception:
+            pass

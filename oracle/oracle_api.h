@@ -15,6 +15,20 @@ int oracle_orb_candidates(const orbpl_orb_params* p, const uint8_t* img, int w, 
 int oracle_orb_extract(const orbpl_orb_params* p, const uint8_t* img, int w, int h, int stride,
                        orbpl_keypoint* kps, uint8_t* desc, int cap, int* n_out, int* level_counts);
 float oracle_fast_atan2(float y, float x);
+int oracle_frame_prepare(const orbpl_camera* cam, const orbpl_keypoint* kps, int n,
+                         const float* depth, orbpl_keypoint* kps_un, float* depth_out,
+                         float* uright, int32_t* grid_cell, float* bounds);
+int oracle_search_by_projection_last(const orbpl_camera* cam, const float* scale_factors,
+                                     int nlevels, const orbpl_match_current* cur,
+                                     const orbpl_match_last* last, float th, int mono,
+                                     int check_ori, int32_t* match, int* nmatches_out);
+int oracle_pose_optimization(const orbpl_camera* cam, const orbpl_pose_problem* P, float* Tcw,
+                             uint8_t* outlier, uint8_t* line_outlier, int* n_inliers);
+void* oracle_vo_create(const orbpl_orb_params* orb, const orbpl_camera* cam, int n_streams);
+void oracle_vo_destroy(void* h);
+int oracle_vo_reset(void* h, const float* Tcw0);
+int oracle_vo_step(void* h, int stream, const uint8_t* gray, const float* depth, float* Tcw_out,
+                   int* out5);
 #ifdef __cplusplus
 }
 #endif

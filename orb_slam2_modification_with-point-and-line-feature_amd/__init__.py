@@ -283,3 +283,206 @@ def DescriptorDistance(a, b):
     a = np.ascontiguousarray(a, np.uint8)
     b = np.ascontiguousarray(b, np.uint8)
     return lib().orbpl_descriptor_distance(_ptr(a), _ptr(b))
+
+
+# ---------------------------------------------------------------------------
+# Frame glue / matcher / pose optimiser / tracker (include/orbpl.h)
+# ---------------------------------------------------------------------------
+class Camera(C.Structure):
+    """orbpl_camera: Camera.* settings (Examples/RGB-D/TUM1.yaml)."""
+    _fields_ = [("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float),
+                ("k1", C.c_float), ("k2", C.c_float), ("p1", C.c_float), ("p2", C.c_float),
+                ("k3", C.c_float), ("bf", C.c_float), ("th_depth", C.c_float),
+                ("width", C.c_int32), ("height", C.c_int32)]
+
+
+def make_camera(cfg):
+    """Camera from a settings dict (synth.TUM1 etc.); mThDepth = bf*ThDepth/fx
+    (Tracking.cc:134-138)."""
+    return Camera(cfg["fx"], cfg["fy"], cfg["cx"], cfg["cy"], cfg["k1"], cfg["k2"], cfg["p1"],
+                  cfg["p2"], cfg["k3"], cfg["bf"], cfg["bf"] * cfg["thdepth"] / cfg["fx"],
+                  cfg["width"], cfg["height"])
+
+
+class MatchCurrent(C.Structure):
+    _fields_ = [("n", C.c_int32), ("Tcw", C.c_void_p), ("kps_un", C.c_void_p),
+                ("desc", C.c_void_p), ("uright", C.c_void_p)]
+
+
+class MatchLast(C.Structure):
+    _fields_ = [("n", C.c_int32), ("Tcw", C.c_void_p), ("kps_un", C.c_void_p),
+                ("has_mp", C.c_void_p), ("outlier", C.c_void_p), ("mp_xyz", C.c_void_p),
+                ("mp_desc", C.c_void_p), ("mp_nobs", C.c_void_p)]
+
+
+class PoseProblem(C.Structure):
+    _fields_ = [("n", C.c_int32), ("kps_un", C.c_void_p), ("uright", C.c_void_p),
+                ("has_mp", C.c_void_p), ("mp_xyz", C.c_void_p), ("nl", C.c_int32),
+                ("kl_obs", C.c_void_p), ("kl_octave", C.c_void_p), ("has_ml", C.c_void_p),
+                ("ml_xyz", C.c_void_p), ("inv_sigma2", C.c_void_p), ("nlevels", C.c_int32)]
+
+
+def _declare_track(L):
+    vp, i, ip = C.c_void_p, C.c_int, C.POINTER(C.c_int)
+    L.orbpl_frame_prepare.argtypes = [vp, vp, i, vp, vp, vp, vp, vp, vp]
+    L.orbm_search_by_projection_last.argtypes = [vp, vp, i, vp, vp, C.c_float, i, i, vp, ip]
+    L.orbpl_pose_optimization.argtypes = [vp, vp, vp, vp, vp, ip]
+    L.orbpl_tracker_create.argtypes = [vp, vp, i, i, C.POINTER(vp)]
+    L.orbpl_tracker_destroy.argtypes = [vp]
+    L.orbpl_tracker_reset.argtypes = [vp, vp]
+    L.orbpl_tracker_step.argtypes = [vp, vp, vp]
+    L.orbpl_tracker_synchronize.argtypes = [vp]
+    L.orbpl_tracker_get_state.argtypes = [vp, vp, vp, vp, vp, vp]
+    L.orbpl_tracker_stage_ms.argtypes = [vp, vp]
+    L.orbpl_tracker_kp_capacity.argtypes = [vp]
+    L.orbpl_tracker_get_frame.argtypes = [vp, i, vp, vp, vp, vp, ip]
+
+
+_declare_orig = _declare
+
+
+def _declare(L):  # noqa: F811
+    _declare_orig(L)
+    _declare_track(L)
+
+
+def _c(a, dt):
+    return np.ascontiguousarray(a, dtype=dt)
+
+
+def frame_prepare(camera, kps, depth=None):
+    """Frame glue of the RGB-D Frame constructor (Frame.cc:135-205) on the GPU.
+    Returns (kps_un, depth, uright, grid_cell, bounds)."""
+    kps = _c(kps, KP_DTYPE)
+    n = len(kps)
+    ku = np.zeros(n, KP_DTYPE)
+    d = np.zeros(n, np.float32)
+    ur = np.zeros(n, np.float32)
+    gc = np.zeros(n, np.int32)
+    b = np.zeros(4, np.float32)
+    dp = None if depth is None else _c(depth, np.float32)
+    check(lib().orbpl_frame_prepare(C.byref(camera), _ptr(kps), n,
+                                    None if dp is None else _ptr(dp), _ptr(ku), _ptr(d), _ptr(ur),
+                                    _ptr(gc), _ptr(b)), "orbpl_frame_prepare")
+    return ku, d, ur, gc, b
+
+
+class ORBmatcher:
+    """ORB_SLAM2::ORBmatcher(nnratio, checkOri) — per-frame SearchByProjection."""
+
+    def __init__(self, nnratio=0.6, checkOri=True):
+        self.nnratio, self.checkOri = nnratio, checkOri
+
+    def SearchByProjectionLastFrame(self, camera, scale_factors, cur, last, th, bMono=False):
+        """SearchByProjection(CurrentFrame, LastFrame, th, bMono)
+        (ORBmatcher.cc:1710-1879). ``cur``/``last`` are dicts of arrays (see
+        tests). Returns (match, nmatches): match[i] = last-frame index or -1."""
+        sf = _c(scale_factors, np.float32)
+        keep = []
+
+        def arr(a, dt):
+            a = _c(a, dt)
+            keep.append(a)
+            return _ptr(a)
+
+        mc = MatchCurrent(len(cur["kps_un"]), arr(cur["Tcw"], np.float32),
+                          arr(cur["kps_un"], KP_DTYPE), arr(cur["desc"], np.uint8),
+                          arr(cur["uright"], np.float32))
+        ml = MatchLast(len(last["kps_un"]), arr(last["Tcw"], np.float32),
+                       arr(last["kps_un"], KP_DTYPE), arr(last["has_mp"], np.uint8),
+                       arr(last["outlier"], np.uint8), arr(last["mp_xyz"], np.float32),
+                       arr(last["mp_desc"], np.uint8), arr(last["mp_nobs"], np.int32))
+        match = np.zeros(max(1, mc.n), np.int32)
+        nm = C.c_int(0)
+        check(lib().orbm_search_by_projection_last(C.byref(camera), _ptr(sf), len(sf),
+                                                   C.byref(mc), C.byref(ml), float(th),
+                                                   int(bMono), int(self.checkOri), _ptr(match),
+                                                   C.byref(nm)), "orbm_search_by_projection_last")
+        return match[:mc.n].copy(), nm.value
+
+
+def pose_optimization(camera, prob, Tcw, outlier, line_outlier=None):
+    """Optimizer::PoseOptimization[WithLines] (Optimizer.cc:375-619, 2132-2486).
+    ``prob``: dict of arrays. Returns (Tcw, outlier, line_outlier, n_inliers)."""
+    keep = []
+
+    def arr(a, dt):
+        a = _c(a, dt)
+        keep.append(a)
+        return _ptr(a)
+
+    n = len(prob["kps_un"])
+    nl = len(prob.get("kl_obs", ()))
+    isg = _c(prob["inv_sigma2"], np.float32)
+    P = PoseProblem(n, arr(prob["kps_un"], KP_DTYPE), arr(prob["uright"], np.float32),
+                    arr(prob["has_mp"], np.uint8), arr(prob["mp_xyz"], np.float32), nl,
+                    arr(prob.get("kl_obs", np.zeros((0, 4))), np.float32),
+                    arr(prob.get("kl_octave", np.zeros(0)), np.int32),
+                    arr(prob.get("has_ml", np.zeros(0)), np.uint8),
+                    arr(prob.get("ml_xyz", np.zeros((0, 6))), np.float32), _ptr(isg), len(isg))
+    T = _c(Tcw, np.float32).copy()
+    out = _c(outlier, np.uint8).copy()
+    lout = _c(line_outlier if line_outlier is not None else np.zeros(nl), np.uint8).copy()
+    nin = C.c_int(0)
+    check(lib().orbpl_pose_optimization(C.byref(camera), C.byref(P), _ptr(T), _ptr(out),
+                                        _ptr(lout), C.byref(nin)), "orbpl_pose_optimization")
+    return T, out, lout, nin.value
+
+
+class Tracker:
+    """Batched RGB-D tracker (orbpl_tracker_*): one TrackWithMotionModel step
+    for n_streams independent streams per call."""
+
+    def __init__(self, orb_params, camera, n_streams, device=0):
+        h = C.c_void_p()
+        self.camera, self.S, self.device = camera, n_streams, device
+        check(lib().orbpl_tracker_create(C.byref(orb_params), C.byref(camera), n_streams, device,
+                                         C.byref(h)), "orbpl_tracker_create")
+        self._h = h
+        self.kp_cap = lib().orbpl_tracker_kp_capacity(h)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().orbpl_tracker_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reset(self, Tcw0=None):
+        T = None if Tcw0 is None else _c(Tcw0, np.float32)
+        check(lib().orbpl_tracker_reset(self._h, None if T is None else _ptr(T)), "reset")
+
+    def step_device(self, d_gray, d_depth):
+        check(lib().orbpl_tracker_step(self._h, C.c_void_p(d_gray), C.c_void_p(d_depth)), "step")
+
+    def synchronize(self):
+        check(lib().orbpl_tracker_synchronize(self._h), "orbpl_tracker_synchronize")
+
+    def state(self):
+        S = self.S
+        T = np.zeros((S, 4, 4), np.float32)
+        nk, nm, ni, nmm = (np.zeros(S, np.int32) for _ in range(4))
+        check(lib().orbpl_tracker_get_state(self._h, _ptr(T), _ptr(nk), _ptr(nm), _ptr(ni),
+                                            _ptr(nmm)), "orbpl_tracker_get_state")
+        return dict(Tcw=T, nkeypoints=nk, nmatches=nm, ninliers=ni, nmatches_map=nmm)
+
+    def stage_ms(self):
+        ms = np.zeros(5, np.float32)
+        check(lib().orbpl_tracker_stage_ms(self._h, _ptr(ms)), "orbpl_tracker_stage_ms")
+        return ms
+
+    def frame(self, stream):
+        K = self.kp_cap
+        ku = np.zeros(K, KP_DTYPE)
+        d = np.zeros((K, 32), np.uint8)
+        m = np.zeros(K, np.int32)
+        o = np.zeros(K, np.uint8)
+        n = C.c_int(0)
+        check(lib().orbpl_tracker_get_frame(self._h, stream, _ptr(ku), _ptr(d), _ptr(m), _ptr(o),
+                                            C.byref(n)), "orbpl_tracker_get_frame")
+        k = n.value
+        return ku[:k], d[:k], m[:k], o[:k]

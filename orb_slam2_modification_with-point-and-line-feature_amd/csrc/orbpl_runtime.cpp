@@ -272,6 +272,8 @@ int orbx_describe(const orbpl_orb_params* p, int width, int height, int* lw, int
 }  // extern "C"
 
 namespace orbpl {
+hipStream_t orbx_stream(orbx_ctx* c) { return c->stream; }
+
 // Whole extraction pipeline on the ctx stream; images already in device memory.
 int orbx_run(orbx_ctx* c, const uint8_t* d_imgs, int batch, int stride, long long frame_pitch,
              orbpl_keypoint_dev* d_kps, uint8_t* d_desc, int kp_pitch, int* d_n) {

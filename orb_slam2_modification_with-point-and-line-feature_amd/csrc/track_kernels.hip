@@ -1,0 +1,1254 @@
+// Per-frame tracking kernels for gfx950: everything Tracking::TrackWithMotionModel
+// (Tracking.cc:1212-1330) runs on the current frame after extraction, for a
+// batch of independent streams (one workgroup per stream where the reference
+// is sequential inside a frame).
+//
+//   k_frame_prepare : Frame glue (Frame.cc:135-205 RGB-D constructor body):
+//                     UndistortKeyPoints, ComputeStereoFromRGBD, PosInGrid
+//   k_predict       : mCurrentFrame.SetPose(mVelocity * mLastFrame.mTcw)
+//   k_match_last    : ORBmatcher::SearchByProjection(Frame&, const Frame&, th,
+//                     bMono) (ORBmatcher.cc:1710-1879) incl. the rotation
+//                     histogram, plus the 2*th retry of TrackWithMotionModel
+//   k_pose          : Optimizer::PoseOptimization[WithLines] (Optimizer.cc:
+//                     375-619, 2132-2486) — the whole 4 x 10 LM loop on device
+//   k_finish        : discard outliers, velocity update (Tracking.cc:479-484),
+//                     and the next frame's map points (StereoInitialization-
+//                     style keyframe: every keypoint with depth, Tracking.cc:
+//                     608-660 / Frame::UnprojectStereo)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "orbpl_math.h"
+#include "track_common.h"
+#include "track_kernels.h"
+
+namespace orbpl {
+
+// ---------------------------------------------------------------------------
+// Frame glue: one thread per keypoint.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_frame_prepare(TrackConsts c, const KeyPointD* __restrict__ kps,
+                                                       const int* __restrict__ n_in, int kp_pitch,
+                                                       const float* __restrict__ depth,
+                                                       long long depth_pitch,
+                                                       KeyPointD* __restrict__ kps_un,
+                                                       float* __restrict__ depth_out,
+                                                       float* __restrict__ uright,
+                                                       int* __restrict__ gcell) {
+  const int f = blockIdx.y;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int n = n_in[f];
+  if (i >= n) return;
+  const long long o = (long long)f * kp_pitch + i;
+  KeyPointD k = kps[o];
+  KeyPointD u = k;
+  if (c.k1 != 0.0f) undistort_point_d(c, k.x, k.y, &u.x, &u.y);
+  kps_un[o] = u;
+  float d_out = -1.f, ur = -1.f;
+  if (depth) {
+    const int v = (int)k.y, uu = (int)k.x;
+    const float d = depth[(long long)f * depth_pitch + (long long)v * c.width + uu];
+    if (d > 0) {
+      d_out = d;
+      ur = u.x - c.bf / d;
+    }
+  }
+  depth_out[o] = d_out;
+  uright[o] = ur;
+  const int px = (int)roundf((u.x - c.minX) * c.gridInvW);
+  const int py = (int)roundf((u.y - c.minY) * c.gridInvH);
+  gcell[o] = (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) ? -1 : px + kGridCols * py;
+}
+
+// ---------------------------------------------------------------------------
+// Constant-velocity prediction (Tracking.cc:1228). One thread per stream.
+// ---------------------------------------------------------------------------
+__global__ void k_predict(StreamState* __restrict__ st, int nstreams) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nstreams) return;
+  StreamState& S = st[s];
+  if (!S.has_last) return;
+  if (S.has_velocity) {
+    float Twl[16], V[16];
+    pose_inverse(S.Tlast2, Twl);
+    gemm44(S.Tlast, Twl, V);       // mVelocity = Tcw(t-1) * Twc(t-2)
+    gemm44(V, S.Tlast, S.Tcw);     // SetPose(mVelocity * mLastFrame.mTcw)
+  } else {
+    for (int k = 0; k < 16; k++) S.Tcw[k] = S.Tlast[k];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// SearchByProjection(CurrentFrame, LastFrame): one 256-thread workgroup per
+// stream. The current frame's 64x48 grid is rebuilt in LDS (stable counting
+// sort = the reference's mGrid cell vectors in index order).
+//   Phase A (parallel over last-frame map points): projection, window and the
+//     unconstrained best candidate: min (distance, grid-scan order).
+//   Phase B (wave 0, ordered): the reference skips candidates already taken by
+//     a map point with Observations() > 0 earlier in the loop. Chunks of 64
+//     points are accepted at once when no point's best is taken by an earlier
+//     one; otherwise the chunk is replayed point by point with re-scans.
+//   Phase C: rotation histogram, ComputeThreeMaxima, removal.
+// ---------------------------------------------------------------------------
+struct MatchShared {
+  int cell_start[kGridCols * kGridRows + 1];
+  int cell_fill[kGridCols * kGridRows];
+  uint16_t items[kMatchMaxKp];
+  float2 xy[kMatchMaxKp];
+  float ur[kMatchMaxKp];
+  float ang[kMatchMaxKp];
+  int8_t oct[kMatchMaxKp];
+  int16_t gc[kMatchMaxKp];        // grid cell (PosInGrid) or -1
+  int best[kMatchMaxKp];          // phase A: (dist << 16 | idx) or -1; later: final candidate
+  int bin[kMatchMaxKp];           // accepted -> histogram bin, else -1
+  int mpw[kMatchMaxKp];           // last writer (last-frame index) per current keypoint
+  uint32_t claimed[kMatchMaxKp / 32];
+  uint32_t removed[kMatchMaxKp / 32];
+  int hist[32];
+  int chunk_cell[256];
+  int wsum[8];
+  int misc[8];
+};
+
+struct MatchArgs {
+  // current frame (per stream pitch kp_pitch)
+  const KeyPointD* cur_kps_un;
+  const uint8_t* cur_desc;
+  const float* cur_uright;
+  const int* cur_gcell;
+  const int* cur_n;
+  // last frame
+  const KeyPointD* last_kps_un;
+  const uint8_t* last_has_mp;
+  const uint8_t* last_outlier;
+  const float* last_xyz;
+  const uint8_t* last_desc;     // map point descriptors
+  const int* last_nobs;
+  const int* last_n;
+  int kp_pitch;
+  // poses
+  const float* Tcw;             // per stream 16 floats (stride pose_stride floats)
+  const float* Tlw;
+  int pose_stride;
+  // outputs
+  int* match;                   // per stream kp_pitch
+  int* nmatches;                // per stream (stride nm_stride ints)
+  int nm_stride;
+  float th;
+  int mono;
+  int check_ori;
+  int retry;                    // TrackWithMotionModel: if nmatches < 20 redo with 2*th
+  const StreamState* active;    // optional: skip streams without a last frame
+};
+
+__device__ __forceinline__ int hamming32(const uint8_t* a, const uint8_t* b) {
+  const uint4 a0 = *reinterpret_cast<const uint4*>(a);
+  const uint4 a1 = *reinterpret_cast<const uint4*>(a + 16);
+  const uint4 b0 = *reinterpret_cast<const uint4*>(b);
+  const uint4 b1 = *reinterpret_cast<const uint4*>(b + 16);
+  return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+         __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
+struct ProjInfo {
+  bool ok;
+  float u, v, invzc, radius;
+  int minLevel, maxLevel;
+  int cx0, cx1, cy0, cy1;
+};
+
+__device__ __forceinline__ ProjInfo project_point(const TrackConsts& c, const float* Tc,
+                                                  const float* X, int nLastOctave, float th,
+                                                  bool bForward, bool bBackward) {
+  ProjInfo p;
+  p.ok = false;
+  float x3Dc[3];
+  gemm_R_x_plus_t(Tc, X, x3Dc);
+  const float xc = x3Dc[0], yc = x3Dc[1];
+  const float invzc = (float)(1.0 / (double)x3Dc[2]);
+  if (invzc < 0) return p;
+  const float u = c.fx * xc * invzc + c.cx;
+  const float v = c.fy * yc * invzc + c.cy;
+  if (u < c.minX || u > c.maxX) return p;
+  if (v < c.minY || v > c.maxY) return p;
+  p.u = u;
+  p.v = v;
+  p.invzc = invzc;
+  p.radius = th * c.scale[nLastOctave];
+  if (bForward) {
+    p.minLevel = nLastOctave;
+    p.maxLevel = -1;
+  } else if (bBackward) {
+    p.minLevel = 0;
+    p.maxLevel = nLastOctave;
+  } else {
+    p.minLevel = nLastOctave - 1;
+    p.maxLevel = nLastOctave + 1;
+  }
+  const float r = p.radius;
+  p.cx0 = max(0, (int)floorf((u - c.minX - r) * c.gridInvW));
+  p.cx1 = min(kGridCols - 1, (int)ceilf((u - c.minX + r) * c.gridInvW));
+  p.cy0 = max(0, (int)floorf((v - c.minY - r) * c.gridInvH));
+  p.cy1 = min(kGridRows - 1, (int)ceilf((v - c.minY + r) * c.gridInvH));
+  if (p.cx0 >= kGridCols || p.cx1 < 0 || p.cy0 >= kGridRows || p.cy1 < 0) return p;
+  p.ok = true;
+  return p;
+}
+
+// Frame::GetFeaturesInArea + the best-candidate loop (ORBmatcher.cc:1789-1826).
+// Returns (dist << 16) | idx of the first minimum in scan order, or -1.
+__device__ int scan_best(const MatchShared& S, const TrackConsts& c, const ProjInfo& p,
+                         const uint8_t* dMP, const uint8_t* cur_desc, bool use_claims,
+                         float mbf) {
+  int bestDist = 256, bestIdx = -1;
+  const bool bCheckLevels = (p.minLevel > 0) || (p.maxLevel >= 0);
+  const float r = p.radius;
+  for (int ix = p.cx0; ix <= p.cx1; ix++) {
+    for (int iy = p.cy0; iy <= p.cy1; iy++) {
+      const int cell = ix + kGridCols * iy;
+      const int b = S.cell_start[cell], e = S.cell_start[cell + 1];
+      for (int q = b; q < e; q++) {
+        const int j = S.items[q];
+        const int oc = S.oct[j];
+        if (bCheckLevels) {
+          if (oc < p.minLevel) continue;
+          if (p.maxLevel >= 0 && oc > p.maxLevel) continue;
+        }
+        const float2 xy = S.xy[j];
+        const float distx = xy.x - p.u, disty = xy.y - p.v;
+        if (!(fabsf(distx) < r && fabsf(disty) < r)) continue;
+        if (use_claims && ((S.claimed[j >> 5] >> (j & 31)) & 1u)) continue;
+        const float urj = S.ur[j];
+        if (urj > 0) {
+          const float ur = p.u - mbf * p.invzc;
+          const float er = fabsf(ur - urj);
+          if (er > p.radius) continue;
+        }
+        const int dist = hamming32(dMP, cur_desc + (long long)j * 32);
+        if (dist < bestDist) {
+          bestDist = dist;
+          bestIdx = j;
+        }
+      }
+    }
+  }
+  return bestIdx < 0 ? -1 : ((bestDist << 16) | bestIdx);
+}
+
+__global__ void __launch_bounds__(256) k_match_last(TrackConsts c, MatchArgs a) {
+  extern __shared__ char smem_raw[];
+  MatchShared& S = *reinterpret_cast<MatchShared*>(smem_raw);
+  const int s = blockIdx.x, t = threadIdx.x;
+  const int wave = t >> 6, lane = t & 63;
+  if (a.active && !a.active[s].has_last) {
+    if (t == 0) a.nmatches[(long long)s * a.nm_stride] = 0;
+    for (int i = t; i < a.cur_n[s]; i += 256) a.match[(long long)s * a.kp_pitch + i] = -1;
+    return;
+  }
+  const int n = min(a.cur_n[s], kMatchMaxKp);
+  const int nl = min(a.last_n[s], kMatchMaxKp);
+  const long long cb = (long long)s * a.kp_pitch;
+  const KeyPointD* ck = a.cur_kps_un + cb;
+  const uint8_t* cdesc = a.cur_desc + cb * 32;
+  const float* Tc = a.Tcw + (long long)s * a.pose_stride;
+  const float* Tl = a.Tlw + (long long)s * a.pose_stride;
+  // ---- current frame into LDS + grid (AssignFeaturesToGrid, Frame.cc:265-287) ----
+  for (int i = t; i < kGridCols * kGridRows; i += 256) {
+    S.cell_start[i] = 0;
+    S.cell_fill[i] = 0;
+  }
+  __syncthreads();
+  for (int i = t; i < n; i += 256) {
+    const KeyPointD k = ck[i];
+    S.xy[i] = make_float2(k.x, k.y);
+    S.ang[i] = k.angle;
+    S.oct[i] = (int8_t)k.octave;
+    S.ur[i] = a.cur_uright[cb + i];
+    int g;
+    if (a.cur_gcell) {
+      g = a.cur_gcell[cb + i];
+    } else {  // Frame::PosInGrid (Frame.cc:527-538)
+      const int px = (int)roundf((k.x - c.minX) * c.gridInvW);
+      const int py = (int)roundf((k.y - c.minY) * c.gridInvH);
+      g = (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) ? -1 : px + kGridCols * py;
+    }
+    S.gc[i] = (int16_t)g;
+    if (g >= 0) atomicAdd(&S.cell_start[g], 1);
+  }
+  __syncthreads();
+  // exclusive scan of 3072 cell counts (12 per thread)
+  {
+    constexpr int kPer = (kGridCols * kGridRows) / 256;
+    int loc[kPer];
+    int sum = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+      loc[k] = S.cell_start[t * kPer + k];
+      sum += loc[k];
+    }
+    int incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      int u = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += u;
+    }
+    if (lane == 63) S.wsum[wave] = incl;
+    __syncthreads();
+    int base = 0;
+    for (int w = 0; w < wave; w++) base += S.wsum[w];
+    int run = base + incl - sum;
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+      S.cell_start[t * kPer + k] = run;
+      run += loc[k];
+    }
+    if (t == 255) S.cell_start[kGridCols * kGridRows] = run;
+    __syncthreads();
+  }
+  // stable placement in index order, 256 keypoints per chunk
+  for (int base = 0; base < n; base += 256) {
+    const int i = base + t;
+    const int g = i < n ? (int)S.gc[i] : -1;
+    S.chunk_cell[t] = g;
+    __syncthreads();
+    if (g >= 0) {
+      int rank = 0;
+      for (int q = 0; q < t; q++) rank += (S.chunk_cell[q] == g);
+      S.items[S.cell_start[g] + S.cell_fill[g] + rank] = (uint16_t)i;
+    }
+    __syncthreads();
+    if (g >= 0) atomicAdd(&S.cell_fill[g], 1);
+    __syncthreads();
+  }
+  // ---- forward/backward motion (ORBmatcher.cc:1724-1744) ----
+  float twc[3], tlc[3];
+  gemm_neg_Rt_t(Tc, twc);
+  gemm_R_x_plus_t(Tl, twc, tlc);
+  const bool bForward = tlc[2] > c.mb && !a.mono;
+  const bool bBackward = -tlc[2] > c.mb && !a.mono;
+  const float mbf = c.bf;
+  float th = a.th;
+  int nmatches = 0;
+  for (int attempt = 0; attempt < 2; attempt++) {
+    // ---- phase A ----
+    for (int i = t; i < nl; i += 256) {
+      int res = -1;
+      const long long li = cb + i;
+      if (a.last_has_mp[li] && !a.last_outlier[li]) {
+        const ProjInfo p = project_point(c, Tc, a.last_xyz + li * 3, a.last_kps_un[li].octave, th,
+                                         bForward, bBackward);
+        if (p.ok) res = scan_best(S, c, p, a.last_desc + li * 32, cdesc, false, mbf);
+      }
+      S.best[i] = res;
+    }
+    for (int i = t; i < n; i += 256) S.mpw[i] = -1;
+    for (int i = t; i < kMatchMaxKp / 32; i += 256) {
+      S.claimed[i] = 0;
+      S.removed[i] = 0;
+    }
+    if (t < 32) S.hist[t] = 0;
+    __syncthreads();
+    // ---- phase B (wave 0, in last-frame index order) ----
+    if (wave == 0) {
+      int acc = 0;
+      for (int base = 0; base < nl; base += 64) {
+        const int i = base + lane;
+        const long long li = cb + i;
+        int bst = -1;
+        bool claimer = false;
+        if (i < nl) {
+          bst = S.best[i];
+          if (bst >= 0 && (bst >> 16) <= 100) claimer = a.last_nobs[li] > 0;
+          else bst = -1;
+        }
+        const int k = bst >= 0 ? (bst & 0xFFFF) : -1;
+        bool conflict = k >= 0 && ((S.claimed[k >> 5] >> (k & 31)) & 1u);
+        for (int q = 0; q < 64; q++) {
+          const int kq = __shfl(k, q, 64);
+          const int cq = __shfl((int)claimer, q, 64);
+          if (q < lane && cq && kq == k && k >= 0) conflict = true;
+        }
+        if (__ballot(conflict) == 0ull) {
+          if (i < nl) {
+            if (k >= 0) {
+              atomicMax(&S.mpw[k], i);
+              if (claimer) atomicOr(&S.claimed[k >> 5], 1u << (k & 31));
+              // histogram bin (ORBmatcher.cc:1835-1845)
+              float rot = a.last_kps_un[li].angle - S.ang[k];
+              if (rot < 0.0f) rot += 360.0f;
+              int b = (int)roundf(rot * (30 / 360.0f));
+              if (b == 30) b = 0;
+              S.bin[i] = b;
+              S.best[i] = k;
+            } else {
+              S.bin[i] = -1;
+            }
+          }
+          acc += __popcll(__ballot(k >= 0));
+        } else {
+          // replay this chunk point by point (lane 0)
+          if (lane == 0) {
+            for (int q = 0; q < 64 && base + q < nl; q++) {
+              const int ii = base + q;
+              const long long lii = cb + ii;
+              int r = S.best[ii];
+              if (r >= 0 && (r >> 16) <= 100) {
+                const int kk = r & 0xFFFF;
+                if ((S.claimed[kk >> 5] >> (kk & 31)) & 1u) {
+                  const ProjInfo p = project_point(c, Tc, a.last_xyz + lii * 3,
+                                                   a.last_kps_un[lii].octave, th, bForward,
+                                                   bBackward);
+                  r = scan_best(S, c, p, a.last_desc + lii * 32, cdesc, true, mbf);
+                }
+              } else if (r >= 0) {
+                r = -1;  // best > TH_HIGH without claims: still > TH_HIGH with claims
+              }
+              if (r >= 0 && (r >> 16) <= 100) {
+                const int kk = r & 0xFFFF;
+                S.mpw[kk] = ii;
+                if (a.last_nobs[lii] > 0) S.claimed[kk >> 5] |= 1u << (kk & 31);
+                float rot = a.last_kps_un[lii].angle - S.ang[kk];
+                if (rot < 0.0f) rot += 360.0f;
+                int b = (int)roundf(rot * (30 / 360.0f));
+                if (b == 30) b = 0;
+                S.bin[ii] = b;
+                S.best[ii] = kk;
+                acc++;
+              } else {
+                S.bin[ii] = -1;
+              }
+            }
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+      if (lane == 0) S.misc[0] = acc;
+    }
+    __syncthreads();
+    nmatches = S.misc[0];
+    // ---- phase C: rotation consistency (ORBmatcher.cc:1850-1876, 2035-2077) ----
+    if (a.check_ori) {
+      for (int i = t; i < nl; i += 256)
+        if (S.bin[i] >= 0) atomicAdd(&S.hist[S.bin[i]], 1);
+      __syncthreads();
+      if (t == 0) {
+        int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+        for (int i = 0; i < 30; i++) {
+          const int sz = S.hist[i];
+          if (sz > max1) {
+            max3 = max2; max2 = max1; max1 = sz; ind3 = ind2; ind2 = ind1; ind1 = i;
+          } else if (sz > max2) {
+            max3 = max2; max2 = sz; ind3 = ind2; ind2 = i;
+          } else if (sz > max3) {
+            max3 = sz; ind3 = i;
+          }
+        }
+        if (max2 < 0.1f * (float)max1) {
+          ind2 = -1; ind3 = -1;
+        } else if (max3 < 0.1f * (float)max1) {
+          ind3 = -1;
+        }
+        S.misc[1] = ind1; S.misc[2] = ind2; S.misc[3] = ind3;
+        S.misc[4] = 0;
+      }
+      __syncthreads();
+      const int ind1 = S.misc[1], ind2 = S.misc[2], ind3 = S.misc[3];
+      int nrem = 0;
+      for (int i = t; i < nl; i += 256) {
+        const int b = S.bin[i];
+        if (b >= 0 && b != ind1 && b != ind2 && b != ind3) {
+          const int k = S.best[i];
+          atomicOr(&S.removed[k >> 5], 1u << (k & 31));
+          nrem++;
+        }
+      }
+      if (nrem) atomicAdd(&S.misc[4], nrem);
+      __syncthreads();
+      nmatches -= S.misc[4];
+    }
+    if (!(a.retry && nmatches < 20 && attempt == 0)) break;
+    th = 2 * a.th;
+    __syncthreads();
+  }
+  for (int i = t; i < n; i += 256) {
+    int m = S.mpw[i];
+    if (a.check_ori && ((S.removed[i >> 5] >> (i & 31)) & 1u)) m = -1;
+    a.match[cb + i] = m;
+  }
+  if (t == 0) a.nmatches[(long long)s * a.nm_stride] = nmatches;
+}
+
+// ---------------------------------------------------------------------------
+// Pose-only Levenberg-Marquardt, one workgroup per stream; all of g2o's
+// control flow (optimization_algorithm_levenberg.cpp:61-164) runs on device,
+// thread 0 solves the 6x6 system and updates the SE3 estimate; H, b and chi2
+// are block reductions in double.
+// ---------------------------------------------------------------------------
+struct Quat { double w, x, y, z; };
+struct SE3d { Quat q; double t[3]; };
+
+__device__ __forceinline__ void normalize_rotation(Quat& q) {
+  if (q.w < 0) { q.w = -q.w; q.x = -q.x; q.y = -q.y; q.z = -q.z; }
+  const double n = sqrt(q.w * q.w + q.x * q.x + q.y * q.y + q.z * q.z);
+  q.w /= n; q.x /= n; q.y /= n; q.z /= n;
+}
+__device__ Quat quat_from_R(const double m[3][3]) {
+  Quat q;
+  double t = m[0][0] + m[1][1] + m[2][2];
+  if (t > 0) {
+    t = sqrt(t + 1.0);
+    q.w = 0.5 * t;
+    t = 0.5 / t;
+    q.x = (m[2][1] - m[1][2]) * t;
+    q.y = (m[0][2] - m[2][0]) * t;
+    q.z = (m[1][0] - m[0][1]) * t;
+  } else {
+    int i = 0;
+    if (m[1][1] > m[0][0]) i = 1;
+    if (m[2][2] > m[i][i]) i = 2;
+    const int j = (i + 1) % 3, k = (j + 1) % 3;
+    t = sqrt(m[i][i] - m[j][j] - m[k][k] + 1.0);
+    double v[3];
+    v[i] = 0.5 * t;
+    t = 0.5 / t;
+    q.w = (m[k][j] - m[j][k]) * t;
+    v[j] = (m[j][i] + m[i][j]) * t;
+    v[k] = (m[k][i] + m[i][k]) * t;
+    q.x = v[0]; q.y = v[1]; q.z = v[2];
+  }
+  return q;
+}
+__device__ __forceinline__ void quat_to_R(const Quat& q, double R[3][3]) {
+  const double tx = 2 * q.x, ty = 2 * q.y, tz = 2 * q.z;
+  const double twx = tx * q.w, twy = ty * q.w, twz = tz * q.w;
+  const double txx = tx * q.x, txy = ty * q.x, txz = tz * q.x;
+  const double tyy = ty * q.y, tyz = tz * q.y, tzz = tz * q.z;
+  R[0][0] = 1 - (tyy + tzz); R[0][1] = txy - twz; R[0][2] = txz + twy;
+  R[1][0] = txy + twz; R[1][1] = 1 - (txx + tzz); R[1][2] = tyz - twx;
+  R[2][0] = txz - twy; R[2][1] = tyz + twx; R[2][2] = 1 - (txx + tyy);
+}
+__device__ __forceinline__ void quat_rotate(const Quat& q, const double v[3], double o[3]) {
+  double uv[3] = {q.y * v[2] - q.z * v[1], q.z * v[0] - q.x * v[2], q.x * v[1] - q.y * v[0]};
+  uv[0] += uv[0]; uv[1] += uv[1]; uv[2] += uv[2];
+  const double c[3] = {q.y * uv[2] - q.z * uv[1], q.z * uv[0] - q.x * uv[2], q.x * uv[1] - q.y * uv[0]};
+  o[0] = v[0] + q.w * uv[0] + c[0];
+  o[1] = v[1] + q.w * uv[1] + c[1];
+  o[2] = v[2] + q.w * uv[2] + c[2];
+}
+__device__ SE3d se3_exp(const double u[6]) {
+  const double w0 = u[0], w1 = u[1], w2 = u[2];
+  const double theta = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
+  const double O[3][3] = {{0, -w2, w1}, {w2, 0, -w0}, {-w1, w0, 0}};
+  double O2[3][3];
+  for (int r = 0; r < 3; r++)
+    for (int cc = 0; cc < 3; cc++) O2[r][cc] = O[r][0] * O[0][cc] + O[r][1] * O[1][cc] + O[r][2] * O[2][cc];
+  double R[3][3], V[3][3];
+  if (theta < 0.00001) {
+    for (int r = 0; r < 3; r++)
+      for (int cc = 0; cc < 3; cc++) {
+        R[r][cc] = (r == cc ? 1.0 : 0.0) + O[r][cc] + O2[r][cc];
+        V[r][cc] = R[r][cc];
+      }
+  } else {
+    const double a = sin(theta) / theta;
+    const double b = (1 - cos(theta)) / (theta * theta);
+    const double c3 = (theta - sin(theta)) / (theta * theta * theta);
+    for (int r = 0; r < 3; r++)
+      for (int cc = 0; cc < 3; cc++) {
+        R[r][cc] = (r == cc ? 1.0 : 0.0) + a * O[r][cc] + b * O2[r][cc];
+        V[r][cc] = (r == cc ? 1.0 : 0.0) + b * O[r][cc] + c3 * O2[r][cc];
+      }
+  }
+  SE3d s;
+  s.q = quat_from_R(R);
+  normalize_rotation(s.q);
+  for (int r = 0; r < 3; r++) s.t[r] = V[r][0] * u[3] + V[r][1] * u[4] + V[r][2] * u[5];
+  return s;
+}
+__device__ SE3d se3_mul(const SE3d& a, const SE3d& b) {
+  SE3d r = a;
+  double rt[3];
+  quat_rotate(a.q, b.t, rt);
+  r.t[0] += rt[0]; r.t[1] += rt[1]; r.t[2] += rt[2];
+  Quat q;
+  q.w = a.q.w * b.q.w - a.q.x * b.q.x - a.q.y * b.q.y - a.q.z * b.q.z;
+  q.x = a.q.w * b.q.x + a.q.x * b.q.w + a.q.y * b.q.z - a.q.z * b.q.y;
+  q.y = a.q.w * b.q.y + a.q.y * b.q.w + a.q.z * b.q.x - a.q.x * b.q.z;
+  q.z = a.q.w * b.q.z + a.q.z * b.q.w + a.q.x * b.q.y - a.q.y * b.q.x;
+  normalize_rotation(q);
+  r.q = q;
+  return r;
+}
+
+struct PoseEdge {
+  float obs[4];   // mono: u,v ; stereo: u,v,ur ; line: sx,sy,ex,ey
+  float X[6];     // point: Xw ; line: world start, end
+  float info;
+  int kind;       // 0 mono, 1 stereo, 2 line
+  int idx;        // frame index
+  int pad;
+};
+
+struct PoseShared {
+  double chi2[kPoseMaxEdges];     // chi2 of the last computed error (stale semantics)
+  uint8_t level[kPoseMaxEdges];
+  uint8_t out_flag[kPoseMaxEdges];
+  int scan[kPoseMaxEdges];
+  double red[4][32];
+  int wsum[8];
+  int misc[8];
+};
+
+struct PoseCam { double fx, fy, cx, cy, bf; };
+
+__device__ void edge_error(const PoseEdge& e, const PoseCam& c, const SE3d& T, const double R[3][3],
+                           double* err) {
+  if (e.kind == 2) {
+    double nw[3], vw[3];
+    const double sp[3] = {e.X[0], e.X[1], e.X[2]}, ep[3] = {e.X[3], e.X[4], e.X[5]};
+    nw[0] = sp[1] * ep[2] - sp[2] * ep[1];
+    nw[1] = sp[2] * ep[0] - sp[0] * ep[2];
+    nw[2] = sp[0] * ep[1] - sp[1] * ep[0];
+    for (int k = 0; k < 3; k++) vw[k] = ep[k] - sp[k];
+    double Rn[3], Rv[3];
+    for (int r = 0; r < 3; r++) {
+      Rn[r] = R[r][0] * nw[0] + R[r][1] * nw[1] + R[r][2] * nw[2];
+      Rv[r] = R[r][0] * vw[0] + R[r][1] * vw[1] + R[r][2] * vw[2];
+    }
+    const double* t = T.t;
+    const double tRv[3] = {-t[2] * Rv[1] + t[1] * Rv[2], t[2] * Rv[0] - t[0] * Rv[2], -t[1] * Rv[0] + t[0] * Rv[1]};
+    const double nc[3] = {Rn[0] + tRv[0], Rn[1] + tRv[1], Rn[2] + tRv[2]};
+    const double l0 = c.fy * nc[0], l1 = c.fx * nc[1];
+    const double l2 = -c.fy * c.cx * nc[0] + -c.fx * c.cy * nc[1] + c.fx * c.fy * nc[2];
+    const double sq = sqrt(l0 * l0 + l1 * l1);
+    err[0] = ((double)e.obs[0] * l0 + (double)e.obs[1] * l1 + l2) / sq;
+    err[1] = ((double)e.obs[2] * l0 + (double)e.obs[3] * l1 + l2) / sq;
+    err[2] = 0;
+    return;
+  }
+  const double X[3] = {e.X[0], e.X[1], e.X[2]};
+  double p[3];
+  quat_rotate(T.q, X, p);
+  p[0] += T.t[0]; p[1] += T.t[1]; p[2] += T.t[2];
+  if (e.kind == 0) {
+    err[0] = (double)e.obs[0] - (p[0] / p[2] * c.fx + c.cx);
+    err[1] = (double)e.obs[1] - (p[1] / p[2] * c.fy + c.cy);
+    err[2] = 0;
+  } else {
+    const float invz = (float)(1.0 / p[2]);
+    const double u = p[0] * (double)invz * c.fx + c.cx;
+    const double v = p[1] * (double)invz * c.fy + c.cy;
+    err[0] = (double)e.obs[0] - u;
+    err[1] = (double)e.obs[1] - v;
+    err[2] = (double)e.obs[2] - (u - c.bf * (double)invz);
+  }
+}
+
+__device__ void edge_jacobian(const PoseEdge& e, const PoseCam& c, const SE3d& T,
+                              const double R[3][3], double J[3][6]) {
+  if (e.kind == 2) {
+    double nw[3], vw[3];
+    const double sp[3] = {e.X[0], e.X[1], e.X[2]}, ep[3] = {e.X[3], e.X[4], e.X[5]};
+    nw[0] = sp[1] * ep[2] - sp[2] * ep[1];
+    nw[1] = sp[2] * ep[0] - sp[0] * ep[2];
+    nw[2] = sp[0] * ep[1] - sp[1] * ep[0];
+    for (int k = 0; k < 3; k++) vw[k] = ep[k] - sp[k];
+    double Rn[3], Rv[3];
+    for (int r = 0; r < 3; r++) {
+      Rn[r] = R[r][0] * nw[0] + R[r][1] * nw[1] + R[r][2] * nw[2];
+      Rv[r] = R[r][0] * vw[0] + R[r][1] * vw[1] + R[r][2] * vw[2];
+    }
+    const double* t = T.t;
+    const double tRv[3] = {-t[2] * Rv[1] + t[1] * Rv[2], t[2] * Rv[0] - t[0] * Rv[2], -t[1] * Rv[0] + t[0] * Rv[1]};
+    const double nc[3] = {Rn[0] + tRv[0], Rn[1] + tRv[1], Rn[2] + tRv[2]};
+    const double l0 = c.fy * nc[0], l1 = c.fx * nc[1];
+    const double l2 = -c.fy * c.cx * nc[0] + -c.fx * c.cy * nc[1] + c.fx * c.fy * nc[2];
+    const double ln = sqrt(l0 * l0 + l1 * l1);
+    const double e2 = (double)e.obs[2] * l0 + (double)e.obs[3] * l1 + l2;
+    // pinned P7: row 0 = end-point values, row 1 = 0
+    const double d0 = ((double)e.obs[2] - (l0 * e2) / (ln * ln)) / ln;
+    const double d1 = ((double)e.obs[3] - (l1 * e2) / (ln * ln)) / ln;
+    const double M0[3] = {d0 * c.fy + 1.0 * (-c.fy * c.cx), d1 * c.fx + 1.0 * (c.fx * c.cy), 1.0 * (c.fx * c.fy)};
+    // D = [-S(Rv) - S(tRv) | -S(Rv)] (rows 0..2 of dLc_ddelta)
+    const double S1[3][3] = {{0, -Rv[2], Rv[1]}, {Rv[2], 0, -Rv[0]}, {-Rv[1], Rv[0], 0}};
+    const double S2[3][3] = {{0, -tRv[2], tRv[1]}, {tRv[2], 0, -tRv[0]}, {-tRv[1], tRv[0], 0}};
+    for (int k = 0; k < 3; k++) {
+      J[0][k] = M0[0] * (-1.0 * S1[0][k] - S2[0][k]) + M0[1] * (-1.0 * S1[1][k] - S2[1][k]) +
+                M0[2] * (-1.0 * S1[2][k] - S2[2][k]);
+      J[0][3 + k] = M0[0] * (-1.0 * S1[0][k]) + M0[1] * (-1.0 * S1[1][k]) + M0[2] * (-1.0 * S1[2][k]);
+      J[1][k] = 0.0;
+      J[1][3 + k] = 0.0;
+    }
+    return;
+  }
+  const double X[3] = {e.X[0], e.X[1], e.X[2]};
+  double p[3];
+  quat_rotate(T.q, X, p);
+  p[0] += T.t[0]; p[1] += T.t[1]; p[2] += T.t[2];
+  const double x = p[0], y = p[1], invz = 1.0 / p[2], invz_2 = invz * invz;
+  J[0][0] = x * y * invz_2 * c.fx;
+  J[0][1] = -(1 + (x * x * invz_2)) * c.fx;
+  J[0][2] = y * invz * c.fx;
+  J[0][3] = -invz * c.fx;
+  J[0][4] = 0;
+  J[0][5] = x * invz_2 * c.fx;
+  J[1][0] = (1 + y * y * invz_2) * c.fy;
+  J[1][1] = -x * y * invz_2 * c.fy;
+  J[1][2] = -x * invz * c.fy;
+  J[1][3] = 0;
+  J[1][4] = -invz * c.fy;
+  J[1][5] = y * invz_2 * c.fy;
+  if (e.kind == 1) {
+    J[2][0] = J[0][0] - c.bf * y * invz_2;
+    J[2][1] = J[0][1] + c.bf * x * invz_2;
+    J[2][2] = J[0][2];
+    J[2][3] = J[0][3];
+    J[2][4] = 0;
+    J[2][5] = J[0][5] - c.bf * invz_2;
+  } else {
+    for (int k = 0; k < 6; k++) J[2][k] = 0;
+  }
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Reduce NV doubles over the block; result valid in every thread.
+template <int NV>
+__device__ void block_sum(double* v, PoseShared& S) {
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+#pragma unroll
+  for (int k = 0; k < NV; k++) v[k] = wave_sum_d(v[k]);
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < NV; k++) S.red[wave][k] = v[k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NV; k++) v[k] = ((S.red[0][k] + S.red[1][k]) + S.red[2][k]) + S.red[3][k];
+  __syncthreads();
+}
+
+__device__ __forceinline__ void huber(double chi, double delta, double dsqr, double* rho0,
+                                      double* rho1) {
+  if (chi <= dsqr) {
+    *rho0 = chi;
+    *rho1 = 1.;
+  } else {
+    const double sq = sqrt(chi);
+    *rho0 = 2 * sq * delta - dsqr;
+    *rho1 = delta / sq;
+  }
+}
+
+__device__ bool solve6(const double A[6][6], const double b[6], double x[6]) {
+  double L[6][6], D[6];
+  for (int i = 0; i < 6; i++)
+    for (int j = 0; j < 6; j++) L[i][j] = 0;
+  for (int j = 0; j < 6; j++) {
+    double d = A[j][j];
+    for (int k = 0; k < j; k++) d -= L[j][k] * L[j][k] * D[k];
+    D[j] = d;
+    if (!(d > 0)) return false;
+    for (int i = j + 1; i < 6; i++) {
+      double s = A[i][j];
+      for (int k = 0; k < j; k++) s -= L[i][k] * L[j][k] * D[k];
+      L[i][j] = s / d;
+    }
+  }
+  double y[6];
+  for (int i = 0; i < 6; i++) {
+    double s = b[i];
+    for (int k = 0; k < i; k++) s -= L[i][k] * y[k];
+    y[i] = s;
+  }
+  for (int i = 5; i >= 0; i--) {
+    double s = y[i] / D[i];
+    for (int k = i + 1; k < 6; k++) s -= L[k][i] * x[k];
+    x[i] = s;
+  }
+  return true;
+}
+
+struct PoseArgs {
+  const KeyPointD* kps_un;
+  const float* uright;
+  const int* match;           // last-frame index per current keypoint, or -1
+  const uint8_t* has_mp;      // alternative to match (host API): 1 = edge
+  const float* mp_xyz;        // with match: last frame's xyz (per stream kp_pitch*3); else own
+  const int* n;
+  int kp_pitch;
+  // lines (host API only)
+  const float* kl_obs;
+  const int* kl_octave;
+  const uint8_t* has_ml;
+  const float* ml_xyz;
+  int nl;
+  float* Tcw;                 // in/out per stream (stride pose_stride)
+  int pose_stride;
+  uint8_t* outlier;           // in/out per stream kp_pitch
+  uint8_t* line_outlier;      // in/out (host API)
+  int* ninliers;              // per stream (stride nm_stride)
+  int nm_stride;
+  const StreamState* active;
+  PoseEdge* edges;            // scratch, per stream kPoseMaxEdges
+};
+
+__device__ void se3_from_T(const float* T, SE3d& s) {
+  double R[3][3];
+  for (int r = 0; r < 3; r++)
+    for (int cc = 0; cc < 3; cc++) R[r][cc] = T[r * 4 + cc];
+  s.q = quat_from_R(R);
+  normalize_rotation(s.q);
+  s.t[0] = T[3]; s.t[1] = T[7]; s.t[2] = T[11];
+}
+
+__global__ void __launch_bounds__(256) k_pose(TrackConsts tc, PoseArgs a) {
+  extern __shared__ char smem_raw[];
+  PoseShared& S = *reinterpret_cast<PoseShared*>(smem_raw);
+  const int s = blockIdx.x, t = threadIdx.x;
+  // TrackWithMotionModel returns before optimising when no last frame exists
+  // or nmatches < 20 after the retry (Tracking.cc:1255-1265).
+  if (a.active && (!a.active[s].has_last || a.active[s].nmatches < 20)) {
+    if (t == 0) a.ninliers[(long long)s * a.nm_stride] = 0;
+    return;
+  }
+  const PoseCam c{tc.fx, tc.fy, tc.cx, tc.cy, tc.bf};
+  const long long cb = (long long)s * a.kp_pitch;
+  const int n = a.n[s];
+  uint8_t* outl = a.outlier + cb;
+  // ---- edges (Optimizer.cc:2190-2283, 2285-2352), compacted in index order ----
+  PoseEdge* E = a.edges + (long long)s * kPoseMaxEdges;
+  const int wave = t >> 6, lane = t & 63;
+  int npts = 0;
+  for (int base = 0; base < n; base += 256) {
+    const int i = base + t;
+    int j = -1;
+    if (i < n) {
+      if (a.match) j = a.match[cb + i];
+      else if (a.has_mp[cb + i]) j = i;
+    }
+    const int flag = j >= 0 ? 1 : 0;
+    int incl = flag;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      int u = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += u;
+    }
+    if (lane == 63) S.wsum[wave] = incl;
+    __syncthreads();
+    int off = npts;
+    int tot = 0;
+    for (int w = 0; w < 4; w++) {
+      if (w < wave) off += S.wsum[w];
+      tot += S.wsum[w];
+    }
+    const int k = off + incl - flag;
+    if (flag && k < kPoseMaxEdges) {
+      PoseEdge e;
+      const KeyPointD kp = a.kps_un[cb + i];
+      const float ur = a.uright[cb + i];
+      e.kind = ur < 0 ? 0 : 1;
+      e.idx = i;
+      e.obs[0] = kp.x;
+      e.obs[1] = kp.y;
+      e.obs[2] = ur;
+      e.obs[3] = 0;
+      e.info = tc.inv_sigma2[kp.octave];
+      const float* X = a.mp_xyz + (cb + j) * 3;
+      e.X[0] = X[0]; e.X[1] = X[1]; e.X[2] = X[2];
+      e.X[3] = e.X[4] = e.X[5] = 0;
+      e.pad = 0;
+      E[k] = e;
+      S.level[k] = 0;
+      S.out_flag[k] = 0;
+      outl[i] = 0;
+    }
+    npts += tot;
+    __syncthreads();
+  }
+  npts = min(npts, kPoseMaxEdges);
+  int nlines = 0;
+  if (t == 0) {
+    int ne = npts;
+    for (int i = 0; i < a.nl; i++) {
+      if (!a.has_ml[i]) continue;
+      if (ne >= kPoseMaxEdges) break;
+      if (i < n) outl[i] = 0;  // reference writes mvbOutlier here (Optimizer.cc:2308)
+      PoseEdge e;
+      e.kind = 2;
+      e.idx = i;
+      for (int q = 0; q < 4; q++) e.obs[q] = a.kl_obs[4 * i + q];
+      e.info = tc.inv_sigma2[a.kl_octave[i]];
+      for (int q = 0; q < 6; q++) e.X[q] = a.ml_xyz[6 * i + q];
+      e.pad = 0;
+      E[ne] = e;
+      S.level[ne] = 0;
+      S.out_flag[ne] = a.line_outlier[i];
+      ne++;
+      nlines++;
+    }
+    S.misc[0] = ne;
+    S.misc[2] = nlines;
+  }
+  __syncthreads();
+  const int ne = S.misc[0];
+  nlines = S.misc[2];
+  float* Tout = a.Tcw + (long long)s * a.pose_stride;
+  if (npts < 3 && nlines < 3) {
+    if (t == 0) a.ninliers[(long long)s * a.nm_stride] = 0;
+    return;
+  }
+  // const float deltaMono = sqrt(5.991) (Optimizer.cc:2184-2186): double sqrt
+  // rounded to float; RobustKernelHuber::setDelta keeps dsqr as a float.
+  const double deltaMono = (double)(float)sqrt(5.991), deltaStereo = (double)(float)sqrt(7.815);
+  const double dsqrMono = (double)(float)(deltaMono * deltaMono);
+  const double dsqrStereo = (double)(float)(deltaStereo * deltaStereo);
+  SE3d T0;
+  se3_from_T(Tout, T0);
+  int nBadOut = 0;
+  bool robust = true;
+  for (int round = 0; round < 4; round++) {
+    SE3d T = T0;
+    // ---- optimizer.optimize(10) ----
+    int nact = 0;
+    for (int k = t; k < ne; k += 256) nact += S.level[k] == 0;
+    {
+      double v = nact;
+      block_sum<1>(&v, S);
+      nact = (int)v;
+    }
+    if (nact > 0) {
+      double lambda = 0, ni = 2;
+      int nBadLM = 0;
+      double x[6] = {0, 0, 0, 0, 0, 0};
+      for (int it = 0; it < 10; it++) {
+        // computeActiveErrors + buildSystem at T (fused: same estimate)
+        double R[3][3];
+        quat_to_R(T.q, R);
+        double acc[28];
+        for (int k = 0; k < 28; k++) acc[k] = 0;
+        for (int k = t; k < ne; k += 256) {
+          if (S.level[k]) continue;
+          const PoseEdge e = E[k];
+          double err[3], J[3][6];
+          edge_error(e, c, T, R, err);
+          const int dim = e.kind == 1 ? 3 : 2;
+          double x2 = 0;
+          for (int d = 0; d < dim; d++) x2 += err[d] * (double)e.info * err[d];
+          S.chi2[k] = x2;
+          double w = 1.0, r0 = x2;
+          if (robust) {
+            const bool isMono = e.kind == 0;
+            huber(x2, isMono ? deltaMono : deltaStereo, isMono ? dsqrMono : dsqrStereo, &r0, &w);
+          }
+          acc[27] += r0;
+          edge_jacobian(e, c, T, R, J);
+          const double info = (double)e.info;
+          int q = 0;
+          for (int i = 0; i < 6; i++) {
+            double bi = 0;
+            for (int d = 0; d < dim; d++) bi += J[d][i] * info * err[d];
+            acc[21 + i] -= w * bi;
+            for (int j = i; j < 6; j++) {
+              double h = 0;
+              for (int d = 0; d < dim; d++) h += J[d][i] * (w * info) * J[d][j];
+              acc[q++] += h;
+            }
+          }
+        }
+        block_sum<28>(acc, S);
+        double H[6][6], b[6];
+        {
+          int q = 0;
+          for (int i = 0; i < 6; i++)
+            for (int j = i; j < 6; j++) {
+              H[i][j] = acc[q];
+              H[j][i] = acc[q];
+              q++;
+            }
+          for (int i = 0; i < 6; i++) b[i] = acc[21 + i];
+        }
+        double currentChi = acc[27];
+        const double iniChi = currentChi;
+        if (it == 0) {
+          double md = 0;
+          for (int j = 0; j < 6; j++) md = fmax(fabs(H[j][j]), md);
+          lambda = 1e-5 * md;
+          ni = 2;
+          nBadLM = 0;
+        }
+        double rho = 0;
+        int qmax = 0;
+        do {
+          const SE3d backup = T;
+          double Hl[6][6];
+          for (int i = 0; i < 6; i++)
+            for (int j = 0; j < 6; j++) Hl[i][j] = H[i][j];
+          for (int j = 0; j < 6; j++) Hl[j][j] += lambda;
+          const bool ok2 = solve6(Hl, b, x);
+          T = se3_mul(se3_exp(x), T);
+          // computeActiveErrors at the trial estimate
+          double R2[3][3];
+          quat_to_R(T.q, R2);
+          double tc2 = 0;
+          for (int k = t; k < ne; k += 256) {
+            if (S.level[k]) continue;
+            const PoseEdge e = E[k];
+            double err[3];
+            edge_error(e, c, T, R2, err);
+            const int dim = e.kind == 1 ? 3 : 2;
+            double x2 = 0;
+            for (int d = 0; d < dim; d++) x2 += err[d] * (double)e.info * err[d];
+            S.chi2[k] = x2;
+            double r0 = x2, w;
+            if (robust) {
+              const bool isMono = e.kind == 0;
+              huber(x2, isMono ? deltaMono : deltaStereo, isMono ? dsqrMono : dsqrStereo, &r0, &w);
+            }
+            tc2 += r0;
+          }
+          block_sum<1>(&tc2, S);
+          double tempChi = ok2 ? tc2 : 1.7976931348623157e308;
+          rho = currentChi - tempChi;
+          double scale = 0;
+          for (int j = 0; j < 6; j++) scale += x[j] * (lambda * x[j] + b[j]);
+          scale += 1e-3;
+          rho /= scale;
+          if (rho > 0 && isfinite(tempChi)) {
+            double al = 1. - pow((2 * rho - 1), 3);
+            al = fmin(al, 2. / 3.);
+            const double sf = fmax(1. / 3., al);
+            lambda *= sf;
+            ni = 2;
+            currentChi = tempChi;
+          } else {
+            lambda *= ni;
+            ni *= 2;
+            T = backup;
+          }
+          qmax++;
+        } while (rho < 0 && qmax < 10);
+        if (qmax == 10 || rho == 0) break;
+        if ((iniChi - currentChi) * 1e3 < iniChi) nBadLM++;
+        else nBadLM = 0;
+        if (nBadLM >= 3) break;
+      }
+    }
+    // ---- classify (Optimizer.cc:2387-2470) ----
+    double R[3][3];
+    quat_to_R(T.q, R);
+    int nbad = 0;
+    for (int k = t; k < ne; k += 256) {
+      const PoseEdge e = E[k];
+      const bool was_out = e.kind == 2 ? (S.out_flag[k] != 0) : (outl[e.idx] != 0);
+      double x2 = S.chi2[k];
+      if (was_out) {
+        double err[3];
+        edge_error(e, c, T, R, err);
+        const int dim = e.kind == 1 ? 3 : 2;
+        x2 = 0;
+        for (int d = 0; d < dim; d++) x2 += err[d] * (double)e.info * err[d];
+        S.chi2[k] = x2;
+      }
+      const float chi2 = (float)x2;
+      const float th = e.kind == 0 ? 5.991f : (e.kind == 1 ? 7.815f : 2 * 7.815f);
+      const bool bad = chi2 > th;
+      if (e.kind == 2) {
+        S.out_flag[k] = bad;
+      } else {
+        outl[e.idx] = bad;
+        nbad += bad;
+      }
+      S.level[k] = bad ? 1 : 0;
+    }
+    {
+      double v = nbad;
+      block_sum<1>(&v, S);
+      nbad = (int)v;
+    }
+    nBadOut = nbad;
+    if (round == 2) robust = false;
+    // every thread ran the same LM control flow on the same reduced sums, so
+    // T is identical in all threads (no broadcast needed)
+    if (round == 3 || ne < 10) {
+      if (t == 0) {
+        double Rf[3][3];
+        quat_to_R(T.q, Rf);
+        for (int r = 0; r < 3; r++) {
+          for (int cc = 0; cc < 3; cc++) Tout[r * 4 + cc] = (float)Rf[r][cc];
+          Tout[r * 4 + 3] = (float)T.t[r];
+        }
+        Tout[12] = 0; Tout[13] = 0; Tout[14] = 0; Tout[15] = 1;
+      }
+      break;
+    }
+    __syncthreads();
+  }
+  for (int k = t; k < ne; k += 256) {
+    const PoseEdge e = E[k];
+    if (e.kind == 2) a.line_outlier[e.idx] = S.out_flag[k];
+  }
+  if (t == 0) a.ninliers[(long long)s * a.nm_stride] = npts - nBadOut;
+}
+
+// ---------------------------------------------------------------------------
+// After PoseOptimization: discard outliers (Tracking.cc:1273-1296), velocity
+// history, and the next frame's map points (all keypoints with depth,
+// UnprojectStereo at the optimised pose, Observations = 1).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_finish(TrackConsts c, StreamState* __restrict__ st,
+                                                const int* __restrict__ n_in, int kp_pitch,
+                                                const KeyPointD* __restrict__ kps_un,
+                                                const float* __restrict__ depth,
+                                                int* __restrict__ match,
+                                                uint8_t* __restrict__ outlier,
+                                                uint8_t* __restrict__ has_mp,
+                                                float* __restrict__ mp_xyz,
+                                                int* __restrict__ nobs) {
+  const int s = blockIdx.x, t = threadIdx.x;
+  StreamState& S = st[s];
+  const int n = n_in[s];
+  const long long cb = (long long)s * kp_pitch;
+  __shared__ float sT[16];
+  __shared__ int s_map;
+  if (t < 16) sT[t] = S.Tcw[t];
+  if (t == 0) s_map = 0;
+  __syncthreads();
+  float Ow[3];
+  gemm_neg_Rt_t(sT, Ow);
+  int nmap = 0;
+  for (int i = t; i < n; i += 256) {
+    const long long o = cb + i;
+    if (S.has_last && match[o] >= 0) {
+      if (outlier[o]) match[o] = -1;
+      else nmap++;
+    }
+    // next frame's map points: keyframe-style creation (Tracking.cc:625-645)
+    const float z = depth[o];
+    outlier[o] = 0;
+    if (z > 0) {
+      const KeyPointD k = kps_un[o];
+      const float x3[3] = {(k.x - c.cx) * z * c.invfx, (k.y - c.cy) * z * c.invfy, z};
+      float w[3];
+      gemm_Rt_x_plus_c(sT, x3, Ow, w);
+      mp_xyz[o * 3] = w[0];
+      mp_xyz[o * 3 + 1] = w[1];
+      mp_xyz[o * 3 + 2] = w[2];
+      has_mp[o] = 1;
+      nobs[o] = 1;
+    } else {
+      has_mp[o] = 0;
+      nobs[o] = 0;
+    }
+  }
+  if (nmap) atomicAdd(&s_map, nmap);
+  __syncthreads();
+  if (t == 0) {
+    S.nmatches_map = s_map;
+    S.ok = S.has_last ? (S.nmatches >= 20 && s_map >= 10) : 1;
+    for (int k = 0; k < 16; k++) {
+      S.Tlast2[k] = S.Tlast[k];
+      S.Tlast[k] = S.Tcw[k];
+    }
+    S.has_velocity = S.has_last;
+    S.has_last = 1;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+size_t match_smem_bytes() { return sizeof(MatchShared); }
+size_t pose_smem_bytes() { return sizeof(PoseShared); }
+
+static void set_smem_attr_once(const void* fn, size_t bytes, bool* done) {
+  if (!*done) {
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    *done = true;
+  }
+}
+
+void launch_frame_prepare(const TrackConsts& c, const KeyPointD* kps, const int* n, int kp_pitch,
+                          const float* depth, long long depth_pitch, KeyPointD* kps_un,
+                          float* depth_out, float* uright, int* gcell, int batch, hipStream_t s) {
+  hipLaunchKernelGGL(k_frame_prepare, dim3((kp_pitch + 255) / 256, batch), dim3(256), 0, s, c, kps, n,
+                     kp_pitch, depth, depth_pitch, kps_un, depth_out, uright, gcell);
+}
+
+void launch_predict(StreamState* st, int nstreams, hipStream_t s) {
+  hipLaunchKernelGGL(k_predict, dim3((nstreams + 63) / 64), dim3(64), 0, s, st, nstreams);
+}
+
+void launch_match_last(const TrackConsts& c, const MatchLaunch& m, int nstreams, hipStream_t s) {
+  static bool done = false;
+  set_smem_attr_once((const void*)k_match_last, sizeof(MatchShared), &done);
+  MatchArgs a;
+  a.cur_kps_un = m.cur_kps_un;
+  a.cur_desc = m.cur_desc;
+  a.cur_uright = m.cur_uright;
+  a.cur_gcell = m.cur_gcell;
+  a.cur_n = m.cur_n;
+  a.last_kps_un = m.last_kps_un;
+  a.last_has_mp = m.last_has_mp;
+  a.last_outlier = m.last_outlier;
+  a.last_xyz = m.last_xyz;
+  a.last_desc = m.last_desc;
+  a.last_nobs = m.last_nobs;
+  a.last_n = m.last_n;
+  a.kp_pitch = m.kp_pitch;
+  a.Tcw = m.Tcw;
+  a.Tlw = m.Tlw;
+  a.pose_stride = m.pose_stride;
+  a.match = m.match;
+  a.nmatches = m.nmatches;
+  a.nm_stride = m.nm_stride;
+  a.th = m.th;
+  a.mono = m.mono;
+  a.check_ori = m.check_ori;
+  a.retry = m.retry;
+  a.active = m.active;
+  hipLaunchKernelGGL(k_match_last, dim3(nstreams), dim3(256), sizeof(MatchShared), s, c, a);
+}
+
+void launch_pose(const TrackConsts& c, const PoseLaunch& p, int nstreams, hipStream_t s) {
+  static bool done = false;
+  set_smem_attr_once((const void*)k_pose, sizeof(PoseShared), &done);
+  PoseArgs a;
+  a.kps_un = p.kps_un;
+  a.uright = p.uright;
+  a.match = p.match;
+  a.has_mp = p.has_mp;
+  a.mp_xyz = p.mp_xyz;
+  a.n = p.n;
+  a.kp_pitch = p.kp_pitch;
+  a.kl_obs = p.kl_obs;
+  a.kl_octave = p.kl_octave;
+  a.has_ml = p.has_ml;
+  a.ml_xyz = p.ml_xyz;
+  a.nl = p.nl;
+  a.Tcw = p.Tcw;
+  a.pose_stride = p.pose_stride;
+  a.outlier = p.outlier;
+  a.line_outlier = p.line_outlier;
+  a.ninliers = p.ninliers;
+  a.nm_stride = p.nm_stride;
+  a.active = p.active;
+  a.edges = p.edges;
+  hipLaunchKernelGGL(k_pose, dim3(nstreams), dim3(256), sizeof(PoseShared), s, c, a);
+}
+
+void launch_finish(const TrackConsts& c, StreamState* st, const int* n, int kp_pitch,
+                   const KeyPointD* kps_un, const float* depth, int* match, uint8_t* outlier,
+                   uint8_t* has_mp, float* mp_xyz, int* nobs, int nstreams, hipStream_t s) {
+  hipLaunchKernelGGL(k_finish, dim3(nstreams), dim3(256), 0, s, c, st, n, kp_pitch, kps_un, depth,
+                     match, outlier, has_mp, mp_xyz, nobs);
+}
+
+}  // namespace orbpl
+
+namespace orbpl {
+size_t pose_edge_bytes() { return sizeof(PoseEdge); }
+}  // namespace orbpl

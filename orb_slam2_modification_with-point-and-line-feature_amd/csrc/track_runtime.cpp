@@ -1,0 +1,546 @@
+// Host runtime + C-ABI of the tracking half of the hot path:
+// orbpl_frame_prepare / orbm_search_by_projection_last / orbpl_pose_optimization
+// (single-frame host-pointer forms, drop-in for Frame / ORBmatcher / Optimizer
+// calls) and the batched device-resident orbpl_tracker.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstddef>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/orbpl.h"
+#include "orb_kernels.h"
+#include "orbpl_runtime.h"
+#include "track_kernels.h"
+
+using namespace orbpl;
+
+#define HIP_CHECK(expr)                                                \
+  do {                                                                 \
+    hipError_t _e = (expr);                                            \
+    if (_e != hipSuccess) return orbpl::hip_fail(_e, #expr, __LINE__); \
+  } while (0)
+
+namespace {
+
+// RAII device buffer for the synchronous host-pointer entry points.
+struct DBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  hipError_t alloc(size_t bytes) {
+    n = bytes;
+    return hipMalloc(&p, bytes ? bytes : 1);
+  }
+  ~DBuf() {
+    if (p) (void)hipFree(p);
+  }
+  template <class T>
+  T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+// Frame constants (Frame.cc:180-203) from the camera and the extractor's
+// scale tables; ComputeImageBounds uses the same undistortion code as the
+// device kernel (host-compiled, same IEEE double sequence).
+int make_consts(const orbpl_camera* cam, const float* scale, const float* inv_sigma2, int nlevels,
+                TrackConsts* out) {
+  if (!cam) return arg_fail("NULL camera");
+  if (nlevels < 1 || nlevels > kMaxLevelsT) return arg_fail("nlevels out of range");
+  TrackConsts c{};
+  c.fx = cam->fx; c.fy = cam->fy; c.cx = cam->cx; c.cy = cam->cy;
+  c.k1 = cam->k1; c.k2 = cam->k2; c.p1 = cam->p1; c.p2 = cam->p2; c.k3 = cam->k3;
+  c.bf = cam->bf;
+  c.mb = cam->bf / cam->fx;
+  c.th_depth = cam->th_depth;
+  c.invfx = 1.0f / cam->fx;
+  c.invfy = 1.0f / cam->fy;
+  c.width = cam->width;
+  c.height = cam->height;
+  if (cam->k1 != 0.0f) {
+    float ux[4], uy[4];
+    const float px[4] = {0.0f, (float)cam->width, 0.0f, (float)cam->width};
+    const float py[4] = {0.0f, 0.0f, (float)cam->height, (float)cam->height};
+    for (int i = 0; i < 4; i++) undistort_point_d(c, px[i], py[i], &ux[i], &uy[i]);
+    c.minX = std::min(ux[0], ux[2]);
+    c.maxX = std::max(ux[1], ux[3]);
+    c.minY = std::min(uy[0], uy[1]);
+    c.maxY = std::max(uy[2], uy[3]);
+  } else {
+    c.minX = 0.0f; c.maxX = (float)cam->width; c.minY = 0.0f; c.maxY = (float)cam->height;
+  }
+  c.gridInvW = static_cast<float>(kGridCols) / static_cast<float>(c.maxX - c.minX);
+  c.gridInvH = static_cast<float>(kGridRows) / static_cast<float>(c.maxY - c.minY);
+  c.nlevels = nlevels;
+  for (int l = 0; l < nlevels; l++) {
+    c.scale[l] = scale ? scale[l] : 1.0f;
+    c.inv_sigma2[l] = inv_sigma2 ? inv_sigma2[l] : 1.0f;
+  }
+  *out = c;
+  return ORBPL_OK;
+}
+
+hipStream_t scratch_stream() { return nullptr; }  // host-pointer APIs use the null stream
+
+}  // namespace
+
+extern "C" {
+
+int orbpl_frame_prepare(const orbpl_camera* cam, const orbpl_keypoint* kps, int n,
+                        const float* depth, orbpl_keypoint* kps_un, float* depth_out,
+                        float* uright_out, int32_t* grid_cell, float* bounds) {
+  if (!cam || n < 0 || (n > 0 && (!kps || !kps_un || !depth_out || !uright_out || !grid_cell)))
+    return arg_fail("bad argument");
+  TrackConsts c;
+  int rc = make_consts(cam, nullptr, nullptr, 1, &c);
+  if (rc) return rc;
+  if (bounds) { bounds[0] = c.minX; bounds[1] = c.maxX; bounds[2] = c.minY; bounds[3] = c.maxY; }
+  if (n == 0) return ORBPL_OK;
+  DBuf dk, dn, dd, dku, ddo, dur, dgc;
+  const size_t imgb = depth ? (size_t)cam->width * cam->height * 4 : 0;
+  HIP_CHECK(dk.alloc((size_t)n * sizeof(KeyPointD)));
+  HIP_CHECK(dn.alloc(4));
+  if (depth) HIP_CHECK(dd.alloc(imgb));
+  HIP_CHECK(dku.alloc((size_t)n * sizeof(KeyPointD)));
+  HIP_CHECK(ddo.alloc((size_t)n * 4));
+  HIP_CHECK(dur.alloc((size_t)n * 4));
+  HIP_CHECK(dgc.alloc((size_t)n * 4));
+  HIP_CHECK(hipMemcpy(dk.p, kps, (size_t)n * sizeof(KeyPointD), hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(dn.p, &n, 4, hipMemcpyHostToDevice));
+  if (depth) HIP_CHECK(hipMemcpy(dd.p, depth, imgb, hipMemcpyHostToDevice));
+  launch_frame_prepare(c, dk.as<KeyPointD>(), dn.as<int>(), n, depth ? dd.as<float>() : nullptr, 0,
+                       dku.as<KeyPointD>(), ddo.as<float>(), dur.as<float>(), dgc.as<int>(), 1,
+                       scratch_stream());
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipMemcpy(kps_un, dku.p, (size_t)n * sizeof(KeyPointD), hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(depth_out, ddo.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(uright_out, dur.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(grid_cell, dgc.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+  return ORBPL_OK;
+}
+
+int orbm_search_by_projection_last(const orbpl_camera* cam, const float* scale_factors, int nlevels,
+                                   const orbpl_match_current* cur, const orbpl_match_last* last,
+                                   float th, int mono, int check_orientation, int32_t* match,
+                                   int* nmatches) {
+  if (!cam || !scale_factors || !cur || !last || !match || !nmatches) return arg_fail("NULL argument");
+  const int n = cur->n, nl = last->n;
+  if (n < 0 || nl < 0 || n > kMatchMaxKp || nl > kMatchMaxKp)
+    return arg_fail("keypoint count exceeds the matcher capacity (2048)");
+  TrackConsts c;
+  int rc = make_consts(cam, scale_factors, nullptr, nlevels, &c);
+  if (rc) return rc;
+  const int P = std::max(1, std::max(n, nl));
+  DBuf d_cku, d_cdesc, d_cur, d_cg, d_cn, d_lku, d_lhas, d_lout, d_lxyz, d_ldesc, d_lnobs, d_ln, d_T,
+      d_match, d_nm;
+  HIP_CHECK(d_cku.alloc((size_t)P * sizeof(KeyPointD)));
+  HIP_CHECK(d_cdesc.alloc((size_t)P * 32));
+  HIP_CHECK(d_cur.alloc((size_t)P * 4));
+  HIP_CHECK(d_cg.alloc((size_t)P * 4));
+  HIP_CHECK(d_cn.alloc(4));
+  HIP_CHECK(d_lku.alloc((size_t)P * sizeof(KeyPointD)));
+  HIP_CHECK(d_lhas.alloc((size_t)P));
+  HIP_CHECK(d_lout.alloc((size_t)P));
+  HIP_CHECK(d_lxyz.alloc((size_t)P * 12));
+  HIP_CHECK(d_ldesc.alloc((size_t)P * 32));
+  HIP_CHECK(d_lnobs.alloc((size_t)P * 4));
+  HIP_CHECK(d_ln.alloc(4));
+  HIP_CHECK(d_T.alloc(32 * 4));
+  HIP_CHECK(d_match.alloc((size_t)P * 4));
+  HIP_CHECK(d_nm.alloc(4));
+  if (n) {
+    HIP_CHECK(hipMemcpy(d_cku.p, cur->kps_un, (size_t)n * sizeof(KeyPointD), hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(d_cdesc.p, cur->desc, (size_t)n * 32, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(d_cur.p, cur->uright, (size_t)n * 4, hipMemcpyHostToDevice));
+  }
+  HIP_CHECK(hipMemcpy(d_cn.p, &n, 4, hipMemcpyHostToDevice));
+  if (nl) {
+    HIP_CHECK(hipMemcpy(d_lku.p, last->kps_un, (size_t)nl * sizeof(KeyPointD), hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(d_lhas.p, last->has_mp, (size_t)nl, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(d_lout.p, last->outlier, (size_t)nl, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(d_lxyz.p, last->mp_xyz, (size_t)nl * 12, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(d_ldesc.p, last->mp_desc, (size_t)nl * 32, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(d_lnobs.p, last->mp_nobs, (size_t)nl * 4, hipMemcpyHostToDevice));
+  }
+  HIP_CHECK(hipMemcpy(d_ln.p, &nl, 4, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(d_T.as<float>(), cur->Tcw, 64, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(d_T.as<float>() + 16, last->Tcw, 64, hipMemcpyHostToDevice));
+  MatchLaunch m{};
+  m.cur_kps_un = d_cku.as<KeyPointD>();
+  m.cur_desc = d_cdesc.as<uint8_t>();
+  m.cur_uright = d_cur.as<float>();
+  m.cur_gcell = nullptr;  // computed on device from kps_un (PosInGrid)
+  m.cur_n = d_cn.as<int>();
+  m.last_kps_un = d_lku.as<KeyPointD>();
+  m.last_has_mp = d_lhas.as<uint8_t>();
+  m.last_outlier = d_lout.as<uint8_t>();
+  m.last_xyz = d_lxyz.as<float>();
+  m.last_desc = d_ldesc.as<uint8_t>();
+  m.last_nobs = d_lnobs.as<int>();
+  m.last_n = d_ln.as<int>();
+  m.kp_pitch = P;
+  m.Tcw = d_T.as<float>();
+  m.Tlw = d_T.as<float>() + 16;
+  m.pose_stride = 32;
+  m.match = d_match.as<int>();
+  m.nmatches = d_nm.as<int>();
+  m.nm_stride = 1;
+  m.th = th;
+  m.mono = mono;
+  m.check_ori = check_orientation;
+  m.retry = 0;
+  m.active = nullptr;
+  launch_match_last(c, m, 1, scratch_stream());
+  HIP_CHECK(hipGetLastError());
+  if (n) HIP_CHECK(hipMemcpy(match, d_match.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(nmatches, d_nm.p, 4, hipMemcpyDeviceToHost));
+  return ORBPL_OK;
+}
+
+int orbpl_pose_optimization(const orbpl_camera* cam, const orbpl_pose_problem* P, float* Tcw,
+                            uint8_t* outlier, uint8_t* line_outlier, int* n_inliers) {
+  if (!cam || !P || !Tcw || !n_inliers) return arg_fail("NULL argument");
+  const int n = P->n, nl = P->nl;
+  if (n < 0 || nl < 0 || n + nl > kPoseMaxEdges) return arg_fail("too many edges (max 2304)");
+  if (n > 0 && (!P->kps_un || !P->uright || !P->has_mp || !P->mp_xyz || !outlier))
+    return arg_fail("NULL point arrays");
+  if (nl > 0 && (!P->kl_obs || !P->kl_octave || !P->has_ml || !P->ml_xyz || !line_outlier))
+    return arg_fail("NULL line arrays");
+  TrackConsts c;
+  int rc = make_consts(cam, nullptr, P->inv_sigma2, P->nlevels, &c);
+  if (rc) return rc;
+  const int Pn = std::max(1, n), Pl = std::max(1, nl);
+  DBuf d_ku, d_ur, d_has, d_xyz, d_n, d_klo, d_klv, d_hml, d_mlx, d_T, d_out, d_lout, d_nin, d_edges;
+  HIP_CHECK(d_ku.alloc((size_t)Pn * sizeof(KeyPointD)));
+  HIP_CHECK(d_ur.alloc((size_t)Pn * 4));
+  HIP_CHECK(d_has.alloc((size_t)Pn));
+  HIP_CHECK(d_xyz.alloc((size_t)Pn * 12));
+  HIP_CHECK(d_n.alloc(4));
+  HIP_CHECK(d_klo.alloc((size_t)Pl * 16));
+  HIP_CHECK(d_klv.alloc((size_t)Pl * 4));
+  HIP_CHECK(d_hml.alloc((size_t)Pl));
+  HIP_CHECK(d_mlx.alloc((size_t)Pl * 24));
+  HIP_CHECK(d_T.alloc(64));
+  HIP_CHECK(d_out.alloc((size_t)Pn));
+  HIP_CHECK(d_lout.alloc((size_t)Pl));
+  HIP_CHECK(d_nin.alloc(4));
+  HIP_CHECK(d_edges.alloc((size_t)kPoseMaxEdges * pose_edge_bytes()));
+  if (n) {
+    HIP_CHECK(hipMemcpy(d_ku.p, P->kps_un, (size_t)n * sizeof(KeyPointD), hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(d_ur.p, P->uright, (size_t)n * 4, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(d_has.p, P->has_mp, (size_t)n, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(d_xyz.p, P->mp_xyz, (size_t)n * 12, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(d_out.p, outlier, (size_t)n, hipMemcpyHostToDevice));
+  }
+  if (nl) {
+    HIP_CHECK(hipMemcpy(d_klo.p, P->kl_obs, (size_t)nl * 16, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(d_klv.p, P->kl_octave, (size_t)nl * 4, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(d_hml.p, P->has_ml, (size_t)nl, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(d_mlx.p, P->ml_xyz, (size_t)nl * 24, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(d_lout.p, line_outlier, (size_t)nl, hipMemcpyHostToDevice));
+  }
+  HIP_CHECK(hipMemcpy(d_n.p, &n, 4, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(d_T.p, Tcw, 64, hipMemcpyHostToDevice));
+  PoseLaunch p{};
+  p.kps_un = d_ku.as<KeyPointD>();
+  p.uright = d_ur.as<float>();
+  p.match = nullptr;
+  p.has_mp = d_has.as<uint8_t>();
+  p.mp_xyz = d_xyz.as<float>();
+  p.n = d_n.as<int>();
+  p.kp_pitch = Pn;
+  p.kl_obs = d_klo.as<float>();
+  p.kl_octave = d_klv.as<int>();
+  p.has_ml = d_hml.as<uint8_t>();
+  p.ml_xyz = d_mlx.as<float>();
+  p.nl = nl;
+  p.Tcw = d_T.as<float>();
+  p.pose_stride = 16;
+  p.outlier = d_out.as<uint8_t>();
+  p.line_outlier = d_lout.as<uint8_t>();
+  p.ninliers = d_nin.as<int>();
+  p.nm_stride = 1;
+  p.active = nullptr;
+  p.edges = reinterpret_cast<PoseEdge*>(d_edges.p);
+  launch_pose(c, p, 1, scratch_stream());
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipMemcpy(Tcw, d_T.p, 64, hipMemcpyDeviceToHost));
+  if (n) HIP_CHECK(hipMemcpy(outlier, d_out.p, (size_t)n, hipMemcpyDeviceToHost));
+  if (nl) HIP_CHECK(hipMemcpy(line_outlier, d_lout.p, (size_t)nl, hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(n_inliers, d_nin.p, 4, hipMemcpyDeviceToHost));
+  return ORBPL_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Batched tracker
+// ---------------------------------------------------------------------------
+struct FrameBufs {
+  KeyPointD* kps = nullptr;
+  uint8_t* desc = nullptr;
+  int* n = nullptr;
+  KeyPointD* kps_un = nullptr;
+  float* depth = nullptr;
+  float* uright = nullptr;
+  int* gcell = nullptr;
+  int* match = nullptr;
+  uint8_t* outlier = nullptr;
+  uint8_t* has_mp = nullptr;
+  float* mp_xyz = nullptr;
+  int* nobs = nullptr;
+};
+
+struct orbpl_tracker {
+  orbx_ctx* ex = nullptr;
+  int device = 0;
+  int S = 0;
+  int W = 0, H = 0;
+  int kp_cap = 0;
+  hipStream_t stream = nullptr;
+  TrackConsts consts{};
+  FrameBufs fb[2];
+  int cur = 0;
+  StreamState* d_state = nullptr;
+  PoseEdge* d_edges = nullptr;
+  hipEvent_t ev[6] = {};
+  bool timed = false;
+  std::vector<void*> allocs;
+};
+
+namespace orbpl {
+hipStream_t orbx_stream(orbx_ctx* c);
+}
+
+static int tr_alloc(orbpl_tracker* t, void** p, size_t bytes) {
+  hipError_t e = hipMalloc(p, bytes ? bytes : 1);
+  if (e != hipSuccess) return hip_fail(e, "hipMalloc", __LINE__);
+  t->allocs.push_back(*p);
+  return hipMemset(*p, 0, bytes ? bytes : 1) == hipSuccess ? ORBPL_OK : ORBPL_ERR_HIP;
+}
+
+extern "C" {
+
+int orbpl_tracker_destroy(orbpl_tracker* t) {
+  if (!t) return ORBPL_OK;
+  (void)hipSetDevice(t->device);
+  for (void* p : t->allocs) (void)hipFree(p);
+  for (auto& e : t->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (t->ex) orbx_destroy(t->ex);
+  delete t;
+  return ORBPL_OK;
+}
+
+int orbpl_tracker_create(const orbpl_orb_params* orb, const orbpl_camera* cam, int n_streams,
+                         int device, orbpl_tracker** out) {
+  if (!orb || !cam || !out || n_streams <= 0) return arg_fail("bad argument");
+  *out = nullptr;
+  orbpl_tracker* t = new orbpl_tracker();
+  t->device = device;
+  t->S = n_streams;
+  t->W = cam->width;
+  t->H = cam->height;
+  int rc = orbx_create(orb, cam->width, cam->height, n_streams, device, &t->ex);
+  if (rc) {
+    delete t;
+    return rc;
+  }
+  t->kp_cap = orbx_max_keypoints(t->ex);
+  if (t->kp_cap > kMatchMaxKp) {
+    orbpl_tracker_destroy(t);
+    return arg_fail("nfeatures too large for the tracker (max 2048 keypoints per frame)");
+  }
+  float scale[16], inv_sigma2[16];
+  int nlev = 0;
+  orbx_get_scale_info(t->ex, &nlev, scale, nullptr, nullptr, inv_sigma2);
+  rc = make_consts(cam, scale, inv_sigma2, nlev, &t->consts);
+  if (rc) {
+    orbpl_tracker_destroy(t);
+    return rc;
+  }
+  t->stream = orbpl::orbx_stream(t->ex);
+  const size_t S = n_streams, K = t->kp_cap;
+#define TA(ptr, bytes)                                        \
+  do {                                                        \
+    int _r = tr_alloc(t, (void**)&(ptr), (bytes));            \
+    if (_r) { orbpl_tracker_destroy(t); return _r; }          \
+  } while (0)
+  for (int b = 0; b < 2; b++) {
+    FrameBufs& f = t->fb[b];
+    TA(f.kps, S * K * sizeof(KeyPointD));
+    TA(f.desc, S * K * 32);
+    TA(f.n, S * 4);
+    TA(f.kps_un, S * K * sizeof(KeyPointD));
+    TA(f.depth, S * K * 4);
+    TA(f.uright, S * K * 4);
+    TA(f.gcell, S * K * 4);
+    TA(f.match, S * K * 4);
+    TA(f.outlier, S * K);
+    TA(f.has_mp, S * K);
+    TA(f.mp_xyz, S * K * 12);
+    TA(f.nobs, S * K * 4);
+  }
+  TA(t->d_state, S * sizeof(StreamState));
+  TA(t->d_edges, S * kPoseMaxEdges * pose_edge_bytes());
+#undef TA
+  for (auto& e : t->ev)
+    if (hipEventCreate(&e) != hipSuccess) {
+      orbpl_tracker_destroy(t);
+      return hip_fail(hipErrorUnknown, "hipEventCreate", __LINE__);
+    }
+  rc = orbpl_tracker_reset(t, nullptr);
+  if (rc) {
+    orbpl_tracker_destroy(t);
+    return rc;
+  }
+  *out = t;
+  return ORBPL_OK;
+}
+
+int orbpl_tracker_reset(orbpl_tracker* t, const float* Tcw0) {
+  if (!t) return arg_fail("NULL tracker");
+  HIP_CHECK(hipSetDevice(t->device));
+  std::vector<StreamState> st(t->S);
+  for (int s = 0; s < t->S; s++) {
+    StreamState z{};
+    for (int k = 0; k < 16; k++) z.Tcw[k] = Tcw0 ? Tcw0[s * 16 + k] : (k % 5 == 0 ? 1.f : 0.f);
+    st[s] = z;
+  }
+  HIP_CHECK(hipMemcpyAsync(t->d_state, st.data(), sizeof(StreamState) * t->S, hipMemcpyHostToDevice,
+                           t->stream));
+  HIP_CHECK(hipStreamSynchronize(t->stream));
+  return ORBPL_OK;
+}
+
+int orbpl_tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_depth) {
+  if (!t || !d_gray || !d_depth) return arg_fail("NULL argument");
+  HIP_CHECK(hipSetDevice(t->device));
+  FrameBufs& C = t->fb[t->cur];
+  FrameBufs& L = t->fb[t->cur ^ 1];
+  const int S = t->S, K = t->kp_cap;
+  hipStream_t s = t->stream;
+  const int pstride = (int)(sizeof(StreamState) / sizeof(float));
+  char* st0 = reinterpret_cast<char*>(t->d_state);
+  float* dTcw = reinterpret_cast<float*>(st0 + offsetof(StreamState, Tcw));
+  float* dTlast = reinterpret_cast<float*>(st0 + offsetof(StreamState, Tlast));
+  int* dNm = reinterpret_cast<int*>(st0 + offsetof(StreamState, nmatches));
+  int* dNin = reinterpret_cast<int*>(st0 + offsetof(StreamState, ninliers));
+  t->timed = true;
+  HIP_CHECK(hipEventRecord(t->ev[0], s));
+  int rc = orbx_run(t->ex, d_gray, S, t->W, (long long)t->W * t->H,
+                    reinterpret_cast<orbpl_keypoint_dev*>(C.kps), C.desc, K, C.n);
+  if (rc) return rc;
+  HIP_CHECK(hipEventRecord(t->ev[1], s));
+  launch_frame_prepare(t->consts, C.kps, C.n, K, d_depth, (long long)t->W * t->H, C.kps_un, C.depth,
+                       C.uright, C.gcell, S, s);
+  launch_predict(t->d_state, S, s);
+  HIP_CHECK(hipEventRecord(t->ev[2], s));
+  MatchLaunch m{};
+  m.cur_kps_un = C.kps_un;
+  m.cur_desc = C.desc;
+  m.cur_uright = C.uright;
+  m.cur_gcell = C.gcell;
+  m.cur_n = C.n;
+  m.last_kps_un = L.kps_un;
+  m.last_has_mp = L.has_mp;
+  m.last_outlier = L.outlier;
+  m.last_xyz = L.mp_xyz;
+  m.last_desc = L.desc;
+  m.last_nobs = L.nobs;
+  m.last_n = L.n;
+  m.kp_pitch = K;
+  m.Tcw = dTcw;
+  m.Tlw = dTlast;
+  m.pose_stride = pstride;
+  m.match = C.match;
+  m.nmatches = dNm;
+  m.nm_stride = pstride;
+  m.th = 15.0f;          // RGB-D (Tracking.cc:1238-1241)
+  m.mono = 0;
+  m.check_ori = 1;       // ORBmatcher(0.9, true) (Tracking.cc:1216)
+  m.retry = 1;
+  m.active = t->d_state;
+  launch_match_last(t->consts, m, S, s);
+  HIP_CHECK(hipEventRecord(t->ev[3], s));
+  PoseLaunch p{};
+  p.kps_un = C.kps_un;
+  p.uright = C.uright;
+  p.match = C.match;
+  p.has_mp = nullptr;
+  p.mp_xyz = L.mp_xyz;
+  p.n = C.n;
+  p.kp_pitch = K;
+  p.nl = 0;
+  p.Tcw = dTcw;
+  p.pose_stride = pstride;
+  p.outlier = C.outlier;
+  p.line_outlier = nullptr;
+  p.ninliers = dNin;
+  p.nm_stride = pstride;
+  p.active = t->d_state;
+  p.edges = t->d_edges;
+  launch_pose(t->consts, p, S, s);
+  HIP_CHECK(hipEventRecord(t->ev[4], s));
+  launch_finish(t->consts, t->d_state, C.n, K, C.kps_un, C.depth, C.match, C.outlier, C.has_mp,
+                C.mp_xyz, C.nobs, S, s);
+  HIP_CHECK(hipEventRecord(t->ev[5], s));
+  HIP_CHECK(hipGetLastError());
+  t->cur ^= 1;
+  return ORBPL_OK;
+}
+
+int orbpl_tracker_synchronize(orbpl_tracker* t) {
+  if (!t) return arg_fail("NULL tracker");
+  return orbx_synchronize(t->ex);
+}
+
+int orbpl_tracker_get_state(orbpl_tracker* t, float* Tcw, int* nkps, int* nmatches, int* ninliers,
+                            int* nmatches_map) {
+  if (!t) return arg_fail("NULL tracker");
+  HIP_CHECK(hipSetDevice(t->device));
+  HIP_CHECK(hipStreamSynchronize(t->stream));
+  std::vector<StreamState> st(t->S);
+  HIP_CHECK(hipMemcpy(st.data(), t->d_state, sizeof(StreamState) * t->S, hipMemcpyDeviceToHost));
+  std::vector<int> n(t->S);
+  // the frame just tracked is the "last" buffer after the step's swap
+  HIP_CHECK(hipMemcpy(n.data(), t->fb[t->cur ^ 1].n, 4 * t->S, hipMemcpyDeviceToHost));
+  for (int s = 0; s < t->S; s++) {
+    if (Tcw) memcpy(Tcw + 16 * s, st[s].Tlast, 64);
+    if (nkps) nkps[s] = n[s];
+    if (nmatches) nmatches[s] = st[s].nmatches;
+    if (ninliers) ninliers[s] = st[s].ninliers;
+    if (nmatches_map) nmatches_map[s] = st[s].nmatches_map;
+  }
+  return ORBPL_OK;
+}
+
+int orbpl_tracker_stage_ms(orbpl_tracker* t, float* ms5) {
+  if (!t || !ms5) return arg_fail("NULL argument");
+  if (!t->timed) return arg_fail("no step recorded yet");
+  HIP_CHECK(hipSetDevice(t->device));
+  HIP_CHECK(hipEventSynchronize(t->ev[5]));
+  for (int i = 0; i < 5; i++) HIP_CHECK(hipEventElapsedTime(&ms5[i], t->ev[i], t->ev[i + 1]));
+  return ORBPL_OK;
+}
+
+int orbpl_tracker_kp_capacity(const orbpl_tracker* t) { return t ? t->kp_cap : 0; }
+
+int orbpl_tracker_get_frame(orbpl_tracker* t, int stream, orbpl_keypoint* kps_un, uint8_t* desc,
+                            int32_t* match, uint8_t* outlier, int* n) {
+  if (!t || stream < 0 || stream >= t->S) return arg_fail("bad argument");
+  HIP_CHECK(hipSetDevice(t->device));
+  HIP_CHECK(hipStreamSynchronize(t->stream));
+  const FrameBufs& F = t->fb[t->cur ^ 1];
+  const size_t K = t->kp_cap, o = (size_t)stream * K;
+  int cnt = 0;
+  HIP_CHECK(hipMemcpy(&cnt, F.n + stream, 4, hipMemcpyDeviceToHost));
+  if (n) *n = cnt;
+  if (kps_un) HIP_CHECK(hipMemcpy(kps_un, F.kps_un + o, K * sizeof(KeyPointD), hipMemcpyDeviceToHost));
+  if (desc) HIP_CHECK(hipMemcpy(desc, F.desc + o * 32, K * 32, hipMemcpyDeviceToHost));
+  if (match) HIP_CHECK(hipMemcpy(match, F.match + o, K * 4, hipMemcpyDeviceToHost));
+  if (outlier) HIP_CHECK(hipMemcpy(outlier, F.outlier + o, K, hipMemcpyDeviceToHost));
+  return ORBPL_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,144 @@
+"""GPU parity of the tracking half against the CPU oracle:
+Frame glue (bit-exact), ORBmatcher::SearchByProjection(Frame, Frame)
+(bit-exact match sets), PoseOptimization (pose within 1e-4, identical
+outlier labels), and the batched tracker vs the oracle VO loop."""
+import numpy as np
+import pytest
+
+from _scenes import match_problem, sequence, frame_data, unproject
+
+pytestmark = pytest.mark.gpu
+
+POSE_TOL = 1e-4   # north_star: pose within 1e-4 RMSE (max-abs used here: stricter)
+
+
+def _u32(a):
+    return np.ascontiguousarray(a).view(np.uint32)
+
+
+@pytest.mark.parametrize("cam_name", ["TUM1", "TUM3"])
+def test_frame_prepare_bit_exact(cam_name, orbpl, oracle):
+    cfg, traj, frames = sequence(2, 3, cam_name)
+    cam_o = oracle.camera(cfg)
+    cam_g = orbpl.make_camera(cfg)
+    kps, desc, _ = oracle.extract(oracle.params(), frames[0][0])
+    ku, d, ur, gc, b = orbpl.frame_prepare(cam_g, kps, frames[0][1])
+    oku, od, our, ogc, ob = oracle.frame_prepare(cam_o, kps, frames[0][1])
+    for f in ("x", "y"):
+        assert np.array_equal(_u32(ku[f]), _u32(oku[f])), f
+    assert np.array_equal(_u32(d), _u32(od))
+    assert np.array_equal(_u32(ur), _u32(our))
+    assert np.array_equal(gc, ogc)
+    assert np.array_equal(_u32(b), _u32(ob))
+    # monocular: no depth
+    ku2, d2, ur2, gc2, _ = orbpl.frame_prepare(cam_g, kps, None)
+    assert np.all(d2 == -1) and np.all(ur2 == -1)
+
+
+@pytest.mark.parametrize("case", [
+    dict(seed=0), dict(seed=1, th=7.0), dict(seed=2, mono=True), dict(seed=0, check_ori=False),
+    dict(seed=1, nobs_zero_frac=0.3), dict(seed=2, outlier_frac=0.2), dict(seed=0, th=30.0),
+    dict(seed=1, pert=(0.05, 0.03)),
+])
+def test_search_by_projection_last_bit_exact(case, orbpl, oracle):
+    case = dict(case)
+    th = case.pop("th", 15.0)
+    mono = case.pop("mono", False)
+    ori = case.pop("check_ori", True)
+    cfg, cam_o, sc, cur, last, _ = match_problem(**case)
+    cam_g = orbpl.make_camera(cfg)
+    m_g, n_g = orbpl.ORBmatcher(0.9, ori).SearchByProjectionLastFrame(cam_g, sc, cur, last, th, mono)
+    m_o, n_o = oracle.search_by_projection_last(cam_o, sc, cur, last, th, mono, ori)
+    assert n_g == n_o
+    assert np.array_equal(m_g, m_o), f"{int((m_g != m_o).sum())} assignments differ"
+    assert n_o > 50
+
+
+def _pose_problem(seed, stereo=True, lines=0, outliers=0.0, pert=(0.02, 0.02)):
+    from _pkg import load_oracle
+    O = load_oracle()
+    cfg, cam_o, sc, cur, last, (f0, f1, T0, T1) = match_problem(seed)
+    m, n = O.search_by_projection_last(cam_o, sc, cur, last, 15.0)
+    has = (m >= 0).astype(np.uint8)
+    xyz = np.zeros((len(m), 3), np.float32)
+    xyz[has == 1] = last["mp_xyz"][m[has == 1]]
+    rng = np.random.default_rng(seed)
+    bad = (rng.random(len(m)) < outliers) & (has == 1)
+    xyz[bad] += rng.normal(size=(bad.sum(), 3)).astype(np.float32) * 0.3
+    ur = cur["uright"] if stereo else np.full(len(m), -1, np.float32)
+    lw, lh, nf, scl, isc = O.level_sizes(O.params(), 640, 480)
+    prob = dict(kps_un=cur["kps_un"], uright=ur, has_mp=has, mp_xyz=xyz,
+                inv_sigma2=(1.0 / (scl * scl)).astype(np.float32))
+    if lines:
+        # synthetic 3D segments in front of the camera, observed at the true pose
+        Twc = np.linalg.inv(T1.astype(np.float64))
+        P = rng.uniform([-1.5, -1, 1.5], [1.5, 1, 4], size=(lines, 2, 3))
+        Pw = P @ Twc[:3, :3].T + Twc[:3, 3]
+        uv = P[..., :2] / P[..., 2:] * [cfg["fx"], cfg["fy"]] + [cfg["cx"], cfg["cy"]]
+        uv += rng.normal(size=uv.shape) * 0.5
+        prob.update(kl_obs=uv.reshape(lines, 4).astype(np.float32),
+                    kl_octave=np.zeros(lines, np.int32),
+                    has_ml=(rng.random(lines) < 0.9).astype(np.uint8),
+                    ml_xyz=Pw.reshape(lines, 6).astype(np.float32))
+    T_init = cur["Tcw"] if pert is None else __import__("_scenes").perturb(T1, *pert, seed=seed + 3)
+    return cfg, cam_o, prob, T_init, T1
+
+
+@pytest.mark.parametrize("case", [
+    dict(seed=0), dict(seed=1, stereo=False), dict(seed=2, outliers=0.15),
+    dict(seed=0, lines=40), dict(seed=1, lines=60, outliers=0.1), dict(seed=2, pert=(0.08, 0.05)),
+])
+def test_pose_optimization_parity(case, orbpl, oracle):
+    cfg, cam_o, prob, T_init, T_true = _pose_problem(**case)
+    cam_g = orbpl.make_camera(cfg)
+    n = len(prob["kps_un"])
+    nl = len(prob.get("kl_obs", ()))
+    out0 = np.zeros(n, np.uint8)
+    lout0 = np.zeros(nl, np.uint8)
+    Tg, og, log_, ng = orbpl.pose_optimization(cam_g, prob, T_init, out0, lout0)
+    To, oo, loo, no = oracle.pose_optimization(cam_o, prob, T_init, out0, lout0)
+    assert np.abs(Tg - To).max() < POSE_TOL, np.abs(Tg - To).max()
+    assert ng == no
+    assert np.array_equal(og, oo)
+    assert np.array_equal(log_, loo)
+    if not case.get("lines"):
+        assert np.abs(To[:3, 3] - T_true[:3, 3]).max() < 0.01   # converged near the truth
+
+
+def test_pose_too_few_correspondences(orbpl, oracle):
+    cfg, cam_o, prob, T_init, _ = _pose_problem(0)
+    prob["has_mp"] = np.zeros_like(prob["has_mp"])
+    prob["has_mp"][:2] = 1
+    n = len(prob["kps_un"])
+    Tg, og, _, ng = orbpl.pose_optimization(orbpl.make_camera(cfg), prob, T_init, np.zeros(n, np.uint8))
+    assert ng == 0 and np.array_equal(Tg, T_init)
+
+
+def test_tracker_matches_oracle_vo(orbpl, oracle):
+    S, F = 3, 5
+    cams = []
+    seqs = [sequence(F, 10 + s) for s in range(S)]
+    cfg = seqs[0][0]
+    orb = oracle.params()
+    vo = oracle.VO(orb, oracle.camera(cfg), S)
+    tr = orbpl.Tracker(orbpl.OrbParams(1000, 1.2, 8, 20, 7), orbpl.make_camera(cfg), S)
+    T0 = np.stack([np.linalg.inv(sq[1][0]).astype(np.float32) for sq in seqs])
+    vo.reset(T0.reshape(S, 16))
+    tr.reset(T0.reshape(S, 16))
+    gray = orbpl.DeviceBuffer(S * 640 * 480)
+    depth = orbpl.DeviceBuffer(S * 640 * 480 * 4)
+    for f in range(F):
+        gray.upload(np.stack([sq[2][f][0] for sq in seqs]))
+        depth.upload(np.stack([sq[2][f][1] for sq in seqs]))
+        tr.step_device(gray.ptr, depth.ptr)
+        tr.synchronize()
+        st = tr.state()
+        for s in range(S):
+            To, so = vo.step(s, seqs[s][2][f][0], seqs[s][2][f][1])
+            assert st["nkeypoints"][s] == so["nkeypoints"]
+            assert st["nmatches"][s] == so["nmatches"], (f, s)
+            assert st["ninliers"][s] == so["ninliers"], (f, s)
+            assert st["nmatches_map"][s] == so["nmatches_map"], (f, s)
+            assert np.abs(st["Tcw"][s] - To).max() < POSE_TOL, (f, s)
+    ms = tr.stage_ms()
+    assert np.all(ms >= 0)
