@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""Benchmark: frames/sec of the per-frame hot path (extract + match + pose).
+
+BASELINE.json metric "frames/sec (extract+match+pose) at 640x480", quoted on
+configs[1] = "TUM fr1_desk RGB-D, ORB point features only, 1 MI355X":
+TUM1.yaml camera + distortion, ORB 1000 features / 1.2 / 8 levels / FAST 20,7.
+
+A step = one Tracking::TrackWithMotionModel pass (ORB extraction, Frame glue,
+SearchByProjection(th=15, retry 30), PoseOptimization, outlier discard) over a
+batch of `--streams` independent synthetic 640x480 RGB-D streams, all inputs
+resident in HBM before the timed region. Frames are rendered from a seeded
+textured room along closed loop trajectories (no datasets on the box).
+
+Multi-GPU: one process per GPU (torchrun), streams sharded across ranks with
+no data-path collective (weak scaling); the gloo process group only carries the
+barrier and the max-over-ranks time.
+
+Prints ONE JSON line (rank 0). See DESIGN.md for the roofline accounting.
+"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+from concurrent.futures import ProcessPoolExecutor
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "tests"))
+
+W, H = 640, 480
+ORB = (1000, 1.2, 8, 20, 7)
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8 TB/s spec
+
+
+def _render(args):
+    i, n, seed = args
+    from _pkg import load_pkg
+    load_pkg()
+    import orbpl.synth as synth
+    traj = synth.loop_trajectory(n, seed=seed)
+    room = synth.default_room(seed)
+    g, d = synth.render(synth.TUM1, traj[i], room, seed=seed * 1000 + i)
+    return g, d
+
+
+def render_loop(n, seed, workers):
+    with ProcessPoolExecutor(max_workers=workers) as ex:
+        out = list(ex.map(_render, [(i, n, seed) for i in range(n)]))
+    return np.stack([o[0] for o in out]), np.stack([o[1] for o in out])
+
+
+def level_areas():
+    from _pkg import load_pkg
+    d = load_pkg().describe(*ORB, width=W, height=H)
+    return [int(a) * int(b) for a, b in zip(d["width"], d["height"])], d
+
+
+def algorithmic_bytes():
+    """Per-frame algorithmic HBM bytes of each kernel."""
+    areas, d = level_areas()
+    S = sum(areas)
+    pads = [(int(a) + 38) * (int(b) + 38) for a, b in zip(d["width"], d["height"])]
+    K = d["max_keypoints"]
+    return {
+        # read the input (level 0) or the previous level, write the padded level
+        "pyramid": W * H + sum(pads) + sum(areas[:-1]),
+        # read each level's content + 3 px halo, write the blurred content
+        "blur": sum((int(a) + 6) * (int(b) + 6) for a, b in zip(d["width"], d["height"])) + S,
+        # read every pyramid level once; candidate output is negligible
+        "fast": S,
+        # candidates in/out of the octree (~4 B per candidate), keypoints out
+        "octree": 0,
+        # per keypoint: 31x31 patch + 512 blurred samples (~2 KB incl. lines), 60 B out
+        "orient_desc": 0,
+    }
+
+
+def cpu_baseline(seconds, threads, gray, depth):
+    """The CPU oracle (C++ restatement, oracle/) running the same per-frame
+    step, one stream per thread (throughput mode), for a bounded wall time."""
+    from _pkg import load_oracle
+    O = load_oracle()
+    import orbpl.synth as synth
+    cam = O.camera(synth.TUM1)
+    counts = [0] * threads
+    stop = time.time() + seconds
+
+    def worker(k):
+        vo = O.VO(O.params(*ORB), cam, 1)
+        n = len(gray)
+        i = 0
+        while time.time() < stop:
+            vo.step(0, gray[(k + i) % n], depth[(k + i) % n])
+            i += 1
+        counts[k] = i
+
+    t0 = time.time()
+    ths = [threading.Thread(target=worker, args=(k,)) for k in range(threads)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    dt = time.time() - t0
+    return sum(counts) / dt, sum(counts), dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--streams", type=int, default=256, help="streams (frames per step) per GPU")
+    ap.add_argument("--loop", type=int, default=32, help="frames in the synthetic loop")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+
+    from _pkg import load_pkg
+    pkg = load_pkg()
+    import orbpl.synth as synth
+
+    S, F = args.streams, args.loop
+    workers = min(16, os.cpu_count() or 4)
+    gray, depth = render_loop(F, seed=1 + rank, workers=workers)
+    # stream s at step t reads loop frame (s + t) mod F: a contiguous window of
+    # a (S + F)-frame replicated buffer, so every step's batch is one slice.
+    rep = np.arange(S + F) % F
+    d_gray = pkg.DeviceBuffer.from_array(gray[rep], device=local_rank)
+    d_depth = pkg.DeviceBuffer.from_array(depth[rep], device=local_rank)
+    cam = pkg.make_camera(synth.TUM1)
+    tr = pkg.Tracker(pkg.OrbParams(*ORB), cam, S, device=local_rank)
+    traj = synth.loop_trajectory(F, seed=1 + rank)
+    tr.reset(np.stack([np.linalg.inv(traj[s % F]).astype(np.float32) for s in range(S)]).reshape(S, 16))
+    fb, db = W * H, W * H * 4
+
+    def step(k):
+        o = k % F
+        tr.step_device(d_gray.ptr + o * fb, d_depth.ptr + o * db)
+
+    for k in range(args.warmup):
+        step(k)
+    tr.synchronize()
+    tr.timings_reset()
+    if dist:
+        dist.barrier()
+    tr.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(args.warmup + k)
+    tr.synchronize()
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if dist:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    st = tr.state()
+    tim = tr.timings(args.steps)                       # (steps, 9) ms, in-stream hipEvents
+    avg = tim.mean(0)
+    stages = dict(zip(tr.STAGES, [round(float(x), 4) for x in avg]))
+    frames = S * args.steps * world
+    value = frames / elapsed
+
+    # roofline of the dominant single-launch kernel
+    ab = algorithmic_bytes()
+    single = {"blur": 1, "fast": 2}
+    dom = max(single, key=lambda k: avg[single[k]])
+    dom_ms = float(avg[single[dom]])
+    bytes_launch = ab[dom] * S
+    achieved = bytes_launch / (dom_ms * 1e-3) / 1e9
+    roof = {"bound": "hbm", "kernel": {"blur": "k_blur", "fast": "k_fast_cells"}[dom],
+            "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+            "algorithmic_bytes_per_launch": bytes_launch, "avg_launch_ms": round(dom_ms, 4)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        thr = args.cpu_threads or min(16, os.cpu_count() or 1)
+        fps, nfr, dt = cpu_baseline(args.cpu_seconds, thr, gray, depth)
+        cpu = {"value": round(fps, 2), "unit": "frames/s", "cores": thr, "kind": "port",
+               "sample": f"{nfr} frames of the same 640x480 RGB-D loop in {dt:.1f} s, oracle/ "
+                         f"C++ restatement, one stream per thread"}
+
+    if rank == 0:
+        out = {
+            "metric": "frames/sec (extract+match+pose) at 640x480",
+            "value": round(value, 2),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (seeded textured-room RGB-D loop, TUM1 intrinsics+distortion)",
+            "config": {"workload": "TUM fr1_desk-like RGB-D, ORB points only (configs[1])",
+                       "image": "640x480", "nfeatures": 1000, "streams_per_gpu": S,
+                       "frames_per_step": S * world, "parallelism": f"streams sharded x{world}"},
+            "stage_ms": stages,
+            "tracking": {"mean_keypoints": float(st["nkeypoints"].mean()),
+                         "mean_matches": float(st["nmatches"].mean()),
+                         "mean_inliers": float(st["ninliers"].mean())},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

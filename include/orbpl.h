@@ -244,6 +244,11 @@ int orbpl_tracker_get_state(orbpl_tracker* tr, float* Tcw, int* nkeypoints, int*
                             int* ninliers, int* nmatches_map);
 /* hipEvent times of the last step (ms): extract, glue, match, pose, finish. */
 int orbpl_tracker_stage_ms(orbpl_tracker* tr, float* ms5);
+/* Per-kernel device times (ms, hipEvents on the tracker stream) of the last
+ * min(max_steps, 64) steps, 9 per step: pyramid (8 launches), blur, fast,
+ * octree, orient+desc, glue+predict, match, pose, finish. */
+int orbpl_tracker_timings(orbpl_tracker* tr, int max_steps, float* ms, int* n_steps);
+int orbpl_tracker_timings_reset(orbpl_tracker* tr);
 /* Per-stream frame outputs of the last step (host copies, kp_cap entries per
  * stream, see orbpl_tracker_kp_capacity): undistorted keypoints, descriptors,
  * match (last-frame index per keypoint or -1), outlier flags. */

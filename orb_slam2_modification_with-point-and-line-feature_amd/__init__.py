@@ -335,6 +335,8 @@ def _declare_track(L):
     L.orbpl_tracker_get_state.argtypes = [vp, vp, vp, vp, vp, vp]
     L.orbpl_tracker_stage_ms.argtypes = [vp, vp]
     L.orbpl_tracker_kp_capacity.argtypes = [vp]
+    L.orbpl_tracker_timings.argtypes = [vp, i, vp, ip]
+    L.orbpl_tracker_timings_reset.argtypes = [vp]
     L.orbpl_tracker_get_frame.argtypes = [vp, i, vp, vp, vp, vp, ip]
 
 
@@ -474,6 +476,20 @@ class Tracker:
         ms = np.zeros(5, np.float32)
         check(lib().orbpl_tracker_stage_ms(self._h, _ptr(ms)), "orbpl_tracker_stage_ms")
         return ms
+
+    STAGES = ("pyramid", "blur", "fast", "octree", "orient_desc", "glue", "match", "pose",
+              "finish")
+
+    def timings(self, max_steps=64):
+        """(n_steps, 9) per-kernel ms of the last steps (hipEvents in-stream)."""
+        ms = np.zeros((max_steps, 9), np.float32)
+        n = C.c_int(0)
+        check(lib().orbpl_tracker_timings(self._h, max_steps, _ptr(ms), C.byref(n)),
+              "orbpl_tracker_timings")
+        return ms[:n.value]
+
+    def timings_reset(self):
+        check(lib().orbpl_tracker_timings_reset(self._h), "orbpl_tracker_timings_reset")
 
     def frame(self, stream):
         K = self.kp_cap

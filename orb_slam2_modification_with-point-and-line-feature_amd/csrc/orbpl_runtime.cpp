@@ -276,24 +276,26 @@ hipStream_t orbx_stream(orbx_ctx* c) { return c->stream; }
 
 // Whole extraction pipeline on the ctx stream; images already in device memory.
 int orbx_run(orbx_ctx* c, const uint8_t* d_imgs, int batch, int stride, long long frame_pitch,
-             orbpl_keypoint_dev* d_kps, uint8_t* d_desc, int kp_pitch, int* d_n) {
+             orbpl_keypoint_dev* d_kps, uint8_t* d_desc, int kp_pitch, int* d_n,
+             hipEvent_t* ext_events) {
   const OrbGeom& g = c->hg.g;
   hipStream_t s = c->stream;
-  c->timed = true;
-  HIP_CHECK(hipEventRecord(c->ev[0], s));
+  c->timed = ext_events == nullptr;
+  hipEvent_t* ev = ext_events ? ext_events : c->ev;
+  HIP_CHECK(hipEventRecord(ev[0], s));
   launch_pyramid(g, c->d_geom, d_imgs, stride, frame_pitch, c->d_pyr, c->d_rs, batch, s);
-  HIP_CHECK(hipEventRecord(c->ev[1], s));
+  HIP_CHECK(hipEventRecord(ev[1], s));
   launch_blur(g, c->d_geom, c->d_pyr, c->d_blur, batch, s);
-  HIP_CHECK(hipEventRecord(c->ev[2], s));
+  HIP_CHECK(hipEventRecord(ev[2], s));
   launch_fast(g, c->d_geom, c->d_cells, c->d_pyr, c->d_cell_cands, c->d_cell_counts,
               c->params.ini_th_fast, c->params.min_th_fast, batch, s);
-  HIP_CHECK(hipEventRecord(c->ev[3], s));
+  HIP_CHECK(hipEventRecord(ev[3], s));
   launch_octree(g, c->d_geom, c->d_cell_cands, c->d_cell_counts, c->d_kcand, c->d_knode,
                 c->d_kp_list, c->d_kp_count, c->d_err, batch, s);
-  HIP_CHECK(hipEventRecord(c->ev[4], s));
+  HIP_CHECK(hipEventRecord(ev[4], s));
   launch_orient_desc(g, c->d_geom, c->d_pyr, c->d_blur, c->d_kp_list, c->d_kp_count, d_kps, d_desc,
                      kp_pitch, d_n, batch, s);
-  HIP_CHECK(hipEventRecord(c->ev[5], s));
+  HIP_CHECK(hipEventRecord(ev[5], s));
   HIP_CHECK(hipGetLastError());
   c->last_batch = batch;
   return ORBPL_OK;

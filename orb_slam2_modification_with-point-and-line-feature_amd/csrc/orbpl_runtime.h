@@ -10,5 +10,7 @@ namespace orbpl {
 int hip_fail(hipError_t e, const char* what, int line);
 int arg_fail(const char* msg);
 int orbx_run(orbx_ctx* c, const uint8_t* d_imgs, int batch, int stride, long long frame_pitch,
-             orbpl_keypoint_dev* d_kps, uint8_t* d_desc, int kp_pitch, int* d_n);
+             orbpl_keypoint_dev* d_kps, uint8_t* d_desc, int kp_pitch, int* d_n,
+             hipEvent_t* ext_events = nullptr);
+hipStream_t orbx_stream(orbx_ctx* c);
 }  // namespace orbpl

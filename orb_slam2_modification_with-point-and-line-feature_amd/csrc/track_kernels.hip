@@ -90,26 +90,6 @@ __global__ void k_predict(StreamState* __restrict__ st, int nstreams) {
 //     one; otherwise the chunk is replayed point by point with re-scans.
 //   Phase C: rotation histogram, ComputeThreeMaxima, removal.
 // ---------------------------------------------------------------------------
-struct MatchShared {
-  int cell_start[kGridCols * kGridRows + 1];
-  int cell_fill[kGridCols * kGridRows];
-  uint16_t items[kMatchMaxKp];
-  float2 xy[kMatchMaxKp];
-  float ur[kMatchMaxKp];
-  float ang[kMatchMaxKp];
-  int8_t oct[kMatchMaxKp];
-  int16_t gc[kMatchMaxKp];        // grid cell (PosInGrid) or -1
-  int best[kMatchMaxKp];          // phase A: (dist << 16 | idx) or -1; later: final candidate
-  int bin[kMatchMaxKp];           // accepted -> histogram bin, else -1
-  int mpw[kMatchMaxKp];           // last writer (last-frame index) per current keypoint
-  uint32_t claimed[kMatchMaxKp / 32];
-  uint32_t removed[kMatchMaxKp / 32];
-  int hist[32];
-  int chunk_cell[256];
-  int wsum[8];
-  int misc[8];
-};
-
 struct MatchArgs {
   // current frame (per stream pitch kp_pitch)
   const KeyPointD* cur_kps_un;
@@ -197,7 +177,8 @@ __device__ __forceinline__ ProjInfo project_point(const TrackConsts& c, const fl
 
 // Frame::GetFeaturesInArea + the best-candidate loop (ORBmatcher.cc:1789-1826).
 // Returns (dist << 16) | idx of the first minimum in scan order, or -1.
-__device__ int scan_best(const MatchShared& S, const TrackConsts& c, const ProjInfo& p,
+template <class SH>
+__device__ int scan_best(const SH& S, const TrackConsts& c, const ProjInfo& p,
                          const uint8_t* dMP, const uint8_t* cur_desc, bool use_claims,
                          float mbf) {
   int bestDist = 256, bestIdx = -1;
@@ -235,9 +216,35 @@ __device__ int scan_best(const MatchShared& S, const TrackConsts& c, const ProjI
   return bestIdx < 0 ? -1 : ((bestDist << 16) | bestIdx);
 }
 
+constexpr int kTopK = 4;
+
+template <int KMAX>
+struct MatchShared {
+  int cell_start[kGridCols * kGridRows + 1];
+  uint16_t items[KMAX];
+  float2 xy[KMAX];
+  float ur[KMAX];
+  float ang[KMAX];
+  int8_t oct[KMAX];
+  int16_t gc[KMAX];               // grid cell (PosInGrid) or -1
+  int top[KMAX * kTopK];          // phase A: best candidates (dist << 16 | idx), sorted;
+                                  // during the grid build: per-cell fill counters
+  uint8_t ntop[KMAX];             // candidates with dist <= TH_HIGH (saturating)
+  int bin[KMAX];                  // accepted -> histogram bin, else -1
+  int sel[KMAX];                  // accepted candidate (current-frame index)
+  int mpw[KMAX];                  // last writer (last-frame index) per current keypoint
+  uint32_t claimed[KMAX / 32];
+  uint32_t removed[KMAX / 32];
+  int hist[32];
+  int wsum[8];
+  int misc[8];
+};
+static_assert(kMatchMaxKp * kTopK >= kGridCols * kGridRows, "top[] doubles as cell fill counters");
+
+template <int KMAX>
 __global__ void __launch_bounds__(256) k_match_last(TrackConsts c, MatchArgs a) {
   extern __shared__ char smem_raw[];
-  MatchShared& S = *reinterpret_cast<MatchShared*>(smem_raw);
+  MatchShared<KMAX>& S = *reinterpret_cast<MatchShared<KMAX>*>(smem_raw);
   const int s = blockIdx.x, t = threadIdx.x;
   const int wave = t >> 6, lane = t & 63;
   if (a.active && !a.active[s].has_last) {
@@ -245,18 +252,15 @@ __global__ void __launch_bounds__(256) k_match_last(TrackConsts c, MatchArgs a) 
     for (int i = t; i < a.cur_n[s]; i += 256) a.match[(long long)s * a.kp_pitch + i] = -1;
     return;
   }
-  const int n = min(a.cur_n[s], kMatchMaxKp);
-  const int nl = min(a.last_n[s], kMatchMaxKp);
+  const int n = min(a.cur_n[s], KMAX);
+  const int nl = min(a.last_n[s], KMAX);
   const long long cb = (long long)s * a.kp_pitch;
   const KeyPointD* ck = a.cur_kps_un + cb;
   const uint8_t* cdesc = a.cur_desc + cb * 32;
   const float* Tc = a.Tcw + (long long)s * a.pose_stride;
   const float* Tl = a.Tlw + (long long)s * a.pose_stride;
   // ---- current frame into LDS + grid (AssignFeaturesToGrid, Frame.cc:265-287) ----
-  for (int i = t; i < kGridCols * kGridRows; i += 256) {
-    S.cell_start[i] = 0;
-    S.cell_fill[i] = 0;
-  }
+  for (int i = t; i < kGridCols * kGridRows; i += 256) S.cell_start[i] = 0;
   __syncthreads();
   for (int i = t; i < n; i += 256) {
     const KeyPointD k = ck[i];
@@ -276,8 +280,7 @@ __global__ void __launch_bounds__(256) k_match_last(TrackConsts c, MatchArgs a) 
     if (g >= 0) atomicAdd(&S.cell_start[g], 1);
   }
   __syncthreads();
-  // exclusive scan of 3072 cell counts (12 per thread)
-  {
+  {  // exclusive scan of the 3072 cell counts (12 per thread)
     constexpr int kPer = (kGridCols * kGridRows) / 256;
     int loc[kPer];
     int sum = 0;
@@ -300,26 +303,32 @@ __global__ void __launch_bounds__(256) k_match_last(TrackConsts c, MatchArgs a) 
 #pragma unroll
     for (int k = 0; k < kPer; k++) {
       S.cell_start[t * kPer + k] = run;
+      S.top[t * kPer + k] = run;  // fill counter
       run += loc[k];
     }
     if (t == 255) S.cell_start[kGridCols * kGridRows] = run;
     __syncthreads();
   }
-  // stable placement in index order, 256 keypoints per chunk
-  for (int base = 0; base < n; base += 256) {
-    const int i = base + t;
-    const int g = i < n ? (int)S.gc[i] : -1;
-    S.chunk_cell[t] = g;
-    __syncthreads();
-    if (g >= 0) {
-      int rank = 0;
-      for (int q = 0; q < t; q++) rank += (S.chunk_cell[q] == g);
-      S.items[S.cell_start[g] + S.cell_fill[g] + rank] = (uint16_t)i;
-    }
-    __syncthreads();
-    if (g >= 0) atomicAdd(&S.cell_fill[g], 1);
-    __syncthreads();
+  // place items (any order), then sort each cell by index: the reference's
+  // mGrid[ix][iy] vectors hold indices in increasing order
+  for (int i = t; i < n; i += 256) {
+    const int g = S.gc[i];
+    if (g >= 0) S.items[atomicAdd(&S.top[g], 1)] = (uint16_t)i;
   }
+  __syncthreads();
+  for (int cell = t; cell < kGridCols * kGridRows; cell += 256) {
+    const int b = S.cell_start[cell], e = S.cell_start[cell + 1];
+    for (int q = b + 1; q < e; q++) {
+      const uint16_t v = S.items[q];
+      int r = q - 1;
+      while (r >= b && S.items[r] > v) {
+        S.items[r + 1] = S.items[r];
+        r--;
+      }
+      S.items[r + 1] = v;
+    }
+  }
+  __syncthreads();
   // ---- forward/backward motion (ORBmatcher.cc:1724-1744) ----
   float twc[3], tlc[3];
   gemm_neg_Rt_t(Tc, twc);
@@ -330,98 +339,145 @@ __global__ void __launch_bounds__(256) k_match_last(TrackConsts c, MatchArgs a) 
   float th = a.th;
   int nmatches = 0;
   for (int attempt = 0; attempt < 2; attempt++) {
-    // ---- phase A ----
+    // ---- phase A: per map point, the first kTopK candidates with distance
+    // <= TH_HIGH in (distance, scan order), and how many such candidates exist
     for (int i = t; i < nl; i += 256) {
-      int res = -1;
+      int tk[kTopK] = {-1, -1, -1, -1};
+      int cnt = 0;
       const long long li = cb + i;
       if (a.last_has_mp[li] && !a.last_outlier[li]) {
         const ProjInfo p = project_point(c, Tc, a.last_xyz + li * 3, a.last_kps_un[li].octave, th,
                                          bForward, bBackward);
-        if (p.ok) res = scan_best(S, c, p, a.last_desc + li * 32, cdesc, false, mbf);
+        if (p.ok) {
+          const uint8_t* dMP = a.last_desc + li * 32;
+          const bool bCheckLevels = (p.minLevel > 0) || (p.maxLevel >= 0);
+          const float r = p.radius;
+          const float urp = p.u - mbf * p.invzc;
+          for (int ix = p.cx0; ix <= p.cx1; ix++) {
+            for (int iy = p.cy0; iy <= p.cy1; iy++) {
+              const int cell = ix + kGridCols * iy;
+              const int b = S.cell_start[cell], e = S.cell_start[cell + 1];
+              for (int q = b; q < e; q++) {
+                const int j = S.items[q];
+                const int oc = S.oct[j];
+                if (bCheckLevels) {
+                  if (oc < p.minLevel) continue;
+                  if (p.maxLevel >= 0 && oc > p.maxLevel) continue;
+                }
+                const float2 xy = S.xy[j];
+                if (!(fabsf(xy.x - p.u) < r && fabsf(xy.y - p.v) < r)) continue;
+                const float urj = S.ur[j];
+                if (urj > 0 && fabsf(urp - urj) > p.radius) continue;
+                const int dist = hamming32(dMP, cdesc + (long long)j * 32);
+                if (dist > 100) continue;
+                cnt++;
+                int v = (dist << 16) | j;
+                // stable insertion: equal distances keep scan order
+#pragma unroll
+                for (int q2 = 0; q2 < kTopK; q2++) {
+                  const int cur = tk[q2];
+                  if (cur < 0 || (v >> 16) < (cur >> 16)) {
+                    tk[q2] = v;
+                    v = cur;
+                    if (v < 0) break;
+                  }
+                }
+              }
+            }
+          }
+        }
       }
-      S.best[i] = res;
+#pragma unroll
+      for (int q2 = 0; q2 < kTopK; q2++) S.top[i * kTopK + q2] = tk[q2];
+      S.ntop[i] = (uint8_t)min(cnt, 255);
     }
     for (int i = t; i < n; i += 256) S.mpw[i] = -1;
-    for (int i = t; i < kMatchMaxKp / 32; i += 256) {
+    for (int i = t; i < KMAX / 32; i += 256) {
       S.claimed[i] = 0;
       S.removed[i] = 0;
     }
     if (t < 32) S.hist[t] = 0;
     __syncthreads();
-    // ---- phase B (wave 0, in last-frame index order) ----
+    // ---- phase B (wave 0): the reference's in-order loop, where a candidate
+    // taken by an earlier map point with Observations() > 0 is skipped ----
     if (wave == 0) {
       int acc = 0;
       for (int base = 0; base < nl; base += 64) {
         const int i = base + lane;
         const long long li = cb + i;
-        int bst = -1;
-        bool claimer = false;
+        const bool valid = i < nl && S.ntop[i] > 0;
+        const bool claimer = valid && a.last_nobs[li] > 0;
+        const int ntk = valid ? min((int)S.ntop[i], kTopK) : 0;
+        bool decided = !valid;
+        int p = 0;
+        int choice = -1;  // >= 0 candidate, -1 none, -2 needs a full re-scan
         if (i < nl) {
-          bst = S.best[i];
-          if (bst >= 0 && (bst >> 16) <= 100) claimer = a.last_nobs[li] > 0;
-          else bst = -1;
+          S.bin[i] = -1;
+          S.sel[i] = -1;
         }
-        const int k = bst >= 0 ? (bst & 0xFFFF) : -1;
-        bool conflict = k >= 0 && ((S.claimed[k >> 5] >> (k & 31)) & 1u);
-        for (int q = 0; q < 64; q++) {
-          const int kq = __shfl(k, q, 64);
-          const int cq = __shfl((int)claimer, q, 64);
-          if (q < lane && cq && kq == k && k >= 0) conflict = true;
-        }
-        if (__ballot(conflict) == 0ull) {
-          if (i < nl) {
-            if (k >= 0) {
+        int start = 0;
+        while (true) {
+          if (!decided && lane >= start) {
+            while (p < ntk) {
+              const int k = S.top[i * kTopK + p] & 0xFFFF;
+              if (!((S.claimed[k >> 5] >> (k & 31)) & 1u)) break;
+              p++;
+            }
+            choice = p < ntk ? (S.top[i * kTopK + p] & 0xFFFF) : (S.ntop[i] > kTopK ? -2 : -1);
+          }
+          // first undecided lane whose choice an earlier undecided claimer takes,
+          // or that needs a re-scan
+          const bool und = !decided && lane >= start;
+          const int cq_flag = (und && claimer && choice >= 0) ? 1 : 0;
+          bool coll = und && choice == -2;
+          for (int q = start; q < 64; q++) {
+            const int chq = __shfl(choice, q, 64);
+            const int flq = __shfl(cq_flag, q, 64);
+            if (q < lane && flq && chq == choice && und && choice >= 0) coll = true;
+          }
+          const unsigned long long cm = __ballot(coll);
+          const int lc = cm ? __ffsll((long long)cm) - 1 : 64;
+          if (und && lane < lc) {
+            if (choice >= 0) {
+              atomicMax(&S.mpw[choice], i);
+              if (claimer) atomicOr(&S.claimed[choice >> 5], 1u << (choice & 31));
+              float rot = a.last_kps_un[li].angle - S.ang[choice];
+              if (rot < 0.0f) rot += 360.0f;
+              int b = (int)roundf(rot * (30 / 360.0f));
+              if (b == 30) b = 0;
+              S.bin[i] = b;
+              S.sel[i] = choice;
+              acc++;
+            }
+            decided = true;
+          }
+          if (lc == 64) break;
+          __builtin_amdgcn_wave_barrier();
+          if (lane == lc && choice == -2) {
+            // all kTopK candidates taken: full re-scan excluding taken ones
+            const ProjInfo pj = project_point(c, Tc, a.last_xyz + li * 3, a.last_kps_un[li].octave,
+                                              th, bForward, bBackward);
+            const int r = scan_best(S, c, pj, a.last_desc + li * 32, cdesc, true, mbf);
+            if (r >= 0 && (r >> 16) <= 100) {
+              const int k = r & 0xFFFF;
               atomicMax(&S.mpw[k], i);
               if (claimer) atomicOr(&S.claimed[k >> 5], 1u << (k & 31));
-              // histogram bin (ORBmatcher.cc:1835-1845)
               float rot = a.last_kps_un[li].angle - S.ang[k];
               if (rot < 0.0f) rot += 360.0f;
               int b = (int)roundf(rot * (30 / 360.0f));
               if (b == 30) b = 0;
               S.bin[i] = b;
-              S.best[i] = k;
-            } else {
-              S.bin[i] = -1;
+              S.sel[i] = k;
+              acc++;
             }
+            decided = true;
           }
-          acc += __popcll(__ballot(k >= 0));
-        } else {
-          // replay this chunk point by point (lane 0)
-          if (lane == 0) {
-            for (int q = 0; q < 64 && base + q < nl; q++) {
-              const int ii = base + q;
-              const long long lii = cb + ii;
-              int r = S.best[ii];
-              if (r >= 0 && (r >> 16) <= 100) {
-                const int kk = r & 0xFFFF;
-                if ((S.claimed[kk >> 5] >> (kk & 31)) & 1u) {
-                  const ProjInfo p = project_point(c, Tc, a.last_xyz + lii * 3,
-                                                   a.last_kps_un[lii].octave, th, bForward,
-                                                   bBackward);
-                  r = scan_best(S, c, p, a.last_desc + lii * 32, cdesc, true, mbf);
-                }
-              } else if (r >= 0) {
-                r = -1;  // best > TH_HIGH without claims: still > TH_HIGH with claims
-              }
-              if (r >= 0 && (r >> 16) <= 100) {
-                const int kk = r & 0xFFFF;
-                S.mpw[kk] = ii;
-                if (a.last_nobs[lii] > 0) S.claimed[kk >> 5] |= 1u << (kk & 31);
-                float rot = a.last_kps_un[lii].angle - S.ang[kk];
-                if (rot < 0.0f) rot += 360.0f;
-                int b = (int)roundf(rot * (30 / 360.0f));
-                if (b == 30) b = 0;
-                S.bin[ii] = b;
-                S.best[ii] = kk;
-                acc++;
-              } else {
-                S.bin[ii] = -1;
-              }
-            }
-          }
+          __builtin_amdgcn_wave_barrier();
+          start = lc;
         }
-        __builtin_amdgcn_wave_barrier();
       }
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
       if (lane == 0) S.misc[0] = acc;
     }
     __syncthreads();
@@ -457,7 +513,7 @@ __global__ void __launch_bounds__(256) k_match_last(TrackConsts c, MatchArgs a) 
       for (int i = t; i < nl; i += 256) {
         const int b = S.bin[i];
         if (b >= 0 && b != ind1 && b != ind2 && b != ind3) {
-          const int k = S.best[i];
+          const int k = S.sel[i];
           atomicOr(&S.removed[k >> 5], 1u << (k & 31));
           nrem++;
         }
@@ -1161,7 +1217,7 @@ __global__ void __launch_bounds__(256) k_finish(TrackConsts c, StreamState* __re
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-size_t match_smem_bytes() { return sizeof(MatchShared); }
+size_t match_smem_bytes() { return sizeof(MatchShared<2048>); }
 size_t pose_smem_bytes() { return sizeof(PoseShared); }
 
 static void set_smem_attr_once(const void* fn, size_t bytes, bool* done) {
@@ -1183,8 +1239,9 @@ void launch_predict(StreamState* st, int nstreams, hipStream_t s) {
 }
 
 void launch_match_last(const TrackConsts& c, const MatchLaunch& m, int nstreams, hipStream_t s) {
-  static bool done = false;
-  set_smem_attr_once((const void*)k_match_last, sizeof(MatchShared), &done);
+  static bool done1 = false, done2 = false;
+  set_smem_attr_once((const void*)k_match_last<1024>, sizeof(MatchShared<1024>), &done1);
+  set_smem_attr_once((const void*)k_match_last<2048>, sizeof(MatchShared<2048>), &done2);
   MatchArgs a;
   a.cur_kps_un = m.cur_kps_un;
   a.cur_desc = m.cur_desc;
@@ -1210,7 +1267,12 @@ void launch_match_last(const TrackConsts& c, const MatchLaunch& m, int nstreams,
   a.check_ori = m.check_ori;
   a.retry = m.retry;
   a.active = m.active;
-  hipLaunchKernelGGL(k_match_last, dim3(nstreams), dim3(256), sizeof(MatchShared), s, c, a);
+  if (m.kp_pitch <= 1024)
+    hipLaunchKernelGGL(k_match_last<1024>, dim3(nstreams), dim3(256), sizeof(MatchShared<1024>), s,
+                       c, a);
+  else
+    hipLaunchKernelGGL(k_match_last<2048>, dim3(nstreams), dim3(256), sizeof(MatchShared<2048>), s,
+                       c, a);
 }
 
 void launch_pose(const TrackConsts& c, const PoseLaunch& p, int nstreams, hipStream_t s) {

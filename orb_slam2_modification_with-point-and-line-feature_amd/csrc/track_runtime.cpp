@@ -303,8 +303,10 @@ struct orbpl_tracker {
   int cur = 0;
   StreamState* d_state = nullptr;
   PoseEdge* d_edges = nullptr;
-  hipEvent_t ev[6] = {};
-  bool timed = false;
+  static constexpr int kRing = 64;   // steps kept in the timing ring
+  static constexpr int kEv = 10;     // events per step
+  std::vector<hipEvent_t> ring;      // kRing * kEv events
+  int ring_pos = 0, ring_count = 0;
   std::vector<void*> allocs;
 };
 
@@ -325,7 +327,7 @@ int orbpl_tracker_destroy(orbpl_tracker* t) {
   if (!t) return ORBPL_OK;
   (void)hipSetDevice(t->device);
   for (void* p : t->allocs) (void)hipFree(p);
-  for (auto& e : t->ev)
+  for (auto& e : t->ring)
     if (e) (void)hipEventDestroy(e);
   if (t->ex) orbx_destroy(t->ex);
   delete t;
@@ -384,7 +386,8 @@ int orbpl_tracker_create(const orbpl_orb_params* orb, const orbpl_camera* cam, i
   TA(t->d_state, S * sizeof(StreamState));
   TA(t->d_edges, S * kPoseMaxEdges * pose_edge_bytes());
 #undef TA
-  for (auto& e : t->ev)
+  t->ring.assign(orbpl_tracker::kRing * orbpl_tracker::kEv, nullptr);
+  for (auto& e : t->ring)
     if (hipEventCreate(&e) != hipSuccess) {
       orbpl_tracker_destroy(t);
       return hip_fail(hipErrorUnknown, "hipEventCreate", __LINE__);
@@ -426,16 +429,14 @@ int orbpl_tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_d
   float* dTlast = reinterpret_cast<float*>(st0 + offsetof(StreamState, Tlast));
   int* dNm = reinterpret_cast<int*>(st0 + offsetof(StreamState, nmatches));
   int* dNin = reinterpret_cast<int*>(st0 + offsetof(StreamState, ninliers));
-  t->timed = true;
-  HIP_CHECK(hipEventRecord(t->ev[0], s));
+  hipEvent_t* ev = &t->ring[(size_t)(t->ring_pos % orbpl_tracker::kRing) * orbpl_tracker::kEv];
   int rc = orbx_run(t->ex, d_gray, S, t->W, (long long)t->W * t->H,
-                    reinterpret_cast<orbpl_keypoint_dev*>(C.kps), C.desc, K, C.n);
+                    reinterpret_cast<orbpl_keypoint_dev*>(C.kps), C.desc, K, C.n, ev);
   if (rc) return rc;
-  HIP_CHECK(hipEventRecord(t->ev[1], s));
   launch_frame_prepare(t->consts, C.kps, C.n, K, d_depth, (long long)t->W * t->H, C.kps_un, C.depth,
                        C.uright, C.gcell, S, s);
   launch_predict(t->d_state, S, s);
-  HIP_CHECK(hipEventRecord(t->ev[2], s));
+  HIP_CHECK(hipEventRecord(ev[6], s));
   MatchLaunch m{};
   m.cur_kps_un = C.kps_un;
   m.cur_desc = C.desc;
@@ -462,7 +463,7 @@ int orbpl_tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_d
   m.retry = 1;
   m.active = t->d_state;
   launch_match_last(t->consts, m, S, s);
-  HIP_CHECK(hipEventRecord(t->ev[3], s));
+  HIP_CHECK(hipEventRecord(ev[7], s));
   PoseLaunch p{};
   p.kps_un = C.kps_un;
   p.uright = C.uright;
@@ -481,11 +482,13 @@ int orbpl_tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_d
   p.active = t->d_state;
   p.edges = t->d_edges;
   launch_pose(t->consts, p, S, s);
-  HIP_CHECK(hipEventRecord(t->ev[4], s));
+  HIP_CHECK(hipEventRecord(ev[8], s));
   launch_finish(t->consts, t->d_state, C.n, K, C.kps_un, C.depth, C.match, C.outlier, C.has_mp,
                 C.mp_xyz, C.nobs, S, s);
-  HIP_CHECK(hipEventRecord(t->ev[5], s));
+  HIP_CHECK(hipEventRecord(ev[9], s));
   HIP_CHECK(hipGetLastError());
+  t->ring_pos++;
+  t->ring_count = std::min(t->ring_count + 1, (int)orbpl_tracker::kRing);
   t->cur ^= 1;
   return ORBPL_OK;
 }
@@ -515,12 +518,35 @@ int orbpl_tracker_get_state(orbpl_tracker* t, float* Tcw, int* nkps, int* nmatch
   return ORBPL_OK;
 }
 
+int orbpl_tracker_timings(orbpl_tracker* t, int max_steps, float* ms, int* n_steps) {
+  if (!t || !ms || !n_steps) return arg_fail("NULL argument");
+  HIP_CHECK(hipSetDevice(t->device));
+  HIP_CHECK(hipStreamSynchronize(t->stream));
+  const int n = std::min(max_steps, t->ring_count);
+  for (int k = 0; k < n; k++) {
+    const int step = t->ring_pos - n + k;
+    hipEvent_t* ev = &t->ring[(size_t)(step % orbpl_tracker::kRing) * orbpl_tracker::kEv];
+    for (int i = 0; i < 9; i++) HIP_CHECK(hipEventElapsedTime(&ms[k * 9 + i], ev[i], ev[i + 1]));
+  }
+  *n_steps = n;
+  return ORBPL_OK;
+}
+
+int orbpl_tracker_timings_reset(orbpl_tracker* t) {
+  if (!t) return arg_fail("NULL tracker");
+  t->ring_count = 0;
+  return ORBPL_OK;
+}
+
 int orbpl_tracker_stage_ms(orbpl_tracker* t, float* ms5) {
   if (!t || !ms5) return arg_fail("NULL argument");
-  if (!t->timed) return arg_fail("no step recorded yet");
-  HIP_CHECK(hipSetDevice(t->device));
-  HIP_CHECK(hipEventSynchronize(t->ev[5]));
-  for (int i = 0; i < 5; i++) HIP_CHECK(hipEventElapsedTime(&ms5[i], t->ev[i], t->ev[i + 1]));
+  if (t->ring_count == 0) return arg_fail("no step recorded yet");
+  float m[9];
+  int n = 0;
+  int rc = orbpl_tracker_timings(t, 1, m, &n);
+  if (rc) return rc;
+  ms5[0] = m[0] + m[1] + m[2] + m[3] + m[4];
+  for (int i = 0; i < 4; i++) ms5[1 + i] = m[5 + i];
   return ORBPL_OK;
 }
 

@@ -220,3 +220,24 @@ def textured_image(width=640, height=480, seed=0, noise_sigma=2.0):
     t = np.array([rng.uniform(-1, 1), rng.uniform(-0.3, 0.3), rng.uniform(-1, 1)])
     gray, _ = render(cam, se3(R, t), default_room(seed), seed=seed, noise_sigma=noise_sigma)
     return gray
+
+
+def loop_trajectory(n, seed=0, step_t=0.012, rot_amp_deg=4.0):
+    """Closed smooth loop of n camera-to-world poses (frame n == frame 0), so a
+    stream can cycle through it indefinitely with continuous motion: a circle
+    whose per-frame chord is ~step_t metres plus periodic rotation of
+    +-rot_amp_deg degrees (<= ~1 deg per frame for n >= 32)."""
+    rng = np.random.default_rng(seed)
+    r = step_t * n / (2 * np.pi)
+    ph = rng.uniform(0, 2 * np.pi, 4)
+    a = np.deg2rad(rot_amp_deg)
+    yaw0 = rng.uniform(-np.pi, np.pi)
+    poses = []
+    for i in range(n):
+        th = 2 * np.pi * i / n
+        t = np.array([r * np.cos(th + ph[0]), 0.1 * r * np.sin(2 * th + ph[1]),
+                      r * np.sin(th + ph[0]) - 0.3])
+        R = rot_xyz(0.5 * a * np.sin(th + ph[2]), yaw0 + a * np.sin(th + ph[3]),
+                    0.3 * a * np.cos(th + ph[2]))
+        poses.append(se3(R, t))
+    return poses
