@@ -59,23 +59,30 @@ def level_areas():
     return [int(a) * int(b) for a, b in zip(d["width"], d["height"])], d
 
 
-def algorithmic_bytes():
-    """Per-frame algorithmic HBM bytes of each kernel."""
+def algorithmic_bytes(n_kp):
+    """Per-frame algorithmic HBM bytes of each kernel:
+    the bytes the kernel must move at minimum (each input read once, each
+    output written once), with n_kp keypoints per frame."""
     areas, d = level_areas()
     S = sum(areas)
-    pads = [(int(a) + 38) * (int(b) + 38) for a, b in zip(d["width"], d["height"])]
-    K = d["max_keypoints"]
+    dims = list(zip((int(a) for a in d["width"]), (int(b) for b in d["height"])))
+    pads = [(a + 38) * (b + 38) for a, b in dims]
     return {
         # read the input (level 0) or the previous level, write the padded level
-        "pyramid": W * H + sum(pads) + sum(areas[:-1]),
+        "pyramid": W * H + sum(areas[:-1]) + sum(pads),
         # read each level's content + 3 px halo, write the blurred content
-        "blur": sum((int(a) + 6) * (int(b) + 6) for a, b in zip(d["width"], d["height"])) + S,
-        # read every pyramid level once; candidate output is negligible
+        "blur": sum((a + 6) * (b + 6) for a, b in dims) + S,
+        # read every pyramid level once (candidate output is ~1 % of it)
         "fast": S,
-        # candidates in/out of the octree (~4 B per candidate), keypoints out
-        "octree": 0,
-        # per keypoint: 31x31 patch + 512 blurred samples (~2 KB incl. lines), 60 B out
-        "orient_desc": 0,
+        # candidates in (4 B) and keypoints out (4 B); ~8 candidates per keypoint
+        "octree": 8 * n_kp * 4 + n_kp * 4,
+        # per keypoint: 31x31 raw patch + 37x37 blurred footprint + 60 B out
+        "orient_desc": n_kp * (961 + 1369 + 60),
+        # current frame (kp 28 + desc 32 + ur 4 + cell 4 + match out 4) and
+        # last frame (kp 28 + flags 2 + xyz 12 + desc 32 + nobs 4)
+        "match": n_kp * (72 + 78),
+        # per keypoint: kp 28 + ur 4 + match 4 + xyz 12 + outlier 2
+        "pose": n_kp * 50,
     }
 
 
@@ -178,17 +185,22 @@ def main():
     frames = S * args.steps * world
     value = frames / elapsed
 
-    # roofline of the dominant single-launch kernel
-    ab = algorithmic_bytes()
-    single = {"blur": 1, "fast": 2}
-    dom = max(single, key=lambda k: avg[single[k]])
-    dom_ms = float(avg[single[dom]])
-    bytes_launch = ab[dom] * S
+    # roofline of the dominant single-launch kernel (pyramid = 8 launches: excluded)
+    n_kp = float(st["nkeypoints"].mean())
+    ab = algorithmic_bytes(n_kp)
+    names = {"blur": "k_blur", "fast": "k_fast_cells", "octree": "k_octree",
+             "orient_desc": "k_orient_desc", "match": "k_match_last", "pose": "k_pose"}
+    idx = {k: tr.STAGES.index(k) for k in names}
+    dom = max(names, key=lambda k: avg[idx[k]])
+    dom_ms = float(avg[idx[dom]])
+    bytes_launch = int(ab[dom] * S)
     achieved = bytes_launch / (dom_ms * 1e-3) / 1e9
-    roof = {"bound": "hbm", "kernel": {"blur": "k_blur", "fast": "k_fast_cells"}[dom],
+    roof = {"bound": "hbm", "kernel": names[dom],
             "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-            "algorithmic_bytes_per_launch": bytes_launch, "avg_launch_ms": round(dom_ms, 4)}
+            "algorithmic_bytes_per_launch": bytes_launch, "avg_launch_ms": round(dom_ms, 4),
+            "per_kernel_GBps": {k: round(ab[k] * S / (float(avg[idx[k]]) * 1e-3) / 1e9, 1)
+                                for k in names}}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
