@@ -32,8 +32,9 @@ __device__ __forceinline__ int reflect101_dev(int p, int len) {
 }
 
 // ---------------------------------------------------------------------------
-// Pyramid level 0: copyMakeBorder(image, 19, REFLECT_101) (ORBextractor.cc:1127)
-// 4 padded pixels per thread, one u32 store.
+// Pyramid level 0 content: the input image, 16 bytes per thread into the
+// 16-B aligned content rows (ORBextractor.cc:1127 minus the border, which
+// k_pyr_border fills for every level at the end).
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_pyr_level0(const uint8_t* __restrict__ img, int stride,
                                                     long long frame_pitch,
@@ -41,93 +42,140 @@ __global__ void __launch_bounds__(256) k_pyr_level0(const uint8_t* __restrict__ 
                                                     const OrbGeom* __restrict__ g) {
   const LevelGeom& L = g->lv[0];
   const int f = blockIdx.z;
-  const int px0 = (blockIdx.x * 64 + threadIdx.x) * 4;
-  const int py = blockIdx.y * 4 + threadIdx.y;
-  if (px0 >= L.pw || py >= L.ph) return;
-  const uint8_t* src = img + (long long)f * frame_pitch;
-  const int sy = reflect101_dev(py - kEdge, L.h);
-  const uint8_t* row = src + (long long)sy * stride;
-  uint32_t packed = 0;
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    int px = px0 + k;
-    uint32_t v = 0;
-    if (px < L.pw) v = row[reflect101_dev(px - kEdge, L.w)];
-    packed |= v << (8 * k);
+  const int x0 = (blockIdx.x * 64 + threadIdx.x) * 16;
+  const int y = blockIdx.y * 4 + threadIdx.y;
+  if (x0 >= L.w || y >= L.h) return;
+  const uint8_t* src = img + (long long)f * frame_pitch + (long long)y * stride + x0;
+  uint8_t* dst = pyr + (long long)f * g->pyr_bytes + content_off(L, x0, y);
+  if (x0 + 16 <= L.w && ((reinterpret_cast<uintptr_t>(src) & 15) == 0)) {
+    *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+  } else {
+    const int n = min(16, L.w - x0);
+    for (int k = 0; k < n; k++) dst[k] = src[k];
   }
-  uint8_t* dst = pyr + (long long)f * g->pyr_bytes + L.pyr_off + (long long)py * L.pitch + px0;
-  *reinterpret_cast<uint32_t*>(dst) = packed;
 }
 
 // ---------------------------------------------------------------------------
-// Pyramid level l >= 1: resize(level l-1, INTER_LINEAR) in OpenCV's 8U
-// fixed-point form (11-bit coefficients, (S>>4)*beta>>16, +2>>2) followed by
-// copyMakeBorder(REFLECT_101 | ISOLATED): each padded pixel evaluates the
-// resize at its reflected content coordinate, so no separate border pass.
-// rs: xofs[w], alpha[w] (a0 | a1<<16), yofs[h], beta[h] for this level.
+// Pyramid level l >= 1 content: resize(level l-1, INTER_LINEAR) in OpenCV's 8U
+// fixed-point form (11-bit coefficients, (S>>4)*beta>>16, +2>>2). One
+// 256-thread block per 128x16 content tile: the source window (<= 64 dwords x
+// 48 rows) is staged in LDS with aligned dword loads, each item produces 4
+// output pixels and one aligned u32 store. rs: xofs[w], alpha[w] (a0|a1<<16),
+// yofs[h], beta[h] of this level.
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_pyr_level(uint8_t* __restrict__ pyr,
                                                    const OrbGeom* __restrict__ g, int level,
                                                    const int* __restrict__ rs_all) {
+  __shared__ uint32_t win[kPyrSrcRows][kPyrSrcDw + 1];
   const LevelGeom& L = g->lv[level];
   const LevelGeom& S = g->lv[level - 1];
-  const int f = blockIdx.z;
-  const int px0 = (blockIdx.x * 64 + threadIdx.x) * 4;
-  const int py = blockIdx.y * 4 + threadIdx.y;
-  if (px0 >= L.pw || py >= L.ph) return;
+  const int f = blockIdx.y;
+  const int ntx = (L.w + kPyrTileW - 1) / kPyrTileW;
+  const int tx = blockIdx.x % ntx, ty = blockIdx.x / ntx;
+  const int x0 = tx * kPyrTileW, y0 = ty * kPyrTileH;
+  const int x1 = min(x0 + kPyrTileW, L.w), y1 = min(y0 + kPyrTileH, L.h);
   const int* rs = rs_all + L.rs_off;
   const int* xofs = rs;
   const int* alpha = rs + L.w;
   const int* yofs = rs + 2 * L.w;
   const int* beta = rs + 2 * L.w + L.h;
   uint8_t* fp = pyr + (long long)f * g->pyr_bytes;
-  const uint8_t* sbase = fp + S.pyr_off + (long long)kEdge * S.pitch + kEdge;
-  const int cy = reflect101_dev(py - kEdge, L.h);
-  const int sy0 = yofs[cy];
-  const int ya = min(max(sy0, 0), S.h - 1);
-  const int yb = min(max(sy0 + 1, 0), S.h - 1);
-  const int bpk = beta[cy];
-  const int b0 = (int)(short)(bpk & 0xFFFF), b1 = (int)(short)(bpk >> 16);
-  const uint8_t* r0 = sbase + (long long)ya * S.pitch;
-  const uint8_t* r1 = sbase + (long long)yb * S.pitch;
-  uint32_t packed = 0;
+  const int a = xofs[x0] & ~3;
+  const int xb = min(xofs[x1 - 1] + 1, S.w - 1);
+  const int ndw = (xb + 1 - a + 3) >> 2;
+  const int ya = min(max(yofs[y0], 0), S.h - 1);
+  const int yb = min(max(yofs[y1 - 1] + 1, 0), S.h - 1);
+  const int nrows = yb - ya + 1;
+  const int t = threadIdx.x;
+  for (int i = t; i < nrows * ndw; i += 256) {
+    const int r = i / ndw, d = i - r * ndw;
+    win[r][d] = *reinterpret_cast<const uint32_t*>(fp + content_off(S, a + 4 * d, ya + r));
+  }
+  __syncthreads();
+  const uint8_t* wb = reinterpret_cast<const uint8_t*>(&win[0][0]);
+  constexpr int kRowB = (kPyrSrcDw + 1) * 4;
+  const int groups = (x1 - x0 + 3) >> 2;
+  for (int i = t; i < (y1 - y0) * groups; i += 256) {
+    const int r = i / groups, gq = i - r * groups;
+    const int y = y0 + r, x = x0 + 4 * gq;
+    const int sy0 = yofs[y];
+    const int r0 = min(max(sy0, 0), S.h - 1) - ya, r1 = min(max(sy0 + 1, 0), S.h - 1) - ya;
+    const int bpk = beta[y];
+    const int b0 = (int)(short)(bpk & 0xFFFF), b1 = (int)(short)(bpk >> 16);
+    uint32_t packed = 0;
 #pragma unroll
-  for (int k = 0; k < 4; k++) {
-    int px = px0 + k;
-    uint32_t v = 0;
-    if (px < L.pw) {
-      int cx = reflect101_dev(px - kEdge, L.w);
-      int sx = xofs[cx];
+    for (int k = 0; k < 4; k++) {
+      const int cx = min(x + k, L.w - 1);
+      const int sx = xofs[cx] - a;
       int h0, h1;
       if (cx < L.xmax) {
-        int apk = alpha[cx];
-        int a0 = (int)(short)(apk & 0xFFFF), a1 = (int)(short)(apk >> 16);
-        h0 = r0[sx] * a0 + r0[sx + 1] * a1;
-        h1 = r1[sx] * a0 + r1[sx + 1] * a1;
+        const int apk = alpha[cx];
+        const int a0 = (int)(short)(apk & 0xFFFF), a1 = (int)(short)(apk >> 16);
+        h0 = wb[r0 * kRowB + sx] * a0 + wb[r0 * kRowB + sx + 1] * a1;
+        h1 = wb[r1 * kRowB + sx] * a0 + wb[r1 * kRowB + sx + 1] * a1;
       } else {
-        h0 = r0[sx] * 2048;
-        h1 = r1[sx] * 2048;
+        h0 = wb[r0 * kRowB + sx] * 2048;
+        h1 = wb[r1 * kRowB + sx] * 2048;
       }
-      v = (uint32_t)((((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2);
+      const uint32_t v = (uint32_t)((((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2);
+      packed |= v << (8 * k);
     }
-    packed |= v << (8 * k);
+    // columns >= w of the last group land in the border, rewritten by k_pyr_border
+    *reinterpret_cast<uint32_t*>(fp + content_off(L, x, y)) = packed;
   }
-  uint8_t* dst = fp + L.pyr_off + (long long)py * L.pitch + px0;
-  *reinterpret_cast<uint32_t*>(dst) = packed;
+}
+
+// ---------------------------------------------------------------------------
+// copyMakeBorder(19, REFLECT_101[|ISOLATED]) of every level, one launch after
+// all levels exist (ORBextractor.cc:1122-1128): border pixel i of a level is
+// enumerated as 19 full top rows, 38 side pixels per content row, 19 full
+// bottom rows.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_pyr_border(uint8_t* __restrict__ pyr,
+                                                    const OrbGeom* __restrict__ g) {
+  const int f = blockIdx.y;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= g->border_total) return;
+  int level = 0;
+  while (level + 1 < g->nlevels && i >= g->lv[level + 1].border_base) level++;
+  const LevelGeom& L = g->lv[level];
+  int idx = i - L.border_base;
+  int px, py;
+  const int top = kEdge * L.pw;
+  if (idx < top) {
+    py = idx / L.pw;
+    px = idx - py * L.pw;
+  } else if ((idx -= top) < 2 * kEdge * L.h) {
+    py = kEdge + idx / (2 * kEdge);
+    const int k = idx - (py - kEdge) * (2 * kEdge);
+    px = k < kEdge ? k : L.w + k;
+  } else {
+    idx -= 2 * kEdge * L.h;
+    py = kEdge + L.h + idx / L.pw;
+    px = idx - (py - kEdge - L.h) * L.pw;
+  }
+  uint8_t* fp = pyr + (long long)f * g->pyr_bytes;
+  const int cx = reflect101_dev(px - kEdge, L.w), cy = reflect101_dev(py - kEdge, L.h);
+  fp[padded_off(L, px, py)] = fp[content_off(L, cx, cy)];
 }
 
 // ---------------------------------------------------------------------------
 // GaussianBlur(7x7, sigma 2, REFLECT_101), 8U fixed-point path (pinned P4):
 // out = (sum_v kv * sum_u ku * I + 2^15) >> 16 with k = {18,34,49,54,49,34,18}.
-// The padded pyramid already holds the REFLECT_101 border, so a 64x16 output
-// tile reads a 70x22 input tile straight from it. One launch covers every
-// level of every frame (tile list in the geometry).
+// The padded pyramid already holds the REFLECT_101 border, so a 128x32 output
+// tile reads its 140x38-byte input window straight from it with aligned dword
+// loads (content column x sits at padded column x + 19; the window starts at
+// padded column ox + 12, a multiple of 4). Horizontal pass: 4 outputs per
+// item from 3 LDS dwords; vertical pass: 4 outputs per item, one aligned u32
+// store into the content-only blurred level (row pitch bpitch).
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_blur(const uint8_t* __restrict__ pyr,
                                               uint8_t* __restrict__ blur,
                                               const OrbGeom* __restrict__ g) {
-  __shared__ uint8_t tin[kBlurTileH + 6][kBlurTileW + 8];
-  __shared__ int tmid[kBlurTileH + 6][kBlurTileW];
+  constexpr int TW = kBlurTileW, TH = kBlurTileH;
+  constexpr int IW = (TW + 32) / 4;          // input dwords per row: content ox-16 .. ox+143
+  __shared__ uint32_t tin[TH + 6][IW + 1];
+  __shared__ int4 tmid[TH + 6][TW / 4];
   const int f = blockIdx.y;
   int tile = blockIdx.x;
   int level = 0;
@@ -135,34 +183,54 @@ __global__ void __launch_bounds__(256) k_blur(const uint8_t* __restrict__ pyr,
   const LevelGeom& L = g->lv[level];
   tile -= L.blur_tile_base;
   const int tx = tile % L.blur_tiles_x, ty = tile / L.blur_tiles_x;
-  const int ox = tx * kBlurTileW, oy = ty * kBlurTileH;  // content coords of tile origin
+  const int ox = tx * TW, oy = ty * TH;  // content coords of the tile origin
   const uint8_t* src = pyr + (long long)f * g->pyr_bytes + L.pyr_off;
   const int t = threadIdx.x;
-  // load (16+6) x (64+6) bytes starting at content (ox-3, oy-3) = padded (ox+16, oy+16)
-  for (int i = t; i < (kBlurTileH + 6) * (kBlurTileW + 6); i += 256) {
-    int r = i / (kBlurTileW + 6), c = i % (kBlurTileW + 6);
-    int px = ox + kEdge - 3 + c, py = oy + kEdge - 3 + r;
-    uint8_t v = 0;
-    if (px < L.pw && py < L.ph) v = src[(long long)py * L.pitch + px];
-    tin[r][c] = v;
+  for (int i = t; i < (TH + 6) * IW; i += 256) {
+    const int r = i / IW, d = i - r * IW;
+    const int py = oy + (kEdge - 3) + r;            // padded row of content row oy-3+r
+    const int bc = kContent0 - 16 + ox + 4 * d;      // byte column in the row (multiple of 4)
+    uint32_t v = 0;
+    if (py < L.ph && bc + 4 <= L.pitch)
+      v = *reinterpret_cast<const uint32_t*>(src + (long long)py * L.pitch + bc);
+    tin[r][d] = v;
   }
   __syncthreads();
   const int k0 = 18, k1 = 34, k2 = 49, k3 = 54;
-  for (int i = t; i < (kBlurTileH + 6) * kBlurTileW; i += 256) {
-    int r = i / kBlurTileW, c = i % kBlurTileW;
-    const uint8_t* p = &tin[r][c];
-    tmid[r][c] = k0 * (p[0] + p[6]) + k1 * (p[1] + p[5]) + k2 * (p[2] + p[4]) + k3 * p[3];
+  for (int i = t; i < (TH + 6) * (TW / 4); i += 256) {
+    const int r = i / (TW / 4), gq = i - r * (TW / 4);
+    // LDS byte j holds content column ox - 16 + j; x = ox + 4gq needs x-3 .. x+6,
+    // i.e. bytes 4gq+13 .. 4gq+22 = dwords gq+3 .. gq+5 starting at byte 1
+    const uint32_t w0 = tin[r][gq + 3], w1 = tin[r][gq + 4], w2 = tin[r][gq + 5];
+    int b[10];
+    b[0] = (w0 >> 8) & 0xFF; b[1] = (w0 >> 16) & 0xFF; b[2] = w0 >> 24;
+    b[3] = w1 & 0xFF; b[4] = (w1 >> 8) & 0xFF; b[5] = (w1 >> 16) & 0xFF; b[6] = w1 >> 24;
+    b[7] = w2 & 0xFF; b[8] = (w2 >> 8) & 0xFF; b[9] = (w2 >> 16) & 0xFF;
+    int4 h;
+    h.x = k0 * (b[0] + b[6]) + k1 * (b[1] + b[5]) + k2 * (b[2] + b[4]) + k3 * b[3];
+    h.y = k0 * (b[1] + b[7]) + k1 * (b[2] + b[6]) + k2 * (b[3] + b[5]) + k3 * b[4];
+    h.z = k0 * (b[2] + b[8]) + k1 * (b[3] + b[7]) + k2 * (b[4] + b[6]) + k3 * b[5];
+    h.w = k0 * (b[3] + b[9]) + k1 * (b[4] + b[8]) + k2 * (b[5] + b[7]) + k3 * b[6];
+    tmid[r][gq] = h;
   }
   __syncthreads();
-  uint8_t* dst = blur + (long long)f * g->pyr_bytes + L.pyr_off;
-  for (int i = t; i < kBlurTileH * kBlurTileW; i += 256) {
-    int r = i / kBlurTileW, c = i % kBlurTileW;
-    int x = ox + c, y = oy + r;
+  uint8_t* dst = blur + (long long)f * g->blur_bytes + L.boff;
+  for (int i = t; i < TH * (TW / 4); i += 256) {
+    const int r = i / (TW / 4), gq = i - r * (TW / 4);
+    const int x = ox + 4 * gq, y = oy + r;
     if (x >= L.w || y >= L.h) continue;
-    int acc = k0 * (tmid[r][c] + tmid[r + 6][c]) + k1 * (tmid[r + 1][c] + tmid[r + 5][c]) +
-              k2 * (tmid[r + 2][c] + tmid[r + 4][c]) + k3 * tmid[r + 3][c];
-    int v = (acc + (1 << 15)) >> 16;
-    dst[(long long)(y + kEdge) * L.pitch + (x + kEdge)] = (uint8_t)(v > 255 ? 255 : v);
+    const int4 a0 = tmid[r][gq], a1 = tmid[r + 1][gq], a2 = tmid[r + 2][gq], a3 = tmid[r + 3][gq],
+               a4 = tmid[r + 4][gq], a5 = tmid[r + 5][gq], a6 = tmid[r + 6][gq];
+    auto vsum = [&](int v0, int v1, int v2, int v3, int v4, int v5, int v6) -> uint32_t {
+      int acc = k0 * (v0 + v6) + k1 * (v1 + v5) + k2 * (v2 + v4) + k3 * v3;
+      int v = (acc + (1 << 15)) >> 16;
+      return (uint32_t)(v > 255 ? 255 : v);
+    };
+    const uint32_t o = vsum(a0.x, a1.x, a2.x, a3.x, a4.x, a5.x, a6.x) |
+                       (vsum(a0.y, a1.y, a2.y, a3.y, a4.y, a5.y, a6.y) << 8) |
+                       (vsum(a0.z, a1.z, a2.z, a3.z, a4.z, a5.z, a6.z) << 16) |
+                       (vsum(a0.w, a1.w, a2.w, a3.w, a4.w, a5.w, a6.w) << 24);
+    *reinterpret_cast<uint32_t*>(dst + (long long)y * L.bpitch + x) = o;
   }
 }
 
@@ -244,8 +312,7 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
   }
   const LevelGeom& L = g->lv[cg.level];
   const int cols = cg.x1 - cg.x0, rows = cg.y1 - cg.y0;
-  const uint8_t* src = pyr + (long long)f * g->pyr_bytes + L.pyr_off +
-                       (long long)(cg.y0 + kEdge) * L.pitch + (cg.x0 + kEdge);
+  const uint8_t* src = pyr + (long long)f * g->pyr_bytes + content_off(L, cg.x0, cg.y0);
   uint8_t* wimg = s_img[wave];
   uint8_t* wm = s_m[wave];
   const int ws = cols;  // LDS window stride
@@ -682,8 +749,7 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
   const uint32_t c = kp_list[(long long)f * g->kp_cap_total + slot];
   const int kx = cand_x(c) + kMinBorder, ky = cand_y(c) + kMinBorder;
   // --- IC_Angle: lane u+15 sums column u over the disc ---
-  const uint8_t* img = pyr + (long long)f * g->pyr_bytes + L.pyr_off +
-                       (long long)(ky + kEdge) * L.pitch + (kx + kEdge);
+  const uint8_t* img = pyr + (long long)f * g->pyr_bytes + content_off(L, kx, ky);
   int m01 = 0, m10 = 0;
   if (lane < 31) {
     const int u = lane - 15;
@@ -707,9 +773,8 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
   const float factorPI = (float)(3.14159265358979323846 / 180.f);
   float a, b;
   cr_cos_sin(angle * factorPI, &a, &b);
-  const uint8_t* bimg = blur + (long long)f * g->pyr_bytes + L.pyr_off +
-                        (long long)(ky + kEdge) * L.pitch + (kx + kEdge);
-  const int step = L.pitch;
+  const uint8_t* bimg = blur + (long long)f * g->blur_bytes + L.boff + (long long)ky * L.bpitch + kx;
+  const int step = L.bpitch;
   uint64_t words[4];
 #pragma unroll
   for (int r = 0; r < 4; r++) {
@@ -757,13 +822,17 @@ void launch_pyramid(const OrbGeom& hg, const OrbGeom* dg, const uint8_t* img, in
                     long long frame_pitch, uint8_t* pyr, const int* rs, int batch, hipStream_t s) {
   for (int l = 0; l < hg.nlevels; l++) {
     const LevelGeom& L = hg.lv[l];
-    dim3 block(64, 4);
-    dim3 grid((L.pw + 255) / 256, (L.ph + 3) / 4, batch);
-    if (l == 0)
+    if (l == 0) {
+      dim3 block(64, 4);
+      dim3 grid(((L.w + 15) / 16 + 63) / 64, (L.h + 3) / 4, batch);
       hipLaunchKernelGGL(k_pyr_level0, grid, block, 0, s, img, stride, frame_pitch, pyr, dg);
-    else
-      hipLaunchKernelGGL(k_pyr_level, grid, block, 0, s, pyr, dg, l, rs);
+    } else {
+      const int tiles = ((L.w + kPyrTileW - 1) / kPyrTileW) * ((L.h + kPyrTileH - 1) / kPyrTileH);
+      hipLaunchKernelGGL(k_pyr_level, dim3(tiles, batch), dim3(256), 0, s, pyr, dg, l, rs);
+    }
   }
+  hipLaunchKernelGGL(k_pyr_border, dim3((hg.border_total + 255) / 256, batch), dim3(256), 0, s, pyr,
+                     dg);
 }
 
 void launch_blur(const OrbGeom& hg, const OrbGeom* dg, const uint8_t* pyr, uint8_t* blur, int batch,

@@ -70,7 +70,8 @@ int build_orb_geometry(int nfeatures, float scale_factor, int nlevels, int W, in
     }
   }
   // --- levels ---
-  long long off = 0;
+  long long off = 0, boff = 0;
+  int border_total = 0;
   int cell_total = 0, kp_total = 0, blur_total = 0;
   int max_slots = 1;
   G.cells.clear();
@@ -86,9 +87,14 @@ int build_orb_geometry(int nfeatures, float scale_factor, int nlevels, int W, in
     }
     L.pw = L.w + 2 * kEdge;
     L.ph = L.h + 2 * kEdge;
-    L.pitch = round_up(L.pw, 16);
+    L.pitch = round_up(kLead + L.pw, 16);
     L.pyr_off = off;
     off += (long long)round_up(L.pitch * L.ph, 256);
+    L.bpitch = round_up(L.w, 16);
+    L.border_base = border_total;
+    border_total += L.pw * L.ph - L.w * L.h;
+    L.boff = boff;
+    boff += (long long)round_up(L.bpitch * L.h, 256);
     L.scale = G.scale[l];
     L.nfeat = nfeat[l];
     L.scaled_patch = (int)(31 * G.scale[l]);
@@ -157,6 +163,8 @@ int build_orb_geometry(int nfeatures, float scale_factor, int nlevels, int W, in
   g.blur_tiles_total = blur_total;
   g.cell_slots = max_slots;
   g.pyr_bytes = off;
+  g.blur_bytes = boff;
+  g.border_total = border_total;
   int cand_total = 0;
   for (int l = 0; l < nlevels; l++) {
     LevelGeom& L = g.lv[l];
@@ -198,6 +206,23 @@ int build_orb_geometry(int nfeatures, float scale_factor, int nlevels, int W, in
       beta[dy] = (b0 & 0xFFFF) | (b1 << 16);
     }
     L.xmax = xmax;
+    for (int x0 = 0; x0 < dw; x0 += kPyrTileW) {
+      const int x1 = std::min(x0 + kPyrTileW, dw);
+      const int a = xofs[x0] & ~3, b = std::min(xofs[x1 - 1] + 1, sw - 1);
+      if ((b + 1 - a + 3) / 4 > kPyrSrcDw) {
+        *err = "scale factor too large for the resize tile";
+        return ORBPL_ERR_ARG;
+      }
+    }
+    for (int y0 = 0; y0 < dh; y0 += kPyrTileH) {
+      const int y1 = std::min(y0 + kPyrTileH, dh);
+      const int a = std::min(std::max(yofs[y0], 0), sh - 1);
+      const int b = std::min(std::max(yofs[y1 - 1] + 1, 0), sh - 1);
+      if (b - a + 1 > kPyrSrcRows) {
+        *err = "scale factor too large for the resize tile";
+        return ORBPL_ERR_ARG;
+      }
+    }
     G.rs.insert(G.rs.end(), xofs.begin(), xofs.end());
     G.rs.insert(G.rs.end(), alpha.begin(), alpha.end());
     G.rs.insert(G.rs.end(), yofs.begin(), yofs.end());

@@ -9,6 +9,10 @@ namespace orbpl {
 constexpr int kMaxLevels = 16;
 constexpr int kEdge = 19;          // EDGE_THRESHOLD (ORBextractor.cc:74)
 constexpr int kMinBorder = 16;     // EDGE_THRESHOLD - 3 (ORBextractor.cc:773)
+// Padded row py of a level starts kLead bytes into its pitch, so that content
+// column 0 (padded column 19) sits at byte 32: content rows are 16-B aligned.
+constexpr int kLead = 13;
+constexpr int kContent0 = kLead + 19;  // = 32
 constexpr int kOctMaxList = 1024;  // octree list capacity per (frame, level)
 constexpr int kMaxCandPerLevel = (1 << 20) - 1;
 
@@ -36,6 +40,9 @@ struct LevelGeom {
   int scaled_patch;    // (int)(PATCH_SIZE * scale)  (ORBextractor.cc:837)
   int blur_tile_base;  // first blur tile of this level
   int blur_tiles_x, blur_tiles_y;
+  int bpitch;          // blurred level row pitch (content only, multiple of 16)
+  int border_base;     // first border pixel of this level (k_pyr_border enumeration)
+  long long boff;      // byte offset of the blurred level inside one frame's blurred buffer
 };
 
 // One FAST window (ORBextractor.cc:789-806): [x0,x1) x [y0,y1) in level
@@ -53,13 +60,30 @@ struct OrbGeom {
   int cand_cap_total;  // sum of cand_cap
   int blur_tiles_total;
   int cell_slots;      // max corners a FAST window can emit: ceil(dw/2)*ceil(dh/2)
+  int border_total;    // border pixels of all levels (per frame)
+  int pyr_tiles_total; // unused (reserved)
   long long pyr_bytes; // bytes of one frame's padded pyramid
+  long long blur_bytes;  // bytes of one frame's blurred (content-only) pyramid
   int umax[16];        // IC_Angle circular patch row extents (ORBextractor.cc:454-469)
   LevelGeom lv[kMaxLevels];
 };
 
-constexpr int kBlurTileW = 64;
-constexpr int kBlurTileH = 16;
+constexpr int kBlurTileW = 128;
+constexpr int kBlurTileH = 32;
+
+// Byte offsets (within one frame's padded pyramid) of a content pixel and of
+// a padded pixel.
+__host__ __device__ inline long long content_off(const LevelGeom& L, int x, int y) {
+  return L.pyr_off + (long long)(y + kEdge) * L.pitch + kContent0 + x;
+}
+__host__ __device__ inline long long padded_off(const LevelGeom& L, int px, int py) {
+  return L.pyr_off + (long long)py * L.pitch + kLead + px;
+}
+
+constexpr int kPyrTileW = 128;   // content tile of the resize kernel
+constexpr int kPyrTileH = 16;
+constexpr int kPyrSrcDw = 64;    // LDS source window: dwords per row
+constexpr int kPyrSrcRows = 48;  // LDS source window: rows
 
 // Candidate packing: x (12 bits) | y (12 bits) << 12 | score (8 bits) << 24,
 // coordinates relative to minBorder (the reference's vToDistributeKeys frame).

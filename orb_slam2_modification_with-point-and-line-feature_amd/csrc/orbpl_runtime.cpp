@@ -194,7 +194,7 @@ int orbx_create(const orbpl_orb_params* p, int width, int height, int max_batch,
   CK(hipMalloc(&c->d_rs, sizeof(int) * c->hg.rs.size()));
   CK(hipMalloc(&c->d_in, B * (size_t)width * height));
   CK(hipMalloc(&c->d_pyr, B * (size_t)g.pyr_bytes));
-  CK(hipMalloc(&c->d_blur, B * (size_t)g.pyr_bytes));
+  CK(hipMalloc(&c->d_blur, B * (size_t)g.blur_bytes));
   CK(hipMalloc(&c->d_cell_cands, B * (size_t)std::max(1, g.ncells_total) * g.cell_slots * 4));
   CK(hipMalloc(&c->d_cell_counts, B * (size_t)std::max(1, g.ncells_total) * 4));
   CK(hipMalloc(&c->d_kcand, B * (size_t)std::max(1, g.cand_cap_total) * 4));
@@ -207,7 +207,7 @@ int orbx_create(const orbpl_orb_params* p, int width, int height, int max_batch,
   CK(hipMalloc(&c->d_err, 4));
   CK(hipMemsetAsync(c->d_err, 0, 4, c->stream));
   CK(hipMemsetAsync(c->d_pyr, 0, B * (size_t)g.pyr_bytes, c->stream));
-  CK(hipMemsetAsync(c->d_blur, 0, B * (size_t)g.pyr_bytes, c->stream));
+  CK(hipMemsetAsync(c->d_blur, 0, B * (size_t)g.blur_bytes, c->stream));
   CK(hipMemcpyAsync(c->d_geom, &g, sizeof(OrbGeom), hipMemcpyHostToDevice, c->stream));
   if (!c->hg.cells.empty())
     CK(hipMemcpyAsync(c->d_cells, c->hg.cells.data(), sizeof(CellGeom) * c->hg.cells.size(),
@@ -376,6 +376,7 @@ int orbx_get_pyramid(orbx_ctx* c, int frame, int level, int padded, int blurred,
   if (level < 0 || level >= g.nlevels || frame < 0 || frame >= c->max_batch)
     return arg_fail("level/frame out of range");
   const LevelGeom& L = g.lv[level];
+  if (blurred) padded = 0;  // the blurred working image has no border (content only)
   const int ow = padded ? L.pw : L.w, oh = padded ? L.ph : L.h;
   if (w) *w = ow;
   if (h) *h = oh;
@@ -383,9 +384,17 @@ int orbx_get_pyramid(orbx_ctx* c, int frame, int level, int padded, int blurred,
   if (out_cap < ow * oh) return ORBPL_ERR_CAPACITY;
   HIP_CHECK(hipSetDevice(c->device));
   HIP_CHECK(hipStreamSynchronize(c->stream));
-  const uint8_t* base = (blurred ? c->d_blur : c->d_pyr) + (size_t)frame * g.pyr_bytes + L.pyr_off;
-  if (!padded) base += (size_t)kEdge * L.pitch + kEdge;
-  HIP_CHECK(hipMemcpy2D(out, ow, base, L.pitch, ow, oh, hipMemcpyDeviceToHost));
+  const uint8_t* base;
+  int pitch;
+  if (blurred) {
+    base = c->d_blur + (size_t)frame * g.blur_bytes + L.boff;
+    pitch = L.bpitch;
+  } else {
+    base = c->d_pyr + (size_t)frame * g.pyr_bytes +
+           (padded ? padded_off(L, 0, 0) : content_off(L, 0, 0));
+    pitch = L.pitch;
+  }
+  HIP_CHECK(hipMemcpy2D(out, ow, base, pitch, ow, oh, hipMemcpyDeviceToHost));
   return ORBPL_OK;
 }
 
