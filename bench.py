@@ -125,6 +125,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pipelined", type=int, default=0,
+                    help="1 = overlap extraction of step t+1 with tracking of step t")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -150,6 +152,7 @@ def main():
     d_depth = pkg.DeviceBuffer.from_array(depth[rep], device=local_rank)
     cam = pkg.make_camera(synth.TUM1)
     tr = pkg.Tracker(pkg.OrbParams(*ORB), cam, S, device=local_rank)
+    tr.set_pipelined(bool(args.pipelined))
     traj = synth.loop_trajectory(F, seed=1 + rank)
     tr.reset(np.stack([np.linalg.inv(traj[s % F]).astype(np.float32) for s in range(S)]).reshape(S, 16))
     fb, db = W * H, W * H * 4

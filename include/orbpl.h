@@ -237,6 +237,9 @@ int orbpl_tracker_reset(orbpl_tracker* tr, const float* Tcw0);
  * contiguous). Asynchronous on the tracker's stream. */
 int orbpl_tracker_step(orbpl_tracker* tr, const uint8_t* d_gray, const float* d_depth);
 int orbpl_tracker_synchronize(orbpl_tracker* tr);
+/* on != 0: extraction of step t+1 may overlap matching/pose of step t (two
+ * HIP streams, three frame buffers). Results are identical either way. */
+int orbpl_tracker_set_pipelined(orbpl_tracker* tr, int on);
 /* Results of the last step, per stream (any pointer may be NULL):
  * Tcw (16 floats), keypoints, SearchByProjection matches, PoseOptimization
  * inliers, map matches after outlier removal. */

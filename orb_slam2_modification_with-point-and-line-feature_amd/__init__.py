@@ -332,6 +332,7 @@ def _declare_track(L):
     L.orbpl_tracker_reset.argtypes = [vp, vp]
     L.orbpl_tracker_step.argtypes = [vp, vp, vp]
     L.orbpl_tracker_synchronize.argtypes = [vp]
+    L.orbpl_tracker_set_pipelined.argtypes = [vp, C.c_int]
     L.orbpl_tracker_get_state.argtypes = [vp, vp, vp, vp, vp, vp]
     L.orbpl_tracker_stage_ms.argtypes = [vp, vp]
     L.orbpl_tracker_kp_capacity.argtypes = [vp]
@@ -463,6 +464,10 @@ class Tracker:
 
     def synchronize(self):
         check(lib().orbpl_tracker_synchronize(self._h), "orbpl_tracker_synchronize")
+
+    def set_pipelined(self, on=True):
+        """Overlap extraction of step t+1 with tracking of step t (2 streams)."""
+        check(lib().orbpl_tracker_set_pipelined(self._h, int(bool(on))), "orbpl_tracker_set_pipelined")
 
     def state(self):
         S = self.S

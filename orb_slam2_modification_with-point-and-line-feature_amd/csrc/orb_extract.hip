@@ -246,49 +246,97 @@ __global__ void __launch_bounds__(256) k_blur(const uint8_t* __restrict__ pyr,
 // One wave per window, 4 windows per 256-thread block. Candidates are
 // written in the reference's row-major emission order into the window's slot.
 // ---------------------------------------------------------------------------
-constexpr int kFastMaxWin = 66;  // window edge <= wcell + 6 <= 65
+// LDS layout of one window (one wave): P[r][q] = pix(a0+q) | pix(a0+q+1) << 16
+// for window row r, where a0 = x0 & ~3 (dword-aligned start of the row), so
+// one ds_read_b32 gives a ring pixel for two horizontally adjacent centres and
+// the 9-arc min/max runs on packed i16 pairs (v_pk_min_i16 / v_pk_max_i16).
+// M[r][q] = m(q) | m(q+1) << 16 in the same coordinates, m clamped to [0,255]
+// and zero outside the detection region.
+//
+// 3x3 NMS at threshold t (FAST_t nonmax_suppression on cornerScore = m - 1):
+// keep p  <=>  m >= max(t+1, 2)  and  m > max(m of the 8 neighbours).
+// (A neighbour n with m_n >= m >= t+1 is itself a corner, so comparing raw m
+// values is the same as the reference's comparison of neighbour scores, where
+// non-corners score 0.)
+__host__ __device__ constexpr int fast_pstride(int win_w) { return ((win_w + 3 + 4) + 3) & ~3; }
+__host__ __device__ constexpr int fast_wave_words(int win_w, int win_h) {
+  return 2 * win_h * fast_pstride(win_w);
+}
 
-__device__ __forceinline__ int fast_m(const uint8_t* w, int ws, int x, int y) {
-  const uint8_t* c = w + y * ws + x;
-  const int v = c[0];
-  int d[16];
-  d[0] = v - c[3 * ws];
-  d[1] = v - c[3 * ws + 1];
-  d[2] = v - c[2 * ws + 2];
-  d[3] = v - c[ws + 3];
-  d[4] = v - c[3];
-  d[5] = v - c[-ws + 3];
-  d[6] = v - c[-2 * ws + 2];
-  d[7] = v - c[-3 * ws + 1];
-  d[8] = v - c[-3 * ws];
-  d[9] = v - c[-3 * ws - 1];
-  d[10] = v - c[-2 * ws - 2];
-  d[11] = v - c[-ws - 3];
-  d[12] = v - c[-3];
-  d[13] = v - c[ws - 3];
-  d[14] = v - c[2 * ws - 2];
-  d[15] = v - c[3 * ws - 1];
-  int mn2[16], mx2[16];
+typedef short fshort2 __attribute__((ext_vector_type(2)));
+typedef unsigned short fushort2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ fshort2 as_s2(uint32_t v) { return __builtin_bit_cast(fshort2, v); }
+__device__ __forceinline__ fushort2 as_u2(uint32_t v) { return __builtin_bit_cast(fushort2, v); }
+__device__ __forceinline__ fshort2 pmin(fshort2 a, fshort2 b) { return __builtin_elementwise_min(a, b); }
+__device__ __forceinline__ fshort2 pmax(fshort2 a, fshort2 b) { return __builtin_elementwise_max(a, b); }
+__device__ __forceinline__ fushort2 pmaxu(fushort2 a, fushort2 b) { return __builtin_elementwise_max(a, b); }
+
+// m = max(A, -B) for the two centres held in P at (r, q) and (r, q + 1).
+__device__ __forceinline__ fshort2 fast_m2(const uint32_t* P, int ps, int r, int q) {
+  const uint32_t* c = P + r * ps + q;
+  const fshort2 v = as_s2(c[0]);
+  fshort2 d[16];
+  d[0] = v - as_s2(c[3 * ps]);
+  d[1] = v - as_s2(c[3 * ps + 1]);
+  d[2] = v - as_s2(c[2 * ps + 2]);
+  d[3] = v - as_s2(c[ps + 3]);
+  d[4] = v - as_s2(c[3]);
+  d[5] = v - as_s2(c[-ps + 3]);
+  d[6] = v - as_s2(c[-2 * ps + 2]);
+  d[7] = v - as_s2(c[-3 * ps + 1]);
+  d[8] = v - as_s2(c[-3 * ps]);
+  d[9] = v - as_s2(c[-3 * ps - 1]);
+  d[10] = v - as_s2(c[-2 * ps - 2]);
+  d[11] = v - as_s2(c[-ps - 3]);
+  d[12] = v - as_s2(c[-3]);
+  d[13] = v - as_s2(c[ps - 3]);
+  d[14] = v - as_s2(c[2 * ps - 2]);
+  d[15] = v - as_s2(c[3 * ps - 1]);
+  fshort2 mn2[16], mx2[16];
 #pragma unroll
   for (int k = 0; k < 16; k++) {
-    mn2[k] = min(d[k], d[(k + 1) & 15]);
-    mx2[k] = max(d[k], d[(k + 1) & 15]);
+    mn2[k] = pmin(d[k], d[(k + 1) & 15]);
+    mx2[k] = pmax(d[k], d[(k + 1) & 15]);
   }
-  int mn4[16], mx4[16];
+  fshort2 mn4[16], mx4[16];
 #pragma unroll
   for (int k = 0; k < 16; k++) {
-    mn4[k] = min(mn2[k], mn2[(k + 2) & 15]);
-    mx4[k] = max(mx2[k], mx2[(k + 2) & 15]);
+    mn4[k] = pmin(mn2[k], mn2[(k + 2) & 15]);
+    mx4[k] = pmax(mx2[k], mx2[(k + 2) & 15]);
   }
-  int A = -1024, B = 1024;
+  fshort2 A = {-1024, -1024}, B = {1024, 1024};
 #pragma unroll
   for (int k = 0; k < 16; k++) {
-    int mn8 = min(mn4[k], mn4[(k + 4) & 15]);
-    int mx8 = max(mx4[k], mx4[(k + 4) & 15]);
-    A = max(A, min(mn8, d[(k + 8) & 15]));
-    B = min(B, max(mx8, d[(k + 8) & 15]));
+    const fshort2 mn8 = pmin(mn4[k], mn4[(k + 4) & 15]);
+    const fshort2 mx8 = pmax(mx4[k], mx4[(k + 4) & 15]);
+    A = pmax(A, pmin(mn8, d[(k + 8) & 15]));
+    B = pmin(B, pmax(mx8, d[(k + 8) & 15]));
   }
-  return max(A, -B);
+  const fshort2 zero = {0, 0}, top = {255, 255};
+  return pmin(pmax(pmax(A, zero - B), zero), top);
+}
+
+// floor(k / n) by multiply-high: inv = ceil(2^32 / n) for n >= 2 (exact for
+// k * n < 2^32), inv = 0 for n == 1.
+__device__ __forceinline__ uint32_t div_inv(int n) {
+  return n > 1 ? (uint32_t)((0xFFFFFFFFull + (unsigned)n) / (unsigned)n) : 0u;
+}
+__device__ __forceinline__ int div_small(int k, uint32_t inv) {
+  return inv ? (int)__umulhi((uint32_t)k, inv) : k;
+}
+
+// NMS for the centre pair at M[r][q], M[r][q+1]: returns (m_lo, m_hi) in
+// *m and the max over each centre's 8 neighbours in *mx.
+__device__ __forceinline__ void nms_pair(const uint32_t* M, int ps, int r, int q, fushort2* m,
+                                         fushort2* mx) {
+  const uint32_t* c = M + r * ps + q;
+  *m = as_u2(c[0]);
+  fushort2 a = pmaxu(as_u2(c[-1]), as_u2(c[1]));
+  a = pmaxu(a, pmaxu(as_u2(c[-ps - 1]), as_u2(c[-ps])));
+  a = pmaxu(a, pmaxu(as_u2(c[-ps + 1]), as_u2(c[ps - 1])));
+  a = pmaxu(a, pmaxu(as_u2(c[ps]), as_u2(c[ps + 1])));
+  *mx = a;
 }
 
 __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ pyr,
@@ -297,8 +345,7 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
                                                     uint32_t* __restrict__ cell_cands,
                                                     int* __restrict__ cell_counts, int ini_th,
                                                     int min_th) {
-  __shared__ uint8_t s_img[4][kFastMaxWin * kFastMaxWin];
-  __shared__ uint8_t s_m[4][kFastMaxWin * kFastMaxWin];
+  extern __shared__ uint32_t fast_smem[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int f = blockIdx.y;
   const int cell = blockIdx.x * 4 + wave;
@@ -310,62 +357,93 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
     if (lane == 0) *cnt_out = 0;
     return;
   }
+  const int ps = fast_pstride(g->fast_win_w);
+  uint32_t* P = fast_smem + wave * fast_wave_words(g->fast_win_w, g->fast_win_h);
+  uint32_t* M = P + g->fast_win_h * ps;
   const LevelGeom& L = g->lv[cg.level];
   const int cols = cg.x1 - cg.x0, rows = cg.y1 - cg.y0;
-  const uint8_t* src = pyr + (long long)f * g->pyr_bytes + content_off(L, cg.x0, cg.y0);
-  uint8_t* wimg = s_img[wave];
-  uint8_t* wm = s_m[wave];
-  const int ws = cols;  // LDS window stride
-  for (int i = lane; i < rows * cols; i += 64) {
-    int r = i / cols, c = i - r * cols;
-    wimg[i] = src[(long long)r * L.pitch + c];
-    wm[i] = 0;
+  const int a0 = cg.x0 & ~3, sh = cg.x0 - a0;
+  // ---- stage the window as u16 pairs: dword j of a row -> P[r][4j .. 4j+3] ----
+  {
+    const uint8_t* rowp = pyr + (long long)f * g->pyr_bytes + content_off(L, a0, cg.y0);
+    const int nd = (sh + cols + 3) >> 2;
+    const uint32_t inv = div_inv(nd);
+    const int ntask = rows * nd;
+    for (int k = lane; k < ntask; k += 64) {
+      const int r = div_small(k, inv), j = k - r * nd;
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(rowp + (long long)r * L.pitch) + j;
+      const uint32_t d0 = src[0], d1 = src[1];
+      uint4 o;
+      o.x = __builtin_amdgcn_perm(d1, d0, 0x0c010c00u);
+      o.y = __builtin_amdgcn_perm(d1, d0, 0x0c020c01u);
+      o.z = __builtin_amdgcn_perm(d1, d0, 0x0c030c02u);
+      o.w = __builtin_amdgcn_perm(d1, d0, 0x0c040c03u);
+      *reinterpret_cast<uint4*>(P + r * ps + 4 * j) = o;
+      *reinterpret_cast<uint4*>(M + r * ps + 4 * j) = make_uint4(0, 0, 0, 0);
+    }
   }
   __builtin_amdgcn_wave_barrier();
-  // detection region: rows [3, rows-4], cols [3, cols-4]
+  // ---- m for the detection region rows [3, rows-3), cols [3, cols-3) ----
   const int dr = rows - 6, dc = cols - 6;
-  const int ndet = (dr > 0 && dc > 0) ? dr * dc : 0;
-  for (int i = lane; i < ndet; i += 64) {
-    int r = i / dc, c = i - r * dc;
-    int m = fast_m(wimg, ws, c + 3, r + 3);
-    wm[(r + 3) * ws + (c + 3)] = (uint8_t)(m < 0 ? 0 : (m > 255 ? 255 : m));
+  const int np = (dc + 1) >> 1;
+  const uint32_t inv_np = div_inv(np);
+  const int npair = (dr > 0 && dc > 0) ? dr * np : 0;
+  uint16_t* M16 = reinterpret_cast<uint16_t*>(M);
+  for (int k = lane; k < npair; k += 64) {
+    const int rr = div_small(k, inv_np), p = k - rr * np;
+    const int r = rr + 3, q = 3 + 2 * p + sh;
+    const fshort2 m2 = fast_m2(P, ps, r, q);
+    const uint32_t lo = (uint32_t)(uint16_t)m2.x;
+    const uint32_t hi = (2 * p + 1 < dc) ? (uint32_t)(uint16_t)m2.y : 0u;
+    M[r * ps + q] = lo | (hi << 16);
+    M16[2 * (r * ps + q - 1) + 1] = (uint16_t)lo;   // M[r][q-1].hi
+    M16[2 * (r * ps + q + 1)] = (uint16_t)hi;       // M[r][q+1].lo
   }
   __builtin_amdgcn_wave_barrier();
-  // NMS test at threshold t for detection pixel i (0 <= i < ndet)
-  auto nms_score = [&](int i, int t) -> int {
-    int r = i / dc, c = i - r * dc;
-    const uint8_t* p = wm + (r + 3) * ws + (c + 3);
-    int m = p[0];
-    if (m < t + 1) return -1;
-    int s = m - 1;
-    auto nb = [&](int mm) { return mm >= t + 1 ? mm - 1 : 0; };
-    // wm is zero outside the detection region, which nb() maps to 0
-    if (s > nb(p[1]) && s > nb(p[-1]) && s > nb(p[-ws - 1]) && s > nb(p[-ws]) &&
-        s > nb(p[-ws + 1]) && s > nb(p[ws - 1]) && s > nb(p[ws]) && s > nb(p[ws + 1]))
-      return s;
-    return -1;
-  };
   int t = ini_th < 0 ? 0 : (ini_th > 255 ? 255 : ini_th);
-  int found = 0;
-  for (int base = 0; base < ndet && !found; base += 64) {
-    int i = base + lane;
-    bool is = i < ndet && nms_score(i, t) >= 0;
-    found = __ballot(is) != 0ull;
+  {
+    const int T = max(t + 1, 2);
+    int found = 0;
+    for (int base = 0; base < npair && !found; base += 64) {
+      const int k = base + lane;
+      bool is = false;
+      if (k < npair) {
+        const int rr = div_small(k, inv_np), p = k - rr * np;
+        fushort2 m, mx;
+        nms_pair(M, ps, rr + 3, 3 + 2 * p + sh, &m, &mx);
+        is = (m.x >= T && m.x > mx.x) || (m.y >= T && m.y > mx.y);
+      }
+      found = __ballot(is) != 0ull;
+    }
+    if (!found) t = min_th < 0 ? 0 : (min_th > 255 ? 255 : min_th);
   }
-  if (!found) t = min_th < 0 ? 0 : (min_th > 255 ? 255 : min_th);
+  const int T = max(t + 1, 2);
   uint32_t* out = cell_cands + ((long long)f * g->ncells_total + cell) * slots;
   const int xoff = cg.x0 - kMinBorder, yoff = cg.y0 - kMinBorder;
   int n = 0;
-  for (int base = 0; base < ndet; base += 64) {
-    int i = base + lane;
-    int s = i < ndet ? nms_score(i, t) : -1;
-    unsigned long long mask = __ballot(s >= 0);
-    if (s >= 0) {
-      int pos = n + __popcll(mask & ((1ull << lane) - 1ull));
-      int r = i / dc, c = i - r * dc;
-      if (pos < slots) out[pos] = pack_cand(xoff + c + 3, yoff + r + 3, s);
+  for (int base = 0; base < npair; base += 64) {
+    const int k = base + lane;
+    bool clo = false, chi = false;
+    int rr = 0, p = 0;
+    fushort2 m = {0, 0};
+    if (k < npair) {
+      rr = div_small(k, inv_np);
+      p = k - rr * np;
+      fushort2 mx;
+      nms_pair(M, ps, rr + 3, 3 + 2 * p + sh, &m, &mx);
+      clo = m.x >= T && m.x > mx.x;
+      chi = m.y >= T && m.y > mx.y;   // m.y == 0 when the pixel is outside
     }
-    n += __popcll(mask);
+    const unsigned long long blo = __ballot(clo), bhi = __ballot(chi);
+    const unsigned long long below = (1ull << lane) - 1ull;
+    int pos = n + __popcll(blo & below) + __popcll(bhi & below);
+    const int x = xoff + 3 + 2 * p, y = yoff + rr + 3;
+    if (clo) {
+      if (pos < slots) out[pos] = pack_cand(x, y, m.x - 1);
+      pos++;
+    }
+    if (chi && pos < slots) out[pos] = pack_cand(x + 1, y, m.y - 1);
+    n += __popcll(blo) + __popcll(bhi);
   }
   if (lane == 0) *cnt_out = n < slots ? n : slots;
 }
@@ -843,8 +921,9 @@ void launch_blur(const OrbGeom& hg, const OrbGeom* dg, const uint8_t* pyr, uint8
 void launch_fast(const OrbGeom& hg, const OrbGeom* dg, const CellGeom* cells, const uint8_t* pyr,
                  uint32_t* cell_cands, int* cell_counts, int ini_th, int min_th, int batch,
                  hipStream_t s) {
-  hipLaunchKernelGGL(k_fast_cells, dim3((hg.ncells_total + 3) / 4, batch), dim3(256), 0, s, pyr, dg,
-                     cells, cell_cands, cell_counts, ini_th, min_th);
+  const size_t smem = 4 * 4 * (size_t)fast_wave_words(hg.fast_win_w, hg.fast_win_h);
+  hipLaunchKernelGGL(k_fast_cells, dim3((hg.ncells_total + 3) / 4, batch), dim3(256), smem, s, pyr,
+                     dg, cells, cell_cands, cell_counts, ini_th, min_th);
 }
 
 void launch_octree(const OrbGeom& hg, const OrbGeom* dg, const uint32_t* cell_cands,

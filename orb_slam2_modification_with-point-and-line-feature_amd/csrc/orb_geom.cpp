@@ -127,6 +127,8 @@ int build_orb_geometry(int nfeatures, float scale_factor, int nlevels, int W, in
           c.y0 = (int16_t)iniY;
           c.x1 = (int16_t)mx;
           c.y1 = (int16_t)my;
+          g.fast_win_w = std::max(g.fast_win_w, c.x1 - c.x0);
+          g.fast_win_h = std::max(g.fast_win_h, c.y1 - c.y0);
           const int dw = c.x1 - c.x0 - 6, dh = c.y1 - c.y0 - 6;
           if (dw > 0 && dh > 0) max_slots = std::max(max_slots, ((dw + 1) / 2) * ((dh + 1) / 2));
           if (c.x1 - c.x0 > 66 || c.y1 - c.y0 > 66) {

@@ -62,6 +62,8 @@ struct OrbGeom {
   int cell_slots;      // max corners a FAST window can emit: ceil(dw/2)*ceil(dh/2)
   int border_total;    // border pixels of all levels (per frame)
   int pyr_tiles_total; // unused (reserved)
+  int fast_win_w;      // largest FAST window (x1 - x0) over all cells
+  int fast_win_h;      // largest FAST window (y1 - y0)
   long long pyr_bytes; // bytes of one frame's padded pyramid
   long long blur_bytes;  // bytes of one frame's blurred (content-only) pyramid
   int umax[16];        // IC_Angle circular patch row extents (ORBextractor.cc:454-469)

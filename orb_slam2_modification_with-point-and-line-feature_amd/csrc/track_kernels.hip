@@ -651,6 +651,7 @@ struct PoseShared {
   uint8_t out_flag[kPoseMaxEdges];
   int scan[kPoseMaxEdges];
   double red[4][32];
+  double sys[1][28];              // reduced H (upper, row-major), b, robust chi2
   int wsum[8];
   int misc[8];
 };
@@ -784,6 +785,38 @@ __device__ void block_sum(double* v, PoseShared& S) {
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < NV; k++) v[k] = ((S.red[0][k] + S.red[1][k]) + S.red[2][k]) + S.red[3][k];
+  __syncthreads();
+}
+
+// One halving step of the transposed wave reduction: lanes whose `mask` bit
+// is set keep the upper half of v[0..2h), the others the lower half, each
+// adding its partner's copy of the half it keeps.
+template <int H>
+__device__ __forceinline__ void tr_step(double* v, int mask) {
+  const bool hi = (threadIdx.x & mask) != 0;
+#pragma unroll
+  for (int k = 0; k < H; k++) {
+    const double send = hi ? v[k] : v[k + H];
+    const double keep = hi ? v[k + H] : v[k];
+    v[k] = keep + __shfl_xor(send, mask, 64);
+  }
+}
+
+// Sum 28 per-thread doubles over the 256-thread block into out[0..28)
+// (shared memory). 29 shuffles per wave instead of 28 full butterflies.
+__device__ void block_sum28_to(double* v, PoseShared& S, double* out) {
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  tr_step<14>(v, 1);   // index k + 14*b0
+  tr_step<7>(v, 2);    // k + 7*b1 + 14*b0, k < 7
+  v[7] = 0;
+  tr_step<4>(v, 4);    // j = k + 4*b2 (j == 7 is padding)
+  tr_step<2>(v, 8);
+  tr_step<1>(v, 16);   // j = b4 + 2*b3 + 4*b2
+  v[0] += __shfl_xor(v[0], 32, 64);
+  const int j = ((lane >> 4) & 1) + 2 * ((lane >> 3) & 1) + 4 * ((lane >> 2) & 1);
+  if (lane < 32 && j < 7) S.red[wave][j + 7 * ((lane >> 1) & 1) + 14 * (lane & 1)] = v[0];
+  __syncthreads();
+  if (t < 28) out[t] = ((S.red[0][t] + S.red[1][t]) + S.red[2][t]) + S.red[3][t];
   __syncthreads();
 }
 
@@ -1015,23 +1048,14 @@ __global__ void __launch_bounds__(256) k_pose(TrackConsts tc, PoseArgs a) {
             }
           }
         }
-        block_sum<28>(acc, S);
-        double H[6][6], b[6];
-        {
-          int q = 0;
-          for (int i = 0; i < 6; i++)
-            for (int j = i; j < 6; j++) {
-              H[i][j] = acc[q];
-              H[j][i] = acc[q];
-              q++;
-            }
-          for (int i = 0; i < 6; i++) b[i] = acc[21 + i];
-        }
-        double currentChi = acc[27];
+        block_sum28_to(acc, S, S.sys[0]);
+        double b[6];
+        for (int i = 0; i < 6; i++) b[i] = S.sys[0][21 + i];
+        double currentChi = S.sys[0][27];
         const double iniChi = currentChi;
         if (it == 0) {
           double md = 0;
-          for (int j = 0; j < 6; j++) md = fmax(fabs(H[j][j]), md);
+          for (int j = 0, q = 0; j < 6; q += 6 - j, j++) md = fmax(fabs(S.sys[0][q]), md);
           lambda = 1e-5 * md;
           ni = 2;
           nBadLM = 0;
@@ -1041,8 +1065,16 @@ __global__ void __launch_bounds__(256) k_pose(TrackConsts tc, PoseArgs a) {
         do {
           const SE3d backup = T;
           double Hl[6][6];
-          for (int i = 0; i < 6; i++)
-            for (int j = 0; j < 6; j++) Hl[i][j] = H[i][j];
+          {
+            const double* sy = S.sys[0];
+            int q = 0;
+            for (int i = 0; i < 6; i++)
+              for (int j = i; j < 6; j++) {
+                Hl[i][j] = sy[q];
+                Hl[j][i] = sy[q];
+                q++;
+              }
+          }
           for (int j = 0; j < 6; j++) Hl[j][j] += lambda;
           const bool ok2 = solve6(Hl, b, x);
           T = se3_mul(se3_exp(x), T);

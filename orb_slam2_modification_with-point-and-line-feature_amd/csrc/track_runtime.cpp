@@ -297,14 +297,20 @@ struct orbpl_tracker {
   int S = 0;
   int W = 0, H = 0;
   int kp_cap = 0;
-  hipStream_t stream = nullptr;
+  // Two HIP streams: extraction (+ frame glue) of step t+1 runs on `stream`
+  // while matching / pose / finish of step t run on `tstream`. Three frame
+  // buffers: step t extracts into fb[t%3] and tracks against fb[(t-1)%3].
+  hipStream_t stream = nullptr;    // owned by the extractor context
+  hipStream_t tstream = nullptr;   // tracking stream
   TrackConsts consts{};
-  FrameBufs fb[2];
-  int cur = 0;
+  FrameBufs fb[3];
+  hipEvent_t ev_free[3] = {};      // fb[b] no longer read as "last frame"
+  bool free_pending[3] = {};
+  int pipelined = 0;               // 0: every stage on `stream`
   StreamState* d_state = nullptr;
   PoseEdge* d_edges = nullptr;
   static constexpr int kRing = 64;   // steps kept in the timing ring
-  static constexpr int kEv = 10;     // events per step
+  static constexpr int kEv = 11;     // events per step
   std::vector<hipEvent_t> ring;      // kRing * kEv events
   int ring_pos = 0, ring_count = 0;
   std::vector<void*> allocs;
@@ -327,8 +333,12 @@ int orbpl_tracker_destroy(orbpl_tracker* t) {
   if (!t) return ORBPL_OK;
   (void)hipSetDevice(t->device);
   for (void* p : t->allocs) (void)hipFree(p);
+  if (t->tstream) (void)hipStreamSynchronize(t->tstream);
   for (auto& e : t->ring)
     if (e) (void)hipEventDestroy(e);
+  for (auto& e : t->ev_free)
+    if (e) (void)hipEventDestroy(e);
+  if (t->tstream) (void)hipStreamDestroy(t->tstream);
   if (t->ex) orbx_destroy(t->ex);
   delete t;
   return ORBPL_OK;
@@ -368,7 +378,7 @@ int orbpl_tracker_create(const orbpl_orb_params* orb, const orbpl_camera* cam, i
     int _r = tr_alloc(t, (void**)&(ptr), (bytes));            \
     if (_r) { orbpl_tracker_destroy(t); return _r; }          \
   } while (0)
-  for (int b = 0; b < 2; b++) {
+  for (int b = 0; b < 3; b++) {
     FrameBufs& f = t->fb[b];
     TA(f.kps, S * K * sizeof(KeyPointD));
     TA(f.desc, S * K * 32);
@@ -392,6 +402,15 @@ int orbpl_tracker_create(const orbpl_orb_params* orb, const orbpl_camera* cam, i
       orbpl_tracker_destroy(t);
       return hip_fail(hipErrorUnknown, "hipEventCreate", __LINE__);
     }
+  for (auto& e : t->ev_free)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      orbpl_tracker_destroy(t);
+      return hip_fail(hipErrorUnknown, "hipEventCreate", __LINE__);
+    }
+  if (hipStreamCreateWithFlags(&t->tstream, hipStreamNonBlocking) != hipSuccess) {
+    orbpl_tracker_destroy(t);
+    return hip_fail(hipErrorUnknown, "hipStreamCreate", __LINE__);
+  }
   rc = orbpl_tracker_reset(t, nullptr);
   if (rc) {
     orbpl_tracker_destroy(t);
@@ -410,19 +429,20 @@ int orbpl_tracker_reset(orbpl_tracker* t, const float* Tcw0) {
     for (int k = 0; k < 16; k++) z.Tcw[k] = Tcw0 ? Tcw0[s * 16 + k] : (k % 5 == 0 ? 1.f : 0.f);
     st[s] = z;
   }
-  HIP_CHECK(hipMemcpyAsync(t->d_state, st.data(), sizeof(StreamState) * t->S, hipMemcpyHostToDevice,
-                           t->stream));
   HIP_CHECK(hipStreamSynchronize(t->stream));
+  if (t->tstream) HIP_CHECK(hipStreamSynchronize(t->tstream));
+  HIP_CHECK(hipMemcpy(t->d_state, st.data(), sizeof(StreamState) * t->S, hipMemcpyHostToDevice));
   return ORBPL_OK;
 }
 
 int orbpl_tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_depth) {
   if (!t || !d_gray || !d_depth) return arg_fail("NULL argument");
   HIP_CHECK(hipSetDevice(t->device));
-  FrameBufs& C = t->fb[t->cur];
-  FrameBufs& L = t->fb[t->cur ^ 1];
+  const int ci = t->ring_pos % 3, li = (t->ring_pos + 2) % 3;
+  FrameBufs& C = t->fb[ci];
+  FrameBufs& L = t->fb[li];
   const int S = t->S, K = t->kp_cap;
-  hipStream_t s = t->stream;
+  hipStream_t s = t->stream, ts = t->pipelined ? t->tstream : t->stream;
   const int pstride = (int)(sizeof(StreamState) / sizeof(float));
   char* st0 = reinterpret_cast<char*>(t->d_state);
   float* dTcw = reinterpret_cast<float*>(st0 + offsetof(StreamState, Tcw));
@@ -430,13 +450,18 @@ int orbpl_tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_d
   int* dNm = reinterpret_cast<int*>(st0 + offsetof(StreamState, nmatches));
   int* dNin = reinterpret_cast<int*>(st0 + offsetof(StreamState, ninliers));
   hipEvent_t* ev = &t->ring[(size_t)(t->ring_pos % orbpl_tracker::kRing) * orbpl_tracker::kEv];
+  // ---- extraction stream: wait until tracking of step t-1 released fb[ci]
+  if (t->free_pending[ci]) HIP_CHECK(hipStreamWaitEvent(s, t->ev_free[ci], 0));
   int rc = orbx_run(t->ex, d_gray, S, t->W, (long long)t->W * t->H,
                     reinterpret_cast<orbpl_keypoint_dev*>(C.kps), C.desc, K, C.n, ev);
   if (rc) return rc;
   launch_frame_prepare(t->consts, C.kps, C.n, K, d_depth, (long long)t->W * t->H, C.kps_un, C.depth,
                        C.uright, C.gcell, S, s);
-  launch_predict(t->d_state, S, s);
   HIP_CHECK(hipEventRecord(ev[6], s));
+  // ---- tracking stream
+  HIP_CHECK(hipStreamWaitEvent(ts, ev[6], 0));
+  HIP_CHECK(hipEventRecord(ev[7], ts));
+  launch_predict(t->d_state, S, ts);
   MatchLaunch m{};
   m.cur_kps_un = C.kps_un;
   m.cur_desc = C.desc;
@@ -462,8 +487,8 @@ int orbpl_tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_d
   m.check_ori = 1;       // ORBmatcher(0.9, true) (Tracking.cc:1216)
   m.retry = 1;
   m.active = t->d_state;
-  launch_match_last(t->consts, m, S, s);
-  HIP_CHECK(hipEventRecord(ev[7], s));
+  launch_match_last(t->consts, m, S, ts);
+  HIP_CHECK(hipEventRecord(ev[8], ts));
   PoseLaunch p{};
   p.kps_un = C.kps_un;
   p.uright = C.uright;
@@ -481,20 +506,32 @@ int orbpl_tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_d
   p.nm_stride = pstride;
   p.active = t->d_state;
   p.edges = t->d_edges;
-  launch_pose(t->consts, p, S, s);
-  HIP_CHECK(hipEventRecord(ev[8], s));
+  launch_pose(t->consts, p, S, ts);
+  HIP_CHECK(hipEventRecord(ev[9], ts));
   launch_finish(t->consts, t->d_state, C.n, K, C.kps_un, C.depth, C.match, C.outlier, C.has_mp,
-                C.mp_xyz, C.nobs, S, s);
-  HIP_CHECK(hipEventRecord(ev[9], s));
+                C.mp_xyz, C.nobs, S, ts);
+  HIP_CHECK(hipEventRecord(ev[10], ts));
+  HIP_CHECK(hipEventRecord(t->ev_free[li], ts));
+  t->free_pending[li] = true;
   HIP_CHECK(hipGetLastError());
   t->ring_pos++;
   t->ring_count = std::min(t->ring_count + 1, (int)orbpl_tracker::kRing);
-  t->cur ^= 1;
+  return ORBPL_OK;
+}
+
+int orbpl_tracker_set_pipelined(orbpl_tracker* t, int on) {
+  if (!t) return arg_fail("NULL tracker");
+  HIP_CHECK(hipSetDevice(t->device));
+  HIP_CHECK(hipStreamSynchronize(t->stream));
+  HIP_CHECK(hipStreamSynchronize(t->tstream));
+  t->pipelined = on ? 1 : 0;
   return ORBPL_OK;
 }
 
 int orbpl_tracker_synchronize(orbpl_tracker* t) {
   if (!t) return arg_fail("NULL tracker");
+  HIP_CHECK(hipSetDevice(t->device));
+  HIP_CHECK(hipStreamSynchronize(t->tstream));
   return orbx_synchronize(t->ex);
 }
 
@@ -503,11 +540,12 @@ int orbpl_tracker_get_state(orbpl_tracker* t, float* Tcw, int* nkps, int* nmatch
   if (!t) return arg_fail("NULL tracker");
   HIP_CHECK(hipSetDevice(t->device));
   HIP_CHECK(hipStreamSynchronize(t->stream));
+  HIP_CHECK(hipStreamSynchronize(t->tstream));
   std::vector<StreamState> st(t->S);
   HIP_CHECK(hipMemcpy(st.data(), t->d_state, sizeof(StreamState) * t->S, hipMemcpyDeviceToHost));
   std::vector<int> n(t->S);
-  // the frame just tracked is the "last" buffer after the step's swap
-  HIP_CHECK(hipMemcpy(n.data(), t->fb[t->cur ^ 1].n, 4 * t->S, hipMemcpyDeviceToHost));
+  // the frame just tracked
+  HIP_CHECK(hipMemcpy(n.data(), t->fb[(t->ring_pos + 2) % 3].n, 4 * t->S, hipMemcpyDeviceToHost));
   for (int s = 0; s < t->S; s++) {
     if (Tcw) memcpy(Tcw + 16 * s, st[s].Tlast, 64);
     if (nkps) nkps[s] = n[s];
@@ -522,11 +560,16 @@ int orbpl_tracker_timings(orbpl_tracker* t, int max_steps, float* ms, int* n_ste
   if (!t || !ms || !n_steps) return arg_fail("NULL argument");
   HIP_CHECK(hipSetDevice(t->device));
   HIP_CHECK(hipStreamSynchronize(t->stream));
+  HIP_CHECK(hipStreamSynchronize(t->tstream));
+  // stage intervals: 5 extraction stages, glue (extraction stream), then
+  // match (incl. prediction), pose, finish (tracking stream)
+  static const int kPair[9][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 6}, {7, 8}, {8, 9}, {9, 10}};
   const int n = std::min(max_steps, t->ring_count);
   for (int k = 0; k < n; k++) {
     const int step = t->ring_pos - n + k;
     hipEvent_t* ev = &t->ring[(size_t)(step % orbpl_tracker::kRing) * orbpl_tracker::kEv];
-    for (int i = 0; i < 9; i++) HIP_CHECK(hipEventElapsedTime(&ms[k * 9 + i], ev[i], ev[i + 1]));
+    for (int i = 0; i < 9; i++)
+      HIP_CHECK(hipEventElapsedTime(&ms[k * 9 + i], ev[kPair[i][0]], ev[kPair[i][1]]));
   }
   *n_steps = n;
   return ORBPL_OK;
@@ -557,7 +600,8 @@ int orbpl_tracker_get_frame(orbpl_tracker* t, int stream, orbpl_keypoint* kps_un
   if (!t || stream < 0 || stream >= t->S) return arg_fail("bad argument");
   HIP_CHECK(hipSetDevice(t->device));
   HIP_CHECK(hipStreamSynchronize(t->stream));
-  const FrameBufs& F = t->fb[t->cur ^ 1];
+  HIP_CHECK(hipStreamSynchronize(t->tstream));
+  const FrameBufs& F = t->fb[(t->ring_pos + 2) % 3];
   const size_t K = t->kp_cap, o = (size_t)stream * K;
   int cnt = 0;
   HIP_CHECK(hipMemcpy(&cnt, F.n + stream, 4, hipMemcpyDeviceToHost));

@@ -142,3 +142,34 @@ def test_tracker_matches_oracle_vo(orbpl, oracle):
             assert np.abs(st["Tcw"][s] - To).max() < POSE_TOL, (f, s)
     ms = tr.stage_ms()
     assert np.all(ms >= 0)
+
+
+def test_tracker_pipelined_matches_oracle_vo(orbpl, oracle):
+    """Two-stream pipelined tracker, steps issued back to back (no host sync
+    between steps): the final state equals the oracle VO after F frames."""
+    S, F = 3, 6
+    seqs = [sequence(F, 20 + s) for s in range(S)]
+    cfg = seqs[0][0]
+    vo = oracle.VO(oracle.params(), oracle.camera(cfg), S)
+    tr = orbpl.Tracker(orbpl.OrbParams(1000, 1.2, 8, 20, 7), orbpl.make_camera(cfg), S)
+    tr.set_pipelined(True)
+    T0 = np.stack([np.linalg.inv(sq[1][0]).astype(np.float32) for sq in seqs])
+    vo.reset(T0.reshape(S, 16))
+    tr.reset(T0.reshape(S, 16))
+    gray = orbpl.DeviceBuffer.from_array(
+        np.stack([np.stack([sq[2][f][0] for sq in seqs]) for f in range(F)]))
+    depth = orbpl.DeviceBuffer.from_array(
+        np.stack([np.stack([sq[2][f][1] for sq in seqs]) for f in range(F)]))
+    fb = S * 640 * 480
+    for f in range(F):
+        tr.step_device(gray.ptr + f * fb, depth.ptr + f * fb * 4)
+    tr.synchronize()
+    st = tr.state()
+    for s in range(S):
+        for f in range(F):
+            To, so = vo.step(s, seqs[s][2][f][0], seqs[s][2][f][1])
+        assert st["nkeypoints"][s] == so["nkeypoints"]
+        assert st["nmatches"][s] == so["nmatches"], s
+        assert st["ninliers"][s] == so["ninliers"], s
+        assert st["nmatches_map"][s] == so["nmatches_map"], s
+        assert np.abs(st["Tcw"][s] - To).max() < POSE_TOL, s
