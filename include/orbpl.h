@@ -34,6 +34,21 @@ typedef struct orbpl_keypoint {
   int32_t octave, class_id;
 } orbpl_keypoint;
 
+/* Mirror of cv::line_descriptor::KeyLine (opencv_contrib 3.4, 68 bytes),
+ * the element type of Frame::mvKeyLines (Frame.h, LineExtractor.h:27). */
+typedef struct orbpl_keyline {
+  float angle;
+  int32_t class_id;
+  int32_t octave;
+  float pt_x, pt_y;
+  float response;
+  float size;
+  float startPointX, startPointY, endPointX, endPointY;
+  float sPointInOctaveX, sPointInOctaveY, ePointInOctaveX, ePointInOctaveY;
+  float lineLength;
+  int32_t numOfPixels;
+} orbpl_keyline;
+
 /* ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST,
  * int minThFAST) — ORBextractor.h:52-53, values from the settings YAML
  * (Tracking.cc:113-125; Examples/RGB-D/TUM1.yaml: 1000, 1.2, 8, 20, 7). */

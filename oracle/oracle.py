@@ -265,3 +265,77 @@ class VO:
             lib().oracle_vo_destroy(self.h)
         except Exception:
             pass
+
+
+# ---------------------------------------------------------------------------
+# line features (lsd_oracle.cpp)
+# ---------------------------------------------------------------------------
+KEYLINE_DTYPE = np.dtype([("angle", "<f4"), ("class_id", "<i4"), ("octave", "<i4"),
+                          ("pt_x", "<f4"), ("pt_y", "<f4"), ("response", "<f4"), ("size", "<f4"),
+                          ("startPointX", "<f4"), ("startPointY", "<f4"), ("endPointX", "<f4"),
+                          ("endPointY", "<f4"), ("sPointInOctaveX", "<f4"),
+                          ("sPointInOctaveY", "<f4"), ("ePointInOctaveX", "<f4"),
+                          ("ePointInOctaveY", "<f4"), ("lineLength", "<f4"),
+                          ("numOfPixels", "<i4")])
+assert KEYLINE_DTYPE.itemsize == 68
+
+_setup_track_orb = _setup
+
+
+def _setup(L):  # noqa: F811
+    _setup_track_orb(L)
+    vp, i, f = C.c_void_p, C.c_int, C.c_float
+    L.oracle_lsd_detect.argtypes = [vp, i, i, vp, i, vp]
+    L.oracle_lsd_stages.argtypes = [vp, i, i, vp, vp, vp, vp, vp, vp]
+    L.oracle_line_extract.argtypes = [vp, i, i, vp, vp, vp, i, vp, vp]
+    L.oracle_lsdm.argtypes = [i, C.c_double, C.c_double]
+    L.oracle_lsdm.restype = C.c_double
+    L.oracle_line_iterator_count.argtypes = [i, i, f, f, f, f]
+
+
+def lsd_detect(img, cap=4096):
+    """Raw LSD segments (x1, y1, x2, y2) in detection order."""
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    out = np.zeros((cap, 4), np.float32)
+    n = C.c_int(0)
+    rc = lib().oracle_lsd_detect(_p(img), w, h, _p(out), cap, C.byref(n))
+    assert rc == 0, rc
+    return out[:n.value].copy()
+
+
+def lsd_stages(img):
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    sw, sh = int(round(w * 0.8)), int(round(h * 0.8))
+    scaled = np.zeros((sh, sw), np.uint8)
+    ang = np.zeros((sh, sw), np.float64)
+    order = np.zeros((sw - 1) * (sh - 1), np.uint32)
+    a, b, n = C.c_int(0), C.c_int(0), C.c_int(0)
+    lib().oracle_lsd_stages(_p(img), w, h, _p(scaled), _p(ang), _p(order), C.byref(a), C.byref(b),
+                            C.byref(n))
+    assert (a.value, b.value) == (sw, sh)
+    return scaled, ang, order[:n.value]
+
+
+def line_extract(img, cap=80):
+    """LineExtractor::ExtractLineSegment: keylines, 32-byte LBD rows, coefficients."""
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    kl = np.zeros(cap, KEYLINE_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    coef = np.zeros((cap, 3), np.float64)
+    n, nd = C.c_int(0), C.c_int(0)
+    rc = lib().oracle_line_extract(_p(img), w, h, _p(kl), _p(desc), _p(coef), cap, C.byref(n),
+                                   C.byref(nd))
+    assert rc == 0, rc
+    k = n.value
+    return kl[:k].copy(), desc[:k].copy(), coef[:k].copy(), nd.value
+
+
+def lsdm(fn, x, y=0.0):
+    return lib().oracle_lsdm(fn, float(x), float(y))
+
+
+def line_iterator_count(w, h, x1, y1, x2, y2):
+    return lib().oracle_line_iterator_count(w, h, x1, y1, x2, y2)

@@ -29,6 +29,14 @@ void oracle_vo_destroy(void* h);
 int oracle_vo_reset(void* h, const float* Tcw0);
 int oracle_vo_step(void* h, int stream, const uint8_t* gray, const float* depth, float* Tcw_out,
                    int* out5);
+/* line features (lsd_oracle.cpp) */
+int oracle_lsd_detect(const uint8_t* img, int W, int H, float* lines, int cap, int* n_out);
+int oracle_lsd_stages(const uint8_t* img, int W, int H, uint8_t* scaled, double* angles,
+                      uint32_t* order, int* sw, int* sh, int* n_order);
+int oracle_line_extract(const uint8_t* img, int W, int H, orbpl_keyline* kl_out, uint8_t* desc,
+                        double* coef, int cap, int* n_out, int* n_detected);
+double oracle_lsdm(int fn, double x, double y);
+int oracle_line_iterator_count(int W, int H, float x1, float y1, float x2, float y2);
 #ifdef __cplusplus
 }
 #endif
