@@ -279,6 +279,36 @@ int orbpl_tracker_get_frame(orbpl_tracker* tr, int stream, orbpl_keypoint* kps_u
  * ---------------------------------------------------------------------- */
 int orbpl_descriptor_distance(const uint8_t* a32, const uint8_t* b32);
 
+/* ------------------------------------------------------------------------
+ * Line features: LineExtractor::ExtractLineSegment (LineExtractor.cpp:12-74)
+ *   LSDDetector::detect(img, keylines, 1, 1)   -> lsdx_detect*
+ * One lsdx_ctx per (device, image geometry, max batch); asynchronous on its
+ * own HIP stream.
+ * ---------------------------------------------------------------------- */
+typedef struct lsdx_ctx lsdx_ctx;
+
+int lsdx_create(int width, int height, int max_batch, int device, lsdx_ctx** out);
+int lsdx_destroy(lsdx_ctx* ctx);
+/* LineSegmentDetector::detect (LSD_REFINE_ADV, scale 0.8) on one host image:
+ * segments (x1, y1, x2, y2) in detection order. ORBPL_ERR_CAPACITY if more
+ * than cap segments (n_out holds the count). */
+int lsdx_detect(lsdx_ctx* ctx, const uint8_t* img, int width, int height, int stride,
+                float* lines, int cap, int* n_out);
+/* The same for `batch` device-resident frames (frame f at d_imgs + f*frame_pitch). */
+int lsdx_detect_batch_device(lsdx_ctx* ctx, const uint8_t* d_imgs, int batch, int stride,
+                             int64_t frame_pitch);
+int lsdx_synchronize(lsdx_ctx* ctx);
+int lsdx_get_lines(lsdx_ctx* ctx, int frame, float* lines, int cap, int* n_out);
+/* Intermediate stages of the last run (parity tests): 0.8-scaled 8-bit image
+ * (sw*sh), fastAtan2 degrees per pixel (-1 = NOTDEF), pseudo-ordered pixels
+ * (x | y << 16, (sw-1)*(sh-1) entries). Any pointer may be NULL. */
+int lsdx_get_stages(lsdx_ctx* ctx, int frame, uint8_t* scaled, float* deg, uint32_t* order,
+                    int* sw, int* sh, int* n_order);
+/* Test hook: the device replica of std::sort(records, key greater) on keys
+ * in [0, 1023]; perm receives the record indices in sorted order. */
+int orbpl_test_introsort(const int32_t* keys, int n, int32_t* perm);
+
+
 #ifdef __cplusplus
 }
 #endif

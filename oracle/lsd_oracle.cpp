@@ -29,8 +29,8 @@
 //       csrc/lsd_math.h (<= 1 ulp from glibc; identical on host and device).
 //   P11 pow(x, integer) = binary exponentiation; sinh = odd Taylor series.
 //   P12 atan2f (KeyLine::angle) = (float)atan2((double)y, (double)x) (P10).
-//   P13 rect_nfa walks the rectangle with double-valued edge steps (OpenCV
-//       3.4 after its rect_nfa fix).
+//   P13 rect_nfa walks the rectangle with double-valued edge steps and the
+//       tail corner's y (OpenCV 3.4 after its rect_nfa fix).
 // std::sort calls are the reference's own (libstdc++ introsort), so ties
 // follow libstdc++'s order exactly as in the reference build.
 // ============================================================================
@@ -517,8 +517,10 @@ struct LSD {
         else if (tailp->x > ordered_x[i].x) tailp = &ordered_x[i];
       }
     tailp->taken = true;
-    // pinned P13: double-valued steps and the tail's y (OpenCV 3.4 after the
-    // rect_nfa fix; the pre-fix integer-division walk misses oblique lines)
+    // pinned P13: double-valued steps and the tail corner's y (OpenCV 3.4
+    // after its rect_nfa fix). The pre-fix text divides integer corner
+    // coordinates and uses the tail's x for its y; that walk loses most
+    // oblique segments (a 30-degree square keeps 1 of 4 sides), see DESIGN.md.
     const double flstep =
         (min_y->y != leftmost->y) ? (min_y->x - leftmost->x) / double(min_y->y - leftmost->y) : 0;
     const double slstep =
@@ -1020,4 +1022,17 @@ int oracle_line_iterator_count(int W, int H, float x1, float y1, float x2, float
   return line_iterator_count(W, H, x1, y1, x2, y2);
 }
 
+}  // extern "C"
+
+extern "C" {
+// std::sort (libstdc++ introsort) of (key, index) records by key descending,
+// the comparator of LSD's ordered_points; returns the index permutation.
+int oracle_introsort_perm(const int* keys, int n, int* perm) {
+  std::vector<lsdo::NormPoint> v(n);
+  for (int i = 0; i < n; i++) v[i] = {i, 0, keys[i]};
+  std::sort(v.begin(), v.end(),
+            [](const lsdo::NormPoint& a, const lsdo::NormPoint& b) { return a.norm > b.norm; });
+  for (int i = 0; i < n; i++) perm[i] = v[i].x;
+  return 0;
+}
 }  // extern "C"

@@ -291,6 +291,7 @@ def _setup(L):  # noqa: F811
     L.oracle_lsdm.argtypes = [i, C.c_double, C.c_double]
     L.oracle_lsdm.restype = C.c_double
     L.oracle_line_iterator_count.argtypes = [i, i, f, f, f, f]
+    L.oracle_introsort_perm.argtypes = [vp, i, vp]
 
 
 def lsd_detect(img, cap=4096):
@@ -339,3 +340,11 @@ def lsdm(fn, x, y=0.0):
 
 def line_iterator_count(w, h, x1, y1, x2, y2):
     return lib().oracle_line_iterator_count(w, h, x1, y1, x2, y2)
+
+
+def introsort_perm(keys):
+    """libstdc++ std::sort permutation of records ordered by key descending."""
+    k = np.ascontiguousarray(keys, np.int32)
+    perm = np.zeros(len(k), np.int32)
+    lib().oracle_introsort_perm(_p(k), len(k), _p(perm))
+    return perm

@@ -37,6 +37,7 @@ int oracle_line_extract(const uint8_t* img, int W, int H, orbpl_keyline* kl_out,
                         double* coef, int cap, int* n_out, int* n_detected);
 double oracle_lsdm(int fn, double x, double y);
 int oracle_line_iterator_count(int W, int H, float x1, float y1, float x2, float y2);
+int oracle_introsort_perm(const int* keys, int n, int* perm);
 #ifdef __cplusplus
 }
 #endif

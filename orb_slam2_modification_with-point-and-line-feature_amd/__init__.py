@@ -507,3 +507,93 @@ class Tracker:
                                             C.byref(n)), "orbpl_tracker_get_frame")
         k = n.value
         return ku[:k], d[:k], m[:k], o[:k]
+
+
+# ---------------------------------------------------------------------------
+# Line features: LineExtractor::ExtractLineSegment (LineExtractor.cpp:12-74)
+# ---------------------------------------------------------------------------
+KEYLINE_DTYPE = np.dtype([("angle", "<f4"), ("class_id", "<i4"), ("octave", "<i4"),
+                          ("pt_x", "<f4"), ("pt_y", "<f4"), ("response", "<f4"), ("size", "<f4"),
+                          ("startPointX", "<f4"), ("startPointY", "<f4"), ("endPointX", "<f4"),
+                          ("endPointY", "<f4"), ("sPointInOctaveX", "<f4"),
+                          ("sPointInOctaveY", "<f4"), ("ePointInOctaveX", "<f4"),
+                          ("ePointInOctaveY", "<f4"), ("lineLength", "<f4"),
+                          ("numOfPixels", "<i4")])
+
+_declare_points = _declare
+
+
+def _declare(L):  # noqa: F811
+    _declare_points(L)
+    vp, i, ip = C.c_void_p, C.c_int, C.POINTER(C.c_int)
+    L.lsdx_create.argtypes = [i, i, i, i, C.POINTER(vp)]
+    L.lsdx_destroy.argtypes = [vp]
+    L.lsdx_detect.argtypes = [vp, vp, i, i, i, vp, i, ip]
+    L.lsdx_detect_batch_device.argtypes = [vp, vp, i, i, C.c_int64]
+    L.lsdx_synchronize.argtypes = [vp]
+    L.lsdx_get_lines.argtypes = [vp, i, vp, i, ip]
+    L.lsdx_get_stages.argtypes = [vp, i, vp, vp, vp, ip, ip, ip]
+    L.orbpl_test_introsort.argtypes = [vp, i, vp]
+
+
+class LineSegmentDetector:
+    """cv::LineSegmentDetector(LSD_REFINE_ADV) as LSDDetector::detect(img, kl, 1, 1)
+    runs it (LineExtractor.cpp:20-21): 0.8 Gaussian sub-sampling, region
+    growing, rectangle refinement, NFA validation. detect() returns the
+    segments (x1, y1, x2, y2) in detection order."""
+
+    def __init__(self, width, height, max_batch=1, device=0):
+        self.W, self.H, self.max_batch, self.device = width, height, max_batch, device
+        h = C.c_void_p()
+        check(lib().lsdx_create(width, height, max_batch, device, C.byref(h)), "lsdx_create")
+        self._h = h
+
+    def __del__(self):
+        try:
+            if getattr(self, "_h", None):
+                lib().lsdx_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+    def detect(self, img, cap=4096):
+        img = np.ascontiguousarray(img, np.uint8)
+        h, w = img.shape
+        out = np.zeros((cap, 4), np.float32)
+        n = C.c_int(0)
+        check(lib().lsdx_detect(self._h, _ptr(img), w, h, w, _ptr(out), cap, C.byref(n)),
+              "lsdx_detect")
+        return out[:n.value].copy()
+
+    def detect_batch_device(self, d_imgs, batch, stride=None, frame_pitch=None):
+        stride = self.W if stride is None else stride
+        frame_pitch = self.W * self.H if frame_pitch is None else frame_pitch
+        check(lib().lsdx_detect_batch_device(self._h, C.c_void_p(d_imgs), batch, stride,
+                                             frame_pitch), "lsdx_detect_batch_device")
+
+    def synchronize(self):
+        check(lib().lsdx_synchronize(self._h), "lsdx_synchronize")
+
+    def lines(self, frame, cap=4096):
+        out = np.zeros((cap, 4), np.float32)
+        n = C.c_int(0)
+        check(lib().lsdx_get_lines(self._h, frame, _ptr(out), cap, C.byref(n)), "lsdx_get_lines")
+        return out[:n.value].copy()
+
+    def stages(self, frame=0):
+        sw, sh = int(round(self.W * 0.8)), int(round(self.H * 0.8))
+        scaled = np.zeros((sh, sw), np.uint8)
+        deg = np.zeros((sh, sw), np.float32)
+        order = np.zeros((sw - 1) * (sh - 1), np.uint32)
+        a, b, n = C.c_int(0), C.c_int(0), C.c_int(0)
+        check(lib().lsdx_get_stages(self._h, frame, _ptr(scaled), _ptr(deg), _ptr(order),
+                                    C.byref(a), C.byref(b), C.byref(n)), "lsdx_get_stages")
+        return scaled, deg, order[:n.value]
+
+
+def test_introsort(keys):
+    """Device replica of std::sort(records, key greater): record order."""
+    k = np.ascontiguousarray(keys, np.int32)
+    perm = np.zeros(len(k), np.int32)
+    check(lib().orbpl_test_introsort(_ptr(k), len(k), _ptr(perm)), "orbpl_test_introsort")
+    return perm

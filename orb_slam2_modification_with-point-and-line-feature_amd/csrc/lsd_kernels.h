@@ -1,0 +1,67 @@
+// Line-feature kernels (LSD + LBD), shared between lsd_kernels.hip and the
+// C-ABI runtime (lsd_runtime.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/orbpl.h"
+
+namespace orbpl {
+
+constexpr int kLsdMaxLines = 4096;    // raw LSD segments kept per frame
+constexpr int kLineKeep = 80;         // LineExtractor.cpp:24
+constexpr int kLsdSortChunk = 256;    // elements per partition chunk
+constexpr float kLsdNotdef = -1.0f;   // NOTDEF marker in the degree map
+
+// Per-frame geometry of the LSD path (host-computed, passed by value).
+struct LsdGeom {
+  int W, H;          // input image
+  int sw, sh;        // 0.8-scaled image
+  int n;             // (sw-1)*(sh-1) pseudo-ordered pixels
+  int gk[7];         // GaussianBlur 8.8 fixed-point kernel (sigma 0.75, 7 taps)
+  int ksize;
+  double rho;        // gradient threshold quant / sin(prec)
+  double prec, p;    // angle tolerance (rad) and its probability
+  double log_nt;     // LOG_NT
+  int min_reg_size;
+  // INTER_LINEAR_EXACT ranges: dx in [rx0, rx1) and dy in [ry0, ry1) interpolate
+  int rx0, rx1, ry0, ry1;
+  // sort scratch capacities
+  int seg_cap, chunk_cap, leaf_cap;
+};
+
+// Device scratch of one frame slot (all pointers are per-batch bases; the
+// kernels index them with the frame number).
+struct LsdScratch {
+  uint8_t* blur;       // W*H
+  uint8_t* scaled;     // sw*sh
+  float* deg;          // sw*sh, fastAtan2 degrees or kLsdNotdef
+  int* q;              // sw*sh, gx^2 + gy^2
+  unsigned* maxq;      // 1 per frame
+  uint32_t* A;         // n: key << 22 | raster index, sorted in place
+  int* Lpos;           // n
+  int* Rpos;           // n
+  int4* seg0;          // seg_cap (first, last, depth, -)
+  int4* seg1;          // seg_cap
+  int4* heap;          // seg_cap
+  int* seg_i;          // 8 * seg_cap: pivot, choff, nL, nR, K, cut, nch, -
+  int* chunk_i;        // 4 * chunk_cap: Lc, Rc, Lpre, Rsuf
+  int2* leaves;        // leaf_cap
+  uint32_t* reg;       // sw*sh region point list (x | y << 16)
+  float* lines;        // kLsdMaxLines * 4
+  int* nlines;         // 1 per frame
+  int* err;            // 1 per frame: capacity overflow flags
+};
+
+void launch_lsd_blur(const LsdGeom& g, const uint8_t* img, int stride, long long frame_pitch,
+                     uint8_t* out, int batch, hipStream_t s);
+void launch_lsd_resize(const LsdGeom& g, const int* tabs, const uint8_t* blur, uint8_t* scaled,
+                       int batch, hipStream_t s);
+void launch_lsd_grad(const LsdGeom& g, const uint8_t* scaled, float* deg, int* q, unsigned* maxq,
+                     int batch, hipStream_t s);
+void launch_lsd_sort(const LsdGeom& g, const LsdScratch& sc, int batch, hipStream_t s);
+void launch_lsd_sort_keys(int n, const int* keys, const LsdScratch& sc, hipStream_t s);
+void launch_lsd_grow(const LsdGeom& g, const LsdScratch& sc, int batch, hipStream_t s);
+size_t lsd_grow_smem(const LsdGeom& g);
+
+}  // namespace orbpl

@@ -1,0 +1,568 @@
+// LSD line segment detection on gfx950 — LineExtractor::ExtractLineSegment's
+// LSDDetector::detect (/root/reference/src/LineExtractor.cpp:20-21; the
+// algorithm is OpenCV 3.4's LineSegmentDetectorImpl, restated in
+// oracle/lsd_oracle.cpp). One launch per stage covers the whole batch:
+//
+//   k_lsd_blur    GaussianBlur 7x7 sigma 0.75, 8U fixed point, REFLECT_101
+//   k_lsd_resize  resize x0.8, INTER_LINEAR_EXACT (8.8 fixed point)
+//   k_lsd_grad    ll_angle: 2x2 gradient, norm, fastAtan2 degrees, max norm
+//   k_lsd_sort    the reference's std::sort of pixels by gradient bin,
+//                 replayed exactly: libstdc++ introsort with every partition
+//                 level executed in parallel (one 1024-thread block / frame)
+//   k_lsd_grow    the greedy seed loop (region growing, rectangle fit,
+//                 refinement, NFA): one wave per frame, wave-uniform serial
+//                 control flow, parallel seed screening and NFA pixel counts
+#include <hip/hip_runtime.h>
+
+#include "lsd_kernels.h"
+#include "lsd_math.h"
+#include "orbpl_math.h"
+
+namespace orbpl {
+
+__device__ __forceinline__ int refl101(int i, int n) {
+  if (n == 1) return 0;
+  while (i < 0 || i >= n) i = i < 0 ? -i : 2 * n - 2 - i;
+  return i;
+}
+
+// ---------------------------------------------------------------------------
+// GaussianBlur (fixed point): 64x32 output tile per 256-thread block; input
+// (64+6)x(32+6) staged in LDS, horizontal pass into LDS, vertical to HBM.
+// ---------------------------------------------------------------------------
+constexpr int kBlTW = 64, kBlTH = 32, kBlR = 3;
+
+__global__ void __launch_bounds__(256) k_lsd_blur(LsdGeom g, const uint8_t* __restrict__ img,
+                                                  int stride, long long frame_pitch,
+                                                  uint8_t* __restrict__ out) {
+  __shared__ uint8_t s_in[kBlTH + 2 * kBlR][kBlTW + 2 * kBlR];
+  __shared__ int s_h[kBlTH + 2 * kBlR][kBlTW];
+  const int f = blockIdx.z, t = threadIdx.x;
+  const int x0 = blockIdx.x * kBlTW, y0 = blockIdx.y * kBlTH;
+  const int W = g.W, H = g.H;
+  const uint8_t* src = img + (long long)f * frame_pitch;
+  for (int i = t; i < (kBlTH + 2 * kBlR) * (kBlTW + 2 * kBlR); i += 256) {
+    const int r = i / (kBlTW + 2 * kBlR), c = i - r * (kBlTW + 2 * kBlR);
+    const int sy = refl101(y0 + r - kBlR, H), sx = refl101(x0 + c - kBlR, W);
+    s_in[r][c] = src[(long long)sy * stride + sx];
+  }
+  __syncthreads();
+  const int n = g.ksize, rr = n / 2;
+  for (int i = t; i < (kBlTH + 2 * kBlR) * kBlTW; i += 256) {
+    const int r = i / kBlTW, c = i - r * kBlTW;
+    int acc = 0;
+    for (int j = 0; j < n; j++) acc += g.gk[j] * s_in[r][c + kBlR + j - rr];
+    s_h[r][c] = acc;
+  }
+  __syncthreads();
+  uint8_t* dst = out + (long long)f * W * H;
+  for (int i = t; i < kBlTH * kBlTW; i += 256) {
+    const int r = i / kBlTW, c = i - r * kBlTW;
+    const int x = x0 + c, y = y0 + r;
+    if (x >= W || y >= H) continue;
+    int acc = 0;
+    // tile row r holds source row refl101(y0 + r - kBlR)
+    for (int j = 0; j < n; j++) acc += g.gk[j] * s_h[r + kBlR + j - rr][c];
+    dst[(long long)y * W + x] = (uint8_t)min(255, (acc + (1 << 15)) >> 16);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// resize x0.8 INTER_LINEAR_EXACT. tabs = xofs[sw], xc1[sw], yofs[sh], yc1[sh].
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_lsd_resize(LsdGeom g, const int* __restrict__ tabs,
+                                                    const uint8_t* __restrict__ blur,
+                                                    uint8_t* __restrict__ scaled) {
+  const int f = blockIdx.y;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int sw = g.sw, sh = g.sh;
+  if (i >= sw * sh) return;
+  const int dy = i / sw, dx = i - dy * sw;
+  const int* xofs = tabs;
+  const int* xc1 = tabs + sw;
+  const int* yofs = tabs + 2 * sw;
+  const int* yc1 = tabs + 2 * sw + sh;
+  const uint8_t* S = blur + (long long)f * g.W * g.H;
+  auto hval = [&](int sy) -> int {
+    const uint8_t* row = S + (long long)sy * g.W;
+    if (dx < g.rx0) return row[0] << 8;
+    if (dx >= g.rx1) return row[xofs[sw - 1]] << 8;
+    const int c1 = xc1[dx], o = xofs[dx];
+    return (256 - c1) * row[o] + c1 * row[o + 1];
+  };
+  int v;
+  if (dy < g.ry0 || dy >= g.ry1) {
+    v = (hval(dy < g.ry0 ? 0 : g.H - 1) + 0x80) >> 8;
+  } else {
+    const int b1 = yc1[dy], b0 = 256 - b1, oy = yofs[dy];
+    v = (hval(oy) * b0 + hval(oy + 1) * b1 + 0x8000) >> 16;
+  }
+  scaled[(long long)f * sw * sh + i] = (uint8_t)min(255, v);
+}
+
+// ---------------------------------------------------------------------------
+// ll_angle: per pixel gx, gy, q = gx^2 + gy^2, degrees (or NOTDEF), max q.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_lsd_grad(LsdGeom g, const uint8_t* __restrict__ scaled,
+                                                  float* __restrict__ deg, int* __restrict__ q,
+                                                  unsigned* __restrict__ maxq) {
+  const int f = blockIdx.y;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int sw = g.sw, sh = g.sh;
+  unsigned mq = 0;
+  if (i < sw * sh) {
+    const int y = i / sw, x = i - y * sw;
+    const long long o = (long long)f * sw * sh + i;
+    float d = kLsdNotdef;
+    int qq = 0;
+    if (x < sw - 1 && y < sh - 1) {
+      const uint8_t* r0 = scaled + (long long)f * sw * sh + (long long)y * sw;
+      const uint8_t* r1 = r0 + sw;
+      const int DA = r1[x + 1] - r0[x];
+      const int BC = r0[x + 1] - r1[x];
+      const int gx = DA + BC, gy = DA - BC;
+      qq = gx * gx + gy * gy;
+      const double norm = sqrt(qq / 4.0);
+      if (norm > g.rho) {
+        d = fast_atan2_deg((float)gx, (float)-gy);
+        mq = (unsigned)qq;
+      }
+    }
+    deg[o] = d;
+    q[o] = qq;
+  }
+  // block max, one atomic per block
+  __shared__ unsigned s_m[4];
+  unsigned m = mq;
+  for (int o = 32; o >= 1; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o, 64));
+  if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned bm = max(max(s_m[0], s_m[1]), max(s_m[2], s_m[3]));
+    if (bm) atomicMax(maxq + f, bm);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// libstdc++ std::sort replay (introsort, comparator key(a) > key(b)).
+//
+// Elements are key << 22 | raster index. The recursion of __introsort_loop
+// is executed level by level: every active segment (> 16 elements, depth
+// left) is partitioned in the same pass. __unguarded_partition on the
+// original array is reproduced in closed form: with L_k the k-th position
+// (from first+1 upwards) whose key <= pivot and R_k the k-th position (from
+// last-1 downwards) whose key >= pivot, the sequential loop swaps pairs
+// (L_k, R_k) while L_k < R_k and returns cut = min(L_K, R_{K-1}) for the
+// first failing K. Segments whose depth budget is exhausted are heap-sorted
+// (std::__partial_sort); the final insertion sort never moves an element
+// across a leaf segment, so it is a stable sort of each leaf.
+// ---------------------------------------------------------------------------
+struct SortPtrs {
+  uint32_t* A;
+  int *Lpos, *Rpos;
+  int4 *seg0, *seg1, *heap;
+  int* si;   // 8 arrays of seg_cap
+  int* ci;   // 4 arrays of chunk_cap
+  int2* leaves;
+  int seg_cap, chunk_cap, leaf_cap;
+  int* err;
+};
+
+__device__ __forceinline__ int skey(uint32_t e) { return (int)(e >> 22); }
+
+constexpr int kSortThreads = 1024, kSortWaves = kSortThreads / 64;
+
+// Exclusive scan of a[0..len) (global) in place by the whole block; returns
+// the total in every thread.
+__device__ int block_scan_global(int* a, int len, int* s_w) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int per = (len + kSortThreads - 1) / kSortThreads;
+  const int b = min(len, t * per), e = min(len, b + per);
+  int sum = 0;
+  for (int i = b; i < e; i++) sum += a[i];
+  int incl = sum;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += u;
+  }
+  if (lane == 63) s_w[wave] = incl;
+  __syncthreads();
+  int off = 0, tot = 0;
+  for (int w = 0; w < kSortWaves; w++) {
+    const int v = s_w[w];
+    if (w < wave) off += v;
+    tot += v;
+  }
+  int run = off + incl - sum;
+  for (int i = b; i < e; i++) {
+    const int v = a[i];
+    a[i] = run;
+    run += v;
+  }
+  __syncthreads();
+  return tot;
+}
+
+__device__ void move_median_to_first(uint32_t* A, int result, int a, int b, int c) {
+  const int ka = skey(A[a]), kb = skey(A[b]), kc = skey(A[c]);
+  int m;
+  if (ka > kb) {
+    if (kb > kc) m = b;
+    else if (ka > kc) m = c;
+    else m = a;
+  } else if (ka > kc) {
+    m = a;
+  } else if (kb > kc) {
+    m = c;
+  } else {
+    m = b;
+  }
+  const uint32_t tmp = A[result];
+  A[result] = A[m];
+  A[m] = tmp;
+}
+
+// libstdc++ __adjust_heap / __push_heap with comp = key greater.
+__device__ void adjust_heap(uint32_t* A, int hole, int len, uint32_t value) {
+  const int top = hole;
+  int second = hole;
+  while (second < (len - 1) / 2) {
+    second = 2 * (second + 1);
+    if (skey(A[second]) > skey(A[second - 1])) second--;
+    A[hole] = A[second];
+    hole = second;
+  }
+  if ((len & 1) == 0 && second == (len - 2) / 2) {
+    second = 2 * (second + 1);
+    A[hole] = A[second - 1];
+    hole = second - 1;
+  }
+  int parent = (hole - 1) / 2;
+  while (hole > top && skey(A[parent]) > skey(value)) {
+    A[hole] = A[parent];
+    hole = parent;
+    parent = (hole - 1) / 2;
+  }
+  A[hole] = value;
+}
+
+// std::__partial_sort(first, last, last): make_heap + sort_heap.
+__device__ void heap_sort_seg(uint32_t* A, int len) {
+  if (len < 2) return;
+  for (int parent = (len - 2) / 2;; parent--) {
+    adjust_heap(A, parent, len, A[parent]);
+    if (parent == 0) break;
+  }
+  for (int last = len; last > 1;) {
+    --last;
+    const uint32_t v = A[last];
+    A[last] = A[0];
+    adjust_heap(A, 0, last, v);
+  }
+}
+
+__device__ void sort_core(const SortPtrs& P, int n) {
+  __shared__ int s_w[kSortWaves];
+  __shared__ int s_nseg, s_next, s_nheap, s_nleaf;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  uint32_t* A = P.A;
+  int* piv = P.si;
+  int* choff = P.si + P.seg_cap;
+  int* nch = P.si + 2 * P.seg_cap;
+  int* sK = P.si + 3 * P.seg_cap;
+  int* scut = P.si + 4 * P.seg_cap;
+  int* Lc = P.ci;
+  int* Rc = P.ci + P.chunk_cap;
+  int* Lpre = P.ci + 2 * P.chunk_cap;
+  int* Rsuf = P.ci + 3 * P.chunk_cap;
+  if (t == 0) {
+    s_nheap = 0;
+    s_nleaf = 0;
+    s_nseg = 0;
+    if (n > 16) {
+      const int lg = 31 - __clz(n);
+      P.seg0[0] = make_int4(0, n, 2 * lg, 0);
+      s_nseg = 1;
+    } else if (n > 1) {
+      P.leaves[0] = make_int2(0, n);
+      s_nleaf = 1;
+    }
+  }
+  __syncthreads();
+  int4* cur = P.seg0;
+  int4* nxt = P.seg1;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  while (true) {
+    const int nseg = s_nseg;
+    if (nseg == 0) break;
+    if (t == 0) s_next = 0;
+    // R1: median of three into first, pivot key, chunk counts
+    for (int s = t; s < nseg; s += kSortThreads) {
+      const int4 sg = cur[s];
+      const int first = sg.x, last = sg.y;
+      const int mid = first + (last - first) / 2;
+      move_median_to_first(A, first, first + 1, mid, last - 1);
+      piv[s] = skey(A[first]);
+      nch[s] = (last - first + kLsdSortChunk - 1) / kLsdSortChunk;
+      choff[s] = nch[s];
+    }
+    __syncthreads();
+    const int nchunks = block_scan_global(choff, nseg, s_w);
+    if (nchunks > P.chunk_cap) {
+      if (t == 0) *P.err |= 1;
+      return;
+    }
+    // R3: per chunk L / R stopper counts
+    for (int ch = wave; ch < nchunks; ch += kSortWaves) {
+      int lo = 0, hi = nseg;  // last segment with choff <= ch
+      while (hi - lo > 1) {
+        const int m = (lo + hi) >> 1;
+        if (choff[m] <= ch) lo = m;
+        else hi = m;
+      }
+      const int s = lo;
+      const int4 sg = cur[s];
+      const int first = sg.x, last = sg.y, p = piv[s];
+      const int b = first + (ch - choff[s]) * kLsdSortChunk;
+      const int e = min(b + kLsdSortChunk, last);
+      int cl = 0, cr = 0;
+      for (int j = 0; j < kLsdSortChunk / 64; j++) {
+        const int i = b + j * 64 + lane;
+        bool fl = false, fr = false;
+        if (i < e) {
+          const int k = skey(A[i]);
+          fl = i > first && k <= p;
+          fr = k >= p;
+        }
+        cl += __popcll(__ballot(fl));
+        cr += __popcll(__ballot(fr));
+      }
+      if (lane == 0) {
+        Lc[ch] = cl;
+        Rc[ch] = cr;
+        Lpre[ch] = cl;
+        Rsuf[ch] = cr;
+      }
+    }
+    __syncthreads();
+    block_scan_global(Lpre, nchunks, s_w);
+    const int totR = block_scan_global(Rsuf, nchunks, s_w);
+    for (int c = t; c < nchunks; c += kSortThreads) Rsuf[c] = totR - Rsuf[c] - Rc[c];
+    __syncthreads();
+    // R5: scatter stopper positions by rank
+    for (int ch = wave; ch < nchunks; ch += kSortWaves) {
+      int lo = 0, hi = nseg;
+      while (hi - lo > 1) {
+        const int m = (lo + hi) >> 1;
+        if (choff[m] <= ch) lo = m;
+        else hi = m;
+      }
+      const int s = lo;
+      const int4 sg = cur[s];
+      const int first = sg.x, last = sg.y, p = piv[s];
+      const int c0 = choff[s], c1 = c0 + nch[s] - 1;
+      const int b = first + (ch - c0) * kLsdSortChunk;
+      const int e = min(b + kLsdSortChunk, last);
+      unsigned long long mL[kLsdSortChunk / 64], mR[kLsdSortChunk / 64];
+#pragma unroll
+      for (int j = 0; j < kLsdSortChunk / 64; j++) {
+        const int i = b + j * 64 + lane;
+        bool fl = false, fr = false;
+        if (i < e) {
+          const int k = skey(A[i]);
+          fl = i > first && k <= p;
+          fr = k >= p;
+        }
+        mL[j] = __ballot(fl);
+        mR[j] = __ballot(fr);
+      }
+      int runL = Lpre[ch] - Lpre[c0];
+      int sufR = Rsuf[ch] - Rsuf[c1];
+#pragma unroll
+      for (int j = kLsdSortChunk / 64 - 1; j >= 0; j--) {
+        const int i = b + j * 64 + lane;
+        if ((mR[j] >> lane) & 1ull) {
+          const int k = sufR + __popcll(mR[j] & ~(below | (1ull << lane)));
+          P.Rpos[first + k] = i;
+        }
+        sufR += __popcll(mR[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < kLsdSortChunk / 64; j++) {
+        const int i = b + j * 64 + lane;
+        if ((mL[j] >> lane) & 1ull) P.Lpos[first + runL + __popcll(mL[j] & below)] = i;
+        runL += __popcll(mL[j]);
+      }
+    }
+    __syncthreads();
+    // R6: swap count K and cut per segment
+    for (int s = t; s < nseg; s += kSortThreads) {
+      const int4 sg = cur[s];
+      const int first = sg.x, last = sg.y;
+      const int c0 = choff[s], c1 = c0 + nch[s] - 1;
+      const int nL = Lpre[c1] + Lc[c1] - Lpre[c0];
+      const int nR = Rsuf[c0] + Rc[c0] - Rsuf[c1];
+      int lo = 0, hi = min(nL, nR);
+      while (lo < hi) {
+        const int m = (lo + hi) >> 1;
+        if (P.Lpos[first + m] < P.Rpos[first + m]) lo = m + 1;
+        else hi = m;
+      }
+      const int K = lo;
+      int cut = last;
+      if (K < nL) cut = min(cut, P.Lpos[first + K]);
+      if (K > 0) cut = min(cut, P.Rpos[first + K - 1]);
+      sK[s] = K;
+      scut[s] = cut;
+    }
+    __syncthreads();
+    // R7: swaps (disjoint pairs)
+    for (int ch = wave; ch < nchunks; ch += kSortWaves) {
+      int lo = 0, hi = nseg;
+      while (hi - lo > 1) {
+        const int m = (lo + hi) >> 1;
+        if (choff[m] <= ch) lo = m;
+        else hi = m;
+      }
+      const int s = lo;
+      const int first = cur[s].x;
+      const int kb = Lpre[ch] - Lpre[choff[s]];
+      const int ke = min(kb + Lc[ch], sK[s]);
+      for (int k = kb + lane; k < ke; k += 64) {
+        const int i = P.Lpos[first + k], j = P.Rpos[first + k];
+        const uint32_t a = A[i], bb = A[j];
+        A[i] = bb;
+        A[j] = a;
+      }
+    }
+    __syncthreads();
+    // R8: children
+    for (int s = t; s < nseg; s += kSortThreads) {
+      const int4 sg = cur[s];
+      const int cut = scut[s], d = sg.z - 1;
+      const int bs[2] = {cut, sg.x}, es[2] = {sg.y, cut};
+      for (int c = 0; c < 2; c++) {
+        const int b = bs[c], e = es[c], size = e - b;
+        if (size > 16) {
+          if (d > 0) {
+            const int idx = atomicAdd(&s_next, 1);
+            if (idx < P.seg_cap) nxt[idx] = make_int4(b, e, d, 0);
+            else atomicOr(P.err, 2);
+          } else {
+            const int idx = atomicAdd(&s_nheap, 1);
+            if (idx < P.seg_cap) P.heap[idx] = make_int4(b, e, 0, 0);
+            else atomicOr(P.err, 2);
+          }
+        } else if (size > 1) {
+          const int idx = atomicAdd(&s_nleaf, 1);
+          if (idx < P.leaf_cap) P.leaves[idx] = make_int2(b, e);
+          else atomicOr(P.err, 4);
+        }
+      }
+    }
+    __syncthreads();
+    if (t == 0) s_nseg = min(s_next, P.seg_cap);
+    int4* tmp = cur;
+    cur = nxt;
+    nxt = tmp;
+    __syncthreads();
+  }
+  const int nheap = min(s_nheap, P.seg_cap), nleaf = min(s_nleaf, P.leaf_cap);
+  for (int h = t; h < nheap; h += kSortThreads) {
+    const int4 sg = P.heap[h];
+    heap_sort_seg(A + sg.x, sg.y - sg.x);
+  }
+  for (int l = t; l < nleaf; l += kSortThreads) {
+    const int2 lf = P.leaves[l];
+    for (int i = lf.x + 1; i < lf.y; i++) {
+      const uint32_t v = A[i];
+      int j = i;
+      while (j > lf.x && skey(v) > skey(A[j - 1])) {
+        A[j] = A[j - 1];
+        j--;
+      }
+      A[j] = v;
+    }
+  }
+  __syncthreads();
+}
+
+__device__ SortPtrs sort_ptrs(const LsdGeom& g, const LsdScratch& sc, int f) {
+  SortPtrs P;
+  const long long n = g.n;
+  P.A = sc.A + f * n;
+  P.Lpos = sc.Lpos + f * n;
+  P.Rpos = sc.Rpos + f * n;
+  P.seg0 = sc.seg0 + (long long)f * g.seg_cap;
+  P.seg1 = sc.seg1 + (long long)f * g.seg_cap;
+  P.heap = sc.heap + (long long)f * g.seg_cap;
+  P.si = sc.seg_i + (long long)f * 8 * g.seg_cap;
+  P.ci = sc.chunk_i + (long long)f * 4 * g.chunk_cap;
+  P.leaves = sc.leaves + (long long)f * g.leaf_cap;
+  P.seg_cap = g.seg_cap;
+  P.chunk_cap = g.chunk_cap;
+  P.leaf_cap = g.leaf_cap;
+  P.err = sc.err + f;
+  return P;
+}
+
+__global__ void __launch_bounds__(kSortThreads) k_lsd_sort(LsdGeom g, LsdScratch sc) {
+  const int f = blockIdx.x;
+  const SortPtrs P = sort_ptrs(g, sc, f);
+  // bins: int(norm * bin_coef), bin_coef = 1023 / max_grad (ll_angle)
+  const unsigned mq = sc.maxq[f];
+  const double max_grad = mq ? sqrt(mq / 4.0) : -1.0;
+  const double bin_coef = max_grad > 0 ? 1023.0 / max_grad : 0.0;
+  const int sw = g.sw, w1 = g.sw - 1;
+  const int* q = sc.q + (long long)f * sw * g.sh;
+  for (int i = threadIdx.x; i < g.n; i += kSortThreads) {
+    const int y = i / w1, x = i - y * w1;
+    const int key = (int)(sqrt(q[y * sw + x] / 4.0) * bin_coef);
+    P.A[i] = ((uint32_t)key << 22) | (uint32_t)i;
+  }
+  __syncthreads();
+  sort_core(P, g.n);
+}
+
+// test hook: sort caller-provided keys (frame slot 0)
+__global__ void __launch_bounds__(kSortThreads) k_lsd_sort_keys(LsdGeom g, LsdScratch sc,
+                                                                const int* __restrict__ keys) {
+  const SortPtrs P = sort_ptrs(g, sc, 0);
+  for (int i = threadIdx.x; i < g.n; i += kSortThreads)
+    P.A[i] = ((uint32_t)keys[i] << 22) | (uint32_t)i;
+  __syncthreads();
+  sort_core(P, g.n);
+}
+
+void launch_lsd_blur(const LsdGeom& g, const uint8_t* img, int stride, long long frame_pitch,
+                     uint8_t* out, int batch, hipStream_t s) {
+  dim3 grid((g.W + kBlTW - 1) / kBlTW, (g.H + kBlTH - 1) / kBlTH, batch);
+  hipLaunchKernelGGL(k_lsd_blur, grid, dim3(256), 0, s, g, img, stride, frame_pitch, out);
+}
+
+void launch_lsd_resize(const LsdGeom& g, const int* tabs, const uint8_t* blur, uint8_t* scaled,
+                       int batch, hipStream_t s) {
+  hipLaunchKernelGGL(k_lsd_resize, dim3((g.sw * g.sh + 255) / 256, batch), dim3(256), 0, s, g,
+                     tabs, blur, scaled);
+}
+
+void launch_lsd_grad(const LsdGeom& g, const uint8_t* scaled, float* deg, int* q, unsigned* maxq,
+                     int batch, hipStream_t s) {
+  hipLaunchKernelGGL(k_lsd_grad, dim3((g.sw * g.sh + 255) / 256, batch), dim3(256), 0, s, g,
+                     scaled, deg, q, maxq);
+}
+
+void launch_lsd_sort(const LsdGeom& g, const LsdScratch& sc, int batch, hipStream_t s) {
+  hipLaunchKernelGGL(k_lsd_sort, dim3(batch), dim3(kSortThreads), 0, s, g, sc);
+}
+
+void launch_lsd_sort_keys(int n, const int* keys, const LsdScratch& sc, hipStream_t s) {
+  LsdGeom g{};
+  g.n = n;
+  g.seg_cap = n / 17 + 2;
+  g.chunk_cap = n / kLsdSortChunk + g.seg_cap + 2;
+  g.leaf_cap = n / 2 + 2;
+  hipLaunchKernelGGL(k_lsd_sort_keys, dim3(1), dim3(kSortThreads), 0, s, g, sc, keys);
+}
+
+}  // namespace orbpl

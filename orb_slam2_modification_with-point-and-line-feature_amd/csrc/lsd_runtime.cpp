@@ -1,0 +1,339 @@
+// Host runtime and C-ABI of the line-feature path (include/orbpl.h, lsdx_*):
+// LineExtractor::ExtractLineSegment (/root/reference/src/LineExtractor.cpp:12-74).
+// One lsdx_ctx = one device + one HIP stream + scratch for max_batch frames of
+// one image geometry.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "../../include/orbpl.h"
+#include "lsd_kernels.h"
+#include "lsd_math.h"
+#include "orbpl_runtime.h"
+
+using namespace orbpl;
+
+#define HIP_CHECK(expr)                                              \
+  do {                                                               \
+    hipError_t _e = (expr);                                          \
+    if (_e != hipSuccess) return orbpl::hip_fail(_e, #expr, __LINE__); \
+  } while (0)
+
+namespace {
+
+// getGaussianKernelBitExact rounded to 8.8 fixed point (GaussianBlur 8U).
+void gauss_kernel_fixed(int n, double sigma, int* k) {
+  const double scale2X = -0.125 / (sigma * sigma);
+  const int n2 = (n - 1) / 2;
+  double vals[16];
+  double sum = 0;
+  for (int i = 0, x = 1 - n; i < n2; i++, x += 2) {
+    vals[i] = lsdm::exp_((double)(x * x) * scale2X);
+    sum += vals[i];
+  }
+  sum = sum * 2 + 1.0;
+  const double mul1 = 1.0 / sum;
+  int s2 = 0;
+  for (int i = 0; i < n2; i++) {
+    const int t = (int)std::lrint(vals[i] * mul1 * 256.0);
+    k[i] = k[n - 1 - i] = t;
+    s2 += t;
+  }
+  k[n2] = 256 - 2 * s2;
+}
+
+// interpolationLinear coefficients (resize_bitExact): offsets, 8.8 c1, range.
+void lin_tab(double inv_scale, int ssize, int dsize, int* ofs, int* c1, int* mn, int* mx) {
+  const double scale = 1.0 / inv_scale;
+  int minofst = 0, maxofst = dsize;
+  for (int d = 0; d < dsize; d++) {
+    const double fval = scale * ((double)d + 0.5) - 0.5;
+    const int ival = (int)std::floor(fval);
+    ofs[d] = 0;
+    c1[d] = 0;
+    if (ival >= 0 && ssize > 1) {
+      if (ival < ssize - 1) {
+        ofs[d] = ival;
+        c1[d] = (int)std::lrint((fval - (double)ival) * 256.0);
+      } else {
+        ofs[d] = ssize - 1;
+        maxofst = std::min(maxofst, d);
+      }
+    } else {
+      minofst = std::max(minofst, d + 1);
+    }
+  }
+  *mn = minofst;
+  *mx = maxofst;
+}
+
+}  // namespace
+
+struct lsdx_ctx {
+  int device = 0, max_batch = 0, W = 0, H = 0;
+  LsdGeom g{};
+  LsdScratch sc{};
+  hipStream_t stream = nullptr;
+  int* d_tabs = nullptr;
+  uint8_t* d_in = nullptr;
+  int last_batch = 0;
+  std::vector<void*> allocs;
+};
+
+static int lx_alloc(lsdx_ctx* c, void** p, size_t bytes) {
+  hipError_t e = hipMalloc(p, bytes ? bytes : 1);
+  if (e != hipSuccess) return hip_fail(e, "hipMalloc", __LINE__);
+  c->allocs.push_back(*p);
+  return ORBPL_OK;
+}
+
+namespace orbpl {
+int lsd_geometry(int W, int H, LsdGeom* out) {
+  if (W < 16 || H < 16 || W > 4096 || H > 4096) return arg_fail("image size out of range [16, 4096]");
+  LsdGeom g{};
+  g.W = W;
+  g.H = H;
+  const double scale = 0.8, sigma_scale = 0.6, quant = 2.0, ang_th = 22.5;
+  g.sw = (int)std::lrint(W * scale);
+  g.sh = (int)std::lrint(H * scale);
+  if (g.sw > 65535 || g.sh > 65535) return arg_fail("image too large");
+  g.n = (g.sw - 1) * (g.sh - 1);
+  if (g.n >= (1 << 22)) return arg_fail("image too large for the LSD pixel order (2^22 pixels)");
+  const double sigma = sigma_scale / scale;
+  const unsigned h = (unsigned)std::ceil(sigma * std::sqrt(2 * 3.0 * lsdm::log_(10.0)));
+  g.ksize = 1 + 2 * (int)h;
+  if (g.ksize > 7) return arg_fail("unexpected LSD Gaussian size");
+  gauss_kernel_fixed(g.ksize, sigma, g.gk);
+  g.prec = 3.14159265358979323846 * ang_th / 180;
+  g.p = ang_th / 180;
+  g.rho = quant / lsdm::sin_(g.prec);
+  g.log_nt = 5 * (lsdm::log10_(double(g.sw)) + lsdm::log10_(double(g.sh))) / 2 + lsdm::log10_(11.0);
+  g.min_reg_size = (int)(size_t)(-g.log_nt / lsdm::log10_(g.p));
+  g.seg_cap = g.n / 17 + 2;
+  g.chunk_cap = g.n / kLsdSortChunk + g.seg_cap + 2;
+  g.leaf_cap = g.n / 2 + 2;
+  *out = g;
+  return ORBPL_OK;
+}
+}  // namespace orbpl
+
+extern "C" {
+
+int lsdx_destroy(lsdx_ctx* c) {
+  if (!c) return ORBPL_OK;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (void* p : c->allocs) (void)hipFree(p);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return ORBPL_OK;
+}
+
+int lsdx_create(int width, int height, int max_batch, int device, lsdx_ctx** out) {
+  if (!out || max_batch <= 0) return arg_fail("bad argument");
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+    arg_fail("no HIP device visible");
+    return ORBPL_ERR_NODEVICE;
+  }
+  if (device < 0 || device >= ndev) return arg_fail("device index out of range");
+  lsdx_ctx* c = new lsdx_ctx();
+  c->device = device;
+  c->max_batch = max_batch;
+  c->W = width;
+  c->H = height;
+  int rc = lsd_geometry(width, height, &c->g);
+  if (rc) {
+    delete c;
+    return rc;
+  }
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return hip_fail(hipErrorUnknown, "hipStreamCreate", __LINE__);
+  }
+  const LsdGeom& g = c->g;
+  const size_t B = max_batch, n = g.n, px = (size_t)g.sw * g.sh;
+  LsdScratch& s = c->sc;
+#define LA(ptr, bytes)                                     \
+  do {                                                     \
+    int _r = lx_alloc(c, (void**)&(ptr), (bytes));         \
+    if (_r) { lsdx_destroy(c); return _r; }                \
+  } while (0)
+  LA(c->d_in, B * width * height);
+  LA(s.blur, B * width * height);
+  LA(s.scaled, B * px);
+  LA(s.deg, B * px * 4);
+  LA(s.q, B * px * 4);
+  LA(s.maxq, B * 4);
+  LA(s.A, B * n * 4);
+  LA(s.Lpos, B * n * 4);
+  LA(s.Rpos, B * n * 4);
+  LA(s.seg0, B * g.seg_cap * sizeof(int4));
+  LA(s.seg1, B * g.seg_cap * sizeof(int4));
+  LA(s.heap, B * g.seg_cap * sizeof(int4));
+  LA(s.seg_i, B * 8 * g.seg_cap * 4);
+  LA(s.chunk_i, B * 4 * g.chunk_cap * 4);
+  LA(s.leaves, B * g.leaf_cap * sizeof(int2));
+  LA(s.reg, B * px * 4);
+  LA(s.lines, B * kLsdMaxLines * 4 * 4);
+  LA(s.nlines, B * 4);
+  LA(s.err, B * 4);
+  LA(c->d_tabs, (size_t)(2 * g.sw + 2 * g.sh) * 4);
+#undef LA
+  std::vector<int> tabs(2 * g.sw + 2 * g.sh);
+  lin_tab(0.8, width, g.sw, tabs.data(), tabs.data() + g.sw, &c->g.rx0, &c->g.rx1);
+  lin_tab(0.8, height, g.sh, tabs.data() + 2 * g.sw, tabs.data() + 2 * g.sw + g.sh, &c->g.ry0,
+          &c->g.ry1);
+  if (hipMemcpy(c->d_tabs, tabs.data(), tabs.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+    lsdx_destroy(c);
+    return hip_fail(hipErrorUnknown, "hipMemcpy", __LINE__);
+  }
+  *out = c;
+  return ORBPL_OK;
+}
+
+int lsdx_detect_batch_device(lsdx_ctx* c, const uint8_t* d_imgs, int batch, int stride,
+                             int64_t frame_pitch) {
+  if (!c || !d_imgs || batch <= 0 || batch > c->max_batch) return arg_fail("bad argument");
+  if (stride < c->W) return arg_fail("stride < width");
+  HIP_CHECK(hipSetDevice(c->device));
+  const LsdGeom& g = c->g;
+  hipStream_t s = c->stream;
+  HIP_CHECK(hipMemsetAsync(c->sc.maxq, 0, (size_t)batch * 4, s));
+  HIP_CHECK(hipMemsetAsync(c->sc.err, 0, (size_t)batch * 4, s));
+  launch_lsd_blur(g, d_imgs, stride, frame_pitch, c->sc.blur, batch, s);
+  launch_lsd_resize(g, c->d_tabs, c->sc.blur, c->sc.scaled, batch, s);
+  launch_lsd_grad(g, c->sc.scaled, c->sc.deg, c->sc.q, c->sc.maxq, batch, s);
+  launch_lsd_sort(g, c->sc, batch, s);
+  launch_lsd_grow(g, c->sc, batch, s);
+  HIP_CHECK(hipGetLastError());
+  c->last_batch = batch;
+  return ORBPL_OK;
+}
+
+int lsdx_synchronize(lsdx_ctx* c) {
+  if (!c) return arg_fail("NULL context");
+  HIP_CHECK(hipSetDevice(c->device));
+  HIP_CHECK(hipStreamSynchronize(c->stream));
+  if (c->last_batch > 0) {
+    std::vector<int> err(c->last_batch);
+    HIP_CHECK(hipMemcpy(err.data(), c->sc.err, err.size() * 4, hipMemcpyDeviceToHost));
+    for (int e : err)
+      if (e) {
+        arg_fail("LSD scratch capacity exceeded on device");
+        return ORBPL_ERR_OVERFLOW;
+      }
+  }
+  return ORBPL_OK;
+}
+
+int lsdx_get_lines(lsdx_ctx* c, int frame, float* lines, int cap, int* n_out) {
+  if (!c || !n_out || frame < 0 || frame >= c->last_batch) return arg_fail("bad argument");
+  int rc = lsdx_synchronize(c);
+  if (rc) return rc;
+  int n = 0;
+  HIP_CHECK(hipMemcpy(&n, c->sc.nlines + frame, 4, hipMemcpyDeviceToHost));
+  *n_out = n;
+  if (n > cap) {
+    arg_fail("line buffer too small");
+    return ORBPL_ERR_CAPACITY;
+  }
+  if (n > 0 && lines)
+    HIP_CHECK(hipMemcpy(lines, c->sc.lines + (size_t)frame * kLsdMaxLines * 4, (size_t)n * 16,
+                        hipMemcpyDeviceToHost));
+  return ORBPL_OK;
+}
+
+int lsdx_detect(lsdx_ctx* c, const uint8_t* img, int width, int height, int stride, float* lines,
+                int cap, int* n_out) {
+  if (!c || !img || !n_out) return arg_fail("NULL argument");
+  if (width != c->W || height != c->H) return arg_fail("image size differs from the context");
+  HIP_CHECK(hipSetDevice(c->device));
+  HIP_CHECK(hipMemcpy2DAsync(c->d_in, width, img, stride, width, height, hipMemcpyHostToDevice,
+                             c->stream));
+  int rc = lsdx_detect_batch_device(c, c->d_in, 1, width, (long long)width * height);
+  if (rc) return rc;
+  return lsdx_get_lines(c, 0, lines, cap, n_out);
+}
+
+int lsdx_get_stages(lsdx_ctx* c, int frame, uint8_t* scaled, float* deg, uint32_t* order,
+                    int* sw, int* sh, int* n_order) {
+  if (!c || frame < 0 || frame >= c->last_batch) return arg_fail("bad argument");
+  int rc = lsdx_synchronize(c);
+  if (rc) return rc;
+  const LsdGeom& g = c->g;
+  const size_t px = (size_t)g.sw * g.sh;
+  if (sw) *sw = g.sw;
+  if (sh) *sh = g.sh;
+  if (n_order) *n_order = g.n;
+  if (scaled) HIP_CHECK(hipMemcpy(scaled, c->sc.scaled + frame * px, px, hipMemcpyDeviceToHost));
+  if (deg) HIP_CHECK(hipMemcpy(deg, c->sc.deg + frame * px, px * 4, hipMemcpyDeviceToHost));
+  if (order) {
+    std::vector<uint32_t> a(g.n);
+    HIP_CHECK(hipMemcpy(a.data(), c->sc.A + (size_t)frame * g.n, (size_t)g.n * 4,
+                        hipMemcpyDeviceToHost));
+    const int w1 = g.sw - 1;
+    for (int i = 0; i < g.n; i++) {
+      const int idx = (int)(a[i] & 0x3FFFFFu);
+      order[i] = (uint32_t)(idx % w1) | ((uint32_t)(idx / w1) << 16);
+    }
+  }
+  return ORBPL_OK;
+}
+
+// Test hook: the device introsort replica on caller keys (values 0..1023);
+// perm receives the sorted record indices.
+int orbpl_test_introsort(const int* keys, int n, int* perm) {
+  if (!keys || !perm || n <= 0 || n >= (1 << 22)) return arg_fail("bad argument");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+    arg_fail("no HIP device visible");
+    return ORBPL_ERR_NODEVICE;
+  }
+  for (int i = 0; i < n; i++)
+    if (keys[i] < 0 || keys[i] > 1023) return arg_fail("keys must be in [0, 1023]");
+  LsdScratch sc{};
+  const int seg_cap = n / 17 + 2, chunk_cap = n / kLsdSortChunk + seg_cap + 2, leaf_cap = n / 2 + 2;
+  std::vector<void*> al;
+  auto A = [&](void** p, size_t b) {
+    hipError_t e = hipMalloc(p, b ? b : 1);
+    if (e == hipSuccess) al.push_back(*p);
+    return e;
+  };
+  int* d_keys = nullptr;
+  hipError_t e = hipSuccess;
+  e = e ? e : A((void**)&d_keys, (size_t)n * 4);
+  e = e ? e : A((void**)&sc.A, (size_t)n * 4);
+  e = e ? e : A((void**)&sc.Lpos, (size_t)n * 4);
+  e = e ? e : A((void**)&sc.Rpos, (size_t)n * 4);
+  e = e ? e : A((void**)&sc.seg0, (size_t)seg_cap * sizeof(int4));
+  e = e ? e : A((void**)&sc.seg1, (size_t)seg_cap * sizeof(int4));
+  e = e ? e : A((void**)&sc.heap, (size_t)seg_cap * sizeof(int4));
+  e = e ? e : A((void**)&sc.seg_i, (size_t)8 * seg_cap * 4);
+  e = e ? e : A((void**)&sc.chunk_i, (size_t)4 * chunk_cap * 4);
+  e = e ? e : A((void**)&sc.leaves, (size_t)leaf_cap * sizeof(int2));
+  e = e ? e : A((void**)&sc.err, 4);
+  int rc = ORBPL_OK, err = 0;
+  std::vector<uint32_t> a(n);
+  if (e == hipSuccess) e = hipMemcpy(d_keys, keys, (size_t)n * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemset(sc.err, 0, 4);
+  if (e == hipSuccess) {
+    launch_lsd_sort_keys(n, d_keys, sc, nullptr);
+    e = hipDeviceSynchronize();
+  }
+  if (e == hipSuccess) e = hipMemcpy(a.data(), sc.A, (size_t)n * 4, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(&err, sc.err, 4, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) rc = hip_fail(e, "introsort test", __LINE__);
+  else if (err) rc = (arg_fail("sort scratch overflow"), ORBPL_ERR_OVERFLOW);
+  for (void* p : al) (void)hipFree(p);
+  if (rc == ORBPL_OK)
+    for (int i = 0; i < n; i++) perm[i] = (int)(a[i] & 0x3FFFFFu);
+  return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,76 @@
+"""GPU parity of the LSD line detector (LineExtractor.cpp:20-21) against the
+CPU oracle (oracle/lsd_oracle.cpp): every stage bit-exact."""
+import numpy as np
+import pytest
+
+from _scenes import sequence
+
+pytestmark = pytest.mark.gpu
+
+
+def _keysets():
+    rng = np.random.default_rng(7)
+    yield "tiny", rng.integers(0, 4, 5)
+    yield "seventeen", rng.integers(0, 3, 17)
+    yield "uniform", rng.integers(0, 1024, 5000)
+    yield "dups", rng.integers(0, 8, 20000)
+    yield "skewed", np.minimum(1023, rng.exponential(30, 100000).astype(int))
+    yield "sorted", np.arange(3000) % 1024
+    yield "reversed", (np.arange(3000)[::-1]) % 1024
+    yield "constant", np.full(4000, 5)
+    yield "organ", np.concatenate([np.arange(2000), np.arange(2000)[::-1]]) % 1024
+
+
+@pytest.mark.parametrize("name,keys", list(_keysets()), ids=[k for k, _ in _keysets()])
+def test_introsort_replica_matches_std_sort(orbpl, oracle, name, keys):
+    keys = np.asarray(keys, np.int32)
+    assert np.array_equal(orbpl.test_introsort(keys), oracle.introsort_perm(keys))
+
+
+@pytest.fixture(scope="module")
+def frames():
+    out = []
+    for seed in (1, 2, 3):
+        cfg, traj, fr = sequence(1, seed)
+        out.append(fr[0][0])
+    return out
+
+
+def test_lsd_stages_bit_exact(orbpl, oracle, frames):
+    det = orbpl.LineSegmentDetector(640, 480)
+    for g in frames:
+        det.detect(g)
+        scaled, deg, order = det.stages(0)
+        s_o, ang_o, ord_o = oracle.lsd_stages(g)
+        assert np.array_equal(scaled, s_o)
+        notdef = ang_o == -1024.0
+        assert np.array_equal(deg < 0, notdef)
+        a = deg.astype(np.float64) * (np.pi / 180)
+        assert np.array_equal(a[~notdef], ang_o[~notdef])
+        assert np.array_equal(order, ord_o)
+
+
+def test_lsd_lines_bit_exact(orbpl, oracle, frames):
+    det = orbpl.LineSegmentDetector(640, 480)
+    for g in frames:
+        L = det.detect(g)
+        Lo = oracle.lsd_detect(g)
+        assert len(L) == len(Lo) and len(L) > 50
+        assert np.array_equal(L, Lo)
+
+
+def test_lsd_batch_device_matches_single(orbpl, oracle, frames):
+    B = len(frames)
+    det = orbpl.LineSegmentDetector(640, 480, max_batch=B)
+    buf = orbpl.DeviceBuffer.from_array(np.stack(frames))
+    det.detect_batch_device(buf.ptr, B)
+    det.synchronize()
+    for f, g in enumerate(frames):
+        assert np.array_equal(det.lines(f), oracle.lsd_detect(g))
+
+
+def test_lsd_kitti_geometry(orbpl, oracle):
+    cfg, traj, fr = sequence(1, 4, cam_name="KITTI00", width=1241, height=376)
+    g = fr[0][0]
+    det = orbpl.LineSegmentDetector(1241, 376)
+    assert np.array_equal(det.detect(g), oracle.lsd_detect(g))
