@@ -307,6 +307,11 @@ int lsdx_get_stages(lsdx_ctx* ctx, int frame, uint8_t* scaled, float* deg, uint3
 /* Test hook: the device replica of std::sort(records, key greater) on keys
  * in [0, 1023]; perm receives the record indices in sorted order. */
 int orbpl_test_introsort(const int32_t* keys, int n, int32_t* perm);
+/* Debug: batch-mean shader-clock counters of the LSD seed loop of the last
+ * run: region growing cycles, fit + refinement cycles, 0, total cycles,
+ * region pixels, neighbourhood prefetches, prefetch cycles, rectangles
+ * passed to NFA validation. */
+int lsdx_debug_profile(lsdx_ctx* ctx, long long* out8);
 
 
 #ifdef __cplusplus

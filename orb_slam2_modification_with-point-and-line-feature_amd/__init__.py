@@ -534,6 +534,7 @@ def _declare(L):  # noqa: F811
     L.lsdx_get_lines.argtypes = [vp, i, vp, i, ip]
     L.lsdx_get_stages.argtypes = [vp, i, vp, vp, vp, ip, ip, ip]
     L.orbpl_test_introsort.argtypes = [vp, i, vp]
+    L.lsdx_debug_profile.argtypes = [vp, vp]
 
 
 class LineSegmentDetector:
@@ -579,6 +580,13 @@ class LineSegmentDetector:
         n = C.c_int(0)
         check(lib().lsdx_get_lines(self._h, frame, _ptr(out), cap, C.byref(n)), "lsdx_get_lines")
         return out[:n.value].copy()
+
+    def debug_profile(self):
+        out = np.zeros(8, np.int64)
+        check(lib().lsdx_debug_profile(self._h, _ptr(out)), "lsdx_debug_profile")
+        keys = ("grow_cyc", "fit_refine_cyc", "reserved", "total_cyc", "region_px", "prefetches",
+                "prefetch_cyc", "candidates")
+        return dict(zip(keys, out.tolist()))
 
     def stages(self, frame=0):
         sw, sh = int(round(self.W * 0.8)), int(round(self.H * 0.8))

@@ -25,7 +25,7 @@ namespace {
 
 constexpr double kPi = 3.14159265358979323846;
 constexpr double kDegToRad = kPi / 180;
-constexpr int kRegLds = 4096;
+constexpr int kRegLds = 512;
 
 struct Rect {
   double x1, y1, x2, y2, width, x, y, theta, dx, dy, prec, p;
@@ -36,12 +36,18 @@ struct Frame {
   const float* deg;
   const int* q;
   uint32_t* used;     // LDS bits
-  uint32_t* reg_l;    // LDS region list
-  uint32_t* reg_g;    // global continuation
+  uint32_t* reg_l;    // LDS region points (x | y << 16)
+  int* regq_l;        // LDS q (gx^2 + gy^2) of each region point
+  float* regd_l;      // LDS degrees of each region point
+  uint32_t* reg_g;    // global continuation: (pt, q, deg) triples
+  float* ring;        // LDS 64 x 9 prefetched 3x3 degree neighbourhoods
   int4* rows;         // LDS rect_nfa rows
+  Rect* rect0;        // LDS: the current rectangle (rec)
+  Rect* rect1;        // LDS: rect_improve's trial rectangle (r)
   int row_cap;
   double log_nt;
   int lane;
+  long long pf_cyc, pf_cnt, seed_cyc;
 };
 
 __device__ __forceinline__ bool used_get(const Frame& F, int x, int y) {
@@ -50,25 +56,63 @@ __device__ __forceinline__ bool used_get(const Frame& F, int x, int y) {
 }
 __device__ __forceinline__ void used_set(Frame& F, int x, int y, bool v) {
   const int i = y * F.sw + x;
-  // every lane performs the same update (wave-uniform serial execution)
+  // the lanes run the same serial program; one of them updates the word
+  // (single writer: a plain read-modify-write)
   if (F.lane == 0) {
-    if (v) atomicOr(&F.used[i >> 5], 1u << (i & 31));
-    else atomicAnd(&F.used[i >> 5], ~(1u << (i & 31)));
+    const uint32_t w = F.used[i >> 5], b = 1u << (i & 31);
+    F.used[i >> 5] = v ? (w | b) : (w & ~b);
   }
   __builtin_amdgcn_wave_barrier();
 }
 __device__ __forceinline__ uint32_t reg_get(const Frame& F, int i) {
-  return i < kRegLds ? F.reg_l[i] : F.reg_g[i - kRegLds];
+  return i < kRegLds ? F.reg_l[i] : F.reg_g[3 * (i - kRegLds)];
 }
-__device__ __forceinline__ void reg_set(Frame& F, int i, uint32_t v) {
-  if (i < kRegLds) F.reg_l[i] = v;
-  else F.reg_g[i - kRegLds] = v;
+__device__ __forceinline__ int regq_get(const Frame& F, int i) {
+  return i < kRegLds ? F.regq_l[i] : (int)F.reg_g[3 * (i - kRegLds) + 1];
+}
+__device__ __forceinline__ float regd_get(const Frame& F, int i) {
+  return i < kRegLds ? F.regd_l[i] : __uint_as_float(F.reg_g[3 * (i - kRegLds) + 2]);
+}
+// point + degree (q is filled in bulk by fill_q when the region is fitted)
+__device__ __forceinline__ void reg_put(Frame& F, int i, uint32_t pt, float d) {
+  if (F.lane == 0) {
+    if (i < kRegLds) {
+      F.reg_l[i] = pt;
+      F.regd_l[i] = d;
+    } else {
+      F.reg_g[3 * (i - kRegLds)] = pt;
+      F.reg_g[3 * (i - kRegLds) + 2] = __float_as_uint(d);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+__device__ __forceinline__ void reg_swap(Frame& F, int i, int j) {
+  const uint32_t pi = reg_get(F, i), pj = reg_get(F, j);
+  const int qi = regq_get(F, i), qj = regq_get(F, j);
+  const float di = regd_get(F, i), dj = regd_get(F, j);
+  __builtin_amdgcn_wave_barrier();
+  if (F.lane == 0) {
+    if (i < kRegLds) { F.reg_l[i] = pj; F.regq_l[i] = qj; F.regd_l[i] = dj; }
+    else { F.reg_g[3 * (i - kRegLds)] = pj; F.reg_g[3 * (i - kRegLds) + 1] = (uint32_t)qj; F.reg_g[3 * (i - kRegLds) + 2] = __float_as_uint(dj); }
+    if (j < kRegLds) { F.reg_l[j] = pi; F.regq_l[j] = qi; F.regd_l[j] = di; }
+    else { F.reg_g[3 * (j - kRegLds)] = pi; F.reg_g[3 * (j - kRegLds) + 1] = (uint32_t)qi; F.reg_g[3 * (j - kRegLds) + 2] = __float_as_uint(di); }
+  }
+  __threadfence_block();
+  __builtin_amdgcn_wave_barrier();
+}
+// q of region points [0, n): all lanes load in parallel
+__device__ __forceinline__ void fill_q(Frame& F, int n) {
+  for (int j = F.lane; j < n; j += 64) {
+    const uint32_t pt = reg_get(F, j);
+    const int v = F.q[(int)(pt >> 16) * F.sw + (int)(pt & 0xFFFF)];
+    if (j < kRegLds) F.regq_l[j] = v;
+    else F.reg_g[3 * (j - kRegLds) + 1] = (uint32_t)v;
+  }
+  __threadfence_block();
   __builtin_amdgcn_wave_barrier();
 }
 __device__ __forceinline__ double deg2ang(float d) { return (double)d * kDegToRad; }
-__device__ __forceinline__ double modgrad(const Frame& F, int x, int y) {
-  return sqrt(F.q[y * F.sw + x] / 4.0);
-}
+__device__ __forceinline__ double modgrad_q(int q) { return sqrt(q / 4.0); }
 
 __device__ __forceinline__ bool aligned_deg(float d, double theta, double prec) {
   if (d < 0.f) return false;  // NOTDEF
@@ -112,6 +156,7 @@ __device__ double log_gamma(double x) {
                        1168.92649479, 83.8676043424, 2.50662827511};
   double a = (x + 0.5) * lsdm::log_(x + 5.5) - (x + 5.5);
   double b = 0;
+#pragma unroll
   for (int n = 0; n < 7; ++n) {
     a -= lsdm::log_(x + double(n));
     b += q[n] * lsdm::powi_(x, double(n));
@@ -119,12 +164,24 @@ __device__ double log_gamma(double x) {
   return a + lsdm::log_(b);
 }
 
-__device__ double nfa(int n, int k, double p, double log_nt) {
+__device__ __forceinline__ double shfl_d(double v, int src) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __shfl((int)(b & 0xFFFFFFFF), src, 64), hi = __shfl((int)(b >> 32), src, 64);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// nfa (lsd.cpp). Wave-parallel, same values as the serial reference: the
+// three log_gamma terms are evaluated on lanes 0-2, and the tail loop's
+// term / bin_tail recurrence is replayed serially while the (expensive)
+// stopping test of 64 consecutive iterations is evaluated one per lane.
+__device__ double nfa(int n, int k, double p, double log_nt, int lane) {
   if (n == 0 || k == 0) return -log_nt;
   if (n == k) return -log_nt - double(n) * lsdm::log10_(p);
   const double p_term = p / (1 - p);
-  const double log1term = log_gamma(double(n) + 1) - log_gamma(double(k) + 1) -
-                          log_gamma(double(n - k) + 1) + double(k) * lsdm::log_(p) +
+  const double garg = lane == 0 ? double(n) + 1 : (lane == 1 ? double(k) + 1 : double(n - k) + 1);
+  const double lg = log_gamma(garg);
+  const double lg0 = shfl_d(lg, 0), lg1 = shfl_d(lg, 1), lg2 = shfl_d(lg, 2);
+  const double log1term = lg0 - lg1 - lg2 + double(k) * lsdm::log_(p) +
                           double(n - k) * lsdm::log_(1.0 - p);
   double term = lsdm::exp_(log1term);
   if (double_equal(term, 0)) {
@@ -133,51 +190,113 @@ __device__ double nfa(int n, int k, double p, double log_nt) {
   }
   double bin_tail = term;
   const double tolerance = 0.1;
-  for (int i = k + 1; i <= n; ++i) {
-    const double bin_term = double(n - i + 1) / double(i);
-    const double mult_term = bin_term * p_term;
-    term *= mult_term;
-    bin_tail += term;
-    if (bin_term < 1) {
-      const double err =
-          term * ((1 - lsdm::powi_(mult_term, double(n - i + 1))) / (1 - mult_term) - 1);
-      if (err < tolerance * fabs(-lsdm::log10_(bin_tail) - log_nt) * bin_tail) break;
+  for (int i0 = k + 1; i0 <= n; i0 += 64) {
+    // serial recurrence; lane l keeps iteration i0 + l
+    double my_term = 0, my_tail = 0, my_bin = 2, my_mult = 0;
+    const int cnt = min(64, n - i0 + 1);
+    for (int l = 0; l < cnt; l++) {
+      const int i = i0 + l;
+      const double bin_term = double(n - i + 1) / double(i);
+      const double mult_term = bin_term * p_term;
+      term *= mult_term;
+      bin_tail += term;
+      if (lane == l) {
+        my_term = term;
+        my_tail = bin_tail;
+        my_bin = bin_term;
+        my_mult = mult_term;
+      }
     }
+    bool stop = false;
+    double my_res = 0;
+    if (lane < cnt && my_bin < 1) {
+      const int i = i0 + lane;
+      const double err =
+          my_term * ((1 - lsdm::powi_(my_mult, double(n - i + 1))) / (1 - my_mult) - 1);
+      const double lt = lsdm::log10_(my_tail);
+      stop = err < tolerance * fabs(-lt - log_nt) * my_tail;
+      my_res = -lt - log_nt;
+    }
+    const unsigned long long m = __ballot(stop);
+    if (m) return shfl_d(my_res, __ffsll((long long)m) - 1);
   }
   return -lsdm::log10_(bin_tail) - log_nt;
 }
 
-// region_grow (lsd.cpp): returns the region size; the region list holds the
-// points in insertion order.
-__device__ int region_grow(Frame& F, int sx, int sy, double& reg_angle, double prec) {
-  const int sw = F.sw, sh = F.sh;
-  int n = 0;
-  reg_set(F, n++, (uint32_t)sx | ((uint32_t)sy << 16));
-  reg_angle = deg2ang(F.deg[sy * sw + sx]);
-  float sumdx = (float)lsdm::cos_(reg_angle);
-  float sumdy = (float)lsdm::sin_(reg_angle);
-  used_set(F, sx, sy, true);
-  for (int i = 0; i < n; i++) {
-    const uint32_t pt = reg_get(F, i);
+// Prefetch the 3x3 degree neighbourhoods of region points [i0, i1) (at most
+// 64) into the ring, one point per lane.
+__device__ __forceinline__ void prefetch_ring(Frame& F, int i0, int i1) {
+  const int j = i0 + F.lane;
+  if (j < i1) {
+    const uint32_t pt = reg_get(F, j);
     const int x = (int)(pt & 0xFFFF), y = (int)(pt >> 16);
-    // the nine degree values are static: load them together
-    float dv[9];
+    float v[9];
 #pragma unroll
     for (int k = 0; k < 9; k++) {
       const int xx = x + (k % 3) - 1, yy = y + (k / 3) - 1;
-      dv[k] = (xx >= 0 && xx < sw && yy >= 0 && yy < sh) ? F.deg[yy * sw + xx] : kLsdNotdef;
+      v[k] = (xx >= 0 && xx < F.sw && yy >= 0 && yy < F.sh) ? F.deg[yy * F.sw + xx] : kLsdNotdef;
+    }
+    float* r = F.ring + (j & 63) * 9;
+#pragma unroll
+    for (int k = 0; k < 9; k++) r[k] = v[k];
+  }
+  __threadfence_block();
+  __builtin_amdgcn_wave_barrier();
+}
+
+// region_grow (lsd.cpp): returns the region size; the region list holds the
+// points in insertion order. Degree neighbourhoods of pending points are
+// fetched 64 at a time (they are static), the USED tests stay in order.
+__device__ __forceinline__ int region_grow(Frame& F, int sx, int sy, double& reg_angle, double prec) {
+  const int sw = F.sw, sh = F.sh;
+  int n = 1;
+  const uint32_t p0 = (uint32_t)sx | ((uint32_t)sy << 16);
+  if (F.lane == 0) F.reg_l[0] = p0;
+  __builtin_amdgcn_wave_barrier();
+  const long long tq0 = clock64();
+  prefetch_ring(F, 0, 1);
+  F.pf_cyc += clock64() - tq0;
+  F.pf_cnt++;
+  int pf_end = 1;
+  const float d0 = F.ring[4];
+  reg_put(F, 0, p0, d0);
+  reg_angle = deg2ang(d0);
+  double s0, c0;
+  lsdm::sincos_(reg_angle, &s0, &c0);
+  float sumdx = (float)c0;
+  float sumdy = (float)s0;
+  used_set(F, sx, sy, true);
+  for (int i = 0; i < n; i++) {
+    if (i == pf_end) {
+      pf_end = min(n, i + 64);
+      const long long tq = clock64();
+      prefetch_ring(F, i, pf_end);
+      F.pf_cyc += clock64() - tq;
+      F.pf_cnt++;
+    }
+    const uint32_t pt = reg_get(F, i);
+    const int x = (int)(pt & 0xFFFF), y = (int)(pt >> 16);
+    const float* dv = F.ring + (i & 63) * 9;
+    // USED bits of the 3x3 block, read once: marking a pixel below changes
+    // only that pixel's own bit, which is not visited again in this block
+    unsigned ub = 0;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+      const int xx = x + (k % 3) - 1, yy = y + (k / 3) - 1;
+      if (xx >= 0 && xx < sw && yy >= 0 && yy < sh && used_get(F, xx, yy)) ub |= 1u << k;
     }
 #pragma unroll
     for (int k = 0; k < 9; k++) {
       const int xx = x + (k % 3) - 1, yy = y + (k / 3) - 1;
       if (xx < 0 || xx >= sw || yy < 0 || yy >= sh) continue;
-      if (!used_get(F, xx, yy) && aligned_deg(dv[k], reg_angle, prec)) {
+      const float d = dv[k];
+      if (!((ub >> k) & 1u) && aligned_deg(d, reg_angle, prec)) {
         used_set(F, xx, yy, true);
-        reg_set(F, n++, (uint32_t)xx | ((uint32_t)yy << 16));
-        float c, s;
-        cr_cos_sin((float)deg2ang(dv[k]), &c, &s);
+        reg_put(F, n++, (uint32_t)xx | ((uint32_t)yy << 16), d);
+        float c, sn;
+        cr_cos_sin((float)deg2ang(d), &c, &sn);
         sumdx += c;
-        sumdy += s;
+        sumdy += sn;
         reg_angle = (double)fast_atan2_deg(sumdy, sumdx) * kDegToRad;
       }
     }
@@ -185,12 +304,13 @@ __device__ int region_grow(Frame& F, int sx, int sy, double& reg_angle, double p
   return n;
 }
 
-__device__ void region2rect(Frame& F, int n, double reg_angle, double prec, double p, Rect& rec) {
+__device__ __forceinline__ void region2rect(Frame& F, int n, double reg_angle, double prec, double p, Rect& rec) {
   double x = 0, y = 0, sum = 0;
+#pragma unroll 4
   for (int i = 0; i < n; ++i) {
     const uint32_t pt = reg_get(F, i);
     const int px = (int)(pt & 0xFFFF), py = (int)(pt >> 16);
-    const double weight = modgrad(F, px, py);
+    const double weight = modgrad_q(regq_get(F, i));
     x += double(px) * weight;
     y += double(py) * weight;
     sum += weight;
@@ -199,10 +319,11 @@ __device__ void region2rect(Frame& F, int n, double reg_angle, double prec, doub
   y /= sum;
   // get_theta
   double Ixx = 0.0, Iyy = 0.0, Ixy = 0.0;
+#pragma unroll 4
   for (int i = 0; i < n; ++i) {
     const uint32_t pt = reg_get(F, i);
     const int px = (int)(pt & 0xFFFF), py = (int)(pt >> 16);
-    const double weight = modgrad(F, px, py);
+    const double weight = modgrad_q(regq_get(F, i));
     const double dx = double(px) - x, dy = double(py) - y;
     Ixx += dy * dy * weight;
     Iyy += dx * dx * weight;
@@ -240,7 +361,7 @@ __device__ void region2rect(Frame& F, int n, double reg_angle, double prec, doub
   if (rec.width < 1.0) rec.width = 1.0;
 }
 
-__device__ bool reduce_region_radius(Frame& F, int& n, double reg_angle, double prec, double p,
+__device__ __forceinline__ bool reduce_region_radius(Frame& F, int& n, double reg_angle, double prec, double p,
                                      Rect& rec, double density, double density_th) {
   const uint32_t p0 = reg_get(F, 0);
   const double xc = double((int)(p0 & 0xFFFF)), yc = double((int)(p0 >> 16));
@@ -254,9 +375,7 @@ __device__ bool reduce_region_radius(Frame& F, int& n, double reg_angle, double 
       const int px = (int)(pt & 0xFFFF), py = (int)(pt >> 16);
       if (distSq(xc, yc, double(px), double(py)) > radSq) {
         used_set(F, px, py, false);
-        const uint32_t last = reg_get(F, n - 1);
-        reg_set(F, i, last);
-        reg_set(F, n - 1, pt);
+        reg_swap(F, i, n - 1);
         n--;
         --i;
       }
@@ -268,14 +387,14 @@ __device__ bool reduce_region_radius(Frame& F, int& n, double reg_angle, double 
   return true;
 }
 
-__device__ bool refine(Frame& F, int& n, double reg_angle, double prec, double p, Rect& rec,
+__device__ __forceinline__ bool refine(Frame& F, int& n, double reg_angle, double prec, double p, Rect& rec,
                        double density_th) {
   double density = double(n) / (dist(rec.x1, rec.y1, rec.x2, rec.y2) * rec.width);
   if (density >= density_th) return true;
   const uint32_t p0 = reg_get(F, 0);
   const int x0 = (int)(p0 & 0xFFFF), y0 = (int)(p0 >> 16);
   const double xc = double(x0), yc = double(y0);
-  const double ang_c = deg2ang(F.deg[y0 * F.sw + x0]);
+  const double ang_c = deg2ang(regd_get(F, 0));
   double sum = 0, s_sum = 0;
   int cnt = 0;
   for (int i = 0; i < n; ++i) {
@@ -283,7 +402,7 @@ __device__ bool refine(Frame& F, int& n, double reg_angle, double prec, double p
     const int px = (int)(pt & 0xFFFF), py = (int)(pt >> 16);
     used_set(F, px, py, false);
     if (dist(xc, yc, px, py) < rec.width) {
-      const double ang_d = angle_diff_signed(deg2ang(F.deg[py * F.sw + px]), ang_c);
+      const double ang_d = angle_diff_signed(deg2ang(regd_get(F, i)), ang_c);
       sum += ang_d;
       s_sum += ang_d * ang_d;
       ++cnt;
@@ -294,74 +413,79 @@ __device__ bool refine(Frame& F, int& n, double reg_angle, double prec, double p
       2.0 * sqrt((s_sum - 2.0 * mean_angle * sum) / double(cnt) + mean_angle * mean_angle);
   n = region_grow(F, x0, y0, reg_angle, tau);
   if (n < 2) return false;
+  fill_q(F, n);
   region2rect(F, n, reg_angle, prec, p, rec);
   density = double(n) / (dist(rec.x1, rec.y1, rec.x2, rec.y2) * rec.width);
   if (density < density_th) return reduce_region_radius(F, n, reg_angle, prec, p, rec, density, density_th);
   return true;
 }
 
-struct Edge {
-  int x, y;
-  bool taken;
-};
-
-__device__ double rect_nfa(Frame& F, const Rect& rec) {
+__device__ __forceinline__ double rect_nfa(Frame& F, const Rect& rec_lds) {
+  const Rect rec = rec_lds;
   const double half_width = rec.width / 2.0;
   const double dyhw = rec.dy * half_width;
   const double dxhw = rec.dx * half_width;
-  Edge e[4];
-  e[0] = {int(rec.x1 - dyhw), int(rec.y1 + dxhw), false};
-  e[1] = {int(rec.x2 - dyhw), int(rec.y2 + dxhw), false};
-  e[2] = {int(rec.x2 + dyhw), int(rec.y2 - dxhw), false};
-  e[3] = {int(rec.x1 + dyhw), int(rec.y1 - dxhw), false};
-  // std::sort of 4 elements = insertion sort (AsmallerB_XorYisSmaller)
-  for (int i = 1; i < 4; i++) {
-    const Edge v = e[i];
-    int j = i;
-    while (j > 0 && ((v.x < e[j - 1].x) || (v.x == e[j - 1].x && v.y < e[j - 1].y))) {
-      e[j] = e[j - 1];
-      j--;
+  // corners, sorted by (x, y) (std::sort of 4 = insertion sort; corners
+  // with equal (x, y) are indistinguishable, so a sorting network is exact)
+  int ex0 = int(rec.x1 - dyhw), ey0 = int(rec.y1 + dxhw);
+  int ex1 = int(rec.x2 - dyhw), ey1 = int(rec.y2 + dxhw);
+  int ex2 = int(rec.x2 + dyhw), ey2 = int(rec.y2 - dxhw);
+  int ex3 = int(rec.x1 + dyhw), ey3 = int(rec.y1 - dxhw);
+  auto cswap = [](int& ax, int& ay, int& bx, int& by) {
+    if ((bx < ax) || (bx == ax && by < ay)) {
+      const int tx = ax, ty = ay;
+      ax = bx; ay = by; bx = tx; by = ty;
     }
-    e[j] = v;
-  }
+  };
+  cswap(ex0, ey0, ex1, ey1);
+  cswap(ex2, ey2, ex3, ey3);
+  cswap(ex0, ey0, ex2, ey2);
+  cswap(ex1, ey1, ex3, ey3);
+  cswap(ex1, ey1, ex2, ey2);
+  auto X = [&](int i) { return i == 0 ? ex0 : (i == 1 ? ex1 : (i == 2 ? ex2 : ex3)); };
+  auto Y = [&](int i) { return i == 0 ? ey0 : (i == 1 ? ey1 : (i == 2 ? ey2 : ey3)); };
   int imin = 0, imax = 0;
+#pragma unroll
   for (int i = 1; i < 4; ++i) {
-    if (e[imin].y > e[i].y) imin = i;
-    if (e[imax].y < e[i].y) imax = i;
+    if (Y(imin) > Y(i)) imin = i;
+    if (Y(imax) < Y(i)) imax = i;
   }
-  e[imin].taken = true;
+  unsigned taken = 1u << imin;
   int il = -1;
+#pragma unroll
   for (int i = 0; i < 4; ++i)
-    if (!e[i].taken) {
+    if (!((taken >> i) & 1u)) {
       if (il < 0) il = i;
-      else if (e[il].x > e[i].x) il = i;
+      else if (X(il) > X(i)) il = i;
     }
-  e[il].taken = true;
+  taken |= 1u << il;
   int ir = -1;
+#pragma unroll
   for (int i = 0; i < 4; ++i)
-    if (!e[i].taken) {
+    if (!((taken >> i) & 1u)) {
       if (ir < 0) ir = i;
-      else if (e[ir].x < e[i].x) ir = i;
+      else if (X(ir) < X(i)) ir = i;
     }
-  e[ir].taken = true;
+  taken |= 1u << ir;
   int it = -1;
+#pragma unroll
   for (int i = 0; i < 4; ++i)
-    if (!e[i].taken) {
+    if (!((taken >> i) & 1u)) {
       if (it < 0) it = i;
-      else if (e[it].x > e[i].x) it = i;
+      else if (X(it) > X(i)) it = i;
     }
-  e[it].taken = true;
-  const Edge mn = e[imin], mx = e[imax], lf = e[il], rt = e[ir], tl = e[it];
+  const int mnx = X(imin), mny = Y(imin), mxy = Y(imax);
+  const int lfx = X(il), lfy = Y(il), rtx = X(ir), rty = Y(ir), tlx = X(it), tly = Y(it);
   // double-valued steps, tail corner's y (pinned P13, oracle rect_nfa)
-  const double flstep = (mn.y != lf.y) ? (mn.x - lf.x) / double(mn.y - lf.y) : 0;
-  const double slstep = (lf.y != tl.y) ? (lf.x - tl.x) / double(lf.y - tl.y) : 0;
-  const double frstep = (mn.y != rt.y) ? (mn.x - rt.x) / double(mn.y - rt.y) : 0;
-  const double srstep = (rt.y != tl.y) ? (rt.x - tl.x) / double(rt.y - tl.y) : 0;
+  const double flstep = (mny != lfy) ? (mnx - lfx) / double(mny - lfy) : 0;
+  const double slstep = (lfy != tly) ? (lfx - tlx) / double(lfy - tly) : 0;
+  const double frstep = (mny != rty) ? (mnx - rtx) / double(mny - rty) : 0;
+  const double srstep = (rty != tly) ? (rtx - tlx) / double(rty - tly) : 0;
   double lstep = flstep, rstep = frstep;
-  double left_x = mn.x, right_x = mn.x;
+  double left_x = mnx, right_x = mnx;
   // serial walk: row ranges into LDS (prefix offsets in .w)
   int nrows = 0, total = 0;
-  for (int y = mn.y; y <= mx.y; ++y) {
+  for (int y = mny; y <= mxy; ++y) {
     // rows outside the image skip the step updates too (the reference's
     // `continue` precedes them)
     if (y < 0 || y >= F.sh) continue;
@@ -371,96 +495,84 @@ __device__ double rect_nfa(Frame& F, const Rect& rec) {
       total += xb - xa + 1;
       nrows++;
     }
-    if (y >= lf.y) lstep = slstep;
-    if (y >= rt.y) rstep = srstep;
+    if (y >= lfy) lstep = slstep;
+    if (y >= rty) rstep = srstep;
     left_x += lstep;
     right_x += rstep;
   }
   __builtin_amdgcn_wave_barrier();
-  // parallel count of aligned pixels
+  // parallel count of aligned pixels, 8 loads in flight per lane
   int alg = 0, r = 0;
-  for (int k = F.lane; k < total; k += 64) {
-    while (r + 1 < nrows && F.rows[r + 1].w <= k) r++;
-    const int4 rw = F.rows[r];
-    const int x = rw.y + (k - rw.w);
-    alg += aligned_deg(F.deg[rw.x * F.sw + x], rec.theta, rec.prec) ? 1 : 0;
+  for (int k0 = F.lane; k0 < total; k0 += 64 * 8) {
+    float dv[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int k = k0 + 64 * u;
+      dv[u] = kLsdNotdef;
+      if (k < total) {
+        while (r + 1 < nrows && F.rows[r + 1].w <= k) r++;
+        const int4 rw = F.rows[r];
+        dv[u] = F.deg[rw.x * F.sw + rw.y + (k - rw.w)];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) alg += aligned_deg(dv[u], rec.theta, rec.prec) ? 1 : 0;
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) alg += __shfl_xor(alg, o, 64);
   __builtin_amdgcn_wave_barrier();
-  return nfa(total, alg, rec.p, F.log_nt);
+  return nfa(total, alg, rec.p, F.log_nt, F.lane);
 }
 
-__device__ double rect_improve(Frame& F, Rect& rec) {
+// rect_improve (lsd.cpp): the five refinement phases in order, each trying
+// five variations of a copy of the best rectangle. Both rectangles live in
+// LDS so that the (non-inlined) rect_nfa calls keep few registers live.
+__device__ __forceinline__ double rect_improve(Frame& F, Rect& rec) {
   const double delta = 0.5, delta_2 = delta / 2.0;
+  Rect& r = *F.rect1;
   double log_nfa = rect_nfa(F, rec);
   if (log_nfa > 0) return log_nfa;
-  Rect r = rec;
-  for (int n = 0; n < 5; ++n) {
-    r.p /= 2;
-    r.prec = r.p * kPi;
-    const double v = rect_nfa(F, r);
-    if (v > log_nfa) {
-      log_nfa = v;
-      rec = r;
-    }
-  }
-  if (log_nfa > 0) return log_nfa;
-  r = rec;
-  for (int n = 0; n < 5; ++n) {
-    if ((r.width - delta) >= 0.5) {
-      r.width -= delta;
-      const double v = rect_nfa(F, r);
-      if (v > log_nfa) {
-        rec = r;
-        log_nfa = v;
+  for (int phase = 0; phase < 5; phase++) {
+    r = rec;
+    __builtin_amdgcn_wave_barrier();
+    for (int n = 0; n < 5; ++n) {
+      bool eval = true;
+      if (phase == 0) {
+        r.p /= 2;
+        r.prec = r.p * kPi;
+      } else if ((r.width - delta) >= 0.5) {
+        if (phase == 1) {
+          r.width -= delta;
+        } else if (phase == 2) {
+          r.x1 += -r.dy * delta_2;
+          r.y1 += r.dx * delta_2;
+          r.x2 += -r.dy * delta_2;
+          r.y2 += r.dx * delta_2;
+          r.width -= delta;
+        } else if (phase == 3) {
+          r.x1 -= -r.dy * delta_2;
+          r.y1 -= r.dx * delta_2;
+          r.x2 -= -r.dy * delta_2;
+          r.y2 -= r.dx * delta_2;
+          r.width -= delta;
+        } else {
+          r.p /= 2;
+          r.prec = r.p * kPi;
+        }
+      } else {
+        eval = false;
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (eval) {
+        const double v = rect_nfa(F, r);
+        if (v > log_nfa) {
+          log_nfa = v;
+          rec = r;
+          __builtin_amdgcn_wave_barrier();
+        }
       }
     }
-  }
-  if (log_nfa > 0) return log_nfa;
-  r = rec;
-  for (int n = 0; n < 5; ++n) {
-    if ((r.width - delta) >= 0.5) {
-      r.x1 += -r.dy * delta_2;
-      r.y1 += r.dx * delta_2;
-      r.x2 += -r.dy * delta_2;
-      r.y2 += r.dx * delta_2;
-      r.width -= delta;
-      const double v = rect_nfa(F, r);
-      if (v > log_nfa) {
-        rec = r;
-        log_nfa = v;
-      }
-    }
-  }
-  if (log_nfa > 0) return log_nfa;
-  r = rec;
-  for (int n = 0; n < 5; ++n) {
-    if ((r.width - delta) >= 0.5) {
-      r.x1 -= -r.dy * delta_2;
-      r.y1 -= r.dx * delta_2;
-      r.x2 -= -r.dy * delta_2;
-      r.y2 -= r.dx * delta_2;
-      r.width -= delta;
-      const double v = rect_nfa(F, r);
-      if (v > log_nfa) {
-        rec = r;
-        log_nfa = v;
-      }
-    }
-  }
-  if (log_nfa > 0) return log_nfa;
-  r = rec;
-  for (int n = 0; n < 5; ++n) {
-    if ((r.width - delta) >= 0.5) {
-      r.p /= 2;
-      r.prec = r.p * kPi;
-      const double v = rect_nfa(F, r);
-      if (v > log_nfa) {
-        rec = r;
-        log_nfa = v;
-      }
-    }
+    if (log_nfa > 0) return log_nfa;
   }
   return log_nfa;
 }
@@ -479,11 +591,18 @@ __global__ void __launch_bounds__(64) k_lsd_grow(LsdGeom g, LsdScratch sc) {
   F.q = sc.q + (long long)f * sw * sh;
   F.used = grow_smem;
   F.reg_l = grow_smem + used_words;
-  F.reg_g = sc.reg + (long long)f * sw * sh;
-  F.rows = reinterpret_cast<int4*>(grow_smem + ((used_words + kRegLds + 3) & ~3));
-  F.row_cap = sh + 2;
+  F.regq_l = reinterpret_cast<int*>(F.reg_l + kRegLds);
+  F.regd_l = reinterpret_cast<float*>(F.regq_l + kRegLds);
+  F.ring = F.regd_l + kRegLds;
+  F.reg_g = sc.reg + (long long)f * 3 * sw * sh;
+  F.rows = reinterpret_cast<int4*>(grow_smem + ((used_words + 3 * kRegLds + 64 * 9 + 3) & ~3));
+  F.rect0 = reinterpret_cast<Rect*>(F.rows);
+  F.rect1 = F.rect0 + 1;
+  F.row_cap = 0;
   F.log_nt = g.log_nt;
   F.lane = lane;
+  F.pf_cyc = 0;
+  F.pf_cnt = 0;
   for (int i = lane; i < used_words; i += 64) F.used[i] = 0;
   __builtin_amdgcn_wave_barrier();
   const uint32_t* A = sc.A + (long long)f * g.n;
@@ -491,6 +610,8 @@ __global__ void __launch_bounds__(64) k_lsd_grow(LsdGeom g, LsdScratch sc) {
   const int w1 = sw - 1;
   const double prec = g.prec, p = g.p;
   int nl = 0;
+  long long pc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const long long tstart = clock64();
   for (int base = 0; base < g.n; base += 64) {
     const int i = base + lane;
     int px = 0, py = 0;
@@ -506,36 +627,122 @@ __global__ void __launch_bounds__(64) k_lsd_grow(LsdGeom g, LsdScratch sc) {
       const int l = __ffsll((long long)mask) - 1;
       const int sx = __shfl(px, l, 64), sy = __shfl(py, l, 64);
       double reg_angle;
+      long long t0 = clock64();
       int n = region_grow(F, sx, sy, reg_angle, prec);
+      long long t1 = clock64();
+      pc[0] += t1 - t0;
+      pc[4] += n;
+      pc[5] += 1;
       if (n >= g.min_reg_size) {
-        Rect rec;
+        Rect& rec = *F.rect0;
+        fill_q(F, n);
         region2rect(F, n, reg_angle, prec, p, rec);
-        if (refine(F, n, reg_angle, prec, p, rec, 0.7)) {
-          const double log_nfa = rect_improve(F, rec);
-          if (log_nfa > 0) {
-            if (nl < kLsdMaxLines) {
-              if (lane == 0) {
-                out[nl * 4 + 0] = float((rec.x1 + 0.5) / 0.8);
-                out[nl * 4 + 1] = float((rec.y1 + 0.5) / 0.8);
-                out[nl * 4 + 2] = float((rec.x2 + 0.5) / 0.8);
-                out[nl * 4 + 3] = float((rec.y2 + 0.5) / 0.8);
-              }
-            } else if (lane == 0) {
-              atomicOr(sc.err + f, 8);
-            }
-            nl++;
+        const bool ok = refine(F, n, reg_angle, prec, p, rec, 0.7);
+        pc[1] += clock64() - t1;
+        if (ok) {
+          // NFA validation (rect_improve) does not touch the USED map: it
+          // runs later for all rectangles at once (k_lsd_validate)
+          if (nl < kLsdMaxCand) {
+            const double* rv = reinterpret_cast<const double*>(F.rect0);
+            if (lane < 12) sc.cand[((long long)f * kLsdMaxCand + nl) * 12 + lane] = rv[lane];
+          } else if (lane == 0) {
+            atomicOr(sc.err + f, 8);
           }
+          nl++;
         }
       }
       mask = __ballot(def && lane > l && !used_get(F, px, py));
     }
   }
-  if (lane == 0) sc.nlines[f] = min(nl, kLsdMaxLines);
+  if (lane == 0) sc.ncand[f] = min(nl, kLsdMaxCand);
+  if (sc.prof && lane == 0) {
+    pc[3] = clock64() - tstart;
+    pc[7] = nl;
+    pc[6] = F.pf_cyc;
+    pc[5] = F.pf_cnt;
+    for (int k = 0; k < 8; k++) sc.prof[f * 8 + k] = pc[k];
+  }
+}
+
+// NFA validation of every refined rectangle (rect_improve), one wave per
+// rectangle, 4 waves per block; the accepted segments are compacted in seed
+// order by k_lsd_compact.
+constexpr int kValBlocks = 32;
+
+__global__ void __launch_bounds__(256) k_lsd_validate(LsdGeom g, LsdScratch sc) {
+  extern __shared__ uint32_t val_smem[];
+  const int f = blockIdx.y, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int sh = g.sh;
+  const size_t per_wave = (size_t)4 * (sh + 2) + (2 * sizeof(Rect)) / 4;
+  uint32_t* base = val_smem + wave * per_wave;
+  Frame F{};
+  F.sw = g.sw;
+  F.sh = sh;
+  F.deg = sc.deg + (long long)f * g.sw * sh;
+  F.rows = reinterpret_cast<int4*>(base);
+  F.rect0 = reinterpret_cast<Rect*>(F.rows + (sh + 2));
+  F.rect1 = F.rect0 + 1;
+  F.row_cap = sh + 2;
+  F.log_nt = g.log_nt;
+  F.lane = lane;
+  const int nc = sc.ncand[f];
+  for (int c = blockIdx.x * 4 + wave; c < nc; c += kValBlocks * 4) {
+    const long long o = (long long)f * kLsdMaxCand + c;
+    double* rv = reinterpret_cast<double*>(F.rect0);
+    if (lane < 12) rv[lane] = sc.cand[o * 12 + lane];
+    __builtin_amdgcn_wave_barrier();
+    Rect& rec = *F.rect0;
+    const double log_nfa = rect_improve(F, rec);
+    if (lane == 0) {
+      const bool ok = log_nfa > 0;
+      sc.cand_ok[o] = ok;
+      if (ok) {
+        sc.cand_line[o * 4 + 0] = float((rec.x1 + 0.5) / 0.8);
+        sc.cand_line[o * 4 + 1] = float((rec.y1 + 0.5) / 0.8);
+        sc.cand_line[o * 4 + 2] = float((rec.x2 + 0.5) / 0.8);
+        sc.cand_line[o * 4 + 3] = float((rec.y2 + 0.5) / 0.8);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+__global__ void __launch_bounds__(64) k_lsd_compact(LsdScratch sc) {
+  const int f = blockIdx.x, lane = threadIdx.x;
+  const int nc = sc.ncand[f];
+  float* out = sc.lines + (long long)f * kLsdMaxLines * 4;
+  int nl = 0;
+  for (int b = 0; b < nc; b += 64) {
+    const int c = b + lane;
+    const long long o = (long long)f * kLsdMaxCand + c;
+    const bool ok = c < nc && sc.cand_ok[o];
+    const unsigned long long m = __ballot(ok);
+    const int pos = nl + __popcll(m & ((1ull << lane) - 1ull));
+    if (ok && pos < kLsdMaxLines) {
+      const float4 v = *reinterpret_cast<const float4*>(sc.cand_line + o * 4);
+      *reinterpret_cast<float4*>(out + pos * 4) = v;
+    }
+    nl += __popcll(m);
+  }
+  if (lane == 0) {
+    sc.nlines[f] = min(nl, kLsdMaxLines);
+    if (nl > kLsdMaxLines) atomicOr(sc.err + f, 8);
+  }
+}
+
+void launch_lsd_validate(const LsdGeom& g, const LsdScratch& sc, int batch, hipStream_t s) {
+  const size_t per_wave = (size_t)4 * (g.sh + 2) * 4 + 2 * sizeof(Rect);
+  const size_t smem = 4 * per_wave;
+  if (smem > 65536)
+    (void)hipFuncSetAttribute((const void*)k_lsd_validate,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  hipLaunchKernelGGL(k_lsd_validate, dim3(kValBlocks, batch), dim3(256), smem, s, g, sc);
+  hipLaunchKernelGGL(k_lsd_compact, dim3(batch), dim3(64), 0, s, sc);
 }
 
 size_t lsd_grow_smem(const LsdGeom& g) {
   const int used_words = (g.sw * g.sh + 31) / 32;
-  return 4 * (size_t)(((used_words + kRegLds + 3) & ~3) + 4 * (g.sh + 2));
+  return 4 * (size_t)(((used_words + 3 * kRegLds + 64 * 9 + 3) & ~3)) + 2 * sizeof(Rect);
 }
 
 void launch_lsd_grow(const LsdGeom& g, const LsdScratch& sc, int batch, hipStream_t s) {

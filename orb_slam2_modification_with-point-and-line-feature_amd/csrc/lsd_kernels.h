@@ -9,6 +9,7 @@
 namespace orbpl {
 
 constexpr int kLsdMaxLines = 4096;    // raw LSD segments kept per frame
+constexpr int kLsdMaxCand = 4096;     // refined rectangles awaiting NFA validation per frame
 constexpr int kLineKeep = 80;         // LineExtractor.cpp:24
 constexpr int kLsdSortChunk = 256;    // elements per partition chunk
 constexpr float kLsdNotdef = -1.0f;   // NOTDEF marker in the degree map
@@ -47,10 +48,15 @@ struct LsdScratch {
   int* seg_i;          // 8 * seg_cap: pivot, choff, nL, nR, K, cut, nch, -
   int* chunk_i;        // 4 * chunk_cap: Lc, Rc, Lpre, Rsuf
   int2* leaves;        // leaf_cap
-  uint32_t* reg;       // sw*sh region point list (x | y << 16)
+  uint32_t* reg;       // 3*sw*sh region overflow (point, q, degrees)
   float* lines;        // kLsdMaxLines * 4
   int* nlines;         // 1 per frame
   int* err;            // 1 per frame: capacity overflow flags
+  long long* prof;     // optional: 8 cycle counters per frame (phase profile)
+  double* cand;        // kLsdMaxCand * 12 per frame: refined rectangles, seed order
+  int* ncand;          // 1 per frame
+  float* cand_line;    // kLsdMaxCand * 4 per frame: validated segment
+  int* cand_ok;        // kLsdMaxCand per frame: log_nfa > log_eps
 };
 
 void launch_lsd_blur(const LsdGeom& g, const uint8_t* img, int stride, long long frame_pitch,
@@ -63,5 +69,6 @@ void launch_lsd_sort(const LsdGeom& g, const LsdScratch& sc, int batch, hipStrea
 void launch_lsd_sort_keys(int n, const int* keys, const LsdScratch& sc, hipStream_t s);
 void launch_lsd_grow(const LsdGeom& g, const LsdScratch& sc, int batch, hipStream_t s);
 size_t lsd_grow_smem(const LsdGeom& g);
+void launch_lsd_validate(const LsdGeom& g, const LsdScratch& sc, int batch, hipStream_t s);
 
 }  // namespace orbpl

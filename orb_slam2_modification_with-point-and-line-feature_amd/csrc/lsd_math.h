@@ -257,6 +257,18 @@ LSDM_HD double sin_(double x) {
   }
 }
 
+LSDM_HD void sincos_(double x, double* s, double* c) {
+  double a, b;
+  const int n = rem_pio2_(x, &a, &b);
+  const double ks = ksin_(a, b), kc = kcos_(a, b);
+  switch (n & 3) {
+    case 0: *s = ks; *c = kc; break;
+    case 1: *s = kc; *c = -ks; break;
+    case 2: *s = -ks; *c = -kc; break;
+    default: *s = -kc; *c = ks; break;
+  }
+}
+
 LSDM_HD double cos_(double x) {
   double a, b;
   const int n = rem_pio2_(x, &a, &b);

@@ -179,10 +179,15 @@ int lsdx_create(int width, int height, int max_batch, int device, lsdx_ctx** out
   LA(s.seg_i, B * 8 * g.seg_cap * 4);
   LA(s.chunk_i, B * 4 * g.chunk_cap * 4);
   LA(s.leaves, B * g.leaf_cap * sizeof(int2));
-  LA(s.reg, B * px * 4);
+  LA(s.reg, B * px * 3 * 4);
   LA(s.lines, B * kLsdMaxLines * 4 * 4);
   LA(s.nlines, B * 4);
   LA(s.err, B * 4);
+  LA(s.prof, B * 8 * 8);
+  LA(s.cand, B * kLsdMaxCand * 12 * 8);
+  LA(s.ncand, B * 4);
+  LA(s.cand_line, B * kLsdMaxCand * 4 * 4);
+  LA(s.cand_ok, B * kLsdMaxCand * 4);
   LA(c->d_tabs, (size_t)(2 * g.sw + 2 * g.sh) * 4);
 #undef LA
   std::vector<int> tabs(2 * g.sw + 2 * g.sh);
@@ -211,6 +216,7 @@ int lsdx_detect_batch_device(lsdx_ctx* c, const uint8_t* d_imgs, int batch, int 
   launch_lsd_grad(g, c->sc.scaled, c->sc.deg, c->sc.q, c->sc.maxq, batch, s);
   launch_lsd_sort(g, c->sc, batch, s);
   launch_lsd_grow(g, c->sc, batch, s);
+  launch_lsd_validate(g, c->sc, batch, s);
   HIP_CHECK(hipGetLastError());
   c->last_batch = batch;
   return ORBPL_OK;
@@ -282,6 +288,22 @@ int lsdx_get_stages(lsdx_ctx* c, int frame, uint8_t* scaled, float* deg, uint32_
       const int idx = (int)(a[i] & 0x3FFFFFu);
       order[i] = (uint32_t)(idx % w1) | ((uint32_t)(idx / w1) << 16);
     }
+  }
+  return ORBPL_OK;
+}
+
+// Debug: per-frame phase cycle counters of the seed loop (grow, fit+refine,
+// rect_improve, total, region pixels, regions, candidate regions, lines).
+int lsdx_debug_profile(lsdx_ctx* c, long long* out8) {
+  if (!c || !out8 || c->last_batch <= 0) return arg_fail("bad argument");
+  int rc = lsdx_synchronize(c);
+  if (rc) return rc;
+  std::vector<long long> p((size_t)c->last_batch * 8);
+  HIP_CHECK(hipMemcpy(p.data(), c->sc.prof, p.size() * 8, hipMemcpyDeviceToHost));
+  for (int k = 0; k < 8; k++) {
+    long long s = 0;
+    for (int f = 0; f < c->last_batch; f++) s += p[(size_t)f * 8 + k];
+    out8[k] = s / c->last_batch;
   }
   return ORBPL_OK;
 }
