@@ -298,6 +298,21 @@ int lsdx_detect(lsdx_ctx* ctx, const uint8_t* img, int width, int height, int st
 int lsdx_detect_batch_device(lsdx_ctx* ctx, const uint8_t* d_imgs, int batch, int stride,
                              int64_t frame_pitch);
 int lsdx_synchronize(lsdx_ctx* ctx);
+/* LineExtractor::ExtractLineSegment(img, key_lines, line_descriptor,
+ * keyline_coefficients) (LineExtractor.cpp:12-74): LSD, KeyLines sorted by
+ * response and cut to the 80 longest when more were found, LBD descriptors
+ * (32 bytes per row, rows follow the KeyLine order), normalised homogeneous
+ * line coefficients (3 doubles per line). */
+int lsdx_extract(lsdx_ctx* ctx, const uint8_t* img, int width, int height, int stride,
+                 orbpl_keyline* keylines, uint8_t* desc, double* coef, int cap, int* n_out);
+int lsdx_extract_batch_device(lsdx_ctx* ctx, const uint8_t* d_imgs, int batch, int stride,
+                              int64_t frame_pitch);
+int lsdx_get_keylines(lsdx_ctx* ctx, int frame, orbpl_keyline* keylines, uint8_t* desc,
+                      double* coef, int cap, int* n_out);
+/* Device buffers of the last extraction: frame f's lines start at
+ * f*80 KeyLines / f*80*32 bytes / f*80*3 doubles; d_n[f] is the count. */
+int lsdx_device_outputs(lsdx_ctx* ctx, orbpl_keyline** d_keylines, uint8_t** d_desc,
+                        double** d_coef, int32_t** d_n);
 int lsdx_get_lines(lsdx_ctx* ctx, int frame, float* lines, int cap, int* n_out);
 /* Intermediate stages of the last run (parity tests): 0.8-scaled 8-bit image
  * (sw*sh), fastAtan2 degrees per pixel (-1 = NOTDEF), pseudo-ordered pixels

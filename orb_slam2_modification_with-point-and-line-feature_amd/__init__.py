@@ -535,6 +535,10 @@ def _declare(L):  # noqa: F811
     L.lsdx_get_stages.argtypes = [vp, i, vp, vp, vp, ip, ip, ip]
     L.orbpl_test_introsort.argtypes = [vp, i, vp]
     L.lsdx_debug_profile.argtypes = [vp, vp]
+    L.lsdx_extract.argtypes = [vp, vp, i, i, i, vp, vp, vp, i, ip]
+    L.lsdx_extract_batch_device.argtypes = [vp, vp, i, i, C.c_int64]
+    L.lsdx_get_keylines.argtypes = [vp, i, vp, vp, vp, i, ip]
+    L.lsdx_device_outputs.argtypes = [vp, vp, vp, vp, vp]
 
 
 class LineSegmentDetector:
@@ -605,3 +609,37 @@ def test_introsort(keys):
     perm = np.zeros(len(k), np.int32)
     check(lib().orbpl_test_introsort(_ptr(k), len(k), _ptr(perm)), "orbpl_test_introsort")
     return perm
+
+
+class LineExtractor(LineSegmentDetector):
+    """ORB_SLAM2::LineExtractor (include/LineExtractor.h:21-56):
+    ExtractLineSegment(img) -> (key_lines, line_descriptor, keyline_coefficients)
+    with scale = 1, num_octaves = 1 as Frame::ExtractLine calls it (Frame.cc:326-328)."""
+
+    def ExtractLineSegment(self, img):
+        img = np.ascontiguousarray(img, np.uint8)
+        h, w = img.shape
+        kl = np.zeros(80, KEYLINE_DTYPE)
+        desc = np.zeros((80, 32), np.uint8)
+        coef = np.zeros((80, 3), np.float64)
+        n = C.c_int(0)
+        check(lib().lsdx_extract(self._h, _ptr(img), w, h, w, _ptr(kl), _ptr(desc), _ptr(coef), 80,
+                                 C.byref(n)), "lsdx_extract")
+        k = n.value
+        return kl[:k].copy(), desc[:k].copy(), coef[:k].copy()
+
+    def extract_batch_device(self, d_imgs, batch, stride=None, frame_pitch=None):
+        stride = self.W if stride is None else stride
+        frame_pitch = self.W * self.H if frame_pitch is None else frame_pitch
+        check(lib().lsdx_extract_batch_device(self._h, C.c_void_p(d_imgs), batch, stride,
+                                              frame_pitch), "lsdx_extract_batch_device")
+
+    def keylines(self, frame):
+        kl = np.zeros(80, KEYLINE_DTYPE)
+        desc = np.zeros((80, 32), np.uint8)
+        coef = np.zeros((80, 3), np.float64)
+        n = C.c_int(0)
+        check(lib().lsdx_get_keylines(self._h, frame, _ptr(kl), _ptr(desc), _ptr(coef), 80,
+                                      C.byref(n)), "lsdx_get_keylines")
+        k = n.value
+        return kl[:k].copy(), desc[:k].copy(), coef[:k].copy()

@@ -59,6 +59,29 @@ struct LsdScratch {
   int* cand_ok;        // kLsdMaxCand per frame: log_nfa > log_eps
 };
 
+// Outputs of LineExtractor::ExtractLineSegment per frame.
+struct LineOut {
+  orbpl_keyline* kl_all;  // kLsdMaxLines per frame: every detected KeyLine
+  orbpl_keyline* kl;      // kLineKeep per frame: the kept KeyLines, sorted
+  uint8_t* desc;          // kLineKeep * 32 per frame: LBD rows
+  double* coef;           // kLineKeep * 3 per frame
+  int* n;                 // kept count per frame
+};
+
+// BinaryDescriptor's local (F_l, 3 bands x 7) and global (F_g, 63 rows)
+// Gaussian weights, as the floats computeLBD multiplies with.
+struct LbdWeights {
+  float gL[21];
+  float gG[63];
+};
+
+void launch_keylines(const LsdGeom& g, const LsdScratch& sc, const LineOut& o, int batch,
+                     hipStream_t s);
+void launch_sobel(int W, int H, const uint8_t* blur5, int16_t* dx, int16_t* dy, int batch,
+                  hipStream_t s);
+void launch_lbd(int W, int H, const int16_t* dx, const int16_t* dy, const LbdWeights& w,
+                const LineOut& o, int batch, hipStream_t s);
+
 void launch_lsd_blur(const LsdGeom& g, const uint8_t* img, int stride, long long frame_pitch,
                      uint8_t* out, int batch, hipStream_t s);
 void launch_lsd_resize(const LsdGeom& g, const int* tabs, const uint8_t* blur, uint8_t* scaled,

@@ -75,7 +75,13 @@ void lin_tab(double inv_scale, int ssize, int dsize, int* ofs, int* c1, int* mn,
 struct lsdx_ctx {
   int device = 0, max_batch = 0, W = 0, H = 0;
   LsdGeom g{};
+  LsdGeom g5{};          // the same geometry with BinaryDescriptor's 5x5 sigma 1 blur
   LsdScratch sc{};
+  LineOut lo{};
+  LbdWeights lw{};
+  uint8_t* blur5 = nullptr;
+  int16_t* sdx = nullptr;
+  int16_t* sdy = nullptr;
   hipStream_t stream = nullptr;
   int* d_tabs = nullptr;
   uint8_t* d_in = nullptr;
@@ -189,7 +195,30 @@ int lsdx_create(int width, int height, int max_batch, int device, lsdx_ctx** out
   LA(s.cand_line, B * kLsdMaxCand * 4 * 4);
   LA(s.cand_ok, B * kLsdMaxCand * 4);
   LA(c->d_tabs, (size_t)(2 * g.sw + 2 * g.sh) * 4);
+  LA(c->blur5, B * width * height);
+  LA(c->sdx, B * width * height * 2);
+  LA(c->sdy, B * width * height * 2);
+  LA(c->lo.kl_all, B * kLsdMaxLines * sizeof(orbpl_keyline));
+  LA(c->lo.kl, B * kLineKeep * sizeof(orbpl_keyline));
+  LA(c->lo.desc, B * kLineKeep * 32);
+  LA(c->lo.coef, B * kLineKeep * 3 * 8);
+  LA(c->lo.n, B * 4);
 #undef LA
+  c->g5 = c->g;
+  c->g5.ksize = 5;
+  gauss_kernel_fixed(5, 1.0, c->g5.gk);
+  // BinaryDescriptor::BinaryDescriptor: F_l (3 bands of width 7) and F_g (63
+  // rows) Gaussian weights, integer centre / sigma, cast to float in use
+  {
+    double u = (7 * 3 - 1) / 2;
+    double sigma = (7 * 2 + 1) / 2;
+    double inv = -1 / (2 * sigma * sigma);
+    for (int i = 0; i < 21; i++) c->lw.gL[i] = (float)lsdm::exp_((i - u) * (i - u) * inv);
+    u = (9 * 7 - 1) / 2;
+    sigma = u;
+    inv = -1 / (2 * sigma * sigma);
+    for (int i = 0; i < 63; i++) c->lw.gG[i] = (float)lsdm::exp_((i - u) * (i - u) * inv);
+  }
   std::vector<int> tabs(2 * g.sw + 2 * g.sh);
   lin_tab(0.8, width, g.sw, tabs.data(), tabs.data() + g.sw, &c->g.rx0, &c->g.rx1);
   lin_tab(0.8, height, g.sh, tabs.data() + 2 * g.sw, tabs.data() + 2 * g.sw + g.sh, &c->g.ry0,
@@ -219,6 +248,62 @@ int lsdx_detect_batch_device(lsdx_ctx* c, const uint8_t* d_imgs, int batch, int 
   launch_lsd_validate(g, c->sc, batch, s);
   HIP_CHECK(hipGetLastError());
   c->last_batch = batch;
+  return ORBPL_OK;
+}
+
+int lsdx_extract_batch_device(lsdx_ctx* c, const uint8_t* d_imgs, int batch, int stride,
+                              int64_t frame_pitch) {
+  int rc = lsdx_detect_batch_device(c, d_imgs, batch, stride, frame_pitch);
+  if (rc) return rc;
+  hipStream_t s = c->stream;
+  launch_keylines(c->g, c->sc, c->lo, batch, s);
+  launch_lsd_blur(c->g5, d_imgs, stride, frame_pitch, c->blur5, batch, s);
+  launch_sobel(c->W, c->H, c->blur5, c->sdx, c->sdy, batch, s);
+  launch_lbd(c->W, c->H, c->sdx, c->sdy, c->lw, c->lo, batch, s);
+  HIP_CHECK(hipGetLastError());
+  return ORBPL_OK;
+}
+
+int lsdx_get_keylines(lsdx_ctx* c, int frame, orbpl_keyline* kl, uint8_t* desc, double* coef,
+                      int cap, int* n_out) {
+  if (!c || !n_out || frame < 0 || frame >= c->last_batch) return arg_fail("bad argument");
+  int rc = lsdx_synchronize(c);
+  if (rc) return rc;
+  int n = 0;
+  HIP_CHECK(hipMemcpy(&n, c->lo.n + frame, 4, hipMemcpyDeviceToHost));
+  *n_out = n;
+  if (n > cap) {
+    arg_fail("keyline buffer too small");
+    return ORBPL_ERR_CAPACITY;
+  }
+  const size_t o = (size_t)frame * kLineKeep;
+  if (n > 0) {
+    if (kl) HIP_CHECK(hipMemcpy(kl, c->lo.kl + o, n * sizeof(orbpl_keyline), hipMemcpyDeviceToHost));
+    if (desc) HIP_CHECK(hipMemcpy(desc, c->lo.desc + o * 32, (size_t)n * 32, hipMemcpyDeviceToHost));
+    if (coef) HIP_CHECK(hipMemcpy(coef, c->lo.coef + o * 3, (size_t)n * 24, hipMemcpyDeviceToHost));
+  }
+  return ORBPL_OK;
+}
+
+int lsdx_extract(lsdx_ctx* c, const uint8_t* img, int width, int height, int stride,
+                 orbpl_keyline* kl, uint8_t* desc, double* coef, int cap, int* n_out) {
+  if (!c || !img || !n_out) return arg_fail("NULL argument");
+  if (width != c->W || height != c->H) return arg_fail("image size differs from the context");
+  HIP_CHECK(hipSetDevice(c->device));
+  HIP_CHECK(hipMemcpy2DAsync(c->d_in, width, img, stride, width, height, hipMemcpyHostToDevice,
+                             c->stream));
+  int rc = lsdx_extract_batch_device(c, c->d_in, 1, width, (int64_t)width * height);
+  if (rc) return rc;
+  return lsdx_get_keylines(c, 0, kl, desc, coef, cap, n_out);
+}
+
+int lsdx_device_outputs(lsdx_ctx* c, orbpl_keyline** d_kl, uint8_t** d_desc, double** d_coef,
+                        int** d_n) {
+  if (!c) return arg_fail("NULL context");
+  if (d_kl) *d_kl = c->lo.kl;
+  if (d_desc) *d_desc = c->lo.desc;
+  if (d_coef) *d_coef = c->lo.coef;
+  if (d_n) *d_n = c->lo.n;
   return ORBPL_OK;
 }
 

@@ -74,3 +74,43 @@ def test_lsd_kitti_geometry(orbpl, oracle):
     g = fr[0][0]
     det = orbpl.LineSegmentDetector(1241, 376)
     assert np.array_equal(det.detect(g), oracle.lsd_detect(g))
+
+
+def _cmp_keylines(kl, desc, coef, kl_o, desc_o, coef_o):
+    assert len(kl) == len(kl_o)
+    for name in kl.dtype.names:
+        assert np.array_equal(kl[name], kl_o[name]), name
+    assert np.array_equal(desc, desc_o)
+    assert np.array_equal(coef, coef_o)
+
+
+def test_line_extract_bit_exact(orbpl, oracle, frames):
+    ex = orbpl.LineExtractor(640, 480)
+    for g in frames:
+        kl, desc, coef = ex.ExtractLineSegment(g)
+        kl_o, desc_o, coef_o, nd = oracle.line_extract(g)
+        assert nd > 80 and len(kl) == 80
+        _cmp_keylines(kl, desc, coef, kl_o, desc_o, coef_o)
+
+
+def test_line_extract_batch_and_few_lines(orbpl, oracle, frames):
+    # a frame with fewer than 80 segments keeps detection order (no sort)
+    few = np.full((480, 640), 60, np.uint8)
+    few[100:300, 200:400] = 180
+    imgs = np.stack(frames + [few])
+    ex = orbpl.LineExtractor(640, 480, max_batch=len(imgs))
+    buf = orbpl.DeviceBuffer.from_array(imgs)
+    ex.extract_batch_device(buf.ptr, len(imgs))
+    ex.synchronize()
+    for f, g in enumerate(imgs):
+        kl_o, desc_o, coef_o, nd = oracle.line_extract(g)
+        _cmp_keylines(*ex.keylines(f), kl_o, desc_o, coef_o)
+    assert 0 < len(ex.keylines(len(imgs) - 1)[0]) < 80
+
+
+def test_line_extract_kitti(orbpl, oracle):
+    cfg, traj, fr = sequence(1, 5, cam_name="KITTI00", width=1241, height=376)
+    g = fr[0][0]
+    ex = orbpl.LineExtractor(1241, 376)
+    kl_o, desc_o, coef_o, nd = oracle.line_extract(g)
+    _cmp_keylines(*ex.ExtractLineSegment(g), kl_o, desc_o, coef_o)
