@@ -243,6 +243,14 @@ typedef struct orbpl_tracker orbpl_tracker;
 
 int orbpl_tracker_create(const orbpl_orb_params* orb, const orbpl_camera* cam, int n_streams,
                          int device, orbpl_tracker** out);
+/* Tracker flags. ORBPL_TRACK_LINES: the point-and-line variant of the
+ * reference's RGB-D tracking (Tracking.cc:1210-1320 with mbUseLines):
+ * LineExtractor per frame (lsdx_*), UndistortKeyLines + line depths,
+ * LineMatcher::SearchByProjection against the last frame's map lines,
+ * PoseOptimization with line edges, line outlier discard and map lines. */
+#define ORBPL_TRACK_LINES 1
+int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam, int n_streams,
+                            int device, int flags, orbpl_tracker** out);
 int orbpl_tracker_destroy(orbpl_tracker* tr);
 /* Forget all stream state; the next step initialises every stream with pose
  * Tcw0 (n_streams x 16 floats row-major, NULL = identity). */
@@ -273,6 +281,20 @@ int orbpl_tracker_timings_reset(orbpl_tracker* tr);
 int orbpl_tracker_kp_capacity(const orbpl_tracker* tr);
 int orbpl_tracker_get_frame(orbpl_tracker* tr, int stream, orbpl_keypoint* kps_un, uint8_t* desc,
                             int32_t* match, uint8_t* outlier, int* n);
+/* Tracking outcome of the last step per stream: ok (TrackWithMotionModel's
+ * return), lines of the frame, LineMatcher matches (every passing pair
+ * counts, as in the reference), line map matches after outlier discard
+ * (outliers decrement, Tracking.cc:1306). Line counts are 0 without lines. */
+int orbpl_tracker_get_status(orbpl_tracker* tr, int* ok, int* nlines, int* line_matches,
+                             int* line_nmatches_map);
+/* Line outputs of the last step (kLineKeep = 80 entries per stream):
+ * undistorted KeyLines, LBD rows, matched last-frame line (-1 none), outlier
+ * flags. ORBPL_TRACK_LINES trackers only. */
+int orbpl_tracker_get_lines(orbpl_tracker* tr, int stream, orbpl_keyline* kl_un, uint8_t* desc,
+                            int32_t* lmatch, uint8_t* loutlier, int* n);
+/* Line stage device times (ms) of the last min(max_steps, 64) steps, 3 per
+ * step: LSD, KeyLines + LBD + UndistortKeyLines, line SearchByProjection. */
+int orbpl_tracker_line_timings(orbpl_tracker* tr, int max_steps, float* ms, int* n_steps);
 
 /* ------------------------------------------------------------------------
  * Hamming distance — ORBmatcher::DescriptorDistance (ORBmatcher.cc:2083-2103)

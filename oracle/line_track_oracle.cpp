@@ -1,0 +1,537 @@
+// ============================================================================
+// ORACLE — TEST INFRASTRUCTURE ONLY. NOT PART OF THE PRODUCT PATH.
+//
+// CPU restatement of the reference's per-frame line tracking:
+//   Frame::UndistortKeyLines            /root/reference/src/Frame.cc:769-845
+//   Frame::ComputeStereoFromRGBD (lines) Frame.cc:1090-1116
+//   LineMatcher::SearchByProjection(Frame&, const Frame&)  LineMatcher.cpp:72-269
+//     LiangBarsky :1389-1460, LineMatching :1463-1504, LineOverLap :1508-1559,
+//     ReprojectionError :1579-1596, UpdateKeyLineData :1601-1624,
+//     DescriptorDistance :20-39, thresholds LineMatcher.h:94-98
+//   Frame::UnprojectStereoLineStart/End  Frame.cc:1176-1204 (the end point uses
+//     mvDepthLineStart, as the reference does)
+// Pinned semantics as in lsd_oracle.cpp (P2, P10-P12) plus:
+//   P14 depth lookups imDepth.at<float>(int(v), int(u)) read the row-major
+//       buffer at v*W + u; an index outside [0, W*H) reads as no depth.
+// ============================================================================
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "../orb_slam2_modification_with-point-and-line-feature_amd/csrc/lsd_math.h"
+#include "oracle_api.h"
+
+namespace line_track {
+
+static int popcnt_dist(const uint8_t* a, const uint8_t* b) {
+  int d = 0;
+  for (int i = 0; i < 32; i++) d += __builtin_popcount((unsigned)(a[i] ^ b[i]));
+  return d;
+}
+
+static float atan2f_pinned(float y, float x) { return (float)lsdm::atan2_((double)y, (double)x); }
+
+// fields recomputed from the end points (UpdateKeyLineData / UndistortKeyLines)
+static void refresh_keyline(orbpl_keyline& kl, int W, int H) {
+  kl.pt_x = (kl.endPointX + kl.startPointX) / 2;
+  kl.pt_y = (kl.endPointY + kl.startPointY) / 2;
+  const double dx = (double)(kl.startPointX - kl.endPointX), dy = (double)(kl.startPointY - kl.endPointY);
+  kl.lineLength = float(std::sqrt(dx * dx + dy * dy));
+  kl.numOfPixels = oracle_line_iterator_count(W, H, kl.startPointX, kl.startPointY, kl.endPointX,
+                                              kl.endPointY);
+  kl.angle = atan2f_pinned(kl.endPointY - kl.startPointY, kl.endPointX - kl.startPointX);
+  kl.size = (kl.endPointX - kl.startPointX) * (kl.endPointY - kl.startPointY);
+  kl.response = kl.lineLength / (float)std::max(W, H);
+}
+
+static bool liang_barsky(const double line[4], double out[4], const float bounds[4]) {
+  const double sx = line[0], sy = line[1], ex = line[2], ey = line[3];
+  double p[4], q[4];
+  p[0] = sx - ex;
+  p[1] = ex - sx;
+  p[2] = sy - ey;
+  p[3] = ey - sy;
+  q[0] = sx - bounds[0];
+  q[1] = bounds[2] - sx;
+  q[2] = sy - bounds[1];
+  q[3] = bounds[3] - sy;
+  if (p[0] == 0) {
+    if (q[0] <= 0 || q[2] <= 0) return false;
+  }
+  if (p[2] == 0) {
+    if (q[2] >= 0 || q[3] >= 0) return false;
+  }
+  double u[4];
+  for (int i = 0; i < 4; i++) u[i] = q[i] / p[i];
+  double u_min = 0, u_max = 1;
+  for (int i = 0; i < 4; i++) {
+    if (p[i] < 0) {
+      if (u_min < u[i]) u_min = u[i];
+    } else {
+      if (u_max > u[i]) u_max = u[i];
+    }
+  }
+  if (u_max >= u_min) {
+    out[0] = sx + std::round(u_min * (ex - sx));
+    out[1] = sy + std::round(u_min * (ey - sy));
+    out[2] = sx + std::round(u_max * (ex - sx));
+    out[3] = sy + std::round(u_max * (ey - sy));
+    return true;
+  }
+  return false;
+}
+
+static bool line_overlap(const orbpl_keyline& a, const orbpl_keyline& b, double th) {
+  const double d1_x = std::abs(a.startPointX - a.endPointX);
+  const double d2_x = std::abs(b.startPointX - b.endPointX);
+  const double min_x = std::min(std::min(a.startPointX, a.endPointX), std::min(b.startPointX, b.endPointX));
+  const double max_x = std::max(std::max(a.startPointX, a.endPointX), std::max(b.startPointX, b.endPointX));
+  const double d1_y = std::abs(a.startPointY - a.endPointY);
+  const double d2_y = std::abs(b.startPointY - b.endPointY);
+  const double min_y = std::min(std::min(a.startPointY, a.endPointY), std::min(b.startPointY, b.endPointY));
+  const double max_y = std::max(std::max(a.startPointY, a.endPointY), std::max(b.startPointY, b.endPointY));
+  if (d1_x == 0 || d2_x == 0) {
+    if ((d1_y + d2_y - max_y + min_y) / std::min(d1_y, d2_y) >= th) return true;
+  }
+  if (d1_y == 0 || d2_y == 0) {
+    if ((d1_x + d2_x - max_x + min_x) / std::min(d1_x, d2_x) >= th) return true;
+  }
+  if ((d1_x + d2_x - max_x + min_x) / std::min(d1_x, d2_x) >= th) {
+    if (d1_y + d2_y + min_y >= max_y) return true;
+    if (max_y - min_y - d1_y - d2_y < 0.3 * std::min(d1_y, d2_y)) return true;
+  } else if ((d1_x + d2_x - max_x + min_x) / std::min(d1_x, d2_x) < th &&
+             (max_x - min_x - d1_x - d2_x) < 0.3 * std::min(d1_x, d2_x)) {
+    if ((d1_y + d2_y - max_y + min_y) / std::min(d1_y, d2_y) >= th) return true;
+  }
+  return false;
+}
+
+static double reprojection_error(const orbpl_keyline& l1, const orbpl_keyline& l2) {
+  const double s1[3] = {l1.startPointX, l1.startPointY, 1}, e1[3] = {l1.endPointX, l1.endPointY, 1};
+  const double c0 = s1[1] * e1[2] - s1[2] * e1[1];
+  const double c1 = s1[2] * e1[0] - s1[0] * e1[2];
+  const double c2 = s1[0] * e1[1] - s1[1] * e1[0];
+  const double nrm = std::sqrt(c0 * c0 + c1 * c1);
+  const double ds = (l2.startPointX * c0 + l2.startPointY * c1 + 1.0 * c2) / nrm;
+  const double de = (l2.endPointX * c0 + l2.endPointY * c1 + 1.0 * c2) / nrm;
+  return std::sqrt(ds * ds + de * de);
+}
+
+static bool line_matching(const orbpl_keyline& k1, const orbpl_keyline& k2, const uint8_t* d1,
+                          const uint8_t* d2, const double off[5]) {
+  const double kPi = 3.14159265358979323846;
+  if (popcnt_dist(d1, d2) > 45 + off[3]) return false;
+  if (std::abs(k1.angle - k2.angle) > 15.0 * kPi / 180.0 + off[0] * kPi / 180.0) return false;
+  if (std::min(k1.lineLength, k2.lineLength) / std::max(k1.lineLength, k2.lineLength) < 0.45 + off[1])
+    return false;
+  if (!line_overlap(k1, k2, 0.5 + off[2])) return false;
+  if (reprojection_error(k1, k2) > 45) return false;
+  return true;
+}
+
+}  // namespace line_track
+
+using namespace line_track;
+
+extern "C" {
+
+// UndistortKeyLines + ComputeStereoFromRGBD for the lines of one frame.
+int oracle_line_frame_prepare(const orbpl_camera* cam, const orbpl_keyline* kl, int nl,
+                              const float* depth, orbpl_keyline* kl_un, float* dstart, float* dend,
+                              float* ur_start, float* ur_end) {
+  const int W = cam->width, H = cam->height;
+  for (int i = 0; i < nl; i++) {
+    orbpl_keyline k = kl[i];
+    if (cam->k1 != 0.0f) {
+      float x, y;
+      oracle_undistort_point(cam, kl[i].startPointX, kl[i].startPointY, &x, &y);
+      k.startPointX = x;
+      k.startPointY = y;
+      oracle_undistort_point(cam, kl[i].endPointX, kl[i].endPointY, &x, &y);
+      k.endPointX = x;
+      k.endPointY = y;
+      k.sPointInOctaveX = k.startPointX;
+      k.sPointInOctaveY = k.startPointY;
+      k.ePointInOctaveX = k.endPointX;
+      k.ePointInOctaveY = k.endPointY;
+      refresh_keyline(k, W, H);
+    }
+    kl_un[i] = k;
+    dstart[i] = dend[i] = ur_start[i] = ur_end[i] = -1;
+    if (!depth) continue;
+    auto at = [&](float v, float u) -> float {
+      const long long idx = (long long)(int)v * W + (int)u;
+      return (idx >= 0 && idx < (long long)W * H) ? depth[idx] : 0.f;
+    };
+    const float ds = at(kl[i].startPointY, kl[i].startPointX);
+    const float de = at(kl[i].endPointY, kl[i].endPointX);
+    if (ds > 0) {
+      dstart[i] = ds;
+      ur_start[i] = k.startPointX - cam->bf / ds;
+    }
+    if (de > 0) {
+      dend[i] = de;
+      ur_end[i] = k.endPointX - cam->bf / de;
+    }
+  }
+  return 0;
+}
+
+// LineMatcher(0.9, true).SearchByProjection(CurrentFrame, LastFrame)
+// Tcw: current pose (16 floats). Last frame map lines: has_ml[i], outlier[i],
+// xyz6[i] (start, end), desc[i]. match[j] = last-frame line index or -1.
+int oracle_line_search_by_projection_last(const orbpl_camera* cam, const float* Tcw, int ncur,
+                                          const orbpl_keyline* cur_kl_un, const uint8_t* cur_desc,
+                                          int nlast, const orbpl_keyline* last_kl_un,
+                                          const uint8_t* has_ml, const uint8_t* last_outlier,
+                                          const float* ml_xyz6, const uint8_t* last_desc,
+                                          int32_t* match, int* nmatches_out) {
+  const int W = cam->width, H = cam->height;
+  double T[12];
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 4; c++) T[r * 4 + c] = Tcw[r * 4 + c];
+  float b4[4];
+  oracle_image_bounds(cam, b4);  // minX, maxX, minY, maxY
+  const float bounds[4] = {b4[0], b4[2], b4[1], b4[3]};
+  std::vector<orbpl_keyline> nk;
+  std::vector<int> nidx;
+  auto xform = [&](const double* X, double* o) {
+    for (int r = 0; r < 3; r++) o[r] = (T[r * 4] * X[0] + T[r * 4 + 1] * X[1] + T[r * 4 + 2] * X[2]) + T[r * 4 + 3];
+  };
+  for (int i = 0; i < nlast; i++) {
+    if (!has_ml[i] || last_outlier[i]) continue;
+    const double Xs[3] = {ml_xyz6[6 * i], ml_xyz6[6 * i + 1], ml_xyz6[6 * i + 2]};
+    const double Xe[3] = {ml_xyz6[6 * i + 3], ml_xyz6[6 * i + 4], ml_xyz6[6 * i + 5]};
+    double cs[3], ce[3];
+    xform(Xs, cs);
+    xform(Xe, ce);
+    if (cs[2] < 0 && ce[2] < 0) continue;
+    double lp[4];
+    bool have = false;
+    if (cs[2] < 0.0 || ce[2] < 0.0) {
+      const double lambda = -1.0 * cs[2] / (cs[2] - ce[2]);
+      const double xc = cs[0] + lambda * (cs[0] - ce[0]);
+      const double yc = cs[1] + lambda * (cs[1] - ce[1]);
+      if (cs[2] < 0.0) {
+        const float u_end = cam->fx * ce[0] / ce[2] + cam->cx;
+        const float v_end = cam->fy * ce[1] / ce[2] + cam->cy;
+        lp[0] = xc; lp[1] = yc; lp[2] = u_end; lp[3] = v_end;
+      } else {
+        const float u_start = cam->fx * cs[0] / cs[2] + cam->cx;
+        const float v_start = cam->fy * cs[1] / cs[2] + cam->cy;
+        lp[0] = u_start; lp[1] = v_start; lp[2] = xc; lp[3] = yc;
+      }
+      have = true;
+    }
+    if (cs[2] > 0.0 && ce[2] > 0.0) {
+      const float u_start = cam->fx * cs[0] / cs[2] + cam->cx;
+      const float v_start = cam->fy * cs[1] / cs[2] + cam->cy;
+      const float u_end = cam->fx * ce[0] / ce[2] + cam->cx;
+      const float v_end = cam->fy * ce[1] / ce[2] + cam->cy;
+      lp[0] = u_start; lp[1] = v_start; lp[2] = u_end; lp[3] = v_end;
+      have = true;
+    }
+    if (!have) continue;
+    double nl4[4];
+    if (!liang_barsky(lp, nl4, bounds)) continue;
+    orbpl_keyline k = last_kl_un[i];
+    k.startPointX = (float)nl4[0];
+    k.startPointY = (float)nl4[1];
+    k.endPointX = (float)nl4[2];
+    k.endPointY = (float)nl4[3];
+    k.sPointInOctaveX = (float)nl4[0];
+    k.sPointInOctaveY = (float)nl4[1];
+    k.ePointInOctaveX = (float)nl4[2];
+    k.ePointInOctaveY = (float)nl4[3];
+    refresh_keyline(k, W, H);
+    nk.push_back(k);
+    nidx.push_back(i);
+  }
+  auto run = [&](const double off[5]) {
+    int cnt = 0;
+    for (int j = 0; j < ncur; j++) {
+      match[j] = -1;
+      for (size_t i = 0; i < nk.size(); i++)
+        if (line_matching(nk[i], cur_kl_un[j], last_desc + 32 * nidx[i], cur_desc + 32 * j, off)) {
+          match[j] = nidx[i];
+          cnt++;
+        }
+    }
+    return cnt;
+  };
+  const double off0[5] = {0, 0, 0, 0, 0};
+  int n = run(off0);
+  if (n * 1.0 / ncur < 0.2) {
+    const double off1[5] = {10.0, -0.1, -0.1, 5, 10};
+    n = run(off1);
+  }
+  *nmatches_out = n;
+  return 0;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Points + lines VO step (Tracking::TrackWithMotionModel, Tracking.cc:1212-
+// 1330, with ORB and LSD/LBD extraction as Frame(RGB-D) runs them, and every
+// frame acting as the next keyframe: map points and map lines are created
+// StereoInitialization-style, Tracking.cc:627-690). Mirrors orbpl_tracker
+// with lines enabled.
+// ---------------------------------------------------------------------------
+namespace line_track {
+
+static void gemm44(const float* A, const float* B, float* Cm) {
+  for (int r = 0; r < 4; r++)
+    for (int c = 0; c < 4; c++) {
+      double s = (double)A[r * 4] * B[c];
+      s += (double)A[r * 4 + 1] * B[4 + c];
+      s += (double)A[r * 4 + 2] * B[8 + c];
+      s += (double)A[r * 4 + 3] * B[12 + c];
+      Cm[r * 4 + c] = (float)s;
+    }
+}
+static void neg_Rt_t(const float* T, float* o) {
+  for (int r = 0; r < 3; r++) {
+    double s = (double)T[0 * 4 + r] * T[3];
+    s += (double)T[1 * 4 + r] * T[7];
+    s += (double)T[2 * 4 + r] * T[11];
+    o[r] = (float)(s * -1.0);
+  }
+}
+static void pose_inv(const float* T, float* Ti) {
+  float ow[3];
+  neg_Rt_t(T, ow);
+  for (int r = 0; r < 3; r++) {
+    for (int c = 0; c < 3; c++) Ti[r * 4 + c] = T[c * 4 + r];
+    Ti[r * 4 + 3] = ow[r];
+  }
+  Ti[12] = 0; Ti[13] = 0; Ti[14] = 0; Ti[15] = 1;
+}
+// Frame::UnprojectStereo*: Rwc * (x, y, z) + Ow, double-accumulated (P6)
+static void unproject(const orbpl_camera& c, const float* T, const float* Ow, float u, float v,
+                      float z, float* w) {
+  const float invfx = 1.0f / c.fx, invfy = 1.0f / c.fy;
+  const float x3[3] = {(u - c.cx) * z * invfx, (v - c.cy) * z * invfy, z};
+  for (int r = 0; r < 3; r++) {
+    double s = (double)T[0 * 4 + r] * x3[0];
+    s += (double)T[1 * 4 + r] * x3[1];
+    s += (double)T[2 * 4 + r] * x3[2];
+    w[r] = (float)(s + (double)Ow[r]);
+  }
+}
+
+struct LStream {
+  bool has_last = false, has_velocity = false;
+  float Tcw[16], Tlast[16], Tlast2[16];
+  std::vector<orbpl_keypoint> kps_un;
+  std::vector<uint8_t> desc, has_mp, outlier;
+  std::vector<float> xyz;
+  std::vector<int32_t> nobs;
+  std::vector<orbpl_keyline> kl_un;
+  std::vector<uint8_t> ldesc, has_ml, loutlier;
+  std::vector<float> lxyz;
+};
+
+struct LVO {
+  orbpl_orb_params orb;
+  orbpl_camera cam;
+  int use_lines;
+  std::vector<LStream> st;
+  std::vector<float> scale, inv_sigma2;
+};
+
+}  // namespace line_track
+
+extern "C" {
+
+void* oracle_lvo_create(const orbpl_orb_params* orb, const orbpl_camera* cam, int n_streams,
+                        int use_lines) {
+  LVO* v = new LVO();
+  v->orb = *orb;
+  v->cam = *cam;
+  v->use_lines = use_lines;
+  v->st.resize(n_streams);
+  v->scale.resize(orb->nlevels);
+  std::vector<float> isc(orb->nlevels);
+  oracle_orb_level_sizes(orb, cam->width, cam->height, nullptr, nullptr, nullptr, v->scale.data(),
+                         isc.data());
+  v->inv_sigma2.resize(orb->nlevels);
+  for (int l = 0; l < orb->nlevels; l++) v->inv_sigma2[l] = 1.0f / (v->scale[l] * v->scale[l]);
+  return v;
+}
+
+void oracle_lvo_destroy(void* h) { delete static_cast<LVO*>(h); }
+
+int oracle_lvo_reset(void* h, const float* Tcw0) {
+  LVO* v = static_cast<LVO*>(h);
+  for (size_t s = 0; s < v->st.size(); s++) {
+    LStream z;
+    for (int k = 0; k < 16; k++) z.Tcw[k] = Tcw0 ? Tcw0[s * 16 + k] : ((k % 5 == 0) ? 1.f : 0.f);
+    v->st[s] = z;
+  }
+  return 0;
+}
+
+// out8: nkeypoints, nmatches, ninliers, nmatches_map, ok, nlines, line_matches,
+// line_nmatches_map
+int oracle_lvo_step(void* h, int stream, const uint8_t* gray, const float* depth, float* Tcw_out,
+                    int* out8) {
+  LVO* v = static_cast<LVO*>(h);
+  LStream& S = v->st[stream];
+  const orbpl_camera& cam = v->cam;
+  const int cap = v->orb.nfeatures * 2 + 64;
+  std::vector<orbpl_keypoint> kps(cap);
+  std::vector<uint8_t> desc((size_t)cap * 32);
+  int n = 0;
+  int rc = oracle_orb_extract(&v->orb, gray, cam.width, cam.height, cam.width, kps.data(),
+                              desc.data(), cap, &n, nullptr);
+  if (rc) return rc;
+  kps.resize(n);
+  desc.resize((size_t)n * 32);
+  std::vector<orbpl_keypoint> ku(n);
+  std::vector<float> dep(n), ur(n);
+  std::vector<int32_t> gc(n);
+  oracle_frame_prepare(&cam, kps.data(), n, depth, ku.data(), dep.data(), ur.data(), gc.data(), nullptr);
+  // lines
+  int nl = 0;
+  std::vector<orbpl_keyline> kl(80), klu;
+  std::vector<uint8_t> ldesc(80 * 32);
+  std::vector<float> lds, lde, lurs, lure;
+  if (v->use_lines) {
+    std::vector<double> coef(80 * 3);
+    int nd = 0;
+    rc = oracle_line_extract(gray, cam.width, cam.height, kl.data(), ldesc.data(), coef.data(), 80,
+                             &nl, &nd);
+    if (rc) return rc;
+    kl.resize(nl);
+    ldesc.resize((size_t)nl * 32);
+    klu.resize(nl);
+    lds.resize(nl); lde.resize(nl); lurs.resize(nl); lure.resize(nl);
+    oracle_line_frame_prepare(&cam, kl.data(), nl, depth, klu.data(), lds.data(), lde.data(),
+                              lurs.data(), lure.data());
+  }
+  std::vector<int32_t> match(n, -1), lmatch(nl, -1);
+  std::vector<uint8_t> outl(n, 0), loutl(nl, 0);
+  int nmatches = 0, ninl = 0, nmap = 0, nlm = 0, lnmap = 0;
+  bool tracked = false;
+  if (S.has_last) {
+    if (S.has_velocity) {
+      float Twl[16], V[16];
+      pose_inv(S.Tlast2, Twl);
+      gemm44(S.Tlast, Twl, V);
+      gemm44(V, S.Tlast, S.Tcw);
+    } else {
+      memcpy(S.Tcw, S.Tlast, 64);
+    }
+    orbpl_match_current cur{n, S.Tcw, ku.data(), desc.data(), ur.data()};
+    orbpl_match_last last{(int)S.kps_un.size(), S.Tlast, S.kps_un.data(), S.has_mp.data(),
+                          S.outlier.data(), S.xyz.data(), S.desc.data(), S.nobs.data()};
+    oracle_search_by_projection_last(&cam, v->scale.data(), (int)v->scale.size(), &cur, &last, 15.0f,
+                                     0, 1, match.data(), &nmatches);
+    if (v->use_lines)
+      oracle_line_search_by_projection_last(&cam, S.Tcw, nl, klu.data(), ldesc.data(),
+                                            (int)S.kl_un.size(), S.kl_un.data(), S.has_ml.data(),
+                                            S.loutlier.data(), S.lxyz.data(), S.ldesc.data(),
+                                            lmatch.data(), &nlm);
+    if (nmatches < 20) {
+      std::fill(match.begin(), match.end(), -1);
+      oracle_search_by_projection_last(&cam, v->scale.data(), (int)v->scale.size(), &cur, &last,
+                                       30.0f, 0, 1, match.data(), &nmatches);
+    }
+    tracked = nmatches >= 20 && (!v->use_lines || nlm >= 15);
+    if (tracked) {
+      std::vector<uint8_t> has(n, 0), hasl(nl, 0);
+      std::vector<float> xyz((size_t)n * 3, 0.f), lobs((size_t)nl * 4, 0.f), lxyz((size_t)nl * 6, 0.f);
+      std::vector<int32_t> loct(nl, 0);
+      for (int i = 0; i < n; i++)
+        if (match[i] >= 0) {
+          has[i] = 1;
+          for (int k = 0; k < 3; k++) xyz[3 * i + k] = S.xyz[3 * match[i] + k];
+        }
+      for (int j = 0; j < nl; j++) {
+        loct[j] = klu[j].octave;
+        lobs[4 * j] = klu[j].startPointX;
+        lobs[4 * j + 1] = klu[j].startPointY;
+        lobs[4 * j + 2] = klu[j].endPointX;
+        lobs[4 * j + 3] = klu[j].endPointY;
+        if (lmatch[j] >= 0) {
+          hasl[j] = 1;
+          for (int k = 0; k < 6; k++) lxyz[6 * j + k] = S.lxyz[6 * lmatch[j] + k];
+        }
+      }
+      orbpl_pose_problem P{};
+      P.n = n;
+      P.kps_un = ku.data();
+      P.uright = ur.data();
+      P.has_mp = has.data();
+      P.mp_xyz = xyz.data();
+      P.nl = nl;
+      P.kl_obs = lobs.data();
+      P.kl_octave = loct.data();
+      P.has_ml = hasl.data();
+      P.ml_xyz = lxyz.data();
+      P.inv_sigma2 = v->inv_sigma2.data();
+      P.nlevels = (int)v->inv_sigma2.size();
+      oracle_pose_optimization(&cam, &P, S.Tcw, outl.data(), loutl.data(), &ninl);
+    }
+    // outlier discard (Tracking.cc:1273-1314); without an optimisation every
+    // flag is clear and the counts report the raw matches
+    for (int i = 0; i < n; i++)
+      if (match[i] >= 0) {
+        if (outl[i]) match[i] = -1;
+        else nmap++;
+      }
+    for (int j = 0; j < nl; j++)
+      if (lmatch[j] >= 0) {
+        if (loutl[j]) {
+          lmatch[j] = -1;
+          lnmap--;  // the reference decrements here (Tracking.cc:1306)
+        } else {
+          lnmap++;
+        }
+      }
+  }
+  // this frame becomes the keyframe of the next one
+  float Ow[3];
+  neg_Rt_t(S.Tcw, Ow);
+  S.kps_un = ku;
+  S.desc = desc;
+  S.has_mp.assign(n, 0);
+  S.outlier.assign(n, 0);
+  S.xyz.assign((size_t)n * 3, 0.f);
+  S.nobs.assign(n, 0);
+  for (int i = 0; i < n; i++)
+    if (dep[i] > 0) {
+      unproject(cam, S.Tcw, Ow, ku[i].x, ku[i].y, dep[i], &S.xyz[3 * i]);
+      S.has_mp[i] = 1;
+      S.nobs[i] = 1;
+    }
+  S.kl_un = klu;
+  S.ldesc = ldesc;
+  S.has_ml.assign(nl, 0);
+  S.loutlier.assign(nl, 0);
+  S.lxyz.assign((size_t)nl * 6, 0.f);
+  for (int j = 0; j < nl; j++)
+    if (lds[j] > 0 && lde[j] > 0) {
+      // UnprojectStereoLineEnd uses mvDepthLineStart (Frame.cc:1192)
+      unproject(cam, S.Tcw, Ow, klu[j].startPointX, klu[j].startPointY, lds[j], &S.lxyz[6 * j]);
+      unproject(cam, S.Tcw, Ow, klu[j].endPointX, klu[j].endPointY, lds[j], &S.lxyz[6 * j + 3]);
+      S.has_ml[j] = 1;
+    }
+  bool ok = true;
+  if (S.has_last) ok = tracked && (v->use_lines ? (nmap >= 10 || lnmap >= 15) : nmap >= 10);
+  memcpy(S.Tlast2, S.Tlast, 64);
+  memcpy(S.Tlast, S.Tcw, 64);
+  S.has_velocity = S.has_last;
+  S.has_last = true;
+  if (Tcw_out) memcpy(Tcw_out, S.Tcw, 64);
+  if (out8) {
+    out8[0] = n; out8[1] = nmatches; out8[2] = ninl; out8[3] = nmap; out8[4] = ok;
+    out8[5] = nl; out8[6] = nlm; out8[7] = lnmap;
+  }
+  return 0;
+}
+
+}  // extern "C"

@@ -348,3 +348,74 @@ def introsort_perm(keys):
     perm = np.zeros(len(k), np.int32)
     lib().oracle_introsort_perm(_p(k), len(k), _p(perm))
     return perm
+
+
+_setup_lines_orb = _setup
+
+
+def _setup(L):  # noqa: F811
+    _setup_lines_orb(L)
+    vp, i, ip = C.c_void_p, C.c_int, C.POINTER(C.c_int)
+    L.oracle_line_frame_prepare.argtypes = [vp, vp, i, vp, vp, vp, vp, vp, vp]
+    L.oracle_line_search_by_projection_last.argtypes = [vp, vp, i, vp, vp, i, vp, vp, vp, vp, vp,
+                                                        vp, ip]
+    L.oracle_lvo_create.argtypes = [vp, vp, i, i]
+    L.oracle_lvo_create.restype = vp
+    L.oracle_lvo_destroy.argtypes = [vp]
+    L.oracle_lvo_reset.argtypes = [vp, vp]
+    L.oracle_lvo_step.argtypes = [vp, i, vp, vp, vp, vp]
+
+
+def line_frame_prepare(cam, kl, depth=None):
+    kl = _c(kl, KEYLINE_DTYPE)
+    n = len(kl)
+    ku = np.zeros(n, KEYLINE_DTYPE)
+    ds, de, us, ue = (np.zeros(n, np.float32) for _ in range(4))
+    dp = None if depth is None else _c(depth, np.float32)
+    lib().oracle_line_frame_prepare(C.byref(cam), _p(kl), n, None if dp is None else _p(dp),
+                                    _p(ku), _p(ds), _p(de), _p(us), _p(ue))
+    return ku, ds, de, us, ue
+
+
+def line_search_by_projection_last(cam, Tcw, cur_kl_un, cur_desc, last_kl_un, has_ml, outlier,
+                                   ml_xyz6, last_desc):
+    keep = [_c(Tcw, np.float32), _c(cur_kl_un, KEYLINE_DTYPE), _c(cur_desc, np.uint8),
+            _c(last_kl_un, KEYLINE_DTYPE), _c(has_ml, np.uint8), _c(outlier, np.uint8),
+            _c(ml_xyz6, np.float32), _c(last_desc, np.uint8)]
+    ncur = len(keep[1])
+    match = np.zeros(max(1, ncur), np.int32)
+    nm = C.c_int(0)
+    lib().oracle_line_search_by_projection_last(C.byref(cam), _p(keep[0]), ncur, _p(keep[1]),
+                                                _p(keep[2]), len(keep[3]), _p(keep[3]), _p(keep[4]),
+                                                _p(keep[5]), _p(keep[6]), _p(keep[7]), _p(match),
+                                                C.byref(nm))
+    return match[:ncur].copy(), nm.value
+
+
+class LVO:
+    """CPU oracle of the points (+ lines) tracker, one stream at a time."""
+
+    def __init__(self, orb_params, cam, n_streams, use_lines=True):
+        self.h = lib().oracle_lvo_create(C.byref(orb_params), C.byref(cam), n_streams,
+                                         int(use_lines))
+
+    def reset(self, Tcw0=None):
+        T = None if Tcw0 is None else _c(Tcw0, np.float32)
+        lib().oracle_lvo_reset(self.h, None if T is None else _p(T))
+
+    def step(self, stream, gray, depth):
+        g = _c(gray, np.uint8)
+        d = _c(depth, np.float32)
+        T = np.zeros(16, np.float32)
+        o = np.zeros(8, np.int32)
+        rc = lib().oracle_lvo_step(self.h, stream, _p(g), _p(d), _p(T), _p(o))
+        assert rc == 0
+        keys = ("nkeypoints", "nmatches", "ninliers", "nmatches_map", "ok", "nlines",
+                "line_matches", "line_nmatches_map")
+        return T.reshape(4, 4), dict(zip(keys, (int(x) for x in o)))
+
+    def __del__(self):
+        try:
+            lib().oracle_lvo_destroy(self.h)
+        except Exception:
+            pass

@@ -38,6 +38,24 @@ int oracle_line_extract(const uint8_t* img, int W, int H, orbpl_keyline* kl_out,
 double oracle_lsdm(int fn, double x, double y);
 int oracle_line_iterator_count(int W, int H, float x1, float y1, float x2, float y2);
 int oracle_introsort_perm(const int* keys, int n, int* perm);
+/* line tracking (line_track_oracle.cpp) */
+void oracle_undistort_point(const orbpl_camera* c, float px, float py, float* ox, float* oy);
+void oracle_image_bounds(const orbpl_camera* c, float* b4);
+int oracle_line_frame_prepare(const orbpl_camera* cam, const orbpl_keyline* kl, int nl,
+                              const float* depth, orbpl_keyline* kl_un, float* dstart, float* dend,
+                              float* ur_start, float* ur_end);
+int oracle_line_search_by_projection_last(const orbpl_camera* cam, const float* Tcw, int ncur,
+                                          const orbpl_keyline* cur_kl_un, const uint8_t* cur_desc,
+                                          int nlast, const orbpl_keyline* last_kl_un,
+                                          const uint8_t* has_ml, const uint8_t* last_outlier,
+                                          const float* ml_xyz6, const uint8_t* last_desc,
+                                          int32_t* match, int* nmatches_out);
+void* oracle_lvo_create(const orbpl_orb_params* orb, const orbpl_camera* cam, int n_streams,
+                        int use_lines);
+void oracle_lvo_destroy(void* h);
+int oracle_lvo_reset(void* h, const float* Tcw0);
+int oracle_lvo_step(void* h, int stream, const uint8_t* gray, const float* depth, float* Tcw_out,
+                    int* out8);
 #ifdef __cplusplus
 }
 #endif

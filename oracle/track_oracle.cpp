@@ -795,6 +795,12 @@ struct VO {
 
 extern "C" {
 
+void oracle_undistort_point(const orbpl_camera* c, float px, float py, float* ox, float* oy) {
+  undistort_point(*c, px, py, ox, oy);
+}
+
+void oracle_image_bounds(const orbpl_camera* c, float* b4) { image_bounds(*c, b4); }
+
 void* oracle_vo_create(const orbpl_orb_params* orb, const orbpl_camera* cam, int n_streams) {
   VO* v = new VO();
   v->orb = *orb;

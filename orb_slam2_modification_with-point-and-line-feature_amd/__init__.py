@@ -339,6 +339,10 @@ def _declare_track(L):
     L.orbpl_tracker_timings.argtypes = [vp, i, vp, ip]
     L.orbpl_tracker_timings_reset.argtypes = [vp]
     L.orbpl_tracker_get_frame.argtypes = [vp, i, vp, vp, vp, vp, ip]
+    L.orbpl_tracker_create_ex.argtypes = [vp, vp, i, i, i, C.POINTER(vp)]
+    L.orbpl_tracker_get_status.argtypes = [vp, vp, vp, vp, vp]
+    L.orbpl_tracker_get_lines.argtypes = [vp, i, vp, vp, vp, vp, ip]
+    L.orbpl_tracker_line_timings.argtypes = [vp, i, vp, ip]
 
 
 _declare_orig = _declare
@@ -434,13 +438,17 @@ def pose_optimization(camera, prob, Tcw, outlier, line_outlier=None):
 
 class Tracker:
     """Batched RGB-D tracker (orbpl_tracker_*): one TrackWithMotionModel step
-    for n_streams independent streams per call."""
+    for n_streams independent streams per call. lines=True selects the
+    point-and-line variant (ORBPL_TRACK_LINES)."""
 
-    def __init__(self, orb_params, camera, n_streams, device=0):
+    TRACK_LINES = 1
+
+    def __init__(self, orb_params, camera, n_streams, device=0, lines=False):
         h = C.c_void_p()
-        self.camera, self.S, self.device = camera, n_streams, device
-        check(lib().orbpl_tracker_create(C.byref(orb_params), C.byref(camera), n_streams, device,
-                                         C.byref(h)), "orbpl_tracker_create")
+        self.camera, self.S, self.device, self.use_lines = camera, n_streams, device, bool(lines)
+        check(lib().orbpl_tracker_create_ex(C.byref(orb_params), C.byref(camera), n_streams, device,
+                                            self.TRACK_LINES if lines else 0, C.byref(h)),
+              "orbpl_tracker_create_ex")
         self._h = h
         self.kp_cap = lib().orbpl_tracker_kp_capacity(h)
 
@@ -476,6 +484,37 @@ class Tracker:
         check(lib().orbpl_tracker_get_state(self._h, _ptr(T), _ptr(nk), _ptr(nm), _ptr(ni),
                                             _ptr(nmm)), "orbpl_tracker_get_state")
         return dict(Tcw=T, nkeypoints=nk, nmatches=nm, ninliers=ni, nmatches_map=nmm)
+
+    def status(self):
+        """ok, nlines, line_matches, line_nmatches_map per stream (last step)."""
+        S = self.S
+        ok, nl, lm, lnm = (np.zeros(S, np.int32) for _ in range(4))
+        check(lib().orbpl_tracker_get_status(self._h, _ptr(ok), _ptr(nl), _ptr(lm), _ptr(lnm)),
+              "orbpl_tracker_get_status")
+        return dict(ok=ok, nlines=nl, line_matches=lm, line_nmatches_map=lnm)
+
+    def lines(self, stream):
+        """Undistorted KeyLines, LBD rows, line match, line outlier of one stream."""
+        K = 80
+        kl = np.zeros(K, KEYLINE_DTYPE)
+        d = np.zeros((K, 32), np.uint8)
+        m = np.zeros(K, np.int32)
+        o = np.zeros(K, np.uint8)
+        n = C.c_int(0)
+        check(lib().orbpl_tracker_get_lines(self._h, stream, _ptr(kl), _ptr(d), _ptr(m), _ptr(o),
+                                            C.byref(n)), "orbpl_tracker_get_lines")
+        k = n.value
+        return kl[:k], d[:k], m[:k], o[:k]
+
+    LINE_STAGES = ("lsd", "keylines_lbd", "line_match")
+
+    def line_timings(self, max_steps=64):
+        """(n_steps, 3) line-stage ms of the last steps (hipEvents in-stream)."""
+        ms = np.zeros((max_steps, 3), np.float32)
+        n = C.c_int(0)
+        check(lib().orbpl_tracker_line_timings(self._h, max_steps, _ptr(ms), C.byref(n)),
+              "orbpl_tracker_line_timings")
+        return ms[:n.value]
 
     def stage_ms(self):
         ms = np.zeros(5, np.float32)

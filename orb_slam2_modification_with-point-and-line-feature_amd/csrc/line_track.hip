@@ -1,0 +1,293 @@
+// Per-frame line tracking on gfx950 (restated in oracle/line_track_oracle.cpp):
+//   k_line_prepare : Frame::UndistortKeyLines (Frame.cc:769-845) and the line
+//                    part of ComputeStereoFromRGBD (Frame.cc:1090-1116)
+//   k_line_match   : LineMatcher::SearchByProjection(Frame&, const Frame&)
+//                    (LineMatcher.cpp:72-269): last-frame MapLines projected
+//                    and Liang-Barsky clipped in parallel, then every
+//                    (projected, current) pair tested by LineMatching in
+//                    parallel; the last passing projected line of each
+//                    current line wins and every pass counts, as in the
+//                    reference's double loop; one relaxed retry
+//   line map update: lives in k_finish (track_kernels.hip)
+#include <hip/hip_runtime.h>
+
+#include "line_common.h"
+#include "lsd_kernels.h"
+#include "track_common.h"
+#include "track_kernels.h"
+
+namespace orbpl {
+
+__global__ void __launch_bounds__(64) k_line_prepare(TrackConsts c, LineTrackArgs a) {
+  const int s = blockIdx.x, lane = threadIdx.x;
+  const int nl = a.nl[s];
+  const long long lb = (long long)s * kLineKeep;
+  const int W = c.width, H = c.height;
+  const float* depth = a.depth + (long long)s * a.depth_pitch;
+  for (int j = lane; j < nl; j += 64) {
+    const orbpl_keyline k0 = a.kl[lb + j];
+    orbpl_keyline k = k0;
+    if (c.k1 != 0.0f) {
+      float x, y;
+      undistort_point_d(c, k0.startPointX, k0.startPointY, &x, &y);
+      k.startPointX = x;
+      k.startPointY = y;
+      undistort_point_d(c, k0.endPointX, k0.endPointY, &x, &y);
+      k.endPointX = x;
+      k.endPointY = y;
+      k.sPointInOctaveX = k.startPointX;
+      k.sPointInOctaveY = k.startPointY;
+      k.ePointInOctaveX = k.endPointX;
+      k.ePointInOctaveY = k.endPointY;
+      refresh_keyline(k, W, H);
+    }
+    a.kl_un[lb + j] = k;
+    // imDepth.at<float>(int(v), int(u)) on the distorted end points (P14)
+    auto at = [&](float v, float u) -> float {
+      const long long idx = (long long)(int)v * W + (int)u;
+      return (idx >= 0 && idx < (long long)W * H) ? depth[idx] : 0.f;
+    };
+    const float ds = at(k0.startPointY, k0.startPointX);
+    const float de = at(k0.endPointY, k0.endPointX);
+    a.dstart[lb + j] = ds > 0 ? ds : -1.f;
+    a.dend[lb + j] = de > 0 ? de : -1.f;
+    a.lmatch[lb + j] = -1;
+    a.loutlier[lb + j] = 0;
+  }
+}
+
+namespace {
+
+// std::min / std::max: (b < a) ? b : a and (a < b) ? b : a
+template <typename T>
+__device__ __forceinline__ T smin(T a, T b) { return (b < a) ? b : a; }
+template <typename T>
+__device__ __forceinline__ T smax(T a, T b) { return (a < b) ? b : a; }
+
+__device__ bool liang_barsky(const double line[4], double out[4], const float b[4]) {
+  const double sx = line[0], sy = line[1], ex = line[2], ey = line[3];
+  double p[4], q[4];
+  p[0] = sx - ex;
+  p[1] = ex - sx;
+  p[2] = sy - ey;
+  p[3] = ey - sy;
+  q[0] = sx - b[0];
+  q[1] = b[2] - sx;
+  q[2] = sy - b[1];
+  q[3] = b[3] - sy;
+  if (p[0] == 0) {
+    if (q[0] <= 0 || q[2] <= 0) return false;
+  }
+  if (p[2] == 0) {
+    if (q[2] >= 0 || q[3] >= 0) return false;
+  }
+  double u_min = 0, u_max = 1;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const double u = q[i] / p[i];
+    if (p[i] < 0) {
+      if (u_min < u) u_min = u;
+    } else {
+      if (u_max > u) u_max = u;
+    }
+  }
+  if (u_max >= u_min) {
+    out[0] = sx + round(u_min * (ex - sx));
+    out[1] = sy + round(u_min * (ey - sy));
+    out[2] = sx + round(u_max * (ex - sx));
+    out[3] = sy + round(u_max * (ey - sy));
+    return true;
+  }
+  return false;
+}
+
+__device__ bool line_overlap(const orbpl_keyline& a, const orbpl_keyline& b, double th) {
+  const double d1_x = fabsf(a.startPointX - a.endPointX);
+  const double d2_x = fabsf(b.startPointX - b.endPointX);
+  const double min_x = smin(smin(a.startPointX, a.endPointX), smin(b.startPointX, b.endPointX));
+  const double max_x = smax(smax(a.startPointX, a.endPointX), smax(b.startPointX, b.endPointX));
+  const double d1_y = fabsf(a.startPointY - a.endPointY);
+  const double d2_y = fabsf(b.startPointY - b.endPointY);
+  const double min_y = smin(smin(a.startPointY, a.endPointY), smin(b.startPointY, b.endPointY));
+  const double max_y = smax(smax(a.startPointY, a.endPointY), smax(b.startPointY, b.endPointY));
+  if (d1_x == 0 || d2_x == 0) {
+    if ((d1_y + d2_y - max_y + min_y) / smin(d1_y, d2_y) >= th) return true;
+  }
+  if (d1_y == 0 || d2_y == 0) {
+    if ((d1_x + d2_x - max_x + min_x) / smin(d1_x, d2_x) >= th) return true;
+  }
+  if ((d1_x + d2_x - max_x + min_x) / smin(d1_x, d2_x) >= th) {
+    if (d1_y + d2_y + min_y >= max_y) return true;
+    if (max_y - min_y - d1_y - d2_y < 0.3 * smin(d1_y, d2_y)) return true;
+  } else if ((d1_x + d2_x - max_x + min_x) / smin(d1_x, d2_x) < th &&
+             (max_x - min_x - d1_x - d2_x) < 0.3 * smin(d1_x, d2_x)) {
+    if ((d1_y + d2_y - max_y + min_y) / smin(d1_y, d2_y) >= th) return true;
+  }
+  return false;
+}
+
+__device__ double reprojection_error(const orbpl_keyline& l1, const orbpl_keyline& l2) {
+  const double s0 = l1.startPointX, s1 = l1.startPointY, s2 = 1;
+  const double e0 = l1.endPointX, e1 = l1.endPointY, e2 = 1;
+  const double c0 = s1 * e2 - s2 * e1, c1 = s2 * e0 - s0 * e2, c2 = s0 * e1 - s1 * e0;
+  const double nrm = sqrt(c0 * c0 + c1 * c1);
+  const double ds = ((double)l2.startPointX * c0 + (double)l2.startPointY * c1 + 1.0 * c2) / nrm;
+  const double de = ((double)l2.endPointX * c0 + (double)l2.endPointY * c1 + 1.0 * c2) / nrm;
+  return sqrt(ds * ds + de * de);
+}
+
+__device__ bool line_matching(const orbpl_keyline& k1, const orbpl_keyline& k2, const uint4* d1,
+                              const uint4* d2, const double off0, const double off1,
+                              const double off2, const double off3) {
+  const double kPi = 3.14159265358979323846;
+  int dist = 0;
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    const uint4 a = d1[q], b = d2[q];
+    dist += __popc(a.x ^ b.x) + __popc(a.y ^ b.y) + __popc(a.z ^ b.z) + __popc(a.w ^ b.w);
+  }
+  if (dist > 45 + off3) return false;
+  if (fabsf(k1.angle - k2.angle) > 15.0 * kPi / 180.0 + off0 * kPi / 180.0) return false;
+  if (smin(k1.lineLength, k2.lineLength) / smax(k1.lineLength, k2.lineLength) < 0.45 + off1)
+    return false;
+  if (!line_overlap(k1, k2, 0.5 + off2)) return false;
+  if (reprojection_error(k1, k2) > 45) return false;
+  return true;
+}
+
+}  // namespace
+
+// One 256-thread block per stream.
+__global__ void __launch_bounds__(256) k_line_match(TrackConsts c, LineTrackArgs a,
+                                                     StreamState* st) {
+  __shared__ orbpl_keyline s_kl[kLineKeep];
+  __shared__ int s_src[kLineKeep];
+  __shared__ int s_np;
+  __shared__ unsigned s_ok[kLineKeep][(kLineKeep + 31) / 32];
+  __shared__ int s_cnt;
+  const int s = blockIdx.x, t = threadIdx.x;
+  const StreamState& S = st[s];
+  if (!S.has_last) {
+    if (t == 0) st[s].nlmatches = 0;
+    return;
+  }
+  const long long lb = (long long)s * kLineKeep;
+  const int ncur = a.nl[s], nlast = a.last_nl[s];
+  const int W = c.width, H = c.height;
+  // ---- project the last frame's map lines with the predicted pose ----
+  bool valid = false;
+  orbpl_keyline k{};
+  if (t < nlast && t < kLineKeep && a.last_has_ml[lb + t] && !a.last_loutlier[lb + t]) {
+    double T[12];
+#pragma unroll
+    for (int q = 0; q < 12; q++) T[q] = S.Tcw[q];
+    const float* X = a.last_ml_xyz + (lb + t) * 6;
+    double cs[3], ce[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+      cs[r] = (T[r * 4] * (double)X[0] + T[r * 4 + 1] * (double)X[1] + T[r * 4 + 2] * (double)X[2]) + T[r * 4 + 3];
+      ce[r] = (T[r * 4] * (double)X[3] + T[r * 4 + 1] * (double)X[4] + T[r * 4 + 2] * (double)X[5]) + T[r * 4 + 3];
+    }
+    double lp[4];
+    bool have = false;
+    if (!(cs[2] < 0 && ce[2] < 0)) {
+      if (cs[2] < 0.0 || ce[2] < 0.0) {
+        const double lambda = -1.0 * cs[2] / (cs[2] - ce[2]);
+        const double xc = cs[0] + lambda * (cs[0] - ce[0]);
+        const double yc = cs[1] + lambda * (cs[1] - ce[1]);
+        if (cs[2] < 0.0) {
+          const float u_end = c.fx * ce[0] / ce[2] + c.cx;
+          const float v_end = c.fy * ce[1] / ce[2] + c.cy;
+          lp[0] = xc; lp[1] = yc; lp[2] = u_end; lp[3] = v_end;
+        } else {
+          const float u_start = c.fx * cs[0] / cs[2] + c.cx;
+          const float v_start = c.fy * cs[1] / cs[2] + c.cy;
+          lp[0] = u_start; lp[1] = v_start; lp[2] = xc; lp[3] = yc;
+        }
+        have = true;
+      }
+      if (cs[2] > 0.0 && ce[2] > 0.0) {
+        const float u_start = c.fx * cs[0] / cs[2] + c.cx;
+        const float v_start = c.fy * cs[1] / cs[2] + c.cy;
+        const float u_end = c.fx * ce[0] / ce[2] + c.cx;
+        const float v_end = c.fy * ce[1] / ce[2] + c.cy;
+        lp[0] = u_start; lp[1] = v_start; lp[2] = u_end; lp[3] = v_end;
+        have = true;
+      }
+    }
+    double nl4[4];
+    const float bounds[4] = {c.minX, c.minY, c.maxX, c.maxY};
+    if (have && liang_barsky(lp, nl4, bounds)) {
+      k = a.last_kl_un[lb + t];
+      k.startPointX = (float)nl4[0];
+      k.startPointY = (float)nl4[1];
+      k.endPointX = (float)nl4[2];
+      k.endPointY = (float)nl4[3];
+      k.sPointInOctaveX = (float)nl4[0];
+      k.sPointInOctaveY = (float)nl4[1];
+      k.ePointInOctaveX = (float)nl4[2];
+      k.ePointInOctaveY = (float)nl4[3];
+      refresh_keyline(k, W, H);
+      valid = true;
+    }
+  }
+  // compaction keeps the projected lines in last-frame index order
+  __shared__ int s_wc[4];
+  const unsigned long long m = __ballot(valid);
+  if ((t & 63) == 0) s_wc[t >> 6] = __popcll(m);
+  __syncthreads();
+  int pos = __popcll(m & ((1ull << (t & 63)) - 1ull));
+  for (int w = 0; w < (t >> 6); w++) pos += s_wc[w];
+  if (valid) {
+    s_kl[pos] = k;
+    s_src[pos] = t;
+  }
+  if (t == 0) s_np = s_wc[0] + s_wc[1] + s_wc[2] + s_wc[3];
+  __syncthreads();
+  const int np = s_np;
+  const uint4* cur_desc = reinterpret_cast<const uint4*>(a.desc + lb * 32);
+  const uint4* last_desc = reinterpret_cast<const uint4*>(a.last_desc + lb * 32);
+  int total = 0;
+  for (int pass = 0; pass < 2; pass++) {
+    const double o0 = pass ? 10.0 : 0, o1 = pass ? -0.1 : 0, o2 = pass ? -0.1 : 0, o3 = pass ? 5 : 0;
+    for (int w = t; w < kLineKeep * ((kLineKeep + 31) / 32); w += 256) (&s_ok[0][0])[w] = 0;
+    if (t == 0) s_cnt = 0;
+    __syncthreads();
+    for (int pr = t; pr < ncur * np; pr += 256) {
+      const int j = pr / np, i = pr - j * np;
+      const orbpl_keyline kc = a.kl_un[lb + j];
+      if (line_matching(s_kl[i], kc, last_desc + 2 * s_src[i], cur_desc + 2 * j, o0, o1, o2, o3))
+        atomicOr(&s_ok[j][i >> 5], 1u << (i & 31));
+    }
+    __syncthreads();
+    int cnt = 0;
+    if (t < ncur) {
+      int last = -1;
+      for (int w = 0; w < (kLineKeep + 31) / 32; w++) {
+        const unsigned b = s_ok[t][w];
+        cnt += __popc(b);
+        if (b) last = w * 32 + 31 - __clz(b);
+      }
+      a.lmatch[lb + t] = last >= 0 ? s_src[last] : -1;
+    }
+    atomicAdd(&s_cnt, cnt);
+    __syncthreads();
+    total = s_cnt;
+    // retry with relaxed thresholds (LineMatcher.cpp:235-261); 0/0 is not < 0.2
+    if (pass == 0 && !(total * 1.0 / ncur < 0.2)) break;
+    __syncthreads();
+  }
+  if (t == 0) st[s].nlmatches = total;
+}
+
+void launch_line_prepare(const TrackConsts& c, const LineTrackArgs& a, int nstreams,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(k_line_prepare, dim3(nstreams), dim3(64), 0, s, c, a);
+}
+
+void launch_line_match(const TrackConsts& c, const LineTrackArgs& a, StreamState* st,
+                       int nstreams, hipStream_t s) {
+  hipLaunchKernelGGL(k_line_match, dim3(nstreams), dim3(256), 0, s, c, a, st);
+}
+
+}  // namespace orbpl

@@ -126,6 +126,47 @@ int lsd_geometry(int W, int H, LsdGeom* out) {
 }
 }  // namespace orbpl
 
+namespace orbpl {
+// Detection (and, with `out`, KeyLines + LBD) of `batch` frames on stream `s`.
+// The tracker calls this with its own per-frame output buffers and stream;
+// `ev_mid` (optional) is recorded between LSD and the LineExtractor stages.
+int lsdx_run(lsdx_ctx* c, const uint8_t* d_imgs, int batch, int stride, int64_t frame_pitch,
+             const LineOut* out, hipStream_t s, hipEvent_t ev_mid) {
+  const LsdGeom& g = c->g;
+  HIP_CHECK(hipMemsetAsync(c->sc.maxq, 0, (size_t)batch * 4, s));
+  HIP_CHECK(hipMemsetAsync(c->sc.err, 0, (size_t)batch * 4, s));
+  launch_lsd_blur(g, d_imgs, stride, frame_pitch, c->sc.blur, batch, s);
+  launch_lsd_resize(g, c->d_tabs, c->sc.blur, c->sc.scaled, batch, s);
+  launch_lsd_grad(g, c->sc.scaled, c->sc.deg, c->sc.q, c->sc.maxq, batch, s);
+  launch_lsd_sort(g, c->sc, batch, s);
+  launch_lsd_grow(g, c->sc, batch, s);
+  launch_lsd_validate(g, c->sc, batch, s);
+  if (ev_mid) HIP_CHECK(hipEventRecord(ev_mid, s));
+  if (out) {
+    LineOut o = *out;
+    o.kl_all = c->lo.kl_all;  // per-frame scratch of the full detection
+    launch_keylines(c->g, c->sc, o, batch, s);
+    launch_lsd_blur(c->g5, d_imgs, stride, frame_pitch, c->blur5, batch, s);
+    launch_sobel(c->W, c->H, c->blur5, c->sdx, c->sdy, batch, s);
+    launch_lbd(c->W, c->H, c->sdx, c->sdy, c->lw, o, batch, s);
+  }
+  HIP_CHECK(hipGetLastError());
+  return ORBPL_OK;
+}
+
+// Device-side capacity flags of the last `batch` frames (caller synchronised).
+int lsdx_check(lsdx_ctx* c, int batch) {
+  std::vector<int> err(batch);
+  HIP_CHECK(hipMemcpy(err.data(), c->sc.err, err.size() * 4, hipMemcpyDeviceToHost));
+  for (int e : err)
+    if (e) {
+      arg_fail("LSD scratch capacity exceeded on device");
+      return ORBPL_ERR_OVERFLOW;
+    }
+  return ORBPL_OK;
+}
+}  // namespace orbpl
+
 extern "C" {
 
 int lsdx_destroy(lsdx_ctx* c) {
@@ -236,31 +277,20 @@ int lsdx_detect_batch_device(lsdx_ctx* c, const uint8_t* d_imgs, int batch, int 
   if (!c || !d_imgs || batch <= 0 || batch > c->max_batch) return arg_fail("bad argument");
   if (stride < c->W) return arg_fail("stride < width");
   HIP_CHECK(hipSetDevice(c->device));
-  const LsdGeom& g = c->g;
-  hipStream_t s = c->stream;
-  HIP_CHECK(hipMemsetAsync(c->sc.maxq, 0, (size_t)batch * 4, s));
-  HIP_CHECK(hipMemsetAsync(c->sc.err, 0, (size_t)batch * 4, s));
-  launch_lsd_blur(g, d_imgs, stride, frame_pitch, c->sc.blur, batch, s);
-  launch_lsd_resize(g, c->d_tabs, c->sc.blur, c->sc.scaled, batch, s);
-  launch_lsd_grad(g, c->sc.scaled, c->sc.deg, c->sc.q, c->sc.maxq, batch, s);
-  launch_lsd_sort(g, c->sc, batch, s);
-  launch_lsd_grow(g, c->sc, batch, s);
-  launch_lsd_validate(g, c->sc, batch, s);
-  HIP_CHECK(hipGetLastError());
+  int rc = orbpl::lsdx_run(c, d_imgs, batch, stride, frame_pitch, nullptr, c->stream, nullptr);
+  if (rc) return rc;
   c->last_batch = batch;
   return ORBPL_OK;
 }
 
 int lsdx_extract_batch_device(lsdx_ctx* c, const uint8_t* d_imgs, int batch, int stride,
                               int64_t frame_pitch) {
-  int rc = lsdx_detect_batch_device(c, d_imgs, batch, stride, frame_pitch);
+  if (!c || !d_imgs || batch <= 0 || batch > c->max_batch) return arg_fail("bad argument");
+  if (stride < c->W) return arg_fail("stride < width");
+  HIP_CHECK(hipSetDevice(c->device));
+  int rc = orbpl::lsdx_run(c, d_imgs, batch, stride, frame_pitch, &c->lo, c->stream, nullptr);
   if (rc) return rc;
-  hipStream_t s = c->stream;
-  launch_keylines(c->g, c->sc, c->lo, batch, s);
-  launch_lsd_blur(c->g5, d_imgs, stride, frame_pitch, c->blur5, batch, s);
-  launch_sobel(c->W, c->H, c->blur5, c->sdx, c->sdy, batch, s);
-  launch_lbd(c->W, c->H, c->sdx, c->sdy, c->lw, c->lo, batch, s);
-  HIP_CHECK(hipGetLastError());
+  c->last_batch = batch;
   return ORBPL_OK;
 }
 
@@ -311,16 +341,7 @@ int lsdx_synchronize(lsdx_ctx* c) {
   if (!c) return arg_fail("NULL context");
   HIP_CHECK(hipSetDevice(c->device));
   HIP_CHECK(hipStreamSynchronize(c->stream));
-  if (c->last_batch > 0) {
-    std::vector<int> err(c->last_batch);
-    HIP_CHECK(hipMemcpy(err.data(), c->sc.err, err.size() * 4, hipMemcpyDeviceToHost));
-    for (int e : err)
-      if (e) {
-        arg_fail("LSD scratch capacity exceeded on device");
-        return ORBPL_ERR_OVERFLOW;
-      }
-  }
-  return ORBPL_OK;
+  return c->last_batch > 0 ? orbpl::lsdx_check(c, c->last_batch) : ORBPL_OK;
 }
 
 int lsdx_get_lines(lsdx_ctx* c, int frame, float* lines, int cap, int* n_out) {

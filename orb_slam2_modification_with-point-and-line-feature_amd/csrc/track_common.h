@@ -124,7 +124,8 @@ struct StreamState {
   int ninliers;        // PoseOptimization return value
   int nmatches_map;    // inliers after discarding outliers
   int ok;              // TrackWithMotionModel success
-  int pad[2];
+  int nlmatches;       // LineMatcher::SearchByProjection result (lines enabled)
+  int nlmatches_map;   // line inliers minus outliers (Tracking.cc:1298-1314)
 };
 
 }  // namespace orbpl

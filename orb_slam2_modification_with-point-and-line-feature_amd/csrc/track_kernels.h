@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include "track_common.h"
+#include "../../include/orbpl.h"
 
 namespace orbpl {
 
@@ -60,7 +61,40 @@ struct PoseLaunch {
   int nm_stride;
   const StreamState* active;
   PoseEdge* edges;
+  // tracker-mode lines (per stream, pitch lpitch): current undistorted
+  // KeyLines, their matched last-frame line, the last frame's map lines
+  const orbpl_keyline* t_kl_un;
+  const int* t_lmatch;
+  const float* t_ml_xyz;
+  const int* t_nl;
+  uint8_t* t_loutlier;
+  int lpitch;
 };
+
+// Per-frame line buffers of the tracker (kLineKeep lines per stream).
+struct LineTrackArgs {
+  const int* nl;                 // lines per stream (current frame)
+  const orbpl_keyline* kl;       // KeyLines as extracted (distorted)
+  orbpl_keyline* kl_un;          // UndistortKeyLines
+  const float* depth;            // depth images
+  long long depth_pitch;
+  float* dstart;                 // mvDepthLineStart (-1 = none)
+  float* dend;                   // mvDepthLineEnd
+  int* lmatch;                   // matched last-frame line, -1 = none
+  uint8_t* loutlier;             // mvbLineOutlier
+  const uint8_t* desc;           // current LBD rows
+  const int* last_nl;
+  const orbpl_keyline* last_kl_un;
+  const uint8_t* last_has_ml;
+  const uint8_t* last_loutlier;
+  const float* last_ml_xyz;      // 6 floats per line: world start, end
+  const uint8_t* last_desc;
+};
+
+void launch_line_prepare(const TrackConsts& c, const LineTrackArgs& a, int nstreams,
+                         hipStream_t s);
+void launch_line_match(const TrackConsts& c, const LineTrackArgs& a, StreamState* st,
+                       int nstreams, hipStream_t s);
 
 size_t match_smem_bytes();
 size_t pose_smem_bytes();
@@ -72,8 +106,21 @@ void launch_frame_prepare(const TrackConsts& c, const KeyPointD* kps, const int*
 void launch_predict(StreamState* st, int nstreams, hipStream_t s);
 void launch_match_last(const TrackConsts& c, const MatchLaunch& m, int nstreams, hipStream_t s);
 void launch_pose(const TrackConsts& c, const PoseLaunch& p, int nstreams, hipStream_t s);
+// Line part of k_finish (all NULL when lines are disabled).
+struct LineFinish {
+  const int* nl;
+  int* lmatch;
+  uint8_t* loutlier;
+  const float* dstart;
+  const float* dend;
+  const orbpl_keyline* kl_un;
+  uint8_t* has_ml;
+  float* ml_xyz;
+};
+
 void launch_finish(const TrackConsts& c, StreamState* st, const int* n, int kp_pitch,
                    const KeyPointD* kps_un, const float* depth, int* match, uint8_t* outlier,
-                   uint8_t* has_mp, float* mp_xyz, int* nobs, int nstreams, hipStream_t s);
+                   uint8_t* has_mp, float* mp_xyz, int* nobs, const LineFinish& lf, int nstreams,
+                   hipStream_t s);
 
 }  // namespace orbpl

@@ -21,6 +21,7 @@
 #include "orbpl_math.h"
 #include "track_common.h"
 #include "track_kernels.h"
+#include "lsd_kernels.h"
 
 namespace orbpl {
 
@@ -883,6 +884,13 @@ struct PoseArgs {
   int nm_stride;
   const StreamState* active;
   PoseEdge* edges;            // scratch, per stream kPoseMaxEdges
+  // tracker-mode lines (see PoseLaunch)
+  const orbpl_keyline* t_kl_un;
+  const int* t_lmatch;
+  const float* t_ml_xyz;
+  const int* t_nl;
+  uint8_t* t_loutlier;
+  int lpitch;
 };
 
 __device__ void se3_from_T(const float* T, SE3d& s) {
@@ -900,7 +908,9 @@ __global__ void __launch_bounds__(256) k_pose(TrackConsts tc, PoseArgs a) {
   const int s = blockIdx.x, t = threadIdx.x;
   // TrackWithMotionModel returns before optimising when no last frame exists
   // or nmatches < 20 after the retry (Tracking.cc:1255-1265).
-  if (a.active && (!a.active[s].has_last || a.active[s].nmatches < 20)) {
+  // (with lines: also when LineMatcher found < 15, Tracking.cc:1260-1265)
+  if (a.active && (!a.active[s].has_last || a.active[s].nmatches < 20 ||
+                   (a.t_kl_un && a.active[s].nlmatches < 15))) {
     if (t == 0) a.ninliers[(long long)s * a.nm_stride] = 0;
     return;
   }
@@ -960,7 +970,37 @@ __global__ void __launch_bounds__(256) k_pose(TrackConsts tc, PoseArgs a) {
   }
   npts = min(npts, kPoseMaxEdges);
   int nlines = 0;
-  if (t == 0) {
+  if (t == 0 && a.t_kl_un) {
+    // tracker mode: edges for the current lines matched to last-frame map lines
+    int ne = npts;
+    const long long lb = (long long)s * a.lpitch;
+    const int nlc = a.t_nl[s];
+    for (int i = 0; i < nlc; i++) {
+      const int m = a.t_lmatch[lb + i];
+      if (m < 0) continue;
+      if (ne >= kPoseMaxEdges) break;
+      if (i < n) outl[i] = 0;  // reference writes mvbOutlier here (Optimizer.cc:2308)
+      const orbpl_keyline kl = a.t_kl_un[lb + i];
+      PoseEdge e;
+      e.kind = 2;
+      e.idx = i;
+      e.obs[0] = kl.startPointX;
+      e.obs[1] = kl.startPointY;
+      e.obs[2] = kl.endPointX;
+      e.obs[3] = kl.endPointY;
+      e.info = tc.inv_sigma2[kl.octave];
+      const float* X = a.t_ml_xyz + (lb + m) * 6;
+      for (int q = 0; q < 6; q++) e.X[q] = X[q];
+      e.pad = 0;
+      E[ne] = e;
+      S.level[ne] = 0;
+      S.out_flag[ne] = a.t_loutlier[lb + i];
+      ne++;
+      nlines++;
+    }
+    S.misc[0] = ne;
+    S.misc[2] = nlines;
+  } else if (t == 0) {
     int ne = npts;
     for (int i = 0; i < a.nl; i++) {
       if (!a.has_ml[i]) continue;
@@ -1177,7 +1217,10 @@ __global__ void __launch_bounds__(256) k_pose(TrackConsts tc, PoseArgs a) {
   }
   for (int k = t; k < ne; k += 256) {
     const PoseEdge e = E[k];
-    if (e.kind == 2) a.line_outlier[e.idx] = S.out_flag[k];
+    if (e.kind == 2) {
+      if (a.t_kl_un) a.t_loutlier[(long long)s * a.lpitch + e.idx] = S.out_flag[k];
+      else a.line_outlier[e.idx] = S.out_flag[k];
+    }
   }
   if (t == 0) a.ninliers[(long long)s * a.nm_stride] = npts - nBadOut;
 }
@@ -1195,15 +1238,18 @@ __global__ void __launch_bounds__(256) k_finish(TrackConsts c, StreamState* __re
                                                 uint8_t* __restrict__ outlier,
                                                 uint8_t* __restrict__ has_mp,
                                                 float* __restrict__ mp_xyz,
-                                                int* __restrict__ nobs) {
+                                                int* __restrict__ nobs, LineFinish lf) {
   const int s = blockIdx.x, t = threadIdx.x;
   StreamState& S = st[s];
   const int n = n_in[s];
   const long long cb = (long long)s * kp_pitch;
   __shared__ float sT[16];
-  __shared__ int s_map;
+  __shared__ int s_map, s_lmap;
   if (t < 16) sT[t] = S.Tcw[t];
-  if (t == 0) s_map = 0;
+  if (t == 0) {
+    s_map = 0;
+    s_lmap = 0;
+  }
   __syncthreads();
   float Ow[3];
   gemm_neg_Rt_t(sT, Ow);
@@ -1233,10 +1279,50 @@ __global__ void __launch_bounds__(256) k_finish(TrackConsts c, StreamState* __re
     }
   }
   if (nmap) atomicAdd(&s_map, nmap);
+  if (lf.nl) {
+    // lines: outlier discard (Tracking.cc:1298-1314; outliers decrement the
+    // count there) and the next frame's map lines (StereoInitialization,
+    // Tracking.cc:668-690; the end point is unprojected with the start
+    // point's depth, Frame.cc:1192)
+    const long long lb = (long long)s * kLineKeep;
+    const int nl = lf.nl[s];
+    int lmap = 0;
+    for (int j = t; j < nl; j += 256) {
+      const long long o = lb + j;
+      if (S.has_last && lf.lmatch[o] >= 0) {
+        if (lf.loutlier[o]) {
+          lf.lmatch[o] = -1;
+          lmap--;
+        } else {
+          lmap++;
+        }
+      }
+      lf.loutlier[o] = 0;
+      const float zs = lf.dstart[o], ze = lf.dend[o];
+      if (zs > 0 && ze > 0) {
+        const orbpl_keyline k = lf.kl_un[o];
+        const float a3[3] = {(k.startPointX - c.cx) * zs * c.invfx, (k.startPointY - c.cy) * zs * c.invfy, zs};
+        const float b3[3] = {(k.endPointX - c.cx) * zs * c.invfx, (k.endPointY - c.cy) * zs * c.invfy, zs};
+        gemm_Rt_x_plus_c(sT, a3, Ow, lf.ml_xyz + o * 6);
+        gemm_Rt_x_plus_c(sT, b3, Ow, lf.ml_xyz + o * 6 + 3);
+        lf.has_ml[o] = 1;
+      } else {
+        lf.has_ml[o] = 0;
+      }
+    }
+    if (lmap) atomicAdd(&s_lmap, lmap);
+  }
   __syncthreads();
   if (t == 0) {
     S.nmatches_map = s_map;
-    S.ok = S.has_last ? (S.nmatches >= 20 && s_map >= 10) : 1;
+    if (lf.nl) {
+      S.nlmatches_map = s_lmap;
+      const bool tracked = S.nmatches >= 20 && S.nlmatches >= 15;
+      S.ok = S.has_last ? (tracked && (s_map >= 10 || s_lmap >= 15)) : 1;
+    } else {
+      S.nlmatches_map = 0;
+      S.ok = S.has_last ? (S.nmatches >= 20 && s_map >= 10) : 1;
+    }
     for (int k = 0; k < 16; k++) {
       S.Tlast2[k] = S.Tlast[k];
       S.Tlast[k] = S.Tcw[k];
@@ -1331,14 +1417,21 @@ void launch_pose(const TrackConsts& c, const PoseLaunch& p, int nstreams, hipStr
   a.nm_stride = p.nm_stride;
   a.active = p.active;
   a.edges = p.edges;
+  a.t_kl_un = p.t_kl_un;
+  a.t_lmatch = p.t_lmatch;
+  a.t_ml_xyz = p.t_ml_xyz;
+  a.t_nl = p.t_nl;
+  a.t_loutlier = p.t_loutlier;
+  a.lpitch = p.lpitch;
   hipLaunchKernelGGL(k_pose, dim3(nstreams), dim3(256), sizeof(PoseShared), s, c, a);
 }
 
 void launch_finish(const TrackConsts& c, StreamState* st, const int* n, int kp_pitch,
                    const KeyPointD* kps_un, const float* depth, int* match, uint8_t* outlier,
-                   uint8_t* has_mp, float* mp_xyz, int* nobs, int nstreams, hipStream_t s) {
+                   uint8_t* has_mp, float* mp_xyz, int* nobs, const LineFinish& lf, int nstreams,
+                   hipStream_t s) {
   hipLaunchKernelGGL(k_finish, dim3(nstreams), dim3(256), 0, s, c, st, n, kp_pitch, kps_un, depth,
-                     match, outlier, has_mp, mp_xyz, nobs);
+                     match, outlier, has_mp, mp_xyz, nobs, lf);
 }
 
 }  // namespace orbpl

@@ -14,6 +14,7 @@
 #include "orb_kernels.h"
 #include "orbpl_runtime.h"
 #include "track_kernels.h"
+#include "lsd_kernels.h"
 
 using namespace orbpl;
 
@@ -289,6 +290,18 @@ struct FrameBufs {
   uint8_t* has_mp = nullptr;
   float* mp_xyz = nullptr;
   int* nobs = nullptr;
+  // lines (kLineKeep per stream)
+  orbpl_keyline* kl = nullptr;
+  orbpl_keyline* kl_un = nullptr;
+  uint8_t* ldesc = nullptr;
+  double* lcoef = nullptr;
+  int* nl = nullptr;
+  float* dstart = nullptr;
+  float* dend = nullptr;
+  int* lmatch = nullptr;
+  uint8_t* loutlier = nullptr;
+  uint8_t* has_ml = nullptr;
+  float* ml_xyz = nullptr;
 };
 
 struct orbpl_tracker {
@@ -307,10 +320,16 @@ struct orbpl_tracker {
   hipEvent_t ev_free[3] = {};      // fb[b] no longer read as "last frame"
   bool free_pending[3] = {};
   int pipelined = 0;               // 0: every stage on `stream`
+  // line features (ORBPL_TRACK_LINES): LSD + LBD + UndistortKeyLines run on
+  // their own stream, concurrently with the ORB extraction of the same step
+  int lines = 0;
+  lsdx_ctx* lx = nullptr;
+  hipStream_t lstream = nullptr;
+  hipEvent_t ev_in = nullptr;      // step start on `stream`
   StreamState* d_state = nullptr;
   PoseEdge* d_edges = nullptr;
   static constexpr int kRing = 64;   // steps kept in the timing ring
-  static constexpr int kEv = 11;     // events per step
+  static constexpr int kEv = 15;     // events per step
   std::vector<hipEvent_t> ring;      // kRing * kEv events
   int ring_pos = 0, ring_count = 0;
   std::vector<void*> allocs;
@@ -338,7 +357,11 @@ int orbpl_tracker_destroy(orbpl_tracker* t) {
     if (e) (void)hipEventDestroy(e);
   for (auto& e : t->ev_free)
     if (e) (void)hipEventDestroy(e);
+  if (t->lstream) (void)hipStreamSynchronize(t->lstream);
+  if (t->ev_in) (void)hipEventDestroy(t->ev_in);
   if (t->tstream) (void)hipStreamDestroy(t->tstream);
+  if (t->lstream) (void)hipStreamDestroy(t->lstream);
+  if (t->lx) lsdx_destroy(t->lx);
   if (t->ex) orbx_destroy(t->ex);
   delete t;
   return ORBPL_OK;
@@ -346,10 +369,17 @@ int orbpl_tracker_destroy(orbpl_tracker* t) {
 
 int orbpl_tracker_create(const orbpl_orb_params* orb, const orbpl_camera* cam, int n_streams,
                          int device, orbpl_tracker** out) {
+  return orbpl_tracker_create_ex(orb, cam, n_streams, device, 0, out);
+}
+
+int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam, int n_streams,
+                            int device, int flags, orbpl_tracker** out) {
   if (!orb || !cam || !out || n_streams <= 0) return arg_fail("bad argument");
+  if (flags & ~ORBPL_TRACK_LINES) return arg_fail("unknown tracker flag");
   *out = nullptr;
   orbpl_tracker* t = new orbpl_tracker();
   t->device = device;
+  t->lines = (flags & ORBPL_TRACK_LINES) ? 1 : 0;
   t->S = n_streams;
   t->W = cam->width;
   t->H = cam->height;
@@ -392,6 +422,20 @@ int orbpl_tracker_create(const orbpl_orb_params* orb, const orbpl_camera* cam, i
     TA(f.has_mp, S * K);
     TA(f.mp_xyz, S * K * 12);
     TA(f.nobs, S * K * 4);
+    if (t->lines) {
+      const size_t L = S * kLineKeep;
+      TA(f.kl, L * sizeof(orbpl_keyline));
+      TA(f.kl_un, L * sizeof(orbpl_keyline));
+      TA(f.ldesc, L * 32);
+      TA(f.lcoef, L * 3 * sizeof(double));
+      TA(f.nl, S * 4);
+      TA(f.dstart, L * 4);
+      TA(f.dend, L * 4);
+      TA(f.lmatch, L * 4);
+      TA(f.loutlier, L);
+      TA(f.has_ml, L);
+      TA(f.ml_xyz, L * 6 * 4);
+    }
   }
   TA(t->d_state, S * sizeof(StreamState));
   TA(t->d_edges, S * kPoseMaxEdges * pose_edge_bytes());
@@ -410,6 +454,18 @@ int orbpl_tracker_create(const orbpl_orb_params* orb, const orbpl_camera* cam, i
   if (hipStreamCreateWithFlags(&t->tstream, hipStreamNonBlocking) != hipSuccess) {
     orbpl_tracker_destroy(t);
     return hip_fail(hipErrorUnknown, "hipStreamCreate", __LINE__);
+  }
+  if (t->lines) {
+    rc = lsdx_create(cam->width, cam->height, n_streams, device, &t->lx);
+    if (rc) {
+      orbpl_tracker_destroy(t);
+      return rc;
+    }
+    if (hipStreamCreateWithFlags(&t->lstream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&t->ev_in, hipEventDisableTiming) != hipSuccess) {
+      orbpl_tracker_destroy(t);
+      return hip_fail(hipErrorUnknown, "hipStreamCreate", __LINE__);
+    }
   }
   rc = orbpl_tracker_reset(t, nullptr);
   if (rc) {
@@ -431,6 +487,7 @@ int orbpl_tracker_reset(orbpl_tracker* t, const float* Tcw0) {
   }
   HIP_CHECK(hipStreamSynchronize(t->stream));
   if (t->tstream) HIP_CHECK(hipStreamSynchronize(t->tstream));
+  if (t->lstream) HIP_CHECK(hipStreamSynchronize(t->lstream));
   HIP_CHECK(hipMemcpy(t->d_state, st.data(), sizeof(StreamState) * t->S, hipMemcpyHostToDevice));
   return ORBPL_OK;
 }
@@ -452,6 +509,38 @@ int orbpl_tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_d
   hipEvent_t* ev = &t->ring[(size_t)(t->ring_pos % orbpl_tracker::kRing) * orbpl_tracker::kEv];
   // ---- extraction stream: wait until tracking of step t-1 released fb[ci]
   if (t->free_pending[ci]) HIP_CHECK(hipStreamWaitEvent(s, t->ev_free[ci], 0));
+  LineTrackArgs la{};
+  if (t->lines) {
+    // ---- line stream: LineExtractor + UndistortKeyLines + line depths
+    HIP_CHECK(hipEventRecord(t->ev_in, s));
+    HIP_CHECK(hipStreamWaitEvent(t->lstream, t->ev_in, 0));
+    HIP_CHECK(hipEventRecord(ev[11], t->lstream));
+    LineOut lo{};
+    lo.kl = C.kl;
+    lo.desc = C.ldesc;
+    lo.coef = C.lcoef;
+    lo.n = C.nl;
+    int lrc = lsdx_run(t->lx, d_gray, S, t->W, (int64_t)t->W * t->H, &lo, t->lstream, ev[12]);
+    if (lrc) return lrc;
+    la.nl = C.nl;
+    la.kl = C.kl;
+    la.kl_un = C.kl_un;
+    la.depth = d_depth;
+    la.depth_pitch = (long long)t->W * t->H;
+    la.dstart = C.dstart;
+    la.dend = C.dend;
+    la.lmatch = C.lmatch;
+    la.loutlier = C.loutlier;
+    la.desc = C.ldesc;
+    la.last_nl = L.nl;
+    la.last_kl_un = L.kl_un;
+    la.last_has_ml = L.has_ml;
+    la.last_loutlier = L.loutlier;
+    la.last_ml_xyz = L.ml_xyz;
+    la.last_desc = L.ldesc;
+    launch_line_prepare(t->consts, la, S, t->lstream);
+    HIP_CHECK(hipEventRecord(ev[13], t->lstream));
+  }
   int rc = orbx_run(t->ex, d_gray, S, t->W, (long long)t->W * t->H,
                     reinterpret_cast<orbpl_keypoint_dev*>(C.kps), C.desc, K, C.n, ev);
   if (rc) return rc;
@@ -460,6 +549,7 @@ int orbpl_tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_d
   HIP_CHECK(hipEventRecord(ev[6], s));
   // ---- tracking stream
   HIP_CHECK(hipStreamWaitEvent(ts, ev[6], 0));
+  if (t->lines) HIP_CHECK(hipStreamWaitEvent(ts, ev[13], 0));
   HIP_CHECK(hipEventRecord(ev[7], ts));
   launch_predict(t->d_state, S, ts);
   MatchLaunch m{};
@@ -489,6 +579,8 @@ int orbpl_tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_d
   m.active = t->d_state;
   launch_match_last(t->consts, m, S, ts);
   HIP_CHECK(hipEventRecord(ev[8], ts));
+  if (t->lines) launch_line_match(t->consts, la, t->d_state, S, ts);
+  HIP_CHECK(hipEventRecord(ev[14], ts));
   PoseLaunch p{};
   p.kps_un = C.kps_un;
   p.uright = C.uright;
@@ -506,10 +598,29 @@ int orbpl_tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_d
   p.nm_stride = pstride;
   p.active = t->d_state;
   p.edges = t->d_edges;
+  if (t->lines) {
+    p.t_kl_un = C.kl_un;
+    p.t_lmatch = C.lmatch;
+    p.t_ml_xyz = L.ml_xyz;
+    p.t_nl = C.nl;
+    p.t_loutlier = C.loutlier;
+    p.lpitch = kLineKeep;
+  }
   launch_pose(t->consts, p, S, ts);
   HIP_CHECK(hipEventRecord(ev[9], ts));
+  LineFinish lf{};
+  if (t->lines) {
+    lf.nl = C.nl;
+    lf.lmatch = C.lmatch;
+    lf.loutlier = C.loutlier;
+    lf.dstart = C.dstart;
+    lf.dend = C.dend;
+    lf.kl_un = C.kl_un;
+    lf.has_ml = C.has_ml;
+    lf.ml_xyz = C.ml_xyz;
+  }
   launch_finish(t->consts, t->d_state, C.n, K, C.kps_un, C.depth, C.match, C.outlier, C.has_mp,
-                C.mp_xyz, C.nobs, S, ts);
+                C.mp_xyz, C.nobs, lf, S, ts);
   HIP_CHECK(hipEventRecord(ev[10], ts));
   HIP_CHECK(hipEventRecord(t->ev_free[li], ts));
   t->free_pending[li] = true;
@@ -532,6 +643,11 @@ int orbpl_tracker_synchronize(orbpl_tracker* t) {
   if (!t) return arg_fail("NULL tracker");
   HIP_CHECK(hipSetDevice(t->device));
   HIP_CHECK(hipStreamSynchronize(t->tstream));
+  if (t->lines) {
+    HIP_CHECK(hipStreamSynchronize(t->lstream));
+    int rc = lsdx_check(t->lx, t->S);
+    if (rc) return rc;
+  }
   return orbx_synchronize(t->ex);
 }
 
@@ -541,6 +657,7 @@ int orbpl_tracker_get_state(orbpl_tracker* t, float* Tcw, int* nkps, int* nmatch
   HIP_CHECK(hipSetDevice(t->device));
   HIP_CHECK(hipStreamSynchronize(t->stream));
   HIP_CHECK(hipStreamSynchronize(t->tstream));
+  if (t->lines) HIP_CHECK(hipStreamSynchronize(t->lstream));
   std::vector<StreamState> st(t->S);
   HIP_CHECK(hipMemcpy(st.data(), t->d_state, sizeof(StreamState) * t->S, hipMemcpyDeviceToHost));
   std::vector<int> n(t->S);
@@ -563,13 +680,34 @@ int orbpl_tracker_timings(orbpl_tracker* t, int max_steps, float* ms, int* n_ste
   HIP_CHECK(hipStreamSynchronize(t->tstream));
   // stage intervals: 5 extraction stages, glue (extraction stream), then
   // match (incl. prediction), pose, finish (tracking stream)
-  static const int kPair[9][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 6}, {7, 8}, {8, 9}, {9, 10}};
+  static const int kPair[9][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 6}, {7, 8}, {14, 9}, {9, 10}};
   const int n = std::min(max_steps, t->ring_count);
   for (int k = 0; k < n; k++) {
     const int step = t->ring_pos - n + k;
     hipEvent_t* ev = &t->ring[(size_t)(step % orbpl_tracker::kRing) * orbpl_tracker::kEv];
     for (int i = 0; i < 9; i++)
       HIP_CHECK(hipEventElapsedTime(&ms[k * 9 + i], ev[kPair[i][0]], ev[kPair[i][1]]));
+  }
+  *n_steps = n;
+  return ORBPL_OK;
+}
+
+int orbpl_tracker_line_timings(orbpl_tracker* t, int max_steps, float* ms, int* n_steps) {
+  if (!t || !ms || !n_steps) return arg_fail("NULL argument");
+  if (!t->lines) return arg_fail("tracker created without ORBPL_TRACK_LINES");
+  HIP_CHECK(hipSetDevice(t->device));
+  HIP_CHECK(hipStreamSynchronize(t->stream));
+  HIP_CHECK(hipStreamSynchronize(t->tstream));
+  HIP_CHECK(hipStreamSynchronize(t->lstream));
+  // LSD (line stream), KeyLines + LBD + UndistortKeyLines (line stream),
+  // LineMatcher::SearchByProjection (tracking stream)
+  static const int kPair[3][2] = {{11, 12}, {12, 13}, {8, 14}};
+  const int n = std::min(max_steps, t->ring_count);
+  for (int k = 0; k < n; k++) {
+    const int step = t->ring_pos - n + k;
+    hipEvent_t* ev = &t->ring[(size_t)(step % orbpl_tracker::kRing) * orbpl_tracker::kEv];
+    for (int i = 0; i < 3; i++)
+      HIP_CHECK(hipEventElapsedTime(&ms[k * 3 + i], ev[kPair[i][0]], ev[kPair[i][1]]));
   }
   *n_steps = n;
   return ORBPL_OK;
@@ -610,6 +748,47 @@ int orbpl_tracker_get_frame(orbpl_tracker* t, int stream, orbpl_keypoint* kps_un
   if (desc) HIP_CHECK(hipMemcpy(desc, F.desc + o * 32, K * 32, hipMemcpyDeviceToHost));
   if (match) HIP_CHECK(hipMemcpy(match, F.match + o, K * 4, hipMemcpyDeviceToHost));
   if (outlier) HIP_CHECK(hipMemcpy(outlier, F.outlier + o, K, hipMemcpyDeviceToHost));
+  return ORBPL_OK;
+}
+
+int orbpl_tracker_get_status(orbpl_tracker* t, int* ok, int* nlines, int* line_matches,
+                             int* line_nmatches_map) {
+  if (!t) return arg_fail("NULL tracker");
+  HIP_CHECK(hipSetDevice(t->device));
+  HIP_CHECK(hipStreamSynchronize(t->stream));
+  HIP_CHECK(hipStreamSynchronize(t->tstream));
+  if (t->lines) HIP_CHECK(hipStreamSynchronize(t->lstream));
+  std::vector<StreamState> st(t->S);
+  HIP_CHECK(hipMemcpy(st.data(), t->d_state, sizeof(StreamState) * t->S, hipMemcpyDeviceToHost));
+  std::vector<int> nl(t->S, 0);
+  if (t->lines)
+    HIP_CHECK(hipMemcpy(nl.data(), t->fb[(t->ring_pos + 2) % 3].nl, 4 * t->S, hipMemcpyDeviceToHost));
+  for (int s = 0; s < t->S; s++) {
+    if (ok) ok[s] = st[s].ok;
+    if (nlines) nlines[s] = nl[s];
+    if (line_matches) line_matches[s] = t->lines ? st[s].nlmatches : 0;
+    if (line_nmatches_map) line_nmatches_map[s] = t->lines ? st[s].nlmatches_map : 0;
+  }
+  return ORBPL_OK;
+}
+
+int orbpl_tracker_get_lines(orbpl_tracker* t, int stream, orbpl_keyline* kl_un, uint8_t* desc,
+                            int32_t* lmatch, uint8_t* loutlier, int* n) {
+  if (!t || stream < 0 || stream >= t->S) return arg_fail("bad argument");
+  if (!t->lines) return arg_fail("tracker created without ORBPL_TRACK_LINES");
+  HIP_CHECK(hipSetDevice(t->device));
+  HIP_CHECK(hipStreamSynchronize(t->stream));
+  HIP_CHECK(hipStreamSynchronize(t->tstream));
+  HIP_CHECK(hipStreamSynchronize(t->lstream));
+  const FrameBufs& F = t->fb[(t->ring_pos + 2) % 3];
+  const size_t K = kLineKeep, o = (size_t)stream * K;
+  int cnt = 0;
+  HIP_CHECK(hipMemcpy(&cnt, F.nl + stream, 4, hipMemcpyDeviceToHost));
+  if (n) *n = cnt;
+  if (kl_un) HIP_CHECK(hipMemcpy(kl_un, F.kl_un + o, K * sizeof(orbpl_keyline), hipMemcpyDeviceToHost));
+  if (desc) HIP_CHECK(hipMemcpy(desc, F.ldesc + o * 32, K * 32, hipMemcpyDeviceToHost));
+  if (lmatch) HIP_CHECK(hipMemcpy(lmatch, F.lmatch + o, K * 4, hipMemcpyDeviceToHost));
+  if (loutlier) HIP_CHECK(hipMemcpy(loutlier, F.loutlier + o, K, hipMemcpyDeviceToHost));
   return ORBPL_OK;
 }
 

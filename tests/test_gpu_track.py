@@ -173,3 +173,47 @@ def test_tracker_pipelined_matches_oracle_vo(orbpl, oracle):
         assert st["ninliers"][s] == so["ninliers"], s
         assert st["nmatches_map"][s] == so["nmatches_map"], s
         assert np.abs(st["Tcw"][s] - To).max() < POSE_TOL, s
+
+
+@pytest.mark.parametrize("pipelined", [False, True])
+def test_tracker_with_lines_matches_oracle_lvo(orbpl, oracle, pipelined):
+    """Point+line tracker (ORBPL_TRACK_LINES) against the oracle LVO loop:
+    identical point and line counts every frame, pose within POSE_TOL, and
+    the last frame's undistorted KeyLines / LBD rows bit-exact."""
+    S, F = 3, 5
+    seqs = [sequence(F, 30 + s) for s in range(S)]
+    cfg = seqs[0][0]
+    lvo = oracle.LVO(oracle.params(), oracle.camera(cfg), S, use_lines=True)
+    tr = orbpl.Tracker(orbpl.OrbParams(1000, 1.2, 8, 20, 7), orbpl.make_camera(cfg), S, lines=True)
+    tr.set_pipelined(pipelined)
+    T0 = np.stack([np.linalg.inv(sq[1][0]).astype(np.float32) for sq in seqs])
+    lvo.reset(T0.reshape(S, 16))
+    tr.reset(T0.reshape(S, 16))
+    gray = orbpl.DeviceBuffer(S * 640 * 480)
+    depth = orbpl.DeviceBuffer(S * 640 * 480 * 4)
+    for f in range(F):
+        gray.upload(np.stack([sq[2][f][0] for sq in seqs]))
+        depth.upload(np.stack([sq[2][f][1] for sq in seqs]))
+        tr.step_device(gray.ptr, depth.ptr)
+        st, ls = tr.state(), tr.status()
+        for s in range(S):
+            To, so = lvo.step(s, seqs[s][2][f][0], seqs[s][2][f][1])
+            got = dict(nkeypoints=st["nkeypoints"][s], nmatches=st["nmatches"][s],
+                       ninliers=st["ninliers"][s], nmatches_map=st["nmatches_map"][s],
+                       ok=ls["ok"][s], nlines=ls["nlines"][s], line_matches=ls["line_matches"][s],
+                       line_nmatches_map=ls["line_nmatches_map"][s])
+            assert {k: int(v) for k, v in got.items()} == so, (f, s)
+            assert np.abs(st["Tcw"][s] - To).max() < POSE_TOL, (f, s)
+    cam_o = oracle.camera(cfg)
+    for s in range(S):
+        g, d = seqs[s][2][F - 1]
+        kl, desc, _, _ = oracle.line_extract(g)
+        ku, _, _, _, _ = oracle.line_frame_prepare(cam_o, kl, d)
+        kl_g, desc_g, lm_g, lo_g = tr.lines(s)
+        assert kl_g.tobytes() == ku.tobytes()
+        assert np.array_equal(desc_g, desc)
+        assert np.all(lo_g == 0)
+        # kept matches = inliers; the map count subtracts the outliers (quirk)
+        assert (lm_g >= 0).sum() >= ls["line_nmatches_map"][s]
+    lt = tr.line_timings()
+    assert lt.shape[1] == 3 and np.all(lt >= 0)

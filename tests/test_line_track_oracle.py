@@ -1,0 +1,103 @@
+"""CPU tests of the line-tracking oracle (oracle/line_track_oracle.cpp):
+Frame::UndistortKeyLines + line depths, LineMatcher::SearchByProjection(Frame,
+Frame) and the point+line TrackWithMotionModel loop (LVO)."""
+import numpy as np
+
+from _scenes import sequence
+
+
+def test_line_frame_prepare_identity_without_distortion(oracle):
+    cfg, _, frames = sequence(1, 3, cam_name="TUM3")
+    gray, depth = frames[0]
+    kl, _, _, _ = oracle.line_extract(gray)
+    ku, ds, de, _, _ = oracle.line_frame_prepare(oracle.camera(cfg), kl, depth)
+    assert len(kl) > 20
+    # k1 == 0: UndistortKeyLines returns the key lines untouched (Frame.cc:771)
+    assert ku.tobytes() == kl.tobytes()
+    # imDepth.at<float>(v, u) at the end points, -1 where no depth (P14)
+    W, H = cfg["width"], cfg["height"]
+    for j in range(len(kl)):
+        for x, y, d in ((kl["startPointX"][j], kl["startPointY"][j], ds[j]),
+                        (kl["endPointX"][j], kl["endPointY"][j], de[j])):
+            idx = int(y) * W + int(x)
+            z = depth.reshape(-1)[idx] if 0 <= idx < W * H else 0.0
+            assert d == (z if z > 0 else -1.0)
+
+
+def test_line_frame_prepare_undistorts_end_points(oracle):
+    cfg, _, frames = sequence(1, 4, cam_name="TUM1")
+    gray, depth = frames[0]
+    kl, _, _, _ = oracle.line_extract(gray)
+    ku, _, _, _, _ = oracle.line_frame_prepare(oracle.camera(cfg), kl, depth)
+    moved = np.abs(ku["startPointX"] - kl["startPointX"]) + np.abs(ku["endPointY"] - kl["endPointY"])
+    assert moved.max() > 0.5
+    # the refreshed fields follow the undistorted end points
+    assert np.array_equal(ku["sPointInOctaveX"], ku["startPointX"])
+    assert np.array_equal(ku["ePointInOctaveY"], ku["endPointY"])
+    assert np.allclose(ku["lineLength"],
+                       np.hypot(ku["endPointX"] - ku["startPointX"],
+                                ku["endPointY"] - ku["startPointY"]), rtol=1e-5)
+
+
+def test_line_search_by_projection_finds_itself(oracle):
+    """The last frame's lines as map lines, projected with the same pose,
+    match the frame's own lines (each current line's last passing projection
+    wins, so a line may take a collinear neighbour; most keep their own)."""
+    cfg, traj, frames = sequence(1, 5, cam_name="TUM3")
+    gray, depth = frames[0]
+    cam = oracle.camera(cfg)
+    kl, desc, _, _ = oracle.line_extract(gray)
+    ku, ds, de, _, _ = oracle.line_frame_prepare(cam, kl, depth)
+    Tcw = np.linalg.inv(traj[0]).astype(np.float32)
+    Twc = np.linalg.inv(Tcw.astype(np.float64))
+    has = ((ds > 0) & (de > 0)).astype(np.uint8)
+    xyz = np.zeros((len(ku), 6), np.float32)
+    for j in range(len(ku)):
+        for e, (u, v, z) in enumerate(((ku["startPointX"][j], ku["startPointY"][j], ds[j]),
+                                       (ku["endPointX"][j], ku["endPointY"][j], de[j]))):
+            Pc = np.array([(u - cfg["cx"]) * z / cfg["fx"], (v - cfg["cy"]) * z / cfg["fy"], z, 1.0])
+            xyz[j, 3 * e:3 * e + 3] = (Twc @ Pc)[:3]
+    match, nm = oracle.line_search_by_projection_last(cam, Tcw, ku, desc, ku, has,
+                                                      np.zeros(len(ku), np.uint8), xyz, desc)
+    assert nm >= has.sum()
+    matched = match >= 0
+    assert matched.sum() >= 0.9 * has.sum()
+    assert (match[matched] == np.arange(len(ku))[matched]).mean() > 0.7
+    # lines without map lines are never matched by index
+    assert not np.isin(np.nonzero(has == 0)[0], match[matched]).any()
+
+
+def test_lvo_without_lines_equals_points_vo(oracle):
+    F = 4
+    cfg, traj, frames = sequence(F, 6)
+    T0 = np.linalg.inv(traj[0]).astype(np.float32).reshape(1, 16)
+    vo = oracle.VO(oracle.params(), oracle.camera(cfg), 1)
+    lvo = oracle.LVO(oracle.params(), oracle.camera(cfg), 1, use_lines=False)
+    vo.reset(T0)
+    lvo.reset(T0)
+    for f in range(F):
+        Ta, sa = vo.step(0, *frames[f])
+        Tb, sb = lvo.step(0, *frames[f])
+        assert np.array_equal(Ta, Tb)
+        for k in ("nkeypoints", "nmatches", "ninliers", "nmatches_map"):
+            assert sa[k] == sb[k], (f, k)
+        assert sb["nlines"] == 0 and sb["line_matches"] == 0
+
+
+def test_lvo_with_lines_tracks(oracle):
+    F = 4
+    cfg, traj, frames = sequence(F, 7)
+    T0 = np.linalg.inv(traj[0]).astype(np.float32).reshape(1, 16)
+    lvo = oracle.LVO(oracle.params(), oracle.camera(cfg), 1, use_lines=True)
+    lvo.reset(T0)
+    for f in range(F):
+        T, s = lvo.step(0, *frames[f])
+        assert 0 < s["nlines"] <= 80
+        if f:
+            assert s["line_matches"] >= 15, s
+            assert s["ok"] == 1
+            assert s["line_nmatches_map"] <= s["line_matches"]
+            # the reference's line edge (P7) pulls the pose off by centimetres
+            # at most on this scene; the tracker must stay near truth
+            Tgt = np.linalg.inv(traj[f])
+            assert np.abs(T[:3, 3] - Tgt[:3, 3]).max() < 0.2
