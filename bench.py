@@ -8,7 +8,10 @@ TUM1.yaml camera + distortion, ORB 1000 features / 1.2 / 8 levels / FAST 20,7.
 A step = one Tracking::TrackWithMotionModel pass (ORB extraction, Frame glue,
 SearchByProjection(th=15, retry 30), PoseOptimization, outlier discard) over a
 batch of `--streams` independent synthetic 640x480 RGB-D streams, all inputs
-resident in HBM before the timed region. Frames are rendered from a seeded
+resident in HBM before the timed region. The configs[2] workload (TUM3, ORB +
+LSD/LBD LineExtractor, LineMatcher::SearchByProjection, line edges in the
+pose) is timed the same way and reported under "secondary" (or as the
+headline with --workload lines). Frames are rendered from a seeded
 textured room along closed loop trajectories (no datasets on the box).
 
 Multi-GPU: one process per GPU (torchrun), streams sharded across ranks with
@@ -37,19 +40,19 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8 TB/s spec
 
 
 def _render(args):
-    i, n, seed = args
+    i, n, seed, cam_name = args
     from _pkg import load_pkg
     load_pkg()
     import orbpl.synth as synth
     traj = synth.loop_trajectory(n, seed=seed)
     room = synth.default_room(seed)
-    g, d = synth.render(synth.TUM1, traj[i], room, seed=seed * 1000 + i)
+    g, d = synth.render(getattr(synth, cam_name), traj[i], room, seed=seed * 1000 + i)
     return g, d
 
 
-def render_loop(n, seed, workers):
+def render_loop(n, seed, workers, cam_name="TUM1"):
     with ProcessPoolExecutor(max_workers=workers) as ex:
-        out = list(ex.map(_render, [(i, n, seed) for i in range(n)]))
+        out = list(ex.map(_render, [(i, n, seed, cam_name) for i in range(n)]))
     return np.stack([o[0] for o in out]), np.stack([o[1] for o in out])
 
 
@@ -86,18 +89,19 @@ def algorithmic_bytes(n_kp):
     }
 
 
-def cpu_baseline(seconds, threads, gray, depth):
+def cpu_baseline(seconds, threads, gray, depth, lines=False):
     """The CPU oracle (C++ restatement, oracle/) running the same per-frame
     step, one stream per thread (throughput mode), for a bounded wall time."""
     from _pkg import load_oracle
     O = load_oracle()
     import orbpl.synth as synth
-    cam = O.camera(synth.TUM1)
+    cam = O.camera(synth.TUM3 if lines else synth.TUM1)
     counts = [0] * threads
     stop = time.time() + seconds
 
     def worker(k):
-        vo = O.VO(O.params(*ORB), cam, 1)
+        vo = (O.LVO(O.params(*ORB), cam, 1, use_lines=True) if lines
+              else O.VO(O.params(*ORB), cam, 1))
         n = len(gray)
         i = 0
         while time.time() < stop:
@@ -115,43 +119,20 @@ def cpu_baseline(seconds, threads, gray, depth):
     return sum(counts) / dt, sum(counts), dt
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--streams", type=int, default=256, help="streams (frames per step) per GPU")
-    ap.add_argument("--loop", type=int, default=32, help="frames in the synthetic loop")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pipelined", type=int, default=0,
-                    help="1 = overlap extraction of step t+1 with tracking of step t")
-    args = ap.parse_args()
-
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        dist.init_process_group("gloo")
-
-    from _pkg import load_pkg
-    pkg = load_pkg()
-    import orbpl.synth as synth
-
-    S, F = args.streams, args.loop
+def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, local_rank, dist):
+    """Time `steps` tracker steps of one workload; returns the measurements."""
+    lines = workload == "lines"
+    cam_name = "TUM3" if lines else "TUM1"
+    F = args.loop
     workers = min(16, os.cpu_count() or 4)
-    gray, depth = render_loop(F, seed=1 + rank, workers=workers)
+    gray, depth = render_loop(F, seed=1 + rank, workers=workers, cam_name=cam_name)
     # stream s at step t reads loop frame (s + t) mod F: a contiguous window of
     # a (S + F)-frame replicated buffer, so every step's batch is one slice.
     rep = np.arange(S + F) % F
     d_gray = pkg.DeviceBuffer.from_array(gray[rep], device=local_rank)
     d_depth = pkg.DeviceBuffer.from_array(depth[rep], device=local_rank)
-    cam = pkg.make_camera(synth.TUM1)
-    tr = pkg.Tracker(pkg.OrbParams(*ORB), cam, S, device=local_rank)
+    cam = pkg.make_camera(getattr(synth, cam_name))
+    tr = pkg.Tracker(pkg.OrbParams(*ORB), cam, S, device=local_rank, lines=lines)
     tr.set_pipelined(bool(args.pipelined))
     traj = synth.loop_trajectory(F, seed=1 + rank)
     tr.reset(np.stack([np.linalg.inv(traj[s % F]).astype(np.float32) for s in range(S)]).reshape(S, 16))
@@ -161,7 +142,7 @@ def main():
         o = k % F
         tr.step_device(d_gray.ptr + o * fb, d_depth.ptr + o * db)
 
-    for k in range(args.warmup):
+    for k in range(warmup):
         step(k)
     tr.synchronize()
     tr.timings_reset()
@@ -169,8 +150,8 @@ def main():
         dist.barrier()
     tr.synchronize()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(args.warmup + k)
+    for k in range(steps):
+        step(warmup + k)
     tr.synchronize()
     if dist:
         dist.barrier()
@@ -182,10 +163,20 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     st = tr.state()
-    tim = tr.timings(args.steps)                       # (steps, 9) ms, in-stream hipEvents
+    tim = tr.timings(steps)                            # (steps, 9) ms, in-stream hipEvents
     avg = tim.mean(0)
     stages = dict(zip(tr.STAGES, [round(float(x), 4) for x in avg]))
-    frames = S * args.steps * world
+    tracking = {"mean_keypoints": float(st["nkeypoints"].mean()),
+                "mean_matches": float(st["nmatches"].mean()),
+                "mean_inliers": float(st["ninliers"].mean()),
+                "ok_frac": float(tr.status()["ok"].mean())}
+    if lines:
+        lt = tr.line_timings(steps).mean(0)
+        stages.update(zip(tr.LINE_STAGES, [round(float(x), 4) for x in lt]))
+        ls = tr.status()
+        tracking.update(mean_lines=float(ls["nlines"].mean()),
+                        mean_line_matches=float(ls["line_matches"].mean()))
+    frames = S * steps * world
     value = frames / elapsed
 
     # roofline of the dominant single-launch kernel (pyramid = 8 launches: excluded)
@@ -204,39 +195,104 @@ def main():
             "algorithmic_bytes_per_launch": bytes_launch, "avg_launch_ms": round(dom_ms, 4),
             "per_kernel_GBps": {k: round(ab[k] * S / (float(avg[idx[k]]) * 1e-3) / 1e9, 1)
                                 for k in names}}
+    tr.close()
+    return dict(S=S, value=value, elapsed=elapsed, stages=stages, tracking=tracking, roof=roof,
+                gray=gray, depth=depth,
+                workload=("TUM fr3_structure_texture_far-like RGB-D, ORB + LSD/LBD lines "
+                          "(configs[2])" if lines else
+                          "TUM fr1_desk-like RGB-D, ORB points only (configs[1])"),
+                data=("synthetic (seeded textured-room RGB-D loop, " +
+                      ("TUM3 intrinsics, no distortion)" if lines else
+                       "TUM1 intrinsics+distortion)")))
 
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--streams", type=int, default=256, help="streams (frames per step) per GPU")
+    ap.add_argument("--loop", type=int, default=32, help="frames in the synthetic loop")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", choices=("points", "lines"), default="points",
+                    help="points = configs[1] (headline); lines = configs[2] ORB + LSD/LBD")
+    ap.add_argument("--secondary-steps", type=int, default=3,
+                    help="steps of the configs[2] lines workload reported under 'secondary' "
+                         "(points runs only; 0 = skip)")
+    ap.add_argument("--lines-streams", type=int, default=256)
+    ap.add_argument("--pipelined", type=int, default=0,
+                    help="1 = overlap extraction of step t+1 with tracking of step t")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+
+    from _pkg import load_pkg
+    pkg = load_pkg()
+    import orbpl.synth as synth
+
+    res = run_workload(pkg, synth, args, args.workload, args.streams, args.steps, args.warmup,
+                       rank, world, local_rank, dist)
+    sec = None
+    if args.workload == "points" and args.secondary_steps > 0:
+        # configs[2] (ORB + LSD/LBD lines), same clock discipline, fewer steps
+        sec = run_workload(pkg, synth, args, "lines", args.lines_streams, args.secondary_steps,
+                           max(1, args.warmup // 2), rank, world, local_rank, dist)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         thr = args.cpu_threads or min(16, os.cpu_count() or 1)
-        fps, nfr, dt = cpu_baseline(args.cpu_seconds, thr, gray, depth)
+        lines = args.workload == "lines"
+        fps, nfr, dt = cpu_baseline(args.cpu_seconds, thr, res["gray"], res["depth"], lines)
         cpu = {"value": round(fps, 2), "unit": "frames/s", "cores": thr, "kind": "port",
                "sample": f"{nfr} frames of the same 640x480 RGB-D loop in {dt:.1f} s, oracle/ "
-                         f"C++ restatement, one stream per thread"}
+                         f"C++ restatement ({'points+lines' if lines else 'points'}), "
+                         f"one stream per thread"}
 
     if rank == 0:
+        S = res["S"]
         out = {
             "metric": "frames/sec (extract+match+pose) at 640x480",
-            "value": round(value, 2),
+            "value": round(res["value"], 2),
             "unit": "frames/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "ms_per_step": round(res["elapsed"] / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (seeded textured-room RGB-D loop, TUM1 intrinsics+distortion)",
-            "config": {"workload": "TUM fr1_desk-like RGB-D, ORB points only (configs[1])",
+            "data": res["data"],
+            "config": {"workload": res["workload"],
                        "image": "640x480", "nfeatures": 1000, "streams_per_gpu": S,
                        "frames_per_step": S * world, "parallelism": f"streams sharded x{world}"},
-            "stage_ms": stages,
-            "tracking": {"mean_keypoints": float(st["nkeypoints"].mean()),
-                         "mean_matches": float(st["nmatches"].mean()),
-                         "mean_inliers": float(st["ninliers"].mean())},
-            "roofline": roof,
+            "stage_ms": res["stages"],
+            "tracking": res["tracking"],
+            "roofline": res["roof"],
             "cpu_baseline": cpu,
         }
+        if sec is not None:
+            out["secondary"] = {
+                "workload": sec["workload"], "value": round(sec["value"], 2),
+                "unit": "frames/s", "steps": args.secondary_steps, "streams_per_gpu": sec["S"],
+                "ms_per_step": round(sec["elapsed"] / args.secondary_steps * 1e3, 3),
+                "stage_ms": sec["stages"], "tracking": sec["tracking"]}
+            if cpu is not None:
+                thr = cpu["cores"]
+                fps, nfr, dt = cpu_baseline(args.cpu_seconds / 2, thr, sec["gray"], sec["depth"],
+                                            lines=True)
+                out["secondary"]["cpu_baseline"] = {
+                    "value": round(fps, 2), "unit": "frames/s", "cores": thr, "kind": "port",
+                    "sample": f"{nfr} frames in {dt:.1f} s, oracle/ C++ restatement "
+                              f"(points+lines), one stream per thread"}
         print(json.dumps(out))
     if dist:
         dist.destroy_process_group()

@@ -345,10 +345,17 @@ int lsdx_get_stages(lsdx_ctx* ctx, int frame, uint8_t* scaled, float* deg, uint3
  * in [0, 1023]; perm receives the record indices in sorted order. */
 int orbpl_test_introsort(const int32_t* keys, int n, int32_t* perm);
 /* Debug: batch-mean shader-clock counters of the LSD seed loop of the last
- * run: region growing cycles, fit + refinement cycles, 0, total cycles,
- * region pixels, neighbourhood prefetches, prefetch cycles, rectangles
- * passed to NFA validation. */
+ * run. Speculative loop (default): growing cycles, rounds, speculative
+ * regions, total cycles, fit + refinement cycles, validate + commit
+ * cycles, critical-path grow steps | cooperative regions << 40, rectangles
+ * passed to NFA validation. Wave-serial loop: growing cycles, fit +
+ * refinement cycles, 0, total cycles, region pixels, prefetches, prefetch
+ * cycles, rectangles. */
 int lsdx_debug_profile(lsdx_ctx* ctx, long long* out8);
+/* on != 0: run the wave-serial seed loop (one region at a time, the direct
+ * restatement) instead of the speculative lane-parallel one. Both give the
+ * same lines; the switch exists for testing and measurement. */
+int lsdx_set_serial_grow(lsdx_ctx* ctx, int on);
 
 
 #ifdef __cplusplus

@@ -574,6 +574,7 @@ def _declare(L):  # noqa: F811
     L.lsdx_get_stages.argtypes = [vp, i, vp, vp, vp, ip, ip, ip]
     L.orbpl_test_introsort.argtypes = [vp, i, vp]
     L.lsdx_debug_profile.argtypes = [vp, vp]
+    L.lsdx_set_serial_grow.argtypes = [vp, i]
     L.lsdx_extract.argtypes = [vp, vp, i, i, i, vp, vp, vp, i, ip]
     L.lsdx_extract_batch_device.argtypes = [vp, vp, i, i, C.c_int64]
     L.lsdx_get_keylines.argtypes = [vp, i, vp, vp, vp, i, ip]
@@ -624,12 +625,20 @@ class LineSegmentDetector:
         check(lib().lsdx_get_lines(self._h, frame, _ptr(out), cap, C.byref(n)), "lsdx_get_lines")
         return out[:n.value].copy()
 
+    def set_serial_grow(self, on=True):
+        """Wave-serial seed loop (restatement order) instead of the
+        speculative lane-parallel one; identical lines."""
+        check(lib().lsdx_set_serial_grow(self._h, int(bool(on))), "lsdx_set_serial_grow")
+
     def debug_profile(self):
         out = np.zeros(8, np.int64)
         check(lib().lsdx_debug_profile(self._h, _ptr(out)), "lsdx_debug_profile")
-        keys = ("grow_cyc", "fit_refine_cyc", "reserved", "total_cyc", "region_px", "prefetches",
-                "prefetch_cyc", "candidates")
-        return dict(zip(keys, out.tolist()))
+        keys = ("grow_cyc", "rounds", "spec_regions", "total_cyc", "fit_cyc", "validate_commit_cyc",
+                "max_steps", "candidates")
+        d = dict(zip(keys, out.tolist()))
+        d["coop_regions"] = d["max_steps"] >> 40
+        d["max_steps"] &= (1 << 40) - 1
+        return d
 
     def stages(self, frame=0):
         sw, sh = int(round(self.W * 0.8)), int(round(self.H * 0.8))

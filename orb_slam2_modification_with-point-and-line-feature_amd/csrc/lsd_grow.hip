@@ -577,6 +577,255 @@ __device__ __forceinline__ double rect_improve(Frame& F, Rect& rec) {
   return log_nfa;
 }
 
+
+// ---------------------------------------------------------------------------
+// Speculative lane-parallel seed loop (k_lsd_spec).
+//
+// Each round takes the next (up to) 64 seeds of the pseudo-ordered list that
+// are defined and NOTUSED, and every lane runs the whole serial per-seed
+// program (region_grow, region2rect, refine) for its own seed against the
+// committed USED map, claiming the pixels it adds in a per-pixel stamp word
+// with atomicMin(round | seed rank | grow generation). A region's result
+// equals the sequential one unless an earlier seed of the same round
+// claimed a pixel the region wanted to add (the region's outcome depends on
+// the USED state of exactly the aligned pixels it adds); such regions see a
+// smaller stamp (during growth or when their claims are re-read after the
+// round) and are not committed. Regions are committed in seed order up to
+// the first real conflict; a conflicting seed that an earlier committed
+// region has covered is skipped exactly as the sequential loop skips USED
+// seeds; the next round resumes at the first uncommitted seed (whose rank 0
+// guarantees progress). The committed regions' final pixel sets are OR-ed
+// into the USED bits, rectangles of refined regions go to the candidate
+// list in seed order. A region longer than a lane's buffer is processed by
+// the wave-cooperative serial code once it is the first uncommitted seed.
+// ---------------------------------------------------------------------------
+enum { kSpecConflict = -1, kSpecOverflow = -2, kSpecSmall = 0, kSpecFail = 1, kSpecCand = 2 };
+
+__device__ __forceinline__ uint32_t ld_stamp(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int pt_x(const uint4& e) { return (int)(e.x & 0xFFFF); }
+__device__ __forceinline__ int pt_y(const uint4& e) { return (int)(e.x >> 16); }
+
+// region_grow for one lane. buf entries: (x | y << 16, degrees, modgrad as
+// a double split lo / hi) in insertion order. Claims are fire-and-forget
+// atomicMin; the own-pixel test re-reads the stamp from L2 (same-address
+// order within the wave). The next list entry is taken from registers (or
+// prefetched with the neighbourhood), so a step costs one memory round trip.
+// Returns the length, kSpecConflict or kSpecOverflow.
+__device__ __forceinline__ uint4 make_entry(int x, int y, const float4& r) {
+  const double w = modgrad_q(__float_as_int(r.y));
+  return make_uint4((uint32_t)x | ((uint32_t)y << 16), __float_as_uint(r.x),
+                    (uint32_t)__double2loint(w), (uint32_t)__double2hiint(w));
+}
+__device__ __forceinline__ double entry_w(const uint4& e) {
+  return __hiloint2double((int)e.w, (int)e.z);
+}
+__device__ __forceinline__ float entry_deg(const uint4& e) { return __uint_as_float(e.y); }
+
+__device__ __forceinline__ int lane_grow(const Frame& F, const float4* __restrict__ pix,
+                                         uint32_t* stamp, uint4* buf, int cap, int sx, int sy,
+                                         double& reg_angle, double prec, uint32_t myval) {
+  const uint32_t mytag = myval >> 1;
+  const int sw = F.sw, sh = F.sh;
+  const int si = sy * sw + sx;
+  if (cap < 1) return kSpecOverflow;
+  if ((ld_stamp(stamp + si) >> 1) < mytag) return kSpecConflict;
+  atomicMin(stamp + si, myval);
+  uint4 cur = make_entry(sx, sy, pix[si]);
+  buf[0] = cur;
+  reg_angle = deg2ang(entry_deg(cur));
+  double s0, c0;
+  lsdm::sincos_(reg_angle, &s0, &c0);
+  float sumdx = (float)c0;
+  float sumdy = (float)s0;
+  int n = 1;
+  for (int i = 0; i < n; i++) {
+    const int x = pt_x(cur), y = pt_y(cur);
+    const int n_start = n;
+    // all loads unconditional (clamped coordinates) so that they are in
+    // flight together; out-of-image neighbours are masked afterwards
+    const uint4 pref = buf[min(i + 1, n_start - 1)];
+    uint32_t st[9];
+    float4 pv[9];
+    unsigned cand = 0;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+      const int xx = x + (k % 3) - 1, yy = y + (k / 3) - 1;
+      const int cx = min(max(xx, 0), sw - 1), cy = min(max(yy, 0), sh - 1);
+      const int idx = cy * sw + cx;
+      st[k] = ld_stamp(stamp + idx);
+      pv[k] = pix[idx];
+      const bool in = xx >= 0 && xx < sw && yy >= 0 && yy < sh;
+      cand |= (in && !((F.used[idx >> 5] >> (idx & 31)) & 1u)) ? (1u << k) : 0u;
+    }
+    uint4 first_add = cur;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+      if (!((cand >> k) & 1u) || st[k] == myval) continue;  // USED (committed or own)
+      if (!aligned_deg(pv[k].x, reg_angle, prec)) continue;
+      if ((st[k] >> 1) < mytag) return kSpecConflict;      // an earlier seed's pixel
+      const int xx = x + (k % 3) - 1, yy = y + (k / 3) - 1;
+      atomicMin(stamp + yy * sw + xx, myval);
+      if (n >= cap) return kSpecOverflow;
+      const uint4 e = make_entry(xx, yy, pv[k]);
+      if (n == n_start) first_add = e;
+      buf[n++] = e;
+      sumdx += pv[k].z;
+      sumdy += pv[k].w;
+      reg_angle = (double)fast_atan2_deg(sumdy, sumdx) * kDegToRad;
+    }
+    cur = (i + 1 < n_start) ? pref : first_add;
+  }
+  return n;
+}
+
+// region2rect over a lane's list (same operation order as region2rect)
+__device__ __forceinline__ void lane_rect(const uint4* buf, int n, double reg_angle, double prec,
+                                          double p, Rect& rec) {
+  // every pass reads the list in batches of 8 unconditional loads (indices
+  // clamped to n - 1, contributions masked) so the loads overlap
+  constexpr int kB = 8;
+  double x = 0, y = 0, sum = 0;
+  for (int i0 = 0; i0 < n; i0 += kB) {
+    uint4 e[kB];
+#pragma unroll
+    for (int u = 0; u < kB; u++) e[u] = buf[min(i0 + u, n - 1)];
+#pragma unroll
+    for (int u = 0; u < kB; u++) {
+      if (i0 + u < n) {
+        const double weight = entry_w(e[u]);
+        x += double(pt_x(e[u])) * weight;
+        y += double(pt_y(e[u])) * weight;
+        sum += weight;
+      }
+    }
+  }
+  x /= sum;
+  y /= sum;
+  double Ixx = 0.0, Iyy = 0.0, Ixy = 0.0;
+  for (int i0 = 0; i0 < n; i0 += kB) {
+    uint4 e[kB];
+#pragma unroll
+    for (int u = 0; u < kB; u++) e[u] = buf[min(i0 + u, n - 1)];
+#pragma unroll
+    for (int u = 0; u < kB; u++) {
+      if (i0 + u < n) {
+        const double weight = entry_w(e[u]);
+        const double dx = double(pt_x(e[u])) - x, dy = double(pt_y(e[u])) - y;
+        Ixx += dy * dy * weight;
+        Iyy += dx * dx * weight;
+        Ixy -= dx * dy * weight;
+      }
+    }
+  }
+  const double lambda = 0.5 * (Ixx + Iyy - sqrt((Ixx - Iyy) * (Ixx - Iyy) + 4.0 * Ixy * Ixy));
+  double theta = (fabs(Ixx) > fabs(Iyy)) ? double(fast_atan2_deg(float(lambda - Ixx), float(Ixy)))
+                                         : double(fast_atan2_deg(float(Ixy), float(lambda - Iyy)));
+  theta *= kDegToRad;
+  if (fabs(angle_diff_signed(theta, reg_angle)) > prec) theta += kPi;
+  const double dx = lsdm::cos_(theta), dy = lsdm::sin_(theta);
+  // l_max / l_min (and w) start at 0, so the reference's else-if is an
+  // independent max / min
+  double l_min = 0, l_max = 0, w_min = 0, w_max = 0;
+  for (int i0 = 0; i0 < n; i0 += kB) {
+    uint4 e[kB];
+#pragma unroll
+    for (int u = 0; u < kB; u++) e[u] = buf[min(i0 + u, n - 1)];
+#pragma unroll
+    for (int u = 0; u < kB; u++) {
+      const double regdx = double(pt_x(e[u])) - x, regdy = double(pt_y(e[u])) - y;
+      const double l = regdx * dx + regdy * dy;
+      const double w = -regdx * dy + regdy * dx;
+      l_max = l > l_max ? l : l_max;
+      l_min = l < l_min ? l : l_min;
+      w_max = w > w_max ? w : w_max;
+      w_min = w < w_min ? w : w_min;
+    }
+  }
+  rec.x1 = x + l_min * dx;
+  rec.y1 = y + l_min * dy;
+  rec.x2 = x + l_max * dx;
+  rec.y2 = y + l_max * dy;
+  rec.width = w_max - w_min;
+  rec.x = x;
+  rec.y = y;
+  rec.theta = theta;
+  rec.dx = dx;
+  rec.dy = dy;
+  rec.prec = prec;
+  rec.p = p;
+  if (rec.width < 1.0) rec.width = 1.0;
+}
+
+// refine + reduce_region_radius for a lane. The region [0, n) came from the
+// first grow; a second grow is appended after it. Returns the status; off /
+// len give the final region, touched the claimed prefix of the buffer.
+__device__ __forceinline__ int lane_refine(const Frame& F, const float4* __restrict__ pix,
+                                           uint32_t* stamp, uint4* buf, int n, double reg_angle,
+                                           double prec, double p, Rect& rec, uint32_t myval1,
+                                           int& off, int& len, int& touched) {
+  const double density_th = 0.7;
+  double density = double(n) / (dist(rec.x1, rec.y1, rec.x2, rec.y2) * rec.width);
+  off = 0;
+  len = n;
+  touched = n;
+  if (density >= density_th) return kSpecCand;
+  const uint4 e0 = buf[0];
+  const int x0 = pt_x(e0), y0 = pt_y(e0);
+  const double xc = double(x0), yc = double(y0);
+  const double ang_c = deg2ang(entry_deg(e0));
+  double sum = 0, s_sum = 0;
+  int cnt = 0;
+  for (int i0 = 0; i0 < n; i0 += 8) {
+    uint4 e[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) e[u] = buf[min(i0 + u, n - 1)];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      if (i0 + u < n && dist(xc, yc, pt_x(e[u]), pt_y(e[u])) < rec.width) {
+        const double ang_d = angle_diff_signed(deg2ang(entry_deg(e[u])), ang_c);
+        sum += ang_d;
+        s_sum += ang_d * ang_d;
+        ++cnt;
+      }
+    }
+  }
+  const double mean_angle = sum / double(cnt);
+  const double tau =
+      2.0 * sqrt((s_sum - 2.0 * mean_angle * sum) / double(cnt) + mean_angle * mean_angle);
+  uint4* g1 = buf + n;
+  int n1 = lane_grow(F, pix, stamp, g1, kLaneCap - n, x0, y0, reg_angle, tau, myval1);
+  if (n1 < 0) return n1;
+  off = n;
+  len = n1;
+  touched = n + n1;
+  if (n1 < 2) return kSpecFail;
+  lane_rect(g1, n1, reg_angle, prec, p, rec);
+  density = double(n1) / (dist(rec.x1, rec.y1, rec.x2, rec.y2) * rec.width);
+  if (density >= density_th) return kSpecCand;
+  // reduce_region_radius
+  const double radSq1 = distSq(xc, yc, rec.x1, rec.y1);
+  const double radSq2 = distSq(xc, yc, rec.x2, rec.y2);
+  double radSq = radSq1 > radSq2 ? radSq1 : radSq2;
+  while (density < density_th) {
+    radSq *= 0.75 * 0.75;
+    for (int i = 0; i < n1; ++i) {
+      const uint4 e = g1[i];
+      if (distSq(xc, yc, double(pt_x(e)), double(pt_y(e))) > radSq) {
+        g1[i] = g1[n1 - 1];
+        g1[n1 - 1] = e;
+        n1--;
+        --i;
+      }
+    }
+    len = n1;
+    if (n1 < 2) return kSpecFail;
+    lane_rect(g1, n1, reg_angle, prec, p, rec);
+    density = double(n1) / (dist(rec.x1, rec.y1, rec.x2, rec.y2) * rec.width);
+  }
+  return kSpecCand;
+}
 }  // namespace
 
 __global__ void __launch_bounds__(64) k_lsd_grow(LsdGeom g, LsdScratch sc) {
@@ -664,6 +913,227 @@ __global__ void __launch_bounds__(64) k_lsd_grow(LsdGeom g, LsdScratch sc) {
   }
 }
 
+
+// Speculative seed loop (see lane_grow): one wave per frame.
+__global__ void __launch_bounds__(64) k_lsd_spec(LsdGeom g, LsdScratch sc) {
+  extern __shared__ uint32_t grow_smem[];
+  __shared__ uint32_t s_pt[kSpecLanes];
+  __shared__ int s_pos[kSpecLanes];
+  const int f = blockIdx.x, lane = threadIdx.x;
+  const int sw = g.sw, sh = g.sh;
+  const int used_words = (sw * sh + 31) / 32;
+  Frame F;
+  F.sw = sw;
+  F.sh = sh;
+  F.deg = sc.deg + (long long)f * sw * sh;
+  F.q = sc.q + (long long)f * sw * sh;
+  F.used = grow_smem;
+  F.reg_l = grow_smem + used_words;
+  F.regq_l = reinterpret_cast<int*>(F.reg_l + kRegLds);
+  F.regd_l = reinterpret_cast<float*>(F.regq_l + kRegLds);
+  F.ring = F.regd_l + kRegLds;
+  F.reg_g = sc.reg + (long long)f * 3 * sw * sh;
+  F.rows = reinterpret_cast<int4*>(grow_smem + ((used_words + 3 * kRegLds + 64 * 9 + 3) & ~3));
+  F.rect0 = reinterpret_cast<Rect*>(F.rows);
+  F.rect1 = F.rect0 + 1;
+  F.row_cap = 0;
+  F.log_nt = g.log_nt;
+  F.lane = lane;
+  F.pf_cyc = 0;
+  F.pf_cnt = 0;
+  for (int i = lane; i < used_words; i += 64) F.used[i] = 0;
+  __builtin_amdgcn_wave_barrier();
+  uint32_t* stamp = sc.stamp + (long long)f * sw * sh;
+  uint4* buf = sc.lbuf + ((long long)f * kSpecLanes + lane) * kLaneCap;
+  const float4* pix = sc.pix + (long long)f * sw * sh;
+  const uint32_t* A = sc.A + (long long)f * g.n;
+  double* cand_out = sc.cand + (long long)f * kLsdMaxCand * 12;
+  const int w1 = sw - 1;
+  const double prec = g.prec, p = g.p;
+  const unsigned long long lt_mask = (1ull << lane) - 1ull;
+  int nl = 0, pos = 0;
+  uint32_t round = 0;
+  long long n_spec = 0, n_rounds = 0, cyc_spec = 0, cyc_fit = 0, cyc_val = 0, max_steps = 0,
+            n_coop = 0;
+  const long long t_all = clock64();
+  while (pos < g.n) {
+    // ---- the next 64 defined, NOTUSED seeds in list order ----
+    int ncand = 0, scan = pos, next_pos = g.n;
+    while (ncand < kSpecLanes && scan < g.n) {
+      const int i = scan + lane;
+      bool c = false;
+      int px = 0, py = 0;
+      if (i < g.n) {
+        const int idx = (int)(A[i] & 0x3FFFFFu);
+        py = idx / w1;
+        px = idx - py * w1;
+        c = F.deg[py * sw + px] >= 0.f && !used_get(F, px, py);
+      }
+      const unsigned long long m = __ballot(c);
+      const int before = __popcll(m & lt_mask);
+      if (c && ncand + before < kSpecLanes) {
+        s_pt[ncand + before] = (uint32_t)px | ((uint32_t)py << 16);
+        s_pos[ncand + before] = i;
+      }
+      const int cnt = __popcll(m);
+      if (ncand + cnt >= kSpecLanes) {
+        const unsigned long long mm = __ballot(c && before == kSpecLanes - ncand - 1);
+        next_pos = scan + __ffsll((long long)mm);
+        ncand = kSpecLanes;
+      } else {
+        ncand += cnt;
+        scan += 64;
+      }
+    }
+    if (ncand == 0) break;
+    __threadfence_block();
+    __builtin_amdgcn_wave_barrier();
+    n_rounds++;
+    n_spec += ncand;
+    // ---- speculative per-lane processing ----
+    const long long t0 = clock64();
+    const uint32_t tag = ((0xFFFFFFu - round) << 7) | (uint32_t)lane;
+    const uint32_t myval0 = (tag << 1) | 1u, myval1 = tag << 1;
+    int status = kSpecConflict, off = 0, len = 0, touched = 0;
+    Rect rec;
+    double reg_angle = 0;
+    int n = 0;
+    if (lane < ncand) {
+      const uint32_t pt = s_pt[lane];
+      n = lane_grow(F, pix, stamp, buf, kLaneCap, (int)(pt & 0xFFFF), (int)(pt >> 16), reg_angle,
+                    prec, myval0);
+    }
+    __builtin_amdgcn_wave_barrier();
+    const long long t1 = clock64();
+    {
+      int mx = n;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
+      max_steps += mx;
+    }
+    if (lane < ncand) {
+      if (n < 0) {
+        status = n;
+      } else if (n < g.min_reg_size) {
+        status = kSpecSmall;
+        len = n;
+        touched = n;
+      } else {
+        lane_rect(buf, n, reg_angle, prec, p, rec);
+        status = lane_refine(F, pix, stamp, buf, n, reg_angle, prec, p, rec, myval1, off, len,
+                             touched);
+      }
+    }
+    __threadfence();
+    __builtin_amdgcn_wave_barrier();
+    const long long t2 = clock64();
+    cyc_spec += t1 - t0;
+    cyc_fit += t2 - t1;
+    // ---- re-read the claims: an earlier seed's smaller stamp = conflict ----
+    bool conflict = lane < ncand && status < 0;
+    if (lane < ncand && status >= 0) {
+      for (int j0 = 0; j0 < touched && !conflict; j0 += 8) {
+        uint32_t ev[8], sv[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) ev[u] = buf[min(j0 + u, touched - 1)].x;
+#pragma unroll
+        for (int u = 0; u < 8; u++) sv[u] = ld_stamp(stamp + (int)(ev[u] >> 16) * sw + (int)(ev[u] & 0xFFFF));
+#pragma unroll
+        for (int u = 0; u < 8; u++) conflict |= (sv[u] >> 1) != tag;
+      }
+    }
+    // ---- commit in seed order ----
+    const unsigned long long cmask = __ballot(conflict);
+    int first = cmask ? __ffsll((long long)cmask) - 1 : ncand;
+    unsigned long long commit = (first >= 64 ? ~0ull : ((1ull << first) - 1ull)) &
+                                (ncand >= 64 ? ~0ull : ((1ull << ncand) - 1ull));
+    int stop = ncand;
+    while (true) {
+      const bool mine = (commit >> lane) & 1ull;
+      if (mine && len > 0) {
+        for (int j0 = off; j0 < off + len; j0 += 8) {
+          uint32_t ev[8];
+#pragma unroll
+          for (int u = 0; u < 8; u++) ev[u] = buf[min(j0 + u, off + len - 1)].x;
+#pragma unroll
+          for (int u = 0; u < 8; u++) {
+            const int id = (int)(ev[u] >> 16) * sw + (int)(ev[u] & 0xFFFF);
+            atomicOr(F.used + (id >> 5), 1u << (id & 31));
+          }
+        }
+      }
+      const unsigned long long cm = __ballot(mine && status == kSpecCand);
+      if (mine && status == kSpecCand) {
+        const int k = nl + __popcll(cm & lt_mask);
+        if (k < kLsdMaxCand) {
+          double* o = cand_out + (long long)k * 12;
+          o[0] = rec.x1; o[1] = rec.y1; o[2] = rec.x2; o[3] = rec.y2;
+          o[4] = rec.width; o[5] = rec.x; o[6] = rec.y; o[7] = rec.theta;
+          o[8] = rec.dx; o[9] = rec.dy; o[10] = rec.prec; o[11] = rec.p;
+        }
+      }
+      nl += __popcll(cm);
+      __threadfence_block();
+      __builtin_amdgcn_wave_barrier();
+      if (first >= ncand) break;
+      const uint32_t spt = s_pt[first];
+      if (used_get(F, (int)(spt & 0xFFFF), (int)(spt >> 16))) {
+        // covered by a committed region: the sequential loop skips it
+        const unsigned long long rest = first >= 63 ? 0ull : (cmask & ~((2ull << first) - 1ull));
+        const int nxt = rest ? __ffsll((long long)rest) - 1 : ncand;
+        commit = ((nxt >= 64 ? ~0ull : ((1ull << nxt) - 1ull)) & ~((2ull << first) - 1ull)) &
+                 (ncand >= 64 ? ~0ull : ((1ull << ncand) - 1ull));
+        first = nxt;
+        continue;
+      }
+      stop = first;
+      break;
+    }
+    cyc_val += clock64() - t2;
+    if (stop < ncand) {
+      pos = s_pos[stop];
+      if (__shfl(status, stop, 64) == kSpecOverflow) {
+        // a region longer than a lane buffer: the wave-cooperative program
+        const uint32_t spt = s_pt[stop];
+        double reg_angle;
+        int n = region_grow(F, (int)(spt & 0xFFFF), (int)(spt >> 16), reg_angle, prec);
+        if (n >= g.min_reg_size) {
+          Rect& rc = *F.rect0;
+          fill_q(F, n);
+          region2rect(F, n, reg_angle, prec, p, rc);
+          if (refine(F, n, reg_angle, prec, p, rc, 0.7)) {
+            if (nl < kLsdMaxCand) {
+              const double* rv = reinterpret_cast<const double*>(F.rect0);
+              if (lane < 12) cand_out[(long long)nl * 12 + lane] = rv[lane];
+            }
+            nl++;
+          }
+        }
+        n_coop++;
+        pos++;
+      }
+    } else {
+      pos = next_pos;
+    }
+    round++;
+  }
+  if (lane == 0) {
+    sc.ncand[f] = min(nl, kLsdMaxCand);
+    if (nl > kLsdMaxCand) atomicOr(sc.err + f, 8);
+  }
+  if (sc.prof && lane == 0) {
+    long long* pr = sc.prof + f * 8;
+    pr[0] = cyc_spec;
+    pr[1] = n_rounds;
+    pr[2] = n_spec;
+    pr[3] = clock64() - t_all;
+    pr[4] = cyc_fit;
+    pr[5] = cyc_val;
+    pr[6] = max_steps | (n_coop << 40);
+    pr[7] = nl;
+  }
+}
+
 // NFA validation of every refined rectangle (rect_improve), one wave per
 // rectangle, 4 waves per block; the accepted segments are compacted in seed
 // order by k_lsd_compact.
@@ -745,12 +1215,18 @@ size_t lsd_grow_smem(const LsdGeom& g) {
   return 4 * (size_t)(((used_words + 3 * kRegLds + 64 * 9 + 3) & ~3)) + 2 * sizeof(Rect);
 }
 
-void launch_lsd_grow(const LsdGeom& g, const LsdScratch& sc, int batch, hipStream_t s) {
+void launch_lsd_grow(const LsdGeom& g, const LsdScratch& sc, int batch, hipStream_t s,
+                     bool serial) {
   const size_t smem = lsd_grow_smem(g);
+  const void* k = serial ? (const void*)k_lsd_grow : (const void*)k_lsd_spec;
   if (smem > 65536)
-    (void)hipFuncSetAttribute((const void*)k_lsd_grow, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)smem);
-  hipLaunchKernelGGL(k_lsd_grow, dim3(batch), dim3(64), smem, s, g, sc);
+    (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  if (serial) {
+    hipLaunchKernelGGL(k_lsd_grow, dim3(batch), dim3(64), smem, s, g, sc);
+  } else {
+    (void)hipMemsetAsync(sc.stamp, 0xFF, (size_t)batch * g.sw * g.sh * 4, s);
+    hipLaunchKernelGGL(k_lsd_spec, dim3(batch), dim3(64), smem, s, g, sc);
+  }
 }
 
 }  // namespace orbpl

@@ -10,6 +10,8 @@ namespace orbpl {
 
 constexpr int kLsdMaxLines = 4096;    // raw LSD segments kept per frame
 constexpr int kLsdMaxCand = 4096;     // refined rectangles awaiting NFA validation per frame
+constexpr int kSpecLanes = 64;        // speculative regions per round (one wave)
+constexpr int kLaneCap = 2048;        // region points a lane can hold (both grows)
 constexpr int kLineKeep = 80;         // LineExtractor.cpp:24
 constexpr int kLsdSortChunk = 256;    // elements per partition chunk
 constexpr float kLsdNotdef = -1.0f;   // NOTDEF marker in the degree map
@@ -57,6 +59,10 @@ struct LsdScratch {
   int* ncand;          // 1 per frame
   float* cand_line;    // kLsdMaxCand * 4 per frame: validated segment
   int* cand_ok;        // kLsdMaxCand per frame: log_nfa > log_eps
+  uint32_t* stamp;     // sw*sh per frame: speculative region claims (0xFF.. = none)
+  uint4* lbuf;         // kSpecLanes * kLaneCap per frame: per-lane region lists
+                       // (x | y << 16, q, degrees, -)
+  float4* pix;         // sw*sh per frame: degrees, q bits, cos, sin
 };
 
 // Outputs of LineExtractor::ExtractLineSegment per frame.
@@ -86,11 +92,14 @@ void launch_lsd_blur(const LsdGeom& g, const uint8_t* img, int stride, long long
                      uint8_t* out, int batch, hipStream_t s);
 void launch_lsd_resize(const LsdGeom& g, const int* tabs, const uint8_t* blur, uint8_t* scaled,
                        int batch, hipStream_t s);
-void launch_lsd_grad(const LsdGeom& g, const uint8_t* scaled, float* deg, int* q, unsigned* maxq,
-                     int batch, hipStream_t s);
+void launch_lsd_grad(const LsdGeom& g, const uint8_t* scaled, float* deg, int* q, float4* pix,
+                     unsigned* maxq, int batch, hipStream_t s);
 void launch_lsd_sort(const LsdGeom& g, const LsdScratch& sc, int batch, hipStream_t s);
 void launch_lsd_sort_keys(int n, const int* keys, const LsdScratch& sc, hipStream_t s);
-void launch_lsd_grow(const LsdGeom& g, const LsdScratch& sc, int batch, hipStream_t s);
+// serial = true: the wave-serial seed loop (k_lsd_grow); false: the
+// speculative lane-parallel loop (k_lsd_spec). Identical results.
+void launch_lsd_grow(const LsdGeom& g, const LsdScratch& sc, int batch, hipStream_t s,
+                     bool serial);
 size_t lsd_grow_smem(const LsdGeom& g);
 void launch_lsd_validate(const LsdGeom& g, const LsdScratch& sc, int batch, hipStream_t s);
 

@@ -86,6 +86,7 @@ struct lsdx_ctx {
   int* d_tabs = nullptr;
   uint8_t* d_in = nullptr;
   int last_batch = 0;
+  bool serial_grow = false;  // lsdx_set_serial_grow: wave-serial seed loop
   std::vector<void*> allocs;
 };
 
@@ -137,9 +138,9 @@ int lsdx_run(lsdx_ctx* c, const uint8_t* d_imgs, int batch, int stride, int64_t 
   HIP_CHECK(hipMemsetAsync(c->sc.err, 0, (size_t)batch * 4, s));
   launch_lsd_blur(g, d_imgs, stride, frame_pitch, c->sc.blur, batch, s);
   launch_lsd_resize(g, c->d_tabs, c->sc.blur, c->sc.scaled, batch, s);
-  launch_lsd_grad(g, c->sc.scaled, c->sc.deg, c->sc.q, c->sc.maxq, batch, s);
+  launch_lsd_grad(g, c->sc.scaled, c->sc.deg, c->sc.q, c->sc.pix, c->sc.maxq, batch, s);
   launch_lsd_sort(g, c->sc, batch, s);
-  launch_lsd_grow(g, c->sc, batch, s);
+  launch_lsd_grow(g, c->sc, batch, s, c->serial_grow);
   launch_lsd_validate(g, c->sc, batch, s);
   if (ev_mid) HIP_CHECK(hipEventRecord(ev_mid, s));
   if (out) {
@@ -235,6 +236,9 @@ int lsdx_create(int width, int height, int max_batch, int device, lsdx_ctx** out
   LA(s.ncand, B * 4);
   LA(s.cand_line, B * kLsdMaxCand * 4 * 4);
   LA(s.cand_ok, B * kLsdMaxCand * 4);
+  LA(s.stamp, B * px * 4);
+  LA(s.lbuf, B * kSpecLanes * kLaneCap * sizeof(uint4));
+  LA(s.pix, B * px * sizeof(float4));
   LA(c->d_tabs, (size_t)(2 * g.sw + 2 * g.sh) * 4);
   LA(c->blur5, B * width * height);
   LA(c->sdx, B * width * height * 2);
@@ -334,6 +338,14 @@ int lsdx_device_outputs(lsdx_ctx* c, orbpl_keyline** d_kl, uint8_t** d_desc, dou
   if (d_desc) *d_desc = c->lo.desc;
   if (d_coef) *d_coef = c->lo.coef;
   if (d_n) *d_n = c->lo.n;
+  return ORBPL_OK;
+}
+
+int lsdx_set_serial_grow(lsdx_ctx* c, int on) {
+  if (!c) return arg_fail("NULL context");
+  int rc = lsdx_synchronize(c);
+  if (rc) return rc;
+  c->serial_grow = on != 0;
   return ORBPL_OK;
 }
 

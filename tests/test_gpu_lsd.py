@@ -50,8 +50,10 @@ def test_lsd_stages_bit_exact(orbpl, oracle, frames):
         assert np.array_equal(order, ord_o)
 
 
-def test_lsd_lines_bit_exact(orbpl, oracle, frames):
+@pytest.mark.parametrize("serial", [False, True], ids=["speculative", "wave_serial"])
+def test_lsd_lines_bit_exact(orbpl, oracle, frames, serial):
     det = orbpl.LineSegmentDetector(640, 480)
+    det.set_serial_grow(serial)
     for g in frames:
         L = det.detect(g)
         Lo = oracle.lsd_detect(g)
@@ -114,3 +116,17 @@ def test_line_extract_kitti(orbpl, oracle):
     ex = orbpl.LineExtractor(1241, 376)
     kl_o, desc_o, coef_o, nd = oracle.line_extract(g)
     _cmp_keylines(*ex.ExtractLineSegment(g), kl_o, desc_o, coef_o)
+
+
+def test_lsd_regions_longer_than_a_lane_buffer(orbpl, oracle):
+    """Sawtooth images: every tooth is one aligned region of ~20k pixels,
+    beyond a lane's speculative buffer, so the speculative loop hands those
+    seeds to the wave-cooperative program. Lines equal the oracle's."""
+    x = np.arange(640)[None, :].repeat(480, 0)
+    y = np.arange(480)[:, None].repeat(640, 1)
+    imgs = [((x * 4) % 256).astype(np.uint8), (((x + 2 * y) * 3) % 256).astype(np.uint8)]
+    det = orbpl.LineSegmentDetector(640, 480)
+    for img in imgs:
+        L = det.detect(img)
+        assert np.array_equal(L, oracle.lsd_detect(img))
+        assert det.debug_profile()["coop_regions"] > 0

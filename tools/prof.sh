@@ -2,18 +2,22 @@
 # Profiling passes on the GPU box (rocprofv3). Kernel trace + stats first,
 # then PMC passes, each counter group in its own run (no tracing domains
 # combined with --pmc). Outputs under gpurun_out/prof_<tag>/.
+# The bench command runs the points headline and the configs[2] lines
+# workload (secondary), so both kernel sets are covered.
 set -o pipefail
 tag=${1:-run}
 out=gpurun_out/prof_$tag
 mkdir -p $out
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-B="$R/bench.py --steps 4 --warmup 2 --no-cpu-baseline"
+B="$R/bench.py --steps 4 --warmup 2 --secondary-steps 2 --no-cpu-baseline"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$out/trace -o run --output-format csv -- python3 $B > $R/$out/trace.log 2>&1 || { echo "trace failed"; tail -5 $R/$out/trace.log; exit 1; }
 echo trace ok
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES SQ_LDS_BANK_CONFLICT -d $R/$out/sq -o run --output-format csv -- python3 $B > $R/$out/sq.log 2>&1 || { echo "sq failed"; tail -5 $R/$out/sq.log; exit 1; }
-echo sq ok
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $R/$out/fetch -o run --output-format csv -- python3 $B > $R/$out/fetch.log 2>&1 || { echo "fetch failed"; tail -5 $R/$out/fetch.log; exit 1; }
 echo fetch ok
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $R/$out/write -o run --output-format csv -- python3 $B > $R/$out/write.log 2>&1 || { echo "write failed"; tail -5 $R/$out/write.log; exit 1; }
 echo write ok
+if [ -n "$SQ" ]; then
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES SQ_LDS_BANK_CONFLICT -d $R/$out/sq -o run --output-format csv -- python3 $B > $R/$out/sq.log 2>&1 || { echo "sq failed"; tail -5 $R/$out/sq.log; exit 1; }
+echo sq ok
+fi
