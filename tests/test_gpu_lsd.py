@@ -124,7 +124,7 @@ def test_lsd_regions_longer_than_a_lane_buffer(orbpl, oracle):
     seeds to the wave-cooperative program. Lines equal the oracle's."""
     x = np.arange(640)[None, :].repeat(480, 0)
     y = np.arange(480)[:, None].repeat(640, 1)
-    imgs = [((x * 4) % 256).astype(np.uint8), (((x + 2 * y) * 3) % 256).astype(np.uint8)]
+    imgs = [((x * 8) % 256).astype(np.uint8), (((x + 2 * y) * 3) % 256).astype(np.uint8)]
     det = orbpl.LineSegmentDetector(640, 480)
     for img in imgs:
         L = det.detect(img)
