@@ -826,6 +826,199 @@ __device__ __forceinline__ int lane_refine(const Frame& F, const float4* __restr
   }
   return kSpecCand;
 }
+
+// ---------------------------------------------------------------------------
+// NFA validation with one lane per rectangle (k_lsd_validate): most
+// candidates are small (tens of pixels) and go through all rect_improve
+// phases, so the serial parts (corner walk, log_gamma, binomial tail)
+// dominate; a lane runs them for its own rectangle exactly as the reference
+// orders them, 64 rectangles per wave.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double nfa_lane(int n, int k, double p, double log_nt) {
+  if (n == 0 || k == 0) return -log_nt;
+  if (n == k) return -log_nt - double(n) * lsdm::log10_(p);
+  const double p_term = p / (1 - p);
+  const double log1term = log_gamma(double(n) + 1) - log_gamma(double(k) + 1) -
+                          log_gamma(double(n - k) + 1) + double(k) * lsdm::log_(p) +
+                          double(n - k) * lsdm::log_(1.0 - p);
+  double term = lsdm::exp_(log1term);
+  if (double_equal(term, 0)) {
+    if (k > n * p) return -log1term / 2.30258509299404568402 - log_nt;
+    return -log_nt;
+  }
+  double bin_tail = term;
+  const double tolerance = 0.1;
+  for (int i = k + 1; i <= n; ++i) {
+    const double bin_term = double(n - i + 1) / double(i);
+    const double mult_term = bin_term * p_term;
+    term *= mult_term;
+    bin_tail += term;
+    if (bin_term < 1) {
+      const double err =
+          term * ((1 - lsdm::powi_(mult_term, double(n - i + 1))) / (1 - mult_term) - 1);
+      if (err < tolerance * fabs(-lsdm::log10_(bin_tail) - log_nt) * bin_tail) break;
+    }
+  }
+  return -lsdm::log10_(bin_tail) - log_nt;
+}
+
+// rect_nfa for one lane: the reference's row walk, pixels counted in
+// batches of 8 loads generated across rows.
+__device__ __forceinline__ double rect_nfa_lane(const float* __restrict__ deg, int sw, int sh,
+                                                const Rect& rec, double log_nt) {
+  const double half_width = rec.width / 2.0;
+  const double dyhw = rec.dy * half_width;
+  const double dxhw = rec.dx * half_width;
+  int ex0 = int(rec.x1 - dyhw), ey0 = int(rec.y1 + dxhw);
+  int ex1 = int(rec.x2 - dyhw), ey1 = int(rec.y2 + dxhw);
+  int ex2 = int(rec.x2 + dyhw), ey2 = int(rec.y2 - dxhw);
+  int ex3 = int(rec.x1 + dyhw), ey3 = int(rec.y1 - dxhw);
+  auto cswap = [](int& ax, int& ay, int& bx, int& by) {
+    if ((bx < ax) || (bx == ax && by < ay)) {
+      const int tx = ax, ty = ay;
+      ax = bx; ay = by; bx = tx; by = ty;
+    }
+  };
+  cswap(ex0, ey0, ex1, ey1);
+  cswap(ex2, ey2, ex3, ey3);
+  cswap(ex0, ey0, ex2, ey2);
+  cswap(ex1, ey1, ex3, ey3);
+  cswap(ex1, ey1, ex2, ey2);
+  auto X = [&](int i) { return i == 0 ? ex0 : (i == 1 ? ex1 : (i == 2 ? ex2 : ex3)); };
+  auto Y = [&](int i) { return i == 0 ? ey0 : (i == 1 ? ey1 : (i == 2 ? ey2 : ey3)); };
+  int imin = 0, imax = 0;
+#pragma unroll
+  for (int i = 1; i < 4; ++i) {
+    if (Y(imin) > Y(i)) imin = i;
+    if (Y(imax) < Y(i)) imax = i;
+  }
+  unsigned taken = 1u << imin;
+  int il = -1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (!((taken >> i) & 1u)) {
+      if (il < 0) il = i;
+      else if (X(il) > X(i)) il = i;
+    }
+  taken |= 1u << il;
+  int ir = -1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (!((taken >> i) & 1u)) {
+      if (ir < 0) ir = i;
+      else if (X(ir) < X(i)) ir = i;
+    }
+  taken |= 1u << ir;
+  int it = -1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (!((taken >> i) & 1u)) {
+      if (it < 0) it = i;
+      else if (X(it) > X(i)) it = i;
+    }
+  const int mnx = X(imin), mny = Y(imin), mxy = Y(imax);
+  const int lfx = X(il), lfy = Y(il), rtx = X(ir), rty = Y(ir), tlx = X(it), tly = Y(it);
+  const double flstep = (mny != lfy) ? (mnx - lfx) / double(mny - lfy) : 0;
+  const double slstep = (lfy != tly) ? (lfx - tlx) / double(lfy - tly) : 0;
+  const double frstep = (mny != rty) ? (mnx - rtx) / double(mny - rty) : 0;
+  const double srstep = (rty != tly) ? (rtx - tlx) / double(rty - tly) : 0;
+  double lstep = flstep, rstep = frstep;
+  double left_x = mnx, right_x = mnx;
+  // walk state: row y, next pixel x, last pixel xe (rows outside the image
+  // are skipped without step updates, as the reference's `continue`)
+  int y = mny, x = 1, xe = 0;
+  while (y <= mxy && (y < 0 || y >= sh)) y++;
+  if (y <= mxy) {
+    x = max((int)left_x, 0);
+    xe = min((int)right_x, sw - 1);
+  }
+  int total = 0, alg = 0;
+  const double theta = rec.theta, prec = rec.prec;
+  while (y <= mxy) {
+    int idx[8];
+    unsigned valid = 0;
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      while (y <= mxy && x > xe) {
+        if (y >= lfy) lstep = slstep;
+        if (y >= rty) rstep = srstep;
+        left_x += lstep;
+        right_x += rstep;
+        y++;
+        while (y <= mxy && (y < 0 || y >= sh)) y++;
+        if (y <= mxy) {
+          x = max((int)left_x, 0);
+          xe = min((int)right_x, sw - 1);
+        }
+      }
+      idx[u] = 0;
+      if (y <= mxy) {
+        idx[u] = y * sw + x;
+        valid |= 1u << u;
+        x++;
+      }
+    }
+    float dv[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) dv[u] = deg[idx[u]];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      if ((valid >> u) & 1u) {
+        total++;
+        alg += aligned_deg(dv[u], theta, prec) ? 1 : 0;
+      }
+    }
+  }
+  return nfa_lane(total, alg, rec.p, log_nt);
+}
+
+__device__ __forceinline__ double rect_improve_lane(const float* __restrict__ deg, int sw, int sh,
+                                                    Rect& rec, double log_nt) {
+  const double delta = 0.5, delta_2 = delta / 2.0;
+  double log_nfa = rect_nfa_lane(deg, sw, sh, rec, log_nt);
+  if (log_nfa > 0) return log_nfa;
+  for (int phase = 0; phase < 5; phase++) {
+    Rect r = rec;
+    for (int n = 0; n < 5; ++n) {
+      bool eval = true;
+      if (phase == 0) {
+        r.p /= 2;
+        r.prec = r.p * kPi;
+      } else if ((r.width - delta) >= 0.5) {
+        if (phase == 1) {
+          r.width -= delta;
+        } else if (phase == 2) {
+          r.x1 += -r.dy * delta_2;
+          r.y1 += r.dx * delta_2;
+          r.x2 += -r.dy * delta_2;
+          r.y2 += r.dx * delta_2;
+          r.width -= delta;
+        } else if (phase == 3) {
+          r.x1 -= -r.dy * delta_2;
+          r.y1 -= r.dx * delta_2;
+          r.x2 -= -r.dy * delta_2;
+          r.y2 -= r.dx * delta_2;
+          r.width -= delta;
+        } else {
+          r.p /= 2;
+          r.prec = r.p * kPi;
+        }
+      } else {
+        eval = false;
+      }
+      if (eval) {
+        const double v = rect_nfa_lane(deg, sw, sh, r, log_nt);
+        if (v > log_nfa) {
+          log_nfa = v;
+          rec = r;
+        }
+      }
+    }
+    if (log_nfa > 0) return log_nfa;
+  }
+  return log_nfa;
+}
+
 }  // namespace
 
 __global__ void __launch_bounds__(64) k_lsd_grow(LsdGeom g, LsdScratch sc) {
@@ -1134,46 +1327,31 @@ __global__ void __launch_bounds__(64) k_lsd_spec(LsdGeom g, LsdScratch sc) {
   }
 }
 
-// NFA validation of every refined rectangle (rect_improve), one wave per
-// rectangle, 4 waves per block; the accepted segments are compacted in seed
-// order by k_lsd_compact.
-constexpr int kValBlocks = 32;
+// NFA validation of every refined rectangle (rect_improve), one lane per
+// rectangle; the accepted segments are compacted in seed order by
+// k_lsd_compact.
+constexpr int kValBlocks = 8;
 
 __global__ void __launch_bounds__(256) k_lsd_validate(LsdGeom g, LsdScratch sc) {
-  extern __shared__ uint32_t val_smem[];
-  const int f = blockIdx.y, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int sh = g.sh;
-  const size_t per_wave = (size_t)4 * (sh + 2) + (2 * sizeof(Rect)) / 4;
-  uint32_t* base = val_smem + wave * per_wave;
-  Frame F{};
-  F.sw = g.sw;
-  F.sh = sh;
-  F.deg = sc.deg + (long long)f * g.sw * sh;
-  F.rows = reinterpret_cast<int4*>(base);
-  F.rect0 = reinterpret_cast<Rect*>(F.rows + (sh + 2));
-  F.rect1 = F.rect0 + 1;
-  F.row_cap = sh + 2;
-  F.log_nt = g.log_nt;
-  F.lane = lane;
+  const int f = blockIdx.y;
   const int nc = sc.ncand[f];
-  for (int c = blockIdx.x * 4 + wave; c < nc; c += kValBlocks * 4) {
+  const float* deg = sc.deg + (long long)f * g.sw * g.sh;
+  for (int c = blockIdx.x * 256 + threadIdx.x; c < nc; c += kValBlocks * 256) {
     const long long o = (long long)f * kLsdMaxCand + c;
-    double* rv = reinterpret_cast<double*>(F.rect0);
-    if (lane < 12) rv[lane] = sc.cand[o * 12 + lane];
-    __builtin_amdgcn_wave_barrier();
-    Rect& rec = *F.rect0;
-    const double log_nfa = rect_improve(F, rec);
-    if (lane == 0) {
-      const bool ok = log_nfa > 0;
-      sc.cand_ok[o] = ok;
-      if (ok) {
-        sc.cand_line[o * 4 + 0] = float((rec.x1 + 0.5) / 0.8);
-        sc.cand_line[o * 4 + 1] = float((rec.y1 + 0.5) / 0.8);
-        sc.cand_line[o * 4 + 2] = float((rec.x2 + 0.5) / 0.8);
-        sc.cand_line[o * 4 + 3] = float((rec.y2 + 0.5) / 0.8);
-      }
+    const double* rv = sc.cand + o * 12;
+    Rect rec;
+    rec.x1 = rv[0]; rec.y1 = rv[1]; rec.x2 = rv[2]; rec.y2 = rv[3];
+    rec.width = rv[4]; rec.x = rv[5]; rec.y = rv[6]; rec.theta = rv[7];
+    rec.dx = rv[8]; rec.dy = rv[9]; rec.prec = rv[10]; rec.p = rv[11];
+    const double log_nfa = rect_improve_lane(deg, g.sw, g.sh, rec, g.log_nt);
+    const bool ok = log_nfa > 0;
+    sc.cand_ok[o] = ok;
+    if (ok) {
+      sc.cand_line[o * 4 + 0] = float((rec.x1 + 0.5) / 0.8);
+      sc.cand_line[o * 4 + 1] = float((rec.y1 + 0.5) / 0.8);
+      sc.cand_line[o * 4 + 2] = float((rec.x2 + 0.5) / 0.8);
+      sc.cand_line[o * 4 + 3] = float((rec.y2 + 0.5) / 0.8);
     }
-    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -1201,12 +1379,7 @@ __global__ void __launch_bounds__(64) k_lsd_compact(LsdScratch sc) {
 }
 
 void launch_lsd_validate(const LsdGeom& g, const LsdScratch& sc, int batch, hipStream_t s) {
-  const size_t per_wave = (size_t)4 * (g.sh + 2) * 4 + 2 * sizeof(Rect);
-  const size_t smem = 4 * per_wave;
-  if (smem > 65536)
-    (void)hipFuncSetAttribute((const void*)k_lsd_validate,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-  hipLaunchKernelGGL(k_lsd_validate, dim3(kValBlocks, batch), dim3(256), smem, s, g, sc);
+  hipLaunchKernelGGL(k_lsd_validate, dim3(kValBlocks, batch), dim3(256), 0, s, g, sc);
   hipLaunchKernelGGL(k_lsd_compact, dim3(batch), dim3(64), 0, s, sc);
 }
 

@@ -10,6 +10,7 @@ namespace orbpl {
 
 constexpr int kLsdMaxLines = 4096;    // raw LSD segments kept per frame
 constexpr int kLsdMaxCand = 4096;     // refined rectangles awaiting NFA validation per frame
+constexpr int kSortLocalMax = 2048;   // introsort segments finished in LDS
 constexpr int kSpecLanes = 64;        // speculative regions per round (one wave)
 constexpr int kLaneCap = 2048;        // region points a lane can hold (both grows)
 constexpr int kLineKeep = 80;         // LineExtractor.cpp:24
@@ -63,6 +64,8 @@ struct LsdScratch {
   uint4* lbuf;         // kSpecLanes * kLaneCap per frame: per-lane region lists
                        // (x | y << 16, q, degrees, -)
   float4* pix;         // sw*sh per frame: degrees, q bits, cos, sin
+  int4* sort_local;    // seg_cap per frame: introsort segments finished in LDS
+  int* sort_nlocal;    // 1 per frame
 };
 
 // Outputs of LineExtractor::ExtractLineSegment per frame.

@@ -173,6 +173,9 @@ struct SortPtrs {
   int2* leaves;
   int seg_cap, chunk_cap, leaf_cap;
   int* err;
+  int4* local;     // segments of <= local_max elements deferred to k_lsd_sort_local
+  int* nlocal;
+  int local_max;   // 0: partition everything here
 };
 
 __device__ __forceinline__ int skey(uint32_t e) { return (int)(e >> 22); }
@@ -181,9 +184,10 @@ constexpr int kSortThreads = 1024, kSortWaves = kSortThreads / 64;
 
 // Exclusive scan of a[0..len) (global) in place by the whole block; returns
 // the total in every thread.
-__device__ int block_scan_global(int* a, int len, int* s_w) {
+template <int NT>
+__device__ __forceinline__ int block_scan_global(int* a, int len, int* s_w) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int per = (len + kSortThreads - 1) / kSortThreads;
+  const int per = (len + NT - 1) / NT;
   const int b = min(len, t * per), e = min(len, b + per);
   int sum = 0;
   for (int i = b; i < e; i++) sum += a[i];
@@ -195,7 +199,7 @@ __device__ int block_scan_global(int* a, int len, int* s_w) {
   if (lane == 63) s_w[wave] = incl;
   __syncthreads();
   int off = 0, tot = 0;
-  for (int w = 0; w < kSortWaves; w++) {
+  for (int w = 0; w < (NT / 64); w++) {
     const int v = s_w[w];
     if (w < wave) off += v;
     tot += v;
@@ -268,8 +272,11 @@ __device__ void heap_sort_seg(uint32_t* A, int len) {
   }
 }
 
-__device__ void sort_core(const SortPtrs& P, int n) {
-  __shared__ int s_w[kSortWaves];
+// Sorts A[first, last) whose introsort depth budget is depth0 (the top
+// level: 2 * floor(log2(n))). NT threads.
+template <int NT>
+__device__ __forceinline__ void sort_core(const SortPtrs& P, int first0, int last0, int depth0) {
+  __shared__ int s_w[(NT / 64)];
   __shared__ int s_nseg, s_next, s_nheap, s_nleaf;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   uint32_t* A = P.A;
@@ -286,12 +293,12 @@ __device__ void sort_core(const SortPtrs& P, int n) {
     s_nheap = 0;
     s_nleaf = 0;
     s_nseg = 0;
+    const int n = last0 - first0;
     if (n > 16) {
-      const int lg = 31 - __clz(n);
-      P.seg0[0] = make_int4(0, n, 2 * lg, 0);
+      P.seg0[0] = make_int4(first0, last0, depth0, 0);
       s_nseg = 1;
     } else if (n > 1) {
-      P.leaves[0] = make_int2(0, n);
+      P.leaves[0] = make_int2(first0, last0);
       s_nleaf = 1;
     }
   }
@@ -304,7 +311,7 @@ __device__ void sort_core(const SortPtrs& P, int n) {
     if (nseg == 0) break;
     if (t == 0) s_next = 0;
     // R1: median of three into first, pivot key, chunk counts
-    for (int s = t; s < nseg; s += kSortThreads) {
+    for (int s = t; s < nseg; s += NT) {
       const int4 sg = cur[s];
       const int first = sg.x, last = sg.y;
       const int mid = first + (last - first) / 2;
@@ -314,13 +321,13 @@ __device__ void sort_core(const SortPtrs& P, int n) {
       choff[s] = nch[s];
     }
     __syncthreads();
-    const int nchunks = block_scan_global(choff, nseg, s_w);
+    const int nchunks = block_scan_global<NT>(choff, nseg, s_w);
     if (nchunks > P.chunk_cap) {
       if (t == 0) *P.err |= 1;
       return;
     }
     // R3: per chunk L / R stopper counts
-    for (int ch = wave; ch < nchunks; ch += kSortWaves) {
+    for (int ch = wave; ch < nchunks; ch += (NT / 64)) {
       int lo = 0, hi = nseg;  // last segment with choff <= ch
       while (hi - lo > 1) {
         const int m = (lo + hi) >> 1;
@@ -352,12 +359,12 @@ __device__ void sort_core(const SortPtrs& P, int n) {
       }
     }
     __syncthreads();
-    block_scan_global(Lpre, nchunks, s_w);
-    const int totR = block_scan_global(Rsuf, nchunks, s_w);
-    for (int c = t; c < nchunks; c += kSortThreads) Rsuf[c] = totR - Rsuf[c] - Rc[c];
+    block_scan_global<NT>(Lpre, nchunks, s_w);
+    const int totR = block_scan_global<NT>(Rsuf, nchunks, s_w);
+    for (int c = t; c < nchunks; c += NT) Rsuf[c] = totR - Rsuf[c] - Rc[c];
     __syncthreads();
     // R5: scatter stopper positions by rank
-    for (int ch = wave; ch < nchunks; ch += kSortWaves) {
+    for (int ch = wave; ch < nchunks; ch += (NT / 64)) {
       int lo = 0, hi = nseg;
       while (hi - lo > 1) {
         const int m = (lo + hi) >> 1;
@@ -403,7 +410,7 @@ __device__ void sort_core(const SortPtrs& P, int n) {
     }
     __syncthreads();
     // R6: swap count K and cut per segment
-    for (int s = t; s < nseg; s += kSortThreads) {
+    for (int s = t; s < nseg; s += NT) {
       const int4 sg = cur[s];
       const int first = sg.x, last = sg.y;
       const int c0 = choff[s], c1 = c0 + nch[s] - 1;
@@ -424,7 +431,7 @@ __device__ void sort_core(const SortPtrs& P, int n) {
     }
     __syncthreads();
     // R7: swaps (disjoint pairs)
-    for (int ch = wave; ch < nchunks; ch += kSortWaves) {
+    for (int ch = wave; ch < nchunks; ch += (NT / 64)) {
       int lo = 0, hi = nseg;
       while (hi - lo > 1) {
         const int m = (lo + hi) >> 1;
@@ -444,14 +451,18 @@ __device__ void sort_core(const SortPtrs& P, int n) {
     }
     __syncthreads();
     // R8: children
-    for (int s = t; s < nseg; s += kSortThreads) {
+    for (int s = t; s < nseg; s += NT) {
       const int4 sg = cur[s];
       const int cut = scut[s], d = sg.z - 1;
       const int bs[2] = {cut, sg.x}, es[2] = {sg.y, cut};
       for (int c = 0; c < 2; c++) {
         const int b = bs[c], e = es[c], size = e - b;
         if (size > 16) {
-          if (d > 0) {
+          if (d > 0 && size <= P.local_max) {
+            const int idx = atomicAdd(P.nlocal, 1);
+            if (idx < P.seg_cap) P.local[idx] = make_int4(b, e, d, 0);
+            else atomicOr(P.err, 2);
+          } else if (d > 0) {
             const int idx = atomicAdd(&s_next, 1);
             if (idx < P.seg_cap) nxt[idx] = make_int4(b, e, d, 0);
             else atomicOr(P.err, 2);
@@ -475,11 +486,11 @@ __device__ void sort_core(const SortPtrs& P, int n) {
     __syncthreads();
   }
   const int nheap = min(s_nheap, P.seg_cap), nleaf = min(s_nleaf, P.leaf_cap);
-  for (int h = t; h < nheap; h += kSortThreads) {
+  for (int h = t; h < nheap; h += NT) {
     const int4 sg = P.heap[h];
     heap_sort_seg(A + sg.x, sg.y - sg.x);
   }
-  for (int l = t; l < nleaf; l += kSortThreads) {
+  for (int l = t; l < nleaf; l += NT) {
     const int2 lf = P.leaves[l];
     for (int i = lf.x + 1; i < lf.y; i++) {
       const uint32_t v = A[i];
@@ -510,7 +521,58 @@ __device__ SortPtrs sort_ptrs(const LsdGeom& g, const LsdScratch& sc, int f) {
   P.chunk_cap = g.chunk_cap;
   P.leaf_cap = g.leaf_cap;
   P.err = sc.err + f;
+  P.local = sc.sort_local + (long long)f * g.seg_cap;
+  P.nlocal = sc.sort_nlocal + f;
+  P.local_max = kSortLocalMax;
   return P;
+}
+
+// The top levels of the introsort run in k_lsd_sort over global memory;
+// segments of at most kSortLocalMax elements are finished here, each loaded
+// into LDS and sorted by one 256-thread block (same partition replay).
+constexpr int kLocalThreads = 256;
+constexpr int kLSeg = kSortLocalMax / 17 + 2;
+constexpr int kLChunk = kSortLocalMax / kLsdSortChunk + kLSeg + 2;
+constexpr int kLLeaf = kSortLocalMax / 2 + 2;
+constexpr int kSortLocalBlocks = 4;
+
+__global__ void __launch_bounds__(kLocalThreads) k_lsd_sort_local(LsdGeom g, LsdScratch sc) {
+  __shared__ uint32_t sA[kSortLocalMax];
+  __shared__ int sL[kSortLocalMax], sR[kSortLocalMax];
+  __shared__ int4 sseg0[kLSeg], sseg1[kLSeg], sheap[kLSeg];
+  __shared__ int ssi[8 * kLSeg];
+  __shared__ int sci[4 * kLChunk];
+  __shared__ int2 sleaves[kLLeaf];
+  const int f = blockIdx.y, t = threadIdx.x;
+  uint32_t* A = sc.A + (long long)f * g.n;
+  const int nloc = min(sc.sort_nlocal[f], g.seg_cap);
+  const int4* loc = sc.sort_local + (long long)f * g.seg_cap;
+  SortPtrs L;
+  L.A = sA;
+  L.Lpos = sL;
+  L.Rpos = sR;
+  L.seg0 = sseg0;
+  L.seg1 = sseg1;
+  L.heap = sheap;
+  L.si = ssi;
+  L.ci = sci;
+  L.leaves = sleaves;
+  L.seg_cap = kLSeg;
+  L.chunk_cap = kLChunk;
+  L.leaf_cap = kLLeaf;
+  L.err = sc.err + f;
+  L.local = nullptr;
+  L.nlocal = nullptr;
+  L.local_max = 0;
+  for (int k = blockIdx.x; k < nloc; k += gridDim.x) {
+    const int4 sg = loc[k];
+    const int m = sg.y - sg.x;
+    for (int i = t; i < m; i += kLocalThreads) sA[i] = A[sg.x + i];
+    __syncthreads();
+    sort_core<kLocalThreads>(L, 0, m, sg.z);
+    for (int i = t; i < m; i += kLocalThreads) A[sg.x + i] = sA[i];
+    __syncthreads();
+  }
 }
 
 __global__ void __launch_bounds__(kSortThreads) k_lsd_sort(LsdGeom g, LsdScratch sc) {
@@ -527,8 +589,9 @@ __global__ void __launch_bounds__(kSortThreads) k_lsd_sort(LsdGeom g, LsdScratch
     const int key = (int)(sqrt(q[y * sw + x] / 4.0) * bin_coef);
     P.A[i] = ((uint32_t)key << 22) | (uint32_t)i;
   }
+  if (threadIdx.x == 0) *P.nlocal = 0;
   __syncthreads();
-  sort_core(P, g.n);
+  sort_core<kSortThreads>(P, 0, g.n, g.n > 16 ? 2 * (31 - __clz(g.n)) : 0);
 }
 
 // test hook: sort caller-provided keys (frame slot 0)
@@ -537,8 +600,9 @@ __global__ void __launch_bounds__(kSortThreads) k_lsd_sort_keys(LsdGeom g, LsdSc
   const SortPtrs P = sort_ptrs(g, sc, 0);
   for (int i = threadIdx.x; i < g.n; i += kSortThreads)
     P.A[i] = ((uint32_t)keys[i] << 22) | (uint32_t)i;
+  if (threadIdx.x == 0) *P.nlocal = 0;
   __syncthreads();
-  sort_core(P, g.n);
+  sort_core<kSortThreads>(P, 0, g.n, g.n > 16 ? 2 * (31 - __clz(g.n)) : 0);
 }
 
 void launch_lsd_blur(const LsdGeom& g, const uint8_t* img, int stride, long long frame_pitch,
@@ -561,6 +625,8 @@ void launch_lsd_grad(const LsdGeom& g, const uint8_t* scaled, float* deg, int* q
 
 void launch_lsd_sort(const LsdGeom& g, const LsdScratch& sc, int batch, hipStream_t s) {
   hipLaunchKernelGGL(k_lsd_sort, dim3(batch), dim3(kSortThreads), 0, s, g, sc);
+  hipLaunchKernelGGL(k_lsd_sort_local, dim3(kSortLocalBlocks, batch), dim3(kLocalThreads), 0, s,
+                     g, sc);
 }
 
 void launch_lsd_sort_keys(int n, const int* keys, const LsdScratch& sc, hipStream_t s) {
@@ -570,6 +636,8 @@ void launch_lsd_sort_keys(int n, const int* keys, const LsdScratch& sc, hipStrea
   g.chunk_cap = n / kLsdSortChunk + g.seg_cap + 2;
   g.leaf_cap = n / 2 + 2;
   hipLaunchKernelGGL(k_lsd_sort_keys, dim3(1), dim3(kSortThreads), 0, s, g, sc, keys);
+  hipLaunchKernelGGL(k_lsd_sort_local, dim3(kSortLocalBlocks, 1), dim3(kLocalThreads), 0, s, g,
+                     sc);
 }
 
 }  // namespace orbpl

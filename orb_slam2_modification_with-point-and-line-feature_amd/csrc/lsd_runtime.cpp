@@ -239,6 +239,8 @@ int lsdx_create(int width, int height, int max_batch, int device, lsdx_ctx** out
   LA(s.stamp, B * px * 4);
   LA(s.lbuf, B * kSpecLanes * kLaneCap * sizeof(uint4));
   LA(s.pix, B * px * sizeof(float4));
+  LA(s.sort_local, B * g.seg_cap * sizeof(int4));
+  LA(s.sort_nlocal, B * 4);
   LA(c->d_tabs, (size_t)(2 * g.sw + 2 * g.sh) * 4);
   LA(c->blur5, B * width * height);
   LA(c->sdx, B * width * height * 2);
@@ -458,6 +460,8 @@ int orbpl_test_introsort(const int* keys, int n, int* perm) {
   e = e ? e : A((void**)&sc.chunk_i, (size_t)4 * chunk_cap * 4);
   e = e ? e : A((void**)&sc.leaves, (size_t)leaf_cap * sizeof(int2));
   e = e ? e : A((void**)&sc.err, 4);
+  e = e ? e : A((void**)&sc.sort_local, (size_t)seg_cap * sizeof(int4));
+  e = e ? e : A((void**)&sc.sort_nlocal, 4);
   int rc = ORBPL_OK, err = 0;
   std::vector<uint32_t> a(n);
   if (e == hipSuccess) e = hipMemcpy(d_keys, keys, (size_t)n * 4, hipMemcpyHostToDevice);
