@@ -599,6 +599,12 @@ __device__ __forceinline__ double rect_improve(Frame& F, Rect& rec) {
 // list in seed order. A region longer than a lane's buffer is processed by
 // the wave-cooperative serial code once it is the first uncommitted seed.
 // ---------------------------------------------------------------------------
+// One wave owns a frame's speculative state, so ordering its own global
+// stores and loads needs only a workgroup-scope fence (s_waitcnt; the CU's
+// L1 is coherent for its waves) - an agent-scope __threadfence would write
+// back the whole L2 on gfx950.
+__device__ __forceinline__ void wg_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+
 enum { kSpecConflict = -1, kSpecOverflow = -2, kSpecSmall = 0, kSpecFail = 1, kSpecCand = 2 };
 
 __device__ __forceinline__ uint32_t ld_stamp(const uint32_t* p) {
@@ -1121,12 +1127,15 @@ __global__ void __launch_bounds__(64) k_lsd_spec(LsdGeom g, LsdScratch sc) {
   F.deg = sc.deg + (long long)f * sw * sh;
   F.q = sc.q + (long long)f * sw * sh;
   F.used = grow_smem;
-  F.reg_l = grow_smem + used_words;
+  // the cooperative fallback's region list head and prefetch ring live in
+  // the (then idle) lane buffers, so LDS holds only the USED bits
+  uint32_t* coop = reinterpret_cast<uint32_t*>(sc.lbuf + (long long)f * kSpecLanes * kLaneCap);
+  F.reg_l = coop;
   F.regq_l = reinterpret_cast<int*>(F.reg_l + kRegLds);
   F.regd_l = reinterpret_cast<float*>(F.regq_l + kRegLds);
   F.ring = F.regd_l + kRegLds;
   F.reg_g = sc.reg + (long long)f * 3 * sw * sh;
-  F.rows = reinterpret_cast<int4*>(grow_smem + ((used_words + 3 * kRegLds + 64 * 9 + 3) & ~3));
+  F.rows = reinterpret_cast<int4*>(grow_smem + ((used_words + 3) & ~3));
   F.rect0 = reinterpret_cast<Rect*>(F.rows);
   F.rect1 = F.rect0 + 1;
   F.row_cap = 0;
@@ -1217,7 +1226,7 @@ __global__ void __launch_bounds__(64) k_lsd_spec(LsdGeom g, LsdScratch sc) {
                              touched);
       }
     }
-    __threadfence();
+    wg_fence();
     __builtin_amdgcn_wave_barrier();
     const long long t2 = clock64();
     cyc_spec += t1 - t0;
@@ -1390,7 +1399,8 @@ size_t lsd_grow_smem(const LsdGeom& g) {
 
 void launch_lsd_grow(const LsdGeom& g, const LsdScratch& sc, int batch, hipStream_t s,
                      bool serial) {
-  const size_t smem = lsd_grow_smem(g);
+  const int used_words = (g.sw * g.sh + 31) / 32;
+  const size_t smem = serial ? lsd_grow_smem(g) : 4 * (size_t)((used_words + 3) & ~3) + 2 * sizeof(Rect);
   const void* k = serial ? (const void*)k_lsd_grow : (const void*)k_lsd_spec;
   if (smem > 65536)
     (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
