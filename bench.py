@@ -89,6 +89,23 @@ def algorithmic_bytes(n_kp):
     }
 
 
+def pmc_traffic(kernel, streams):
+    """HBM bytes per launch of `kernel` from the committed PMC summary of the
+    same bench command (tools/prof.sh + tools/pmc_traffic.py; FETCH_SIZE x2
+    gfx950 correction + WRITE_SIZE), scaled to this run's stream count. PMC
+    counters need their own rocprofv3 passes, so they cannot be read live."""
+    for rnd in ("r01",):
+        f = ROOT / "profiles" / rnd / "pmc_traffic.json"
+        if f.exists():
+            d = json.load(open(f))
+            e = d.get(kernel)
+            meta = d.get("_meta", {})
+            if e and e.get("traffic_bytes") and meta.get("streams"):
+                return (int(e["traffic_bytes"] * streams / meta["streams"]),
+                        f"profiles/{rnd}/pmc_traffic.json ({meta['streams']} streams, scaled)")
+    return None, None
+
+
 def cpu_baseline(seconds, threads, gray, depth, lines=False):
     """The CPU oracle (C++ restatement, oracle/) running the same per-frame
     step, one stream per thread (throughput mode), for a bounded wall time."""
@@ -189,9 +206,11 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, loca
     dom_ms = float(avg[idx[dom]])
     bytes_launch = int(ab[dom] * S)
     achieved = bytes_launch / (dom_ms * 1e-3) / 1e9
+    traffic, tsrc = pmc_traffic(names[dom], S)
     roof = {"bound": "hbm", "kernel": names[dom],
             "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+            "traffic_source": tsrc,
             "algorithmic_bytes_per_launch": bytes_launch, "avg_launch_ms": round(dom_ms, 4),
             "per_kernel_GBps": {k: round(ab[k] * S / (float(avg[idx[k]]) * 1e-3) / 1e9, 1)
                                 for k in names}}
@@ -221,7 +240,7 @@ def main():
     ap.add_argument("--secondary-steps", type=int, default=3,
                     help="steps of the configs[2] lines workload reported under 'secondary' "
                          "(points runs only; 0 = skip)")
-    ap.add_argument("--lines-streams", type=int, default=256)
+    ap.add_argument("--lines-streams", type=int, default=1536)
     ap.add_argument("--pipelined", type=int, default=0,
                     help="1 = overlap extraction of step t+1 with tracking of step t")
     args = ap.parse_args()

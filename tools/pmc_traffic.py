@@ -1,0 +1,65 @@
+"""Summarise a tools/prof.sh run into per-kernel HBM traffic per launch.
+
+Reads gpurun_out/prof_<tag>/{trace,fetch,write}/ (rocprofv3 csv) and writes
+profiles/<round>/pmc_traffic.json:
+  {kernel: {"launches", "avg_ns", "fetch_bytes", "write_bytes", "traffic_bytes"}}
+per launch, averaged over the launches of the profiled bench command.
+gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts half
+the bytes of wide coalesced reads, so fetch_bytes = 2 * FETCH_SIZE; WRITE_SIZE
+is taken as is. Both counters are in KiB.
+
+usage: python tools/pmc_traffic.py <tag> <round> [streams]
+"""
+import collections
+import csv
+import json
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def short(name):
+    n = name.split("(")[0]
+    n = n.replace("void ", "").replace("orbpl::", "")
+    return n.split("<")[0]
+
+
+def main():
+    tag, rnd = sys.argv[1], sys.argv[2]
+    base = ROOT / "gpurun_out" / f"prof_{tag}"
+    out = {}
+    dur = collections.defaultdict(list)
+    for r in csv.DictReader(open(base / "trace" / "run_kernel_trace.csv")):
+        dur[short(r["Kernel_Name"])].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    cnt = {}
+    for part in ("fetch", "write"):
+        vals = collections.defaultdict(list)
+        for r in csv.DictReader(open(base / part / "run_counter_collection.csv")):
+            vals[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
+        cnt[part] = vals
+    for k, v in dur.items():
+        if "rocclr" in k:
+            continue
+        f = cnt["fetch"].get(k, [])
+        w = cnt["write"].get(k, [])
+        fb = 2.0 * 1024.0 * sum(f) / len(f) if f else None
+        wb = 1024.0 * sum(w) / len(w) if w else None
+        out[k] = {"launches": len(v), "avg_ns": sum(v) / len(v),
+                  "fetch_bytes": fb, "write_bytes": wb,
+                  "traffic_bytes": (fb + wb) if fb is not None and wb is not None else None}
+    out["_meta"] = {"streams": int(sys.argv[3]) if len(sys.argv) > 3 else 256,
+                    "source": f"gpurun_out/prof_{tag}", "correction": "fetch x2 (gfx950)"}
+    dst = ROOT / "profiles" / rnd / "pmc_traffic.json"
+    dst.parent.mkdir(parents=True, exist_ok=True)
+    json.dump(out, open(dst, "w"), indent=1, sort_keys=True)
+    for k in sorted((k for k in out if k != "_meta"),
+                    key=lambda k: -out[k]["avg_ns"] * out[k]["launches"])[:14]:
+        e = out[k]
+        tb = e["traffic_bytes"]
+        print(f"{k:28s} n={e['launches']:3d} avg {e['avg_ns'] / 1e3:9.1f} us  traffic "
+              f"{(tb or 0) / 1e6:9.2f} MB/launch")
+
+
+if __name__ == "__main__":
+    main()

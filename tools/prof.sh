@@ -2,15 +2,18 @@
 # Profiling passes on the GPU box (rocprofv3). Kernel trace + stats first,
 # then PMC passes, each counter group in its own run (no tracing domains
 # combined with --pmc). Outputs under gpurun_out/prof_<tag>/.
-# The bench command runs the points headline and the configs[2] lines
-# workload (secondary), so both kernel sets are covered.
 set -o pipefail
 tag=${1:-run}
 out=gpurun_out/prof_$tag
 mkdir -p $out
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-B="$R/bench.py --steps 4 --warmup 2 --secondary-steps 2 --no-cpu-baseline"
+# points headline (256 streams) by default; MODE=lines profiles configs[2]
+if [ "$MODE" = "lines" ]; then
+  B="$R/bench.py --workload lines --streams 1536 --steps 3 --warmup 1 --no-cpu-baseline"
+else
+  B="$R/bench.py --steps 4 --warmup 2 --secondary-steps 0 --no-cpu-baseline"
+fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$out/trace -o run --output-format csv -- python3 $B > $R/$out/trace.log 2>&1 || { echo "trace failed"; tail -5 $R/$out/trace.log; exit 1; }
 echo trace ok
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $R/$out/fetch -o run --output-format csv -- python3 $B > $R/$out/fetch.log 2>&1 || { echo "fetch failed"; tail -5 $R/$out/fetch.log; exit 1; }
