@@ -297,6 +297,30 @@ int orbpl_tracker_get_lines(orbpl_tracker* tr, int stream, orbpl_keyline* kl_un,
 int orbpl_tracker_line_timings(orbpl_tracker* tr, int max_steps, float* ms, int* n_steps);
 
 /* ------------------------------------------------------------------------
+ * Line tracking, single frame, host pointers (n <= 80 = LineExtractor's cap)
+ * ---------------------------------------------------------------------- */
+/* Frame::UndistortKeyLines (Frame.cc:769-845) + the line part of
+ * ComputeStereoFromRGBD (Frame.cc:1090-1116): undistorted key lines, depth
+ * at the distorted end points (-1 = none; imDepth.at<float>(int(v), int(u))
+ * on the row-major image) and uRight = x_un - bf / depth (-1 = none). depth
+ * may be NULL (no depth: all -1). */
+int orbpl_line_frame_prepare(const orbpl_camera* cam, const orbpl_keyline* kl, int n,
+                             const float* depth, orbpl_keyline* kl_un, float* dstart, float* dend,
+                             float* ur_start, float* ur_end);
+/* LineMatcher(0.9, true).SearchByProjection(CurrentFrame, LastFrame)
+ * (LineMatcher.cpp:72-269): last-frame map lines (has_ml, outlier flags,
+ * world start/end xyz x6, LBD rows) projected with Tcw and Liang-Barsky
+ * clipped to the image bounds; every (projected, current) pair passing
+ * LineMatching counts, the last passing one wins; one relaxed retry when
+ * matches / ncur < 0.2. match[j] = last-frame index or -1. */
+int orbl_search_by_projection_last(const orbpl_camera* cam, const float* Tcw, int ncur,
+                                   const orbpl_keyline* cur_kl_un, const uint8_t* cur_desc,
+                                   int nlast, const orbpl_keyline* last_kl_un,
+                                   const uint8_t* has_ml, const uint8_t* last_outlier,
+                                   const float* ml_xyz6, const uint8_t* last_desc, int32_t* match,
+                                   int* nmatches);
+
+/* ------------------------------------------------------------------------
  * Hamming distance — ORBmatcher::DescriptorDistance (ORBmatcher.cc:2083-2103)
  * ---------------------------------------------------------------------- */
 int orbpl_descriptor_distance(const uint8_t* a32, const uint8_t* b32);

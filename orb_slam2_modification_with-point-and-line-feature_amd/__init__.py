@@ -340,6 +340,8 @@ def _declare_track(L):
     L.orbpl_tracker_timings_reset.argtypes = [vp]
     L.orbpl_tracker_get_frame.argtypes = [vp, i, vp, vp, vp, vp, ip]
     L.orbpl_tracker_create_ex.argtypes = [vp, vp, i, i, i, C.POINTER(vp)]
+    L.orbpl_line_frame_prepare.argtypes = [vp, vp, i, vp, vp, vp, vp, vp, vp]
+    L.orbl_search_by_projection_last.argtypes = [vp, vp, i, vp, vp, i, vp, vp, vp, vp, vp, vp, ip]
     L.orbpl_tracker_get_status.argtypes = [vp, vp, vp, vp, vp]
     L.orbpl_tracker_get_lines.argtypes = [vp, i, vp, vp, vp, vp, ip]
     L.orbpl_tracker_line_timings.argtypes = [vp, i, vp, ip]
@@ -434,6 +436,41 @@ def pose_optimization(camera, prob, Tcw, outlier, line_outlier=None):
     check(lib().orbpl_pose_optimization(C.byref(camera), C.byref(P), _ptr(T), _ptr(out),
                                         _ptr(lout), C.byref(nin)), "orbpl_pose_optimization")
     return T, out, lout, nin.value
+
+
+def line_frame_prepare(camera, kl, depth=None):
+    """Frame::UndistortKeyLines + line depths (orbpl_line_frame_prepare):
+    (kl_un, depth_start, depth_end, uright_start, uright_end)."""
+    kl = np.ascontiguousarray(kl, KEYLINE_DTYPE)
+    n = len(kl)
+    ku = np.zeros(n, KEYLINE_DTYPE)
+    ds, de, us, ue = (np.zeros(n, np.float32) for _ in range(4))
+    dp = None if depth is None else np.ascontiguousarray(depth, np.float32)
+    check(lib().orbpl_line_frame_prepare(C.byref(camera), _ptr(kl), n,
+                                         None if dp is None else _ptr(dp), _ptr(ku), _ptr(ds),
+                                         _ptr(de), _ptr(us), _ptr(ue)), "orbpl_line_frame_prepare")
+    return ku, ds, de, us, ue
+
+
+class LineMatcher:
+    """LineMatcher(0.9, true) tracking overload on the GPU."""
+
+    @staticmethod
+    def SearchByProjectionLastFrame(camera, Tcw, cur_kl_un, cur_desc, last_kl_un, has_ml, outlier,
+                                    ml_xyz6, last_desc):
+        keep = [np.ascontiguousarray(Tcw, np.float32), np.ascontiguousarray(cur_kl_un, KEYLINE_DTYPE),
+                np.ascontiguousarray(cur_desc, np.uint8),
+                np.ascontiguousarray(last_kl_un, KEYLINE_DTYPE), np.ascontiguousarray(has_ml, np.uint8),
+                np.ascontiguousarray(outlier, np.uint8), np.ascontiguousarray(ml_xyz6, np.float32),
+                np.ascontiguousarray(last_desc, np.uint8)]
+        ncur = len(keep[1])
+        match = np.zeros(max(1, ncur), np.int32)
+        nm = C.c_int(0)
+        check(lib().orbl_search_by_projection_last(
+            C.byref(camera), _ptr(keep[0]), ncur, _ptr(keep[1]), _ptr(keep[2]), len(keep[3]),
+            _ptr(keep[3]), _ptr(keep[4]), _ptr(keep[5]), _ptr(keep[6]), _ptr(keep[7]), _ptr(match),
+            C.byref(nm)), "orbl_search_by_projection_last")
+        return match[:ncur].copy(), nm.value
 
 
 class Tracker:

@@ -23,7 +23,7 @@ __global__ void __launch_bounds__(64) k_line_prepare(TrackConsts c, LineTrackArg
   const int nl = a.nl[s];
   const long long lb = (long long)s * kLineKeep;
   const int W = c.width, H = c.height;
-  const float* depth = a.depth + (long long)s * a.depth_pitch;
+  const float* depth = a.depth ? a.depth + (long long)s * a.depth_pitch : nullptr;
   for (int j = lane; j < nl; j += 64) {
     const orbpl_keyline k0 = a.kl[lb + j];
     orbpl_keyline k = k0;
@@ -45,12 +45,16 @@ __global__ void __launch_bounds__(64) k_line_prepare(TrackConsts c, LineTrackArg
     // imDepth.at<float>(int(v), int(u)) on the distorted end points (P14)
     auto at = [&](float v, float u) -> float {
       const long long idx = (long long)(int)v * W + (int)u;
-      return (idx >= 0 && idx < (long long)W * H) ? depth[idx] : 0.f;
+      return (depth && idx >= 0 && idx < (long long)W * H) ? depth[idx] : 0.f;
     };
     const float ds = at(k0.startPointY, k0.startPointX);
     const float de = at(k0.endPointY, k0.endPointX);
     a.dstart[lb + j] = ds > 0 ? ds : -1.f;
     a.dend[lb + j] = de > 0 ? de : -1.f;
+    if (a.ur_start) {
+      a.ur_start[lb + j] = ds > 0 ? k.startPointX - c.bf / ds : -1.f;
+      a.ur_end[lb + j] = de > 0 ? k.endPointX - c.bf / de : -1.f;
+    }
     a.lmatch[lb + j] = -1;
     a.loutlier[lb + j] = 0;
   }
@@ -172,7 +176,7 @@ __global__ void __launch_bounds__(256) k_line_match(TrackConsts c, LineTrackArgs
     return;
   }
   const long long lb = (long long)s * kLineKeep;
-  const int ncur = a.nl[s], nlast = a.last_nl[s];
+  const int ncur = min(a.nl[s], kLineKeep), nlast = min(a.last_nl[s], kLineKeep);
   const int W = c.width, H = c.height;
   // ---- project the last frame's map lines with the predicted pose ----
   bool valid = false;

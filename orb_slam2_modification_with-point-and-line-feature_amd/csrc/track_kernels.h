@@ -80,6 +80,8 @@ struct LineTrackArgs {
   long long depth_pitch;
   float* dstart;                 // mvDepthLineStart (-1 = none)
   float* dend;                   // mvDepthLineEnd
+  float* ur_start;               // optional (host API): start.x - bf / depth, -1 = none
+  float* ur_end;
   int* lmatch;                   // matched last-frame line, -1 = none
   uint8_t* loutlier;             // mvbLineOutlier
   const uint8_t* desc;           // current LBD rows

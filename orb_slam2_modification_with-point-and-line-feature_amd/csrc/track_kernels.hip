@@ -373,13 +373,16 @@ __global__ void __launch_bounds__(256) k_match_last(TrackConsts c, MatchArgs a) 
                 if (dist > 100) continue;
                 cnt++;
                 int v = (dist << 16) | j;
-                // stable insertion: equal distances keep scan order
+                // stable insertion: equal distances keep scan order; once
+                // inserted, the displaced entries shift down one place each
+                bool ins = false;
 #pragma unroll
                 for (int q2 = 0; q2 < kTopK; q2++) {
                   const int cur = tk[q2];
-                  if (cur < 0 || (v >> 16) < (cur >> 16)) {
+                  if (ins || cur < 0 || (v >> 16) < (cur >> 16)) {
                     tk[q2] = v;
                     v = cur;
+                    ins = true;
                     if (v < 0) break;
                   }
                 }

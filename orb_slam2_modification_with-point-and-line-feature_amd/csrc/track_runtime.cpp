@@ -272,6 +272,118 @@ int orbpl_pose_optimization(const orbpl_camera* cam, const orbpl_pose_problem* P
   return ORBPL_OK;
 }
 
+int orbpl_line_frame_prepare(const orbpl_camera* cam, const orbpl_keyline* kl, int n,
+                             const float* depth, orbpl_keyline* kl_un, float* dstart, float* dend,
+                             float* ur_start, float* ur_end) {
+  if (!cam || n < 0 || (n > 0 && (!kl || !kl_un || !dstart || !dend || !ur_start || !ur_end)))
+    return arg_fail("bad argument");
+  if (n > kLineKeep) return arg_fail("more key lines than LineExtractor keeps (80)");
+  TrackConsts c;
+  int rc = make_consts(cam, nullptr, nullptr, 1, &c);
+  if (rc) return rc;
+  if (n == 0) return ORBPL_OK;
+  DBuf dn, dkl, dku, dd, dds, dde, dus, due;
+  const size_t imgb = depth ? (size_t)cam->width * cam->height * 4 : 0;
+  HIP_CHECK(dn.alloc(4));
+  HIP_CHECK(dkl.alloc((size_t)kLineKeep * sizeof(orbpl_keyline)));
+  HIP_CHECK(dku.alloc((size_t)kLineKeep * sizeof(orbpl_keyline)));
+  if (depth) HIP_CHECK(dd.alloc(imgb));
+  HIP_CHECK(dds.alloc(kLineKeep * 4));
+  HIP_CHECK(dde.alloc(kLineKeep * 4));
+  HIP_CHECK(dus.alloc(kLineKeep * 4));
+  HIP_CHECK(due.alloc(kLineKeep * 4));
+  DBuf dlm, dlo;
+  HIP_CHECK(dlm.alloc(kLineKeep * 4));
+  HIP_CHECK(dlo.alloc(kLineKeep));
+  HIP_CHECK(hipMemcpy(dn.p, &n, 4, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(dkl.p, kl, (size_t)n * sizeof(orbpl_keyline), hipMemcpyHostToDevice));
+  if (depth) HIP_CHECK(hipMemcpy(dd.p, depth, imgb, hipMemcpyHostToDevice));
+  LineTrackArgs a{};
+  a.nl = dn.as<int>();
+  a.kl = dkl.as<orbpl_keyline>();
+  a.kl_un = dku.as<orbpl_keyline>();
+  a.depth = depth ? dd.as<float>() : nullptr;
+  a.depth_pitch = 0;
+  a.dstart = dds.as<float>();
+  a.dend = dde.as<float>();
+  a.ur_start = dus.as<float>();
+  a.ur_end = due.as<float>();
+  a.lmatch = dlm.as<int>();
+  a.loutlier = dlo.as<uint8_t>();
+  launch_line_prepare(c, a, 1, scratch_stream());
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipMemcpy(kl_un, dku.p, (size_t)n * sizeof(orbpl_keyline), hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(dstart, dds.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(dend, dde.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(ur_start, dus.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(ur_end, due.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+  return ORBPL_OK;
+}
+
+int orbl_search_by_projection_last(const orbpl_camera* cam, const float* Tcw, int ncur,
+                                   const orbpl_keyline* cur_kl_un, const uint8_t* cur_desc,
+                                   int nlast, const orbpl_keyline* last_kl_un,
+                                   const uint8_t* has_ml, const uint8_t* last_outlier,
+                                   const float* ml_xyz6, const uint8_t* last_desc, int32_t* match,
+                                   int* nmatches) {
+  if (!cam || !Tcw || !nmatches || ncur < 0 || nlast < 0) return arg_fail("bad argument");
+  if (ncur > kLineKeep || nlast > kLineKeep)
+    return arg_fail("more key lines than LineExtractor keeps (80)");
+  if ((ncur > 0 && (!cur_kl_un || !cur_desc || !match)) ||
+      (nlast > 0 && (!last_kl_un || !has_ml || !last_outlier || !ml_xyz6 || !last_desc)))
+    return arg_fail("NULL line arrays");
+  TrackConsts c;
+  int rc = make_consts(cam, nullptr, nullptr, 1, &c);
+  if (rc) return rc;
+  const size_t L = kLineKeep;
+  DBuf dn, dln, dku, dde, dlk, dhm, dlo, dxyz, dld, dm, dst;
+  HIP_CHECK(dn.alloc(4));
+  HIP_CHECK(dln.alloc(4));
+  HIP_CHECK(dku.alloc(L * sizeof(orbpl_keyline)));
+  HIP_CHECK(dde.alloc(L * 32));
+  HIP_CHECK(dlk.alloc(L * sizeof(orbpl_keyline)));
+  HIP_CHECK(dhm.alloc(L));
+  HIP_CHECK(dlo.alloc(L));
+  HIP_CHECK(dxyz.alloc(L * 24));
+  HIP_CHECK(dld.alloc(L * 32));
+  HIP_CHECK(dm.alloc(L * 4));
+  HIP_CHECK(dst.alloc(sizeof(StreamState)));
+  StreamState st{};
+  memcpy(st.Tcw, Tcw, 64);
+  st.has_last = 1;
+  HIP_CHECK(hipMemcpy(dst.p, &st, sizeof(st), hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(dn.p, &ncur, 4, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(dln.p, &nlast, 4, hipMemcpyHostToDevice));
+  if (ncur) {
+    HIP_CHECK(hipMemcpy(dku.p, cur_kl_un, ncur * sizeof(orbpl_keyline), hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dde.p, cur_desc, (size_t)ncur * 32, hipMemcpyHostToDevice));
+  }
+  if (nlast) {
+    HIP_CHECK(hipMemcpy(dlk.p, last_kl_un, nlast * sizeof(orbpl_keyline), hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dhm.p, has_ml, nlast, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dlo.p, last_outlier, nlast, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dxyz.p, ml_xyz6, (size_t)nlast * 24, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dld.p, last_desc, (size_t)nlast * 32, hipMemcpyHostToDevice));
+  }
+  LineTrackArgs a{};
+  a.nl = dn.as<int>();
+  a.kl_un = dku.as<orbpl_keyline>();
+  a.desc = dde.as<uint8_t>();
+  a.lmatch = dm.as<int>();
+  a.last_nl = dln.as<int>();
+  a.last_kl_un = dlk.as<orbpl_keyline>();
+  a.last_has_ml = dhm.as<uint8_t>();
+  a.last_loutlier = dlo.as<uint8_t>();
+  a.last_ml_xyz = dxyz.as<float>();
+  a.last_desc = dld.as<uint8_t>();
+  launch_line_match(c, a, dst.as<StreamState>(), 1, scratch_stream());
+  HIP_CHECK(hipGetLastError());
+  if (ncur) HIP_CHECK(hipMemcpy(match, dm.p, (size_t)ncur * 4, hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(&st, dst.p, sizeof(st), hipMemcpyDeviceToHost));
+  *nmatches = st.nlmatches;
+  return ORBPL_OK;
+}
+
 }  // extern "C"
 
 // ---------------------------------------------------------------------------

@@ -33,8 +33,24 @@ def image_for(name, w, h, seed):
     return synth.textured_image(w, h, seed=seed)
 
 
+LINE_CASES = [
+    # name, width, height, seed: LineExtractor::ExtractLineSegment (LSD + top-80 + LBD)
+    ("vga_s1", 640, 480, 1),
+    ("kitti_s4", 1241, 376, 4),
+]
+
+
 def main():
     O = load_oracle()
+    for name, w, h, seed in LINE_CASES:
+        img = image_for(name, w, h, seed)
+        lines = O.lsd_detect(img)
+        kl, desc, coef, nd = O.line_extract(img)
+        np.savez_compressed(
+            HERE / f"lines_{name}.npz", sha256=hashlib.sha256(img.tobytes()).hexdigest(),
+            width=w, height=h, seed=seed, lsd_lines=lines, keylines=kl.view(np.uint8),
+            desc=desc, coef=coef, n_detected=nd)
+        print("lines", name, len(lines), len(kl))
     for name, w, h, seed, pp in CASES:
         img = image_for(name, w, h, seed)
         p = O.params(*pp)

@@ -1,5 +1,7 @@
 """GPU parity of the LSD line detector (LineExtractor.cpp:20-21) against the
 CPU oracle (oracle/lsd_oracle.cpp): every stage bit-exact."""
+from pathlib import Path
+
 import numpy as np
 import pytest
 
@@ -130,3 +132,18 @@ def test_lsd_regions_longer_than_a_lane_buffer(orbpl, oracle):
         L = det.detect(img)
         assert np.array_equal(L, oracle.lsd_detect(img))
         assert det.debug_profile()["coop_regions"] > 0
+
+
+LINE_GOLDEN = sorted((Path(__file__).resolve().parent / "golden").glob("lines_*.npz"))
+
+
+@pytest.mark.parametrize("path", LINE_GOLDEN, ids=[p.stem for p in LINE_GOLDEN])
+def test_line_extract_matches_golden(orbpl, synth, path):
+    z = np.load(path)
+    w, h = int(z["width"]), int(z["height"])
+    img = synth.textured_image(w, h, seed=int(z["seed"]))
+    det = orbpl.LineExtractor(w, h)
+    assert np.array_equal(det.detect(img), z["lsd_lines"])
+    kl, desc, coef = det.ExtractLineSegment(img)
+    assert kl.view(np.uint8).tobytes() == z["keylines"].tobytes()
+    assert np.array_equal(desc, z["desc"]) and np.array_equal(coef, z["coef"])

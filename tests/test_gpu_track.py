@@ -217,3 +217,98 @@ def test_tracker_with_lines_matches_oracle_lvo(orbpl, oracle, pipelined):
         assert (lm_g >= 0).sum() >= ls["line_nmatches_map"][s]
     lt = tr.line_timings()
     assert lt.shape[1] == 3 and np.all(lt >= 0)
+
+
+@pytest.mark.parametrize("cam_name", ["TUM1", "TUM3"])
+def test_line_frame_prepare_bit_exact(orbpl, oracle, cam_name):
+    cfg, _, fr = sequence(1, 41, cam_name=cam_name)
+    g, d = fr[0]
+    kl, _, _, _ = oracle.line_extract(g)
+    got = orbpl.line_frame_prepare(orbpl.make_camera(cfg), kl, d)
+    exp = oracle.line_frame_prepare(oracle.camera(cfg), kl, d)
+    assert got[0].tobytes() == exp[0].tobytes()
+    for a, b in zip(got[1:], exp[1:]):
+        assert np.array_equal(a, b)
+    got = orbpl.line_frame_prepare(orbpl.make_camera(cfg), kl, None)
+    assert np.all(got[1] == -1) and np.all(got[4] == -1)
+
+
+def _map_lines(cfg, ku, ds, de, Tcw):
+    """Map lines of a frame as the tracker builds them (start depth for both
+    end points, Frame.cc:1192), world coordinates in float."""
+    has = ((ds > 0) & (de > 0)).astype(np.uint8)
+    Twc = np.linalg.inv(Tcw.astype(np.float64))
+    xyz = np.zeros((len(ku), 6), np.float32)
+    for j in range(len(ku)):
+        z = float(ds[j])
+        for e, (u, v) in enumerate(((ku["startPointX"][j], ku["startPointY"][j]),
+                                    (ku["endPointX"][j], ku["endPointY"][j]))):
+            P = np.array([(u - cfg["cx"]) * z / cfg["fx"], (v - cfg["cy"]) * z / cfg["fy"], z, 1.0])
+            xyz[j, 3 * e:3 * e + 3] = (Twc @ P)[:3]
+    return has, xyz
+
+
+@pytest.mark.parametrize("case", ["next_frame", "perturbed", "outliers"])
+def test_line_search_by_projection_last_bit_exact(orbpl, oracle, case):
+    cfg, traj, fr = sequence(2, 42, cam_name="TUM1")
+    cam_o, cam_g = oracle.camera(cfg), orbpl.make_camera(cfg)
+    frames = []
+    for g, d in fr:
+        kl, desc, _, _ = oracle.line_extract(g)
+        ku, ds, de, _, _ = oracle.line_frame_prepare(cam_o, kl, d)
+        frames.append((ku, desc, ds, de))
+    T0 = np.linalg.inv(traj[0]).astype(np.float32)
+    T1 = np.linalg.inv(traj[1]).astype(np.float32)
+    if case == "perturbed":
+        T1 = T1.copy()
+        T1[:3, 3] += np.float32([0.01, -0.005, 0.01])
+    has, xyz = _map_lines(cfg, frames[0][0], frames[0][2], frames[0][3], T0)
+    out = np.zeros(len(has), np.uint8)
+    if case == "outliers":
+        out[::3] = 1
+    args = (T1, frames[1][0], frames[1][1], frames[0][0], has, out, xyz, frames[0][1])
+    m_g, n_g = orbpl.LineMatcher.SearchByProjectionLastFrame(cam_g, *args)
+    m_o, n_o = oracle.line_search_by_projection_last(cam_o, *args)
+    assert n_g == n_o and n_o > 10
+    assert np.array_equal(m_g, m_o)
+
+
+def _unproject_p6(cfg, ku, dep, T):
+    """Frame::UnprojectStereo as the tracker computes it (float pixel terms,
+    double-accumulated Rwc x + Ow, P6)."""
+    invfx = np.float32(1.0) / np.float32(cfg["fx"])
+    invfy = np.float32(1.0) / np.float32(cfg["fy"])
+    cx, cy = np.float32(cfg["cx"]), np.float32(cfg["cy"])
+    z = dep.astype(np.float32)
+    x3 = np.stack([(ku["x"] - cx) * z * invfx, (ku["y"] - cy) * z * invfy, z], 1).astype(np.float32)
+    Td = T.astype(np.float64)
+    Ow = [np.float32(-(Td[0, r] * Td[0, 3] + Td[1, r] * Td[1, 3] + Td[2, r] * Td[2, 3]))
+          for r in range(3)]
+    out = np.zeros_like(x3)
+    for r in range(3):
+        s = Td[0, r] * x3[:, 0].astype(np.float64) + Td[1, r] * x3[:, 1].astype(np.float64)
+        s = s + Td[2, r] * x3[:, 2].astype(np.float64)
+        out[:, r] = (s + np.float64(Ow[r])).astype(np.float32)
+    return out
+
+
+@pytest.mark.parametrize("seed", [5, 6, 7, 8])
+def test_search_by_projection_tie_order(orbpl, oracle, seed):
+    """Equal-distance candidates displaced by a better later one keep their
+    grid-scan order (regression: TUM3 seed 5, last point 911 -> 996)."""
+    cfg, traj, fr = sequence(2, seed, cam_name="TUM3")
+    cam_o = oracle.camera(cfg)
+    f0 = frame_data(oracle, cam_o, cfg, *fr[0])
+    f1 = frame_data(oracle, cam_o, cfg, *fr[1])
+    T0 = np.linalg.inv(traj[0]).astype(np.float32)
+    has = (f0["depth"] > 0).astype(np.uint8)
+    xyz = _unproject_p6(cfg, f0["kps_un"], np.where(f0["depth"] > 0, f0["depth"], 0), T0)
+    last = dict(Tcw=T0, kps_un=f0["kps_un"], has_mp=has, outlier=np.zeros(len(has), np.uint8),
+                mp_xyz=xyz, mp_desc=f0["desc"], mp_nobs=np.ones(len(has), np.int32))
+    cur = dict(Tcw=T0, kps_un=f1["kps_un"], desc=f1["desc"], uright=f1["uright"])
+    sc = oracle.level_sizes(oracle.params(), 640, 480)[3]
+    for ori in (True, False):
+        m_o, n_o = oracle.search_by_projection_last(cam_o, sc, cur, last, 15.0, False, ori)
+        m_g, n_g = orbpl.ORBmatcher(0.9, ori).SearchByProjectionLastFrame(
+            orbpl.make_camera(cfg), sc, cur, last, 15.0, False)
+        assert n_g == n_o and np.array_equal(m_g, m_o), (ori, np.nonzero(m_g != m_o)[0][:5])

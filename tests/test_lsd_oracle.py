@@ -1,6 +1,8 @@
 """CPU tests of the line-feature oracle (oracle/lsd_oracle.cpp) and of the
 pinned math it shares with the kernels (csrc/lsd_math.h)."""
+import hashlib
 import math
+from pathlib import Path
 
 import numpy as np
 import pytest
@@ -81,3 +83,18 @@ def test_line_extract_keeps_80_longest(oracle):
     c = np.cross(s, e)
     assert np.allclose(coef, c / np.linalg.norm(c, axis=1, keepdims=True))
     assert np.all(kl["octave"] == 0) and len(set(kl["class_id"])) == 80
+
+
+LINE_GOLDEN = sorted((Path(__file__).resolve().parent / "golden").glob("lines_*.npz"))
+
+
+@pytest.mark.parametrize("path", LINE_GOLDEN, ids=[p.stem for p in LINE_GOLDEN])
+def test_line_oracle_matches_golden(path, oracle, synth):
+    z = np.load(path)
+    img = synth.textured_image(int(z["width"]), int(z["height"]), seed=int(z["seed"]))
+    assert hashlib.sha256(img.tobytes()).hexdigest() == str(z["sha256"])
+    assert np.array_equal(oracle.lsd_detect(img), z["lsd_lines"])
+    kl, desc, coef, nd = oracle.line_extract(img)
+    assert kl.view(np.uint8).tobytes() == z["keylines"].tobytes()
+    assert np.array_equal(desc, z["desc"]) and np.array_equal(coef, z["coef"])
+    assert nd == int(z["n_detected"])
