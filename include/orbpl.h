@@ -199,6 +199,38 @@ int orbm_search_by_projection_last(const orbpl_camera* cam, const float* scale_f
                                    int check_orientation, int32_t* match, int* nmatches);
 
 /* ------------------------------------------------------------------------
+ * Tracking::SearchLocalPoints pieces (TrackLocalMap)
+ * ---------------------------------------------------------------------- */
+/* Frame::IsInFrustum(MapPoint*, view_cos_limit) (Frame.cc:345-401) for n map
+ * points (world xyz, normal, GetMin/MaxDistanceInvariance) with
+ * MapPoint::PredictScale (MapPoint.cc:416-431); outputs the mTrack* fields:
+ * in_view (mbTrackInView), proj_x/y, proj_xr (u - bf/z), level
+ * (mnTrackScaleLevel, -1 when not in view), view_cos (mTrackViewCos).
+ * scale_factor = ORBextractor scale factor (mfLogScaleFactor = logf of it). */
+int orbpl_frame_is_in_frustum(const orbpl_camera* cam, float scale_factor, int nlevels,
+                              const float* Tcw, int n, const float* xyz, const float* normal,
+                              const float* min_dist, const float* max_dist, float view_cos_limit,
+                              uint8_t* in_view, float* proj_x, float* proj_y, float* proj_xr,
+                              int32_t* level, float* view_cos);
+/* ORBmatcher(nnratio).SearchByProjection(F, vpLocalMapPoints, th)
+ * (ORBmatcher.cc:72-183): radius RadiusByViewingCos(view_cos) (x th when
+ * th != 1) x scale[level], levels [level-1, level], best and second by
+ * Hamming, TH_HIGH 100, ratio test only when both are on the same level.
+ * cur_nobs[i] = Observations() of the map point already at keypoint i (0 or
+ * NULL: none); keypoints holding one with Observations() > 0 are skipped, as
+ * are keypoints claimed during the call. match[i] = index of the last local
+ * map point assigned to keypoint i in this call (the reference overwrites
+ * F.mvpMapPoints[i]), -1 = unchanged. *nmatches = return value. */
+int orbm_search_by_projection_local(const orbpl_camera* cam, const float* scale_factors,
+                                    int nlevels, const orbpl_match_current* cur, int nmp,
+                                    const uint8_t* in_view, const float* proj_x,
+                                    const float* proj_y, const float* proj_xr,
+                                    const int32_t* level, const float* view_cos,
+                                    const uint8_t* mp_desc, const int32_t* mp_nobs,
+                                    const int32_t* cur_nobs, float th, float nnratio,
+                                    int32_t* match, int* nmatches);
+
+/* ------------------------------------------------------------------------
  * Optimizer::PoseOptimization / PoseOptimizationWithLines
  * (Optimizer.cc:375-619, 2132-2486): 4 rounds x 10 Levenberg-Marquardt
  * iterations on one SE3 vertex, Huber kernel in rounds 0-2, chi2 outlier

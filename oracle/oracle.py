@@ -163,6 +163,10 @@ def _setup_track(L):
     L.oracle_frame_prepare.argtypes = [vp, vp, i, vp, vp, vp, vp, vp, vp]
     L.oracle_search_by_projection_last.argtypes = [vp, vp, i, vp, vp, C.c_float, i, i, vp, ip]
     L.oracle_pose_optimization.argtypes = [vp, vp, vp, vp, vp, ip]
+    L.oracle_frame_is_in_frustum.argtypes = [vp, C.c_float, i, vp, i, vp, vp, vp, vp, C.c_float,
+                                             vp, vp, vp, vp, vp, vp]
+    L.oracle_search_by_projection_local.argtypes = [vp, vp, i, vp, i, vp, vp, vp, vp, vp, vp, vp,
+                                                    vp, vp, C.c_float, C.c_float, vp, ip]
     L.oracle_vo_create.argtypes = [vp, vp, i]
     L.oracle_vo_create.restype = vp
     L.oracle_vo_destroy.argtypes = [vp]
@@ -213,6 +217,46 @@ def search_by_projection_last(cam, scale_factors, cur, last, th, mono=False, che
                                            float(th), int(mono), int(check_ori), _p(match),
                                            C.byref(nm))
     return match[:mc.n].copy(), nm.value
+
+
+def frame_is_in_frustum(cam, log_scale_factor, nlevels, Tcw, mps, view_cos_limit=0.5):
+    n = len(mps["xyz"])
+    keep = [_c(Tcw, np.float32), _c(mps["xyz"], np.float32), _c(mps["normal"], np.float32),
+            _c(mps["min_dist"], np.float32), _c(mps["max_dist"], np.float32)]
+    out = dict(in_view=np.zeros(n, np.uint8), proj_x=np.zeros(n, np.float32),
+               proj_y=np.zeros(n, np.float32), proj_xr=np.zeros(n, np.float32),
+               level=np.zeros(n, np.int32), view_cos=np.zeros(n, np.float32))
+    lib().oracle_frame_is_in_frustum(
+        C.byref(cam), C.c_float(log_scale_factor), int(nlevels), _p(keep[0]), n, _p(keep[1]),
+        _p(keep[2]), _p(keep[3]), _p(keep[4]), C.c_float(view_cos_limit), _p(out["in_view"]),
+        _p(out["proj_x"]), _p(out["proj_y"]), _p(out["proj_xr"]), _p(out["level"]),
+        _p(out["view_cos"]))
+    return out
+
+
+def search_by_projection_local(cam, scale_factors, cur, track, mp_desc, mp_nobs, cur_nobs, th,
+                               nnratio):
+    keep = []
+
+    def arr(a, dt):
+        a = _c(a, dt)
+        keep.append(a)
+        return _p(a)
+
+    sf = _c(scale_factors, np.float32)
+    n = len(cur["kps_un"])
+    mc = MatchCurrent(n, arr(np.eye(4), np.float32), arr(cur["kps_un"], KP_DTYPE),
+                      arr(cur["desc"], np.uint8), arr(cur["uright"], np.float32))
+    match = np.zeros(max(1, n), np.int32)
+    nm = C.c_int(0)
+    lib().oracle_search_by_projection_local(
+        C.byref(cam), _p(sf), len(sf), C.byref(mc), len(track["in_view"]),
+        arr(track["in_view"], np.uint8), arr(track["proj_x"], np.float32),
+        arr(track["proj_y"], np.float32), arr(track["proj_xr"], np.float32),
+        arr(track["level"], np.int32), arr(track["view_cos"], np.float32), arr(mp_desc, np.uint8),
+        arr(mp_nobs, np.int32), None if cur_nobs is None else arr(cur_nobs, np.int32),
+        C.c_float(th), C.c_float(nnratio), _p(match), C.byref(nm))
+    return match[:n].copy(), nm.value
 
 
 def pose_optimization(cam, prob, Tcw, outlier, line_outlier=None):

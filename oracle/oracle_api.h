@@ -22,6 +22,19 @@ int oracle_search_by_projection_last(const orbpl_camera* cam, const float* scale
                                      int nlevels, const orbpl_match_current* cur,
                                      const orbpl_match_last* last, float th, int mono,
                                      int check_ori, int32_t* match, int* nmatches_out);
+int oracle_frame_is_in_frustum(const orbpl_camera* cam, float log_scale_factor, int nlevels,
+                               const float* Tcw, int n, const float* xyz, const float* normal,
+                               const float* min_dist, const float* max_dist, float view_cos_limit,
+                               uint8_t* in_view, float* proj_x, float* proj_y, float* proj_xr,
+                               int32_t* level, float* view_cos);
+int oracle_search_by_projection_local(const orbpl_camera* cam, const float* scale_factors,
+                                      int nlevels, const orbpl_match_current* cur, int nmp,
+                                      const uint8_t* in_view, const float* proj_x,
+                                      const float* proj_y, const float* proj_xr,
+                                      const int32_t* level, const float* view_cos,
+                                      const uint8_t* mp_desc, const int32_t* mp_nobs,
+                                      const int32_t* cur_nobs, float th, float nnratio,
+                                      int32_t* match, int* nmatches_out);
 int oracle_pose_optimization(const orbpl_camera* cam, const orbpl_pose_problem* P, float* Tcw,
                              uint8_t* outlier, uint8_t* line_outlier, int* n_inliers);
 void* oracle_vo_create(const orbpl_orb_params* orb, const orbpl_camera* cam, int n_streams);

@@ -31,6 +31,7 @@
 #include <limits>
 #include <vector>
 
+#include "../orb_slam2_modification_with-point-and-line-feature_amd/csrc/lsd_math.h"
 #include "oracle_api.h"
 
 namespace oracle_track {
@@ -928,6 +929,148 @@ int oracle_vo_step(void* h, int stream, const uint8_t* gray, const float* depth,
   if (out5) {
     out5[0] = n; out5[1] = nmatches; out5[2] = ninl; out5[3] = nmap; out5[4] = ok;
   }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Tracking::SearchLocalPoints pieces: Frame::IsInFrustum(MapPoint*, 0.5)
+// (Frame.cc:345-401) with MapPoint::PredictScale (MapPoint.cc:416-431), and
+// ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th)
+// (ORBmatcher.cc:72-183) with RadiusByViewingCos (:186-193).
+// Pinned: P15 logf = (float)log((double)x) (fdlibm, P10);
+// P16 cv::norm of a float 3-vector = sqrt of double squares, one rounding;
+// Mat::dot of float 3-vectors = float products summed in double (OpenCV's
+// scalar tail for len < 4).
+// ---------------------------------------------------------------------------
+int oracle_frame_is_in_frustum(const orbpl_camera* cam, float log_scale_factor, int nlevels,
+                               const float* Tcw, int n, const float* xyz, const float* normal,
+                               const float* min_dist, const float* max_dist, float view_cos_limit,
+                               uint8_t* in_view, float* proj_x, float* proj_y, float* proj_xr,
+                               int32_t* level, float* view_cos) {
+  float b[4];
+  image_bounds(*cam, b);
+  float Ow[3];
+  for (int r = 0; r < 3; r++) {
+    double s = (double)Tcw[0 * 4 + r] * Tcw[3];
+    s += (double)Tcw[1 * 4 + r] * Tcw[7];
+    s += (double)Tcw[2 * 4 + r] * Tcw[11];
+    Ow[r] = (float)(s * -1.0);
+  }
+  for (int i = 0; i < n; i++) {
+    in_view[i] = 0;
+    proj_x[i] = proj_y[i] = proj_xr[i] = view_cos[i] = 0.f;
+    level[i] = -1;
+    float Pc[3];
+    gemm33(Tcw, xyz + 3 * i, Pc);
+    if (Pc[2] < 0.0f) continue;
+    const float invz = 1.0f / Pc[2];
+    const float u = cam->fx * Pc[0] * invz + cam->cx;
+    const float v = cam->fy * Pc[1] * invz + cam->cy;
+    if (u < b[0] || u > b[1]) continue;
+    if (v < b[2] || v > b[3]) continue;
+    const float PO[3] = {xyz[3 * i] - Ow[0], xyz[3 * i + 1] - Ow[1], xyz[3 * i + 2] - Ow[2]};
+    const float dist = (float)std::sqrt((double)PO[0] * PO[0] + (double)PO[1] * PO[1] +
+                                        (double)PO[2] * PO[2]);
+    if (dist < min_dist[i] || dist > max_dist[i]) continue;
+    const float* Pn = normal + 3 * i;
+    double dot = 0;
+    for (int k = 0; k < 3; k++) dot += (double)(float)(PO[k] * Pn[k]);
+    const float vc = (float)(dot / (double)dist);
+    if (vc < view_cos_limit) continue;
+    const float ratio = max_dist[i] / dist;
+    int ns = (int)std::ceil((float)lsdm::log_((double)ratio) / log_scale_factor);
+    if (ns < 0) ns = 0;
+    else if (ns >= nlevels) ns = nlevels - 1;
+    in_view[i] = 1;
+    proj_x[i] = u;
+    proj_xr[i] = u - cam->bf * invz;
+    proj_y[i] = v;
+    level[i] = ns;
+    view_cos[i] = vc;
+  }
+  return 0;
+}
+
+int oracle_search_by_projection_local(const orbpl_camera* cam, const float* scale_factors,
+                                      int nlevels, const orbpl_match_current* cur, int nmp,
+                                      const uint8_t* in_view, const float* proj_x,
+                                      const float* proj_y, const float* proj_xr,
+                                      const int32_t* level, const float* view_cos,
+                                      const uint8_t* mp_desc, const int32_t* mp_nobs,
+                                      const int32_t* cur_nobs, float th, float nnratio,
+                                      int32_t* match, int* nmatches_out) {
+  (void)nlevels;
+  const int TH_HIGH = 100;
+  Grid g;
+  grid_constants(*cam, g);
+  for (int i = 0; i < cur->n; i++) {
+    int px, py;
+    if (pos_in_grid(g, cur->kps_un[i].x, cur->kps_un[i].y, &px, &py)) g.cells[px][py].push_back(i);
+  }
+  // Observations() of the map point currently in F.mvpMapPoints[idx]
+  std::vector<int> obs(cur->n);
+  for (int i = 0; i < cur->n; i++) {
+    obs[i] = cur_nobs ? cur_nobs[i] : 0;
+    match[i] = -1;
+  }
+  const bool bFactor = th != 1.0;
+  int nmatches = 0;
+  for (int i = 0; i < nmp; i++) {
+    if (!in_view[i]) continue;
+    const int nPredictedLevel = level[i];
+    float r = (view_cos[i] > 0.998) ? 2.5f : 4.0f;
+    if (bFactor) r *= th;
+    const float rad = r * scale_factors[nPredictedLevel];
+    const float x = proj_x[i], y = proj_y[i];
+    const int minLevel = nPredictedLevel - 1, maxLevel = nPredictedLevel;
+    std::vector<int> vIdx;
+    const int nMinCellX = std::max(0, (int)std::floor((x - g.minX - rad) * g.invW));
+    const int nMaxCellX = std::min((int)ORBPL_GRID_COLS - 1, (int)std::ceil((x - g.minX + rad) * g.invW));
+    const int nMinCellY = std::max(0, (int)std::floor((y - g.minY - rad) * g.invH));
+    const int nMaxCellY = std::min((int)ORBPL_GRID_ROWS - 1, (int)std::ceil((y - g.minY + rad) * g.invH));
+    if (!(nMinCellX >= ORBPL_GRID_COLS || nMaxCellX < 0 || nMinCellY >= ORBPL_GRID_ROWS || nMaxCellY < 0)) {
+      const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+      for (int ix = nMinCellX; ix <= nMaxCellX; ix++)
+        for (int iy = nMinCellY; iy <= nMaxCellY; iy++)
+          for (int j : g.cells[ix][iy]) {
+            const orbpl_keypoint& k = cur->kps_un[j];
+            if (bCheckLevels) {
+              if (k.octave < minLevel) continue;
+              if (maxLevel >= 0 && k.octave > maxLevel) continue;
+            }
+            const float distx = k.x - x, disty = k.y - y;
+            if (std::fabs(distx) < rad && std::fabs(disty) < rad) vIdx.push_back(j);
+          }
+    }
+    if (vIdx.empty()) continue;
+    const uint8_t* dMP = mp_desc + 32 * i;
+    int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+    for (int idx : vIdx) {
+      if (obs[idx] > 0) continue;
+      if (cur->uright[idx] > 0) {
+        const float er = std::fabs(proj_xr[i] - cur->uright[idx]);
+        if (er > r * scale_factors[nPredictedLevel]) continue;
+      }
+      const int dist = desc_dist(dMP, cur->desc + 32 * idx);
+      if (dist < bestDist) {
+        bestDist2 = bestDist;
+        bestDist = dist;
+        bestLevel2 = bestLevel;
+        bestLevel = cur->kps_un[idx].octave;
+        bestIdx = idx;
+      } else if (dist < bestDist2) {
+        bestLevel2 = cur->kps_un[idx].octave;
+        bestDist2 = dist;
+      }
+    }
+    if (bestDist <= TH_HIGH) {
+      if (bestLevel == bestLevel2 && bestDist > nnratio * bestDist2) continue;
+      match[bestIdx] = i;
+      obs[bestIdx] = mp_nobs[i];
+      nmatches++;
+    }
+  }
+  *nmatches_out = nmatches;
   return 0;
 }
 

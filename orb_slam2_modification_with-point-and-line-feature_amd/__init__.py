@@ -341,6 +341,10 @@ def _declare_track(L):
     L.orbpl_tracker_get_frame.argtypes = [vp, i, vp, vp, vp, vp, ip]
     L.orbpl_tracker_create_ex.argtypes = [vp, vp, i, i, i, C.POINTER(vp)]
     L.orbpl_line_frame_prepare.argtypes = [vp, vp, i, vp, vp, vp, vp, vp, vp]
+    L.orbpl_frame_is_in_frustum.argtypes = [vp, C.c_float, i, vp, i, vp, vp, vp, vp, C.c_float,
+                                            vp, vp, vp, vp, vp, vp]
+    L.orbm_search_by_projection_local.argtypes = [vp, vp, i, vp, i, vp, vp, vp, vp, vp, vp, vp, vp,
+                                                  vp, C.c_float, C.c_float, vp, ip]
     L.orbl_search_by_projection_last.argtypes = [vp, vp, i, vp, vp, i, vp, vp, vp, vp, vp, vp, ip]
     L.orbpl_tracker_get_status.argtypes = [vp, vp, vp, vp, vp]
     L.orbpl_tracker_get_lines.argtypes = [vp, i, vp, vp, vp, vp, ip]
@@ -408,6 +412,50 @@ class ORBmatcher:
                                                    int(bMono), int(self.checkOri), _ptr(match),
                                                    C.byref(nm)), "orbm_search_by_projection_last")
         return match[:mc.n].copy(), nm.value
+
+    def SearchByProjectionLocalMap(self, camera, scale_factors, cur, track, mp_desc, mp_nobs,
+                                   cur_nobs, th):
+        """SearchByProjection(F, vpLocalMapPoints, th) (ORBmatcher.cc:72-183);
+        ``track`` = frame_is_in_frustum output. Returns (match, nmatches)."""
+        sf = _c(scale_factors, np.float32)
+        keep = []
+
+        def arr(a, dt):
+            a = _c(a, dt)
+            keep.append(a)
+            return _ptr(a)
+
+        n = len(cur["kps_un"])
+        mc = MatchCurrent(n, arr(np.eye(4), np.float32), arr(cur["kps_un"], KP_DTYPE),
+                          arr(cur["desc"], np.uint8), arr(cur["uright"], np.float32))
+        nmp = len(track["in_view"])
+        match = np.zeros(max(1, n), np.int32)
+        nm = C.c_int(0)
+        check(lib().orbm_search_by_projection_local(
+            C.byref(camera), _ptr(sf), len(sf), C.byref(mc), nmp, arr(track["in_view"], np.uint8),
+            arr(track["proj_x"], np.float32), arr(track["proj_y"], np.float32),
+            arr(track["proj_xr"], np.float32), arr(track["level"], np.int32),
+            arr(track["view_cos"], np.float32), arr(mp_desc, np.uint8), arr(mp_nobs, np.int32),
+            None if cur_nobs is None else arr(cur_nobs, np.int32), float(th), float(self.nnratio),
+            _ptr(match), C.byref(nm)), "orbm_search_by_projection_local")
+        return match[:n].copy(), nm.value
+
+
+def frame_is_in_frustum(camera, scale_factor, nlevels, Tcw, mps, view_cos_limit=0.5):
+    """Frame::IsInFrustum(MapPoint*, limit) for the map points in ``mps`` (dict:
+    xyz, normal, min_dist, max_dist). Returns the mTrack* fields as a dict."""
+    n = len(mps["xyz"])
+    keep = [_c(Tcw, np.float32), _c(mps["xyz"], np.float32), _c(mps["normal"], np.float32),
+            _c(mps["min_dist"], np.float32), _c(mps["max_dist"], np.float32)]
+    out = dict(in_view=np.zeros(n, np.uint8), proj_x=np.zeros(n, np.float32),
+               proj_y=np.zeros(n, np.float32), proj_xr=np.zeros(n, np.float32),
+               level=np.zeros(n, np.int32), view_cos=np.zeros(n, np.float32))
+    check(lib().orbpl_frame_is_in_frustum(
+        C.byref(camera), float(scale_factor), int(nlevels), _ptr(keep[0]), n, _ptr(keep[1]),
+        _ptr(keep[2]), _ptr(keep[3]), _ptr(keep[4]), float(view_cos_limit), _ptr(out["in_view"]),
+        _ptr(out["proj_x"]), _ptr(out["proj_y"]), _ptr(out["proj_xr"]), _ptr(out["level"]),
+        _ptr(out["view_cos"])), "orbpl_frame_is_in_frustum")
+    return out
 
 
 def pose_optimization(camera, prob, Tcw, outlier, line_outlier=None):

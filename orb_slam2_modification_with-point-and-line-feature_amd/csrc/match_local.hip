@@ -1,0 +1,307 @@
+// Tracking::SearchLocalPoints on gfx950 (restated in oracle/track_oracle.cpp):
+//   k_in_frustum   : Frame::IsInFrustum(MapPoint*, viewCosLimit) (Frame.cc:345-401)
+//                    + MapPoint::PredictScale (MapPoint.cc:416-431), thread per point
+//   k_match_local  : ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&,
+//                    th) (ORBmatcher.cc:72-183), one workgroup per frame:
+//     grid build    - AssignFeaturesToGrid in LDS (cells hold increasing indices)
+//     phase A       - every map point in parallel: best and second candidate
+//                     (the reference's running top-2 in grid-scan order) with
+//                     the keypoints already holding a map point with
+//                     Observations() > 0 skipped
+//     phase B       - wave 0, map points in order: a point's outcome can only
+//                     change if its best or second candidate is claimed by an
+//                     earlier accepted point (removing any other candidate
+//                     leaves the running top-2 unchanged), so chunks of 64 are
+//                     decided at once up to the first such collision, which is
+//                     re-scanned against the claims; the last writer of a
+//                     keypoint wins, as F.mvpMapPoints[bestIdx] = pMP does
+#include <hip/hip_runtime.h>
+
+#include "lsd_math.h"
+#include "track_common.h"
+#include "track_kernels.h"
+
+namespace orbpl {
+
+__global__ void __launch_bounds__(256) k_in_frustum(TrackConsts c, float log_scale, InFrustumArgs a) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  a.in_view[i] = 0;
+  a.proj_x[i] = 0.f;
+  a.proj_y[i] = 0.f;
+  a.proj_xr[i] = 0.f;
+  a.view_cos[i] = 0.f;
+  a.level[i] = -1;
+  const float* T = a.Tcw;
+  const float P[3] = {a.xyz[3 * i], a.xyz[3 * i + 1], a.xyz[3 * i + 2]};
+  float Pc[3];
+  gemm_R_x_plus_t(T, P, Pc);
+  if (Pc[2] < 0.0f) return;
+  const float invz = 1.0f / Pc[2];
+  const float u = c.fx * Pc[0] * invz + c.cx;
+  const float v = c.fy * Pc[1] * invz + c.cy;
+  if (u < c.minX || u > c.maxX) return;
+  if (v < c.minY || v > c.maxY) return;
+  float Ow[3];
+  gemm_neg_Rt_t(T, Ow);
+  const float PO[3] = {P[0] - Ow[0], P[1] - Ow[1], P[2] - Ow[2]};
+  // cv::norm (P16): double squares, one rounding
+  const float dist =
+      (float)sqrt((double)PO[0] * PO[0] + (double)PO[1] * PO[1] + (double)PO[2] * PO[2]);
+  if (dist < a.min_dist[i] || dist > a.max_dist[i]) return;
+  // Mat::dot (P16): float products, double sum
+  double dot = 0;
+#pragma unroll
+  for (int k = 0; k < 3; k++) dot += (double)(float)(PO[k] * a.normal[3 * i + k]);
+  const float vc = (float)(dot / (double)dist);
+  if (vc < a.view_cos_limit) return;
+  const float ratio = a.max_dist[i] / dist;
+  int ns = (int)ceilf((float)lsdm::log_((double)ratio) / log_scale);  // P15
+  if (ns < 0) ns = 0;
+  else if (ns >= c.nlevels) ns = c.nlevels - 1;
+  a.in_view[i] = 1;
+  a.proj_x[i] = u;
+  a.proj_xr[i] = u - c.bf * invz;
+  a.proj_y[i] = v;
+  a.level[i] = ns;
+  a.view_cos[i] = vc;
+}
+
+namespace {
+
+constexpr int kLocalKp = 2048;
+
+struct LocalShared {
+  int cell_start[kGridCols * kGridRows + 1];
+  int fill[kGridCols * kGridRows];
+  uint16_t items[kLocalKp];
+  float2 xy[kLocalKp];
+  float ur[kLocalKp];
+  int8_t oct[kLocalKp];
+  int16_t gc[kLocalKp];
+  int mw[kLocalKp];                 // last writer (map point index) per keypoint
+  uint32_t claimed[kLocalKp / 32];  // holds a map point with Observations() > 0
+  int wsum[8];
+};
+
+struct Top2 {
+  int bd, bi, bl;   // best distance, index, level
+  int sd, si, sl;   // second distance, index of the candidate that set it, level
+};
+
+__device__ __forceinline__ int hamming32l(const uint8_t* a, const uint8_t* b) {
+  const uint4 a0 = *reinterpret_cast<const uint4*>(a);
+  const uint4 a1 = *reinterpret_cast<const uint4*>(a + 16);
+  const uint4 b0 = *reinterpret_cast<const uint4*>(b);
+  const uint4 b1 = *reinterpret_cast<const uint4*>(b + 16);
+  return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+         __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
+// GetFeaturesInArea(x, y, r*scale, level-1, level) + the best / second loop
+// (ORBmatcher.cc:96-160) against the current claims.
+__device__ Top2 local_scan(const LocalShared& S, const TrackConsts& c, const LocalArgs& a,
+                           const uint8_t* cdesc, int i) {
+  Top2 t{256, -1, -1, 256, -1, -1};
+  const int lev = a.level[i];
+  float r = (a.view_cos[i] > 0.998) ? 2.5f : 4.0f;
+  if (a.th != 1.0) r *= a.th;
+  const float rad = r * c.scale[lev];
+  const float x = a.proj_x[i], y = a.proj_y[i], xr = a.proj_xr[i];
+  const int minLevel = lev - 1, maxLevel = lev;
+  const int cx0 = max(0, (int)floorf((x - c.minX - rad) * c.gridInvW));
+  const int cx1 = min(kGridCols - 1, (int)ceilf((x - c.minX + rad) * c.gridInvW));
+  const int cy0 = max(0, (int)floorf((y - c.minY - rad) * c.gridInvH));
+  const int cy1 = min(kGridRows - 1, (int)ceilf((y - c.minY + rad) * c.gridInvH));
+  if (cx0 >= kGridCols || cx1 < 0 || cy0 >= kGridRows || cy1 < 0) return t;
+  const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+  const uint8_t* dMP = a.mp_desc + (long long)i * 32;
+  for (int ix = cx0; ix <= cx1; ix++)
+    for (int iy = cy0; iy <= cy1; iy++) {
+      const int cell = ix + kGridCols * iy;
+      const int b = S.cell_start[cell], e = S.cell_start[cell + 1];
+      for (int q = b; q < e; q++) {
+        const int j = S.items[q];
+        const int oc = S.oct[j];
+        if (bCheckLevels) {
+          if (oc < minLevel) continue;
+          if (maxLevel >= 0 && oc > maxLevel) continue;
+        }
+        const float2 p = S.xy[j];
+        if (!(fabsf(p.x - x) < rad && fabsf(p.y - y) < rad)) continue;
+        if ((S.claimed[j >> 5] >> (j & 31)) & 1u) continue;
+        const float urj = S.ur[j];
+        if (urj > 0 && fabsf(xr - urj) > r * c.scale[lev]) continue;
+        const int dist = hamming32l(dMP, cdesc + (long long)j * 32);
+        if (dist < t.bd) {
+          t.sd = t.bd;
+          t.si = t.bi;
+          t.sl = t.bl;
+          t.bd = dist;
+          t.bi = j;
+          t.bl = oc;
+        } else if (dist < t.sd) {
+          t.sd = dist;
+          t.si = j;
+          t.sl = oc;
+        }
+      }
+    }
+  return t;
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(256) k_match_local(TrackConsts c, LocalArgs a) {
+  extern __shared__ char smem_local[];
+  LocalShared& S = *reinterpret_cast<LocalShared*>(smem_local);
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  const int n = min(a.n, kLocalKp);
+  const uint8_t* cdesc = a.desc;
+  // ---- grid (AssignFeaturesToGrid with PosInGrid, Frame.cc:265-287, 527-538) ----
+  for (int i = t; i < kGridCols * kGridRows; i += 256) S.cell_start[i] = 0;
+  for (int i = t; i < kLocalKp / 32; i += 256) S.claimed[i] = 0;
+  __syncthreads();
+  for (int i = t; i < n; i += 256) {
+    const KeyPointD k = a.kps_un[i];
+    S.xy[i] = make_float2(k.x, k.y);
+    S.oct[i] = (int8_t)k.octave;
+    S.ur[i] = a.uright[i];
+    S.mw[i] = -1;
+    const int px = (int)roundf((k.x - c.minX) * c.gridInvW);
+    const int py = (int)roundf((k.y - c.minY) * c.gridInvH);
+    const int g = (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) ? -1 : px + kGridCols * py;
+    S.gc[i] = (int16_t)g;
+    if (g >= 0) atomicAdd(&S.cell_start[g], 1);
+    if (a.cur_nobs && a.cur_nobs[i] > 0) atomicOr(&S.claimed[i >> 5], 1u << (i & 31));
+  }
+  __syncthreads();
+  {
+    constexpr int kPer = (kGridCols * kGridRows) / 256;
+    int loc[kPer];
+    int sum = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+      loc[k] = S.cell_start[t * kPer + k];
+      sum += loc[k];
+    }
+    int incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += u;
+    }
+    if (lane == 63) S.wsum[wave] = incl;
+    __syncthreads();
+    int base = 0;
+    for (int w = 0; w < wave; w++) base += S.wsum[w];
+    int run = base + incl - sum;
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+      S.cell_start[t * kPer + k] = run;
+      S.fill[t * kPer + k] = run;
+      run += loc[k];
+    }
+    if (t == 255) S.cell_start[kGridCols * kGridRows] = run;
+    __syncthreads();
+  }
+  for (int i = t; i < n; i += 256) {
+    const int g = S.gc[i];
+    if (g >= 0) S.items[atomicAdd(&S.fill[g], 1)] = (uint16_t)i;
+  }
+  __syncthreads();
+  for (int cell = t; cell < kGridCols * kGridRows; cell += 256) {
+    const int b = S.cell_start[cell], e = S.cell_start[cell + 1];
+    for (int q = b + 1; q < e; q++) {
+      const uint16_t v = S.items[q];
+      int r = q - 1;
+      while (r >= b && S.items[r] > v) {
+        S.items[r + 1] = S.items[r];
+        r--;
+      }
+      S.items[r + 1] = v;
+    }
+  }
+  __syncthreads();
+  // ---- phase A ----
+  for (int i = t; i < a.nmp; i += 256) {
+    Top2 r{256, -1, -1, 256, -1, -1};
+    if (a.in_view[i]) r = local_scan(S, c, a, cdesc, i);
+    a.scratch[i] = make_int4(r.bi, r.bd | (r.bl << 16), r.si, r.sd | (r.sl << 16));
+  }
+  __syncthreads();
+  // ---- phase B (wave 0, map point order) ----
+  if (wave == 0) {
+    int acc = 0;
+    for (int base = 0; base < a.nmp; base += 64) {
+      const int i = base + lane;
+      Top2 r{256, -1, -1, 256, -1, -1};
+      if (i < a.nmp) {
+        const int4 v = a.scratch[i];
+        r.bi = v.x;
+        r.bd = (int)(short)(v.y & 0xFFFF);
+        r.bl = (int)(short)(v.y >> 16);
+        r.si = v.z;
+        r.sd = (int)(short)(v.w & 0xFFFF);
+        r.sl = (int)(short)(v.w >> 16);
+      }
+      const int nobs = i < a.nmp ? a.mp_nobs[i] : 0;
+      bool decided = !(i < a.nmp && r.bi >= 0);
+      int start = 0;
+      while (true) {
+        const bool und = !decided && lane >= start;
+        const bool accept = und && r.bd <= 100 && !(r.bl == r.sl && r.bd > a.nnratio * r.sd);
+        const bool claimer = accept && nobs > 0;
+        bool coll = und && (((S.claimed[r.bi >> 5] >> (r.bi & 31)) & 1u) ||
+                            (r.si >= 0 && ((S.claimed[r.si >> 5] >> (r.si & 31)) & 1u)));
+        const int myclaim = claimer ? r.bi : -1;
+        for (int q = start; q < 64; q++) {
+          const int cq = __shfl(myclaim, q, 64);
+          if (q < lane && und && cq >= 0 && (cq == r.bi || cq == r.si)) coll = true;
+        }
+        const unsigned long long cm = __ballot(coll);
+        const int lc = cm ? __ffsll((long long)cm) - 1 : 64;
+        if (und && lane < lc) {
+          if (accept) {
+            atomicMax(&S.mw[r.bi], i);
+            if (claimer) atomicOr(&S.claimed[r.bi >> 5], 1u << (r.bi & 31));
+            acc++;
+          }
+          decided = true;
+        }
+        if (lc == 64) break;
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+        if (lane == lc) {
+          r = local_scan(S, c, a, cdesc, i);
+          if (r.bi < 0) decided = true;
+        }
+        __builtin_amdgcn_wave_barrier();
+        start = lc;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if (lane == 0) *a.nmatches = acc;
+  }
+  __syncthreads();
+  for (int i = t; i < n; i += 256) a.match[i] = S.mw[i];
+}
+
+void launch_in_frustum(const TrackConsts& c, float log_scale, const InFrustumArgs& a,
+                       hipStream_t s) {
+  if (a.n <= 0) return;
+  hipLaunchKernelGGL(k_in_frustum, dim3((a.n + 255) / 256), dim3(256), 0, s, c, log_scale, a);
+}
+
+void launch_match_local(const TrackConsts& c, const LocalArgs& a, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_match_local,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, sizeof(LocalShared));
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_match_local, dim3(1), dim3(256), sizeof(LocalShared), s, c, a);
+}
+
+}  // namespace orbpl

@@ -98,6 +98,50 @@ void launch_line_prepare(const TrackConsts& c, const LineTrackArgs& a, int nstre
 void launch_line_match(const TrackConsts& c, const LineTrackArgs& a, StreamState* st,
                        int nstreams, hipStream_t s);
 
+// Frame::IsInFrustum for a list of map points (match_local.hip).
+struct InFrustumArgs {
+  int n;
+  const float* Tcw;
+  const float* xyz;        // n x 3 world positions
+  const float* normal;     // n x 3 mean viewing directions
+  const float* min_dist;   // GetMinDistanceInvariance
+  const float* max_dist;   // GetMaxDistanceInvariance
+  float view_cos_limit;
+  uint8_t* in_view;        // mbTrackInView
+  float* proj_x;           // mTrackProjX
+  float* proj_y;
+  float* proj_xr;
+  int* level;              // mnTrackScaleLevel
+  float* view_cos;         // mTrackViewCos
+};
+
+// ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th).
+struct LocalArgs {
+  const KeyPointD* kps_un;
+  const uint8_t* desc;
+  const float* uright;
+  int n;
+  const int* cur_nobs;     // Observations() of the map point already at a keypoint (0: none)
+  int nmp;
+  const uint8_t* in_view;
+  const float* proj_x;
+  const float* proj_y;
+  const float* proj_xr;
+  const int* level;
+  const float* view_cos;
+  const uint8_t* mp_desc;
+  const int* mp_nobs;
+  float th;
+  float nnratio;
+  int* match;              // per keypoint: last local map point assigned, -1
+  int* nmatches;
+  int4* scratch;           // nmp entries
+};
+
+void launch_in_frustum(const TrackConsts& c, float log_scale, const InFrustumArgs& a,
+                       hipStream_t s);
+void launch_match_local(const TrackConsts& c, const LocalArgs& a, hipStream_t s);
+
 size_t match_smem_bytes();
 size_t pose_smem_bytes();
 size_t pose_edge_bytes();

@@ -15,6 +15,7 @@
 #include "orbpl_runtime.h"
 #include "track_kernels.h"
 #include "lsd_kernels.h"
+#include "lsd_math.h"
 
 using namespace orbpl;
 
@@ -269,6 +270,132 @@ int orbpl_pose_optimization(const orbpl_camera* cam, const orbpl_pose_problem* P
   if (n) HIP_CHECK(hipMemcpy(outlier, d_out.p, (size_t)n, hipMemcpyDeviceToHost));
   if (nl) HIP_CHECK(hipMemcpy(line_outlier, d_lout.p, (size_t)nl, hipMemcpyDeviceToHost));
   HIP_CHECK(hipMemcpy(n_inliers, d_nin.p, 4, hipMemcpyDeviceToHost));
+  return ORBPL_OK;
+}
+
+int orbpl_frame_is_in_frustum(const orbpl_camera* cam, float scale_factor, int nlevels,
+                              const float* Tcw, int n, const float* xyz, const float* normal,
+                              const float* min_dist, const float* max_dist, float view_cos_limit,
+                              uint8_t* in_view, float* proj_x, float* proj_y, float* proj_xr,
+                              int32_t* level, float* view_cos) {
+  if (!cam || !Tcw || n < 0 || nlevels < 1 || nlevels > kMaxLevelsT) return arg_fail("bad argument");
+  if (n > 0 && (!xyz || !normal || !min_dist || !max_dist || !in_view || !proj_x || !proj_y ||
+                !proj_xr || !level || !view_cos))
+    return arg_fail("NULL map point arrays");
+  TrackConsts c;
+  int rc = make_consts(cam, nullptr, nullptr, nlevels, &c);
+  if (rc) return rc;
+  if (n == 0) return ORBPL_OK;
+  // Frame::mfLogScaleFactor = log(mfScaleFactor) on a float (P15)
+  const float log_scale = (float)lsdm::log_((double)scale_factor);
+  DBuf dT, dx, dn, dmi, dma, div, dpx, dpy, dpr, dl, dvc;
+  HIP_CHECK(dT.alloc(64));
+  HIP_CHECK(dx.alloc((size_t)n * 12));
+  HIP_CHECK(dn.alloc((size_t)n * 12));
+  HIP_CHECK(dmi.alloc((size_t)n * 4));
+  HIP_CHECK(dma.alloc((size_t)n * 4));
+  HIP_CHECK(div.alloc(n));
+  HIP_CHECK(dpx.alloc((size_t)n * 4));
+  HIP_CHECK(dpy.alloc((size_t)n * 4));
+  HIP_CHECK(dpr.alloc((size_t)n * 4));
+  HIP_CHECK(dl.alloc((size_t)n * 4));
+  HIP_CHECK(dvc.alloc((size_t)n * 4));
+  HIP_CHECK(hipMemcpy(dT.p, Tcw, 64, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(dx.p, xyz, (size_t)n * 12, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(dn.p, normal, (size_t)n * 12, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(dmi.p, min_dist, (size_t)n * 4, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(dma.p, max_dist, (size_t)n * 4, hipMemcpyHostToDevice));
+  InFrustumArgs a{n, dT.as<float>(), dx.as<float>(), dn.as<float>(), dmi.as<float>(),
+                  dma.as<float>(), view_cos_limit, div.as<uint8_t>(), dpx.as<float>(),
+                  dpy.as<float>(), dpr.as<float>(), dl.as<int>(), dvc.as<float>()};
+  launch_in_frustum(c, log_scale, a, scratch_stream());
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipMemcpy(in_view, div.p, n, hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(proj_x, dpx.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(proj_y, dpy.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(proj_xr, dpr.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(level, dl.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(view_cos, dvc.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+  return ORBPL_OK;
+}
+
+int orbm_search_by_projection_local(const orbpl_camera* cam, const float* scale_factors,
+                                    int nlevels, const orbpl_match_current* cur, int nmp,
+                                    const uint8_t* in_view, const float* proj_x,
+                                    const float* proj_y, const float* proj_xr,
+                                    const int32_t* level, const float* view_cos,
+                                    const uint8_t* mp_desc, const int32_t* mp_nobs,
+                                    const int32_t* cur_nobs, float th, float nnratio,
+                                    int32_t* match, int* nmatches) {
+  if (!cam || !scale_factors || !cur || !nmatches || nmp < 0) return arg_fail("bad argument");
+  const int n = cur->n;
+  if (n < 0 || n > kMatchMaxKp) return arg_fail("keypoint count exceeds the matcher capacity (2048)");
+  if (n > 0 && (!cur->kps_un || !cur->desc || !cur->uright || !match)) return arg_fail("NULL frame arrays");
+  if (nmp > 0 && (!in_view || !proj_x || !proj_y || !proj_xr || !level || !view_cos || !mp_desc ||
+                  !mp_nobs))
+    return arg_fail("NULL map point arrays");
+  for (int i = 0; i < nmp; i++)
+    if (in_view[i] && (level[i] < 0 || level[i] >= nlevels)) return arg_fail("level out of range");
+  TrackConsts c;
+  int rc = make_consts(cam, scale_factors, nullptr, nlevels, &c);
+  if (rc) return rc;
+  const int P = std::max(1, n), M = std::max(1, nmp);
+  DBuf dku, dde, dur, dcn, div, dpx, dpy, dpr, dl, dvc, dmd, dmn, dm, dnm, dsc;
+  HIP_CHECK(dku.alloc((size_t)P * sizeof(KeyPointD)));
+  HIP_CHECK(dde.alloc((size_t)P * 32));
+  HIP_CHECK(dur.alloc((size_t)P * 4));
+  HIP_CHECK(dcn.alloc((size_t)P * 4));
+  HIP_CHECK(div.alloc(M));
+  HIP_CHECK(dpx.alloc((size_t)M * 4));
+  HIP_CHECK(dpy.alloc((size_t)M * 4));
+  HIP_CHECK(dpr.alloc((size_t)M * 4));
+  HIP_CHECK(dl.alloc((size_t)M * 4));
+  HIP_CHECK(dvc.alloc((size_t)M * 4));
+  HIP_CHECK(dmd.alloc((size_t)M * 32));
+  HIP_CHECK(dmn.alloc((size_t)M * 4));
+  HIP_CHECK(dm.alloc((size_t)P * 4));
+  HIP_CHECK(dnm.alloc(4));
+  HIP_CHECK(dsc.alloc((size_t)M * sizeof(int4)));
+  if (n) {
+    HIP_CHECK(hipMemcpy(dku.p, cur->kps_un, (size_t)n * sizeof(KeyPointD), hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dde.p, cur->desc, (size_t)n * 32, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dur.p, cur->uright, (size_t)n * 4, hipMemcpyHostToDevice));
+    if (cur_nobs) HIP_CHECK(hipMemcpy(dcn.p, cur_nobs, (size_t)n * 4, hipMemcpyHostToDevice));
+  }
+  if (nmp) {
+    HIP_CHECK(hipMemcpy(div.p, in_view, nmp, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dpx.p, proj_x, (size_t)nmp * 4, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dpy.p, proj_y, (size_t)nmp * 4, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dpr.p, proj_xr, (size_t)nmp * 4, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dl.p, level, (size_t)nmp * 4, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dvc.p, view_cos, (size_t)nmp * 4, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dmd.p, mp_desc, (size_t)nmp * 32, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dmn.p, mp_nobs, (size_t)nmp * 4, hipMemcpyHostToDevice));
+  }
+  LocalArgs a{};
+  a.kps_un = dku.as<KeyPointD>();
+  a.desc = dde.as<uint8_t>();
+  a.uright = dur.as<float>();
+  a.n = n;
+  a.cur_nobs = cur_nobs ? dcn.as<int>() : nullptr;
+  a.nmp = nmp;
+  a.in_view = div.as<uint8_t>();
+  a.proj_x = dpx.as<float>();
+  a.proj_y = dpy.as<float>();
+  a.proj_xr = dpr.as<float>();
+  a.level = dl.as<int>();
+  a.view_cos = dvc.as<float>();
+  a.mp_desc = dmd.as<uint8_t>();
+  a.mp_nobs = dmn.as<int>();
+  a.th = th;
+  a.nnratio = nnratio;
+  a.match = dm.as<int>();
+  a.nmatches = dnm.as<int>();
+  a.scratch = dsc.as<int4>();
+  launch_match_local(c, a, scratch_stream());
+  HIP_CHECK(hipGetLastError());
+  if (n) HIP_CHECK(hipMemcpy(match, dm.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(nmatches, dnm.p, 4, hipMemcpyDeviceToHost));
   return ORBPL_OK;
 }
 

@@ -73,3 +73,40 @@ def match_problem(seed=0, nobs_zero_frac=0.0, outlier_frac=0.0, pert=(0.01, 0.01
                uright=f1["uright"])
     lw, lh, nf, sc, isc = O.level_sizes(O.params(), 640, 480)
     return cfg, cam, sc, cur, last, (f0, f1, T0, T1)
+
+
+def local_map_problem(seed=0, cam_name="TUM1", nobs_zero_frac=0.1, cur_claim_frac=0.2):
+    """A local map for SearchLocalPoints: map points from frames 0 and 1 of a
+    seeded sequence (world position from depth at the true pose, normal and
+    scale-invariance distances as MapPoint::UpdateNormalAndDepth sets them,
+    keypoint descriptor, Observations()), the current frame = frame 3 at its
+    true pose, and some current keypoints already holding a map point."""
+    O = load_oracle()
+    cfg, traj, frames = sequence(4, seed, cam_name=cam_name)
+    cam = O.camera(cfg)
+    lw, lh, nf, sc, isc = O.level_sizes(O.params(), cfg["width"], cfg["height"])
+    rng = np.random.default_rng(seed + 11)
+    xyz, nrm, dmin, dmax, desc, nobs = [], [], [], [], [], []
+    for k in (0, 1):
+        fd = frame_data(O, cam, cfg, *frames[k])
+        Tk = np.linalg.inv(traj[k]).astype(np.float32)
+        ok = fd["depth"] > 0
+        P = unproject(cfg, fd["kps_un"][ok], fd["depth"][ok], Tk)
+        Ow = traj[k][:3, 3].astype(np.float64)
+        v = P.astype(np.float64) - Ow
+        d = np.linalg.norm(v, axis=1)
+        mx = (d * sc[fd["kps_un"]["octave"][ok]]).astype(np.float32)
+        xyz.append(P)
+        nrm.append((v / d[:, None]).astype(np.float32))
+        dmax.append(mx)
+        dmin.append((mx / sc[-1]).astype(np.float32))
+        desc.append(fd["desc"][ok])
+        nobs.append(np.where(rng.random(ok.sum()) < nobs_zero_frac, 0,
+                             rng.integers(1, 4, ok.sum())).astype(np.int32))
+    mps = dict(xyz=np.concatenate(xyz), normal=np.concatenate(nrm), min_dist=np.concatenate(dmin),
+               max_dist=np.concatenate(dmax), desc=np.concatenate(desc), nobs=np.concatenate(nobs))
+    f3 = frame_data(O, cam, cfg, *frames[3])
+    cur = dict(kps_un=f3["kps_un"], desc=f3["desc"], uright=f3["uright"])
+    cur_nobs = np.where(rng.random(len(f3["kps_un"])) < cur_claim_frac, 1, 0).astype(np.int32)
+    T3 = np.linalg.inv(traj[3]).astype(np.float32)
+    return cfg, cam, sc, mps, cur, cur_nobs, T3

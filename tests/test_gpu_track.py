@@ -312,3 +312,32 @@ def test_search_by_projection_tie_order(orbpl, oracle, seed):
         m_g, n_g = orbpl.ORBmatcher(0.9, ori).SearchByProjectionLastFrame(
             orbpl.make_camera(cfg), sc, cur, last, 15.0, False)
         assert n_g == n_o and np.array_equal(m_g, m_o), (ori, np.nonzero(m_g != m_o)[0][:5])
+
+
+def _log_scale(oracle):
+    return float(np.float32(oracle.lsdm(1, float(np.float32(1.2)))))
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_in_frustum_bit_exact(orbpl, oracle, seed):
+    from _scenes import local_map_problem
+    cfg, cam_o, sc, mps, cur, cur_nobs, T3 = local_map_problem(seed)
+    g = orbpl.frame_is_in_frustum(orbpl.make_camera(cfg), 1.2, 8, T3, mps, 0.5)
+    o = oracle.frame_is_in_frustum(cam_o, _log_scale(oracle), 8, T3, mps, 0.5)
+    for k in o:
+        assert np.array_equal(g[k], o[k]), k
+    assert 0.2 * len(mps["xyz"]) < o["in_view"].sum() < len(mps["xyz"])
+
+
+@pytest.mark.parametrize("th,nnratio,claims", [(3.0, 0.8, True), (1.0, 0.6, False), (5.0, 0.8, True)])
+def test_search_by_projection_local_bit_exact(orbpl, oracle, th, nnratio, claims):
+    from _scenes import local_map_problem
+    cfg, cam_o, sc, mps, cur, cur_nobs, T3 = local_map_problem(3)
+    track = oracle.frame_is_in_frustum(cam_o, _log_scale(oracle), 8, T3, mps, 0.5)
+    cn = cur_nobs if claims else None
+    m_o, n_o = oracle.search_by_projection_local(cam_o, sc, cur, track, mps["desc"], mps["nobs"],
+                                                 cn, th, nnratio)
+    m_g, n_g = orbpl.ORBmatcher(nnratio).SearchByProjectionLocalMap(
+        orbpl.make_camera(cfg), sc, cur, track, mps["desc"], mps["nobs"], cn, th)
+    assert n_g == n_o and n_o > 100
+    assert np.array_equal(m_g, m_o), np.nonzero(m_g != m_o)[0][:5]

@@ -1,0 +1,38 @@
+"""CPU tests of the SearchLocalPoints oracle (oracle/track_oracle.cpp):
+Frame::IsInFrustum + PredictScale and the local-map SearchByProjection."""
+import numpy as np
+
+from _scenes import local_map_problem
+
+
+def _log_scale(oracle):
+    return float(np.float32(oracle.lsdm(1, float(np.float32(1.2)))))
+
+
+def test_in_frustum_fields(oracle):
+    cfg, cam, sc, mps, cur, cur_nobs, T3 = local_map_problem(1)
+    tr = oracle.frame_is_in_frustum(cam, _log_scale(oracle), 8, T3, mps, 0.5)
+    v = tr["in_view"] > 0
+    assert v.sum() > 0.5 * len(v)
+    # projections inside the image, levels in range, viewing cosine above the limit
+    assert np.all((tr["proj_x"][v] >= 0) & (tr["proj_x"][v] <= cfg["width"]))
+    assert np.all((tr["level"][v] >= 0) & (tr["level"][v] < 8)) and np.all(tr["level"][~v] == -1)
+    assert np.all(tr["view_cos"][v] >= 0.5)
+    # a point behind the camera is never in view
+    far = dict(mps)
+    far["xyz"] = -mps["xyz"][:5] * 100
+    assert oracle.frame_is_in_frustum(cam, _log_scale(oracle), 8, T3, far, 0.5)["in_view"].sum() == 0
+
+
+def test_local_map_matches_are_geometric(oracle):
+    cfg, cam, sc, mps, cur, cur_nobs, T3 = local_map_problem(2)
+    tr = oracle.frame_is_in_frustum(cam, _log_scale(oracle), 8, T3, mps, 0.5)
+    m, n = oracle.search_by_projection_local(cam, sc, cur, tr, mps["desc"], mps["nobs"], cur_nobs,
+                                             3.0, 0.8)
+    assert n > 100 and (m >= 0).sum() <= n
+    # claimed keypoints (Observations() > 0) are never reassigned
+    assert np.all(m[cur_nobs > 0] == -1)
+    j = np.nonzero(m >= 0)[0]
+    dx = cur["kps_un"]["x"][j] - tr["proj_x"][m[j]]
+    dy = cur["kps_un"]["y"][j] - tr["proj_y"][m[j]]
+    assert np.median(np.hypot(dx, dy)) < 3.0
