@@ -352,6 +352,22 @@ int orbl_search_by_projection_last(const orbpl_camera* cam, const float* Tcw, in
                                    const float* ml_xyz6, const uint8_t* last_desc, int32_t* match,
                                    int* nmatches);
 
+/* Frame::IsInFrustum(MapLine*) (Frame.cc:403-430): in_view unless both
+ * world end points (xyz6 = start, end) are behind the camera. */
+int orbl_frame_is_in_frustum(const float* Tcw, int n, const float* xyz6, uint8_t* in_view);
+/* LineMatcher::SearchByProjection(F, vpLocalMapLines) (LineMatcher.cpp:755-952,
+ * valid = mbTrackInView) and SearchByProjection(F, RefKF) (:527-721, valid =
+ * mvpMapLines[i] != NULL): any number of map lines (world xyz6, LBD rows).
+ * Current lines whose map line has Observations() > 0 (cur_nobs, NULL: none)
+ * are skipped in the first pass. match[j] = map line index assigned to
+ * current line j, -1 = unchanged; *wiped = 1 when the relaxed retry ran, which
+ * first clears every F.mvpMapLines entry (-1 then means NULL). */
+int orbl_search_by_projection_list(const orbpl_camera* cam, const float* Tcw, int ncur,
+                                   const orbpl_keyline* cur_kl_un, const uint8_t* cur_desc,
+                                   const int32_t* cur_nobs, int nml, const uint8_t* valid,
+                                   const float* ml_xyz6, const uint8_t* ml_desc, int32_t* match,
+                                   int* nmatches, int* wiped);
+
 /* ------------------------------------------------------------------------
  * Hamming distance — ORBmatcher::DescriptorDistance (ORBmatcher.cc:2083-2103)
  * ---------------------------------------------------------------------- */

@@ -179,15 +179,24 @@ int oracle_line_frame_prepare(const orbpl_camera* cam, const orbpl_keyline* kl, 
   return 0;
 }
 
-// LineMatcher(0.9, true).SearchByProjection(CurrentFrame, LastFrame)
-// Tcw: current pose (16 floats). Last frame map lines: has_ml[i], outlier[i],
-// xyz6[i] (start, end), desc[i]. match[j] = last-frame line index or -1.
-int oracle_line_search_by_projection_last(const orbpl_camera* cam, const float* Tcw, int ncur,
-                                          const orbpl_keyline* cur_kl_un, const uint8_t* cur_desc,
-                                          int nlast, const orbpl_keyline* last_kl_un,
-                                          const uint8_t* has_ml, const uint8_t* last_outlier,
-                                          const float* ml_xyz6, const uint8_t* last_desc,
-                                          int32_t* match, int* nmatches_out) {
+}  // extern "C"
+
+namespace line_track {
+// The LineMatcher::SearchByProjection overloads share one body
+// (LineMatcher.cpp:72-269 last frame, :527-721 reference keyframe, :755-952
+// local map): map lines `valid` are projected with Tcw, clipped
+// (LiangBarsky) and rebuilt (UpdateKeyLineData on a copy of base_kl[i], or on
+// a default KeyLine when base_kl is NULL - every field LineMatching reads is
+// rewritten); current lines whose map line has Observations() > 0 are skipped
+// in the first pass; every passing pair counts, the last passing map line
+// wins; if matches / ncur < 0.2 all assignments are wiped (*wiped = 1) and the
+// relaxed pass runs.
+static int line_search_core(const orbpl_camera* cam, const float* Tcw, int ncur,
+                            const orbpl_keyline* cur_kl_un, const uint8_t* cur_desc,
+                            const int32_t* cur_nobs, int nlast, const uint8_t* valid,
+                            const orbpl_keyline* base_kl, const float* ml_xyz6,
+                            const uint8_t* last_desc, int32_t* match, int* nmatches_out,
+                            int* wiped) {
   const int W = cam->width, H = cam->height;
   double T[12];
   for (int r = 0; r < 3; r++)
@@ -201,7 +210,7 @@ int oracle_line_search_by_projection_last(const orbpl_camera* cam, const float* 
     for (int r = 0; r < 3; r++) o[r] = (T[r * 4] * X[0] + T[r * 4 + 1] * X[1] + T[r * 4 + 2] * X[2]) + T[r * 4 + 3];
   };
   for (int i = 0; i < nlast; i++) {
-    if (!has_ml[i] || last_outlier[i]) continue;
+    if (!valid[i]) continue;
     const double Xs[3] = {ml_xyz6[6 * i], ml_xyz6[6 * i + 1], ml_xyz6[6 * i + 2]};
     const double Xe[3] = {ml_xyz6[6 * i + 3], ml_xyz6[6 * i + 4], ml_xyz6[6 * i + 5]};
     double cs[3], ce[3];
@@ -236,7 +245,8 @@ int oracle_line_search_by_projection_last(const orbpl_camera* cam, const float* 
     if (!have) continue;
     double nl4[4];
     if (!liang_barsky(lp, nl4, bounds)) continue;
-    orbpl_keyline k = last_kl_un[i];
+    orbpl_keyline k{};
+    if (base_kl) k = base_kl[i];
     k.startPointX = (float)nl4[0];
     k.startPointY = (float)nl4[1];
     k.endPointX = (float)nl4[2];
@@ -249,10 +259,11 @@ int oracle_line_search_by_projection_last(const orbpl_camera* cam, const float* 
     nk.push_back(k);
     nidx.push_back(i);
   }
-  auto run = [&](const double off[5]) {
+  auto run = [&](const double off[5], bool skip) {
     int cnt = 0;
     for (int j = 0; j < ncur; j++) {
       match[j] = -1;
+      if (skip && cur_nobs && cur_nobs[j] > 0) continue;
       for (size_t i = 0; i < nk.size(); i++)
         if (line_matching(nk[i], cur_kl_un[j], last_desc + 32 * nidx[i], cur_desc + 32 * j, off)) {
           match[j] = nidx[i];
@@ -262,14 +273,66 @@ int oracle_line_search_by_projection_last(const orbpl_camera* cam, const float* 
     return cnt;
   };
   const double off0[5] = {0, 0, 0, 0, 0};
-  int n = run(off0);
+  int n = run(off0, true);
+  if (wiped) *wiped = 0;
   if (n * 1.0 / ncur < 0.2) {
     const double off1[5] = {10.0, -0.1, -0.1, 5, 10};
-    n = run(off1);
+    n = run(off1, false);
+    if (wiped) *wiped = 1;
   }
   *nmatches_out = n;
   return 0;
 }
+}  // namespace line_track
+
+extern "C" {
+
+// LineMatcher(0.9, true).SearchByProjection(CurrentFrame, LastFrame)
+// Tcw: current pose (16 floats). Last frame map lines: has_ml[i], outlier[i],
+// xyz6[i] (start, end), desc[i]. match[j] = last-frame line index or -1.
+int oracle_line_search_by_projection_last(const orbpl_camera* cam, const float* Tcw, int ncur,
+                                          const orbpl_keyline* cur_kl_un, const uint8_t* cur_desc,
+                                          int nlast, const orbpl_keyline* last_kl_un,
+                                          const uint8_t* has_ml, const uint8_t* last_outlier,
+                                          const float* ml_xyz6, const uint8_t* last_desc,
+                                          int32_t* match, int* nmatches_out) {
+  std::vector<uint8_t> valid(nlast);
+  for (int i = 0; i < nlast; i++) valid[i] = has_ml[i] && !last_outlier[i];
+  return line_track::line_search_core(cam, Tcw, ncur, cur_kl_un, cur_desc, nullptr, nlast,
+                                      valid.data(), last_kl_un, ml_xyz6, last_desc, match,
+                                      nmatches_out, nullptr);
+}
+
+// The local-map (valid = mbTrackInView) and reference-keyframe (valid =
+// mvpMapLines[i] != NULL) overloads; cur_nobs = Observations() of the map
+// line already at each current line (NULL: none).
+int oracle_line_search_by_projection_list(const orbpl_camera* cam, const float* Tcw, int ncur,
+                                          const orbpl_keyline* cur_kl_un, const uint8_t* cur_desc,
+                                          const int32_t* cur_nobs, int nml, const uint8_t* valid,
+                                          const float* ml_xyz6, const uint8_t* ml_desc,
+                                          int32_t* match, int* nmatches_out, int* wiped) {
+  return line_track::line_search_core(cam, Tcw, ncur, cur_kl_un, cur_desc, cur_nobs, nml, valid,
+                                      nullptr, ml_xyz6, ml_desc, match, nmatches_out, wiped);
+}
+
+// Frame::IsInFrustum(MapLine*) (Frame.cc:403-430): in view unless both end
+// points are behind the camera (Rcw X + tcw in float, P6).
+int oracle_line_is_in_frustum(const float* Tcw, int n, const float* xyz6, uint8_t* in_view) {
+  for (int i = 0; i < n; i++) {
+    float zs = 0, ze = 0;
+    for (int e = 0; e < 2; e++) {
+      const float* X = xyz6 + 6 * i + 3 * e;
+      double s = (double)Tcw[8] * X[0];
+      s += (double)Tcw[9] * X[1];
+      s += (double)Tcw[10] * X[2];
+      const float z = (float)(s + (double)Tcw[11]);
+      (e ? ze : zs) = z;
+    }
+    in_view[i] = !(zs < 0.0f && ze < 0.0f);
+  }
+  return 0;
+}
+
 
 }  // extern "C"
 

@@ -403,6 +403,9 @@ def _setup(L):  # noqa: F811
     L.oracle_line_frame_prepare.argtypes = [vp, vp, i, vp, vp, vp, vp, vp, vp]
     L.oracle_line_search_by_projection_last.argtypes = [vp, vp, i, vp, vp, i, vp, vp, vp, vp, vp,
                                                         vp, ip]
+    L.oracle_line_search_by_projection_list.argtypes = [vp, vp, i, vp, vp, vp, i, vp, vp, vp, vp,
+                                                        ip, ip]
+    L.oracle_line_is_in_frustum.argtypes = [vp, i, vp, vp]
     L.oracle_lvo_create.argtypes = [vp, vp, i, i]
     L.oracle_lvo_create.restype = vp
     L.oracle_lvo_destroy.argtypes = [vp]
@@ -419,6 +422,29 @@ def line_frame_prepare(cam, kl, depth=None):
     lib().oracle_line_frame_prepare(C.byref(cam), _p(kl), n, None if dp is None else _p(dp),
                                     _p(ku), _p(ds), _p(de), _p(us), _p(ue))
     return ku, ds, de, us, ue
+
+
+def line_is_in_frustum(Tcw, ml_xyz6):
+    T = _c(Tcw, np.float32)
+    X = _c(ml_xyz6, np.float32)
+    out = np.zeros(len(X), np.uint8)
+    lib().oracle_line_is_in_frustum(_p(T), len(X), _p(X), _p(out))
+    return out
+
+
+def line_search_by_projection_list(cam, Tcw, cur_kl_un, cur_desc, cur_nobs, valid, ml_xyz6,
+                                   ml_desc):
+    keep = [_c(Tcw, np.float32), _c(cur_kl_un, KEYLINE_DTYPE), _c(cur_desc, np.uint8),
+            _c(valid, np.uint8), _c(ml_xyz6, np.float32), _c(ml_desc, np.uint8)]
+    cn = None if cur_nobs is None else _c(cur_nobs, np.int32)
+    ncur = len(keep[1])
+    match = np.zeros(max(1, ncur), np.int32)
+    nm, wiped = C.c_int(0), C.c_int(0)
+    lib().oracle_line_search_by_projection_list(
+        C.byref(cam), _p(keep[0]), ncur, _p(keep[1]), _p(keep[2]), None if cn is None else _p(cn),
+        len(keep[3]), _p(keep[3]), _p(keep[4]), _p(keep[5]), _p(match), C.byref(nm),
+        C.byref(wiped))
+    return match[:ncur].copy(), nm.value, bool(wiped.value)
 
 
 def line_search_by_projection_last(cam, Tcw, cur_kl_un, cur_desc, last_kl_un, has_ml, outlier,

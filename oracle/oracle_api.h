@@ -63,6 +63,12 @@ int oracle_line_search_by_projection_last(const orbpl_camera* cam, const float* 
                                           const uint8_t* has_ml, const uint8_t* last_outlier,
                                           const float* ml_xyz6, const uint8_t* last_desc,
                                           int32_t* match, int* nmatches_out);
+int oracle_line_search_by_projection_list(const orbpl_camera* cam, const float* Tcw, int ncur,
+                                          const orbpl_keyline* cur_kl_un, const uint8_t* cur_desc,
+                                          const int32_t* cur_nobs, int nml, const uint8_t* valid,
+                                          const float* ml_xyz6, const uint8_t* ml_desc,
+                                          int32_t* match, int* nmatches_out, int* wiped);
+int oracle_line_is_in_frustum(const float* Tcw, int n, const float* xyz6, uint8_t* in_view);
 void* oracle_lvo_create(const orbpl_orb_params* orb, const orbpl_camera* cam, int n_streams,
                         int use_lines);
 void oracle_lvo_destroy(void* h);

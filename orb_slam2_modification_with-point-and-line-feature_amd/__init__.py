@@ -341,6 +341,8 @@ def _declare_track(L):
     L.orbpl_tracker_get_frame.argtypes = [vp, i, vp, vp, vp, vp, ip]
     L.orbpl_tracker_create_ex.argtypes = [vp, vp, i, i, i, C.POINTER(vp)]
     L.orbpl_line_frame_prepare.argtypes = [vp, vp, i, vp, vp, vp, vp, vp, vp]
+    L.orbl_frame_is_in_frustum.argtypes = [vp, i, vp, vp]
+    L.orbl_search_by_projection_list.argtypes = [vp, vp, i, vp, vp, vp, i, vp, vp, vp, vp, ip, ip]
     L.orbpl_frame_is_in_frustum.argtypes = [vp, C.c_float, i, vp, i, vp, vp, vp, vp, C.c_float,
                                             vp, vp, vp, vp, vp, vp]
     L.orbm_search_by_projection_local.argtypes = [vp, vp, i, vp, i, vp, vp, vp, vp, vp, vp, vp, vp,
@@ -501,7 +503,21 @@ def line_frame_prepare(camera, kl, depth=None):
 
 
 class LineMatcher:
-    """LineMatcher(0.9, true) tracking overload on the GPU."""
+    """LineMatcher(0.9, true) tracking overloads on the GPU."""
+
+    @staticmethod
+    def SearchByProjectionLocalMap(camera, Tcw, cur_kl_un, cur_desc, cur_nobs, in_view, ml_xyz6,
+                                   ml_desc):
+        """SearchByProjection(F, vpLocalMapLines): (match, nmatches, wiped)."""
+        return _line_search_list(camera, Tcw, cur_kl_un, cur_desc, cur_nobs, in_view, ml_xyz6,
+                                 ml_desc)
+
+    @staticmethod
+    def SearchByProjectionRefKF(camera, Tcw, cur_kl_un, cur_desc, cur_nobs, has_ml, ml_xyz6,
+                                ml_desc):
+        """SearchByProjection(F, RefKF): (match, nmatches, wiped)."""
+        return _line_search_list(camera, Tcw, cur_kl_un, cur_desc, cur_nobs, has_ml, ml_xyz6,
+                                 ml_desc)
 
     @staticmethod
     def SearchByProjectionLastFrame(camera, Tcw, cur_kl_un, cur_desc, last_kl_un, has_ml, outlier,
@@ -519,6 +535,31 @@ class LineMatcher:
             _ptr(keep[3]), _ptr(keep[4]), _ptr(keep[5]), _ptr(keep[6]), _ptr(keep[7]), _ptr(match),
             C.byref(nm)), "orbl_search_by_projection_last")
         return match[:ncur].copy(), nm.value
+
+
+def line_is_in_frustum(Tcw, ml_xyz6):
+    """Frame::IsInFrustum(MapLine*) for n map lines (n x 6 world end points)."""
+    T = np.ascontiguousarray(Tcw, np.float32)
+    X = np.ascontiguousarray(ml_xyz6, np.float32)
+    out = np.zeros(len(X), np.uint8)
+    check(lib().orbl_frame_is_in_frustum(_ptr(T), len(X), _ptr(X), _ptr(out)),
+          "orbl_frame_is_in_frustum")
+    return out
+
+
+def _line_search_list(camera, Tcw, cur_kl_un, cur_desc, cur_nobs, valid, ml_xyz6, ml_desc):
+    keep = [np.ascontiguousarray(Tcw, np.float32), np.ascontiguousarray(cur_kl_un, KEYLINE_DTYPE),
+            np.ascontiguousarray(cur_desc, np.uint8), np.ascontiguousarray(valid, np.uint8),
+            np.ascontiguousarray(ml_xyz6, np.float32), np.ascontiguousarray(ml_desc, np.uint8)]
+    cn = None if cur_nobs is None else np.ascontiguousarray(cur_nobs, np.int32)
+    ncur = len(keep[1])
+    match = np.zeros(max(1, ncur), np.int32)
+    nm, wiped = C.c_int(0), C.c_int(0)
+    check(lib().orbl_search_by_projection_list(
+        C.byref(camera), _ptr(keep[0]), ncur, _ptr(keep[1]), _ptr(keep[2]),
+        None if cn is None else _ptr(cn), len(keep[3]), _ptr(keep[3]), _ptr(keep[4]),
+        _ptr(keep[5]), _ptr(match), C.byref(nm), C.byref(wiped)), "orbl_search_by_projection_list")
+    return match[:ncur].copy(), nm.value, bool(wiped.value)
 
 
 class Tracker:

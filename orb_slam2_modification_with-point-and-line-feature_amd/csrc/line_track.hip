@@ -161,6 +161,59 @@ __device__ bool line_matching(const orbpl_keyline& k1, const orbpl_keyline& k2, 
 
 }  // namespace
 
+// Project map line X (6 floats) with T (row-major 3x4 double copy), clip
+// to the image bounds and rebuild the KeyLine (LineMatcher.cpp:118-193,
+// UpdateKeyLineData :1601-1624). Returns false when the line is not seen.
+__device__ bool project_map_line(const TrackConsts& c, const double T[12], const float* X,
+                                 orbpl_keyline& k) {
+  double cs[3], ce[3];
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    cs[r] = (T[r * 4] * (double)X[0] + T[r * 4 + 1] * (double)X[1] + T[r * 4 + 2] * (double)X[2]) + T[r * 4 + 3];
+    ce[r] = (T[r * 4] * (double)X[3] + T[r * 4 + 1] * (double)X[4] + T[r * 4 + 2] * (double)X[5]) + T[r * 4 + 3];
+  }
+  if (cs[2] < 0 && ce[2] < 0) return false;
+  double lp[4];
+  bool have = false;
+  if (cs[2] < 0.0 || ce[2] < 0.0) {
+    const double lambda = -1.0 * cs[2] / (cs[2] - ce[2]);
+    const double xc = cs[0] + lambda * (cs[0] - ce[0]);
+    const double yc = cs[1] + lambda * (cs[1] - ce[1]);
+    if (cs[2] < 0.0) {
+      const float u_end = c.fx * ce[0] / ce[2] + c.cx;
+      const float v_end = c.fy * ce[1] / ce[2] + c.cy;
+      lp[0] = xc; lp[1] = yc; lp[2] = u_end; lp[3] = v_end;
+    } else {
+      const float u_start = c.fx * cs[0] / cs[2] + c.cx;
+      const float v_start = c.fy * cs[1] / cs[2] + c.cy;
+      lp[0] = u_start; lp[1] = v_start; lp[2] = xc; lp[3] = yc;
+    }
+    have = true;
+  }
+  if (cs[2] > 0.0 && ce[2] > 0.0) {
+    const float u_start = c.fx * cs[0] / cs[2] + c.cx;
+    const float v_start = c.fy * cs[1] / cs[2] + c.cy;
+    const float u_end = c.fx * ce[0] / ce[2] + c.cx;
+    const float v_end = c.fy * ce[1] / ce[2] + c.cy;
+    lp[0] = u_start; lp[1] = v_start; lp[2] = u_end; lp[3] = v_end;
+    have = true;
+  }
+  if (!have) return false;
+  double nl4[4];
+  const float bounds[4] = {c.minX, c.minY, c.maxX, c.maxY};
+  if (!liang_barsky(lp, nl4, bounds)) return false;
+  k.startPointX = (float)nl4[0];
+  k.startPointY = (float)nl4[1];
+  k.endPointX = (float)nl4[2];
+  k.endPointY = (float)nl4[3];
+  k.sPointInOctaveX = (float)nl4[0];
+  k.sPointInOctaveY = (float)nl4[1];
+  k.ePointInOctaveX = (float)nl4[2];
+  k.ePointInOctaveY = (float)nl4[3];
+  refresh_keyline(k, c.width, c.height);
+  return true;
+}
+
 // One 256-thread block per stream.
 __global__ void __launch_bounds__(256) k_line_match(TrackConsts c, LineTrackArgs a,
                                                      StreamState* st) {
@@ -292,6 +345,101 @@ void launch_line_prepare(const TrackConsts& c, const LineTrackArgs& a, int nstre
 void launch_line_match(const TrackConsts& c, const LineTrackArgs& a, StreamState* st,
                        int nstreams, hipStream_t s) {
   hipLaunchKernelGGL(k_line_match, dim3(nstreams), dim3(256), 0, s, c, a, st);
+}
+
+
+// LineMatcher::SearchByProjection(Frame&, const vector<MapLine*>&) and
+// (Frame&, KeyFrame*) (LineMatcher.cpp:755-952, 527-721): any number of map
+// lines. One 256-thread block: the valid map lines are projected and
+// compacted in order into global scratch, then every (projected, current)
+// pair is tested; per current line the last passing projected line wins
+// (atomicMax), every pass counts.
+__global__ void __launch_bounds__(256) k_line_match_list(TrackConsts c, LineListArgs a) {
+  __shared__ int s_wc[4];
+  __shared__ int s_np, s_cnt;
+  __shared__ int s_last[kLineKeep];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  double T[12];
+#pragma unroll
+  for (int q = 0; q < 12; q++) T[q] = a.Tcw[q];
+  if (t == 0) s_np = 0;
+  __syncthreads();
+  for (int base = 0; base < a.nml; base += 256) {
+    const int i = base + t;
+    orbpl_keyline k{};
+    const bool ok = i < a.nml && a.valid[i] && project_map_line(c, T, a.ml_xyz6 + (long long)i * 6, k);
+    const unsigned long long m = __ballot(ok);
+    if (lane == 0) s_wc[wave] = __popcll(m);
+    __syncthreads();
+    int pos = s_np + __popcll(m & ((1ull << lane) - 1ull));
+    for (int w = 0; w < wave; w++) pos += s_wc[w];
+    if (ok) {
+      a.proj_kl[pos] = k;
+      a.proj_src[pos] = i;
+    }
+    __syncthreads();
+    if (t == 0) s_np += s_wc[0] + s_wc[1] + s_wc[2] + s_wc[3];
+    __syncthreads();
+  }
+  const int np = s_np, ncur = min(a.ncur, kLineKeep);
+  const uint4* cur_desc = reinterpret_cast<const uint4*>(a.cur_desc);
+  const uint4* ml_desc = reinterpret_cast<const uint4*>(a.ml_desc);
+  int total = 0, wiped = 0;
+  for (int pass = 0; pass < 2; pass++) {
+    const double o0 = pass ? 10.0 : 0, o1 = pass ? -0.1 : 0, o2 = pass ? -0.1 : 0, o3 = pass ? 5 : 0;
+    for (int j = t; j < ncur; j += 256) s_last[j] = -1;
+    if (t == 0) s_cnt = 0;
+    __syncthreads();
+    int cnt = 0;
+    for (long long pr = t; pr < (long long)ncur * np; pr += 256) {
+      const int j = (int)(pr / np), i = (int)(pr - (long long)j * np);
+      if (pass == 0 && a.cur_nobs && a.cur_nobs[j] > 0) continue;
+      const orbpl_keyline kp = a.proj_kl[i];
+      const orbpl_keyline kc = a.cur_kl_un[j];
+      if (line_matching(kp, kc, ml_desc + 2 * a.proj_src[i], cur_desc + 2 * j, o0, o1, o2, o3)) {
+        atomicMax(&s_last[j], i);
+        cnt++;
+      }
+    }
+    if (cnt) atomicAdd(&s_cnt, cnt);
+    __syncthreads();
+    total = s_cnt;
+    wiped = pass;
+    if (pass == 0 && !(total * 1.0 / ncur < 0.2)) break;
+    __syncthreads();
+  }
+  for (int j = t; j < ncur; j += 256) a.match[j] = s_last[j] >= 0 ? a.proj_src[s_last[j]] : -1;
+  if (t == 0) {
+    *a.nmatches = total;
+    if (a.wiped) *a.wiped = wiped;
+  }
+}
+
+// Frame::IsInFrustum(MapLine*) (Frame.cc:403-430)
+__global__ void k_line_in_frustum(const float* __restrict__ Tcw, int n, const float* __restrict__ xyz6,
+                                  uint8_t* __restrict__ in_view) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float z[2];
+#pragma unroll
+  for (int e = 0; e < 2; e++) {
+    const float* X = xyz6 + (long long)i * 6 + 3 * e;
+    double s = (double)Tcw[8] * X[0];
+    s += (double)Tcw[9] * X[1];
+    s += (double)Tcw[10] * X[2];
+    z[e] = (float)(s + (double)Tcw[11]);
+  }
+  in_view[i] = !(z[0] < 0.0f && z[1] < 0.0f);
+}
+
+void launch_line_match_list(const TrackConsts& c, const LineListArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_line_match_list, dim3(1), dim3(256), 0, s, c, a);
+}
+
+void launch_line_in_frustum(const float* Tcw, int n, const float* xyz6, uint8_t* in_view,
+                            hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_line_in_frustum, dim3((n + 255) / 256), dim3(256), 0, s, Tcw, n, xyz6, in_view);
 }
 
 }  // namespace orbpl

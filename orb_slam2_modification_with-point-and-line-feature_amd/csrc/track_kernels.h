@@ -93,6 +93,27 @@ struct LineTrackArgs {
   const uint8_t* last_desc;
 };
 
+// LineMatcher local-map / reference-keyframe overloads (any number of map lines).
+struct LineListArgs {
+  const float* Tcw;              // 16 floats
+  int ncur;
+  const orbpl_keyline* cur_kl_un;
+  const uint8_t* cur_desc;
+  const int* cur_nobs;           // optional: Observations() of the map line already at each line
+  int nml;
+  const uint8_t* valid;          // mbTrackInView / mvpMapLines[i] != NULL
+  const float* ml_xyz6;
+  const uint8_t* ml_desc;
+  orbpl_keyline* proj_kl;        // scratch, nml entries
+  int* proj_src;                 // scratch, nml entries
+  int* match;                    // per current line: map line index or -1 (unchanged / wiped)
+  int* nmatches;
+  int* wiped;                    // 1 when the relaxed retry ran (all assignments cleared first)
+};
+void launch_line_match_list(const TrackConsts& c, const LineListArgs& a, hipStream_t s);
+void launch_line_in_frustum(const float* Tcw, int n, const float* xyz6, uint8_t* in_view,
+                            hipStream_t s);
+
 void launch_line_prepare(const TrackConsts& c, const LineTrackArgs& a, int nstreams,
                          hipStream_t s);
 void launch_line_match(const TrackConsts& c, const LineTrackArgs& a, StreamState* st,

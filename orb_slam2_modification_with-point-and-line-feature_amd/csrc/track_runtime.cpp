@@ -511,6 +511,82 @@ int orbl_search_by_projection_last(const orbpl_camera* cam, const float* Tcw, in
   return ORBPL_OK;
 }
 
+int orbl_frame_is_in_frustum(const float* Tcw, int n, const float* xyz6, uint8_t* in_view) {
+  if (!Tcw || n < 0 || (n > 0 && (!xyz6 || !in_view))) return arg_fail("bad argument");
+  if (n == 0) return ORBPL_OK;
+  DBuf dT, dx, dv;
+  HIP_CHECK(dT.alloc(64));
+  HIP_CHECK(dx.alloc((size_t)n * 24));
+  HIP_CHECK(dv.alloc(n));
+  HIP_CHECK(hipMemcpy(dT.p, Tcw, 64, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(dx.p, xyz6, (size_t)n * 24, hipMemcpyHostToDevice));
+  launch_line_in_frustum(dT.as<float>(), n, dx.as<float>(), dv.as<uint8_t>(), scratch_stream());
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipMemcpy(in_view, dv.p, n, hipMemcpyDeviceToHost));
+  return ORBPL_OK;
+}
+
+int orbl_search_by_projection_list(const orbpl_camera* cam, const float* Tcw, int ncur,
+                                   const orbpl_keyline* cur_kl_un, const uint8_t* cur_desc,
+                                   const int32_t* cur_nobs, int nml, const uint8_t* valid,
+                                   const float* ml_xyz6, const uint8_t* ml_desc, int32_t* match,
+                                   int* nmatches, int* wiped) {
+  if (!cam || !Tcw || !nmatches || ncur < 0 || nml < 0) return arg_fail("bad argument");
+  if (ncur > kLineKeep) return arg_fail("more key lines than LineExtractor keeps (80)");
+  if ((ncur > 0 && (!cur_kl_un || !cur_desc || !match)) ||
+      (nml > 0 && (!valid || !ml_xyz6 || !ml_desc)))
+    return arg_fail("NULL line arrays");
+  TrackConsts c;
+  int rc = make_consts(cam, nullptr, nullptr, 1, &c);
+  if (rc) return rc;
+  const size_t L = kLineKeep, M = std::max(1, nml);
+  DBuf dT, dku, dde, dcn, dv, dx, dmd, dpk, dps, dm, dnm, dw;
+  HIP_CHECK(dT.alloc(64));
+  HIP_CHECK(dku.alloc(L * sizeof(orbpl_keyline)));
+  HIP_CHECK(dde.alloc(L * 32));
+  HIP_CHECK(dcn.alloc(L * 4));
+  HIP_CHECK(dv.alloc(M));
+  HIP_CHECK(dx.alloc(M * 24));
+  HIP_CHECK(dmd.alloc(M * 32));
+  HIP_CHECK(dpk.alloc(M * sizeof(orbpl_keyline)));
+  HIP_CHECK(dps.alloc(M * 4));
+  HIP_CHECK(dm.alloc(L * 4));
+  HIP_CHECK(dnm.alloc(4));
+  HIP_CHECK(dw.alloc(4));
+  HIP_CHECK(hipMemcpy(dT.p, Tcw, 64, hipMemcpyHostToDevice));
+  if (ncur) {
+    HIP_CHECK(hipMemcpy(dku.p, cur_kl_un, ncur * sizeof(orbpl_keyline), hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dde.p, cur_desc, (size_t)ncur * 32, hipMemcpyHostToDevice));
+    if (cur_nobs) HIP_CHECK(hipMemcpy(dcn.p, cur_nobs, (size_t)ncur * 4, hipMemcpyHostToDevice));
+  }
+  if (nml) {
+    HIP_CHECK(hipMemcpy(dv.p, valid, nml, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dx.p, ml_xyz6, (size_t)nml * 24, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dmd.p, ml_desc, (size_t)nml * 32, hipMemcpyHostToDevice));
+  }
+  LineListArgs a{};
+  a.Tcw = dT.as<float>();
+  a.ncur = ncur;
+  a.cur_kl_un = dku.as<orbpl_keyline>();
+  a.cur_desc = dde.as<uint8_t>();
+  a.cur_nobs = cur_nobs ? dcn.as<int>() : nullptr;
+  a.nml = nml;
+  a.valid = dv.as<uint8_t>();
+  a.ml_xyz6 = dx.as<float>();
+  a.ml_desc = dmd.as<uint8_t>();
+  a.proj_kl = dpk.as<orbpl_keyline>();
+  a.proj_src = dps.as<int>();
+  a.match = dm.as<int>();
+  a.nmatches = dnm.as<int>();
+  a.wiped = dw.as<int>();
+  launch_line_match_list(c, a, scratch_stream());
+  HIP_CHECK(hipGetLastError());
+  if (ncur) HIP_CHECK(hipMemcpy(match, dm.p, (size_t)ncur * 4, hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(nmatches, dnm.p, 4, hipMemcpyDeviceToHost));
+  if (wiped) HIP_CHECK(hipMemcpy(wiped, dw.p, 4, hipMemcpyDeviceToHost));
+  return ORBPL_OK;
+}
+
 }  // extern "C"
 
 // ---------------------------------------------------------------------------

@@ -110,3 +110,35 @@ def local_map_problem(seed=0, cam_name="TUM1", nobs_zero_frac=0.1, cur_claim_fra
     cur_nobs = np.where(rng.random(len(f3["kps_un"])) < cur_claim_frac, 1, 0).astype(np.int32)
     T3 = np.linalg.inv(traj[3]).astype(np.float32)
     return cfg, cam, sc, mps, cur, cur_nobs, T3
+
+
+def line_map_problem(seed=0, cam_name="TUM1", claim_frac=0.15):
+    """Map lines from frames 0 and 1 (end points unprojected with their own
+    depths at the true poses, LBD rows), the current frame 2's undistorted key
+    lines and LBD rows at its true pose, and some current lines already
+    holding a map line with Observations() > 0."""
+    O = load_oracle()
+    cfg, traj, frames = sequence(3, seed, cam_name=cam_name)
+    cam = O.camera(cfg)
+    xyz, desc = [], []
+    for k in (0, 1):
+        g, d = frames[k]
+        kl, ld, _, _ = O.line_extract(g)
+        ku, ds, de, _, _ = O.line_frame_prepare(cam, kl, d)
+        ok = (ds > 0) & (de > 0)
+        Twc = traj[k].astype(np.float64)
+        for j in np.nonzero(ok)[0]:
+            row = []
+            for (u, v, z) in ((ku["startPointX"][j], ku["startPointY"][j], ds[j]),
+                              (ku["endPointX"][j], ku["endPointY"][j], de[j])):
+                P = np.array([(u - cfg["cx"]) * z / cfg["fx"], (v - cfg["cy"]) * z / cfg["fy"], z, 1.0])
+                row.extend((Twc @ P)[:3])
+            xyz.append(row)
+            desc.append(ld[j])
+    g, d = frames[2]
+    kl, ld, _, _ = O.line_extract(g)
+    ku, _, _, _, _ = O.line_frame_prepare(cam, kl, d)
+    rng = np.random.default_rng(seed + 3)
+    cur_nobs = np.where(rng.random(len(ku)) < claim_frac, 1, 0).astype(np.int32)
+    T2 = np.linalg.inv(traj[2]).astype(np.float32)
+    return (cfg, cam, np.array(xyz, np.float32), np.array(desc, np.uint8), ku, ld, cur_nobs, T2)

@@ -341,3 +341,33 @@ def test_search_by_projection_local_bit_exact(orbpl, oracle, th, nnratio, claims
         orbpl.make_camera(cfg), sc, cur, track, mps["desc"], mps["nobs"], cn, th)
     assert n_g == n_o and n_o > 100
     assert np.array_equal(m_g, m_o), np.nonzero(m_g != m_o)[0][:5]
+
+
+@pytest.mark.parametrize("case", ["local_map", "ref_kf", "retry"])
+def test_line_search_by_projection_list_bit_exact(orbpl, oracle, case):
+    from _scenes import line_map_problem
+    cfg, cam_o, xyz, desc, ku, ld, cur_nobs, T2 = line_map_problem(5)
+    cam_g = orbpl.make_camera(cfg)
+    if case == "retry":   # a pose far off: few matches, the relaxed pass runs
+        T0 = T2
+        for off in (0.3, 0.6, 1.0, 2.0, 4.0):
+            T2 = T0.copy()
+            T2[:3, 3] += np.float32([off, 0.0, 0.5 * off])
+            v = oracle.line_is_in_frustum(T2, xyz)
+            if oracle.line_search_by_projection_list(cam_o, T2, ku, ld, cur_nobs, v, xyz, desc)[2]:
+                break
+    valid = oracle.line_is_in_frustum(T2, xyz)
+    assert np.array_equal(orbpl.line_is_in_frustum(T2, xyz), valid)
+    if case == "ref_kf":
+        valid = np.ones(len(xyz), np.uint8)
+        valid[::7] = 0
+    cn = None if case == "ref_kf" else cur_nobs
+    m_o, n_o, w_o = oracle.line_search_by_projection_list(cam_o, T2, ku, ld, cn, valid, xyz, desc)
+    m_g, n_g, w_g = orbpl.LineMatcher.SearchByProjectionLocalMap(cam_g, T2, ku, ld, cn, valid, xyz,
+                                                                 desc)
+    assert (n_g, w_g) == (n_o, w_o)
+    assert np.array_equal(m_g, m_o)
+    if case == "retry":
+        assert w_o
+    else:
+        assert n_o > 20 and not w_o

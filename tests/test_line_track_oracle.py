@@ -101,3 +101,26 @@ def test_lvo_with_lines_tracks(oracle):
             # at most on this scene; the tracker must stay near truth
             Tgt = np.linalg.inv(traj[f])
             assert np.abs(T[:3, 3] - Tgt[:3, 3]).max() < 0.2
+
+
+def test_list_overload_equals_last_frame_overload(oracle):
+    """The local-map / ref-KF body with valid = has_ml && !outlier and no
+    claims gives the last-frame overload's result (the projected KeyLine's
+    base fields are all rewritten by UpdateKeyLineData)."""
+    from _scenes import line_map_problem
+    cfg, cam, xyz, desc, ku, ld, cur_nobs, T2 = line_map_problem(4)
+    n = len(xyz)
+    rng = np.random.default_rng(0)
+    has = (rng.random(n) < 0.9).astype(np.uint8)
+    out = (rng.random(n) < 0.1).astype(np.uint8)
+    base = np.zeros(n, ku.dtype)
+    m1, n1 = oracle.line_search_by_projection_last(cam, T2, ku, ld, base, has, out, xyz, desc)
+    m2, n2, w = oracle.line_search_by_projection_list(cam, T2, ku, ld, None, has & (1 - out), xyz,
+                                                      desc)
+    assert n1 == n2 and np.array_equal(m1, m2) and n1 > 10
+
+
+def test_line_in_frustum(oracle):
+    T = np.eye(4, dtype=np.float32)
+    X = np.array([[0, 0, 1, 0, 0, 2], [0, 0, -1, 0, 0, 2], [0, 0, -1, 0, 0, -2]], np.float32)
+    assert oracle.line_is_in_frustum(T, X).tolist() == [1, 1, 0]
