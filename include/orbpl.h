@@ -230,6 +230,19 @@ int orbm_search_by_projection_local(const orbpl_camera* cam, const float* scale_
                                     const int32_t* cur_nobs, float th, float nnratio,
                                     int32_t* match, int* nmatches);
 
+/* ORBmatcher(nnratio, checkOri).SearchByBoW(pKF, F, vpMapPointMatches)
+ * (ORBmatcher.cc:247-410). The DBoW2 FeatureVectors are passed as one
+ * vocabulary node id per feature (-1: none; ids < 2^21 - 1): features meet
+ * only within a node, keyframe features in index order, a frame feature taken
+ * earlier in the call is skipped; TH_LOW 50 and best < nnratio * second; then
+ * the 30-bin rotation check (kf_angle = mvKeysUn, f_angle = mvKeys). kf_valid
+ * = the keyframe's map point exists and is not bad. match[j] = keyframe
+ * feature index whose map point goes to frame feature j, or -1. n <= 2048. */
+int orbm_search_by_bow(int nkf, const int32_t* kf_node, const uint8_t* kf_valid,
+                       const uint8_t* kf_desc, const float* kf_angle, int nf, const int32_t* f_node,
+                       const uint8_t* f_desc, const float* f_angle, float nnratio, int check_ori,
+                       int32_t* match, int* nmatches);
+
 /* ------------------------------------------------------------------------
  * Optimizer::PoseOptimization / PoseOptimizationWithLines
  * (Optimizer.cc:375-619, 2132-2486): 4 rounds x 10 Levenberg-Marquardt

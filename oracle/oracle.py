@@ -163,6 +163,7 @@ def _setup_track(L):
     L.oracle_frame_prepare.argtypes = [vp, vp, i, vp, vp, vp, vp, vp, vp]
     L.oracle_search_by_projection_last.argtypes = [vp, vp, i, vp, vp, C.c_float, i, i, vp, ip]
     L.oracle_pose_optimization.argtypes = [vp, vp, vp, vp, vp, ip]
+    L.oracle_search_by_bow.argtypes = [i, vp, vp, vp, vp, i, vp, vp, vp, C.c_float, i, vp, ip]
     L.oracle_frame_is_in_frustum.argtypes = [vp, C.c_float, i, vp, i, vp, vp, vp, vp, C.c_float,
                                              vp, vp, vp, vp, vp, vp]
     L.oracle_search_by_projection_local.argtypes = [vp, vp, i, vp, i, vp, vp, vp, vp, vp, vp, vp,
@@ -257,6 +258,20 @@ def search_by_projection_local(cam, scale_factors, cur, track, mp_desc, mp_nobs,
         arr(mp_nobs, np.int32), None if cur_nobs is None else arr(cur_nobs, np.int32),
         C.c_float(th), C.c_float(nnratio), _p(match), C.byref(nm))
     return match[:n].copy(), nm.value
+
+
+def search_by_bow(kf_node, kf_valid, kf_desc, kf_angle, f_node, f_desc, f_angle, nnratio=0.7,
+                  check_ori=True):
+    keep = [_c(kf_node, np.int32), _c(kf_valid, np.uint8), _c(kf_desc, np.uint8),
+            _c(kf_angle, np.float32), _c(f_node, np.int32), _c(f_desc, np.uint8),
+            _c(f_angle, np.float32)]
+    nf = len(keep[4])
+    match = np.zeros(max(1, nf), np.int32)
+    nm = C.c_int(0)
+    lib().oracle_search_by_bow(len(keep[0]), _p(keep[0]), _p(keep[1]), _p(keep[2]), _p(keep[3]),
+                               nf, _p(keep[4]), _p(keep[5]), _p(keep[6]), C.c_float(nnratio),
+                               int(check_ori), _p(match), C.byref(nm))
+    return match[:nf].copy(), nm.value
 
 
 def pose_optimization(cam, prob, Tcw, outlier, line_outlier=None):

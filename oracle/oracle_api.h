@@ -35,6 +35,10 @@ int oracle_search_by_projection_local(const orbpl_camera* cam, const float* scal
                                       const uint8_t* mp_desc, const int32_t* mp_nobs,
                                       const int32_t* cur_nobs, float th, float nnratio,
                                       int32_t* match, int* nmatches_out);
+int oracle_search_by_bow(int nkf, const int32_t* kf_node, const uint8_t* kf_valid,
+                         const uint8_t* kf_desc, const float* kf_angle, int nf,
+                         const int32_t* f_node, const uint8_t* f_desc, const float* f_angle,
+                         float nnratio, int check_ori, int32_t* match, int* nmatches_out);
 int oracle_pose_optimization(const orbpl_camera* cam, const orbpl_pose_problem* P, float* Tcw,
                              uint8_t* outlier, uint8_t* line_outlier, int* n_inliers);
 void* oracle_vo_create(const orbpl_orb_params* orb, const orbpl_camera* cam, int n_streams);

@@ -24,6 +24,7 @@
 // parity unpinned against the real reference binary (no fixtures exist).
 // ============================================================================
 #include <algorithm>
+#include <map>
 #include <cfloat>
 #include <cmath>
 #include <cstdint>
@@ -1068,6 +1069,94 @@ int oracle_search_by_projection_local(const orbpl_camera* cam, const float* scal
       match[bestIdx] = i;
       obs[bestIdx] = mp_nobs[i];
       nmatches++;
+    }
+  }
+  *nmatches_out = nmatches;
+  return 0;
+}
+
+// ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&)
+// (ORBmatcher.cc:247-410). The DBoW2 FeatureVectors are given as one node id
+// per feature (-1: no node); DBoW2 adds features to a node in index order,
+// so a node's list is its features in increasing index. kf_valid[i] = the
+// keyframe's map point i exists and is not bad. match[j] = keyframe feature
+// index whose map point is assigned to frame feature j, or -1.
+int oracle_search_by_bow(int nkf, const int32_t* kf_node, const uint8_t* kf_valid,
+                         const uint8_t* kf_desc, const float* kf_angle, int nf,
+                         const int32_t* f_node, const uint8_t* f_desc, const float* f_angle,
+                         float nnratio, int check_ori, int32_t* match, int* nmatches_out) {
+  const int HISTO_LENGTH = 30, TH_LOW = 50;
+  std::map<int, std::vector<int>> fvKF, fvF;
+  for (int i = 0; i < nkf; i++)
+    if (kf_node[i] >= 0) fvKF[kf_node[i]].push_back(i);
+  for (int j = 0; j < nf; j++)
+    if (f_node[j] >= 0) fvF[f_node[j]].push_back(j);
+  for (int j = 0; j < nf; j++) match[j] = -1;
+  std::vector<int> rotHist[HISTO_LENGTH];
+  const float factor = HISTO_LENGTH / 360.0f;
+  int nmatches = 0;
+  auto KFit = fvKF.begin(), Fit = fvF.begin();
+  while (KFit != fvKF.end() && Fit != fvF.end()) {
+    if (KFit->first == Fit->first) {
+      for (int iKF : KFit->second) {
+        if (!kf_valid[iKF]) continue;
+        int bestDist1 = 256, bestIdxF = -1, bestDist2 = 256;
+        for (int iF : Fit->second) {
+          if (match[iF] >= 0) continue;
+          const int dist = desc_dist(kf_desc + 32 * iKF, f_desc + 32 * iF);
+          if (dist < bestDist1) {
+            bestDist2 = bestDist1;
+            bestDist1 = dist;
+            bestIdxF = iF;
+          } else if (dist < bestDist2) {
+            bestDist2 = dist;
+          }
+        }
+        if (bestDist1 <= TH_LOW) {
+          if (static_cast<float>(bestDist1) < nnratio * static_cast<float>(bestDist2)) {
+            match[bestIdxF] = iKF;
+            if (check_ori) {
+              float rot = kf_angle[iKF] - f_angle[bestIdxF];
+              if (rot < 0.0) rot += 360.0f;
+              int bin = (int)std::round(rot * factor);
+              if (bin == HISTO_LENGTH) bin = 0;
+              rotHist[bin].push_back(bestIdxF);
+            }
+            nmatches++;
+          }
+        }
+      }
+      ++KFit;
+      ++Fit;
+    } else if (KFit->first < Fit->first) {
+      KFit = fvKF.lower_bound(Fit->first);
+    } else {
+      Fit = fvF.lower_bound(KFit->first);
+    }
+  }
+  if (check_ori) {
+    int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+    for (int i = 0; i < HISTO_LENGTH; i++) {
+      const int sz = (int)rotHist[i].size();
+      if (sz > max1) {
+        max3 = max2; max2 = max1; max1 = sz; ind3 = ind2; ind2 = ind1; ind1 = i;
+      } else if (sz > max2) {
+        max3 = max2; max2 = sz; ind3 = ind2; ind2 = i;
+      } else if (sz > max3) {
+        max3 = sz; ind3 = i;
+      }
+    }
+    if (max2 < 0.1f * (float)max1) {
+      ind2 = -1; ind3 = -1;
+    } else if (max3 < 0.1f * (float)max1) {
+      ind3 = -1;
+    }
+    for (int i = 0; i < HISTO_LENGTH; i++) {
+      if (i == ind1 || i == ind2 || i == ind3) continue;
+      for (int j : rotHist[i]) {
+        match[j] = -1;
+        nmatches--;
+      }
     }
   }
   *nmatches_out = nmatches;

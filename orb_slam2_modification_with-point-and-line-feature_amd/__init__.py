@@ -342,6 +342,7 @@ def _declare_track(L):
     L.orbpl_tracker_create_ex.argtypes = [vp, vp, i, i, i, C.POINTER(vp)]
     L.orbpl_line_frame_prepare.argtypes = [vp, vp, i, vp, vp, vp, vp, vp, vp]
     L.orbl_frame_is_in_frustum.argtypes = [vp, i, vp, vp]
+    L.orbm_search_by_bow.argtypes = [i, vp, vp, vp, vp, i, vp, vp, vp, C.c_float, i, vp, ip]
     L.orbl_search_by_projection_list.argtypes = [vp, vp, i, vp, vp, vp, i, vp, vp, vp, vp, ip, ip]
     L.orbpl_frame_is_in_frustum.argtypes = [vp, C.c_float, i, vp, i, vp, vp, vp, vp, C.c_float,
                                             vp, vp, vp, vp, vp, vp]
@@ -414,6 +415,21 @@ class ORBmatcher:
                                                    int(bMono), int(self.checkOri), _ptr(match),
                                                    C.byref(nm)), "orbm_search_by_projection_last")
         return match[:mc.n].copy(), nm.value
+
+    def SearchByBoW(self, kf_node, kf_valid, kf_desc, kf_angle, f_node, f_desc, f_angle):
+        """SearchByBoW(pKF, F) (ORBmatcher.cc:247-410) with per-feature
+        vocabulary node ids. Returns (match, nmatches)."""
+        keep = [_c(kf_node, np.int32), _c(kf_valid, np.uint8), _c(kf_desc, np.uint8),
+                _c(kf_angle, np.float32), _c(f_node, np.int32), _c(f_desc, np.uint8),
+                _c(f_angle, np.float32)]
+        nf = len(keep[4])
+        match = np.zeros(max(1, nf), np.int32)
+        nm = C.c_int(0)
+        check(lib().orbm_search_by_bow(len(keep[0]), _ptr(keep[0]), _ptr(keep[1]), _ptr(keep[2]),
+                                       _ptr(keep[3]), nf, _ptr(keep[4]), _ptr(keep[5]),
+                                       _ptr(keep[6]), float(self.nnratio), int(self.checkOri),
+                                       _ptr(match), C.byref(nm)), "orbm_search_by_bow")
+        return match[:nf].copy(), nm.value
 
     def SearchByProjectionLocalMap(self, camera, scale_factors, cur, track, mp_desc, mp_nobs,
                                    cur_nobs, th):

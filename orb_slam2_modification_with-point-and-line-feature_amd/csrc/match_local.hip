@@ -304,4 +304,144 @@ void launch_match_local(const TrackConsts& c, const LocalArgs& a, hipStream_t s)
   hipLaunchKernelGGL(k_match_local, dim3(1), dim3(256), sizeof(LocalShared), s, c, a);
 }
 
+
+// ---------------------------------------------------------------------------
+// ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&)
+// (ORBmatcher.cc:247-410). Features sharing a vocabulary node are compared
+// only with each other and a frame feature is claimed only by keyframe
+// features of its own node, so nodes are independent: both feature lists are
+// sorted by (node, index) in LDS (bitonic), every common node is walked by
+// one thread in the reference's order, then the rotation histogram.
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int kBowMax = 2048;
+__device__ void bitonic_sort(uint32_t* a, int n) {
+  for (int k = 2; k <= n; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int l = i ^ j;
+        if (l > i) {
+          const uint32_t x = a[i], y = a[l];
+          if (((i & k) == 0) ? (x > y) : (x < y)) {
+            a[i] = y;
+            a[l] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+}
+}  // namespace
+
+__global__ void __launch_bounds__(256) k_match_bow(BowArgs a) {
+  __shared__ uint32_t skf[kBowMax], sf[kBowMax];
+  __shared__ int smatch[kBowMax];
+  __shared__ int sbin[kBowMax];
+  __shared__ int hist[32];
+  __shared__ int s_n, s_ind[3];
+  const int t = threadIdx.x;
+  const int nkf = min(a.nkf, kBowMax), nf = min(a.nf, kBowMax);
+  // key = node << 11 | index; features without a node sort last
+  for (int i = t; i < kBowMax; i += 256) {
+    skf[i] = (i < nkf && a.kf_node[i] >= 0) ? ((uint32_t)a.kf_node[i] << 11) | (uint32_t)i : 0xFFFFFFFFu;
+    sf[i] = (i < nf && a.f_node[i] >= 0) ? ((uint32_t)a.f_node[i] << 11) | (uint32_t)i : 0xFFFFFFFFu;
+    smatch[i] = -1;
+    sbin[i] = -1;
+  }
+  if (t < 32) hist[t] = 0;
+  if (t == 0) s_n = 0;
+  __syncthreads();
+  bitonic_sort(skf, kBowMax);
+  bitonic_sort(sf, kBowMax);
+  // one thread per keyframe node (first position of each node run)
+  int nm = 0;
+  for (int p = t; p < kBowMax; p += 256) {
+    const uint32_t key = skf[p];
+    if (key == 0xFFFFFFFFu) continue;
+    const uint32_t node = key >> 11;
+    if (p > 0 && (skf[p - 1] >> 11) == node && skf[p - 1] != 0xFFFFFFFFu) continue;
+    // frame run of the same node
+    // node ids are < 2^21 - 1, so the 0xFFFFFFFF sentinels sort above every node
+    int lo = 0, hi = kBowMax;
+    while (lo < hi) {
+      const int m = (lo + hi) >> 1;
+      if ((sf[m] >> 11) < node) lo = m + 1;
+      else hi = m;
+    }
+    int fe = lo;
+    while (fe < kBowMax && sf[fe] != 0xFFFFFFFFu && (sf[fe] >> 11) == node) fe++;
+    const int fb = lo;
+    if (fb == fe) continue;
+    for (int q = p; q < kBowMax && skf[q] != 0xFFFFFFFFu && (skf[q] >> 11) == node; q++) {
+      const int iKF = (int)(skf[q] & 0x7FF);
+      if (!a.kf_valid[iKF]) continue;
+      int bestDist1 = 256, bestIdxF = -1, bestDist2 = 256;
+      for (int r = fb; r < fe; r++) {
+        const int iF = (int)(sf[r] & 0x7FF);
+        if (smatch[iF] >= 0) continue;
+        const int dist = hamming32l(a.kf_desc + (long long)iKF * 32, a.f_desc + (long long)iF * 32);
+        if (dist < bestDist1) {
+          bestDist2 = bestDist1;
+          bestDist1 = dist;
+          bestIdxF = iF;
+        } else if (dist < bestDist2) {
+          bestDist2 = dist;
+        }
+      }
+      if (bestDist1 <= 50 && static_cast<float>(bestDist1) < a.nnratio * static_cast<float>(bestDist2)) {
+        smatch[bestIdxF] = iKF;
+        if (a.check_ori) {
+          float rot = a.kf_angle[iKF] - a.f_angle[bestIdxF];
+          if (rot < 0.0f) rot += 360.0f;
+          int bin = (int)roundf(rot * (30 / 360.0f));
+          if (bin == 30) bin = 0;
+          sbin[bestIdxF] = bin;
+          atomicAdd(&hist[bin], 1);
+        }
+        nm++;
+      }
+    }
+  }
+  if (nm) atomicAdd(&s_n, nm);
+  __syncthreads();
+  if (a.check_ori) {
+    if (t == 0) {
+      int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+      for (int i = 0; i < 30; i++) {
+        const int sz = hist[i];
+        if (sz > max1) {
+          max3 = max2; max2 = max1; max1 = sz; ind3 = ind2; ind2 = ind1; ind1 = i;
+        } else if (sz > max2) {
+          max3 = max2; max2 = sz; ind3 = ind2; ind2 = i;
+        } else if (sz > max3) {
+          max3 = sz; ind3 = i;
+        }
+      }
+      if (max2 < 0.1f * (float)max1) {
+        ind2 = -1; ind3 = -1;
+      } else if (max3 < 0.1f * (float)max1) {
+        ind3 = -1;
+      }
+      s_ind[0] = ind1; s_ind[1] = ind2; s_ind[2] = ind3;
+    }
+    __syncthreads();
+    int rem = 0;
+    for (int j = t; j < nf; j += 256) {
+      const int b = sbin[j];
+      if (b >= 0 && b != s_ind[0] && b != s_ind[1] && b != s_ind[2]) {
+        smatch[j] = -1;
+        rem++;
+      }
+    }
+    if (rem) atomicSub(&s_n, rem);
+    __syncthreads();
+  }
+  for (int j = t; j < nf; j += 256) a.match[j] = smatch[j];
+  if (t == 0) *a.nmatches = s_n;
+}
+
+void launch_match_bow(const BowArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_match_bow, dim3(1), dim3(256), 0, s, a);
+}
+
 }  // namespace orbpl

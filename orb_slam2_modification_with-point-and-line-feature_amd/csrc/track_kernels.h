@@ -159,6 +159,24 @@ struct LocalArgs {
   int4* scratch;           // nmp entries
 };
 
+// ORBmatcher::SearchByBoW(KeyFrame*, Frame&) with per-feature node ids.
+struct BowArgs {
+  int nkf;
+  const int* kf_node;
+  const uint8_t* kf_valid;
+  const uint8_t* kf_desc;
+  const float* kf_angle;
+  int nf;
+  const int* f_node;
+  const uint8_t* f_desc;
+  const float* f_angle;
+  float nnratio;
+  int check_ori;
+  int* match;
+  int* nmatches;
+};
+void launch_match_bow(const BowArgs& a, hipStream_t s);
+
 void launch_in_frustum(const TrackConsts& c, float log_scale, const InFrustumArgs& a,
                        hipStream_t s);
 void launch_match_local(const TrackConsts& c, const LocalArgs& a, hipStream_t s);

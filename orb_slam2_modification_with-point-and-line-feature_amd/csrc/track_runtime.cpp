@@ -511,6 +511,51 @@ int orbl_search_by_projection_last(const orbpl_camera* cam, const float* Tcw, in
   return ORBPL_OK;
 }
 
+int orbm_search_by_bow(int nkf, const int32_t* kf_node, const uint8_t* kf_valid,
+                       const uint8_t* kf_desc, const float* kf_angle, int nf, const int32_t* f_node,
+                       const uint8_t* f_desc, const float* f_angle, float nnratio, int check_ori,
+                       int32_t* match, int* nmatches) {
+  if (nkf < 0 || nf < 0 || !nmatches) return arg_fail("bad argument");
+  if (nkf > 2048 || nf > 2048) return arg_fail("more than 2048 features");
+  if ((nkf > 0 && (!kf_node || !kf_valid || !kf_desc || !kf_angle)) ||
+      (nf > 0 && (!f_node || !f_desc || !f_angle || !match)))
+    return arg_fail("NULL feature arrays");
+  for (int i = 0; i < nkf; i++)
+    if (kf_node[i] >= (1 << 21) - 1) return arg_fail("vocabulary node id >= 2^21 - 1");
+  for (int i = 0; i < nf; i++)
+    if (f_node[i] >= (1 << 21) - 1) return arg_fail("vocabulary node id >= 2^21 - 1");
+  const size_t K = std::max(1, nkf), F = std::max(1, nf);
+  DBuf dkn, dkv, dkd, dka, dfn, dfd, dfa, dm, dnm;
+  HIP_CHECK(dkn.alloc(K * 4));
+  HIP_CHECK(dkv.alloc(K));
+  HIP_CHECK(dkd.alloc(K * 32));
+  HIP_CHECK(dka.alloc(K * 4));
+  HIP_CHECK(dfn.alloc(F * 4));
+  HIP_CHECK(dfd.alloc(F * 32));
+  HIP_CHECK(dfa.alloc(F * 4));
+  HIP_CHECK(dm.alloc(F * 4));
+  HIP_CHECK(dnm.alloc(4));
+  if (nkf) {
+    HIP_CHECK(hipMemcpy(dkn.p, kf_node, K * 4, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dkv.p, kf_valid, K, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dkd.p, kf_desc, K * 32, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dka.p, kf_angle, K * 4, hipMemcpyHostToDevice));
+  }
+  if (nf) {
+    HIP_CHECK(hipMemcpy(dfn.p, f_node, F * 4, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dfd.p, f_desc, F * 32, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dfa.p, f_angle, F * 4, hipMemcpyHostToDevice));
+  }
+  BowArgs a{nkf, dkn.as<int>(), dkv.as<uint8_t>(), dkd.as<uint8_t>(), dka.as<float>(), nf,
+            dfn.as<int>(), dfd.as<uint8_t>(), dfa.as<float>(), nnratio, check_ori,
+            dm.as<int>(), dnm.as<int>()};
+  launch_match_bow(a, scratch_stream());
+  HIP_CHECK(hipGetLastError());
+  if (nf) HIP_CHECK(hipMemcpy(match, dm.p, F * 4, hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(nmatches, dnm.p, 4, hipMemcpyDeviceToHost));
+  return ORBPL_OK;
+}
+
 int orbl_frame_is_in_frustum(const float* Tcw, int n, const float* xyz6, uint8_t* in_view) {
   if (!Tcw || n < 0 || (n > 0 && (!xyz6 || !in_view))) return arg_fail("bad argument");
   if (n == 0) return ORBPL_OK;

@@ -142,3 +142,24 @@ def line_map_problem(seed=0, cam_name="TUM1", claim_frac=0.15):
     cur_nobs = np.where(rng.random(len(ku)) < claim_frac, 1, 0).astype(np.int32)
     T2 = np.linalg.inv(traj[2]).astype(np.float32)
     return (cfg, cam, np.array(xyz, np.float32), np.array(desc, np.uint8), ku, ld, cur_nobs, T2)
+
+
+def bow_problem(seed=0, bits=12):
+    """Keyframe = frame 0, frame = frame 1 of a seeded sequence, with a
+    stand-in vocabulary: a feature's node is the top `bits` bits of its
+    descriptor (similar descriptors share nodes, as DBoW2 words do; the
+    reference's ORBvoc.txt is not available). ~5 % of the features get no
+    node, ~10 % of the keyframe map points are invalid."""
+    O = load_oracle()
+    cfg, traj, frames = sequence(2, seed)
+    p = O.params()
+    k0, d0, _ = O.extract(p, frames[0][0])
+    k1, d1, _ = O.extract(p, frames[1][0])
+    rng = np.random.default_rng(seed + 5)
+
+    def nodes(d):
+        v = (d[:, 0].astype(np.int64) << 8 | d[:, 1].astype(np.int64)) >> (16 - bits)
+        return np.where(rng.random(len(d)) < 0.05, -1, v).astype(np.int32)
+
+    return dict(kf_node=nodes(d0), kf_valid=(rng.random(len(d0)) > 0.1).astype(np.uint8),
+                kf_desc=d0, kf_angle=k0["angle"], f_node=nodes(d1), f_desc=d1, f_angle=k1["angle"])

@@ -371,3 +371,14 @@ def test_line_search_by_projection_list_bit_exact(orbpl, oracle, case):
         assert w_o
     else:
         assert n_o > 20 and not w_o
+
+
+@pytest.mark.parametrize("bits,nnratio,ori", [(12, 0.7, True), (8, 0.75, True), (16, 0.7, False),
+                                              (6, 0.9, True)])
+def test_search_by_bow_bit_exact(orbpl, oracle, bits, nnratio, ori):
+    from _scenes import bow_problem
+    b = bow_problem(2, bits)
+    m_o, n_o = oracle.search_by_bow(**b, nnratio=nnratio, check_ori=ori)
+    m_g, n_g = orbpl.ORBmatcher(nnratio, ori).SearchByBoW(**b)
+    assert n_g == n_o and n_o > 20
+    assert np.array_equal(m_g, m_o)

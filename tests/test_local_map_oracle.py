@@ -36,3 +36,18 @@ def test_local_map_matches_are_geometric(oracle):
     dx = cur["kps_un"]["x"][j] - tr["proj_x"][m[j]]
     dy = cur["kps_un"]["y"][j] - tr["proj_y"][m[j]]
     assert np.median(np.hypot(dx, dy)) < 3.0
+
+
+def test_search_by_bow_oracle_properties(oracle):
+    from _scenes import bow_problem
+    b = bow_problem(1)
+    m, n = oracle.search_by_bow(**b)
+    j = np.nonzero(m >= 0)[0]
+    assert n == len(j) > 50
+    # matched pairs share a node, have a valid keyframe map point and pass TH_LOW
+    assert np.all(b["kf_node"][m[j]] == b["f_node"][j])
+    assert np.all(b["kf_valid"][m[j]] == 1)
+    d = np.unpackbits(b["kf_desc"][m[j]] ^ b["f_desc"][j], axis=1).sum(1)
+    assert d.max() <= 50
+    # a keyframe feature is used at most once per node walk
+    assert len(np.unique(m[j])) == len(j)
