@@ -198,6 +198,16 @@ int orbm_search_by_projection_last(const orbpl_camera* cam, const float* scale_f
                                    const orbpl_match_last* last, float th, int mono,
                                    int check_orientation, int32_t* match, int* nmatches);
 
+/* Frame::ComputeStereoMatches (Frame.cc:886-1063) for a stereo pair whose
+ * left / right images were extracted by `left` / `right` (batch frame
+ * `frame`; their pyramids are the reference's mvImagePyramid): uRight and
+ * depth per left keypoint (-1: none). kl / kr = mvKeys / mvKeysRight as
+ * returned by orbx_extract. n, nr <= 4096, image height <= 1024. */
+int orbpl_stereo_matches(const orbpl_camera* cam, orbx_ctx* left, orbx_ctx* right, int frame,
+                         const orbpl_keypoint* kl, const uint8_t* dl, int n,
+                         const orbpl_keypoint* kr, const uint8_t* dr, int nr, float* uright,
+                         float* depth);
+
 /* ------------------------------------------------------------------------
  * Tracking::SearchLocalPoints pieces (TrackLocalMap)
  * ---------------------------------------------------------------------- */

@@ -163,6 +163,8 @@ def _setup_track(L):
     L.oracle_frame_prepare.argtypes = [vp, vp, i, vp, vp, vp, vp, vp, vp]
     L.oracle_search_by_projection_last.argtypes = [vp, vp, i, vp, vp, C.c_float, i, i, vp, ip]
     L.oracle_pose_optimization.argtypes = [vp, vp, vp, vp, vp, ip]
+    L.oracle_stereo_matches.argtypes = [vp, vp, vp, i, vp, vp, vp, vp, vp, vp, i, vp, vp, i, vp,
+                                        vp]
     L.oracle_search_by_bow.argtypes = [i, vp, vp, vp, vp, i, vp, vp, vp, C.c_float, i, vp, ip]
     L.oracle_frame_is_in_frustum.argtypes = [vp, C.c_float, i, vp, i, vp, vp, vp, vp, C.c_float,
                                              vp, vp, vp, vp, vp, vp]
@@ -272,6 +274,30 @@ def search_by_bow(kf_node, kf_valid, kf_desc, kf_angle, f_node, f_desc, f_angle,
                                nf, _p(keep[4]), _p(keep[5]), _p(keep[6]), C.c_float(nnratio),
                                int(check_ori), _p(match), C.byref(nm))
     return match[:nf].copy(), nm.value
+
+
+def stereo_matches(cam, p, left, right, kl, dl, kr, dr):
+    """Frame::ComputeStereoMatches on the oracle's own pyramids of the pair."""
+    left = np.ascontiguousarray(left, np.uint8)
+    right = np.ascontiguousarray(right, np.uint8)
+    h, w = left.shape
+    lw, lh, _, sc, isc = level_sizes(p, w, h)
+    pl = np.concatenate([x.reshape(-1) for x in pyramid(p, left)])
+    pr = np.concatenate([x.reshape(-1) for x in pyramid(p, right)])
+    kl = _c(kl, KP_DTYPE)
+    kr = _c(kr, KP_DTYPE)
+    dl = _c(dl, np.uint8)
+    dr = _c(dr, np.uint8)
+    ur = np.zeros(max(1, len(kl)), np.float32)
+    dp = np.zeros(max(1, len(kl)), np.float32)
+    lw = _c(lw, np.int32)
+    lh = _c(lh, np.int32)
+    sc = _c(sc, np.float32)
+    isc = _c(isc, np.float32)
+    lib().oracle_stereo_matches(C.byref(cam), _p(sc), _p(isc), len(sc), _p(lw), _p(lh), _p(pl),
+                                _p(pr), _p(kl), _p(dl), len(kl), _p(kr), _p(dr), len(kr), _p(ur),
+                                _p(dp))
+    return ur[:len(kl)].copy(), dp[:len(kl)].copy()
 
 
 def pose_optimization(cam, prob, Tcw, outlier, line_outlier=None):

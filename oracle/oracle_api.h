@@ -39,6 +39,11 @@ int oracle_search_by_bow(int nkf, const int32_t* kf_node, const uint8_t* kf_vali
                          const uint8_t* kf_desc, const float* kf_angle, int nf,
                          const int32_t* f_node, const uint8_t* f_desc, const float* f_angle,
                          float nnratio, int check_ori, int32_t* match, int* nmatches_out);
+int oracle_stereo_matches(const orbpl_camera* cam, const float* scale, const float* inv_scale,
+                          int nlevels, const int32_t* lw, const int32_t* lh, const uint8_t* pyrL,
+                          const uint8_t* pyrR, const orbpl_keypoint* kl, const uint8_t* dl, int n,
+                          const orbpl_keypoint* kr, const uint8_t* dr, int nr, float* uright,
+                          float* depth);
 int oracle_pose_optimization(const orbpl_camera* cam, const orbpl_pose_problem* P, float* Tcw,
                              uint8_t* outlier, uint8_t* line_outlier, int* n_inliers);
 void* oracle_vo_create(const orbpl_orb_params* orb, const orbpl_camera* cam, int n_streams);

@@ -24,6 +24,7 @@
 // parity unpinned against the real reference binary (no fixtures exist).
 // ============================================================================
 #include <algorithm>
+#include <climits>
 #include <map>
 #include <cfloat>
 #include <cmath>
@@ -1160,6 +1161,128 @@ int oracle_search_by_bow(int nkf, const int32_t* kf_node, const uint8_t* kf_vali
     }
   }
   *nmatches_out = nmatches;
+  return 0;
+}
+
+// Frame::ComputeStereoMatches (Frame.cc:886-1063): ORB descriptor search
+// along the right image's row bands, SAD refinement on the pyramid level
+// (11x11 window, +-5 columns), parabolic sub-pixel fit, median-based
+// outlier rejection. Pyramids are the padded levels of oracle_orb_pyramid
+// ((w+38)x(h+38), content at (19, 19)). The SAD of integer-valued float
+// windows is exact in any summation order, so it is computed in integers.
+int oracle_stereo_matches(const orbpl_camera* cam, const float* scale, const float* inv_scale,
+                          int nlevels, const int32_t* lw, const int32_t* lh, const uint8_t* pyrL,
+                          const uint8_t* pyrR, const orbpl_keypoint* kl, const uint8_t* dl, int n,
+                          const orbpl_keypoint* kr, const uint8_t* dr, int nr, float* uright,
+                          float* depth) {
+  const int TH_HIGH = 100, TH_LOW = 50;
+  std::vector<size_t> loff(nlevels);
+  size_t off = 0;
+  for (int l = 0; l < nlevels; l++) {
+    loff[l] = off;
+    off += (size_t)(lw[l] + 38) * (lh[l] + 38);
+  }
+  auto pix = [&](const uint8_t* pyr, int l, int x, int y) -> int {
+    return pyr[loff[l] + (size_t)(y + 19) * (lw[l] + 38) + x + 19];
+  };
+  for (int i = 0; i < n; i++) uright[i] = depth[i] = -1.0f;
+  const int thOrbDist = (TH_HIGH + TH_LOW) / 2;
+  const int nRows = lh[0];
+  std::vector<std::vector<int>> rows(nRows);
+  for (int iR = 0; iR < nr; iR++) {
+    const float kpY = kr[iR].y;
+    const float r = 2.0f * scale[kr[iR].octave];
+    const int maxr = (int)std::ceil(kpY + r);
+    const int minr = (int)std::floor(kpY - r);
+    for (int yi = minr; yi <= maxr; yi++)
+      if (yi >= 0 && yi < nRows) rows[yi].push_back(iR);
+  }
+  const float mb = cam->bf / cam->fx, mbf = cam->bf;
+  const float minZ = mb, minD = 0, maxD = mbf / minZ;
+  std::vector<std::pair<int, int>> vDistIdx;
+  for (int iL = 0; iL < n; iL++) {
+    const orbpl_keypoint& kpL = kl[iL];
+    const int levelL = kpL.octave;
+    const float vL = kpL.y, uL = kpL.x;
+    const int row = (int)vL;
+    if (row < 0 || row >= nRows || rows[row].empty()) continue;
+    const float minU = uL - maxD, maxU = uL - minD;
+    if (maxU < 0) continue;
+    int bestDist = TH_HIGH;
+    int bestIdxR = 0;
+    for (int iR : rows[row]) {
+      const orbpl_keypoint& kpR = kr[iR];
+      if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
+      const float uR = kpR.x;
+      if (uR >= minU && uR <= maxU) {
+        const int dist = desc_dist(dl + 32 * iL, dr + 32 * iR);
+        if (dist < bestDist) {
+          bestDist = dist;
+          bestIdxR = iR;
+        }
+      }
+    }
+    if (bestDist >= thOrbDist) continue;
+    const float uR0 = kr[bestIdxR].x;
+    const float scaleFactor = inv_scale[kpL.octave];
+    const float scaleduL = std::round(kpL.x * scaleFactor);
+    const float scaledvL = std::round(kpL.y * scaleFactor);
+    const float scaleduR0 = std::round(uR0 * scaleFactor);
+    const int w = 5, L = 5;
+    const int l = kpL.octave;
+    const int cuL = (int)scaleduL, cvL = (int)scaledvL, cuR = (int)scaleduR0;
+    const float iniu = scaleduR0 + L - w;
+    const float endu = scaleduR0 + L + w + 1;
+    if (iniu < 0 || endu >= lw[l]) continue;
+    // windows outside the level (the reference's ROI would assert) are skipped
+    if (cvL - w < 0 || cvL + w >= lh[l] || cuL - w < 0 || cuL + w >= lw[l] || cuR - L - w < 0)
+      continue;
+    const int cL = pix(pyrL, l, cuL, cvL);
+    int bestD = INT_MAX, bestincR = 0;
+    float vDists[2 * 5 + 1];
+    for (int incR = -L; incR <= L; incR++) {
+      const int cR = pix(pyrR, l, cuR + incR, cvL);
+      int sad = 0;
+      for (int yy = -w; yy <= w; yy++)
+        for (int xx = -w; xx <= w; xx++) {
+          const int a = pix(pyrL, l, cuL + xx, cvL + yy) - cL;
+          const int b = pix(pyrR, l, cuR + incR + xx, cvL + yy) - cR;
+          sad += std::abs(a - b);
+        }
+      const float dist = (float)sad;
+      if (dist < bestD) {
+        bestD = (int)dist;
+        bestincR = incR;
+      }
+      vDists[L + incR] = dist;
+    }
+    if (bestincR == -L || bestincR == L) continue;
+    const float dist1 = vDists[L + bestincR - 1];
+    const float dist2 = vDists[L + bestincR];
+    const float dist3 = vDists[L + bestincR + 1];
+    const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
+    if (deltaR < -1 || deltaR > 1) continue;
+    float bestuR = scale[kpL.octave] * ((float)scaleduR0 + (float)bestincR + deltaR);
+    float disparity = (uL - bestuR);
+    if (disparity >= minD && disparity < maxD) {
+      if (disparity <= 0) {
+        disparity = 0.01;
+        bestuR = uL - 0.01;
+      }
+      depth[iL] = mbf / disparity;
+      uright[iL] = bestuR;
+      vDistIdx.push_back(std::make_pair(bestD, iL));
+    }
+  }
+  if (vDistIdx.empty()) return 0;
+  std::sort(vDistIdx.begin(), vDistIdx.end());
+  const float median = vDistIdx[vDistIdx.size() / 2].first;
+  const float thDist = 1.5f * 1.4f * median;
+  for (int i = (int)vDistIdx.size() - 1; i >= 0; i--) {
+    if (vDistIdx[i].first < thDist) break;
+    uright[vDistIdx[i].second] = -1;
+    depth[vDistIdx[i].second] = -1;
+  }
   return 0;
 }
 

@@ -342,6 +342,7 @@ def _declare_track(L):
     L.orbpl_tracker_create_ex.argtypes = [vp, vp, i, i, i, C.POINTER(vp)]
     L.orbpl_line_frame_prepare.argtypes = [vp, vp, i, vp, vp, vp, vp, vp, vp]
     L.orbl_frame_is_in_frustum.argtypes = [vp, i, vp, vp]
+    L.orbpl_stereo_matches.argtypes = [vp, vp, vp, i, vp, vp, i, vp, vp, i, vp, vp]
     L.orbm_search_by_bow.argtypes = [i, vp, vp, vp, vp, i, vp, vp, vp, C.c_float, i, vp, ip]
     L.orbl_search_by_projection_list.argtypes = [vp, vp, i, vp, vp, vp, i, vp, vp, vp, vp, ip, ip]
     L.orbpl_frame_is_in_frustum.argtypes = [vp, C.c_float, i, vp, i, vp, vp, vp, vp, C.c_float,
@@ -457,6 +458,21 @@ class ORBmatcher:
             None if cur_nobs is None else arr(cur_nobs, np.int32), float(th), float(self.nnratio),
             _ptr(match), C.byref(nm)), "orbm_search_by_projection_local")
         return match[:n].copy(), nm.value
+
+
+def stereo_matches(camera, left, right, kl, dl, kr, dr, frame=0):
+    """Frame::ComputeStereoMatches with the pyramids of two ORBextractor
+    objects (left / right) that extracted the pair: (uright, depth)."""
+    kl = _c(kl, KP_DTYPE)
+    kr = _c(kr, KP_DTYPE)
+    dl = _c(dl, np.uint8)
+    dr = _c(dr, np.uint8)
+    ur = np.zeros(max(1, len(kl)), np.float32)
+    dp = np.zeros(max(1, len(kl)), np.float32)
+    check(lib().orbpl_stereo_matches(C.byref(camera), left._h, right._h, frame, _ptr(kl), _ptr(dl),
+                                     len(kl), _ptr(kr), _ptr(dr), len(kr), _ptr(ur), _ptr(dp)),
+          "orbpl_stereo_matches")
+    return ur[:len(kl)].copy(), dp[:len(kl)].copy()
 
 
 def frame_is_in_frustum(camera, scale_factor, nlevels, Tcw, mps, view_cos_limit=0.5):

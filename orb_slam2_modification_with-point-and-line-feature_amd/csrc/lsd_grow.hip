@@ -1054,7 +1054,6 @@ __global__ void __launch_bounds__(64) k_lsd_grow(LsdGeom g, LsdScratch sc) {
   for (int i = lane; i < used_words; i += 64) F.used[i] = 0;
   __builtin_amdgcn_wave_barrier();
   const uint32_t* A = sc.A + (long long)f * g.n;
-  float* out = sc.lines + (long long)f * kLsdMaxLines * 4;
   const int w1 = sw - 1;
   const double prec = g.prec, p = g.p;
   int nl = 0;

@@ -369,6 +369,21 @@ int orbx_extract_batch_device(orbx_ctx* c, const uint8_t* d_imgs, int batch, int
                   reinterpret_cast<orbpl_keypoint_dev*>(d_kps), d_desc, kp_pitch, d_n);
 }
 
+}  // extern "C"
+
+namespace orbpl {
+// Device view of a context's padded pyramid of batch frame `frame` (internal).
+int orbx_device_pyramid(orbx_ctx* c, int frame, const uint8_t** base, const OrbGeom** geom,
+                        hipStream_t* stream) {
+  if (!c || frame < 0 || frame >= c->max_batch) return arg_fail("bad argument");
+  *base = c->d_pyr + (size_t)frame * c->hg.g.pyr_bytes;
+  *geom = &c->hg.g;
+  *stream = c->stream;
+  return ORBPL_OK;
+}
+}  // namespace orbpl
+
+extern "C" {
 int orbx_get_pyramid(orbx_ctx* c, int frame, int level, int padded, int blurred, uint8_t* out,
                      int out_cap, int* w, int* h) {
   if (!c) return arg_fail("NULL ctx");

@@ -13,4 +13,7 @@ int orbx_run(orbx_ctx* c, const uint8_t* d_imgs, int batch, int stride, long lon
              orbpl_keypoint_dev* d_kps, uint8_t* d_desc, int kp_pitch, int* d_n,
              hipEvent_t* ext_events = nullptr);
 hipStream_t orbx_stream(orbx_ctx* c);
+struct OrbGeom;
+int orbx_device_pyramid(orbx_ctx* c, int frame, const uint8_t** base, const OrbGeom** geom,
+                        hipStream_t* stream);
 }  // namespace orbpl

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "orb_geom.h"
 #include "track_common.h"
 #include "../../include/orbpl.h"
 
@@ -176,6 +177,30 @@ struct BowArgs {
   int* nmatches;
 };
 void launch_match_bow(const BowArgs& a, hipStream_t s);
+
+// Frame::ComputeStereoMatches (stereo.hip).
+struct StereoArgs {
+  int n;
+  const KeyPointD* kl;           // left mvKeys
+  const uint8_t* dl;
+  int nr;
+  const KeyPointD* kr;           // right mvKeysRight
+  const uint8_t* dr;
+  const uint8_t* pyrL;           // one frame's padded pyramids (orbx layout)
+  const uint8_t* pyrR;
+  LevelGeom lv[8];
+  float scale[8];
+  float inv_scale[8];
+  int nrows;
+  float mb, mbf;
+  float* uright;                 // mvuRight (-1: none)
+  float* depth;                  // mvDepth
+  int* sad;                      // scratch n
+  uint16_t* entries;             // scratch: row band entries
+  int entry_cap;
+  int* err;
+};
+void launch_stereo(const StereoArgs& a, hipStream_t s);
 
 void launch_in_frustum(const TrackConsts& c, float log_scale, const InFrustumArgs& a,
                        hipStream_t s);

@@ -556,6 +556,78 @@ int orbm_search_by_bow(int nkf, const int32_t* kf_node, const uint8_t* kf_valid,
   return ORBPL_OK;
 }
 
+int orbpl_stereo_matches(const orbpl_camera* cam, orbx_ctx* left, orbx_ctx* right, int frame,
+                         const orbpl_keypoint* kl, const uint8_t* dl, int n,
+                         const orbpl_keypoint* kr, const uint8_t* dr, int nr, float* uright,
+                         float* depth) {
+  if (!cam || !left || !right || n < 0 || nr < 0) return arg_fail("bad argument");
+  if (n > 4096 || nr > 4096) return arg_fail("more than 4096 keypoints");
+  if ((n > 0 && (!kl || !dl || !uright || !depth)) || (nr > 0 && (!kr || !dr)))
+    return arg_fail("NULL keypoint arrays");
+  const uint8_t *pl = nullptr, *pr = nullptr;
+  const OrbGeom *gl = nullptr, *gr = nullptr;
+  hipStream_t sl, sr;
+  int rc = orbx_device_pyramid(left, frame, &pl, &gl, &sl);
+  if (rc) return rc;
+  rc = orbx_device_pyramid(right, frame, &pr, &gr, &sr);
+  if (rc) return rc;
+  if (gl->nlevels != gr->nlevels || gl->W != gr->W || gl->H != gr->H || gl->nlevels > 8)
+    return arg_fail("left and right extractors differ");
+  if (gl->H > 1024) return arg_fail("image taller than 1024 rows");
+  if (n == 0) return ORBPL_OK;
+  HIP_CHECK(hipStreamSynchronize(sl));
+  HIP_CHECK(hipStreamSynchronize(sr));
+  const int cap = std::max(1, nr) * 20;
+  DBuf dkl, ddl, dkr, ddr, dur, ddp, dsad, dent, derr;
+  HIP_CHECK(dkl.alloc((size_t)n * sizeof(KeyPointD)));
+  HIP_CHECK(ddl.alloc((size_t)n * 32));
+  HIP_CHECK(dkr.alloc((size_t)std::max(1, nr) * sizeof(KeyPointD)));
+  HIP_CHECK(ddr.alloc((size_t)std::max(1, nr) * 32));
+  HIP_CHECK(dur.alloc((size_t)n * 4));
+  HIP_CHECK(ddp.alloc((size_t)n * 4));
+  HIP_CHECK(dsad.alloc((size_t)n * 4));
+  HIP_CHECK(dent.alloc((size_t)cap * 2));
+  HIP_CHECK(derr.alloc(4));
+  HIP_CHECK(hipMemset(derr.p, 0, 4));
+  HIP_CHECK(hipMemcpy(dkl.p, kl, (size_t)n * sizeof(KeyPointD), hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(ddl.p, dl, (size_t)n * 32, hipMemcpyHostToDevice));
+  if (nr) {
+    HIP_CHECK(hipMemcpy(dkr.p, kr, (size_t)nr * sizeof(KeyPointD), hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(ddr.p, dr, (size_t)nr * 32, hipMemcpyHostToDevice));
+  }
+  StereoArgs a{};
+  a.n = n;
+  a.kl = dkl.as<KeyPointD>();
+  a.dl = ddl.as<uint8_t>();
+  a.nr = nr;
+  a.kr = dkr.as<KeyPointD>();
+  a.dr = ddr.as<uint8_t>();
+  a.pyrL = pl;
+  a.pyrR = pr;
+  for (int l = 0; l < gl->nlevels; l++) {
+    a.lv[l] = gl->lv[l];
+    a.scale[l] = gl->lv[l].scale;
+    a.inv_scale[l] = 1.0f / gl->lv[l].scale;
+  }
+  a.nrows = gl->H;
+  a.mb = cam->bf / cam->fx;
+  a.mbf = cam->bf;
+  a.uright = dur.as<float>();
+  a.depth = ddp.as<float>();
+  a.sad = dsad.as<int>();
+  a.entries = dent.as<uint16_t>();
+  a.entry_cap = cap;
+  a.err = derr.as<int>();
+  launch_stereo(a, scratch_stream());
+  HIP_CHECK(hipGetLastError());
+  int err = 0;
+  HIP_CHECK(hipMemcpy(&err, derr.p, 4, hipMemcpyDeviceToHost));
+  if (err) return (arg_fail("stereo row band capacity exceeded"), ORBPL_ERR_OVERFLOW);
+  HIP_CHECK(hipMemcpy(uright, dur.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(depth, ddp.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+  return ORBPL_OK;
+}
+
 int orbl_frame_is_in_frustum(const float* Tcw, int n, const float* xyz6, uint8_t* in_view) {
   if (!Tcw || n < 0 || (n > 0 && (!xyz6 || !in_view))) return arg_fail("bad argument");
   if (n == 0) return ORBPL_OK;

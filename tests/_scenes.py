@@ -163,3 +163,19 @@ def bow_problem(seed=0, bits=12):
 
     return dict(kf_node=nodes(d0), kf_valid=(rng.random(len(d0)) > 0.1).astype(np.uint8),
                 kf_desc=d0, kf_angle=k0["angle"], f_node=nodes(d1), f_desc=d1, f_angle=k1["angle"])
+
+
+@functools.lru_cache(maxsize=4)
+def stereo_pair(seed=0, cam_name="KITTI00"):
+    """A rectified stereo pair: the right camera sits mb = bf / fx metres
+    along the left camera's x axis (Frame.cc:62-63), same room and noise."""
+    load_pkg()
+    import orbpl.synth as synth
+    cfg = dict(getattr(synth, cam_name))
+    room = synth.default_room(seed)
+    Twc = synth.trajectory(1, seed=seed)[0]
+    shift = np.eye(4)
+    shift[0, 3] = cfg["bf"] / cfg["fx"]
+    left, _ = synth.render(cfg, Twc, room, seed=seed)
+    right, _ = synth.render(cfg, Twc @ shift, room, seed=seed)
+    return cfg, left, right

@@ -382,3 +382,25 @@ def test_search_by_bow_bit_exact(orbpl, oracle, bits, nnratio, ori):
     m_g, n_g = orbpl.ORBmatcher(nnratio, ori).SearchByBoW(**b)
     assert n_g == n_o and n_o > 20
     assert np.array_equal(m_g, m_o)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_stereo_matches_bit_exact(orbpl, oracle, seed):
+    """Frame::ComputeStereoMatches on the GPU pyramids of both extractors vs
+    the oracle on its own pyramids: uRight and depth bit-exact."""
+    from _scenes import stereo_pair
+    cfg, left, right = stereo_pair(seed)
+    W, H = cfg["width"], cfg["height"]
+    exl = orbpl.ORBextractor(2000, 1.2, 8, 20, 7, width=W, height=H)
+    exr = orbpl.ORBextractor(2000, 1.2, 8, 20, 7, width=W, height=H)
+    kl, dl = exl(left)
+    kr, dr = exr(right)
+    ur_g, d_g = orbpl.stereo_matches(orbpl.make_camera(cfg), exl, exr, kl, dl, kr, dr)
+    p = oracle.params(2000, 1.2, 8, 20, 7)
+    ur_o, d_o = oracle.stereo_matches(oracle.camera(cfg), p, left, right, kl, dl, kr, dr)
+    assert (d_o > 0).sum() > 0.3 * len(kl)
+    assert np.array_equal(_u32(ur_g), _u32(ur_o)), np.nonzero(_u32(ur_g) != _u32(ur_o))[0][:5]
+    assert np.array_equal(_u32(d_g), _u32(d_o))
+    # no right keypoints: nothing matches
+    ur0, d0 = orbpl.stereo_matches(orbpl.make_camera(cfg), exl, exr, kl, dl, kr[:0], dr[:0])
+    assert np.all(ur0 == -1) and np.all(d0 == -1)
