@@ -136,6 +136,67 @@ def cpu_baseline(seconds, threads, gray, depth, lines=False):
     return sum(counts) / dt, sum(counts), dt
 
 
+def accuracy_gpu(pkg, cam, lines, d_gray, d_depth, traj, A, F, local_rank):
+    """Untimed accuracy leg: A streams tracked over a whole loop of F frames
+    (stream s starts at loop frame s at its true pose); returns the (A, F, 4, 4)
+    Tcw poses after every step."""
+    tr = pkg.Tracker(pkg.OrbParams(*ORB), cam, A, device=local_rank, lines=lines)
+    tr.reset(np.stack([np.linalg.inv(traj[s % F]).astype(np.float32) for s in range(A)]).reshape(
+        A, 16))
+    out = np.zeros((A, F, 4, 4), np.float32)
+    for t in range(F):
+        tr.step_device(d_gray.ptr + t * W * H, d_depth.ptr + t * W * H * 4)
+        tr.synchronize()
+        out[:, t] = tr.state()["Tcw"]
+    tr.close()
+    return out
+
+
+def accuracy_ref(gray, depth, traj, A, lines):
+    """The oracle's VO loop (the reference restatement) over the same A x F
+    frames, one host thread per stream; returns its (A, F, 4, 4) poses."""
+    from _pkg import load_oracle
+    O = load_oracle()
+    import orbpl.synth as synth
+    cam = O.camera(synth.TUM3 if lines else synth.TUM1)
+    F = len(gray)
+    out = np.zeros((A, F, 4, 4), np.float32)
+
+    def worker(s):
+        vo = (O.LVO(O.params(*ORB), cam, 1, use_lines=True) if lines
+              else O.VO(O.params(*ORB), cam, 1))
+        vo.reset(np.linalg.inv(traj[s % F]).astype(np.float32).reshape(1, 16))
+        for t in range(F):
+            f = (s + t) % F
+            out[s, t] = vo.step(0, gray[f], depth[f])[0]
+
+    ths = [threading.Thread(target=worker, args=(s,)) for s in range(A)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    return out
+
+
+def ate_report(T_gpu, T_ref, traj):
+    """ATE RMSE (m) of the GPU poses vs the reference restatement's poses of
+    the same frames (raw: both start at the same pose) and of both vs the
+    ground truth (rigidly aligned, as TUM's evaluate_ate)."""
+    import orbpl.tum as tum
+    A, F = T_gpu.shape[:2]
+    gt = np.stack([np.linalg.inv(traj[(s + t) % F]) for s in range(A) for t in range(F)])
+    cg = tum.camera_centres(T_gpu.reshape(-1, 4, 4))
+    cgt = tum.camera_centres(gt)
+    rep = {"streams": A, "frames_per_stream": F,
+           "ate_rmse_vs_gt_m": round(tum.ate(cg, cgt)["rmse"], 6)}
+    if T_ref is not None:
+        cr = tum.camera_centres(T_ref.reshape(-1, 4, 4))
+        rep["ate_rmse_vs_ref_m"] = float(f"{tum.ate(cg, cr, aligned=False)['rmse']:.3e}")
+        rep["max_abs_pose_diff_vs_ref"] = float(f"{np.abs(T_gpu - T_ref).max():.3e}")
+        rep["ref_ate_rmse_vs_gt_m"] = round(tum.ate(cr, cgt)["rmse"], 6)
+    return rep
+
+
 def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, local_rank, dist):
     """Time `steps` tracker steps of one workload; returns the measurements."""
     lines = workload == "lines"
@@ -215,7 +276,11 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, loca
             "per_kernel_GBps": {k: round(ab[k] * S / (float(avg[idx[k]]) * 1e-3) / 1e9, 1)
                                 for k in names}}
     tr.close()
-    return dict(S=S, value=value, elapsed=elapsed, stages=stages, tracking=tracking, roof=roof,
+    A = min(args.ate_streams, S)
+    T_acc = (accuracy_gpu(pkg, cam, lines, d_gray, d_depth, traj, A, F, local_rank)
+             if A > 0 else None)
+    return dict(S=S, value=value, T_acc=T_acc, traj=traj, elapsed=elapsed, stages=stages,
+                tracking=tracking, roof=roof,
                 gray=gray, depth=depth,
                 workload=("TUM fr3_structure_texture_far-like RGB-D, ORB + LSD/LBD lines "
                           "(configs[2])" if lines else
@@ -241,6 +306,9 @@ def main():
                     help="steps of the configs[2] lines workload reported under 'secondary' "
                          "(points runs only; 0 = skip)")
     ap.add_argument("--lines-streams", type=int, default=1536)
+    ap.add_argument("--ate-streams", type=int, default=8,
+                    help="streams of the untimed accuracy leg (ATE vs ground truth and vs the "
+                         "reference restatement over one loop); 0 = skip")
     ap.add_argument("--pipelined", type=int, default=0,
                     help="1 = overlap extraction of step t+1 with tracking of step t")
     args = ap.parse_args()
@@ -270,6 +338,12 @@ def main():
         thr = args.cpu_threads or min(16, os.cpu_count() or 1)
         lines = args.workload == "lines"
         fps, nfr, dt = cpu_baseline(args.cpu_seconds, thr, res["gray"], res["depth"], lines)
+        if res["T_acc"] is not None:
+            res["T_ref"] = accuracy_ref(res["gray"], res["depth"], res["traj"],
+                                        len(res["T_acc"]), lines)
+        if sec is not None and sec["T_acc"] is not None:
+            sec["T_ref"] = accuracy_ref(sec["gray"], sec["depth"], sec["traj"],
+                                        len(sec["T_acc"]), True)
         cpu = {"value": round(fps, 2), "unit": "frames/s", "cores": thr, "kind": "port",
                "sample": f"{nfr} frames of the same 640x480 RGB-D loop in {dt:.1f} s, oracle/ "
                          f"C++ restatement ({'points+lines' if lines else 'points'}), "
@@ -278,7 +352,7 @@ def main():
     if rank == 0:
         S = res["S"]
         out = {
-            "metric": "frames/sec (extract+match+pose) at 640x480",
+            "metric": "frames/sec (extract+match+pose) at 640x480; ATE RMSE vs ref",
             "value": round(res["value"], 2),
             "unit": "frames/s",
             "n_gpus": world,
@@ -298,12 +372,17 @@ def main():
             "roofline": res["roof"],
             "cpu_baseline": cpu,
         }
+        if res["T_acc"] is not None:
+            out["accuracy"] = ate_report(res["T_acc"], res.get("T_ref"), res["traj"])
         if sec is not None:
             out["secondary"] = {
                 "workload": sec["workload"], "value": round(sec["value"], 2),
                 "unit": "frames/s", "steps": args.secondary_steps, "streams_per_gpu": sec["S"],
                 "ms_per_step": round(sec["elapsed"] / args.secondary_steps * 1e3, 3),
                 "stage_ms": sec["stages"], "tracking": sec["tracking"]}
+            if sec["T_acc"] is not None:
+                out["secondary"]["accuracy"] = ate_report(sec["T_acc"], sec.get("T_ref"),
+                                                          sec["traj"])
             if cpu is not None:
                 thr = cpu["cores"]
                 fps, nfr, dt = cpu_baseline(args.cpu_seconds / 2, thr, sec["gray"], sec["depth"],
