@@ -11,8 +11,11 @@ batch of `--streams` independent synthetic 640x480 RGB-D streams, all inputs
 resident in HBM before the timed region. The configs[2] workload (TUM3, ORB +
 LSD/LBD LineExtractor, LineMatcher::SearchByProjection, line edges in the
 pose) is timed the same way and reported under "secondary" (or as the
-headline with --workload lines). Frames are rendered from a seeded
-textured room along closed loop trajectories (no datasets on the box).
+headline with --workload lines), and so is configs[3] (KITTI 00 camera,
+1241x376 rectified stereo pairs, ORB 2000 on both images, ComputeStereoMatches,
+th = 7 matching, pose) under "stereo" (or --workload kitti). Frames are
+rendered from a seeded textured room along closed loop trajectories (no
+datasets on the box).
 
 Multi-GPU: one process per GPU (torchrun), streams sharded across ranks with
 no data-path collective (weak scaling); the gloo process group only carries the
@@ -38,41 +41,62 @@ W, H = 640, 480
 ORB = (1000, 1.2, 8, 20, 7)
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8 TB/s spec
 
+# BASELINE.json configs[1..3]: camera (orbpl.synth), ORB parameters, sensor
+WORKLOADS = {
+    "points": dict(cam="TUM1", orb=ORB, lines=False, stereo=False,
+                   desc="TUM fr1_desk-like RGB-D, ORB points only (configs[1])",
+                   data="synthetic (seeded textured-room RGB-D loop, TUM1 intrinsics+distortion)"),
+    "lines": dict(cam="TUM3", orb=ORB, lines=True, stereo=False,
+                  desc="TUM fr3_structure_texture_far-like RGB-D, ORB + LSD/LBD lines (configs[2])",
+                  data="synthetic (seeded textured-room RGB-D loop, TUM3 intrinsics, no distortion)"),
+    "kitti": dict(cam="KITTI00", orb=(2000, 1.2, 8, 20, 7), lines=False, stereo=True,
+                  desc="KITTI 00-like stereo 1241x376, ORB 2000 both images + ComputeStereoMatches "
+                       "+ PoseOptimization (configs[3]; the reference's stereo Frame has no lines)",
+                  data="synthetic (seeded textured-room rectified stereo loop, KITTI 00 intrinsics, "
+                       "bf 386.1448)"),
+}
+
 
 def _render(args):
-    i, n, seed, cam_name = args
+    i, n, seed, cam_name, stereo = args
     from _pkg import load_pkg
     load_pkg()
     import orbpl.synth as synth
     traj = synth.loop_trajectory(n, seed=seed)
     room = synth.default_room(seed)
-    g, d = synth.render(getattr(synth, cam_name), traj[i], room, seed=seed * 1000 + i)
+    cam = getattr(synth, cam_name)
+    g, d = synth.render(cam, traj[i], room, seed=seed * 1000 + i)
+    if stereo:  # right image of the rectified pair: camera at +mb along x
+        shift = np.eye(4)
+        shift[0, 3] = cam["bf"] / cam["fx"]
+        d, _ = synth.render(cam, traj[i] @ shift, room, seed=seed * 1000 + i)
     return g, d
 
 
-def render_loop(n, seed, workers, cam_name="TUM1"):
+def render_loop(n, seed, workers, cam_name="TUM1", stereo=False):
+    """(gray, depth) of an n-frame loop, or (left, right) for stereo."""
     with ProcessPoolExecutor(max_workers=workers) as ex:
-        out = list(ex.map(_render, [(i, n, seed, cam_name) for i in range(n)]))
+        out = list(ex.map(_render, [(i, n, seed, cam_name, stereo) for i in range(n)]))
     return np.stack([o[0] for o in out]), np.stack([o[1] for o in out])
 
 
-def level_areas():
+def level_areas(w=W, h=H, orb=ORB):
     from _pkg import load_pkg
-    d = load_pkg().describe(*ORB, width=W, height=H)
+    d = load_pkg().describe(*orb, width=w, height=h)
     return [int(a) * int(b) for a, b in zip(d["width"], d["height"])], d
 
 
-def algorithmic_bytes(n_kp):
+def algorithmic_bytes(n_kp, w=W, h=H, orb=ORB):
     """Per-frame algorithmic HBM bytes of each kernel:
     the bytes the kernel must move at minimum (each input read once, each
     output written once), with n_kp keypoints per frame."""
-    areas, d = level_areas()
+    areas, d = level_areas(w, h, orb)
     S = sum(areas)
     dims = list(zip((int(a) for a in d["width"]), (int(b) for b in d["height"])))
     pads = [(a + 38) * (b + 38) for a, b in dims]
     return {
         # read the input (level 0) or the previous level, write the padded level
-        "pyramid": W * H + sum(areas[:-1]) + sum(pads),
+        "pyramid": w * h + sum(areas[:-1]) + sum(pads),
         # read each level's content + 3 px halo, write the blurred content
         "blur": sum((a + 6) * (b + 6) for a, b in dims) + S,
         # read every pyramid level once (candidate output is ~1 % of it)
@@ -106,23 +130,33 @@ def pmc_traffic(kernel, streams):
     return None, None
 
 
-def cpu_baseline(seconds, threads, gray, depth, lines=False):
+def _oracle_vo(O, wl):
+    """The oracle's VO loop for a workload; returns (vo, step(vo, a, b))."""
+    import orbpl.synth as synth
+    cam = O.camera(getattr(synth, wl["cam"]))
+    if wl["stereo"]:
+        return (O.LVO(O.params(*wl["orb"]), cam, 1, use_lines=False),
+                lambda vo, a, b: vo.step_stereo(0, a, b))
+    if wl["lines"]:
+        return O.LVO(O.params(*wl["orb"]), cam, 1, use_lines=True), lambda vo, a, b: vo.step(0, a, b)
+    return O.VO(O.params(*wl["orb"]), cam, 1), lambda vo, a, b: vo.step(0, a, b)
+
+
+def cpu_baseline(seconds, threads, gray, depth, workload="points"):
     """The CPU oracle (C++ restatement, oracle/) running the same per-frame
     step, one stream per thread (throughput mode), for a bounded wall time."""
     from _pkg import load_oracle
     O = load_oracle()
-    import orbpl.synth as synth
-    cam = O.camera(synth.TUM3 if lines else synth.TUM1)
+    wl = WORKLOADS[workload]
     counts = [0] * threads
     stop = time.time() + seconds
 
     def worker(k):
-        vo = (O.LVO(O.params(*ORB), cam, 1, use_lines=True) if lines
-              else O.VO(O.params(*ORB), cam, 1))
+        vo, vstep = _oracle_vo(O, wl)
         n = len(gray)
         i = 0
         while time.time() < stop:
-            vo.step(0, gray[(k + i) % n], depth[(k + i) % n])
+            vstep(vo, gray[(k + i) % n], depth[(k + i) % n])
             i += 1
         counts[k] = i
 
@@ -136,39 +170,41 @@ def cpu_baseline(seconds, threads, gray, depth, lines=False):
     return sum(counts) / dt, sum(counts), dt
 
 
-def accuracy_gpu(pkg, cam, lines, d_gray, d_depth, traj, A, F, local_rank):
+def accuracy_gpu(pkg, cam, wl, d_gray, d_depth, traj, A, F, local_rank, fb, db):
     """Untimed accuracy leg: A streams tracked over a whole loop of F frames
     (stream s starts at loop frame s at its true pose); returns the (A, F, 4, 4)
     Tcw poses after every step."""
-    tr = pkg.Tracker(pkg.OrbParams(*ORB), cam, A, device=local_rank, lines=lines)
+    tr = pkg.Tracker(pkg.OrbParams(*wl["orb"]), cam, A, device=local_rank, lines=wl["lines"],
+                     stereo=wl["stereo"])
     tr.reset(np.stack([np.linalg.inv(traj[s % F]).astype(np.float32) for s in range(A)]).reshape(
         A, 16))
     out = np.zeros((A, F, 4, 4), np.float32)
     for t in range(F):
-        tr.step_device(d_gray.ptr + t * W * H, d_depth.ptr + t * W * H * 4)
+        if wl["stereo"]:
+            tr.step_stereo_device(d_gray.ptr + t * fb, d_depth.ptr + t * db)
+        else:
+            tr.step_device(d_gray.ptr + t * fb, d_depth.ptr + t * db)
         tr.synchronize()
         out[:, t] = tr.state()["Tcw"]
     tr.close()
     return out
 
 
-def accuracy_ref(gray, depth, traj, A, lines):
+def accuracy_ref(gray, depth, traj, A, workload):
     """The oracle's VO loop (the reference restatement) over the same A x F
     frames, one host thread per stream; returns its (A, F, 4, 4) poses."""
     from _pkg import load_oracle
     O = load_oracle()
-    import orbpl.synth as synth
-    cam = O.camera(synth.TUM3 if lines else synth.TUM1)
+    wl = WORKLOADS[workload]
     F = len(gray)
     out = np.zeros((A, F, 4, 4), np.float32)
 
     def worker(s):
-        vo = (O.LVO(O.params(*ORB), cam, 1, use_lines=True) if lines
-              else O.VO(O.params(*ORB), cam, 1))
+        vo, vstep = _oracle_vo(O, wl)
         vo.reset(np.linalg.inv(traj[s % F]).astype(np.float32).reshape(1, 16))
         for t in range(F):
             f = (s + t) % F
-            out[s, t] = vo.step(0, gray[f], depth[f])[0]
+            out[s, t] = vstep(vo, gray[f], depth[f])[0]
 
     ths = [threading.Thread(target=worker, args=(s,)) for s in range(A)]
     for t in ths:
@@ -199,26 +235,32 @@ def ate_report(T_gpu, T_ref, traj):
 
 def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, local_rank, dist):
     """Time `steps` tracker steps of one workload; returns the measurements."""
-    lines = workload == "lines"
-    cam_name = "TUM3" if lines else "TUM1"
+    wl = WORKLOADS[workload]
+    lines, stereo, cam_name = wl["lines"], wl["stereo"], wl["cam"]
     F = args.loop
     workers = min(16, os.cpu_count() or 4)
-    gray, depth = render_loop(F, seed=1 + rank, workers=workers, cam_name=cam_name)
+    gray, depth = render_loop(F, seed=1 + rank, workers=workers, cam_name=cam_name, stereo=stereo)
+    fh, fw = gray.shape[1:]
     # stream s at step t reads loop frame (s + t) mod F: a contiguous window of
     # a (S + F)-frame replicated buffer, so every step's batch is one slice.
     rep = np.arange(S + F) % F
     d_gray = pkg.DeviceBuffer.from_array(gray[rep], device=local_rank)
     d_depth = pkg.DeviceBuffer.from_array(depth[rep], device=local_rank)
     cam = pkg.make_camera(getattr(synth, cam_name))
-    tr = pkg.Tracker(pkg.OrbParams(*ORB), cam, S, device=local_rank, lines=lines)
+    tr = pkg.Tracker(pkg.OrbParams(*wl["orb"]), cam, S, device=local_rank, lines=lines,
+                     stereo=stereo)
     tr.set_pipelined(bool(args.pipelined))
     traj = synth.loop_trajectory(F, seed=1 + rank)
     tr.reset(np.stack([np.linalg.inv(traj[s % F]).astype(np.float32) for s in range(S)]).reshape(S, 16))
-    fb, db = W * H, W * H * 4
+    fb = fw * fh
+    db = fb * depth.itemsize   # right image (u8) for stereo, depth (f32) otherwise
 
     def step(k):
         o = k % F
-        tr.step_device(d_gray.ptr + o * fb, d_depth.ptr + o * db)
+        if stereo:
+            tr.step_stereo_device(d_gray.ptr + o * fb, d_depth.ptr + o * db)
+        else:
+            tr.step_device(d_gray.ptr + o * fb, d_depth.ptr + o * db)
 
     for k in range(warmup):
         step(k)
@@ -254,12 +296,15 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, loca
         ls = tr.status()
         tracking.update(mean_lines=float(ls["nlines"].mean()),
                         mean_line_matches=float(ls["line_matches"].mean()))
+    if stereo:
+        stt = tr.stereo_timings(steps).mean(0)
+        stages.update(zip(tr.STEREO_STAGES, [round(float(x), 4) for x in stt]))
     frames = S * steps * world
     value = frames / elapsed
 
     # roofline of the dominant single-launch kernel (pyramid = 8 launches: excluded)
     n_kp = float(st["nkeypoints"].mean())
-    ab = algorithmic_bytes(n_kp)
+    ab = algorithmic_bytes(n_kp, fw, fh, wl["orb"])
     names = {"blur": "k_blur", "fast": "k_fast_cells", "octree": "k_octree",
              "orient_desc": "k_orient_desc", "match": "k_match_last", "pose": "k_pose"}
     idx = {k: tr.STAGES.index(k) for k in names}
@@ -267,7 +312,7 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, loca
     dom_ms = float(avg[idx[dom]])
     bytes_launch = int(ab[dom] * S)
     achieved = bytes_launch / (dom_ms * 1e-3) / 1e9
-    traffic, tsrc = pmc_traffic(names[dom], S)
+    traffic, tsrc = pmc_traffic(names[dom], S) if workload == "points" else (None, None)
     roof = {"bound": "hbm", "kernel": names[dom],
             "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
@@ -277,17 +322,11 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, loca
                                 for k in names}}
     tr.close()
     A = min(args.ate_streams, S)
-    T_acc = (accuracy_gpu(pkg, cam, lines, d_gray, d_depth, traj, A, F, local_rank)
+    T_acc = (accuracy_gpu(pkg, cam, wl, d_gray, d_depth, traj, A, F, local_rank, fb, db)
              if A > 0 else None)
     return dict(S=S, value=value, T_acc=T_acc, traj=traj, elapsed=elapsed, stages=stages,
-                tracking=tracking, roof=roof,
-                gray=gray, depth=depth,
-                workload=("TUM fr3_structure_texture_far-like RGB-D, ORB + LSD/LBD lines "
-                          "(configs[2])" if lines else
-                          "TUM fr1_desk-like RGB-D, ORB points only (configs[1])"),
-                data=("synthetic (seeded textured-room RGB-D loop, " +
-                      ("TUM3 intrinsics, no distortion)" if lines else
-                       "TUM1 intrinsics+distortion)")))
+                tracking=tracking, roof=roof, gray=gray, depth=depth, workload=wl["desc"],
+                data=wl["data"], image=f"{fw}x{fh}", nfeatures=wl["orb"][0])
 
 
 def main():
@@ -300,12 +339,17 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=("points", "lines"), default="points",
-                    help="points = configs[1] (headline); lines = configs[2] ORB + LSD/LBD")
+    ap.add_argument("--workload", choices=("points", "lines", "kitti"), default="points",
+                    help="points = configs[1] (headline); lines = configs[2] ORB + LSD/LBD; "
+                         "kitti = configs[3] stereo")
     ap.add_argument("--secondary-steps", type=int, default=3,
                     help="steps of the configs[2] lines workload reported under 'secondary' "
                          "(points runs only; 0 = skip)")
     ap.add_argument("--lines-streams", type=int, default=1536)
+    ap.add_argument("--stereo-steps", type=int, default=3,
+                    help="steps of the configs[3] stereo workload reported under 'stereo' "
+                         "(points runs only; 0 = skip)")
+    ap.add_argument("--stereo-streams", type=int, default=256)
     ap.add_argument("--ate-streams", type=int, default=8,
                     help="streams of the untimed accuracy leg (ATE vs ground truth and vs the "
                          "reference restatement over one loop); 0 = skip")
@@ -328,26 +372,31 @@ def main():
 
     res = run_workload(pkg, synth, args, args.workload, args.streams, args.steps, args.warmup,
                        rank, world, local_rank, dist)
-    sec = None
+    # other BASELINE configs, same clock discipline, fewer steps (points runs only):
+    # configs[2] (ORB + LSD/LBD lines) under "secondary", configs[3] (stereo) under "stereo"
+    others = {}
     if args.workload == "points" and args.secondary_steps > 0:
-        # configs[2] (ORB + LSD/LBD lines), same clock discipline, fewer steps
-        sec = run_workload(pkg, synth, args, "lines", args.lines_streams, args.secondary_steps,
-                           max(1, args.warmup // 2), rank, world, local_rank, dist)
+        others["secondary"] = ("lines", run_workload(
+            pkg, synth, args, "lines", args.lines_streams, args.secondary_steps,
+            max(1, args.warmup // 2), rank, world, local_rank, dist), args.secondary_steps)
+    if args.workload == "points" and args.stereo_steps > 0:
+        others["stereo"] = ("kitti", run_workload(
+            pkg, synth, args, "kitti", args.stereo_streams, args.stereo_steps,
+            max(1, args.warmup // 2), rank, world, local_rank, dist), args.stereo_steps)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         thr = args.cpu_threads or min(16, os.cpu_count() or 1)
-        lines = args.workload == "lines"
-        fps, nfr, dt = cpu_baseline(args.cpu_seconds, thr, res["gray"], res["depth"], lines)
+        fps, nfr, dt = cpu_baseline(args.cpu_seconds, thr, res["gray"], res["depth"],
+                                    args.workload)
         if res["T_acc"] is not None:
             res["T_ref"] = accuracy_ref(res["gray"], res["depth"], res["traj"],
-                                        len(res["T_acc"]), lines)
-        if sec is not None and sec["T_acc"] is not None:
-            sec["T_ref"] = accuracy_ref(sec["gray"], sec["depth"], sec["traj"],
-                                        len(sec["T_acc"]), True)
+                                        len(res["T_acc"]), args.workload)
+        for key, (wname, o, _) in others.items():
+            if o["T_acc"] is not None:
+                o["T_ref"] = accuracy_ref(o["gray"], o["depth"], o["traj"], len(o["T_acc"]), wname)
         cpu = {"value": round(fps, 2), "unit": "frames/s", "cores": thr, "kind": "port",
-               "sample": f"{nfr} frames of the same 640x480 RGB-D loop in {dt:.1f} s, oracle/ "
-                         f"C++ restatement ({'points+lines' if lines else 'points'}), "
-                         f"one stream per thread"}
+               "sample": f"{nfr} frames of the same {res['image']} loop in {dt:.1f} s, oracle/ "
+                         f"C++ restatement ({args.workload} workload), one stream per thread"}
 
     if rank == 0:
         S = res["S"]
@@ -365,7 +414,7 @@ def main():
             "dtype": "u8",
             "data": res["data"],
             "config": {"workload": res["workload"],
-                       "image": "640x480", "nfeatures": 1000, "streams_per_gpu": S,
+                       "image": res["image"], "nfeatures": res["nfeatures"], "streams_per_gpu": S,
                        "frames_per_step": S * world, "parallelism": f"streams sharded x{world}"},
             "stage_ms": res["stages"],
             "tracking": res["tracking"],
@@ -374,23 +423,24 @@ def main():
         }
         if res["T_acc"] is not None:
             out["accuracy"] = ate_report(res["T_acc"], res.get("T_ref"), res["traj"])
-        if sec is not None:
-            out["secondary"] = {
-                "workload": sec["workload"], "value": round(sec["value"], 2),
-                "unit": "frames/s", "steps": args.secondary_steps, "streams_per_gpu": sec["S"],
-                "ms_per_step": round(sec["elapsed"] / args.secondary_steps * 1e3, 3),
-                "stage_ms": sec["stages"], "tracking": sec["tracking"]}
-            if sec["T_acc"] is not None:
-                out["secondary"]["accuracy"] = ate_report(sec["T_acc"], sec.get("T_ref"),
-                                                          sec["traj"])
+        for key, (wname, o, nsteps) in others.items():
+            out[key] = {
+                "workload": o["workload"], "value": round(o["value"], 2),
+                "unit": "frames/s", "image": o["image"], "nfeatures": o["nfeatures"],
+                "steps": nsteps, "streams_per_gpu": o["S"],
+                "ms_per_step": round(o["elapsed"] / nsteps * 1e3, 3),
+                "stage_ms": o["stages"], "tracking": o["tracking"], "roofline": o["roof"],
+                "data": o["data"]}
+            if o["T_acc"] is not None:
+                out[key]["accuracy"] = ate_report(o["T_acc"], o.get("T_ref"), o["traj"])
             if cpu is not None:
                 thr = cpu["cores"]
-                fps, nfr, dt = cpu_baseline(args.cpu_seconds / 2, thr, sec["gray"], sec["depth"],
-                                            lines=True)
-                out["secondary"]["cpu_baseline"] = {
+                fps, nfr, dt = cpu_baseline(args.cpu_seconds / 2, thr, o["gray"], o["depth"],
+                                            wname)
+                out[key]["cpu_baseline"] = {
                     "value": round(fps, 2), "unit": "frames/s", "cores": thr, "kind": "port",
                     "sample": f"{nfr} frames in {dt:.1f} s, oracle/ C++ restatement "
-                              f"(points+lines), one stream per thread"}
+                              f"({wname} workload), one stream per thread"}
         print(json.dumps(out))
     if dist:
         dist.destroy_process_group()

@@ -304,6 +304,13 @@ int orbpl_tracker_create(const orbpl_orb_params* orb, const orbpl_camera* cam, i
  * LineMatcher::SearchByProjection against the last frame's map lines,
  * PoseOptimization with line edges, line outlier discard and map lines. */
 #define ORBPL_TRACK_LINES 1
+/* ORBPL_TRACK_STEREO: the reference's stereo tracking (Tracking::GrabImageStereo,
+ * Tracking.cc:180-208): Frame(imLeft, imRight) runs ORB on both images
+ * concurrently (Frame.cc:88-91), UndistortKeyPoints, ComputeStereoMatches
+ * (Frame.cc:886-1063) for depth / uRight; SearchByProjection uses th = 7
+ * (Tracking.cc:1238-1241). The stereo Frame extracts no lines, so this flag
+ * excludes ORBPL_TRACK_LINES. Images up to 1024 rows. */
+#define ORBPL_TRACK_STEREO 2
 int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam, int n_streams,
                             int device, int flags, orbpl_tracker** out);
 int orbpl_tracker_destroy(orbpl_tracker* tr);
@@ -314,6 +321,9 @@ int orbpl_tracker_reset(orbpl_tracker* tr, const float* Tcw0);
  * d_depth: n_streams frames of width*height float metres (device memory,
  * contiguous). Asynchronous on the tracker's stream. */
 int orbpl_tracker_step(orbpl_tracker* tr, const uint8_t* d_gray, const float* d_depth);
+/* Stereo step (ORBPL_TRACK_STEREO trackers): d_left / d_right hold n_streams
+ * rectified frames of width*height u8 each (device memory, contiguous). */
+int orbpl_tracker_step_stereo(orbpl_tracker* tr, const uint8_t* d_left, const uint8_t* d_right);
 int orbpl_tracker_synchronize(orbpl_tracker* tr);
 /* on != 0: extraction of step t+1 may overlap matching/pose of step t (two
  * HIP streams, three frame buffers). Results are identical either way. */
@@ -350,6 +360,9 @@ int orbpl_tracker_get_lines(orbpl_tracker* tr, int stream, orbpl_keyline* kl_un,
 /* Line stage device times (ms) of the last min(max_steps, 64) steps, 3 per
  * step: LSD, KeyLines + LBD + UndistortKeyLines, line SearchByProjection. */
 int orbpl_tracker_line_timings(orbpl_tracker* tr, int max_steps, float* ms, int* n_steps);
+/* Stereo stage device times (ms) of the last min(max_steps, 64) steps, 2 per
+ * step: right-image ORB extraction, ComputeStereoMatches. */
+int orbpl_tracker_stereo_timings(orbpl_tracker* tr, int max_steps, float* ms, int* n_steps);
 
 /* ------------------------------------------------------------------------
  * Line tracking, single frame, host pointers (n <= 80 = LineExtractor's cap)

@@ -437,11 +437,17 @@ int oracle_lvo_reset(void* h, const float* Tcw0) {
   return 0;
 }
 
-// out8: nkeypoints, nmatches, ninliers, nmatches_map, ok, nlines, line_matches,
-// line_nmatches_map
-int oracle_lvo_step(void* h, int stream, const uint8_t* gray, const float* depth, float* Tcw_out,
-                    int* out8) {
-  LVO* v = static_cast<LVO*>(h);
+}  // extern "C"
+
+namespace line_track {
+
+// One TrackWithMotionModel step. RGB-D (right == NULL): Frame(imGray, imDepth)
+// (Frame.cc:135-205). Stereo (right != NULL): Frame(imLeft, imRight)
+// (Frame.cc:70-131): ORB on both images, UndistortKeyPoints, then
+// ComputeStereoMatches on the two extractors' pyramids; the stereo Frame
+// extracts no lines, and SearchByProjection uses th = 7 (Tracking.cc:1238-1241).
+static int lvo_step(LVO* v, int stream, const uint8_t* gray, const float* depth,
+                    const uint8_t* right, float* Tcw_out, int* out8) {
   LStream& S = v->st[stream];
   const orbpl_camera& cam = v->cam;
   const int cap = v->orb.nfeatures * 2 + 64;
@@ -456,13 +462,36 @@ int oracle_lvo_step(void* h, int stream, const uint8_t* gray, const float* depth
   std::vector<orbpl_keypoint> ku(n);
   std::vector<float> dep(n), ur(n);
   std::vector<int32_t> gc(n);
-  oracle_frame_prepare(&cam, kps.data(), n, depth, ku.data(), dep.data(), ur.data(), gc.data(), nullptr);
+  oracle_frame_prepare(&cam, kps.data(), n, right ? nullptr : depth, ku.data(), dep.data(),
+                       ur.data(), gc.data(), nullptr);
+  if (right) {
+    std::vector<orbpl_keypoint> kr(cap);
+    std::vector<uint8_t> dr((size_t)cap * 32);
+    int nr = 0;
+    rc = oracle_orb_extract(&v->orb, right, cam.width, cam.height, cam.width, kr.data(), dr.data(),
+                            cap, &nr, nullptr);
+    if (rc) return rc;
+    const int L = v->orb.nlevels;
+    std::vector<int32_t> lw(L), lh(L);
+    std::vector<float> sc(L), isc(L);
+    oracle_orb_level_sizes(&v->orb, cam.width, cam.height, lw.data(), lh.data(), nullptr,
+                           sc.data(), isc.data());
+    size_t tot = 0;
+    for (int l = 0; l < L; l++) tot += (size_t)(lw[l] + 38) * (lh[l] + 38);
+    std::vector<uint8_t> pl(tot), pr(tot);
+    oracle_orb_pyramid(&v->orb, gray, cam.width, cam.height, cam.width, pl.data(), 0);
+    oracle_orb_pyramid(&v->orb, right, cam.width, cam.height, cam.width, pr.data(), 0);
+    oracle_stereo_matches(&cam, sc.data(), isc.data(), L, lw.data(), lh.data(), pl.data(),
+                          pr.data(), kps.data(), desc.data(), n, kr.data(), dr.data(), nr,
+                          ur.data(), dep.data());
+  }
+  const float th = right ? 7.0f : 15.0f;
   // lines
   int nl = 0;
   std::vector<orbpl_keyline> kl(80), klu;
   std::vector<uint8_t> ldesc(80 * 32);
   std::vector<float> lds, lde, lurs, lure;
-  if (v->use_lines) {
+  if (v->use_lines && !right) {
     std::vector<double> coef(80 * 3);
     int nd = 0;
     rc = oracle_line_extract(gray, cam.width, cam.height, kl.data(), ldesc.data(), coef.data(), 80,
@@ -491,9 +520,9 @@ int oracle_lvo_step(void* h, int stream, const uint8_t* gray, const float* depth
     orbpl_match_current cur{n, S.Tcw, ku.data(), desc.data(), ur.data()};
     orbpl_match_last last{(int)S.kps_un.size(), S.Tlast, S.kps_un.data(), S.has_mp.data(),
                           S.outlier.data(), S.xyz.data(), S.desc.data(), S.nobs.data()};
-    oracle_search_by_projection_last(&cam, v->scale.data(), (int)v->scale.size(), &cur, &last, 15.0f,
+    oracle_search_by_projection_last(&cam, v->scale.data(), (int)v->scale.size(), &cur, &last, th,
                                      0, 1, match.data(), &nmatches);
-    if (v->use_lines)
+    if (v->use_lines && !right)
       oracle_line_search_by_projection_last(&cam, S.Tcw, nl, klu.data(), ldesc.data(),
                                             (int)S.kl_un.size(), S.kl_un.data(), S.has_ml.data(),
                                             S.loutlier.data(), S.lxyz.data(), S.ldesc.data(),
@@ -501,9 +530,9 @@ int oracle_lvo_step(void* h, int stream, const uint8_t* gray, const float* depth
     if (nmatches < 20) {
       std::fill(match.begin(), match.end(), -1);
       oracle_search_by_projection_last(&cam, v->scale.data(), (int)v->scale.size(), &cur, &last,
-                                       30.0f, 0, 1, match.data(), &nmatches);
+                                       2.0f * th, 0, 1, match.data(), &nmatches);
     }
-    tracked = nmatches >= 20 && (!v->use_lines || nlm >= 15);
+    tracked = nmatches >= 20 && (!v->use_lines || right || nlm >= 15);
     if (tracked) {
       std::vector<uint8_t> has(n, 0), hasl(nl, 0);
       std::vector<float> xyz((size_t)n * 3, 0.f), lobs((size_t)nl * 4, 0.f), lxyz((size_t)nl * 6, 0.f);
@@ -584,7 +613,8 @@ int oracle_lvo_step(void* h, int stream, const uint8_t* gray, const float* depth
       S.has_ml[j] = 1;
     }
   bool ok = true;
-  if (S.has_last) ok = tracked && (v->use_lines ? (nmap >= 10 || lnmap >= 15) : nmap >= 10);
+  if (S.has_last)
+    ok = tracked && (v->use_lines && !right ? (nmap >= 10 || lnmap >= 15) : nmap >= 10);
   memcpy(S.Tlast2, S.Tlast, 64);
   memcpy(S.Tlast, S.Tcw, 64);
   S.has_velocity = S.has_last;
@@ -595,6 +625,25 @@ int oracle_lvo_step(void* h, int stream, const uint8_t* gray, const float* depth
     out8[5] = nl; out8[6] = nlm; out8[7] = lnmap;
   }
   return 0;
+}
+
+}  // namespace line_track
+
+extern "C" {
+
+// out8: nkeypoints, nmatches, ninliers, nmatches_map, ok, nlines, line_matches,
+// line_nmatches_map
+int oracle_lvo_step(void* h, int stream, const uint8_t* gray, const float* depth, float* Tcw_out,
+                    int* out8) {
+  return line_track::lvo_step(static_cast<line_track::LVO*>(h), stream, gray, depth, nullptr,
+                              Tcw_out, out8);
+}
+
+// Stereo TrackWithMotionModel step (points only, see lvo_step).
+int oracle_lvo_step_stereo(void* h, int stream, const uint8_t* left, const uint8_t* right,
+                           float* Tcw_out, int* out8) {
+  return line_track::lvo_step(static_cast<line_track::LVO*>(h), stream, left, nullptr, right,
+                              Tcw_out, out8);
 }
 
 }  // extern "C"

@@ -452,6 +452,7 @@ def _setup(L):  # noqa: F811
     L.oracle_lvo_destroy.argtypes = [vp]
     L.oracle_lvo_reset.argtypes = [vp, vp]
     L.oracle_lvo_step.argtypes = [vp, i, vp, vp, vp, vp]
+    L.oracle_lvo_step_stereo.argtypes = [vp, i, vp, vp, vp, vp]
 
 
 def line_frame_prepare(cam, kl, depth=None):
@@ -520,6 +521,18 @@ class LVO:
         T = np.zeros(16, np.float32)
         o = np.zeros(8, np.int32)
         rc = lib().oracle_lvo_step(self.h, stream, _p(g), _p(d), _p(T), _p(o))
+        assert rc == 0
+        keys = ("nkeypoints", "nmatches", "ninliers", "nmatches_map", "ok", "nlines",
+                "line_matches", "line_nmatches_map")
+        return T.reshape(4, 4), dict(zip(keys, (int(x) for x in o)))
+
+    def step_stereo(self, stream, left, right):
+        """Stereo Frame + TrackWithMotionModel (points only, th = 7)."""
+        gl = _c(left, np.uint8)
+        gr = _c(right, np.uint8)
+        T = np.zeros(16, np.float32)
+        o = np.zeros(8, np.int32)
+        rc = lib().oracle_lvo_step_stereo(self.h, stream, _p(gl), _p(gr), _p(T), _p(o))
         assert rc == 0
         keys = ("nkeypoints", "nmatches", "ninliers", "nmatches_map", "ok", "nlines",
                 "line_matches", "line_nmatches_map")

@@ -244,6 +244,16 @@ class ORBextractor:
     def synchronize(self):
         check(lib().orbx_synchronize(self._h), "orbx_synchronize")
 
+    STEREO_STAGES = ("right_extract", "stereo_match")
+
+    def stereo_timings(self, max_steps=64):
+        """(n_steps, 2) stereo-stage ms of the last steps (hipEvents in-stream)."""
+        ms = np.zeros((max_steps, 2), np.float32)
+        n = C.c_int(0)
+        check(lib().orbpl_tracker_stereo_timings(self._h, max_steps, _ptr(ms), C.byref(n)),
+              "orbpl_tracker_stereo_timings")
+        return ms[:n.value]
+
     def stage_ms(self):
         ms = np.zeros(5, np.float32)
         check(lib().orbx_last_stage_ms(self._h, _ptr(ms)), "orbx_last_stage_ms")
@@ -353,6 +363,8 @@ def _declare_track(L):
     L.orbpl_tracker_get_status.argtypes = [vp, vp, vp, vp, vp]
     L.orbpl_tracker_get_lines.argtypes = [vp, i, vp, vp, vp, vp, ip]
     L.orbpl_tracker_line_timings.argtypes = [vp, i, vp, ip]
+    L.orbpl_tracker_step_stereo.argtypes = [vp, vp, vp]
+    L.orbpl_tracker_stereo_timings.argtypes = [vp, i, vp, ip]
 
 
 _declare_orig = _declare
@@ -595,17 +607,21 @@ def _line_search_list(camera, Tcw, cur_kl_un, cur_desc, cur_nobs, valid, ml_xyz6
 
 
 class Tracker:
-    """Batched RGB-D tracker (orbpl_tracker_*): one TrackWithMotionModel step
-    for n_streams independent streams per call. lines=True selects the
-    point-and-line variant (ORBPL_TRACK_LINES)."""
+    """Batched RGB-D / stereo tracker (orbpl_tracker_*): one
+    TrackWithMotionModel step for n_streams independent streams per call.
+    lines=True selects the point-and-line variant (ORBPL_TRACK_LINES),
+    stereo=True the stereo Frame (ORBPL_TRACK_STEREO, points only)."""
 
     TRACK_LINES = 1
+    TRACK_STEREO = 2
 
-    def __init__(self, orb_params, camera, n_streams, device=0, lines=False):
+    def __init__(self, orb_params, camera, n_streams, device=0, lines=False, stereo=False):
         h = C.c_void_p()
         self.camera, self.S, self.device, self.use_lines = camera, n_streams, device, bool(lines)
+        self.stereo = bool(stereo)
+        flags = (self.TRACK_LINES if lines else 0) | (self.TRACK_STEREO if stereo else 0)
         check(lib().orbpl_tracker_create_ex(C.byref(orb_params), C.byref(camera), n_streams, device,
-                                            self.TRACK_LINES if lines else 0, C.byref(h)),
+                                            flags, C.byref(h)),
               "orbpl_tracker_create_ex")
         self._h = h
         self.kp_cap = lib().orbpl_tracker_kp_capacity(h)
@@ -627,6 +643,11 @@ class Tracker:
 
     def step_device(self, d_gray, d_depth):
         check(lib().orbpl_tracker_step(self._h, C.c_void_p(d_gray), C.c_void_p(d_depth)), "step")
+
+    def step_stereo_device(self, d_left, d_right):
+        """Stereo step: device pointers to n_streams left / right frames."""
+        check(lib().orbpl_tracker_step_stereo(self._h, C.c_void_p(d_left), C.c_void_p(d_right)),
+              "orbpl_tracker_step_stereo")
 
     def synchronize(self):
         check(lib().orbpl_tracker_synchronize(self._h), "orbpl_tracker_synchronize")
@@ -672,6 +693,16 @@ class Tracker:
         n = C.c_int(0)
         check(lib().orbpl_tracker_line_timings(self._h, max_steps, _ptr(ms), C.byref(n)),
               "orbpl_tracker_line_timings")
+        return ms[:n.value]
+
+    STEREO_STAGES = ("right_extract", "stereo_match")
+
+    def stereo_timings(self, max_steps=64):
+        """(n_steps, 2) stereo-stage ms of the last steps (hipEvents in-stream)."""
+        ms = np.zeros((max_steps, 2), np.float32)
+        n = C.c_int(0)
+        check(lib().orbpl_tracker_stereo_timings(self._h, max_steps, _ptr(ms), C.byref(n)),
+              "orbpl_tracker_stereo_timings")
         return ms[:n.value]
 
     def stage_ms(self):

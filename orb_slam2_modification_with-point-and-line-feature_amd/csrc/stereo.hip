@@ -1,6 +1,6 @@
 // Frame::ComputeStereoMatches (Frame.cc:886-1063) on gfx950, restated in
 // oracle/track_oracle.cpp (oracle_stereo_matches). One 256-thread workgroup
-// per stereo pair:
+// per stereo pair of the batch (blockIdx.x = frame):
 //   1. row bands: every right keypoint is entered, in index order, in the
 //      lists of the rows floor(y - 2 s) .. ceil(y + 2 s) (counting sort in
 //      LDS, lists kept in increasing index like vRowIndices);
@@ -60,6 +60,22 @@ __global__ void __launch_bounds__(256) k_stereo(StereoArgs a) {
   __shared__ uint32_t keys[kStereoKp];
   __shared__ int s_cnt, s_wsum[4];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int f = blockIdx.x;
+  {  // this frame's slice of the batch
+    const long long o = (long long)f * a.kp_pitch;
+    a.n = a.n_arr ? a.n_arr[f] : a.n;
+    a.nr = a.nr_arr ? a.nr_arr[f] : a.nr;
+    a.kl += o;
+    a.kr += o;
+    a.dl += o * 32;
+    a.dr += o * 32;
+    a.uright += o;
+    a.depth += o;
+    a.sad += o;
+    a.pyrL += (long long)f * a.pyr_pitch;
+    a.pyrR += (long long)f * a.pyr_pitch;
+    a.entries += (long long)f * a.entry_cap;
+  }
   const int n = min(a.n, kStereoKp), nr = min(a.nr, kStereoKp);
   const int nRows = a.nrows;
   // ---- 1. row bands ----
@@ -247,8 +263,8 @@ __global__ void __launch_bounds__(256) k_stereo(StereoArgs a) {
   }
 }
 
-void launch_stereo(const StereoArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_stereo, dim3(1), dim3(256), 0, s, a);
+void launch_stereo(const StereoArgs& a, int batch, hipStream_t s) {
+  hipLaunchKernelGGL(k_stereo, dim3(batch), dim3(256), 0, s, a);
 }
 
 }  // namespace orbpl

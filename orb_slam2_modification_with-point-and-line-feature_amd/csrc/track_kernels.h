@@ -180,6 +180,13 @@ void launch_match_bow(const BowArgs& a, hipStream_t s);
 
 // Frame::ComputeStereoMatches (stereo.hip).
 struct StereoArgs {
+  // Batched: frame f = blockIdx.x reads counts n_arr[f] / nr_arr[f] (or n /
+  // nr when NULL), keypoint rows at f * kp_pitch (kl, dl, kr, dr, uright,
+  // depth, sad), pyramids at f * pyr_pitch, entries at f * entry_cap.
+  const int* n_arr;
+  const int* nr_arr;
+  long long kp_pitch;
+  long long pyr_pitch;
   int n;
   const KeyPointD* kl;           // left mvKeys
   const uint8_t* dl;
@@ -200,7 +207,7 @@ struct StereoArgs {
   int entry_cap;
   int* err;
 };
-void launch_stereo(const StereoArgs& a, hipStream_t s);
+void launch_stereo(const StereoArgs& a, int batch, hipStream_t s);
 
 void launch_in_frustum(const TrackConsts& c, float log_scale, const InFrustumArgs& a,
                        hipStream_t s);

@@ -618,7 +618,7 @@ int orbpl_stereo_matches(const orbpl_camera* cam, orbx_ctx* left, orbx_ctx* righ
   a.entries = dent.as<uint16_t>();
   a.entry_cap = cap;
   a.err = derr.as<int>();
-  launch_stereo(a, scratch_stream());
+  launch_stereo(a, 1, scratch_stream());
   HIP_CHECK(hipGetLastError());
   int err = 0;
   HIP_CHECK(hipMemcpy(&err, derr.p, 4, hipMemcpyDeviceToHost));
@@ -758,10 +758,24 @@ struct orbpl_tracker {
   lsdx_ctx* lx = nullptr;
   hipStream_t lstream = nullptr;
   hipEvent_t ev_in = nullptr;      // step start on `stream`
+  // stereo (ORBPL_TRACK_STEREO): the right image's ORB extraction runs on the
+  // right extractor's stream, concurrently with the left one; the batched
+  // ComputeStereoMatches then fills depth / uRight on the extraction stream
+  int stereo = 0;
+  orbx_ctx* exr = nullptr;
+  hipStream_t rstream = nullptr;   // owned by exr
+  hipEvent_t ev_rin = nullptr;     // step start on `stream`
+  KeyPointD* r_kps = nullptr;      // right keypoints (S x kp_cap), one buffer
+  uint8_t* r_desc = nullptr;
+  int* r_n = nullptr;
+  int* st_sad = nullptr;           // stereo scratch: SAD per left keypoint
+  uint16_t* st_entries = nullptr;  // stereo scratch: row-band entries
+  int st_entry_cap = 0;            // entries per frame
+  int* d_err = nullptr;            // stereo capacity flag
   StreamState* d_state = nullptr;
   PoseEdge* d_edges = nullptr;
   static constexpr int kRing = 64;   // steps kept in the timing ring
-  static constexpr int kEv = 15;     // events per step
+  static constexpr int kEv = 18;     // events per step
   std::vector<hipEvent_t> ring;      // kRing * kEv events
   int ring_pos = 0, ring_count = 0;
   std::vector<void*> allocs;
@@ -790,7 +804,10 @@ int orbpl_tracker_destroy(orbpl_tracker* t) {
   for (auto& e : t->ev_free)
     if (e) (void)hipEventDestroy(e);
   if (t->lstream) (void)hipStreamSynchronize(t->lstream);
+  if (t->rstream) (void)hipStreamSynchronize(t->rstream);
   if (t->ev_in) (void)hipEventDestroy(t->ev_in);
+  if (t->ev_rin) (void)hipEventDestroy(t->ev_rin);
+  if (t->exr) orbx_destroy(t->exr);
   if (t->tstream) (void)hipStreamDestroy(t->tstream);
   if (t->lstream) (void)hipStreamDestroy(t->lstream);
   if (t->lx) lsdx_destroy(t->lx);
@@ -807,11 +824,17 @@ int orbpl_tracker_create(const orbpl_orb_params* orb, const orbpl_camera* cam, i
 int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam, int n_streams,
                             int device, int flags, orbpl_tracker** out) {
   if (!orb || !cam || !out || n_streams <= 0) return arg_fail("bad argument");
-  if (flags & ~ORBPL_TRACK_LINES) return arg_fail("unknown tracker flag");
+  if (flags & ~(ORBPL_TRACK_LINES | ORBPL_TRACK_STEREO)) return arg_fail("unknown tracker flag");
+  // the reference's stereo Frame extracts no lines (Frame.cc:70-131)
+  if ((flags & ORBPL_TRACK_LINES) && (flags & ORBPL_TRACK_STEREO))
+    return arg_fail("ORBPL_TRACK_LINES and ORBPL_TRACK_STEREO are exclusive");
+  if ((flags & ORBPL_TRACK_STEREO) && cam->height > 1024)
+    return arg_fail("stereo tracking supports images up to 1024 rows");
   *out = nullptr;
   orbpl_tracker* t = new orbpl_tracker();
   t->device = device;
   t->lines = (flags & ORBPL_TRACK_LINES) ? 1 : 0;
+  t->stereo = (flags & ORBPL_TRACK_STEREO) ? 1 : 0;
   t->S = n_streams;
   t->W = cam->width;
   t->H = cam->height;
@@ -871,6 +894,16 @@ int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam
   }
   TA(t->d_state, S * sizeof(StreamState));
   TA(t->d_edges, S * kPoseMaxEdges * pose_edge_bytes());
+  if (t->stereo) {
+    // a right keypoint spans at most 4 * scale + 2 <= 18 rows (8 levels of 1.2)
+    t->st_entry_cap = (int)K * 20;
+    TA(t->r_kps, S * K * sizeof(KeyPointD));
+    TA(t->r_desc, S * K * 32);
+    TA(t->r_n, S * 4);
+    TA(t->st_sad, S * K * 4);
+    TA(t->st_entries, S * (size_t)t->st_entry_cap * 2);
+    TA(t->d_err, 4);
+  }
 #undef TA
   t->ring.assign(orbpl_tracker::kRing * orbpl_tracker::kEv, nullptr);
   for (auto& e : t->ring)
@@ -899,6 +932,18 @@ int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam
       return hip_fail(hipErrorUnknown, "hipStreamCreate", __LINE__);
     }
   }
+  if (t->stereo) {
+    rc = orbx_create(orb, cam->width, cam->height, n_streams, device, &t->exr);
+    if (rc) {
+      orbpl_tracker_destroy(t);
+      return rc;
+    }
+    t->rstream = orbpl::orbx_stream(t->exr);
+    if (hipEventCreateWithFlags(&t->ev_rin, hipEventDisableTiming) != hipSuccess) {
+      orbpl_tracker_destroy(t);
+      return hip_fail(hipErrorUnknown, "hipEventCreate", __LINE__);
+    }
+  }
   rc = orbpl_tracker_reset(t, nullptr);
   if (rc) {
     orbpl_tracker_destroy(t);
@@ -920,12 +965,17 @@ int orbpl_tracker_reset(orbpl_tracker* t, const float* Tcw0) {
   HIP_CHECK(hipStreamSynchronize(t->stream));
   if (t->tstream) HIP_CHECK(hipStreamSynchronize(t->tstream));
   if (t->lstream) HIP_CHECK(hipStreamSynchronize(t->lstream));
+  if (t->rstream) HIP_CHECK(hipStreamSynchronize(t->rstream));
   HIP_CHECK(hipMemcpy(t->d_state, st.data(), sizeof(StreamState) * t->S, hipMemcpyHostToDevice));
   return ORBPL_OK;
 }
 
-int orbpl_tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_depth) {
-  if (!t || !d_gray || !d_depth) return arg_fail("NULL argument");
+}  // extern "C"
+
+// One TrackWithMotionModel step for every stream: RGB-D (d_depth) or stereo
+// (d_right, ORBPL_TRACK_STEREO trackers).
+static int tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_depth,
+                        const uint8_t* d_right) {
   HIP_CHECK(hipSetDevice(t->device));
   const int ci = t->ring_pos % 3, li = (t->ring_pos + 2) % 3;
   FrameBufs& C = t->fb[ci];
@@ -941,6 +991,18 @@ int orbpl_tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_d
   hipEvent_t* ev = &t->ring[(size_t)(t->ring_pos % orbpl_tracker::kRing) * orbpl_tracker::kEv];
   // ---- extraction stream: wait until tracking of step t-1 released fb[ci]
   if (t->free_pending[ci]) HIP_CHECK(hipStreamWaitEvent(s, t->ev_free[ci], 0));
+  if (t->stereo) {
+    // ---- right stream: ORB on the right images (Frame.cc:88-91). Ordered
+    // after the previous step's stereo matching, which read r_kps and the
+    // right pyramid on `s`.
+    HIP_CHECK(hipEventRecord(t->ev_rin, s));
+    HIP_CHECK(hipStreamWaitEvent(t->rstream, t->ev_rin, 0));
+    HIP_CHECK(hipEventRecord(ev[15], t->rstream));
+    int rrc = orbx_run(t->exr, d_right, S, t->W, (long long)t->W * t->H,
+                       reinterpret_cast<orbpl_keypoint_dev*>(t->r_kps), t->r_desc, K, t->r_n);
+    if (rrc) return rrc;
+    HIP_CHECK(hipEventRecord(ev[16], t->rstream));
+  }
   LineTrackArgs la{};
   if (t->lines) {
     // ---- line stream: LineExtractor + UndistortKeyLines + line depths
@@ -976,8 +1038,45 @@ int orbpl_tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_d
   int rc = orbx_run(t->ex, d_gray, S, t->W, (long long)t->W * t->H,
                     reinterpret_cast<orbpl_keypoint_dev*>(C.kps), C.desc, K, C.n, ev);
   if (rc) return rc;
-  launch_frame_prepare(t->consts, C.kps, C.n, K, d_depth, (long long)t->W * t->H, C.kps_un, C.depth,
-                       C.uright, C.gcell, S, s);
+  launch_frame_prepare(t->consts, C.kps, C.n, K, t->stereo ? nullptr : d_depth,
+                       (long long)t->W * t->H, C.kps_un, C.depth, C.uright, C.gcell, S, s);
+  if (t->stereo) {
+    // ComputeStereoMatches (Frame.cc:886-1063) for the whole batch
+    HIP_CHECK(hipStreamWaitEvent(s, ev[16], 0));
+    HIP_CHECK(hipEventRecord(ev[17], s));
+    const uint8_t *pl = nullptr, *pr = nullptr;
+    const OrbGeom *gl = nullptr, *gr = nullptr;
+    hipStream_t sl, sr;
+    int prc = orbx_device_pyramid(t->ex, 0, &pl, &gl, &sl);
+    if (!prc) prc = orbx_device_pyramid(t->exr, 0, &pr, &gr, &sr);
+    if (prc) return prc;
+    StereoArgs a{};
+    a.n_arr = C.n;
+    a.nr_arr = t->r_n;
+    a.kp_pitch = K;
+    a.pyr_pitch = (long long)gl->pyr_bytes;
+    a.kl = C.kps;
+    a.dl = C.desc;
+    a.kr = t->r_kps;
+    a.dr = t->r_desc;
+    a.pyrL = pl;
+    a.pyrR = pr;
+    for (int l = 0; l < gl->nlevels; l++) {
+      a.lv[l] = gl->lv[l];
+      a.scale[l] = gl->lv[l].scale;
+      a.inv_scale[l] = 1.0f / gl->lv[l].scale;
+    }
+    a.nrows = gl->H;
+    a.mb = t->consts.mb;
+    a.mbf = t->consts.bf;
+    a.uright = C.uright;
+    a.depth = C.depth;
+    a.sad = t->st_sad;
+    a.entries = t->st_entries;
+    a.entry_cap = t->st_entry_cap;
+    a.err = t->d_err;
+    launch_stereo(a, S, s);
+  }
   HIP_CHECK(hipEventRecord(ev[6], s));
   // ---- tracking stream
   HIP_CHECK(hipStreamWaitEvent(ts, ev[6], 0));
@@ -1004,7 +1103,7 @@ int orbpl_tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_d
   m.match = C.match;
   m.nmatches = dNm;
   m.nm_stride = pstride;
-  m.th = 15.0f;          // RGB-D (Tracking.cc:1238-1241)
+  m.th = t->stereo ? 7.0f : 15.0f;   // Tracking.cc:1238-1241
   m.mono = 0;
   m.check_ori = 1;       // ORBmatcher(0.9, true) (Tracking.cc:1216)
   m.retry = 1;
@@ -1062,6 +1161,20 @@ int orbpl_tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_d
   return ORBPL_OK;
 }
 
+extern "C" {
+
+int orbpl_tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_depth) {
+  if (!t || !d_gray || !d_depth) return arg_fail("NULL argument");
+  if (t->stereo) return arg_fail("stereo tracker: use orbpl_tracker_step_stereo");
+  return tracker_step(t, d_gray, d_depth, nullptr);
+}
+
+int orbpl_tracker_step_stereo(orbpl_tracker* t, const uint8_t* d_left, const uint8_t* d_right) {
+  if (!t || !d_left || !d_right) return arg_fail("NULL argument");
+  if (!t->stereo) return arg_fail("tracker created without ORBPL_TRACK_STEREO");
+  return tracker_step(t, d_left, nullptr, d_right);
+}
+
 int orbpl_tracker_set_pipelined(orbpl_tracker* t, int on) {
   if (!t) return arg_fail("NULL tracker");
   HIP_CHECK(hipSetDevice(t->device));
@@ -1079,6 +1192,14 @@ int orbpl_tracker_synchronize(orbpl_tracker* t) {
     HIP_CHECK(hipStreamSynchronize(t->lstream));
     int rc = lsdx_check(t->lx, t->S);
     if (rc) return rc;
+  }
+  if (t->stereo) {
+    int rc = orbx_synchronize(t->exr);
+    if (rc) return rc;
+    HIP_CHECK(hipStreamSynchronize(t->stream));
+    int err = 0;
+    HIP_CHECK(hipMemcpy(&err, t->d_err, 4, hipMemcpyDeviceToHost));
+    if (err) return (arg_fail("stereo row band capacity exceeded"), ORBPL_ERR_OVERFLOW);
   }
   return orbx_synchronize(t->ex);
 }
@@ -1140,6 +1261,26 @@ int orbpl_tracker_line_timings(orbpl_tracker* t, int max_steps, float* ms, int* 
     hipEvent_t* ev = &t->ring[(size_t)(step % orbpl_tracker::kRing) * orbpl_tracker::kEv];
     for (int i = 0; i < 3; i++)
       HIP_CHECK(hipEventElapsedTime(&ms[k * 3 + i], ev[kPair[i][0]], ev[kPair[i][1]]));
+  }
+  *n_steps = n;
+  return ORBPL_OK;
+}
+
+int orbpl_tracker_stereo_timings(orbpl_tracker* t, int max_steps, float* ms, int* n_steps) {
+  if (!t || !ms || !n_steps) return arg_fail("NULL argument");
+  if (!t->stereo) return arg_fail("tracker created without ORBPL_TRACK_STEREO");
+  HIP_CHECK(hipSetDevice(t->device));
+  HIP_CHECK(hipStreamSynchronize(t->stream));
+  HIP_CHECK(hipStreamSynchronize(t->tstream));
+  HIP_CHECK(hipStreamSynchronize(t->rstream));
+  // right ORB extraction (right stream), ComputeStereoMatches (extraction stream)
+  static const int kPair[2][2] = {{15, 16}, {17, 6}};
+  const int n = std::min(max_steps, t->ring_count);
+  for (int k = 0; k < n; k++) {
+    const int step = t->ring_pos - n + k;
+    hipEvent_t* ev = &t->ring[(size_t)(step % orbpl_tracker::kRing) * orbpl_tracker::kEv];
+    for (int i = 0; i < 2; i++)
+      HIP_CHECK(hipEventElapsedTime(&ms[k * 2 + i], ev[kPair[i][0]], ev[kPair[i][1]]));
   }
   *n_steps = n;
   return ORBPL_OK;

@@ -179,3 +179,22 @@ def stereo_pair(seed=0, cam_name="KITTI00"):
     left, _ = synth.render(cfg, Twc, room, seed=seed)
     right, _ = synth.render(cfg, Twc @ shift, room, seed=seed)
     return cfg, left, right
+
+
+@functools.lru_cache(maxsize=8)
+def stereo_sequence(n=3, seed=0, cam_name="KITTI00"):
+    """n rectified stereo pairs along a seeded trajectory (right camera at
+    +mb along the left camera's x axis): cfg, Twc list, [(left, right)]."""
+    load_pkg()
+    import orbpl.synth as synth
+    cfg = dict(getattr(synth, cam_name))
+    room = synth.default_room(seed)
+    traj = synth.trajectory(n, seed=seed)
+    shift = np.eye(4)
+    shift[0, 3] = cfg["bf"] / cfg["fx"]
+    pairs = []
+    for i, T in enumerate(traj):
+        left, _ = synth.render(cfg, T, room, seed=seed * 100 + i)
+        right, _ = synth.render(cfg, T @ shift, room, seed=seed * 100 + i)
+        pairs.append((left, right))
+    return cfg, traj, pairs

@@ -219,6 +219,55 @@ def test_tracker_with_lines_matches_oracle_lvo(orbpl, oracle, pipelined):
     assert lt.shape[1] == 3 and np.all(lt >= 0)
 
 
+@pytest.mark.parametrize("pipelined", [False, True])
+def test_stereo_tracker_matches_oracle(orbpl, oracle, pipelined):
+    """Stereo tracker (ORBPL_TRACK_STEREO, KITTI 00 camera, 2000 features):
+    ORB on both images, batched ComputeStereoMatches, th = 7 matching and the
+    pose, against the oracle's stereo VO loop: identical counts every frame,
+    pose within POSE_TOL."""
+    from _scenes import stereo_sequence
+    S, F = 2, 4
+    seqs = [stereo_sequence(F, 50 + s) for s in range(S)]
+    cfg = seqs[0][0]
+    W, H = cfg["width"], cfg["height"]
+    lvo = oracle.LVO(oracle.params(2000), oracle.camera(cfg), S, use_lines=False)
+    tr = orbpl.Tracker(orbpl.OrbParams(2000, 1.2, 8, 20, 7), orbpl.make_camera(cfg), S, stereo=True)
+    tr.set_pipelined(pipelined)
+    T0 = np.stack([np.linalg.inv(sq[1][0]).astype(np.float32) for sq in seqs])
+    lvo.reset(T0.reshape(S, 16))
+    tr.reset(T0.reshape(S, 16))
+    left = orbpl.DeviceBuffer(S * W * H)
+    right = orbpl.DeviceBuffer(S * W * H)
+    for f in range(F):
+        left.upload(np.stack([sq[2][f][0] for sq in seqs]))
+        right.upload(np.stack([sq[2][f][1] for sq in seqs]))
+        tr.step_stereo_device(left.ptr, right.ptr)
+        tr.synchronize()
+        st, ls = tr.state(), tr.status()
+        for s in range(S):
+            To, so = lvo.step_stereo(s, *seqs[s][2][f])
+            got = dict(nkeypoints=st["nkeypoints"][s], nmatches=st["nmatches"][s],
+                       ninliers=st["ninliers"][s], nmatches_map=st["nmatches_map"][s],
+                       ok=ls["ok"][s], nlines=ls["nlines"][s], line_matches=ls["line_matches"][s],
+                       line_nmatches_map=ls["line_nmatches_map"][s])
+            assert {k: int(v) for k, v in got.items()} == so, (f, s)
+            assert np.abs(st["Tcw"][s] - To).max() < POSE_TOL, (f, s)
+        if f > 0:
+            assert st["nmatches"].min() >= 100
+    stt = tr.stereo_timings()
+    assert stt.shape[1] == 2 and np.all(stt >= 0)
+    with pytest.raises(RuntimeError):
+        tr.step_device(left.ptr, right.ptr)
+
+
+def test_stereo_tracker_rejects_lines(orbpl):
+    from _scenes import stereo_sequence
+    cfg = stereo_sequence(1, 50)[0]
+    with pytest.raises(RuntimeError):
+        orbpl.Tracker(orbpl.OrbParams(2000, 1.2, 8, 20, 7), orbpl.make_camera(cfg), 1, lines=True,
+                      stereo=True)
+
+
 @pytest.mark.parametrize("cam_name", ["TUM1", "TUM3"])
 def test_line_frame_prepare_bit_exact(orbpl, oracle, cam_name):
     cfg, _, fr = sequence(1, 41, cam_name=cam_name)

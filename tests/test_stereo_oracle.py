@@ -39,3 +39,18 @@ def test_stereo_no_right_keypoints(oracle):
     kl, dl, _ = oracle.extract(p, left)
     ur, d = oracle.stereo_matches(oracle.camera(cfg), p, left, right, kl, dl, kl[:0], dl[:0])
     assert np.all(ur == -1) and np.all(d == -1)
+
+
+def test_stereo_vo_follows_the_trajectory(oracle):
+    """The oracle's stereo TrackWithMotionModel loop (Frame(imLeft, imRight),
+    th = 7) tracks the rendered KITTI-camera sequence to a few mm."""
+    from _scenes import stereo_sequence
+    cfg, traj, pairs = stereo_sequence(3, 51)
+    lvo = oracle.LVO(oracle.params(2000), oracle.camera(cfg), 1, use_lines=False)
+    lvo.reset(np.linalg.inv(traj[0]).astype(np.float32).reshape(1, 16))
+    for f, (l, r) in enumerate(pairs):
+        T, st = lvo.step_stereo(0, l, r)
+        assert st["ok"] == 1 and st["nlines"] == 0
+        if f:
+            assert st["nmatches"] >= 100 and st["ninliers"] >= 0.8 * st["nmatches"]
+        assert np.abs(T - np.linalg.inv(traj[f])).max() < 5e-3
