@@ -54,29 +54,60 @@ WORKLOADS = {
                        "+ PoseOptimization (configs[3]; the reference's stereo Frame has no lines)",
                   data="synthetic (seeded textured-room rectified stereo loop, KITTI 00 intrinsics, "
                        "bf 386.1448)"),
+    "rig": dict(cam="RIG720", orb=(2000, 1.2, 8, 20, 7), lines=False, stereo=False, cams=8,
+                desc="synthetic 1280x720 8-camera rig (45 deg yaw spacing), RGB-D, ORB 2000 "
+                     "(configs[4]); stream 8r+c = camera c of rig r",
+                data="synthetic (seeded textured-room RGB-D loop of an 8-camera rig, 1280x720)"),
 }
 
 
+class Layout:
+    """Which rendered loop frame stream s reads at step t. cams == 1: stream s
+    reads loop frame (s + t) mod F. Rig (cams == 8): stream s = 8 r + c is
+    camera c of rig r and reads rig frame (r + t) mod F of camera c. Rendered
+    frames are ordered [frame][camera]; the device buffer replicates them so
+    that every step's batch is one contiguous slice starting at t * cams."""
+
+    def __init__(self, traj, cams=1):
+        import orbpl.synth as synth
+        self.traj, self.F, self.cams = traj, len(traj), cams
+        self.off = [synth.rig_offset(c, cams) if cams > 1 else np.eye(4) for c in range(cams)]
+
+    def elem(self, s, t):
+        r, c = divmod(s, self.cams)
+        return ((r + t) % self.F) * self.cams + c
+
+    def Twc(self, s, t):
+        r, c = divmod(s, self.cams)
+        return self.traj[(r + t) % self.F] @ self.off[c]
+
+    def replicated(self, S):
+        return np.arange((S // self.cams + self.F) * self.cams) % (self.F * self.cams)
+
+
 def _render(args):
-    i, n, seed, cam_name, stereo = args
+    e, n, seed, cam_name, stereo, cams = args
     from _pkg import load_pkg
     load_pkg()
     import orbpl.synth as synth
     traj = synth.loop_trajectory(n, seed=seed)
     room = synth.default_room(seed)
     cam = getattr(synth, cam_name)
-    g, d = synth.render(cam, traj[i], room, seed=seed * 1000 + i)
+    i, c = divmod(e, cams)
+    Twc = traj[i] @ synth.rig_offset(c, cams) if cams > 1 else traj[i]
+    g, d = synth.render(cam, Twc, room, seed=seed * 1000 + e)
     if stereo:  # right image of the rectified pair: camera at +mb along x
         shift = np.eye(4)
         shift[0, 3] = cam["bf"] / cam["fx"]
-        d, _ = synth.render(cam, traj[i] @ shift, room, seed=seed * 1000 + i)
+        d, _ = synth.render(cam, Twc @ shift, room, seed=seed * 1000 + e)
     return g, d
 
 
-def render_loop(n, seed, workers, cam_name="TUM1", stereo=False):
-    """(gray, depth) of an n-frame loop, or (left, right) for stereo."""
+def render_loop(n, seed, workers, cam_name="TUM1", stereo=False, cams=1):
+    """(gray, depth) of an n-frame loop ([frame][camera] for a rig), or
+    (left, right) for stereo."""
     with ProcessPoolExecutor(max_workers=workers) as ex:
-        out = list(ex.map(_render, [(i, n, seed, cam_name, stereo) for i in range(n)]))
+        out = list(ex.map(_render, [(e, n, seed, cam_name, stereo, cams) for e in range(n * cams)]))
     return np.stack([o[0] for o in out]), np.stack([o[1] for o in out])
 
 
@@ -142,7 +173,7 @@ def _oracle_vo(O, wl):
     return O.VO(O.params(*wl["orb"]), cam, 1), lambda vo, a, b: vo.step(0, a, b)
 
 
-def cpu_baseline(seconds, threads, gray, depth, workload="points"):
+def cpu_baseline(seconds, threads, gray, depth, L, workload="points"):
     """The CPU oracle (C++ restatement, oracle/) running the same per-frame
     step, one stream per thread (throughput mode), for a bounded wall time."""
     from _pkg import load_oracle
@@ -153,10 +184,10 @@ def cpu_baseline(seconds, threads, gray, depth, workload="points"):
 
     def worker(k):
         vo, vstep = _oracle_vo(O, wl)
-        n = len(gray)
         i = 0
-        while time.time() < stop:
-            vstep(vo, gray[(k + i) % n], depth[(k + i) % n])
+        while time.time() < stop:   # worker k runs stream k of the layout
+            e = L.elem(k, i)
+            vstep(vo, gray[e], depth[e])
             i += 1
         counts[k] = i
 
@@ -170,41 +201,43 @@ def cpu_baseline(seconds, threads, gray, depth, workload="points"):
     return sum(counts) / dt, sum(counts), dt
 
 
-def accuracy_gpu(pkg, cam, wl, d_gray, d_depth, traj, A, F, local_rank, fb, db):
+def accuracy_gpu(pkg, cam, wl, d_gray, d_depth, L, A, local_rank, fb, db):
     """Untimed accuracy leg: A streams tracked over a whole loop of F frames
-    (stream s starts at loop frame s at its true pose); returns the (A, F, 4, 4)
+    (Layout L, each stream starts at its true pose); returns the (A, F, 4, 4)
     Tcw poses after every step."""
+    F = L.F
     tr = pkg.Tracker(pkg.OrbParams(*wl["orb"]), cam, A, device=local_rank, lines=wl["lines"],
                      stereo=wl["stereo"])
-    tr.reset(np.stack([np.linalg.inv(traj[s % F]).astype(np.float32) for s in range(A)]).reshape(
+    tr.reset(np.stack([np.linalg.inv(L.Twc(s, 0)).astype(np.float32) for s in range(A)]).reshape(
         A, 16))
     out = np.zeros((A, F, 4, 4), np.float32)
     for t in range(F):
+        o = t * L.cams
         if wl["stereo"]:
-            tr.step_stereo_device(d_gray.ptr + t * fb, d_depth.ptr + t * db)
+            tr.step_stereo_device(d_gray.ptr + o * fb, d_depth.ptr + o * db)
         else:
-            tr.step_device(d_gray.ptr + t * fb, d_depth.ptr + t * db)
+            tr.step_device(d_gray.ptr + o * fb, d_depth.ptr + o * db)
         tr.synchronize()
         out[:, t] = tr.state()["Tcw"]
     tr.close()
     return out
 
 
-def accuracy_ref(gray, depth, traj, A, workload):
+def accuracy_ref(gray, depth, L, A, workload):
     """The oracle's VO loop (the reference restatement) over the same A x F
     frames, one host thread per stream; returns its (A, F, 4, 4) poses."""
     from _pkg import load_oracle
     O = load_oracle()
     wl = WORKLOADS[workload]
-    F = len(gray)
+    F = L.F
     out = np.zeros((A, F, 4, 4), np.float32)
 
     def worker(s):
         vo, vstep = _oracle_vo(O, wl)
-        vo.reset(np.linalg.inv(traj[s % F]).astype(np.float32).reshape(1, 16))
+        vo.reset(np.linalg.inv(L.Twc(s, 0)).astype(np.float32).reshape(1, 16))
         for t in range(F):
-            f = (s + t) % F
-            out[s, t] = vstep(vo, gray[f], depth[f])[0]
+            e = L.elem(s, t)
+            out[s, t] = vstep(vo, gray[e], depth[e])[0]
 
     ths = [threading.Thread(target=worker, args=(s,)) for s in range(A)]
     for t in ths:
@@ -214,13 +247,13 @@ def accuracy_ref(gray, depth, traj, A, workload):
     return out
 
 
-def ate_report(T_gpu, T_ref, traj):
+def ate_report(T_gpu, T_ref, L):
     """ATE RMSE (m) of the GPU poses vs the reference restatement's poses of
     the same frames (raw: both start at the same pose) and of both vs the
     ground truth (rigidly aligned, as TUM's evaluate_ate)."""
     import orbpl.tum as tum
     A, F = T_gpu.shape[:2]
-    gt = np.stack([np.linalg.inv(traj[(s + t) % F]) for s in range(A) for t in range(F)])
+    gt = np.stack([np.linalg.inv(L.Twc(s, t)) for s in range(A) for t in range(F)])
     cg = tum.camera_centres(T_gpu.reshape(-1, 4, 4))
     cgt = tum.camera_centres(gt)
     rep = {"streams": A, "frames_per_stream": F,
@@ -237,26 +270,30 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, loca
     """Time `steps` tracker steps of one workload; returns the measurements."""
     wl = WORKLOADS[workload]
     lines, stereo, cam_name = wl["lines"], wl["stereo"], wl["cam"]
-    F = args.loop
+    cams = wl.get("cams", 1)
+    F = args.loop if cams == 1 else args.rig_loop
+    if S % cams:
+        raise SystemExit(f"--streams must be a multiple of the rig's {cams} cameras")
     workers = min(16, os.cpu_count() or 4)
-    gray, depth = render_loop(F, seed=1 + rank, workers=workers, cam_name=cam_name, stereo=stereo)
+    gray, depth = render_loop(F, seed=1 + rank, workers=workers, cam_name=cam_name, stereo=stereo,
+                              cams=cams)
     fh, fw = gray.shape[1:]
-    # stream s at step t reads loop frame (s + t) mod F: a contiguous window of
-    # a (S + F)-frame replicated buffer, so every step's batch is one slice.
-    rep = np.arange(S + F) % F
+    traj = synth.loop_trajectory(F, seed=1 + rank)
+    L = Layout(traj, cams)
+    # every step's batch is one contiguous slice of a replicated buffer (Layout)
+    rep = L.replicated(S)
     d_gray = pkg.DeviceBuffer.from_array(gray[rep], device=local_rank)
     d_depth = pkg.DeviceBuffer.from_array(depth[rep], device=local_rank)
     cam = pkg.make_camera(getattr(synth, cam_name))
     tr = pkg.Tracker(pkg.OrbParams(*wl["orb"]), cam, S, device=local_rank, lines=lines,
                      stereo=stereo)
     tr.set_pipelined(bool(args.pipelined))
-    traj = synth.loop_trajectory(F, seed=1 + rank)
-    tr.reset(np.stack([np.linalg.inv(traj[s % F]).astype(np.float32) for s in range(S)]).reshape(S, 16))
+    tr.reset(np.stack([np.linalg.inv(L.Twc(s, 0)).astype(np.float32) for s in range(S)]).reshape(S, 16))
     fb = fw * fh
     db = fb * depth.itemsize   # right image (u8) for stereo, depth (f32) otherwise
 
     def step(k):
-        o = k % F
+        o = (k % F) * cams
         if stereo:
             tr.step_stereo_device(d_gray.ptr + o * fb, d_depth.ptr + o * db)
         else:
@@ -322,9 +359,9 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, loca
                                 for k in names}}
     tr.close()
     A = min(args.ate_streams, S)
-    T_acc = (accuracy_gpu(pkg, cam, wl, d_gray, d_depth, traj, A, F, local_rank, fb, db)
+    T_acc = (accuracy_gpu(pkg, cam, wl, d_gray, d_depth, L, A, local_rank, fb, db)
              if A > 0 else None)
-    return dict(S=S, value=value, T_acc=T_acc, traj=traj, elapsed=elapsed, stages=stages,
+    return dict(S=S, value=value, T_acc=T_acc, layout=L, elapsed=elapsed, stages=stages,
                 tracking=tracking, roof=roof, gray=gray, depth=depth, workload=wl["desc"],
                 data=wl["data"], image=f"{fw}x{fh}", nfeatures=wl["orb"][0])
 
@@ -339,9 +376,11 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=("points", "lines", "kitti"), default="points",
+    ap.add_argument("--workload", choices=tuple(WORKLOADS), default="points",
                     help="points = configs[1] (headline); lines = configs[2] ORB + LSD/LBD; "
-                         "kitti = configs[3] stereo")
+                         "kitti = configs[3] stereo; rig = configs[4] 1280x720 8-camera rig")
+    ap.add_argument("--rig-loop", type=int, default=12,
+                    help="rig frames in the synthetic loop (x8 camera renders)")
     ap.add_argument("--secondary-steps", type=int, default=3,
                     help="steps of the configs[2] lines workload reported under 'secondary' "
                          "(points runs only; 0 = skip)")
@@ -350,6 +389,10 @@ def main():
                     help="steps of the configs[3] stereo workload reported under 'stereo' "
                          "(points runs only; 0 = skip)")
     ap.add_argument("--stereo-streams", type=int, default=256)
+    ap.add_argument("--rig-steps", type=int, default=3,
+                    help="steps of the configs[4] 8-camera rig workload reported under 'rig' "
+                         "(points runs only; 0 = skip)")
+    ap.add_argument("--rig-streams", type=int, default=256, help="rig cameras per GPU (x8)")
     ap.add_argument("--ate-streams", type=int, default=8,
                     help="streams of the untimed accuracy leg (ATE vs ground truth and vs the "
                          "reference restatement over one loop); 0 = skip")
@@ -373,7 +416,8 @@ def main():
     res = run_workload(pkg, synth, args, args.workload, args.streams, args.steps, args.warmup,
                        rank, world, local_rank, dist)
     # other BASELINE configs, same clock discipline, fewer steps (points runs only):
-    # configs[2] (ORB + LSD/LBD lines) under "secondary", configs[3] (stereo) under "stereo"
+    # configs[2] (ORB + LSD/LBD lines) under "secondary", configs[3] (stereo) under "stereo",
+    # configs[4] (1280x720 8-camera rig) under "rig"
     others = {}
     if args.workload == "points" and args.secondary_steps > 0:
         others["secondary"] = ("lines", run_workload(
@@ -383,17 +427,21 @@ def main():
         others["stereo"] = ("kitti", run_workload(
             pkg, synth, args, "kitti", args.stereo_streams, args.stereo_steps,
             max(1, args.warmup // 2), rank, world, local_rank, dist), args.stereo_steps)
+    if args.workload == "points" and args.rig_steps > 0:
+        others["rig"] = ("rig", run_workload(
+            pkg, synth, args, "rig", args.rig_streams, args.rig_steps,
+            max(1, args.warmup // 2), rank, world, local_rank, dist), args.rig_steps)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         thr = args.cpu_threads or min(16, os.cpu_count() or 1)
         fps, nfr, dt = cpu_baseline(args.cpu_seconds, thr, res["gray"], res["depth"],
-                                    args.workload)
+                                    res["layout"], args.workload)
         if res["T_acc"] is not None:
-            res["T_ref"] = accuracy_ref(res["gray"], res["depth"], res["traj"],
+            res["T_ref"] = accuracy_ref(res["gray"], res["depth"], res["layout"],
                                         len(res["T_acc"]), args.workload)
         for key, (wname, o, _) in others.items():
             if o["T_acc"] is not None:
-                o["T_ref"] = accuracy_ref(o["gray"], o["depth"], o["traj"], len(o["T_acc"]), wname)
+                o["T_ref"] = accuracy_ref(o["gray"], o["depth"], o["layout"], len(o["T_acc"]), wname)
         cpu = {"value": round(fps, 2), "unit": "frames/s", "cores": thr, "kind": "port",
                "sample": f"{nfr} frames of the same {res['image']} loop in {dt:.1f} s, oracle/ "
                          f"C++ restatement ({args.workload} workload), one stream per thread"}
@@ -422,7 +470,7 @@ def main():
             "cpu_baseline": cpu,
         }
         if res["T_acc"] is not None:
-            out["accuracy"] = ate_report(res["T_acc"], res.get("T_ref"), res["traj"])
+            out["accuracy"] = ate_report(res["T_acc"], res.get("T_ref"), res["layout"])
         for key, (wname, o, nsteps) in others.items():
             out[key] = {
                 "workload": o["workload"], "value": round(o["value"], 2),
@@ -432,11 +480,11 @@ def main():
                 "stage_ms": o["stages"], "tracking": o["tracking"], "roofline": o["roof"],
                 "data": o["data"]}
             if o["T_acc"] is not None:
-                out[key]["accuracy"] = ate_report(o["T_acc"], o.get("T_ref"), o["traj"])
+                out[key]["accuracy"] = ate_report(o["T_acc"], o.get("T_ref"), o["layout"])
             if cpu is not None:
                 thr = cpu["cores"]
                 fps, nfr, dt = cpu_baseline(args.cpu_seconds / 2, thr, o["gray"], o["depth"],
-                                            wname)
+                                            o["layout"], wname)
                 out[key]["cpu_baseline"] = {
                     "value": round(fps, 2), "unit": "frames/s", "cores": thr, "kind": "port",
                     "sample": f"{nfr} frames in {dt:.1f} s, oracle/ C++ restatement "

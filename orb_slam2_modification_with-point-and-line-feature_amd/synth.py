@@ -26,6 +26,18 @@ KITTI00 = dict(fx=718.856, fy=718.856, cx=607.1928, cy=185.2157, k1=0.0, k2=0.0,
                p2=0.0, k3=0.0, width=1241, height=376, bf=386.1448, thdepth=35.0,
                depth_factor=1.0)
 
+# BASELINE configs[4]: synthetic 1280x720 camera of an 8-camera rig (no
+# distortion, 90 deg horizontal field of view, RGB-D depth)
+RIG720 = dict(fx=640.0, fy=640.0, cx=639.5, cy=359.5, k1=0.0, k2=0.0, p1=0.0, p2=0.0, k3=0.0,
+              width=1280, height=720, bf=40.0, thdepth=40.0, depth_factor=5000.0)
+RIG_CAMERAS = 8
+
+
+def rig_offset(k, n=RIG_CAMERAS):
+    """Camera-to-rig pose of rig camera k: yaw k * 360/n degrees (45 deg spacing
+    for 8 cameras) about the rig's y axis, shared optical centre."""
+    return se3(rot_xyz(0.0, 2 * np.pi * k / n, 0.0), np.zeros(3))
+
 
 def _hash2(ix, iy, seed):
     """uint32 hash of integer lattice coordinates -> float in [0, 1)."""

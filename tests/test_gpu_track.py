@@ -260,6 +260,42 @@ def test_stereo_tracker_matches_oracle(orbpl, oracle, pipelined):
         tr.step_device(left.ptr, right.ptr)
 
 
+def test_tracker_rig_720p_matches_oracle(orbpl, oracle):
+    """configs[4] geometry: two cameras of the synthetic 1280x720 8-camera rig
+    (RGB-D, ORB 2000) tracked for 3 frames, identical counts, pose within
+    POSE_TOL of the oracle VO loop."""
+    load_pkg = __import__("_pkg").load_pkg
+    load_pkg()
+    import orbpl.synth as synth
+    cfg = dict(synth.RIG720)
+    traj = synth.loop_trajectory(12, seed=3)
+    room = synth.default_room(3)
+    cams = (0, 3)
+    S, F = len(cams), 3
+    frames = [[synth.render(cfg, traj[t] @ synth.rig_offset(c), room, seed=30 + 8 * t + c)
+               for c in cams] for t in range(F)]
+    vo = oracle.VO(oracle.params(2000), oracle.camera(cfg), S)
+    tr = orbpl.Tracker(orbpl.OrbParams(2000, 1.2, 8, 20, 7), orbpl.make_camera(cfg), S)
+    T0 = np.stack([np.linalg.inv(traj[0] @ synth.rig_offset(c)).astype(np.float32) for c in cams])
+    vo.reset(T0.reshape(S, 16))
+    tr.reset(T0.reshape(S, 16))
+    W, H = cfg["width"], cfg["height"]
+    gray = orbpl.DeviceBuffer(S * W * H)
+    depth = orbpl.DeviceBuffer(S * W * H * 4)
+    for t in range(F):
+        gray.upload(np.stack([g for g, _ in frames[t]]))
+        depth.upload(np.stack([d for _, d in frames[t]]))
+        tr.step_device(gray.ptr, depth.ptr)
+        tr.synchronize()
+        st = tr.state()
+        for s in range(S):
+            To, so = vo.step(s, *frames[t][s])
+            assert st["nkeypoints"][s] == so["nkeypoints"]
+            assert st["nmatches"][s] == so["nmatches"], (t, s)
+            assert st["ninliers"][s] == so["ninliers"], (t, s)
+            assert np.abs(st["Tcw"][s] - To).max() < POSE_TOL, (t, s)
+
+
 def test_stereo_tracker_rejects_lines(orbpl):
     from _scenes import stereo_sequence
     cfg = stereo_sequence(1, 50)[0]
