@@ -396,7 +396,7 @@ def main():
     ap.add_argument("--ate-streams", type=int, default=8,
                     help="streams of the untimed accuracy leg (ATE vs ground truth and vs the "
                          "reference restatement over one loop); 0 = skip")
-    ap.add_argument("--pipelined", type=int, default=0,
+    ap.add_argument("--pipelined", type=int, default=1,
                     help="1 = overlap extraction of step t+1 with tracking of step t")
     args = ap.parse_args()
 

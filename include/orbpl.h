@@ -137,6 +137,10 @@ int orbx_synchronize(orbx_ctx* ctx);
  * (pyramid, blur, fast, octree, desc) measured with hipEvents on the ctx
  * stream. */
 int orbx_last_stage_ms(const orbx_ctx* ctx, float* ms5);
+/* Debug: k_pyramid phase times (ns) of block (band 0, frame 0) in the last
+ * launch, 4 per level (content, side borders, mirror rows, blur); needs
+ * ORBPL_PYR_PROFILE in the environment when the context is created. */
+int orbx_debug_pyr_profile(orbx_ctx* ctx, long long* out, int cap, int* n);
 
 
 /* ------------------------------------------------------------------------

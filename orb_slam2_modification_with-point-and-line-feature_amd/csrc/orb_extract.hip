@@ -3,8 +3,8 @@
 //
 // Pipeline per batch of frames (all kernels take the frame index from
 // blockIdx.y/z, so one launch covers the whole batch):
-//   k_pyr_level0 / k_pyr_level : ComputePyramid  (ORBextractor.cc:1107-1132)
-//   k_blur                     : GaussianBlur 7x7 s=2 per level (:1084-1086)
+//   k_pyramid                  : ComputePyramid (ORBextractor.cc:1107-1132) +
+//                                GaussianBlur 7x7 s=2 per level (:1084-1086)
 //   k_fast_cells               : per-cell FAST(20) -> FAST(7) fallback (:789-827)
 //   k_octree                   : DistributeOctTree (:539-763) + border/octave (:837-847)
 //   k_orient_desc              : IC_Angle (:77-104) + computeOrbDescriptor (:108-147)
@@ -29,209 +29,6 @@ __device__ __forceinline__ int reflect101_dev(int p, int len) {
   if (p < 0) p = -p;
   if (p >= len) p = 2 * len - 2 - p;
   return p;
-}
-
-// ---------------------------------------------------------------------------
-// Pyramid level 0 content: the input image, 16 bytes per thread into the
-// 16-B aligned content rows (ORBextractor.cc:1127 minus the border, which
-// k_pyr_border fills for every level at the end).
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_pyr_level0(const uint8_t* __restrict__ img, int stride,
-                                                    long long frame_pitch,
-                                                    uint8_t* __restrict__ pyr,
-                                                    const OrbGeom* __restrict__ g) {
-  const LevelGeom& L = g->lv[0];
-  const int f = blockIdx.z;
-  const int x0 = (blockIdx.x * 64 + threadIdx.x) * 16;
-  const int y = blockIdx.y * 4 + threadIdx.y;
-  if (x0 >= L.w || y >= L.h) return;
-  const uint8_t* src = img + (long long)f * frame_pitch + (long long)y * stride + x0;
-  uint8_t* dst = pyr + (long long)f * g->pyr_bytes + content_off(L, x0, y);
-  if (x0 + 16 <= L.w && ((reinterpret_cast<uintptr_t>(src) & 15) == 0)) {
-    *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
-  } else {
-    const int n = min(16, L.w - x0);
-    for (int k = 0; k < n; k++) dst[k] = src[k];
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Pyramid level l >= 1 content: resize(level l-1, INTER_LINEAR) in OpenCV's 8U
-// fixed-point form (11-bit coefficients, (S>>4)*beta>>16, +2>>2). One
-// 256-thread block per 128x16 content tile: the source window (<= 64 dwords x
-// 48 rows) is staged in LDS with aligned dword loads, each item produces 4
-// output pixels and one aligned u32 store. rs: xofs[w], alpha[w] (a0|a1<<16),
-// yofs[h], beta[h] of this level.
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_pyr_level(uint8_t* __restrict__ pyr,
-                                                   const OrbGeom* __restrict__ g, int level,
-                                                   const int* __restrict__ rs_all) {
-  __shared__ uint32_t win[kPyrSrcRows][kPyrSrcDw + 1];
-  const LevelGeom& L = g->lv[level];
-  const LevelGeom& S = g->lv[level - 1];
-  const int f = blockIdx.y;
-  const int ntx = (L.w + kPyrTileW - 1) / kPyrTileW;
-  const int tx = blockIdx.x % ntx, ty = blockIdx.x / ntx;
-  const int x0 = tx * kPyrTileW, y0 = ty * kPyrTileH;
-  const int x1 = min(x0 + kPyrTileW, L.w), y1 = min(y0 + kPyrTileH, L.h);
-  const int* rs = rs_all + L.rs_off;
-  const int* xofs = rs;
-  const int* alpha = rs + L.w;
-  const int* yofs = rs + 2 * L.w;
-  const int* beta = rs + 2 * L.w + L.h;
-  uint8_t* fp = pyr + (long long)f * g->pyr_bytes;
-  const int a = xofs[x0] & ~3;
-  const int xb = min(xofs[x1 - 1] + 1, S.w - 1);
-  const int ndw = (xb + 1 - a + 3) >> 2;
-  const int ya = min(max(yofs[y0], 0), S.h - 1);
-  const int yb = min(max(yofs[y1 - 1] + 1, 0), S.h - 1);
-  const int nrows = yb - ya + 1;
-  const int t = threadIdx.x;
-  for (int i = t; i < nrows * ndw; i += 256) {
-    const int r = i / ndw, d = i - r * ndw;
-    win[r][d] = *reinterpret_cast<const uint32_t*>(fp + content_off(S, a + 4 * d, ya + r));
-  }
-  __syncthreads();
-  const uint8_t* wb = reinterpret_cast<const uint8_t*>(&win[0][0]);
-  constexpr int kRowB = (kPyrSrcDw + 1) * 4;
-  const int groups = (x1 - x0 + 3) >> 2;
-  for (int i = t; i < (y1 - y0) * groups; i += 256) {
-    const int r = i / groups, gq = i - r * groups;
-    const int y = y0 + r, x = x0 + 4 * gq;
-    const int sy0 = yofs[y];
-    const int r0 = min(max(sy0, 0), S.h - 1) - ya, r1 = min(max(sy0 + 1, 0), S.h - 1) - ya;
-    const int bpk = beta[y];
-    const int b0 = (int)(short)(bpk & 0xFFFF), b1 = (int)(short)(bpk >> 16);
-    uint32_t packed = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int cx = min(x + k, L.w - 1);
-      const int sx = xofs[cx] - a;
-      int h0, h1;
-      if (cx < L.xmax) {
-        const int apk = alpha[cx];
-        const int a0 = (int)(short)(apk & 0xFFFF), a1 = (int)(short)(apk >> 16);
-        h0 = wb[r0 * kRowB + sx] * a0 + wb[r0 * kRowB + sx + 1] * a1;
-        h1 = wb[r1 * kRowB + sx] * a0 + wb[r1 * kRowB + sx + 1] * a1;
-      } else {
-        h0 = wb[r0 * kRowB + sx] * 2048;
-        h1 = wb[r1 * kRowB + sx] * 2048;
-      }
-      const uint32_t v = (uint32_t)((((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2);
-      packed |= v << (8 * k);
-    }
-    // columns >= w of the last group land in the border, rewritten by k_pyr_border
-    *reinterpret_cast<uint32_t*>(fp + content_off(L, x, y)) = packed;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// copyMakeBorder(19, REFLECT_101[|ISOLATED]) of every level, one launch after
-// all levels exist (ORBextractor.cc:1122-1128): border pixel i of a level is
-// enumerated as 19 full top rows, 38 side pixels per content row, 19 full
-// bottom rows.
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_pyr_border(uint8_t* __restrict__ pyr,
-                                                    const OrbGeom* __restrict__ g) {
-  const int f = blockIdx.y;
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= g->border_total) return;
-  int level = 0;
-  while (level + 1 < g->nlevels && i >= g->lv[level + 1].border_base) level++;
-  const LevelGeom& L = g->lv[level];
-  int idx = i - L.border_base;
-  int px, py;
-  const int top = kEdge * L.pw;
-  if (idx < top) {
-    py = idx / L.pw;
-    px = idx - py * L.pw;
-  } else if ((idx -= top) < 2 * kEdge * L.h) {
-    py = kEdge + idx / (2 * kEdge);
-    const int k = idx - (py - kEdge) * (2 * kEdge);
-    px = k < kEdge ? k : L.w + k;
-  } else {
-    idx -= 2 * kEdge * L.h;
-    py = kEdge + L.h + idx / L.pw;
-    px = idx - (py - kEdge - L.h) * L.pw;
-  }
-  uint8_t* fp = pyr + (long long)f * g->pyr_bytes;
-  const int cx = reflect101_dev(px - kEdge, L.w), cy = reflect101_dev(py - kEdge, L.h);
-  fp[padded_off(L, px, py)] = fp[content_off(L, cx, cy)];
-}
-
-// ---------------------------------------------------------------------------
-// GaussianBlur(7x7, sigma 2, REFLECT_101), 8U fixed-point path (pinned P4):
-// out = (sum_v kv * sum_u ku * I + 2^15) >> 16 with k = {18,34,49,54,49,34,18}.
-// The padded pyramid already holds the REFLECT_101 border, so a 128x32 output
-// tile reads its 140x38-byte input window straight from it with aligned dword
-// loads (content column x sits at padded column x + 19; the window starts at
-// padded column ox + 12, a multiple of 4). Horizontal pass: 4 outputs per
-// item from 3 LDS dwords; vertical pass: 4 outputs per item, one aligned u32
-// store into the content-only blurred level (row pitch bpitch).
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_blur(const uint8_t* __restrict__ pyr,
-                                              uint8_t* __restrict__ blur,
-                                              const OrbGeom* __restrict__ g) {
-  constexpr int TW = kBlurTileW, TH = kBlurTileH;
-  constexpr int IW = (TW + 32) / 4;          // input dwords per row: content ox-16 .. ox+143
-  __shared__ uint32_t tin[TH + 6][IW + 1];
-  __shared__ int4 tmid[TH + 6][TW / 4];
-  const int f = blockIdx.y;
-  int tile = blockIdx.x;
-  int level = 0;
-  while (level + 1 < g->nlevels && tile >= g->lv[level + 1].blur_tile_base) level++;
-  const LevelGeom& L = g->lv[level];
-  tile -= L.blur_tile_base;
-  const int tx = tile % L.blur_tiles_x, ty = tile / L.blur_tiles_x;
-  const int ox = tx * TW, oy = ty * TH;  // content coords of the tile origin
-  const uint8_t* src = pyr + (long long)f * g->pyr_bytes + L.pyr_off;
-  const int t = threadIdx.x;
-  for (int i = t; i < (TH + 6) * IW; i += 256) {
-    const int r = i / IW, d = i - r * IW;
-    const int py = oy + (kEdge - 3) + r;            // padded row of content row oy-3+r
-    const int bc = kContent0 - 16 + ox + 4 * d;      // byte column in the row (multiple of 4)
-    uint32_t v = 0;
-    if (py < L.ph && bc + 4 <= L.pitch)
-      v = *reinterpret_cast<const uint32_t*>(src + (long long)py * L.pitch + bc);
-    tin[r][d] = v;
-  }
-  __syncthreads();
-  const int k0 = 18, k1 = 34, k2 = 49, k3 = 54;
-  for (int i = t; i < (TH + 6) * (TW / 4); i += 256) {
-    const int r = i / (TW / 4), gq = i - r * (TW / 4);
-    // LDS byte j holds content column ox - 16 + j; x = ox + 4gq needs x-3 .. x+6,
-    // i.e. bytes 4gq+13 .. 4gq+22 = dwords gq+3 .. gq+5 starting at byte 1
-    const uint32_t w0 = tin[r][gq + 3], w1 = tin[r][gq + 4], w2 = tin[r][gq + 5];
-    int b[10];
-    b[0] = (w0 >> 8) & 0xFF; b[1] = (w0 >> 16) & 0xFF; b[2] = w0 >> 24;
-    b[3] = w1 & 0xFF; b[4] = (w1 >> 8) & 0xFF; b[5] = (w1 >> 16) & 0xFF; b[6] = w1 >> 24;
-    b[7] = w2 & 0xFF; b[8] = (w2 >> 8) & 0xFF; b[9] = (w2 >> 16) & 0xFF;
-    int4 h;
-    h.x = k0 * (b[0] + b[6]) + k1 * (b[1] + b[5]) + k2 * (b[2] + b[4]) + k3 * b[3];
-    h.y = k0 * (b[1] + b[7]) + k1 * (b[2] + b[6]) + k2 * (b[3] + b[5]) + k3 * b[4];
-    h.z = k0 * (b[2] + b[8]) + k1 * (b[3] + b[7]) + k2 * (b[4] + b[6]) + k3 * b[5];
-    h.w = k0 * (b[3] + b[9]) + k1 * (b[4] + b[8]) + k2 * (b[5] + b[7]) + k3 * b[6];
-    tmid[r][gq] = h;
-  }
-  __syncthreads();
-  uint8_t* dst = blur + (long long)f * g->blur_bytes + L.boff;
-  for (int i = t; i < TH * (TW / 4); i += 256) {
-    const int r = i / (TW / 4), gq = i - r * (TW / 4);
-    const int x = ox + 4 * gq, y = oy + r;
-    if (x >= L.w || y >= L.h) continue;
-    const int4 a0 = tmid[r][gq], a1 = tmid[r + 1][gq], a2 = tmid[r + 2][gq], a3 = tmid[r + 3][gq],
-               a4 = tmid[r + 4][gq], a5 = tmid[r + 5][gq], a6 = tmid[r + 6][gq];
-    auto vsum = [&](int v0, int v1, int v2, int v3, int v4, int v5, int v6) -> uint32_t {
-      int acc = k0 * (v0 + v6) + k1 * (v1 + v5) + k2 * (v2 + v4) + k3 * v3;
-      int v = (acc + (1 << 15)) >> 16;
-      return (uint32_t)(v > 255 ? 255 : v);
-    };
-    const uint32_t o = vsum(a0.x, a1.x, a2.x, a3.x, a4.x, a5.x, a6.x) |
-                       (vsum(a0.y, a1.y, a2.y, a3.y, a4.y, a5.y, a6.y) << 8) |
-                       (vsum(a0.z, a1.z, a2.z, a3.z, a4.z, a5.z, a6.z) << 16) |
-                       (vsum(a0.w, a1.w, a2.w, a3.w, a4.w, a5.w, a6.w) << 24);
-    *reinterpret_cast<uint32_t*>(dst + (long long)y * L.bpitch + x) = o;
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -324,6 +121,226 @@ __device__ __forceinline__ uint32_t div_inv(int n) {
 }
 __device__ __forceinline__ int div_small(int k, uint32_t inv) {
   return inv ? (int)__umulhi((uint32_t)k, inv) : k;
+}
+
+// ---------------------------------------------------------------------------
+// ComputePyramid (ORBextractor.cc:1107-1132) and the per-level GaussianBlur
+// (:1084-1086) in ONE launch. Block (band b, frame f) owns content rows
+// [oa, ob) of every level and computes, level after level:
+//   1. content rows [na, nb) (own rows plus the halo the next level and the
+//      blur need; host-computed, PyrBand): level 0 = the input image, level
+//      l >= 1 = resize(level l-1, INTER_LINEAR) in OpenCV's 8U fixed point
+//      (11-bit coefficients, (S>>4)*beta>>16, +2>>2) from full-width source
+//      row chunks staged in LDS;
+//   2. copyMakeBorder(19, REFLECT_101[|ISOLATED]): the 19+19 side pixels of
+//      rows [na, nb), then every top/bottom mirror row whose source row lies
+//      in [na, nb) (a whole padded row copy);
+//   3. the 7x7 sigma=2 blur of the own rows [oa, ob) from the padded level
+//      (pinned P4: out = (sum_v kv sum_u ku I + 2^15) >> 16, k = {18,34,49,
+//      54,49,34,18}; the horizontal sums fit u16 and stay in LDS).
+// Halo rows are computed by both neighbouring bands with identical values and
+// every store writes exactly its own bytes, so the overlaps are benign. A
+// level's rows are only read after the block's own __syncthreads.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void pyr_resize_rows(const LevelGeom& L, const LevelGeom& S,
+                                                const int* __restrict__ rs, uint8_t* fp, int na,
+                                                int nb, uint32_t* psm) {
+  const int t = threadIdx.x;
+  const int* xofs = rs;
+  const int* alpha = rs + L.w;
+  const int* yofs = rs + 2 * L.w;
+  const int* beta = rs + 2 * L.w + L.h;
+  const int ndw = (S.w + 3) >> 2;      // dwords of a source content row
+  const int rstride = ndw + 1;         // LDS row stride (odd: fewer bank conflicts)
+  const int rowB = rstride * 4;
+  const int groups = (L.w + 3) >> 2;   // 4 output pixels per item
+  const uint32_t inv_ndw = div_inv(ndw), inv_groups = div_inv(groups);
+  const uint8_t* wb = reinterpret_cast<const uint8_t*>(psm);
+  for (int y0 = na; y0 < nb; y0 += L.rchunk) {
+    const int y1 = min(y0 + L.rchunk, nb);
+    const int ya = min(max(yofs[y0], 0), S.h - 1);
+    const int yb = min(max(yofs[y1 - 1] + 1, 0), S.h - 1);
+    const int nrows = yb - ya + 1;
+    for (int i = t; i < nrows * ndw; i += kPyrThreads) {
+      const int r = div_small(i, inv_ndw), d = i - r * ndw;
+      psm[r * rstride + d] = *reinterpret_cast<const uint32_t*>(fp + content_off(S, 4 * d, ya + r));
+    }
+    __syncthreads();
+    for (int i = t; i < (y1 - y0) * groups; i += kPyrThreads) {
+      const int r = div_small(i, inv_groups), gq = i - r * groups;
+      const int y = y0 + r, x = 4 * gq;
+      const int sy0 = yofs[y];
+      const int r0 = min(max(sy0, 0), S.h - 1) - ya, r1 = min(max(sy0 + 1, 0), S.h - 1) - ya;
+      const int bpk = beta[y];
+      const int b0 = (int)(short)(bpk & 0xFFFF), b1 = (int)(short)(bpk >> 16);
+      uint32_t packed = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int cx = min(x + k, L.w - 1);
+        const int sx = xofs[cx];
+        int h0, h1;
+        if (cx < L.xmax) {
+          const int apk = alpha[cx];
+          const int a0 = (int)(short)(apk & 0xFFFF), a1 = (int)(short)(apk >> 16);
+          h0 = wb[r0 * rowB + sx] * a0 + wb[r0 * rowB + sx + 1] * a1;
+          h1 = wb[r1 * rowB + sx] * a0 + wb[r1 * rowB + sx + 1] * a1;
+        } else {
+          h0 = wb[r0 * rowB + sx] * 2048;
+          h1 = wb[r1 * rowB + sx] * 2048;
+        }
+        const uint32_t v = (uint32_t)((((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2);
+        packed |= v << (8 * k);
+      }
+      uint8_t* dst = fp + content_off(L, x, y);
+      if (x + 4 <= L.w) {
+        *reinterpret_cast<uint32_t*>(dst) = packed;
+      } else {  // last partial group: the border bytes belong to step 2
+        for (int k = 0; k < L.w - x; k++) dst[k] = (uint8_t)(packed >> (8 * k));
+      }
+    }
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ void pyr_blur_rows(const LevelGeom& L, const uint8_t* fp, uint8_t* bp,
+                                              int oa, int ob, uint32_t* psm) {
+  const int t = threadIdx.x;
+  const int G4 = (L.w + 3) >> 2;       // output groups of 4 pixels per row
+  const int ndw = G4 + 2;              // staged dwords per row: content cols -4 .. 4*G4+3
+  const int rstride = ndw + 1;
+  const int BCH = L.bchunk;
+  uint32_t* tin = psm;
+  uint16_t* tmid = reinterpret_cast<uint16_t*>(psm + (((BCH + 6) * rstride + 1) & ~1));
+  const int mstride = 4 * G4;          // u16 per row of horizontal sums
+  const uint32_t inv_ndw = div_inv(ndw), inv_g4 = div_inv(G4);
+  const int k0 = 18, k1 = 34, k2 = 49, k3 = 54;
+  for (int y0 = oa; y0 < ob; y0 += BCH) {
+    const int y1 = min(y0 + BCH, ob);
+    const int nr = y1 - y0 + 6;
+    for (int i = t; i < nr * ndw; i += kPyrThreads) {
+      const int r = div_small(i, inv_ndw), d = i - r * ndw;
+      const int py = y0 - 3 + r + kEdge;                 // padded row
+      tin[r * rstride + d] = *reinterpret_cast<const uint32_t*>(
+          fp + L.pyr_off + (long long)py * L.pitch + kContent0 - 4 + 4 * d);
+    }
+    __syncthreads();
+    for (int i = t; i < nr * G4; i += kPyrThreads) {
+      const int r = div_small(i, inv_g4), gq = i - r * G4;
+      // LDS byte j of a row holds content column j - 4; x = 4 gq needs
+      // columns x-3 .. x+6 = bytes 4gq+1 .. 4gq+10 = dwords gq .. gq+2
+      const uint32_t w0 = tin[r * rstride + gq], w1 = tin[r * rstride + gq + 1],
+                     w2 = tin[r * rstride + gq + 2];
+      int b[10];
+      b[0] = (w0 >> 8) & 0xFF; b[1] = (w0 >> 16) & 0xFF; b[2] = w0 >> 24;
+      b[3] = w1 & 0xFF; b[4] = (w1 >> 8) & 0xFF; b[5] = (w1 >> 16) & 0xFF; b[6] = w1 >> 24;
+      b[7] = w2 & 0xFF; b[8] = (w2 >> 8) & 0xFF; b[9] = (w2 >> 16) & 0xFF;
+      const uint32_t h0 = k0 * (b[0] + b[6]) + k1 * (b[1] + b[5]) + k2 * (b[2] + b[4]) + k3 * b[3];
+      const uint32_t h1 = k0 * (b[1] + b[7]) + k1 * (b[2] + b[6]) + k2 * (b[3] + b[5]) + k3 * b[4];
+      const uint32_t h2 = k0 * (b[2] + b[8]) + k1 * (b[3] + b[7]) + k2 * (b[4] + b[6]) + k3 * b[5];
+      const uint32_t h3 = k0 * (b[3] + b[9]) + k1 * (b[4] + b[8]) + k2 * (b[5] + b[7]) + k3 * b[6];
+      *reinterpret_cast<uint2*>(tmid + r * mstride + 4 * gq) = make_uint2(h0 | (h1 << 16), h2 | (h3 << 16));
+    }
+    __syncthreads();
+    for (int i = t; i < (y1 - y0) * G4; i += kPyrThreads) {
+      const int r = div_small(i, inv_g4), gq = i - r * G4;
+      uint2 a[7];
+#pragma unroll
+      for (int v = 0; v < 7; v++) a[v] = *reinterpret_cast<const uint2*>(tmid + (r + v) * mstride + 4 * gq);
+      auto vsum = [&](int sh, bool hi) -> uint32_t {
+        int s[7];
+#pragma unroll
+        for (int v = 0; v < 7; v++) s[v] = (int)(((hi ? a[v].y : a[v].x) >> sh) & 0xFFFF);
+        const int acc = k0 * (s[0] + s[6]) + k1 * (s[1] + s[5]) + k2 * (s[2] + s[4]) + k3 * s[3];
+        const int o = (acc + (1 << 15)) >> 16;
+        return (uint32_t)(o > 255 ? 255 : o);
+      };
+      const uint32_t o = vsum(0, false) | (vsum(16, false) << 8) | (vsum(0, true) << 16) |
+                         (vsum(16, true) << 24);
+      *reinterpret_cast<uint32_t*>(bp + L.boff + (long long)(y0 + r) * L.bpitch + 4 * gq) = o;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(kPyrThreads) k_pyramid(const uint8_t* __restrict__ img, int stride,
+                                                         long long frame_pitch, uint8_t* pyr,
+                                                         uint8_t* __restrict__ blur,
+                                                         const OrbGeom* __restrict__ g,
+                                                         const int* __restrict__ rs_all,
+                                                         const PyrBand* __restrict__ bands,
+                                                         long long* __restrict__ prof) {
+  extern __shared__ uint32_t psm[];
+  const int t = threadIdx.x;
+  const int f = blockIdx.y;
+  // debug: phase time stamps of block (0, 0) (4 per level after the start)
+  const bool stamp = prof && t == 0 && blockIdx.x == 0 && f == 0;
+  if (stamp) prof[0] = (long long)wall_clock64();
+  const PyrBand& B = bands[blockIdx.x];
+  uint8_t* fp = pyr + (long long)f * g->pyr_bytes;
+  uint8_t* bp = blur + (long long)f * g->blur_bytes;
+  const int nl = g->nlevels;
+  for (int l = 0; l < nl; l++) {
+    const LevelGeom& L = g->lv[l];
+    const int na = B.na[l], nb = B.nb[l];
+    // ---- 1. content rows [na, nb) ----
+    if (l == 0) {
+      const uint8_t* src = img + (long long)f * frame_pitch;
+      const int nv = (L.w + 15) >> 4;
+      const uint32_t inv_nv = div_inv(nv);
+      for (int i = t; i < (nb - na) * nv; i += kPyrThreads) {
+        const int rr = div_small(i, inv_nv);
+        const int r = na + rr, c = (i - rr * nv) * 16;
+        const uint8_t* s = src + (long long)r * stride + c;
+        uint8_t* d = fp + content_off(L, c, r);
+        if (c + 16 <= L.w && ((reinterpret_cast<uintptr_t>(s) & 15) == 0)) {
+          *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(s);
+        } else {
+          const int n = min(16, L.w - c);
+          for (int k = 0; k < n; k++) d[k] = s[k];
+        }
+      }
+      __syncthreads();
+    } else {
+      pyr_resize_rows(L, g->lv[l - 1], rs_all + L.rs_off, fp, na, nb, psm);
+    }
+    if (stamp) prof[1 + 4 * l] = (long long)wall_clock64();
+    // ---- 2a. side borders of rows [na, nb) ----
+    for (int i = t; i < (nb - na) * 2 * kEdge; i += kPyrThreads) {
+      const int rr = i / (2 * kEdge), k = i - rr * 2 * kEdge;
+      const int r = na + rr;
+      const int px = k < kEdge ? k : L.w + k;          // padded column
+      const int cx = reflect101_dev(px - kEdge, L.w);
+      fp[padded_off(L, px, r + kEdge)] = fp[content_off(L, cx, r)];
+    }
+    __syncthreads();
+    if (stamp) prof[2 + 4 * l] = (long long)wall_clock64();
+    // ---- 2b. top / bottom mirror rows with a source row in [na, nb) ----
+    {
+      const int t0 = max(na, 1), t1 = min(nb, kEdge + 1);               // y = -cy
+      const int b0 = max(na, L.h - 1 - kEdge), b1 = min(nb, L.h - 1);   // y = 2h-2-cy
+      const int nt = max(0, t1 - t0), nbm = max(0, b1 - b0);
+      const int nq = L.pitch >> 4;
+      for (int i = t; i < (nt + nbm) * nq; i += kPyrThreads) {
+        const int k = i / nq, q = i - k * nq;
+        int cy, py;
+        if (k < nt) {
+          cy = t0 + k;
+          py = kEdge - cy;
+        } else {
+          cy = b0 + (k - nt);
+          py = 2 * L.h - 2 - cy + kEdge;
+        }
+        const uint4* s = reinterpret_cast<const uint4*>(fp + L.pyr_off + (long long)(cy + kEdge) * L.pitch) + q;
+        uint4* d = reinterpret_cast<uint4*>(fp + L.pyr_off + (long long)py * L.pitch) + q;
+        *d = *s;
+      }
+    }
+    __syncthreads();
+    if (stamp) prof[3 + 4 * l] = (long long)wall_clock64();
+    // ---- 3. blurred own rows ----
+    pyr_blur_rows(L, fp, bp, B.oa[l], B.ob[l], psm);
+    if (stamp) prof[4 + 4 * l] = (long long)wall_clock64();
+  }
 }
 
 // NMS for the centre pair at M[r][q], M[r][q+1]: returns (m_lo, m_hi) in
@@ -897,25 +914,11 @@ hipError_t upload_pattern(hipStream_t s) {
 size_t octree_smem_bytes() { return sizeof(OctShared); }
 
 void launch_pyramid(const OrbGeom& hg, const OrbGeom* dg, const uint8_t* img, int stride,
-                    long long frame_pitch, uint8_t* pyr, const int* rs, int batch, hipStream_t s) {
-  for (int l = 0; l < hg.nlevels; l++) {
-    const LevelGeom& L = hg.lv[l];
-    if (l == 0) {
-      dim3 block(64, 4);
-      dim3 grid(((L.w + 15) / 16 + 63) / 64, (L.h + 3) / 4, batch);
-      hipLaunchKernelGGL(k_pyr_level0, grid, block, 0, s, img, stride, frame_pitch, pyr, dg);
-    } else {
-      const int tiles = ((L.w + kPyrTileW - 1) / kPyrTileW) * ((L.h + kPyrTileH - 1) / kPyrTileH);
-      hipLaunchKernelGGL(k_pyr_level, dim3(tiles, batch), dim3(256), 0, s, pyr, dg, l, rs);
-    }
-  }
-  hipLaunchKernelGGL(k_pyr_border, dim3((hg.border_total + 255) / 256, batch), dim3(256), 0, s, pyr,
-                     dg);
-}
-
-void launch_blur(const OrbGeom& hg, const OrbGeom* dg, const uint8_t* pyr, uint8_t* blur, int batch,
-                 hipStream_t s) {
-  hipLaunchKernelGGL(k_blur, dim3(hg.blur_tiles_total, batch), dim3(256), 0, s, pyr, blur, dg);
+                    long long frame_pitch, uint8_t* pyr, uint8_t* blur, const int* rs,
+                    const PyrBand* bands, int nbands, int batch, long long* prof,
+                    hipStream_t s) {
+  hipLaunchKernelGGL(k_pyramid, dim3(nbands, batch), dim3(kPyrThreads), kPyrLds, s, img, stride,
+                     frame_pitch, pyr, blur, dg, rs, bands, prof);
 }
 
 void launch_fast(const OrbGeom& hg, const OrbGeom* dg, const CellGeom* cells, const uint8_t* pyr,

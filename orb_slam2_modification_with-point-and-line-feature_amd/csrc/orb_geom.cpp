@@ -71,8 +71,7 @@ int build_orb_geometry(int nfeatures, float scale_factor, int nlevels, int W, in
   }
   // --- levels ---
   long long off = 0, boff = 0;
-  int border_total = 0;
-  int cell_total = 0, kp_total = 0, blur_total = 0;
+  int cell_total = 0, kp_total = 0;
   int max_slots = 1;
   G.cells.clear();
   G.rs.clear();
@@ -91,8 +90,6 @@ int build_orb_geometry(int nfeatures, float scale_factor, int nlevels, int W, in
     L.pyr_off = off;
     off += (long long)round_up(L.pitch * L.ph, 256);
     L.bpitch = round_up(L.w, 16);
-    L.border_base = border_total;
-    border_total += L.pw * L.ph - L.w * L.h;
     L.boff = boff;
     boff += (long long)round_up(L.bpitch * L.h, 256);
     L.scale = G.scale[l];
@@ -153,20 +150,21 @@ int build_orb_geometry(int nfeatures, float scale_factor, int nlevels, int W, in
     }
     L.kp_base = kp_total;
     kp_total += L.kp_cap;
-    // blur tiles
-    L.blur_tiles_x = (L.w + kBlurTileW - 1) / kBlurTileW;
-    L.blur_tiles_y = (L.h + kBlurTileH - 1) / kBlurTileH;
-    L.blur_tile_base = blur_total;
-    blur_total += L.blur_tiles_x * L.blur_tiles_y;
+    // k_pyramid blur chunk: (BCH + 6) staged rows of ceil(w/4) + 3 dwords
+    // plus (BCH + 6) rows of 4 * ceil(w/4) u16 horizontal sums
+    {
+      const int G4 = (L.w + 3) / 4;
+      const int per_row = 4 * (G4 + 3) + 2 * 4 * G4;
+      L.bchunk = std::min(32, kPyrLds / per_row - 7);
+      if (L.bchunk < 1) { *err = "image too wide for the blur staging"; return ORBPL_ERR_ARG; }
+    }
   }
   for (int l = 0; l < nlevels; l++) G.cells.insert(G.cells.end(), lvl_cells[l].begin(), lvl_cells[l].end());
   g.ncells_total = cell_total;
   g.kp_cap_total = kp_total;
-  g.blur_tiles_total = blur_total;
   g.cell_slots = max_slots;
   g.pyr_bytes = off;
   g.blur_bytes = boff;
-  g.border_total = border_total;
   int cand_total = 0;
   for (int l = 0; l < nlevels; l++) {
     LevelGeom& L = g.lv[l];
@@ -208,22 +206,23 @@ int build_orb_geometry(int nfeatures, float scale_factor, int nlevels, int W, in
       beta[dy] = (b0 & 0xFFFF) | (b1 << 16);
     }
     L.xmax = xmax;
-    for (int x0 = 0; x0 < dw; x0 += kPyrTileW) {
-      const int x1 = std::min(x0 + kPyrTileW, dw);
-      const int a = xofs[x0] & ~3, b = std::min(xofs[x1 - 1] + 1, sw - 1);
-      if ((b + 1 - a + 3) / 4 > kPyrSrcDw) {
-        *err = "scale factor too large for the resize tile";
-        return ORBPL_ERR_ARG;
+    // k_pyramid resize chunk: the largest CH <= 32 whose source rows (for any
+    // chunk start) fit the LDS staging at (ceil(sw/4) + 1) dwords per row
+    {
+      const int rowB = 4 * ((sw + 3) / 4 + 1);
+      const int max_rows = kPyrLds / rowB;
+      int ch = 32;
+      for (; ch >= 1; ch--) {
+        int worst = 0;
+        for (int y0 = 0; y0 + ch - 1 < dh; y0++) {
+          const int a = std::min(std::max(yofs[y0], 0), sh - 1);
+          const int b = std::min(std::max(yofs[y0 + ch - 1] + 1, 0), sh - 1);
+          worst = std::max(worst, b - a + 1);
+        }
+        if (worst <= max_rows) break;
       }
-    }
-    for (int y0 = 0; y0 < dh; y0 += kPyrTileH) {
-      const int y1 = std::min(y0 + kPyrTileH, dh);
-      const int a = std::min(std::max(yofs[y0], 0), sh - 1);
-      const int b = std::min(std::max(yofs[y1 - 1] + 1, 0), sh - 1);
-      if (b - a + 1 > kPyrSrcRows) {
-        *err = "scale factor too large for the resize tile";
-        return ORBPL_ERR_ARG;
-      }
+      if (ch < 1) { *err = "image too wide for the resize staging"; return ORBPL_ERR_ARG; }
+      L.rchunk = ch;
     }
     G.rs.insert(G.rs.end(), xofs.begin(), xofs.end());
     G.rs.insert(G.rs.end(), alpha.begin(), alpha.end());
@@ -231,6 +230,29 @@ int build_orb_geometry(int nfeatures, float scale_factor, int nlevels, int W, in
     G.rs.insert(G.rs.end(), beta.begin(), beta.end());
   }
   if (G.rs.empty()) G.rs.push_back(0);
+  // --- k_pyramid row bands for B = 1, 2, 4, 8 ---
+  // own rows partition each level; need rows = own +- 3 (blur) united with
+  // the source rows (yofs, yofs + 1, clamped) of the next level's need rows
+  G.bands.assign(2 * kPyrMaxBands - 1, PyrBand{});
+  for (int B = 1; B <= kPyrMaxBands; B *= 2) {
+    for (int b = 0; b < B; b++) {
+      PyrBand& P = G.bands[pyr_band_base(B) + b];
+      for (int l = nlevels - 1; l >= 0; l--) {
+        const int h = g.lv[l].h;
+        P.oa[l] = (int)((long long)b * h / B);
+        P.ob[l] = (int)((long long)(b + 1) * h / B);
+        int na = std::max(0, P.oa[l] - 3), nb = std::min(h, P.ob[l] + 3);
+        if (l + 1 < nlevels) {
+          const LevelGeom& U = g.lv[l + 1];
+          const int* yofs = G.rs.data() + U.rs_off + 2 * U.w;
+          na = std::min(na, std::min(std::max(yofs[P.na[l + 1]], 0), h - 1));
+          nb = std::max(nb, std::min(std::max(yofs[P.nb[l + 1] - 1] + 1, 0), h - 1) + 1);
+        }
+        P.na[l] = na;
+        P.nb[l] = nb;
+      }
+    }
+  }
   return ORBPL_OK;
 }
 

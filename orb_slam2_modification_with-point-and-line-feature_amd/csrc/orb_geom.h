@@ -38,10 +38,10 @@ struct LevelGeom {
   int rs_off;          // offset of the resize tables (levels >= 1) in ints
   int xmax;            // first dx whose sx + 1 >= src width (OpenCV resize)
   int scaled_patch;    // (int)(PATCH_SIZE * scale)  (ORBextractor.cc:837)
-  int blur_tile_base;  // first blur tile of this level
-  int blur_tiles_x, blur_tiles_y;
+  int rchunk;          // k_pyramid: output rows per resize chunk (source rows fit kPyrLds)
+  int bchunk;          // k_pyramid: output rows per blur chunk
   int bpitch;          // blurred level row pitch (content only, multiple of 16)
-  int border_base;     // first border pixel of this level (k_pyr_border enumeration)
+  int pad1;
   long long boff;      // byte offset of the blurred level inside one frame's blurred buffer
 };
 
@@ -58,10 +58,7 @@ struct OrbGeom {
   int ncells_total;
   int kp_cap_total;    // sum of kp_cap (per-frame list array size)
   int cand_cap_total;  // sum of cand_cap
-  int blur_tiles_total;
   int cell_slots;      // max corners a FAST window can emit: ceil(dw/2)*ceil(dh/2)
-  int border_total;    // border pixels of all levels (per frame)
-  int pyr_tiles_total; // unused (reserved)
   int fast_win_w;      // largest FAST window (x1 - x0) over all cells
   int fast_win_h;      // largest FAST window (y1 - y0)
   long long pyr_bytes; // bytes of one frame's padded pyramid
@@ -70,8 +67,18 @@ struct OrbGeom {
   LevelGeom lv[kMaxLevels];
 };
 
-constexpr int kBlurTileW = 128;
-constexpr int kBlurTileH = 32;
+// k_pyramid (fused pyramid + borders + blur): one block per (row band,
+// frame). Band b owns content rows [oa, ob) of every level and computes rows
+// [na, nb) (own rows plus the halo that the blur and the next level read).
+constexpr int kPyrThreads = 512;
+constexpr int kPyrLds = 40 * 1024;   // dynamic LDS per block (resize / blur staging)
+constexpr int kPyrMaxBands = 8;      // bands for B = 1, 2, 4, 8 are precomputed
+struct PyrBand {
+  int na[kMaxLevels], nb[kMaxLevels];
+  int oa[kMaxLevels], ob[kMaxLevels];
+};
+// index of the first band of the B-band partition in the band table
+__host__ __device__ inline int pyr_band_base(int B) { return B - 1; }
 
 // Byte offsets (within one frame's padded pyramid) of a content pixel and of
 // a padded pixel.
@@ -81,11 +88,6 @@ __host__ __device__ inline long long content_off(const LevelGeom& L, int x, int 
 __host__ __device__ inline long long padded_off(const LevelGeom& L, int px, int py) {
   return L.pyr_off + (long long)py * L.pitch + kLead + px;
 }
-
-constexpr int kPyrTileW = 128;   // content tile of the resize kernel
-constexpr int kPyrTileH = 16;
-constexpr int kPyrSrcDw = 64;    // LDS source window: dwords per row
-constexpr int kPyrSrcRows = 48;  // LDS source window: rows
 
 // Candidate packing: x (12 bits) | y (12 bits) << 12 | score (8 bits) << 24,
 // coordinates relative to minBorder (the reference's vToDistributeKeys frame).

@@ -18,10 +18,12 @@ struct orbpl_keypoint_dev {
 hipError_t upload_pattern(hipStream_t s);
 size_t octree_smem_bytes();
 
+// Padded pyramid + borders + blurred levels of `batch` frames (k_pyramid);
+// bands = the nbands-band partition (pyr_band_base(nbands) in the table).
 void launch_pyramid(const OrbGeom& hg, const OrbGeom* dg, const uint8_t* img, int stride,
-                    long long frame_pitch, uint8_t* pyr, const int* rs, int batch, hipStream_t s);
-void launch_blur(const OrbGeom& hg, const OrbGeom* dg, const uint8_t* pyr, uint8_t* blur, int batch,
-                 hipStream_t s);
+                    long long frame_pitch, uint8_t* pyr, uint8_t* blur, const int* rs,
+                    const PyrBand* bands, int nbands, int batch, long long* prof,
+                    hipStream_t s);
 void launch_fast(const OrbGeom& hg, const OrbGeom* dg, const CellGeom* cells, const uint8_t* pyr,
                  uint32_t* cell_cands, int* cell_counts, int ini_th, int min_th, int batch,
                  hipStream_t s);
@@ -39,6 +41,7 @@ struct OrbHostGeom {
   OrbGeom g;
   std::vector<CellGeom> cells;
   std::vector<int> rs;           // resize tables for all levels >= 1
+  std::vector<PyrBand> bands;    // k_pyramid row bands for B = 1, 2, 4, 8 (15 entries)
   std::vector<float> scale, inv_scale, sigma2, inv_sigma2;
 };
 int build_orb_geometry(int nfeatures, float scale_factor, int nlevels, int W, int H,

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -49,6 +50,9 @@ struct orbx_ctx {
   OrbGeom* d_geom = nullptr;
   CellGeom* d_cells = nullptr;
   int* d_rs = nullptr;
+  PyrBand* d_bands = nullptr;
+  long long* d_pyr_prof = nullptr;   // ORBPL_PYR_PROFILE: k_pyramid phase stamps
+  int pyr_bands = 0;           // 0 = choose per batch (ORBPL_PYR_BANDS overrides)
   uint8_t* d_in = nullptr;
   uint8_t* d_pyr = nullptr;
   uint8_t* d_blur = nullptr;
@@ -142,7 +146,7 @@ int orbpl_descriptor_distance(const uint8_t* a, const uint8_t* b) {
 static void free_ctx(orbx_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  void* ptrs[] = {c->d_geom, c->d_cells, c->d_rs, c->d_in, c->d_pyr, c->d_blur, c->d_cell_cands,
+  void* ptrs[] = {c->d_geom, c->d_cells, c->d_rs, c->d_bands, c->d_pyr_prof, c->d_in, c->d_pyr, c->d_blur, c->d_cell_cands,
                   c->d_cell_counts, c->d_kcand, c->d_knode, c->d_kp_list, c->d_kp_count,
                   c->d_out_kps, c->d_out_desc, c->d_out_n, c->d_err};
   for (void* p : ptrs)
@@ -192,6 +196,7 @@ int orbx_create(const orbpl_orb_params* p, int width, int height, int max_batch,
   CK(hipMalloc(&c->d_geom, sizeof(OrbGeom)));
   CK(hipMalloc(&c->d_cells, sizeof(CellGeom) * std::max<size_t>(1, c->hg.cells.size())));
   CK(hipMalloc(&c->d_rs, sizeof(int) * c->hg.rs.size()));
+  CK(hipMalloc(&c->d_bands, sizeof(PyrBand) * c->hg.bands.size()));
   CK(hipMalloc(&c->d_in, B * (size_t)width * height));
   CK(hipMalloc(&c->d_pyr, B * (size_t)g.pyr_bytes));
   CK(hipMalloc(&c->d_blur, B * (size_t)g.blur_bytes));
@@ -214,10 +219,35 @@ int orbx_create(const orbpl_orb_params* p, int width, int height, int max_batch,
                       hipMemcpyHostToDevice, c->stream));
   CK(hipMemcpyAsync(c->d_rs, c->hg.rs.data(), sizeof(int) * c->hg.rs.size(), hipMemcpyHostToDevice,
                     c->stream));
+  CK(hipMemcpyAsync(c->d_bands, c->hg.bands.data(), sizeof(PyrBand) * c->hg.bands.size(),
+                    hipMemcpyHostToDevice, c->stream));
+  if (const char* e = getenv("ORBPL_PYR_BANDS")) {
+    const int b = atoi(e);
+    if (b == 1 || b == 2 || b == 4 || b == 8) c->pyr_bands = b;
+  }
+  if (getenv("ORBPL_PYR_PROFILE")) {
+    CK(hipMalloc(&c->d_pyr_prof, 8 * (1 + 4 * kMaxLevels)));
+    CK(hipMemsetAsync(c->d_pyr_prof, 0, 8 * (1 + 4 * kMaxLevels), c->stream));
+  }
   CK(upload_pattern(c->stream));
   CK(hipStreamSynchronize(c->stream));
 #undef CK
   *out = c;
+  return ORBPL_OK;
+}
+
+// Debug (ORBPL_PYR_PROFILE set at create): k_pyramid phase times of block
+// (band 0, frame 0) in the last launch, ns, 4 per level: content, side
+// borders, mirror rows, blur.
+int orbx_debug_pyr_profile(orbx_ctx* c, long long* out, int cap, int* n) {
+  if (!c || !out || !n) return arg_fail("bad argument");
+  if (!c->d_pyr_prof) return arg_fail("ORBPL_PYR_PROFILE was not set when the context was created");
+  HIP_CHECK(hipStreamSynchronize(c->stream));
+  const int L = c->hg.g.nlevels;
+  std::vector<long long> p(1 + 4 * kMaxLevels);
+  HIP_CHECK(hipMemcpy(p.data(), c->d_pyr_prof, p.size() * 8, hipMemcpyDeviceToHost));
+  *n = std::min(cap, 4 * L);
+  for (int i = 0; i < *n; i++) out[i] = (p[i + 1] - p[i]) * 10;   // wall clock: 100 MHz
   return ORBPL_OK;
 }
 
@@ -283,9 +313,16 @@ int orbx_run(orbx_ctx* c, const uint8_t* d_imgs, int batch, int stride, long lon
   c->timed = ext_events == nullptr;
   hipEvent_t* ev = ext_events ? ext_events : c->ev;
   HIP_CHECK(hipEventRecord(ev[0], s));
-  launch_pyramid(g, c->d_geom, d_imgs, stride, frame_pitch, c->d_pyr, c->d_rs, batch, s);
+  // row bands per frame: enough blocks for ~4 per CU (256 CUs), at most 8
+  int nb = c->pyr_bands;
+  if (!nb) {
+    nb = 1;
+    while (nb < kPyrMaxBands && nb * batch < 1024) nb *= 2;
+  }
+  launch_pyramid(g, c->d_geom, d_imgs, stride, frame_pitch, c->d_pyr, c->d_blur, c->d_rs,
+                 c->d_bands + pyr_band_base(nb), nb, batch, c->d_pyr_prof, s);
   HIP_CHECK(hipEventRecord(ev[1], s));
-  launch_blur(g, c->d_geom, c->d_pyr, c->d_blur, batch, s);
+  // the blur is fused into k_pyramid: the blur stage interval stays empty
   HIP_CHECK(hipEventRecord(ev[2], s));
   launch_fast(g, c->d_geom, c->d_cells, c->d_pyr, c->d_cell_cands, c->d_cell_counts,
               c->params.ini_th_fast, c->params.min_th_fast, batch, s);

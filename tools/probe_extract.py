@@ -32,3 +32,17 @@ ex.synchronize()
 dt = (time.time() - t) / R
 n = d_n.download(np.int32, B)
 print(f"B={B} wall {dt*1e3:.2f} ms/batch -> {B/dt:.0f} fps; stages ms (pyr, blur, fast, octree, desc) = {np.round(ms, 3).tolist()} ; n[0:4]={n[:4].tolist()}")
+if getattr(pkg.lib(), "orbx_debug_pyr_profile", None) is not None and __import__("os").environ.get(
+        "ORBPL_PYR_PROFILE"):
+    import ctypes as C
+    out = np.zeros(64, np.int64)
+    n = C.c_int(0)
+    L = pkg.lib()
+    L.orbx_debug_pyr_profile.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_int)]
+    pkg.check(L.orbx_debug_pyr_profile(ex._h, out.ctypes.data_as(C.c_void_p), 64, C.byref(n)),
+              "orbx_debug_pyr_profile")
+    ph = out[:n.value].reshape(-1, 4) / 1000.0
+    print("k_pyramid block(0,0) phases us [content, side, mirror, blur] per level:")
+    for l, r in enumerate(ph):
+        print(f"  L{l}: " + " ".join(f"{x:7.1f}" for x in r))
+    print(f"  total {ph.sum():.1f} us")
