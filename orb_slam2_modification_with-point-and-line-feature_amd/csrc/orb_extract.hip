@@ -127,138 +127,188 @@ __device__ __forceinline__ int div_small(int k, uint32_t inv) {
 // ComputePyramid (ORBextractor.cc:1107-1132) and the per-level GaussianBlur
 // (:1084-1086) in ONE launch. Block (band b, frame f) owns content rows
 // [oa, ob) of every level and computes, level after level:
-//   1. content rows [na, nb) (own rows plus the halo the next level and the
-//      blur need; host-computed, PyrBand): level 0 = the input image, level
-//      l >= 1 = resize(level l-1, INTER_LINEAR) in OpenCV's 8U fixed point
-//      (11-bit coefficients, (S>>4)*beta>>16, +2>>2) from full-width source
-//      row chunks staged in LDS;
+//   1. content rows [na, nb) (own rows plus the halo that the blur and the
+//      next level read; host-computed, PyrBand): level 0 = the input image,
+//      level l >= 1 = resize(level l-1, INTER_LINEAR) in OpenCV's 8U fixed
+//      point (11-bit coefficients, (S>>4)*beta>>16, +2>>2);
 //   2. copyMakeBorder(19, REFLECT_101[|ISOLATED]): the 19+19 side pixels of
 //      rows [na, nb), then every top/bottom mirror row whose source row lies
 //      in [na, nb) (a whole padded row copy);
-//   3. the 7x7 sigma=2 blur of the own rows [oa, ob) from the padded level
-//      (pinned P4: out = (sum_v kv sum_u ku I + 2^15) >> 16, k = {18,34,49,
-//      54,49,34,18}; the horizontal sums fit u16 and stay in LDS).
-// Halo rows are computed by both neighbouring bands with identical values and
-// every store writes exactly its own bytes, so the overlaps are benign. A
-// level's rows are only read after the block's own __syncthreads.
+//   3. the 7x7 sigma=2 blur of the own rows [oa, ob) (pinned P4: out =
+//      (sum_v kv sum_u ku I + 2^15) >> 16, k = {18,34,49,54,49,34,18}).
+// Resize and blur run as column walks: a thread owns 4 adjacent output
+// columns and walks down a row segment, with its resize coefficients (or the
+// 7 rows of horizontal blur sums) in registers and the source dwords read
+// straight from the just-written level (L1/L2): no LDS staging, three
+// barriers per level. Halo rows are computed by both neighbouring bands with
+// identical values and every store writes exactly its own bytes, so the
+// overlaps are benign.
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t byte_of(uint32_t w0, uint32_t w1, uint32_t w2, int p) {
+  // byte p (0..11) of the 12-byte little-endian window w0 | w1 | w2
+  const uint32_t lo = p < 4 ? w0 : (p < 8 ? w1 : w2);
+  return (lo >> (8 * (p & 3))) & 0xFF;
+}
+
+// Row segments of a walk (tasks = groups x nseg, rps rows per segment): the
+// split with the fewest sequential rows per thread, counting `warm` extra
+// rows per segment (the blur's 6 warm-up rows) and idle lanes of the last
+// round of tasks. Block-uniform.
+__device__ __forceinline__ void walk_split(int groups, int rows, int warm, int* nseg, int* rps) {
+  int best = 1, best_cost = 0x7fffffff;
+  for (int s = 1; s <= 64 && s <= rows; s++) {
+    const int r = (rows + s - 1) / s;
+    const int cost = ((groups * s + kPyrThreads - 1) / kPyrThreads) * (r + warm);
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = s;
+    }
+  }
+  *nseg = best;
+  *rps = (rows + best - 1) / best;
+}
+
 __device__ __forceinline__ void pyr_resize_rows(const LevelGeom& L, const LevelGeom& S,
                                                 const int* __restrict__ rs, uint8_t* fp, int na,
-                                                int nb, uint32_t* psm) {
-  const int t = threadIdx.x;
+                                                int nb) {
   const int* xofs = rs;
   const int* alpha = rs + L.w;
   const int* yofs = rs + 2 * L.w;
   const int* beta = rs + 2 * L.w + L.h;
-  const int ndw = (S.w + 3) >> 2;      // dwords of a source content row
-  const int rstride = ndw + 1;         // LDS row stride (odd: fewer bank conflicts)
-  const int rowB = rstride * 4;
-  const int groups = (L.w + 3) >> 2;   // 4 output pixels per item
-  const uint32_t inv_ndw = div_inv(ndw), inv_groups = div_inv(groups);
-  const uint8_t* wb = reinterpret_cast<const uint8_t*>(psm);
-  for (int y0 = na; y0 < nb; y0 += L.rchunk) {
-    const int y1 = min(y0 + L.rchunk, nb);
-    const int ya = min(max(yofs[y0], 0), S.h - 1);
-    const int yb = min(max(yofs[y1 - 1] + 1, 0), S.h - 1);
-    const int nrows = yb - ya + 1;
-    for (int i = t; i < nrows * ndw; i += kPyrThreads) {
-      const int r = div_small(i, inv_ndw), d = i - r * ndw;
-      psm[r * rstride + d] = *reinterpret_cast<const uint32_t*>(fp + content_off(S, 4 * d, ya + r));
-    }
-    __syncthreads();
-    for (int i = t; i < (y1 - y0) * groups; i += kPyrThreads) {
-      const int r = div_small(i, inv_groups), gq = i - r * groups;
-      const int y = y0 + r, x = 4 * gq;
-      const int sy0 = yofs[y];
-      const int r0 = min(max(sy0, 0), S.h - 1) - ya, r1 = min(max(sy0 + 1, 0), S.h - 1) - ya;
-      const int bpk = beta[y];
-      const int b0 = (int)(short)(bpk & 0xFFFF), b1 = (int)(short)(bpk >> 16);
-      uint32_t packed = 0;
+  const int groups = (L.w + 3) >> 2;
+  int nseg, rps;
+  walk_split(groups, nb - na, 2, &nseg, &rps);
+  const uint8_t* src0 = fp + content_off(S, 0, 0);
+  for (int task = threadIdx.x; task < groups * nseg; task += kPyrThreads) {
+    const int seg = task / groups, gq = task - seg * groups;
+    const int ra = na + seg * rps, rb = min(ra + rps, nb);
+    const int x = 4 * gq;
+    const int d0 = xofs[x] >> 2;                 // first source dword of the group
+    int p0[4], a0[4], a1[4];
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const int cx = min(x + k, L.w - 1);
-        const int sx = xofs[cx];
-        int h0, h1;
-        if (cx < L.xmax) {
-          const int apk = alpha[cx];
-          const int a0 = (int)(short)(apk & 0xFFFF), a1 = (int)(short)(apk >> 16);
-          h0 = wb[r0 * rowB + sx] * a0 + wb[r0 * rowB + sx + 1] * a1;
-          h1 = wb[r1 * rowB + sx] * a0 + wb[r1 * rowB + sx + 1] * a1;
-        } else {
-          h0 = wb[r0 * rowB + sx] * 2048;
-          h1 = wb[r1 * rowB + sx] * 2048;
-        }
-        const uint32_t v = (uint32_t)((((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2);
-        packed |= v << (8 * k);
-      }
-      uint8_t* dst = fp + content_off(L, x, y);
-      if (x + 4 <= L.w) {
-        *reinterpret_cast<uint32_t*>(dst) = packed;
-      } else {  // last partial group: the border bytes belong to step 2
-        for (int k = 0; k < L.w - x; k++) dst[k] = (uint8_t)(packed >> (8 * k));
+    for (int k = 0; k < 4; k++) {
+      const int cx = min(x + k, L.w - 1);
+      p0[k] = xofs[cx] - 4 * d0;                 // byte of sx in the 12-byte window
+      if (cx < L.xmax) {
+        const int apk = alpha[cx];
+        a0[k] = (int)(short)(apk & 0xFFFF);
+        a1[k] = (int)(short)(apk >> 16);
+      } else {
+        a0[k] = 2048;                            // sx + 1 >= src width: only sx
+        a1[k] = 0;
       }
     }
-    __syncthreads();
+    // 4 rows per iteration: all 24 source dwords are loaded before any is used
+    for (int y = ra; y < rb; y += 4) {
+      int bq[4];
+      uint32_t u[4][3], v[4][3];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int yy = min(y + j, rb - 1);
+        const int sy0 = yofs[yy];
+        bq[j] = beta[yy];
+        const uint32_t* q0 = reinterpret_cast<const uint32_t*>(
+            src0 + (long long)min(max(sy0, 0), S.h - 1) * S.pitch) + d0;
+        const uint32_t* q1 = reinterpret_cast<const uint32_t*>(
+            src0 + (long long)min(max(sy0 + 1, 0), S.h - 1) * S.pitch) + d0;
+#pragma unroll
+        for (int e = 0; e < 3; e++) {
+          u[j][e] = q0[e];
+          v[j][e] = q1[e];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        if (y + j >= rb) break;
+        const int b0 = (int)(short)(bq[j] & 0xFFFF), b1 = (int)(short)(bq[j] >> 16);
+        uint32_t packed = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          // a1 == 0 at the right edge: the (unused) sx + 1 byte may be border
+          const int h0 = (int)byte_of(u[j][0], u[j][1], u[j][2], p0[k]) * a0[k] +
+                         (int)byte_of(u[j][0], u[j][1], u[j][2], p0[k] + 1) * a1[k];
+          const int h1 = (int)byte_of(v[j][0], v[j][1], v[j][2], p0[k]) * a0[k] +
+                         (int)byte_of(v[j][0], v[j][1], v[j][2], p0[k] + 1) * a1[k];
+          const uint32_t o =
+              (uint32_t)((((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2);
+          packed |= o << (8 * k);
+        }
+        uint8_t* dst = fp + content_off(L, x, y + j);
+        if (x + 4 <= L.w) {
+          *reinterpret_cast<uint32_t*>(dst) = packed;
+        } else {  // last partial group: the border bytes belong to step 2
+          for (int k = 0; k < L.w - x; k++) dst[k] = (uint8_t)(packed >> (8 * k));
+        }
+      }
+    }
   }
 }
 
-__device__ __forceinline__ void pyr_blur_rows(const LevelGeom& L, const uint8_t* fp, uint8_t* bp,
-                                              int oa, int ob, uint32_t* psm) {
-  const int t = threadIdx.x;
-  const int G4 = (L.w + 3) >> 2;       // output groups of 4 pixels per row
-  const int ndw = G4 + 2;              // staged dwords per row: content cols -4 .. 4*G4+3
-  const int rstride = ndw + 1;
-  const int BCH = L.bchunk;
-  uint32_t* tin = psm;
-  uint16_t* tmid = reinterpret_cast<uint16_t*>(psm + (((BCH + 6) * rstride + 1) & ~1));
-  const int mstride = 4 * G4;          // u16 per row of horizontal sums
-  const uint32_t inv_ndw = div_inv(ndw), inv_g4 = div_inv(G4);
+// horizontal 7-tap sums of content columns x .. x+3 from the padded row's
+// dwords w0 | w1 | w2 = content columns x-4 .. x+7, packed as 4 x u16
+__device__ __forceinline__ uint2 blur_h4(uint32_t w0, uint32_t w1, uint32_t w2) {
   const int k0 = 18, k1 = 34, k2 = 49, k3 = 54;
-  for (int y0 = oa; y0 < ob; y0 += BCH) {
-    const int y1 = min(y0 + BCH, ob);
-    const int nr = y1 - y0 + 6;
-    for (int i = t; i < nr * ndw; i += kPyrThreads) {
-      const int r = div_small(i, inv_ndw), d = i - r * ndw;
-      const int py = y0 - 3 + r + kEdge;                 // padded row
-      tin[r * rstride + d] = *reinterpret_cast<const uint32_t*>(
-          fp + L.pyr_off + (long long)py * L.pitch + kContent0 - 4 + 4 * d);
-    }
-    __syncthreads();
-    for (int i = t; i < nr * G4; i += kPyrThreads) {
-      const int r = div_small(i, inv_g4), gq = i - r * G4;
-      // LDS byte j of a row holds content column j - 4; x = 4 gq needs
-      // columns x-3 .. x+6 = bytes 4gq+1 .. 4gq+10 = dwords gq .. gq+2
-      const uint32_t w0 = tin[r * rstride + gq], w1 = tin[r * rstride + gq + 1],
-                     w2 = tin[r * rstride + gq + 2];
-      int b[10];
-      b[0] = (w0 >> 8) & 0xFF; b[1] = (w0 >> 16) & 0xFF; b[2] = w0 >> 24;
-      b[3] = w1 & 0xFF; b[4] = (w1 >> 8) & 0xFF; b[5] = (w1 >> 16) & 0xFF; b[6] = w1 >> 24;
-      b[7] = w2 & 0xFF; b[8] = (w2 >> 8) & 0xFF; b[9] = (w2 >> 16) & 0xFF;
-      const uint32_t h0 = k0 * (b[0] + b[6]) + k1 * (b[1] + b[5]) + k2 * (b[2] + b[4]) + k3 * b[3];
-      const uint32_t h1 = k0 * (b[1] + b[7]) + k1 * (b[2] + b[6]) + k2 * (b[3] + b[5]) + k3 * b[4];
-      const uint32_t h2 = k0 * (b[2] + b[8]) + k1 * (b[3] + b[7]) + k2 * (b[4] + b[6]) + k3 * b[5];
-      const uint32_t h3 = k0 * (b[3] + b[9]) + k1 * (b[4] + b[8]) + k2 * (b[5] + b[7]) + k3 * b[6];
-      *reinterpret_cast<uint2*>(tmid + r * mstride + 4 * gq) = make_uint2(h0 | (h1 << 16), h2 | (h3 << 16));
-    }
-    __syncthreads();
-    for (int i = t; i < (y1 - y0) * G4; i += kPyrThreads) {
-      const int r = div_small(i, inv_g4), gq = i - r * G4;
-      uint2 a[7];
+  int b[10];
+  b[0] = (w0 >> 8) & 0xFF; b[1] = (w0 >> 16) & 0xFF; b[2] = w0 >> 24;
+  b[3] = w1 & 0xFF; b[4] = (w1 >> 8) & 0xFF; b[5] = (w1 >> 16) & 0xFF; b[6] = w1 >> 24;
+  b[7] = w2 & 0xFF; b[8] = (w2 >> 8) & 0xFF; b[9] = (w2 >> 16) & 0xFF;
+  const uint32_t h0 = k0 * (b[0] + b[6]) + k1 * (b[1] + b[5]) + k2 * (b[2] + b[4]) + k3 * b[3];
+  const uint32_t h1 = k0 * (b[1] + b[7]) + k1 * (b[2] + b[6]) + k2 * (b[3] + b[5]) + k3 * b[4];
+  const uint32_t h2 = k0 * (b[2] + b[8]) + k1 * (b[3] + b[7]) + k2 * (b[4] + b[6]) + k3 * b[5];
+  const uint32_t h3 = k0 * (b[3] + b[9]) + k1 * (b[4] + b[8]) + k2 * (b[5] + b[7]) + k3 * b[6];
+  return make_uint2(h0 | (h1 << 16), h2 | (h3 << 16));
+}
+
+__device__ __forceinline__ uint32_t blur_v1(const uint2* h, int hi, int sh) {
+  const int k0 = 18, k1 = 34, k2 = 49, k3 = 54;
+  int s[7];
 #pragma unroll
-      for (int v = 0; v < 7; v++) a[v] = *reinterpret_cast<const uint2*>(tmid + (r + v) * mstride + 4 * gq);
-      auto vsum = [&](int sh, bool hi) -> uint32_t {
-        int s[7];
+  for (int v = 0; v < 7; v++) s[v] = (int)(((hi ? h[v].y : h[v].x) >> sh) & 0xFFFF);
+  const int acc = k0 * (s[0] + s[6]) + k1 * (s[1] + s[5]) + k2 * (s[2] + s[4]) + k3 * s[3];
+  const int o = (acc + (1 << 15)) >> 16;
+  return (uint32_t)(o > 255 ? 255 : o);
+}
+
+__device__ __forceinline__ void pyr_blur_rows(const LevelGeom& L, const uint8_t* fp, uint8_t* bp,
+                                              int oa, int ob) {
+  const int G4 = (L.w + 3) >> 2;
+  int nseg, rps;
+  walk_split(G4, ob - oa, 6, &nseg, &rps);
+  for (int task = threadIdx.x; task < G4 * nseg; task += kPyrThreads) {
+    const int seg = task / G4, gq = task - seg * G4;
+    const int ra = oa + seg * rps, rb = min(ra + rps, ob);
+    if (ra >= rb) continue;
+    // padded row py holds content column x-4 at byte kContent0 - 4 + x
+    const uint32_t* col = reinterpret_cast<const uint32_t*>(fp + L.pyr_off + kContent0 - 4 + 4 * gq);
+    const int pw = L.pitch >> 2;
+    uint2 h[7];
 #pragma unroll
-        for (int v = 0; v < 7; v++) s[v] = (int)(((hi ? a[v].y : a[v].x) >> sh) & 0xFFFF);
-        const int acc = k0 * (s[0] + s[6]) + k1 * (s[1] + s[5]) + k2 * (s[2] + s[4]) + k3 * s[3];
-        const int o = (acc + (1 << 15)) >> 16;
-        return (uint32_t)(o > 255 ? 255 : o);
-      };
-      const uint32_t o = vsum(0, false) | (vsum(16, false) << 8) | (vsum(0, true) << 16) |
-                         (vsum(16, true) << 24);
-      *reinterpret_cast<uint32_t*>(bp + L.boff + (long long)(y0 + r) * L.bpitch + 4 * gq) = o;
+    for (int v = 0; v < 6; v++) {
+      const uint32_t* q = col + (long long)(ra - 3 + v + kEdge) * pw;
+      h[v + 1] = blur_h4(q[0], q[1], q[2]);
     }
-    __syncthreads();
+    uint8_t* out = bp + L.boff + 4 * gq;
+    // 4 rows per iteration: the 12 source dwords are loaded before any is used
+    for (int y = ra; y < rb; y += 4) {
+      uint32_t w[4][3];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t* q = col + (long long)(min(y + j, rb - 1) + 3 + kEdge) * pw;
+        w[j][0] = q[0];
+        w[j][1] = q[1];
+        w[j][2] = q[2];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        if (y + j >= rb) break;
+#pragma unroll
+        for (int v = 0; v < 6; v++) h[v] = h[v + 1];
+        h[6] = blur_h4(w[j][0], w[j][1], w[j][2]);
+        const uint32_t o = blur_v1(h, 0, 0) | (blur_v1(h, 0, 16) << 8) |
+                           (blur_v1(h, 1, 0) << 16) | (blur_v1(h, 1, 16) << 24);
+        *reinterpret_cast<uint32_t*>(out + (long long)(y + j) * L.bpitch) = o;
+      }
+    }
   }
 }
 
@@ -269,7 +319,6 @@ __global__ void __launch_bounds__(kPyrThreads) k_pyramid(const uint8_t* __restri
                                                          const int* __restrict__ rs_all,
                                                          const PyrBand* __restrict__ bands,
                                                          long long* __restrict__ prof) {
-  extern __shared__ uint32_t psm[];
   const int t = threadIdx.x;
   const int f = blockIdx.y;
   // debug: phase time stamps of block (0, 0) (4 per level after the start)
@@ -299,10 +348,10 @@ __global__ void __launch_bounds__(kPyrThreads) k_pyramid(const uint8_t* __restri
           for (int k = 0; k < n; k++) d[k] = s[k];
         }
       }
-      __syncthreads();
     } else {
-      pyr_resize_rows(L, g->lv[l - 1], rs_all + L.rs_off, fp, na, nb, psm);
+      pyr_resize_rows(L, g->lv[l - 1], rs_all + L.rs_off, fp, na, nb);
     }
+    __syncthreads();
     if (stamp) prof[1 + 4 * l] = (long long)wall_clock64();
     // ---- 2a. side borders of rows [na, nb) ----
     for (int i = t; i < (nb - na) * 2 * kEdge; i += kPyrThreads) {
@@ -330,15 +379,16 @@ __global__ void __launch_bounds__(kPyrThreads) k_pyramid(const uint8_t* __restri
           cy = b0 + (k - nt);
           py = 2 * L.h - 2 - cy + kEdge;
         }
-        const uint4* s = reinterpret_cast<const uint4*>(fp + L.pyr_off + (long long)(cy + kEdge) * L.pitch) + q;
+        const uint4* s =
+            reinterpret_cast<const uint4*>(fp + L.pyr_off + (long long)(cy + kEdge) * L.pitch) + q;
         uint4* d = reinterpret_cast<uint4*>(fp + L.pyr_off + (long long)py * L.pitch) + q;
         *d = *s;
       }
     }
     __syncthreads();
     if (stamp) prof[3 + 4 * l] = (long long)wall_clock64();
-    // ---- 3. blurred own rows ----
-    pyr_blur_rows(L, fp, bp, B.oa[l], B.ob[l], psm);
+    // ---- 3. blurred own rows (the next level only reads content rows) ----
+    pyr_blur_rows(L, fp, bp, B.oa[l], B.ob[l]);
     if (stamp) prof[4 + 4 * l] = (long long)wall_clock64();
   }
 }
@@ -917,7 +967,7 @@ void launch_pyramid(const OrbGeom& hg, const OrbGeom* dg, const uint8_t* img, in
                     long long frame_pitch, uint8_t* pyr, uint8_t* blur, const int* rs,
                     const PyrBand* bands, int nbands, int batch, long long* prof,
                     hipStream_t s) {
-  hipLaunchKernelGGL(k_pyramid, dim3(nbands, batch), dim3(kPyrThreads), kPyrLds, s, img, stride,
+  hipLaunchKernelGGL(k_pyramid, dim3(nbands, batch), dim3(kPyrThreads), 0, s, img, stride,
                      frame_pitch, pyr, blur, dg, rs, bands, prof);
 }
 

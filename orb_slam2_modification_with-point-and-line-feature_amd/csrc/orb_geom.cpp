@@ -150,14 +150,6 @@ int build_orb_geometry(int nfeatures, float scale_factor, int nlevels, int W, in
     }
     L.kp_base = kp_total;
     kp_total += L.kp_cap;
-    // k_pyramid blur chunk: (BCH + 6) staged rows of ceil(w/4) + 3 dwords
-    // plus (BCH + 6) rows of 4 * ceil(w/4) u16 horizontal sums
-    {
-      const int G4 = (L.w + 3) / 4;
-      const int per_row = 4 * (G4 + 3) + 2 * 4 * G4;
-      L.bchunk = std::min(32, kPyrLds / per_row - 7);
-      if (L.bchunk < 1) { *err = "image too wide for the blur staging"; return ORBPL_ERR_ARG; }
-    }
   }
   for (int l = 0; l < nlevels; l++) G.cells.insert(G.cells.end(), lvl_cells[l].begin(), lvl_cells[l].end());
   g.ncells_total = cell_total;
@@ -206,23 +198,14 @@ int build_orb_geometry(int nfeatures, float scale_factor, int nlevels, int W, in
       beta[dy] = (b0 & 0xFFFF) | (b1 << 16);
     }
     L.xmax = xmax;
-    // k_pyramid resize chunk: the largest CH <= 32 whose source rows (for any
-    // chunk start) fit the LDS staging at (ceil(sw/4) + 1) dwords per row
-    {
-      const int rowB = 4 * ((sw + 3) / 4 + 1);
-      const int max_rows = kPyrLds / rowB;
-      int ch = 32;
-      for (; ch >= 1; ch--) {
-        int worst = 0;
-        for (int y0 = 0; y0 + ch - 1 < dh; y0++) {
-          const int a = std::min(std::max(yofs[y0], 0), sh - 1);
-          const int b = std::min(std::max(yofs[y0 + ch - 1] + 1, 0), sh - 1);
-          worst = std::max(worst, b - a + 1);
-        }
-        if (worst <= max_rows) break;
+    // k_pyramid resize walk: the source bytes of 4 adjacent output columns
+    // (xofs .. xofs + 1) must lie in 3 dwords from xofs[x] & ~3
+    for (int x = 0; x < dw; x += 4) {
+      const int x3 = std::min(x + 3, dw - 1);
+      if (xofs[x3] + 1 - (xofs[x] & ~3) > 11) {
+        *err = "scale factor too large for the resize walk";
+        return ORBPL_ERR_ARG;
       }
-      if (ch < 1) { *err = "image too wide for the resize staging"; return ORBPL_ERR_ARG; }
-      L.rchunk = ch;
     }
     G.rs.insert(G.rs.end(), xofs.begin(), xofs.end());
     G.rs.insert(G.rs.end(), alpha.begin(), alpha.end());

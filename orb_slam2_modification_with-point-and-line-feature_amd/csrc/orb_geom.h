@@ -38,8 +38,7 @@ struct LevelGeom {
   int rs_off;          // offset of the resize tables (levels >= 1) in ints
   int xmax;            // first dx whose sx + 1 >= src width (OpenCV resize)
   int scaled_patch;    // (int)(PATCH_SIZE * scale)  (ORBextractor.cc:837)
-  int rchunk;          // k_pyramid: output rows per resize chunk (source rows fit kPyrLds)
-  int bchunk;          // k_pyramid: output rows per blur chunk
+  int pad2, pad3;
   int bpitch;          // blurred level row pitch (content only, multiple of 16)
   int pad1;
   long long boff;      // byte offset of the blurred level inside one frame's blurred buffer
@@ -70,8 +69,7 @@ struct OrbGeom {
 // k_pyramid (fused pyramid + borders + blur): one block per (row band,
 // frame). Band b owns content rows [oa, ob) of every level and computes rows
 // [na, nb) (own rows plus the halo that the blur and the next level read).
-constexpr int kPyrThreads = 512;
-constexpr int kPyrLds = 40 * 1024;   // dynamic LDS per block (resize / blur staging)
+constexpr int kPyrThreads = 256;
 constexpr int kPyrMaxBands = 8;      // bands for B = 1, 2, 4, 8 are precomputed
 struct PyrBand {
   int na[kMaxLevels], nb[kMaxLevels];
