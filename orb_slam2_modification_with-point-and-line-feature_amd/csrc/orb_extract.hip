@@ -57,7 +57,7 @@ __device__ __forceinline__ int reflect101_dev(int p, int len) {
 // non-corners score 0.)
 __host__ __device__ constexpr int fast_pstride(int win_w) { return ((win_w + 3 + 4) + 3) & ~3; }
 __host__ __device__ constexpr int fast_wave_words(int win_w, int win_h) {
-  return 2 * win_h * fast_pstride(win_w);
+  return win_h * fast_pstride(win_w);
 }
 
 typedef short fshort2 __attribute__((ext_vector_type(2)));
@@ -112,6 +112,64 @@ __device__ __forceinline__ fshort2 fast_m2(const uint32_t* P, int ps, int r, int
   }
   const fshort2 zero = {0, 0}, top = {255, 255};
   return pmin(pmax(pmax(A, zero - B), zero), top);
+}
+
+// m = max(A, -B) for the centre pair (x, x+1) from a register window: R[k] =
+// bytes x-3 .. x+4 of row (centre row + k - 3) as two dwords (.x = bytes
+// 0-3, .y = bytes 4-7). A ring pixel at (dx, dy) pairs with its right
+// neighbour in one v_perm_b32: (pix(x+dx) | pix(x+1+dx) << 16).
+__device__ __forceinline__ uint32_t ring_pair(const uint2* R, int dy, int dx) {
+  const uint32_t j = (uint32_t)(3 + dx);
+  return __builtin_amdgcn_perm(R[3 + dy].y, R[3 + dy].x, j | (0x0cu << 8) | ((j + 1) << 16) | (0x0cu << 24));
+}
+
+__device__ __forceinline__ fshort2 fast_m2_regs(const uint2* R) {
+  const fshort2 v = as_s2(ring_pair(R, 0, 0));
+  fshort2 d[16];
+  d[0] = v - as_s2(ring_pair(R, 3, 0));
+  d[1] = v - as_s2(ring_pair(R, 3, 1));
+  d[2] = v - as_s2(ring_pair(R, 2, 2));
+  d[3] = v - as_s2(ring_pair(R, 1, 3));
+  d[4] = v - as_s2(ring_pair(R, 0, 3));
+  d[5] = v - as_s2(ring_pair(R, -1, 3));
+  d[6] = v - as_s2(ring_pair(R, -2, 2));
+  d[7] = v - as_s2(ring_pair(R, -3, 1));
+  d[8] = v - as_s2(ring_pair(R, -3, 0));
+  d[9] = v - as_s2(ring_pair(R, -3, -1));
+  d[10] = v - as_s2(ring_pair(R, -2, -2));
+  d[11] = v - as_s2(ring_pair(R, -1, -3));
+  d[12] = v - as_s2(ring_pair(R, 0, -3));
+  d[13] = v - as_s2(ring_pair(R, 1, -3));
+  d[14] = v - as_s2(ring_pair(R, 2, -2));
+  d[15] = v - as_s2(ring_pair(R, 3, -1));
+  fshort2 mn2[16], mx2[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    mn2[k] = pmin(d[k], d[(k + 1) & 15]);
+    mx2[k] = pmax(d[k], d[(k + 1) & 15]);
+  }
+  fshort2 mn4[16], mx4[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    mn4[k] = pmin(mn2[k], mn2[(k + 2) & 15]);
+    mx4[k] = pmax(mx2[k], mx2[(k + 2) & 15]);
+  }
+  fshort2 A = {-1024, -1024}, B = {1024, 1024};
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const fshort2 mn8 = pmin(mn4[k], mn4[(k + 4) & 15]);
+    const fshort2 mx8 = pmax(mx4[k], mx4[(k + 4) & 15]);
+    A = pmax(A, pmin(mn8, d[(k + 8) & 15]));
+    B = pmin(B, pmax(mx8, d[(k + 8) & 15]));
+  }
+  const fshort2 zero = {0, 0}, top = {255, 255};
+  return pmin(pmax(pmax(A, zero - B), zero), top);
+}
+
+// 8 bytes x-3 .. x+4 of a row from the 3 aligned dwords at q (x-3 = 4 q + o)
+__device__ __forceinline__ uint2 load_ring_row(const uint32_t* q, uint32_t o) {
+  const uint32_t w0 = q[0], w1 = q[1], w2 = q[2];
+  return make_uint2(__builtin_amdgcn_alignbyte(w1, w0, o), __builtin_amdgcn_alignbyte(w2, w1, o));
 }
 
 // floor(k / n) by multiply-high: inv = ceil(2^32 / n) for n >= 2 (exact for
@@ -425,46 +483,55 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
     return;
   }
   const int ps = fast_pstride(g->fast_win_w);
-  uint32_t* P = fast_smem + wave * fast_wave_words(g->fast_win_w, g->fast_win_h);
-  uint32_t* M = P + g->fast_win_h * ps;
+  uint32_t* M = fast_smem + wave * fast_wave_words(g->fast_win_w, g->fast_win_h);
   const LevelGeom& L = g->lv[cg.level];
   const int cols = cg.x1 - cg.x0, rows = cg.y1 - cg.y0;
-  const int a0 = cg.x0 & ~3, sh = cg.x0 - a0;
-  // ---- stage the window as u16 pairs: dword j of a row -> P[r][4j .. 4j+3] ----
+  const int sh = cg.x0 & 3;
+  // M column q <-> window column q - sh; zero the window (outside = 0)
   {
-    const uint8_t* rowp = pyr + (long long)f * g->pyr_bytes + content_off(L, a0, cg.y0);
-    const int nd = (sh + cols + 3) >> 2;
-    const uint32_t inv = div_inv(nd);
-    const int ntask = rows * nd;
-    for (int k = lane; k < ntask; k += 64) {
-      const int r = div_small(k, inv), j = k - r * nd;
-      const uint32_t* src = reinterpret_cast<const uint32_t*>(rowp + (long long)r * L.pitch) + j;
-      const uint32_t d0 = src[0], d1 = src[1];
-      uint4 o;
-      o.x = __builtin_amdgcn_perm(d1, d0, 0x0c010c00u);
-      o.y = __builtin_amdgcn_perm(d1, d0, 0x0c020c01u);
-      o.z = __builtin_amdgcn_perm(d1, d0, 0x0c030c02u);
-      o.w = __builtin_amdgcn_perm(d1, d0, 0x0c040c03u);
-      *reinterpret_cast<uint4*>(P + r * ps + 4 * j) = o;
-      *reinterpret_cast<uint4*>(M + r * ps + 4 * j) = make_uint4(0, 0, 0, 0);
-    }
+    const int nq = rows * ps / 4;
+    for (int k = lane; k < nq; k += 64) reinterpret_cast<uint4*>(M)[k] = make_uint4(0, 0, 0, 0);
   }
   __builtin_amdgcn_wave_barrier();
-  // ---- m for the detection region rows [3, rows-3), cols [3, cols-3) ----
+  // ---- m for the detection region rows [3, rows-3), cols [3, cols-3):
+  // lane = (column pair p, row segment); each lane walks its rows with the
+  // 7 ring rows of its pair in registers, loaded straight from the level ----
   const int dr = rows - 6, dc = cols - 6;
   const int np = (dc + 1) >> 1;
   const uint32_t inv_np = div_inv(np);
   const int npair = (dr > 0 && dc > 0) ? dr * np : 0;
   uint16_t* M16 = reinterpret_cast<uint16_t*>(M);
-  for (int k = lane; k < npair; k += 64) {
-    const int rr = div_small(k, inv_np), p = k - rr * np;
-    const int r = rr + 3, q = 3 + 2 * p + sh;
-    const fshort2 m2 = fast_m2(P, ps, r, q);
-    const uint32_t lo = (uint32_t)(uint16_t)m2.x;
-    const uint32_t hi = (2 * p + 1 < dc) ? (uint32_t)(uint16_t)m2.y : 0u;
-    M[r * ps + q] = lo | (hi << 16);
-    M16[2 * (r * ps + q - 1) + 1] = (uint16_t)lo;   // M[r][q-1].hi
-    M16[2 * (r * ps + q + 1)] = (uint16_t)hi;       // M[r][q+1].lo
+  if (npair > 0) {
+    const int nseg = max(1, 64 / np);
+    const int rps = (dr + nseg - 1) / nseg;
+    const int seg = div_small(lane, inv_np), p = lane - seg * np;
+    if (seg < nseg) {
+      const int ra = seg * rps, rb = min(ra + rps, dr);   // detection rows
+      const int cx = cg.x0 + 3 + 2 * p;                    // content column of the left centre
+      const int abase = (cx - 3) & ~3;
+      const uint32_t o = (uint32_t)((cx - 3) - abase);
+      const int pdw = L.pitch >> 2;
+      // window row w = content row cg.y0 + w; detection row r = window row r + 3
+      const uint32_t* col = reinterpret_cast<const uint32_t*>(
+          pyr + (long long)f * g->pyr_bytes + content_off(L, abase, cg.y0));
+      uint2 R[7];
+#pragma unroll
+      for (int k = 0; k < 6; k++) R[k + 1] = load_ring_row(col + (long long)(ra + k) * pdw, o);
+      const int q = 3 + 2 * p + sh;
+      const bool has_hi = 2 * p + 1 < dc;
+      for (int r = ra; r < rb; r++) {
+#pragma unroll
+        for (int k = 0; k < 6; k++) R[k] = R[k + 1];
+        R[6] = load_ring_row(col + (long long)(r + 6) * pdw, o);
+        const fshort2 m2 = fast_m2_regs(R);
+        const int wr = r + 3;
+        const uint32_t lo = (uint32_t)(uint16_t)m2.x;
+        const uint32_t hi = has_hi ? (uint32_t)(uint16_t)m2.y : 0u;
+        M[wr * ps + q] = lo | (hi << 16);
+        M16[2 * (wr * ps + q - 1) + 1] = (uint16_t)lo;   // M[wr][q-1].hi
+        M16[2 * (wr * ps + q + 1)] = (uint16_t)hi;       // M[wr][q+1].lo
+      }
+    }
   }
   __builtin_amdgcn_wave_barrier();
   int t = ini_th < 0 ? 0 : (ini_th > 255 ? 255 : ini_th);
@@ -893,13 +960,16 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
   if (opos >= kp_pitch) return;
   const uint32_t c = kp_list[(long long)f * g->kp_cap_total + slot];
   const int kx = cand_x(c) + kMinBorder, ky = cand_y(c) + kMinBorder;
-  // --- IC_Angle: lane u+15 sums column u over the disc ---
+  // --- IC_Angle: 62 lanes, lane = column u + 15 and half of the disc rows
+  // (v in [-15, 0) or [0, 15]) ---
   const uint8_t* img = pyr + (long long)f * g->pyr_bytes + content_off(L, kx, ky);
   int m01 = 0, m10 = 0;
-  if (lane < 31) {
-    const int u = lane - 15;
+  if (lane < 62) {
+    const int half = lane >= 31 ? 1 : 0;
+    const int u = lane - 31 * half - 15;
     const int au = u < 0 ? -u : u;
-    for (int v = -15; v <= 15; v++) {
+    const int v0 = half ? 0 : -15, v1 = half ? 15 : -1;
+    for (int v = v0; v <= v1; v++) {
       const int av = v < 0 ? -v : v;
       if (au <= g->umax[av]) {
         int val = img[(long long)v * L.pitch + u];
