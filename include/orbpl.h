@@ -344,6 +344,10 @@ int orbpl_tracker_stage_ms(orbpl_tracker* tr, float* ms5);
  * octree, orient+desc, glue+predict, match, pose, finish. */
 int orbpl_tracker_timings(orbpl_tracker* tr, int max_steps, float* ms, int* n_steps);
 int orbpl_tracker_timings_reset(orbpl_tracker* tr);
+/* Debug (ORBPL_POSE_PROFILE set): stream 0's PoseOptimization phase times of
+ * the last step in ns (edges, linearize reduction, solve+exp, trial errors,
+ * classify), the LM iteration / trial counts, the linearize edge loop (ns). */
+int orbpl_tracker_debug_pose_profile(orbpl_tracker* tr, long long* out8);
 /* Per-stream frame outputs of the last step (host copies, kp_cap entries per
  * stream, see orbpl_tracker_kp_capacity): undistorted keypoints, descriptors,
  * match (last-frame index per keypoint or -1), outlier flags. */

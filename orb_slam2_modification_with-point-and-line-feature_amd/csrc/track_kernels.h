@@ -223,6 +223,8 @@ void launch_frame_prepare(const TrackConsts& c, const KeyPointD* kps, const int*
 void launch_predict(StreamState* st, int nstreams, hipStream_t s);
 void launch_match_last(const TrackConsts& c, const MatchLaunch& m, int nstreams, hipStream_t s);
 void launch_pose(const TrackConsts& c, const PoseLaunch& p, int nstreams, hipStream_t s);
+// debug: stream 0 phase ticks of the last k_pose launch (ORBPL_POSE_PROFILE)
+int read_pose_profile(long long* out8);
 // Line part of k_finish (all NULL when lines are disabled).
 struct LineFinish {
   const int* nl;

@@ -16,6 +16,8 @@
 //                     style keyframe: every keypoint with depth, Tracking.cc:
 //                     608-660 / Frame::UnprojectStereo)
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 #include <stdint.h>
 
 #include "orbpl_math.h"
@@ -739,6 +741,8 @@ __device__ void edge_jacobian(const PoseEdge& e, const PoseCam& c, const SE3d& T
       J[0][3 + k] = M0[0] * (-1.0 * S1[0][k]) + M0[1] * (-1.0 * S1[1][k]) + M0[2] * (-1.0 * S1[2][k]);
       J[1][k] = 0.0;
       J[1][3 + k] = 0.0;
+      J[2][k] = 0.0;
+      J[2][3 + k] = 0.0;
     }
     return;
   }
@@ -837,28 +841,38 @@ __device__ __forceinline__ void huber(double chi, double delta, double dsqr, dou
 }
 
 __device__ bool solve6(const double A[6][6], const double b[6], double x[6]) {
+  // LDL^T without pivoting (pinned P8); fully unrolled so every array index
+  // is a compile-time constant (registers, no scratch)
   double L[6][6], D[6];
-  for (int i = 0; i < 6; i++)
-    for (int j = 0; j < 6; j++) L[i][j] = 0;
+  bool ok = true;
+#pragma unroll
   for (int j = 0; j < 6; j++) {
     double d = A[j][j];
+#pragma unroll
     for (int k = 0; k < j; k++) d -= L[j][k] * L[j][k] * D[k];
     D[j] = d;
-    if (!(d > 0)) return false;
+    ok = ok && (d > 0);
+#pragma unroll
     for (int i = j + 1; i < 6; i++) {
       double s = A[i][j];
+#pragma unroll
       for (int k = 0; k < j; k++) s -= L[i][k] * L[j][k] * D[k];
       L[i][j] = s / d;
     }
   }
+  if (!ok) return false;
   double y[6];
+#pragma unroll
   for (int i = 0; i < 6; i++) {
     double s = b[i];
+#pragma unroll
     for (int k = 0; k < i; k++) s -= L[i][k] * y[k];
     y[i] = s;
   }
+#pragma unroll
   for (int i = 5; i >= 0; i--) {
     double s = y[i] / D[i];
+#pragma unroll
     for (int k = i + 1; k < 6; k++) s -= L[k][i] * x[k];
     x[i] = s;
   }
@@ -894,7 +908,13 @@ struct PoseArgs {
   const int* t_nl;
   uint8_t* t_loutlier;
   int lpitch;
+  int prof;                   // debug: phase stamps of stream 0 into g_pose_prof
 };
+
+// debug (ORBPL_POSE_PROFILE): accumulated wall-clock ticks (100 MHz) of
+// stream 0's pose: [0] edges, [1] linearize+reduce, [2] solve+exp,
+// [3] trial errors+reduce, [4] classify, [5] LM iterations, [6] trials
+__device__ long long g_pose_prof[8];
 
 __device__ void se3_from_T(const float* T, SE3d& s) {
   double R[3][3];
@@ -918,6 +938,16 @@ __global__ void __launch_bounds__(256) k_pose(TrackConsts tc, PoseArgs a) {
     return;
   }
   const PoseCam c{tc.fx, tc.fy, tc.cx, tc.cy, tc.bf};
+  const bool stamp = a.prof && s == 0 && t == 0;
+  long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  long long t0 = stamp ? (long long)wall_clock64() : 0;
+  auto lap = [&](int k) {
+    if (stamp) {
+      const long long t1 = (long long)wall_clock64();
+      pt[k] += t1 - t0;
+      t0 = t1;
+    }
+  };
   const long long cb = (long long)s * a.kp_pitch;
   const int n = a.n[s];
   uint8_t* outl = a.outlier + cb;
@@ -1026,6 +1056,7 @@ __global__ void __launch_bounds__(256) k_pose(TrackConsts tc, PoseArgs a) {
     S.misc[2] = nlines;
   }
   __syncthreads();
+  lap(0);
   const int ne = S.misc[0];
   nlines = S.misc[2];
   float* Tout = a.Tcw + (long long)s * a.pose_stride;
@@ -1067,9 +1098,11 @@ __global__ void __launch_bounds__(256) k_pose(TrackConsts tc, PoseArgs a) {
           const PoseEdge e = E[k];
           double err[3], J[3][6];
           edge_error(e, c, T, R, err);
-          const int dim = e.kind == 1 ? 3 : 2;
-          double x2 = 0;
-          for (int d = 0; d < dim; d++) x2 += err[d] * (double)e.info * err[d];
+          // rows beyond the edge's dimension are zero (err[2] = 0 and J row 2
+          // = 0 for mono and line edges): adding them leaves every sum exact
+          double x2 = err[0] * (double)e.info * err[0];
+          x2 += err[1] * (double)e.info * err[1];
+          x2 += err[2] * (double)e.info * err[2];
           S.chi2[k] = x2;
           double w = 1.0, r0 = x2;
           if (robust) {
@@ -1079,19 +1112,29 @@ __global__ void __launch_bounds__(256) k_pose(TrackConsts tc, PoseArgs a) {
           acc[27] += r0;
           edge_jacobian(e, c, T, R, J);
           const double info = (double)e.info;
-          int q = 0;
+          const double wi = w * info;
+#pragma unroll
           for (int i = 0; i < 6; i++) {
-            double bi = 0;
-            for (int d = 0; d < dim; d++) bi += J[d][i] * info * err[d];
+            double bi = J[0][i] * info * err[0];
+            bi += J[1][i] * info * err[1];
+            bi += J[2][i] * info * err[2];
             acc[21 + i] -= w * bi;
+          }
+#pragma unroll
+          for (int i = 0; i < 6; i++) {
+#pragma unroll
             for (int j = i; j < 6; j++) {
-              double h = 0;
-              for (int d = 0; d < dim; d++) h += J[d][i] * (w * info) * J[d][j];
-              acc[q++] += h;
+              double h = J[0][i] * wi * J[0][j];
+              h += J[1][i] * wi * J[1][j];
+              h += J[2][i] * wi * J[2][j];
+              acc[6 * i - i * (i - 1) / 2 + (j - i)] += h;
             }
           }
         }
+        lap(7);
         block_sum28_to(acc, S, S.sys[0]);
+        lap(1);
+        pt[5]++;
         double b[6];
         for (int i = 0; i < 6; i++) b[i] = S.sys[0][21 + i];
         double currentChi = S.sys[0][27];
@@ -1110,17 +1153,21 @@ __global__ void __launch_bounds__(256) k_pose(TrackConsts tc, PoseArgs a) {
           double Hl[6][6];
           {
             const double* sy = S.sys[0];
-            int q = 0;
+#pragma unroll
             for (int i = 0; i < 6; i++)
+#pragma unroll
               for (int j = i; j < 6; j++) {
-                Hl[i][j] = sy[q];
-                Hl[j][i] = sy[q];
-                q++;
+                const double v = sy[6 * i - i * (i - 1) / 2 + (j - i)];
+                Hl[i][j] = v;
+                Hl[j][i] = v;
               }
           }
+#pragma unroll
           for (int j = 0; j < 6; j++) Hl[j][j] += lambda;
           const bool ok2 = solve6(Hl, b, x);
           T = se3_mul(se3_exp(x), T);
+          lap(2);
+          pt[6]++;
           // computeActiveErrors at the trial estimate
           double R2[3][3];
           quat_to_R(T.q, R2);
@@ -1142,6 +1189,7 @@ __global__ void __launch_bounds__(256) k_pose(TrackConsts tc, PoseArgs a) {
             tc2 += r0;
           }
           block_sum<1>(&tc2, S);
+          lap(3);
           double tempChi = ok2 ? tc2 : 1.7976931348623157e308;
           rho = currentChi - tempChi;
           double scale = 0;
@@ -1201,6 +1249,7 @@ __global__ void __launch_bounds__(256) k_pose(TrackConsts tc, PoseArgs a) {
       nbad = (int)v;
     }
     nBadOut = nbad;
+    lap(4);
     if (round == 2) robust = false;
     // every thread ran the same LM control flow on the same reduced sums, so
     // T is identical in all threads (no broadcast needed)
@@ -1226,6 +1275,9 @@ __global__ void __launch_bounds__(256) k_pose(TrackConsts tc, PoseArgs a) {
     }
   }
   if (t == 0) a.ninliers[(long long)s * a.nm_stride] = npts - nBadOut;
+  if (stamp)
+    for (int k = 0; k < 8; k++) g_pose_prof[k] = pt[k];
+  // (pt[7]: linearize edge loop only; pt[1]: its block reduction)
 }
 
 // ---------------------------------------------------------------------------
@@ -1396,6 +1448,10 @@ void launch_match_last(const TrackConsts& c, const MatchLaunch& m, int nstreams,
                        c, a);
 }
 
+int read_pose_profile(long long* out8) {
+  return hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_pose_prof), 8 * sizeof(long long)) == hipSuccess ? 0 : -1;
+}
+
 void launch_pose(const TrackConsts& c, const PoseLaunch& p, int nstreams, hipStream_t s) {
   static bool done = false;
   set_smem_attr_once((const void*)k_pose, sizeof(PoseShared), &done);
@@ -1426,6 +1482,8 @@ void launch_pose(const TrackConsts& c, const PoseLaunch& p, int nstreams, hipStr
   a.t_nl = p.t_nl;
   a.t_loutlier = p.t_loutlier;
   a.lpitch = p.lpitch;
+  static const int prof = getenv("ORBPL_POSE_PROFILE") ? 1 : 0;
+  a.prof = prof;
   hipLaunchKernelGGL(k_pose, dim3(nstreams), dim3(256), sizeof(PoseShared), s, c, a);
 }
 

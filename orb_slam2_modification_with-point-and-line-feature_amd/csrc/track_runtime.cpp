@@ -1286,6 +1286,22 @@ int orbpl_tracker_stereo_timings(orbpl_tracker* t, int max_steps, float* ms, int
   return ORBPL_OK;
 }
 
+// Debug (ORBPL_POSE_PROFILE): stream 0's PoseOptimization phase times of the
+// last step, ns: edges, linearize+reduce, solve+exp, trial errors+reduce,
+// classify; then LM iterations and trials (counts).
+int orbpl_tracker_debug_pose_profile(orbpl_tracker* t, long long* out7) {  // 8 values
+  if (!t || !out7) return arg_fail("NULL argument");
+  HIP_CHECK(hipSetDevice(t->device));
+  HIP_CHECK(hipDeviceSynchronize());
+  long long p[8];
+  if (read_pose_profile(p)) return arg_fail("pose profile unavailable");
+  for (int k = 0; k < 5; k++) out7[k] = p[k] * 10;
+  out7[5] = p[5];
+  out7[6] = p[6];
+  out7[7] = p[7] * 10;
+  return ORBPL_OK;
+}
+
 int orbpl_tracker_timings_reset(orbpl_tracker* t) {
   if (!t) return arg_fail("NULL tracker");
   t->ring_count = 0;
