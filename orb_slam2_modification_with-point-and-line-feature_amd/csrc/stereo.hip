@@ -61,28 +61,27 @@ __global__ void __launch_bounds__(256) k_stereo(StereoArgs a) {
   __shared__ int s_cnt, s_wsum[4];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int f = blockIdx.x;
-  {  // this frame's slice of the batch
-    const long long o = (long long)f * a.kp_pitch;
-    a.n = a.n_arr ? a.n_arr[f] : a.n;
-    a.nr = a.nr_arr ? a.nr_arr[f] : a.nr;
-    a.kl += o;
-    a.kr += o;
-    a.dl += o * 32;
-    a.dr += o * 32;
-    a.uright += o;
-    a.depth += o;
-    a.sad += o;
-    a.pyrL += (long long)f * a.pyr_pitch;
-    a.pyrR += (long long)f * a.pyr_pitch;
-    a.entries += (long long)f * a.entry_cap;
-  }
-  const int n = min(a.n, kStereoKp), nr = min(a.nr, kStereoKp);
+  // this frame's slice of the batch (locals: the kernel argument stays
+  // read-only, so its level table is never copied to scratch)
+  const long long fo = (long long)f * a.kp_pitch;
+  const KeyPointD* __restrict__ a_kl = a.kl + fo;
+  const KeyPointD* __restrict__ a_kr = a.kr + fo;
+  const uint8_t* __restrict__ a_dl = a.dl + fo * 32;
+  const uint8_t* __restrict__ a_dr = a.dr + fo * 32;
+  float* __restrict__ a_uright = a.uright + fo;
+  float* __restrict__ a_depth = a.depth + fo;
+  int* __restrict__ a_sad = a.sad + fo;
+  const uint8_t* a_pyrL = a.pyrL + (long long)f * a.pyr_pitch;
+  const uint8_t* a_pyrR = a.pyrR + (long long)f * a.pyr_pitch;
+  uint16_t* __restrict__ a_entries = a.entries + (long long)f * a.entry_cap;
+  const int n = min(a.n_arr ? a.n_arr[f] : a.n, kStereoKp);
+  const int nr = min(a.nr_arr ? a.nr_arr[f] : a.nr, kStereoKp);
   const int nRows = a.nrows;
   // ---- 1. row bands ----
   for (int i = t; i <= kStereoRows; i += 256) row_start[i] = 0;
   __syncthreads();
   for (int iR = t; iR < nr; iR += 256) {
-    const KeyPointD k = a.kr[iR];
+    const KeyPointD k = a_kr[iR];
     const float r = 2.0f * a.scale[k.octave];
     const int maxr = (int)ceilf(k.y + r), minr = (int)floorf(k.y - r);
     for (int yi = max(minr, 0); yi <= min(maxr, nRows - 1); yi++) atomicAdd(&row_start[yi], 1);
@@ -120,23 +119,23 @@ __global__ void __launch_bounds__(256) k_stereo(StereoArgs a) {
     return;
   }
   for (int iR = t; iR < nr; iR += 256) {
-    const KeyPointD k = a.kr[iR];
+    const KeyPointD k = a_kr[iR];
     const float r = 2.0f * a.scale[k.octave];
     const int maxr = (int)ceilf(k.y + r), minr = (int)floorf(k.y - r);
     for (int yi = max(minr, 0); yi <= min(maxr, nRows - 1); yi++)
-      a.entries[atomicAdd(&row_fill[yi], 1)] = (uint16_t)iR;
+      a_entries[atomicAdd(&row_fill[yi], 1)] = (uint16_t)iR;
   }
   __syncthreads();
   for (int row = t; row < nRows; row += 256) {  // increasing index within a row
     const int b = row_start[row], e = row_start[row + 1];
     for (int q = b + 1; q < e; q++) {
-      const uint16_t v = a.entries[q];
+      const uint16_t v = a_entries[q];
       int r = q - 1;
-      while (r >= b && a.entries[r] > v) {
-        a.entries[r + 1] = a.entries[r];
+      while (r >= b && a_entries[r] > v) {
+        a_entries[r + 1] = a_entries[r];
         r--;
       }
-      a.entries[r + 1] = v;
+      a_entries[r + 1] = v;
     }
   }
   if (t == 0) s_cnt = 0;
@@ -144,10 +143,10 @@ __global__ void __launch_bounds__(256) k_stereo(StereoArgs a) {
   // ---- 2. per left keypoint ----
   const float mbf = a.mbf, minZ = a.mb, minD = 0, maxD = mbf / minZ;
   for (int iL = t; iL < n; iL += 256) {
-    a.uright[iL] = -1.0f;
-    a.depth[iL] = -1.0f;
-    a.sad[iL] = -1;
-    const KeyPointD kpL = a.kl[iL];
+    a_uright[iL] = -1.0f;
+    a_depth[iL] = -1.0f;
+    a_sad[iL] = -1;
+    const KeyPointD kpL = a_kl[iL];
     const int levelL = kpL.octave;
     const float vL = kpL.y, uL = kpL.x;
     const int row = (int)vL;
@@ -157,14 +156,14 @@ __global__ void __launch_bounds__(256) k_stereo(StereoArgs a) {
     const float minU = uL - maxD, maxU = uL - minD;
     if (maxU < 0) continue;
     int bestDist = 100, bestIdxR = 0;
-    const uint8_t* dL = a.dl + (long long)iL * 32;
+    const uint8_t* dL = a_dl + (long long)iL * 32;
     for (int q = rb; q < re; q++) {
-      const int iR = a.entries[q];
-      const KeyPointD kpR = a.kr[iR];
+      const int iR = a_entries[q];
+      const KeyPointD kpR = a_kr[iR];
       if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
       const float uR = kpR.x;
       if (uR >= minU && uR <= maxU) {
-        const int dist = ham32(dL, a.dr + (long long)iR * 32);
+        const int dist = ham32(dL, a_dr + (long long)iR * 32);
         if (dist < bestDist) {
           bestDist = dist;
           bestIdxR = iR;
@@ -172,7 +171,7 @@ __global__ void __launch_bounds__(256) k_stereo(StereoArgs a) {
       }
     }
     if (bestDist >= (100 + 50) / 2) continue;
-    const float uR0 = a.kr[bestIdxR].x;
+    const float uR0 = a_kr[bestIdxR].x;
     const float scaleFactor = a.inv_scale[levelL];
     const float scaleduL = roundf(kpL.x * scaleFactor);
     const float scaledvL = roundf(kpL.y * scaleFactor);
@@ -184,8 +183,8 @@ __global__ void __launch_bounds__(256) k_stereo(StereoArgs a) {
     const float endu = scaleduR0 + L + w + 1;
     if (iniu < 0 || endu >= G.w) continue;
     if (cvL - w < 0 || cvL + w >= G.h || cuL - w < 0 || cuL + w >= G.w || cuR - L - w < 0) continue;
-    const uint8_t* PL = a.pyrL + content_off(G, 0, 0);
-    const uint8_t* PR = a.pyrR + content_off(G, 0, 0);
+    const uint8_t* PL = a_pyrL + content_off(G, 0, 0);
+    const uint8_t* PR = a_pyrR + content_off(G, 0, 0);
     const int cL = PL[(long long)cvL * G.pitch + cuL];
     int sads[11];
 #pragma unroll
@@ -236,9 +235,9 @@ __global__ void __launch_bounds__(256) k_stereo(StereoArgs a) {
         disparity = 0.01f;
         bestuR = (float)((double)uL - 0.01);
       }
-      a.depth[iL] = mbf / disparity;
-      a.uright[iL] = bestuR;
-      a.sad[iL] = bestD;
+      a_depth[iL] = mbf / disparity;
+      a_uright[iL] = bestuR;
+      a_sad[iL] = bestD;
       atomicAdd(&s_cnt, 1);
     }
   }
@@ -247,7 +246,7 @@ __global__ void __launch_bounds__(256) k_stereo(StereoArgs a) {
   const int cnt = s_cnt;
   if (cnt == 0) return;
   for (int i = t; i < kStereoKp; i += 256) {
-    const int d = i < n ? a.sad[i] : -1;
+    const int d = i < n ? a_sad[i] : -1;
     keys[i] = d >= 0 ? ((uint32_t)d << 12) | (uint32_t)i : 0xFFFFFFFFu;
   }
   __syncthreads();
@@ -255,10 +254,10 @@ __global__ void __launch_bounds__(256) k_stereo(StereoArgs a) {
   const float median = (float)(int)(keys[cnt / 2] >> 12);
   const float thDist = 1.5f * 1.4f * median;
   for (int iL = t; iL < n; iL += 256) {
-    const int d = a.sad[iL];
+    const int d = a_sad[iL];
     if (d >= 0 && !(d < thDist)) {
-      a.uright[iL] = -1.0f;
-      a.depth[iL] = -1.0f;
+      a_uright[iL] = -1.0f;
+      a_depth[iL] = -1.0f;
     }
   }
 }
