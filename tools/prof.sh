@@ -10,9 +10,9 @@ cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 # points headline (256 streams) by default; MODE=lines profiles configs[2]
 if [ "$MODE" = "lines" ]; then
-  B="$R/bench.py --workload lines --streams 1536 --steps 3 --warmup 1 --no-cpu-baseline"
+  B="$R/bench.py --workload lines --streams 1536 --steps 3 --warmup 1 --ate-streams 0 --no-cpu-baseline"
 else
-  B="$R/bench.py --steps 4 --warmup 2 --secondary-steps 0 --no-cpu-baseline"
+  B="$R/bench.py --steps 20 --warmup 5 --secondary-steps 0 --stereo-steps 0 --rig-steps 0 --ate-streams 0 --no-cpu-baseline"
 fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$out/trace -o run --output-format csv -- python3 $B > $R/$out/trace.log 2>&1 || { echo "trace failed"; tail -5 $R/$out/trace.log; exit 1; }
 echo trace ok
