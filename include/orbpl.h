@@ -348,6 +348,10 @@ int orbpl_tracker_timings_reset(orbpl_tracker* tr);
  * the last step in ns (edges, linearize reduction, solve+exp, trial errors,
  * classify), the LM iteration / trial counts, the linearize edge loop (ns). */
 int orbpl_tracker_debug_pose_profile(orbpl_tracker* tr, long long* out8);
+/* Debug (ORBPL_MATCH_PROFILE set): stream 0's last-frame SearchByProjection
+ * phase times of the last step in ns (grid, candidates, ordered claims,
+ * rotation check, output). */
+int orbpl_tracker_debug_match_profile(orbpl_tracker* tr, long long* out5);
 /* Per-stream frame outputs of the last step (host copies, kp_cap entries per
  * stream, see orbpl_tracker_kp_capacity): undistorted keypoints, descriptors,
  * match (last-frame index per keypoint or -1), outlier flags. */

@@ -225,6 +225,8 @@ void launch_match_last(const TrackConsts& c, const MatchLaunch& m, int nstreams,
 void launch_pose(const TrackConsts& c, const PoseLaunch& p, int nstreams, hipStream_t s);
 // debug: stream 0 phase ticks of the last k_pose launch (ORBPL_POSE_PROFILE)
 int read_pose_profile(long long* out8);
+// debug: stream 0 phase ticks of the last k_match_last launch (ORBPL_MATCH_PROFILE)
+int read_match_profile(long long* out8);
 // Line part of k_finish (all NULL when lines are disabled).
 struct LineFinish {
   const int* nl;

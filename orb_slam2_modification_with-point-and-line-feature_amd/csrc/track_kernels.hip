@@ -122,7 +122,12 @@ struct MatchArgs {
   int check_ori;
   int retry;                    // TrackWithMotionModel: if nmatches < 20 redo with 2*th
   const StreamState* active;    // optional: skip streams without a last frame
+  int prof;                     // debug: phase stamps of stream 0 into g_match_prof
 };
+
+// debug (ORBPL_MATCH_PROFILE): wall-clock ticks (100 MHz) of stream 0's
+// SearchByProjection: [0] grid, [1] phase A, [2] phase B, [3] phase C, [4] output
+__device__ long long g_match_prof[8];
 
 __device__ __forceinline__ int hamming32(const uint8_t* a, const uint8_t* b) {
   const uint4 a0 = *reinterpret_cast<const uint4*>(a);
@@ -132,6 +137,18 @@ __device__ __forceinline__ int hamming32(const uint8_t* a, const uint8_t* b) {
   return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
          __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
 }
+
+// Hamming distance of a descriptor held in registers and one in LDS
+__device__ __forceinline__ int hamming_rl(uint4 a0, uint4 a1, const uint4* b) {
+  const uint4 b0 = b[0], b1 = b[1];
+  return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+         __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
+// Current-frame descriptors are staged in LDS when they fit (KMAX <= 1024:
+// 32 KB); the 2048-keypoint variant reads them from global memory.
+__host__ __device__ constexpr bool match_desc_lds(int kmax) { return kmax <= 1024; }
+__host__ __device__ constexpr int match_desc_slots(int kmax) { return match_desc_lds(kmax) ? 2 * kmax : 1; }
 
 struct ProjInfo {
   bool ok;
@@ -180,39 +197,43 @@ __device__ __forceinline__ ProjInfo project_point(const TrackConsts& c, const fl
 
 // Frame::GetFeaturesInArea + the best-candidate loop (ORBmatcher.cc:1789-1826).
 // Returns (dist << 16) | idx of the first minimum in scan order, or -1.
-template <class SH>
+template <bool kLdsDesc, class SH>
 __device__ int scan_best(const SH& S, const TrackConsts& c, const ProjInfo& p,
                          const uint8_t* dMP, const uint8_t* cur_desc, bool use_claims,
                          float mbf) {
+  const uint4 m0 = *reinterpret_cast<const uint4*>(dMP);
+  const uint4 m1 = *reinterpret_cast<const uint4*>(dMP + 16);
   int bestDist = 256, bestIdx = -1;
   const bool bCheckLevels = (p.minLevel > 0) || (p.maxLevel >= 0);
   const float r = p.radius;
+  // cells are numbered column-major (ix * rows + iy), so the reference's
+  // inner iy loop over one grid column is one contiguous run of items
   for (int ix = p.cx0; ix <= p.cx1; ix++) {
-    for (int iy = p.cy0; iy <= p.cy1; iy++) {
-      const int cell = ix + kGridCols * iy;
-      const int b = S.cell_start[cell], e = S.cell_start[cell + 1];
-      for (int q = b; q < e; q++) {
-        const int j = S.items[q];
-        const int oc = S.oct[j];
-        if (bCheckLevels) {
-          if (oc < p.minLevel) continue;
-          if (p.maxLevel >= 0 && oc > p.maxLevel) continue;
-        }
-        const float2 xy = S.xy[j];
-        const float distx = xy.x - p.u, disty = xy.y - p.v;
-        if (!(fabsf(distx) < r && fabsf(disty) < r)) continue;
-        if (use_claims && ((S.claimed[j >> 5] >> (j & 31)) & 1u)) continue;
-        const float urj = S.ur[j];
-        if (urj > 0) {
-          const float ur = p.u - mbf * p.invzc;
-          const float er = fabsf(ur - urj);
-          if (er > p.radius) continue;
-        }
-        const int dist = hamming32(dMP, cur_desc + (long long)j * 32);
-        if (dist < bestDist) {
-          bestDist = dist;
-          bestIdx = j;
-        }
+    const int b = S.cell_start[ix * kGridRows + p.cy0];
+    const int e = S.cell_start[ix * kGridRows + p.cy1 + 1];
+    for (int q = b; q < e; q++) {
+      const int j = S.items[q];
+      const int oc = S.oct[j];
+      if (bCheckLevels) {
+        if (oc < p.minLevel) continue;
+        if (p.maxLevel >= 0 && oc > p.maxLevel) continue;
+      }
+      const float2 xy = S.xy[j];
+      const float distx = xy.x - p.u, disty = xy.y - p.v;
+      if (!(fabsf(distx) < r && fabsf(disty) < r)) continue;
+      if (use_claims && ((S.claimed[j >> 5] >> (j & 31)) & 1u)) continue;
+      const float urj = S.ur[j];
+      if (urj > 0) {
+        const float ur = p.u - mbf * p.invzc;
+        const float er = fabsf(ur - urj);
+        if (er > p.radius) continue;
+      }
+      int dist;
+      if constexpr (kLdsDesc) dist = hamming_rl(m0, m1, &S.desc[2 * j]);
+      else dist = hamming32(dMP, cur_desc + (long long)j * 32);
+      if (dist < bestDist) {
+        bestDist = dist;
+        bestIdx = j;
       }
     }
   }
@@ -236,8 +257,10 @@ struct MatchShared {
   int bin[KMAX];                  // accepted -> histogram bin, else -1
   int sel[KMAX];                  // accepted candidate (current-frame index)
   int mpw[KMAX];                  // last writer (last-frame index) per current keypoint
+  int fc[KMAX];                   // phase B: first claimer lane per candidate (INT_MAX: none)
   uint32_t claimed[KMAX / 32];
   uint32_t removed[KMAX / 32];
+  uint4 desc[match_desc_slots(KMAX)];   // current descriptors (KMAX <= 1024)
   int hist[32];
   int wsum[8];
   int misc[8];
@@ -250,6 +273,16 @@ __global__ void __launch_bounds__(256) k_match_last(TrackConsts c, MatchArgs a) 
   MatchShared<KMAX>& S = *reinterpret_cast<MatchShared<KMAX>*>(smem_raw);
   const int s = blockIdx.x, t = threadIdx.x;
   const int wave = t >> 6, lane = t & 63;
+  const bool stamp = a.prof && s == 0 && t == 0;
+  long long mt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  long long m0 = stamp ? (long long)wall_clock64() : 0;
+  auto lap = [&](int k) {
+    if (stamp) {
+      const long long m1 = (long long)wall_clock64();
+      mt[k] += m1 - m0;
+      m0 = m1;
+    }
+  };
   if (a.active && !a.active[s].has_last) {
     if (t == 0) a.nmatches[(long long)s * a.nm_stride] = 0;
     for (int i = t; i < a.cur_n[s]; i += 256) a.match[(long long)s * a.kp_pitch + i] = -1;
@@ -279,8 +312,14 @@ __global__ void __launch_bounds__(256) k_match_last(TrackConsts c, MatchArgs a) 
       const int py = (int)roundf((k.y - c.minY) * c.gridInvH);
       g = (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) ? -1 : px + kGridCols * py;
     }
+    if (g >= 0) g = (g % kGridCols) * kGridRows + g / kGridCols;   // column-major cell
     S.gc[i] = (int16_t)g;
     if (g >= 0) atomicAdd(&S.cell_start[g], 1);
+    if constexpr (match_desc_lds(KMAX)) {
+      const uint4* dsrc = reinterpret_cast<const uint4*>(cdesc + (long long)i * 32);
+      S.desc[2 * i] = dsrc[0];
+      S.desc[2 * i + 1] = dsrc[1];
+    }
   }
   __syncthreads();
   {  // exclusive scan of the 3072 cell counts (12 per thread)
@@ -332,6 +371,7 @@ __global__ void __launch_bounds__(256) k_match_last(TrackConsts c, MatchArgs a) 
     }
   }
   __syncthreads();
+  lap(0);
   // ---- forward/backward motion (ORBmatcher.cc:1724-1744) ----
   float twc[3], tlc[3];
   gemm_neg_Rt_t(Tc, twc);
@@ -353,40 +393,44 @@ __global__ void __launch_bounds__(256) k_match_last(TrackConsts c, MatchArgs a) 
                                          bForward, bBackward);
         if (p.ok) {
           const uint8_t* dMP = a.last_desc + li * 32;
+          const uint4 m0 = *reinterpret_cast<const uint4*>(dMP);
+          const uint4 m1 = *reinterpret_cast<const uint4*>(dMP + 16);
           const bool bCheckLevels = (p.minLevel > 0) || (p.maxLevel >= 0);
           const float r = p.radius;
           const float urp = p.u - mbf * p.invzc;
+          // column-major cells: one contiguous item run per grid column,
+          // in the reference's (ix outer, iy inner) scan order
           for (int ix = p.cx0; ix <= p.cx1; ix++) {
-            for (int iy = p.cy0; iy <= p.cy1; iy++) {
-              const int cell = ix + kGridCols * iy;
-              const int b = S.cell_start[cell], e = S.cell_start[cell + 1];
-              for (int q = b; q < e; q++) {
-                const int j = S.items[q];
-                const int oc = S.oct[j];
-                if (bCheckLevels) {
-                  if (oc < p.minLevel) continue;
-                  if (p.maxLevel >= 0 && oc > p.maxLevel) continue;
-                }
-                const float2 xy = S.xy[j];
-                if (!(fabsf(xy.x - p.u) < r && fabsf(xy.y - p.v) < r)) continue;
-                const float urj = S.ur[j];
-                if (urj > 0 && fabsf(urp - urj) > p.radius) continue;
-                const int dist = hamming32(dMP, cdesc + (long long)j * 32);
-                if (dist > 100) continue;
-                cnt++;
-                int v = (dist << 16) | j;
-                // stable insertion: equal distances keep scan order; once
-                // inserted, the displaced entries shift down one place each
-                bool ins = false;
+            const int b = S.cell_start[ix * kGridRows + p.cy0];
+            const int e = S.cell_start[ix * kGridRows + p.cy1 + 1];
+            for (int q = b; q < e; q++) {
+              const int j = S.items[q];
+              const int oc = S.oct[j];
+              if (bCheckLevels) {
+                if (oc < p.minLevel) continue;
+                if (p.maxLevel >= 0 && oc > p.maxLevel) continue;
+              }
+              const float2 xy = S.xy[j];
+              if (!(fabsf(xy.x - p.u) < r && fabsf(xy.y - p.v) < r)) continue;
+              const float urj = S.ur[j];
+              if (urj > 0 && fabsf(urp - urj) > p.radius) continue;
+              int dist;
+              if constexpr (match_desc_lds(KMAX)) dist = hamming_rl(m0, m1, &S.desc[2 * j]);
+              else dist = hamming32(dMP, cdesc + (long long)j * 32);
+              if (dist > 100) continue;
+              cnt++;
+              int v = (dist << 16) | j;
+              // stable insertion: equal distances keep scan order; once
+              // inserted, the displaced entries shift down one place each
+              bool ins = false;
 #pragma unroll
-                for (int q2 = 0; q2 < kTopK; q2++) {
-                  const int cur = tk[q2];
-                  if (ins || cur < 0 || (v >> 16) < (cur >> 16)) {
-                    tk[q2] = v;
-                    v = cur;
-                    ins = true;
-                    if (v < 0) break;
-                  }
+              for (int q2 = 0; q2 < kTopK; q2++) {
+                const int cur = tk[q2];
+                if (ins || cur < 0 || (v >> 16) < (cur >> 16)) {
+                  tk[q2] = v;
+                  v = cur;
+                  ins = true;
+                  if (v < 0) break;
                 }
               }
             }
@@ -397,13 +441,17 @@ __global__ void __launch_bounds__(256) k_match_last(TrackConsts c, MatchArgs a) 
       for (int q2 = 0; q2 < kTopK; q2++) S.top[i * kTopK + q2] = tk[q2];
       S.ntop[i] = (uint8_t)min(cnt, 255);
     }
-    for (int i = t; i < n; i += 256) S.mpw[i] = -1;
+    for (int i = t; i < n; i += 256) {
+      S.mpw[i] = -1;
+      S.fc[i] = 0x7fffffff;
+    }
     for (int i = t; i < KMAX / 32; i += 256) {
       S.claimed[i] = 0;
       S.removed[i] = 0;
     }
     if (t < 32) S.hist[t] = 0;
     __syncthreads();
+    lap(1);
     // ---- phase B (wave 0): the reference's in-order loop, where a candidate
     // taken by an earlier map point with Observations() > 0 is skipped ----
     if (wave == 0) {
@@ -432,15 +480,17 @@ __global__ void __launch_bounds__(256) k_match_last(TrackConsts c, MatchArgs a) 
             choice = p < ntk ? (S.top[i * kTopK + p] & 0xFFFF) : (S.ntop[i] > kTopK ? -2 : -1);
           }
           // first undecided lane whose choice an earlier undecided claimer takes,
-          // or that needs a re-scan
+          // or that needs a re-scan: every undecided claimer posts its lane to
+          // its choice (atomicMin), then each lane compares the first poster
           const bool und = !decided && lane >= start;
-          const int cq_flag = (und && claimer && choice >= 0) ? 1 : 0;
+          const bool cq = und && claimer && choice >= 0;
+          if (cq) atomicMin(&S.fc[choice], lane);
+          __threadfence_block();
           bool coll = und && choice == -2;
-          for (int q = start; q < 64; q++) {
-            const int chq = __shfl(choice, q, 64);
-            const int flq = __shfl(cq_flag, q, 64);
-            if (q < lane && flq && chq == choice && und && choice >= 0) coll = true;
-          }
+          if (und && choice >= 0 && S.fc[choice] < lane) coll = true;
+          __threadfence_block();
+          if (cq) S.fc[choice] = 0x7fffffff;
+          __threadfence_block();
           const unsigned long long cm = __ballot(coll);
           const int lc = cm ? __ffsll((long long)cm) - 1 : 64;
           if (und && lane < lc) {
@@ -463,7 +513,8 @@ __global__ void __launch_bounds__(256) k_match_last(TrackConsts c, MatchArgs a) 
             // all kTopK candidates taken: full re-scan excluding taken ones
             const ProjInfo pj = project_point(c, Tc, a.last_xyz + li * 3, a.last_kps_un[li].octave,
                                               th, bForward, bBackward);
-            const int r = scan_best(S, c, pj, a.last_desc + li * 32, cdesc, true, mbf);
+            const int r = scan_best<match_desc_lds(KMAX)>(S, c, pj, a.last_desc + li * 32, cdesc,
+                                                          true, mbf);
             if (r >= 0 && (r >> 16) <= 100) {
               const int k = r & 0xFFFF;
               atomicMax(&S.mpw[k], i);
@@ -487,6 +538,7 @@ __global__ void __launch_bounds__(256) k_match_last(TrackConsts c, MatchArgs a) 
       if (lane == 0) S.misc[0] = acc;
     }
     __syncthreads();
+    lap(2);
     nmatches = S.misc[0];
     // ---- phase C: rotation consistency (ORBmatcher.cc:1850-1876, 2035-2077) ----
     if (a.check_ori) {
@@ -528,6 +580,7 @@ __global__ void __launch_bounds__(256) k_match_last(TrackConsts c, MatchArgs a) 
       __syncthreads();
       nmatches -= S.misc[4];
     }
+    lap(3);
     if (!(a.retry && nmatches < 20 && attempt == 0)) break;
     th = 2 * a.th;
     __syncthreads();
@@ -538,6 +591,9 @@ __global__ void __launch_bounds__(256) k_match_last(TrackConsts c, MatchArgs a) 
     a.match[cb + i] = m;
   }
   if (t == 0) a.nmatches[(long long)s * a.nm_stride] = nmatches;
+  lap(4);
+  if (stamp)
+    for (int k = 0; k < 8; k++) g_match_prof[k] = mt[k];
 }
 
 // ---------------------------------------------------------------------------
@@ -1440,12 +1496,18 @@ void launch_match_last(const TrackConsts& c, const MatchLaunch& m, int nstreams,
   a.check_ori = m.check_ori;
   a.retry = m.retry;
   a.active = m.active;
+  static const int prof = getenv("ORBPL_MATCH_PROFILE") ? 1 : 0;
+  a.prof = prof;
   if (m.kp_pitch <= 1024)
     hipLaunchKernelGGL(k_match_last<1024>, dim3(nstreams), dim3(256), sizeof(MatchShared<1024>), s,
                        c, a);
   else
     hipLaunchKernelGGL(k_match_last<2048>, dim3(nstreams), dim3(256), sizeof(MatchShared<2048>), s,
                        c, a);
+}
+
+int read_match_profile(long long* out8) {
+  return hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_match_prof), 8 * sizeof(long long)) == hipSuccess ? 0 : -1;
 }
 
 int read_pose_profile(long long* out8) {

@@ -1302,6 +1302,19 @@ int orbpl_tracker_debug_pose_profile(orbpl_tracker* t, long long* out7) {  // 8 
   return ORBPL_OK;
 }
 
+// Debug (ORBPL_MATCH_PROFILE): stream 0's SearchByProjection(last frame)
+// phase times of the last step, ns: grid, candidates, ordered claims,
+// rotation check, output.
+int orbpl_tracker_debug_match_profile(orbpl_tracker* t, long long* out5) {
+  if (!t || !out5) return arg_fail("NULL argument");
+  HIP_CHECK(hipSetDevice(t->device));
+  HIP_CHECK(hipDeviceSynchronize());
+  long long p[8];
+  if (read_match_profile(p)) return arg_fail("match profile unavailable");
+  for (int k = 0; k < 5; k++) out5[k] = p[k] * 10;
+  return ORBPL_OK;
+}
+
 int orbpl_tracker_timings_reset(orbpl_tracker* t) {
   if (!t) return arg_fail("NULL tracker");
   t->ring_count = 0;

@@ -45,3 +45,11 @@ if os.environ.get("ORBPL_POSE_PROFILE"):
     print("pose stream 0 (us):", {n: round(v / 1000, 1) for n, v in zip(names, out[:5])},
           "iterations", int(out[5]), "trials", int(out[6]),
           "of which linearize edge loop", round(out[7] / 1000, 1))
+if os.environ.get("ORBPL_MATCH_PROFILE"):
+    lib = pkg.lib()
+    lib.orbpl_tracker_debug_match_profile.argtypes = [C.c_void_p, C.c_void_p]
+    out = np.zeros(5, np.int64)
+    pkg.check(lib.orbpl_tracker_debug_match_profile(tr._h, out.ctypes.data_as(C.c_void_p)),
+              "match profile")
+    names = ("grid", "candidates", "ordered_claims", "rotation", "output")
+    print("match stream 0 (us):", {n: round(v / 1000, 1) for n, v in zip(names, out)})
