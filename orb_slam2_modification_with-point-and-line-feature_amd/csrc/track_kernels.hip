@@ -241,6 +241,10 @@ __device__ int scan_best(const SH& S, const TrackConsts& c, const ProjInfo& p,
 }
 
 constexpr int kTopK = 4;
+// k_match_last block size: one block per stream, so the stream count bounds the
+// grid; 1024 threads put all last-frame map points of a stream in one round
+constexpr int kMatchThreads = 1024;
+static_assert((kGridCols * kGridRows) % kMatchThreads == 0, "cell scan split");
 
 template <int KMAX>
 struct MatchShared {
@@ -262,13 +266,13 @@ struct MatchShared {
   uint32_t removed[KMAX / 32];
   uint4 desc[match_desc_slots(KMAX)];   // current descriptors (KMAX <= 1024)
   int hist[32];
-  int wsum[8];
+  int wsum[kMatchThreads / 64];
   int misc[8];
 };
 static_assert(kMatchMaxKp * kTopK >= kGridCols * kGridRows, "top[] doubles as cell fill counters");
 
 template <int KMAX>
-__global__ void __launch_bounds__(256) k_match_last(TrackConsts c, MatchArgs a) {
+__global__ void __launch_bounds__(kMatchThreads) k_match_last(TrackConsts c, MatchArgs a) {
   extern __shared__ char smem_raw[];
   MatchShared<KMAX>& S = *reinterpret_cast<MatchShared<KMAX>*>(smem_raw);
   const int s = blockIdx.x, t = threadIdx.x;
@@ -285,7 +289,7 @@ __global__ void __launch_bounds__(256) k_match_last(TrackConsts c, MatchArgs a) 
   };
   if (a.active && !a.active[s].has_last) {
     if (t == 0) a.nmatches[(long long)s * a.nm_stride] = 0;
-    for (int i = t; i < a.cur_n[s]; i += 256) a.match[(long long)s * a.kp_pitch + i] = -1;
+    for (int i = t; i < a.cur_n[s]; i += kMatchThreads) a.match[(long long)s * a.kp_pitch + i] = -1;
     return;
   }
   const int n = min(a.cur_n[s], KMAX);
@@ -296,9 +300,9 @@ __global__ void __launch_bounds__(256) k_match_last(TrackConsts c, MatchArgs a) 
   const float* Tc = a.Tcw + (long long)s * a.pose_stride;
   const float* Tl = a.Tlw + (long long)s * a.pose_stride;
   // ---- current frame into LDS + grid (AssignFeaturesToGrid, Frame.cc:265-287) ----
-  for (int i = t; i < kGridCols * kGridRows; i += 256) S.cell_start[i] = 0;
+  for (int i = t; i < kGridCols * kGridRows; i += kMatchThreads) S.cell_start[i] = 0;
   __syncthreads();
-  for (int i = t; i < n; i += 256) {
+  for (int i = t; i < n; i += kMatchThreads) {
     const KeyPointD k = ck[i];
     S.xy[i] = make_float2(k.x, k.y);
     S.ang[i] = k.angle;
@@ -322,8 +326,8 @@ __global__ void __launch_bounds__(256) k_match_last(TrackConsts c, MatchArgs a) 
     }
   }
   __syncthreads();
-  {  // exclusive scan of the 3072 cell counts (12 per thread)
-    constexpr int kPer = (kGridCols * kGridRows) / 256;
+  {  // exclusive scan of the 3072 cell counts (kPer per thread)
+    constexpr int kPer = (kGridCols * kGridRows) / kMatchThreads;
     int loc[kPer];
     int sum = 0;
 #pragma unroll
@@ -348,17 +352,17 @@ __global__ void __launch_bounds__(256) k_match_last(TrackConsts c, MatchArgs a) 
       S.top[t * kPer + k] = run;  // fill counter
       run += loc[k];
     }
-    if (t == 255) S.cell_start[kGridCols * kGridRows] = run;
+    if (t == kMatchThreads - 1) S.cell_start[kGridCols * kGridRows] = run;
     __syncthreads();
   }
   // place items (any order), then sort each cell by index: the reference's
   // mGrid[ix][iy] vectors hold indices in increasing order
-  for (int i = t; i < n; i += 256) {
+  for (int i = t; i < n; i += kMatchThreads) {
     const int g = S.gc[i];
     if (g >= 0) S.items[atomicAdd(&S.top[g], 1)] = (uint16_t)i;
   }
   __syncthreads();
-  for (int cell = t; cell < kGridCols * kGridRows; cell += 256) {
+  for (int cell = t; cell < kGridCols * kGridRows; cell += kMatchThreads) {
     const int b = S.cell_start[cell], e = S.cell_start[cell + 1];
     for (int q = b + 1; q < e; q++) {
       const uint16_t v = S.items[q];
@@ -384,7 +388,7 @@ __global__ void __launch_bounds__(256) k_match_last(TrackConsts c, MatchArgs a) 
   for (int attempt = 0; attempt < 2; attempt++) {
     // ---- phase A: per map point, the first kTopK candidates with distance
     // <= TH_HIGH in (distance, scan order), and how many such candidates exist
-    for (int i = t; i < nl; i += 256) {
+    for (int i = t; i < nl; i += kMatchThreads) {
       int tk[kTopK] = {-1, -1, -1, -1};
       int cnt = 0;
       const long long li = cb + i;
@@ -441,11 +445,11 @@ __global__ void __launch_bounds__(256) k_match_last(TrackConsts c, MatchArgs a) 
       for (int q2 = 0; q2 < kTopK; q2++) S.top[i * kTopK + q2] = tk[q2];
       S.ntop[i] = (uint8_t)min(cnt, 255);
     }
-    for (int i = t; i < n; i += 256) {
+    for (int i = t; i < n; i += kMatchThreads) {
       S.mpw[i] = -1;
       S.fc[i] = 0x7fffffff;
     }
-    for (int i = t; i < KMAX / 32; i += 256) {
+    for (int i = t; i < KMAX / 32; i += kMatchThreads) {
       S.claimed[i] = 0;
       S.removed[i] = 0;
     }
@@ -542,7 +546,7 @@ __global__ void __launch_bounds__(256) k_match_last(TrackConsts c, MatchArgs a) 
     nmatches = S.misc[0];
     // ---- phase C: rotation consistency (ORBmatcher.cc:1850-1876, 2035-2077) ----
     if (a.check_ori) {
-      for (int i = t; i < nl; i += 256)
+      for (int i = t; i < nl; i += kMatchThreads)
         if (S.bin[i] >= 0) atomicAdd(&S.hist[S.bin[i]], 1);
       __syncthreads();
       if (t == 0) {
@@ -568,7 +572,7 @@ __global__ void __launch_bounds__(256) k_match_last(TrackConsts c, MatchArgs a) 
       __syncthreads();
       const int ind1 = S.misc[1], ind2 = S.misc[2], ind3 = S.misc[3];
       int nrem = 0;
-      for (int i = t; i < nl; i += 256) {
+      for (int i = t; i < nl; i += kMatchThreads) {
         const int b = S.bin[i];
         if (b >= 0 && b != ind1 && b != ind2 && b != ind3) {
           const int k = S.sel[i];
@@ -585,7 +589,7 @@ __global__ void __launch_bounds__(256) k_match_last(TrackConsts c, MatchArgs a) 
     th = 2 * a.th;
     __syncthreads();
   }
-  for (int i = t; i < n; i += 256) {
+  for (int i = t; i < n; i += kMatchThreads) {
     int m = S.mpw[i];
     if (a.check_ori && ((S.removed[i >> 5] >> (i & 31)) & 1u)) m = -1;
     a.match[cb + i] = m;
@@ -1499,10 +1503,10 @@ void launch_match_last(const TrackConsts& c, const MatchLaunch& m, int nstreams,
   static const int prof = getenv("ORBPL_MATCH_PROFILE") ? 1 : 0;
   a.prof = prof;
   if (m.kp_pitch <= 1024)
-    hipLaunchKernelGGL(k_match_last<1024>, dim3(nstreams), dim3(256), sizeof(MatchShared<1024>), s,
+    hipLaunchKernelGGL(k_match_last<1024>, dim3(nstreams), dim3(kMatchThreads), sizeof(MatchShared<1024>), s,
                        c, a);
   else
-    hipLaunchKernelGGL(k_match_last<2048>, dim3(nstreams), dim3(256), sizeof(MatchShared<2048>), s,
+    hipLaunchKernelGGL(k_match_last<2048>, dim3(nstreams), dim3(kMatchThreads), sizeof(MatchShared<2048>), s,
                        c, a);
 }
 
