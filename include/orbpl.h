@@ -141,6 +141,10 @@ int orbx_last_stage_ms(const orbx_ctx* ctx, float* ms5);
  * launch, 4 per level (content, side borders, mirror rows, blur); needs
  * ORBPL_PYR_PROFILE in the environment when the context is created. */
 int orbx_debug_pyr_profile(orbx_ctx* ctx, long long* out, int cap, int* n);
+/* Debug: k_octree per-level block of frame 0 in the last launch (ORBPL_OCT_PROFILE
+ * set before the first launch): 8 values per level (setup ns, pass loop ns, 0,
+ * retain ns, passes, candidates, final list size, 0), 16 levels. */
+int orbx_debug_octree_profile(orbx_ctx* ctx, long long* out128);
 
 
 /* ------------------------------------------------------------------------

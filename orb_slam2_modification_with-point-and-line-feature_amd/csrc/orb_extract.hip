@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 #include "orb_geom.h"
 #include "orbpl_math.h"
 #include "orb_kernels.h"
@@ -657,6 +659,11 @@ __device__ int block_excl_scan(int* vals, int n, int* s_wsum) {
 // divide nodes in descending (size, creation) order and stop at the first
 // node after which size >= N (prefix sums over the speculative child counts).
 // ---------------------------------------------------------------------------
+// Keys' node indices live in LDS (u16) for levels with at most kOctLdsCand
+// FAST candidates (every level of a 640x480 frame), else in global memory;
+// 8 KB keeps two blocks per CU.
+constexpr int kOctLdsCand = 4096;
+
 struct OctShared {
   uint2 rect[2][kOctMaxList];       // (x0 | y0<<16, x1 | y1<<16)
   int cnt[2][kOctMaxList];
@@ -669,6 +676,7 @@ struct OctShared {
   int scan[kOctMaxList];
   int wsum[8];
   int misc[8];
+  uint16_t kn[kOctLdsCand];         // node of each key when total <= kOctLdsCand
 };
 
 __device__ __forceinline__ uint2 mk_rect(int x0, int y0, int x1, int y1) {
@@ -692,6 +700,12 @@ __device__ __forceinline__ uint2 child_rect(uint2 r, int c) {
   }
 }
 
+// debug (ORBPL_OCT_PROFILE): wall-clock ticks of block (level = blockIdx.x,
+// frame 0): [8 * level + 0] setup, [+1] passes, [+2] phase-2 passes,
+// [+3] retain, [+4] number of passes, [+5] candidates, [+6] final size
+__device__ long long g_oct_prof[8 * 16];
+__device__ int g_oct_prof_on;
+
 __global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
                                                 const uint32_t* __restrict__ cell_cands,
                                                 const int* __restrict__ cell_counts,
@@ -705,6 +719,16 @@ __global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
   const int level = blockIdx.x, f = blockIdx.y, t = threadIdx.x;
   const LevelGeom& L = g->lv[level];
   const int N = L.nfeat;
+  const bool stamp = g_oct_prof_on && f == 0 && t == 0;
+  long long ot[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  long long o0 = stamp ? (long long)wall_clock64() : 0;
+  auto lap = [&](int k) {
+    if (stamp) {
+      const long long o1 = (long long)wall_clock64();
+      ot[k] += o1 - o0;
+      o0 = o1;
+    }
+  };
   const int slots = g->cell_slots;
   int* out_count = kp_count + (long long)f * g->nlevels + level;
   uint32_t* out_list = kp_list + (long long)f * g->kp_cap_total + L.kp_base;
@@ -721,26 +745,35 @@ __global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
     if (t == 0) *out_count = 0;
     return;
   }
-  {
-    const int wave = t >> 6, lane = t & 63;
-    const uint32_t* cc = cell_cands + ((long long)f * g->ncells_total + L.cell_base) * slots;
-    for (int c = wave; c < ncells; c += 4) {
-      int n = ccnt[c], o = S.scan[c];
-      for (int i = lane; i < n; i += 64) K[o + i] = cc[(long long)c * slots + i];
-    }
-  }
-  // ---- 2. initial nodes (ORBextractor.cc:543-585) ----
+  const bool kn_lds = total <= kOctLdsCand;   // block-uniform
+  auto kn_get = [&](int k) -> int { return kn_lds ? (int)S.kn[k] : KN[k]; };
+  auto kn_set = [&](int k, int v) {
+    if (kn_lds) S.kn[k] = (uint16_t)v;
+    else KN[k] = v;
+  };
+  // ---- 2. initial nodes (ORBextractor.cc:543-585), fused with the gather:
+  // thread per key position k, its cell = the last cell whose prefix <= k ----
   const int nIni = L.n_ini;
   const float hX = L.hx;
   const int H = L.max_border_y - kMinBorder;
   for (int i = t; i < nIni; i += 256) S.child[i] = 0;
   __syncthreads();
-  for (int k = t; k < total; k += 256) {
-    uint32_t c = K[k];
-    int idx = (int)((float)cand_x(c) / hX);
-    if (idx >= nIni) idx = nIni - 1;
-    KN[k] = idx;
-    atomicAdd(&S.child[idx], 1);
+  {
+    const uint32_t* cc = cell_cands + ((long long)f * g->ncells_total + L.cell_base) * slots;
+    for (int k = t; k < total; k += 256) {
+      int lo = 0, hi = ncells - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (S.scan[mid] <= k) lo = mid;
+        else hi = mid - 1;
+      }
+      const uint32_t c = cc[(long long)lo * slots + (k - S.scan[lo])];
+      K[k] = c;
+      int idx = (int)((float)cand_x(c) / hX);
+      if (idx >= nIni) idx = nIni - 1;
+      kn_set(k, idx);
+      atomicAdd(&S.child[idx], 1);
+    }
   }
   __syncthreads();
   // list = nonempty initial nodes in order
@@ -757,15 +790,17 @@ __global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
     }
   }
   __syncthreads();
-  for (int k = t; k < total; k += 256) KN[k] = S.upos[KN[k]];
+  for (int k = t; k < total; k += 256) kn_set(k, S.upos[kn_get(k)]);
   // expandable list (for phase 2): empty until a pass creates children
   int nexp = 0;
   bool finish = false;
   bool phase2 = false;
   __syncthreads();
 
+  lap(0);
   while (!finish) {
     const int prevSize = size;
+    ot[4]++;
     // ---- choose the nodes to divide and their processing rank ----
     int nproc;  // number of candidate nodes (speculative in phase 2)
     if (!phase2) {
@@ -803,7 +838,7 @@ __global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
     __syncthreads();
     // ---- sweep 1: child counts ----
     for (int k = t; k < total; k += 256) {
-      int e = KN[k];
+      int e = kn_get(k);
       int r = S.rank[e];
       if (r >= 0) {
         uint32_t c = K[k];
@@ -878,7 +913,7 @@ __global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
     __syncthreads();
     // ---- sweep 2: re-index keys ----
     for (int k = t; k < total; k += 256) {
-      int e = KN[k];
+      int e = kn_get(k);
       int r = S.rank[e];
       int ne;
       if (r >= 0) {
@@ -887,7 +922,7 @@ __global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
       } else {
         ne = S.upos[e];
       }
-      KN[k] = ne;
+      kn_set(k, ne);
     }
     // ---- expandable children in creation order (rank asc, child asc) ----
     for (int r = t; r < kproc; r += 256) {
@@ -922,13 +957,14 @@ __global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
       phase2 = true;
     }
   }
+  lap(1);
   // ---- retain the best key per node (strict >, first in candidate order) ----
   for (int i = t; i < size; i += 256) S.child[i] = 0;
   __syncthreads();
   for (int k = t; k < total; k += 256) {
     uint32_t c = K[k];
     int key = (cand_s(c) << 20) | (kMaxCandPerLevel - k);
-    atomicMax(&S.child[KN[k]], key);
+    atomicMax(&S.child[kn_get(k)], key);
   }
   __syncthreads();
   const int cap = L.kp_cap;
@@ -940,6 +976,11 @@ __global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
     if (size > cap) atomicOr(err_flag, 4);
     *out_count = size < cap ? size : cap;
   }
+  lap(3);
+  ot[5] = total;
+  ot[6] = size;
+  if (stamp)
+    for (int k = 0; k < 8; k++) g_oct_prof[8 * level + k] = ot[k];
 }
 
 // ---------------------------------------------------------------------------
@@ -1049,6 +1090,11 @@ hipError_t upload_pattern(hipStream_t s) {
 
 size_t octree_smem_bytes() { return sizeof(OctShared); }
 
+int read_octree_profile(long long* out128) {
+  return hipMemcpyFromSymbol(out128, HIP_SYMBOL(g_oct_prof), 128 * sizeof(long long)) == hipSuccess
+             ? 0 : -1;
+}
+
 void launch_pyramid(const OrbGeom& hg, const OrbGeom* dg, const uint8_t* img, int stride,
                     long long frame_pitch, uint8_t* pyr, uint8_t* blur, const int* rs,
                     const PyrBand* bands, int nbands, int batch, long long* prof,
@@ -1073,6 +1119,13 @@ void launch_octree(const OrbGeom& hg, const OrbGeom* dg, const uint32_t* cell_ca
     (void)hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
                         (int)sizeof(OctShared));
     attr_set = true;
+  }
+  static bool prof_set = false;
+  if (!prof_set) {
+    const int on = getenv("ORBPL_OCT_PROFILE") ? 1 : 0;
+    (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_oct_prof_on), &on, sizeof(int), 0,
+                                 hipMemcpyHostToDevice, s);
+    prof_set = true;
   }
   hipLaunchKernelGGL(k_octree, dim3(hg.nlevels, batch), dim3(256), sizeof(OctShared), s, dg,
                      cell_cands, cell_counts, kcand, knode, kp_list, kp_count, err_flag);

@@ -251,6 +251,18 @@ int orbx_debug_pyr_profile(orbx_ctx* c, long long* out, int cap, int* n) {
   return ORBPL_OK;
 }
 
+// Debug (ORBPL_OCT_PROFILE set): k_octree per-level block of frame 0 in the
+// last launch, 8 values per level: setup ns, pass loop ns, -, retain ns,
+// passes, candidates, final list size, -.
+int orbx_debug_octree_profile(orbx_ctx* c, long long* out128) {
+  if (!c || !out128) return arg_fail("bad argument");
+  HIP_CHECK(hipStreamSynchronize(c->stream));
+  if (read_octree_profile(out128)) return arg_fail("octree profile unavailable");
+  for (int l = 0; l < 16; l++)
+    for (int k : {0, 1, 2, 3}) out128[8 * l + k] *= 10;
+  return ORBPL_OK;
+}
+
 int orbx_destroy(orbx_ctx* c) {
   free_ctx(c);
   return ORBPL_OK;

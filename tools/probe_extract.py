@@ -46,3 +46,13 @@ if getattr(pkg.lib(), "orbx_debug_pyr_profile", None) is not None and __import__
     for l, r in enumerate(ph):
         print(f"  L{l}: " + " ".join(f"{x:7.1f}" for x in r))
     print(f"  total {ph.sum():.1f} us")
+if __import__("os").environ.get("ORBPL_OCT_PROFILE"):
+    import ctypes as C
+    L = pkg.lib()
+    L.orbx_debug_octree_profile.argtypes = [C.c_void_p, C.c_void_p]
+    out = np.zeros(128, np.int64)
+    pkg.check(L.orbx_debug_octree_profile(ex._h, out.ctypes.data_as(C.c_void_p)), "octree profile")
+    o = out.reshape(16, 8)
+    print("k_octree frame 0 per level: setup_us pass_us retain_us passes cands size")
+    for l in range(8):
+        print(f"  L{l}: {o[l,0]/1000:7.1f} {o[l,1]/1000:7.1f} {o[l,3]/1000:7.1f} {o[l,4]:4d} {o[l,5]:6d} {o[l,6]:5d}")
