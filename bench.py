@@ -339,10 +339,12 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, loca
     frames = S * steps * world
     value = frames / elapsed
 
-    # roofline of the dominant single-launch kernel (pyramid = 8 launches: excluded)
+    # roofline of the dominant single-launch kernel; k_pyramid (pyramid +
+    # borders + blur, one launch) is timed by the "pyramid" stage
     n_kp = float(st["nkeypoints"].mean())
     ab = algorithmic_bytes(n_kp, fw, fh, wl["orb"])
-    names = {"blur": "k_blur", "fast": "k_fast_cells", "octree": "k_octree",
+    ab["pyramid"] = ab["pyramid"] + ab.pop("blur")
+    names = {"pyramid": "k_pyramid", "fast": "k_fast_cells", "octree": "k_octree",
              "orient_desc": "k_orient_desc", "match": "k_match_last", "pose": "k_pose"}
     idx = {k: tr.STAGES.index(k) for k in names}
     dom = max(names, key=lambda k: avg[idx[k]])
@@ -357,6 +359,24 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, loca
             "algorithmic_bytes_per_launch": bytes_launch, "avg_launch_ms": round(dom_ms, 4),
             "per_kernel_GBps": {k: round(ab[k] * S / (float(avg[idx[k]]) * 1e-3) / 1e9, 1)
                                 for k in names}}
+    if args.pipelined and args.isolated_steps > 0:
+        # untimed: more steps with the two HIP streams serialised, so each
+        # kernel's in-stream hipEvent time is its own (pipelined event times
+        # include the other stream's occupancy of the CUs)
+        tr.set_pipelined(False)
+        tr.timings_reset()
+        for k in range(args.isolated_steps):
+            step(warmup + steps + k)
+        tr.synchronize()
+        iso = tr.timings(args.isolated_steps).mean(0)
+        idom = max(names, key=lambda k: iso[idx[k]])
+        ims = float(iso[idx[idom]])
+        roof["isolated"] = {
+            "stage_ms": dict(zip(tr.STAGES, [round(float(x), 4) for x in iso])),
+            "kernel": names[idom], "avg_launch_ms": round(ims, 4),
+            "achieved": round(ab[idom] * S / (ims * 1e-3) / 1e9, 2),
+            "frac": round(ab[idom] * S / (ims * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+            "steps": args.isolated_steps}
     tr.close()
     A = min(args.ate_streams, S)
     T_acc = (accuracy_gpu(pkg, cam, wl, d_gray, d_depth, L, A, local_rank, fb, db)
@@ -396,6 +416,9 @@ def main():
     ap.add_argument("--ate-streams", type=int, default=8,
                     help="streams of the untimed accuracy leg (ATE vs ground truth and vs the "
                          "reference restatement over one loop); 0 = skip")
+    ap.add_argument("--isolated-steps", type=int, default=5,
+                    help="untimed non-pipelined steps after the timed region: per-kernel "
+                         "times without the other stream's interference (roofline.isolated)")
     ap.add_argument("--pipelined", type=int, default=1,
                     help="1 = overlap extraction of step t+1 with tracking of step t")
     args = ap.parse_args()

@@ -190,6 +190,20 @@ __device__ __forceinline__ uint2 load_ring_row(const uint32_t* q, uint32_t o) {
   return make_uint2(__builtin_amdgcn_alignbyte(w1, w0, o), __builtin_amdgcn_alignbyte(w2, w1, o));
 }
 
+// XCD-aware block remap (cdna_hip_programming.md T1): blocks are dealt
+// round-robin over the 8 XCDs, so give the blocks that share an XCD a
+// contiguous range of the grid (here: the same frames), keeping a frame's
+// pyramid re-reads in one XCD's L2. Bijective for any grid size.
+__device__ __forceinline__ void xcd_block(int* bx, int* by) {
+  const int nx = gridDim.x;
+  const int nwg = nx * gridDim.y;
+  const int orig = blockIdx.x + nx * blockIdx.y;
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  *by = wg / nx;
+  *bx = wg - *by * nx;
+}
+
 // floor(k / n) by multiply-high: inv = ceil(2^32 / n) for n >= 2 (exact for
 // k * n < 2^32), inv = 0 for n == 1.
 __device__ __forceinline__ uint32_t div_inv(int n) {
@@ -490,8 +504,9 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
                                                     int min_th) {
   extern __shared__ uint32_t fast_smem[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int f = blockIdx.y;
-  const int cell = blockIdx.x * 4 + wave;
+  int bx, f;
+  xcd_block(&bx, &f);
+  const int cell = bx * 4 + wave;
   if (cell >= g->ncells_total) return;
   const CellGeom cg = cells[cell];
   const int slots = g->cell_slots;
@@ -988,6 +1003,11 @@ __global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
 // IC_Angle on the unblurred level, computeOrbDescriptor on the blurred level,
 // output rows ordered level by level (ORBextractor.cc:1075-1104).
 // ---------------------------------------------------------------------------
+// debug (ORBPL_OCT_PROFILE also enables it): phase ticks of frame 0's first
+// keypoint wave: [0] slot setup, [1] kp load, [2] IC_Angle, [3] atan2/cos/sin,
+// [4] BRIEF tests, [5] stores
+__device__ long long g_od_prof[8];
+
 __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__ pyr,
                                                      const uint8_t* __restrict__ blur,
                                                      const OrbGeom* __restrict__ g,
@@ -997,9 +1017,20 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
                                                      uint8_t* __restrict__ out_desc,
                                                      int kp_pitch, int* __restrict__ out_n) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int f = blockIdx.y;
-  const int slot = blockIdx.x * 4 + wave;
+  int bx, f;
+  xcd_block(&bx, &f);
+  const int slot = bx * 4 + wave;
   if (slot >= g->kp_cap_total) return;
+  const bool stamp = g_oct_prof_on && f == 0 && slot == 0 && lane == 0;
+  long long dt[6] = {0, 0, 0, 0, 0, 0};
+  long long d0 = stamp ? (long long)wall_clock64() : 0;
+  auto lap = [&](int k) {
+    if (stamp) {
+      const long long d1 = (long long)wall_clock64();
+      dt[k] = d1 - d0;
+      d0 = d1;
+    }
+  };
   int level = 0;
   while (level + 1 < g->nlevels && slot >= g->lv[level + 1].kp_base) level++;
   const LevelGeom& L = g->lv[level];
@@ -1015,8 +1046,11 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
   if (idx >= cnts[level]) return;
   const int opos = offset + idx;
   if (opos >= kp_pitch) return;
+  lap(0);
   const uint32_t c = kp_list[(long long)f * g->kp_cap_total + slot];
   const int kx = cand_x(c) + kMinBorder, ky = cand_y(c) + kMinBorder;
+  if (stamp) (void)__builtin_amdgcn_readfirstlane(kx);
+  lap(1);
   // --- IC_Angle: 62 lanes, lane = column u + 15 and half of the disc rows
   // (v in [-15, 0) or [0, 15]) ---
   const uint8_t* img = pyr + (long long)f * g->pyr_bytes + content_off(L, kx, ky);
@@ -1025,14 +1059,22 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
     const int half = lane >= 31 ? 1 : 0;
     const int u = lane - 31 * half - 15;
     const int au = u < 0 ? -u : u;
-    const int v0 = half ? 0 : -15, v1 = half ? 15 : -1;
-    for (int v = v0; v <= v1; v++) {
+    const int v0 = half ? 0 : -15;
+    // all 16 loads of the lane's column issue before any is used (the loop
+    // with a use per load waited one memory latency per row)
+    int val[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const int v = v0 + k;
       const int av = v < 0 ? -v : v;
-      if (au <= g->umax[av]) {
-        int val = img[(long long)v * L.pitch + u];
-        m10 += u * val;
-        m01 += v * val;
-      }
+      const bool in = (half || k < 15) && au <= g->umax[av];
+      val[k] = in ? (int)img[(long long)v * L.pitch + u] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const int v = v0 + k;
+      m10 += u * val[k];
+      m01 += v * val[k];
     }
   }
 #pragma unroll
@@ -1040,11 +1082,14 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
     m10 += __shfl_xor(m10, o, 64);
     m01 += __shfl_xor(m01, o, 64);
   }
+  lap(2);
   const float angle = fast_atan2_deg((float)m01, (float)m10);
   // --- steered BRIEF on the blurred level ---
   const float factorPI = (float)(3.14159265358979323846 / 180.f);
   float a, b;
   cr_cos_sin(angle * factorPI, &a, &b);
+  if (stamp) (void)__builtin_amdgcn_readfirstlane(__float_as_int(a + b));
+  lap(3);
   const uint8_t* bimg = blur + (long long)f * g->blur_bytes + L.boff + (long long)ky * L.bpitch + kx;
   const int step = L.bpitch;
   uint64_t words[4];
@@ -1057,6 +1102,7 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
     const int v2 = bimg[cv_round(x2 * b + y2 * a) * step + cv_round(x2 * a - y2 * b)];
     words[r] = __ballot(v1 < v2);
   }
+  lap(4);
   uint8_t* d = out_desc + ((long long)f * kp_pitch + opos) * 32;
   if (lane < 4) {
     uint64_t w = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
@@ -1078,6 +1124,9 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
     kp.class_id = -1;
     out_kps[(long long)f * kp_pitch + opos] = kp;
   }
+  lap(5);
+  if (stamp)
+    for (int k = 0; k < 6; k++) g_od_prof[k] = dt[k];
 }
 
 // ---------------------------------------------------------------------------
@@ -1089,6 +1138,10 @@ hipError_t upload_pattern(hipStream_t s) {
 }
 
 size_t octree_smem_bytes() { return sizeof(OctShared); }
+
+int read_od_profile(long long* out8) {
+  return hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_od_prof), 6 * sizeof(long long)) == hipSuccess ? 0 : -1;
+}
 
 int read_octree_profile(long long* out128) {
   return hipMemcpyFromSymbol(out128, HIP_SYMBOL(g_oct_prof), 128 * sizeof(long long)) == hipSuccess

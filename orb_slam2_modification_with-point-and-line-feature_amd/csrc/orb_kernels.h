@@ -19,6 +19,7 @@ hipError_t upload_pattern(hipStream_t s);
 size_t octree_smem_bytes();
 // debug: k_octree phase ticks per level of frame 0 (ORBPL_OCT_PROFILE)
 int read_octree_profile(long long* out128);
+int read_od_profile(long long* out8);
 
 // Padded pyramid + borders + blurred levels of `batch` frames (k_pyramid);
 // bands = the nbands-band partition (pyr_band_base(nbands) in the table).

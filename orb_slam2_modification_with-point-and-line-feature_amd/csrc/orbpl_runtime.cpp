@@ -260,6 +260,11 @@ int orbx_debug_octree_profile(orbx_ctx* c, long long* out128) {
   if (read_octree_profile(out128)) return arg_fail("octree profile unavailable");
   for (int l = 0; l < 16; l++)
     for (int k : {0, 1, 2, 3}) out128[8 * l + k] *= 10;
+  // level slots 8..15 are unused by 8-level pyramids: the orient/desc phases
+  // of frame 0's first keypoint go to out128[120..125] (ns)
+  long long od[6];
+  if (read_od_profile(od) == 0)
+    for (int k = 0; k < 6; k++) out128[120 + k] = od[k] * 10;
   return ORBPL_OK;
 }
 

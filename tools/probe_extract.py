@@ -56,3 +56,5 @@ if __import__("os").environ.get("ORBPL_OCT_PROFILE"):
     print("k_octree frame 0 per level: setup_us pass_us retain_us passes cands size")
     for l in range(8):
         print(f"  L{l}: {o[l,0]/1000:7.1f} {o[l,1]/1000:7.1f} {o[l,3]/1000:7.1f} {o[l,4]:4d} {o[l,5]:6d} {o[l,6]:5d}")
+    print("k_orient_desc first keypoint phases ns [setup, kp load, IC, trig, BRIEF, store]:",
+          out[120:126].tolist())
