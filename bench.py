@@ -287,7 +287,10 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, loca
     cam = pkg.make_camera(getattr(synth, cam_name))
     tr = pkg.Tracker(pkg.OrbParams(*wl["orb"]), cam, S, device=local_rank, lines=lines,
                      stereo=stereo)
-    tr.set_pipelined(bool(args.pipelined))
+    # pipelining overlaps extraction of step t+1 with tracking of step t; the
+    # lines workload is bound by the LSD stream, which the overlap only slows
+    pipelined = args.pipelined if args.pipelined >= 0 else (0 if lines else 1)
+    tr.set_pipelined(bool(pipelined))
     tr.reset(np.stack([np.linalg.inv(L.Twc(s, 0)).astype(np.float32) for s in range(S)]).reshape(S, 16))
     fb = fw * fh
     db = fb * depth.itemsize   # right image (u8) for stereo, depth (f32) otherwise
@@ -348,7 +351,7 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, loca
              "orient_desc": "k_orient_desc", "match": "k_match_last", "pose": "k_pose"}
     idx = {k: tr.STAGES.index(k) for k in names}
     iso = None
-    if args.pipelined and args.isolated_steps > 0:
+    if pipelined and args.isolated_steps > 0:
         # untimed: more steps with the two HIP streams serialised, so each
         # kernel's in-stream hipEvent time is its own. In the pipelined timed
         # region a kernel's event time also counts the time it waits for CUs
@@ -423,8 +426,9 @@ def main():
     ap.add_argument("--isolated-steps", type=int, default=5,
                     help="untimed non-pipelined steps after the timed region: per-kernel "
                          "times without the other stream's interference (roofline.isolated)")
-    ap.add_argument("--pipelined", type=int, default=1,
-                    help="1 = overlap extraction of step t+1 with tracking of step t")
+    ap.add_argument("--pipelined", type=int, default=-1,
+                    help="1 = overlap extraction of step t+1 with tracking of step t; 0 = no; "
+                         "-1 = per workload (on, except for the LSD-bound lines workload)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
