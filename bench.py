@@ -411,7 +411,9 @@ def main():
     ap.add_argument("--secondary-steps", type=int, default=3,
                     help="steps of the configs[2] lines workload reported under 'secondary' "
                          "(points runs only; 0 = skip)")
-    ap.add_argument("--lines-streams", type=int, default=1536)
+    ap.add_argument("--lines-streams", type=int, default=3072,
+                    help="streams of the lines workload: the LSD seed loop is one wave per "
+                         "frame, latency-bound, so it needs many frames in flight")
     ap.add_argument("--stereo-steps", type=int, default=3,
                     help="steps of the configs[3] stereo workload reported under 'stereo' "
                          "(points runs only; 0 = skip)")

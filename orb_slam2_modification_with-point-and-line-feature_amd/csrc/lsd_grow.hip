@@ -35,7 +35,8 @@ struct Frame {
   int sw, sh;
   const float* deg;
   const int* q;
-  uint32_t* used;     // LDS bits
+  uint32_t* used;     // LDS bits (k_lsd_grow)
+  uint32_t* ustamp;   // k_lsd_spec: USED lives in the claim stamps (0 = USED)
   uint32_t* reg_l;    // LDS region points (x | y << 16)
   int* regq_l;        // LDS q (gx^2 + gy^2) of each region point
   float* regd_l;      // LDS degrees of each region point
@@ -50,15 +51,26 @@ struct Frame {
   long long pf_cyc, pf_cnt, seed_cyc;
 };
 
+// USED state. k_lsd_grow keeps a bitmap in LDS. k_lsd_spec keeps it in the
+// per-pixel claim stamp (global, read at L2 like the claims): 0 = USED
+// (below every claim tag), anything else = not USED. Freeing LDS of the
+// 24 KB bitmap lets twice as many frames share a CU.
 __device__ __forceinline__ bool used_get(const Frame& F, int x, int y) {
   const int i = y * F.sw + x;
+  if (F.ustamp)
+    return __hip_atomic_load(F.ustamp + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
   return (F.used[i >> 5] >> (i & 31)) & 1u;
 }
 __device__ __forceinline__ void used_set(Frame& F, int x, int y, bool v) {
   const int i = y * F.sw + x;
   // the lanes run the same serial program; one of them updates the word
   // (single writer: a plain read-modify-write)
-  if (F.lane == 0) {
+  if (F.ustamp) {
+    if (F.lane == 0)
+      __hip_atomic_store(F.ustamp + i, v ? 0u : 0xFFFFFFFFu, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  } else if (F.lane == 0) {
     const uint32_t w = F.used[i >> 5], b = 1u << (i & 31);
     F.used[i >> 5] = v ? (w | b) : (w & ~b);
   }
@@ -663,7 +675,7 @@ __device__ __forceinline__ int lane_grow(const Frame& F, const float4* __restric
       st[k] = ld_stamp(stamp + idx);
       pv[k] = pix[idx];
       const bool in = xx >= 0 && xx < sw && yy >= 0 && yy < sh;
-      cand |= (in && !((F.used[idx >> 5] >> (idx & 31)) & 1u)) ? (1u << k) : 0u;
+      cand |= (in && st[k] != 0u) ? (1u << k) : 0u;   // stamp 0 = USED
     }
     uint4 first_add = cur;
 #pragma unroll
@@ -1038,6 +1050,7 @@ __global__ void __launch_bounds__(64) k_lsd_grow(LsdGeom g, LsdScratch sc) {
   F.deg = sc.deg + (long long)f * sw * sh;
   F.q = sc.q + (long long)f * sw * sh;
   F.used = grow_smem;
+  F.ustamp = nullptr;
   F.reg_l = grow_smem + used_words;
   F.regq_l = reinterpret_cast<int*>(F.reg_l + kRegLds);
   F.regd_l = reinterpret_cast<float*>(F.regq_l + kRegLds);
@@ -1125,7 +1138,7 @@ __global__ void __launch_bounds__(64) k_lsd_spec(LsdGeom g, LsdScratch sc) {
   F.sh = sh;
   F.deg = sc.deg + (long long)f * sw * sh;
   F.q = sc.q + (long long)f * sw * sh;
-  F.used = grow_smem;
+  F.used = nullptr;
   // the cooperative fallback's region list head and prefetch ring live in
   // the (then idle) lane buffers, so LDS holds only the USED bits
   uint32_t* coop = reinterpret_cast<uint32_t*>(sc.lbuf + (long long)f * kSpecLanes * kLaneCap);
@@ -1134,7 +1147,7 @@ __global__ void __launch_bounds__(64) k_lsd_spec(LsdGeom g, LsdScratch sc) {
   F.regd_l = reinterpret_cast<float*>(F.regq_l + kRegLds);
   F.ring = F.regd_l + kRegLds;
   F.reg_g = sc.reg + (long long)f * 3 * sw * sh;
-  F.rows = reinterpret_cast<int4*>(grow_smem + ((used_words + 3) & ~3));
+  F.rows = reinterpret_cast<int4*>(grow_smem);
   F.rect0 = reinterpret_cast<Rect*>(F.rows);
   F.rect1 = F.rect0 + 1;
   F.row_cap = 0;
@@ -1142,9 +1155,9 @@ __global__ void __launch_bounds__(64) k_lsd_spec(LsdGeom g, LsdScratch sc) {
   F.lane = lane;
   F.pf_cyc = 0;
   F.pf_cnt = 0;
-  for (int i = lane; i < used_words; i += 64) F.used[i] = 0;
-  __builtin_amdgcn_wave_barrier();
-  uint32_t* stamp = sc.stamp + (long long)f * sw * sh;
+  uint32_t* stamp = sc.stamp + (long long)f * sw * sh;   // 0xFFFFFFFF at launch
+  F.ustamp = stamp;
+  (void)used_words;
   uint4* buf = sc.lbuf + ((long long)f * kSpecLanes + lane) * kLaneCap;
   const float4* pix = sc.pix + (long long)f * sw * sh;
   const uint32_t* A = sc.A + (long long)f * g.n;
@@ -1259,7 +1272,7 @@ __global__ void __launch_bounds__(64) k_lsd_spec(LsdGeom g, LsdScratch sc) {
 #pragma unroll
           for (int u = 0; u < 8; u++) {
             const int id = (int)(ev[u] >> 16) * sw + (int)(ev[u] & 0xFFFF);
-            atomicOr(F.used + (id >> 5), 1u << (id & 31));
+            __hip_atomic_store(stamp + id, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
         }
       }
@@ -1398,8 +1411,7 @@ size_t lsd_grow_smem(const LsdGeom& g) {
 
 void launch_lsd_grow(const LsdGeom& g, const LsdScratch& sc, int batch, hipStream_t s,
                      bool serial) {
-  const int used_words = (g.sw * g.sh + 31) / 32;
-  const size_t smem = serial ? lsd_grow_smem(g) : 4 * (size_t)((used_words + 3) & ~3) + 2 * sizeof(Rect);
+  const size_t smem = serial ? lsd_grow_smem(g) : 2 * sizeof(Rect);
   const void* k = serial ? (const void*)k_lsd_grow : (const void*)k_lsd_spec;
   if (smem > 65536)
     (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
