@@ -180,7 +180,7 @@ struct SortPtrs {
 
 __device__ __forceinline__ int skey(uint32_t e) { return (int)(e >> 22); }
 
-constexpr int kSortThreads = 1024;
+constexpr int kSortThreads = 512;
 
 // Exclusive scan of a[0..len) (global) in place by the whole block; returns
 // the total in every thread.
