@@ -70,51 +70,7 @@ __device__ __forceinline__ fushort2 as_u2(uint32_t v) { return __builtin_bit_cas
 __device__ __forceinline__ fshort2 pmin(fshort2 a, fshort2 b) { return __builtin_elementwise_min(a, b); }
 __device__ __forceinline__ fshort2 pmax(fshort2 a, fshort2 b) { return __builtin_elementwise_max(a, b); }
 __device__ __forceinline__ fushort2 pmaxu(fushort2 a, fushort2 b) { return __builtin_elementwise_max(a, b); }
-
-// m = max(A, -B) for the two centres held in P at (r, q) and (r, q + 1).
-__device__ __forceinline__ fshort2 fast_m2(const uint32_t* P, int ps, int r, int q) {
-  const uint32_t* c = P + r * ps + q;
-  const fshort2 v = as_s2(c[0]);
-  fshort2 d[16];
-  d[0] = v - as_s2(c[3 * ps]);
-  d[1] = v - as_s2(c[3 * ps + 1]);
-  d[2] = v - as_s2(c[2 * ps + 2]);
-  d[3] = v - as_s2(c[ps + 3]);
-  d[4] = v - as_s2(c[3]);
-  d[5] = v - as_s2(c[-ps + 3]);
-  d[6] = v - as_s2(c[-2 * ps + 2]);
-  d[7] = v - as_s2(c[-3 * ps + 1]);
-  d[8] = v - as_s2(c[-3 * ps]);
-  d[9] = v - as_s2(c[-3 * ps - 1]);
-  d[10] = v - as_s2(c[-2 * ps - 2]);
-  d[11] = v - as_s2(c[-ps - 3]);
-  d[12] = v - as_s2(c[-3]);
-  d[13] = v - as_s2(c[ps - 3]);
-  d[14] = v - as_s2(c[2 * ps - 2]);
-  d[15] = v - as_s2(c[3 * ps - 1]);
-  fshort2 mn2[16], mx2[16];
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    mn2[k] = pmin(d[k], d[(k + 1) & 15]);
-    mx2[k] = pmax(d[k], d[(k + 1) & 15]);
-  }
-  fshort2 mn4[16], mx4[16];
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    mn4[k] = pmin(mn2[k], mn2[(k + 2) & 15]);
-    mx4[k] = pmax(mx2[k], mx2[(k + 2) & 15]);
-  }
-  fshort2 A = {-1024, -1024}, B = {1024, 1024};
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    const fshort2 mn8 = pmin(mn4[k], mn4[(k + 4) & 15]);
-    const fshort2 mx8 = pmax(mx4[k], mx4[(k + 4) & 15]);
-    A = pmax(A, pmin(mn8, d[(k + 8) & 15]));
-    B = pmin(B, pmax(mx8, d[(k + 8) & 15]));
-  }
-  const fshort2 zero = {0, 0}, top = {255, 255};
-  return pmin(pmax(pmax(A, zero - B), zero), top);
-}
+__device__ __forceinline__ fushort2 pminu(fushort2 a, fushort2 b) { return __builtin_elementwise_min(a, b); }
 
 // m = max(A, -B) for the centre pair (x, x+1) from a register window: R[k] =
 // bytes x-3 .. x+4 of row (centre row + k - 3) as two dwords (.x = bytes
@@ -125,63 +81,78 @@ __device__ __forceinline__ uint32_t ring_pair(const uint2* R, int dy, int dx) {
   return __builtin_amdgcn_perm(R[3 + dy].y, R[3 + dy].x, j | (0x0cu << 8) | ((j + 1) << 16) | (0x0cu << 24));
 }
 
+// Arc extrema of one side for the 8 windows of 8 ring pixels that start at
+// an odd index: W[j] = op(p[2j+1 .. 2j+8]) (indices mod 16). With the halves
+// p[0..7], p[8..15], the window from odd j < 8 is suffix(first half, j) +
+// prefix(second half, j - 1) and the one from j + 8 the mirror; only odd
+// suffixes and even prefixes are needed, and they share the pair ops
+// (1,2), (3,4), (5,6) of each half: 9 ops per half + 8 combines.
+template <bool kMax>
+__device__ __forceinline__ void fast_windows(const fushort2* p, fushort2* W) {
+  auto op = [](fushort2 a, fushort2 b) { return kMax ? pmaxu(a, b) : pminu(a, b); };
+  fushort2 s[2][4], pr[2][4];   // s[h][i] = suffix from 2i+1, pr[h][i] = prefix to 2i
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const fushort2* d = p + 8 * h;
+    const fushort2 q12 = op(d[1], d[2]), q34 = op(d[3], d[4]), q56 = op(d[5], d[6]);
+    s[h][3] = d[7];
+    s[h][2] = op(q56, d[7]);
+    s[h][1] = op(q34, s[h][2]);
+    s[h][0] = op(q12, s[h][1]);
+    pr[h][0] = d[0];
+    pr[h][1] = op(d[0], q12);
+    pr[h][2] = op(pr[h][1], q34);
+    pr[h][3] = op(pr[h][2], q56);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    W[i] = op(s[0][i], pr[1][i]);       // window from 2i + 1
+    W[i + 4] = op(s[1][i], pr[0][i]);   // window from 2i + 9
+  }
+}
+
+// FAST score m = max(A, -B) of the 16-pixel ring (cv::FAST's cornerScore:
+// A = max over the 16 circular 9-arcs of min(v - p), B = min over the arcs of
+// max(v - p)) in pixel space: A = v - min_arcs max(p), B = v - max_arcs
+// min(p), so no per-pixel differences. Arcs k and k + 1 (k even) share the
+// 8-window from k + 1:  min(max arc k, max arc k+1) = max(W[k+1], min(p[k],
+// p[k+9])). 98 packed u16 ops for two centres (was 134 with differences).
 __device__ __forceinline__ fshort2 fast_m2_regs(const uint2* R) {
-  const fshort2 v = as_s2(ring_pair(R, 0, 0));
-  fshort2 d[16];
-  d[0] = v - as_s2(ring_pair(R, 3, 0));
-  d[1] = v - as_s2(ring_pair(R, 3, 1));
-  d[2] = v - as_s2(ring_pair(R, 2, 2));
-  d[3] = v - as_s2(ring_pair(R, 1, 3));
-  d[4] = v - as_s2(ring_pair(R, 0, 3));
-  d[5] = v - as_s2(ring_pair(R, -1, 3));
-  d[6] = v - as_s2(ring_pair(R, -2, 2));
-  d[7] = v - as_s2(ring_pair(R, -3, 1));
-  d[8] = v - as_s2(ring_pair(R, -3, 0));
-  d[9] = v - as_s2(ring_pair(R, -3, -1));
-  d[10] = v - as_s2(ring_pair(R, -2, -2));
-  d[11] = v - as_s2(ring_pair(R, -1, -3));
-  d[12] = v - as_s2(ring_pair(R, 0, -3));
-  d[13] = v - as_s2(ring_pair(R, 1, -3));
-  d[14] = v - as_s2(ring_pair(R, 2, -2));
-  d[15] = v - as_s2(ring_pair(R, 3, -1));
-  // A = max_k min(d[k..k+8]), B = min_k max(d[k..k+8]) over the 16 circular
-  // 9-arcs, van Herk / Gil-Werman style: with the halves d[0..7], d[8..15],
-  // the arc from k < 8 is suffix(first half, k) + prefix(second half, k) and
-  // the arc from k + 8 is suffix(second half, k) + prefix(first half, k):
-  // 28 prefix/suffix + 16 combine + 15 reduce = 59 packed ops per side (80
-  // with the doubling tree). min/max are exact in any order.
-  fshort2 sn0[8], pn0[8], sn1[8], pn1[8], sx0[8], px0[8], sx1[8], px1[8];
-  sn0[7] = sx0[7] = d[7];
-  sn1[7] = sx1[7] = d[15];
-  pn0[0] = px0[0] = d[0];
-  pn1[0] = px1[0] = d[8];
+  const fushort2 v = as_u2(ring_pair(R, 0, 0));
+  fushort2 p[16];
+  p[0] = as_u2(ring_pair(R, 3, 0));
+  p[1] = as_u2(ring_pair(R, 3, 1));
+  p[2] = as_u2(ring_pair(R, 2, 2));
+  p[3] = as_u2(ring_pair(R, 1, 3));
+  p[4] = as_u2(ring_pair(R, 0, 3));
+  p[5] = as_u2(ring_pair(R, -1, 3));
+  p[6] = as_u2(ring_pair(R, -2, 2));
+  p[7] = as_u2(ring_pair(R, -3, 1));
+  p[8] = as_u2(ring_pair(R, -3, 0));
+  p[9] = as_u2(ring_pair(R, -3, -1));
+  p[10] = as_u2(ring_pair(R, -2, -2));
+  p[11] = as_u2(ring_pair(R, -1, -3));
+  p[12] = as_u2(ring_pair(R, 0, -3));
+  p[13] = as_u2(ring_pair(R, 1, -3));
+  p[14] = as_u2(ring_pair(R, 2, -2));
+  p[15] = as_u2(ring_pair(R, 3, -1));
+  fushort2 Wx[8], Wn[8];
+  fast_windows<true>(p, Wx);
+  fast_windows<false>(p, Wn);
+  // W[i] = window from 2i + 1, shared by arcs 2i and 2i + 1
+  fushort2 Ap = pmaxu(Wx[0], pminu(p[0], p[9]));
+  fushort2 Bp = pminu(Wn[0], pmaxu(p[0], p[9]));
 #pragma unroll
-  for (int k = 6; k >= 0; k--) {
-    sn0[k] = pmin(sn0[k + 1], d[k]);
-    sx0[k] = pmax(sx0[k + 1], d[k]);
-    sn1[k] = pmin(sn1[k + 1], d[k + 8]);
-    sx1[k] = pmax(sx1[k + 1], d[k + 8]);
+  for (int i = 1; i < 8; i++) {
+    const int k = 2 * i;
+    Ap = pminu(Ap, pmaxu(Wx[i], pminu(p[k], p[(k + 9) & 15])));
+    Bp = pmaxu(Bp, pminu(Wn[i], pmaxu(p[k], p[(k + 9) & 15])));
   }
-#pragma unroll
-  for (int k = 1; k < 8; k++) {
-    pn0[k] = pmin(pn0[k - 1], d[k]);
-    px0[k] = pmax(px0[k - 1], d[k]);
-    pn1[k] = pmin(pn1[k - 1], d[k + 8]);
-    px1[k] = pmax(px1[k - 1], d[k + 8]);
-  }
-  fshort2 A = pmin(sn0[0], pn1[0]), B = pmax(sx0[0], px1[0]);
-#pragma unroll
-  for (int k = 1; k < 8; k++) {
-    A = pmax(A, pmin(sn0[k], pn1[k]));
-    B = pmin(B, pmax(sx0[k], px1[k]));
-  }
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    A = pmax(A, pmin(sn1[k], pn0[k]));
-    B = pmin(B, pmax(sx1[k], px0[k]));
-  }
-  const fshort2 zero = {0, 0}, top = {255, 255};
-  return pmin(pmax(pmax(A, zero - B), zero), top);
+  const fshort2 zero = {0, 0};
+  const fshort2 sv = as_s2(__builtin_bit_cast(uint32_t, v));
+  const fshort2 A = sv - as_s2(__builtin_bit_cast(uint32_t, Ap));
+  const fshort2 nB = as_s2(__builtin_bit_cast(uint32_t, Bp)) - sv;
+  return pmax(pmax(A, nB), zero);
 }
 
 // 8 bytes x-3 .. x+4 of a row from the 3 aligned dwords at q (x-3 = 4 q + o)
