@@ -979,6 +979,18 @@ __global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
 // [4] BRIEF tests, [5] stores
 __device__ long long g_od_prof[8];
 
+// BRIEF patch staged in LDS: rotated pattern points lie within radius 18.39
+// of the keypoint (|bit_pattern_31_| <= 13), so every test reads rows and
+// columns ky-18 .. ky+18, kx-18 .. kx+18 of the blurred level. The patch is
+// 37 rows of 10 aligned dwords (bytes o .. o+36, o = (kx-18) & 3): 6 wide
+// loads per lane that issue with the IC_Angle loads, before the angle is
+// known, instead of 8 scattered byte loads (one cache line per lane) after it.
+constexpr int kBriefR = 18;
+constexpr int kBriefRows = 2 * kBriefR + 1;
+constexpr int kBriefRowDw = 10;
+constexpr int kBriefDw = kBriefRows * kBriefRowDw;   // 370
+constexpr int kBriefLoads = (kBriefDw + 63) / 64;    // 6
+
 __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__ pyr,
                                                      const uint8_t* __restrict__ blur,
                                                      const OrbGeom* __restrict__ g,
@@ -987,6 +999,7 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
                                                      orbpl_keypoint_dev* __restrict__ out_kps,
                                                      uint8_t* __restrict__ out_desc,
                                                      int kp_pitch, int* __restrict__ out_n) {
+  __shared__ uint32_t s_patch[4][kBriefDw];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int bx, f;
   xcd_block(&bx, &f);
@@ -1022,6 +1035,19 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
   const int kx = cand_x(c) + kMinBorder, ky = cand_y(c) + kMinBorder;
   if (stamp) (void)__builtin_amdgcn_readfirstlane(kx);
   lap(1);
+  // --- BRIEF patch loads (consumed after the angle) ---
+  const int bx0 = kx - kBriefR;
+  const uint32_t* prow = reinterpret_cast<const uint32_t*>(
+      blur + (long long)f * g->blur_bytes + L.boff + (long long)(ky - kBriefR) * L.bpitch +
+      (bx0 & ~3));
+  const int pdw = L.bpitch >> 2;
+  uint32_t pv[kBriefLoads];
+#pragma unroll
+  for (int j = 0; j < kBriefLoads; j++) {
+    const int i = lane + 64 * j;
+    const int r = i / kBriefRowDw, q = i - r * kBriefRowDw;
+    pv[j] = i < kBriefDw ? prow[r * pdw + q] : 0u;
+  }
   // --- IC_Angle: 62 lanes, lane = column u + 15 and half of the disc rows
   // (v in [-15, 0) or [0, 15]) ---
   const uint8_t* img = pyr + (long long)f * g->pyr_bytes + content_off(L, kx, ky);
@@ -1061,8 +1087,17 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
   cr_cos_sin(angle * factorPI, &a, &b);
   if (stamp) (void)__builtin_amdgcn_readfirstlane(__float_as_int(a + b));
   lap(3);
-  const uint8_t* bimg = blur + (long long)f * g->blur_bytes + L.boff + (long long)ky * L.bpitch + kx;
-  const int step = L.bpitch;
+  uint32_t* patch = s_patch[wave];
+#pragma unroll
+  for (int j = 0; j < kBriefLoads; j++) {
+    const int i = lane + 64 * j;
+    if (i < kBriefDw) patch[i] = pv[j];
+  }
+  __builtin_amdgcn_wave_barrier();
+  // centre byte of the patch: row kBriefR, byte (bx0 & 3) + kBriefR
+  const uint8_t* bimg = reinterpret_cast<const uint8_t*>(patch) + kBriefR * 4 * kBriefRowDw +
+                        (bx0 & 3) + kBriefR;
+  const int step = 4 * kBriefRowDw;
   uint64_t words[4];
 #pragma unroll
   for (int r = 0; r < 4; r++) {
