@@ -985,6 +985,10 @@ __device__ long long g_od_prof[8];
 // 37 rows of 10 aligned dwords (bytes o .. o+36, o = (kx-18) & 3): 6 wide
 // loads per lane that issue with the IC_Angle loads, before the angle is
 // known, instead of 8 scattered byte loads (one cache line per lane) after it.
+constexpr int kIcR = 15;                             // HALF_PATCH_SIZE
+constexpr int kIcRowDw = 9;                          // bytes o .. o+30, o <= 3
+constexpr int kIcDw = (2 * kIcR + 1) * kIcRowDw;     // 279
+constexpr int kIcLoads = (kIcDw + 63) / 64;          // 5
 constexpr int kBriefR = 18;
 constexpr int kBriefRows = 2 * kBriefR + 1;
 constexpr int kBriefRowDw = 10;
@@ -1035,6 +1039,19 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
   const int kx = cand_x(c) + kMinBorder, ky = cand_y(c) + kMinBorder;
   if (stamp) (void)__builtin_amdgcn_readfirstlane(kx);
   lap(1);
+  // --- IC_Angle patch loads: rows ky-15 .. ky+15 as 9 aligned dwords each
+  // (bytes o .. o+30 from the aligned base, o = address & 3), 5 per lane ---
+  const uint8_t* irow0 = pyr + (long long)f * g->pyr_bytes + content_off(L, kx - kIcR, ky - kIcR);
+  const int io = (int)(reinterpret_cast<uintptr_t>(irow0) & 3);
+  const uint32_t* irow = reinterpret_cast<const uint32_t*>(irow0 - io);
+  const int ipdw = L.pitch >> 2;
+  uint32_t iv[kIcLoads];
+#pragma unroll
+  for (int j = 0; j < kIcLoads; j++) {
+    const int i = lane + 64 * j;
+    const int r = i / kIcRowDw, q = i - r * kIcRowDw;
+    iv[j] = i < kIcDw ? irow[r * ipdw + q] : 0u;
+  }
   // --- BRIEF patch loads (consumed after the angle) ---
   const int bx0 = kx - kBriefR;
   const uint32_t* prow = reinterpret_cast<const uint32_t*>(
@@ -1048,31 +1065,27 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
     const int r = i / kBriefRowDw, q = i - r * kBriefRowDw;
     pv[j] = i < kBriefDw ? prow[r * pdw + q] : 0u;
   }
-  // --- IC_Angle: 62 lanes, lane = column u + 15 and half of the disc rows
-  // (v in [-15, 0) or [0, 15]) ---
-  const uint8_t* img = pyr + (long long)f * g->pyr_bytes + content_off(L, kx, ky);
+  // --- IC_Angle moments: pixel (u, v) of the disc |u| <= umax[|v|]; each
+  // lane takes the 4 pixels of its dwords (integer sums: any order) ---
   int m01 = 0, m10 = 0;
-  if (lane < 62) {
-    const int half = lane >= 31 ? 1 : 0;
-    const int u = lane - 31 * half - 15;
-    const int au = u < 0 ? -u : u;
-    const int v0 = half ? 0 : -15;
-    // all 16 loads of the lane's column issue before any is used (the loop
-    // with a use per load waited one memory latency per row)
-    int val[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-      const int v = v0 + k;
-      const int av = v < 0 ? -v : v;
-      const bool in = (half || k < 15) && au <= g->umax[av];
-      val[k] = in ? (int)img[(long long)v * L.pitch + u] : 0;
-    }
+  for (int j = 0; j < kIcLoads; j++) {
+    const int i = lane + 64 * j;
+    const int r = i / kIcRowDw, q = i - r * kIcRowDw;
+    const int v = r - kIcR;
+    const int um = i < kIcDw ? g->umax[v < 0 ? -v : v] : -1;
+    const int u0 = 4 * q - io - kIcR;   // u of the dword's byte 0
+    int s0 = 0, s1 = 0;
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-      const int v = v0 + k;
-      m10 += u * val[k];
-      m01 += v * val[k];
+    for (int bq = 0; bq < 4; bq++) {
+      const int u = u0 + bq;
+      const int px = (int)((iv[j] >> (8 * bq)) & 0xFFu);
+      const int w = (u <= um && -u <= um) ? px : 0;
+      s0 += w;
+      s1 += u * w;
     }
+    m10 += s1;
+    m01 += v * s0;
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
