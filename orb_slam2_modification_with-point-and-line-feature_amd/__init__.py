@@ -18,7 +18,8 @@ from pathlib import Path
 import numpy as np
 
 PKG_DIR = Path(__file__).resolve().parent
-LIB_PATH = PKG_DIR / "liborbpl.so"
+# ORBPL_LIB: an alternative build of the same library (dev A/B runs)
+LIB_PATH = Path(os.environ.get("ORBPL_LIB") or (PKG_DIR / "liborbpl.so"))
 
 KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
                      ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])

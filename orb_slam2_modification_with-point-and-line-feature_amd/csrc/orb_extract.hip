@@ -215,6 +215,17 @@ __device__ __forceinline__ uint32_t byte_of(uint32_t w0, uint32_t w1, uint32_t w
 // split with the fewest sequential rows per thread, counting `warm` extra
 // rows per segment (the blur's 6 warm-up rows) and idle lanes of the last
 // round of tasks. Block-uniform.
+// rows of a column walk whose loads are in flight together (latency-bound:
+// the walks are few and long; registers allow 8 at 4 waves per SIMD)
+#ifndef ORBPL_PYR_DEPTH
+#define ORBPL_PYR_DEPTH 8
+#endif
+constexpr int kPyrDepth = ORBPL_PYR_DEPTH;        // blur walk
+#ifndef ORBPL_PYR_RS_DEPTH
+#define ORBPL_PYR_RS_DEPTH 4
+#endif
+constexpr int kPyrRsDepth = ORBPL_PYR_RS_DEPTH;   // resize walk (2 source rows per row)
+
 __device__ __forceinline__ void walk_split(int groups, int rows, int warm, int* nseg, int* rps) {
   int best = 1, best_cost = 0x7fffffff;
   for (int s = 1; s <= 64 && s <= rows; s++) {
@@ -239,7 +250,7 @@ __device__ __forceinline__ void pyr_resize_rows(const LevelGeom& L, const LevelG
   const int groups = (L.w + 3) >> 2;
   int nseg, rps;
   walk_split(groups, nb - na, 2, &nseg, &rps);
-  const uint8_t* src0 = fp + content_off(S, 0, 0);
+  const uint32_t* src0w = reinterpret_cast<const uint32_t*>(fp + content_off(S, 0, 0));
   for (int task = threadIdx.x; task < groups * nseg; task += kPyrThreads) {
     const int seg = task / groups, gq = task - seg * groups;
     const int ra = na + seg * rps, rb = min(ra + rps, nb);
@@ -259,27 +270,26 @@ __device__ __forceinline__ void pyr_resize_rows(const LevelGeom& L, const LevelG
         a1[k] = 0;
       }
     }
-    // 4 rows per iteration: all 24 source dwords are loaded before any is used
-    for (int y = ra; y < rb; y += 4) {
-      int bq[4];
-      uint32_t u[4][3], v[4][3];
+    // kPyrRsDepth rows per iteration: all source dwords are loaded before any is used
+    for (int y = ra; y < rb; y += kPyrRsDepth) {
+      int bq[kPyrRsDepth];
+      uint32_t u[kPyrRsDepth][3], v[kPyrRsDepth][3];
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
+      for (int j = 0; j < kPyrRsDepth; j++) {
         const int yy = min(y + j, rb - 1);
         const int sy0 = yofs[yy];
         bq[j] = beta[yy];
-        const uint32_t* q0 = reinterpret_cast<const uint32_t*>(
-            src0 + (long long)min(max(sy0, 0), S.h - 1) * S.pitch) + d0;
-        const uint32_t* q1 = reinterpret_cast<const uint32_t*>(
-            src0 + (long long)min(max(sy0 + 1, 0), S.h - 1) * S.pitch) + d0;
+        // uniform base + 32-bit per-lane dword offsets (saddr loads)
+        const int q0 = min(max(sy0, 0), S.h - 1) * (S.pitch >> 2) + d0;
+        const int q1 = min(max(sy0 + 1, 0), S.h - 1) * (S.pitch >> 2) + d0;
 #pragma unroll
         for (int e = 0; e < 3; e++) {
-          u[j][e] = q0[e];
-          v[j][e] = q1[e];
+          u[j][e] = src0w[q0 + e];
+          v[j][e] = src0w[q1 + e];
         }
       }
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
+      for (int j = 0; j < kPyrRsDepth; j++) {
         if (y + j >= rb) break;
         const int b0 = (int)(short)(bq[j] & 0xFFFF), b1 = (int)(short)(bq[j] >> 16);
         uint32_t packed = 0;
@@ -305,29 +315,64 @@ __device__ __forceinline__ void pyr_resize_rows(const LevelGeom& L, const LevelG
   }
 }
 
-// horizontal 7-tap sums of content columns x .. x+3 from the padded row's
-// dwords w0 | w1 | w2 = content columns x-4 .. x+7, packed as 4 x u16
-__device__ __forceinline__ uint2 blur_h4(uint32_t w0, uint32_t w1, uint32_t w2) {
-  const int k0 = 18, k1 = 34, k2 = 49, k3 = 54;
-  int b[10];
-  b[0] = (w0 >> 8) & 0xFF; b[1] = (w0 >> 16) & 0xFF; b[2] = w0 >> 24;
-  b[3] = w1 & 0xFF; b[4] = (w1 >> 8) & 0xFF; b[5] = (w1 >> 16) & 0xFF; b[6] = w1 >> 24;
-  b[7] = w2 & 0xFF; b[8] = (w2 >> 8) & 0xFF; b[9] = (w2 >> 16) & 0xFF;
-  const uint32_t h0 = k0 * (b[0] + b[6]) + k1 * (b[1] + b[5]) + k2 * (b[2] + b[4]) + k3 * b[3];
-  const uint32_t h1 = k0 * (b[1] + b[7]) + k1 * (b[2] + b[6]) + k2 * (b[3] + b[5]) + k3 * b[4];
-  const uint32_t h2 = k0 * (b[2] + b[8]) + k1 * (b[3] + b[7]) + k2 * (b[4] + b[6]) + k3 * b[5];
-  const uint32_t h3 = k0 * (b[3] + b[9]) + k1 * (b[4] + b[8]) + k2 * (b[5] + b[7]) + k3 * b[6];
-  return make_uint2(h0 | (h1 << 16), h2 | (h3 << 16));
+// GaussianBlur 7x7, sigma 2, 8U fixed point (cv::GaussianBlur bit-exact
+// path): taps 18 34 49 54 49 34 18 (/256) each way, horizontal sums exact
+// in u16 (<= 255 * 256), the vertical sum exact in u32, one rounding
+// (acc + 2^15) >> 16 (<= 255: no clamp needed).
+//
+// (b_j, b_j+1) as u16x2 from the 12-byte window w0 | w1 | w2, b_j = byte j+1
+template <int j>
+__device__ __forceinline__ fushort2 blur_pair(uint32_t w0, uint32_t w1, uint32_t w2) {
+  constexpr int i = j + 1;
+  if constexpr (i + 1 <= 7)
+    return as_u2(__builtin_amdgcn_perm(w1, w0, (uint32_t)(i | (0x0c << 8) | ((i + 1) << 16) | (0x0c << 24))));
+  else
+    return as_u2(__builtin_amdgcn_perm(w2, w1, (uint32_t)((i - 4) | (0x0c << 8) | ((i - 3) << 16) | (0x0c << 24))));
 }
 
-__device__ __forceinline__ uint32_t blur_v1(const uint2* h, int hi, int sh) {
-  const int k0 = 18, k1 = 34, k2 = 49, k3 = 54;
-  int s[7];
-#pragma unroll
-  for (int v = 0; v < 7; v++) s[v] = (int)(((hi ? h[v].y : h[v].x) >> sh) & 0xFFFF);
-  const int acc = k0 * (s[0] + s[6]) + k1 * (s[1] + s[5]) + k2 * (s[2] + s[4]) + k3 * s[3];
-  const int o = (acc + (1 << 15)) >> 16;
-  return (uint32_t)(o > 255 ? 255 : o);
+// horizontal 7-tap sums of content columns x .. x+3 from the padded row's
+// dwords w0 | w1 | w2 = content columns x-4 .. x+7, packed as 4 x u16
+// (packed u16 arithmetic: two columns per instruction)
+__device__ __forceinline__ uint2 blur_h4(uint32_t w0, uint32_t w1, uint32_t w2) {
+  const fushort2 P0 = blur_pair<0>(w0, w1, w2), P1 = blur_pair<1>(w0, w1, w2);
+  const fushort2 P2 = blur_pair<2>(w0, w1, w2), P3 = blur_pair<3>(w0, w1, w2);
+  const fushort2 P4 = blur_pair<4>(w0, w1, w2), P5 = blur_pair<5>(w0, w1, w2);
+  const fushort2 P6 = blur_pair<6>(w0, w1, w2), P7 = blur_pair<7>(w0, w1, w2);
+  const fushort2 P8 = blur_pair<8>(w0, w1, w2);
+  const fushort2 k0 = {18, 18}, k1 = {34, 34}, k2 = {49, 49}, k3 = {54, 54};
+  const fushort2 h01 = k0 * (P0 + P6) + k1 * (P1 + P5) + k2 * (P2 + P4) + k3 * P3;
+  const fushort2 h23 = k0 * (P2 + P8) + k1 * (P3 + P7) + k2 * (P4 + P6) + k3 * P5;
+  return make_uint2(__builtin_bit_cast(uint32_t, h01), __builtin_bit_cast(uint32_t, h23));
+}
+
+// vertical 7-tap of one packed word (2 columns) of the ring h[0..6]: rows v
+// and 6-v paired into u16x2 (v_perm) and summed with v_dot2_u32_u16
+__device__ __forceinline__ void blur_v2(uint32_t h0, uint32_t h1, uint32_t h2, uint32_t h3,
+                                        uint32_t h4, uint32_t h5, uint32_t h6, uint32_t* lo,
+                                        uint32_t* hi) {
+  const fushort2 k0 = {18, 18}, k1 = {34, 34}, k2 = {49, 49};
+  const fushort2 kc_lo = {54, 0}, kc_hi = {0, 54};
+  constexpr uint32_t kLo = 0x05040100u, kHi = 0x07060302u;   // (a.lo, b.lo), (a.hi, b.hi)
+  uint32_t a = __builtin_amdgcn_udot2(as_u2(__builtin_amdgcn_perm(h6, h0, kLo)), k0, 1u << 15, false);
+  a = __builtin_amdgcn_udot2(as_u2(__builtin_amdgcn_perm(h5, h1, kLo)), k1, a, false);
+  a = __builtin_amdgcn_udot2(as_u2(__builtin_amdgcn_perm(h4, h2, kLo)), k2, a, false);
+  a = __builtin_amdgcn_udot2(as_u2(h3), kc_lo, a, false);
+  uint32_t b = __builtin_amdgcn_udot2(as_u2(__builtin_amdgcn_perm(h6, h0, kHi)), k0, 1u << 15, false);
+  b = __builtin_amdgcn_udot2(as_u2(__builtin_amdgcn_perm(h5, h1, kHi)), k1, b, false);
+  b = __builtin_amdgcn_udot2(as_u2(__builtin_amdgcn_perm(h4, h2, kHi)), k2, b, false);
+  b = __builtin_amdgcn_udot2(as_u2(h3), kc_hi, b, false);
+  *lo = a;
+  *hi = b;
+}
+
+// the 4 blurred bytes of a ring h[0..6] (byte 2 of each 32-bit sum)
+__device__ __forceinline__ uint32_t blur_v4(const uint2* h) {
+  uint32_t a0, a1, a2, a3;
+  blur_v2(h[0].x, h[1].x, h[2].x, h[3].x, h[4].x, h[5].x, h[6].x, &a0, &a1);
+  blur_v2(h[0].y, h[1].y, h[2].y, h[3].y, h[4].y, h[5].y, h[6].y, &a2, &a3);
+  const uint32_t p01 = __builtin_amdgcn_perm(a1, a0, 0x0c0c0602u);   // a0.b2 | a1.b2 << 8
+  const uint32_t p23 = __builtin_amdgcn_perm(a3, a2, 0x06020c0cu);   // a2.b2 << 16 | a3.b2 << 24
+  return p01 | p23;
 }
 
 __device__ __forceinline__ void pyr_blur_rows(const LevelGeom& L, const uint8_t* fp, uint8_t* bp,
@@ -340,33 +385,34 @@ __device__ __forceinline__ void pyr_blur_rows(const LevelGeom& L, const uint8_t*
     const int ra = oa + seg * rps, rb = min(ra + rps, ob);
     if (ra >= rb) continue;
     // padded row py holds content column x-4 at byte kContent0 - 4 + x
-    const uint32_t* col = reinterpret_cast<const uint32_t*>(fp + L.pyr_off + kContent0 - 4 + 4 * gq);
+    // uniform base + 32-bit per-lane offsets (saddr loads: one VGPR per row)
+    const uint32_t* col = reinterpret_cast<const uint32_t*>(fp + L.pyr_off);
+    const int c0 = (kContent0 - 4) / 4 + gq;
     const int pw = L.pitch >> 2;
     uint2 h[7];
 #pragma unroll
     for (int v = 0; v < 6; v++) {
-      const uint32_t* q = col + (long long)(ra - 3 + v + kEdge) * pw;
-      h[v + 1] = blur_h4(q[0], q[1], q[2]);
+      const int q = (ra - 3 + v + kEdge) * pw + c0;
+      h[v + 1] = blur_h4(col[q], col[q + 1], col[q + 2]);
     }
     uint8_t* out = bp + L.boff + 4 * gq;
-    // 4 rows per iteration: the 12 source dwords are loaded before any is used
-    for (int y = ra; y < rb; y += 4) {
-      uint32_t w[4][3];
+    // kPyrDepth rows per iteration: the source dwords are loaded before any is used
+    for (int y = ra; y < rb; y += kPyrDepth) {
+      uint32_t w[kPyrDepth][3];
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const uint32_t* q = col + (long long)(min(y + j, rb - 1) + 3 + kEdge) * pw;
-        w[j][0] = q[0];
-        w[j][1] = q[1];
-        w[j][2] = q[2];
+      for (int j = 0; j < kPyrDepth; j++) {
+        const int q = (min(y + j, rb - 1) + 3 + kEdge) * pw + c0;
+        w[j][0] = col[q];
+        w[j][1] = col[q + 1];
+        w[j][2] = col[q + 2];
       }
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
+      for (int j = 0; j < kPyrDepth; j++) {
         if (y + j >= rb) break;
 #pragma unroll
         for (int v = 0; v < 6; v++) h[v] = h[v + 1];
         h[6] = blur_h4(w[j][0], w[j][1], w[j][2]);
-        const uint32_t o = blur_v1(h, 0, 0) | (blur_v1(h, 0, 16) << 8) |
-                           (blur_v1(h, 1, 0) << 16) | (blur_v1(h, 1, 16) << 24);
+        const uint32_t o = blur_v4(h);
         *reinterpret_cast<uint32_t*>(out + (long long)(y + j) * L.bpitch) = o;
       }
     }
