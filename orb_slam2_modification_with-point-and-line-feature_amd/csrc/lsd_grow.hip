@@ -1067,16 +1067,17 @@ __global__ void __launch_bounds__(64) k_lsd_grow(LsdGeom g, LsdScratch sc) {
   for (int i = lane; i < used_words; i += 64) F.used[i] = 0;
   __builtin_amdgcn_wave_barrier();
   const uint32_t* A = sc.A + (long long)f * g.n;
+  const int nlist = sc.sort_nge[f];   // later list entries are NOTDEF
   const int w1 = sw - 1;
   const double prec = g.prec, p = g.p;
   int nl = 0;
   long long pc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const long long tstart = clock64();
-  for (int base = 0; base < g.n; base += 64) {
+  for (int base = 0; base < nlist; base += 64) {
     const int i = base + lane;
     int px = 0, py = 0;
     bool def = false;
-    if (i < g.n) {
+    if (i < nlist) {
       const int idx = (int)(A[i] & 0x3FFFFFu);
       py = idx / w1;
       px = idx - py * w1;
@@ -1161,6 +1162,7 @@ __global__ void __launch_bounds__(64) k_lsd_spec(LsdGeom g, LsdScratch sc) {
   uint4* buf = sc.lbuf + ((long long)f * kSpecLanes + lane) * kLaneCap;
   const float4* pix = sc.pix + (long long)f * sw * sh;
   const uint32_t* A = sc.A + (long long)f * g.n;
+  const int nlist = sc.sort_nge[f];   // later list entries are NOTDEF
   double* cand_out = sc.cand + (long long)f * kLsdMaxCand * 12;
   const int w1 = sw - 1;
   const double prec = g.prec, p = g.p;
@@ -1170,14 +1172,14 @@ __global__ void __launch_bounds__(64) k_lsd_spec(LsdGeom g, LsdScratch sc) {
   long long n_spec = 0, n_rounds = 0, cyc_spec = 0, cyc_fit = 0, cyc_val = 0, max_steps = 0,
             n_coop = 0;
   const long long t_all = clock64();
-  while (pos < g.n) {
+  while (pos < nlist) {
     // ---- the next 64 defined, NOTUSED seeds in list order ----
-    int ncand = 0, scan = pos, next_pos = g.n;
-    while (ncand < kSpecLanes && scan < g.n) {
+    int ncand = 0, scan = pos, next_pos = nlist;
+    while (ncand < kSpecLanes && scan < nlist) {
       const int i = scan + lane;
       bool c = false;
       int px = 0, py = 0;
-      if (i < g.n) {
+      if (i < nlist) {
         const int idx = (int)(A[i] & 0x3FFFFFu);
         py = idx / w1;
         px = idx - py * w1;

@@ -66,6 +66,9 @@ struct LsdScratch {
   float4* pix;         // sw*sh per frame: degrees, q bits, cos, sin
   int4* sort_local;    // seg_cap per frame: introsort segments finished in LDS
   int* sort_nlocal;    // 1 per frame
+  int* sort_kt;        // 1 per frame: key bound, key < kt => NOTDEF pixel
+  int* sort_nge;       // 1 per frame: elements with key >= kt (the list's
+                       // exactly sorted prefix; every later pixel is NOTDEF)
 };
 
 // Outputs of LineExtractor::ExtractLineSegment per frame.

@@ -176,6 +176,7 @@ struct SortPtrs {
   int4* local;     // segments of <= local_max elements deferred to k_lsd_sort_local
   int* nlocal;
   int local_max;   // 0: partition everything here
+  int kt;          // segments whose key bound is < kt hold only NOTDEF pixels
 };
 
 __device__ __forceinline__ int skey(uint32_t e) { return (int)(e >> 22); }
@@ -275,7 +276,15 @@ __device__ void heap_sort_seg(uint32_t* A, int len) {
 // Sorts A[first, last) whose introsort depth budget is depth0 (the top
 // level: 2 * floor(log2(n))). NT threads.
 template <int NT>
-__device__ __forceinline__ void sort_core(const SortPtrs& P, int first0, int last0, int depth0) {
+//
+// Segments carry an upper bound of their keys in .w: the right part of a
+// partition (keys <= pivot) gets min(bound, pivot key). A segment whose bound
+// is below P.kt holds only NOTDEF pixels (ll_angle: key < int(rho *
+// bin_coef) implies norm < rho), which the seed loop never takes, so its
+// internal order is irrelevant and it is not sorted further; every other
+// segment is replayed exactly.
+__device__ __forceinline__ void sort_core(const SortPtrs& P, int first0, int last0, int depth0,
+                                          int ub0) {
   __shared__ int s_w[(NT / 64)];
   __shared__ int s_nseg, s_next, s_nheap, s_nleaf;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -294,8 +303,10 @@ __device__ __forceinline__ void sort_core(const SortPtrs& P, int first0, int las
     s_nleaf = 0;
     s_nseg = 0;
     const int n = last0 - first0;
-    if (n > 16) {
-      P.seg0[0] = make_int4(first0, last0, depth0, 0);
+    if (ub0 < P.kt) {
+      // nothing to order
+    } else if (n > 16) {
+      P.seg0[0] = make_int4(first0, last0, depth0, ub0);
       s_nseg = 1;
     } else if (n > 1) {
       P.leaves[0] = make_int2(first0, last0);
@@ -455,16 +466,19 @@ __device__ __forceinline__ void sort_core(const SortPtrs& P, int first0, int las
       const int4 sg = cur[s];
       const int cut = scut[s], d = sg.z - 1;
       const int bs[2] = {cut, sg.x}, es[2] = {sg.y, cut};
+      const int ubs[2] = {min(sg.w, piv[s]), sg.w};   // [cut, last): keys <= pivot
       for (int c = 0; c < 2; c++) {
-        const int b = bs[c], e = es[c], size = e - b;
-        if (size > 16) {
+        const int b = bs[c], e = es[c], size = e - b, ub = ubs[c];
+        if (ub < P.kt) {
+          // only NOTDEF pixels: order irrelevant
+        } else if (size > 16) {
           if (d > 0 && size <= P.local_max) {
             const int idx = atomicAdd(P.nlocal, 1);
-            if (idx < P.seg_cap) P.local[idx] = make_int4(b, e, d, 0);
+            if (idx < P.seg_cap) P.local[idx] = make_int4(b, e, d, ub);
             else atomicOr(P.err, 2);
           } else if (d > 0) {
             const int idx = atomicAdd(&s_next, 1);
-            if (idx < P.seg_cap) nxt[idx] = make_int4(b, e, d, 0);
+            if (idx < P.seg_cap) nxt[idx] = make_int4(b, e, d, ub);
             else atomicOr(P.err, 2);
           } else {
             const int idx = atomicAdd(&s_nheap, 1);
@@ -524,6 +538,7 @@ __device__ SortPtrs sort_ptrs(const LsdGeom& g, const LsdScratch& sc, int f) {
   P.local = sc.sort_local + (long long)f * g.seg_cap;
   P.nlocal = sc.sort_nlocal + f;
   P.local_max = kSortLocalMax;
+  P.kt = -(1 << 30);
   return P;
 }
 
@@ -564,12 +579,13 @@ __global__ void __launch_bounds__(kLocalThreads) k_lsd_sort_local(LsdGeom g, Lsd
   L.local = nullptr;
   L.nlocal = nullptr;
   L.local_max = 0;
+  L.kt = sc.sort_kt[f];
   for (int k = blockIdx.x; k < nloc; k += gridDim.x) {
     const int4 sg = loc[k];
     const int m = sg.y - sg.x;
     for (int i = t; i < m; i += kLocalThreads) sA[i] = A[sg.x + i];
     __syncthreads();
-    sort_core<kLocalThreads>(L, 0, m, sg.z);
+    sort_core<kLocalThreads>(L, 0, m, sg.z, sg.w);
     for (int i = t; i < m; i += kLocalThreads) A[sg.x + i] = sA[i];
     __syncthreads();
   }
@@ -577,21 +593,36 @@ __global__ void __launch_bounds__(kLocalThreads) k_lsd_sort_local(LsdGeom g, Lsd
 
 __global__ void __launch_bounds__(kSortThreads) k_lsd_sort(LsdGeom g, LsdScratch sc) {
   const int f = blockIdx.x;
-  const SortPtrs P = sort_ptrs(g, sc, f);
+  SortPtrs P = sort_ptrs(g, sc, f);
   // bins: int(norm * bin_coef), bin_coef = 1023 / max_grad (ll_angle)
   const unsigned mq = sc.maxq[f];
   const double max_grad = mq ? sqrt(mq / 4.0) : -1.0;
   const double bin_coef = max_grad > 0 ? 1023.0 / max_grad : 0.0;
+  // key < kt => norm < rho => NOTDEF (both from the same double norm; no
+  // defined pixel at all: everything is NOTDEF)
+  const int kt = mq ? (int)(g.rho * bin_coef) : 1 << 30;
+  P.kt = kt;
   const int sw = g.sw, w1 = g.sw - 1;
   const int* q = sc.q + (long long)f * sw * g.sh;
+  __shared__ int s_nge;
+  if (threadIdx.x == 0) s_nge = 0;
+  __syncthreads();
+  int nge = 0;
   for (int i = threadIdx.x; i < g.n; i += kSortThreads) {
     const int y = i / w1, x = i - y * w1;
     const int key = (int)(sqrt(q[y * sw + x] / 4.0) * bin_coef);
     P.A[i] = ((uint32_t)key << 22) | (uint32_t)i;
+    nge += key >= kt;
   }
+  for (int o = 32; o >= 1; o >>= 1) nge += __shfl_xor(nge, o, 64);
+  if ((threadIdx.x & 63) == 0 && nge) atomicAdd(&s_nge, nge);
   if (threadIdx.x == 0) *P.nlocal = 0;
   __syncthreads();
-  sort_core<kSortThreads>(P, 0, g.n, g.n > 16 ? 2 * (31 - __clz(g.n)) : 0);
+  if (threadIdx.x == 0) {
+    sc.sort_kt[f] = kt;
+    sc.sort_nge[f] = s_nge;
+  }
+  sort_core<kSortThreads>(P, 0, g.n, g.n > 16 ? 2 * (31 - __clz(g.n)) : 0, 1023);
 }
 
 // test hook: sort caller-provided keys (frame slot 0)
@@ -600,9 +631,13 @@ __global__ void __launch_bounds__(kSortThreads) k_lsd_sort_keys(LsdGeom g, LsdSc
   const SortPtrs P = sort_ptrs(g, sc, 0);
   for (int i = threadIdx.x; i < g.n; i += kSortThreads)
     P.A[i] = ((uint32_t)keys[i] << 22) | (uint32_t)i;
-  if (threadIdx.x == 0) *P.nlocal = 0;
+  if (threadIdx.x == 0) {
+    *P.nlocal = 0;
+    sc.sort_kt[0] = P.kt;   // no NOTDEF semantics: sort everything
+    sc.sort_nge[0] = g.n;
+  }
   __syncthreads();
-  sort_core<kSortThreads>(P, 0, g.n, g.n > 16 ? 2 * (31 - __clz(g.n)) : 0);
+  sort_core<kSortThreads>(P, 0, g.n, g.n > 16 ? 2 * (31 - __clz(g.n)) : 0, 1 << 30);
 }
 
 void launch_lsd_blur(const LsdGeom& g, const uint8_t* img, int stride, long long frame_pitch,

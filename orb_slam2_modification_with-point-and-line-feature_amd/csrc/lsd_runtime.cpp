@@ -241,6 +241,8 @@ int lsdx_create(int width, int height, int max_batch, int device, lsdx_ctx** out
   LA(s.pix, B * px * sizeof(float4));
   LA(s.sort_local, B * g.seg_cap * sizeof(int4));
   LA(s.sort_nlocal, B * 4);
+  LA(s.sort_kt, B * 4);
+  LA(s.sort_nge, B * 4);
   LA(c->d_tabs, (size_t)(2 * g.sw + 2 * g.sh) * 4);
   LA(c->blur5, B * width * height);
   LA(c->sdx, B * width * height * 2);
@@ -462,6 +464,8 @@ int orbpl_test_introsort(const int* keys, int n, int* perm) {
   e = e ? e : A((void**)&sc.err, 4);
   e = e ? e : A((void**)&sc.sort_local, (size_t)seg_cap * sizeof(int4));
   e = e ? e : A((void**)&sc.sort_nlocal, 4);
+  e = e ? e : A((void**)&sc.sort_kt, 4);
+  e = e ? e : A((void**)&sc.sort_nge, 4);
   int rc = ORBPL_OK, err = 0;
   std::vector<uint32_t> a(n);
   if (e == hipSuccess) e = hipMemcpy(d_keys, keys, (size_t)n * 4, hipMemcpyHostToDevice);

@@ -49,7 +49,14 @@ def test_lsd_stages_bit_exact(orbpl, oracle, frames):
         assert np.array_equal(deg < 0, notdef)
         a = deg.astype(np.float64) * (np.pi / 180)
         assert np.array_equal(a[~notdef], ang_o[~notdef])
-        assert np.array_equal(order, ord_o)
+        # pseudo-ordering: the list up to its last defined (non-NOTDEF) pixel
+        # is the reference's std::sort order exactly; the tail holds only
+        # NOTDEF pixels, which the seed loop never takes and the device sort
+        # leaves in partition order (same elements)
+        defined = ~notdef[ord_o >> 16, ord_o & 0xFFFF]   # list entries: x | y << 16
+        last = int(np.nonzero(defined)[0].max()) + 1 if defined.any() else 0
+        assert np.array_equal(order[:last], ord_o[:last])
+        assert np.array_equal(np.sort(order), np.sort(ord_o))
 
 
 @pytest.mark.parametrize("serial", [False, True], ids=["speculative", "wave_serial"])
