@@ -513,6 +513,8 @@ __device__ __forceinline__ void nms_pair(const uint32_t* M, int ps, int r, int q
   *mx = a;
 }
 
+__device__ __forceinline__ int wave_incl_scan(int v);
+
 __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ pyr,
                                                     const OrbGeom* __restrict__ g,
                                                     const CellGeom* __restrict__ cells,
@@ -534,6 +536,11 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
   }
   const int ps = fast_pstride(g->fast_win_w);
   uint32_t* M = fast_smem + wave * fast_wave_words(g->fast_win_w, g->fast_win_h);
+  // candidate bit masks of detection row r (bit p = column pair p) in the
+  // last 4 words of m-plane row r + 3, which no m or NMS access reaches
+  // (they end at column cols <= win_w < ps - 4): mask[r * ps + j],
+  // j = 0 lo / 1 hi pixel at min_th, 2 lo / 3 hi at ini_th
+  uint32_t* mask = M + 3 * ps + ps - 4;
   const LevelGeom& L = g->lv[cg.level];
   const int cols = cg.x1 - cg.x0, rows = cg.y1 - cg.y0;
   const int sh = cg.x0 & 3;
@@ -543,33 +550,54 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
     for (int k = lane; k < nq; k += 64) reinterpret_cast<uint4*>(M)[k] = make_uint4(0, 0, 0, 0);
   }
   __builtin_amdgcn_wave_barrier();
+  const int t_ini = max((ini_th < 0 ? 0 : (ini_th > 255 ? 255 : ini_th)) + 1, 2);
+  const int t_min = max((min_th < 0 ? 0 : (min_th > 255 ? 255 : min_th)) + 1, 2);
   // ---- m for the detection region rows [3, rows-3), cols [3, cols-3):
   // lane = (column pair p, row segment); each lane walks its rows with the
-  // 7 ring rows of its pair in registers, loaded straight from the level ----
+  // 7 ring rows of its pair in registers, loaded straight from the level.
+  // The raw-m NMS (a candidate is a local maximum of m with m >= T; the
+  // neighbours' raw m stand in for cv::FAST's thresholded scores, which only
+  // differ where m < T <= the centre's) runs in the same walk one row behind:
+  // the row above / below come from the lane's own registers, the left / right
+  // neighbour pixels from the adjacent lanes. The first and last row of each
+  // segment are finished from the m plane in LDS afterwards. ----
   const int dr = rows - 6, dc = cols - 6;
   const int np = (dc + 1) >> 1;
   const uint32_t inv_np = div_inv(np);
   const int npair = (dr > 0 && dc > 0) ? dr * np : 0;
   uint16_t* M16 = reinterpret_cast<uint16_t*>(M);
+  int nseg = 1, rps = dr;
+  bool any_ini = false;
   if (npair > 0) {
-    const int nseg = max(1, 64 / np);
-    const int rps = (dr + nseg - 1) / nseg;
+    nseg = max(1, 64 / np);
+    rps = (dr + nseg - 1) / nseg;
     const int seg = div_small(lane, inv_np), p = lane - seg * np;
-    if (seg < nseg) {
-      const int ra = seg * rps, rb = min(ra + rps, dr);   // detection rows
-      const int cx = cg.x0 + 3 + 2 * p;                    // content column of the left centre
-      const int abase = (cx - 3) & ~3;
-      const uint32_t o = (uint32_t)((cx - 3) - abase);
-      const int pdw = L.pitch >> 2;
-      // window row w = content row cg.y0 + w; detection row r = window row r + 3
-      const uint32_t* col = reinterpret_cast<const uint32_t*>(
-          pyr + (long long)f * g->pyr_bytes + content_off(L, abase, cg.y0));
-      uint2 R[7];
+    const bool in_seg = seg < nseg;
+    const int ra = in_seg ? seg * rps : 0, rb = in_seg ? min(ra + rps, dr) : 0;
+    const int cx = cg.x0 + 3 + 2 * p;                    // content column of the left centre
+    const int abase = (cx - 3) & ~3;
+    const uint32_t o = (uint32_t)((cx - 3) - abase);
+    const int pdw = L.pitch >> 2;
+    // window row w = content row cg.y0 + w; detection row r = window row r + 3
+    const uint32_t* col = reinterpret_cast<const uint32_t*>(
+        pyr + (long long)f * g->pyr_bytes + content_off(L, abase, cg.y0));
+    const int q = 3 + 2 * p + sh;
+    const bool has_hi = 2 * p + 1 < dc;
+    const bool has_left = p > 0, has_right = p + 1 < np;
+    const uint32_t pbit = 1u << p;
+    uint2 R[7];
+    if (in_seg) {
 #pragma unroll
       for (int k = 0; k < 6; k++) R[k + 1] = load_ring_row(col + (long long)(ra + k) * pdw, o);
-      const int q = 3 + 2 * p + sh;
-      const bool has_hi = 2 * p + 1 < dc;
-      for (int r = ra; r < rb; r++) {
+    }
+    // rows r-1, r-2 of the walk: packed m, 3-wide row max, centre-excluded max
+    uint32_t m1 = 0, rmax1 = 0, rmax2 = 0, cmax1 = 0;
+    const int nit = __builtin_amdgcn_readfirstlane(rps);   // the longest segment
+    for (int i = 0; i < nit; i++) {
+      const int r = ra + i;
+      const bool act = r < rb;
+      uint32_t m = 0;
+      if (act) {
 #pragma unroll
         for (int k = 0; k < 6; k++) R[k] = R[k + 1];
         R[6] = load_ring_row(col + (long long)(r + 6) * pdw, o);
@@ -577,57 +605,97 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
         const int wr = r + 3;
         const uint32_t lo = (uint32_t)(uint16_t)m2.x;
         const uint32_t hi = has_hi ? (uint32_t)(uint16_t)m2.y : 0u;
-        M[wr * ps + q] = lo | (hi << 16);
+        m = lo | (hi << 16);
+        M[wr * ps + q] = m;
         M16[2 * (wr * ps + q - 1) + 1] = (uint16_t)lo;   // M[wr][q-1].hi
         M16[2 * (wr * ps + q + 1)] = (uint16_t)hi;       // M[wr][q+1].lo
+      }
+      // all lanes: neighbour pixels of the same row from the adjacent lanes
+      const uint32_t lhi = (uint32_t)__shfl_up((int)(m >> 16), 1, 64);
+      const uint32_t rlo = (uint32_t)__shfl_down((int)(m & 0xFFFFu), 1, 64);
+      if (act) {
+        const uint32_t Pl = (has_left ? lhi : 0u) | (m << 16);        // (x-1, x)
+        const uint32_t Pr = (m >> 16) | ((has_right ? rlo : 0u) << 16);  // (x+1, x+2)
+        const fushort2 cm = pmaxu(as_u2(Pl), as_u2(Pr));
+        const uint32_t cmax = __builtin_bit_cast(uint32_t, cm);
+        const uint32_t rmax = __builtin_bit_cast(uint32_t, pmaxu(cm, as_u2(m)));
+        if (i >= 2) {
+          // NMS of row r-1 (interior: rows r-2 and r are this segment's)
+          const fushort2 mx = pmaxu(pmaxu(as_u2(rmax2), as_u2(rmax)), as_u2(cmax1));
+          const fushort2 mc = as_u2(m1);
+          const bool lmax_lo = mc.x > mx.x, lmax_hi = mc.y > mx.y;
+          const int row = r - 1;
+          uint32_t* mr = mask + row * ps;
+          if (lmax_lo && mc.x >= t_min) atomicOr(mr, pbit);
+          if (lmax_hi && mc.y >= t_min) atomicOr(mr + 1, pbit);
+          const bool ilo = lmax_lo && mc.x >= t_ini, ihi = lmax_hi && mc.y >= t_ini;
+          if (ilo) atomicOr(mr + 2, pbit);
+          if (ihi) atomicOr(mr + 3, pbit);
+          any_ini |= ilo || ihi;
+        }
+        rmax2 = rmax1;
+        rmax1 = rmax;
+        cmax1 = cmax;
+        m1 = m;
       }
     }
   }
   __builtin_amdgcn_wave_barrier();
-  int t = ini_th < 0 ? 0 : (ini_th > 255 ? 255 : ini_th);
-  {
-    const int T = max(t + 1, 2);
-    int found = 0;
-    for (int base = 0; base < npair && !found; base += 64) {
-      const int k = base + lane;
-      bool is = false;
-      if (k < npair) {
-        const int rr = div_small(k, inv_np), p = k - rr * np;
-        fushort2 m, mx;
-        nms_pair(M, ps, rr + 3, 3 + 2 * p + sh, &m, &mx);
-        is = (m.x >= T && m.x > mx.x) || (m.y >= T && m.y > mx.y);
-      }
-      found = __ballot(is) != 0ull;
+  // ---- segment edge rows (first and last of each segment) from the m plane ----
+  if (npair > 0) {
+    const int nedge = 2 * nseg * np;
+    for (int k = lane; k < nedge; k += 64) {
+      const int e = div_small(k, inv_np), p = k - e * np;
+      const int sg = e >> 1;
+      const int ra = sg * rps, rb = min(ra + rps, dr);
+      if (ra >= rb) continue;
+      const int row = (e & 1) ? rb - 1 : ra;
+      if ((e & 1) && rb - 1 == ra) continue;   // one-row segment: done once
+      fushort2 m, mx;
+      nms_pair(M, ps, row + 3, 3 + 2 * p + sh, &m, &mx);
+      const bool lmax_lo = m.x > mx.x, lmax_hi = m.y > mx.y;
+      const uint32_t pbit = 1u << p;
+      uint32_t* mr = mask + row * ps;
+      if (lmax_lo && m.x >= t_min) atomicOr(mr, pbit);
+      if (lmax_hi && m.y >= t_min) atomicOr(mr + 1, pbit);
+      const bool ilo = lmax_lo && m.x >= t_ini, ihi = lmax_hi && m.y >= t_ini;
+      if (ilo) atomicOr(mr + 2, pbit);
+      if (ihi) atomicOr(mr + 3, pbit);
+      any_ini |= ilo || ihi;
     }
-    if (!found) t = min_th < 0 ? 0 : (min_th > 255 ? 255 : min_th);
   }
-  const int T = max(t + 1, 2);
+  __builtin_amdgcn_wave_barrier();
+  // ---- emission in raster order: cv::FAST at ini_th, or at min_th when the
+  // cell has no corner at ini_th (ORBextractor.cc:807-817); lane = row ----
+  const bool use_ini = __ballot(any_ini) != 0ull;
+  const int j0 = use_ini ? 2 : 0;
   uint32_t* out = cell_cands + ((long long)f * g->ncells_total + cell) * slots;
   const int xoff = cg.x0 - kMinBorder, yoff = cg.y0 - kMinBorder;
-  int n = 0;
-  for (int base = 0; base < npair; base += 64) {
-    const int k = base + lane;
-    bool clo = false, chi = false;
-    int rr = 0, p = 0;
-    fushort2 m = {0, 0};
-    if (k < npair) {
-      rr = div_small(k, inv_np);
-      p = k - rr * np;
-      fushort2 mx;
-      nms_pair(M, ps, rr + 3, 3 + 2 * p + sh, &m, &mx);
-      clo = m.x >= T && m.x > mx.x;
-      chi = m.y >= T && m.y > mx.y;   // m.y == 0 when the pixel is outside
-    }
-    const unsigned long long blo = __ballot(clo), bhi = __ballot(chi);
-    const unsigned long long below = (1ull << lane) - 1ull;
-    int pos = n + __popcll(blo & below) + __popcll(bhi & below);
-    const int x = xoff + 3 + 2 * p, y = yoff + rr + 3;
-    if (clo) {
+  uint32_t blo = 0, bhi = 0;
+  if (lane < dr && npair > 0) {
+    blo = mask[lane * ps + j0];
+    bhi = mask[lane * ps + j0 + 1];
+  }
+  const int cnt = __popc(blo) + __popc(bhi);
+  const int incl = wave_incl_scan(cnt);
+  const int n = __shfl(incl, 63, 64);
+  int pos = incl - cnt;
+  const int y = yoff + lane + 3;
+  const uint32_t* Mrow = M + (lane + 3) * ps + 3 + sh;
+  uint32_t rem = blo | bhi;
+  while (rem) {
+    const int p = __builtin_ctz(rem);
+    rem &= rem - 1;
+    const fushort2 m = as_u2(Mrow[2 * p]);
+    const int x = xoff + 3 + 2 * p;
+    if ((blo >> p) & 1u) {
       if (pos < slots) out[pos] = pack_cand(x, y, m.x - 1);
       pos++;
     }
-    if (chi && pos < slots) out[pos] = pack_cand(x + 1, y, m.y - 1);
-    n += __popcll(blo) + __popcll(bhi);
+    if ((bhi >> p) & 1u) {
+      if (pos < slots) out[pos] = pack_cand(x + 1, y, m.y - 1);
+      pos++;
+    }
   }
   if (lane == 0) *cnt_out = n < slots ? n : slots;
 }
