@@ -57,9 +57,11 @@ __device__ __forceinline__ int reflect101_dev(int p, int len) {
 // (A neighbour n with m_n >= m >= t+1 is itself a corner, so comparing raw m
 // values is the same as the reference's comparison of neighbour scores, where
 // non-corners score 0.)
-__host__ __device__ constexpr int fast_pstride(int win_w) { return ((win_w + 3 + 4) + 3) & ~3; }
+// m plane of a FAST window: one u16 per window pixel, rows of fast_pstride
+// u16 (a multiple of 8: whole uint4s), then 4 candidate mask words per row
+__host__ __device__ constexpr int fast_pstride(int win_w) { return (win_w + 7) & ~7; }
 __host__ __device__ constexpr int fast_wave_words(int win_w, int win_h) {
-  return win_h * fast_pstride(win_w);
+  return win_h * (fast_pstride(win_w) / 2) + 4 * win_h;
 }
 
 typedef short fshort2 __attribute__((ext_vector_type(2)));
@@ -515,7 +517,11 @@ __device__ __forceinline__ void nms_pair(const uint32_t* M, int ps, int r, int q
 
 __device__ __forceinline__ int wave_incl_scan(int v);
 
-__global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ pyr,
+// minimum waves per SIMD for k_fast_cells (register budget); see DESIGN.md
+#ifndef ORBPL_FAST_MINW
+#define ORBPL_FAST_MINW 1
+#endif
+__global__ void __launch_bounds__(256, ORBPL_FAST_MINW) k_fast_cells(const uint8_t* __restrict__ pyr,
                                                     const OrbGeom* __restrict__ g,
                                                     const CellGeom* __restrict__ cells,
                                                     uint32_t* __restrict__ cell_cands,
@@ -534,20 +540,19 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
     if (lane == 0) *cnt_out = 0;
     return;
   }
-  const int ps = fast_pstride(g->fast_win_w);
+  const int pw = fast_pstride(g->fast_win_w);   // u16 per m-plane row
+  const int pw2 = pw >> 1;                      // dwords per row: dword d = pixels (2d, 2d+1)
   uint32_t* M = fast_smem + wave * fast_wave_words(g->fast_win_w, g->fast_win_h);
-  // candidate bit masks of detection row r (bit p = column pair p) in the
-  // last 4 words of m-plane row r + 3, which no m or NMS access reaches
-  // (they end at column cols <= win_w < ps - 4): mask[r * ps + j],
-  // j = 0 lo / 1 hi pixel at min_th, 2 lo / 3 hi at ini_th
-  uint32_t* mask = M + 3 * ps + ps - 4;
+  // candidate bit masks of detection row r (bit p = column pair p):
+  // mask[4 r + j], j = 0 lo / 1 hi pixel at min_th, 2 lo / 3 hi at ini_th
+  uint32_t* mask = M + g->fast_win_h * pw2;
   const LevelGeom& L = g->lv[cg.level];
   const int cols = cg.x1 - cg.x0, rows = cg.y1 - cg.y0;
-  const int sh = cg.x0 & 3;
-  // M column q <-> window column q - sh; zero the window (outside = 0)
+  // zero the window's m (outside the detection region = 0) and the masks
   {
-    const int nq = rows * ps / 4;
+    const int nq = rows * pw2 / 4;
     for (int k = lane; k < nq; k += 64) reinterpret_cast<uint4*>(M)[k] = make_uint4(0, 0, 0, 0);
+    for (int k = lane; k < 4 * g->fast_win_h; k += 64) mask[k] = 0;
   }
   __builtin_amdgcn_wave_barrier();
   const int t_ini = max((ini_th < 0 ? 0 : (ini_th > 255 ? 255 : ini_th)) + 1, 2);
@@ -581,7 +586,6 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
     // window row w = content row cg.y0 + w; detection row r = window row r + 3
     const uint32_t* col = reinterpret_cast<const uint32_t*>(
         pyr + (long long)f * g->pyr_bytes + content_off(L, abase, cg.y0));
-    const int q = 3 + 2 * p + sh;
     const bool has_hi = 2 * p + 1 < dc;
     const bool has_left = p > 0, has_right = p + 1 < np;
     const uint32_t pbit = 1u << p;
@@ -606,9 +610,8 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
         const uint32_t lo = (uint32_t)(uint16_t)m2.x;
         const uint32_t hi = has_hi ? (uint32_t)(uint16_t)m2.y : 0u;
         m = lo | (hi << 16);
-        M[wr * ps + q] = m;
-        M16[2 * (wr * ps + q - 1) + 1] = (uint16_t)lo;   // M[wr][q-1].hi
-        M16[2 * (wr * ps + q + 1)] = (uint16_t)hi;       // M[wr][q+1].lo
+        M16[wr * pw + 3 + 2 * p] = (uint16_t)lo;   // window column x = 3 + 2p
+        M16[wr * pw + 4 + 2 * p] = (uint16_t)hi;
       }
       // all lanes: neighbour pixels of the same row from the adjacent lanes
       const uint32_t lhi = (uint32_t)__shfl_up((int)(m >> 16), 1, 64);
@@ -625,7 +628,7 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
           const fushort2 mc = as_u2(m1);
           const bool lmax_lo = mc.x > mx.x, lmax_hi = mc.y > mx.y;
           const int row = r - 1;
-          uint32_t* mr = mask + row * ps;
+          uint32_t* mr = mask + 4 * row;
           if (lmax_lo && mc.x >= t_min) atomicOr(mr, pbit);
           if (lmax_hi && mc.y >= t_min) atomicOr(mr + 1, pbit);
           const bool ilo = lmax_lo && mc.x >= t_ini, ihi = lmax_hi && mc.y >= t_ini;
@@ -651,11 +654,24 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
       if (ra >= rb) continue;
       const int row = (e & 1) ? rb - 1 : ra;
       if ((e & 1) && rb - 1 == ra) continue;   // one-row segment: done once
-      fushort2 m, mx;
-      nms_pair(M, ps, row + 3, 3 + 2 * p + sh, &m, &mx);
+      // rows wr-1, wr, wr+1: dword 1+p = pixels (x-1, x), dword 2+p = (x+1, x+2)
+      fushort2 rm[3], cmc = {0, 0}, m = {0, 0};
+#pragma unroll
+      for (int d = 0; d < 3; d++) {
+        const uint32_t* w = M + (row + 2 + d) * pw2 + 1 + p;
+        const uint32_t A = w[0], B = w[1];
+        const fushort2 cm = pmaxu(as_u2(A), as_u2(B));
+        const fushort2 mm = as_u2(__builtin_amdgcn_perm(B, A, 0x05040302u));   // (x, x+1)
+        rm[d] = pmaxu(cm, mm);
+        if (d == 1) {
+          cmc = cm;
+          m = mm;
+        }
+      }
+      const fushort2 mx = pmaxu(pmaxu(rm[0], rm[2]), cmc);
       const bool lmax_lo = m.x > mx.x, lmax_hi = m.y > mx.y;
       const uint32_t pbit = 1u << p;
-      uint32_t* mr = mask + row * ps;
+      uint32_t* mr = mask + 4 * row;
       if (lmax_lo && m.x >= t_min) atomicOr(mr, pbit);
       if (lmax_hi && m.y >= t_min) atomicOr(mr + 1, pbit);
       const bool ilo = lmax_lo && m.x >= t_ini, ihi = lmax_hi && m.y >= t_ini;
@@ -673,20 +689,20 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
   const int xoff = cg.x0 - kMinBorder, yoff = cg.y0 - kMinBorder;
   uint32_t blo = 0, bhi = 0;
   if (lane < dr && npair > 0) {
-    blo = mask[lane * ps + j0];
-    bhi = mask[lane * ps + j0 + 1];
+    blo = mask[4 * lane + j0];
+    bhi = mask[4 * lane + j0 + 1];
   }
   const int cnt = __popc(blo) + __popc(bhi);
   const int incl = wave_incl_scan(cnt);
   const int n = __shfl(incl, 63, 64);
   int pos = incl - cnt;
   const int y = yoff + lane + 3;
-  const uint32_t* Mrow = M + (lane + 3) * ps + 3 + sh;
+  const uint32_t* Mrow = M + (lane + 3) * pw2 + 1;
   uint32_t rem = blo | bhi;
   while (rem) {
     const int p = __builtin_ctz(rem);
     rem &= rem - 1;
-    const fushort2 m = as_u2(Mrow[2 * p]);
+    const fushort2 m = as_u2(__builtin_amdgcn_perm(Mrow[p + 1], Mrow[p], 0x05040302u));
     const int x = xoff + 3 + 2 * p;
     if ((blo >> p) & 1u) {
       if (pos < slots) out[pos] = pack_cand(x, y, m.x - 1);
