@@ -462,13 +462,45 @@ __global__ void __launch_bounds__(kPyrThreads) k_pyramid(const uint8_t* __restri
     }
     __syncthreads();
     if (stamp) prof[1 + 4 * l] = (long long)wall_clock64();
-    // ---- 2a. side borders of rows [na, nb) ----
-    for (int i = t; i < (nb - na) * 2 * kEdge; i += kPyrThreads) {
-      const int rr = i / (2 * kEdge), k = i - rr * 2 * kEdge;
-      const int r = na + rr;
-      const int px = k < kEdge ? k : L.w + k;          // padded column
-      const int cx = reflect101_dev(px - kEdge, L.w);
-      fp[padded_off(L, px, r + kEdge)] = fp[content_off(L, cx, r)];
+    // ---- 2a. side borders of rows [na, nb): thread per (row, side), the 19
+    // mirrored bytes (reflect-101: content 19..1 on the left, w-2..w-20 on the
+    // right) from aligned dword loads issued together ----
+    if (L.w >= kEdge + 2) {
+      for (int i = t; i < (nb - na) * 2; i += kPyrThreads) {
+        const int r = na + (i >> 1), side = i & 1;
+        uint8_t* prow = fp + L.pyr_off + (long long)(r + kEdge) * L.pitch;   // padded row
+        const int c0 = side ? L.w - kEdge - 1 : 0;        // first content byte used
+        const int a = kContent0 + c0;                     // its byte in the row
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(prow + (a & ~3));
+        const int o = a & 3;
+        uint32_t w[6];
+#pragma unroll
+        for (int k = 0; k < 6; k++) w[k] = src[k];
+        // byte j of the 20-byte run c0 .. c0+19: w[(o + j) >> 2] >> 8 * ((o + j) & 3)
+        auto byte_at = [&](int j) -> uint8_t {
+          const int b = o + j;
+          uint32_t v = w[0];
+#pragma unroll
+          for (int k = 1; k < 6; k++) v = (b >> 2) == k ? w[k] : v;
+          return (uint8_t)(v >> (8 * (b & 3)));
+        };
+        if (side == 0) {
+#pragma unroll
+          for (int px = 0; px < kEdge; px++) prow[kLead + px] = byte_at(kEdge - px);   // content 19 - px
+        } else {
+#pragma unroll
+          for (int k = 0; k < kEdge; k++)                   // content w - 2 - k = c0 + 18 - k
+            prow[kLead + L.w + kEdge + k] = byte_at(kEdge - 1 - k);
+        }
+      }
+    } else {
+      for (int i = t; i < (nb - na) * 2 * kEdge; i += kPyrThreads) {
+        const int rr = i / (2 * kEdge), k = i - rr * 2 * kEdge;
+        const int r = na + rr;
+        const int px = k < kEdge ? k : L.w + k;          // padded column
+        const int cx = reflect101_dev(px - kEdge, L.w);
+        fp[padded_off(L, px, r + kEdge)] = fp[content_off(L, cx, r)];
+      }
     }
     __syncthreads();
     if (stamp) prof[2 + 4 * l] = (long long)wall_clock64();
