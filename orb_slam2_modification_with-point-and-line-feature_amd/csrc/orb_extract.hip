@@ -258,18 +258,23 @@ __device__ __forceinline__ void pyr_resize_rows(const LevelGeom& L, const LevelG
     const int ra = na + seg * rps, rb = min(ra + rps, nb);
     const int x = 4 * gq;
     const int d0 = xofs[x] >> 2;                 // first source dword of the group
-    int p0[4], a0[4], a1[4];
+    // per column: the source pair (sx, sx + 1) as u16x2 by one v_perm from
+    // the low (bytes 0-7) or high (bytes 4-11) half of the 12-byte window,
+    // weighted by (alpha0, alpha1) in one v_dot2_u32_u16
+    uint32_t sel[4];
+    bool hiw[4];
+    fushort2 cf[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const int cx = min(x + k, L.w - 1);
-      p0[k] = xofs[cx] - 4 * d0;                 // byte of sx in the 12-byte window
+      const int p0 = xofs[cx] - 4 * d0;          // byte of sx in the 12-byte window
+      hiw[k] = p0 > 6;
+      const uint32_t pp = (uint32_t)(hiw[k] ? p0 - 4 : p0);
+      sel[k] = pp | (0x0cu << 8) | ((pp + 1) << 16) | (0x0cu << 24);
       if (cx < L.xmax) {
-        const int apk = alpha[cx];
-        a0[k] = (int)(short)(apk & 0xFFFF);
-        a1[k] = (int)(short)(apk >> 16);
+        cf[k] = as_u2((uint32_t)alpha[cx]);      // (alpha0, alpha1), both in [0, 2048]
       } else {
-        a0[k] = 2048;                            // sx + 1 >= src width: only sx
-        a1[k] = 0;
+        cf[k] = fushort2{2048, 0};               // sx + 1 >= src width: only sx
       }
     }
     // kPyrRsDepth rows per iteration: all source dwords are loaded before any is used
@@ -297,11 +302,13 @@ __device__ __forceinline__ void pyr_resize_rows(const LevelGeom& L, const LevelG
         uint32_t packed = 0;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-          // a1 == 0 at the right edge: the (unused) sx + 1 byte may be border
-          const int h0 = (int)byte_of(u[j][0], u[j][1], u[j][2], p0[k]) * a0[k] +
-                         (int)byte_of(u[j][0], u[j][1], u[j][2], p0[k] + 1) * a1[k];
-          const int h1 = (int)byte_of(v[j][0], v[j][1], v[j][2], p0[k]) * a0[k] +
-                         (int)byte_of(v[j][0], v[j][1], v[j][2], p0[k] + 1) * a1[k];
+          // alpha1 == 0 at the right edge: the (unused) sx + 1 byte may be border
+          const uint32_t tu = hiw[k] ? __builtin_amdgcn_perm(u[j][2], u[j][1], sel[k])
+                                     : __builtin_amdgcn_perm(u[j][1], u[j][0], sel[k]);
+          const uint32_t tv = hiw[k] ? __builtin_amdgcn_perm(v[j][2], v[j][1], sel[k])
+                                     : __builtin_amdgcn_perm(v[j][1], v[j][0], sel[k]);
+          const int h0 = (int)__builtin_amdgcn_udot2(as_u2(tu), cf[k], 0u, false);
+          const int h1 = (int)__builtin_amdgcn_udot2(as_u2(tv), cf[k], 0u, false);
           const uint32_t o =
               (uint32_t)((((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2);
           packed |= o << (8 * k);
