@@ -12,6 +12,7 @@
 // Bit-exactness against the CPU oracle relies on integer arithmetic for every
 // image stage and on orbpl_math.h for the two float stages.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <stdint.h>
 
 #include <cstdlib>
@@ -819,16 +820,22 @@ __device__ int block_excl_scan(int* vals, int n, int* s_wsum) {
 // 8 KB keeps two blocks per CU.
 constexpr int kOctLdsCand = 4096;
 
+// The node list never exceeds the level's kp_cap = max(N + 3, 4 nIni) (a
+// phase-1 pass starts only while size + 3 nexp <= N, phase 2 stops at the
+// first size >= N), so the list arrays are sized by kCap = the smallest of
+// 256 / 512 / 1024 that holds every level's kp_cap: at 1000 features 27 KB
+// of LDS per workgroup (5 per CU) instead of 74 KB (2 per CU).
+template <int kCap>
 struct OctShared {
-  uint2 rect[2][kOctMaxList];       // (x0 | y0<<16, x1 | y1<<16)
-  int cnt[2][kOctMaxList];
-  int rank[kOctMaxList];            // processing rank of a list entry, -1 = untouched
-  int upos[kOctMaxList];            // new position of an untouched entry
-  int child[4 * kOctMaxList];       // child counts, then child positions
-  int exp_pos[kOctMaxList];         // expandable children (creation order): list position
-  int exp_cnt[kOctMaxList];
-  int proc[kOctMaxList];            // processing order -> list position (phase 2)
-  int scan[kOctMaxList];
+  uint2 rect[2][kCap];              // (x0 | y0<<16, x1 | y1<<16)
+  int cnt[2][kCap];
+  int rank[kCap];                   // processing rank of a list entry, -1 = untouched
+  int upos[kCap];                   // new position of an untouched entry
+  int child[4 * kCap];              // child counts, then child positions
+  int exp_pos[kCap];                // expandable children (creation order): list position
+  int exp_cnt[kCap];
+  int proc[kCap];                   // processing order -> list position (phase 2)
+  int scan[kOctMaxList];            // also the cell-count scan (<= 1024 cells)
   int wsum[8];
   int misc[8];
   uint16_t kn[kOctLdsCand];         // node of each key when total <= kOctLdsCand
@@ -861,6 +868,7 @@ __device__ __forceinline__ uint2 child_rect(uint2 r, int c) {
 __device__ long long g_oct_prof[8 * 16];
 __device__ int g_oct_prof_on;
 
+template <int kCap>
 __global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
                                                 const uint32_t* __restrict__ cell_cands,
                                                 const int* __restrict__ cell_counts,
@@ -870,7 +878,7 @@ __global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
                                                 int* __restrict__ kp_count,
                                                 int* __restrict__ err_flag) {
   extern __shared__ char smem_raw[];
-  OctShared& S = *reinterpret_cast<OctShared*>(smem_raw);
+  OctShared<kCap>& S = *reinterpret_cast<OctShared<kCap>*>(smem_raw);
   const int level = blockIdx.x, f = blockIdx.y, t = threadIdx.x;
   const LevelGeom& L = g->lv[level];
   const int N = L.nfeat;
@@ -985,7 +993,7 @@ __global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
     }
     __syncthreads();
     if (nproc == 0) break;  // nothing divisible: size == prevSize -> finish
-    if (4 * nproc > 4 * kOctMaxList) {
+    if (4 * nproc > 4 * kCap) {
       if (t == 0) atomicOr(err_flag, 1);
       break;
     }
@@ -1061,7 +1069,7 @@ __global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
       }
     }
     const int newSize = nchild + nunt;
-    if (newSize > kOctMaxList) {
+    if (newSize > kCap) {
       if (t == 0) atomicOr(err_flag, 2);
       break;
     }
@@ -1325,7 +1333,6 @@ hipError_t upload_pattern(hipStream_t s) {
                                 hipMemcpyHostToDevice, s);
 }
 
-size_t octree_smem_bytes() { return sizeof(OctShared); }
 
 int read_od_profile(long long* out8) {
   return hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_od_prof), 6 * sizeof(long long)) == hipSuccess ? 0 : -1;
@@ -1357,10 +1364,13 @@ void launch_octree(const OrbGeom& hg, const OrbGeom* dg, const uint32_t* cell_ca
                    int* kp_count, int* err_flag, int batch, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)sizeof(OctShared));
+    (void)hipFuncSetAttribute((const void*)k_octree<1024>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)sizeof(OctShared<1024>));
     attr_set = true;
   }
+  int cap = 0;
+  for (int l = 0; l < hg.nlevels; l++) cap = std::max(cap, hg.lv[l].kp_cap);
   static bool prof_set = false;
   if (!prof_set) {
     const int on = getenv("ORBPL_OCT_PROFILE") ? 1 : 0;
@@ -1368,8 +1378,18 @@ void launch_octree(const OrbGeom& hg, const OrbGeom* dg, const uint32_t* cell_ca
                                  hipMemcpyHostToDevice, s);
     prof_set = true;
   }
-  hipLaunchKernelGGL(k_octree, dim3(hg.nlevels, batch), dim3(256), sizeof(OctShared), s, dg,
-                     cell_cands, cell_counts, kcand, knode, kp_list, kp_count, err_flag);
+  if (cap <= 256)
+    hipLaunchKernelGGL(k_octree<256>, dim3(hg.nlevels, batch), dim3(256),
+                       sizeof(OctShared<256>), s, dg, cell_cands, cell_counts, kcand, knode,
+                       kp_list, kp_count, err_flag);
+  else if (cap <= 512)
+    hipLaunchKernelGGL(k_octree<512>, dim3(hg.nlevels, batch), dim3(256),
+                       sizeof(OctShared<512>), s, dg, cell_cands, cell_counts, kcand, knode,
+                       kp_list, kp_count, err_flag);
+  else
+    hipLaunchKernelGGL(k_octree<1024>, dim3(hg.nlevels, batch), dim3(256),
+                       sizeof(OctShared<1024>), s, dg, cell_cands, cell_counts, kcand, knode,
+                       kp_list, kp_count, err_flag);
 }
 
 void launch_orient_desc(const OrbGeom& hg, const OrbGeom* dg, const uint8_t* pyr,

@@ -16,7 +16,6 @@ struct orbpl_keypoint_dev {
 };
 
 hipError_t upload_pattern(hipStream_t s);
-size_t octree_smem_bytes();
 // debug: k_octree phase ticks per level of frame 0 (ORBPL_OCT_PROFILE)
 int read_octree_profile(long long* out128);
 int read_od_profile(long long* out8);
