@@ -985,7 +985,12 @@ __device__ void se3_from_T(const float* T, SE3d& s) {
   s.t[0] = T[3]; s.t[1] = T[7]; s.t[2] = T[11];
 }
 
-__global__ void __launch_bounds__(256) k_pose(TrackConsts tc, PoseArgs a) {
+// minimum waves per SIMD for k_pose (register budget; it shares CUs with the
+// extraction kernels in the pipelined tracker)
+#ifndef ORBPL_POSE_MINW
+#define ORBPL_POSE_MINW 1
+#endif
+__global__ void __launch_bounds__(256, ORBPL_POSE_MINW) k_pose(TrackConsts tc, PoseArgs a) {
   extern __shared__ char smem_raw[];
   PoseShared& S = *reinterpret_cast<PoseShared*>(smem_raw);
   const int s = blockIdx.x, t = threadIdx.x;
