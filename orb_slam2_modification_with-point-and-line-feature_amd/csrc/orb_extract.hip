@@ -214,12 +214,8 @@ __device__ __forceinline__ uint32_t byte_of(uint32_t w0, uint32_t w1, uint32_t w
   return (lo >> (8 * (p & 3))) & 0xFF;
 }
 
-// Row segments of a walk (tasks = groups x nseg, rps rows per segment): the
-// split with the fewest sequential rows per thread, counting `warm` extra
-// rows per segment (the blur's 6 warm-up rows) and idle lanes of the last
-// round of tasks. Block-uniform.
-// rows of a column walk whose loads are in flight together (latency-bound:
-// the walks are few and long; registers allow 8 at 4 waves per SIMD)
+// rows of a column walk whose loads are in flight together (registers allow
+// 8 for the blur at 4 waves per SIMD; 4 for the resize, 2 source rows each)
 #ifndef ORBPL_PYR_DEPTH
 #define ORBPL_PYR_DEPTH 8
 #endif
@@ -229,6 +225,10 @@ constexpr int kPyrDepth = ORBPL_PYR_DEPTH;        // blur walk
 #endif
 constexpr int kPyrRsDepth = ORBPL_PYR_RS_DEPTH;   // resize walk (2 source rows per row)
 
+// Row segments of a walk (tasks = groups x nseg, rps rows per segment): the
+// split with the fewest sequential rows per thread, counting `warm` extra
+// rows per segment (the blur's 6 warm-up rows) and idle lanes of the last
+// round of tasks. Block-uniform.
 __device__ __forceinline__ void walk_split(int groups, int rows, int warm, int* nseg, int* rps) {
   int best = 1, best_cost = 0x7fffffff;
   for (int s = 1; s <= 64 && s <= rows; s++) {
