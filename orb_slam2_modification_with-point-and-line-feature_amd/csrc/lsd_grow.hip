@@ -1355,7 +1355,10 @@ __global__ void __launch_bounds__(64) k_lsd_spec(LsdGeom g, LsdScratch sc) {
 // k_lsd_compact.
 constexpr int kValBlocks = 8;
 
-__global__ void __launch_bounds__(256) k_lsd_validate(LsdGeom g, LsdScratch sc) {
+#ifndef ORBPL_VAL_MINW
+#define ORBPL_VAL_MINW 8   // 8 waves/SIMD (64 VGPRs, some scratch): 33.1 ms per 3072 frames; 6: 34.5; unbounded (111 VGPRs, 4 waves): 39.8
+#endif
+__global__ void __launch_bounds__(256, ORBPL_VAL_MINW) k_lsd_validate(LsdGeom g, LsdScratch sc) {
   const int f = blockIdx.y;
   const int nc = sc.ncand[f];
   const float* deg = sc.deg + (long long)f * g.sw * g.sh;
