@@ -171,6 +171,7 @@ struct SortPtrs {
   int* si;   // 8 arrays of seg_cap
   int* ci;   // 4 arrays of chunk_cap
   int2* leaves;
+  uint32_t* leaves_p;   // LDS variant: first | last << 16 (positions < 65536); null = leaves
   int seg_cap, chunk_cap, leaf_cap;
   int* err;
   int4* local;     // segments of <= local_max elements deferred to k_lsd_sort_local
@@ -309,7 +310,8 @@ __device__ __forceinline__ void sort_core(const SortPtrs& P, int first0, int las
       P.seg0[0] = make_int4(first0, last0, depth0, ub0);
       s_nseg = 1;
     } else if (n > 1) {
-      P.leaves[0] = make_int2(first0, last0);
+      if (P.leaves_p) P.leaves_p[0] = (uint32_t)first0 | ((uint32_t)last0 << 16);
+      else P.leaves[0] = make_int2(first0, last0);
       s_nleaf = 1;
     }
   }
@@ -487,7 +489,10 @@ __device__ __forceinline__ void sort_core(const SortPtrs& P, int first0, int las
           }
         } else if (size > 1) {
           const int idx = atomicAdd(&s_nleaf, 1);
-          if (idx < P.leaf_cap) P.leaves[idx] = make_int2(b, e);
+          if (idx < P.leaf_cap) {
+            if (P.leaves_p) P.leaves_p[idx] = (uint32_t)b | ((uint32_t)e << 16);
+            else P.leaves[idx] = make_int2(b, e);
+          }
           else atomicOr(P.err, 4);
         }
       }
@@ -505,7 +510,8 @@ __device__ __forceinline__ void sort_core(const SortPtrs& P, int first0, int las
     heap_sort_seg(A + sg.x, sg.y - sg.x);
   }
   for (int l = t; l < nleaf; l += NT) {
-    const int2 lf = P.leaves[l];
+    const int2 lf = P.leaves_p ? make_int2((int)(P.leaves_p[l] & 0xFFFFu), (int)(P.leaves_p[l] >> 16))
+                               : P.leaves[l];
     for (int i = lf.x + 1; i < lf.y; i++) {
       const uint32_t v = A[i];
       int j = i;
@@ -531,6 +537,7 @@ __device__ SortPtrs sort_ptrs(const LsdGeom& g, const LsdScratch& sc, int f) {
   P.si = sc.seg_i + (long long)f * 8 * g.seg_cap;
   P.ci = sc.chunk_i + (long long)f * 4 * g.chunk_cap;
   P.leaves = sc.leaves + (long long)f * g.leaf_cap;
+  P.leaves_p = nullptr;
   P.seg_cap = g.seg_cap;
   P.chunk_cap = g.chunk_cap;
   P.leaf_cap = g.leaf_cap;
@@ -551,13 +558,13 @@ constexpr int kLChunk = kSortLocalMax / kLsdSortChunk + kLSeg + 2;
 constexpr int kLLeaf = kSortLocalMax / 2 + 2;
 constexpr int kSortLocalBlocks = 4;
 
-__global__ void __launch_bounds__(kLocalThreads) k_lsd_sort_local(LsdGeom g, LsdScratch sc) {
+__global__ void __launch_bounds__(kLocalThreads, 4) k_lsd_sort_local(LsdGeom g, LsdScratch sc) {
   __shared__ uint32_t sA[kSortLocalMax];
   __shared__ int sL[kSortLocalMax], sR[kSortLocalMax];
   __shared__ int4 sseg0[kLSeg], sseg1[kLSeg], sheap[kLSeg];
   __shared__ int ssi[8 * kLSeg];
   __shared__ int sci[4 * kLChunk];
-  __shared__ int2 sleaves[kLLeaf];
+  __shared__ uint32_t sleaves[kLLeaf];   // packed: 40.6 KB of LDS in all, 4 blocks per CU
   const int f = blockIdx.y, t = threadIdx.x;
   uint32_t* A = sc.A + (long long)f * g.n;
   const int nloc = min(sc.sort_nlocal[f], g.seg_cap);
@@ -571,7 +578,8 @@ __global__ void __launch_bounds__(kLocalThreads) k_lsd_sort_local(LsdGeom g, Lsd
   L.heap = sheap;
   L.si = ssi;
   L.ci = sci;
-  L.leaves = sleaves;
+  L.leaves = nullptr;
+  L.leaves_p = sleaves;
   L.seg_cap = kLSeg;
   L.chunk_cap = kLChunk;
   L.leaf_cap = kLLeaf;
