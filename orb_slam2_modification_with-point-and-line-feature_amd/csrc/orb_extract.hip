@@ -1172,7 +1172,10 @@ constexpr int kBriefRowDw = 10;
 constexpr int kBriefDw = kBriefRows * kBriefRowDw;   // 370
 constexpr int kBriefLoads = (kBriefDw + 63) / 64;    // 6
 
-__global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__ pyr,
+#ifndef ORBPL_OD_MINW
+#define ORBPL_OD_MINW 1
+#endif
+__global__ void __launch_bounds__(256, ORBPL_OD_MINW) k_orient_desc(const uint8_t* __restrict__ pyr,
                                                      const uint8_t* __restrict__ blur,
                                                      const OrbGeom* __restrict__ g,
                                                      const uint32_t* __restrict__ kp_list,
