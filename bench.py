@@ -8,24 +8,34 @@ TUM1.yaml camera + distortion, ORB 1000 features / 1.2 / 8 levels / FAST 20,7.
 A step = one Tracking::TrackWithMotionModel pass (ORB extraction, Frame glue,
 SearchByProjection(th=15, retry 30), PoseOptimization, outlier discard) over a
 batch of `--streams` independent synthetic 640x480 RGB-D streams, all inputs
-resident in HBM before the timed region. The configs[2] workload (TUM3, ORB +
-LSD/LBD LineExtractor, LineMatcher::SearchByProjection, line edges in the
-pose) is timed the same way and reported under "secondary" (or as the
-headline with --workload lines), and so is configs[3] (KITTI 00 camera,
-1241x376 rectified stereo pairs, ORB 2000 on both images, ComputeStereoMatches,
-th = 7 matching, pose) under "stereo" (or --workload kitti). Frames are
-rendered from a seeded textured room along closed loop trajectories (no
-datasets on the box).
+resident in HBM before the timed region. The other BASELINE configs are timed
+the same way and reported in the same JSON line: configs[2] (TUM3, ORB +
+LSD/LBD LineExtractor, LineMatcher::SearchByProjection, line edges) under
+"secondary", configs[3] (KITTI 00 camera, 1241x376 rectified stereo pairs, ORB
+2000 on both images, ComputeStereoMatches, LineExtractor on both images with
+the defined stereo line depths, th = 7, pose with line edges) under "stereo",
+configs[4] (1280x720 8-camera rig) under "rig". Frames are rendered from a
+seeded textured room along closed-loop trajectories (no datasets on the box).
 
-Multi-GPU: one process per GPU (torchrun), streams sharded across ranks with
-no data-path collective (weak scaling); the gloo process group only carries the
-barrier and the max-over-ranks time.
+Parity: every timed tracker records its streams' poses and counts on the
+device (orbpl_tracker_set_history); after the timed region streams 0, S/2 and
+S-1 of every rank are replayed by the CPU oracle on the same frames and
+compared (counts exact, pose max-abs < 1e-4) under "parity".
 
-Prints ONE JSON line (rank 0). See DESIGN.md for the roofline accounting.
+Multi-GPU: `--gpus N` (without torchrun's environment) starts N ranks with
+torch.distributed.run before anything touches the GPU; under torchrun each
+rank reads RANK / LOCAL_RANK / WORLD_SIZE, uses device LOCAL_RANK (mod the
+visible devices) and tracks its own streams (weak scaling, no data-path
+collective); the gloo group carries the barriers, the max-over-ranks time and
+the per-rank parity reports.
+
+Prints ONE JSON line (rank 0). See DESIGN.md §5 for the roofline accounting.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import threading
 import time
@@ -40,8 +50,9 @@ sys.path.insert(0, str(ROOT / "tests"))
 W, H = 640, 480
 ORB = (1000, 1.2, 8, 20, 7)
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8 TB/s spec
+POSE_TOL = 1e-4         # north_star: pose within 1e-4
 
-# BASELINE.json configs[1..3]: camera (orbpl.synth), ORB parameters, sensor
+# BASELINE.json configs[1..4]: camera (orbpl.synth), ORB parameters, sensor
 WORKLOADS = {
     "points": dict(cam="TUM1", orb=ORB, lines=False, stereo=False,
                    desc="TUM fr1_desk-like RGB-D, ORB points only (configs[1])",
@@ -49,11 +60,17 @@ WORKLOADS = {
     "lines": dict(cam="TUM3", orb=ORB, lines=True, stereo=False,
                   desc="TUM fr3_structure_texture_far-like RGB-D, ORB + LSD/LBD lines (configs[2])",
                   data="synthetic (seeded textured-room RGB-D loop, TUM3 intrinsics, no distortion)"),
-    "kitti": dict(cam="KITTI00", orb=(2000, 1.2, 8, 20, 7), lines=False, stereo=True,
-                  desc="KITTI 00-like stereo 1241x376, ORB 2000 both images + ComputeStereoMatches "
-                       "+ PoseOptimization (configs[3]; the reference's stereo Frame has no lines)",
+    "kitti": dict(cam="KITTI00", orb=(2000, 1.2, 8, 20, 7), lines=True, stereo=True,
+                  desc="KITTI 00-like stereo 1241x376, ORB 2000 + LSD/LBD on both images, "
+                       "ComputeStereoMatches + stereo line depths (defined mode P17) + "
+                       "PoseOptimizationWithLines (configs[3])",
                   data="synthetic (seeded textured-room rectified stereo loop, KITTI 00 intrinsics, "
                        "bf 386.1448)"),
+    "kitti_points": dict(cam="KITTI00", orb=(2000, 1.2, 8, 20, 7), lines=False, stereo=True,
+                         desc="KITTI 00-like stereo 1241x376, ORB 2000 both images + "
+                              "ComputeStereoMatches + PoseOptimization (points only)",
+                         data="synthetic (seeded textured-room rectified stereo loop, KITTI 00 "
+                              "intrinsics, bf 386.1448)"),
     "rig": dict(cam="RIG720", orb=(2000, 1.2, 8, 20, 7), lines=False, stereo=False, cams=8,
                 desc="synthetic 1280x720 8-camera rig (45 deg yaw spacing), RGB-D, ORB 2000 "
                      "(configs[4]); stream 8r+c = camera c of rig r",
@@ -117,19 +134,22 @@ def level_areas(w=W, h=H, orb=ORB):
     return [int(a) * int(b) for a, b in zip(d["width"], d["height"])], d
 
 
-def algorithmic_bytes(n_kp, w=W, h=H, orb=ORB):
-    """Per-frame algorithmic HBM bytes of each kernel:
-    the bytes the kernel must move at minimum (each input read once, each
-    output written once), with n_kp keypoints per frame."""
+def algorithmic_bytes(n_kp, w=W, h=H, orb=ORB, n_lines=80):
+    """Per-frame algorithmic HBM bytes of each kernel: the
+    bytes the kernel must move at minimum (each input read once, each output
+    written once), with n_kp keypoints per frame. LSD works on the 0.8-scaled
+    image (sA pixels, LSD's `scale` of LineSegmentDetector)."""
     areas, d = level_areas(w, h, orb)
     S = sum(areas)
     dims = list(zip((int(a) for a in d["width"]), (int(b) for b in d["height"])))
     pads = [(a + 38) * (b + 38) for a, b in dims]
+    A0 = w * h
+    sA = int(np.ceil(w * 0.8)) * int(np.ceil(h * 0.8))
     return {
-        # read the input (level 0) or the previous level, write the padded level
-        "pyramid": w * h + sum(areas[:-1]) + sum(pads),
-        # read each level's content + 3 px halo, write the blurred content
-        "blur": sum((a + 6) * (b + 6) for a, b in dims) + S,
+        # read the input (level 0) or the previous level, write the padded
+        # level; read each level's content + 3 px halo, write the blurred content
+        "pyramid": w * h + sum(areas[:-1]) + sum(pads) +
+                   sum((a + 6) * (b + 6) for a, b in dims) + S,
         # read every pyramid level once (candidate output is ~1 % of it)
         "fast": S,
         # candidates in (4 B) and keypoints out (4 B); ~8 candidates per keypoint
@@ -141,132 +161,142 @@ def algorithmic_bytes(n_kp, w=W, h=H, orb=ORB):
         "match": n_kp * (72 + 78),
         # per keypoint: kp 28 + ur 4 + match 4 + xyz 12 + outlier 2
         "pose": n_kp * 50,
+        # LSD: read the image, write the scaled u8 image, the angle (f32) and
+        # the gradient-norm key (i32) per scaled pixel
+        "lsd_prep": A0 + sA * 9,
+        # pseudo-ordering: read the keys, write the pixel order (4 B each)
+        "lsd_sort": sA * 8,
+        # seed loop: read the order, the angles and the USED/region state once,
+        # write the state once (4 + 4 + 1 + 1 B per scaled pixel)
+        "lsd_seed": sA * 10,
+        # NFA validation: each rectangle's pixels' angles, bounded by one read
+        "lsd_validate": sA * 4,
+        # KeyLines: segments in (16 B x ~1500), 80 KeyLines (68 B) + 80 coef (24 B) out
+        "keylines": 1500 * 16 + n_lines * (68 + 24),
+        # LBD: read the image, 5x5 blur out + in, Sobel dx/dy i16 out + in,
+        # 80 x 32 B descriptors out
+        "lbd": A0 + 2 * A0 + 2 * 4 * A0 + n_lines * 32,
+        # UndistortKeyLines + line depths: 80 KeyLines in and out, 160 depth reads
+        "line_prepare": n_lines * (68 * 2 + 8 + 8),
     }
 
 
-def pmc_traffic(kernel, streams):
+KERNELS = {"pyramid": "k_pyramid", "fast": "k_fast_cells", "octree": "k_octree",
+           "orient_desc": "k_orient_desc", "match": "k_match_last", "pose": "k_pose",
+           "lsd_prep": "k_lsd_blur+k_lsd_resize+k_lsd_grad", "lsd_sort": "k_lsd_sort+k_lsd_sort_local",
+           "lsd_seed": "k_lsd_spec", "lsd_validate": "k_lsd_validate+k_lsd_compact",
+           "keylines": "k_keylines", "lbd": "k_lsd_blur+k_sobel+k_lbd",
+           "line_prepare": "k_line_prepare"}
+
+
+def pmc_traffic(kernel, workload, streams):
     """HBM bytes per launch of `kernel` from the committed PMC summary of the
-    same bench command (tools/prof.sh + tools/pmc_traffic.py; FETCH_SIZE x2
-    gfx950 correction + WRITE_SIZE), scaled to this run's stream count. PMC
-    counters need their own rocprofv3 passes, so they cannot be read live."""
-    for rnd in ("r01",):
-        f = ROOT / "profiles" / rnd / "pmc_traffic.json"
-        if f.exists():
-            d = json.load(open(f))
-            e = d.get(kernel)
-            meta = d.get("_meta", {})
-            if e and e.get("traffic_bytes") and meta.get("streams"):
-                return (int(e["traffic_bytes"] * streams / meta["streams"]),
-                        f"profiles/{rnd}/pmc_traffic.json ({meta['streams']} streams, scaled)")
+    same workload (tools/prof.sh + tools/pmc_traffic.py: FETCH_SIZE x2 gfx950
+    correction + WRITE_SIZE), scaled to this run's stream count. PMC counters
+    need their own rocprofv3 passes, so they cannot be read live. Stage
+    kernels joined with '+' sum their parts."""
+    for rnd in ("r02", "r01"):
+        f = ROOT / "profiles" / rnd / f"pmc_traffic_{workload}.json"
+        if not f.exists() and workload == "points":
+            f = ROOT / "profiles" / rnd / "pmc_traffic.json"
+        if not f.exists():
+            continue
+        d = json.load(open(f))
+        meta = d.get("_meta", {})
+        parts = kernel.split("+")
+        es = [d.get(k) for k in parts]
+        if all(e and e.get("traffic_bytes") for e in es) and meta.get("streams"):
+            tb = sum(e["traffic_bytes"] for e in es)
+            return (int(tb * streams / meta["streams"]),
+                    f"{f.relative_to(ROOT)} ({meta['streams']} streams, scaled)")
     return None, None
 
 
-def _oracle_vo(O, wl):
-    """The oracle's VO loop for a workload; returns (vo, step(vo, a, b))."""
+def oracle_vo(O, wl):
+    """The oracle's VO loop for a workload; returns (vo, step(vo, s, a, b))."""
     import orbpl.synth as synth
     cam = O.camera(getattr(synth, wl["cam"]))
     if wl["stereo"]:
-        return (O.LVO(O.params(*wl["orb"]), cam, 1, use_lines=False),
+        return (O.LVO(O.params(*wl["orb"]), cam, 1, use_lines=wl["lines"]),
                 lambda vo, a, b: vo.step_stereo(0, a, b))
     if wl["lines"]:
         return O.LVO(O.params(*wl["orb"]), cam, 1, use_lines=True), lambda vo, a, b: vo.step(0, a, b)
     return O.VO(O.params(*wl["orb"]), cam, 1), lambda vo, a, b: vo.step(0, a, b)
 
 
-def cpu_baseline(seconds, threads, gray, depth, L, workload="points"):
-    """The CPU oracle (C++ restatement, oracle/) running the same per-frame
-    step, one stream per thread (throughput mode), for a bounded wall time."""
+OUT8 = ("nkeypoints", "nmatches", "ninliers", "nmatches_map", "ok", "nlines", "line_matches",
+        "line_nmatches_map")
+
+
+def parity_check(T_gpu, C_gpu, streams, gray, depth, L, workload):
+    """Replay `streams` of the timed tracker on the CPU oracle over the same
+    frames (one host thread per stream) and compare every step: the 8 counts
+    exactly, the pose to POSE_TOL. T_gpu[k]: (n, 4, 4), C_gpu[k]: (n, 8)."""
     from _pkg import load_oracle
-    O = load_oracle()
-    wl = WORKLOADS[workload]
-    counts = [0] * threads
-    stop = time.time() + seconds
-
-    def worker(k):
-        vo, vstep = _oracle_vo(O, wl)
-        i = 0
-        while time.time() < stop:   # worker k runs stream k of the layout
-            e = L.elem(k, i)
-            vstep(vo, gray[e], depth[e])
-            i += 1
-        counts[k] = i
-
-    t0 = time.time()
-    ths = [threading.Thread(target=worker, args=(k,)) for k in range(threads)]
-    for t in ths:
-        t.start()
-    for t in ths:
-        t.join()
-    dt = time.time() - t0
-    return sum(counts) / dt, sum(counts), dt
-
-
-def accuracy_gpu(pkg, cam, wl, d_gray, d_depth, L, A, local_rank, fb, db):
-    """Untimed accuracy leg: A streams tracked over a whole loop of F frames
-    (Layout L, each stream starts at its true pose); returns the (A, F, 4, 4)
-    Tcw poses after every step."""
-    F = L.F
-    tr = pkg.Tracker(pkg.OrbParams(*wl["orb"]), cam, A, device=local_rank, lines=wl["lines"],
-                     stereo=wl["stereo"])
-    tr.reset(np.stack([np.linalg.inv(L.Twc(s, 0)).astype(np.float32) for s in range(A)]).reshape(
-        A, 16))
-    out = np.zeros((A, F, 4, 4), np.float32)
-    for t in range(F):
-        o = t * L.cams
-        if wl["stereo"]:
-            tr.step_stereo_device(d_gray.ptr + o * fb, d_depth.ptr + o * db)
-        else:
-            tr.step_device(d_gray.ptr + o * fb, d_depth.ptr + o * db)
-        tr.synchronize()
-        out[:, t] = tr.state()["Tcw"]
-    tr.close()
-    return out
-
-
-def accuracy_ref(gray, depth, L, A, workload):
-    """The oracle's VO loop (the reference restatement) over the same A x F
-    frames, one host thread per stream; returns its (A, F, 4, 4) poses."""
-    from _pkg import load_oracle
-    O = load_oracle()
-    wl = WORKLOADS[workload]
-    F = L.F
-    out = np.zeros((A, F, 4, 4), np.float32)
-
-    def worker(s):
-        vo, vstep = _oracle_vo(O, wl)
-        vo.reset(np.linalg.inv(L.Twc(s, 0)).astype(np.float32).reshape(1, 16))
-        for t in range(F):
-            e = L.elem(s, t)
-            out[s, t] = vstep(vo, gray[e], depth[e])[0]
-
-    ths = [threading.Thread(target=worker, args=(s,)) for s in range(A)]
-    for t in ths:
-        t.start()
-    for t in ths:
-        t.join()
-    return out
-
-
-def ate_report(T_gpu, T_ref, L):
-    """ATE RMSE (m) of the GPU poses vs the reference restatement's poses of
-    the same frames (raw: both start at the same pose) and of both vs the
-    ground truth (rigidly aligned, as TUM's evaluate_ate)."""
     import orbpl.tum as tum
-    A, F = T_gpu.shape[:2]
-    gt = np.stack([np.linalg.inv(L.Twc(s, t)) for s in range(A) for t in range(F)])
-    cg = tum.camera_centres(T_gpu.reshape(-1, 4, 4))
+    O = load_oracle()
+    wl = WORKLOADS[workload]
+    n = min(len(T) for T in T_gpu)
+    T_ref = np.zeros((len(streams), n, 4, 4), np.float32)
+    C_ref = np.zeros((len(streams), n, 8), np.int32)
+
+    def worker(k, s):
+        vo, vstep = oracle_vo(O, wl)
+        vo.reset(np.linalg.inv(L.Twc(s, 0)).astype(np.float32).reshape(1, 16))
+        for t in range(n):
+            e = L.elem(s, t)
+            T, st = vstep(vo, gray[e], depth[e])
+            T_ref[k, t] = T
+            C_ref[k, t] = [st[key] for key in OUT8]
+
+    ths = [threading.Thread(target=worker, args=(k, s)) for k, s in enumerate(streams)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    Tg = np.stack([T[:n] for T in T_gpu])
+    Cg = np.stack([c[:n] for c in C_gpu])
+    bad = [(int(streams[k]), int(t), OUT8[i]) for k, t, i in zip(*np.nonzero(Cg != C_ref))]
+    dmax = float(np.abs(Tg - T_ref).max()) if n else 0.0
+    gt = np.stack([np.linalg.inv(L.Twc(s, t)) for s in streams for t in range(n)])
+    cg = tum.camera_centres(Tg.reshape(-1, 4, 4))
+    cr = tum.camera_centres(T_ref.reshape(-1, 4, 4))
     cgt = tum.camera_centres(gt)
-    rep = {"streams": A, "frames_per_stream": F,
-           "ate_rmse_vs_gt_m": round(tum.ate(cg, cgt)["rmse"], 6)}
-    if T_ref is not None:
-        cr = tum.camera_centres(T_ref.reshape(-1, 4, 4))
-        rep["ate_rmse_vs_ref_m"] = float(f"{tum.ate(cg, cr, aligned=False)['rmse']:.3e}")
-        rep["max_abs_pose_diff_vs_ref"] = float(f"{np.abs(T_gpu - T_ref).max():.3e}")
-        rep["ref_ate_rmse_vs_gt_m"] = round(tum.ate(cr, cgt)["rmse"], 6)
-    return rep
+    return {"source": "timed tracker (device-side per-step history)", "streams": [int(s) for s in streams],
+            "steps_checked": n, "counts_equal": not bad, "count_mismatches": bad[:10],
+            "max_abs_pose_diff_vs_ref": float(f"{dmax:.3e}"), "pose_tol": POSE_TOL,
+            "pass": (not bad) and dmax < POSE_TOL,
+            "ate_rmse_vs_gt_m": round(tum.ate(cg, cgt)["rmse"], 6) if n > 2 else None,
+            "ref_ate_rmse_vs_gt_m": round(tum.ate(cr, cgt)["rmse"], 6) if n > 2 else None}
 
 
-def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, local_rank, dist):
+def max_over_ranks(dist, elapsed):
+    """The timed region's wall time, max over ranks (gloo all_reduce)."""
+    if not dist:
+        return elapsed
+    import torch
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def gather_parity(dist, world, parity):
+    """Every rank's parity report on every rank (gloo all_gather_object)."""
+    if not dist:
+        return parity
+    allp = [None] * world
+    dist.all_gather_object(allp, parity)
+    return {"all_ranks_pass": all(p is not None and p["pass"] for p in allp), "by_rank": allp}
+
+
+def torchrun_cmd(ngpus, argv, port):
+    """The command `--gpus N` runs: one rank per GPU under torch.distributed.run."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={ngpus}", "--master-addr", "127.0.0.1", "--master-port", str(port),
+            str(Path(__file__).resolve())] + list(argv)
+
+
+def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, device, dist):
     """Time `steps` tracker steps of one workload; returns the measurements."""
     wl = WORKLOADS[workload]
     lines, stereo, cam_name = wl["lines"], wl["stereo"], wl["cam"]
@@ -282,16 +312,16 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, loca
     L = Layout(traj, cams)
     # every step's batch is one contiguous slice of a replicated buffer (Layout)
     rep = L.replicated(S)
-    d_gray = pkg.DeviceBuffer.from_array(gray[rep], device=local_rank)
-    d_depth = pkg.DeviceBuffer.from_array(depth[rep], device=local_rank)
+    d_gray = pkg.DeviceBuffer.from_array(gray[rep], device=device)
+    d_depth = pkg.DeviceBuffer.from_array(depth[rep], device=device)
     cam = pkg.make_camera(getattr(synth, cam_name))
-    tr = pkg.Tracker(pkg.OrbParams(*wl["orb"]), cam, S, device=local_rank, lines=lines,
-                     stereo=stereo)
+    tr = pkg.Tracker(pkg.OrbParams(*wl["orb"]), cam, S, device=device, lines=lines, stereo=stereo)
     # pipelining overlaps extraction of step t+1 with tracking of step t; the
-    # lines workload is bound by the LSD stream, which the overlap only slows
+    # LSD-bound line workloads gain nothing from it
     pipelined = args.pipelined if args.pipelined >= 0 else (0 if lines else 1)
     tr.set_pipelined(bool(pipelined))
     tr.reset(np.stack([np.linalg.inv(L.Twc(s, 0)).astype(np.float32) for s in range(S)]).reshape(S, 16))
+    tr.set_history(warmup + steps)
     fb = fw * fh
     db = fb * depth.itemsize   # right image (u8) for stereo, depth (f32) otherwise
 
@@ -316,16 +346,12 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, loca
     if dist:
         dist.barrier()
     t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if dist:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(dist, t1 - t0)
     st = tr.state()
     tim = tr.timings(steps)                            # (steps, 9) ms, in-stream hipEvents
     avg = tim.mean(0)
     stages = dict(zip(tr.STAGES, [round(float(x), 4) for x in avg]))
+    stage_avg = dict(zip(tr.STAGES, [float(x) for x in avg]))
     tracking = {"mean_keypoints": float(st["nkeypoints"].mean()),
                 "mean_matches": float(st["nmatches"].mean()),
                 "mean_inliers": float(st["ninliers"].mean()),
@@ -333,6 +359,9 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, loca
     if lines:
         lt = tr.line_timings(steps).mean(0)
         stages.update(zip(tr.LINE_STAGES, [round(float(x), 4) for x in lt]))
+        ls_t = tr.lsd_timings(steps).mean(0)
+        stages.update(zip(tr.LSD_STAGES, [round(float(x), 4) for x in ls_t]))
+        stage_avg.update(zip(tr.LSD_STAGES, [float(x) for x in ls_t]))
         ls = tr.status()
         tracking.update(mean_lines=float(ls["nlines"].mean()),
                         mean_line_matches=float(ls["line_matches"].mean()))
@@ -342,14 +371,16 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, loca
     frames = S * steps * world
     value = frames / elapsed
 
-    # roofline of the dominant single-launch kernel; k_pyramid (pyramid +
-    # borders + blur, one launch) is timed by the "pyramid" stage
+    # device-side history of the timed tracker: streams 0, S/2, S-1
+    samp = sorted({0, S // 2, S - 1})
+    hist = [tr.history(s, warmup + steps) for s in samp]
+
+    # roofline of the dominant single-stage kernel
     n_kp = float(st["nkeypoints"].mean())
     ab = algorithmic_bytes(n_kp, fw, fh, wl["orb"])
-    ab["pyramid"] = ab["pyramid"] + ab.pop("blur")
-    names = {"pyramid": "k_pyramid", "fast": "k_fast_cells", "octree": "k_octree",
-             "orient_desc": "k_orient_desc", "match": "k_match_last", "pose": "k_pose"}
-    idx = {k: tr.STAGES.index(k) for k in names}
+    cand = ["pyramid", "fast", "octree", "orient_desc", "match", "pose"]
+    if lines:
+        cand += list(tr.LSD_STAGES)
     iso = None
     if pipelined and args.isolated_steps > 0:
         # untimed: more steps with the two HIP streams serialised, so each
@@ -362,35 +393,178 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, loca
         for k in range(args.isolated_steps):
             step(warmup + steps + k)
         tr.synchronize()
-        iso = tr.timings(args.isolated_steps).mean(0)
-    sel = iso if iso is not None else avg
-    dom = max(names, key=lambda k: sel[idx[k]])
-    dom_ms = float(avg[idx[dom]])          # live: timed region, in-stream hipEvents
+        iso = dict(zip(tr.STAGES, [float(x) for x in tr.timings(args.isolated_steps).mean(0)]))
+    sel = iso if iso is not None else stage_avg
+    dom = max(cand, key=lambda k: sel.get(k, stage_avg[k]))
+    dom_ms = stage_avg[dom]          # live: timed region, in-stream hipEvents
     bytes_launch = int(ab[dom] * S)
     achieved = bytes_launch / (dom_ms * 1e-3) / 1e9
-    traffic, tsrc = pmc_traffic(names[dom], S) if workload == "points" else (None, None)
-    roof = {"bound": "hbm", "kernel": names[dom],
+    traffic, tsrc = pmc_traffic(KERNELS[dom], workload, S)
+    roof = {"bound": "hbm", "kernel": KERNELS[dom], "stage": dom,
             "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
             "traffic_source": tsrc,
+            "traffic_over_algorithmic": round(traffic / bytes_launch, 2) if traffic else None,
             "algorithmic_bytes_per_launch": bytes_launch, "avg_launch_ms": round(dom_ms, 4),
-            "per_kernel_GBps": {k: round(ab[k] * S / (float(avg[idx[k]]) * 1e-3) / 1e9, 1)
-                                for k in names}}
+            "per_kernel_GBps": {k: round(ab[k] * S / (stage_avg[k] * 1e-3) / 1e9, 1)
+                                for k in cand if stage_avg[k] > 0}}
     if iso is not None:
-        ims = float(iso[idx[dom]])
+        ims = iso[dom]
         roof["isolated"] = {
-            "stage_ms": dict(zip(tr.STAGES, [round(float(x), 4) for x in iso])),
+            "stage_ms": {k: round(v, 4) for k, v in iso.items()},
             "avg_launch_ms": round(ims, 4),
             "achieved": round(bytes_launch / (ims * 1e-3) / 1e9, 2),
             "frac": round(bytes_launch / (ims * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
             "steps": args.isolated_steps}
     tr.close()
-    A = min(args.ate_streams, S)
-    T_acc = (accuracy_gpu(pkg, cam, wl, d_gray, d_depth, L, A, local_rank, fb, db)
-             if A > 0 else None)
-    return dict(S=S, value=value, T_acc=T_acc, layout=L, elapsed=elapsed, stages=stages,
-                tracking=tracking, roof=roof, gray=gray, depth=depth, workload=wl["desc"],
-                data=wl["data"], image=f"{fw}x{fh}", nfeatures=wl["orb"][0])
+    del d_gray, d_depth
+    return dict(S=S, value=value, layout=L, elapsed=elapsed, stages=stages, tracking=tracking,
+                roof=roof, gray=gray, depth=depth, workload=wl["desc"], data=wl["data"],
+                image=f"{fw}x{fh}", nfeatures=wl["orb"][0], samp=samp, hist=hist, wname=workload,
+                pipelined=bool(pipelined))
+
+
+def sweep(pkg, synth, workload, sizes, steps, device):
+    """Per-step latency and throughput at several batch sizes (untimed for the
+    headline; each size gets its own tracker, 1 warm-up step)."""
+    wl = WORKLOADS[workload]
+    F = 8
+    gray, depth = render_loop(F, seed=7, workers=min(16, os.cpu_count() or 4), cam_name=wl["cam"],
+                              stereo=wl["stereo"])
+    fh, fw = gray.shape[1:]
+    L = Layout(synth.loop_trajectory(F, seed=7))
+    cam = pkg.make_camera(getattr(synth, wl["cam"]))
+    out = []
+    for S in sizes:
+        rep = L.replicated(S)
+        d_gray = pkg.DeviceBuffer.from_array(gray[rep], device=device)
+        d_depth = pkg.DeviceBuffer.from_array(depth[rep], device=device)
+        tr = pkg.Tracker(pkg.OrbParams(*wl["orb"]), cam, S, device=device, lines=wl["lines"],
+                         stereo=wl["stereo"])
+        tr.set_pipelined(not wl["lines"])
+        tr.reset(np.stack([np.linalg.inv(L.Twc(s, 0)).astype(np.float32)
+                           for s in range(S)]).reshape(S, 16))
+        fb, db = fw * fh, fw * fh * depth.itemsize
+
+        def step(k):
+            o = k % F
+            if wl["stereo"]:
+                tr.step_stereo_device(d_gray.ptr + o * fb, d_depth.ptr + o * db)
+            else:
+                tr.step_device(d_gray.ptr + o * fb, d_depth.ptr + o * db)
+
+        step(0)
+        tr.synchronize()
+        lat = []
+        for k in range(steps):     # latency: one step issued and waited for
+            t0 = time.perf_counter()
+            step(1 + k)
+            tr.synchronize()
+            lat.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()   # throughput: steps back to back
+        for k in range(steps):
+            step(1 + steps + k)
+        tr.synchronize()
+        thr = S * steps / (time.perf_counter() - t0)
+        out.append({"streams": S, "latency_ms_per_step": round(1e3 * float(np.median(lat)), 3),
+                    "fps": round(thr, 1)})
+        tr.close()
+        del d_gray, d_depth
+    return out
+
+
+def host_info():
+    """Host CPU facts for the CPU baseline: model, logical CPUs (nproc), the
+    CPUs this process may use (affinity) and the cgroup CPU quota."""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = float(q) / float(p)
+    except (OSError, ValueError):
+        pass
+    aff = len(os.sched_getaffinity(0))
+    usable = aff if quota is None else max(1, min(aff, int(quota)))
+    # the GPU box gives a one-GPU job a 16-CPU share (nproc shows the whole
+    # machine there); OMP_NUM_THREADS carries that share
+    share = os.environ.get("OMP_NUM_THREADS")
+    if share and share.isdigit():
+        usable = min(usable, int(share))
+    return {"model": model, "nproc": os.cpu_count(), "affinity_cpus": aff, "cgroup_quota": quota,
+            "usable_cores": usable}
+
+
+def cpu_baseline(seconds, threads, gray, depth, L, workload="points"):
+    """Throughput mode (BASELINE.md §2 mode 2): the CPU oracle running the
+    same per-frame step, one stream per host thread, for a bounded wall time."""
+    from _pkg import load_oracle
+    O = load_oracle()
+    wl = WORKLOADS[workload]
+    counts = [0] * threads
+    stop = time.time() + seconds
+
+    def worker(k):
+        vo, vstep = oracle_vo(O, wl)
+        i = 0
+        while time.time() < stop:   # worker k runs stream k of the layout
+            e = L.elem(k, i)
+            vstep(vo, gray[e], depth[e])
+            i += 1
+        counts[k] = i
+
+    t0 = time.time()
+    ths = [threading.Thread(target=worker, args=(k,)) for k in range(threads)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    dt = time.time() - t0
+    return sum(counts) / dt, sum(counts), dt
+
+
+def cpu_reference_faithful(seconds, gray, depth, L, workload):
+    """BASELINE.md §2 mode 1: one stream as the reference runs it, ORB and
+    the LineExtractor on two host threads per frame (Frame.cc:152-155),
+    matching and pose on the tracking thread; per-frame latency."""
+    from _pkg import load_oracle
+    import orbpl.synth as synth
+    O = load_oracle()
+    wl = WORKLOADS[workload]
+    cam = O.camera(getattr(synth, wl["cam"]))
+    vo = O.LVO(O.params(*wl["orb"]), cam, 1, use_lines=wl["lines"], flags=O.TWO_THREADS)
+    vo.reset(np.linalg.inv(L.Twc(0, 0)).astype(np.float32).reshape(1, 16))
+    lat = []
+    stop = time.time() + seconds
+    i = 0
+    while time.time() < stop or i < 3:
+        e = L.elem(0, i)
+        t0 = time.perf_counter()
+        if wl["stereo"]:
+            vo.step_stereo(0, gray[e], depth[e])
+        else:
+            vo.step(0, gray[e], depth[e])
+        lat.append(time.perf_counter() - t0)
+        i += 1
+    lat = np.array(lat[2:]) * 1e3   # the first frames have no last frame
+    return {"value": round(1e3 / float(lat.mean()), 2), "unit": "frames/s",
+            "threads_per_frame": 2 if wl["lines"] else 1,
+            "median_ms_per_frame": round(float(np.median(lat)), 3),
+            "mean_ms_per_frame": round(float(lat.mean()), 3), "frames": int(len(lat)),
+            "sample": f"one stream, {len(lat)} frames after 2 warm-up frames"}
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
 def main():
@@ -401,11 +575,11 @@ def main():
     ap.add_argument("--streams", type=int, default=256, help="streams (frames per step) per GPU")
     ap.add_argument("--loop", type=int, default=32, help="frames in the synthetic loop")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the host's usable cores")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workload", choices=tuple(WORKLOADS), default="points",
                     help="points = configs[1] (headline); lines = configs[2] ORB + LSD/LBD; "
-                         "kitti = configs[3] stereo; rig = configs[4] 1280x720 8-camera rig")
+                         "kitti = configs[3] stereo points+lines; rig = configs[4] 1280x720 rig")
     ap.add_argument("--rig-loop", type=int, default=12,
                     help="rig frames in the synthetic loop (x8 camera renders)")
     ap.add_argument("--secondary-steps", type=int, default=3,
@@ -417,67 +591,94 @@ def main():
     ap.add_argument("--stereo-steps", type=int, default=3,
                     help="steps of the configs[3] stereo workload reported under 'stereo' "
                          "(points runs only; 0 = skip)")
-    ap.add_argument("--stereo-streams", type=int, default=256)
+    ap.add_argument("--stereo-streams", type=int, default=1024)
     ap.add_argument("--rig-steps", type=int, default=3,
                     help="steps of the configs[4] 8-camera rig workload reported under 'rig' "
                          "(points runs only; 0 = skip)")
     ap.add_argument("--rig-streams", type=int, default=256, help="rig cameras per GPU (x8)")
-    ap.add_argument("--ate-streams", type=int, default=8,
-                    help="streams of the untimed accuracy leg (ATE vs ground truth and vs the "
-                         "reference restatement over one loop); 0 = skip")
     ap.add_argument("--isolated-steps", type=int, default=5,
                     help="untimed non-pipelined steps after the timed region: per-kernel "
                          "times without the other stream's interference (roofline.isolated)")
     ap.add_argument("--pipelined", type=int, default=-1,
                     help="1 = overlap extraction of step t+1 with tracking of step t; 0 = no; "
-                         "-1 = per workload (on, except for the LSD-bound lines workload)")
+                         "-1 = per workload (on, except for the LSD-bound line workloads)")
+    ap.add_argument("--sweep", type=int, default=1,
+                    help="1 = per-step latency / fps at batch 1..1024 (points) and 1..256 "
+                         "(lines) after the timed runs (points runs, rank 0 only)")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="skip the oracle replay of the timed trackers' sampled streams")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU, started before anything here touches the GPU
+        sys.exit(subprocess.call(torchrun_cmd(args.gpus, sys.argv[1:], _free_port())))
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
-        import torch
+        import torch  # noqa: F401
         import torch.distributed as dist
         dist.init_process_group("gloo")
 
-    from _pkg import load_pkg
+    from _pkg import load_oracle, load_pkg
     pkg = load_pkg()
     import orbpl.synth as synth
+    O = load_oracle()
+    oracle_build = O.use_variant("best")   # -O3 -march build for the CPU legs
+    ndev = pkg.device_count()
+    device = local_rank % max(1, ndev)
 
     res = run_workload(pkg, synth, args, args.workload, args.streams, args.steps, args.warmup,
-                       rank, world, local_rank, dist)
-    # other BASELINE configs, same clock discipline, fewer steps (points runs only):
-    # configs[2] (ORB + LSD/LBD lines) under "secondary", configs[3] (stereo) under "stereo",
-    # configs[4] (1280x720 8-camera rig) under "rig"
+                       rank, world, device, dist)
+    res["nsteps"] = args.steps
+    # other BASELINE configs, same clock discipline, fewer steps (points runs only)
     others = {}
     if args.workload == "points" and args.secondary_steps > 0:
-        others["secondary"] = ("lines", run_workload(
-            pkg, synth, args, "lines", args.lines_streams, args.secondary_steps,
-            max(1, args.warmup // 2), rank, world, local_rank, dist), args.secondary_steps)
+        others["secondary"] = run_workload(pkg, synth, args, "lines", args.lines_streams,
+                                           args.secondary_steps, max(1, args.warmup // 2), rank,
+                                           world, device, dist)
+        others["secondary"]["nsteps"] = args.secondary_steps
     if args.workload == "points" and args.stereo_steps > 0:
-        others["stereo"] = ("kitti", run_workload(
-            pkg, synth, args, "kitti", args.stereo_streams, args.stereo_steps,
-            max(1, args.warmup // 2), rank, world, local_rank, dist), args.stereo_steps)
+        others["stereo"] = run_workload(pkg, synth, args, "kitti", args.stereo_streams,
+                                        args.stereo_steps, max(1, args.warmup // 2), rank, world,
+                                        device, dist)
+        others["stereo"]["nsteps"] = args.stereo_steps
     if args.workload == "points" and args.rig_steps > 0:
-        others["rig"] = ("rig", run_workload(
-            pkg, synth, args, "rig", args.rig_streams, args.rig_steps,
-            max(1, args.warmup // 2), rank, world, local_rank, dist), args.rig_steps)
+        others["rig"] = run_workload(pkg, synth, args, "rig", args.rig_streams, args.rig_steps,
+                                     max(1, args.warmup // 2), rank, world, device, dist)
+        others["rig"]["nsteps"] = args.rig_steps
+
+    # parity of every timed tracker's sampled streams against the oracle
+    for r in [res] + list(others.values()):
+        if args.no_parity:
+            r["parity"] = None
+            continue
+        r["parity"] = gather_parity(dist, world, parity_check(
+            [h[0] for h in r["hist"]], [h[1] for h in r["hist"]], r["samp"], r["gray"], r["depth"],
+            r["layout"], r["wname"]))
+
+    sweeps = None
+    if rank == 0 and world == 1 and args.sweep and args.workload == "points":
+        sweeps = {"points": sweep(pkg, synth, "points", (1, 16, 64, 256, 1024), 5, device),
+                  "lines": sweep(pkg, synth, "lines", (1, 16, 64, 256), 2, device)}
+
     cpu = None
+    host = host_info()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        thr = args.cpu_threads or min(16, os.cpu_count() or 1)
+        thr = args.cpu_threads or host["usable_cores"]
         fps, nfr, dt = cpu_baseline(args.cpu_seconds, thr, res["gray"], res["depth"],
                                     res["layout"], args.workload)
-        if res["T_acc"] is not None:
-            res["T_ref"] = accuracy_ref(res["gray"], res["depth"], res["layout"],
-                                        len(res["T_acc"]), args.workload)
-        for key, (wname, o, _) in others.items():
-            if o["T_acc"] is not None:
-                o["T_ref"] = accuracy_ref(o["gray"], o["depth"], o["layout"], len(o["T_acc"]), wname)
         cpu = {"value": round(fps, 2), "unit": "frames/s", "cores": thr, "kind": "port",
                "sample": f"{nfr} frames of the same {res['image']} loop in {dt:.1f} s, oracle/ "
-                         f"C++ restatement ({args.workload} workload), one stream per thread"}
+                         f"C++ restatement ({args.workload} workload), one stream per thread",
+               "build": f"oracle/_build ({oracle_build}: -O3 -march=x86-64-{oracle_build})"
+                        if oracle_build != "O2" else "oracle/_build (-O2)",
+               "host": host,
+               "reference_faithful": cpu_reference_faithful(args.cpu_seconds / 4, res["gray"],
+                                                            res["depth"], res["layout"],
+                                                            args.workload)}
 
     if rank == 0:
         S = res["S"]
@@ -496,32 +697,34 @@ def main():
             "data": res["data"],
             "config": {"workload": res["workload"],
                        "image": res["image"], "nfeatures": res["nfeatures"], "streams_per_gpu": S,
-                       "frames_per_step": S * world, "parallelism": f"streams sharded x{world}"},
+                       "frames_per_step": S * world, "parallelism": f"streams sharded x{world}",
+                       "pipelined": res["pipelined"]},
             "stage_ms": res["stages"],
             "tracking": res["tracking"],
             "roofline": res["roof"],
+            "parity": res["parity"],
             "cpu_baseline": cpu,
         }
-        if res["T_acc"] is not None:
-            out["accuracy"] = ate_report(res["T_acc"], res.get("T_ref"), res["layout"])
-        for key, (wname, o, nsteps) in others.items():
+        if sweeps:
+            out["sweep"] = sweeps
+        for key, o in others.items():
             out[key] = {
                 "workload": o["workload"], "value": round(o["value"], 2),
                 "unit": "frames/s", "image": o["image"], "nfeatures": o["nfeatures"],
-                "steps": nsteps, "streams_per_gpu": o["S"],
-                "ms_per_step": round(o["elapsed"] / nsteps * 1e3, 3),
+                "steps": o["nsteps"], "streams_per_gpu": o["S"],
+                "ms_per_step": round(o["elapsed"] / o["nsteps"] * 1e3, 3),
                 "stage_ms": o["stages"], "tracking": o["tracking"], "roofline": o["roof"],
-                "data": o["data"]}
-            if o["T_acc"] is not None:
-                out[key]["accuracy"] = ate_report(o["T_acc"], o.get("T_ref"), o["layout"])
+                "parity": o["parity"], "data": o["data"]}
             if cpu is not None:
                 thr = cpu["cores"]
                 fps, nfr, dt = cpu_baseline(args.cpu_seconds / 2, thr, o["gray"], o["depth"],
-                                            o["layout"], wname)
+                                            o["layout"], o["wname"])
                 out[key]["cpu_baseline"] = {
                     "value": round(fps, 2), "unit": "frames/s", "cores": thr, "kind": "port",
                     "sample": f"{nfr} frames in {dt:.1f} s, oracle/ C++ restatement "
-                              f"({wname} workload), one stream per thread"}
+                              f"({o['wname']} workload), one stream per thread",
+                    "reference_faithful": cpu_reference_faithful(
+                        args.cpu_seconds / 4, o["gray"], o["depth"], o["layout"], o["wname"])}
         print(json.dumps(out))
     if dist:
         dist.destroy_process_group()

@@ -316,8 +316,13 @@ int orbpl_tracker_create(const orbpl_orb_params* orb, const orbpl_camera* cam, i
  * Tracking.cc:180-208): Frame(imLeft, imRight) runs ORB on both images
  * concurrently (Frame.cc:88-91), UndistortKeyPoints, ComputeStereoMatches
  * (Frame.cc:886-1063) for depth / uRight; SearchByProjection uses th = 7
- * (Tracking.cc:1238-1241). The stereo Frame extracts no lines, so this flag
- * excludes ORBPL_TRACK_LINES. Images up to 1024 rows. */
+ * (Tracking.cc:1238-1241). Images up to 1024 rows.
+ * ORBPL_TRACK_STEREO | ORBPL_TRACK_LINES (BASELINE configs[3], a DEFINED mode:
+ * the reference's stereo Frame extracts no lines but PoseOptimizationWithLines
+ * loops over NL, Optimizer.cc:2287-2303): LineExtractor on both images, line
+ * end-point depths from the best LBD match on the right image whose line
+ * passes the angle / length / row-overlap / disparity tests,
+ * then the RGB-D line path (line matching, line edges, map lines). */
 #define ORBPL_TRACK_STEREO 2
 int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam, int n_streams,
                             int device, int flags, orbpl_tracker** out);
@@ -376,8 +381,26 @@ int orbpl_tracker_get_lines(orbpl_tracker* tr, int stream, orbpl_keyline* kl_un,
 /* Line stage device times (ms) of the last min(max_steps, 64) steps, 3 per
  * step: LSD, KeyLines + LBD + UndistortKeyLines, line SearchByProjection. */
 int orbpl_tracker_line_timings(orbpl_tracker* tr, int max_steps, float* ms, int* n_steps);
-/* Stereo stage device times (ms) of the last min(max_steps, 64) steps, 2 per
- * step: right-image ORB extraction, ComputeStereoMatches. */
+/* Per-step history of every stream, recorded on the device by D2D copies at
+ * the end of each step (no host synchronisation inside a step): the next
+ * max_steps steps after the call are kept (0 = off; a new call clears it).
+ * get_history returns stream `stream`'s first min(max_steps, recorded) steps:
+ * Tcw (16 floats per step) and 8 counts per step in the oracle's order:
+ * nkeypoints, nmatches, ninliers, nmatches_map, ok, nlines, line_matches,
+ * line_nmatches_map. */
+int orbpl_tracker_set_history(orbpl_tracker* tr, int max_steps);
+int orbpl_tracker_get_history(orbpl_tracker* tr, int stream, int max_steps, float* Tcw,
+                              int* counts8, int* n_steps);
+/* LSD / LineExtractor kernel times (ms) of the last min(max_steps, 64) steps,
+ * 7 per step (line stream): k_lsd_blur + k_lsd_resize + k_lsd_grad, the
+ * pseudo-ordering sort (k_lsd_sort + k_lsd_sort_local), the seed loop
+ * (k_lsd_spec), NFA validation + compaction, KeyLines (k_keylines), blur5 +
+ * Sobel + LBD, UndistortKeyLines + line depths. */
+int orbpl_tracker_lsd_timings(orbpl_tracker* tr, int max_steps, float* ms, int* n_steps);
+/* Stereo stage device times (ms) of the last min(max_steps, 64) steps, 4 per
+ * step: right-image ORB extraction, ComputeStereoMatches, and with
+ * ORBPL_TRACK_LINES the right-image LineExtractor and the stereo line depths
+ * (k_stereo_lines); 0 without lines. */
 int orbpl_tracker_stereo_timings(orbpl_tracker* tr, int max_steps, float* ms, int* n_steps);
 
 /* ------------------------------------------------------------------------

@@ -18,6 +18,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "../orb_slam2_modification_with-point-and-line-feature_amd/csrc/lsd_math.h"
@@ -315,6 +316,64 @@ int oracle_line_search_by_projection_list(const orbpl_camera* cam, const float* 
                                       nullptr, ml_xyz6, ml_desc, match, nmatches_out, wiped);
 }
 
+// Stereo line depths — a DEFINED mode: the reference's
+// stereo Frame extracts no lines (Frame.cc:70-131) yet PoseOptimizationWithLines
+// loops over NL (Optimizer.cc:2287-2303), so configs[3] "KITTI stereo
+// points+lines" needs a definition. LineExtractor runs on both rectified
+// images; left line i takes the right line j with the smallest LBD Hamming
+// distance (first j on ties) among those that pass, in this order:
+//   Hamming <= 45 (LineMatcher's TH), |angle_i - angle_j| <= 10 deg,
+//   min/max length >= 0.45, both lines non-horizontal (|dy| >= 0.25 length),
+//   row overlap >= 0.5 of the shorter row span, and both end-point
+//   disparities d = x_i - x_j(y_i) in (0, maxD), maxD = mbf / mb
+//   (ComputeStereoMatches' range, Frame.cc:897-899), where x_j(y) is the
+//   right line's x on row y (double arithmetic).
+// depth = mbf / (float)d for the start and end points (float division); no
+// match leaves -1. kl = left KeyLines (rectified: distorted == undistorted).
+int oracle_stereo_line_depths(const orbpl_camera* cam, const orbpl_keyline* kl,
+                              const uint8_t* desc, int nl, const orbpl_keyline* kr,
+                              const uint8_t* desc_r, int nr, float* dstart, float* dend) {
+  const double kPi = 3.14159265358979323846;
+  const float maxD = cam->bf / (cam->bf / cam->fx);
+  for (int i = 0; i < nl; i++) {
+    dstart[i] = -1.0f;
+    dend[i] = -1.0f;
+    const orbpl_keyline& a = kl[i];
+    const double ady = (double)a.endPointY - a.startPointY;
+    if (std::fabs(ady) < 0.25 * a.lineLength) continue;
+    const double ay0 = std::min(a.startPointY, a.endPointY), ay1 = std::max(a.startPointY, a.endPointY);
+    int best = 46;
+    float bs = -1.0f, be = -1.0f;
+    for (int j = 0; j < nr; j++) {
+      const orbpl_keyline& b = kr[j];
+      const int dist = popcnt_dist(desc + (size_t)i * 32, desc_r + (size_t)j * 32);
+      if (dist > 45 || dist >= best) continue;
+      if (std::fabs((double)a.angle - (double)b.angle) > 10.0 * kPi / 180.0) continue;
+      if (std::min(a.lineLength, b.lineLength) / std::max(a.lineLength, b.lineLength) < 0.45f)
+        continue;
+      const double bdy = (double)b.endPointY - b.startPointY;
+      if (std::fabs(bdy) < 0.25 * b.lineLength) continue;
+      const double by0 = std::min(b.startPointY, b.endPointY), by1 = std::max(b.startPointY, b.endPointY);
+      const double ov = std::min(ay1, by1) - std::max(ay0, by0);
+      if (ov < 0.5 * std::min(ay1 - ay0, by1 - by0)) continue;
+      const double slope = ((double)b.endPointX - b.startPointX) / bdy;
+      const double xs = b.startPointX + ((double)a.startPointY - b.startPointY) * slope;
+      const double xe = b.startPointX + ((double)a.endPointY - b.startPointY) * slope;
+      const float ds = (float)((double)a.startPointX - xs);
+      const float de = (float)((double)a.endPointX - xe);
+      if (!(ds > 0.0f && ds < maxD && de > 0.0f && de < maxD)) continue;
+      best = dist;
+      bs = cam->bf / ds;
+      be = cam->bf / de;
+    }
+    if (best <= 45) {
+      dstart[i] = bs;
+      dend[i] = be;
+    }
+  }
+  return 0;
+}
+
 // Frame::IsInFrustum(MapLine*) (Frame.cc:403-430): in view unless both end
 // points are behind the camera (Rcw X + tcw in float, P6).
 int oracle_line_is_in_frustum(const float* Tcw, int n, const float* xyz6, uint8_t* in_view) {
@@ -397,10 +456,15 @@ struct LStream {
   std::vector<float> lxyz;
 };
 
+// oracle_lvo_create_ex flags: the tracker's ORBPL_TRACK_* bits plus
+constexpr int kTwoThreads = 1 << 16;  // ORB || LineExtractor on two host threads per
+                                      // frame (Frame.cc:152-155), CPU baseline mode
+
 struct LVO {
   orbpl_orb_params orb;
   orbpl_camera cam;
   int use_lines;
+  int flags;
   std::vector<LStream> st;
   std::vector<float> scale, inv_sigma2;
 };
@@ -409,12 +473,13 @@ struct LVO {
 
 extern "C" {
 
-void* oracle_lvo_create(const orbpl_orb_params* orb, const orbpl_camera* cam, int n_streams,
-                        int use_lines) {
+void* oracle_lvo_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam, int n_streams,
+                           int flags) {
   LVO* v = new LVO();
   v->orb = *orb;
   v->cam = *cam;
-  v->use_lines = use_lines;
+  v->flags = flags;
+  v->use_lines = (flags & ORBPL_TRACK_LINES) ? 1 : 0;
   v->st.resize(n_streams);
   v->scale.resize(orb->nlevels);
   std::vector<float> isc(orb->nlevels);
@@ -425,12 +490,17 @@ void* oracle_lvo_create(const orbpl_orb_params* orb, const orbpl_camera* cam, in
   return v;
 }
 
+void* oracle_lvo_create(const orbpl_orb_params* orb, const orbpl_camera* cam, int n_streams,
+                        int use_lines) {
+  return oracle_lvo_create_ex(orb, cam, n_streams, use_lines ? ORBPL_TRACK_LINES : 0);
+}
+
 void oracle_lvo_destroy(void* h) { delete static_cast<LVO*>(h); }
 
 int oracle_lvo_reset(void* h, const float* Tcw0) {
   LVO* v = static_cast<LVO*>(h);
   for (size_t s = 0; s < v->st.size(); s++) {
-    LStream z;
+    LStream z{};
     for (int k = 0; k < 16; k++) z.Tcw[k] = Tcw0 ? Tcw0[s * 16 + k] : ((k % 5 == 0) ? 1.f : 0.f);
     v->st[s] = z;
   }
@@ -451,12 +521,50 @@ static int lvo_step(LVO* v, int stream, const uint8_t* gray, const float* depth,
   LStream& S = v->st[stream];
   const orbpl_camera& cam = v->cam;
   const int cap = v->orb.nfeatures * 2 + 64;
+  // lines: LineExtractor + UndistortKeyLines + line depths (Frame.cc:152-166);
+  // with kTwoThreads on a second host thread concurrently with ORB, as the
+  // reference's Frame(RGB-D) runs them (Frame.cc:152-155)
+  int nl = 0, lrc = 0;
+  std::vector<orbpl_keyline> kl(80), klu;
+  std::vector<uint8_t> ldesc(80 * 32);
+  std::vector<float> lds, lde, lurs, lure;
+  auto extract_lines = [&]() {
+    std::vector<double> coef(80 * 3);
+    int nd = 0;
+    lrc = oracle_line_extract(gray, cam.width, cam.height, kl.data(), ldesc.data(), coef.data(), 80,
+                              &nl, &nd);
+    if (lrc) return;
+    kl.resize(nl);
+    ldesc.resize((size_t)nl * 32);
+    klu.resize(nl);
+    lds.resize(nl); lde.resize(nl); lurs.resize(nl); lure.resize(nl);
+    oracle_line_frame_prepare(&cam, kl.data(), nl, right ? nullptr : depth, klu.data(),
+                              lds.data(), lde.data(), lurs.data(), lure.data());
+    if (right) {
+      // stereo: LineExtractor on the right image, end-point depths by the
+      // defined stereo line matching (P17)
+      std::vector<orbpl_keyline> klr(80);
+      std::vector<uint8_t> ldr(80 * 32);
+      int nr = 0, ndr = 0;
+      lrc = oracle_line_extract(right, cam.width, cam.height, klr.data(), ldr.data(), coef.data(),
+                                80, &nr, &ndr);
+      if (lrc) return;
+      oracle_stereo_line_depths(&cam, klu.data(), ldesc.data(), nl, klr.data(), ldr.data(), nr,
+                                lds.data(), lde.data());
+    }
+  };
+  const bool do_lines = v->use_lines != 0;
+  std::thread lthread;
+  if (do_lines && (v->flags & kTwoThreads)) lthread = std::thread(extract_lines);
   std::vector<orbpl_keypoint> kps(cap);
   std::vector<uint8_t> desc((size_t)cap * 32);
   int n = 0;
   int rc = oracle_orb_extract(&v->orb, gray, cam.width, cam.height, cam.width, kps.data(),
                               desc.data(), cap, &n, nullptr);
+  if (lthread.joinable()) lthread.join();
+  else if (do_lines) extract_lines();
   if (rc) return rc;
+  if (lrc) return lrc;
   kps.resize(n);
   desc.resize((size_t)n * 32);
   std::vector<orbpl_keypoint> ku(n);
@@ -486,24 +594,6 @@ static int lvo_step(LVO* v, int stream, const uint8_t* gray, const float* depth,
                           ur.data(), dep.data());
   }
   const float th = right ? 7.0f : 15.0f;
-  // lines
-  int nl = 0;
-  std::vector<orbpl_keyline> kl(80), klu;
-  std::vector<uint8_t> ldesc(80 * 32);
-  std::vector<float> lds, lde, lurs, lure;
-  if (v->use_lines && !right) {
-    std::vector<double> coef(80 * 3);
-    int nd = 0;
-    rc = oracle_line_extract(gray, cam.width, cam.height, kl.data(), ldesc.data(), coef.data(), 80,
-                             &nl, &nd);
-    if (rc) return rc;
-    kl.resize(nl);
-    ldesc.resize((size_t)nl * 32);
-    klu.resize(nl);
-    lds.resize(nl); lde.resize(nl); lurs.resize(nl); lure.resize(nl);
-    oracle_line_frame_prepare(&cam, kl.data(), nl, depth, klu.data(), lds.data(), lde.data(),
-                              lurs.data(), lure.data());
-  }
   std::vector<int32_t> match(n, -1), lmatch(nl, -1);
   std::vector<uint8_t> outl(n, 0), loutl(nl, 0);
   int nmatches = 0, ninl = 0, nmap = 0, nlm = 0, lnmap = 0;
@@ -522,7 +612,7 @@ static int lvo_step(LVO* v, int stream, const uint8_t* gray, const float* depth,
                           S.outlier.data(), S.xyz.data(), S.desc.data(), S.nobs.data()};
     oracle_search_by_projection_last(&cam, v->scale.data(), (int)v->scale.size(), &cur, &last, th,
                                      0, 1, match.data(), &nmatches);
-    if (v->use_lines && !right)
+    if (v->use_lines)
       oracle_line_search_by_projection_last(&cam, S.Tcw, nl, klu.data(), ldesc.data(),
                                             (int)S.kl_un.size(), S.kl_un.data(), S.has_ml.data(),
                                             S.loutlier.data(), S.lxyz.data(), S.ldesc.data(),
@@ -532,7 +622,7 @@ static int lvo_step(LVO* v, int stream, const uint8_t* gray, const float* depth,
       oracle_search_by_projection_last(&cam, v->scale.data(), (int)v->scale.size(), &cur, &last,
                                        2.0f * th, 0, 1, match.data(), &nmatches);
     }
-    tracked = nmatches >= 20 && (!v->use_lines || right || nlm >= 15);
+    tracked = nmatches >= 20 && (!v->use_lines || nlm >= 15);
     if (tracked) {
       std::vector<uint8_t> has(n, 0), hasl(nl, 0);
       std::vector<float> xyz((size_t)n * 3, 0.f), lobs((size_t)nl * 4, 0.f), lxyz((size_t)nl * 6, 0.f);
@@ -614,7 +704,7 @@ static int lvo_step(LVO* v, int stream, const uint8_t* gray, const float* depth,
     }
   bool ok = true;
   if (S.has_last)
-    ok = tracked && (v->use_lines && !right ? (nmap >= 10 || lnmap >= 15) : nmap >= 10);
+    ok = tracked && (v->use_lines ? (nmap >= 10 || lnmap >= 15) : nmap >= 10);
   memcpy(S.Tlast2, S.Tlast, 64);
   memcpy(S.Tlast, S.Tcw, 64);
   S.has_velocity = S.has_last;

@@ -15,6 +15,41 @@ import numpy as np
 
 HERE = Path(__file__).resolve().parent
 LIB_PATH = HERE / "_build" / "liborbpl_oracle.so"
+# -O3 -march builds of the same sources (oracle/Makefile) for the CPU baseline
+VARIANTS = {"O2": "liborbpl_oracle.so", "v3": "liborbpl_oracle_v3.so",
+            "v4": "liborbpl_oracle_v4.so"}
+
+
+def host_isa_level():
+    """Highest x86-64 micro-architecture level this host runs ("v4": AVX-512
+    F/BW/CD/DQ/VL, "v3": AVX2/FMA/BMI2, else "O2"), from /proc/cpuinfo."""
+    try:
+        flags = set()
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("flags"):
+                flags = set(line.split(":", 1)[1].split())
+                break
+    except OSError:
+        return "O2"
+    v3 = {"avx2", "fma", "bmi1", "bmi2", "movbe", "f16c", "lzcnt" if "lzcnt" in flags else "abm"}
+    v4 = {"avx512f", "avx512bw", "avx512cd", "avx512dq", "avx512vl"}
+    if v3 <= flags and v4 <= flags:
+        return "v4"
+    if v3 <= flags:
+        return "v3"
+    return "O2"
+
+
+def use_variant(name):
+    """Select the oracle build before the first call ("O2", "v3", "v4" or
+    "best" = the highest level the host runs). Returns the variant used."""
+    global LIB_PATH
+    if _lib is not None:
+        raise RuntimeError("oracle library already loaded")
+    if name == "best":
+        name = host_isa_level()
+    LIB_PATH = HERE / "_build" / VARIANTS[name]
+    return name
 
 
 class OrbParams(C.Structure):
@@ -42,6 +77,8 @@ def lib():
     if _lib is None:
         if not LIB_PATH.exists():
             build()
+        if not LIB_PATH.exists():
+            raise FileNotFoundError(LIB_PATH)
         _lib = C.CDLL(str(LIB_PATH))
         _setup(_lib)
     return _lib
@@ -447,8 +484,11 @@ def _setup(L):  # noqa: F811
     L.oracle_line_search_by_projection_list.argtypes = [vp, vp, i, vp, vp, vp, i, vp, vp, vp, vp,
                                                         ip, ip]
     L.oracle_line_is_in_frustum.argtypes = [vp, i, vp, vp]
+    L.oracle_stereo_line_depths.argtypes = [vp, vp, vp, i, vp, vp, i, vp, vp]
     L.oracle_lvo_create.argtypes = [vp, vp, i, i]
     L.oracle_lvo_create.restype = vp
+    L.oracle_lvo_create_ex.argtypes = [vp, vp, i, i]
+    L.oracle_lvo_create_ex.restype = vp
     L.oracle_lvo_destroy.argtypes = [vp]
     L.oracle_lvo_reset.argtypes = [vp, vp]
     L.oracle_lvo_step.argtypes = [vp, i, vp, vp, vp, vp]
@@ -504,12 +544,31 @@ def line_search_by_projection_last(cam, Tcw, cur_kl_un, cur_desc, last_kl_un, ha
     return match[:ncur].copy(), nm.value
 
 
-class LVO:
-    """CPU oracle of the points (+ lines) tracker, one stream at a time."""
+TRACK_LINES, TRACK_STEREO, TRACK_LOCAL_MAP, TRACK_FIXED_LINE_JAC = 1, 2, 4, 8
+TWO_THREADS = 1 << 16
 
-    def __init__(self, orb_params, cam, n_streams, use_lines=True):
-        self.h = lib().oracle_lvo_create(C.byref(orb_params), C.byref(cam), n_streams,
-                                         int(use_lines))
+
+def stereo_line_depths(cam, kl, desc, kr, desc_r):
+    """P17 stereo line end-point depths (dstart, dend) of the left lines."""
+    kl = np.ascontiguousarray(kl)
+    kr = np.ascontiguousarray(kr)
+    d = _c(desc, np.uint8)
+    dr = _c(desc_r, np.uint8)
+    ds = np.zeros(max(1, len(kl)), np.float32)
+    de = np.zeros(max(1, len(kl)), np.float32)
+    lib().oracle_stereo_line_depths(C.byref(cam), _p(kl), _p(d), len(kl), _p(kr), _p(dr), len(kr),
+                                    _p(ds), _p(de))
+    return ds[:len(kl)], de[:len(kl)]
+
+
+class LVO:
+    """CPU oracle of the points (+ lines) tracker, one stream at a time.
+    flags: extra ORBPL_TRACK_* bits (TRACK_LOCAL_MAP, ...) and TWO_THREADS
+    (ORB || LineExtractor on two host threads per frame, Frame.cc:152-155)."""
+
+    def __init__(self, orb_params, cam, n_streams, use_lines=True, flags=0):
+        f = (TRACK_LINES if use_lines else 0) | flags
+        self.h = lib().oracle_lvo_create_ex(C.byref(orb_params), C.byref(cam), n_streams, f)
 
     def reset(self, Tcw0=None):
         T = None if Tcw0 is None else _c(Tcw0, np.float32)
@@ -527,7 +586,8 @@ class LVO:
         return T.reshape(4, 4), dict(zip(keys, (int(x) for x in o)))
 
     def step_stereo(self, stream, left, right):
-        """Stereo Frame + TrackWithMotionModel (points only, th = 7)."""
+        """Stereo Frame + TrackWithMotionModel (th = 7); with lines the defined
+        stereo line mode (LineExtractor on both images, P17 line depths)."""
         gl = _c(left, np.uint8)
         gr = _c(right, np.uint8)
         T = np.zeros(16, np.float32)

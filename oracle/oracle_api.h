@@ -77,9 +77,15 @@ int oracle_line_search_by_projection_list(const orbpl_camera* cam, const float* 
                                           const int32_t* cur_nobs, int nml, const uint8_t* valid,
                                           const float* ml_xyz6, const uint8_t* ml_desc,
                                           int32_t* match, int* nmatches_out, int* wiped);
+int oracle_stereo_line_depths(const orbpl_camera* cam, const orbpl_keyline* kl,
+                              const uint8_t* desc, int nl, const orbpl_keyline* kr,
+                              const uint8_t* desc_r, int nr, float* dstart, float* dend);
 int oracle_line_is_in_frustum(const float* Tcw, int n, const float* xyz6, uint8_t* in_view);
 void* oracle_lvo_create(const orbpl_orb_params* orb, const orbpl_camera* cam, int n_streams,
                         int use_lines);
+/* flags: ORBPL_TRACK_* bits (orbpl.h) | 1 << 16 (ORB || lines on two host threads) */
+void* oracle_lvo_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam, int n_streams,
+                           int flags);
 void oracle_lvo_destroy(void* h);
 int oracle_lvo_reset(void* h, const float* Tcw0);
 int oracle_lvo_step(void* h, int stream, const uint8_t* gray, const float* depth, float* Tcw_out,

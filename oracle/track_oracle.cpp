@@ -825,7 +825,7 @@ void oracle_vo_destroy(void* h) { delete static_cast<VO*>(h); }
 int oracle_vo_reset(void* h, const float* Tcw0) {
   VO* v = static_cast<VO*>(h);
   for (size_t s = 0; s < v->st.size(); s++) {
-    VOStream z;
+    VOStream z{};
     for (int k = 0; k < 16; k++) z.Tcw[k] = Tcw0 ? Tcw0[s * 16 + k] : ((k % 5 == 0) ? 1.f : 0.f);
     v->st[s] = z;
   }

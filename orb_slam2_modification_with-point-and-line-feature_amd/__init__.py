@@ -245,16 +245,6 @@ class ORBextractor:
     def synchronize(self):
         check(lib().orbx_synchronize(self._h), "orbx_synchronize")
 
-    STEREO_STAGES = ("right_extract", "stereo_match")
-
-    def stereo_timings(self, max_steps=64):
-        """(n_steps, 2) stereo-stage ms of the last steps (hipEvents in-stream)."""
-        ms = np.zeros((max_steps, 2), np.float32)
-        n = C.c_int(0)
-        check(lib().orbpl_tracker_stereo_timings(self._h, max_steps, _ptr(ms), C.byref(n)),
-              "orbpl_tracker_stereo_timings")
-        return ms[:n.value]
-
     def stage_ms(self):
         ms = np.zeros(5, np.float32)
         check(lib().orbx_last_stage_ms(self._h, _ptr(ms)), "orbx_last_stage_ms")
@@ -366,6 +356,9 @@ def _declare_track(L):
     L.orbpl_tracker_line_timings.argtypes = [vp, i, vp, ip]
     L.orbpl_tracker_step_stereo.argtypes = [vp, vp, vp]
     L.orbpl_tracker_stereo_timings.argtypes = [vp, i, vp, ip]
+    L.orbpl_tracker_lsd_timings.argtypes = [vp, i, vp, ip]
+    L.orbpl_tracker_set_history.argtypes = [vp, i]
+    L.orbpl_tracker_get_history.argtypes = [vp, i, i, vp, vp, ip]
 
 
 _declare_orig = _declare
@@ -611,7 +604,8 @@ class Tracker:
     """Batched RGB-D / stereo tracker (orbpl_tracker_*): one
     TrackWithMotionModel step for n_streams independent streams per call.
     lines=True selects the point-and-line variant (ORBPL_TRACK_LINES),
-    stereo=True the stereo Frame (ORBPL_TRACK_STEREO, points only)."""
+    stereo=True the stereo Frame (ORBPL_TRACK_STEREO); both = the defined
+    stereo points+lines mode."""
 
     TRACK_LINES = 1
     TRACK_STEREO = 2
@@ -696,11 +690,43 @@ class Tracker:
               "orbpl_tracker_line_timings")
         return ms[:n.value]
 
-    STEREO_STAGES = ("right_extract", "stereo_match")
+    LSD_STAGES = ("lsd_prep", "lsd_sort", "lsd_seed", "lsd_validate", "keylines", "lbd",
+                  "line_prepare")
+    # the kernels each LSD stage event pair brackets
+    LSD_KERNELS = {"lsd_prep": "k_lsd_blur+k_lsd_resize+k_lsd_grad",
+                   "lsd_sort": "k_lsd_sort+k_lsd_sort_local", "lsd_seed": "k_lsd_spec",
+                   "lsd_validate": "k_lsd_validate+k_lsd_compact", "keylines": "k_keylines",
+                   "lbd": "k_lsd_blur+k_sobel+k_lbd", "line_prepare": "k_line_prepare"}
+
+    def lsd_timings(self, max_steps=64):
+        """(n_steps, 7) LSD / LineExtractor kernel ms of the last steps."""
+        ms = np.zeros((max_steps, 7), np.float32)
+        n = C.c_int(0)
+        check(lib().orbpl_tracker_lsd_timings(self._h, max_steps, _ptr(ms), C.byref(n)),
+              "orbpl_tracker_lsd_timings")
+        return ms[:n.value]
+
+    def set_history(self, max_steps):
+        """Record every stream's pose and counts for the next max_steps steps."""
+        check(lib().orbpl_tracker_set_history(self._h, int(max_steps)), "orbpl_tracker_set_history")
+
+    def history(self, stream, max_steps=4096):
+        """(Tcw (n,4,4), counts (n,8)) of one stream's recorded steps; counts in
+        the oracle's out8 order (nkeypoints, nmatches, ninliers, nmatches_map,
+        ok, nlines, line_matches, line_nmatches_map)."""
+        T = np.zeros((max_steps, 4, 4), np.float32)
+        cnt = np.zeros((max_steps, 8), np.int32)
+        n = C.c_int(0)
+        check(lib().orbpl_tracker_get_history(self._h, stream, max_steps, _ptr(T), _ptr(cnt),
+                                              C.byref(n)), "orbpl_tracker_get_history")
+        return T[:n.value], cnt[:n.value]
+
+    STEREO_STAGES = ("right_extract", "stereo_match", "right_lines", "stereo_lines")
 
     def stereo_timings(self, max_steps=64):
-        """(n_steps, 2) stereo-stage ms of the last steps (hipEvents in-stream)."""
-        ms = np.zeros((max_steps, 2), np.float32)
+        """(n_steps, 4) stereo-stage ms of the last steps (hipEvents in-stream);
+        the line stages are 0 without lines."""
+        ms = np.zeros((max_steps, 4), np.float32)
         n = C.c_int(0)
         check(lib().orbpl_tracker_stereo_timings(self._h, max_steps, _ptr(ms), C.byref(n)),
               "orbpl_tracker_stereo_timings")

@@ -347,6 +347,65 @@ void launch_line_match(const TrackConsts& c, const LineTrackArgs& a, StreamState
   hipLaunchKernelGGL(k_line_match, dim3(nstreams), dim3(256), 0, s, c, a, st);
 }
 
+// Stereo line depths (the defined mode P17, oracle_stereo_line_depths): one
+// 128-thread block per stereo pair, the right KeyLines and LBD rows in LDS,
+// thread i scans the right lines for left line i in index order with the
+// same double / float operation sequence as the oracle.
+__global__ void __launch_bounds__(128) k_stereo_lines(TrackConsts c, StereoLineArgs a) {
+  __shared__ orbpl_keyline s_kr[kLineKeep];
+  __shared__ uint4 s_dr[kLineKeep * 2];
+  const int s = blockIdx.x, t = threadIdx.x;
+  const long long lb = (long long)s * kLineKeep;
+  const int nl = a.nl[s], nr = min(a.nr[s], kLineKeep);
+  for (int j = t; j < nr; j += 128) s_kr[j] = a.kr[lb + j];
+  for (int j = t; j < nr * 2; j += 128)
+    s_dr[j] = reinterpret_cast<const uint4*>(a.desc_r + lb * 32)[j];
+  __syncthreads();
+  if (t >= nl) return;
+  const double kPi = 3.14159265358979323846;
+  const float maxD = c.bf / c.mb;
+  const orbpl_keyline ka = a.kl[lb + t];
+  const uint4* da = reinterpret_cast<const uint4*>(a.desc + (lb + t) * 32);
+  const uint4 a0 = da[0], a1 = da[1];
+  float bs = -1.0f, be = -1.0f;
+  const double ady = (double)ka.endPointY - ka.startPointY;
+  if (fabs(ady) >= 0.25 * ka.lineLength) {
+    const double ay0 = smin(ka.startPointY, ka.endPointY), ay1 = smax(ka.startPointY, ka.endPointY);
+    int best = 46;
+    for (int j = 0; j < nr; j++) {
+      const uint4 b0 = s_dr[2 * j], b1 = s_dr[2 * j + 1];
+      const int dist = __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) +
+                       __popc(a0.w ^ b0.w) + __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) +
+                       __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+      if (dist > 45 || dist >= best) continue;
+      const orbpl_keyline& kb = s_kr[j];
+      if (fabs((double)ka.angle - (double)kb.angle) > 10.0 * kPi / 180.0) continue;
+      if (smin(ka.lineLength, kb.lineLength) / smax(ka.lineLength, kb.lineLength) < 0.45f) continue;
+      const double bdy = (double)kb.endPointY - kb.startPointY;
+      if (fabs(bdy) < 0.25 * kb.lineLength) continue;
+      const double by0 = smin(kb.startPointY, kb.endPointY), by1 = smax(kb.startPointY, kb.endPointY);
+      const double ov = smin(ay1, by1) - smax(ay0, by0);
+      if (ov < 0.5 * smin(ay1 - ay0, by1 - by0)) continue;
+      const double slope = ((double)kb.endPointX - kb.startPointX) / bdy;
+      const double xs = kb.startPointX + ((double)ka.startPointY - kb.startPointY) * slope;
+      const double xe = kb.startPointX + ((double)ka.endPointY - kb.startPointY) * slope;
+      const float ds = (float)((double)ka.startPointX - xs);
+      const float de = (float)((double)ka.endPointX - xe);
+      if (!(ds > 0.0f && ds < maxD && de > 0.0f && de < maxD)) continue;
+      best = dist;
+      bs = c.bf / ds;
+      be = c.bf / de;
+    }
+  }
+  a.dstart[lb + t] = bs;
+  a.dend[lb + t] = be;
+}
+
+void launch_stereo_lines(const TrackConsts& c, const StereoLineArgs& a, int nstreams,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(k_stereo_lines, dim3(nstreams), dim3(128), 0, s, c, a);
+}
+
 
 // LineMatcher::SearchByProjection(Frame&, const vector<MapLine*>&) and
 // (Frame&, KeyFrame*) (LineMatcher.cpp:755-952, 527-721): any number of map

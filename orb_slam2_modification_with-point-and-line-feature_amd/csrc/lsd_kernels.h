@@ -112,7 +112,8 @@ void launch_lsd_validate(const LsdGeom& g, const LsdScratch& sc, int batch, hipS
 // Host runtime (lsd_runtime.cpp): LSD (+ LineExtractor when `out` is set) of
 // `batch` frames on stream `s`; lsdx_check reads the device capacity flags.
 int lsdx_run(lsdx_ctx* c, const uint8_t* d_imgs, int batch, int stride, int64_t frame_pitch,
-             const LineOut* out, hipStream_t s, hipEvent_t ev_mid);
+             const LineOut* out, hipStream_t s, hipEvent_t ev_mid,
+             const hipEvent_t* ev_stage = nullptr);
 int lsdx_check(lsdx_ctx* c, int batch);
 
 }  // namespace orbpl

@@ -78,8 +78,9 @@ LSDM_HD double exp_(double x) {
   c = x - t * (P1 + t * (P2 + t * (P3 + t * (P4 + t * P5))));
   if (k == 0) return 1.0 - ((x * c) / (c - 2.0) - x);
   y = 1.0 - ((lo - (x * c) / (2.0 - c)) - hi);
-  if (k >= -1021) return with_hi(y, hi_word(y) + (k << 20));
-  return with_hi(y, hi_word(y) + ((k + 1000) << 20)) * twom1000;
+  // exponent adjust without shifting a negative int (UB before C++20)
+  if (k >= -1021) return with_hi(y, (int32_t)((uint32_t)hi_word(y) + ((uint32_t)k << 20)));
+  return with_hi(y, (int32_t)((uint32_t)hi_word(y) + ((uint32_t)(k + 1000) << 20))) * twom1000;
 }
 
 // ---- log (fdlibm e_log.c), x > 0 finite ----
@@ -339,7 +340,7 @@ LSDM_HD double atan2_(double y, double x) {
   const int32_t ix = hx & 0x7fffffff, iy = hy & 0x7fffffff;
   if ((ix | ((lx | (0u - lx)) >> 31)) > 0x7ff00000 || (iy | ((ly | (0u - ly)) >> 31)) > 0x7ff00000)
     return x + y;  // NaN
-  if (((hx - 0x3ff00000) | lx) == 0) return atan_(y);  // x == 1
+  if ((((uint32_t)hx - 0x3ff00000u) | lx) == 0) return atan_(y);  // x == 1 (no signed wrap)
   const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
   if ((iy | ly) == 0) {  // y == 0
     switch (m) {

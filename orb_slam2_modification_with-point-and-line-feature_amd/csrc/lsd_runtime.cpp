@@ -132,24 +132,31 @@ namespace orbpl {
 // The tracker calls this with its own per-frame output buffers and stream;
 // `ev_mid` (optional) is recorded between LSD and the LineExtractor stages.
 int lsdx_run(lsdx_ctx* c, const uint8_t* d_imgs, int batch, int stride, int64_t frame_pitch,
-             const LineOut* out, hipStream_t s, hipEvent_t ev_mid) {
+             const LineOut* out, hipStream_t s, hipEvent_t ev_mid, const hipEvent_t* ev_stage) {
+  // ev_stage (optional, 5 events): after blur/resize/grad, after the
+  // pseudo-ordering sort, after the seed loop, after KeyLines, after LBD
   const LsdGeom& g = c->g;
   HIP_CHECK(hipMemsetAsync(c->sc.maxq, 0, (size_t)batch * 4, s));
   HIP_CHECK(hipMemsetAsync(c->sc.err, 0, (size_t)batch * 4, s));
   launch_lsd_blur(g, d_imgs, stride, frame_pitch, c->sc.blur, batch, s);
   launch_lsd_resize(g, c->d_tabs, c->sc.blur, c->sc.scaled, batch, s);
   launch_lsd_grad(g, c->sc.scaled, c->sc.deg, c->sc.q, c->sc.pix, c->sc.maxq, batch, s);
+  if (ev_stage) HIP_CHECK(hipEventRecord(ev_stage[0], s));
   launch_lsd_sort(g, c->sc, batch, s);
+  if (ev_stage) HIP_CHECK(hipEventRecord(ev_stage[1], s));
   launch_lsd_grow(g, c->sc, batch, s, c->serial_grow);
+  if (ev_stage) HIP_CHECK(hipEventRecord(ev_stage[2], s));
   launch_lsd_validate(g, c->sc, batch, s);
   if (ev_mid) HIP_CHECK(hipEventRecord(ev_mid, s));
   if (out) {
     LineOut o = *out;
     o.kl_all = c->lo.kl_all;  // per-frame scratch of the full detection
     launch_keylines(c->g, c->sc, o, batch, s);
+    if (ev_stage) HIP_CHECK(hipEventRecord(ev_stage[3], s));
     launch_lsd_blur(c->g5, d_imgs, stride, frame_pitch, c->blur5, batch, s);
     launch_sobel(c->W, c->H, c->blur5, c->sdx, c->sdy, batch, s);
     launch_lbd(c->W, c->H, c->sdx, c->sdy, c->lw, o, batch, s);
+    if (ev_stage) HIP_CHECK(hipEventRecord(ev_stage[4], s));
   }
   HIP_CHECK(hipGetLastError());
   return ORBPL_OK;

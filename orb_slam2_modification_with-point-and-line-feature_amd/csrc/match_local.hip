@@ -20,6 +20,7 @@
 #include "lsd_math.h"
 #include "track_common.h"
 #include "track_kernels.h"
+#include "orbpl_runtime.h"
 
 namespace orbpl {
 
@@ -295,12 +296,7 @@ void launch_in_frustum(const TrackConsts& c, float log_scale, const InFrustumArg
 }
 
 void launch_match_local(const TrackConsts& c, const LocalArgs& a, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_match_local,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, sizeof(LocalShared));
-    attr = true;
-  }
+  set_smem_attr((const void*)k_match_local, sizeof(LocalShared));
   hipLaunchKernelGGL(k_match_local, dim3(1), dim3(256), sizeof(LocalShared), s, c, a);
 }
 

@@ -20,6 +20,7 @@
 #include "orb_geom.h"
 #include "orbpl_math.h"
 #include "orb_kernels.h"
+#include "orbpl_runtime.h"
 
 namespace orbpl {
 
@@ -1365,21 +1366,13 @@ void launch_fast(const OrbGeom& hg, const OrbGeom* dg, const CellGeom* cells, co
 void launch_octree(const OrbGeom& hg, const OrbGeom* dg, const uint32_t* cell_cands,
                    const int* cell_counts, uint32_t* kcand, int* knode, uint32_t* kp_list,
                    int* kp_count, int* err_flag, int batch, hipStream_t s) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)k_octree<1024>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)sizeof(OctShared<1024>));
-    attr_set = true;
-  }
+  set_smem_attr((const void*)k_octree<1024>, sizeof(OctShared<1024>));
   int cap = 0;
   for (int l = 0; l < hg.nlevels; l++) cap = std::max(cap, hg.lv[l].kp_cap);
-  static bool prof_set = false;
-  if (!prof_set) {
+  if (once_per_device((const void*)&g_oct_prof_on)) {
     const int on = getenv("ORBPL_OCT_PROFILE") ? 1 : 0;
     (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_oct_prof_on), &on, sizeof(int), 0,
                                  hipMemcpyHostToDevice, s);
-    prof_set = true;
   }
   if (cap <= 256)
     hipLaunchKernelGGL(k_octree<256>, dim3(hg.nlevels, batch), dim3(256),

@@ -6,7 +6,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <set>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/orbpl.h"
@@ -33,6 +36,20 @@ int hip_fail(hipError_t e, const char* what, int line) {
 int arg_fail(const char* msg) {
   g_last_error = msg;
   return ORBPL_ERR_ARG;
+}
+
+bool once_per_device(const void* key) {
+  static std::mutex mu;
+  static std::set<std::pair<const void*, int>> seen;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(mu);
+  return seen.insert({key, dev}).second;
+}
+
+void set_smem_attr(const void* fn, size_t bytes) {
+  if (once_per_device(fn))
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
 }  // namespace orbpl

@@ -9,6 +9,12 @@ struct orbx_ctx;
 namespace orbpl {
 int hip_fail(hipError_t e, const char* what, int line);
 int arg_fail(const char* msg);
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device):
+// HIP function attributes are per device, so a process-wide flag would skip
+// the second device. Thread-safe; the current device is hipGetDevice's.
+void set_smem_attr(const void* fn, size_t bytes);
+// Run `init` once per (key, device) (thread-safe); returns true the first time.
+bool once_per_device(const void* key);
 int orbx_run(orbx_ctx* c, const uint8_t* d_imgs, int batch, int stride, long long frame_pitch,
              orbpl_keypoint_dev* d_kps, uint8_t* d_desc, int kp_pitch, int* d_n,
              hipEvent_t* ext_events = nullptr);

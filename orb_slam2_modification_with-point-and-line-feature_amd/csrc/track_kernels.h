@@ -94,6 +94,21 @@ struct LineTrackArgs {
   const uint8_t* last_desc;
 };
 
+// Stereo line depths (P17): left lines kl (the tracker's kl_un; rectified)
+// and right KeyLines kr of the same pair, kLineKeep per stream.
+struct StereoLineArgs {
+  const int* nl;
+  const orbpl_keyline* kl;
+  const uint8_t* desc;
+  const int* nr;
+  const orbpl_keyline* kr;
+  const uint8_t* desc_r;
+  float* dstart;
+  float* dend;
+};
+void launch_stereo_lines(const TrackConsts& c, const StereoLineArgs& a, int nstreams,
+                         hipStream_t s);
+
 // LineMatcher local-map / reference-keyframe overloads (any number of map lines).
 struct LineListArgs {
   const float* Tcw;              // 16 floats

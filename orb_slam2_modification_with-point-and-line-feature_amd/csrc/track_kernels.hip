@@ -24,6 +24,7 @@
 #include "track_common.h"
 #include "track_kernels.h"
 #include "lsd_kernels.h"
+#include "orbpl_runtime.h"
 
 namespace orbpl {
 
@@ -1458,12 +1459,6 @@ __global__ void __launch_bounds__(256) k_finish(TrackConsts c, StreamState* __re
 size_t match_smem_bytes() { return sizeof(MatchShared<2048>); }
 size_t pose_smem_bytes() { return sizeof(PoseShared); }
 
-static void set_smem_attr_once(const void* fn, size_t bytes, bool* done) {
-  if (!*done) {
-    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-    *done = true;
-  }
-}
 
 void launch_frame_prepare(const TrackConsts& c, const KeyPointD* kps, const int* n, int kp_pitch,
                           const float* depth, long long depth_pitch, KeyPointD* kps_un,
@@ -1477,9 +1472,8 @@ void launch_predict(StreamState* st, int nstreams, hipStream_t s) {
 }
 
 void launch_match_last(const TrackConsts& c, const MatchLaunch& m, int nstreams, hipStream_t s) {
-  static bool done1 = false, done2 = false;
-  set_smem_attr_once((const void*)k_match_last<1024>, sizeof(MatchShared<1024>), &done1);
-  set_smem_attr_once((const void*)k_match_last<2048>, sizeof(MatchShared<2048>), &done2);
+  set_smem_attr((const void*)k_match_last<1024>, sizeof(MatchShared<1024>));
+  set_smem_attr((const void*)k_match_last<2048>, sizeof(MatchShared<2048>));
   MatchArgs a;
   a.cur_kps_un = m.cur_kps_un;
   a.cur_desc = m.cur_desc;
@@ -1524,8 +1518,7 @@ int read_pose_profile(long long* out8) {
 }
 
 void launch_pose(const TrackConsts& c, const PoseLaunch& p, int nstreams, hipStream_t s) {
-  static bool done = false;
-  set_smem_attr_once((const void*)k_pose, sizeof(PoseShared), &done);
+  set_smem_attr((const void*)k_pose, sizeof(PoseShared));
   PoseArgs a;
   a.kps_un = p.kps_un;
   a.uright = p.uright;

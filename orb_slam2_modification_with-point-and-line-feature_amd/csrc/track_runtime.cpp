@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cstddef>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -772,12 +773,29 @@ struct orbpl_tracker {
   uint16_t* st_entries = nullptr;  // stereo scratch: row-band entries
   int st_entry_cap = 0;            // entries per frame
   int* d_err = nullptr;            // stereo capacity flag
+  // stereo + lines (P17): LineExtractor on the right images on its own
+  // stream, then k_stereo_lines on the line stream
+  lsdx_ctx* lxr = nullptr;
+  hipStream_t rlstream = nullptr;
+  hipEvent_t ev_rlin = nullptr;    // step start on `stream`
+  hipEvent_t ev_sl_done = nullptr; // k_stereo_lines finished reading the right lines
+  orbpl_keyline* r_kl = nullptr;   // right KeyLines (S x kLineKeep), one buffer
+  uint8_t* r_ldesc = nullptr;
+  double* r_lcoef = nullptr;
+  int* r_nl = nullptr;
   StreamState* d_state = nullptr;
   PoseEdge* d_edges = nullptr;
   static constexpr int kRing = 64;   // steps kept in the timing ring
-  static constexpr int kEv = 18;     // events per step
+  static constexpr int kEv = 26;     // events per step
   std::vector<hipEvent_t> ring;      // kRing * kEv events
   int ring_pos = 0, ring_count = 0;
+  // per-step history (orbpl_tracker_set_history): StreamState and keypoint /
+  // line counts of every stream after each step, device-side D2D copies on
+  // the tracking stream (no host synchronisation inside a step)
+  int hist_cap = 0, hist_count = 0;
+  StreamState* d_hist_state = nullptr;
+  int* d_hist_n = nullptr;
+  int* d_hist_nl = nullptr;
   std::vector<void*> allocs;
 };
 
@@ -805,6 +823,11 @@ int orbpl_tracker_destroy(orbpl_tracker* t) {
     if (e) (void)hipEventDestroy(e);
   if (t->lstream) (void)hipStreamSynchronize(t->lstream);
   if (t->rstream) (void)hipStreamSynchronize(t->rstream);
+  if (t->rlstream) (void)hipStreamSynchronize(t->rlstream);
+  if (t->ev_rlin) (void)hipEventDestroy(t->ev_rlin);
+  if (t->ev_sl_done) (void)hipEventDestroy(t->ev_sl_done);
+  if (t->rlstream) (void)hipStreamDestroy(t->rlstream);
+  if (t->lxr) lsdx_destroy(t->lxr);
   if (t->ev_in) (void)hipEventDestroy(t->ev_in);
   if (t->ev_rin) (void)hipEventDestroy(t->ev_rin);
   if (t->exr) orbx_destroy(t->exr);
@@ -825,9 +848,8 @@ int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam
                             int device, int flags, orbpl_tracker** out) {
   if (!orb || !cam || !out || n_streams <= 0) return arg_fail("bad argument");
   if (flags & ~(ORBPL_TRACK_LINES | ORBPL_TRACK_STEREO)) return arg_fail("unknown tracker flag");
-  // the reference's stereo Frame extracts no lines (Frame.cc:70-131)
-  if ((flags & ORBPL_TRACK_LINES) && (flags & ORBPL_TRACK_STEREO))
-    return arg_fail("ORBPL_TRACK_LINES and ORBPL_TRACK_STEREO are exclusive");
+  // ORBPL_TRACK_LINES | ORBPL_TRACK_STEREO: the defined stereo line mode (P17;
+  // the reference's stereo Frame extracts no lines, Frame.cc:70-131)
   if ((flags & ORBPL_TRACK_STEREO) && cam->height > 1024)
     return arg_fail("stereo tracking supports images up to 1024 rows");
   *out = nullptr;
@@ -897,12 +919,24 @@ int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam
   if (t->stereo) {
     // a right keypoint spans at most 4 * scale + 2 <= 18 rows (8 levels of 1.2)
     t->st_entry_cap = (int)K * 20;
+    // test hook: a smaller row-band capacity forces the overflow path
+    if (const char* e = getenv("ORBPL_STEREO_ENTRY_CAP")) {
+      const int v = atoi(e);
+      if (v > 0 && v < t->st_entry_cap) t->st_entry_cap = v;
+    }
     TA(t->r_kps, S * K * sizeof(KeyPointD));
     TA(t->r_desc, S * K * 32);
     TA(t->r_n, S * 4);
     TA(t->st_sad, S * K * 4);
     TA(t->st_entries, S * (size_t)t->st_entry_cap * 2);
     TA(t->d_err, 4);
+    if (t->lines) {
+      const size_t L = S * kLineKeep;
+      TA(t->r_kl, L * sizeof(orbpl_keyline));
+      TA(t->r_ldesc, L * 32);
+      TA(t->r_lcoef, L * 3 * sizeof(double));
+      TA(t->r_nl, S * 4);
+    }
   }
 #undef TA
   t->ring.assign(orbpl_tracker::kRing * orbpl_tracker::kEv, nullptr);
@@ -943,6 +977,19 @@ int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam
       orbpl_tracker_destroy(t);
       return hip_fail(hipErrorUnknown, "hipEventCreate", __LINE__);
     }
+    if (t->lines) {
+      rc = lsdx_create(cam->width, cam->height, n_streams, device, &t->lxr);
+      if (rc) {
+        orbpl_tracker_destroy(t);
+        return rc;
+      }
+      if (hipStreamCreateWithFlags(&t->rlstream, hipStreamNonBlocking) != hipSuccess ||
+          hipEventCreateWithFlags(&t->ev_rlin, hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&t->ev_sl_done, hipEventDisableTiming) != hipSuccess) {
+        orbpl_tracker_destroy(t);
+        return hip_fail(hipErrorUnknown, "hipStreamCreate", __LINE__);
+      }
+    }
   }
   rc = orbpl_tracker_reset(t, nullptr);
   if (rc) {
@@ -966,7 +1013,10 @@ int orbpl_tracker_reset(orbpl_tracker* t, const float* Tcw0) {
   if (t->tstream) HIP_CHECK(hipStreamSynchronize(t->tstream));
   if (t->lstream) HIP_CHECK(hipStreamSynchronize(t->lstream));
   if (t->rstream) HIP_CHECK(hipStreamSynchronize(t->rstream));
+  if (t->rlstream) HIP_CHECK(hipStreamSynchronize(t->rlstream));
   HIP_CHECK(hipMemcpy(t->d_state, st.data(), sizeof(StreamState) * t->S, hipMemcpyHostToDevice));
+  if (t->d_err) HIP_CHECK(hipMemset(t->d_err, 0, 4));
+  t->hist_count = 0;
   return ORBPL_OK;
 }
 
@@ -1003,6 +1053,22 @@ static int tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_
     if (rrc) return rrc;
     HIP_CHECK(hipEventRecord(ev[16], t->rstream));
   }
+  if (t->lines && t->stereo) {
+    // ---- right line stream: LineExtractor on the right images (P17), after
+    // the previous step's k_stereo_lines has read the right KeyLines
+    HIP_CHECK(hipEventRecord(t->ev_rlin, s));
+    HIP_CHECK(hipStreamWaitEvent(t->rlstream, t->ev_rlin, 0));
+    HIP_CHECK(hipStreamWaitEvent(t->rlstream, t->ev_sl_done, 0));
+    HIP_CHECK(hipEventRecord(ev[23], t->rlstream));
+    LineOut ro{};
+    ro.kl = t->r_kl;
+    ro.desc = t->r_ldesc;
+    ro.coef = t->r_lcoef;
+    ro.n = t->r_nl;
+    int lrc = lsdx_run(t->lxr, d_right, S, t->W, (int64_t)t->W * t->H, &ro, t->rlstream, nullptr);
+    if (lrc) return lrc;
+    HIP_CHECK(hipEventRecord(ev[24], t->rlstream));
+  }
   LineTrackArgs la{};
   if (t->lines) {
     // ---- line stream: LineExtractor + UndistortKeyLines + line depths
@@ -1014,7 +1080,8 @@ static int tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_
     lo.desc = C.ldesc;
     lo.coef = C.lcoef;
     lo.n = C.nl;
-    int lrc = lsdx_run(t->lx, d_gray, S, t->W, (int64_t)t->W * t->H, &lo, t->lstream, ev[12]);
+    int lrc = lsdx_run(t->lx, d_gray, S, t->W, (int64_t)t->W * t->H, &lo, t->lstream, ev[12],
+                       &ev[18]);
     if (lrc) return lrc;
     la.nl = C.nl;
     la.kl = C.kl;
@@ -1033,6 +1100,14 @@ static int tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_
     la.last_ml_xyz = L.ml_xyz;
     la.last_desc = L.ldesc;
     launch_line_prepare(t->consts, la, S, t->lstream);
+    if (t->stereo) {
+      // end-point depths from the right image's lines (P17)
+      HIP_CHECK(hipStreamWaitEvent(t->lstream, ev[24], 0));
+      HIP_CHECK(hipEventRecord(ev[25], t->lstream));
+      StereoLineArgs sa{C.nl, C.kl_un, C.ldesc, t->r_nl, t->r_kl, t->r_ldesc, C.dstart, C.dend};
+      launch_stereo_lines(t->consts, sa, S, t->lstream);
+      HIP_CHECK(hipEventRecord(t->ev_sl_done, t->lstream));
+    }
     HIP_CHECK(hipEventRecord(ev[13], t->lstream));
   }
   int rc = orbx_run(t->ex, d_gray, S, t->W, (long long)t->W * t->H,
@@ -1153,6 +1228,14 @@ static int tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_
   launch_finish(t->consts, t->d_state, C.n, K, C.kps_un, C.depth, C.match, C.outlier, C.has_mp,
                 C.mp_xyz, C.nobs, lf, S, ts);
   HIP_CHECK(hipEventRecord(ev[10], ts));
+  if (t->hist_count < t->hist_cap) {
+    const size_t k = (size_t)t->hist_count++ * S;
+    HIP_CHECK(hipMemcpyAsync(t->d_hist_state + k, t->d_state, sizeof(StreamState) * S,
+                             hipMemcpyDeviceToDevice, ts));
+    HIP_CHECK(hipMemcpyAsync(t->d_hist_n + k, C.n, 4 * (size_t)S, hipMemcpyDeviceToDevice, ts));
+    if (t->lines)
+      HIP_CHECK(hipMemcpyAsync(t->d_hist_nl + k, C.nl, 4 * (size_t)S, hipMemcpyDeviceToDevice, ts));
+  }
   HIP_CHECK(hipEventRecord(t->ev_free[li], ts));
   t->free_pending[li] = true;
   HIP_CHECK(hipGetLastError());
@@ -1196,10 +1279,19 @@ int orbpl_tracker_synchronize(orbpl_tracker* t) {
   if (t->stereo) {
     int rc = orbx_synchronize(t->exr);
     if (rc) return rc;
+    if (t->lxr) {
+      HIP_CHECK(hipStreamSynchronize(t->rlstream));
+      rc = lsdx_check(t->lxr, t->S);
+      if (rc) return rc;
+    }
     HIP_CHECK(hipStreamSynchronize(t->stream));
     int err = 0;
     HIP_CHECK(hipMemcpy(&err, t->d_err, 4, hipMemcpyDeviceToHost));
-    if (err) return (arg_fail("stereo row band capacity exceeded"), ORBPL_ERR_OVERFLOW);
+    if (err) {
+      // reported once: clear the flag so that later steps start clean
+      HIP_CHECK(hipMemset(t->d_err, 0, 4));
+      return (arg_fail("stereo row band capacity exceeded"), ORBPL_ERR_OVERFLOW);
+    }
   }
   return orbx_synchronize(t->ex);
 }
@@ -1266,6 +1358,72 @@ int orbpl_tracker_line_timings(orbpl_tracker* t, int max_steps, float* ms, int* 
   return ORBPL_OK;
 }
 
+int orbpl_tracker_set_history(orbpl_tracker* t, int max_steps) {
+  if (!t || max_steps < 0) return arg_fail("bad argument");
+  HIP_CHECK(hipSetDevice(t->device));
+  HIP_CHECK(hipStreamSynchronize(t->stream));
+  HIP_CHECK(hipStreamSynchronize(t->tstream));
+  for (void* p : {(void*)t->d_hist_state, (void*)t->d_hist_n, (void*)t->d_hist_nl})
+    if (p) {
+      t->allocs.erase(std::remove(t->allocs.begin(), t->allocs.end(), p), t->allocs.end());
+      HIP_CHECK(hipFree(p));
+    }
+  t->d_hist_state = nullptr;
+  t->d_hist_n = t->d_hist_nl = nullptr;
+  t->hist_cap = t->hist_count = 0;
+  if (max_steps == 0) return ORBPL_OK;
+  const size_t n = (size_t)max_steps * t->S;
+  int rc = tr_alloc(t, (void**)&t->d_hist_state, n * sizeof(StreamState));
+  if (!rc) rc = tr_alloc(t, (void**)&t->d_hist_n, n * 4);
+  if (!rc) rc = tr_alloc(t, (void**)&t->d_hist_nl, n * 4);
+  if (rc) return rc;
+  t->hist_cap = max_steps;
+  return ORBPL_OK;
+}
+
+int orbpl_tracker_get_history(orbpl_tracker* t, int stream, int max_steps, float* Tcw,
+                              int* counts8, int* n_steps) {
+  if (!t || !n_steps || stream < 0 || stream >= t->S || max_steps < 0) return arg_fail("bad argument");
+  HIP_CHECK(hipSetDevice(t->device));
+  HIP_CHECK(hipStreamSynchronize(t->tstream));
+  const int n = std::min(max_steps, t->hist_count);
+  *n_steps = n;
+  for (int k = 0; k < n; k++) {
+    const size_t o = (size_t)k * t->S + stream;
+    StreamState st;
+    int nk = 0, nl = 0;
+    HIP_CHECK(hipMemcpy(&st, t->d_hist_state + o, sizeof(st), hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemcpy(&nk, t->d_hist_n + o, 4, hipMemcpyDeviceToHost));
+    if (t->lines) HIP_CHECK(hipMemcpy(&nl, t->d_hist_nl + o, 4, hipMemcpyDeviceToHost));
+    if (Tcw) memcpy(Tcw + 16 * k, st.Tlast, 64);
+    if (counts8) {
+      int* c = counts8 + 8 * k;
+      c[0] = nk; c[1] = st.nmatches; c[2] = st.ninliers; c[3] = st.nmatches_map; c[4] = st.ok;
+      c[5] = nl; c[6] = t->lines ? st.nlmatches : 0; c[7] = t->lines ? st.nlmatches_map : 0;
+    }
+  }
+  return ORBPL_OK;
+}
+
+int orbpl_tracker_lsd_timings(orbpl_tracker* t, int max_steps, float* ms, int* n_steps) {
+  if (!t || !ms || !n_steps) return arg_fail("NULL argument");
+  if (!t->lines) return arg_fail("tracker created without ORBPL_TRACK_LINES");
+  HIP_CHECK(hipSetDevice(t->device));
+  HIP_CHECK(hipStreamSynchronize(t->lstream));
+  // line stream: blur+resize+grad, sort, seed loop, validate, KeyLines,
+  // blur5+Sobel+LBD, UndistortKeyLines + line depths
+  static const int kPair[7][2] = {{11, 18}, {18, 19}, {19, 20}, {20, 12}, {12, 21}, {21, 22}, {22, 13}};
+  const int n = std::min(max_steps, t->ring_count);
+  for (int k = 0; k < n; k++) {
+    const int step = t->ring_pos - n + k;
+    hipEvent_t* ev = &t->ring[(size_t)(step % orbpl_tracker::kRing) * orbpl_tracker::kEv];
+    for (int i = 0; i < 7; i++)
+      HIP_CHECK(hipEventElapsedTime(&ms[k * 7 + i], ev[kPair[i][0]], ev[kPair[i][1]]));
+  }
+  *n_steps = n;
+  return ORBPL_OK;
+}
+
 int orbpl_tracker_stereo_timings(orbpl_tracker* t, int max_steps, float* ms, int* n_steps) {
   if (!t || !ms || !n_steps) return arg_fail("NULL argument");
   if (!t->stereo) return arg_fail("tracker created without ORBPL_TRACK_STEREO");
@@ -1273,14 +1431,21 @@ int orbpl_tracker_stereo_timings(orbpl_tracker* t, int max_steps, float* ms, int
   HIP_CHECK(hipStreamSynchronize(t->stream));
   HIP_CHECK(hipStreamSynchronize(t->tstream));
   HIP_CHECK(hipStreamSynchronize(t->rstream));
-  // right ORB extraction (right stream), ComputeStereoMatches (extraction stream)
-  static const int kPair[2][2] = {{15, 16}, {17, 6}};
+  // right ORB extraction (right stream), ComputeStereoMatches (extraction
+  // stream); with lines: right LineExtractor (right line stream),
+  // k_stereo_lines (line stream); 0 without lines
+  static const int kPair[4][2] = {{15, 16}, {17, 6}, {23, 24}, {25, 13}};
+  if (t->rlstream) HIP_CHECK(hipStreamSynchronize(t->rlstream));
+  if (t->lstream) HIP_CHECK(hipStreamSynchronize(t->lstream));
   const int n = std::min(max_steps, t->ring_count);
   for (int k = 0; k < n; k++) {
     const int step = t->ring_pos - n + k;
     hipEvent_t* ev = &t->ring[(size_t)(step % orbpl_tracker::kRing) * orbpl_tracker::kEv];
-    for (int i = 0; i < 2; i++)
-      HIP_CHECK(hipEventElapsedTime(&ms[k * 2 + i], ev[kPair[i][0]], ev[kPair[i][1]]));
+    for (int i = 0; i < 4; i++) {
+      ms[k * 4 + i] = 0.0f;
+      if (i < 2 || t->lines)
+        HIP_CHECK(hipEventElapsedTime(&ms[k * 4 + i], ev[kPair[i][0]], ev[kPair[i][1]]));
+    }
   }
   *n_steps = n;
   return ORBPL_OK;

@@ -1,0 +1,77 @@
+"""The N>1 path of bench.py on CPU (gloo, world size 2): the max-over-ranks
+wall time, the per-rank parity gather, the `--gpus N` launcher command, and
+a 2-rank torchrun of bench's own rank bootstrap (env contract: RANK /
+LOCAL_RANK / WORLD_SIZE, MASTER_ADDR 127.0.0.1)."""
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import torch.multiprocessing as mp
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    t = bench.max_over_ranks(dist, 1.0 + rank)        # rank 1 is the slow one
+    par = bench.gather_parity(dist, world, {"pass": rank == 0 or q is None, "rank": rank})
+    q.put((rank, t, par))
+    dist.destroy_process_group()
+
+
+def test_max_time_and_parity_gather_ws2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    for rank, t, par in res:
+        assert t == 2.0                                  # the max over ranks
+        assert [p["rank"] for p in par["by_rank"]] == [0, 1]
+        assert par["all_ranks_pass"] is False            # rank 1 reported a failure
+
+
+def test_gpus_flag_builds_torchrun_command():
+    import bench
+    cmd = bench.torchrun_cmd(8, ["--gpus", "8", "--steps", "3"], 29555)
+    assert cmd[1:4] == ["-m", "torch.distributed.run", "--nnodes=1"]
+    assert "--nproc-per-node=8" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-4:] == ["--gpus", "8", "--steps", "3"]
+    assert cmd[-5].endswith("bench.py")
+
+
+def test_torchrun_two_ranks_env_contract():
+    """torch.distributed.run with 2 ranks on CPU: each rank sees the env that
+    bench.py reads and reaches the gloo barrier."""
+    code = ("import os, torch.distributed as d; d.init_process_group('gloo'); d.barrier(); "
+            "print('rank', os.environ['RANK'], os.environ['LOCAL_RANK'], os.environ['WORLD_SIZE'])")
+    script = Path(os.environ.get("TMPDIR", "/tmp")) / f"orbpl_ws2_{os.getpid()}.py"
+    script.write_text(code)
+    try:
+        out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                              "--nproc-per-node=2", "--master-addr", "127.0.0.1", "--master-port",
+                              str(_port()), str(script)], capture_output=True, text=True,
+                             timeout=180)
+    finally:
+        script.unlink()
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = sorted(line for line in out.stdout.splitlines() if line.startswith("rank"))
+    assert lines == ["rank 0 0 2", "rank 1 1 2"]

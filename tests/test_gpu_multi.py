@@ -1,0 +1,30 @@
+"""world_size 2 on the GPU box: `bench.py --gpus 2` starts two ranks with
+torch.distributed.run (device = LOCAL_RANK mod the visible devices, so both
+share the one GPU of a test box), each tracks its own streams, and both
+ranks' sampled streams of the timed trackers match the oracle."""
+import json
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def test_bench_two_ranks():
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--streams", "16", "--steps", "2",
+           "--warmup", "1", "--loop", "8", "--secondary-steps", "0", "--stereo-steps", "0",
+           "--rig-steps", "0", "--no-cpu-baseline", "--sweep", "0", "--isolated-steps", "0"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=400, cwd=str(ROOT))
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = [x for x in out.stdout.splitlines() if x.startswith("{")][-1]
+    r = json.loads(line)
+    assert r["n_gpus"] == 2
+    assert r["config"]["frames_per_step"] == 32
+    assert r["value"] > 0
+    par = r["parity"]
+    assert par["all_ranks_pass"], par
+    assert len(par["by_rank"]) == 2
+    assert all(p["steps_checked"] == 3 for p in par["by_rank"])

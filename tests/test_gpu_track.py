@@ -156,6 +156,7 @@ def test_tracker_pipelined_matches_oracle_vo(orbpl, oracle):
     T0 = np.stack([np.linalg.inv(sq[1][0]).astype(np.float32) for sq in seqs])
     vo.reset(T0.reshape(S, 16))
     tr.reset(T0.reshape(S, 16))
+    tr.set_history(F)
     gray = orbpl.DeviceBuffer.from_array(
         np.stack([np.stack([sq[2][f][0] for sq in seqs]) for f in range(F)]))
     depth = orbpl.DeviceBuffer.from_array(
@@ -166,8 +167,13 @@ def test_tracker_pipelined_matches_oracle_vo(orbpl, oracle):
     tr.synchronize()
     st = tr.state()
     for s in range(S):
+        Th, Ch = tr.history(s)      # device-side per-step history (bench parity source)
+        assert len(Th) == F
         for f in range(F):
             To, so = vo.step(s, seqs[s][2][f][0], seqs[s][2][f][1])
+            assert np.abs(Th[f] - To).max() < POSE_TOL, (s, f)
+            assert Ch[f][0] == so["nkeypoints"] and Ch[f][1] == so["nmatches"], (s, f)
+            assert Ch[f][2] == so["ninliers"] and Ch[f][3] == so["nmatches_map"], (s, f)
         assert st["nkeypoints"][s] == so["nkeypoints"]
         assert st["nmatches"][s] == so["nmatches"], s
         assert st["ninliers"][s] == so["ninliers"], s
@@ -219,19 +225,23 @@ def test_tracker_with_lines_matches_oracle_lvo(orbpl, oracle, pipelined):
     assert lt.shape[1] == 3 and np.all(lt >= 0)
 
 
-@pytest.mark.parametrize("pipelined", [False, True])
-def test_stereo_tracker_matches_oracle(orbpl, oracle, pipelined):
+@pytest.mark.parametrize("pipelined,lines", [(False, False), (True, False), (False, True),
+                                             (True, True)])
+def test_stereo_tracker_matches_oracle(orbpl, oracle, pipelined, lines):
     """Stereo tracker (ORBPL_TRACK_STEREO, KITTI 00 camera, 2000 features):
     ORB on both images, batched ComputeStereoMatches, th = 7 matching and the
     pose, against the oracle's stereo VO loop: identical counts every frame,
-    pose within POSE_TOL."""
+    pose within POSE_TOL. With lines (configs[3], the defined P17 mode):
+    LineExtractor on both images, stereo line depths, line matching and line
+    edges; the last frame's KeyLines bit-exact."""
     from _scenes import stereo_sequence
     S, F = 2, 4
     seqs = [stereo_sequence(F, 50 + s) for s in range(S)]
     cfg = seqs[0][0]
     W, H = cfg["width"], cfg["height"]
-    lvo = oracle.LVO(oracle.params(2000), oracle.camera(cfg), S, use_lines=False)
-    tr = orbpl.Tracker(orbpl.OrbParams(2000, 1.2, 8, 20, 7), orbpl.make_camera(cfg), S, stereo=True)
+    lvo = oracle.LVO(oracle.params(2000), oracle.camera(cfg), S, use_lines=lines)
+    tr = orbpl.Tracker(orbpl.OrbParams(2000, 1.2, 8, 20, 7), orbpl.make_camera(cfg), S, stereo=True,
+                       lines=lines)
     tr.set_pipelined(pipelined)
     T0 = np.stack([np.linalg.inv(sq[1][0]).astype(np.float32) for sq in seqs])
     lvo.reset(T0.reshape(S, 16))
@@ -254,8 +264,20 @@ def test_stereo_tracker_matches_oracle(orbpl, oracle, pipelined):
             assert np.abs(st["Tcw"][s] - To).max() < POSE_TOL, (f, s)
         if f > 0:
             assert st["nmatches"].min() >= 100
+            if lines:
+                assert ls["line_matches"].min() >= 15
     stt = tr.stereo_timings()
-    assert stt.shape[1] == 2 and np.all(stt >= 0)
+    assert stt.shape[1] == 4 and np.all(stt >= 0)
+    if lines:
+        assert np.all(stt[:, 2:] > 0)
+        cam_o = oracle.camera(cfg)
+        for s in range(S):
+            g, r = seqs[s][2][F - 1]
+            kl, desc, _, _ = oracle.line_extract(g)
+            ku, _, _, _, _ = oracle.line_frame_prepare(cam_o, kl, None)
+            kl_g, desc_g, _, _ = tr.lines(s)
+            assert kl_g.tobytes() == ku.tobytes()
+            assert np.array_equal(desc_g, desc)
     with pytest.raises(RuntimeError):
         tr.step_device(left.ptr, right.ptr)
 
@@ -296,12 +318,30 @@ def test_tracker_rig_720p_matches_oracle(orbpl, oracle):
             assert np.abs(st["Tcw"][s] - To).max() < POSE_TOL, (t, s)
 
 
-def test_stereo_tracker_rejects_lines(orbpl):
+def test_stereo_overflow_reported_once(orbpl, monkeypatch):
+    """A row-band capacity overflow in ComputeStereoMatches (forced with a tiny
+    ORBPL_STEREO_ENTRY_CAP) is reported as ORBPL_ERR_OVERFLOW by one
+    synchronize, then cleared: the next synchronize succeeds, and reset
+    clears it too."""
     from _scenes import stereo_sequence
-    cfg = stereo_sequence(1, 50)[0]
-    with pytest.raises(RuntimeError):
-        orbpl.Tracker(orbpl.OrbParams(2000, 1.2, 8, 20, 7), orbpl.make_camera(cfg), 1, lines=True,
-                      stereo=True)
+    cfg, traj, pairs = stereo_sequence(1, 50)
+    W, H = cfg["width"], cfg["height"]
+    monkeypatch.setenv("ORBPL_STEREO_ENTRY_CAP", "16")
+    tr = orbpl.Tracker(orbpl.OrbParams(2000, 1.2, 8, 20, 7), orbpl.make_camera(cfg), 1, stereo=True)
+    monkeypatch.delenv("ORBPL_STEREO_ENTRY_CAP")
+    left = orbpl.DeviceBuffer.from_array(pairs[0][0])
+    right = orbpl.DeviceBuffer.from_array(pairs[0][1])
+    tr.step_stereo_device(left.ptr, right.ptr)
+    with pytest.raises(orbpl.OrbplError, match="-5"):
+        tr.synchronize()
+    tr.synchronize()            # reported once
+    tr.step_stereo_device(left.ptr, right.ptr)
+    with pytest.raises(orbpl.OrbplError, match="-5"):
+        tr.synchronize()
+    tr.step_stereo_device(left.ptr, right.ptr)
+    tr.reset()                  # reset clears the flag as well
+    tr.synchronize()
+    tr.close()
 
 
 @pytest.mark.parametrize("cam_name", ["TUM1", "TUM3"])
