@@ -240,20 +240,27 @@ def parity_check(T_gpu, C_gpu, streams, gray, depth, L, workload):
     T_ref = np.zeros((len(streams), n, 4, 4), np.float32)
     C_ref = np.zeros((len(streams), n, 8), np.int32)
 
+    errors = []
+
     def worker(k, s):
-        vo, vstep = oracle_vo(O, wl)
-        vo.reset(np.linalg.inv(L.Twc(s, 0)).astype(np.float32).reshape(1, 16))
-        for t in range(n):
-            e = L.elem(s, t)
-            T, st = vstep(vo, gray[e], depth[e])
-            T_ref[k, t] = T
-            C_ref[k, t] = [st[key] for key in OUT8]
+        try:
+            vo, vstep = oracle_vo(O, wl)
+            vo.reset(np.linalg.inv(L.Twc(s, 0)).astype(np.float32).reshape(1, 16))
+            for t in range(n):
+                e = L.elem(s, t)
+                T, st = vstep(vo, gray[e], depth[e])
+                T_ref[k, t] = T
+                C_ref[k, t] = [st.get(key, 0) for key in OUT8]   # VO: no line counts
+        except Exception as ex:  # surface, do not let a thread swallow it
+            errors.append(ex)
 
     ths = [threading.Thread(target=worker, args=(k, s)) for k, s in enumerate(streams)]
     for t in ths:
         t.start()
     for t in ths:
         t.join()
+    if errors:
+        raise errors[0]
     Tg = np.stack([T[:n] for T in T_gpu])
     Cg = np.stack([c[:n] for c in C_gpu])
     bad = [(int(streams[k]), int(t), OUT8[i]) for k, t, i in zip(*np.nonzero(Cg != C_ref))]

@@ -289,6 +289,17 @@ typedef struct orbpl_pose_problem {
  * (nInitialCorrespondences - nBad, 0 if < 3 correspondences). */
 int orbpl_pose_optimization(const orbpl_camera* cam, const orbpl_pose_problem* prob, float* Tcw,
                             uint8_t* outlier, uint8_t* line_outlier, int* n_inliers);
+/* Pose options. ORBPL_POSE_FIXED_LINE_JAC: the analytic EdgeLineOnlyPose
+ * Jacobian ("--fixed-line-jacobian") instead of the
+ * reference's as-written one (types_line_expmap.h:138-152: row 0 overwritten
+ * by the end point, row 1 uninitialised -> 0 (pinned P7), +fx*cy in dI_dLc,
+ * R*v in place of n_c in dLc_ddelta): de_i/dl = ((x_i - l0 N_i/ln^2)/ln,
+ * (y_i - l1 N_i/ln^2)/ln, 1/ln), l = K_line n_c, dn_c/d(w,u) =
+ * [-[n_c]x | -[v_c]x] under g2o's left update exp(d) * T. */
+#define ORBPL_POSE_FIXED_LINE_JAC 1
+int orbpl_pose_optimization_ex(const orbpl_camera* cam, const orbpl_pose_problem* prob, int flags,
+                               float* Tcw, uint8_t* outlier, uint8_t* line_outlier,
+                               int* n_inliers);
 
 
 /* ------------------------------------------------------------------------
@@ -324,6 +335,9 @@ int orbpl_tracker_create(const orbpl_orb_params* orb, const orbpl_camera* cam, i
  * passes the angle / length / row-overlap / disparity tests,
  * then the RGB-D line path (line matching, line edges, map lines). */
 #define ORBPL_TRACK_STEREO 2
+/* ORBPL_TRACK_FIXED_LINE_JAC: PoseOptimizationWithLines with the analytic line
+ * Jacobian (ORBPL_POSE_FIXED_LINE_JAC) in every tracker pose. */
+#define ORBPL_TRACK_FIXED_LINE_JAC 8
 int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam, int n_streams,
                             int device, int flags, orbpl_tracker** out);
 int orbpl_tracker_destroy(orbpl_tracker* tr);

@@ -656,7 +656,9 @@ static int lvo_step(LVO* v, int stream, const uint8_t* gray, const float* depth,
       P.ml_xyz = lxyz.data();
       P.inv_sigma2 = v->inv_sigma2.data();
       P.nlevels = (int)v->inv_sigma2.size();
-      oracle_pose_optimization(&cam, &P, S.Tcw, outl.data(), loutl.data(), &ninl);
+      oracle_pose_optimization_ex(&cam, &P,
+                                  (v->flags & ORBPL_TRACK_FIXED_LINE_JAC) ? ORBPL_POSE_FIXED_LINE_JAC : 0,
+                                  S.Tcw, outl.data(), loutl.data(), &ninl);
     }
     // outlier discard (Tracking.cc:1273-1314); without an optimisation every
     // flag is clear and the counts report the raw matches

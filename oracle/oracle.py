@@ -200,6 +200,7 @@ def _setup_track(L):
     L.oracle_frame_prepare.argtypes = [vp, vp, i, vp, vp, vp, vp, vp, vp]
     L.oracle_search_by_projection_last.argtypes = [vp, vp, i, vp, vp, C.c_float, i, i, vp, ip]
     L.oracle_pose_optimization.argtypes = [vp, vp, vp, vp, vp, ip]
+    L.oracle_pose_optimization_ex.argtypes = [vp, vp, i, vp, vp, vp, ip]
     L.oracle_stereo_matches.argtypes = [vp, vp, vp, i, vp, vp, vp, vp, vp, vp, i, vp, vp, i, vp,
                                         vp]
     L.oracle_search_by_bow.argtypes = [i, vp, vp, vp, vp, i, vp, vp, vp, C.c_float, i, vp, ip]
@@ -337,7 +338,7 @@ def stereo_matches(cam, p, left, right, kl, dl, kr, dr):
     return ur[:len(kl)].copy(), dp[:len(kl)].copy()
 
 
-def pose_optimization(cam, prob, Tcw, outlier, line_outlier=None):
+def pose_optimization(cam, prob, Tcw, outlier, line_outlier=None, fixed_line_jac=False):
     keep = []
 
     def arr(a, dt):
@@ -358,7 +359,8 @@ def pose_optimization(cam, prob, Tcw, outlier, line_outlier=None):
     out = _c(outlier, np.uint8).copy()
     lout = _c(line_outlier if line_outlier is not None else np.zeros(nl), np.uint8).copy()
     nin = C.c_int(0)
-    lib().oracle_pose_optimization(C.byref(cam), C.byref(P), _p(T), _p(out), _p(lout), C.byref(nin))
+    lib().oracle_pose_optimization_ex(C.byref(cam), C.byref(P), int(bool(fixed_line_jac)), _p(T),
+                                      _p(out), _p(lout), C.byref(nin))
     return T, out, lout, nin.value
 
 

@@ -46,6 +46,10 @@ int oracle_stereo_matches(const orbpl_camera* cam, const float* scale, const flo
                           float* depth);
 int oracle_pose_optimization(const orbpl_camera* cam, const orbpl_pose_problem* P, float* Tcw,
                              uint8_t* outlier, uint8_t* line_outlier, int* n_inliers);
+/* flags: ORBPL_POSE_FIXED_LINE_JAC (orbpl.h) = analytic line Jacobian */
+int oracle_pose_optimization_ex(const orbpl_camera* cam, const orbpl_pose_problem* P, int flags,
+                                float* Tcw, uint8_t* outlier, uint8_t* line_outlier,
+                                int* n_inliers);
 void* oracle_vo_create(const orbpl_orb_params* orb, const orbpl_camera* cam, int n_streams);
 void oracle_vo_destroy(void* h);
 int oracle_vo_reset(void* h, const float* Tcw0);

@@ -253,7 +253,10 @@ struct Edge {
   int dim;
 };
 
-struct Cam { double fx, fy, cx, cy, bf; };
+struct Cam {
+  double fx, fy, cx, cy, bf;
+  int fixed_line_jac;  // 1: analytic EdgeLineOnlyPose Jacobian (ORBPL_POSE_FIXED_LINE_JAC)
+};
 
 static void edge_error(const Edge& e, const Cam& c, const SE3& T, double* err) {
   if (e.kind == 2) {
@@ -308,16 +311,44 @@ static void edge_jacobian(const Edge& e, const Cam& c, const SE3& T, double J[3]
     double l0 = c.fy * nc[0], l1 = c.fx * nc[1];
     double l2 = -c.fy * c.cx * nc[0] + -c.fx * c.cy * nc[1] + c.fx * c.fy * nc[2];
     double ln = std::sqrt(std::pow(l0, 2) + std::pow(l1, 2));
-    double e2 = e.obs[2] * l0 + e.obs[3] * l1 + l2;
-    // P7: row 0 holds the end-point values, row 1 pinned to zero
-    double dd[2][3] = {{(e.obs[2] - (l0 * e2) / (ln * ln)) / ln, (e.obs[3] - (l1 * e2) / (ln * ln)) / ln, 1.0},
-                       {0.0, 0.0, 0.0}};
-    const double A[3][3] = {{c.fy, 0, 0}, {0, c.fx, 0}, {-c.fy * c.cx, c.fx * c.cy, c.fx * c.fy}};
     auto skew = [](const double v[3], double S[3][3]) {
       S[0][0] = 0; S[0][1] = -v[2]; S[0][2] = v[1];
       S[1][0] = v[2]; S[1][1] = 0; S[1][2] = -v[0];
       S[2][0] = -v[1]; S[2][1] = v[0]; S[2][2] = 0;
     };
+    if (c.fixed_line_jac) {
+      // Analytic form (--fixed-line-jacobian): with the
+      // left perturbation exp(d) T, d = (w, u), the camera Plucker line moves
+      // as dn = w x n_c + u x v_c, so dn/dd = [-[n_c]x | -[v_c]x]; the two
+      // end-point distances e_i = (x_i l0 + y_i l1 + l2) / |l_01| give
+      // de_i/dl = ((x_i - l0 N_i / ln^2) / ln, (y_i - l1 N_i / ln^2) / ln, 1 / ln)
+      // and l = K_line n_c with K_line as in computeError (-fx*cy).
+      const double N[2] = {e.obs[0] * l0 + e.obs[1] * l1 + l2, e.obs[2] * l0 + e.obs[3] * l1 + l2};
+      double dd[2][3];
+      for (int r = 0; r < 2; r++) {
+        dd[r][0] = (e.obs[2 * r] - (l0 * N[r]) / (ln * ln)) / ln;
+        dd[r][1] = (e.obs[2 * r + 1] - (l1 * N[r]) / (ln * ln)) / ln;
+        dd[r][2] = 1.0 / ln;
+      }
+      const double A[3][3] = {{c.fy, 0, 0}, {0, c.fx, 0}, {-c.fy * c.cx, -c.fx * c.cy, c.fx * c.fy}};
+      double Sn[3][3], Sv[3][3];
+      skew(nc, Sn);
+      skew(Rv, Sv);
+      double M[2][3];
+      for (int r = 0; r < 2; r++)
+        for (int k = 0; k < 3; k++) M[r][k] = dd[r][0] * A[0][k] + dd[r][1] * A[1][k] + dd[r][2] * A[2][k];
+      for (int r = 0; r < 2; r++)
+        for (int k = 0; k < 3; k++) {
+          J[r][k] = -(M[r][0] * Sn[0][k] + M[r][1] * Sn[1][k] + M[r][2] * Sn[2][k]);
+          J[r][3 + k] = -(M[r][0] * Sv[0][k] + M[r][1] * Sv[1][k] + M[r][2] * Sv[2][k]);
+        }
+      return;
+    }
+    double e2 = e.obs[2] * l0 + e.obs[3] * l1 + l2;
+    // P7: row 0 holds the end-point values, row 1 pinned to zero
+    double dd[2][3] = {{(e.obs[2] - (l0 * e2) / (ln * ln)) / ln, (e.obs[3] - (l1 * e2) / (ln * ln)) / ln, 1.0},
+                       {0.0, 0.0, 0.0}};
+    const double A[3][3] = {{c.fy, 0, 0}, {0, c.fx, 0}, {-c.fy * c.cx, c.fx * c.cy, c.fx * c.fy}};
     double S1[3][3], S2[3][3];
     skew(Rv, S1);
     skew(tRv, S2);
@@ -664,9 +695,11 @@ int oracle_search_by_projection_last(const orbpl_camera* cam, const float* scale
   return 0;
 }
 
-int oracle_pose_optimization(const orbpl_camera* cam, const orbpl_pose_problem* P, float* Tcw,
-                             uint8_t* outlier, uint8_t* line_outlier, int* n_inliers) {
-  Cam c{cam->fx, cam->fy, cam->cx, cam->cy, cam->bf};
+int oracle_pose_optimization_ex(const orbpl_camera* cam, const orbpl_pose_problem* P, int flags,
+                                float* Tcw, uint8_t* outlier, uint8_t* line_outlier,
+                                int* n_inliers) {
+  Cam c{cam->fx, cam->fy, cam->cx, cam->cy, cam->bf,
+        (flags & ORBPL_POSE_FIXED_LINE_JAC) ? 1 : 0};
   const float deltaMono = std::sqrt(5.991), deltaStereo = std::sqrt(7.815);
   std::vector<Edge> E;
   int nInitial = 0, nLineInitial = 0;
@@ -739,6 +772,11 @@ int oracle_pose_optimization(const orbpl_camera* cam, const orbpl_pose_problem* 
   se3_to_T(lm.T, Tcw);
   *n_inliers = nInitial - nBad;
   return 0;
+}
+
+int oracle_pose_optimization(const orbpl_camera* cam, const orbpl_pose_problem* P, float* Tcw,
+                             uint8_t* outlier, uint8_t* line_outlier, int* n_inliers) {
+  return oracle_pose_optimization_ex(cam, P, 0, Tcw, outlier, line_outlier, n_inliers);
 }
 
 }  // extern "C"

@@ -328,6 +328,7 @@ def _declare_track(L):
     L.orbpl_frame_prepare.argtypes = [vp, vp, i, vp, vp, vp, vp, vp, vp]
     L.orbm_search_by_projection_last.argtypes = [vp, vp, i, vp, vp, C.c_float, i, i, vp, ip]
     L.orbpl_pose_optimization.argtypes = [vp, vp, vp, vp, vp, ip]
+    L.orbpl_pose_optimization_ex.argtypes = [vp, vp, i, vp, vp, vp, ip]
     L.orbpl_tracker_create.argtypes = [vp, vp, i, i, C.POINTER(vp)]
     L.orbpl_tracker_destroy.argtypes = [vp]
     L.orbpl_tracker_reset.argtypes = [vp, vp]
@@ -498,9 +499,11 @@ def frame_is_in_frustum(camera, scale_factor, nlevels, Tcw, mps, view_cos_limit=
     return out
 
 
-def pose_optimization(camera, prob, Tcw, outlier, line_outlier=None):
+def pose_optimization(camera, prob, Tcw, outlier, line_outlier=None, fixed_line_jac=False):
     """Optimizer::PoseOptimization[WithLines] (Optimizer.cc:375-619, 2132-2486).
-    ``prob``: dict of arrays. Returns (Tcw, outlier, line_outlier, n_inliers)."""
+    ``prob``: dict of arrays. Returns (Tcw, outlier, line_outlier, n_inliers).
+    fixed_line_jac: the analytic line Jacobian (ORBPL_POSE_FIXED_LINE_JAC)
+    instead of the reference's as-written one (pinned P7)."""
     keep = []
 
     def arr(a, dt):
@@ -521,8 +524,9 @@ def pose_optimization(camera, prob, Tcw, outlier, line_outlier=None):
     out = _c(outlier, np.uint8).copy()
     lout = _c(line_outlier if line_outlier is not None else np.zeros(nl), np.uint8).copy()
     nin = C.c_int(0)
-    check(lib().orbpl_pose_optimization(C.byref(camera), C.byref(P), _ptr(T), _ptr(out),
-                                        _ptr(lout), C.byref(nin)), "orbpl_pose_optimization")
+    check(lib().orbpl_pose_optimization_ex(C.byref(camera), C.byref(P), int(bool(fixed_line_jac)),
+                                           _ptr(T), _ptr(out), _ptr(lout), C.byref(nin)),
+          "orbpl_pose_optimization_ex")
     return T, out, lout, nin.value
 
 
@@ -609,12 +613,17 @@ class Tracker:
 
     TRACK_LINES = 1
     TRACK_STEREO = 2
+    TRACK_LOCAL_MAP = 4
+    TRACK_FIXED_LINE_JAC = 8
 
-    def __init__(self, orb_params, camera, n_streams, device=0, lines=False, stereo=False):
+    def __init__(self, orb_params, camera, n_streams, device=0, lines=False, stereo=False,
+                 local_map=False, fixed_line_jac=False):
         h = C.c_void_p()
         self.camera, self.S, self.device, self.use_lines = camera, n_streams, device, bool(lines)
         self.stereo = bool(stereo)
-        flags = (self.TRACK_LINES if lines else 0) | (self.TRACK_STEREO if stereo else 0)
+        flags = ((self.TRACK_LINES if lines else 0) | (self.TRACK_STEREO if stereo else 0) |
+                 (self.TRACK_LOCAL_MAP if local_map else 0) |
+                 (self.TRACK_FIXED_LINE_JAC if fixed_line_jac else 0))
         check(lib().orbpl_tracker_create_ex(C.byref(orb_params), C.byref(camera), n_streams, device,
                                             flags, C.byref(h)),
               "orbpl_tracker_create_ex")

@@ -70,6 +70,7 @@ struct PoseLaunch {
   const int* t_nl;
   uint8_t* t_loutlier;
   int lpitch;
+  int fixed_line_jac;           // ORBPL_POSE_FIXED_LINE_JAC (analytic line Jacobian)
 };
 
 // Per-frame line buffers of the tracker (kLineKeep lines per stream).

@@ -723,7 +723,10 @@ struct PoseShared {
   int misc[8];
 };
 
-struct PoseCam { double fx, fy, cx, cy, bf; };
+struct PoseCam {
+  double fx, fy, cx, cy, bf;
+  int fixed_line_jac;  // ORBPL_POSE_FIXED_LINE_JAC: analytic line Jacobian
+};
 
 __device__ void edge_error(const PoseEdge& e, const PoseCam& c, const SE3d& T, const double R[3][3],
                            double* err) {
@@ -788,6 +791,32 @@ __device__ void edge_jacobian(const PoseEdge& e, const PoseCam& c, const SE3d& T
     const double l0 = c.fy * nc[0], l1 = c.fx * nc[1];
     const double l2 = -c.fy * c.cx * nc[0] + -c.fx * c.cy * nc[1] + c.fx * c.fy * nc[2];
     const double ln = sqrt(l0 * l0 + l1 * l1);
+    if (c.fixed_line_jac) {
+      // analytic form (oracle edge_jacobian, ORBPL_POSE_FIXED_LINE_JAC):
+      // J_r = dd_r K_line [-[n_c]x | -[v_c]x]
+      const double N[2] = {(double)e.obs[0] * l0 + (double)e.obs[1] * l1 + l2,
+                           (double)e.obs[2] * l0 + (double)e.obs[3] * l1 + l2};
+      const double Sn[3][3] = {{0, -nc[2], nc[1]}, {nc[2], 0, -nc[0]}, {-nc[1], nc[0], 0}};
+      const double Sv[3][3] = {{0, -Rv[2], Rv[1]}, {Rv[2], 0, -Rv[0]}, {-Rv[1], Rv[0], 0}};
+      const double A[3][3] = {{c.fy, 0, 0}, {0, c.fx, 0}, {-c.fy * c.cx, -c.fx * c.cy, c.fx * c.fy}};
+#pragma unroll
+      for (int r = 0; r < 2; r++) {
+        const double dd0 = ((double)e.obs[2 * r] - (l0 * N[r]) / (ln * ln)) / ln;
+        const double dd1 = ((double)e.obs[2 * r + 1] - (l1 * N[r]) / (ln * ln)) / ln;
+        const double dd2 = 1.0 / ln;
+        double M[3];
+#pragma unroll
+        for (int k = 0; k < 3; k++) M[k] = dd0 * A[0][k] + dd1 * A[1][k] + dd2 * A[2][k];
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+          J[r][k] = -(M[0] * Sn[0][k] + M[1] * Sn[1][k] + M[2] * Sn[2][k]);
+          J[r][3 + k] = -(M[0] * Sv[0][k] + M[1] * Sv[1][k] + M[2] * Sv[2][k]);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 6; k++) J[2][k] = 0.0;
+      return;
+    }
     const double e2 = (double)e.obs[2] * l0 + (double)e.obs[3] * l1 + l2;
     // pinned P7: row 0 = end-point values, row 1 = 0
     const double d0 = ((double)e.obs[2] - (l0 * e2) / (ln * ln)) / ln;
@@ -970,6 +999,7 @@ struct PoseArgs {
   uint8_t* t_loutlier;
   int lpitch;
   int prof;                   // debug: phase stamps of stream 0 into g_pose_prof
+  int fixed_line_jac;         // ORBPL_POSE_FIXED_LINE_JAC
 };
 
 // debug (ORBPL_POSE_PROFILE): accumulated wall-clock ticks (100 MHz) of
@@ -1003,7 +1033,7 @@ __global__ void __launch_bounds__(256, ORBPL_POSE_MINW) k_pose(TrackConsts tc, P
     if (t == 0) a.ninliers[(long long)s * a.nm_stride] = 0;
     return;
   }
-  const PoseCam c{tc.fx, tc.fy, tc.cx, tc.cy, tc.bf};
+  const PoseCam c{tc.fx, tc.fy, tc.cx, tc.cy, tc.bf, a.fixed_line_jac};
   const bool stamp = a.prof && s == 0 && t == 0;
   long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   long long t0 = stamp ? (long long)wall_clock64() : 0;
@@ -1546,6 +1576,7 @@ void launch_pose(const TrackConsts& c, const PoseLaunch& p, int nstreams, hipStr
   a.t_nl = p.t_nl;
   a.t_loutlier = p.t_loutlier;
   a.lpitch = p.lpitch;
+  a.fixed_line_jac = p.fixed_line_jac;
   static const int prof = getenv("ORBPL_POSE_PROFILE") ? 1 : 0;
   a.prof = prof;
   hipLaunchKernelGGL(k_pose, dim3(nstreams), dim3(256), sizeof(PoseShared), s, c, a);

@@ -202,7 +202,14 @@ int orbm_search_by_projection_last(const orbpl_camera* cam, const float* scale_f
 
 int orbpl_pose_optimization(const orbpl_camera* cam, const orbpl_pose_problem* P, float* Tcw,
                             uint8_t* outlier, uint8_t* line_outlier, int* n_inliers) {
+  return orbpl_pose_optimization_ex(cam, P, 0, Tcw, outlier, line_outlier, n_inliers);
+}
+
+int orbpl_pose_optimization_ex(const orbpl_camera* cam, const orbpl_pose_problem* P, int flags,
+                               float* Tcw, uint8_t* outlier, uint8_t* line_outlier,
+                               int* n_inliers) {
   if (!cam || !P || !Tcw || !n_inliers) return arg_fail("NULL argument");
+  if (flags & ~ORBPL_POSE_FIXED_LINE_JAC) return arg_fail("unknown pose flag");
   const int n = P->n, nl = P->nl;
   if (n < 0 || nl < 0 || n + nl > kPoseMaxEdges) return arg_fail("too many edges (max 2304)");
   if (n > 0 && (!P->kps_un || !P->uright || !P->has_mp || !P->mp_xyz || !outlier))
@@ -265,6 +272,7 @@ int orbpl_pose_optimization(const orbpl_camera* cam, const orbpl_pose_problem* P
   p.nm_stride = 1;
   p.active = nullptr;
   p.edges = reinterpret_cast<PoseEdge*>(d_edges.p);
+  p.fixed_line_jac = (flags & ORBPL_POSE_FIXED_LINE_JAC) ? 1 : 0;
   launch_pose(c, p, 1, scratch_stream());
   HIP_CHECK(hipGetLastError());
   HIP_CHECK(hipMemcpy(Tcw, d_T.p, 64, hipMemcpyDeviceToHost));
@@ -763,6 +771,7 @@ struct orbpl_tracker {
   // right extractor's stream, concurrently with the left one; the batched
   // ComputeStereoMatches then fills depth / uRight on the extraction stream
   int stereo = 0;
+  int fixed_line_jac = 0;          // ORBPL_TRACK_FIXED_LINE_JAC
   orbx_ctx* exr = nullptr;
   hipStream_t rstream = nullptr;   // owned by exr
   hipEvent_t ev_rin = nullptr;     // step start on `stream`
@@ -847,7 +856,8 @@ int orbpl_tracker_create(const orbpl_orb_params* orb, const orbpl_camera* cam, i
 int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam, int n_streams,
                             int device, int flags, orbpl_tracker** out) {
   if (!orb || !cam || !out || n_streams <= 0) return arg_fail("bad argument");
-  if (flags & ~(ORBPL_TRACK_LINES | ORBPL_TRACK_STEREO)) return arg_fail("unknown tracker flag");
+  if (flags & ~(ORBPL_TRACK_LINES | ORBPL_TRACK_STEREO | ORBPL_TRACK_FIXED_LINE_JAC))
+    return arg_fail("unknown tracker flag");
   // ORBPL_TRACK_LINES | ORBPL_TRACK_STEREO: the defined stereo line mode (P17;
   // the reference's stereo Frame extracts no lines, Frame.cc:70-131)
   if ((flags & ORBPL_TRACK_STEREO) && cam->height > 1024)
@@ -857,6 +867,7 @@ int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam
   t->device = device;
   t->lines = (flags & ORBPL_TRACK_LINES) ? 1 : 0;
   t->stereo = (flags & ORBPL_TRACK_STEREO) ? 1 : 0;
+  t->fixed_line_jac = (flags & ORBPL_TRACK_FIXED_LINE_JAC) ? 1 : 0;
   t->S = n_streams;
   t->W = cam->width;
   t->H = cam->height;
@@ -1212,6 +1223,7 @@ static int tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_
     p.t_loutlier = C.loutlier;
     p.lpitch = kLineKeep;
   }
+  p.fixed_line_jac = t->fixed_line_jac;
   launch_pose(t->consts, p, S, ts);
   HIP_CHECK(hipEventRecord(ev[9], ts));
   LineFinish lf{};

@@ -87,22 +87,26 @@ def _pose_problem(seed, stereo=True, lines=0, outliers=0.0, pert=(0.02, 0.02)):
 @pytest.mark.parametrize("case", [
     dict(seed=0), dict(seed=1, stereo=False), dict(seed=2, outliers=0.15),
     dict(seed=0, lines=40), dict(seed=1, lines=60, outliers=0.1), dict(seed=2, pert=(0.08, 0.05)),
+    dict(seed=0, lines=40, fixed=True), dict(seed=1, lines=60, outliers=0.1, fixed=True),
 ])
 def test_pose_optimization_parity(case, orbpl, oracle):
+    case = dict(case)
+    fixed = case.pop("fixed", False)
     cfg, cam_o, prob, T_init, T_true = _pose_problem(**case)
     cam_g = orbpl.make_camera(cfg)
     n = len(prob["kps_un"])
     nl = len(prob.get("kl_obs", ()))
     out0 = np.zeros(n, np.uint8)
     lout0 = np.zeros(nl, np.uint8)
-    Tg, og, log_, ng = orbpl.pose_optimization(cam_g, prob, T_init, out0, lout0)
-    To, oo, loo, no = oracle.pose_optimization(cam_o, prob, T_init, out0, lout0)
+    Tg, og, log_, ng = orbpl.pose_optimization(cam_g, prob, T_init, out0, lout0, fixed)
+    To, oo, loo, no = oracle.pose_optimization(cam_o, prob, T_init, out0, lout0, fixed)
     assert np.abs(Tg - To).max() < POSE_TOL, np.abs(Tg - To).max()
     assert ng == no
     assert np.array_equal(og, oo)
     assert np.array_equal(log_, loo)
-    if not case.get("lines"):
-        assert np.abs(To[:3, 3] - T_true[:3, 3]).max() < 0.01   # converged near the truth
+    if not case.get("lines") or fixed:
+        # converged near the truth (the as-written line Jacobian, P7, pulls off it)
+        assert np.abs(To[:3, 3] - T_true[:3, 3]).max() < 0.01
 
 
 def test_pose_too_few_correspondences(orbpl, oracle):
@@ -181,16 +185,18 @@ def test_tracker_pipelined_matches_oracle_vo(orbpl, oracle):
         assert np.abs(st["Tcw"][s] - To).max() < POSE_TOL, s
 
 
-@pytest.mark.parametrize("pipelined", [False, True])
-def test_tracker_with_lines_matches_oracle_lvo(orbpl, oracle, pipelined):
+@pytest.mark.parametrize("pipelined,fixed", [(False, False), (True, False), (False, True)])
+def test_tracker_with_lines_matches_oracle_lvo(orbpl, oracle, pipelined, fixed):
     """Point+line tracker (ORBPL_TRACK_LINES) against the oracle LVO loop:
     identical point and line counts every frame, pose within POSE_TOL, and
     the last frame's undistorted KeyLines / LBD rows bit-exact."""
     S, F = 3, 5
     seqs = [sequence(F, 30 + s) for s in range(S)]
     cfg = seqs[0][0]
-    lvo = oracle.LVO(oracle.params(), oracle.camera(cfg), S, use_lines=True)
-    tr = orbpl.Tracker(orbpl.OrbParams(1000, 1.2, 8, 20, 7), orbpl.make_camera(cfg), S, lines=True)
+    lvo = oracle.LVO(oracle.params(), oracle.camera(cfg), S, use_lines=True,
+                     flags=oracle.TRACK_FIXED_LINE_JAC if fixed else 0)
+    tr = orbpl.Tracker(orbpl.OrbParams(1000, 1.2, 8, 20, 7), orbpl.make_camera(cfg), S, lines=True,
+                       fixed_line_jac=fixed)
     tr.set_pipelined(pipelined)
     T0 = np.stack([np.linalg.inv(sq[1][0]).astype(np.float32) for sq in seqs])
     lvo.reset(T0.reshape(S, 16))
