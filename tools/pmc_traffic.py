@@ -8,7 +8,8 @@ gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts half
 the bytes of wide coalesced reads, so fetch_bytes = 2 * FETCH_SIZE; WRITE_SIZE
 is taken as is. Both counters are in KiB.
 
-usage: python tools/pmc_traffic.py <tag> <round> [streams]
+usage: python tools/pmc_traffic.py <tag> <round> [streams] [workload]
+(workload: points -> pmc_traffic_points.json, lines, kitti, ...)
 """
 import collections
 import csv
@@ -48,9 +49,10 @@ def main():
         out[k] = {"launches": len(v), "avg_ns": sum(v) / len(v),
                   "fetch_bytes": fb, "write_bytes": wb,
                   "traffic_bytes": (fb + wb) if fb is not None and wb is not None else None}
-    out["_meta"] = {"streams": int(sys.argv[3]) if len(sys.argv) > 3 else 256,
+    wl = sys.argv[4] if len(sys.argv) > 4 else "points"
+    out["_meta"] = {"streams": int(sys.argv[3]) if len(sys.argv) > 3 else 256, "workload": wl,
                     "source": f"gpurun_out/prof_{tag}", "correction": "fetch x2 (gfx950)"}
-    dst = ROOT / "profiles" / rnd / "pmc_traffic.json"
+    dst = ROOT / "profiles" / rnd / f"pmc_traffic_{wl}.json"
     dst.parent.mkdir(parents=True, exist_ok=True)
     json.dump(out, open(dst, "w"), indent=1, sort_keys=True)
     for k in sorted((k for k in out if k != "_meta"),
