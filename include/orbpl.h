@@ -335,6 +335,15 @@ int orbpl_tracker_create(const orbpl_orb_params* orb, const orbpl_camera* cam, i
  * passes the angle / length / row-overlap / disparity tests,
  * then the RGB-D line path (line matching, line edges, map lines). */
 #define ORBPL_TRACK_STEREO 2
+/* ORBPL_TRACK_LOCAL_MAP: Tracking::TrackLocalMap after TrackWithMotionModel
+ * (Tracking.cc:1332-1420): the local map is the map points / lines of the last
+ * 4 frames (every tracked frame is a keyframe) minus those the
+ * frame already holds or rejected; SearchLocalPoints (IsInFrustum 0.5,
+ * ORBmatcher(0.8).SearchByProjection th 3 RGB-D / 1 stereo, 5 for the first
+ * frames), SearchLocalLines (LineMatcher(0.8) local-map overload with its
+ * relaxed retry), a second PoseOptimizationWithLines over all matches and the
+ * mnMatchesInliers / mnLineMatchesInliers decision. */
+#define ORBPL_TRACK_LOCAL_MAP 4
 /* ORBPL_TRACK_FIXED_LINE_JAC: PoseOptimizationWithLines with the analytic line
  * Jacobian (ORBPL_POSE_FIXED_LINE_JAC) in every tracker pose. */
 #define ORBPL_TRACK_FIXED_LINE_JAC 8

@@ -444,8 +444,25 @@ static void unproject(const orbpl_camera& c, const float* T, const float* Ow, fl
   }
 }
 
+// One keyframe's map in the local map (ORBPL_TRACK_LOCAL_MAP): every tracked
+// frame is a keyframe whose map points are its keypoints with depth, with
+// MapPoint::UpdateNormalAndDepth's normal and scale-invariance distances
+// (MapPoint.cc:329-372, one observation; pinned P18).
+struct KFMap {
+  int n = 0, nl = 0;
+  std::vector<float> xyz, normal, dmin, dmax;  // dmin / dmax: Get{Min,Max}DistanceInvariance
+  std::vector<uint8_t> has, desc;
+  std::vector<float> lxyz;
+  std::vector<uint8_t> lhas, ldesc;
+};
+constexpr int kLocalKFs = 4;   // the local keyframes: the last 4 frames (P18)
+
 struct LStream {
   bool has_last = false, has_velocity = false;
+  int frame_id = 0;            // Frame::mnId
+  std::vector<KFMap> local;    // most recent first, at most kLocalKFs
+  int lm[4] = {0, 0, 0, 0};    // last step: local point matches, point inliers,
+                               // local line matches, line inliers
   float Tcw[16], Tlast[16], Tlast2[16];
   std::vector<orbpl_keypoint> kps_un;
   std::vector<uint8_t> desc, has_mp, outlier;
@@ -510,6 +527,195 @@ int oracle_lvo_reset(void* h, const float* Tcw0) {
 }  // extern "C"
 
 namespace line_track {
+
+// Pose problem of the current frame from per-keypoint / per-line world
+// positions (has* = an edge) and PoseOptimizationWithLines on it.
+static int optimize_pose(LVO* v, LStream& S, int n, const std::vector<orbpl_keypoint>& ku,
+                         const std::vector<float>& ur, const std::vector<uint8_t>& has,
+                         const std::vector<float>& xyz, int nl,
+                         const std::vector<orbpl_keyline>& klu, const std::vector<uint8_t>& hasl,
+                         const std::vector<float>& lxyz, std::vector<uint8_t>& outl,
+                         std::vector<uint8_t>& loutl) {
+  std::vector<float> lobs((size_t)nl * 4, 0.f);
+  std::vector<int32_t> loct(nl, 0);
+  for (int j = 0; j < nl; j++) {
+    loct[j] = klu[j].octave;
+    lobs[4 * j] = klu[j].startPointX;
+    lobs[4 * j + 1] = klu[j].startPointY;
+    lobs[4 * j + 2] = klu[j].endPointX;
+    lobs[4 * j + 3] = klu[j].endPointY;
+  }
+  orbpl_pose_problem P{};
+  P.n = n;
+  P.kps_un = ku.data();
+  P.uright = ur.data();
+  P.has_mp = has.data();
+  P.mp_xyz = xyz.data();
+  P.nl = nl;
+  P.kl_obs = lobs.data();
+  P.kl_octave = loct.data();
+  P.has_ml = hasl.data();
+  P.ml_xyz = lxyz.data();
+  P.inv_sigma2 = v->inv_sigma2.data();
+  P.nlevels = (int)v->inv_sigma2.size();
+  int ninl = 0;
+  oracle_pose_optimization_ex(&v->cam, &P,
+                              (v->flags & ORBPL_TRACK_FIXED_LINE_JAC) ? ORBPL_POSE_FIXED_LINE_JAC : 0,
+                              S.Tcw, outl.data(), loutl.data(), &ninl);
+  return ninl;
+}
+
+// Tracking::TrackLocalMap (Tracking.cc:1332-1420) with the defined local map
+// P18: the local keyframes are the last kLocalKFs frames (most recent
+// first), the local map points / lines their map points / lines in index
+// order, minus those the current frame already holds or that the motion
+// model rejected as outliers (mnLastFrameSeen, Tracking.cc:1285-1292,
+// 1750-1768). SearchLocalPoints (:1746-1813): IsInFrustum(pMP, 0.5) at the
+// optimised pose, ORBmatcher(0.8).SearchByProjection with th = 3 (RGB-D) /
+// 1 (stereo), 5 while mnId < mnLastRelocFrameId + 2; SearchLocalLines
+// (:1816-1865): IsInFrustum(pML, 0.5), LineMatcher(0.8).SearchByProjection(F,
+// local lines) with its relaxed retry (which wipes every current line
+// assignment first). Then PoseOptimizationWithLines over all matches and the
+// inlier decision (:1396-1419; mnLastRelocFrameId = 0, mMaxFrames = 30).
+static bool track_local_map(LVO* v, LStream& S, bool stereo, int n,
+                            const std::vector<orbpl_keypoint>& ku, const std::vector<uint8_t>& desc,
+                            const std::vector<float>& ur, const std::vector<int32_t>& match,
+                            const std::vector<int32_t>& match_pre, int nl,
+                            const std::vector<orbpl_keyline>& klu,
+                            const std::vector<uint8_t>& ldesc, const std::vector<int32_t>& lmatch,
+                            const std::vector<int32_t>& lmatch_pre) {
+  const orbpl_camera& cam = v->cam;
+  const int K = (int)S.local.size();
+  const int nlev = (int)v->scale.size();
+  // ---- SearchLocalPoints ----
+  std::vector<uint8_t> seen0(K ? S.local[0].n : 0, 0);
+  for (int i = 0; i < n; i++)
+    if (match_pre[i] >= 0) seen0[match_pre[i]] = 1;
+  std::vector<int32_t> cur_nobs(n);
+  for (int i = 0; i < n; i++) cur_nobs[i] = match[i] >= 0 ? 1 : 0;
+  std::vector<float> Lx, Ln, Lmin, Lmax;
+  std::vector<uint8_t> Ld;
+  for (int k = 0; k < K; k++) {
+    const KFMap& m = S.local[k];
+    for (int j = 0; j < m.n; j++) {
+      if (!m.has[j] || (k == 0 && seen0[j])) continue;
+      Lx.insert(Lx.end(), &m.xyz[3 * j], &m.xyz[3 * j] + 3);
+      Ln.insert(Ln.end(), &m.normal[3 * j], &m.normal[3 * j] + 3);
+      Lmin.push_back(m.dmin[j]);
+      Lmax.push_back(m.dmax[j]);
+      Ld.insert(Ld.end(), &m.desc[32 * j], &m.desc[32 * j] + 32);
+    }
+  }
+  const int nloc = (int)Lmin.size();
+  std::vector<uint8_t> inview(nloc);
+  std::vector<float> px(nloc), py(nloc), pxr(nloc), vcos(nloc);
+  std::vector<int32_t> lev(nloc), mp_nobs(nloc, 1), lm(n, -1);
+  const float log_scale = (float)lsdm::log_((double)v->orb.scale_factor);   // P15
+  oracle_frame_is_in_frustum(&cam, log_scale, nlev, S.Tcw, nloc, Lx.data(), Ln.data(), Lmin.data(),
+                             Lmax.data(), 0.5f, inview.data(), px.data(), py.data(), pxr.data(),
+                             lev.data(), vcos.data());
+  int nto = 0;
+  for (int i = 0; i < nloc; i++) nto += inview[i];
+  int nlocal = 0;
+  if (nto > 0) {
+    const float th = S.frame_id < 2 ? 5.0f : (stereo ? 1.0f : 3.0f);
+    orbpl_match_current cur{n, S.Tcw, ku.data(), desc.data(), ur.data()};
+    oracle_search_by_projection_local(&cam, v->scale.data(), nlev, &cur, nloc, inview.data(),
+                                      px.data(), py.data(), pxr.data(), lev.data(), vcos.data(),
+                                      Ld.data(), mp_nobs.data(), cur_nobs.data(), th, 0.8f,
+                                      lm.data(), &nlocal);
+  }
+  // ---- SearchLocalLines ----
+  std::vector<float> LLx;
+  std::vector<uint8_t> LLd;
+  std::vector<int32_t> llm(nl, -1);
+  int nllocal = 0, wiped = 0;
+  if (v->use_lines) {
+    std::vector<uint8_t> seen0l(K ? S.local[0].nl : 0, 0);
+    for (int j = 0; j < nl; j++)
+      if (lmatch_pre[j] >= 0) seen0l[lmatch_pre[j]] = 1;
+    std::vector<int32_t> cur_nobs_l(nl);
+    for (int j = 0; j < nl; j++) cur_nobs_l[j] = lmatch[j] >= 0 ? 1 : 0;
+    for (int k = 0; k < K; k++) {
+      const KFMap& m = S.local[k];
+      for (int j = 0; j < m.nl; j++) {
+        if (!m.lhas[j] || (k == 0 && seen0l[j])) continue;
+        LLx.insert(LLx.end(), &m.lxyz[6 * j], &m.lxyz[6 * j] + 6);
+        LLd.insert(LLd.end(), &m.ldesc[32 * j], &m.ldesc[32 * j] + 32);
+      }
+    }
+    const int nll = (int)LLd.size() / 32;
+    std::vector<uint8_t> lvalid(nll);
+    oracle_line_is_in_frustum(S.Tcw, nll, LLx.data(), lvalid.data());
+    int ntol = 0;
+    for (int i = 0; i < nll; i++) ntol += lvalid[i];
+    if (ntol > 0)
+      oracle_line_search_by_projection_list(&cam, S.Tcw, nl, klu.data(), ldesc.data(),
+                                            cur_nobs_l.data(), nll, lvalid.data(), LLx.data(),
+                                            LLd.data(), llm.data(), &nllocal, &wiped);
+  }
+  // ---- PoseOptimizationWithLines over every match ----
+  std::vector<uint8_t> has(n, 0), hasl(nl, 0), outl(n, 0), loutl(nl, 0);
+  std::vector<float> xyz((size_t)n * 3, 0.f), lxyz((size_t)nl * 6, 0.f);
+  for (int i = 0; i < n; i++) {
+    const float* src = match[i] >= 0 ? &S.xyz[3 * match[i]] : lm[i] >= 0 ? &Lx[3 * lm[i]] : nullptr;
+    if (!src) continue;
+    has[i] = 1;
+    for (int k = 0; k < 3; k++) xyz[3 * i + k] = src[k];
+  }
+  for (int j = 0; j < nl; j++) {
+    const float* src = (!wiped && lmatch[j] >= 0) ? &S.lxyz[6 * lmatch[j]]
+                       : llm[j] >= 0             ? &LLx[6 * llm[j]]
+                                                 : nullptr;
+    if (!src) continue;
+    hasl[j] = 1;
+    for (int k = 0; k < 6; k++) lxyz[6 * j + k] = src[k];
+  }
+  optimize_pose(v, S, n, ku, ur, has, xyz, nl, klu, hasl, lxyz, outl, loutl);
+  int inl = 0, linl = 0;
+  for (int i = 0; i < n; i++) inl += has[i] && !outl[i];
+  for (int j = 0; j < nl; j++) linl += hasl[j] && !loutl[j];
+  S.lm[0] = nlocal;
+  S.lm[1] = inl;
+  S.lm[2] = nllocal;
+  S.lm[3] = linl;
+  if (S.frame_id < 30 && inl + linl < 60) return false;
+  return !(inl < 30 && linl < 20);
+}
+
+// The current frame joins the local map as its newest keyframe (its map
+// points / lines were just created from depth in S.xyz / S.lxyz).
+static void push_local_kf(LVO* v, LStream& S, const float* Ow,
+                          const std::vector<orbpl_keypoint>& ku, const std::vector<uint8_t>& desc,
+                          const std::vector<uint8_t>& ldesc) {
+  KFMap m;
+  m.n = (int)ku.size();
+  m.xyz = S.xyz;
+  m.has = S.has_mp;
+  m.desc = desc;
+  m.normal.assign((size_t)m.n * 3, 0.f);
+  m.dmin.assign(m.n, 0.f);
+  m.dmax.assign(m.n, 0.f);
+  const int nlev = (int)v->scale.size();
+  for (int i = 0; i < m.n; i++) {
+    if (!m.has[i]) continue;
+    const float PO[3] = {m.xyz[3 * i] - Ow[0], m.xyz[3 * i + 1] - Ow[1], m.xyz[3 * i + 2] - Ow[2]};
+    const double nd = std::sqrt((double)PO[0] * PO[0] + (double)PO[1] * PO[1] + (double)PO[2] * PO[2]);
+    const float inv = (float)(1.0 / nd);
+    for (int k = 0; k < 3; k++) m.normal[3 * i + k] = PO[k] * inv;
+    const float dist = (float)nd;
+    const float maxd = dist * v->scale[ku[i].octave];
+    const float mind = maxd / v->scale[nlev - 1];
+    m.dmax[i] = 1.2f * maxd;
+    m.dmin[i] = 0.8f * mind;
+  }
+  m.nl = (int)S.has_ml.size();
+  m.lxyz = S.lxyz;
+  m.lhas = S.has_ml;
+  m.ldesc = ldesc;
+  S.local.insert(S.local.begin(), std::move(m));
+  if ((int)S.local.size() > kLocalKFs) S.local.pop_back();
+}
 
 // One TrackWithMotionModel step. RGB-D (right == NULL): Frame(imGray, imDepth)
 // (Frame.cc:135-205). Stereo (right != NULL): Frame(imLeft, imRight)
@@ -597,7 +803,8 @@ static int lvo_step(LVO* v, int stream, const uint8_t* gray, const float* depth,
   std::vector<int32_t> match(n, -1), lmatch(nl, -1);
   std::vector<uint8_t> outl(n, 0), loutl(nl, 0);
   int nmatches = 0, ninl = 0, nmap = 0, nlm = 0, lnmap = 0;
-  bool tracked = false;
+  bool tracked = false, motion_ok = false, local_ok = true;
+  S.lm[0] = S.lm[1] = S.lm[2] = S.lm[3] = 0;
   if (S.has_last) {
     if (S.has_velocity) {
       float Twl[16], V[16];
@@ -660,6 +867,7 @@ static int lvo_step(LVO* v, int stream, const uint8_t* gray, const float* depth,
                                   (v->flags & ORBPL_TRACK_FIXED_LINE_JAC) ? ORBPL_POSE_FIXED_LINE_JAC : 0,
                                   S.Tcw, outl.data(), loutl.data(), &ninl);
     }
+    const std::vector<int32_t> match_pre = match, lmatch_pre = lmatch;
     // outlier discard (Tracking.cc:1273-1314); without an optimisation every
     // flag is clear and the counts report the raw matches
     for (int i = 0; i < n; i++)
@@ -676,6 +884,10 @@ static int lvo_step(LVO* v, int stream, const uint8_t* gray, const float* depth,
           lnmap++;
         }
       }
+    motion_ok = tracked && (v->use_lines ? (nmap >= 10 || lnmap >= 15) : nmap >= 10);
+    if ((v->flags & ORBPL_TRACK_LOCAL_MAP) && motion_ok)
+      local_ok = track_local_map(v, S, right != nullptr, n, ku, desc, ur, match, match_pre, nl, klu,
+                                 ldesc, lmatch, lmatch_pre);
   }
   // this frame becomes the keyframe of the next one
   float Ow[3];
@@ -704,9 +916,10 @@ static int lvo_step(LVO* v, int stream, const uint8_t* gray, const float* depth,
       unproject(cam, S.Tcw, Ow, klu[j].endPointX, klu[j].endPointY, lds[j], &S.lxyz[6 * j + 3]);
       S.has_ml[j] = 1;
     }
+  if (v->flags & ORBPL_TRACK_LOCAL_MAP) push_local_kf(v, S, Ow, ku, desc, ldesc);
   bool ok = true;
-  if (S.has_last)
-    ok = tracked && (v->use_lines ? (nmap >= 10 || lnmap >= 15) : nmap >= 10);
+  if (S.has_last) ok = motion_ok && local_ok;
+  S.frame_id++;
   memcpy(S.Tlast2, S.Tlast, 64);
   memcpy(S.Tlast, S.Tcw, 64);
   S.has_velocity = S.has_last;
@@ -731,7 +944,16 @@ int oracle_lvo_step(void* h, int stream, const uint8_t* gray, const float* depth
                               Tcw_out, out8);
 }
 
-// Stereo TrackWithMotionModel step (points only, see lvo_step).
+// TrackLocalMap counts of the stream's last step (ORBPL_TRACK_LOCAL_MAP):
+// local point matches, point inliers (mnMatchesInliers), local line matches,
+// line inliers (mnLineMatchesInliers); zeros when it did not run.
+int oracle_lvo_local_stats(void* h, int stream, int* out4) {
+  const line_track::LStream& S = static_cast<line_track::LVO*>(h)->st[stream];
+  for (int k = 0; k < 4; k++) out4[k] = S.lm[k];
+  return 0;
+}
+
+// Stereo TrackWithMotionModel step (see lvo_step).
 int oracle_lvo_step_stereo(void* h, int stream, const uint8_t* left, const uint8_t* right,
                            float* Tcw_out, int* out8) {
   return line_track::lvo_step(static_cast<line_track::LVO*>(h), stream, left, nullptr, right,

@@ -495,6 +495,7 @@ def _setup(L):  # noqa: F811
     L.oracle_lvo_reset.argtypes = [vp, vp]
     L.oracle_lvo_step.argtypes = [vp, i, vp, vp, vp, vp]
     L.oracle_lvo_step_stereo.argtypes = [vp, i, vp, vp, vp, vp]
+    L.oracle_lvo_local_stats.argtypes = [vp, i, vp]
 
 
 def line_frame_prepare(cam, kl, depth=None):
@@ -586,6 +587,14 @@ class LVO:
         keys = ("nkeypoints", "nmatches", "ninliers", "nmatches_map", "ok", "nlines",
                 "line_matches", "line_nmatches_map")
         return T.reshape(4, 4), dict(zip(keys, (int(x) for x in o)))
+
+    def local_stats(self, stream):
+        """TrackLocalMap counts of the stream's last step: local point matches,
+        point inliers, local line matches, line inliers."""
+        o = np.zeros(4, np.int32)
+        lib().oracle_lvo_local_stats(self.h, stream, _p(o))
+        return dict(zip(("local_matches", "local_inliers", "local_line_matches",
+                         "local_line_inliers"), (int(x) for x in o)))
 
     def step_stereo(self, stream, left, right):
         """Stereo Frame + TrackWithMotionModel (th = 7); with lines the defined

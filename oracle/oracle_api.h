@@ -94,6 +94,7 @@ void oracle_lvo_destroy(void* h);
 int oracle_lvo_reset(void* h, const float* Tcw0);
 int oracle_lvo_step(void* h, int stream, const uint8_t* gray, const float* depth, float* Tcw_out,
                     int* out8);
+int oracle_lvo_local_stats(void* h, int stream, int* out4);
 int oracle_lvo_step_stereo(void* h, int stream, const uint8_t* left, const uint8_t* right,
                            float* Tcw_out, int* out8);
 #ifdef __cplusplus
