@@ -212,45 +212,51 @@ def pmc_traffic(kernel, workload, streams):
     return None, None
 
 
-def oracle_vo(O, wl):
-    """The oracle's VO loop for a workload; returns (vo, step(vo, s, a, b))."""
+def oracle_flags(O, args):
+    return ((O.TRACK_LOCAL_MAP if args.local_map else 0) |
+            (O.TRACK_FIXED_LINE_JAC if args.fixed_line_jacobian else 0))
+
+
+def oracle_vo(O, wl, flags=0):
+    """The oracle's tracking loop for a workload (oracle/line_track_oracle.cpp
+    LVO with the tracker's flags); returns (vo, step(vo, a, b))."""
     import orbpl.synth as synth
     cam = O.camera(getattr(synth, wl["cam"]))
+    vo = O.LVO(O.params(*wl["orb"]), cam, 1, use_lines=wl["lines"], flags=flags)
     if wl["stereo"]:
-        return (O.LVO(O.params(*wl["orb"]), cam, 1, use_lines=wl["lines"]),
-                lambda vo, a, b: vo.step_stereo(0, a, b))
-    if wl["lines"]:
-        return O.LVO(O.params(*wl["orb"]), cam, 1, use_lines=True), lambda vo, a, b: vo.step(0, a, b)
-    return O.VO(O.params(*wl["orb"]), cam, 1), lambda vo, a, b: vo.step(0, a, b)
+        return vo, lambda vo, a, b: vo.step_stereo(0, a, b)
+    return vo, lambda vo, a, b: vo.step(0, a, b)
 
 
 OUT8 = ("nkeypoints", "nmatches", "ninliers", "nmatches_map", "ok", "nlines", "line_matches",
-        "line_nmatches_map")
+        "line_nmatches_map", "local_matches", "local_inliers", "local_line_matches",
+        "local_line_inliers")
 
 
-def parity_check(T_gpu, C_gpu, streams, gray, depth, L, workload):
+def parity_check(T_gpu, C_gpu, streams, gray, depth, L, workload, flags=0):
     """Replay `streams` of the timed tracker on the CPU oracle over the same
-    frames (one host thread per stream) and compare every step: the 8 counts
-    exactly, the pose to POSE_TOL. T_gpu[k]: (n, 4, 4), C_gpu[k]: (n, 8)."""
+    frames (one host thread per stream) and compare every step: the 12 counts
+    exactly, the pose to POSE_TOL. T_gpu[k]: (n, 4, 4), C_gpu[k]: (n, 12)."""
     from _pkg import load_oracle
     import orbpl.tum as tum
     O = load_oracle()
     wl = WORKLOADS[workload]
     n = min(len(T) for T in T_gpu)
     T_ref = np.zeros((len(streams), n, 4, 4), np.float32)
-    C_ref = np.zeros((len(streams), n, 8), np.int32)
+    C_ref = np.zeros((len(streams), n, 12), np.int32)
 
     errors = []
 
     def worker(k, s):
         try:
-            vo, vstep = oracle_vo(O, wl)
+            vo, vstep = oracle_vo(O, wl, flags)
             vo.reset(np.linalg.inv(L.Twc(s, 0)).astype(np.float32).reshape(1, 16))
             for t in range(n):
                 e = L.elem(s, t)
                 T, st = vstep(vo, gray[e], depth[e])
+                st.update(vo.local_stats(0))
                 T_ref[k, t] = T
-                C_ref[k, t] = [st.get(key, 0) for key in OUT8]   # VO: no line counts
+                C_ref[k, t] = [st[key] for key in OUT8]
         except Exception as ex:  # surface, do not let a thread swallow it
             errors.append(ex)
 
@@ -322,7 +328,8 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
     d_gray = pkg.DeviceBuffer.from_array(gray[rep], device=device)
     d_depth = pkg.DeviceBuffer.from_array(depth[rep], device=device)
     cam = pkg.make_camera(getattr(synth, cam_name))
-    tr = pkg.Tracker(pkg.OrbParams(*wl["orb"]), cam, S, device=device, lines=lines, stereo=stereo)
+    tr = pkg.Tracker(pkg.OrbParams(*wl["orb"]), cam, S, device=device, lines=lines, stereo=stereo,
+                     local_map=bool(args.local_map), fixed_line_jac=bool(args.fixed_line_jacobian))
     # pipelining overlaps extraction of step t+1 with tracking of step t; the
     # LSD-bound line workloads gain nothing from it
     pipelined = args.pipelined if args.pipelined >= 0 else (0 if lines else 1)
@@ -363,6 +370,13 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
                 "mean_matches": float(st["nmatches"].mean()),
                 "mean_inliers": float(st["ninliers"].mean()),
                 "ok_frac": float(tr.status()["ok"].mean())}
+    if args.local_map:
+        lst = tr.local_stats()
+        tracking.update(mean_local_matches=float(lst["local_matches"].mean()),
+                        mean_local_inliers=float(lst["local_inliers"].mean()))
+        if lines:
+            tracking.update(mean_local_line_matches=float(lst["local_line_matches"].mean()),
+                            mean_local_line_inliers=float(lst["local_line_inliers"].mean()))
     if lines:
         lt = tr.line_timings(steps).mean(0)
         stages.update(zip(tr.LINE_STAGES, [round(float(x), 4) for x in lt]))
@@ -431,7 +445,7 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
                 pipelined=bool(pipelined))
 
 
-def sweep(pkg, synth, workload, sizes, steps, device):
+def sweep(pkg, synth, workload, sizes, steps, device, local_map=True):
     """Per-step latency and throughput at several batch sizes (untimed for the
     headline; each size gets its own tracker, 1 warm-up step)."""
     wl = WORKLOADS[workload]
@@ -447,7 +461,7 @@ def sweep(pkg, synth, workload, sizes, steps, device):
         d_gray = pkg.DeviceBuffer.from_array(gray[rep], device=device)
         d_depth = pkg.DeviceBuffer.from_array(depth[rep], device=device)
         tr = pkg.Tracker(pkg.OrbParams(*wl["orb"]), cam, S, device=device, lines=wl["lines"],
-                         stereo=wl["stereo"])
+                         stereo=wl["stereo"], local_map=local_map)
         tr.set_pipelined(not wl["lines"])
         tr.reset(np.stack([np.linalg.inv(L.Twc(s, 0)).astype(np.float32)
                            for s in range(S)]).reshape(S, 16))
@@ -509,7 +523,7 @@ def host_info():
             "usable_cores": usable}
 
 
-def cpu_baseline(seconds, threads, gray, depth, L, workload="points"):
+def cpu_baseline(seconds, threads, gray, depth, L, workload="points", flags=0):
     """Throughput mode (BASELINE.md §2 mode 2): the CPU oracle running the
     same per-frame step, one stream per host thread, for a bounded wall time."""
     from _pkg import load_oracle
@@ -519,7 +533,7 @@ def cpu_baseline(seconds, threads, gray, depth, L, workload="points"):
     stop = time.time() + seconds
 
     def worker(k):
-        vo, vstep = oracle_vo(O, wl)
+        vo, vstep = oracle_vo(O, wl, flags)
         i = 0
         while time.time() < stop:   # worker k runs stream k of the layout
             e = L.elem(k, i)
@@ -537,7 +551,7 @@ def cpu_baseline(seconds, threads, gray, depth, L, workload="points"):
     return sum(counts) / dt, sum(counts), dt
 
 
-def cpu_reference_faithful(seconds, gray, depth, L, workload):
+def cpu_reference_faithful(seconds, gray, depth, L, workload, flags=0):
     """BASELINE.md §2 mode 1: one stream as the reference runs it, ORB and
     the LineExtractor on two host threads per frame (Frame.cc:152-155),
     matching and pose on the tracking thread; per-frame latency."""
@@ -546,7 +560,7 @@ def cpu_reference_faithful(seconds, gray, depth, L, workload):
     O = load_oracle()
     wl = WORKLOADS[workload]
     cam = O.camera(getattr(synth, wl["cam"]))
-    vo = O.LVO(O.params(*wl["orb"]), cam, 1, use_lines=wl["lines"], flags=O.TWO_THREADS)
+    vo = O.LVO(O.params(*wl["orb"]), cam, 1, use_lines=wl["lines"], flags=O.TWO_THREADS | flags)
     vo.reset(np.linalg.inv(L.Twc(0, 0)).astype(np.float32).reshape(1, 16))
     lat = []
     stop = time.time() + seconds
@@ -612,6 +626,13 @@ def main():
     ap.add_argument("--sweep", type=int, default=1,
                     help="1 = per-step latency / fps at batch 1..1024 (points) and 1..256 "
                          "(lines) after the timed runs (points runs, rank 0 only)")
+    ap.add_argument("--local-map", type=int, default=1,
+                    help="1 = every step runs TrackWithMotionModel + TrackLocalMap (the "
+                         "reference's per-frame Track, Tracking.cc:1332-1420; local map = the "
+                         "last 4 frames, DESIGN.md P18); 0 = TrackWithMotionModel only")
+    ap.add_argument("--fixed-line-jacobian", type=int, default=0,
+                    help="1 = the analytic line-edge Jacobian instead of the reference's "
+                         "as-written one (pinned P7)")
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the oracle replay of the timed trackers' sampled streams")
     args = ap.parse_args()
@@ -664,19 +685,21 @@ def main():
             continue
         r["parity"] = gather_parity(dist, world, parity_check(
             [h[0] for h in r["hist"]], [h[1] for h in r["hist"]], r["samp"], r["gray"], r["depth"],
-            r["layout"], r["wname"]))
+            r["layout"], r["wname"], oracle_flags(O, args)))
 
     sweeps = None
     if rank == 0 and world == 1 and args.sweep and args.workload == "points":
-        sweeps = {"points": sweep(pkg, synth, "points", (1, 16, 64, 256, 1024), 5, device),
-                  "lines": sweep(pkg, synth, "lines", (1, 16, 64, 256), 2, device)}
+        lmf = bool(args.local_map)
+        sweeps = {"points": sweep(pkg, synth, "points", (1, 16, 64, 256, 1024), 5, device, lmf),
+                  "lines": sweep(pkg, synth, "lines", (1, 16, 64, 256), 2, device, lmf)}
 
     cpu = None
     host = host_info()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         thr = args.cpu_threads or host["usable_cores"]
+        ofl = oracle_flags(O, args)
         fps, nfr, dt = cpu_baseline(args.cpu_seconds, thr, res["gray"], res["depth"],
-                                    res["layout"], args.workload)
+                                    res["layout"], args.workload, ofl)
         cpu = {"value": round(fps, 2), "unit": "frames/s", "cores": thr, "kind": "port",
                "sample": f"{nfr} frames of the same {res['image']} loop in {dt:.1f} s, oracle/ "
                          f"C++ restatement ({args.workload} workload), one stream per thread",
@@ -685,7 +708,7 @@ def main():
                "host": host,
                "reference_faithful": cpu_reference_faithful(args.cpu_seconds / 4, res["gray"],
                                                             res["depth"], res["layout"],
-                                                            args.workload)}
+                                                            args.workload, ofl)}
 
     if rank == 0:
         S = res["S"]
@@ -705,7 +728,8 @@ def main():
             "config": {"workload": res["workload"],
                        "image": res["image"], "nfeatures": res["nfeatures"], "streams_per_gpu": S,
                        "frames_per_step": S * world, "parallelism": f"streams sharded x{world}",
-                       "pipelined": res["pipelined"]},
+                       "pipelined": res["pipelined"], "track_local_map": bool(args.local_map),
+                       "fixed_line_jacobian": bool(args.fixed_line_jacobian)},
             "stage_ms": res["stages"],
             "tracking": res["tracking"],
             "roofline": res["roof"],
@@ -725,13 +749,13 @@ def main():
             if cpu is not None:
                 thr = cpu["cores"]
                 fps, nfr, dt = cpu_baseline(args.cpu_seconds / 2, thr, o["gray"], o["depth"],
-                                            o["layout"], o["wname"])
+                                            o["layout"], o["wname"], ofl)
                 out[key]["cpu_baseline"] = {
                     "value": round(fps, 2), "unit": "frames/s", "cores": thr, "kind": "port",
                     "sample": f"{nfr} frames in {dt:.1f} s, oracle/ C++ restatement "
                               f"({o['wname']} workload), one stream per thread",
                     "reference_faithful": cpu_reference_faithful(
-                        args.cpu_seconds / 4, o["gray"], o["depth"], o["layout"], o["wname"])}
+                        args.cpu_seconds / 4, o["gray"], o["depth"], o["layout"], o["wname"], ofl)}
         print(json.dumps(out))
     if dist:
         dist.destroy_process_group()

@@ -372,8 +372,10 @@ int orbpl_tracker_get_state(orbpl_tracker* tr, float* Tcw, int* nkeypoints, int*
 /* hipEvent times of the last step (ms): extract, glue, match, pose, finish. */
 int orbpl_tracker_stage_ms(orbpl_tracker* tr, float* ms5);
 /* Per-kernel device times (ms, hipEvents on the tracker stream) of the last
- * min(max_steps, 64) steps, 9 per step: pyramid (8 launches), blur, fast,
- * octree, orient+desc, glue+predict, match, pose, finish. */
+ * min(max_steps, 64) steps, 10 per step: pyramid (+ borders + blur, one
+ * launch), blur (0), fast, octree, orient+desc, glue+predict, match, pose,
+ * finish, local_map (TrackLocalMap: gather, IsInFrustum, local point and line
+ * search, second pose, counts; 0 without ORBPL_TRACK_LOCAL_MAP). */
 int orbpl_tracker_timings(orbpl_tracker* tr, int max_steps, float* ms, int* n_steps);
 int orbpl_tracker_timings_reset(orbpl_tracker* tr);
 /* Debug (ORBPL_POSE_PROFILE set): stream 0's PoseOptimization phase times of
@@ -408,12 +410,18 @@ int orbpl_tracker_line_timings(orbpl_tracker* tr, int max_steps, float* ms, int*
  * the end of each step (no host synchronisation inside a step): the next
  * max_steps steps after the call are kept (0 = off; a new call clears it).
  * get_history returns stream `stream`'s first min(max_steps, recorded) steps:
- * Tcw (16 floats per step) and 8 counts per step in the oracle's order:
+ * Tcw (16 floats per step) and 12 counts per step in the oracle's order:
  * nkeypoints, nmatches, ninliers, nmatches_map, ok, nlines, line_matches,
- * line_nmatches_map. */
+ * line_nmatches_map, then the TrackLocalMap counts (0 when it did not run):
+ * local matches, mnMatchesInliers, local line matches, mnLineMatchesInliers. */
 int orbpl_tracker_set_history(orbpl_tracker* tr, int max_steps);
 int orbpl_tracker_get_history(orbpl_tracker* tr, int stream, int max_steps, float* Tcw,
-                              int* counts8, int* n_steps);
+                              int* counts12, int* n_steps);
+/* TrackLocalMap outcome of the last step per stream (ORBPL_TRACK_LOCAL_MAP; 0
+ * where it did not run): SearchLocalPoints matches, mnMatchesInliers,
+ * SearchLocalLines matches (every passing pair counts), mnLineMatchesInliers. */
+int orbpl_tracker_get_local_stats(orbpl_tracker* tr, int* local_matches, int* local_inliers,
+                                  int* local_line_matches, int* local_line_inliers);
 /* LSD / LineExtractor kernel times (ms) of the last min(max_steps, 64) steps,
  * 7 per step (line stream): k_lsd_blur + k_lsd_resize + k_lsd_grad, the
  * pseudo-ordering sort (k_lsd_sort + k_lsd_sort_local), the seed loop

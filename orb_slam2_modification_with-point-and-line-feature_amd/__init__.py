@@ -360,6 +360,7 @@ def _declare_track(L):
     L.orbpl_tracker_lsd_timings.argtypes = [vp, i, vp, ip]
     L.orbpl_tracker_set_history.argtypes = [vp, i]
     L.orbpl_tracker_get_history.argtypes = [vp, i, i, vp, vp, ip]
+    L.orbpl_tracker_get_local_stats.argtypes = [vp, vp, vp, vp, vp]
 
 
 _declare_orig = _declare
@@ -676,6 +677,14 @@ class Tracker:
               "orbpl_tracker_get_status")
         return dict(ok=ok, nlines=nl, line_matches=lm, line_nmatches_map=lnm)
 
+    def local_stats(self):
+        """TrackLocalMap counts per stream of the last step (local_map=True)."""
+        S = self.S
+        a, b, c, d = (np.zeros(S, np.int32) for _ in range(4))
+        check(lib().orbpl_tracker_get_local_stats(self._h, _ptr(a), _ptr(b), _ptr(c), _ptr(d)),
+              "orbpl_tracker_get_local_stats")
+        return dict(local_matches=a, local_inliers=b, local_line_matches=c, local_line_inliers=d)
+
     def lines(self, stream):
         """Undistorted KeyLines, LBD rows, line match, line outlier of one stream."""
         K = 80
@@ -720,11 +729,12 @@ class Tracker:
         check(lib().orbpl_tracker_set_history(self._h, int(max_steps)), "orbpl_tracker_set_history")
 
     def history(self, stream, max_steps=4096):
-        """(Tcw (n,4,4), counts (n,8)) of one stream's recorded steps; counts in
-        the oracle's out8 order (nkeypoints, nmatches, ninliers, nmatches_map,
-        ok, nlines, line_matches, line_nmatches_map)."""
+        """(Tcw (n,4,4), counts (n,12)) of one stream's recorded steps; counts in
+        the oracle's order (nkeypoints, nmatches, ninliers, nmatches_map, ok,
+        nlines, line_matches, line_nmatches_map, local_matches, local_inliers,
+        local_line_matches, local_line_inliers)."""
         T = np.zeros((max_steps, 4, 4), np.float32)
-        cnt = np.zeros((max_steps, 8), np.int32)
+        cnt = np.zeros((max_steps, 12), np.int32)
         n = C.c_int(0)
         check(lib().orbpl_tracker_get_history(self._h, stream, max_steps, _ptr(T), _ptr(cnt),
                                               C.byref(n)), "orbpl_tracker_get_history")
@@ -747,11 +757,11 @@ class Tracker:
         return ms
 
     STAGES = ("pyramid", "blur", "fast", "octree", "orient_desc", "glue", "match", "pose",
-              "finish")
+              "finish", "local_map")
 
     def timings(self, max_steps=64):
-        """(n_steps, 9) per-kernel ms of the last steps (hipEvents in-stream)."""
-        ms = np.zeros((max_steps, 9), np.float32)
+        """(n_steps, 10) per-kernel ms of the last steps (hipEvents in-stream)."""
+        ms = np.zeros((max_steps, 10), np.float32)
         n = C.c_int(0)
         check(lib().orbpl_tracker_timings(self._h, max_steps, _ptr(ms), C.byref(n)),
               "orbpl_tracker_timings")

@@ -414,7 +414,44 @@ void launch_stereo_lines(const TrackConsts& c, const StereoLineArgs& a, int nstr
 // pair is tested; per current line the last passing projected line wins
 // (atomicMax), every pass counts.
 __global__ void __launch_bounds__(256) k_line_match_list(TrackConsts c, LineListArgs a) {
+  if (a.ncur_arr) {  // batched: stream blockIdx.x
+    const int b = blockIdx.x;
+    const long long co = (long long)b * a.cur_pitch, mo = (long long)b * a.ml_pitch;
+    a.ncur = a.ncur_arr[b];
+    a.nml = a.nml_arr[b];
+    a.Tcw += (long long)b * a.pose_stride;
+    a.cur_kl_un += co;
+    a.cur_desc += co * 32;
+    if (a.cur_nobs) a.cur_nobs += co;
+    a.match += co;
+    a.valid += mo;
+    a.ml_xyz6 += mo * 6;
+    a.ml_desc += mo * 32;
+    a.proj_kl += mo;
+    a.proj_src += mo;
+    a.nmatches += (long long)b * a.nm_stride;
+    if (a.wiped) a.wiped += (long long)b * a.nm_stride;
+  }
   __shared__ int s_wc[4];
+  __shared__ int s_nto;
+  if (a.ncur_arr) {
+    // SearchLocalLines calls the matcher only when some local line is in the
+    // frustum (nToMatch > 0, Tracking.cc:1851)
+    if (threadIdx.x == 0) s_nto = 0;
+    __syncthreads();
+    int v = 0;
+    for (int i = threadIdx.x; i < a.nml; i += 256) v |= a.valid[i];
+    if (v) s_nto = 1;
+    __syncthreads();
+    if (!s_nto) {
+      for (int j = threadIdx.x; j < a.ncur; j += 256) a.match[j] = -1;
+      if (threadIdx.x == 0) {
+        *a.nmatches = 0;
+        if (a.wiped) *a.wiped = 0;
+      }
+      return;
+    }
+  }
   __shared__ int s_np, s_cnt;
   __shared__ int s_last[kLineKeep];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -491,8 +528,37 @@ __global__ void k_line_in_frustum(const float* __restrict__ Tcw, int n, const fl
   in_view[i] = !(z[0] < 0.0f && z[1] < 0.0f);
 }
 
-void launch_line_match_list(const TrackConsts& c, const LineListArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_line_match_list, dim3(1), dim3(256), 0, s, c, a);
+void launch_line_match_list(const TrackConsts& c, const LineListArgs& a, hipStream_t s,
+                            int nstreams) {
+  hipLaunchKernelGGL(k_line_match_list, dim3(a.ncur_arr ? nstreams : 1), dim3(256), 0, s, c, a);
+}
+
+__global__ void k_line_in_frustum_b(const float* __restrict__ Tcw, int pose_stride,
+                                    const int* __restrict__ n_arr, long long pitch,
+                                    const float* __restrict__ xyz6, uint8_t* __restrict__ in_view) {
+  const int b = blockIdx.y;
+  const long long o = (long long)b * pitch;
+  const float* T = Tcw + (long long)b * pose_stride;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n_arr[b]) return;
+  float z[2];
+#pragma unroll
+  for (int e = 0; e < 2; e++) {
+    const float* X = xyz6 + (o + i) * 6 + 3 * e;
+    double s = (double)T[8] * X[0];
+    s += (double)T[9] * X[1];
+    s += (double)T[10] * X[2];
+    z[e] = (float)(s + (double)T[11]);
+  }
+  in_view[o + i] = !(z[0] < 0.0f && z[1] < 0.0f);
+}
+
+void launch_line_in_frustum_batched(const float* Tcw, int pose_stride, const int* n_arr,
+                                    long long pitch, const float* xyz6, uint8_t* in_view,
+                                    int nstreams, hipStream_t s) {
+  if (pitch <= 0) return;
+  hipLaunchKernelGGL(k_line_in_frustum_b, dim3((unsigned)((pitch + 255) / 256), nstreams), dim3(256), 0,
+                     s, Tcw, pose_stride, n_arr, pitch, xyz6, in_view);
 }
 
 void launch_line_in_frustum(const float* Tcw, int n, const float* xyz6, uint8_t* in_view,

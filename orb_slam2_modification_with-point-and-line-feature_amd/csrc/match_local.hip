@@ -26,6 +26,22 @@ namespace orbpl {
 
 __global__ void __launch_bounds__(256) k_in_frustum(TrackConsts c, float log_scale, InFrustumArgs a) {
   const int i = blockIdx.x * 256 + threadIdx.x;
+  if (a.n_arr) {  // batched: stream blockIdx.y
+    const int b = blockIdx.y;
+    const long long o = (long long)b * a.pitch;
+    a.n = a.n_arr[b];
+    a.Tcw += (long long)b * a.pose_stride;
+    a.xyz += o * 3;
+    a.normal += o * 3;
+    a.min_dist += o;
+    a.max_dist += o;
+    a.in_view += o;
+    a.proj_x += o;
+    a.proj_y += o;
+    a.proj_xr += o;
+    a.level += o;
+    a.view_cos += o;
+  }
   if (i >= a.n) return;
   a.in_view[i] = 0;
   a.proj_x[i] = 0.f;
@@ -154,6 +170,27 @@ __device__ Top2 local_scan(const LocalShared& S, const TrackConsts& c, const Loc
 }  // namespace
 
 __global__ void __launch_bounds__(256) k_match_local(TrackConsts c, LocalArgs a) {
+  if (a.n_arr) {  // batched: stream blockIdx.x
+    const int b = blockIdx.x;
+    const long long ko = (long long)b * a.kp_pitch, mo = (long long)b * a.mp_pitch;
+    a.n = a.n_arr[b];
+    a.nmp = a.nmp_arr[b];
+    a.kps_un += ko;
+    a.desc += ko * 32;
+    a.uright += ko;
+    if (a.cur_nobs) a.cur_nobs += ko;
+    a.match += ko;
+    a.in_view += mo;
+    a.proj_x += mo;
+    a.proj_y += mo;
+    a.proj_xr += mo;
+    a.level += mo;
+    a.view_cos += mo;
+    a.mp_desc += mo * 32;
+    if (a.mp_nobs) a.mp_nobs += mo;
+    a.scratch += mo;
+    a.nmatches += (long long)b * a.nm_stride;
+  }
   extern __shared__ char smem_local[];
   LocalShared& S = *reinterpret_cast<LocalShared*>(smem_local);
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
@@ -246,7 +283,7 @@ __global__ void __launch_bounds__(256) k_match_local(TrackConsts c, LocalArgs a)
         r.sd = (int)(short)(v.w & 0xFFFF);
         r.sl = (int)(short)(v.w >> 16);
       }
-      const int nobs = i < a.nmp ? a.mp_nobs[i] : 0;
+      const int nobs = i < a.nmp ? (a.mp_nobs ? a.mp_nobs[i] : 1) : 0;
       bool decided = !(i < a.nmp && r.bi >= 0);
       int start = 0;
       while (true) {
@@ -290,14 +327,17 @@ __global__ void __launch_bounds__(256) k_match_local(TrackConsts c, LocalArgs a)
 }
 
 void launch_in_frustum(const TrackConsts& c, float log_scale, const InFrustumArgs& a,
-                       hipStream_t s) {
-  if (a.n <= 0) return;
-  hipLaunchKernelGGL(k_in_frustum, dim3((a.n + 255) / 256), dim3(256), 0, s, c, log_scale, a);
+                       hipStream_t s, int nstreams) {
+  const long long n = a.n_arr ? a.pitch : a.n;
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_in_frustum, dim3((unsigned)((n + 255) / 256), a.n_arr ? nstreams : 1),
+                     dim3(256), 0, s, c, log_scale, a);
 }
 
-void launch_match_local(const TrackConsts& c, const LocalArgs& a, hipStream_t s) {
+void launch_match_local(const TrackConsts& c, const LocalArgs& a, hipStream_t s, int nstreams) {
   set_smem_attr((const void*)k_match_local, sizeof(LocalShared));
-  hipLaunchKernelGGL(k_match_local, dim3(1), dim3(256), sizeof(LocalShared), s, c, a);
+  hipLaunchKernelGGL(k_match_local, dim3(a.n_arr ? nstreams : 1), dim3(256), sizeof(LocalShared), s,
+                     c, a);
 }
 
 

@@ -126,6 +126,15 @@ struct StreamState {
   int ok;              // TrackWithMotionModel success
   int nlmatches;       // LineMatcher::SearchByProjection result (lines enabled)
   int nlmatches_map;   // line inliers minus outliers (Tracking.cc:1298-1314)
+  // TrackLocalMap (ORBPL_TRACK_LOCAL_MAP)
+  int lm_active;       // TrackWithMotionModel succeeded: the local map step runs
+  int lm_nlocal;       // SearchLocalPoints matches
+  int lm_nllocal;      // SearchLocalLines matches (every passing pair counts)
+  int lm_wiped;        // the line matcher's relaxed retry cleared the line assignments
+  int lm_ninl;         // second PoseOptimization's return value
+  int lm_inl;          // mnMatchesInliers
+  int lm_linl;         // mnLineMatchesInliers
+  int lm_ok;           // TrackLocalMap's decision
 };
 
 }  // namespace orbpl

@@ -71,6 +71,7 @@ struct PoseLaunch {
   uint8_t* t_loutlier;
   int lpitch;
   int fixed_line_jac;           // ORBPL_POSE_FIXED_LINE_JAC (analytic line Jacobian)
+  int gate_lm;                  // 1: run only streams with active[s].lm_active (TrackLocalMap)
 };
 
 // Per-frame line buffers of the tracker (kLineKeep lines per stream).
@@ -126,10 +127,25 @@ struct LineListArgs {
   int* match;                    // per current line: map line index or -1 (unchanged / wiped)
   int* nmatches;
   int* wiped;                    // 1 when the relaxed retry ran (all assignments cleared first)
+  // batched (tracker TrackLocalMap): block s reads ncur_arr[s] / nml_arr[s]
+  // and offsets the current-line arrays by s * cur_pitch, the map-line
+  // arrays and scratch by s * ml_pitch, Tcw by s * pose_stride, the outputs
+  // nmatches / wiped by s * nm_stride. NULL ncur_arr = one frame.
+  const int* ncur_arr;
+  const int* nml_arr;
+  long long cur_pitch;
+  long long ml_pitch;
+  int pose_stride;
+  int nm_stride;
 };
-void launch_line_match_list(const TrackConsts& c, const LineListArgs& a, hipStream_t s);
+void launch_line_match_list(const TrackConsts& c, const LineListArgs& a, hipStream_t s,
+                            int nstreams = 1);
 void launch_line_in_frustum(const float* Tcw, int n, const float* xyz6, uint8_t* in_view,
                             hipStream_t s);
+// batched: stream b = blockIdx.y tests n_arr[b] lines at xyz6 + b * pitch * 6
+void launch_line_in_frustum_batched(const float* Tcw, int pose_stride, const int* n_arr,
+                                    long long pitch, const float* xyz6, uint8_t* in_view,
+                                    int nstreams, hipStream_t s);
 
 void launch_line_prepare(const TrackConsts& c, const LineTrackArgs& a, int nstreams,
                          hipStream_t s);
@@ -151,6 +167,11 @@ struct InFrustumArgs {
   float* proj_xr;
   int* level;              // mnTrackScaleLevel
   float* view_cos;         // mTrackViewCos
+  // batched (tracker TrackLocalMap): stream b = blockIdx.y reads n_arr[b]
+  // points at offset b * pitch of every array and Tcw + b * pose_stride
+  const int* n_arr;
+  long long pitch;
+  int pose_stride;
 };
 
 // ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th).
@@ -174,6 +195,14 @@ struct LocalArgs {
   int* match;              // per keypoint: last local map point assigned, -1
   int* nmatches;
   int4* scratch;           // nmp entries
+  // batched (tracker TrackLocalMap): block b reads n_arr[b] / nmp_arr[b],
+  // offsets the keypoint arrays by b * kp_pitch, the map point arrays and
+  // scratch by b * mp_pitch, nmatches by b * nm_stride; mp_nobs NULL = 1
+  const int* n_arr;
+  const int* nmp_arr;
+  long long kp_pitch;
+  long long mp_pitch;
+  int nm_stride;
 };
 
 // ORBmatcher::SearchByBoW(KeyFrame*, Frame&) with per-feature node ids.
@@ -226,8 +255,9 @@ struct StereoArgs {
 void launch_stereo(const StereoArgs& a, int batch, hipStream_t s);
 
 void launch_in_frustum(const TrackConsts& c, float log_scale, const InFrustumArgs& a,
-                       hipStream_t s);
-void launch_match_local(const TrackConsts& c, const LocalArgs& a, hipStream_t s);
+                       hipStream_t s, int nstreams = 1);
+void launch_match_local(const TrackConsts& c, const LocalArgs& a, hipStream_t s,
+                        int nstreams = 1);
 
 size_t match_smem_bytes();
 size_t pose_smem_bytes();
@@ -243,6 +273,73 @@ void launch_pose(const TrackConsts& c, const PoseLaunch& p, int nstreams, hipStr
 int read_pose_profile(long long* out8);
 // debug: stream 0 phase ticks of the last k_match_last launch (ORBPL_MATCH_PROFILE)
 int read_match_profile(long long* out8);
+// TrackLocalMap for the batched tracker (local_map.hip). Per stream s:
+// keypoint arrays at s * kp_pitch, line arrays at s * kLineKeep, the ring of
+// the last K keyframes at (s * K + slot) * kp_pitch (lines: * kLineKeep), the
+// gathered local lists at s * lp (lines: s * llp).
+struct LocalMapArgs {
+  StreamState* st;
+  int kp_pitch;
+  int lines;
+  // current frame: motion-model matches / outliers, map after k_finish
+  const int* n;
+  const int* match;
+  const uint8_t* outlier;
+  const int* nl;
+  const int* lmatch;
+  const uint8_t* loutlier;
+  const KeyPointD* kps_un;
+  const uint8_t* desc;
+  const uint8_t* ldesc;
+  const uint8_t* has_mp;
+  const float* mp_xyz;
+  const uint8_t* has_ml;
+  const float* ml_xyz;
+  // last frame's map (motion-model matches point into it)
+  const float* last_xyz;
+  const float* last_lxyz;
+  // keyframe ring
+  int K, nslots, head, push_slot;
+  float* r_xyz;
+  float* r_nrm;
+  float* r_dmin;
+  float* r_dmax;
+  uint8_t* r_has;
+  uint8_t* r_desc;
+  int* r_n;
+  float* rl_xyz;
+  uint8_t* rl_has;
+  uint8_t* rl_desc;
+  int* rl_n;
+  // gathered local lists
+  long long lp, llp;
+  float* l_xyz;
+  float* l_nrm;
+  float* l_dmin;
+  float* l_dmax;
+  uint8_t* l_desc;
+  int* l_n;
+  float* ll_xyz;
+  uint8_t* ll_desc;
+  int* ll_n;
+  int* cur_nobs;
+  int* cur_nobs_l;
+  // local search results
+  const int* lm_match;
+  const int* llm_match;
+  // the second pose's inputs / outputs
+  int* match2;
+  float* xyz2;
+  int* lmatch2;
+  float* lxyz2;
+  uint8_t* outlier2;
+  uint8_t* loutlier2;
+};
+void launch_lm_gather(const LocalMapArgs& a, int nstreams, hipStream_t s);
+void launch_lm_assemble(const LocalMapArgs& a, int nstreams, hipStream_t s);
+void launch_lm_count(const LocalMapArgs& a, int frame_id, int nstreams, hipStream_t s);
+void launch_lm_push(const TrackConsts& c, const LocalMapArgs& a, int nstreams, hipStream_t s);
+
 // Line part of k_finish (all NULL when lines are disabled).
 struct LineFinish {
   const int* nl;
@@ -258,6 +355,6 @@ struct LineFinish {
 void launch_finish(const TrackConsts& c, StreamState* st, const int* n, int kp_pitch,
                    const KeyPointD* kps_un, const float* depth, int* match, uint8_t* outlier,
                    uint8_t* has_mp, float* mp_xyz, int* nobs, const LineFinish& lf, int nstreams,
-                   hipStream_t s);
+                   hipStream_t s, int local_map = 0);
 
 }  // namespace orbpl

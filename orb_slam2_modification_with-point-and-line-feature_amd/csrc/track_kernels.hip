@@ -1000,6 +1000,7 @@ struct PoseArgs {
   int lpitch;
   int prof;                   // debug: phase stamps of stream 0 into g_pose_prof
   int fixed_line_jac;         // ORBPL_POSE_FIXED_LINE_JAC
+  int gate_lm;                // run only active[s].lm_active streams
 };
 
 // debug (ORBPL_POSE_PROFILE): accumulated wall-clock ticks (100 MHz) of
@@ -1028,8 +1029,10 @@ __global__ void __launch_bounds__(256, ORBPL_POSE_MINW) k_pose(TrackConsts tc, P
   // TrackWithMotionModel returns before optimising when no last frame exists
   // or nmatches < 20 after the retry (Tracking.cc:1255-1265).
   // (with lines: also when LineMatcher found < 15, Tracking.cc:1260-1265)
-  if (a.active && (!a.active[s].has_last || a.active[s].nmatches < 20 ||
-                   (a.t_kl_un && a.active[s].nlmatches < 15))) {
+  // TrackLocalMap's pose runs only where TrackWithMotionModel succeeded
+  if (a.gate_lm ? !a.active[s].lm_active
+                : (a.active && (!a.active[s].has_last || a.active[s].nmatches < 20 ||
+                                (a.t_kl_un && a.active[s].nlmatches < 15)))) {
     if (t == 0) a.ninliers[(long long)s * a.nm_stride] = 0;
     return;
   }
@@ -1389,7 +1392,8 @@ __global__ void __launch_bounds__(256) k_finish(TrackConsts c, StreamState* __re
                                                 uint8_t* __restrict__ outlier,
                                                 uint8_t* __restrict__ has_mp,
                                                 float* __restrict__ mp_xyz,
-                                                int* __restrict__ nobs, LineFinish lf) {
+                                                int* __restrict__ nobs, LineFinish lf,
+                                                int local_map) {
   const int s = blockIdx.x, t = threadIdx.x;
   StreamState& S = st[s];
   const int n = n_in[s];
@@ -1474,6 +1478,9 @@ __global__ void __launch_bounds__(256) k_finish(TrackConsts c, StreamState* __re
       S.nlmatches_map = 0;
       S.ok = S.has_last ? (S.nmatches >= 20 && s_map >= 10) : 1;
     }
+    // TrackLocalMap runs after a successful TrackWithMotionModel and decides
+    // the frame's outcome (Tracking.cc:433-436)
+    if (local_map && S.has_last) S.ok = S.ok && S.lm_ok;
     for (int k = 0; k < 16; k++) {
       S.Tlast2[k] = S.Tlast[k];
       S.Tlast[k] = S.Tcw[k];
@@ -1577,6 +1584,7 @@ void launch_pose(const TrackConsts& c, const PoseLaunch& p, int nstreams, hipStr
   a.t_loutlier = p.t_loutlier;
   a.lpitch = p.lpitch;
   a.fixed_line_jac = p.fixed_line_jac;
+  a.gate_lm = p.gate_lm;
   static const int prof = getenv("ORBPL_POSE_PROFILE") ? 1 : 0;
   a.prof = prof;
   hipLaunchKernelGGL(k_pose, dim3(nstreams), dim3(256), sizeof(PoseShared), s, c, a);
@@ -1585,9 +1593,9 @@ void launch_pose(const TrackConsts& c, const PoseLaunch& p, int nstreams, hipStr
 void launch_finish(const TrackConsts& c, StreamState* st, const int* n, int kp_pitch,
                    const KeyPointD* kps_un, const float* depth, int* match, uint8_t* outlier,
                    uint8_t* has_mp, float* mp_xyz, int* nobs, const LineFinish& lf, int nstreams,
-                   hipStream_t s) {
+                   hipStream_t s, int local_map) {
   hipLaunchKernelGGL(k_finish, dim3(nstreams), dim3(256), 0, s, c, st, n, kp_pitch, kps_un, depth,
-                     match, outlier, has_mp, mp_xyz, nobs, lf);
+                     match, outlier, has_mp, mp_xyz, nobs, lf, local_map);
 }
 
 }  // namespace orbpl

@@ -795,9 +795,38 @@ struct orbpl_tracker {
   StreamState* d_state = nullptr;
   PoseEdge* d_edges = nullptr;
   static constexpr int kRing = 64;   // steps kept in the timing ring
-  static constexpr int kEv = 26;     // events per step
+  static constexpr int kEv = 27;     // events per step
   std::vector<hipEvent_t> ring;      // kRing * kEv events
   int ring_pos = 0, ring_count = 0;
+  // TrackLocalMap (ORBPL_TRACK_LOCAL_MAP): ring of the last kLmK keyframes'
+  // maps, the gathered local lists and the second pose's buffers
+  static constexpr int kLmK = 4;
+  int local_map = 0;
+  int lm_step = 0;                 // frames since reset (Frame::mnId)
+  float scale_factor = 1.2f;
+  long long lp = 0, llp = 0;
+  float *kr_xyz = nullptr, *kr_nrm = nullptr, *kr_dmin = nullptr, *kr_dmax = nullptr;
+  uint8_t *kr_has = nullptr, *kr_desc = nullptr;
+  int* kr_n = nullptr;
+  float* rl_xyz = nullptr;
+  uint8_t *rl_has = nullptr, *rl_desc = nullptr;
+  int* rl_n = nullptr;
+  float *l_xyz = nullptr, *l_nrm = nullptr, *l_dmin = nullptr, *l_dmax = nullptr;
+  uint8_t* l_desc = nullptr;
+  int* l_n = nullptr;
+  uint8_t* l_inview = nullptr;
+  float *l_px = nullptr, *l_py = nullptr, *l_pxr = nullptr, *l_vcos = nullptr;
+  int* l_level = nullptr;
+  int4* l_scratch = nullptr;
+  float* ll_xyz = nullptr;
+  uint8_t *ll_desc = nullptr, *ll_valid = nullptr;
+  int* ll_n = nullptr;
+  orbpl_keyline* ll_proj = nullptr;
+  int* ll_src = nullptr;
+  int *cur_nobs = nullptr, *cur_nobs_l = nullptr, *lm_match = nullptr, *llm_match = nullptr;
+  int *match2 = nullptr, *lmatch2 = nullptr;
+  float *xyz2 = nullptr, *lxyz2 = nullptr;
+  uint8_t *outlier2 = nullptr, *loutlier2 = nullptr;
   // per-step history (orbpl_tracker_set_history): StreamState and keypoint /
   // line counts of every stream after each step, device-side D2D copies on
   // the tracking stream (no host synchronisation inside a step)
@@ -856,7 +885,8 @@ int orbpl_tracker_create(const orbpl_orb_params* orb, const orbpl_camera* cam, i
 int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam, int n_streams,
                             int device, int flags, orbpl_tracker** out) {
   if (!orb || !cam || !out || n_streams <= 0) return arg_fail("bad argument");
-  if (flags & ~(ORBPL_TRACK_LINES | ORBPL_TRACK_STEREO | ORBPL_TRACK_FIXED_LINE_JAC))
+  if (flags & ~(ORBPL_TRACK_LINES | ORBPL_TRACK_STEREO | ORBPL_TRACK_LOCAL_MAP |
+                ORBPL_TRACK_FIXED_LINE_JAC))
     return arg_fail("unknown tracker flag");
   // ORBPL_TRACK_LINES | ORBPL_TRACK_STEREO: the defined stereo line mode (P17;
   // the reference's stereo Frame extracts no lines, Frame.cc:70-131)
@@ -868,6 +898,8 @@ int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam
   t->lines = (flags & ORBPL_TRACK_LINES) ? 1 : 0;
   t->stereo = (flags & ORBPL_TRACK_STEREO) ? 1 : 0;
   t->fixed_line_jac = (flags & ORBPL_TRACK_FIXED_LINE_JAC) ? 1 : 0;
+  t->local_map = (flags & ORBPL_TRACK_LOCAL_MAP) ? 1 : 0;
+  t->scale_factor = orb->scale_factor;
   t->S = n_streams;
   t->W = cam->width;
   t->H = cam->height;
@@ -926,6 +958,54 @@ int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam
     }
   }
   TA(t->d_state, S * sizeof(StreamState));
+  if (t->local_map) {
+    const size_t R = S * orbpl_tracker::kLmK * K, RL = S * orbpl_tracker::kLmK * kLineKeep;
+    t->lp = (long long)orbpl_tracker::kLmK * K;
+    t->llp = (long long)orbpl_tracker::kLmK * kLineKeep;
+    const size_t LP = S * (size_t)t->lp, LLP = S * (size_t)t->llp;
+    TA(t->kr_xyz, R * 12);
+    TA(t->kr_nrm, R * 12);
+    TA(t->kr_dmin, R * 4);
+    TA(t->kr_dmax, R * 4);
+    TA(t->kr_has, R);
+    TA(t->kr_desc, R * 32);
+    TA(t->kr_n, S * orbpl_tracker::kLmK * 4);
+    TA(t->l_xyz, LP * 12);
+    TA(t->l_nrm, LP * 12);
+    TA(t->l_dmin, LP * 4);
+    TA(t->l_dmax, LP * 4);
+    TA(t->l_desc, LP * 32);
+    TA(t->l_n, S * 4);
+    TA(t->l_inview, LP);
+    TA(t->l_px, LP * 4);
+    TA(t->l_py, LP * 4);
+    TA(t->l_pxr, LP * 4);
+    TA(t->l_vcos, LP * 4);
+    TA(t->l_level, LP * 4);
+    TA(t->l_scratch, LP * sizeof(int4));
+    TA(t->cur_nobs, S * K * 4);
+    TA(t->lm_match, S * K * 4);
+    TA(t->match2, S * K * 4);
+    TA(t->xyz2, S * K * 12);
+    TA(t->outlier2, S * K);
+    if (t->lines) {
+      TA(t->rl_xyz, RL * 24);
+      TA(t->rl_has, RL);
+      TA(t->rl_desc, RL * 32);
+      TA(t->rl_n, S * orbpl_tracker::kLmK * 4);
+      TA(t->ll_xyz, LLP * 24);
+      TA(t->ll_desc, LLP * 32);
+      TA(t->ll_valid, LLP);
+      TA(t->ll_n, S * 4);
+      TA(t->ll_proj, LLP * sizeof(orbpl_keyline));
+      TA(t->ll_src, LLP * 4);
+      TA(t->cur_nobs_l, S * kLineKeep * 4);
+      TA(t->llm_match, S * kLineKeep * 4);
+      TA(t->lmatch2, S * kLineKeep * 4);
+      TA(t->lxyz2, S * kLineKeep * 24);
+      TA(t->loutlier2, S * kLineKeep);
+    }
+  }
   TA(t->d_edges, S * kPoseMaxEdges * pose_edge_bytes());
   if (t->stereo) {
     // a right keypoint spans at most 4 * scale + 2 <= 18 rows (8 levels of 1.2)
@@ -1028,6 +1108,7 @@ int orbpl_tracker_reset(orbpl_tracker* t, const float* Tcw0) {
   HIP_CHECK(hipMemcpy(t->d_state, st.data(), sizeof(StreamState) * t->S, hipMemcpyHostToDevice));
   if (t->d_err) HIP_CHECK(hipMemset(t->d_err, 0, 4));
   t->hist_count = 0;
+  t->lm_step = 0;
   return ORBPL_OK;
 }
 
@@ -1226,6 +1307,132 @@ static int tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_
   p.fixed_line_jac = t->fixed_line_jac;
   launch_pose(t->consts, p, S, ts);
   HIP_CHECK(hipEventRecord(ev[9], ts));
+  LocalMapArgs lm{};
+  if (t->local_map) {
+    // ---- TrackLocalMap (Tracking.cc:1332-1420), defined local map P18 ----
+    const int K4 = orbpl_tracker::kLmK, fid = t->lm_step;
+    lm.st = t->d_state;
+    lm.kp_pitch = K;
+    lm.lines = t->lines;
+    lm.n = C.n;
+    lm.match = C.match;
+    lm.outlier = C.outlier;
+    lm.nl = C.nl;
+    lm.lmatch = C.lmatch;
+    lm.loutlier = C.loutlier;
+    lm.kps_un = C.kps_un;
+    lm.desc = C.desc;
+    lm.ldesc = C.ldesc;
+    lm.has_mp = C.has_mp;
+    lm.mp_xyz = C.mp_xyz;
+    lm.has_ml = C.has_ml;
+    lm.ml_xyz = C.ml_xyz;
+    lm.last_xyz = L.mp_xyz;
+    lm.last_lxyz = L.ml_xyz;
+    lm.K = K4;
+    lm.nslots = std::min(fid, K4);
+    lm.head = ((fid - 1) % K4 + K4) % K4;
+    lm.push_slot = fid % K4;
+    lm.r_xyz = t->kr_xyz; lm.r_nrm = t->kr_nrm; lm.r_dmin = t->kr_dmin; lm.r_dmax = t->kr_dmax;
+    lm.r_has = t->kr_has; lm.r_desc = t->kr_desc; lm.r_n = t->kr_n;
+    lm.rl_xyz = t->rl_xyz; lm.rl_has = t->rl_has; lm.rl_desc = t->rl_desc; lm.rl_n = t->rl_n;
+    lm.lp = t->lp;
+    lm.llp = t->llp;
+    lm.l_xyz = t->l_xyz; lm.l_nrm = t->l_nrm; lm.l_dmin = t->l_dmin; lm.l_dmax = t->l_dmax;
+    lm.l_desc = t->l_desc; lm.l_n = t->l_n;
+    lm.ll_xyz = t->ll_xyz; lm.ll_desc = t->ll_desc; lm.ll_n = t->ll_n;
+    lm.cur_nobs = t->cur_nobs;
+    lm.cur_nobs_l = t->cur_nobs_l;
+    lm.lm_match = t->lm_match;
+    lm.llm_match = t->llm_match;
+    lm.match2 = t->match2; lm.xyz2 = t->xyz2; lm.lmatch2 = t->lmatch2; lm.lxyz2 = t->lxyz2;
+    lm.outlier2 = t->outlier2; lm.loutlier2 = t->loutlier2;
+    launch_lm_gather(lm, S, ts);
+    // SearchLocalPoints: IsInFrustum(pMP, 0.5), ORBmatcher(0.8).SearchByProjection
+    InFrustumArgs fa{};
+    fa.Tcw = dTcw;
+    fa.xyz = t->l_xyz;
+    fa.normal = t->l_nrm;
+    fa.min_dist = t->l_dmin;
+    fa.max_dist = t->l_dmax;
+    fa.view_cos_limit = 0.5f;
+    fa.in_view = t->l_inview;
+    fa.proj_x = t->l_px;
+    fa.proj_y = t->l_py;
+    fa.proj_xr = t->l_pxr;
+    fa.level = t->l_level;
+    fa.view_cos = t->l_vcos;
+    fa.n_arr = t->l_n;
+    fa.pitch = t->lp;
+    fa.pose_stride = pstride;
+    const float log_scale = (float)lsdm::log_((double)t->scale_factor);   // P15
+    launch_in_frustum(t->consts, log_scale, fa, ts, S);
+    char* stb = reinterpret_cast<char*>(t->d_state);
+    LocalArgs ma{};
+    ma.kps_un = C.kps_un;
+    ma.desc = C.desc;
+    ma.uright = C.uright;
+    ma.cur_nobs = t->cur_nobs;
+    ma.in_view = t->l_inview;
+    ma.proj_x = t->l_px;
+    ma.proj_y = t->l_py;
+    ma.proj_xr = t->l_pxr;
+    ma.level = t->l_level;
+    ma.view_cos = t->l_vcos;
+    ma.mp_desc = t->l_desc;
+    ma.mp_nobs = nullptr;
+    ma.th = fid < 2 ? 5.0f : (t->stereo ? 1.0f : 3.0f);
+    ma.nnratio = 0.8f;
+    ma.match = t->lm_match;
+    ma.nmatches = reinterpret_cast<int*>(stb + offsetof(StreamState, lm_nlocal));
+    ma.scratch = t->l_scratch;
+    ma.n_arr = C.n;
+    ma.nmp_arr = t->l_n;
+    ma.kp_pitch = K;
+    ma.mp_pitch = t->lp;
+    ma.nm_stride = pstride;
+    launch_match_local(t->consts, ma, ts, S);
+    if (t->lines) {
+      // SearchLocalLines: IsInFrustum(pML, 0.5), LineMatcher(0.8) local-map overload
+      launch_line_in_frustum_batched(dTcw, pstride, t->ll_n, t->llp, t->ll_xyz, t->ll_valid, S, ts);
+      LineListArgs la3{};
+      la3.Tcw = dTcw;
+      la3.cur_kl_un = C.kl_un;
+      la3.cur_desc = C.ldesc;
+      la3.cur_nobs = t->cur_nobs_l;
+      la3.valid = t->ll_valid;
+      la3.ml_xyz6 = t->ll_xyz;
+      la3.ml_desc = t->ll_desc;
+      la3.proj_kl = t->ll_proj;
+      la3.proj_src = t->ll_src;
+      la3.match = t->llm_match;
+      la3.nmatches = reinterpret_cast<int*>(stb + offsetof(StreamState, lm_nllocal));
+      la3.wiped = reinterpret_cast<int*>(stb + offsetof(StreamState, lm_wiped));
+      la3.ncur_arr = C.nl;
+      la3.nml_arr = t->ll_n;
+      la3.cur_pitch = kLineKeep;
+      la3.ml_pitch = t->llp;
+      la3.pose_stride = pstride;
+      la3.nm_stride = pstride;
+      launch_line_match_list(t->consts, la3, ts, S);
+    }
+    launch_lm_assemble(lm, S, ts);
+    // PoseOptimizationWithLines over every match of the frame
+    PoseLaunch p2 = p;
+    p2.match = t->match2;
+    p2.mp_xyz = t->xyz2;
+    p2.outlier = t->outlier2;
+    p2.ninliers = reinterpret_cast<int*>(stb + offsetof(StreamState, lm_ninl));
+    if (t->lines) {
+      p2.t_lmatch = t->lmatch2;
+      p2.t_ml_xyz = t->lxyz2;
+      p2.t_loutlier = t->loutlier2;
+    }
+    p2.gate_lm = 1;
+    launch_pose(t->consts, p2, S, ts);
+    launch_lm_count(lm, fid, S, ts);
+  }
+  HIP_CHECK(hipEventRecord(ev[26], ts));
   LineFinish lf{};
   if (t->lines) {
     lf.nl = C.nl;
@@ -1238,7 +1445,11 @@ static int tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_
     lf.ml_xyz = C.ml_xyz;
   }
   launch_finish(t->consts, t->d_state, C.n, K, C.kps_un, C.depth, C.match, C.outlier, C.has_mp,
-                C.mp_xyz, C.nobs, lf, S, ts);
+                C.mp_xyz, C.nobs, lf, S, ts, t->local_map);
+  if (t->local_map) {
+    launch_lm_push(t->consts, lm, S, ts);   // the frame joins the local map
+    t->lm_step++;
+  }
   HIP_CHECK(hipEventRecord(ev[10], ts));
   if (t->hist_count < t->hist_cap) {
     const size_t k = (size_t)t->hist_count++ * S;
@@ -1337,13 +1548,15 @@ int orbpl_tracker_timings(orbpl_tracker* t, int max_steps, float* ms, int* n_ste
   HIP_CHECK(hipStreamSynchronize(t->tstream));
   // stage intervals: 5 extraction stages, glue (extraction stream), then
   // match (incl. prediction), pose, finish (tracking stream)
-  static const int kPair[9][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 6}, {7, 8}, {14, 9}, {9, 10}};
+  // (+ TrackLocalMap: gather, frustum, local matching, second pose, count)
+  static const int kPair[10][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 6},
+                                   {7, 8}, {14, 9}, {26, 10}, {9, 26}};
   const int n = std::min(max_steps, t->ring_count);
   for (int k = 0; k < n; k++) {
     const int step = t->ring_pos - n + k;
     hipEvent_t* ev = &t->ring[(size_t)(step % orbpl_tracker::kRing) * orbpl_tracker::kEv];
-    for (int i = 0; i < 9; i++)
-      HIP_CHECK(hipEventElapsedTime(&ms[k * 9 + i], ev[kPair[i][0]], ev[kPair[i][1]]));
+    for (int i = 0; i < 10; i++)
+      HIP_CHECK(hipEventElapsedTime(&ms[k * 10 + i], ev[kPair[i][0]], ev[kPair[i][1]]));
   }
   *n_steps = n;
   return ORBPL_OK;
@@ -1394,7 +1607,7 @@ int orbpl_tracker_set_history(orbpl_tracker* t, int max_steps) {
 }
 
 int orbpl_tracker_get_history(orbpl_tracker* t, int stream, int max_steps, float* Tcw,
-                              int* counts8, int* n_steps) {
+                              int* counts12, int* n_steps) {
   if (!t || !n_steps || stream < 0 || stream >= t->S || max_steps < 0) return arg_fail("bad argument");
   HIP_CHECK(hipSetDevice(t->device));
   HIP_CHECK(hipStreamSynchronize(t->tstream));
@@ -1408,10 +1621,13 @@ int orbpl_tracker_get_history(orbpl_tracker* t, int stream, int max_steps, float
     HIP_CHECK(hipMemcpy(&nk, t->d_hist_n + o, 4, hipMemcpyDeviceToHost));
     if (t->lines) HIP_CHECK(hipMemcpy(&nl, t->d_hist_nl + o, 4, hipMemcpyDeviceToHost));
     if (Tcw) memcpy(Tcw + 16 * k, st.Tlast, 64);
-    if (counts8) {
-      int* c = counts8 + 8 * k;
+    if (counts12) {
+      int* c = counts12 + 12 * k;
       c[0] = nk; c[1] = st.nmatches; c[2] = st.ninliers; c[3] = st.nmatches_map; c[4] = st.ok;
       c[5] = nl; c[6] = t->lines ? st.nlmatches : 0; c[7] = t->lines ? st.nlmatches_map : 0;
+      const bool lm = t->local_map && st.lm_active;
+      c[8] = lm ? st.lm_nlocal : 0; c[9] = lm ? st.lm_inl : 0;
+      c[10] = lm && t->lines ? st.lm_nllocal : 0; c[11] = lm && t->lines ? st.lm_linl : 0;
     }
   }
   return ORBPL_OK;
@@ -1501,12 +1717,13 @@ int orbpl_tracker_timings_reset(orbpl_tracker* t) {
 int orbpl_tracker_stage_ms(orbpl_tracker* t, float* ms5) {
   if (!t || !ms5) return arg_fail("NULL argument");
   if (t->ring_count == 0) return arg_fail("no step recorded yet");
-  float m[9];
+  float m[10];
   int n = 0;
   int rc = orbpl_tracker_timings(t, 1, m, &n);
   if (rc) return rc;
   ms5[0] = m[0] + m[1] + m[2] + m[3] + m[4];
   for (int i = 0; i < 4; i++) ms5[1 + i] = m[5 + i];
+  ms5[3] += m[9];   // pose: both PoseOptimizations (+ the local map search)
   return ORBPL_OK;
 }
 
@@ -1547,6 +1764,24 @@ int orbpl_tracker_get_status(orbpl_tracker* t, int* ok, int* nlines, int* line_m
     if (nlines) nlines[s] = nl[s];
     if (line_matches) line_matches[s] = t->lines ? st[s].nlmatches : 0;
     if (line_nmatches_map) line_nmatches_map[s] = t->lines ? st[s].nlmatches_map : 0;
+  }
+  return ORBPL_OK;
+}
+
+int orbpl_tracker_get_local_stats(orbpl_tracker* t, int* local_matches, int* local_inliers,
+                                  int* local_line_matches, int* local_line_inliers) {
+  if (!t) return arg_fail("NULL tracker");
+  HIP_CHECK(hipSetDevice(t->device));
+  HIP_CHECK(hipStreamSynchronize(t->tstream));
+  HIP_CHECK(hipStreamSynchronize(t->stream));
+  std::vector<StreamState> st(t->S);
+  HIP_CHECK(hipMemcpy(st.data(), t->d_state, sizeof(StreamState) * t->S, hipMemcpyDeviceToHost));
+  for (int s = 0; s < t->S; s++) {
+    const bool lm = t->local_map && st[s].lm_active;
+    if (local_matches) local_matches[s] = lm ? st[s].lm_nlocal : 0;
+    if (local_inliers) local_inliers[s] = lm ? st[s].lm_inl : 0;
+    if (local_line_matches) local_line_matches[s] = lm && t->lines ? st[s].lm_nllocal : 0;
+    if (local_line_inliers) local_line_inliers[s] = lm && t->lines ? st[s].lm_linl : 0;
   }
   return ORBPL_OK;
 }

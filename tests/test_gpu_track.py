@@ -535,3 +535,62 @@ def test_stereo_matches_bit_exact(orbpl, oracle, seed):
     # no right keypoints: nothing matches
     ur0, d0 = orbpl.stereo_matches(orbpl.make_camera(cfg), exl, exr, kl, dl, kr[:0], dr[:0])
     assert np.all(ur0 == -1) and np.all(d0 == -1)
+
+
+@pytest.mark.parametrize("lines,stereo,pipelined,fixed", [
+    (False, False, False, False), (True, False, False, False), (True, False, True, True),
+    (True, True, False, True)])
+def test_tracker_local_map_matches_oracle(orbpl, oracle, lines, stereo, pipelined, fixed):
+    """TrackWithMotionModel + TrackLocalMap (ORBPL_TRACK_LOCAL_MAP, defined
+    local map P18: the last 4 frames' map points / lines) against the oracle
+    LVO loop with the same flags: every frame's 8 tracking counts and the 4
+    TrackLocalMap counts identical, pose within POSE_TOL, through 6 frames
+    (the ring fills and wraps)."""
+    from _scenes import stereo_sequence
+    S, F = 2, 6
+    if stereo:
+        seqs = [stereo_sequence(F, 70 + s) for s in range(S)]
+        orb = (2000, 1.2, 8, 20, 7)
+    else:
+        seqs = [sequence(F, 80 + s, cam_name="TUM3" if lines else "TUM1") for s in range(S)]
+        orb = (1000, 1.2, 8, 20, 7)
+    cfg = seqs[0][0]
+    W, H = cfg["width"], cfg["height"]
+    flags = oracle.TRACK_LOCAL_MAP | (oracle.TRACK_FIXED_LINE_JAC if fixed else 0)
+    lvo = oracle.LVO(oracle.params(*orb), oracle.camera(cfg), S, use_lines=lines, flags=flags)
+    tr = orbpl.Tracker(orbpl.OrbParams(*orb), orbpl.make_camera(cfg), S, lines=lines, stereo=stereo,
+                       local_map=True, fixed_line_jac=fixed)
+    tr.set_pipelined(pipelined)
+    T0 = np.stack([np.linalg.inv(sq[1][0]).astype(np.float32) for sq in seqs])
+    lvo.reset(T0.reshape(S, 16))
+    tr.reset(T0.reshape(S, 16))
+    tr.set_history(F)
+    a = orbpl.DeviceBuffer(S * W * H)
+    b = orbpl.DeviceBuffer(S * W * H * (1 if stereo else 4))
+    keys = ("nkeypoints", "nmatches", "ninliers", "nmatches_map", "ok", "nlines", "line_matches",
+            "line_nmatches_map")
+    lkeys = ("local_matches", "local_inliers", "local_line_matches", "local_line_inliers")
+    ref = [[None] * F for _ in range(S)]
+    for f in range(F):
+        a.upload(np.stack([sq[2][f][0] for sq in seqs]))
+        b.upload(np.stack([sq[2][f][1] for sq in seqs]))
+        if stereo:
+            tr.step_stereo_device(a.ptr, b.ptr)
+        else:
+            tr.step_device(a.ptr, b.ptr)
+        if not pipelined:
+            tr.synchronize()
+        for s in range(S):
+            g, d = seqs[s][2][f]
+            To, so = lvo.step_stereo(s, g, d) if stereo else lvo.step(s, g, d)
+            ref[s][f] = (To, [so[k] for k in keys] + [lvo.local_stats(s)[k] for k in lkeys])
+    tr.synchronize()
+    for s in range(S):
+        Th, Ch = tr.history(s)
+        assert len(Th) == F
+        for f in range(F):
+            To, co = ref[s][f]
+            assert [int(x) for x in Ch[f]] == co, (s, f, list(Ch[f]), co)
+            assert np.abs(Th[f] - To).max() < POSE_TOL, (s, f)
+        assert ref[s][F - 1][1][8] > 0       # local map matches were found
+        assert ref[s][F - 1][1][4] == 1      # and tracking succeeded
