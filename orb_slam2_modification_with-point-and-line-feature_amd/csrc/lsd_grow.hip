@@ -36,7 +36,8 @@ struct Frame {
   const float* deg;
   const int* q;
   uint32_t* used;     // LDS bits (k_lsd_grow)
-  uint32_t* ustamp;   // k_lsd_spec: USED lives in the claim stamps (0 = USED)
+  uint64_t* usd;      // k_lsd_spec: USED lives in the claim stamps (high words, 0 = USED)
+  int tw;             // tiles per row of usd
   uint32_t* reg_l;    // LDS region points (x | y << 16)
   int* regq_l;        // LDS q (gx^2 + gy^2) of each region point
   float* regd_l;      // LDS degrees of each region point
@@ -55,20 +56,24 @@ struct Frame {
 // per-pixel claim stamp (global, read at L2 like the claims): 0 = USED
 // (below every claim tag), anything else = not USED. Freeing LDS of the
 // 24 KB bitmap lets twice as many frames share a CU.
+__device__ __forceinline__ uint32_t* sd_hi(uint64_t* sd, int idx) {
+  return reinterpret_cast<uint32_t*>(sd + idx) + 1;
+}
 __device__ __forceinline__ bool used_get(const Frame& F, int x, int y) {
+  if (F.usd)
+    return __hip_atomic_load(sd_hi(F.usd, lsd_sd_index(x, y, F.tw)), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT) == 0u;
   const int i = y * F.sw + x;
-  if (F.ustamp)
-    return __hip_atomic_load(F.ustamp + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
   return (F.used[i >> 5] >> (i & 31)) & 1u;
 }
 __device__ __forceinline__ void used_set(Frame& F, int x, int y, bool v) {
   const int i = y * F.sw + x;
   // the lanes run the same serial program; one of them updates the word
   // (single writer: a plain read-modify-write)
-  if (F.ustamp) {
+  if (F.usd) {
     if (F.lane == 0)
-      __hip_atomic_store(F.ustamp + i, v ? 0u : 0xFFFFFFFFu, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(sd_hi(F.usd, lsd_sd_index(x, y, F.tw)), v ? 0u : 0xFFFFFFFFu,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   } else if (F.lane == 0) {
     const uint32_t w = F.used[i >> 5], b = 1u << (i & 31);
@@ -619,38 +624,47 @@ __device__ __forceinline__ void wg_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ
 
 enum { kSpecConflict = -1, kSpecOverflow = -2, kSpecSmall = 0, kSpecFail = 1, kSpecCand = 2 };
 
-__device__ __forceinline__ uint32_t ld_stamp(const uint32_t* p) {
+__device__ __forceinline__ uint32_t ld_stamp(uint64_t* sd, int idx) {
+  return __hip_atomic_load(sd_hi(sd, idx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_sd(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ int pt_x(const uint4& e) { return (int)(e.x & 0xFFFF); }
 __device__ __forceinline__ int pt_y(const uint4& e) { return (int)(e.x >> 16); }
 
-// region_grow for one lane. buf entries: (x | y << 16, degrees, modgrad as
-// a double split lo / hi) in insertion order. Claims are fire-and-forget
-// atomicMin; the own-pixel test re-reads the stamp from L2 (same-address
-// order within the wave). The next list entry is taken from registers (or
-// prefetched with the neighbourhood), so a step costs one memory round trip.
-// Returns the length, kSpecConflict or kSpecOverflow.
-__device__ __forceinline__ uint4 make_entry(int x, int y, const float4& r) {
-  const double w = modgrad_q(__float_as_int(r.y));
-  return make_uint4((uint32_t)x | ((uint32_t)y << 16), __float_as_uint(r.x),
-                    (uint32_t)__double2loint(w), (uint32_t)__double2hiint(w));
-}
+// region_grow for one lane over the packed pixel words (degrees + claim
+// stamp, one 8-byte load per neighbour). buf entries: (x | y << 16, degrees,
+// modgrad as a double split lo / hi), the weight filled by lane_fill_w before
+// a fit. Claims are fire-and-forget 64-bit atomicMin on (stamp << 32 | deg
+// bits) - the low word is constant per pixel, so the minimum is the stamps'.
+// The own-pixel test re-reads the stamp from L2 (same-address order within
+// the wave). The angle terms cos / sin of an added pixel are computed from its
+// degrees exactly as the reference's region_grow does (P2). Returns the
+// length, kSpecConflict or kSpecOverflow.
 __device__ __forceinline__ double entry_w(const uint4& e) {
   return __hiloint2double((int)e.w, (int)e.z);
 }
 __device__ __forceinline__ float entry_deg(const uint4& e) { return __uint_as_float(e.y); }
 
-__device__ __forceinline__ int lane_grow(const Frame& F, const float4* __restrict__ pix,
-                                         uint32_t* stamp, uint4* buf, int cap, int sx, int sy,
-                                         double& reg_angle, double prec, uint32_t myval) {
+__device__ __forceinline__ void add_angle(float d, float& sumdx, float& sumdy) {
+  float c, sn;
+  cr_cos_sin((float)((double)d * (3.14159265358979323846 / 180)), &c, &sn);
+  sumdx += c;
+  sumdy += sn;
+}
+
+__device__ __forceinline__ int lane_grow(const Frame& F, uint64_t* sd, uint4* buf, int cap, int sx,
+                                         int sy, double& reg_angle, double prec, uint32_t myval) {
   const uint32_t mytag = myval >> 1;
-  const int sw = F.sw, sh = F.sh;
-  const int si = sy * sw + sx;
+  const int sw = F.sw, sh = F.sh, tw = F.tw;
+  const int si = lsd_sd_index(sx, sy, tw);
   if (cap < 1) return kSpecOverflow;
-  if ((ld_stamp(stamp + si) >> 1) < mytag) return kSpecConflict;
-  atomicMin(stamp + si, myval);
-  uint4 cur = make_entry(sx, sy, pix[si]);
+  const uint64_t v0 = ld_sd(sd + si);
+  if (((uint32_t)(v0 >> 32) >> 1) < mytag) return kSpecConflict;
+  atomicMin(reinterpret_cast<unsigned long long*>(sd + si),
+            ((unsigned long long)myval << 32) | (uint32_t)v0);
+  uint4 cur = make_uint4((uint32_t)sx | ((uint32_t)sy << 16), (uint32_t)v0, 0u, 0u);
   buf[0] = cur;
   reg_angle = deg2ang(entry_deg(cur));
   double s0, c0;
@@ -664,38 +678,59 @@ __device__ __forceinline__ int lane_grow(const Frame& F, const float4* __restric
     // all loads unconditional (clamped coordinates) so that they are in
     // flight together; out-of-image neighbours are masked afterwards
     const uint4 pref = buf[min(i + 1, n_start - 1)];
-    uint32_t st[9];
-    float4 pv[9];
+    uint64_t v[9];
     unsigned cand = 0;
 #pragma unroll
     for (int k = 0; k < 9; k++) {
       const int xx = x + (k % 3) - 1, yy = y + (k / 3) - 1;
       const int cx = min(max(xx, 0), sw - 1), cy = min(max(yy, 0), sh - 1);
-      const int idx = cy * sw + cx;
-      st[k] = ld_stamp(stamp + idx);
-      pv[k] = pix[idx];
+      v[k] = ld_sd(sd + lsd_sd_index(cx, cy, tw));
       const bool in = xx >= 0 && xx < sw && yy >= 0 && yy < sh;
-      cand |= (in && st[k] != 0u) ? (1u << k) : 0u;   // stamp 0 = USED
+      cand |= (in && (uint32_t)(v[k] >> 32) != 0u) ? (1u << k) : 0u;   // stamp 0 = USED
     }
     uint4 first_add = cur;
 #pragma unroll
     for (int k = 0; k < 9; k++) {
-      if (!((cand >> k) & 1u) || st[k] == myval) continue;  // USED (committed or own)
-      if (!aligned_deg(pv[k].x, reg_angle, prec)) continue;
-      if ((st[k] >> 1) < mytag) return kSpecConflict;      // an earlier seed's pixel
+      const uint32_t st = (uint32_t)(v[k] >> 32);
+      if (!((cand >> k) & 1u) || st == myval) continue;  // USED (committed or own)
+      const float d = __uint_as_float((uint32_t)v[k]);
+      if (!aligned_deg(d, reg_angle, prec)) continue;
+      if ((st >> 1) < mytag) return kSpecConflict;      // an earlier seed's pixel
       const int xx = x + (k % 3) - 1, yy = y + (k / 3) - 1;
-      atomicMin(stamp + yy * sw + xx, myval);
+      atomicMin(reinterpret_cast<unsigned long long*>(sd + lsd_sd_index(xx, yy, tw)),
+                ((unsigned long long)myval << 32) | (uint32_t)v[k]);
       if (n >= cap) return kSpecOverflow;
-      const uint4 e = make_entry(xx, yy, pv[k]);
+      const uint4 e = make_uint4((uint32_t)xx | ((uint32_t)yy << 16), (uint32_t)v[k], 0u, 0u);
       if (n == n_start) first_add = e;
       buf[n++] = e;
-      sumdx += pv[k].z;
-      sumdy += pv[k].w;
+      add_angle(d, sumdx, sumdy);
       reg_angle = (double)fast_atan2_deg(sumdy, sumdx) * kDegToRad;
     }
     cur = (i + 1 < n_start) ? pref : first_add;
   }
   return n;
+}
+
+// the weights modgrad = sqrt(q / 4) of a lane list's points (ll_angle's
+// modgrad, LSD's region weights), 8 independent loads in flight
+__device__ __forceinline__ void lane_fill_w(const int* __restrict__ q, int sw, uint4* buf, int n) {
+  for (int i0 = 0; i0 < n; i0 += 8) {
+    uint4 e[8];
+    int qv[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) e[u] = buf[min(i0 + u, n - 1)];
+#pragma unroll
+    for (int u = 0; u < 8; u++) qv[u] = q[pt_y(e[u]) * sw + pt_x(e[u])];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      if (i0 + u < n) {
+        const double w = modgrad_q(qv[u]);
+        e[u].z = (uint32_t)__double2loint(w);
+        e[u].w = (uint32_t)__double2hiint(w);
+        buf[i0 + u] = e[u];
+      }
+    }
+  }
 }
 
 // region2rect over a lane's list (same operation order as region2rect)
@@ -779,8 +814,8 @@ __device__ __forceinline__ void lane_rect(const uint4* buf, int n, double reg_an
 // refine + reduce_region_radius for a lane. The region [0, n) came from the
 // first grow; a second grow is appended after it. Returns the status; off /
 // len give the final region, touched the claimed prefix of the buffer.
-__device__ __forceinline__ int lane_refine(const Frame& F, const float4* __restrict__ pix,
-                                           uint32_t* stamp, uint4* buf, int n, double reg_angle,
+__device__ __forceinline__ int lane_refine(const Frame& F, uint64_t* sd, uint4* buf, int n,
+                                           double reg_angle,
                                            double prec, double p, Rect& rec, uint32_t myval1,
                                            int& off, int& len, int& touched) {
   const double density_th = 0.7;
@@ -813,12 +848,13 @@ __device__ __forceinline__ int lane_refine(const Frame& F, const float4* __restr
   const double tau =
       2.0 * sqrt((s_sum - 2.0 * mean_angle * sum) / double(cnt) + mean_angle * mean_angle);
   uint4* g1 = buf + n;
-  int n1 = lane_grow(F, pix, stamp, g1, kLaneCap - n, x0, y0, reg_angle, tau, myval1);
+  int n1 = lane_grow(F, sd, g1, kLaneCap - n, x0, y0, reg_angle, tau, myval1);
   if (n1 < 0) return n1;
   off = n;
   len = n1;
   touched = n + n1;
   if (n1 < 2) return kSpecFail;
+  lane_fill_w(F.q, F.sw, g1, n1);
   lane_rect(g1, n1, reg_angle, prec, p, rec);
   density = double(n1) / (dist(rec.x1, rec.y1, rec.x2, rec.y2) * rec.width);
   if (density >= density_th) return kSpecCand;
@@ -1050,7 +1086,8 @@ __global__ void __launch_bounds__(64) k_lsd_grow(LsdGeom g, LsdScratch sc) {
   F.deg = sc.deg + (long long)f * sw * sh;
   F.q = sc.q + (long long)f * sw * sh;
   F.used = grow_smem;
-  F.ustamp = nullptr;
+  F.usd = nullptr;
+  F.tw = 0;
   F.reg_l = grow_smem + used_words;
   F.regq_l = reinterpret_cast<int*>(F.reg_l + kRegLds);
   F.regd_l = reinterpret_cast<float*>(F.regq_l + kRegLds);
@@ -1156,11 +1193,11 @@ __global__ void __launch_bounds__(64) k_lsd_spec(LsdGeom g, LsdScratch sc) {
   F.lane = lane;
   F.pf_cyc = 0;
   F.pf_cnt = 0;
-  uint32_t* stamp = sc.stamp + (long long)f * sw * sh;   // 0xFFFFFFFF at launch
-  F.ustamp = stamp;
+  uint64_t* sd = sc.sd + (long long)f * lsd_sd_words(sw, sh);   // stamps unclaimed at launch
+  F.usd = sd;
+  F.tw = lsd_sd_tw(sw);
   (void)used_words;
   uint4* buf = sc.lbuf + ((long long)f * kSpecLanes + lane) * kLaneCap;
-  const float4* pix = sc.pix + (long long)f * sw * sh;
   const uint32_t* A = sc.A + (long long)f * g.n;
   const int nlist = sc.sort_nge[f];   // later list entries are NOTDEF
   double* cand_out = sc.cand + (long long)f * kLsdMaxCand * 12;
@@ -1183,7 +1220,9 @@ __global__ void __launch_bounds__(64) k_lsd_spec(LsdGeom g, LsdScratch sc) {
         const int idx = (int)(A[i] & 0x3FFFFFu);
         py = idx / w1;
         px = idx - py * w1;
-        c = F.deg[py * sw + px] >= 0.f && !used_get(F, px, py);
+        // one packed load: defined (degrees) and NOTUSED (stamp)
+        const uint64_t v = ld_sd(sd + lsd_sd_index(px, py, F.tw));
+        c = __uint_as_float((uint32_t)v) >= 0.f && (uint32_t)(v >> 32) != 0u;
       }
       const unsigned long long m = __ballot(c);
       const int before = __popcll(m & lt_mask);
@@ -1216,8 +1255,8 @@ __global__ void __launch_bounds__(64) k_lsd_spec(LsdGeom g, LsdScratch sc) {
     int n = 0;
     if (lane < ncand) {
       const uint32_t pt = s_pt[lane];
-      n = lane_grow(F, pix, stamp, buf, kLaneCap, (int)(pt & 0xFFFF), (int)(pt >> 16), reg_angle,
-                    prec, myval0);
+      n = lane_grow(F, sd, buf, kLaneCap, (int)(pt & 0xFFFF), (int)(pt >> 16), reg_angle, prec,
+                    myval0);
     }
     __builtin_amdgcn_wave_barrier();
     const long long t1 = clock64();
@@ -1235,9 +1274,9 @@ __global__ void __launch_bounds__(64) k_lsd_spec(LsdGeom g, LsdScratch sc) {
         len = n;
         touched = n;
       } else {
+        lane_fill_w(F.q, sw, buf, n);
         lane_rect(buf, n, reg_angle, prec, p, rec);
-        status = lane_refine(F, pix, stamp, buf, n, reg_angle, prec, p, rec, myval1, off, len,
-                             touched);
+        status = lane_refine(F, sd, buf, n, reg_angle, prec, p, rec, myval1, off, len, touched);
       }
     }
     wg_fence();
@@ -1253,7 +1292,8 @@ __global__ void __launch_bounds__(64) k_lsd_spec(LsdGeom g, LsdScratch sc) {
 #pragma unroll
         for (int u = 0; u < 8; u++) ev[u] = buf[min(j0 + u, touched - 1)].x;
 #pragma unroll
-        for (int u = 0; u < 8; u++) sv[u] = ld_stamp(stamp + (int)(ev[u] >> 16) * sw + (int)(ev[u] & 0xFFFF));
+        for (int u = 0; u < 8; u++)
+          sv[u] = ld_stamp(sd, lsd_sd_index((int)(ev[u] & 0xFFFF), (int)(ev[u] >> 16), F.tw));
 #pragma unroll
         for (int u = 0; u < 8; u++) conflict |= (sv[u] >> 1) != tag;
       }
@@ -1273,8 +1313,8 @@ __global__ void __launch_bounds__(64) k_lsd_spec(LsdGeom g, LsdScratch sc) {
           for (int u = 0; u < 8; u++) ev[u] = buf[min(j0 + u, off + len - 1)].x;
 #pragma unroll
           for (int u = 0; u < 8; u++) {
-            const int id = (int)(ev[u] >> 16) * sw + (int)(ev[u] & 0xFFFF);
-            __hip_atomic_store(stamp + id, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int id = lsd_sd_index((int)(ev[u] & 0xFFFF), (int)(ev[u] >> 16), F.tw);
+            __hip_atomic_store(sd_hi(sd, id), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
         }
       }
@@ -1423,7 +1463,6 @@ void launch_lsd_grow(const LsdGeom& g, const LsdScratch& sc, int batch, hipStrea
   if (serial) {
     hipLaunchKernelGGL(k_lsd_grow, dim3(batch), dim3(64), smem, s, g, sc);
   } else {
-    (void)hipMemsetAsync(sc.stamp, 0xFF, (size_t)batch * g.sw * g.sh * 4, s);
     hipLaunchKernelGGL(k_lsd_spec, dim3(batch), dim3(64), smem, s, g, sc);
   }
 }

@@ -36,6 +36,17 @@ struct LsdGeom {
 
 // Device scratch of one frame slot (all pointers are per-batch bases; the
 // kernels index them with the frame number).
+// Seed-loop pixel words: 4x4-pixel tiles of 8-byte words, so that a 3x3
+// neighbourhood touches 2.25 128-byte lines on average (row-major float4
+// records + separate stamps touched ~7).
+__host__ __device__ inline int lsd_sd_tw(int sw) { return (sw + 3) >> 2; }
+__host__ __device__ inline long long lsd_sd_words(int sw, int sh) {
+  return (long long)lsd_sd_tw(sw) * ((sh + 3) >> 2) * 16;
+}
+__host__ __device__ inline int lsd_sd_index(int x, int y, int tw) {
+  return ((((y >> 2) * tw) + (x >> 2)) << 4) | ((y & 3) << 2) | (x & 3);
+}
+
 struct LsdScratch {
   uint8_t* blur;       // W*H
   uint8_t* scaled;     // sw*sh
@@ -60,10 +71,12 @@ struct LsdScratch {
   int* ncand;          // 1 per frame
   float* cand_line;    // kLsdMaxCand * 4 per frame: validated segment
   int* cand_ok;        // kLsdMaxCand per frame: log_nfa > log_eps
-  uint32_t* stamp;     // sw*sh per frame: speculative region claims (0xFF.. = none)
+  uint64_t* sd;        // lsd_sd_words(g) per frame, 4x4-pixel tiles (lsd_sd_index):
+                       // low word = the pixel's degrees (float bits), high word =
+                       // the speculative seed loop's claim stamp (0 = USED,
+                       // 0xFFFFFFFF = unclaimed); written by k_lsd_grad
   uint4* lbuf;         // kSpecLanes * kLaneCap per frame: per-lane region lists
-                       // (x | y << 16, q, degrees, -)
-  float4* pix;         // sw*sh per frame: degrees, q bits, cos, sin
+                       // (x | y << 16, degrees, modgrad as a double lo / hi)
   int4* sort_local;    // seg_cap per frame: introsort segments finished in LDS
   int* sort_nlocal;    // 1 per frame
   int* sort_kt;        // 1 per frame: key bound, key < kt => NOTDEF pixel
@@ -98,7 +111,7 @@ void launch_lsd_blur(const LsdGeom& g, const uint8_t* img, int stride, long long
                      uint8_t* out, int batch, hipStream_t s);
 void launch_lsd_resize(const LsdGeom& g, const int* tabs, const uint8_t* blur, uint8_t* scaled,
                        int batch, hipStream_t s);
-void launch_lsd_grad(const LsdGeom& g, const uint8_t* scaled, float* deg, int* q, float4* pix,
+void launch_lsd_grad(const LsdGeom& g, const uint8_t* scaled, float* deg, int* q, uint64_t* sd,
                      unsigned* maxq, int batch, hipStream_t s);
 void launch_lsd_sort(const LsdGeom& g, const LsdScratch& sc, int batch, hipStream_t s);
 void launch_lsd_sort_keys(int n, const int* keys, const LsdScratch& sc, hipStream_t s);

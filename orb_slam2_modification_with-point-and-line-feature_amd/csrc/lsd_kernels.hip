@@ -105,7 +105,7 @@ __global__ void __launch_bounds__(256) k_lsd_resize(LsdGeom g, const int* __rest
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_lsd_grad(LsdGeom g, const uint8_t* __restrict__ scaled,
                                                   float* __restrict__ deg, int* __restrict__ q,
-                                                  float4* __restrict__ pix,
+                                                  uint64_t* __restrict__ sd,
                                                   unsigned* __restrict__ maxq) {
   const int f = blockIdx.y;
   const int i = blockIdx.x * 256 + threadIdx.x;
@@ -131,12 +131,9 @@ __global__ void __launch_bounds__(256) k_lsd_grad(LsdGeom g, const uint8_t* __re
     }
     deg[o] = d;
     q[o] = qq;
-    // per-pixel record of the speculative seed loop: the degrees, q and the
-    // region_grow angle terms cos / sin (float)(d * pi / 180), correctly
-    // rounded (P2)
-    float c = 0.f, sn = 0.f;
-    if (d >= 0.f) cr_cos_sin((float)((double)d * (3.14159265358979323846 / 180)), &c, &sn);
-    pix[o] = make_float4(d, __int_as_float(qq), c, sn);
+    // the speculative seed loop's pixel word: degrees + unclaimed stamp
+    sd[(long long)f * lsd_sd_words(sw, sh) + lsd_sd_index(x, y, lsd_sd_tw(sw))] =
+        (0xFFFFFFFFull << 32) | (uint64_t)__float_as_uint(d);
   }
   // block max, one atomic per block
   __shared__ unsigned s_m[4];
@@ -660,10 +657,10 @@ void launch_lsd_resize(const LsdGeom& g, const int* tabs, const uint8_t* blur, u
                      tabs, blur, scaled);
 }
 
-void launch_lsd_grad(const LsdGeom& g, const uint8_t* scaled, float* deg, int* q, float4* pix,
+void launch_lsd_grad(const LsdGeom& g, const uint8_t* scaled, float* deg, int* q, uint64_t* sd,
                      unsigned* maxq, int batch, hipStream_t s) {
   hipLaunchKernelGGL(k_lsd_grad, dim3((g.sw * g.sh + 255) / 256, batch), dim3(256), 0, s, g,
-                     scaled, deg, q, pix, maxq);
+                     scaled, deg, q, sd, maxq);
 }
 
 void launch_lsd_sort(const LsdGeom& g, const LsdScratch& sc, int batch, hipStream_t s) {

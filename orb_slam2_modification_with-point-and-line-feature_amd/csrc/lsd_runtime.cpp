@@ -140,7 +140,7 @@ int lsdx_run(lsdx_ctx* c, const uint8_t* d_imgs, int batch, int stride, int64_t 
   HIP_CHECK(hipMemsetAsync(c->sc.err, 0, (size_t)batch * 4, s));
   launch_lsd_blur(g, d_imgs, stride, frame_pitch, c->sc.blur, batch, s);
   launch_lsd_resize(g, c->d_tabs, c->sc.blur, c->sc.scaled, batch, s);
-  launch_lsd_grad(g, c->sc.scaled, c->sc.deg, c->sc.q, c->sc.pix, c->sc.maxq, batch, s);
+  launch_lsd_grad(g, c->sc.scaled, c->sc.deg, c->sc.q, c->sc.sd, c->sc.maxq, batch, s);
   if (ev_stage) HIP_CHECK(hipEventRecord(ev_stage[0], s));
   launch_lsd_sort(g, c->sc, batch, s);
   if (ev_stage) HIP_CHECK(hipEventRecord(ev_stage[1], s));
@@ -243,9 +243,8 @@ int lsdx_create(int width, int height, int max_batch, int device, lsdx_ctx** out
   LA(s.ncand, B * 4);
   LA(s.cand_line, B * kLsdMaxCand * 4 * 4);
   LA(s.cand_ok, B * kLsdMaxCand * 4);
-  LA(s.stamp, B * px * 4);
+  LA(s.sd, B * (size_t)lsd_sd_words(g.sw, g.sh) * 8);
   LA(s.lbuf, B * kSpecLanes * kLaneCap * sizeof(uint4));
-  LA(s.pix, B * px * sizeof(float4));
   LA(s.sort_local, B * g.seg_cap * sizeof(int4));
   LA(s.sort_nlocal, B * 4);
   LA(s.sort_kt, B * 4);
