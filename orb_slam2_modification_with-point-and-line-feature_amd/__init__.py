@@ -108,11 +108,11 @@ class DeviceBuffer:
         b.upload(arr)
         return b
 
-    def upload(self, arr):
+    def upload(self, arr, offset=0):
         arr = np.ascontiguousarray(arr)
-        assert arr.nbytes <= self.nbytes
-        check(lib().orbpl_memcpy_htod(self.device, C.c_void_p(self.ptr), _ptr(arr), arr.nbytes),
-              "orbpl_memcpy_htod")
+        assert 0 <= offset and offset + arr.nbytes <= self.nbytes
+        check(lib().orbpl_memcpy_htod(self.device, C.c_void_p(self.ptr + offset), _ptr(arr),
+                                      arr.nbytes), "orbpl_memcpy_htod")
 
     def download(self, dtype, shape):
         out = np.empty(shape, dtype)

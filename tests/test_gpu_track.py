@@ -565,19 +565,22 @@ def test_tracker_local_map_matches_oracle(orbpl, oracle, lines, stereo, pipeline
     lvo.reset(T0.reshape(S, 16))
     tr.reset(T0.reshape(S, 16))
     tr.set_history(F)
-    a = orbpl.DeviceBuffer(S * W * H)
-    b = orbpl.DeviceBuffer(S * W * H * (1 if stereo else 4))
+    # one device slot per frame: pipelined steps return before extraction has
+    # read its input, so a reused upload buffer would race the next upload
+    fa, fb = S * W * H, S * W * H * (1 if stereo else 4)
+    a = orbpl.DeviceBuffer(F * fa)
+    b = orbpl.DeviceBuffer(F * fb)
     keys = ("nkeypoints", "nmatches", "ninliers", "nmatches_map", "ok", "nlines", "line_matches",
             "line_nmatches_map")
     lkeys = ("local_matches", "local_inliers", "local_line_matches", "local_line_inliers")
     ref = [[None] * F for _ in range(S)]
     for f in range(F):
-        a.upload(np.stack([sq[2][f][0] for sq in seqs]))
-        b.upload(np.stack([sq[2][f][1] for sq in seqs]))
+        a.upload(np.stack([sq[2][f][0] for sq in seqs]), offset=f * fa)
+        b.upload(np.stack([sq[2][f][1] for sq in seqs]), offset=f * fb)
         if stereo:
-            tr.step_stereo_device(a.ptr, b.ptr)
+            tr.step_stereo_device(a.ptr + f * fa, b.ptr + f * fb)
         else:
-            tr.step_device(a.ptr, b.ptr)
+            tr.step_device(a.ptr + f * fa, b.ptr + f * fb)
         if not pipelined:
             tr.synchronize()
         for s in range(S):
