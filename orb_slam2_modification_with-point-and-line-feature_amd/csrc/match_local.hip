@@ -4,16 +4,19 @@
 //   k_match_local  : ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&,
 //                    th) (ORBmatcher.cc:72-183), one workgroup per frame:
 //     grid build    - AssignFeaturesToGrid in LDS (cells hold increasing indices)
-//     phase A       - every map point in parallel: best and second candidate
-//                     (the reference's running top-2 in grid-scan order) with
-//                     the keypoints already holding a map point with
+//     phase A       - every map point in parallel: its first 4 candidates in
+//                     (distance, grid-scan position) order, whose first two
+//                     are the reference's running best / second, with the
+//                     keypoints already holding a map point with
 //                     Observations() > 0 skipped
 //     phase B       - wave 0, map points in order: a point's outcome can only
 //                     change if its best or second candidate is claimed by an
 //                     earlier accepted point (removing any other candidate
 //                     leaves the running top-2 unchanged), so chunks of 64 are
-//                     decided at once up to the first such collision, which is
-//                     re-scanned against the claims; the last writer of a
+//                     decided at once up to the first such collision; lanes
+//                     whose candidates committed points claimed take the next
+//                     unclaimed entries of their list (a new scan when it runs
+//                     out), all together; the last writer of a
 //                     keypoint wins, as F.mvpMapPoints[bestIdx] = pMP does
 #include <hip/hip_runtime.h>
 
@@ -87,18 +90,24 @@ __global__ void __launch_bounds__(256) k_in_frustum(TrackConsts c, float log_sca
 namespace {
 
 constexpr int kLocalKp = 2048;
+constexpr int kLocalThreads = 1024;   // 16 waves: phase A and the grid build; wave 0 runs phase B
+constexpr int kCells = kGridCols * kGridRows;
 
+// 126 KB: one workgroup per CU, the current frame's descriptors in LDS
 struct LocalShared {
-  int cell_start[kGridCols * kGridRows + 1];
-  int fill[kGridCols * kGridRows];
-  uint16_t items[kLocalKp];
+  uint4 desc[kLocalKp * 2];         // current descriptors (32 B rows)
   float2 xy[kLocalKp];
   float ur[kLocalKp];
-  int8_t oct[kLocalKp];
-  int16_t gc[kLocalKp];
   int mw[kLocalKp];                 // last writer (map point index) per keypoint
+  int own[kLocalKp];                // phase B: (round << 6) | (63 - lane) of the round's
+                                    // first claimer per keypoint
+  uint16_t fill[kCells];             // (4-byte aligned: counters are added in pairs)
+  uint16_t cell_start[kCells + 2];
+  uint16_t items[kLocalKp];
+  int16_t gc[kLocalKp];
+  int8_t oct[kLocalKp];
   uint32_t claimed[kLocalKp / 32];  // holds a map point with Observations() > 0
-  int wsum[8];
+  int wsum[kLocalThreads / 64];
 };
 
 struct Top2 {
@@ -115,11 +124,35 @@ __device__ __forceinline__ int hamming32l(const uint8_t* a, const uint8_t* b) {
          __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
 }
 
-// GetFeaturesInArea(x, y, r*scale, level-1, level) + the best / second loop
+// The reference's running best / second pair (ORBmatcher.cc:128-145, strict
+// comparisons) is the first two candidates in (distance, scan position) order:
+// the best is the earliest candidate of minimal distance, the second the
+// earliest other candidate of the next distance (or of the same one). Claims
+// only remove candidates, so the pair under later claims is the first two
+// unclaimed entries of that order. The scan keeps the first kTopK entries of
+// it; entry = index (11 bits) | distance << 11 (9 bits) | level << 20 (4 bits),
+// all ones = empty (no candidate has distance 511); the count of candidates
+// (saturated at 255) rides in entry 0's top byte in the scratch record.
+constexpr int kTopK = 4;
+constexpr uint32_t kEmpty = 0xFFFFFFu;
+
+struct TopList {
+  uint32_t e[kTopK];
+  int cnt;
+};
+
+__device__ __forceinline__ bool is_claimed(const LocalShared& S, int j) {
+  return (S.claimed[j >> 5] >> (j & 31)) & 1u;
+}
+
+// GetFeaturesInArea(x, y, r*scale, level-1, level) + the candidate loop
 // (ORBmatcher.cc:96-160) against the current claims.
-__device__ Top2 local_scan(const LocalShared& S, const TrackConsts& c, const LocalArgs& a,
-                           const uint8_t* cdesc, int i) {
-  Top2 t{256, -1, -1, 256, -1, -1};
+__device__ TopList local_scan(const LocalShared& S, const TrackConsts& c, const LocalArgs& a,
+                              int i) {
+  TopList t;
+#pragma unroll
+  for (int k = 0; k < kTopK; k++) t.e[k] = kEmpty;
+  t.cnt = 0;
   const int lev = a.level[i];
   float r = (a.view_cos[i] > 0.998) ? 2.5f : 4.0f;
   if (a.th != 1.0) r *= a.th;
@@ -132,7 +165,8 @@ __device__ Top2 local_scan(const LocalShared& S, const TrackConsts& c, const Loc
   const int cy1 = min(kGridRows - 1, (int)ceilf((y - c.minY + rad) * c.gridInvH));
   if (cx0 >= kGridCols || cx1 < 0 || cy0 >= kGridRows || cy1 < 0) return t;
   const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
-  const uint8_t* dMP = a.mp_desc + (long long)i * 32;
+  const uint4* dp = reinterpret_cast<const uint4*>(a.mp_desc + (long long)i * 32);
+  const uint4 m0 = dp[0], m1 = dp[1];
   for (int ix = cx0; ix <= cx1; ix++)
     for (int iy = cy0; iy <= cy1; iy++) {
       const int cell = ix + kGridCols * iy;
@@ -146,30 +180,58 @@ __device__ Top2 local_scan(const LocalShared& S, const TrackConsts& c, const Loc
         }
         const float2 p = S.xy[j];
         if (!(fabsf(p.x - x) < rad && fabsf(p.y - y) < rad)) continue;
-        if ((S.claimed[j >> 5] >> (j & 31)) & 1u) continue;
+        if (is_claimed(S, j)) continue;
         const float urj = S.ur[j];
         if (urj > 0 && fabsf(xr - urj) > r * c.scale[lev]) continue;
-        const int dist = hamming32l(dMP, cdesc + (long long)j * 32);
-        if (dist < t.bd) {
-          t.sd = t.bd;
-          t.si = t.bi;
-          t.sl = t.bl;
-          t.bd = dist;
-          t.bi = j;
-          t.bl = oc;
-        } else if (dist < t.sd) {
-          t.sd = dist;
-          t.si = j;
-          t.sl = oc;
+        const uint4 c0 = S.desc[2 * j], c1 = S.desc[2 * j + 1];
+        const int dist = __popc(m0.x ^ c0.x) + __popc(m0.y ^ c0.y) + __popc(m0.z ^ c0.z) +
+                         __popc(m0.w ^ c0.w) + __popc(m1.x ^ c1.x) + __popc(m1.y ^ c1.y) +
+                         __popc(m1.z ^ c1.z) + __popc(m1.w ^ c1.w);
+        if (dist >= 256) continue;   // never below the initial 256 of either slot
+        t.cnt++;
+        // insert after every kept entry of distance <= dist (scan order breaks ties)
+        uint32_t v = (uint32_t)j | ((uint32_t)dist << 11) | ((uint32_t)oc << 20);
+#pragma unroll
+        for (int k = 0; k < kTopK; k++) {
+          const uint32_t ek = t.e[k];
+          const bool take = ek == kEmpty || (int)((ek >> 11) & 511) > dist;
+          if (take) {
+            t.e[k] = v;
+            v = ek;
+          }
+          if (take && ek == kEmpty) break;
         }
       }
     }
   return t;
 }
 
+// the first two unclaimed entries; *full = the list cannot decide (fewer than
+// two unclaimed entries while candidates beyond the kept ones exist)
+__device__ __forceinline__ Top2 pick2(const LocalShared& S, const TopList& t, bool* full) {
+  Top2 r{256, -1, -1, 256, -1, -1};
+  int found = 0;
+#pragma unroll
+  for (int k = 0; k < kTopK; k++) {
+    const uint32_t ek = t.e[k];
+    if (ek == kEmpty || found == 2) continue;
+    const int j = (int)(ek & 2047);
+    if (is_claimed(S, j)) continue;
+    const int d = (int)((ek >> 11) & 511), l = (int)((ek >> 20) & 15);
+    if (found == 0) {
+      r.bi = j; r.bd = d; r.bl = l;
+    } else {
+      r.si = j; r.sd = d; r.sl = l;
+    }
+    found++;
+  }
+  *full = found < 2 && t.cnt > kTopK;
+  return r;
+}
+
 }  // namespace
 
-__global__ void __launch_bounds__(256) k_match_local(TrackConsts c, LocalArgs a) {
+__global__ void __launch_bounds__(kLocalThreads) k_match_local(TrackConsts c, LocalArgs a) {
   if (a.n_arr) {  // batched: stream blockIdx.x
     const int b = blockIdx.x;
     const long long ko = (long long)b * a.kp_pitch, mo = (long long)b * a.mp_pitch;
@@ -195,27 +257,32 @@ __global__ void __launch_bounds__(256) k_match_local(TrackConsts c, LocalArgs a)
   LocalShared& S = *reinterpret_cast<LocalShared*>(smem_local);
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
   const int n = min(a.n, kLocalKp);
-  const uint8_t* cdesc = a.desc;
   // ---- grid (AssignFeaturesToGrid with PosInGrid, Frame.cc:265-287, 527-538) ----
-  for (int i = t; i < kGridCols * kGridRows; i += 256) S.cell_start[i] = 0;
-  for (int i = t; i < kLocalKp / 32; i += 256) S.claimed[i] = 0;
+  for (int i = t; i < kCells; i += kLocalThreads) S.cell_start[i] = 0;
+  for (int i = t; i < kLocalKp / 32; i += kLocalThreads) S.claimed[i] = 0;
+  {
+    const uint4* d = reinterpret_cast<const uint4*>(a.desc);
+    for (int i = t; i < 2 * n; i += kLocalThreads) S.desc[i] = d[i];
+  }
   __syncthreads();
-  for (int i = t; i < n; i += 256) {
+  for (int i = t; i < n; i += kLocalThreads) {
     const KeyPointD k = a.kps_un[i];
     S.xy[i] = make_float2(k.x, k.y);
     S.oct[i] = (int8_t)k.octave;
     S.ur[i] = a.uright[i];
     S.mw[i] = -1;
+    S.own[i] = 0;
     const int px = (int)roundf((k.x - c.minX) * c.gridInvW);
     const int py = (int)roundf((k.y - c.minY) * c.gridInvH);
     const int g = (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) ? -1 : px + kGridCols * py;
     S.gc[i] = (int16_t)g;
-    if (g >= 0) atomicAdd(&S.cell_start[g], 1);
+    if (g >= 0) atomicAdd(reinterpret_cast<unsigned int*>(&S.cell_start[g & ~1]), 1u << (16 * (g & 1)));
     if (a.cur_nobs && a.cur_nobs[i] > 0) atomicOr(&S.claimed[i >> 5], 1u << (i & 31));
   }
   __syncthreads();
   {
-    constexpr int kPer = (kGridCols * kGridRows) / 256;
+    constexpr int kPer = kCells / kLocalThreads;
+    static_assert(kCells % kLocalThreads == 0, "cells per thread");
     int loc[kPer];
     int sum = 0;
 #pragma unroll
@@ -236,19 +303,25 @@ __global__ void __launch_bounds__(256) k_match_local(TrackConsts c, LocalArgs a)
     int run = base + incl - sum;
 #pragma unroll
     for (int k = 0; k < kPer; k++) {
-      S.cell_start[t * kPer + k] = run;
-      S.fill[t * kPer + k] = run;
+      S.cell_start[t * kPer + k] = (uint16_t)run;
+      S.fill[t * kPer + k] = (uint16_t)run;
       run += loc[k];
     }
-    if (t == 255) S.cell_start[kGridCols * kGridRows] = run;
+    if (t == kLocalThreads - 1) S.cell_start[kCells] = (uint16_t)run;
     __syncthreads();
   }
-  for (int i = t; i < n; i += 256) {
+  for (int i = t; i < n; i += kLocalThreads) {
     const int g = S.gc[i];
-    if (g >= 0) S.items[atomicAdd(&S.fill[g], 1)] = (uint16_t)i;
+    if (g >= 0) {
+      // 16-bit fill counters packed in pairs: add to the word, take this half
+      const unsigned int sh = 16 * (g & 1);
+      const unsigned int old =
+          atomicAdd(reinterpret_cast<unsigned int*>(&S.fill[g & ~1]), 1u << sh);
+      S.items[(old >> sh) & 0xFFFFu] = (uint16_t)i;
+    }
   }
   __syncthreads();
-  for (int cell = t; cell < kGridCols * kGridRows; cell += 256) {
+  for (int cell = t; cell < kCells; cell += kLocalThreads) {
     const int b = S.cell_start[cell], e = S.cell_start[cell + 1];
     for (int q = b + 1; q < e; q++) {
       const uint16_t v = S.items[q];
@@ -262,44 +335,81 @@ __global__ void __launch_bounds__(256) k_match_local(TrackConsts c, LocalArgs a)
   }
   __syncthreads();
   // ---- phase A ----
-  for (int i = t; i < a.nmp; i += 256) {
-    Top2 r{256, -1, -1, 256, -1, -1};
-    if (a.in_view[i]) r = local_scan(S, c, a, cdesc, i);
-    a.scratch[i] = make_int4(r.bi, r.bd | (r.bl << 16), r.si, r.sd | (r.sl << 16));
+  for (int i = t; i < a.nmp; i += kLocalThreads) {
+    TopList r;
+#pragma unroll
+    for (int k = 0; k < kTopK; k++) r.e[k] = kEmpty;
+    r.cnt = 0;
+    if (a.in_view[i]) r = local_scan(S, c, a, i);
+    a.scratch[i] = make_int4((int)(r.e[0] | ((uint32_t)min(r.cnt, 255) << 24)), (int)r.e[1],
+                             (int)r.e[2], (int)r.e[3]);
   }
   __syncthreads();
   // ---- phase B (wave 0, map point order) ----
+  // Rounds over a chunk of 64 map points. A lane whose best or second
+  // candidate was claimed by a committed point rescans against the committed
+  // claims (all stale lanes of the chunk in parallel); the round's claimers
+  // then stamp their keypoint in S.own, a lane whose best or second candidate
+  // carries a stamp of an earlier lane collides, and the chunk commits in
+  // order up to the first collision. The colliding lane is stale in the next
+  // round (its candidate is now claimed) and so is rescanned, which makes
+  // every lane's committed outcome the one of the sequential loop.
   if (wave == 0) {
-    int acc = 0;
+    int acc = 0, round = 0;
     for (int base = 0; base < a.nmp; base += 64) {
       const int i = base + lane;
-      Top2 r{256, -1, -1, 256, -1, -1};
+      TopList lst;
+#pragma unroll
+      for (int k = 0; k < kTopK; k++) lst.e[k] = kEmpty;
+      lst.cnt = 0;
       if (i < a.nmp) {
         const int4 v = a.scratch[i];
-        r.bi = v.x;
-        r.bd = (int)(short)(v.y & 0xFFFF);
-        r.bl = (int)(short)(v.y >> 16);
-        r.si = v.z;
-        r.sd = (int)(short)(v.w & 0xFFFF);
-        r.sl = (int)(short)(v.w >> 16);
+        lst.e[0] = (uint32_t)v.x & kEmpty;
+        lst.cnt = (int)((uint32_t)v.x >> 24);
+        lst.e[1] = (uint32_t)v.y;
+        lst.e[2] = (uint32_t)v.z;
+        lst.e[3] = (uint32_t)v.w;
+      }
+      // the pair under the claims of the earlier chunks
+      bool full;
+      Top2 r = pick2(S, lst, &full);
+      if (full) {
+        lst = local_scan(S, c, a, i);
+        r = pick2(S, lst, &full);
       }
       const int nobs = i < a.nmp ? (a.mp_nobs ? a.mp_nobs[i] : 1) : 0;
       bool decided = !(i < a.nmp && r.bi >= 0);
-      int start = 0;
       while (true) {
-        const bool und = !decided && lane >= start;
-        const bool accept = und && r.bd <= 100 && !(r.bl == r.sl && r.bd > a.nnratio * r.sd);
+        round++;
+        const bool stale = !decided && (is_claimed(S, r.bi) || (r.si >= 0 && is_claimed(S, r.si)));
+        if (stale) {
+          // the pair under the committed claims: from the kept list, or a new
+          // scan when the list runs out
+          r = pick2(S, lst, &full);
+          if (full) {
+            lst = local_scan(S, c, a, i);
+            r = pick2(S, lst, &full);
+          }
+          if (r.bi < 0) decided = true;
+        }
+        const bool accept = !decided && r.bd <= 100 && !(r.bl == r.sl && r.bd > a.nnratio * r.sd);
         const bool claimer = accept && nobs > 0;
-        bool coll = und && (((S.claimed[r.bi >> 5] >> (r.bi & 31)) & 1u) ||
-                            (r.si >= 0 && ((S.claimed[r.si >> 5] >> (r.si & 31)) & 1u)));
-        const int myclaim = claimer ? r.bi : -1;
-        for (int q = start; q < 64; q++) {
-          const int cq = __shfl(myclaim, q, 64);
-          if (q < lane && und && cq >= 0 && (cq == r.bi || cq == r.si)) coll = true;
+        const int key = (round << 6) | (63 - lane);
+        if (claimer) atomicMax(&S.own[r.bi], key);
+        __threadfence_block();
+        __builtin_amdgcn_wave_barrier();
+        bool coll = false;
+        if (!decided) {
+          const int ob = S.own[r.bi];
+          coll = (ob >> 6) == round && 63 - (ob & 63) < lane;
+          if (r.si >= 0) {
+            const int os = S.own[r.si];
+            coll = coll || ((os >> 6) == round && 63 - (os & 63) < lane);
+          }
         }
         const unsigned long long cm = __ballot(coll);
         const int lc = cm ? __ffsll((long long)cm) - 1 : 64;
-        if (und && lane < lc) {
+        if (!decided && lane < lc) {
           if (accept) {
             atomicMax(&S.mw[r.bi], i);
             if (claimer) atomicOr(&S.claimed[r.bi >> 5], 1u << (r.bi & 31));
@@ -310,12 +420,6 @@ __global__ void __launch_bounds__(256) k_match_local(TrackConsts c, LocalArgs a)
         if (lc == 64) break;
         __threadfence_block();
         __builtin_amdgcn_wave_barrier();
-        if (lane == lc) {
-          r = local_scan(S, c, a, cdesc, i);
-          if (r.bi < 0) decided = true;
-        }
-        __builtin_amdgcn_wave_barrier();
-        start = lc;
       }
     }
 #pragma unroll
@@ -323,7 +427,7 @@ __global__ void __launch_bounds__(256) k_match_local(TrackConsts c, LocalArgs a)
     if (lane == 0) *a.nmatches = acc;
   }
   __syncthreads();
-  for (int i = t; i < n; i += 256) a.match[i] = S.mw[i];
+  for (int i = t; i < n; i += kLocalThreads) a.match[i] = S.mw[i];
 }
 
 void launch_in_frustum(const TrackConsts& c, float log_scale, const InFrustumArgs& a,
@@ -336,7 +440,7 @@ void launch_in_frustum(const TrackConsts& c, float log_scale, const InFrustumArg
 
 void launch_match_local(const TrackConsts& c, const LocalArgs& a, hipStream_t s, int nstreams) {
   set_smem_attr((const void*)k_match_local, sizeof(LocalShared));
-  hipLaunchKernelGGL(k_match_local, dim3(a.n_arr ? nstreams : 1), dim3(256), sizeof(LocalShared), s,
+  hipLaunchKernelGGL(k_match_local, dim3(a.n_arr ? nstreams : 1), dim3(kLocalThreads), sizeof(LocalShared), s,
                      c, a);
 }
 
