@@ -13,6 +13,8 @@ int arg_fail(const char* msg);
 // HIP function attributes are per device, so a process-wide flag would skip
 // the second device. Thread-safe; the current device is hipGetDevice's.
 void set_smem_attr(const void* fn, size_t bytes);
+// compute units of the current device (cached per device)
+int device_cu_count();
 // Run `init` once per (key, device) (thread-safe); returns true the first time.
 bool once_per_device(const void* key);
 int orbx_run(orbx_ctx* c, const uint8_t* d_imgs, int batch, int stride, long long frame_pitch,

@@ -713,10 +713,10 @@ struct PoseEdge {
 };
 
 struct PoseShared {
-  double chi2[kPoseMaxEdges];     // chi2 of the last computed error (stale semantics)
+  float chi2[kPoseMaxEdges];      // (float) chi2 of the last computed error (stale
+                                  // semantics; only its float is ever compared)
   uint8_t level[kPoseMaxEdges];
   uint8_t out_flag[kPoseMaxEdges];
-  int scan[kPoseMaxEdges];
   double red[4][32];
   double sys[1][28];              // reduced H (upper, row-major), b, robust chi2
   int wsum[8];
@@ -872,17 +872,23 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 }
 
 // Reduce NV doubles over the block; result valid in every thread.
-template <int NV>
+template <int NV, int kPoseWaves>
 __device__ void block_sum(double* v, PoseShared& S) {
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
 #pragma unroll
   for (int k = 0; k < NV; k++) v[k] = wave_sum_d(v[k]);
+  if (kPoseWaves == 1) return;
   if (lane == 0)
 #pragma unroll
     for (int k = 0; k < NV; k++) S.red[wave][k] = v[k];
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < NV; k++) v[k] = ((S.red[0][k] + S.red[1][k]) + S.red[2][k]) + S.red[3][k];
+  for (int k = 0; k < NV; k++) {
+    double r = S.red[0][k];
+#pragma unroll
+    for (int w = 1; w < kPoseWaves; w++) r += S.red[w][k];
+    v[k] = r;
+  }
   __syncthreads();
 }
 
@@ -900,8 +906,9 @@ __device__ __forceinline__ void tr_step(double* v, int mask) {
   }
 }
 
-// Sum 28 per-thread doubles over the 256-thread block into out[0..28)
+// Sum 28 per-thread doubles over the block into out[0..28)
 // (shared memory). 29 shuffles per wave instead of 28 full butterflies.
+template <int kPoseWaves>
 __device__ void block_sum28_to(double* v, PoseShared& S, double* out) {
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
   tr_step<14>(v, 1);   // index k + 14*b0
@@ -914,7 +921,12 @@ __device__ void block_sum28_to(double* v, PoseShared& S, double* out) {
   const int j = ((lane >> 4) & 1) + 2 * ((lane >> 3) & 1) + 4 * ((lane >> 2) & 1);
   if (lane < 32 && j < 7) S.red[wave][j + 7 * ((lane >> 1) & 1) + 14 * (lane & 1)] = v[0];
   __syncthreads();
-  if (t < 28) out[t] = ((S.red[0][t] + S.red[1][t]) + S.red[2][t]) + S.red[3][t];
+  if (t < 28) {
+    double r = S.red[0][t];
+#pragma unroll
+    for (int w = 1; w < kPoseWaves; w++) r += S.red[w][t];
+    out[t] = r;
+  }
   __syncthreads();
 }
 
@@ -1022,7 +1034,12 @@ __device__ void se3_from_T(const float* T, SE3d& s) {
 #ifndef ORBPL_POSE_MINW
 #define ORBPL_POSE_MINW 1
 #endif
-__global__ void __launch_bounds__(256, ORBPL_POSE_MINW) k_pose(TrackConsts tc, PoseArgs a) {
+// kPoseThreads threads per stream (one workgroup per stream): 256 while the
+// streams fit one workgroup per CU, fewer (more streams per CU at the same
+// 314-VGPR footprint) beyond; see launch_pose
+template <int kPoseThreads>
+__global__ void __launch_bounds__(kPoseThreads, ORBPL_POSE_MINW) k_pose(TrackConsts tc, PoseArgs a) {
+  constexpr int kPoseWaves = kPoseThreads / 64;
   extern __shared__ char smem_raw[];
   PoseShared& S = *reinterpret_cast<PoseShared*>(smem_raw);
   const int s = blockIdx.x, t = threadIdx.x;
@@ -1054,7 +1071,7 @@ __global__ void __launch_bounds__(256, ORBPL_POSE_MINW) k_pose(TrackConsts tc, P
   PoseEdge* E = a.edges + (long long)s * kPoseMaxEdges;
   const int wave = t >> 6, lane = t & 63;
   int npts = 0;
-  for (int base = 0; base < n; base += 256) {
+  for (int base = 0; base < n; base += kPoseThreads) {
     const int i = base + t;
     int j = -1;
     if (i < n) {
@@ -1072,7 +1089,7 @@ __global__ void __launch_bounds__(256, ORBPL_POSE_MINW) k_pose(TrackConsts tc, P
     __syncthreads();
     int off = npts;
     int tot = 0;
-    for (int w = 0; w < 4; w++) {
+    for (int w = 0; w < kPoseWaves; w++) {
       if (w < wave) off += S.wsum[w];
       tot += S.wsum[w];
     }
@@ -1176,10 +1193,10 @@ __global__ void __launch_bounds__(256, ORBPL_POSE_MINW) k_pose(TrackConsts tc, P
     SE3d T = T0;
     // ---- optimizer.optimize(10) ----
     int nact = 0;
-    for (int k = t; k < ne; k += 256) nact += S.level[k] == 0;
+    for (int k = t; k < ne; k += kPoseThreads) nact += S.level[k] == 0;
     {
       double v = nact;
-      block_sum<1>(&v, S);
+      block_sum<1, kPoseWaves>(&v, S);
       nact = (int)v;
     }
     if (nact > 0) {
@@ -1192,7 +1209,7 @@ __global__ void __launch_bounds__(256, ORBPL_POSE_MINW) k_pose(TrackConsts tc, P
         quat_to_R(T.q, R);
         double acc[28];
         for (int k = 0; k < 28; k++) acc[k] = 0;
-        for (int k = t; k < ne; k += 256) {
+        for (int k = t; k < ne; k += kPoseThreads) {
           if (S.level[k]) continue;
           const PoseEdge e = E[k];
           double err[3], J[3][6];
@@ -1202,7 +1219,7 @@ __global__ void __launch_bounds__(256, ORBPL_POSE_MINW) k_pose(TrackConsts tc, P
           double x2 = err[0] * (double)e.info * err[0];
           x2 += err[1] * (double)e.info * err[1];
           x2 += err[2] * (double)e.info * err[2];
-          S.chi2[k] = x2;
+          S.chi2[k] = (float)x2;
           double w = 1.0, r0 = x2;
           if (robust) {
             const bool isMono = e.kind == 0;
@@ -1231,7 +1248,7 @@ __global__ void __launch_bounds__(256, ORBPL_POSE_MINW) k_pose(TrackConsts tc, P
           }
         }
         lap(7);
-        block_sum28_to(acc, S, S.sys[0]);
+        block_sum28_to<kPoseWaves>(acc, S, S.sys[0]);
         lap(1);
         pt[5]++;
         double b[6];
@@ -1271,7 +1288,7 @@ __global__ void __launch_bounds__(256, ORBPL_POSE_MINW) k_pose(TrackConsts tc, P
           double R2[3][3];
           quat_to_R(T.q, R2);
           double tc2 = 0;
-          for (int k = t; k < ne; k += 256) {
+          for (int k = t; k < ne; k += kPoseThreads) {
             if (S.level[k]) continue;
             const PoseEdge e = E[k];
             double err[3];
@@ -1279,7 +1296,7 @@ __global__ void __launch_bounds__(256, ORBPL_POSE_MINW) k_pose(TrackConsts tc, P
             const int dim = e.kind == 1 ? 3 : 2;
             double x2 = 0;
             for (int d = 0; d < dim; d++) x2 += err[d] * (double)e.info * err[d];
-            S.chi2[k] = x2;
+            S.chi2[k] = (float)x2;
             double r0 = x2, w;
             if (robust) {
               const bool isMono = e.kind == 0;
@@ -1287,7 +1304,7 @@ __global__ void __launch_bounds__(256, ORBPL_POSE_MINW) k_pose(TrackConsts tc, P
             }
             tc2 += r0;
           }
-          block_sum<1>(&tc2, S);
+          block_sum<1, kPoseWaves>(&tc2, S);
           lap(3);
           double tempChi = ok2 ? tc2 : 1.7976931348623157e308;
           rho = currentChi - tempChi;
@@ -1319,19 +1336,19 @@ __global__ void __launch_bounds__(256, ORBPL_POSE_MINW) k_pose(TrackConsts tc, P
     double R[3][3];
     quat_to_R(T.q, R);
     int nbad = 0;
-    for (int k = t; k < ne; k += 256) {
+    for (int k = t; k < ne; k += kPoseThreads) {
       const PoseEdge e = E[k];
       const bool was_out = e.kind == 2 ? (S.out_flag[k] != 0) : (outl[e.idx] != 0);
-      double x2 = S.chi2[k];
+      float chi2 = S.chi2[k];
       if (was_out) {
         double err[3];
         edge_error(e, c, T, R, err);
         const int dim = e.kind == 1 ? 3 : 2;
-        x2 = 0;
+        double x2 = 0;
         for (int d = 0; d < dim; d++) x2 += err[d] * (double)e.info * err[d];
-        S.chi2[k] = x2;
+        chi2 = (float)x2;
+        S.chi2[k] = chi2;
       }
-      const float chi2 = (float)x2;
       const float th = e.kind == 0 ? 5.991f : (e.kind == 1 ? 7.815f : 2 * 7.815f);
       const bool bad = chi2 > th;
       if (e.kind == 2) {
@@ -1344,7 +1361,7 @@ __global__ void __launch_bounds__(256, ORBPL_POSE_MINW) k_pose(TrackConsts tc, P
     }
     {
       double v = nbad;
-      block_sum<1>(&v, S);
+      block_sum<1, kPoseWaves>(&v, S);
       nbad = (int)v;
     }
     nBadOut = nbad;
@@ -1366,7 +1383,7 @@ __global__ void __launch_bounds__(256, ORBPL_POSE_MINW) k_pose(TrackConsts tc, P
     }
     __syncthreads();
   }
-  for (int k = t; k < ne; k += 256) {
+  for (int k = t; k < ne; k += kPoseThreads) {
     const PoseEdge e = E[k];
     if (e.kind == 2) {
       if (a.t_kl_un) a.t_loutlier[(long long)s * a.lpitch + e.idx] = S.out_flag[k];
@@ -1555,7 +1572,6 @@ int read_pose_profile(long long* out8) {
 }
 
 void launch_pose(const TrackConsts& c, const PoseLaunch& p, int nstreams, hipStream_t s) {
-  set_smem_attr((const void*)k_pose, sizeof(PoseShared));
   PoseArgs a;
   a.kps_un = p.kps_un;
   a.uright = p.uright;
@@ -1587,7 +1603,20 @@ void launch_pose(const TrackConsts& c, const PoseLaunch& p, int nstreams, hipStr
   a.gate_lm = p.gate_lm;
   static const int prof = getenv("ORBPL_POSE_PROFILE") ? 1 : 0;
   a.prof = prof;
-  hipLaunchKernelGGL(k_pose, dim3(nstreams), dim3(256), sizeof(PoseShared), s, c, a);
+  // one wave per SIMD at k_pose's register footprint: 256 threads per stream
+  // while nstreams * waves <= 4 per CU (lowest latency per stream), then
+  // 128 / 64 (256 streams: 0.40 / 0.50 / 0.71 ms; 1024: 1.48 / 1.00 / 0.80)
+  const int cus = device_cu_count();
+  if (nstreams * 4 <= 4 * cus) {
+    set_smem_attr((const void*)k_pose<256>, sizeof(PoseShared));
+    hipLaunchKernelGGL(k_pose<256>, dim3(nstreams), dim3(256), sizeof(PoseShared), s, c, a);
+  } else if (nstreams * 2 <= 4 * cus) {
+    set_smem_attr((const void*)k_pose<128>, sizeof(PoseShared));
+    hipLaunchKernelGGL(k_pose<128>, dim3(nstreams), dim3(128), sizeof(PoseShared), s, c, a);
+  } else {
+    set_smem_attr((const void*)k_pose<64>, sizeof(PoseShared));
+    hipLaunchKernelGGL(k_pose<64>, dim3(nstreams), dim3(64), sizeof(PoseShared), s, c, a);
+  }
 }
 
 void launch_finish(const TrackConsts& c, StreamState* st, const int* n, int kp_pitch,
