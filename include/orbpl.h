@@ -248,6 +248,46 @@ int orbm_search_by_projection_local(const orbpl_camera* cam, const float* scale_
                                     const int32_t* cur_nobs, float th, float nnratio,
                                     int32_t* match, int* nmatches);
 
+/* ---- DBoW2 ORB vocabulary (ORBVocabulary = TemplatedVocabulary<FORB::
+ * TDescriptor, FORB>, Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h) ---- */
+typedef struct orbv_vocab orbv_vocab;
+/* TemplatedVocabulary::loadFromTextFile (TemplatedVocabulary.h:1338-1420),
+ * System.cc:65: "k L scoring weighting" then one node per line (parent,
+ * isLeaf, 32 descriptor bytes, weight). A line without tokens (the one after a
+ * final '\n') makes no node (pinned P19). Host-only; word ids follow the
+ * isLeaf lines in node order. */
+int orbv_load_text(const char* path, orbv_vocab** out);
+/* The same vocabulary from flat node arrays (node 0 = root, parent[i] < i):
+ * a rank's copy of the vocabulary rank 0 loaded and broadcast. */
+int orbv_create(int k, int L, int scoring, int weighting, int n_nodes, const int32_t* parent,
+                const uint8_t* leaf_flag, const uint8_t* desc, const double* weight,
+                orbv_vocab** out);
+int orbv_destroy(orbv_vocab* v);
+/* out6 = k, L, scoring, weighting, n_nodes, n_words */
+int orbv_info(const orbv_vocab* v, int* out6);
+/* the flat node arrays orbv_create takes (n_nodes entries; desc 32 B rows) */
+int orbv_export(const orbv_vocab* v, int32_t* parent, uint8_t* leaf_flag, uint8_t* desc,
+                double* weight);
+/* copy the tree to `device` (CSR children, descriptors, words, weights) */
+int orbv_upload(orbv_vocab* v, int device);
+/* TemplatedVocabulary::transform(features, BowVector, FeatureVector, levelsup)
+ * (TemplatedVocabulary.h:1127-1205, 1226-1262) as Frame::ComputeBoW calls it
+ * (Frame.cc:730, levelsup 4): the BowVector as bow_n (word, value) pairs in
+ * word order, the FeatureVector as the node (at level L - levelsup) of every
+ * feature, -1 for a stopped word (weight 0). n <= 4096; bow buffers >= n. */
+int orbv_transform(orbv_vocab* v, int device, const uint8_t* desc, int n, int levelsup,
+                   uint32_t* bow_words, double* bow_vals, int* bow_n, int32_t* feat_node);
+/* The same for nframes device-resident frames: frame f's descriptors at
+ * d_desc + f * desc_pitch * 32 (d_n[f] of them, <= max_n <= 4096); outputs
+ * per frame at f * out_pitch (feature word / weight / node, BowVector), the
+ * BowVector length in d_bow_n[f]; d_err bit 1 = a frame above 4096 features.
+ * `stream` = a hipStream_t (NULL: the vocabulary's own stream). */
+int orbv_transform_batch_device(orbv_vocab* v, const uint8_t* d_desc, int64_t desc_pitch,
+                                const int* d_n, int nframes, int max_n, int levelsup,
+                                int32_t* d_feat_node, int32_t* d_feat_word, double* d_feat_weight,
+                                uint32_t* d_bow_words, double* d_bow_vals, int* d_bow_n,
+                                int64_t out_pitch, int* d_err, void* stream);
+
 /* ORBmatcher(nnratio, checkOri).SearchByBoW(pKF, F, vpMapPointMatches)
  * (ORBmatcher.cc:247-410). The DBoW2 FeatureVectors are passed as one
  * vocabulary node id per feature (-1: none; ids < 2^21 - 1): features meet

@@ -614,3 +614,62 @@ class LVO:
             lib().oracle_lvo_destroy(self.h)
         except Exception:
             pass
+
+
+# ---- DBoW2 vocabulary (bow_oracle.cpp) ----
+def _setup_voc(L):
+    vp, i = C.c_void_p, C.c_int
+    L.oracle_voc_load_text.argtypes = [C.c_char_p]
+    L.oracle_voc_load_text.restype = vp
+    L.oracle_voc_destroy.argtypes = [vp]
+    L.oracle_voc_info.argtypes = [vp, vp]
+    L.oracle_voc_nodes.argtypes = [vp, vp, vp, vp, vp, vp]
+    L.oracle_voc_transform.argtypes = [vp, vp, i, i, vp, vp, C.POINTER(C.c_int), vp, vp, vp]
+
+
+class Vocabulary:
+    """ORBVocabulary::loadFromTextFile + transform (TemplatedVocabulary.h:1338,
+    1127-1262)."""
+
+    def __init__(self, path):
+        L = lib()
+        if not hasattr(L, "_voc_ready"):
+            _setup_voc(L)
+            L._voc_ready = True
+        self.h = L.oracle_voc_load_text(str(path).encode())
+        if not self.h:
+            raise ValueError(f"vocabulary load failed: {path}")
+        info = np.zeros(6, np.int32)
+        L.oracle_voc_info(self.h, _p(info))
+        self.k, self.L, self.scoring, self.weighting, self.n_nodes, self.n_words = map(int, info)
+
+    def nodes(self):
+        n = self.n_nodes
+        parent = np.zeros(n, np.int32)
+        leaf = np.zeros(n, np.uint8)
+        word = np.zeros(n, np.int32)
+        weight = np.zeros(n, np.float64)
+        desc = np.zeros((n, 32), np.uint8)
+        lib().oracle_voc_nodes(self.h, _p(parent), _p(leaf), _p(word), _p(weight), _p(desc))
+        return dict(parent=parent, leaf=leaf, word=word, weight=weight, desc=desc)
+
+    def transform(self, desc, levelsup=4):
+        """-> (bow_words u32, bow_values f64, feat_node i32 (-1 = stopped),
+        feat_word i32, feat_weight f64)"""
+        desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        n = len(desc)
+        words = np.zeros(max(1, n), np.uint32)
+        vals = np.zeros(max(1, n), np.float64)
+        node = np.zeros(max(1, n), np.int32)
+        fw = np.zeros(max(1, n), np.int32)
+        fwt = np.zeros(max(1, n), np.float64)
+        bn = C.c_int(0)
+        lib().oracle_voc_transform(self.h, _p(desc), n, levelsup, _p(words), _p(vals), C.byref(bn),
+                                   _p(node), _p(fw), _p(fwt))
+        k = bn.value
+        return words[:k].copy(), vals[:k].copy(), node[:n].copy(), fw[:n].copy(), fwt[:n].copy()
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().oracle_voc_destroy(self.h)
+            self.h = None

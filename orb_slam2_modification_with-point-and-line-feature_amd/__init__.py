@@ -926,3 +926,99 @@ class LineExtractor(LineSegmentDetector):
                                       C.byref(n)), "lsdx_get_keylines")
         k = n.value
         return kl[:k].copy(), desc[:k].copy(), coef[:k].copy()
+
+
+# ---------------------------------------------------------------------------
+# DBoW2 ORB vocabulary (ORBVocabulary, Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h)
+# ---------------------------------------------------------------------------
+def _declare_voc(L):
+    vp, i, ip = C.c_void_p, C.c_int, C.POINTER(C.c_int)
+    L.orbv_load_text.argtypes = [C.c_char_p, C.POINTER(vp)]
+    L.orbv_create.argtypes = [i, i, i, i, i, vp, vp, vp, vp, C.POINTER(vp)]
+    L.orbv_destroy.argtypes = [vp]
+    L.orbv_info.argtypes = [vp, vp]
+    L.orbv_export.argtypes = [vp, vp, vp, vp, vp]
+    L.orbv_upload.argtypes = [vp, i]
+    L.orbv_transform.argtypes = [vp, i, vp, i, i, vp, vp, ip, vp]
+    L.orbv_transform_batch_device.argtypes = [vp, vp, C.c_int64, vp, i, i, i, vp, vp, vp, vp, vp,
+                                              vp, C.c_int64, vp, vp]
+
+
+_declare_prev_voc = _declare
+
+
+def _declare(L):  # noqa: F811
+    _declare_prev_voc(L)
+    _declare_voc(L)
+
+
+class ORBVocabulary:
+    """TemplatedVocabulary<FORB::TDescriptor, FORB>: loadFromTextFile (host),
+    transform on the GPU. Construct with `path` (the reference's text format)
+    or `arrays` (dict from to_arrays(): parent, leaf, desc, weight, k, L,
+    scoring, weighting) - e.g. a rank's copy of rank 0's broadcast."""
+
+    def __init__(self, path=None, arrays=None, device=0):
+        h = C.c_void_p()
+        if path is not None:
+            check(lib().orbv_load_text(str(path).encode(), C.byref(h)), "orbv_load_text")
+        else:
+            a = arrays
+            par = _c(a["parent"], np.int32)
+            leaf = _c(a["leaf"], np.uint8)
+            desc = _c(a["desc"], np.uint8)
+            wt = _c(a["weight"], np.float64)
+            check(lib().orbv_create(int(a["k"]), int(a["L"]), int(a["scoring"]),
+                                    int(a["weighting"]), len(par), _ptr(par), _ptr(leaf),
+                                    _ptr(desc), _ptr(wt), C.byref(h)), "orbv_create")
+        self._h = h
+        self.device = device
+        info = np.zeros(6, np.int32)
+        check(lib().orbv_info(self._h, _ptr(info)), "orbv_info")
+        self.k, self.L, self.scoring, self.weighting, self.n_nodes, self.n_words = map(int, info)
+
+    @classmethod
+    def loadFromTextFile(cls, path, device=0):
+        return cls(path=path, device=device)
+
+    def to_arrays(self):
+        n = self.n_nodes
+        a = dict(parent=np.zeros(n, np.int32), leaf=np.zeros(n, np.uint8),
+                 desc=np.zeros((n, 32), np.uint8), weight=np.zeros(n, np.float64))
+        check(lib().orbv_export(self._h, _ptr(a["parent"]), _ptr(a["leaf"]), _ptr(a["desc"]),
+                                _ptr(a["weight"])), "orbv_export")
+        a.update(k=self.k, L=self.L, scoring=self.scoring, weighting=self.weighting)
+        return a
+
+    def upload(self):
+        check(lib().orbv_upload(self._h, self.device), "orbv_upload")
+
+    def transform(self, desc, levelsup=4):
+        """-> (bow_words u32, bow_values f64, feat_node i32 per feature, -1 = stopped)"""
+        desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        n = len(desc)
+        words = np.zeros(max(1, n), np.uint32)
+        vals = np.zeros(max(1, n), np.float64)
+        node = np.zeros(max(1, n), np.int32)
+        bn = C.c_int(0)
+        check(lib().orbv_transform(self._h, self.device, _ptr(desc), n, levelsup, _ptr(words),
+                                   _ptr(vals), C.byref(bn), _ptr(node)), "orbv_transform")
+        k = bn.value
+        return words[:k].copy(), vals[:k].copy(), node[:n].copy()
+
+    def transform_batch_device(self, d_desc, desc_pitch, d_n, nframes, max_n, levelsup, out,
+                               stream=None):
+        """out: dict of DeviceBuffers feat_node, feat_word, feat_weight,
+        bow_words, bow_vals, bow_n, err (pitch out['pitch'])."""
+        check(lib().orbv_transform_batch_device(
+            self._h, C.c_void_p(d_desc), desc_pitch, C.c_void_p(d_n), nframes, max_n, levelsup,
+            C.c_void_p(out["feat_node"].ptr), C.c_void_p(out["feat_word"].ptr),
+            C.c_void_p(out["feat_weight"].ptr), C.c_void_p(out["bow_words"].ptr),
+            C.c_void_p(out["bow_vals"].ptr), C.c_void_p(out["bow_n"].ptr), out["pitch"],
+            C.c_void_p(out["err"].ptr), None if stream is None else C.c_void_p(stream)),
+            "orbv_transform_batch_device")
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.orbv_destroy(self._h)
+            self._h = None

@@ -253,3 +253,105 @@ def loop_trajectory(n, seed=0, step_t=0.012, rot_amp_deg=4.0):
                     0.3 * a * np.cos(th + ph[2]))
         poses.append(se3(R, t))
     return poses
+
+
+# ---------------------------------------------------------------------------
+# Synthetic ORB vocabulary (the reference's ORBvoc.txt is not in its
+# checkout): a complete k-ary tree of depth L built DBoW2-style by
+# hierarchical k-medians on binary descriptors (seeded centres, member
+# majority bits), TF-IDF word weights idf = log(N / N_i) over the training
+# documents (0 for unseen or ubiquitous words = stopped), written in DBoW2's
+# text format (TemplatedVocabulary::saveToTextFile, TemplatedVocabulary.h:1427).
+# Node ids are breadth-first, so a node's children are contiguous.
+# ---------------------------------------------------------------------------
+def _hamming_rows(X, Cc):
+    """X [m,4] u64, Cc [k,4] u64 -> [m,k] Hamming distances."""
+    return np.bitwise_count(X[:, None, :] ^ Cc[None, :, :]).sum(-1)
+
+
+def _majority(X):
+    """Bitwise majority of rows X [m,4] u64 (FORB::meanValue: bit set when
+    its count >= ceil(m / 2))."""
+    bits = np.unpackbits(X.view(np.uint8).reshape(len(X), 32), axis=1)
+    need = (len(X) + 1) // 2
+    return np.packbits((bits.sum(0) >= need).astype(np.uint8)).view(np.uint64).reshape(4)
+
+
+def vocabulary_tree(train, k=10, L=5, seed=0, iters=3):
+    """train: list of [n_i, 32] u8 descriptor arrays (one per document).
+    Returns dict(parent, desc [N,32] u8, leaf, weight, first_child, k, L)."""
+    rng = np.random.default_rng(seed)
+    docs = [np.ascontiguousarray(d, np.uint8).reshape(-1, 32) for d in train]
+    X = np.concatenate(docs).view(np.uint64).reshape(-1, 4)
+    nn = (k ** (L + 1) - 1) // (k - 1)
+    desc = np.zeros((nn, 4), np.uint64)
+    parent = np.full(nn, -1, np.int64)
+    members = {0: np.arange(len(X))}
+    nxt = 1
+    first_child = np.full(nn, -1, np.int64)
+    for node in range(nn):
+        level = 0 if node == 0 else int(np.floor(np.log(node * (k - 1) + 1) / np.log(k) + 1e-9))
+        if level >= L:
+            break
+        idx = members.pop(node, np.zeros(0, np.int64))
+        m = len(idx)
+        if m >= k:
+            Cc = X[idx[rng.choice(m, k, replace=False)]].copy()
+            for _ in range(iters):
+                a = _hamming_rows(X[idx], Cc).argmin(1)
+                for c in range(k):
+                    sel = idx[a == c]
+                    if len(sel):
+                        Cc[c] = _majority(X[sel])
+            a = _hamming_rows(X[idx], Cc).argmin(1)
+        else:
+            Cc = rng.integers(0, 2 ** 63, size=(k, 4), dtype=np.uint64)
+            if m:
+                Cc[:m] = X[idx]
+            a = _hamming_rows(X[idx], Cc).argmin(1) if m else np.zeros(0, np.int64)
+        first_child[node] = nxt
+        for c in range(k):
+            desc[nxt + c] = Cc[c]
+            parent[nxt + c] = node
+            members[nxt + c] = idx[a == c]
+        nxt += k
+    leaf = first_child < 0
+    tree = dict(parent=parent, desc=desc.view(np.uint8).reshape(nn, 32), leaf=leaf,
+                first_child=first_child, k=k, L=L, weight=np.zeros(nn))
+    # idf over the documents
+    N = len(docs)
+    Ni = np.zeros(nn, np.int64)
+    for d in docs:
+        Ni[np.unique(vocabulary_words(tree, d))] += 1
+    w = np.zeros(nn)
+    seen = (Ni > 0) & leaf
+    w[seen] = np.log(N / Ni[seen])
+    tree["weight"] = w
+    return tree
+
+
+def vocabulary_words(tree, desc):
+    """Leaf node of every descriptor (strict <: first minimal child)."""
+    D = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32).view(np.uint64).reshape(-1, 4)
+    V = tree["desc"].view(np.uint64).reshape(-1, 4)
+    k = tree["k"]
+    node = np.zeros(len(D), np.int64)
+    while True:
+        fc = tree["first_child"][node]
+        if np.all(fc < 0):
+            return node
+        ch = fc[:, None] + np.arange(k)[None, :]
+        d = np.bitwise_count(D[:, None, :] ^ V[ch]).sum(-1)
+        node = np.where(fc >= 0, ch[np.arange(len(D)), d.argmin(1)], node)
+
+
+def vocabulary_text(tree, scoring=0, weighting=0):
+    """DBoW2 text format: "k L  scoring weighting", then one line per node
+    1..N-1: parent, isLeaf, 32 descriptor bytes, weight (C++ stream default
+    formatting), each line ended by '\\n' like saveToTextFile's endl."""
+    out = [f"{tree['k']} {tree['L']}  {scoring} {weighting}\n"]
+    for i in range(1, len(tree["parent"])):
+        d = " ".join(str(int(b)) for b in tree["desc"][i])
+        out.append(f"{int(tree['parent'][i])} {1 if tree['leaf'][i] else 0} {d}  "
+                   f"{tree['weight'][i]:g}\n")
+    return "".join(out)
