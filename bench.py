@@ -309,7 +309,74 @@ def torchrun_cmd(ngpus, argv, port):
             str(Path(__file__).resolve())] + list(argv)
 
 
-def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, device, dist):
+def share_tree(tree, dist):
+    """Rank 0's vocabulary tree on every rank (broadcast)."""
+    if dist:
+        box = [tree]
+        dist.broadcast_object_list(box, src=0)
+        tree = box[0]
+    return tree
+
+
+def shared_idf(synth, tree, docs, dist, rccl_device=None):
+    """TF-IDF word weights (synth.idf_weights) over every rank's training
+    documents: each rank counts the documents its words occur in, one SUM
+    all-reduce of the counts (+ the document count) - RCCL on `rccl_device`
+    when given, gloo otherwise."""
+    nn = len(tree["parent"])
+    ni = np.zeros(nn + 1, np.float64)
+    for d in docs:
+        ni[np.unique(synth.vocabulary_words(tree, d))] += 1
+    ni[nn] = len(docs)
+    backend = "none"
+    if dist:
+        import torch
+        if rccl_device is not None:
+            backend = "rccl"
+            if not hasattr(shared_idf, "group"):
+                shared_idf.group = dist.new_group(backend="nccl")
+            torch.cuda.set_device(rccl_device)
+            t = torch.from_numpy(ni).to(f"cuda:{rccl_device}")
+            dist.all_reduce(t, group=shared_idf.group)
+            ni = t.cpu().numpy()
+        else:
+            backend = "gloo"
+            t = torch.from_numpy(ni)
+            dist.all_reduce(t)
+            ni = t.numpy()
+    n_docs, ni = ni[nn], ni[:nn]
+    return synth.idf_weights(tree, ni, n_docs), int(n_docs), backend
+
+
+def build_vocabulary(pkg, synth, args, rank, world, device, dist):
+    """The ORB vocabulary every rank's trackers share: rank 0
+    builds the tree (seeded hierarchical k-medians, synth.vocabulary_tree, on
+    the GPU extractor's descriptors of its rendered training frames) and
+    broadcasts it; the TF-IDF weights come from every rank's own training
+    frames through one all-reduce (shared_idf)."""
+    k, L = 10, args.vocab_levels
+    frames, _ = render_loop(6, seed=100 + rank, workers=min(16, os.cpu_count() or 4))
+    ex = pkg.ORBextractor(1000, 1.2, 8, 20, 7, width=W, height=H, device=device)
+    docs = [ex(f)[1] for f in frames]
+    ex.close()
+    tree = share_tree(synth.vocabulary_tree(docs, k=k, L=L, seed=1) if rank == 0 else None, dist)
+    rccl = None
+    if dist:
+        import torch
+        if pkg.device_count() >= world and torch.cuda.is_available():
+            rccl = device
+    w, n_docs, backend = shared_idf(synth, tree, docs, dist, rccl)
+    voc = pkg.ORBVocabulary(arrays=dict(parent=tree["parent"], leaf=tree["leaf"], desc=tree["desc"],
+                                        weight=w, k=k, L=L, scoring=0, weighting=0), device=device)
+    info = {"k": k, "L": L, "nodes": voc.n_nodes, "words": voc.n_words,
+            "stopped_words": int(((w == 0) & tree["leaf"]).sum()), "levelsup": 4,
+            "documents": n_docs, "idf_reduction": backend,
+            "source": "synthetic: seeded hierarchical k-medians on rendered frames' ORB "
+                      "descriptors (the reference's ORBvoc.txt is not in its checkout)"}
+    return voc, info
+
+
+def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, device, dist, voc=None):
     """Time `steps` tracker steps of one workload; returns the measurements."""
     wl = WORKLOADS[workload]
     lines, stereo, cam_name = wl["lines"], wl["stereo"], wl["cam"]
@@ -334,6 +401,8 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
     # LSD-bound line workloads gain nothing from it
     pipelined = args.pipelined if args.pipelined >= 0 else (0 if lines else 1)
     tr.set_pipelined(bool(pipelined))
+    if voc is not None:
+        tr.set_vocabulary(voc, 4)    # KeyFrame::ComputeBoW of every frame (P18)
     tr.reset(np.stack([np.linalg.inv(L.Twc(s, 0)).astype(np.float32) for s in range(S)]).reshape(S, 16))
     tr.set_history(warmup + steps)
     fb = fw * fh
@@ -633,6 +702,10 @@ def main():
     ap.add_argument("--fixed-line-jacobian", type=int, default=0,
                     help="1 = the analytic line-edge Jacobian instead of the reference's "
                          "as-written one (pinned P7)")
+    ap.add_argument("--bow", type=int, default=1,
+                    help="1 = every frame's KeyFrame::ComputeBoW with a shared synthetic "
+                         "vocabulary (broadcast + IDF all-reduce over ranks); 0 = off")
+    ap.add_argument("--vocab-levels", type=int, default=5, help="vocabulary depth L (k = 10)")
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the oracle replay of the timed trackers' sampled streams")
     args = ap.parse_args()
@@ -658,24 +731,26 @@ def main():
     ndev = pkg.device_count()
     device = local_rank % max(1, ndev)
 
+    voc, voc_info = build_vocabulary(pkg, synth, args, rank, world, device, dist) if args.bow \
+        else (None, None)
     res = run_workload(pkg, synth, args, args.workload, args.streams, args.steps, args.warmup,
-                       rank, world, device, dist)
+                       rank, world, device, dist, voc)
     res["nsteps"] = args.steps
     # other BASELINE configs, same clock discipline, fewer steps (points runs only)
     others = {}
     if args.workload == "points" and args.secondary_steps > 0:
         others["secondary"] = run_workload(pkg, synth, args, "lines", args.lines_streams,
                                            args.secondary_steps, max(1, args.warmup // 2), rank,
-                                           world, device, dist)
+                                           world, device, dist, voc)
         others["secondary"]["nsteps"] = args.secondary_steps
     if args.workload == "points" and args.stereo_steps > 0:
         others["stereo"] = run_workload(pkg, synth, args, "kitti", args.stereo_streams,
                                         args.stereo_steps, max(1, args.warmup // 2), rank, world,
-                                        device, dist)
+                                        device, dist, voc)
         others["stereo"]["nsteps"] = args.stereo_steps
     if args.workload == "points" and args.rig_steps > 0:
         others["rig"] = run_workload(pkg, synth, args, "rig", args.rig_streams, args.rig_steps,
-                                     max(1, args.warmup // 2), rank, world, device, dist)
+                                     max(1, args.warmup // 2), rank, world, device, dist, voc)
         others["rig"]["nsteps"] = args.rig_steps
 
     # parity of every timed tracker's sampled streams against the oracle
@@ -729,7 +804,9 @@ def main():
                        "image": res["image"], "nfeatures": res["nfeatures"], "streams_per_gpu": S,
                        "frames_per_step": S * world, "parallelism": f"streams sharded x{world}",
                        "pipelined": res["pipelined"], "track_local_map": bool(args.local_map),
-                       "fixed_line_jacobian": bool(args.fixed_line_jacobian)},
+                       "fixed_line_jacobian": bool(args.fixed_line_jacobian),
+                       "keyframe_bow": bool(args.bow)},
+            "vocabulary": voc_info,
             "stage_ms": res["stages"],
             "tracking": res["tracking"],
             "roofline": res["roof"],

@@ -412,10 +412,12 @@ int orbpl_tracker_get_state(orbpl_tracker* tr, float* Tcw, int* nkeypoints, int*
 /* hipEvent times of the last step (ms): extract, glue, match, pose, finish. */
 int orbpl_tracker_stage_ms(orbpl_tracker* tr, float* ms5);
 /* Per-kernel device times (ms, hipEvents on the tracker stream) of the last
- * min(max_steps, 64) steps, 10 per step: pyramid (+ borders + blur, one
+ * min(max_steps, 64) steps, 11 per step: pyramid (+ borders + blur, one
  * launch), blur (0), fast, octree, orient+desc, glue+predict, match, pose,
  * finish, local_map (TrackLocalMap: gather, IsInFrustum, local point and line
- * search, second pose, counts; 0 without ORBPL_TRACK_LOCAL_MAP). */
+ * search, second pose, counts; 0 without ORBPL_TRACK_LOCAL_MAP), bow
+ * (KeyFrame::ComputeBoW; 0 without a vocabulary). Stereo matching counts in
+ * glue. */
 int orbpl_tracker_timings(orbpl_tracker* tr, int max_steps, float* ms, int* n_steps);
 int orbpl_tracker_timings_reset(orbpl_tracker* tr);
 /* Debug (ORBPL_POSE_PROFILE set): stream 0's PoseOptimization phase times of
@@ -457,6 +459,15 @@ int orbpl_tracker_line_timings(orbpl_tracker* tr, int max_steps, float* ms, int*
 int orbpl_tracker_set_history(orbpl_tracker* tr, int max_steps);
 int orbpl_tracker_get_history(orbpl_tracker* tr, int stream, int max_steps, float* Tcw,
                               int* counts12, int* n_steps);
+/* KeyFrame::ComputeBoW (KeyFrame.cc:67; every tracked frame is a keyframe,
+ * P18) with `voc` (uploaded to the tracker's device; not owned, must outlive
+ * the tracker or be unset with NULL): each step transforms the frame's
+ * descriptors on the extraction stream (levelsup: Frame::ComputeBoW's 4). */
+int orbpl_tracker_set_vocabulary(orbpl_tracker* tr, orbv_vocab* voc, int levelsup);
+/* the last step's BowVector / FeatureVector of one stream (buffers of the
+ * tracker's keypoint capacity); n = its keypoints */
+int orbpl_tracker_get_bow(orbpl_tracker* tr, int stream, uint32_t* bow_words, double* bow_vals,
+                          int* bow_n, int32_t* feat_node, int* n);
 /* TrackLocalMap outcome of the last step per stream (ORBPL_TRACK_LOCAL_MAP; 0
  * where it did not run): SearchLocalPoints matches, mnMatchesInliers,
  * SearchLocalLines matches (every passing pair counts), mnLineMatchesInliers. */

@@ -361,6 +361,8 @@ def _declare_track(L):
     L.orbpl_tracker_set_history.argtypes = [vp, i]
     L.orbpl_tracker_get_history.argtypes = [vp, i, i, vp, vp, ip]
     L.orbpl_tracker_get_local_stats.argtypes = [vp, vp, vp, vp, vp]
+    L.orbpl_tracker_set_vocabulary.argtypes = [vp, vp, i]
+    L.orbpl_tracker_get_bow.argtypes = [vp, i, vp, vp, ip, vp, ip]
 
 
 _declare_orig = _declare
@@ -677,6 +679,25 @@ class Tracker:
               "orbpl_tracker_get_status")
         return dict(ok=ok, nlines=nl, line_matches=lm, line_nmatches_map=lnm)
 
+    def set_vocabulary(self, voc, levelsup=4):
+        """KeyFrame::ComputeBoW of every step's frame with an ORBVocabulary
+        (None: off). The tracker keeps a reference so the vocabulary outlives
+        its use."""
+        check(lib().orbpl_tracker_set_vocabulary(self._h, voc._h if voc is not None else None,
+                                                 levelsup), "orbpl_tracker_set_vocabulary")
+        self._voc = voc
+
+    def bow(self, stream):
+        """The last step's (bow_words, bow_values, feat_node) of one stream."""
+        K = self.kp_cap
+        w = np.zeros(K, np.uint32)
+        v = np.zeros(K, np.float64)
+        node = np.zeros(K, np.int32)
+        bn, n = C.c_int(0), C.c_int(0)
+        check(lib().orbpl_tracker_get_bow(self._h, stream, _ptr(w), _ptr(v), C.byref(bn),
+                                          _ptr(node), C.byref(n)), "orbpl_tracker_get_bow")
+        return w[:bn.value].copy(), v[:bn.value].copy(), node[:n.value].copy()
+
     def local_stats(self):
         """TrackLocalMap counts per stream of the last step (local_map=True)."""
         S = self.S
@@ -757,11 +778,11 @@ class Tracker:
         return ms
 
     STAGES = ("pyramid", "blur", "fast", "octree", "orient_desc", "glue", "match", "pose",
-              "finish", "local_map")
+              "finish", "local_map", "bow")
 
     def timings(self, max_steps=64):
-        """(n_steps, 10) per-kernel ms of the last steps (hipEvents in-stream)."""
-        ms = np.zeros((max_steps, 10), np.float32)
+        """(n_steps, 11) per-kernel ms of the last steps (hipEvents in-stream)."""
+        ms = np.zeros((max_steps, 11), np.float32)
         n = C.c_int(0)
         check(lib().orbpl_tracker_timings(self._h, max_steps, _ptr(ms), C.byref(n)),
               "orbpl_tracker_timings")

@@ -102,6 +102,7 @@ __global__ void __launch_bounds__(256) k_bow_words(VocDev v, BowBatch b) {
 
 __global__ void __launch_bounds__(256) k_bow_vector(VocDev v, BowBatch b) {
   __shared__ uint32_t key[kBowMaxFeat];
+  __shared__ double sval[kBowMaxFeat];   // BowVector values in word order
   __shared__ int wsum[4];
   __shared__ double s_norm;
   const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -158,29 +159,35 @@ __global__ void __launch_bounds__(256) k_bow_vector(VocDev v, BowBatch b) {
       for (int q = p + 1; q < np && key[q] != kNoKey && (key[q] >> 12) == (k >> 12); q++)
         val += b.feat_weight[o + (key[q] & 4095u)];
     b.bow_words[o + r] = k >> 12;
-    b.bow_vals[o + r] = val;
+    sval[r] = val;
     r++;
   }
   __syncthreads();
+  double div = 1.0;
   if (v.norm == 0 && v.tf && nruns > 0) {
-    const double nd = (double)nruns;
-    for (int q = t; q < nruns; q += 256) b.bow_vals[o + q] /= nd;
+    div = (double)nruns;
   } else if (v.norm) {
     if (t == 0) {
+      // one sequential sum in word order (BowVector::normalize), loads from
+      // LDS eight ahead of the dependent adds
       double norm = 0.0;
-      if (v.norm == 1) {
-        for (int q = 0; q < nruns; q++) norm += fabs(b.bow_vals[o + q]);
-      } else {
-        for (int q = 0; q < nruns; q++) norm += b.bow_vals[o + q] * b.bow_vals[o + q];
-        norm = sqrt(norm);
+      int q = 0;
+      for (; q + 8 <= nruns; q += 8) {
+        double x[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) x[u] = sval[q + u];
+#pragma unroll
+        for (int u = 0; u < 8; u++) norm += v.norm == 1 ? fabs(x[u]) : x[u] * x[u];
       }
+      for (; q < nruns; q++) norm += v.norm == 1 ? fabs(sval[q]) : sval[q] * sval[q];
+      if (v.norm == 2) norm = sqrt(norm);
       s_norm = norm;
     }
     __syncthreads();
-    const double norm = s_norm;
-    if (norm > 0.0)
-      for (int q = t; q < nruns; q += 256) b.bow_vals[o + q] /= norm;
+    div = s_norm > 0.0 ? s_norm : 1.0;
   }
+  const bool scale = (v.norm == 0 && v.tf) || (v.norm && s_norm > 0.0);
+  for (int q = t; q < nruns; q += 256) b.bow_vals[o + q] = scale ? sval[q] / div : sval[q];
   if (t == 0) b.bow_n[f] = nruns;
 }
 

@@ -743,6 +743,13 @@ struct FrameBufs {
   uint8_t* loutlier = nullptr;
   uint8_t* has_ml = nullptr;
   float* ml_xyz = nullptr;
+  // DBoW2 (orbpl_tracker_set_vocabulary): KeyFrame::ComputeBoW of the frame
+  int32_t* feat_node = nullptr;   // FeatureVector: node per keypoint, -1 = stopped
+  int32_t* feat_word = nullptr;
+  double* feat_weight = nullptr;
+  uint32_t* bow_words = nullptr;  // BowVector (word order)
+  double* bow_vals = nullptr;
+  int* bow_n = nullptr;
 };
 
 struct orbpl_tracker {
@@ -795,7 +802,7 @@ struct orbpl_tracker {
   StreamState* d_state = nullptr;
   PoseEdge* d_edges = nullptr;
   static constexpr int kRing = 64;   // steps kept in the timing ring
-  static constexpr int kEv = 27;     // events per step
+  static constexpr int kEv = 28;     // events per step
   std::vector<hipEvent_t> ring;      // kRing * kEv events
   int ring_pos = 0, ring_count = 0;
   // TrackLocalMap (ORBPL_TRACK_LOCAL_MAP): ring of the last kLmK keyframes'
@@ -803,6 +810,9 @@ struct orbpl_tracker {
   static constexpr int kLmK = 4;
   int local_map = 0;
   int lm_step = 0;                 // frames since reset (Frame::mnId)
+  orbv_vocab* voc = nullptr;       // orbpl_tracker_set_vocabulary (not owned)
+  int voc_levelsup = 4;
+  int* d_bow_err = nullptr;
   float scale_factor = 1.2f;
   long long lp = 0, llp = 0;
   float *kr_xyz = nullptr, *kr_nrm = nullptr, *kr_dmin = nullptr, *kr_dmax = nullptr;
@@ -1244,6 +1254,15 @@ static int tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_
     a.err = t->d_err;
     launch_stereo(a, S, s);
   }
+  HIP_CHECK(hipEventRecord(ev[27], s));
+  if (t->voc) {
+    // every tracked frame is a keyframe (P18): KeyFrame::ComputeBoW
+    // (KeyFrame.cc:67, Frame.cc:730) on the extraction stream
+    rc = orbv_transform_batch_device(t->voc, C.desc, K, C.n, S, K, t->voc_levelsup, C.feat_node,
+                                     C.feat_word, C.feat_weight, C.bow_words, C.bow_vals, C.bow_n,
+                                     K, t->d_bow_err, (void*)s);
+    if (rc) return rc;
+  }
   HIP_CHECK(hipEventRecord(ev[6], s));
   // ---- tracking stream
   HIP_CHECK(hipStreamWaitEvent(ts, ev[6], 0));
@@ -1549,14 +1568,15 @@ int orbpl_tracker_timings(orbpl_tracker* t, int max_steps, float* ms, int* n_ste
   // stage intervals: 5 extraction stages, glue (extraction stream), then
   // match (incl. prediction), pose, finish (tracking stream)
   // (+ TrackLocalMap: gather, frustum, local matching, second pose, count)
-  static const int kPair[10][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 6},
-                                   {7, 8}, {14, 9}, {26, 10}, {9, 26}};
+  // (+ KeyFrame::ComputeBoW with a vocabulary; 0 without)
+  static const int kPair[11][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 27},
+                                   {7, 8}, {14, 9}, {26, 10}, {9, 26}, {27, 6}};
   const int n = std::min(max_steps, t->ring_count);
   for (int k = 0; k < n; k++) {
     const int step = t->ring_pos - n + k;
     hipEvent_t* ev = &t->ring[(size_t)(step % orbpl_tracker::kRing) * orbpl_tracker::kEv];
-    for (int i = 0; i < 10; i++)
-      HIP_CHECK(hipEventElapsedTime(&ms[k * 10 + i], ev[kPair[i][0]], ev[kPair[i][1]]));
+    for (int i = 0; i < 11; i++)
+      HIP_CHECK(hipEventElapsedTime(&ms[k * 11 + i], ev[kPair[i][0]], ev[kPair[i][1]]));
   }
   *n_steps = n;
   return ORBPL_OK;
@@ -1765,6 +1785,65 @@ int orbpl_tracker_get_status(orbpl_tracker* t, int* ok, int* nlines, int* line_m
     if (line_matches) line_matches[s] = t->lines ? st[s].nlmatches : 0;
     if (line_nmatches_map) line_nmatches_map[s] = t->lines ? st[s].nlmatches_map : 0;
   }
+  return ORBPL_OK;
+}
+
+int orbpl_tracker_set_vocabulary(orbpl_tracker* t, orbv_vocab* voc, int levelsup) {
+  if (!t) return arg_fail("NULL tracker");
+  HIP_CHECK(hipSetDevice(t->device));
+  HIP_CHECK(hipStreamSynchronize(t->stream));
+  HIP_CHECK(hipStreamSynchronize(t->tstream));
+  if (!voc) {
+    t->voc = nullptr;
+    return ORBPL_OK;
+  }
+  if (t->kp_cap > 4096) return arg_fail("orbpl_tracker_set_vocabulary: > 4096 keypoints per frame");
+  const int rc = orbv_upload(voc, t->device);
+  if (rc) return rc;
+  if (!t->d_bow_err) {
+    const size_t SK = (size_t)t->S * t->kp_cap;
+    auto alloc = [&](void** p, size_t bytes) -> int {
+      HIP_CHECK(hipMalloc(p, bytes));
+      t->allocs.push_back(*p);
+      return ORBPL_OK;
+    };
+    for (FrameBufs& f : t->fb) {
+      if (alloc((void**)&f.feat_node, SK * 4) || alloc((void**)&f.feat_word, SK * 4) ||
+          alloc((void**)&f.feat_weight, SK * 8) || alloc((void**)&f.bow_words, SK * 4) ||
+          alloc((void**)&f.bow_vals, SK * 8) || alloc((void**)&f.bow_n, (size_t)t->S * 4))
+        return ORBPL_ERR_HIP;
+      HIP_CHECK(hipMemset(f.bow_n, 0, (size_t)t->S * 4));
+    }
+    if (alloc((void**)&t->d_bow_err, 4)) return ORBPL_ERR_HIP;
+    HIP_CHECK(hipMemset(t->d_bow_err, 0, 4));
+  }
+  t->voc = voc;
+  t->voc_levelsup = levelsup;
+  return ORBPL_OK;
+}
+
+int orbpl_tracker_get_bow(orbpl_tracker* t, int stream, uint32_t* bow_words, double* bow_vals,
+                          int* bow_n, int32_t* feat_node, int* n) {
+  if (!t || stream < 0 || stream >= t->S) return arg_fail("bad argument");
+  if (!t->d_bow_err) return arg_fail("orbpl_tracker_get_bow: no vocabulary set");
+  HIP_CHECK(hipSetDevice(t->device));
+  HIP_CHECK(hipStreamSynchronize(t->stream));
+  HIP_CHECK(hipStreamSynchronize(t->tstream));
+  const FrameBufs& F = t->fb[(t->ring_pos + 2) % 3];
+  const size_t K = t->kp_cap, o = (size_t)stream * K;
+  int cnt = 0, bn = 0, err = 0;
+  HIP_CHECK(hipMemcpy(&cnt, F.n + stream, 4, hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(&bn, F.bow_n + stream, 4, hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(&err, t->d_bow_err, 4, hipMemcpyDeviceToHost));
+  if (err) {
+    HIP_CHECK(hipMemset(t->d_bow_err, 0, 4));
+    return arg_fail("BoW transform: feature capacity exceeded");
+  }
+  if (n) *n = cnt;
+  if (bow_n) *bow_n = bn;
+  if (bow_words && bn) HIP_CHECK(hipMemcpy(bow_words, F.bow_words + o, 4 * (size_t)bn, hipMemcpyDeviceToHost));
+  if (bow_vals && bn) HIP_CHECK(hipMemcpy(bow_vals, F.bow_vals + o, 8 * (size_t)bn, hipMemcpyDeviceToHost));
+  if (feat_node && cnt) HIP_CHECK(hipMemcpy(feat_node, F.feat_node + o, 4 * (size_t)cnt, hipMemcpyDeviceToHost));
   return ORBPL_OK;
 }
 

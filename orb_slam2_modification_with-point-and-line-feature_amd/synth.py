@@ -259,8 +259,10 @@ def loop_trajectory(n, seed=0, step_t=0.012, rot_amp_deg=4.0):
 # Synthetic ORB vocabulary (the reference's ORBvoc.txt is not in its
 # checkout): a complete k-ary tree of depth L built DBoW2-style by
 # hierarchical k-medians on binary descriptors (seeded centres, member
-# majority bits), TF-IDF word weights idf = log(N / N_i) over the training
-# documents (0 for unseen or ubiquitous words = stopped), written in DBoW2's
+# majority bits), TF-IDF word weights idf = log((N + 1) / (N_i + 1)) over the
+# training documents (smoothed so that, as with ORBvoc's large training set,
+# nearly every word carries a weight; a word in every document is stopped,
+# weight 0), written in DBoW2's
 # text format (TemplatedVocabulary::saveToTextFile, TemplatedVocabulary.h:1427).
 # Node ids are breadth-first, so a node's children are contiguous.
 # ---------------------------------------------------------------------------
@@ -323,11 +325,16 @@ def vocabulary_tree(train, k=10, L=5, seed=0, iters=3):
     Ni = np.zeros(nn, np.int64)
     for d in docs:
         Ni[np.unique(vocabulary_words(tree, d))] += 1
-    w = np.zeros(nn)
-    seen = (Ni > 0) & leaf
-    w[seen] = np.log(N / Ni[seen])
-    tree["weight"] = w
+    tree["weight"] = idf_weights(tree, Ni, N)
     return tree
+
+
+def idf_weights(tree, Ni, N):
+    """Leaf weights log((N + 1) / (N_i + 1)) (0 for inner nodes)."""
+    w = np.zeros(len(tree["parent"]))
+    leaf = tree["leaf"]
+    w[leaf] = np.log((N + 1.0) / (np.asarray(Ni, np.float64)[leaf] + 1.0))
+    return w
 
 
 def vocabulary_words(tree, desc):

@@ -73,5 +73,59 @@ def test_torchrun_two_ranks_env_contract():
     finally:
         script.unlink()
     assert out.returncode == 0, out.stderr[-2000:]
-    lines = sorted(line for line in out.stdout.splitlines() if line.startswith("rank"))
+    # the two ranks share stdout: their lines may interleave
+    import re
+    lines = sorted(re.findall(r"rank \d \d \d", out.stdout))
     assert lines == ["rank 0 0 2", "rank 1 1 2"]
+
+
+def _vocab_rank(rank, world, port, q):
+    import numpy as np
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    sys.path.insert(0, str(ROOT / "tests"))
+    from _pkg import load_pkg
+    load_pkg()
+    import orbpl.synth as synth
+    rng = np.random.default_rng(5 + rank)
+    docs = [rng.integers(0, 256, (200, 32), dtype=np.uint8) for _ in range(3)]
+    tree = synth.vocabulary_tree(docs, k=4, L=3, seed=2) if rank == 0 else None
+    tree = bench.share_tree(tree, dist)
+    w, n_docs, backend = bench.shared_idf(synth, tree, docs, dist)
+    q.put((rank, tree["desc"].tobytes(), w, n_docs, backend,
+           [d.tobytes() for d in docs]))
+    dist.destroy_process_group()
+
+
+def test_shared_vocabulary_ws2():
+    """Rank 0's vocabulary tree reaches rank 1 (broadcast) and the IDF weights
+    from the all-reduced document counts equal those of one process holding
+    every rank's documents."""
+    import numpy as np
+    sys.path.insert(0, str(ROOT / "tests"))
+    from _pkg import load_pkg
+    load_pkg()
+    import orbpl.synth as synth
+    import bench
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_vocab_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in ps)
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    (_, t0, w0, n0, b0, d0), (_, t1, w1, n1, b1, d1) = res
+    assert t0 == t1 and np.array_equal(w0, w1) and n0 == n1 == 6 and b0 == "gloo"
+    docs = [np.frombuffer(b, np.uint8).reshape(-1, 32) for b in d0 + d1]
+    rng = np.random.default_rng(5)
+    tree = synth.vocabulary_tree([rng.integers(0, 256, (200, 32), dtype=np.uint8)
+                                  for _ in range(3)], k=4, L=3, seed=2)
+    assert tree["desc"].tobytes() == t0
+    w, n, _ = bench.shared_idf(synth, tree, docs, None)
+    assert n == 6 and np.array_equal(w, w0)
+    assert (w0 > 0).sum() > 10

@@ -69,7 +69,7 @@ def test_synthetic_vocabulary_pinned(orbpl, oracle):
     for k in ("parent", "leaf", "desc", "weight"):
         assert np.array_equal(g[k], on[k]), k
     assert o.n_nodes == 11111 and o.n_words == 10000
-    assert 0 < (on["weight"][on["leaf"] == 1] > 0).sum() < 10000   # stopped words exist
+    assert (on["weight"][on["leaf"] == 1] > 0).sum() > 9000   # nearly every word weighted
     from _vocab import training_descriptors
     desc = training_descriptors(2, seed=9)[1]
     words, vals, node, fw, fwt = o.transform(desc, levelsup=2)

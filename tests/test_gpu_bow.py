@@ -94,3 +94,35 @@ def test_search_by_bow_real_nodes(orbpl, oracle):
     om, on = oracle.search_by_bow(n0, valid, d0, k0["angle"], n1, d1, k1["angle"], 0.7, True)
     assert np.array_equal(gm, om) and gn == on
     assert gn > 100
+
+
+@pytest.mark.parametrize("pipelined", [False, True])
+def test_tracker_keyframe_bow(orbpl, oracle, pipelined):
+    """orbpl_tracker_set_vocabulary: every step's frame gets KeyFrame::
+    ComputeBoW (levelsup 4) on the device, bit-exact with the oracle's
+    transform of the oracle's descriptors of the same frame."""
+    from _scenes import sequence
+    path, _ = vocabulary(k=10, L=5, seed=3, n_frames=8)
+    voc = orbpl.ORBVocabulary(path)
+    o = oracle.Vocabulary(path)
+    S, F = 2, 3
+    seqs = [sequence(F, 40 + s) for s in range(S)]
+    cfg = seqs[0][0]
+    tr = orbpl.Tracker(orbpl.OrbParams(1000, 1.2, 8, 20, 7), orbpl.make_camera(cfg), S)
+    tr.set_pipelined(pipelined)
+    tr.set_vocabulary(voc, 4)
+    T0 = np.stack([np.linalg.inv(sq[1][0]).astype(np.float32) for sq in seqs])
+    tr.reset(T0.reshape(S, 16))
+    g = orbpl.DeviceBuffer(F * S * 640 * 480)
+    d = orbpl.DeviceBuffer(F * S * 640 * 480 * 4)
+    p = oracle.params()
+    for f in range(F):
+        g.upload(np.stack([sq[2][f][0] for sq in seqs]), offset=f * S * 640 * 480)
+        d.upload(np.stack([sq[2][f][1] for sq in seqs]), offset=f * S * 640 * 480 * 4)
+        tr.step_device(g.ptr + f * S * 640 * 480, d.ptr + f * S * 640 * 480 * 4)
+        for s in range(S):
+            gw, gv, gn = tr.bow(s)
+            _, desc, _ = oracle.extract(p, seqs[s][2][f][0])
+            ow, ov, on, _, _ = o.transform(desc, levelsup=4)
+            assert np.array_equal(gw, ow) and np.array_equal(gv.view(np.uint64), ov.view(np.uint64))
+            assert np.array_equal(gn, on)
