@@ -514,6 +514,60 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
                 pipelined=bool(pipelined))
 
 
+def run_ingress(pkg, synth, args, S, steps, warmup, rank, world, device, dist, voc=None):
+    """The headline workload fed from host memory (GrabImageRGBD's inputs):
+    u8 gray + 16-bit TUM depth (DepthMapFactor 5000) in page-locked host
+    buffers, each step's batch copied host-to-device on the tracker's copy
+    stream while the previous steps' kernels run (orbpl_tracker_step_host),
+    depth converted on the device. The timed region includes the copies."""
+    wl = WORKLOADS["points"]
+    F = args.loop
+    gray, depth = render_loop(F, seed=1 + rank, workers=min(16, os.cpu_count() or 4))
+    d16 = np.clip(np.round(depth * 5000.0), 0, 65535).astype(np.uint16)
+    d32 = d16.astype(np.float32) * (np.float32(1.0) / np.float32(5000.0))   # P21
+    traj = synth.loop_trajectory(F, seed=1 + rank)
+    L = Layout(traj)
+    rep = L.replicated(S)
+    hg = pkg.HostBuffer((len(rep), H, W), np.uint8)
+    hd = pkg.HostBuffer((len(rep), H, W), np.uint16)
+    hg.array[:] = gray[rep]
+    hd.array[:] = d16[rep]
+    tr = pkg.Tracker(pkg.OrbParams(*wl["orb"]), pkg.make_camera(synth.TUM1), S, device=device,
+                     local_map=bool(args.local_map))
+    tr.set_pipelined(True)
+    if voc is not None:
+        tr.set_vocabulary(voc, 4)
+    tr.reset(np.stack([np.linalg.inv(L.Twc(s, 0)).astype(np.float32) for s in range(S)]).reshape(S, 16))
+    tr.set_history(warmup + steps)
+
+    def step(k):
+        o = k % F
+        tr.step_host(hg.ptr + o * W * H, hd.ptr + o * W * H * 2, 5000.0)
+
+    for k in range(warmup):
+        step(k)
+    tr.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(warmup + k)
+    tr.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = max_over_ranks(dist, time.perf_counter() - t0)
+    samp = sorted({0, S // 2, S - 1})
+    hist = [tr.history(s, warmup + steps) for s in samp]
+    tr.close()
+    step_bytes = S * W * H * 3
+    out = dict(S=S, value=S * steps * world / elapsed, elapsed=elapsed, nsteps=steps, samp=samp,
+               hist=hist, layout=L, gray=gray, depth=d32, wname="points",
+               h2d_GBps=round(step_bytes * steps / elapsed / 1e9, 2), bytes_per_step=step_bytes)
+    hg.free()
+    hd.free()
+    return out
+
+
 def sweep(pkg, synth, workload, sizes, steps, device, local_map=True):
     """Per-step latency and throughput at several batch sizes (untimed for the
     headline; each size gets its own tracker, 1 warm-up step)."""
@@ -706,6 +760,9 @@ def main():
                     help="1 = every frame's KeyFrame::ComputeBoW with a shared synthetic "
                          "vocabulary (broadcast + IDF all-reduce over ranks); 0 = off")
     ap.add_argument("--vocab-levels", type=int, default=5, help="vocabulary depth L (k = 10)")
+    ap.add_argument("--ingress-steps", type=int, default=20,
+                    help="steps of the host-memory ingress leg (u8 gray + u16 depth copied "
+                         "host-to-device inside the timed region; points runs only; 0 = skip)")
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the oracle replay of the timed trackers' sampled streams")
     args = ap.parse_args()
@@ -753,8 +810,12 @@ def main():
                                      max(1, args.warmup // 2), rank, world, device, dist, voc)
         others["rig"]["nsteps"] = args.rig_steps
 
+    ingress = None
+    if args.workload == "points" and args.ingress_steps > 0:
+        ingress = run_ingress(pkg, synth, args, args.streams, args.ingress_steps,
+                              args.warmup, rank, world, device, dist, voc)
     # parity of every timed tracker's sampled streams against the oracle
-    for r in [res] + list(others.values()):
+    for r in [res] + list(others.values()) + ([ingress] if ingress else []):
         if args.no_parity:
             r["parity"] = None
             continue
@@ -815,6 +876,17 @@ def main():
         }
         if sweeps:
             out["sweep"] = sweeps
+        if ingress:
+            out["ingress"] = {
+                "workload": "the headline workload from page-locked host memory: u8 gray + "
+                            "16-bit depth (DepthMapFactor 5000) copied host-to-device on a copy "
+                            "stream overlapped with the kernels, depth converted on the device; "
+                            "copies inside the timed region",
+                "value": round(ingress["value"], 2), "unit": "frames/s",
+                "streams_per_gpu": ingress["S"], "steps": ingress["nsteps"],
+                "ms_per_step": round(ingress["elapsed"] / ingress["nsteps"] * 1e3, 3),
+                "h2d_bytes_per_step": ingress["bytes_per_step"],
+                "h2d_GBps_per_gpu": ingress["h2d_GBps"], "parity": ingress["parity"]}
         for key, o in others.items():
             out[key] = {
                 "workload": o["workload"], "value": round(o["value"], 2),

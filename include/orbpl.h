@@ -71,6 +71,10 @@ const char* orbpl_version(void);
  * reference's C++ Tracking, ctypes tests, bench). Synchronous copies. */
 int orbpl_dev_malloc(int device, int64_t bytes, void** out);
 int orbpl_dev_free(int device, void* ptr);
+/* page-locked host memory (hipHostMalloc): the source of asynchronous
+ * host-to-device frame copies (orbpl_tracker_step_host) */
+int orbpl_host_alloc(int64_t bytes, void** out);
+int orbpl_host_free(void* ptr);
 int orbpl_memcpy_htod(int device, void* dst, const void* src, int64_t bytes);
 int orbpl_memcpy_dtoh(int device, void* dst, const void* src, int64_t bytes);
 int orbpl_memset_d(int device, void* dst, int value, int64_t bytes);
@@ -400,6 +404,16 @@ int orbpl_tracker_step(orbpl_tracker* tr, const uint8_t* d_gray, const float* d_
 /* Stereo step (ORBPL_TRACK_STEREO trackers): d_left / d_right hold n_streams
  * rectified frames of width*height u8 each (device memory, contiguous). */
 int orbpl_tracker_step_stereo(orbpl_tracker* tr, const uint8_t* d_left, const uint8_t* d_right);
+/* Tracking::GrabImageRGBD from host buffers (Tracking.cc:225-248): n_streams
+ * gray frames and n_streams 16-bit depth maps (TUM PNG depth, raw units),
+ * copied asynchronously on the tracker's copy stream into one of 3 device
+ * slots (pinned memory from orbpl_host_alloc makes the copy overlap the
+ * previous steps' kernels), depth converted as imDepth.convertTo(CV_32F,
+ * 1.0f / depth_map_factor) (pinned P21: float(v) * (1.0f / factor); TUM:
+ * DepthMapFactor 5000), then the step. The host buffers may be reused after
+ * the next orbpl_tracker_synchronize. */
+int orbpl_tracker_step_host(orbpl_tracker* tr, const uint8_t* h_gray, const uint16_t* h_depth,
+                            float depth_map_factor);
 int orbpl_tracker_synchronize(orbpl_tracker* tr);
 /* on != 0: extraction of step t+1 may overlap matching/pose of step t (two
  * HIP streams, three frame buffers). Results are identical either way. */

@@ -76,6 +76,8 @@ def _declare(L):
     L.orbpl_dev_malloc.argtypes = [i, C.c_int64, C.POINTER(vp)]
     L.orbpl_dev_free.argtypes = [i, vp]
     L.orbpl_memcpy_htod.argtypes = [i, vp, vp, C.c_int64]
+    L.orbpl_host_alloc.argtypes = [C.c_int64, C.POINTER(vp)]
+    L.orbpl_host_free.argtypes = [vp]
     L.orbpl_memcpy_dtoh.argtypes = [i, vp, vp, C.c_int64]
     L.orbpl_memset_d.argtypes = [i, vp, i, C.c_int64]
     L.orbpl_device_synchronize.argtypes = [i]
@@ -128,6 +130,31 @@ class DeviceBuffer:
     def free(self):
         if self.ptr:
             lib().orbpl_dev_free(self.device, C.c_void_p(self.ptr))
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class HostBuffer:
+    """Page-locked host allocation (orbpl_host_alloc) viewed as a numpy array."""
+
+    def __init__(self, shape, dtype):
+        self.dtype, self.shape = np.dtype(dtype), tuple(np.atleast_1d(shape))
+        nbytes = int(np.prod(self.shape)) * self.dtype.itemsize
+        p = C.c_void_p()
+        check(lib().orbpl_host_alloc(nbytes, C.byref(p)), "orbpl_host_alloc")
+        self.ptr = p.value
+        buf = (C.c_uint8 * nbytes).from_address(self.ptr)
+        self.array = np.frombuffer(buf, np.uint8, nbytes).view(self.dtype).reshape(self.shape)
+
+    def free(self):
+        if self.ptr:
+            self.array = None
+            lib().orbpl_host_free(C.c_void_p(self.ptr))
             self.ptr = None
 
     def __del__(self):
@@ -362,6 +389,7 @@ def _declare_track(L):
     L.orbpl_tracker_get_history.argtypes = [vp, i, i, vp, vp, ip]
     L.orbpl_tracker_get_local_stats.argtypes = [vp, vp, vp, vp, vp]
     L.orbpl_tracker_set_vocabulary.argtypes = [vp, vp, i]
+    L.orbpl_tracker_step_host.argtypes = [vp, vp, vp, C.c_float]
     L.orbpl_tracker_get_bow.argtypes = [vp, i, vp, vp, ip, vp, ip]
 
 
@@ -650,6 +678,12 @@ class Tracker:
 
     def step_device(self, d_gray, d_depth):
         check(lib().orbpl_tracker_step(self._h, C.c_void_p(d_gray), C.c_void_p(d_depth)), "step")
+
+    def step_host(self, h_gray, h_depth16, depth_map_factor=5000.0):
+        """GrabImageRGBD from host memory: h_gray / h_depth16 = host pointers
+        (HostBuffer.ptr) to n_streams u8 frames and u16 depth maps."""
+        check(lib().orbpl_tracker_step_host(self._h, C.c_void_p(h_gray), C.c_void_p(h_depth16),
+                                            C.c_float(depth_map_factor)), "orbpl_tracker_step_host")
 
     def step_stereo_device(self, d_left, d_right):
         """Stereo step: device pointers to n_streams left / right frames."""

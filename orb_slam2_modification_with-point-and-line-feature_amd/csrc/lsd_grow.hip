@@ -1164,7 +1164,13 @@ __global__ void __launch_bounds__(64) k_lsd_grow(LsdGeom g, LsdScratch sc) {
 
 
 // Speculative seed loop (see lane_grow): one wave per frame.
-__global__ void __launch_bounds__(64) k_lsd_spec(LsdGeom g, LsdScratch sc) {
+// ORBPL_SPEC_MINW: waves per SIMD the register budget must allow (frames in
+// flight per CU = 4x; the loop is latency-bound, so more frames in flight
+// raise throughput until the memory system saturates)
+#ifndef ORBPL_SPEC_MINW
+#define ORBPL_SPEC_MINW 1
+#endif
+__global__ void __launch_bounds__(64, ORBPL_SPEC_MINW) k_lsd_spec(LsdGeom g, LsdScratch sc) {
   extern __shared__ uint32_t grow_smem[];
   __shared__ uint32_t s_pt[kSpecLanes];
   __shared__ int s_pos[kSpecLanes];

@@ -140,6 +140,17 @@ int orbpl_dev_free(int device, void* ptr) {
   return ORBPL_OK;
 }
 
+int orbpl_host_alloc(int64_t bytes, void** out) {
+  if (!out || bytes < 0) return arg_fail("bad argument");
+  HIP_CHECK(hipHostMalloc(out, (size_t)(bytes > 0 ? bytes : 1), hipHostMallocDefault));
+  return ORBPL_OK;
+}
+
+int orbpl_host_free(void* ptr) {
+  if (ptr) HIP_CHECK(hipHostFree(ptr));
+  return ORBPL_OK;
+}
+
 int orbpl_memcpy_htod(int device, void* dst, const void* src, int64_t bytes) {
   HIP_CHECK(hipSetDevice(device));
   if (bytes > 0) HIP_CHECK(hipMemcpy(dst, src, (size_t)bytes, hipMemcpyHostToDevice));

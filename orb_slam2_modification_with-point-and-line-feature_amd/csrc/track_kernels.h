@@ -267,6 +267,9 @@ void launch_frame_prepare(const TrackConsts& c, const KeyPointD* kps, const int*
                           const float* depth, long long depth_pitch, KeyPointD* kps_un,
                           float* depth_out, float* uright, int* gcell, int batch, hipStream_t s);
 void launch_predict(StreamState* st, int nstreams, hipStream_t s);
+// GrabImageRGBD's imDepth.convertTo(CV_32F, mDepthMapFactor) (Tracking.cc:234-235):
+// depth = float(v) * scale, scale = 1.0f / DepthMapFactor (pinned P21)
+void launch_depth_u16(const uint16_t* in, float* out, long long n, float scale, hipStream_t s);
 void launch_match_last(const TrackConsts& c, const MatchLaunch& m, int nstreams, hipStream_t s);
 void launch_pose(const TrackConsts& c, const PoseLaunch& p, int nstreams, hipStream_t s);
 // debug: stream 0 phase ticks of the last k_pose launch (ORBPL_POSE_PROFILE)

@@ -810,6 +810,16 @@ struct orbpl_tracker {
   static constexpr int kLmK = 4;
   int local_map = 0;
   int lm_step = 0;                 // frames since reset (Frame::mnId)
+  // host-buffer ingress (orbpl_tracker_step_host): 3 device slots of gray,
+  // u16 depth and converted f32 depth, filled on a copy stream
+  static constexpr int kIn = 3;
+  hipStream_t cstream = nullptr;
+  uint8_t* in_gray[kIn] = {};
+  uint16_t* in_d16[kIn] = {};
+  float* in_depth[kIn] = {};
+  hipEvent_t in_copied[kIn] = {}, in_done_s[kIn] = {}, in_done_l[kIn] = {};
+  bool in_used[kIn] = {};
+  int in_pos = 0;
   orbv_vocab* voc = nullptr;       // orbpl_tracker_set_vocabulary (not owned)
   int voc_levelsup = 4;
   int* d_bow_err = nullptr;
@@ -879,6 +889,15 @@ int orbpl_tracker_destroy(orbpl_tracker* t) {
   if (t->ev_in) (void)hipEventDestroy(t->ev_in);
   if (t->ev_rin) (void)hipEventDestroy(t->ev_rin);
   if (t->exr) orbx_destroy(t->exr);
+  if (t->cstream) {
+    (void)hipStreamSynchronize(t->cstream);
+    (void)hipStreamDestroy(t->cstream);
+  }
+  for (int k = 0; k < orbpl_tracker::kIn; k++) {
+    if (t->in_copied[k]) (void)hipEventDestroy(t->in_copied[k]);
+    if (t->in_done_s[k]) (void)hipEventDestroy(t->in_done_s[k]);
+    if (t->in_done_l[k]) (void)hipEventDestroy(t->in_done_l[k]);
+  }
   if (t->tstream) (void)hipStreamDestroy(t->tstream);
   if (t->lstream) (void)hipStreamDestroy(t->lstream);
   if (t->lx) lsdx_destroy(t->lx);
@@ -1110,6 +1129,7 @@ int orbpl_tracker_reset(orbpl_tracker* t, const float* Tcw0) {
     for (int k = 0; k < 16; k++) z.Tcw[k] = Tcw0 ? Tcw0[s * 16 + k] : (k % 5 == 0 ? 1.f : 0.f);
     st[s] = z;
   }
+  if (t->cstream) HIP_CHECK(hipStreamSynchronize(t->cstream));
   HIP_CHECK(hipStreamSynchronize(t->stream));
   if (t->tstream) HIP_CHECK(hipStreamSynchronize(t->tstream));
   if (t->lstream) HIP_CHECK(hipStreamSynchronize(t->lstream));
@@ -1494,6 +1514,53 @@ int orbpl_tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_d
   return tracker_step(t, d_gray, d_depth, nullptr);
 }
 
+int orbpl_tracker_step_host(orbpl_tracker* t, const uint8_t* h_gray, const uint16_t* h_depth,
+                            float depth_map_factor) {
+  if (!t || !h_gray || !h_depth) return arg_fail("NULL argument");
+  if (t->stereo) return arg_fail("stereo tracker: orbpl_tracker_step_host takes RGB-D frames");
+  if (!(depth_map_factor > 0.f)) return arg_fail("depth_map_factor must be > 0");
+  HIP_CHECK(hipSetDevice(t->device));
+  const size_t npx = (size_t)t->S * t->W * t->H;
+  if (!t->cstream) {
+    HIP_CHECK(hipStreamCreateWithFlags(&t->cstream, hipStreamNonBlocking));
+    for (int k = 0; k < orbpl_tracker::kIn; k++) {
+      void* p = nullptr;
+      HIP_CHECK(hipMalloc(&p, npx));
+      t->allocs.push_back(p);
+      t->in_gray[k] = (uint8_t*)p;
+      HIP_CHECK(hipMalloc(&p, npx * 2));
+      t->allocs.push_back(p);
+      t->in_d16[k] = (uint16_t*)p;
+      HIP_CHECK(hipMalloc(&p, npx * 4));
+      t->allocs.push_back(p);
+      t->in_depth[k] = (float*)p;
+      HIP_CHECK(hipEventCreateWithFlags(&t->in_copied[k], hipEventDisableTiming));
+      HIP_CHECK(hipEventCreateWithFlags(&t->in_done_s[k], hipEventDisableTiming));
+      HIP_CHECK(hipEventCreateWithFlags(&t->in_done_l[k], hipEventDisableTiming));
+    }
+  }
+  const int k = t->in_pos % orbpl_tracker::kIn;
+  // the slot's previous frames must have been read (extraction + line stream)
+  if (t->in_used[k]) {
+    HIP_CHECK(hipStreamWaitEvent(t->cstream, t->in_done_s[k], 0));
+    if (t->lines) HIP_CHECK(hipStreamWaitEvent(t->cstream, t->in_done_l[k], 0));
+  }
+  HIP_CHECK(hipMemcpyAsync(t->in_gray[k], h_gray, npx, hipMemcpyHostToDevice, t->cstream));
+  HIP_CHECK(hipMemcpyAsync(t->in_d16[k], h_depth, npx * 2, hipMemcpyHostToDevice, t->cstream));
+  HIP_CHECK(hipEventRecord(t->in_copied[k], t->cstream));
+  HIP_CHECK(hipStreamWaitEvent(t->stream, t->in_copied[k], 0));
+  // mDepthMapFactor = 1.0f / DepthMapFactor (Tracking.cc:142-146)
+  launch_depth_u16(t->in_d16[k], t->in_depth[k], (long long)npx, 1.0f / depth_map_factor,
+                   t->stream);
+  const int rc = tracker_step(t, t->in_gray[k], t->in_depth[k], nullptr);
+  if (rc) return rc;
+  HIP_CHECK(hipEventRecord(t->in_done_s[k], t->stream));
+  if (t->lines) HIP_CHECK(hipEventRecord(t->in_done_l[k], t->lstream));
+  t->in_used[k] = true;
+  t->in_pos++;
+  return ORBPL_OK;
+}
+
 int orbpl_tracker_step_stereo(orbpl_tracker* t, const uint8_t* d_left, const uint8_t* d_right) {
   if (!t || !d_left || !d_right) return arg_fail("NULL argument");
   if (!t->stereo) return arg_fail("tracker created without ORBPL_TRACK_STEREO");
@@ -1512,6 +1579,7 @@ int orbpl_tracker_set_pipelined(orbpl_tracker* t, int on) {
 int orbpl_tracker_synchronize(orbpl_tracker* t) {
   if (!t) return arg_fail("NULL tracker");
   HIP_CHECK(hipSetDevice(t->device));
+  if (t->cstream) HIP_CHECK(hipStreamSynchronize(t->cstream));
   HIP_CHECK(hipStreamSynchronize(t->tstream));
   if (t->lines) {
     HIP_CHECK(hipStreamSynchronize(t->lstream));

@@ -597,3 +597,43 @@ def test_tracker_local_map_matches_oracle(orbpl, oracle, lines, stereo, pipeline
             assert np.abs(Th[f] - To).max() < POSE_TOL, (s, f)
         assert ref[s][F - 1][1][8] > 0       # local map matches were found
         assert ref[s][F - 1][1][4] == 1      # and tracking succeeded
+
+
+@pytest.mark.parametrize("lines", [False, True])
+def test_tracker_step_host_u16_depth(orbpl, oracle, lines):
+    """orbpl_tracker_step_host: frames from pinned host memory, 16-bit TUM
+    depth converted on the device as imDepth.convertTo(CV_32F, 1/5000)
+    (pinned P21), pipelined: the same counts and poses as the oracle loop on
+    the converted depth."""
+    S, F = 2, 4
+    seqs = [sequence(F, 60 + s, cam_name="TUM3" if lines else "TUM1") for s in range(S)]
+    cfg = seqs[0][0]
+    scale = np.float32(1.0) / np.float32(5000.0)
+    lvo = oracle.LVO(oracle.params(), oracle.camera(cfg), S, use_lines=lines)
+    tr = orbpl.Tracker(orbpl.OrbParams(1000, 1.2, 8, 20, 7), orbpl.make_camera(cfg), S, lines=lines)
+    tr.set_pipelined(True)
+    T0 = np.stack([np.linalg.inv(sq[1][0]).astype(np.float32) for sq in seqs])
+    lvo.reset(T0.reshape(S, 16))
+    tr.reset(T0.reshape(S, 16))
+    tr.set_history(F)
+    hg, hd, d32 = [], [], []
+    for f in range(F):
+        g = orbpl.HostBuffer((S, 480, 640), np.uint8)
+        d = orbpl.HostBuffer((S, 480, 640), np.uint16)
+        g.array[:] = np.stack([sq[2][f][0] for sq in seqs])
+        d.array[:] = np.clip(np.round(np.stack([sq[2][f][1] for sq in seqs]) * 5000.0), 0, 65535)
+        hg.append(g)
+        hd.append(d)
+        d32.append(d.array.astype(np.float32) * scale)
+        tr.step_host(g.ptr, d.ptr, 5000.0)
+    tr.synchronize()
+    for s in range(S):
+        Th, Ch = tr.history(s)
+        for f in range(F):
+            To, so = lvo.step(s, seqs[s][2][f][0], np.ascontiguousarray(d32[f][s]))
+            keys = ("nkeypoints", "nmatches", "ninliers", "nmatches_map", "ok", "nlines",
+                    "line_matches", "line_nmatches_map")
+            assert [int(x) for x in Ch[f][:8]] == [so[k] for k in keys], (s, f)
+            assert np.abs(Th[f] - To).max() < POSE_TOL, (s, f)
+    for b in hg + hd:
+        b.free()
