@@ -61,6 +61,8 @@ struct BowBatch {
   int* err;                     // bit 1: more than kBowMaxFeat features
 };
 
+}  // namespace
+
 __device__ __forceinline__ int dist256(const uint4& a0, const uint4& a1, const uint4* b) {
   const uint4 b0 = b[0], b1 = b[1];
   return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
@@ -190,6 +192,8 @@ __global__ void __launch_bounds__(256) k_bow_vector(VocDev v, BowBatch b) {
   for (int q = t; q < nruns; q += 256) b.bow_vals[o + q] = scale ? sval[q] / div : sval[q];
   if (t == 0) b.bow_n[f] = nruns;
 }
+
+namespace {
 
 int norm_of(int scoring) {
   switch (scoring) {

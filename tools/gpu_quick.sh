@@ -17,7 +17,7 @@ rc=$?; echo "pytest exit $rc"; tail -3 gpurun_out/quick_tests.log
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
 rm -rf $R/gpurun_out/prof_quick
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_quick -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --sweep 0 --secondary-steps 0 --stereo-steps 0 --rig-steps 0 --isolated-steps 0 "$@" > $R/gpurun_out/quick_bench.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_quick -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --sweep 0 --secondary-steps 0 --stereo-steps 0 --rig-steps 0 --isolated-steps 0 --ingress-steps 0 "$@" > $R/gpurun_out/quick_bench.log 2>&1
 rc=$?; echo "trace exit $rc"; tail -c 300 $R/gpurun_out/quick_bench.log
 [ $rc -ne 0 ] && exit $rc
 cut -d, -f1-4 $R/gpurun_out/prof_quick/run_kernel_stats.csv | cut -c1-160 | head -16

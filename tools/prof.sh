@@ -11,7 +11,7 @@ out=gpurun_out/prof_$tag
 mkdir -p $out
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-COMMON="--no-cpu-baseline --no-parity --sweep 0 --secondary-steps 0 --stereo-steps 0 --rig-steps 0 --isolated-steps 0"
+COMMON="--no-cpu-baseline --no-parity --sweep 0 --secondary-steps 0 --stereo-steps 0 --rig-steps 0 --isolated-steps 0 --ingress-steps 0"
 case "$MODE" in
   lines) B="$R/bench.py --workload lines --streams 3072 --steps 3 --warmup 1 $COMMON" ;;
   kitti) B="$R/bench.py --workload kitti --streams 1024 --steps 3 --warmup 1 $COMMON" ;;
