@@ -391,6 +391,16 @@ int orbpl_tracker_create(const orbpl_orb_params* orb, const orbpl_camera* cam, i
 /* ORBPL_TRACK_FIXED_LINE_JAC: PoseOptimizationWithLines with the analytic line
  * Jacobian (ORBPL_POSE_FIXED_LINE_JAC) in every tracker pose. */
 #define ORBPL_TRACK_FIXED_LINE_JAC 8
+/* ORBPL_TRACK_REFKF: Tracking::Track's choice between TrackWithMotionModel
+ * and TrackReferenceKeyFrame (Tracking.cc:324-338, 942-1032; needs a
+ * vocabulary, orbpl_tracker_set_vocabulary): the first frame after the
+ * initial one (no velocity) and every frame whose motion-model tracking
+ * fails are tracked against the reference keyframe (the last frame, P18) by
+ * ORBmatcher(0.7, true).SearchByBoW + LineMatcher's reference-keyframe
+ * overload from the pose of the last frame, then PoseOptimizationWithLines
+ * and the outlier discard; success = 10 map inliers (and, with lines, a
+ * line count of 10 after the reference's outlier decrement). Pinned P22. */
+#define ORBPL_TRACK_REFKF 16
 int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam, int n_streams,
                             int device, int flags, orbpl_tracker** out);
 int orbpl_tracker_destroy(orbpl_tracker* tr);
@@ -482,6 +492,8 @@ int orbpl_tracker_set_vocabulary(orbpl_tracker* tr, orbv_vocab* voc, int levelsu
  * tracker's keypoint capacity); n = its keypoints */
 int orbpl_tracker_get_bow(orbpl_tracker* tr, int stream, uint32_t* bow_words, double* bow_vals,
                           int* bow_n, int32_t* feat_node, int* n);
+/* per stream: 1 when the last step ran TrackReferenceKeyFrame (ORBPL_TRACK_REFKF) */
+int orbpl_tracker_get_trk(orbpl_tracker* tr, int* trk);
 /* TrackLocalMap outcome of the last step per stream (ORBPL_TRACK_LOCAL_MAP; 0
  * where it did not run): SearchLocalPoints matches, mnMatchesInliers,
  * SearchLocalLines matches (every passing pair counts), mnLineMatchesInliers. */

@@ -471,6 +471,9 @@ struct LStream {
   std::vector<orbpl_keyline> kl_un;
   std::vector<uint8_t> ldesc, has_ml, loutlier;
   std::vector<float> lxyz;
+  std::vector<int32_t> fnode;  // FeatureVector (KeyFrame::ComputeBoW): node per keypoint
+  std::vector<float> kangle;   // keypoint angles (mvKeys / mvKeysUn)
+  int trk = 0;                 // the last step ran TrackReferenceKeyFrame
 };
 
 // oracle_lvo_create_ex flags: the tracker's ORBPL_TRACK_* bits plus
@@ -482,6 +485,7 @@ struct LVO {
   orbpl_camera cam;
   int use_lines;
   int flags;
+  void* voc = nullptr;          // oracle vocabulary (ORBPL_TRACK_REFKF / ComputeBoW)
   std::vector<LStream> st;
   std::vector<float> scale, inv_sigma2;
 };
@@ -800,12 +804,24 @@ static int lvo_step(LVO* v, int stream, const uint8_t* gray, const float* depth,
                           ur.data(), dep.data());
   }
   const float th = right ? 7.0f : 15.0f;
-  std::vector<int32_t> match(n, -1), lmatch(nl, -1);
+  std::vector<int32_t> match(n, -1), lmatch(nl, -1), match_pre, lmatch_pre;
   std::vector<uint8_t> outl(n, 0), loutl(nl, 0);
   int nmatches = 0, ninl = 0, nmap = 0, nlm = 0, lnmap = 0;
   bool tracked = false, motion_ok = false, local_ok = true;
   S.lm[0] = S.lm[1] = S.lm[2] = S.lm[3] = 0;
-  if (S.has_last) {
+  // KeyFrame::ComputeBoW of the frame (every frame is a keyframe, P18)
+  std::vector<int32_t> fnode(n, -1);
+  if (v->voc) {
+    std::vector<uint32_t> bw(n + 1);
+    std::vector<double> bv(n + 1), fwt(n + 1);
+    std::vector<int32_t> fw(n + 1);
+    int bn = 0;
+    oracle_voc_transform(v->voc, desc.data(), n, 4, bw.data(), bv.data(), &bn, fnode.data(),
+                         fw.data(), fwt.data());
+  }
+  const bool refkf = (v->flags & ORBPL_TRACK_REFKF) && v->voc;
+  S.trk = 0;
+  if (S.has_last && !(refkf && !S.has_velocity)) {
     if (S.has_velocity) {
       float Twl[16], V[16];
       pose_inv(S.Tlast2, Twl);
@@ -867,7 +883,8 @@ static int lvo_step(LVO* v, int stream, const uint8_t* gray, const float* depth,
                                   (v->flags & ORBPL_TRACK_FIXED_LINE_JAC) ? ORBPL_POSE_FIXED_LINE_JAC : 0,
                                   S.Tcw, outl.data(), loutl.data(), &ninl);
     }
-    const std::vector<int32_t> match_pre = match, lmatch_pre = lmatch;
+    match_pre = match;
+    lmatch_pre = lmatch;
     // outlier discard (Tracking.cc:1273-1314); without an optimisation every
     // flag is clear and the counts report the raw matches
     for (int i = 0; i < n; i++)
@@ -885,10 +902,81 @@ static int lvo_step(LVO* v, int stream, const uint8_t* gray, const float* depth,
         }
       }
     motion_ok = tracked && (v->use_lines ? (nmap >= 10 || lnmap >= 15) : nmap >= 10);
-    if ((v->flags & ORBPL_TRACK_LOCAL_MAP) && motion_ok)
-      local_ok = track_local_map(v, S, right != nullptr, n, ku, desc, ur, match, match_pre, nl, klu,
-                                 ldesc, lmatch, lmatch_pre);
   }
+  if (match_pre.empty() && lmatch_pre.empty()) {
+    match_pre = match;
+    lmatch_pre = lmatch;
+  }
+  if (S.has_last && refkf && !motion_ok) {
+    // ---- TrackReferenceKeyFrame (Tracking.cc:942-1032), reference keyframe =
+    // the last frame (P18, P22) ----
+    S.trk = 1;
+    memcpy(S.Tcw, S.Tlast, 64);   // SetPose(mLastFrame.mTcw)
+    std::vector<float> fang(n);
+    for (int i = 0; i < n; i++) fang[i] = ku[i].angle;
+    const int nkf = (int)S.kps_un.size();
+    std::vector<int32_t> bm(n, -1);
+    nmatches = 0;
+    oracle_search_by_bow(nkf, S.fnode.data(), S.has_mp.data(), S.desc.data(), S.kangle.data(), n,
+                         fnode.data(), desc.data(), fang.data(), 0.7f, 1, bm.data(), &nmatches);
+    // lines: the reference-keyframe overload over the frame's current line
+    // assignments (the motion model's, after its outlier discard; none when
+    // it did not run), LineMatcher.cpp:527-754
+    std::vector<int32_t> lcur(nl, -1), tl(nl, -1), cur_nobs_l(nl, 0);
+    if (S.has_velocity)
+      for (int j = 0; j < nl; j++) lcur[j] = lmatch[j];
+    for (int j = 0; j < nl; j++) cur_nobs_l[j] = lcur[j] >= 0 ? 1 : 0;
+    int ntl = 0, wiped = 0;
+    if (v->use_lines)
+      oracle_line_search_by_projection_list(&cam, S.Tcw, nl, klu.data(), ldesc.data(),
+                                            cur_nobs_l.data(), (int)S.kl_un.size(),
+                                            S.has_ml.data(), S.lxyz.data(), S.ldesc.data(),
+                                            tl.data(), &ntl, &wiped);
+    for (int j = 0; j < nl; j++) lmatch[j] = (!wiped && lcur[j] >= 0) ? lcur[j] : tl[j];
+    nlm = ntl;
+    match = bm;
+    std::fill(outl.begin(), outl.end(), 0);
+    std::fill(loutl.begin(), loutl.end(), 0);
+    ninl = 0;
+    const bool go = nmatches >= 15 && (!v->use_lines || ntl >= 10);
+    if (go) {
+      std::vector<uint8_t> has(n, 0), hasl(nl, 0);
+      std::vector<float> xyz((size_t)n * 3, 0.f), lxyz((size_t)nl * 6, 0.f);
+      for (int i = 0; i < n; i++)
+        if (match[i] >= 0) {
+          has[i] = 1;
+          for (int k = 0; k < 3; k++) xyz[3 * i + k] = S.xyz[3 * match[i] + k];
+        }
+      for (int j = 0; j < nl; j++)
+        if (lmatch[j] >= 0) {
+          hasl[j] = 1;
+          for (int k = 0; k < 6; k++) lxyz[6 * j + k] = S.lxyz[6 * lmatch[j] + k];
+        }
+      ninl = optimize_pose(v, S, n, ku, ur, has, xyz, nl, klu, hasl, lxyz, outl, loutl);
+    }
+    match_pre = match;
+    lmatch_pre = lmatch;
+    nmap = 0;
+    lnmap = 0;
+    for (int i = 0; i < n; i++)
+      if (match[i] >= 0) {
+        if (outl[i]) match[i] = -1;
+        else nmap++;
+      }
+    for (int j = 0; j < nl; j++)
+      if (lmatch[j] >= 0) {
+        if (loutl[j]) {
+          lmatch[j] = -1;
+          lnmap--;
+        } else {
+          lnmap++;
+        }
+      }
+    motion_ok = go && nmap >= 10 && (!v->use_lines || lnmap >= 10);
+  }
+  if (S.has_last && (v->flags & ORBPL_TRACK_LOCAL_MAP) && motion_ok)
+    local_ok = track_local_map(v, S, right != nullptr, n, ku, desc, ur, match, match_pre, nl, klu,
+                               ldesc, lmatch, lmatch_pre);
   // this frame becomes the keyframe of the next one
   float Ow[3];
   neg_Rt_t(S.Tcw, Ow);
@@ -904,6 +992,9 @@ static int lvo_step(LVO* v, int stream, const uint8_t* gray, const float* depth,
       S.has_mp[i] = 1;
       S.nobs[i] = 1;
     }
+  S.fnode = fnode;
+  S.kangle.resize(n);
+  for (int i = 0; i < n; i++) S.kangle[i] = ku[i].angle;
   S.kl_un = klu;
   S.ldesc = ldesc;
   S.has_ml.assign(nl, 0);
@@ -947,6 +1038,16 @@ int oracle_lvo_step(void* h, int stream, const uint8_t* gray, const float* depth
 // TrackLocalMap counts of the stream's last step (ORBPL_TRACK_LOCAL_MAP):
 // local point matches, point inliers (mnMatchesInliers), local line matches,
 // line inliers (mnLineMatchesInliers); zeros when it did not run.
+// the vocabulary (oracle_voc_load_text handle) of KeyFrame::ComputeBoW and
+// ORBPL_TRACK_REFKF; not owned
+int oracle_lvo_set_vocabulary(void* h, void* voc) {
+  static_cast<line_track::LVO*>(h)->voc = voc;
+  return 0;
+}
+
+// 1 when the stream's last step ran TrackReferenceKeyFrame
+int oracle_lvo_trk(void* h, int stream) { return static_cast<line_track::LVO*>(h)->st[stream].trk; }
+
 int oracle_lvo_local_stats(void* h, int stream, int* out4) {
   const line_track::LStream& S = static_cast<line_track::LVO*>(h)->st[stream];
   for (int k = 0; k < 4; k++) out4[k] = S.lm[k];

@@ -496,6 +496,8 @@ def _setup(L):  # noqa: F811
     L.oracle_lvo_step.argtypes = [vp, i, vp, vp, vp, vp]
     L.oracle_lvo_step_stereo.argtypes = [vp, i, vp, vp, vp, vp]
     L.oracle_lvo_local_stats.argtypes = [vp, i, vp]
+    L.oracle_lvo_set_vocabulary.argtypes = [vp, vp]
+    L.oracle_lvo_trk.argtypes = [vp, i]
 
 
 def line_frame_prepare(cam, kl, depth=None):
@@ -547,7 +549,7 @@ def line_search_by_projection_last(cam, Tcw, cur_kl_un, cur_desc, last_kl_un, ha
     return match[:ncur].copy(), nm.value
 
 
-TRACK_LINES, TRACK_STEREO, TRACK_LOCAL_MAP, TRACK_FIXED_LINE_JAC = 1, 2, 4, 8
+TRACK_LINES, TRACK_STEREO, TRACK_LOCAL_MAP, TRACK_FIXED_LINE_JAC, TRACK_REFKF = 1, 2, 4, 8, 16
 TWO_THREADS = 1 << 16
 
 
@@ -587,6 +589,15 @@ class LVO:
         keys = ("nkeypoints", "nmatches", "ninliers", "nmatches_map", "ok", "nlines",
                 "line_matches", "line_nmatches_map")
         return T.reshape(4, 4), dict(zip(keys, (int(x) for x in o)))
+
+    def set_vocabulary(self, voc):
+        """KeyFrame::ComputeBoW / TrackReferenceKeyFrame vocabulary (Vocabulary)."""
+        self._voc = voc
+        lib().oracle_lvo_set_vocabulary(self.h, voc.h if voc is not None else None)
+
+    def trk(self, stream):
+        """1 when the stream's last step ran TrackReferenceKeyFrame."""
+        return int(lib().oracle_lvo_trk(self.h, stream))
 
     def local_stats(self, stream):
         """TrackLocalMap counts of the stream's last step: local point matches,

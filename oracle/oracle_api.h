@@ -35,6 +35,11 @@ int oracle_search_by_projection_local(const orbpl_camera* cam, const float* scal
                                       const uint8_t* mp_desc, const int32_t* mp_nobs,
                                       const int32_t* cur_nobs, float th, float nnratio,
                                       int32_t* match, int* nmatches_out);
+/* DBoW2 vocabulary (bow_oracle.cpp) */
+void* oracle_voc_load_text(const char* path);
+int oracle_voc_transform(void* h, const uint8_t* desc, int n, int levelsup, uint32_t* bow_words,
+                         double* bow_vals, int* bow_n, int32_t* feat_node, int32_t* feat_word,
+                         double* feat_weight);
 int oracle_search_by_bow(int nkf, const int32_t* kf_node, const uint8_t* kf_valid,
                          const uint8_t* kf_desc, const float* kf_angle, int nf,
                          const int32_t* f_node, const uint8_t* f_desc, const float* f_angle,

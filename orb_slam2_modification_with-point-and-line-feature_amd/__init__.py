@@ -391,6 +391,7 @@ def _declare_track(L):
     L.orbpl_tracker_set_vocabulary.argtypes = [vp, vp, i]
     L.orbpl_tracker_step_host.argtypes = [vp, vp, vp, C.c_float]
     L.orbpl_tracker_get_bow.argtypes = [vp, i, vp, vp, ip, vp, ip]
+    L.orbpl_tracker_get_trk.argtypes = [vp, vp]
 
 
 _declare_orig = _declare
@@ -646,15 +647,17 @@ class Tracker:
     TRACK_STEREO = 2
     TRACK_LOCAL_MAP = 4
     TRACK_FIXED_LINE_JAC = 8
+    TRACK_REFKF = 16
 
     def __init__(self, orb_params, camera, n_streams, device=0, lines=False, stereo=False,
-                 local_map=False, fixed_line_jac=False):
+                 local_map=False, fixed_line_jac=False, refkf=False):
         h = C.c_void_p()
         self.camera, self.S, self.device, self.use_lines = camera, n_streams, device, bool(lines)
         self.stereo = bool(stereo)
         flags = ((self.TRACK_LINES if lines else 0) | (self.TRACK_STEREO if stereo else 0) |
                  (self.TRACK_LOCAL_MAP if local_map else 0) |
-                 (self.TRACK_FIXED_LINE_JAC if fixed_line_jac else 0))
+                 (self.TRACK_FIXED_LINE_JAC if fixed_line_jac else 0) |
+                 (self.TRACK_REFKF if refkf else 0))
         check(lib().orbpl_tracker_create_ex(C.byref(orb_params), C.byref(camera), n_streams, device,
                                             flags, C.byref(h)),
               "orbpl_tracker_create_ex")
@@ -720,6 +723,12 @@ class Tracker:
         check(lib().orbpl_tracker_set_vocabulary(self._h, voc._h if voc is not None else None,
                                                  levelsup), "orbpl_tracker_set_vocabulary")
         self._voc = voc
+
+    def trk(self):
+        """Per stream: 1 when the last step ran TrackReferenceKeyFrame."""
+        out = np.zeros(self.S, np.int32)
+        check(lib().orbpl_tracker_get_trk(self._h, _ptr(out)), "orbpl_tracker_get_trk")
+        return out
 
     def bow(self, stream):
         """The last step's (bow_words, bow_values, feat_node) of one stream."""

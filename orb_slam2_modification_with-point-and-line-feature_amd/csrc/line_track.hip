@@ -434,7 +434,7 @@ __global__ void __launch_bounds__(256) k_line_match_list(TrackConsts c, LineList
   }
   __shared__ int s_wc[4];
   __shared__ int s_nto;
-  if (a.ncur_arr) {
+  if (a.ncur_arr && !a.refkf) {
     // SearchLocalLines calls the matcher only when some local line is in the
     // frustum (nToMatch > 0, Tracking.cc:1851)
     if (threadIdx.x == 0) s_nto = 0;

@@ -94,7 +94,8 @@ __global__ void __launch_bounds__(256) k_lm_gather(LocalMapArgs a) {
   lnmap = block_sum(lnmap, wsum);
   const bool tracked = S.nmatches >= 20 && (!a.lines || S.nlmatches >= 15);
   const bool motion_ok =
-      S.has_last && tracked && (a.lines ? (nmap >= 10 || lnmap >= 15) : nmap >= 10);
+      S.has_last && (S.trk ? (S.trk_go && nmap >= 10 && (!a.lines || lnmap >= 10))
+                           : (tracked && (a.lines ? (nmap >= 10 || lnmap >= 15) : nmap >= 10)));
   if (t == 0) {
     S.lm_active = motion_ok ? 1 : 0;
     S.lm_nlocal = S.lm_nllocal = S.lm_wiped = S.lm_ninl = S.lm_inl = S.lm_linl = 0;
@@ -258,6 +259,89 @@ __global__ void __launch_bounds__(256) k_lm_push(TrackConsts c, LocalMapArgs a) 
     }
     if (t == 0) a.rl_n[s * a.K + a.push_slot] = nl;
   }
+}
+
+// ---------------------------------------------------------------------------
+// Tracking::TrackReferenceKeyFrame (Tracking.cc:942-1032) for the streams
+// that need it (ORBPL_TRACK_REFKF, P22; restated in oracle/line_track_oracle.cpp
+// lvo_step): the first frame without a velocity and every frame whose motion
+// model failed, against the last frame as the reference keyframe.
+//   k_trk_prep  : TrackWithMotionModel's outcome (as k_lm_gather), the
+//                 decision, SetPose(mLastFrame.mTcw), fresh point matches /
+//                 outlier flags, the frame's line assignments kept for the
+//                 keyframe line search (the motion model's, outliers removed)
+//   k_trk_bow   : ORBmatcher(0.7, true).SearchByBoW(pKF, F) per stream (the
+//                 SearchByBoW kernel's body on the stream's FeatureVectors)
+//   k_trk_merge : the keyframe line search's matches over the kept
+//                 assignments (all cleared when its relaxed retry ran), the
+//                 15 / 10 match gates of the pose
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_trk_prep(TrkArgs a) {
+  __shared__ int wsum[4];
+  const int s = blockIdx.x, t = threadIdx.x;
+  StreamState& S = a.st[s];
+  const int K = a.kp_pitch;
+  const long long cb = (long long)s * K, lb = (long long)s * kLineKeep;
+  const int n = a.n[s], nl = a.lines ? a.nl[s] : 0;
+  const bool tracked = S.nmatches >= 20 && (!a.lines || S.nlmatches >= 15);
+  int nmap = 0, lnmap = 0;
+  for (int i = t; i < n; i += 256) nmap += a.match[cb + i] >= 0 && !a.outlier[cb + i];
+  for (int j = t; j < nl; j += 256)
+    if (a.lmatch[lb + j] >= 0) lnmap += a.loutlier[lb + j] ? -1 : 1;
+  nmap = block_sum(nmap, wsum);
+  lnmap = block_sum(lnmap, wsum);
+  const bool mm_ok = S.has_velocity && tracked &&
+                     (a.lines ? (nmap >= 10 || lnmap >= 15) : nmap >= 10);
+  const bool trk = S.has_last && !mm_ok;
+  __syncthreads();
+  if (t == 0) {
+    S.trk = trk ? 1 : 0;
+    S.trk_go = 0;
+    if (trk) {
+      for (int k = 0; k < 16; k++) S.Tcw[k] = S.Tlast[k];
+      S.ninliers = 0;
+      S.nmatches = 0;
+    }
+    a.nml[s] = trk && a.lines ? a.last_nl[s] : 0;
+  }
+  if (!trk) return;
+  for (int i = t; i < n; i += 256) {
+    a.match[cb + i] = -1;
+    a.outlier[cb + i] = 0;
+  }
+  for (int j = t; j < nl; j += 256) {
+    const int m = a.lmatch[lb + j];
+    // the motion model's assignments after its outlier discard (none when it
+    // did not run: no velocity)
+    const int keep = (S.has_velocity && m >= 0 && !(tracked && a.loutlier[lb + j])) ? m : -1;
+    a.lcur[lb + j] = keep;
+    a.cur_nobs_l[lb + j] = keep >= 0 ? 1 : 0;
+    a.loutlier[lb + j] = 0;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_trk_merge(TrkArgs a) {
+  const int s = blockIdx.x, t = threadIdx.x;
+  StreamState& S = a.st[s];
+  if (!S.trk) return;
+  const long long lb = (long long)s * kLineKeep;
+  const int nl = a.lines ? a.nl[s] : 0;
+  const bool wiped = a.lines && S.trk_wiped;
+  for (int j = t; j < nl; j += 256) {
+    const int c = a.lcur[lb + j];
+    a.lmatch[lb + j] = (!wiped && c >= 0) ? c : a.tlm[lb + j];
+  }
+  if (t == 0) {
+    if (a.lines) S.nlmatches = S.trk_nlm;
+    S.trk_go = S.nmatches >= 15 && (!a.lines || S.trk_nlm >= 10);
+  }
+}
+
+void launch_trk_prep(const TrkArgs& a, int nstreams, hipStream_t s) {
+  hipLaunchKernelGGL(k_trk_prep, dim3(nstreams), dim3(256), 0, s, a);
+}
+void launch_trk_merge(const TrkArgs& a, int nstreams, hipStream_t s) {
+  hipLaunchKernelGGL(k_trk_merge, dim3(nstreams), dim3(256), 0, s, a);
 }
 
 void launch_lm_gather(const LocalMapArgs& a, int nstreams, hipStream_t s) {

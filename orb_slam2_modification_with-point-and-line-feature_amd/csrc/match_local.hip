@@ -473,12 +473,22 @@ __device__ void bitonic_sort(uint32_t* a, int n) {
 }
 }  // namespace
 
-__global__ void __launch_bounds__(256) k_match_bow(BowArgs a) {
-  __shared__ uint32_t skf[kBowMax], sf[kBowMax];
-  __shared__ int smatch[kBowMax];
-  __shared__ int sbin[kBowMax];
-  __shared__ int hist[32];
-  __shared__ int s_n, s_ind[3];
+struct BowShared {
+  uint32_t skf[kBowMax], sf[kBowMax];
+  int smatch[kBowMax];
+  int sbin[kBowMax];
+  int hist[32];
+  int s_n, s_ind[3];
+};
+
+__device__ void match_bow_body(const BowArgs& a, BowShared& B) {
+  uint32_t* skf = B.skf;
+  uint32_t* sf = B.sf;
+  int* smatch = B.smatch;
+  int* sbin = B.sbin;
+  int* hist = B.hist;
+  int& s_n = B.s_n;
+  int* s_ind = B.s_ind;
   const int t = threadIdx.x;
   const int nkf = min(a.nkf, kBowMax), nf = min(a.nf, kBowMax);
   // key = node << 11 | index; features without a node sort last
@@ -531,7 +541,8 @@ __global__ void __launch_bounds__(256) k_match_bow(BowArgs a) {
       if (bestDist1 <= 50 && static_cast<float>(bestDist1) < a.nnratio * static_cast<float>(bestDist2)) {
         smatch[bestIdxF] = iKF;
         if (a.check_ori) {
-          float rot = a.kf_angle[iKF] - a.f_angle[bestIdxF];
+          float rot = a.kf_angle[(long long)iKF * a.kf_angle_stride] -
+                    a.f_angle[(long long)bestIdxF * a.f_angle_stride];
           if (rot < 0.0f) rot += 360.0f;
           int bin = (int)roundf(rot * (30 / 360.0f));
           if (bin == 30) bin = 0;
@@ -580,8 +591,45 @@ __global__ void __launch_bounds__(256) k_match_bow(BowArgs a) {
   if (t == 0) *a.nmatches = s_n;
 }
 
+__global__ void __launch_bounds__(256) k_match_bow(BowArgs a) {
+  __shared__ BowShared B;
+  match_bow_body(a, B);
+}
+
 void launch_match_bow(const BowArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_match_bow, dim3(1), dim3(256), 0, s, a);
+}
+
+// TrackReferenceKeyFrame's ORBmatcher(0.7, true).SearchByBoW(pKF, F)
+// (Tracking.cc:947-952) for every stream with st[s].trk: the last frame's
+// FeatureVector / map points / descriptors against the current frame's
+__global__ void __launch_bounds__(256) k_trk_bow(TrkArgs a) {
+  __shared__ BowShared B;
+  const int s = blockIdx.x;
+  StreamState& S = a.st[s];
+  if (!S.trk) return;
+  const long long cb = (long long)s * a.kp_pitch;
+  BowArgs b;
+  b.nkf = a.last_n[s];
+  b.kf_node = a.last_feat_node + cb;
+  b.kf_valid = a.last_has_mp + cb;
+  b.kf_desc = a.last_desc + cb * 32;
+  b.kf_angle = &a.last_kps_un[cb].angle;
+  b.kf_angle_stride = (int)(sizeof(KeyPointD) / sizeof(float));
+  b.nf = a.n[s];
+  b.f_node = a.feat_node + cb;
+  b.f_desc = a.desc + cb * 32;
+  b.f_angle = &a.kps_un[cb].angle;
+  b.f_angle_stride = (int)(sizeof(KeyPointD) / sizeof(float));
+  b.nnratio = 0.7f;
+  b.check_ori = 1;
+  b.match = a.match + cb;
+  b.nmatches = &S.nmatches;
+  match_bow_body(b, B);
+}
+
+void launch_trk_bow(const TrkArgs& a, int nstreams, hipStream_t s) {
+  hipLaunchKernelGGL(k_trk_bow, dim3(nstreams), dim3(256), 0, s, a);
 }
 
 }  // namespace orbpl

@@ -135,6 +135,11 @@ struct StreamState {
   int lm_inl;          // mnMatchesInliers
   int lm_linl;         // mnLineMatchesInliers
   int lm_ok;           // TrackLocalMap's decision
+  // TrackReferenceKeyFrame (ORBPL_TRACK_REFKF, P22)
+  int trk;             // this step tracks against the reference keyframe
+  int trk_go;          // enough BoW / line matches: the pose ran
+  int trk_nlm;         // reference-keyframe line matches
+  int trk_wiped;       // that line search's relaxed retry cleared the assignments
 };
 
 }  // namespace orbpl

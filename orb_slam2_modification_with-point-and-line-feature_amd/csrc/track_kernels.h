@@ -72,6 +72,7 @@ struct PoseLaunch {
   int lpitch;
   int fixed_line_jac;           // ORBPL_POSE_FIXED_LINE_JAC (analytic line Jacobian)
   int gate_lm;                  // 1: run only streams with active[s].lm_active (TrackLocalMap)
+                                // 2: only active[s].trk && trk_go (TrackReferenceKeyFrame)
 };
 
 // Per-frame line buffers of the tracker (kLineKeep lines per stream).
@@ -127,6 +128,7 @@ struct LineListArgs {
   int* match;                    // per current line: map line index or -1 (unchanged / wiped)
   int* nmatches;
   int* wiped;                    // 1 when the relaxed retry ran (all assignments cleared first)
+  int refkf;                     // batched reference-keyframe overload: no nToMatch gate
   // batched (tracker TrackLocalMap): block s reads ncur_arr[s] / nml_arr[s]
   // and offsets the current-line arrays by s * cur_pitch, the map-line
   // arrays and scratch by s * ml_pitch, Tcw by s * pose_stride, the outputs
@@ -206,6 +208,38 @@ struct LocalArgs {
 };
 
 // ORBmatcher::SearchByBoW(KeyFrame*, Frame&) with per-feature node ids.
+// TrackReferenceKeyFrame over the batch (ORBPL_TRACK_REFKF, local_map.hip)
+struct TrkArgs {
+  StreamState* st;
+  int kp_pitch;
+  int lines;
+  // current frame (after the motion model's matching / pose)
+  const int* n;
+  int* match;
+  uint8_t* outlier;
+  const int* nl;
+  int* lmatch;
+  uint8_t* loutlier;
+  const KeyPointD* kps_un;
+  const uint8_t* desc;
+  const int* feat_node;
+  // the reference keyframe = the last frame
+  const int* last_n;
+  const int* last_nl;
+  const KeyPointD* last_kps_un;
+  const uint8_t* last_desc;
+  const uint8_t* last_has_mp;
+  const int* last_feat_node;
+  // scratch
+  int* lcur;        // the frame's line assignments before the search [S][kLineKeep]
+  int* cur_nobs_l;  // Observations() of those (1 / 0)
+  int* tlm;         // the reference-keyframe line search's matches
+  int* nml;         // per stream: the keyframe's lines to search (0 = stream not tracked by it)
+};
+void launch_trk_prep(const TrkArgs& a, int nstreams, hipStream_t s);
+void launch_trk_bow(const TrkArgs& a, int nstreams, hipStream_t s);
+void launch_trk_merge(const TrkArgs& a, int nstreams, hipStream_t s);
+
 struct BowArgs {
   int nkf;
   const int* kf_node;
@@ -220,6 +254,7 @@ struct BowArgs {
   int check_ori;
   int* match;
   int* nmatches;
+  int kf_angle_stride = 1, f_angle_stride = 1;   // floats between consecutive angles
 };
 void launch_match_bow(const BowArgs& a, hipStream_t s);
 

@@ -1012,7 +1012,7 @@ struct PoseArgs {
   int lpitch;
   int prof;                   // debug: phase stamps of stream 0 into g_pose_prof
   int fixed_line_jac;         // ORBPL_POSE_FIXED_LINE_JAC
-  int gate_lm;                // run only active[s].lm_active streams
+  int gate_lm;                // 1: only active[s].lm_active; 2: only trk && trk_go
 };
 
 // debug (ORBPL_POSE_PROFILE): accumulated wall-clock ticks (100 MHz) of
@@ -1047,7 +1047,11 @@ __global__ void __launch_bounds__(kPoseThreads, ORBPL_POSE_MINW) k_pose(TrackCon
   // or nmatches < 20 after the retry (Tracking.cc:1255-1265).
   // (with lines: also when LineMatcher found < 15, Tracking.cc:1260-1265)
   // TrackLocalMap's pose runs only where TrackWithMotionModel succeeded
-  if (a.gate_lm ? !a.active[s].lm_active
+  // (the TrackReferenceKeyFrame pose leaves every other stream's count alone:
+  // it is the motion model's)
+  if (a.gate_lm == 2 && !(a.active[s].trk && a.active[s].trk_go)) return;
+  if (a.gate_lm ? (a.gate_lm == 1 ? !a.active[s].lm_active
+                                  : !(a.active[s].trk && a.active[s].trk_go))
                 : (a.active && (!a.active[s].has_last || a.active[s].nmatches < 20 ||
                                 (a.t_kl_un && a.active[s].nlmatches < 15)))) {
     if (t == 0) a.ninliers[(long long)s * a.nm_stride] = 0;
@@ -1495,6 +1499,8 @@ __global__ void __launch_bounds__(256) k_finish(TrackConsts c, StreamState* __re
       S.nlmatches_map = 0;
       S.ok = S.has_last ? (S.nmatches >= 20 && s_map >= 10) : 1;
     }
+    // TrackReferenceKeyFrame's decision (Tracking.cc:1031)
+    if (S.has_last && S.trk) S.ok = S.trk_go && s_map >= 10 && (!lf.nl || s_lmap >= 10);
     // TrackLocalMap runs after a successful TrackWithMotionModel and decides
     // the frame's outcome (Tracking.cc:433-436)
     if (local_map && S.has_last) S.ok = S.ok && S.lm_ok;

@@ -809,6 +809,10 @@ struct orbpl_tracker {
   // maps, the gathered local lists and the second pose's buffers
   static constexpr int kLmK = 4;
   int local_map = 0;
+  int refkf = 0;                   // ORBPL_TRACK_REFKF (needs a vocabulary)
+  int *trk_lcur = nullptr, *trk_nobs = nullptr, *trk_lm = nullptr, *trk_nml = nullptr;
+  orbpl_keyline* trk_proj = nullptr;
+  int* trk_src = nullptr;
   int lm_step = 0;                 // frames since reset (Frame::mnId)
   // host-buffer ingress (orbpl_tracker_step_host): 3 device slots of gray,
   // u16 depth and converted f32 depth, filled on a copy stream
@@ -915,7 +919,7 @@ int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam
                             int device, int flags, orbpl_tracker** out) {
   if (!orb || !cam || !out || n_streams <= 0) return arg_fail("bad argument");
   if (flags & ~(ORBPL_TRACK_LINES | ORBPL_TRACK_STEREO | ORBPL_TRACK_LOCAL_MAP |
-                ORBPL_TRACK_FIXED_LINE_JAC))
+                ORBPL_TRACK_FIXED_LINE_JAC | ORBPL_TRACK_REFKF))
     return arg_fail("unknown tracker flag");
   // ORBPL_TRACK_LINES | ORBPL_TRACK_STEREO: the defined stereo line mode (P17;
   // the reference's stereo Frame extracts no lines, Frame.cc:70-131)
@@ -928,6 +932,7 @@ int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam
   t->stereo = (flags & ORBPL_TRACK_STEREO) ? 1 : 0;
   t->fixed_line_jac = (flags & ORBPL_TRACK_FIXED_LINE_JAC) ? 1 : 0;
   t->local_map = (flags & ORBPL_TRACK_LOCAL_MAP) ? 1 : 0;
+  t->refkf = (flags & ORBPL_TRACK_REFKF) ? 1 : 0;
   t->scale_factor = orb->scale_factor;
   t->S = n_streams;
   t->W = cam->width;
@@ -1036,6 +1041,15 @@ int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam
     }
   }
   TA(t->d_edges, S * kPoseMaxEdges * pose_edge_bytes());
+  if (t->refkf) {
+    const size_t L = S * kLineKeep;
+    TA(t->trk_lcur, L * 4);
+    TA(t->trk_nobs, L * 4);
+    TA(t->trk_lm, L * 4);
+    TA(t->trk_nml, S * 4);
+    TA(t->trk_proj, L * sizeof(orbpl_keyline));
+    TA(t->trk_src, L * 4);
+  }
   if (t->stereo) {
     // a right keypoint spans at most 4 * scale + 2 <= 18 rows (8 levels of 1.2)
     t->st_entry_cap = (int)K * 20;
@@ -1148,6 +1162,8 @@ int orbpl_tracker_reset(orbpl_tracker* t, const float* Tcw0) {
 // (d_right, ORBPL_TRACK_STEREO trackers).
 static int tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_depth,
                         const uint8_t* d_right) {
+  if (t->refkf && !t->voc)
+    return arg_fail("ORBPL_TRACK_REFKF tracker: orbpl_tracker_set_vocabulary first");
   HIP_CHECK(hipSetDevice(t->device));
   const int ci = t->ring_pos % 3, li = (t->ring_pos + 2) % 3;
   FrameBufs& C = t->fb[ci];
@@ -1345,6 +1361,64 @@ static int tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_
   }
   p.fixed_line_jac = t->fixed_line_jac;
   launch_pose(t->consts, p, S, ts);
+  if (t->refkf) {
+    // ---- TrackReferenceKeyFrame where the motion model did not run or
+    // failed (Tracking.cc:324-338, 942-1032; P22) ----
+    TrkArgs ta{};
+    ta.st = t->d_state;
+    ta.kp_pitch = K;
+    ta.lines = t->lines;
+    ta.n = C.n;
+    ta.match = C.match;
+    ta.outlier = C.outlier;
+    ta.nl = C.nl;
+    ta.lmatch = C.lmatch;
+    ta.loutlier = C.loutlier;
+    ta.kps_un = C.kps_un;
+    ta.desc = C.desc;
+    ta.feat_node = C.feat_node;
+    ta.last_n = L.n;
+    ta.last_nl = L.nl;
+    ta.last_kps_un = L.kps_un;
+    ta.last_desc = L.desc;
+    ta.last_has_mp = L.has_mp;
+    ta.last_feat_node = L.feat_node;
+    ta.lcur = t->trk_lcur;
+    ta.cur_nobs_l = t->trk_nobs;
+    ta.tlm = t->trk_lm;
+    ta.nml = t->trk_nml;
+    launch_trk_prep(ta, S, ts);
+    launch_trk_bow(ta, S, ts);
+    if (t->lines) {
+      // LineMatcher(0.7, true).SearchByProjection(mCurrentFrame, mpReferenceKF)
+      char* stb = reinterpret_cast<char*>(t->d_state);
+      LineListArgs lr{};
+      lr.Tcw = dTcw;
+      lr.cur_kl_un = C.kl_un;
+      lr.cur_desc = C.ldesc;
+      lr.cur_nobs = t->trk_nobs;
+      lr.valid = L.has_ml;      // mvpMapLines[i] != NULL
+      lr.ml_xyz6 = L.ml_xyz;
+      lr.ml_desc = L.ldesc;
+      lr.proj_kl = t->trk_proj;
+      lr.proj_src = t->trk_src;
+      lr.match = t->trk_lm;
+      lr.nmatches = reinterpret_cast<int*>(stb + offsetof(StreamState, trk_nlm));
+      lr.wiped = reinterpret_cast<int*>(stb + offsetof(StreamState, trk_wiped));
+      lr.refkf = 1;
+      lr.ncur_arr = C.nl;
+      lr.nml_arr = t->trk_nml;
+      lr.cur_pitch = kLineKeep;
+      lr.ml_pitch = kLineKeep;
+      lr.pose_stride = pstride;
+      lr.nm_stride = pstride;
+      launch_line_match_list(t->consts, lr, ts, S);
+    }
+    launch_trk_merge(ta, S, ts);
+    PoseLaunch pt = p;
+    pt.gate_lm = 2;
+    launch_pose(t->consts, pt, S, ts);
+  }
   HIP_CHECK(hipEventRecord(ev[9], ts));
   LocalMapArgs lm{};
   if (t->local_map) {
@@ -1912,6 +1986,17 @@ int orbpl_tracker_get_bow(orbpl_tracker* t, int stream, uint32_t* bow_words, dou
   if (bow_words && bn) HIP_CHECK(hipMemcpy(bow_words, F.bow_words + o, 4 * (size_t)bn, hipMemcpyDeviceToHost));
   if (bow_vals && bn) HIP_CHECK(hipMemcpy(bow_vals, F.bow_vals + o, 8 * (size_t)bn, hipMemcpyDeviceToHost));
   if (feat_node && cnt) HIP_CHECK(hipMemcpy(feat_node, F.feat_node + o, 4 * (size_t)cnt, hipMemcpyDeviceToHost));
+  return ORBPL_OK;
+}
+
+int orbpl_tracker_get_trk(orbpl_tracker* t, int* trk) {
+  if (!t || !trk) return arg_fail("NULL argument");
+  HIP_CHECK(hipSetDevice(t->device));
+  HIP_CHECK(hipStreamSynchronize(t->stream));
+  HIP_CHECK(hipStreamSynchronize(t->tstream));
+  std::vector<StreamState> st(t->S);
+  HIP_CHECK(hipMemcpy(st.data(), t->d_state, sizeof(StreamState) * t->S, hipMemcpyDeviceToHost));
+  for (int s = 0; s < t->S; s++) trk[s] = t->refkf ? st[s].trk : 0;
   return ORBPL_OK;
 }
 

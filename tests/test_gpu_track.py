@@ -637,3 +637,59 @@ def test_tracker_step_host_u16_depth(orbpl, oracle, lines):
             assert np.abs(Th[f] - To).max() < POSE_TOL, (s, f)
     for b in hg + hd:
         b.free()
+
+
+@pytest.mark.parametrize("lines,local_map,pipelined", [(False, False, False), (False, True, True),
+                                                       (True, True, False), (True, False, True)])
+def test_tracker_refkf_matches_oracle(orbpl, oracle, lines, local_map, pipelined):
+    """ORBPL_TRACK_REFKF (P22): the first tracked frame and every motion-model
+    failure go through TrackReferenceKeyFrame (SearchByBoW on the frames'
+    device-computed FeatureVectors + the reference-keyframe line search +
+    pose); every frame's counts and the TRK choice identical to the oracle
+    loop, pose within POSE_TOL. Stream 1's frame 3 is its image turned by
+    180 degrees: the motion model fails there (and after it), so
+    TrackReferenceKeyFrame runs on a failure too."""
+    from _vocab import vocabulary
+    path, _ = vocabulary(k=10, L=5, seed=3, n_frames=8)
+    voc = orbpl.ORBVocabulary(path)
+    ovoc = oracle.Vocabulary(path)
+    S, F = 2, 5
+    seqs = [sequence(F, 90 + s, cam_name="TUM3" if lines else "TUM1") for s in range(S)]
+    frames = [[sq[2][f] for f in range(F)] for sq in seqs]
+    g3, d3 = frames[1][3]
+    frames[1][3] = (np.ascontiguousarray(g3[::-1, ::-1]), np.ascontiguousarray(d3[::-1, ::-1]))
+    cfg = seqs[0][0]
+    flags = oracle.TRACK_REFKF | (oracle.TRACK_LOCAL_MAP if local_map else 0)
+    lvo = oracle.LVO(oracle.params(), oracle.camera(cfg), S, use_lines=lines, flags=flags)
+    lvo.set_vocabulary(ovoc)
+    tr = orbpl.Tracker(orbpl.OrbParams(1000, 1.2, 8, 20, 7), orbpl.make_camera(cfg), S, lines=lines,
+                       local_map=local_map, refkf=True)
+    tr.set_vocabulary(voc, 4)
+    tr.set_pipelined(pipelined)
+    T0 = np.stack([np.linalg.inv(sq[1][0]).astype(np.float32) for sq in seqs])
+    lvo.reset(T0.reshape(S, 16))
+    tr.reset(T0.reshape(S, 16))
+    tr.set_history(F)
+    fa, fb = S * 640 * 480, S * 640 * 480 * 4
+    a = orbpl.DeviceBuffer(F * fa)
+    b = orbpl.DeviceBuffer(F * fb)
+    keys = ("nkeypoints", "nmatches", "ninliers", "nmatches_map", "ok", "nlines", "line_matches",
+            "line_nmatches_map")
+    lkeys = ("local_matches", "local_inliers", "local_line_matches", "local_line_inliers")
+    trk_seen = 0
+    for f in range(F):
+        a.upload(np.stack([frames[s][f][0] for s in range(S)]), offset=f * fa)
+        b.upload(np.stack([frames[s][f][1] for s in range(S)]), offset=f * fb)
+        tr.step_device(a.ptr + f * fa, b.ptr + f * fb)
+        gtrk = tr.trk()
+        for s in range(S):
+            To, so = lvo.step(s, *frames[s][f])
+            assert int(gtrk[s]) == lvo.trk(s), (s, f)
+            trk_seen += lvo.trk(s)
+            if s == 1 and f >= 3:
+                assert lvo.trk(s) == 1, f      # the motion model failed
+            Th, Ch = tr.history(s)
+            ref = [so[k] for k in keys] + [lvo.local_stats(s)[k] for k in lkeys]
+            assert [int(x) for x in Ch[f]] == ref, (s, f, list(Ch[f]), ref)
+            assert np.abs(Th[f] - To).max() < POSE_TOL, (s, f)
+    assert trk_seen >= S + 2    # every stream's first tracked frame, and the failures
