@@ -214,15 +214,32 @@ def pmc_traffic(kernel, workload, streams):
 
 def oracle_flags(O, args):
     return ((O.TRACK_LOCAL_MAP if args.local_map else 0) |
-            (O.TRACK_FIXED_LINE_JAC if args.fixed_line_jacobian else 0))
+            (O.TRACK_FIXED_LINE_JAC if args.fixed_line_jacobian else 0) |
+            (O.TRACK_REFKF if args.refkf and args.bow else 0))
+
+
+# the shared vocabulary's node arrays (build_vocabulary): the oracle loops get
+# the same tree (KeyFrame::ComputeBoW, TrackReferenceKeyFrame)
+VOCAB = {"arrays": None, "oracle": None}
+
+
+def oracle_vocabulary(O):
+    if VOCAB["arrays"] is None:
+        return None
+    if VOCAB["oracle"] is None:
+        VOCAB["oracle"] = O.Vocabulary(arrays=VOCAB["arrays"])
+    return VOCAB["oracle"]
 
 
 def oracle_vo(O, wl, flags=0):
     """The oracle's tracking loop for a workload (oracle/line_track_oracle.cpp
-    LVO with the tracker's flags); returns (vo, step(vo, a, b))."""
+    LVO with the tracker's flags and vocabulary); returns (vo, step(vo, a, b))."""
     import orbpl.synth as synth
     cam = O.camera(getattr(synth, wl["cam"]))
     vo = O.LVO(O.params(*wl["orb"]), cam, 1, use_lines=wl["lines"], flags=flags)
+    voc = oracle_vocabulary(O)
+    if voc is not None:
+        vo.set_vocabulary(voc)
     if wl["stereo"]:
         return vo, lambda vo, a, b: vo.step_stereo(0, a, b)
     return vo, lambda vo, a, b: vo.step(0, a, b)
@@ -366,8 +383,10 @@ def build_vocabulary(pkg, synth, args, rank, world, device, dist):
         if pkg.device_count() >= world and torch.cuda.is_available():
             rccl = device
     w, n_docs, backend = shared_idf(synth, tree, docs, dist, rccl)
-    voc = pkg.ORBVocabulary(arrays=dict(parent=tree["parent"], leaf=tree["leaf"], desc=tree["desc"],
-                                        weight=w, k=k, L=L, scoring=0, weighting=0), device=device)
+    arrays = dict(parent=tree["parent"], leaf=tree["leaf"], desc=tree["desc"], weight=w, k=k, L=L,
+                  scoring=0, weighting=0)
+    voc = pkg.ORBVocabulary(arrays=arrays, device=device)
+    VOCAB["arrays"] = arrays
     info = {"k": k, "L": L, "nodes": voc.n_nodes, "words": voc.n_words,
             "stopped_words": int(((w == 0) & tree["leaf"]).sum()), "levelsup": 4,
             "documents": n_docs, "idf_reduction": backend,
@@ -396,7 +415,8 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
     d_depth = pkg.DeviceBuffer.from_array(depth[rep], device=device)
     cam = pkg.make_camera(getattr(synth, cam_name))
     tr = pkg.Tracker(pkg.OrbParams(*wl["orb"]), cam, S, device=device, lines=lines, stereo=stereo,
-                     local_map=bool(args.local_map), fixed_line_jac=bool(args.fixed_line_jacobian))
+                     local_map=bool(args.local_map), fixed_line_jac=bool(args.fixed_line_jacobian),
+                     refkf=bool(args.refkf and voc is not None))
     # pipelining overlaps extraction of step t+1 with tracking of step t; the
     # LSD-bound line workloads gain nothing from it
     pipelined = args.pipelined if args.pipelined >= 0 else (0 if lines else 1)
@@ -533,7 +553,7 @@ def run_ingress(pkg, synth, args, S, steps, warmup, rank, world, device, dist, v
     hg.array[:] = gray[rep]
     hd.array[:] = d16[rep]
     tr = pkg.Tracker(pkg.OrbParams(*wl["orb"]), pkg.make_camera(synth.TUM1), S, device=device,
-                     local_map=bool(args.local_map))
+                     local_map=bool(args.local_map), refkf=bool(args.refkf and voc is not None))
     tr.set_pipelined(True)
     if voc is not None:
         tr.set_vocabulary(voc, 4)
@@ -568,7 +588,7 @@ def run_ingress(pkg, synth, args, S, steps, warmup, rank, world, device, dist, v
     return out
 
 
-def sweep(pkg, synth, workload, sizes, steps, device, local_map=True):
+def sweep(pkg, synth, workload, sizes, steps, device, local_map=True, voc=None, refkf=False):
     """Per-step latency and throughput at several batch sizes (untimed for the
     headline; each size gets its own tracker, 1 warm-up step)."""
     wl = WORKLOADS[workload]
@@ -584,8 +604,11 @@ def sweep(pkg, synth, workload, sizes, steps, device, local_map=True):
         d_gray = pkg.DeviceBuffer.from_array(gray[rep], device=device)
         d_depth = pkg.DeviceBuffer.from_array(depth[rep], device=device)
         tr = pkg.Tracker(pkg.OrbParams(*wl["orb"]), cam, S, device=device, lines=wl["lines"],
-                         stereo=wl["stereo"], local_map=local_map)
+                         stereo=wl["stereo"], local_map=local_map,
+                         refkf=bool(refkf and voc is not None))
         tr.set_pipelined(not wl["lines"])
+        if voc is not None:
+            tr.set_vocabulary(voc, 4)
         tr.reset(np.stack([np.linalg.inv(L.Twc(s, 0)).astype(np.float32)
                            for s in range(S)]).reshape(S, 16))
         fb, db = fw * fh, fw * fh * depth.itemsize
@@ -684,6 +707,9 @@ def cpu_reference_faithful(seconds, gray, depth, L, workload, flags=0):
     wl = WORKLOADS[workload]
     cam = O.camera(getattr(synth, wl["cam"]))
     vo = O.LVO(O.params(*wl["orb"]), cam, 1, use_lines=wl["lines"], flags=O.TWO_THREADS | flags)
+    voc = oracle_vocabulary(O)
+    if voc is not None:
+        vo.set_vocabulary(voc)
     vo.reset(np.linalg.inv(L.Twc(0, 0)).astype(np.float32).reshape(1, 16))
     lat = []
     stop = time.time() + seconds
@@ -760,6 +786,9 @@ def main():
                     help="1 = every frame's KeyFrame::ComputeBoW with a shared synthetic "
                          "vocabulary (broadcast + IDF all-reduce over ranks); 0 = off")
     ap.add_argument("--vocab-levels", type=int, default=5, help="vocabulary depth L (k = 10)")
+    ap.add_argument("--refkf", type=int, default=1,
+                    help="1 = Tracking::Track's TrackReferenceKeyFrame for the first tracked "
+                         "frame and motion-model failures (needs --bow; DESIGN.md P22)")
     ap.add_argument("--ingress-steps", type=int, default=20,
                     help="steps of the host-memory ingress leg (u8 gray + u16 depth copied "
                          "host-to-device inside the timed region; points runs only; 0 = skip)")
@@ -826,8 +855,10 @@ def main():
     sweeps = None
     if rank == 0 and world == 1 and args.sweep and args.workload == "points":
         lmf = bool(args.local_map)
-        sweeps = {"points": sweep(pkg, synth, "points", (1, 16, 64, 256, 1024), 5, device, lmf),
-                  "lines": sweep(pkg, synth, "lines", (1, 16, 64, 256), 2, device, lmf)}
+        rk = bool(args.refkf)
+        sweeps = {"points": sweep(pkg, synth, "points", (1, 16, 64, 256, 1024), 5, device, lmf,
+                                  voc, rk),
+                  "lines": sweep(pkg, synth, "lines", (1, 16, 64, 256), 2, device, lmf, voc, rk)}
 
     cpu = None
     host = host_info()
@@ -866,7 +897,8 @@ def main():
                        "frames_per_step": S * world, "parallelism": f"streams sharded x{world}",
                        "pipelined": res["pipelined"], "track_local_map": bool(args.local_map),
                        "fixed_line_jacobian": bool(args.fixed_line_jacobian),
-                       "keyframe_bow": bool(args.bow)},
+                       "keyframe_bow": bool(args.bow),
+                       "track_reference_keyframe": bool(args.bow and args.refkf)},
             "vocabulary": voc_info,
             "stage_ms": res["stages"],
             "tracking": res["tracking"],

@@ -150,6 +150,33 @@ void* oracle_voc_load_text(const char* path) {
   return v;
 }
 
+// the same tree from flat node arrays (node 0 = root, parent[i] < i; word
+// ids follow the leaf flags in node order), e.g. the bench's shared vocabulary
+void* oracle_voc_create(int k, int L, int scoring, int weighting, int n_nodes,
+                        const int32_t* parent, const uint8_t* leaf, const uint8_t* desc,
+                        const double* weight) {
+  if (n_nodes < 1) return nullptr;
+  Voc* v = new Voc();
+  v->k = k;
+  v->L = L;
+  v->scoring = scoring;
+  v->weighting = weighting;
+  v->nodes.resize(n_nodes);
+  for (int i = 1; i < n_nodes; i++) {
+    if (parent[i] < 0 || parent[i] >= i) {
+      delete v;
+      return nullptr;
+    }
+    Node& nd = v->nodes[i];
+    nd.parent = parent[i];
+    v->nodes[parent[i]].children.push_back(i);
+    std::memcpy(nd.desc, desc + 32 * (size_t)i, 32);
+    nd.weight = weight[i];
+    if (leaf[i]) nd.word_id = v->nwords++;
+  }
+  return v;
+}
+
 void oracle_voc_destroy(void* h) { delete static_cast<Voc*>(h); }
 
 int oracle_voc_info(void* h, int* out6) {

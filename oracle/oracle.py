@@ -636,18 +636,28 @@ def _setup_voc(L):
     L.oracle_voc_info.argtypes = [vp, vp]
     L.oracle_voc_nodes.argtypes = [vp, vp, vp, vp, vp, vp]
     L.oracle_voc_transform.argtypes = [vp, vp, i, i, vp, vp, C.POINTER(C.c_int), vp, vp, vp]
+    L.oracle_voc_create.argtypes = [i, i, i, i, i, vp, vp, vp, vp]
+    L.oracle_voc_create.restype = vp
 
 
 class Vocabulary:
     """ORBVocabulary::loadFromTextFile + transform (TemplatedVocabulary.h:1338,
     1127-1262)."""
 
-    def __init__(self, path):
+    def __init__(self, path=None, arrays=None):
         L = lib()
         if not hasattr(L, "_voc_ready"):
             _setup_voc(L)
             L._voc_ready = True
-        self.h = L.oracle_voc_load_text(str(path).encode())
+        if path is not None:
+            self.h = L.oracle_voc_load_text(str(path).encode())
+        else:
+            a = arrays
+            self._keep = [_c(a["parent"], np.int32), _c(a["leaf"], np.uint8),
+                          _c(a["desc"], np.uint8), _c(a["weight"], np.float64)]
+            self.h = L.oracle_voc_create(int(a["k"]), int(a["L"]), int(a["scoring"]),
+                                         int(a["weighting"]), len(self._keep[0]),
+                                         *[_p(x) for x in self._keep])
         if not self.h:
             raise ValueError(f"vocabulary load failed: {path}")
         info = np.zeros(6, np.int32)
