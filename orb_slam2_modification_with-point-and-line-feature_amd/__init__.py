@@ -94,6 +94,17 @@ def _ptr(a):
     return a.ctypes.data_as(C.c_void_p)
 
 
+def _rows_u8(image):
+    """A 2-D u8 image as (array, row pitch in bytes): a view whose rows are
+    contiguous (a cv::Mat ROI: step > cols) is passed as is with its pitch,
+    anything else is copied contiguous."""
+    a = np.asarray(image)
+    if a.dtype == np.uint8 and a.ndim == 2 and a.strides[1] == 1 and a.strides[0] >= a.shape[1]:
+        return a, int(a.strides[0])
+    a = np.ascontiguousarray(a, dtype=np.uint8)
+    return a, (a.shape[1] if a.ndim == 2 else 0)
+
+
 class DeviceBuffer:
     """Owned device allocation (hipMalloc via the C-ABI)."""
 
@@ -250,14 +261,14 @@ class ORBextractor:
         in the reference (ORBextractor.h:56)."""
         if image is None or image.size == 0:
             return np.zeros(0, KP_DTYPE), None
-        img = np.ascontiguousarray(image, dtype=np.uint8)
+        img, stride = _rows_u8(image)
         assert img.ndim == 2, "CV_8UC1 image expected (ORBextractor.cc:1050)"
         h, w = img.shape
         cap = self.max_keypoints
         kps = np.zeros(cap, KP_DTYPE)
         desc = np.zeros((cap, 32), np.uint8)
         n = C.c_int(0)
-        check(lib().orbx_extract(self._h, _ptr(img), w, h, w, _ptr(kps), _ptr(desc), cap,
+        check(lib().orbx_extract(self._h, _ptr(img), w, h, stride, _ptr(kps), _ptr(desc), cap,
                                  C.byref(n)), "orbx_extract")
         k = n.value
         return kps[:k].copy(), (desc[:k].copy() if k else None)
@@ -964,14 +975,14 @@ class LineExtractor(LineSegmentDetector):
     with scale = 1, num_octaves = 1 as Frame::ExtractLine calls it (Frame.cc:326-328)."""
 
     def ExtractLineSegment(self, img):
-        img = np.ascontiguousarray(img, np.uint8)
+        img, stride = _rows_u8(img)
         h, w = img.shape
         kl = np.zeros(80, KEYLINE_DTYPE)
         desc = np.zeros((80, 32), np.uint8)
         coef = np.zeros((80, 3), np.float64)
         n = C.c_int(0)
-        check(lib().lsdx_extract(self._h, _ptr(img), w, h, w, _ptr(kl), _ptr(desc), _ptr(coef), 80,
-                                 C.byref(n)), "lsdx_extract")
+        check(lib().lsdx_extract(self._h, _ptr(img), w, h, stride, _ptr(kl), _ptr(desc), _ptr(coef),
+                                 80, C.byref(n)), "lsdx_extract")
         k = n.value
         return kl[:k].copy(), desc[:k].copy(), coef[:k].copy()
 

@@ -1213,9 +1213,13 @@ __global__ void __launch_bounds__(kPoseThreads, ORBPL_POSE_MINW) k_pose(TrackCon
         quat_to_R(T.q, R);
         double acc[28];
         for (int k = 0; k < 28; k++) acc[k] = 0;
+        // the next edge's load is issued before this edge's arithmetic
+        PoseEdge e_next;
+        if (t < ne) e_next = E[t];
         for (int k = t; k < ne; k += kPoseThreads) {
+          const PoseEdge e = e_next;
+          if (k + kPoseThreads < ne) e_next = E[k + kPoseThreads];
           if (S.level[k]) continue;
-          const PoseEdge e = E[k];
           double err[3], J[3][6];
           edge_error(e, c, T, R, err);
           // rows beyond the edge's dimension are zero (err[2] = 0 and J row 2
@@ -1292,9 +1296,12 @@ __global__ void __launch_bounds__(kPoseThreads, ORBPL_POSE_MINW) k_pose(TrackCon
           double R2[3][3];
           quat_to_R(T.q, R2);
           double tc2 = 0;
+          PoseEdge e_next;
+          if (t < ne) e_next = E[t];
           for (int k = t; k < ne; k += kPoseThreads) {
+            const PoseEdge e = e_next;
+            if (k + kPoseThreads < ne) e_next = E[k + kPoseThreads];
             if (S.level[k]) continue;
-            const PoseEdge e = E[k];
             double err[3];
             edge_error(e, c, T, R2, err);
             const int dim = e.kind == 1 ? 3 : 2;

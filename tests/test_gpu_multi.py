@@ -28,3 +28,18 @@ def test_bench_two_ranks():
     assert par["all_ranks_pass"], par
     assert len(par["by_rank"]) == 2
     assert all(p["steps_checked"] == 3 for p in par["by_rank"])
+
+
+def test_bench_lines_1024_streams_parity():
+    """The lines workload timed at 1024 streams (the LSD scratch of every
+    stream resident at once): the timed tracker's sampled streams 0, 512 and
+    1023 match the oracle loop bit-exact (counts) / within POSE_TOL (pose)."""
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--workload", "lines", "--streams", "1024",
+           "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--sweep", "0",
+           "--isolated-steps", "0", "--ingress-steps", "0"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=400, cwd=str(ROOT))
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads([x for x in out.stdout.splitlines() if x.startswith("{")][-1])
+    assert r["config"]["streams_per_gpu"] == 1024 and r["tracking"]["mean_lines"] > 50
+    par = r["parity"]
+    assert par["pass"] and par["streams"] == [0, 512, 1023] and par["steps_checked"] == 3, par
