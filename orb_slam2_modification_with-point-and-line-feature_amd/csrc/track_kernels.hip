@@ -17,6 +17,7 @@
 //                     608-660 / Frame::UnprojectStereo)
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstdlib>
 #include <stdint.h>
 
@@ -610,6 +611,25 @@ __global__ void __launch_bounds__(kMatchThreads) k_match_last(TrackConsts c, Mat
 struct Quat { double w, x, y, z; };
 struct SE3d { Quat q; double t[3]; };
 
+// Every thread of a k_pose workgroup runs the same LM control on the same
+// reduced sums, so the estimate and its rotation are uniform: readfirstlane
+// lets them live in scalar registers instead of 32 VGPRs.
+__device__ __forceinline__ double uni(double v) {
+  const int lo = __builtin_amdgcn_readfirstlane(__double2loint(v));
+  const int hi = __builtin_amdgcn_readfirstlane(__double2hiint(v));
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ void uni(SE3d& T) {
+  T.q.w = uni(T.q.w); T.q.x = uni(T.q.x); T.q.y = uni(T.q.y); T.q.z = uni(T.q.z);
+  T.t[0] = uni(T.t[0]); T.t[1] = uni(T.t[1]); T.t[2] = uni(T.t[2]);
+}
+__device__ __forceinline__ void uni(double R[3][3]) {
+#pragma unroll
+  for (int r = 0; r < 3; r++)
+#pragma unroll
+    for (int c = 0; c < 3; c++) R[r][c] = uni(R[r][c]);
+}
+
 __device__ __forceinline__ void normalize_rotation(Quat& q) {
   if (q.w < 0) { q.w = -q.w; q.x = -q.x; q.y = -q.y; q.z = -q.z; }
   const double n = sqrt(q.w * q.w + q.x * q.x + q.y * q.y + q.z * q.z);
@@ -1029,16 +1049,11 @@ __device__ void se3_from_T(const float* T, SE3d& s) {
   s.t[0] = T[3]; s.t[1] = T[7]; s.t[2] = T[11];
 }
 
-// minimum waves per SIMD for k_pose (register budget; it shares CUs with the
-// extraction kernels in the pipelined tracker)
-#ifndef ORBPL_POSE_MINW
-#define ORBPL_POSE_MINW 1
-#endif
-// kPoseThreads threads per stream (one workgroup per stream): 256 while the
-// streams fit one workgroup per CU, fewer (more streams per CU at the same
-// 314-VGPR footprint) beyond; see launch_pose
-template <int kPoseThreads>
-__global__ void __launch_bounds__(kPoseThreads, ORBPL_POSE_MINW) k_pose(TrackConsts tc, PoseArgs a) {
+// kPoseThreads threads per stream (one workgroup per stream), kMinWaves waves
+// per SIMD the register budget must allow (1: ~300 VGPRs; 2: 256 and a few
+// spills); launch_pose picks both from the streams per CU
+template <int kPoseThreads, int kMinWaves>
+__global__ void __launch_bounds__(kPoseThreads, kMinWaves) k_pose(TrackConsts tc, PoseArgs a) {
   constexpr int kPoseWaves = kPoseThreads / 64;
   extern __shared__ char smem_raw[];
   PoseShared& S = *reinterpret_cast<PoseShared*>(smem_raw);
@@ -1195,6 +1210,7 @@ __global__ void __launch_bounds__(kPoseThreads, ORBPL_POSE_MINW) k_pose(TrackCon
   bool robust = true;
   for (int round = 0; round < 4; round++) {
     SE3d T = T0;
+    uni(T);
     // ---- optimizer.optimize(10) ----
     int nact = 0;
     for (int k = t; k < ne; k += kPoseThreads) nact += S.level[k] == 0;
@@ -1211,6 +1227,7 @@ __global__ void __launch_bounds__(kPoseThreads, ORBPL_POSE_MINW) k_pose(TrackCon
         // computeActiveErrors + buildSystem at T (fused: same estimate)
         double R[3][3];
         quat_to_R(T.q, R);
+        uni(R);
         double acc[28];
         for (int k = 0; k < 28; k++) acc[k] = 0;
         // the next edge's load is issued before this edge's arithmetic
@@ -1290,11 +1307,13 @@ __global__ void __launch_bounds__(kPoseThreads, ORBPL_POSE_MINW) k_pose(TrackCon
           for (int j = 0; j < 6; j++) Hl[j][j] += lambda;
           const bool ok2 = solve6(Hl, b, x);
           T = se3_mul(se3_exp(x), T);
+          uni(T);
           lap(2);
           pt[6]++;
           // computeActiveErrors at the trial estimate
           double R2[3][3];
           quat_to_R(T.q, R2);
+          uni(R2);
           double tc2 = 0;
           PoseEdge e_next;
           if (t < ne) e_next = E[t];
@@ -1334,6 +1353,7 @@ __global__ void __launch_bounds__(kPoseThreads, ORBPL_POSE_MINW) k_pose(TrackCon
             lambda *= ni;
             ni *= 2;
             T = backup;
+            uni(T);
           }
           qmax++;
         } while (rho < 0 && qmax < 10);
@@ -1346,6 +1366,7 @@ __global__ void __launch_bounds__(kPoseThreads, ORBPL_POSE_MINW) k_pose(TrackCon
     // ---- classify (Optimizer.cc:2387-2470) ----
     double R[3][3];
     quat_to_R(T.q, R);
+    uni(R);
     int nbad = 0;
     for (int k = t; k < ne; k += kPoseThreads) {
       const PoseEdge e = E[k];
@@ -1646,20 +1667,33 @@ void launch_pose(const TrackConsts& c, const PoseLaunch& p, int nstreams, hipStr
   a.gate_lm = p.gate_lm;
   static const int prof = getenv("ORBPL_POSE_PROFILE") ? 1 : 0;
   a.prof = prof;
-  // one wave per SIMD at k_pose's register footprint: 256 threads per stream
-  // while nstreams * waves <= 4 per CU (lowest latency per stream), then
-  // 128 / 64 (256 streams: 0.40 / 0.50 / 0.71 ms; 1024: 1.48 / 1.00 / 0.80)
+  // threads per stream by streams per CU: the widest workgroup while every
+  // stream gets its own CU (lowest latency per stream), then narrower ones so
+  // that more streams share a CU at one wave per SIMD. At 512 / 1024 streams:
+  // 128x1 0.50 / 0.96 ms, 64x1 0.70 / 0.72, 128x2 0.72 / 0.84, 64x2 0.74 / 1.08
+  // (isolated; "threads x waves per SIMD"). ORBPL_POSE_CFG="threads,waves"
+  // overrides (A/B runs).
   const int cus = device_cu_count();
-  if (nstreams * 4 <= 4 * cus) {
-    set_smem_attr((const void*)k_pose<256>, sizeof(PoseShared));
-    hipLaunchKernelGGL(k_pose<256>, dim3(nstreams), dim3(256), sizeof(PoseShared), s, c, a);
-  } else if (nstreams * 2 <= 4 * cus) {
-    set_smem_attr((const void*)k_pose<128>, sizeof(PoseShared));
-    hipLaunchKernelGGL(k_pose<128>, dim3(nstreams), dim3(128), sizeof(PoseShared), s, c, a);
-  } else {
-    set_smem_attr((const void*)k_pose<64>, sizeof(PoseShared));
-    hipLaunchKernelGGL(k_pose<64>, dim3(nstreams), dim3(64), sizeof(PoseShared), s, c, a);
+  int nt = 256, mw = 1;
+  if (nstreams > cus) nt = 128;
+  if (nstreams > 2 * cus) nt = 64;   // (2 waves per SIMD measured slower at 512 / 1024)
+  static const char* cfg = getenv("ORBPL_POSE_CFG");
+  if (cfg) sscanf(cfg, "%d,%d", &nt, &mw);
+#define ORBPL_POSE_LAUNCH(NT, MW)                                                            \
+  if (nt == NT && mw == MW) {                                                                 \
+    set_smem_attr((const void*)k_pose<NT, MW>, sizeof(PoseShared));                           \
+    hipLaunchKernelGGL((k_pose<NT, MW>), dim3(nstreams), dim3(NT), sizeof(PoseShared), s, c, a); \
+    return;                                                                                   \
   }
+  ORBPL_POSE_LAUNCH(256, 1)
+  ORBPL_POSE_LAUNCH(128, 1)
+  ORBPL_POSE_LAUNCH(64, 1)
+  ORBPL_POSE_LAUNCH(256, 2)
+  ORBPL_POSE_LAUNCH(128, 2)
+  ORBPL_POSE_LAUNCH(64, 2)
+#undef ORBPL_POSE_LAUNCH
+  set_smem_attr((const void*)k_pose<64, 1>, sizeof(PoseShared));
+  hipLaunchKernelGGL((k_pose<64, 1>), dim3(nstreams), dim3(64), sizeof(PoseShared), s, c, a);
 }
 
 void launch_finish(const TrackConsts& c, StreamState* st, const int* n, int kp_pitch,
