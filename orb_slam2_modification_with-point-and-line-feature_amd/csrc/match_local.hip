@@ -89,11 +89,13 @@ __global__ void __launch_bounds__(256) k_in_frustum(TrackConsts c, float log_sca
 
 namespace {
 
-constexpr int kLocalKp = 2048;
 constexpr int kLocalThreads = 1024;   // 16 waves: phase A and the grid build; wave 0 runs phase B
 constexpr int kCells = kGridCols * kGridRows;
 
-// 126 KB: one workgroup per CU, the current frame's descriptors in LDS
+// the current frame's keypoints (grid, descriptors, claims) in LDS for up to
+// kLocalKp keypoints: 126 KB at 2048 (one workgroup per CU), 63 KB at 1024
+// (two per CU: the 1000-feature configurations)
+template <int kLocalKp>
 struct LocalShared {
   uint4 desc[kLocalKp * 2];         // current descriptors (32 B rows)
   float2 xy[kLocalKp];
@@ -141,13 +143,15 @@ struct TopList {
   int cnt;
 };
 
-__device__ __forceinline__ bool is_claimed(const LocalShared& S, int j) {
+template <int KP>
+__device__ __forceinline__ bool is_claimed(const LocalShared<KP>& S, int j) {
   return (S.claimed[j >> 5] >> (j & 31)) & 1u;
 }
 
 // GetFeaturesInArea(x, y, r*scale, level-1, level) + the candidate loop
 // (ORBmatcher.cc:96-160) against the current claims.
-__device__ TopList local_scan(const LocalShared& S, const TrackConsts& c, const LocalArgs& a,
+template <int KP>
+__device__ TopList local_scan(const LocalShared<KP>& S, const TrackConsts& c, const LocalArgs& a,
                               int i) {
   TopList t;
 #pragma unroll
@@ -208,7 +212,8 @@ __device__ TopList local_scan(const LocalShared& S, const TrackConsts& c, const 
 
 // the first two unclaimed entries; *full = the list cannot decide (fewer than
 // two unclaimed entries while candidates beyond the kept ones exist)
-__device__ __forceinline__ Top2 pick2(const LocalShared& S, const TopList& t, bool* full) {
+template <int KP>
+__device__ __forceinline__ Top2 pick2(const LocalShared<KP>& S, const TopList& t, bool* full) {
   Top2 r{256, -1, -1, 256, -1, -1};
   int found = 0;
 #pragma unroll
@@ -231,6 +236,7 @@ __device__ __forceinline__ Top2 pick2(const LocalShared& S, const TopList& t, bo
 
 }  // namespace
 
+template <int kLocalKp>
 __global__ void __launch_bounds__(kLocalThreads) k_match_local(TrackConsts c, LocalArgs a) {
   if (a.n_arr) {  // batched: stream blockIdx.x
     const int b = blockIdx.x;
@@ -254,7 +260,7 @@ __global__ void __launch_bounds__(kLocalThreads) k_match_local(TrackConsts c, Lo
     a.nmatches += (long long)b * a.nm_stride;
   }
   extern __shared__ char smem_local[];
-  LocalShared& S = *reinterpret_cast<LocalShared*>(smem_local);
+  LocalShared<kLocalKp>& S = *reinterpret_cast<LocalShared<kLocalKp>*>(smem_local);
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
   const int n = min(a.n, kLocalKp);
   // ---- grid (AssignFeaturesToGrid with PosInGrid, Frame.cc:265-287, 527-538) ----
@@ -439,8 +445,15 @@ void launch_in_frustum(const TrackConsts& c, float log_scale, const InFrustumArg
 }
 
 void launch_match_local(const TrackConsts& c, const LocalArgs& a, hipStream_t s, int nstreams) {
-  set_smem_attr((const void*)k_match_local, sizeof(LocalShared));
-  hipLaunchKernelGGL(k_match_local, dim3(a.n_arr ? nstreams : 1), dim3(kLocalThreads), sizeof(LocalShared), s,
+  const int cap = a.n_arr ? a.kp_pitch : a.n;   // keypoints a frame can hold
+  if (cap <= 1024) {
+    set_smem_attr((const void*)k_match_local<1024>, sizeof(LocalShared<1024>));
+    hipLaunchKernelGGL(k_match_local<1024>, dim3(a.n_arr ? nstreams : 1), dim3(kLocalThreads),
+                       sizeof(LocalShared<1024>), s, c, a);
+    return;
+  }
+  set_smem_attr((const void*)k_match_local<2048>, sizeof(LocalShared<2048>));
+  hipLaunchKernelGGL(k_match_local<2048>, dim3(a.n_arr ? nstreams : 1), dim3(kLocalThreads), sizeof(LocalShared<2048>), s,
                      c, a);
 }
 
