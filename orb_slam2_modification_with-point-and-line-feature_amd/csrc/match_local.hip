@@ -3,7 +3,8 @@
 //                    + MapPoint::PredictScale (MapPoint.cc:416-431), thread per point
 //   k_match_local  : ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&,
 //                    th) (ORBmatcher.cc:72-183), one workgroup per frame:
-//     grid build    - AssignFeaturesToGrid in LDS (cells hold increasing indices)
+//     index build   - the grid keypoints as records sorted by (octave, column,
+//                     row, index) in LDS, one range per (octave, column)
 //     phase A       - every map point in parallel: its first 4 candidates in
 //                     (distance, grid-scan position) order, whose first two
 //                     are the reference's running best / second, with the
@@ -89,32 +90,53 @@ __global__ void __launch_bounds__(256) k_in_frustum(TrackConsts c, float log_sca
 
 namespace {
 
-constexpr int kLocalThreads = 1024;   // 16 waves: phase A and the grid build; wave 0 runs phase B
-constexpr int kCells = kGridCols * kGridRows;
+constexpr int kLocalThreads = 1024;   // 16 waves: the index build and phase A; wave 0 runs phase B
+constexpr int kLevelCols = kMaxLevelsT * kGridCols;   // (octave, grid column) ranges
 
-// the current frame's keypoints (grid, descriptors, claims) in LDS for up to
-// kLocalKp keypoints: 126 KB at 2048 (one workgroup per CU), 63 KB at 1024
-// (two per CU: the 1000-feature configurations)
+// The current frame's keypoints in LDS for up to kLocalKp keypoints: 140 KB at
+// 2048 (one workgroup per CU), 71 KB at 1024 (two per CU: the 1000-feature
+// configurations). The keypoints in the grid are held as records sorted by
+// (octave, column, row, index): the candidates of one octave in one grid
+// column are one contiguous range, in the reference's scan order.
 template <int kLocalKp>
 struct LocalShared {
-  uint4 desc[kLocalKp * 2];         // current descriptors (32 B rows)
-  float2 xy[kLocalKp];
-  float ur[kLocalKp];
-  int mw[kLocalKp];                 // last writer (map point index) per keypoint
-  int own[kLocalKp];                // phase B: (round << 6) | (63 - lane) of the round's
-                                    // first claimer per keypoint
-  uint16_t fill[kCells];             // (4-byte aligned: counters are added in pairs)
-  uint16_t cell_start[kCells + 2];
-  uint16_t items[kLocalKp];
-  int16_t gc[kLocalKp];
+  uint4 desc[kLocalKp * 2];          // current descriptors (32 B rows), by keypoint
+  float4 rec[kLocalKp];              // sorted records: x, y, uRight, bits(column | row | index)
+  int mw[kLocalKp];                  // last writer (map point index) per keypoint
+  int own[kLocalKp];                 // phase B: (round << 6) | (63 - lane) of the round's
+                                     // first claimer per keypoint
+  uint32_t skey[kLocalKp];           // sort keys: octave << 23 | scan key
+  uint16_t list[4 * kLocalKp];       // in-view map points of a window, by predicted level
+  uint16_t lc_start[kLevelCols + 1]; // first record of each (octave, column)
   int8_t oct[kLocalKp];
-  uint32_t claimed[kLocalKp / 32];  // holds a map point with Observations() > 0
-  int wsum[kLocalThreads / 64];
+  uint32_t claimed[kLocalKp / 32];   // holds a map point with Observations() > 0
+  int lvl_cnt[kMaxLevelsT];
+  int lvl_pos[kMaxLevelsT];
 };
 
 struct Top2 {
   int bd, bi, bl;   // best distance, index, level
   int sd, si, sl;   // second distance, index of the candidate that set it, level
+};
+
+// The reference's running best / second pair (ORBmatcher.cc:128-145, strict
+// comparisons) is the first two candidates in (distance, scan position) order:
+// the best is the earliest candidate of minimal distance, the second the
+// earliest other candidate of the next distance (or of the same one). Claims
+// only remove candidates, so the pair under later claims is the first two
+// unclaimed entries of that order. GetFeaturesInArea scans grid columns, then
+// rows, then the cell's keypoints in index order (Frame.cc:406-441), so the
+// scan position of a keypoint is its scan key column << 17 | row << 11 | index.
+// The scan keeps the first kTopK entries of (distance, scan key) order as
+// entry = distance << 23 | scan key (all ones = empty: no candidate has
+// distance 255 and row 63); bit 31 of the last entry flags more candidates than
+// the list holds.
+constexpr int kTopK = 4;
+constexpr uint32_t kEmpty = 0xFFFFFFFFu;
+constexpr uint32_t kMore = 0x80000000u;
+
+struct TopList {
+  uint32_t e[kTopK];
 };
 
 __device__ __forceinline__ int hamming32l(const uint8_t* a, const uint8_t* b) {
@@ -126,87 +148,67 @@ __device__ __forceinline__ int hamming32l(const uint8_t* a, const uint8_t* b) {
          __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
 }
 
-// The reference's running best / second pair (ORBmatcher.cc:128-145, strict
-// comparisons) is the first two candidates in (distance, scan position) order:
-// the best is the earliest candidate of minimal distance, the second the
-// earliest other candidate of the next distance (or of the same one). Claims
-// only remove candidates, so the pair under later claims is the first two
-// unclaimed entries of that order. The scan keeps the first kTopK entries of
-// it; entry = index (11 bits) | distance << 11 (9 bits) | level << 20 (4 bits),
-// all ones = empty (no candidate has distance 511); the count of candidates
-// (saturated at 255) rides in entry 0's top byte in the scratch record.
-constexpr int kTopK = 4;
-constexpr uint32_t kEmpty = 0xFFFFFFu;
-
-struct TopList {
-  uint32_t e[kTopK];
-  int cnt;
-};
-
 template <int KP>
 __device__ __forceinline__ bool is_claimed(const LocalShared<KP>& S, int j) {
   return (S.claimed[j >> 5] >> (j & 31)) & 1u;
 }
 
 // GetFeaturesInArea(x, y, r*scale, level-1, level) + the candidate loop
-// (ORBmatcher.cc:96-160) against the current claims.
+// (ORBmatcher.cc:96-160) against the current claims. The cell window of
+// GetFeaturesInArea holds every keypoint that passes the exact |dx|, |dy| < r
+// test (PosInGrid rounds, the window floors / ceils), so the scan visits the
+// window's columns of the two octaves only and keeps the scan order by key.
 template <int KP>
 __device__ TopList local_scan(const LocalShared<KP>& S, const TrackConsts& c, const LocalArgs& a,
                               int i) {
   TopList t;
 #pragma unroll
   for (int k = 0; k < kTopK; k++) t.e[k] = kEmpty;
-  t.cnt = 0;
+  int cnt = 0;
   const int lev = a.level[i];
   float r = (a.view_cos[i] > 0.998) ? 2.5f : 4.0f;
   if (a.th != 1.0) r *= a.th;
   const float rad = r * c.scale[lev];
   const float x = a.proj_x[i], y = a.proj_y[i], xr = a.proj_xr[i];
-  const int minLevel = lev - 1, maxLevel = lev;
   const int cx0 = max(0, (int)floorf((x - c.minX - rad) * c.gridInvW));
   const int cx1 = min(kGridCols - 1, (int)ceilf((x - c.minX + rad) * c.gridInvW));
   const int cy0 = max(0, (int)floorf((y - c.minY - rad) * c.gridInvH));
   const int cy1 = min(kGridRows - 1, (int)ceilf((y - c.minY + rad) * c.gridInvH));
   if (cx0 >= kGridCols || cx1 < 0 || cy0 >= kGridRows || cy1 < 0) return t;
-  const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
   const uint4* dp = reinterpret_cast<const uint4*>(a.mp_desc + (long long)i * 32);
   const uint4 m0 = dp[0], m1 = dp[1];
-  for (int ix = cx0; ix <= cx1; ix++)
-    for (int iy = cy0; iy <= cy1; iy++) {
-      const int cell = ix + kGridCols * iy;
-      const int b = S.cell_start[cell], e = S.cell_start[cell + 1];
-      for (int q = b; q < e; q++) {
-        const int j = S.items[q];
-        const int oc = S.oct[j];
-        if (bCheckLevels) {
-          if (oc < minLevel) continue;
-          if (maxLevel >= 0 && oc > maxLevel) continue;
-        }
-        const float2 p = S.xy[j];
-        if (!(fabsf(p.x - x) < rad && fabsf(p.y - y) < rad)) continue;
-        if (is_claimed(S, j)) continue;
-        const float urj = S.ur[j];
-        if (urj > 0 && fabsf(xr - urj) > r * c.scale[lev]) continue;
-        const uint4 c0 = S.desc[2 * j], c1 = S.desc[2 * j + 1];
-        const int dist = __popc(m0.x ^ c0.x) + __popc(m0.y ^ c0.y) + __popc(m0.z ^ c0.z) +
-                         __popc(m0.w ^ c0.w) + __popc(m1.x ^ c1.x) + __popc(m1.y ^ c1.y) +
-                         __popc(m1.z ^ c1.z) + __popc(m1.w ^ c1.w);
-        if (dist >= 256) continue;   // never below the initial 256 of either slot
-        t.cnt++;
-        // insert after every kept entry of distance <= dist (scan order breaks ties)
-        uint32_t v = (uint32_t)j | ((uint32_t)dist << 11) | ((uint32_t)oc << 20);
+  // octaves lev-1 and lev (bCheckLevels always holds: maxLevel = lev >= 0)
+  for (int L = max(lev - 1, 0); L <= lev; L++) {
+    const int id0 = L * kGridCols;
+    int k = S.lc_start[id0 + cx0];
+    const int kend = S.lc_start[id0 + cx1 + 1];
+    while (k < kend) {
+      const float4 R = S.rec[k++];
+      const uint32_t w = __float_as_uint(R.w);
+      const int row = (int)((w >> 11) & 63);
+      if (row < cy0 || row > cy1) continue;
+      if (!(fabsf(R.x - x) < rad && fabsf(R.y - y) < rad)) continue;
+      const int j = (int)(w & 2047);
+      if (is_claimed(S, j)) continue;
+      if (R.z > 0 && fabsf(xr - R.z) > rad) continue;
+      const uint4 c0 = S.desc[2 * j], c1 = S.desc[2 * j + 1];
+      const uint32_t dist = __popc(m0.x ^ c0.x) + __popc(m0.y ^ c0.y) + __popc(m0.z ^ c0.z) +
+                            __popc(m0.w ^ c0.w) + __popc(m1.x ^ c1.x) + __popc(m1.y ^ c1.y) +
+                            __popc(m1.z ^ c1.z) + __popc(m1.w ^ c1.w);
+      if (dist >= 256) continue;   // never below the initial 256 of either slot
+      cnt++;
+      // sorted insert: the list stays ascending in (distance, scan key)
+      uint32_t v = (dist << 23) | (w & 0x7FFFFFu);
 #pragma unroll
-        for (int k = 0; k < kTopK; k++) {
-          const uint32_t ek = t.e[k];
-          const bool take = ek == kEmpty || (int)((ek >> 11) & 511) > dist;
-          if (take) {
-            t.e[k] = v;
-            v = ek;
-          }
-          if (take && ek == kEmpty) break;
-        }
+      for (int q = 0; q < kTopK; q++) {
+        const uint32_t eq = t.e[q];
+        const bool lt = v < eq;
+        t.e[q] = lt ? v : eq;
+        v = lt ? eq : v;
       }
     }
+  }
+  if (cnt > kTopK) t.e[kTopK - 1] |= kMore;
   return t;
 }
 
@@ -222,7 +224,7 @@ __device__ __forceinline__ Top2 pick2(const LocalShared<KP>& S, const TopList& t
     if (ek == kEmpty || found == 2) continue;
     const int j = (int)(ek & 2047);
     if (is_claimed(S, j)) continue;
-    const int d = (int)((ek >> 11) & 511), l = (int)((ek >> 20) & 15);
+    const int d = (int)((ek >> 23) & 255), l = S.oct[j];
     if (found == 0) {
       r.bi = j; r.bd = d; r.bl = l;
     } else {
@@ -230,7 +232,8 @@ __device__ __forceinline__ Top2 pick2(const LocalShared<KP>& S, const TopList& t
     }
     found++;
   }
-  *full = found < 2 && t.cnt > kTopK;
+  const uint32_t last = t.e[kTopK - 1];
+  *full = found < 2 && last != kEmpty && (last & kMore);
   return r;
 }
 
@@ -263,94 +266,97 @@ __global__ void __launch_bounds__(kLocalThreads) k_match_local(TrackConsts c, Lo
   LocalShared<kLocalKp>& S = *reinterpret_cast<LocalShared<kLocalKp>*>(smem_local);
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
   const int n = min(a.n, kLocalKp);
-  // ---- grid (AssignFeaturesToGrid with PosInGrid, Frame.cc:265-287, 527-538) ----
-  for (int i = t; i < kCells; i += kLocalThreads) S.cell_start[i] = 0;
+#ifdef ORBPL_LOCAL_PROF
+  long long tp0 = wall_clock64(), tp1 = 0, tp2 = 0;
+#endif
+  // ---- keypoint index (AssignFeaturesToGrid with PosInGrid, Frame.cc:265-287, 527-538) ----
   for (int i = t; i < kLocalKp / 32; i += kLocalThreads) S.claimed[i] = 0;
   {
     const uint4* d = reinterpret_cast<const uint4*>(a.desc);
     for (int i = t; i < 2 * n; i += kLocalThreads) S.desc[i] = d[i];
   }
   __syncthreads();
-  for (int i = t; i < n; i += kLocalThreads) {
-    const KeyPointD k = a.kps_un[i];
-    S.xy[i] = make_float2(k.x, k.y);
-    S.oct[i] = (int8_t)k.octave;
-    S.ur[i] = a.uright[i];
-    S.mw[i] = -1;
-    S.own[i] = 0;
-    const int px = (int)roundf((k.x - c.minX) * c.gridInvW);
-    const int py = (int)roundf((k.y - c.minY) * c.gridInvH);
-    const int g = (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) ? -1 : px + kGridCols * py;
-    S.gc[i] = (int16_t)g;
-    if (g >= 0) atomicAdd(reinterpret_cast<unsigned int*>(&S.cell_start[g & ~1]), 1u << (16 * (g & 1)));
-    if (a.cur_nobs && a.cur_nobs[i] > 0) atomicOr(&S.claimed[i >> 5], 1u << (i & 31));
+  for (int i = t; i < kLocalKp; i += kLocalThreads) {
+    uint32_t key = kEmpty;
+    if (i < n) {
+      const KeyPointD k = a.kps_un[i];
+      S.oct[i] = (int8_t)k.octave;
+      S.mw[i] = -1;
+      S.own[i] = 0;
+      const int px = (int)roundf((k.x - c.minX) * c.gridInvW);
+      const int py = (int)roundf((k.y - c.minY) * c.gridInvH);
+      if (px >= 0 && px < kGridCols && py >= 0 && py < kGridRows && k.octave >= 0 &&
+          k.octave < kMaxLevelsT)
+        key = (uint32_t)k.octave << 23 | (uint32_t)px << 17 | (uint32_t)py << 11 | (uint32_t)i;
+      if (a.cur_nobs && a.cur_nobs[i] > 0) atomicOr(&S.claimed[i >> 5], 1u << (i & 31));
+    }
+    S.skey[i] = key;
   }
   __syncthreads();
-  {
-    constexpr int kPer = kCells / kLocalThreads;
-    static_assert(kCells % kLocalThreads == 0, "cells per thread");
-    int loc[kPer];
-    int sum = 0;
-#pragma unroll
-    for (int k = 0; k < kPer; k++) {
-      loc[k] = S.cell_start[t * kPer + k];
-      sum += loc[k];
-    }
-    int incl = sum;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int u = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += u;
-    }
-    if (lane == 63) S.wsum[wave] = incl;
-    __syncthreads();
-    int base = 0;
-    for (int w = 0; w < wave; w++) base += S.wsum[w];
-    int run = base + incl - sum;
-#pragma unroll
-    for (int k = 0; k < kPer; k++) {
-      S.cell_start[t * kPer + k] = (uint16_t)run;
-      S.fill[t * kPer + k] = (uint16_t)run;
-      run += loc[k];
-    }
-    if (t == kLocalThreads - 1) S.cell_start[kCells] = (uint16_t)run;
-    __syncthreads();
-  }
-  for (int i = t; i < n; i += kLocalThreads) {
-    const int g = S.gc[i];
-    if (g >= 0) {
-      // 16-bit fill counters packed in pairs: add to the word, take this half
-      const unsigned int sh = 16 * (g & 1);
-      const unsigned int old =
-          atomicAdd(reinterpret_cast<unsigned int*>(&S.fill[g & ~1]), 1u << sh);
-      S.items[(old >> sh) & 0xFFFFu] = (uint16_t)i;
-    }
-  }
-  __syncthreads();
-  for (int cell = t; cell < kCells; cell += kLocalThreads) {
-    const int b = S.cell_start[cell], e = S.cell_start[cell + 1];
-    for (int q = b + 1; q < e; q++) {
-      const uint16_t v = S.items[q];
-      int r = q - 1;
-      while (r >= b && S.items[r] > v) {
-        S.items[r + 1] = S.items[r];
-        r--;
+  // bitonic sort of the keys (the padding sorts last)
+  for (int size = 2; size <= kLocalKp; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int p = t; p < kLocalKp / 2; p += kLocalThreads) {
+        const int lo = 2 * p - (p & (stride - 1)), hi = lo + stride;
+        const uint32_t u = S.skey[lo], v = S.skey[hi];
+        if ((u > v) == ((lo & size) == 0)) {
+          S.skey[lo] = v;
+          S.skey[hi] = u;
+        }
       }
-      S.items[r + 1] = v;
+      __syncthreads();
+    }
+  for (int k = t; k < kLocalKp; k += kLocalThreads) {
+    const uint32_t key = S.skey[k];
+    const int cur = key == kEmpty ? kLevelCols : (int)(key >> 17);
+    const int prev = k == 0 ? -1 : (S.skey[k - 1] == kEmpty ? kLevelCols : (int)(S.skey[k - 1] >> 17));
+    for (int id = prev + 1; id <= cur; id++) S.lc_start[id] = (uint16_t)k;
+    if (k == kLocalKp - 1)
+      for (int id = cur + 1; id <= kLevelCols; id++) S.lc_start[id] = (uint16_t)kLocalKp;
+    if (key != kEmpty) {
+      const int j = (int)(key & 2047);
+      const KeyPointD kp = a.kps_un[j];
+      S.rec[k] = make_float4(kp.x, kp.y, a.uright[j], __uint_as_float(key & 0x7FFFFFu));
     }
   }
   __syncthreads();
-  // ---- phase A ----
-  for (int i = t; i < a.nmp; i += kLocalThreads) {
-    TopList r;
-#pragma unroll
-    for (int k = 0; k < kTopK; k++) r.e[k] = kEmpty;
-    r.cnt = 0;
-    if (a.in_view[i]) r = local_scan(S, c, a, i);
-    a.scratch[i] = make_int4((int)(r.e[0] | ((uint32_t)min(r.cnt, 255) << 24)), (int)r.e[1],
-                             (int)r.e[2], (int)r.e[3]);
+#ifdef ORBPL_LOCAL_PROF
+  tp1 = wall_clock64();
+#endif
+  // ---- phase A: windows of in-view map points, grouped by predicted level
+  // (similar scan lengths per wave) ----
+  constexpr int kList = 4 * kLocalKp;
+  for (int base = 0; base < a.nmp; base += kList) {
+    const int m = min(kList, a.nmp - base);
+    if (t < kMaxLevelsT) S.lvl_cnt[t] = 0;
+    __syncthreads();
+    for (int i = t; i < m; i += kLocalThreads)
+      if (a.in_view[base + i]) atomicAdd(&S.lvl_cnt[a.level[base + i]], 1);
+    __syncthreads();
+    if (t == 0) {
+      int run = 0;
+      for (int l = 0; l < kMaxLevelsT; l++) {
+        S.lvl_pos[l] = run;
+        run += S.lvl_cnt[l];
+      }
+      S.lvl_cnt[0] = run;   // the window's in-view count
+    }
+    __syncthreads();
+    const int nlist = S.lvl_cnt[0];
+    for (int i = t; i < m; i += kLocalThreads)
+      if (a.in_view[base + i]) S.list[atomicAdd(&S.lvl_pos[a.level[base + i]], 1)] = (uint16_t)i;
+    __syncthreads();
+    for (int p = t; p < nlist; p += kLocalThreads) {
+      const int i = base + S.list[p];
+      const TopList r = local_scan(S, c, a, i);
+      a.scratch[i] = make_int4((int)r.e[0], (int)r.e[1], (int)r.e[2], (int)r.e[3]);
+    }
+    __syncthreads();
   }
-  __syncthreads();
+#ifdef ORBPL_LOCAL_PROF
+  tp2 = wall_clock64();
+  int prof_rounds = 0, prof_rescans = 0;
+#endif
   // ---- phase B (wave 0, map point order) ----
   // Rounds over a chunk of 64 map points. A lane whose best or second
   // candidate was claimed by a committed point rescans against the committed
@@ -367,11 +373,9 @@ __global__ void __launch_bounds__(kLocalThreads) k_match_local(TrackConsts c, Lo
       TopList lst;
 #pragma unroll
       for (int k = 0; k < kTopK; k++) lst.e[k] = kEmpty;
-      lst.cnt = 0;
-      if (i < a.nmp) {
+      if (i < a.nmp && a.in_view[i]) {
         const int4 v = a.scratch[i];
-        lst.e[0] = (uint32_t)v.x & kEmpty;
-        lst.cnt = (int)((uint32_t)v.x >> 24);
+        lst.e[0] = (uint32_t)v.x;
         lst.e[1] = (uint32_t)v.y;
         lst.e[2] = (uint32_t)v.z;
         lst.e[3] = (uint32_t)v.w;
@@ -387,12 +391,18 @@ __global__ void __launch_bounds__(kLocalThreads) k_match_local(TrackConsts c, Lo
       bool decided = !(i < a.nmp && r.bi >= 0);
       while (true) {
         round++;
+#ifdef ORBPL_LOCAL_PROF
+        prof_rounds++;
+#endif
         const bool stale = !decided && (is_claimed(S, r.bi) || (r.si >= 0 && is_claimed(S, r.si)));
         if (stale) {
           // the pair under the committed claims: from the kept list, or a new
           // scan when the list runs out
           r = pick2(S, lst, &full);
           if (full) {
+#ifdef ORBPL_LOCAL_PROF
+            prof_rescans++;
+#endif
             lst = local_scan(S, c, a, i);
             r = pick2(S, lst, &full);
           }
@@ -431,6 +441,14 @@ __global__ void __launch_bounds__(kLocalThreads) k_match_local(TrackConsts c, Lo
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
     if (lane == 0) *a.nmatches = acc;
+#ifdef ORBPL_LOCAL_PROF
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) prof_rescans += __shfl_xor(prof_rescans, o, 64);
+    if (lane == 0 && blockIdx.x % 128 == 0)
+      printf("local blk %d n %d nmp %d grid %lld A %lld B %lld rounds %d rescans %d acc %d\n",
+             (int)blockIdx.x, n, a.nmp, tp1 - tp0, tp2 - tp1, wall_clock64() - tp2, prof_rounds,
+             prof_rescans, acc);
+#endif
   }
   __syncthreads();
   for (int i = t; i < n; i += kLocalThreads) a.match[i] = S.mw[i];

@@ -474,6 +474,33 @@ def test_search_by_projection_local_bit_exact(orbpl, oracle, th, nnratio, claims
     assert np.array_equal(m_g, m_o), np.nonzero(m_g != m_o)[0][:5]
 
 
+def test_search_by_projection_local_many_points_bit_exact(orbpl, oracle):
+    """More map points than one in-view window of k_match_local holds (4 x the
+    keypoint capacity): the map tiled three times with a few descriptor bits
+    flipped per copy, so copies compete for the same keypoints."""
+    from _scenes import local_map_problem
+    cfg, cam_o, sc, mps, cur, cur_nobs, T3 = local_map_problem(4)
+    rng = np.random.default_rng(7)
+    tiles = []
+    for k in range(3):
+        d = mps["desc"].copy()
+        if k:
+            flip = rng.integers(0, 256, (len(d), 2))
+            for c in range(2):
+                d[np.arange(len(d)), flip[:, c] // 8] ^= (1 << (flip[:, c] % 8)).astype(np.uint8)
+        tiles.append(d)
+    big = {key: np.concatenate([v] * 3) for key, v in mps.items()}
+    big["desc"] = np.concatenate(tiles)
+    assert len(big["xyz"]) > 4 * 1024
+    track = oracle.frame_is_in_frustum(cam_o, _log_scale(oracle), 8, T3, big, 0.5)
+    m_o, n_o = oracle.search_by_projection_local(cam_o, sc, cur, track, big["desc"], big["nobs"],
+                                                 cur_nobs, 3.0, 0.8)
+    m_g, n_g = orbpl.ORBmatcher(0.8).SearchByProjectionLocalMap(
+        orbpl.make_camera(cfg), sc, cur, track, big["desc"], big["nobs"], cur_nobs, 3.0)
+    assert n_g == n_o and n_o > 100
+    assert np.array_equal(m_g, m_o), np.nonzero(m_g != m_o)[0][:5]
+
+
 @pytest.mark.parametrize("case", ["local_map", "ref_kf", "retry"])
 def test_line_search_by_projection_list_bit_exact(orbpl, oracle, case):
     from _scenes import line_map_problem
