@@ -148,6 +148,15 @@ __device__ __forceinline__ int hamming32l(const uint8_t* a, const uint8_t* b) {
          __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
 }
 
+// the wave's LDS operations so far are complete and the compiler moves no
+// memory access across (one wave: LDS executes its operations in order). Unlike
+// a workgroup fence it does not wait for the wave's outstanding global loads
+// (phase B's next-chunk prefetch).
+__device__ __forceinline__ void lds_wave_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
 template <int KP>
 __device__ __forceinline__ bool is_claimed(const LocalShared<KP>& S, int j) {
   return (S.claimed[j >> 5] >> (j & 31)) & 1u;
@@ -216,21 +225,30 @@ __device__ TopList local_scan(const LocalShared<KP>& S, const TrackConsts& c, co
 // two unclaimed entries while candidates beyond the kept ones exist)
 template <int KP>
 __device__ __forceinline__ Top2 pick2(const LocalShared<KP>& S, const TopList& t, bool* full) {
+  // the claim words and octaves of all entries first (independent LDS reads,
+  // one round trip), then the choice in registers
+  uint32_t cw[kTopK];
+  int ol[kTopK];
+#pragma unroll
+  for (int k = 0; k < kTopK; k++) {
+    const int j = t.e[k] == kEmpty ? 0 : (int)(t.e[k] & 2047);
+    cw[k] = S.claimed[j >> 5];
+    ol[k] = S.oct[j];
+  }
   Top2 r{256, -1, -1, 256, -1, -1};
   int found = 0;
 #pragma unroll
   for (int k = 0; k < kTopK; k++) {
     const uint32_t ek = t.e[k];
-    if (ek == kEmpty || found == 2) continue;
     const int j = (int)(ek & 2047);
-    if (is_claimed(S, j)) continue;
-    const int d = (int)((ek >> 23) & 255), l = S.oct[j];
-    if (found == 0) {
-      r.bi = j; r.bd = d; r.bl = l;
-    } else {
-      r.si = j; r.sd = d; r.sl = l;
+    const bool use = ek != kEmpty && found < 2 && !((cw[k] >> (j & 31)) & 1u);
+    const int d = (int)((ek >> 23) & 255);
+    if (use && found == 0) {
+      r.bi = j; r.bd = d; r.bl = ol[k];
+    } else if (use) {
+      r.si = j; r.sd = d; r.sl = ol[k];
     }
-    found++;
+    found += use;
   }
   const uint32_t last = t.e[kTopK - 1];
   *full = found < 2 && last != kEmpty && (last & kMore);
@@ -368,17 +386,31 @@ __global__ void __launch_bounds__(kLocalThreads) k_match_local(TrackConsts c, Lo
   // every lane's committed outcome the one of the sequential loop.
   if (wave == 0) {
     int acc = 0, round = 0;
+    // the next chunk's lists, in-view flags and Observations() are loaded one
+    // chunk ahead (their latency overlaps the current chunk's rounds)
+    int4 nv = make_int4(0, 0, 0, 0);
+    int nin = 0, nnobs = 0;
+    if (lane < a.nmp) {
+      nv = a.scratch[lane];
+      nin = a.in_view[lane];
+      nnobs = a.mp_nobs ? a.mp_nobs[lane] : 1;
+    }
     for (int base = 0; base < a.nmp; base += 64) {
       const int i = base + lane;
       TopList lst;
 #pragma unroll
       for (int k = 0; k < kTopK; k++) lst.e[k] = kEmpty;
-      if (i < a.nmp && a.in_view[i]) {
-        const int4 v = a.scratch[i];
-        lst.e[0] = (uint32_t)v.x;
-        lst.e[1] = (uint32_t)v.y;
-        lst.e[2] = (uint32_t)v.z;
-        lst.e[3] = (uint32_t)v.w;
+      if (i < a.nmp && nin) {
+        lst.e[0] = (uint32_t)nv.x;
+        lst.e[1] = (uint32_t)nv.y;
+        lst.e[2] = (uint32_t)nv.z;
+        lst.e[3] = (uint32_t)nv.w;
+      }
+      const int nobs = i < a.nmp ? nnobs : 0;
+      if (i + 64 < a.nmp) {
+        nv = a.scratch[i + 64];
+        nin = a.in_view[i + 64];
+        nnobs = a.mp_nobs ? a.mp_nobs[i + 64] : 1;
       }
       // the pair under the claims of the earlier chunks
       bool full;
@@ -387,14 +419,14 @@ __global__ void __launch_bounds__(kLocalThreads) k_match_local(TrackConsts c, Lo
         lst = local_scan(S, c, a, i);
         r = pick2(S, lst, &full);
       }
-      const int nobs = i < a.nmp ? (a.mp_nobs ? a.mp_nobs[i] : 1) : 0;
       bool decided = !(i < a.nmp && r.bi >= 0);
       while (true) {
         round++;
 #ifdef ORBPL_LOCAL_PROF
         prof_rounds++;
 #endif
-        const bool stale = !decided && (is_claimed(S, r.bi) || (r.si >= 0 && is_claimed(S, r.si)));
+        const bool stale =
+            !decided && ((int)is_claimed(S, max(r.bi, 0)) | (int)(r.si >= 0 && is_claimed(S, max(r.si, 0))));
         if (stale) {
           // the pair under the committed claims: from the kept list, or a new
           // scan when the list runs out
@@ -412,17 +444,11 @@ __global__ void __launch_bounds__(kLocalThreads) k_match_local(TrackConsts c, Lo
         const bool claimer = accept && nobs > 0;
         const int key = (round << 6) | (63 - lane);
         if (claimer) atomicMax(&S.own[r.bi], key);
-        __threadfence_block();
-        __builtin_amdgcn_wave_barrier();
-        bool coll = false;
-        if (!decided) {
-          const int ob = S.own[r.bi];
-          coll = (ob >> 6) == round && 63 - (ob & 63) < lane;
-          if (r.si >= 0) {
-            const int os = S.own[r.si];
-            coll = coll || ((os >> 6) == round && 63 - (os & 63) < lane);
-          }
-        }
+        lds_wave_sync();
+        // both stamps read at once (index 0 stands in for a missing candidate)
+        const int ob = S.own[max(r.bi, 0)], os = S.own[max(r.si, 0)];
+        const bool coll = !decided && (((ob >> 6) == round && 63 - (ob & 63) < lane) ||
+                                       (r.si >= 0 && (os >> 6) == round && 63 - (os & 63) < lane));
         const unsigned long long cm = __ballot(coll);
         const int lc = cm ? __ffsll((long long)cm) - 1 : 64;
         if (!decided && lane < lc) {
@@ -434,8 +460,7 @@ __global__ void __launch_bounds__(kLocalThreads) k_match_local(TrackConsts c, Lo
           decided = true;
         }
         if (lc == 64) break;
-        __threadfence_block();
-        __builtin_amdgcn_wave_barrier();
+        lds_wave_sync();
       }
     }
 #pragma unroll

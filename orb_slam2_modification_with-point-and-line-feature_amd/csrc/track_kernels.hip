@@ -1357,6 +1357,9 @@ __global__ void __launch_bounds__(kPoseThreads, kMinWaves) k_pose(TrackConsts tc
           }
           qmax++;
         } while (rho < 0 && qmax < 10);
+#ifdef ORBPL_POSE_TRIALS
+        if (s == 0 && t == 0) printf("pose blk0 round %d it %d trials %d rho %g\n", round, it, qmax, rho);
+#endif
         if (qmax == 10 || rho == 0) break;
         if ((iniChi - currentChi) * 1e3 < iniChi) nBadLM++;
         else nBadLM = 0;

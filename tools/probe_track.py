@@ -1,6 +1,7 @@
 """Tracker probe (dev tool): per-stage device times of the points tracker on
 the bench's synthetic loop, plus stream 0's PoseOptimization phase profile
-when ORBPL_POSE_PROFILE is set. Usage: probe_track.py [streams] [pipelined]."""
+when ORBPL_POSE_PROFILE is set (the stream's last pose launch: TrackLocalMap's
+with local_map=1). Usage: probe_track.py [streams] [pipelined] [local_map]."""
 import ctypes as C
 import os
 import sys
@@ -19,13 +20,14 @@ import orbpl.synth as synth  # noqa: E402
 
 S = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 pipelined = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+local_map = int(sys.argv[3]) if len(sys.argv) > 3 else 0
 F = 32
 gray, depth = bench.render_loop(F, seed=1, workers=min(16, os.cpu_count() or 4))
 L = bench.Layout(synth.loop_trajectory(F, seed=1))
 rep = L.replicated(S)
 d_gray = pkg.DeviceBuffer.from_array(gray[rep])
 d_depth = pkg.DeviceBuffer.from_array(depth[rep])
-tr = pkg.Tracker(pkg.OrbParams(*bench.ORB), pkg.make_camera(synth.TUM1), S)
+tr = pkg.Tracker(pkg.OrbParams(*bench.ORB), pkg.make_camera(synth.TUM1), S, local_map=bool(local_map))
 tr.set_pipelined(bool(pipelined))
 tr.reset(np.stack([np.linalg.inv(L.Twc(s, 0)).astype(np.float32) for s in range(S)]).reshape(S, 16))
 fb, db = 640 * 480, 640 * 480 * 4
