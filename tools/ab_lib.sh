@@ -1,0 +1,21 @@
+#!/bin/bash
+# Headline bench A/B over libraries and settings: each item of $1 is
+# "<variant>[:NAME=VALUE]" (variant "cur" = the in-tree library, else
+# variants/<variant>/liborbpl.so); stream counts in $2 (default 256); $3 rounds.
+set -o pipefail
+mkdir -p gpurun_out/ab
+IT=${1:-cur}
+SS=${2:-256}
+RN=${3:-2}
+B="--no-cpu-baseline --no-parity --sweep 0 --secondary-steps 0 --stereo-steps 0 --rig-steps 0 --ingress-steps 0 --isolated-steps 0"
+for r in $(seq 1 $RN); do
+  for s in $SS; do
+    for it in $IT; do
+      v=${it%%:*}; e=""; [ "$it" != "$v" ] && e=${it#*:}
+      L=""; [ "$v" != cur ] && L=variants/$v/liborbpl.so
+      tag=$(echo "$it" | tr ':=,' '___')
+      env ORBPL_LIB=$L $e timeout -k 10 200 python bench.py --streams $s --steps 10 --warmup 3 $B > gpurun_out/ab/lib_${tag}_$s.log 2>&1 || { echo "fail $it $s"; tail -5 gpurun_out/ab/lib_${tag}_$s.log; exit 1; }
+      grep '^{' gpurun_out/ab/lib_${tag}_$s.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$it', $s, round(d['value']), d['ms_per_step'])"
+    done
+  done
+done
