@@ -243,10 +243,13 @@ __device__ int scan_best(const SH& S, const TrackConsts& c, const ProjInfo& p,
 }
 
 constexpr int kTopK = 4;
-// k_match_last block size: one block per stream, so the stream count bounds the
-// grid; 1024 threads put all last-frame map points of a stream in one round
+// k_match_last block size: one block per stream. The kernel takes up to
+// kMatchThreads; it launches with kMatchLaunchThreads: in pipelined tracking it
+// shares the CUs with the next batch's extraction, and a 4-wave workgroup is
+// placed as soon as one extraction workgroup retires where a 16-wave one waits
+// for a CU to drain (256 streams: 97.1k frames/s at 256 threads, 91.2k at 1024)
 constexpr int kMatchThreads = 1024;
-static_assert((kGridCols * kGridRows) % kMatchThreads == 0, "cell scan split");
+constexpr int kMatchLaunchThreads = 256;
 
 template <int KMAX>
 struct MatchShared {
@@ -273,8 +276,9 @@ struct MatchShared {
 };
 static_assert(kMatchMaxKp * kTopK >= kGridCols * kGridRows, "top[] doubles as cell fill counters");
 
-template <int KMAX>
-__global__ void __launch_bounds__(kMatchThreads) k_match_last(TrackConsts c, MatchArgs a) {
+template <int KMAX, int NT>
+__global__ void __launch_bounds__(NT) k_match_last(TrackConsts c, MatchArgs a) {
+  static_assert((kGridCols * kGridRows) % NT == 0 && NT <= kMatchThreads, "cell scan split");
   extern __shared__ char smem_raw[];
   MatchShared<KMAX>& S = *reinterpret_cast<MatchShared<KMAX>*>(smem_raw);
   const int s = blockIdx.x, t = threadIdx.x;
@@ -291,7 +295,7 @@ __global__ void __launch_bounds__(kMatchThreads) k_match_last(TrackConsts c, Mat
   };
   if (a.active && !a.active[s].has_last) {
     if (t == 0) a.nmatches[(long long)s * a.nm_stride] = 0;
-    for (int i = t; i < a.cur_n[s]; i += kMatchThreads) a.match[(long long)s * a.kp_pitch + i] = -1;
+    for (int i = t; i < a.cur_n[s]; i += NT) a.match[(long long)s * a.kp_pitch + i] = -1;
     return;
   }
   const int n = min(a.cur_n[s], KMAX);
@@ -302,9 +306,9 @@ __global__ void __launch_bounds__(kMatchThreads) k_match_last(TrackConsts c, Mat
   const float* Tc = a.Tcw + (long long)s * a.pose_stride;
   const float* Tl = a.Tlw + (long long)s * a.pose_stride;
   // ---- current frame into LDS + grid (AssignFeaturesToGrid, Frame.cc:265-287) ----
-  for (int i = t; i < kGridCols * kGridRows; i += kMatchThreads) S.cell_start[i] = 0;
+  for (int i = t; i < kGridCols * kGridRows; i += NT) S.cell_start[i] = 0;
   __syncthreads();
-  for (int i = t; i < n; i += kMatchThreads) {
+  for (int i = t; i < n; i += NT) {
     const KeyPointD k = ck[i];
     S.xy[i] = make_float2(k.x, k.y);
     S.ang[i] = k.angle;
@@ -329,7 +333,7 @@ __global__ void __launch_bounds__(kMatchThreads) k_match_last(TrackConsts c, Mat
   }
   __syncthreads();
   {  // exclusive scan of the 3072 cell counts (kPer per thread)
-    constexpr int kPer = (kGridCols * kGridRows) / kMatchThreads;
+    constexpr int kPer = (kGridCols * kGridRows) / NT;
     int loc[kPer];
     int sum = 0;
 #pragma unroll
@@ -354,17 +358,17 @@ __global__ void __launch_bounds__(kMatchThreads) k_match_last(TrackConsts c, Mat
       S.top[t * kPer + k] = run;  // fill counter
       run += loc[k];
     }
-    if (t == kMatchThreads - 1) S.cell_start[kGridCols * kGridRows] = run;
+    if (t == NT - 1) S.cell_start[kGridCols * kGridRows] = run;
     __syncthreads();
   }
   // place items (any order), then sort each cell by index: the reference's
   // mGrid[ix][iy] vectors hold indices in increasing order
-  for (int i = t; i < n; i += kMatchThreads) {
+  for (int i = t; i < n; i += NT) {
     const int g = S.gc[i];
     if (g >= 0) S.items[atomicAdd(&S.top[g], 1)] = (uint16_t)i;
   }
   __syncthreads();
-  for (int cell = t; cell < kGridCols * kGridRows; cell += kMatchThreads) {
+  for (int cell = t; cell < kGridCols * kGridRows; cell += NT) {
     const int b = S.cell_start[cell], e = S.cell_start[cell + 1];
     for (int q = b + 1; q < e; q++) {
       const uint16_t v = S.items[q];
@@ -390,7 +394,7 @@ __global__ void __launch_bounds__(kMatchThreads) k_match_last(TrackConsts c, Mat
   for (int attempt = 0; attempt < 2; attempt++) {
     // ---- phase A: per map point, the first kTopK candidates with distance
     // <= TH_HIGH in (distance, scan order), and how many such candidates exist
-    for (int i = t; i < nl; i += kMatchThreads) {
+    for (int i = t; i < nl; i += NT) {
       int tk[kTopK] = {-1, -1, -1, -1};
       int cnt = 0;
       const long long li = cb + i;
@@ -447,11 +451,11 @@ __global__ void __launch_bounds__(kMatchThreads) k_match_last(TrackConsts c, Mat
       for (int q2 = 0; q2 < kTopK; q2++) S.top[i * kTopK + q2] = tk[q2];
       S.ntop[i] = (uint8_t)min(cnt, 255);
     }
-    for (int i = t; i < n; i += kMatchThreads) {
+    for (int i = t; i < n; i += NT) {
       S.mpw[i] = -1;
       S.fc[i] = 0x7fffffff;
     }
-    for (int i = t; i < KMAX / 32; i += kMatchThreads) {
+    for (int i = t; i < KMAX / 32; i += NT) {
       S.claimed[i] = 0;
       S.removed[i] = 0;
     }
@@ -548,7 +552,7 @@ __global__ void __launch_bounds__(kMatchThreads) k_match_last(TrackConsts c, Mat
     nmatches = S.misc[0];
     // ---- phase C: rotation consistency (ORBmatcher.cc:1850-1876, 2035-2077) ----
     if (a.check_ori) {
-      for (int i = t; i < nl; i += kMatchThreads)
+      for (int i = t; i < nl; i += NT)
         if (S.bin[i] >= 0) atomicAdd(&S.hist[S.bin[i]], 1);
       __syncthreads();
       if (t == 0) {
@@ -574,7 +578,7 @@ __global__ void __launch_bounds__(kMatchThreads) k_match_last(TrackConsts c, Mat
       __syncthreads();
       const int ind1 = S.misc[1], ind2 = S.misc[2], ind3 = S.misc[3];
       int nrem = 0;
-      for (int i = t; i < nl; i += kMatchThreads) {
+      for (int i = t; i < nl; i += NT) {
         const int b = S.bin[i];
         if (b >= 0 && b != ind1 && b != ind2 && b != ind3) {
           const int k = S.sel[i];
@@ -591,7 +595,7 @@ __global__ void __launch_bounds__(kMatchThreads) k_match_last(TrackConsts c, Mat
     th = 2 * a.th;
     __syncthreads();
   }
-  for (int i = t; i < n; i += kMatchThreads) {
+  for (int i = t; i < n; i += NT) {
     int m = S.mpw[i];
     if (a.check_ori && ((S.removed[i >> 5] >> (i & 31)) & 1u)) m = -1;
     a.match[cb + i] = m;
@@ -1593,8 +1597,6 @@ void launch_predict(StreamState* st, int nstreams, hipStream_t s) {
 }
 
 void launch_match_last(const TrackConsts& c, const MatchLaunch& m, int nstreams, hipStream_t s) {
-  set_smem_attr((const void*)k_match_last<1024>, sizeof(MatchShared<1024>));
-  set_smem_attr((const void*)k_match_last<2048>, sizeof(MatchShared<2048>));
   MatchArgs a;
   a.cur_kps_un = m.cur_kps_un;
   a.cur_desc = m.cur_desc;
@@ -1622,12 +1624,28 @@ void launch_match_last(const TrackConsts& c, const MatchLaunch& m, int nstreams,
   a.active = m.active;
   static const int prof = getenv("ORBPL_MATCH_PROFILE") ? 1 : 0;
   a.prof = prof;
-  if (m.kp_pitch <= 1024)
-    hipLaunchKernelGGL(k_match_last<1024>, dim3(nstreams), dim3(kMatchThreads), sizeof(MatchShared<1024>), s,
-                       c, a);
-  else
-    hipLaunchKernelGGL(k_match_last<2048>, dim3(nstreams), dim3(kMatchThreads), sizeof(MatchShared<2048>), s,
-                       c, a);
+  // threads per frame (ORBPL_MATCH_NT overrides, A/B runs)
+  static const char* nt_env = getenv("ORBPL_MATCH_NT");
+  const int nt = nt_env ? atoi(nt_env) : kMatchLaunchThreads;
+#define ORBPL_MATCH_LAUNCH(KM, NTH)                                                          \
+  if ((KM == 1024) == (m.kp_pitch <= 1024) && nt == NTH) {                                   \
+    set_smem_attr((const void*)k_match_last<KM, NTH>, sizeof(MatchShared<KM>));             \
+    hipLaunchKernelGGL((k_match_last<KM, NTH>), dim3(nstreams), dim3(NTH),                  \
+                       sizeof(MatchShared<KM>), s, c, a);                                    \
+    return;                                                                                  \
+  }
+  ORBPL_MATCH_LAUNCH(1024, 1024)
+  ORBPL_MATCH_LAUNCH(1024, 512)
+  ORBPL_MATCH_LAUNCH(1024, 256)
+  ORBPL_MATCH_LAUNCH(1024, 128)
+  ORBPL_MATCH_LAUNCH(2048, 1024)
+  ORBPL_MATCH_LAUNCH(2048, 512)
+  ORBPL_MATCH_LAUNCH(2048, 256)
+  ORBPL_MATCH_LAUNCH(2048, 128)
+#undef ORBPL_MATCH_LAUNCH
+  set_smem_attr((const void*)k_match_last<2048, 1024>, sizeof(MatchShared<2048>));
+  hipLaunchKernelGGL((k_match_last<2048, 1024>), dim3(nstreams), dim3(1024), sizeof(MatchShared<2048>), s,
+                     c, a);
 }
 
 int read_match_profile(long long* out8) {
