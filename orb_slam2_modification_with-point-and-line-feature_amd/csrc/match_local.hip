@@ -21,6 +21,8 @@
 //                     keypoint wins, as F.mvpMapPoints[bestIdx] = pMP does
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "lsd_math.h"
 #include "track_common.h"
 #include "track_kernels.h"
@@ -90,7 +92,7 @@ __global__ void __launch_bounds__(256) k_in_frustum(TrackConsts c, float log_sca
 
 namespace {
 
-constexpr int kLocalThreads = 1024;   // 16 waves: the index build and phase A; wave 0 runs phase B
+constexpr int kLocalThreads = 1024;   // widest build: the index build and phase A; wave 0 runs phase B
 constexpr int kLevelCols = kMaxLevelsT * kGridCols;   // (octave, grid column) ranges
 
 // The current frame's keypoints in LDS for up to kLocalKp keypoints: 140 KB at
@@ -257,8 +259,8 @@ __device__ __forceinline__ Top2 pick2(const LocalShared<KP>& S, const TopList& t
 
 }  // namespace
 
-template <int kLocalKp>
-__global__ void __launch_bounds__(kLocalThreads) k_match_local(TrackConsts c, LocalArgs a) {
+template <int kLocalKp, int NT>
+__global__ void __launch_bounds__(NT) k_match_local(TrackConsts c, LocalArgs a) {
   if (a.n_arr) {  // batched: stream blockIdx.x
     const int b = blockIdx.x;
     const long long ko = (long long)b * a.kp_pitch, mo = (long long)b * a.mp_pitch;
@@ -288,13 +290,13 @@ __global__ void __launch_bounds__(kLocalThreads) k_match_local(TrackConsts c, Lo
   long long tp0 = wall_clock64(), tp1 = 0, tp2 = 0;
 #endif
   // ---- keypoint index (AssignFeaturesToGrid with PosInGrid, Frame.cc:265-287, 527-538) ----
-  for (int i = t; i < kLocalKp / 32; i += kLocalThreads) S.claimed[i] = 0;
+  for (int i = t; i < kLocalKp / 32; i += NT) S.claimed[i] = 0;
   {
     const uint4* d = reinterpret_cast<const uint4*>(a.desc);
-    for (int i = t; i < 2 * n; i += kLocalThreads) S.desc[i] = d[i];
+    for (int i = t; i < 2 * n; i += NT) S.desc[i] = d[i];
   }
   __syncthreads();
-  for (int i = t; i < kLocalKp; i += kLocalThreads) {
+  for (int i = t; i < kLocalKp; i += NT) {
     uint32_t key = kEmpty;
     if (i < n) {
       const KeyPointD k = a.kps_un[i];
@@ -314,7 +316,7 @@ __global__ void __launch_bounds__(kLocalThreads) k_match_local(TrackConsts c, Lo
   // bitonic sort of the keys (the padding sorts last)
   for (int size = 2; size <= kLocalKp; size <<= 1)
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int p = t; p < kLocalKp / 2; p += kLocalThreads) {
+      for (int p = t; p < kLocalKp / 2; p += NT) {
         const int lo = 2 * p - (p & (stride - 1)), hi = lo + stride;
         const uint32_t u = S.skey[lo], v = S.skey[hi];
         if ((u > v) == ((lo & size) == 0)) {
@@ -324,7 +326,7 @@ __global__ void __launch_bounds__(kLocalThreads) k_match_local(TrackConsts c, Lo
       }
       __syncthreads();
     }
-  for (int k = t; k < kLocalKp; k += kLocalThreads) {
+  for (int k = t; k < kLocalKp; k += NT) {
     const uint32_t key = S.skey[k];
     const int cur = key == kEmpty ? kLevelCols : (int)(key >> 17);
     const int prev = k == 0 ? -1 : (S.skey[k - 1] == kEmpty ? kLevelCols : (int)(S.skey[k - 1] >> 17));
@@ -348,7 +350,7 @@ __global__ void __launch_bounds__(kLocalThreads) k_match_local(TrackConsts c, Lo
     const int m = min(kList, a.nmp - base);
     if (t < kMaxLevelsT) S.lvl_cnt[t] = 0;
     __syncthreads();
-    for (int i = t; i < m; i += kLocalThreads)
+    for (int i = t; i < m; i += NT)
       if (a.in_view[base + i]) atomicAdd(&S.lvl_cnt[a.level[base + i]], 1);
     __syncthreads();
     if (t == 0) {
@@ -361,10 +363,10 @@ __global__ void __launch_bounds__(kLocalThreads) k_match_local(TrackConsts c, Lo
     }
     __syncthreads();
     const int nlist = S.lvl_cnt[0];
-    for (int i = t; i < m; i += kLocalThreads)
+    for (int i = t; i < m; i += NT)
       if (a.in_view[base + i]) S.list[atomicAdd(&S.lvl_pos[a.level[base + i]], 1)] = (uint16_t)i;
     __syncthreads();
-    for (int p = t; p < nlist; p += kLocalThreads) {
+    for (int p = t; p < nlist; p += NT) {
       const int i = base + S.list[p];
       const TopList r = local_scan(S, c, a, i);
       a.scratch[i] = make_int4((int)r.e[0], (int)r.e[1], (int)r.e[2], (int)r.e[3]);
@@ -476,7 +478,7 @@ __global__ void __launch_bounds__(kLocalThreads) k_match_local(TrackConsts c, Lo
 #endif
   }
   __syncthreads();
-  for (int i = t; i < n; i += kLocalThreads) a.match[i] = S.mw[i];
+  for (int i = t; i < n; i += NT) a.match[i] = S.mw[i];
 }
 
 void launch_in_frustum(const TrackConsts& c, float log_scale, const InFrustumArgs& a,
@@ -489,15 +491,30 @@ void launch_in_frustum(const TrackConsts& c, float log_scale, const InFrustumArg
 
 void launch_match_local(const TrackConsts& c, const LocalArgs& a, hipStream_t s, int nstreams) {
   const int cap = a.n_arr ? a.kp_pitch : a.n;   // keypoints a frame can hold
-  if (cap <= 1024) {
-    set_smem_attr((const void*)k_match_local<1024>, sizeof(LocalShared<1024>));
-    hipLaunchKernelGGL(k_match_local<1024>, dim3(a.n_arr ? nstreams : 1), dim3(kLocalThreads),
-                       sizeof(LocalShared<1024>), s, c, a);
-    return;
+  // threads per frame: narrower workgroups are placed sooner beside the next
+  // batch's extraction and pack more frames per CU once frames outnumber CUs
+  // (256 / 1024 streams: 512 threads 98.2k / 116.9k frames/s, 256 threads
+  // 97.6k / 120.8k, 1024 threads 97.2k / 114.3k). ORBPL_LOCAL_NT overrides.
+  static const char* nt_env = getenv("ORBPL_LOCAL_NT");
+  int nt = nstreams > device_cu_count() ? 256 : 512;
+  if (nt_env) nt = atoi(nt_env);
+#define ORBPL_LOCAL_LAUNCH(KP, NTH)                                                              \
+  if ((KP == 1024) == (cap <= 1024) && nt == NTH) {                                             \
+    set_smem_attr((const void*)k_match_local<KP, NTH>, sizeof(LocalShared<KP>));               \
+    hipLaunchKernelGGL((k_match_local<KP, NTH>), dim3(a.n_arr ? nstreams : 1), dim3(NTH),      \
+                       sizeof(LocalShared<KP>), s, c, a);                                       \
+    return;                                                                                     \
   }
-  set_smem_attr((const void*)k_match_local<2048>, sizeof(LocalShared<2048>));
-  hipLaunchKernelGGL(k_match_local<2048>, dim3(a.n_arr ? nstreams : 1), dim3(kLocalThreads), sizeof(LocalShared<2048>), s,
-                     c, a);
+  ORBPL_LOCAL_LAUNCH(1024, 1024)
+  ORBPL_LOCAL_LAUNCH(1024, 512)
+  ORBPL_LOCAL_LAUNCH(1024, 256)
+  ORBPL_LOCAL_LAUNCH(2048, 1024)
+  ORBPL_LOCAL_LAUNCH(2048, 512)
+  ORBPL_LOCAL_LAUNCH(2048, 256)
+#undef ORBPL_LOCAL_LAUNCH
+  set_smem_attr((const void*)k_match_local<2048, 1024>, sizeof(LocalShared<2048>));
+  hipLaunchKernelGGL((k_match_local<2048, 1024>), dim3(a.n_arr ? nstreams : 1), dim3(1024),
+                     sizeof(LocalShared<2048>), s, c, a);
 }
 
 
