@@ -512,8 +512,8 @@ void launch_match_local(const TrackConsts& c, const LocalArgs& a, hipStream_t s,
   ORBPL_LOCAL_LAUNCH(2048, 512)
   ORBPL_LOCAL_LAUNCH(2048, 256)
 #undef ORBPL_LOCAL_LAUNCH
-  set_smem_attr((const void*)k_match_local<2048, 1024>, sizeof(LocalShared<2048>));
-  hipLaunchKernelGGL((k_match_local<2048, 1024>), dim3(a.n_arr ? nstreams : 1), dim3(1024),
+  set_smem_attr((const void*)k_match_local<2048, kLocalThreads>, sizeof(LocalShared<2048>));
+  hipLaunchKernelGGL((k_match_local<2048, kLocalThreads>), dim3(a.n_arr ? nstreams : 1), dim3(kLocalThreads),
                      sizeof(LocalShared<2048>), s, c, a);
 }
 
@@ -554,7 +554,9 @@ struct BowShared {
   int s_n, s_ind[3];
 };
 
-__device__ void match_bow_body(const BowArgs& a, BowShared& B) {
+// fdl (LDS, 2 uint4 per feature, nf entries) stages the frame's descriptors:
+// the per-node loops compare against them from LDS instead of global memory.
+__device__ void match_bow_body(const BowArgs& a, BowShared& B, uint4* fdl) {
   uint32_t* skf = B.skf;
   uint32_t* sf = B.sf;
   int* smatch = B.smatch;
@@ -573,9 +575,17 @@ __device__ void match_bow_body(const BowArgs& a, BowShared& B) {
   }
   if (t < 32) hist[t] = 0;
   if (t == 0) s_n = 0;
+  if (fdl) {
+    const uint4* d = reinterpret_cast<const uint4*>(a.f_desc);
+    for (int i = t; i < 2 * nf; i += 256) fdl[i] = d[i];
+  }
   __syncthreads();
-  bitonic_sort(skf, kBowMax);
-  bitonic_sort(sf, kBowMax);
+  // the padding sorts last: sorting the next power of two above the counts
+  // leaves the same runs
+  int ns = 64;
+  while (ns < nkf || ns < nf) ns <<= 1;
+  bitonic_sort(skf, ns);
+  bitonic_sort(sf, ns);
   // one thread per keyframe node (first position of each node run)
   int nm = 0;
   for (int p = t; p < kBowMax; p += 256) {
@@ -598,11 +608,24 @@ __device__ void match_bow_body(const BowArgs& a, BowShared& B) {
     for (int q = p; q < kBowMax && skf[q] != 0xFFFFFFFFu && (skf[q] >> 11) == node; q++) {
       const int iKF = (int)(skf[q] & 0x7FF);
       if (!a.kf_valid[iKF]) continue;
+      const uint4* kd = reinterpret_cast<const uint4*>(a.kf_desc + (long long)iKF * 32);
+      const uint4 k0 = kd[0], k1 = kd[1];
       int bestDist1 = 256, bestIdxF = -1, bestDist2 = 256;
       for (int r = fb; r < fe; r++) {
         const int iF = (int)(sf[r] & 0x7FF);
         if (smatch[iF] >= 0) continue;
-        const int dist = hamming32l(a.kf_desc + (long long)iKF * 32, a.f_desc + (long long)iF * 32);
+        uint4 f0, f1;
+        if (fdl) {
+          f0 = fdl[2 * iF];
+          f1 = fdl[2 * iF + 1];
+        } else {
+          const uint4* fd = reinterpret_cast<const uint4*>(a.f_desc + (long long)iF * 32);
+          f0 = fd[0];
+          f1 = fd[1];
+        }
+        const int dist = __popc(k0.x ^ f0.x) + __popc(k0.y ^ f0.y) + __popc(k0.z ^ f0.z) +
+                         __popc(k0.w ^ f0.w) + __popc(k1.x ^ f1.x) + __popc(k1.y ^ f1.y) +
+                         __popc(k1.z ^ f1.z) + __popc(k1.w ^ f1.w);
         if (dist < bestDist1) {
           bestDist2 = bestDist1;
           bestDist1 = dist;
@@ -666,21 +689,28 @@ __device__ void match_bow_body(const BowArgs& a, BowShared& B) {
 
 __global__ void __launch_bounds__(256) k_match_bow(BowArgs a) {
   __shared__ BowShared B;
-  match_bow_body(a, B);
+  extern __shared__ uint4 bow_fdl[];
+  match_bow_body(a, B, bow_fdl);
 }
 
 void launch_match_bow(const BowArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_match_bow, dim3(1), dim3(256), 0, s, a);
+  const size_t smem = (size_t)2 * sizeof(uint4) * (size_t)min(max(a.nf, 0), kBowMax);
+  set_smem_attr((const void*)k_match_bow, sizeof(BowShared) + (size_t)2 * sizeof(uint4) * kBowMax);
+  hipLaunchKernelGGL(k_match_bow, dim3(1), dim3(256), smem, s, a);
 }
 
 // TrackReferenceKeyFrame's ORBmatcher(0.7, true).SearchByBoW(pKF, F)
 // (Tracking.cc:947-952) for every stream with st[s].trk: the last frame's
 // FeatureVector / map points / descriptors against the current frame's
-__global__ void __launch_bounds__(256) k_trk_bow(TrkArgs a) {
+// A persistent grid: workgroup g takes streams g, g + grid, ... (only the
+// few streams whose motion model failed have work; a workgroup per stream
+// would have every one of them placed beside the next batch's extraction).
+__global__ void __launch_bounds__(256) k_trk_bow(TrkArgs a, int nstreams) {
   __shared__ BowShared B;
-  const int s = blockIdx.x;
+  extern __shared__ uint4 trk_fdl[];
+  for (int s = blockIdx.x; s < nstreams; s += gridDim.x) {
   StreamState& S = a.st[s];
-  if (!S.trk) return;
+  if (!S.trk) continue;
   const long long cb = (long long)s * a.kp_pitch;
   BowArgs b;
   b.nkf = a.last_n[s];
@@ -698,11 +728,16 @@ __global__ void __launch_bounds__(256) k_trk_bow(TrkArgs a) {
   b.check_ori = 1;
   b.match = a.match + cb;
   b.nmatches = &S.nmatches;
-  match_bow_body(b, B);
+  match_bow_body(b, B, a.kp_pitch <= kBowMax ? trk_fdl : nullptr);
+  __syncthreads();   // B and trk_fdl are reused by the next stream
+  }
 }
 
 void launch_trk_bow(const TrkArgs& a, int nstreams, hipStream_t s) {
-  hipLaunchKernelGGL(k_trk_bow, dim3(nstreams), dim3(256), 0, s, a);
+  const size_t smem = a.kp_pitch <= kBowMax ? (size_t)2 * sizeof(uint4) * a.kp_pitch : 0;
+  set_smem_attr((const void*)k_trk_bow, sizeof(BowShared) + (size_t)2 * sizeof(uint4) * kBowMax);
+  const int grid = min(nstreams, 2 * device_cu_count());
+  hipLaunchKernelGGL(k_trk_bow, dim3(grid), dim3(256), smem, s, a, nstreams);
 }
 
 }  // namespace orbpl
