@@ -21,6 +21,16 @@
 
 namespace orbpl {
 
+// Scope of the seed loop's stamp loads / stores. One wave owns a frame's
+// stamps, and the CU's vector L1 is coherent for its own waves' stores and
+// atomics (the memory model's workgroup scope needs no L1 invalidation outside
+// tgsplit mode), so workgroup-scope loads may hit L1 where agent-scope ones
+// (sc1) went to L2 for every neighbourhood: 153.8 -> 140.7 ms per 3072 frames,
+// bit-exact (test_gpu_lsd). A/B builds override.
+#ifndef ORBPL_LSD_SCOPE
+#define ORBPL_LSD_SCOPE __HIP_MEMORY_SCOPE_WORKGROUP
+#endif
+
 namespace {
 
 constexpr double kPi = 3.14159265358979323846;
@@ -62,7 +72,7 @@ __device__ __forceinline__ uint32_t* sd_hi(uint64_t* sd, int idx) {
 __device__ __forceinline__ bool used_get(const Frame& F, int x, int y) {
   if (F.usd)
     return __hip_atomic_load(sd_hi(F.usd, lsd_sd_index(x, y, F.tw)), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT) == 0u;
+                             ORBPL_LSD_SCOPE) == 0u;
   const int i = y * F.sw + x;
   return (F.used[i >> 5] >> (i & 31)) & 1u;
 }
@@ -73,7 +83,7 @@ __device__ __forceinline__ void used_set(Frame& F, int x, int y, bool v) {
   if (F.usd) {
     if (F.lane == 0)
       __hip_atomic_store(sd_hi(F.usd, lsd_sd_index(x, y, F.tw)), v ? 0u : 0xFFFFFFFFu,
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                         __ATOMIC_RELAXED, ORBPL_LSD_SCOPE);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   } else if (F.lane == 0) {
     const uint32_t w = F.used[i >> 5], b = 1u << (i & 31);
@@ -625,10 +635,10 @@ __device__ __forceinline__ void wg_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ
 enum { kSpecConflict = -1, kSpecOverflow = -2, kSpecSmall = 0, kSpecFail = 1, kSpecCand = 2 };
 
 __device__ __forceinline__ uint32_t ld_stamp(uint64_t* sd, int idx) {
-  return __hip_atomic_load(sd_hi(sd, idx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __hip_atomic_load(sd_hi(sd, idx), __ATOMIC_RELAXED, ORBPL_LSD_SCOPE);
 }
 __device__ __forceinline__ uint64_t ld_sd(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, ORBPL_LSD_SCOPE);
 }
 __device__ __forceinline__ int pt_x(const uint4& e) { return (int)(e.x & 0xFFFF); }
 __device__ __forceinline__ int pt_y(const uint4& e) { return (int)(e.x >> 16); }
@@ -1320,7 +1330,7 @@ __global__ void __launch_bounds__(64, ORBPL_SPEC_MINW) k_lsd_spec(LsdGeom g, Lsd
 #pragma unroll
           for (int u = 0; u < 8; u++) {
             const int id = lsd_sd_index((int)(ev[u] & 0xFFFF), (int)(ev[u] >> 16), F.tw);
-            __hip_atomic_store(sd_hi(sd, id), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(sd_hi(sd, id), 0u, __ATOMIC_RELAXED, ORBPL_LSD_SCOPE);
           }
         }
       }
