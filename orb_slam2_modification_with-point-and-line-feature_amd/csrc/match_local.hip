@@ -736,7 +736,8 @@ __global__ void __launch_bounds__(256) k_trk_bow(TrkArgs a, int nstreams) {
 void launch_trk_bow(const TrkArgs& a, int nstreams, hipStream_t s) {
   const size_t smem = a.kp_pitch <= kBowMax ? (size_t)2 * sizeof(uint4) * a.kp_pitch : 0;
   set_smem_attr((const void*)k_trk_bow, sizeof(BowShared) + (size_t)2 * sizeof(uint4) * kBowMax);
-  const int grid = min(nstreams, 2 * device_cu_count());
+  static const char* g_env = getenv("ORBPL_TRK_BOW_GRID");   // A/B runs
+  const int grid = min(nstreams, g_env ? atoi(g_env) : 2 * device_cu_count());
   hipLaunchKernelGGL(k_trk_bow, dim3(grid), dim3(256), smem, s, a, nstreams);
 }
 
