@@ -420,7 +420,9 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
                      refkf=bool(args.refkf and voc is not None))
     # pipelining overlaps extraction of step t+1 with tracking of step t; the
     # LSD-bound line workloads gain nothing from it
-    pipelined = args.pipelined if args.pipelined >= 0 else (0 if lines else 1)
+    # pipelined for every workload (lines too: the next batch's LSD overlaps
+    # this batch's matching and pose, 9.5k -> 9.8k frames/s at 3072 streams)
+    pipelined = args.pipelined if args.pipelined >= 0 else 1
     tr.set_pipelined(bool(pipelined))
     if voc is not None:
         tr.set_vocabulary(voc, 4)    # KeyFrame::ComputeBoW of every frame (P18)
@@ -607,7 +609,7 @@ def sweep(pkg, synth, workload, sizes, steps, device, local_map=True, voc=None, 
         tr = pkg.Tracker(pkg.OrbParams(*wl["orb"]), cam, S, device=device, lines=wl["lines"],
                          stereo=wl["stereo"], local_map=local_map,
                          refkf=bool(refkf and voc is not None))
-        tr.set_pipelined(not wl["lines"])
+        tr.set_pipelined(True)
         if voc is not None:
             tr.set_vocabulary(voc, 4)
         tr.reset(np.stack([np.linalg.inv(L.Twc(s, 0)).astype(np.float32)

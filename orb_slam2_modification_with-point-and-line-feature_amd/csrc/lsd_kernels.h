@@ -111,6 +111,12 @@ void launch_lsd_blur(const LsdGeom& g, const uint8_t* img, int stride, long long
                      uint8_t* out, int batch, hipStream_t s);
 void launch_lsd_resize(const LsdGeom& g, const int* tabs, const uint8_t* blur, uint8_t* scaled,
                        int batch, hipStream_t s);
+// fused blur + resize + grad: scaled-image tiles of kPrTW x kPrTH; the
+// source span of a tile must fit kPrSC x kPrSR (lsd_prep_fits) and ksize be 7
+constexpr int kPrTW = 64, kPrTH = 16, kPrSC = 96, kPrSR = 32, kPrR = 3;
+void launch_lsd_prep(const LsdGeom& g, const int* tabs, const uint8_t* img, int stride,
+                     long long frame_pitch, uint8_t* scaled, float* deg, int* q, uint64_t* sd,
+                     unsigned* maxq, int batch, hipStream_t s);
 void launch_lsd_grad(const LsdGeom& g, const uint8_t* scaled, float* deg, int* q, uint64_t* sd,
                      unsigned* maxq, int batch, hipStream_t s);
 void launch_lsd_sort(const LsdGeom& g, const LsdScratch& sc, int batch, hipStream_t s);

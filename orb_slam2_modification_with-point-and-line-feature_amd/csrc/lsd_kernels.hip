@@ -148,6 +148,155 @@ __global__ void __launch_bounds__(256) k_lsd_grad(LsdGeom g, const uint8_t* __re
 }
 
 // ---------------------------------------------------------------------------
+// k_lsd_prep: k_lsd_blur + k_lsd_resize + k_lsd_grad fused per tile of the
+// scaled image (the same integer arithmetic, in the same order): the block's
+// source span (rows / columns the resize taps of its kPrTW+1 x kPrTH+1 scaled
+// pixels read) is loaded once with the blur halo, blurred in LDS (horizontal
+// sums as u16: 255 x 256 fits), resized in LDS, and the gradient of the core
+// kPrTW x kPrTH pixels written with the scaled image. The blurred image never
+// goes to HBM. The host checks the spans fit (lsdx_create) and the kernel
+// size is 7, else the three-kernel path runs.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_lsd_prep(LsdGeom g, const int* __restrict__ tabs,
+                                                  const uint8_t* __restrict__ img, int stride,
+                                                  long long frame_pitch,
+                                                  uint8_t* __restrict__ scaled,
+                                                  float* __restrict__ deg, int* __restrict__ q,
+                                                  uint64_t* __restrict__ sd,
+                                                  unsigned* __restrict__ maxq) {
+  __shared__ uint8_t s_in[kPrSR + 2 * kPrR][kPrSC + 2 * kPrR];
+  __shared__ uint16_t s_h[kPrSR + 2 * kPrR][kPrSC];
+  __shared__ uint8_t s_b[kPrSR][kPrSC];
+  __shared__ uint8_t s_s[kPrTH + 1][kPrTW + 4];
+  __shared__ int s_xo[kPrTW + 1], s_xc[kPrTW + 1], s_yo[kPrTH + 1], s_yc[kPrTH + 1];
+  __shared__ int s_span[4];   // source column min / max, row min / max
+  __shared__ unsigned s_m[4];
+  const int f = blockIdx.z, t = threadIdx.x;
+  const int x0 = blockIdx.x * kPrTW, y0 = blockIdx.y * kPrTH;
+  const int W = g.W, H = g.H, sw = g.sw, sh = g.sh;
+  const int nx = min(kPrTW + 1, sw - x0), ny = min(kPrTH + 1, sh - y0);
+  const int* xofs = tabs;
+  const int* xc1 = tabs + sw;
+  const int* yofs = tabs + 2 * sw;
+  const int* yc1 = tabs + 2 * sw + sh;
+  const int xlast = xofs[sw - 1];
+  if (t < 4) s_span[t] = (t & 1) ? -1 : 0x7fffffff;
+  __syncthreads();
+  if (t < nx) {
+    const int dx = x0 + t;
+    int lo, hi;
+    if (dx < g.rx0) lo = hi = 0;
+    else if (dx >= g.rx1) lo = hi = xlast;
+    else {
+      lo = xofs[dx];
+      hi = lo + 1;
+    }
+    s_xo[t] = xofs[dx];
+    s_xc[t] = xc1[dx];
+    atomicMin(&s_span[0], lo);
+    atomicMax(&s_span[1], hi);
+  }
+  if (t >= 128 && t - 128 < ny) {
+    const int i = t - 128, dy = y0 + i;
+    int lo, hi;
+    if (dy < g.ry0) lo = hi = 0;
+    else if (dy >= g.ry1) lo = hi = H - 1;
+    else {
+      lo = yofs[dy];
+      hi = lo + 1;
+    }
+    s_yo[i] = yofs[dy];
+    s_yc[i] = yc1[dy];
+    atomicMin(&s_span[2], lo);
+    atomicMax(&s_span[3], hi);
+  }
+  __syncthreads();
+  const int sx0 = s_span[0], sy0 = s_span[2];
+  const int ncol = s_span[1] - sx0 + 1, nrow = s_span[3] - sy0 + 1;
+  // the source span with the blur halo (REFLECT_101 as k_lsd_blur)
+  const uint8_t* src = img + (long long)f * frame_pitch;
+  const int icols = ncol + 2 * kPrR, irows = nrow + 2 * kPrR;
+  for (int i = t; i < irows * icols; i += 256) {
+    const int r = i / icols, c = i - r * icols;
+    s_in[r][c] = src[(long long)refl101(sy0 + r - kPrR, H) * stride + refl101(sx0 + c - kPrR, W)];
+  }
+  __syncthreads();
+  for (int i = t; i < irows * ncol; i += 256) {
+    const int r = i / ncol, c = i - r * ncol;
+    int acc = 0;
+#pragma unroll
+    for (int j = 0; j < 2 * kPrR + 1; j++) acc += g.gk[j] * s_in[r][c + j];
+    s_h[r][c] = (uint16_t)acc;
+  }
+  __syncthreads();
+  for (int i = t; i < nrow * ncol; i += 256) {
+    const int r = i / ncol, c = i - r * ncol;
+    int acc = 0;
+#pragma unroll
+    for (int j = 0; j < 2 * kPrR + 1; j++) acc += g.gk[j] * (int)s_h[r + j][c];
+    s_b[r][c] = (uint8_t)min(255, (acc + (1 << 15)) >> 16);
+  }
+  __syncthreads();
+  // resize (k_lsd_resize's arithmetic) of the scaled tile incl. the +1 halo
+  for (int i = t; i < ny * nx; i += 256) {
+    const int r = i / nx, c = i - r * nx;
+    const int dx = x0 + c, dy = y0 + r;
+    auto hval = [&](int sy) -> int {
+      const uint8_t* row = s_b[sy - sy0];
+      if (dx < g.rx0) return row[0 - sx0] << 8;
+      if (dx >= g.rx1) return row[xlast - sx0] << 8;
+      const int c1 = s_xc[c], o = s_xo[c] - sx0;
+      return (256 - c1) * row[o] + c1 * row[o + 1];
+    };
+    int v;
+    if (dy < g.ry0 || dy >= g.ry1) {
+      v = (hval(dy < g.ry0 ? 0 : H - 1) + 0x80) >> 8;
+    } else {
+      const int b1 = s_yc[r], b0 = 256 - b1, oy = s_yo[r];
+      v = (hval(oy) * b0 + hval(oy + 1) * b1 + 0x8000) >> 16;
+    }
+    s_s[r][c] = (uint8_t)min(255, v);
+  }
+  __syncthreads();
+  // the scaled image and ll_angle (k_lsd_grad's arithmetic) of the core tile
+  unsigned mq = 0;
+  const int tw = lsd_sd_tw(sw);
+  const long long fo = (long long)f * sw * sh;
+  uint64_t* fsd = sd + (long long)f * lsd_sd_words(sw, sh);
+  for (int i = t; i < kPrTH * kPrTW; i += 256) {
+    const int r = i / kPrTW, c = i - r * kPrTW;
+    const int x = x0 + c, y = y0 + r;
+    if (x >= sw || y >= sh) continue;
+    const long long o = fo + (long long)y * sw + x;
+    scaled[o] = s_s[r][c];
+    float d = kLsdNotdef;
+    int qq = 0;
+    if (x < sw - 1 && y < sh - 1) {
+      const int DA = s_s[r + 1][c + 1] - s_s[r][c];
+      const int BC = s_s[r][c + 1] - s_s[r + 1][c];
+      const int gx = DA + BC, gy = DA - BC;
+      qq = gx * gx + gy * gy;
+      const double norm = sqrt(qq / 4.0);
+      if (norm > g.rho) {
+        d = fast_atan2_deg((float)gx, (float)-gy);
+        mq = max(mq, (unsigned)qq);
+      }
+    }
+    deg[o] = d;
+    q[o] = qq;
+    fsd[lsd_sd_index(x, y, tw)] = (0xFFFFFFFFull << 32) | (uint64_t)__float_as_uint(d);
+  }
+  unsigned m = mq;
+  for (int o = 32; o >= 1; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o, 64));
+  if ((t & 63) == 0) s_m[t >> 6] = m;
+  __syncthreads();
+  if (t == 0) {
+    const unsigned bm = max(max(s_m[0], s_m[1]), max(s_m[2], s_m[3]));
+    if (bm) atomicMax(maxq + f, bm);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // libstdc++ std::sort replay (introsort, comparator key(a) > key(b)).
 //
 // Elements are key << 22 | raster index. The recursion of __introsort_loop
@@ -655,6 +804,14 @@ void launch_lsd_resize(const LsdGeom& g, const int* tabs, const uint8_t* blur, u
                        int batch, hipStream_t s) {
   hipLaunchKernelGGL(k_lsd_resize, dim3((g.sw * g.sh + 255) / 256, batch), dim3(256), 0, s, g,
                      tabs, blur, scaled);
+}
+
+void launch_lsd_prep(const LsdGeom& g, const int* tabs, const uint8_t* img, int stride,
+                     long long frame_pitch, uint8_t* scaled, float* deg, int* q, uint64_t* sd,
+                     unsigned* maxq, int batch, hipStream_t s) {
+  dim3 grid((g.sw + kPrTW - 1) / kPrTW, (g.sh + kPrTH - 1) / kPrTH, batch);
+  hipLaunchKernelGGL(k_lsd_prep, grid, dim3(256), 0, s, g, tabs, img, stride, frame_pitch, scaled,
+                     deg, q, sd, maxq);
 }
 
 void launch_lsd_grad(const LsdGeom& g, const uint8_t* scaled, float* deg, int* q, uint64_t* sd,

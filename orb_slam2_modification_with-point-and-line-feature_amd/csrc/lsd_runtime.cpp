@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -87,6 +88,7 @@ struct lsdx_ctx {
   uint8_t* d_in = nullptr;
   int last_batch = 0;
   bool serial_grow = false;  // lsdx_set_serial_grow: wave-serial seed loop
+  bool fused_prep = false;   // k_lsd_prep (the tiles' source spans fit; ksize 7)
   std::vector<void*> allocs;
 };
 
@@ -138,9 +140,14 @@ int lsdx_run(lsdx_ctx* c, const uint8_t* d_imgs, int batch, int stride, int64_t 
   const LsdGeom& g = c->g;
   HIP_CHECK(hipMemsetAsync(c->sc.maxq, 0, (size_t)batch * 4, s));
   HIP_CHECK(hipMemsetAsync(c->sc.err, 0, (size_t)batch * 4, s));
-  launch_lsd_blur(g, d_imgs, stride, frame_pitch, c->sc.blur, batch, s);
-  launch_lsd_resize(g, c->d_tabs, c->sc.blur, c->sc.scaled, batch, s);
-  launch_lsd_grad(g, c->sc.scaled, c->sc.deg, c->sc.q, c->sc.sd, c->sc.maxq, batch, s);
+  if (c->fused_prep) {
+    launch_lsd_prep(g, c->d_tabs, d_imgs, stride, frame_pitch, c->sc.scaled, c->sc.deg, c->sc.q,
+                    c->sc.sd, c->sc.maxq, batch, s);
+  } else {
+    launch_lsd_blur(g, d_imgs, stride, frame_pitch, c->sc.blur, batch, s);
+    launch_lsd_resize(g, c->d_tabs, c->sc.blur, c->sc.scaled, batch, s);
+    launch_lsd_grad(g, c->sc.scaled, c->sc.deg, c->sc.q, c->sc.sd, c->sc.maxq, batch, s);
+  }
   if (ev_stage) HIP_CHECK(hipEventRecord(ev_stage[0], s));
   launch_lsd_sort(g, c->sc, batch, s);
   if (ev_stage) HIP_CHECK(hipEventRecord(ev_stage[1], s));
@@ -281,6 +288,35 @@ int lsdx_create(int width, int height, int max_batch, int device, lsdx_ctx** out
   if (hipMemcpy(c->d_tabs, tabs.data(), tabs.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
     lsdx_destroy(c);
     return hip_fail(hipErrorUnknown, "hipMemcpy", __LINE__);
+  }
+  // k_lsd_prep's per-tile source spans (the resize taps of a tile's scaled
+  // pixels + 1) must fit its LDS tile
+  {
+    auto span = [](const int* ofs, int d0, int d1, int mn, int mx, int last, int* lo, int* hi) {
+      *lo = 1 << 30;
+      *hi = -1;
+      for (int d = d0; d < d1; d++) {
+        const int a = d < mn ? 0 : (d >= mx ? last : ofs[d]);
+        const int b = d < mn ? 0 : (d >= mx ? last : ofs[d] + 1);
+        *lo = std::min(*lo, a);
+        *hi = std::max(*hi, b);
+      }
+    };
+    bool ok = c->g.ksize == 2 * kPrR + 1;
+    for (int x0 = 0; ok && x0 < c->g.sw; x0 += kPrTW) {
+      int lo, hi;
+      span(tabs.data(), x0, std::min(x0 + kPrTW + 1, c->g.sw), c->g.rx0, c->g.rx1,
+           tabs[c->g.sw - 1], &lo, &hi);
+      ok = hi - lo + 1 <= kPrSC;
+    }
+    for (int y0 = 0; ok && y0 < c->g.sh; y0 += kPrTH) {
+      int lo, hi;
+      span(tabs.data() + 2 * c->g.sw, y0, std::min(y0 + kPrTH + 1, c->g.sh), c->g.ry0, c->g.ry1,
+           height - 1, &lo, &hi);
+      ok = hi - lo + 1 <= kPrSR;
+    }
+    const char* e = getenv("ORBPL_LSD_PREP");   // "0": the three-kernel path (A/B)
+    c->fused_prep = ok && !(e && e[0] == '0');
   }
   *out = c;
   return ORBPL_OK;
