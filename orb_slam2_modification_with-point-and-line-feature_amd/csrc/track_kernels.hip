@@ -149,7 +149,10 @@ __device__ __forceinline__ int hamming_rl(uint4 a0, uint4 a1, const uint4* b) {
 
 // Current-frame descriptors are staged in LDS when they fit (KMAX <= 1024:
 // 32 KB); the 2048-keypoint variant reads them from global memory.
-__host__ __device__ constexpr bool match_desc_lds(int kmax) { return kmax <= 1024; }
+#ifndef ORBPL_MATCH_DESC_LDS_MAX
+#define ORBPL_MATCH_DESC_LDS_MAX 1024
+#endif
+__host__ __device__ constexpr bool match_desc_lds(int kmax) { return kmax <= ORBPL_MATCH_DESC_LDS_MAX; }
 __host__ __device__ constexpr int match_desc_slots(int kmax) { return match_desc_lds(kmax) ? 2 * kmax : 1; }
 
 struct ProjInfo {
