@@ -507,6 +507,9 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
             step(warmup + steps + k)
         tr.synchronize()
         iso = dict(zip(tr.STAGES, [float(x) for x in tr.timings(args.isolated_steps).mean(0)]))
+        if lines:
+            iso.update(zip(tr.LSD_STAGES,
+                           [float(x) for x in tr.lsd_timings(args.isolated_steps).mean(0)]))
     sel = iso if iso is not None else stage_avg
     dom = max(cand, key=lambda k: sel.get(k, stage_avg[k]))
     dom_ms = stage_avg[dom]          # live: timed region, in-stream hipEvents
