@@ -59,6 +59,28 @@ def test_lsd_stages_bit_exact(orbpl, oracle, frames):
         assert np.array_equal(np.sort(order), np.sort(ord_o))
 
 
+@pytest.mark.parametrize("fused", ["1", "0"], ids=["k_lsd_prep", "blur_resize_grad"])
+def test_lsd_front_paths_bit_exact(orbpl, oracle, frames, fused, monkeypatch):
+    """Both LSD fronts against the oracle's scaled image and angles: the fused
+    per-tile k_lsd_prep (default) and the three-kernel path it falls back to
+    where a tile's source span does not fit (ORBPL_LSD_PREP=0 at create),
+    on VGA and on the KITTI geometry (1241x376: ragged last tiles)."""
+    monkeypatch.setenv("ORBPL_LSD_PREP", fused)
+    cfg, traj, fr = sequence(1, 4, cam_name="KITTI00", width=1241, height=376)
+    for (W, H), imgs in (((640, 480), frames[:2]), ((1241, 376), [fr[0][0]])):
+        det = orbpl.LineSegmentDetector(W, H)
+        for g in imgs:
+            L = det.detect(g)
+            scaled, deg, order = det.stages(0)
+            s_o, ang_o, ord_o = oracle.lsd_stages(g)
+            assert np.array_equal(scaled, s_o)
+            notdef = ang_o == -1024.0
+            assert np.array_equal(deg < 0, notdef)
+            a = deg.astype(np.float64) * (np.pi / 180)
+            assert np.array_equal(a[~notdef], ang_o[~notdef])
+            assert np.array_equal(L, oracle.lsd_detect(g))
+
+
 @pytest.mark.parametrize("serial", [False, True], ids=["speculative", "wave_serial"])
 def test_lsd_lines_bit_exact(orbpl, oracle, frames, serial):
     det = orbpl.LineSegmentDetector(640, 480)
