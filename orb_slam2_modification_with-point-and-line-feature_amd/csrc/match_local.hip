@@ -495,7 +495,7 @@ void launch_match_local(const TrackConsts& c, const LocalArgs& a, hipStream_t s,
   // batch's extraction and pack more frames per CU once frames outnumber CUs
   // (256 / 1024 streams: 512 threads 98.2k / 116.9k frames/s, 256 threads
   // 97.6k / 120.8k, 1024 threads 97.2k / 114.3k). ORBPL_LOCAL_NT overrides.
-  static const char* nt_env = getenv("ORBPL_LOCAL_NT");
+  const char* nt_env = getenv("ORBPL_LOCAL_NT");   // read per launch: tests vary it
   int nt = nstreams > device_cu_count() ? 256 : 512;
   if (nt_env) nt = atoi(nt_env);
 #define ORBPL_LOCAL_LAUNCH(KP, NTH)                                                              \

@@ -1628,7 +1628,7 @@ void launch_match_last(const TrackConsts& c, const MatchLaunch& m, int nstreams,
   static const int prof = getenv("ORBPL_MATCH_PROFILE") ? 1 : 0;
   a.prof = prof;
   // threads per frame (ORBPL_MATCH_NT overrides, A/B runs)
-  static const char* nt_env = getenv("ORBPL_MATCH_NT");
+  const char* nt_env = getenv("ORBPL_MATCH_NT");   // read per launch: tests vary it
   const int nt = nt_env ? atoi(nt_env) : kMatchLaunchThreads;
 #define ORBPL_MATCH_LAUNCH(KM, NTH)                                                          \
   if ((KM == 1024) == (m.kp_pitch <= 1024) && nt == NTH) {                                   \

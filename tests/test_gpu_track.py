@@ -474,6 +474,41 @@ def test_search_by_projection_local_bit_exact(orbpl, oracle, th, nnratio, claims
     assert np.array_equal(m_g, m_o), np.nonzero(m_g != m_o)[0][:5]
 
 
+@pytest.mark.parametrize("nt", ["1024", "512", "256", "128"])
+def test_matcher_workgroup_widths_bit_exact(orbpl, oracle, nt, monkeypatch):
+    """k_match_last (ORBPL_MATCH_NT) and k_match_local (ORBPL_LOCAL_NT; 128
+    is not built for it) at every workgroup width they are built for: the
+    same matches as the oracle (the launches pick 256 / 512-or-256 by batch)."""
+    monkeypatch.setenv("ORBPL_MATCH_NT", nt)
+    if nt != "128":
+        monkeypatch.setenv("ORBPL_LOCAL_NT", nt)
+    cfg, traj, fr = sequence(2, 5, cam_name="TUM3")
+    cam_o = oracle.camera(cfg)
+    f0 = frame_data(oracle, cam_o, cfg, *fr[0])
+    f1 = frame_data(oracle, cam_o, cfg, *fr[1])
+    T0 = np.linalg.inv(traj[0]).astype(np.float32)
+    has = (f0["depth"] > 0).astype(np.uint8)
+    xyz = _unproject_p6(cfg, f0["kps_un"], np.where(f0["depth"] > 0, f0["depth"], 0), T0)
+    last = dict(Tcw=T0, kps_un=f0["kps_un"], has_mp=has, outlier=np.zeros(len(has), np.uint8),
+                mp_xyz=xyz, mp_desc=f0["desc"], mp_nobs=np.ones(len(has), np.int32))
+    cur = dict(Tcw=T0, kps_un=f1["kps_un"], desc=f1["desc"], uright=f1["uright"])
+    sc = oracle.level_sizes(oracle.params(), 640, 480)[3]
+    m_o, n_o = oracle.search_by_projection_last(cam_o, sc, cur, last, 15.0, False, True)
+    m_g, n_g = orbpl.ORBmatcher(0.9, True).SearchByProjectionLastFrame(
+        orbpl.make_camera(cfg), sc, cur, last, 15.0, False)
+    assert n_g == n_o and n_o > 100 and np.array_equal(m_g, m_o)
+    if nt == "128":
+        return
+    from _scenes import local_map_problem
+    cfg, cam_o, sc, mps, cur, cur_nobs, T3 = local_map_problem(3)
+    track = oracle.frame_is_in_frustum(cam_o, _log_scale(oracle), 8, T3, mps, 0.5)
+    m_o, n_o = oracle.search_by_projection_local(cam_o, sc, cur, track, mps["desc"], mps["nobs"],
+                                                 cur_nobs, 3.0, 0.8)
+    m_g, n_g = orbpl.ORBmatcher(0.8).SearchByProjectionLocalMap(
+        orbpl.make_camera(cfg), sc, cur, track, mps["desc"], mps["nobs"], cur_nobs, 3.0)
+    assert n_g == n_o and n_o > 100 and np.array_equal(m_g, m_o)
+
+
 def test_search_by_projection_local_many_points_bit_exact(orbpl, oracle):
     """More map points than one in-view window of k_match_local holds (4 x the
     keypoint capacity): the map tiled three times with a few descriptor bits
