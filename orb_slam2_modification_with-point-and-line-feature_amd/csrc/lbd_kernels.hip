@@ -375,6 +375,68 @@ void launch_keylines(const LsdGeom& g, const LsdScratch& sc, const LineOut& o, i
   hipLaunchKernelGGL(k_keylines, dim3(batch), dim3(64), 0, s, g, sc, o);
 }
 
+// BinaryDescriptor's 5x5 sigma-1 GaussianBlur (k_lsd_blur's fixed point) and
+// computeSobel fused per 64x32 tile: the tile's input with both halos (blur 2
+// + Sobel 1, REFLECT_101) in LDS, the blur at the tile's pixels and their
+// Sobel neighbours, then dx / dy. The blurred image never goes to HBM. The
+// Sobel taps outside the image read the blur at REFLECT_101 coordinates; with
+// a symmetric kernel that is the blur of the reflected input, which is what
+// the tile computes at those virtual coordinates.
+constexpr int kBsTW = 64, kBsTH = 32, kBsR = 2;
+__global__ void __launch_bounds__(256) k_blur_sobel(LsdGeom g5, const uint8_t* __restrict__ img,
+                                                    int stride, long long frame_pitch,
+                                                    int16_t* __restrict__ dx,
+                                                    int16_t* __restrict__ dy) {
+  constexpr int kIW = kBsTW + 2 + 2 * kBsR, kIH = kBsTH + 2 + 2 * kBsR;   // 70 x 38
+  constexpr int kBW = kBsTW + 2, kBH = kBsTH + 2;                          // 66 x 34
+  __shared__ uint8_t s_in[kIH][kIW];
+  __shared__ uint16_t s_h[kIH][kBW];
+  __shared__ uint8_t s_b[kBH][kBW + 2];
+  const int f = blockIdx.z, t = threadIdx.x;
+  const int x0 = blockIdx.x * kBsTW, y0 = blockIdx.y * kBsTH;
+  const int W = g5.W, H = g5.H;
+  const uint8_t* src = img + (long long)f * frame_pitch;
+  for (int i = t; i < kIH * kIW; i += 256) {
+    const int r = i / kIW, c = i - r * kIW;
+    s_in[r][c] = src[(long long)refl(y0 - 1 - kBsR + r, H) * stride + refl(x0 - 1 - kBsR + c, W)];
+  }
+  __syncthreads();
+  for (int i = t; i < kIH * kBW; i += 256) {
+    const int r = i / kBW, c = i - r * kBW;
+    int acc = 0;
+#pragma unroll
+    for (int j = 0; j < 2 * kBsR + 1; j++) acc += g5.gk[j] * s_in[r][c + j];
+    s_h[r][c] = (uint16_t)acc;
+  }
+  __syncthreads();
+  for (int i = t; i < kBH * kBW; i += 256) {
+    const int r = i / kBW, c = i - r * kBW;
+    int acc = 0;
+#pragma unroll
+    for (int j = 0; j < 2 * kBsR + 1; j++) acc += g5.gk[j] * (int)s_h[r + j][c];
+    s_b[r][c] = (uint8_t)min(255, (acc + (1 << 15)) >> 16);
+  }
+  __syncthreads();
+  const long long fo = (long long)f * W * H;
+  for (int i = t; i < kBsTH * kBsTW; i += 256) {
+    const int r = i / kBsTW, c = i - r * kBsTW;
+    const int x = x0 + c, y = y0 + r;
+    if (x >= W || y >= H) continue;
+    // s_b[r + 1 + dy][c + 1 + dx] = blur at (x + dx, y + dy)
+    auto B = [&](int ddx, int ddy) { return (int)s_b[r + 1 + ddy][c + 1 + ddx]; };
+    const int gx = (B(1, -1) - B(-1, -1)) + 2 * (B(1, 0) - B(-1, 0)) + (B(1, 1) - B(-1, 1));
+    const int gy = (B(-1, 1) - B(-1, -1)) + 2 * (B(0, 1) - B(0, -1)) + (B(1, 1) - B(1, -1));
+    dx[fo + (long long)y * W + x] = (int16_t)gx;
+    dy[fo + (long long)y * W + x] = (int16_t)gy;
+  }
+}
+
+void launch_blur_sobel(const LsdGeom& g5, const uint8_t* img, int stride, long long frame_pitch,
+                       int16_t* dx, int16_t* dy, int batch, hipStream_t s) {
+  dim3 grid((g5.W + kBsTW - 1) / kBsTW, (g5.H + kBsTH - 1) / kBsTH, batch);
+  hipLaunchKernelGGL(k_blur_sobel, grid, dim3(256), 0, s, g5, img, stride, frame_pitch, dx, dy);
+}
+
 void launch_sobel(int W, int H, const uint8_t* blur5, int16_t* dx, int16_t* dy, int batch,
                   hipStream_t s) {
   hipLaunchKernelGGL(k_sobel, dim3((W * H + 255) / 256, batch), dim3(256), 0, s, W, H, blur5, dx,

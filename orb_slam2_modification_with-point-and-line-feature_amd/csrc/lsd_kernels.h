@@ -102,6 +102,9 @@ struct LbdWeights {
 
 void launch_keylines(const LsdGeom& g, const LsdScratch& sc, const LineOut& o, int batch,
                      hipStream_t s);
+// the 5x5 blur (g5, ksize 5) and computeSobel fused per tile
+void launch_blur_sobel(const LsdGeom& g5, const uint8_t* img, int stride, long long frame_pitch,
+                       int16_t* dx, int16_t* dy, int batch, hipStream_t s);
 void launch_sobel(int W, int H, const uint8_t* blur5, int16_t* dx, int16_t* dy, int batch,
                   hipStream_t s);
 void launch_lbd(int W, int H, const int16_t* dx, const int16_t* dy, const LbdWeights& w,

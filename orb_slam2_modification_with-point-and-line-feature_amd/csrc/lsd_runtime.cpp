@@ -160,8 +160,13 @@ int lsdx_run(lsdx_ctx* c, const uint8_t* d_imgs, int batch, int stride, int64_t 
     o.kl_all = c->lo.kl_all;  // per-frame scratch of the full detection
     launch_keylines(c->g, c->sc, o, batch, s);
     if (ev_stage) HIP_CHECK(hipEventRecord(ev_stage[3], s));
-    launch_lsd_blur(c->g5, d_imgs, stride, frame_pitch, c->blur5, batch, s);
-    launch_sobel(c->W, c->H, c->blur5, c->sdx, c->sdy, batch, s);
+    const char* e = getenv("ORBPL_BLUR_SOBEL");   // "0": separate blur + Sobel (A/B)
+    if (c->g5.ksize == 5 && !(e && e[0] == '0')) {
+      launch_blur_sobel(c->g5, d_imgs, stride, frame_pitch, c->sdx, c->sdy, batch, s);
+    } else {
+      launch_lsd_blur(c->g5, d_imgs, stride, frame_pitch, c->blur5, batch, s);
+      launch_sobel(c->W, c->H, c->blur5, c->sdx, c->sdy, batch, s);
+    }
     launch_lbd(c->W, c->H, c->sdx, c->sdy, c->lw, o, batch, s);
     if (ev_stage) HIP_CHECK(hipEventRecord(ev_stage[4], s));
   }

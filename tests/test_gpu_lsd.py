@@ -117,7 +117,11 @@ def _cmp_keylines(kl, desc, coef, kl_o, desc_o, coef_o):
     assert np.array_equal(coef, coef_o)
 
 
-def test_line_extract_bit_exact(orbpl, oracle, frames):
+@pytest.mark.parametrize("fused", ["1", "0"], ids=["blur_sobel", "blur_then_sobel"])
+def test_line_extract_bit_exact(orbpl, oracle, frames, fused, monkeypatch):
+    """KeyLines, LBD rows and coefficients; the LBD gradients from the fused
+    5x5 blur + Sobel kernel (default) and from the separate kernels."""
+    monkeypatch.setenv("ORBPL_BLUR_SOBEL", fused)
     ex = orbpl.LineExtractor(640, 480)
     for g in frames:
         kl, desc, coef = ex.ExtractLineSegment(g)
