@@ -58,7 +58,8 @@ struct BowBatch {
   double* bow_vals;
   int* bow_n;
   long long out_pitch;
-  int* err;                     // bit 1: more than kBowMaxFeat features
+  int* err;                     // bit 1: more than kBowMaxFeat (or cap) features
+  int cap;                      // k_bow_vector's LDS keys: a power of two >= max_n
 };
 
 }  // namespace
@@ -102,16 +103,19 @@ __global__ void __launch_bounds__(256) k_bow_words(VocDev v, BowBatch b) {
   b.feat_node[o] = w > 0 ? nid : -1;
 }
 
+// LDS sized by the batch's feature cap (b.cap: 12 KB at 1000 features
+// instead of a static 48 KB, so more frames share a CU)
 __global__ void __launch_bounds__(256) k_bow_vector(VocDev v, BowBatch b) {
-  __shared__ uint32_t key[kBowMaxFeat];
-  __shared__ double sval[kBowMaxFeat];   // BowVector values in word order
+  extern __shared__ double bow_dyn[];
+  double* sval = bow_dyn;                                        // BowVector values in word order
+  uint32_t* key = reinterpret_cast<uint32_t*>(bow_dyn + b.cap);  // sort keys
   __shared__ int wsum[4];
   __shared__ double s_norm;
   const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
   int n = b.n[f];
-  if (n > kBowMaxFeat) {
+  if (n > b.cap) {
     if (t == 0) atomicOr(b.err, 2);
-    n = kBowMaxFeat;
+    n = b.cap;
   }
   const long long o = (long long)f * b.out_pitch;
   int np = 1;
@@ -465,11 +469,14 @@ int orbv_transform_batch_device(orbv_vocab* v, const uint8_t* d_desc, int64_t de
     HIP_CHECK(hipMemsetAsync(d_feat_node, 0xFF, 4 * (size_t)(out_pitch * nframes), s));
     return ORBPL_OK;
   }
+  int cap = 1;
+  while (cap < max_n) cap <<= 1;
   BowBatch b{d_desc, desc_pitch, d_n, levelsup, d_feat_node, d_feat_word, d_feat_weight,
-             d_bow_words, d_bow_vals, d_bow_n, out_pitch, d_err};
+             d_bow_words, d_bow_vals, d_bow_n, out_pitch, d_err, cap};
   if (max_n > 0)
     hipLaunchKernelGGL(k_bow_words, dim3((max_n + 255) / 256, nframes), dim3(256), 0, s, vd, b);
-  hipLaunchKernelGGL(k_bow_vector, dim3(nframes), dim3(256), 0, s, vd, b);
+  set_smem_attr((const void*)k_bow_vector, (size_t)kBowMaxFeat * 12);
+  hipLaunchKernelGGL(k_bow_vector, dim3(nframes), dim3(256), (size_t)cap * 12, s, vd, b);
   HIP_CHECK(hipGetLastError());
   return ORBPL_OK;
 }
