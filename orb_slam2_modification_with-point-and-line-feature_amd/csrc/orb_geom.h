@@ -69,7 +69,10 @@ struct OrbGeom {
 // k_pyramid (fused pyramid + borders + blur): one block per (row band,
 // frame). Band b owns content rows [oa, ob) of every level and computes rows
 // [na, nb) (own rows plus the halo that the blur and the next level read).
-constexpr int kPyrThreads = 256;
+#ifndef ORBPL_PYR_THREADS
+#define ORBPL_PYR_THREADS 256
+#endif
+constexpr int kPyrThreads = ORBPL_PYR_THREADS;   // k_pyramid block (A/B builds override)
 constexpr int kPyrMaxBands = 8;      // bands for B = 1, 2, 4, 8 are precomputed
 struct PyrBand {
   int na[kMaxLevels], nb[kMaxLevels];
