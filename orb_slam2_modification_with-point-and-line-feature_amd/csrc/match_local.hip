@@ -702,15 +702,16 @@ void launch_match_bow(const BowArgs& a, hipStream_t s) {
 // TrackReferenceKeyFrame's ORBmatcher(0.7, true).SearchByBoW(pKF, F)
 // (Tracking.cc:947-952) for every stream with st[s].trk: the last frame's
 // FeatureVector / map points / descriptors against the current frame's
-// A persistent grid: workgroup g takes streams g, g + grid, ... (only the
-// few streams whose motion model failed have work; a workgroup per stream
-// would have every one of them placed beside the next batch's extraction).
-__global__ void __launch_bounds__(256) k_trk_bow(TrkArgs a, int nstreams) {
+// One workgroup per stream; only the streams whose motion model failed have
+// work (the rest return at once). The frame's descriptors stay in global
+// memory here: 32 KB more LDS on every workgroup of the launch made it slower
+// to place beside the next batch's extraction (a persistent grid with LDS
+// descriptors measured 2.2 ms per step against 0.3-0.8 ms this way).
+__global__ void __launch_bounds__(256) k_trk_bow(TrkArgs a) {
   __shared__ BowShared B;
-  extern __shared__ uint4 trk_fdl[];
-  for (int s = blockIdx.x; s < nstreams; s += gridDim.x) {
+  const int s = blockIdx.x;
   StreamState& S = a.st[s];
-  if (!S.trk) continue;
+  if (!S.trk) return;
   const long long cb = (long long)s * a.kp_pitch;
   BowArgs b;
   b.nkf = a.last_n[s];
@@ -728,17 +729,11 @@ __global__ void __launch_bounds__(256) k_trk_bow(TrkArgs a, int nstreams) {
   b.check_ori = 1;
   b.match = a.match + cb;
   b.nmatches = &S.nmatches;
-  match_bow_body(b, B, a.kp_pitch <= kBowMax ? trk_fdl : nullptr);
-  __syncthreads();   // B and trk_fdl are reused by the next stream
-  }
+  match_bow_body(b, B, nullptr);
 }
 
 void launch_trk_bow(const TrkArgs& a, int nstreams, hipStream_t s) {
-  const size_t smem = a.kp_pitch <= kBowMax ? (size_t)2 * sizeof(uint4) * a.kp_pitch : 0;
-  set_smem_attr((const void*)k_trk_bow, sizeof(BowShared) + (size_t)2 * sizeof(uint4) * kBowMax);
-  static const char* g_env = getenv("ORBPL_TRK_BOW_GRID");   // A/B runs
-  const int grid = min(nstreams, g_env ? atoi(g_env) : 2 * device_cu_count());
-  hipLaunchKernelGGL(k_trk_bow, dim3(grid), dim3(256), smem, s, a, nstreams);
+  hipLaunchKernelGGL(k_trk_bow, dim3(nstreams), dim3(256), 0, s, a);
 }
 
 }  // namespace orbpl
