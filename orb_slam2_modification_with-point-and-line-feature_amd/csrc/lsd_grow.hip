@@ -1409,16 +1409,28 @@ __global__ void __launch_bounds__(64, ORBPL_SPEC_MINW) k_lsd_spec(LsdGeom g, Lsd
 // NFA validation of every refined rectangle (rect_improve), one lane per
 // rectangle; the accepted segments are compacted in seed order by
 // k_lsd_compact.
-constexpr int kValBlocks = 8;
+#ifndef ORBPL_VAL_BLOCKS
+#define ORBPL_VAL_BLOCKS 8
+#endif
+constexpr int kValBlocks = ORBPL_VAL_BLOCKS;   // workgroups per frame
 
 #ifndef ORBPL_VAL_MINW
 #define ORBPL_VAL_MINW 8   // 8 waves/SIMD (64 VGPRs, some scratch): 33.1 ms per 3072 frames; 6: 34.5; unbounded (111 VGPRs, 4 waves): 39.8
 #endif
+// Lanes take rectangles from a workgroup-wide counter (block b owns the
+// rectangles c = b (mod kValBlocks)): a lane whose rectangle was cheap takes
+// the next one instead of idling until the wave's costliest walk ends (the
+// improvement loop runs rect_nfa up to ~25 times on rejected rectangles).
 __global__ void __launch_bounds__(256, ORBPL_VAL_MINW) k_lsd_validate(LsdGeom g, LsdScratch sc) {
+  __shared__ int s_next;
   const int f = blockIdx.y;
   const int nc = sc.ncand[f];
   const float* deg = sc.deg + (long long)f * g.sw * g.sh;
-  for (int c = blockIdx.x * 256 + threadIdx.x; c < nc; c += kValBlocks * 256) {
+  if (threadIdx.x == 0) s_next = 256;
+  __syncthreads();
+  for (int k = threadIdx.x;; k = atomicAdd(&s_next, 1)) {
+    const int c = blockIdx.x + k * kValBlocks;
+    if (c >= nc) break;
     const long long o = (long long)f * kLsdMaxCand + c;
     const double* rv = sc.cand + o * 12;
     Rect rec;
