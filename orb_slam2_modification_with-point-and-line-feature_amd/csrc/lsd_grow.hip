@@ -1409,18 +1409,19 @@ __global__ void __launch_bounds__(64, ORBPL_SPEC_MINW) k_lsd_spec(LsdGeom g, Lsd
 // NFA validation of every refined rectangle (rect_improve), one lane per
 // rectangle; the accepted segments are compacted in seed order by
 // k_lsd_compact.
-#ifndef ORBPL_VAL_BLOCKS
-#define ORBPL_VAL_BLOCKS 8
-#endif
-constexpr int kValBlocks = ORBPL_VAL_BLOCKS;   // workgroups per frame
+// workgroups per frame: 8 for small batches (one frame's rectangles spread
+// wide), 2 from 1024 frames on (each lane then takes ~3 rectangles from the
+// counter: 27.4 -> 24.2 ms per 3072 frames)
+constexpr int kValBlocksSmall = 8, kValBlocksLarge = 2;
 
 #ifndef ORBPL_VAL_MINW
 #define ORBPL_VAL_MINW 8   // 8 waves/SIMD (64 VGPRs, some scratch): 33.1 ms per 3072 frames; 6: 34.5; unbounded (111 VGPRs, 4 waves): 39.8
 #endif
 // Lanes take rectangles from a workgroup-wide counter (block b owns the
-// rectangles c = b (mod kValBlocks)): a lane whose rectangle was cheap takes
+// rectangles c = b (mod gridDim.x)): a lane whose rectangle was cheap takes
 // the next one instead of idling until the wave's costliest walk ends (the
 // improvement loop runs rect_nfa up to ~25 times on rejected rectangles).
+// gridDim.x = workgroups per frame.
 __global__ void __launch_bounds__(256, ORBPL_VAL_MINW) k_lsd_validate(LsdGeom g, LsdScratch sc) {
   __shared__ int s_next;
   const int f = blockIdx.y;
@@ -1429,7 +1430,7 @@ __global__ void __launch_bounds__(256, ORBPL_VAL_MINW) k_lsd_validate(LsdGeom g,
   if (threadIdx.x == 0) s_next = 256;
   __syncthreads();
   for (int k = threadIdx.x;; k = atomicAdd(&s_next, 1)) {
-    const int c = blockIdx.x + k * kValBlocks;
+    const int c = blockIdx.x + k * (int)gridDim.x;
     if (c >= nc) break;
     const long long o = (long long)f * kLsdMaxCand + c;
     const double* rv = sc.cand + o * 12;
@@ -1473,7 +1474,8 @@ __global__ void __launch_bounds__(64) k_lsd_compact(LsdScratch sc) {
 }
 
 void launch_lsd_validate(const LsdGeom& g, const LsdScratch& sc, int batch, hipStream_t s) {
-  hipLaunchKernelGGL(k_lsd_validate, dim3(kValBlocks, batch), dim3(256), 0, s, g, sc);
+  const int nblk = batch >= 1024 ? kValBlocksLarge : kValBlocksSmall;
+  hipLaunchKernelGGL(k_lsd_validate, dim3(nblk, batch), dim3(256), 0, s, g, sc);
   hipLaunchKernelGGL(k_lsd_compact, dim3(batch), dim3(64), 0, s, sc);
 }
 
