@@ -821,6 +821,68 @@ __device__ __forceinline__ void lane_rect(const uint4* buf, int n, double reg_an
   if (rec.width < 1.0) rec.width = 1.0;
 }
 
+// One pass of reduce_region_radius's removal scan (lsd.cpp reduce_region_radius:
+// "swap with the last point, pop, re-test i") over a lane list, without its
+// chain of dependent loads. The scan's result is fixed by the points alone:
+// the kept ("near") points end in [0, nn), nn = their count; a near point in
+// [0, nn) keeps its slot and the k-th far point there (in index order) is
+// replaced by the k-th near point of [nn, n) counted from the end. So one
+// batched counting pass, then a merge of a forward stream over [0, nn) and a
+// backward stream over [nn, n), several loads in flight per refill. Each slot
+// is read by one stream before any store reaches it (stores go to slots the
+// storing stream has consumed), so the windows never hold stale points. The
+// far points stay in [nn, n) (their order is immaterial: the claim re-check
+// reads the touched prefix as a set), and only their point words: the scan
+// tests only point words, a near point moved forward carries all four.
+__device__ __forceinline__ bool lane_far(uint32_t pt, double xc, double yc, double radSq) {
+  return distSq(xc, yc, double(pt & 0xFFFF), double(pt >> 16)) > radSq;
+}
+__device__ __forceinline__ int lane_reduce_pass(uint4* g1, int n, double xc, double yc,
+                                                double radSq) {
+  constexpr int kB = 8, kBb = 4;
+  const uint32_t* gx = reinterpret_cast<const uint32_t*>(g1);
+  int nn = 0;
+  for (int i0 = 0; i0 < n; i0 += kB) {
+    uint32_t e[kB];
+#pragma unroll
+    for (int u = 0; u < kB; u++) e[u] = gx[4 * min(i0 + u, n - 1)];
+#pragma unroll
+    for (int u = 0; u < kB; u++) nn += (i0 + u < n && !lane_far(e[u], xc, yc, radSq)) ? 1 : 0;
+  }
+  if (nn == n) return n;
+  uint32_t fw[kB];
+  uint4 bw[kBb];
+  int fcnt = 0, bcnt = 0, bpos = n - 1;
+  for (int fpos = 0; fpos < nn; fpos++) {
+    if (fcnt == 0) {
+#pragma unroll
+      for (int u = 0; u < kB; u++) fw[u] = gx[4 * min(fpos + u, nn - 1)];
+      fcnt = kB;
+    }
+    const uint32_t e = fw[0];
+#pragma unroll
+    for (int u = 0; u < kB - 1; u++) fw[u] = fw[u + 1];
+    fcnt--;
+    if (!lane_far(e, xc, yc, radSq)) continue;
+    uint4 b;
+    do {   // [nn, n) holds exactly as many near points as [0, nn) far ones
+      if (bcnt == 0) {
+#pragma unroll
+        for (int u = 0; u < kBb; u++) bw[u] = g1[max(bpos - u, nn)];
+        bcnt = kBb;
+      }
+      b = bw[0];
+#pragma unroll
+      for (int u = 0; u < kBb - 1; u++) bw[u] = bw[u + 1];
+      bcnt--;
+      bpos--;
+    } while (lane_far(b.x, xc, yc, radSq));
+    g1[fpos] = b;
+    reinterpret_cast<uint32_t*>(g1)[4 * (bpos + 1)] = e;
+  }
+  return nn;
+}
+
 // refine + reduce_region_radius for a lane. The region [0, n) came from the
 // first grow; a second grow is appended after it. Returns the status; off /
 // len give the final region, touched the claimed prefix of the buffer.
@@ -874,15 +936,7 @@ __device__ __forceinline__ int lane_refine(const Frame& F, uint64_t* sd, uint4* 
   double radSq = radSq1 > radSq2 ? radSq1 : radSq2;
   while (density < density_th) {
     radSq *= 0.75 * 0.75;
-    for (int i = 0; i < n1; ++i) {
-      const uint4 e = g1[i];
-      if (distSq(xc, yc, double(pt_x(e)), double(pt_y(e))) > radSq) {
-        g1[i] = g1[n1 - 1];
-        g1[n1 - 1] = e;
-        n1--;
-        --i;
-      }
-    }
+    n1 = lane_reduce_pass(g1, n1, xc, yc, radSq);
     len = n1;
     if (n1 < 2) return kSpecFail;
     lane_rect(g1, n1, reg_angle, prec, p, rec);
