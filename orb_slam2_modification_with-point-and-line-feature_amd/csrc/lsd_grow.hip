@@ -47,6 +47,7 @@ struct Frame {
   const int* q;
   uint32_t* used;     // LDS bits (k_lsd_grow)
   uint64_t* usd;      // k_lsd_spec: USED lives in the claim stamps (high words, 0 = USED)
+  const uint64_t* cs; // k_lsd_spec: the angle-term plane (cos | sin << 32, lsd_sd_frame_words)
   int tw;             // tiles per row of usd
   uint32_t* reg_l;    // LDS region points (x | y << 16)
   int* regq_l;        // LDS q (gx^2 + gy^2) of each region point
@@ -645,24 +646,19 @@ __device__ __forceinline__ int pt_y(const uint4& e) { return (int)(e.x >> 16); }
 
 // region_grow for one lane over the packed pixel words (degrees + claim
 // stamp, one 8-byte load per neighbour). buf entries: (x | y << 16, degrees,
-// modgrad as a double split lo / hi), the weight filled by lane_fill_w before
-// a fit. Claims are fire-and-forget 64-bit atomicMin on (stamp << 32 | deg
+// modgrad as a double split lo / hi), the weight stored by lane_rect's first
+// pass. Claims are fire-and-forget 64-bit atomicMin on (stamp << 32 | deg
 // bits) - the low word is constant per pixel, so the minimum is the stamps'.
 // The own-pixel test re-reads the stamp from L2 (same-address order within
-// the wave). The angle terms cos / sin of an added pixel are computed from its
-// degrees exactly as the reference's region_grow does (P2). Returns the
+// the wave). The angle terms cos / sin of an added pixel (the reference's
+// region_grow arithmetic, P2) come precomputed from the angle-term plane,
+// loaded with the neighbourhood, so the serial chain per added pixel is the
+// two adds and the atan2. Returns the
 // length, kSpecConflict or kSpecOverflow.
 __device__ __forceinline__ double entry_w(const uint4& e) {
   return __hiloint2double((int)e.w, (int)e.z);
 }
 __device__ __forceinline__ float entry_deg(const uint4& e) { return __uint_as_float(e.y); }
-
-__device__ __forceinline__ void add_angle(float d, float& sumdx, float& sumdy) {
-  float c, sn;
-  cr_cos_sin((float)((double)d * (3.14159265358979323846 / 180)), &c, &sn);
-  sumdx += c;
-  sumdy += sn;
-}
 
 __device__ __forceinline__ int lane_grow(const Frame& F, uint64_t* sd, uint4* buf, int cap, int sx,
                                          int sy, double& reg_angle, double prec, uint32_t myval) {
@@ -688,13 +684,14 @@ __device__ __forceinline__ int lane_grow(const Frame& F, uint64_t* sd, uint4* bu
     // all loads unconditional (clamped coordinates) so that they are in
     // flight together; out-of-image neighbours are masked afterwards
     const uint4 pref = buf[min(i + 1, n_start - 1)];
-    uint64_t v[9];
+    uint64_t v[9], cs[9];
     unsigned cand = 0;
 #pragma unroll
     for (int k = 0; k < 9; k++) {
       const int xx = x + (k % 3) - 1, yy = y + (k / 3) - 1;
       const int cx = min(max(xx, 0), sw - 1), cy = min(max(yy, 0), sh - 1);
       v[k] = ld_sd(sd + lsd_sd_index(cx, cy, tw));
+      cs[k] = F.cs[lsd_sd_index(cx, cy, tw)];
       const bool in = xx >= 0 && xx < sw && yy >= 0 && yy < sh;
       cand |= (in && (uint32_t)(v[k] >> 32) != 0u) ? (1u << k) : 0u;   // stamp 0 = USED
     }
@@ -713,7 +710,8 @@ __device__ __forceinline__ int lane_grow(const Frame& F, uint64_t* sd, uint4* bu
       const uint4 e = make_uint4((uint32_t)xx | ((uint32_t)yy << 16), (uint32_t)v[k], 0u, 0u);
       if (n == n_start) first_add = e;
       buf[n++] = e;
-      add_angle(d, sumdx, sumdy);
+      sumdx += __uint_as_float((uint32_t)cs[k]);          // add_angle(d) terms
+      sumdy += __uint_as_float((uint32_t)(cs[k] >> 32));
       reg_angle = (double)fast_atan2_deg(sumdy, sumdx) * kDegToRad;
     }
     cur = (i + 1 < n_start) ? pref : first_add;
@@ -721,45 +719,50 @@ __device__ __forceinline__ int lane_grow(const Frame& F, uint64_t* sd, uint4* bu
   return n;
 }
 
-// the weights modgrad = sqrt(q / 4) of a lane list's points (ll_angle's
-// modgrad, LSD's region weights), 8 independent loads in flight
-__device__ __forceinline__ void lane_fill_w(const int* __restrict__ q, int sw, uint4* buf, int n) {
-  for (int i0 = 0; i0 < n; i0 += 8) {
-    uint4 e[8];
-    int qv[8];
-#pragma unroll
-    for (int u = 0; u < 8; u++) e[u] = buf[min(i0 + u, n - 1)];
-#pragma unroll
-    for (int u = 0; u < 8; u++) qv[u] = q[pt_y(e[u]) * sw + pt_x(e[u])];
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-      if (i0 + u < n) {
-        const double w = modgrad_q(qv[u]);
-        e[u].z = (uint32_t)__double2loint(w);
-        e[u].w = (uint32_t)__double2hiint(w);
-        buf[i0 + u] = e[u];
-      }
-    }
-  }
-}
-
-// region2rect over a lane's list (same operation order as region2rect)
-__device__ __forceinline__ void lane_rect(const uint4* buf, int n, double reg_angle, double prec,
-                                          double p, Rect& rec) {
-  // every pass reads the list in batches of 8 unconditional loads (indices
-  // clamped to n - 1, contributions masked) so the loads overlap
-  constexpr int kB = 8;
+// region2rect over a lane's list (same operation order as region2rect).
+// With q given, the first pass also stores the weights modgrad = sqrt(q / 4)
+// (ll_angle's modgrad, LSD's region weights) into the list: the point words
+// it loads give the q addresses, so the fill costs no pass of its own. Every
+// pass reads the list in batches of unconditional loads (indices clamped to
+// n - 1, contributions masked) so the loads overlap.
+__device__ __forceinline__ void lane_rect(uint4* buf, int n, double reg_angle, double prec,
+                                          double p, Rect& rec, const int* __restrict__ q = nullptr,
+                                          int sw = 0) {
+  constexpr int kB = 8, kB3 = 16;
+  const uint32_t* bx = reinterpret_cast<const uint32_t*>(buf);
   double x = 0, y = 0, sum = 0;
   for (int i0 = 0; i0 < n; i0 += kB) {
-    uint4 e[kB];
+    uint32_t pt[kB];
+    double w[kB];
+    if (q) {
+      int qv[kB];
 #pragma unroll
-    for (int u = 0; u < kB; u++) e[u] = buf[min(i0 + u, n - 1)];
+      for (int u = 0; u < kB; u++) pt[u] = bx[4 * min(i0 + u, n - 1)];
+#pragma unroll
+      for (int u = 0; u < kB; u++) qv[u] = q[(int)(pt[u] >> 16) * sw + (int)(pt[u] & 0xFFFF)];
+#pragma unroll
+      for (int u = 0; u < kB; u++) {
+        w[u] = modgrad_q(qv[u]);
+        if (i0 + u < n)
+          *reinterpret_cast<uint2*>(reinterpret_cast<uint32_t*>(buf + i0 + u) + 2) =
+              make_uint2((uint32_t)__double2loint(w[u]), (uint32_t)__double2hiint(w[u]));
+      }
+    } else {
+      uint4 e[kB];
+#pragma unroll
+      for (int u = 0; u < kB; u++) e[u] = buf[min(i0 + u, n - 1)];
+#pragma unroll
+      for (int u = 0; u < kB; u++) {
+        pt[u] = e[u].x;
+        w[u] = entry_w(e[u]);
+      }
+    }
 #pragma unroll
     for (int u = 0; u < kB; u++) {
       if (i0 + u < n) {
-        const double weight = entry_w(e[u]);
-        x += double(pt_x(e[u])) * weight;
-        y += double(pt_y(e[u])) * weight;
+        const double weight = w[u];
+        x += double(pt[u] & 0xFFFF) * weight;
+        y += double(pt[u] >> 16) * weight;
         sum += weight;
       }
     }
@@ -791,13 +794,13 @@ __device__ __forceinline__ void lane_rect(const uint4* buf, int n, double reg_an
   // l_max / l_min (and w) start at 0, so the reference's else-if is an
   // independent max / min
   double l_min = 0, l_max = 0, w_min = 0, w_max = 0;
-  for (int i0 = 0; i0 < n; i0 += kB) {
-    uint4 e[kB];
+  for (int i0 = 0; i0 < n; i0 += kB3) {   // point words only
+    uint32_t pt[kB3];
 #pragma unroll
-    for (int u = 0; u < kB; u++) e[u] = buf[min(i0 + u, n - 1)];
+    for (int u = 0; u < kB3; u++) pt[u] = bx[4 * min(i0 + u, n - 1)];
 #pragma unroll
-    for (int u = 0; u < kB; u++) {
-      const double regdx = double(pt_x(e[u])) - x, regdy = double(pt_y(e[u])) - y;
+    for (int u = 0; u < kB3; u++) {
+      const double regdx = double(pt[u] & 0xFFFF) - x, regdy = double(pt[u] >> 16) - y;
       const double l = regdx * dx + regdy * dy;
       const double w = -regdx * dy + regdy * dx;
       l_max = l > l_max ? l : l_max;
@@ -926,8 +929,7 @@ __device__ __forceinline__ int lane_refine(const Frame& F, uint64_t* sd, uint4* 
   len = n1;
   touched = n + n1;
   if (n1 < 2) return kSpecFail;
-  lane_fill_w(F.q, F.sw, g1, n1);
-  lane_rect(g1, n1, reg_angle, prec, p, rec);
+  lane_rect(g1, n1, reg_angle, prec, p, rec, F.q, F.sw);
   density = double(n1) / (dist(rec.x1, rec.y1, rec.x2, rec.y2) * rec.width);
   if (density >= density_th) return kSpecCand;
   // reduce_region_radius
@@ -1263,8 +1265,9 @@ __global__ void __launch_bounds__(64, ORBPL_SPEC_MINW) k_lsd_spec(LsdGeom g, Lsd
   F.lane = lane;
   F.pf_cyc = 0;
   F.pf_cnt = 0;
-  uint64_t* sd = sc.sd + (long long)f * lsd_sd_words(sw, sh);   // stamps unclaimed at launch
+  uint64_t* sd = sc.sd + (long long)f * lsd_sd_frame_words(sw, sh);   // stamps unclaimed at launch
   F.usd = sd;
+  F.cs = sd + lsd_sd_words(sw, sh);
   F.tw = lsd_sd_tw(sw);
   (void)used_words;
   uint4* buf = sc.lbuf + ((long long)f * kSpecLanes + lane) * kLaneCap;
@@ -1344,8 +1347,7 @@ __global__ void __launch_bounds__(64, ORBPL_SPEC_MINW) k_lsd_spec(LsdGeom g, Lsd
         len = n;
         touched = n;
       } else {
-        lane_fill_w(F.q, sw, buf, n);
-        lane_rect(buf, n, reg_angle, prec, p, rec);
+        lane_rect(buf, n, reg_angle, prec, p, rec, F.q, sw);
         status = lane_refine(F, sd, buf, n, reg_angle, prec, p, rec, myval1, off, len, touched);
       }
     }

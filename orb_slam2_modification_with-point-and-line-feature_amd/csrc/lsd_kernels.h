@@ -43,6 +43,13 @@ __host__ __device__ inline int lsd_sd_tw(int sw) { return (sw + 3) >> 2; }
 __host__ __device__ inline long long lsd_sd_words(int sw, int sh) {
   return (long long)lsd_sd_tw(sw) * ((sh + 3) >> 2) * 16;
 }
+// per frame: the pixel words (lsd_sd_words) followed by the angle-term plane
+// in the same tiles: (cos | sin << 32) of the pixel's float angle, the
+// region_grow accumulation terms (P2), so a grow step adds a pixel without
+// evaluating them on its serial chain
+__host__ __device__ inline long long lsd_sd_frame_words(int sw, int sh) {
+  return 2 * lsd_sd_words(sw, sh);
+}
 __host__ __device__ inline int lsd_sd_index(int x, int y, int tw) {
   return ((((y >> 2) * tw) + (x >> 2)) << 4) | ((y & 3) << 2) | (x & 3);
 }

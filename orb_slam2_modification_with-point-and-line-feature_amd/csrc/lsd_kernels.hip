@@ -19,6 +19,19 @@
 #include "orbpl_math.h"
 
 namespace orbpl {
+// region_grow's accumulation terms of a pixel (lsd.cpp region_grow: sumdx +=
+// cos(angle), sumdy += sin(angle), float angle; P2 pins correctly rounded
+// float cos / sin): (cos | sin << 32), the same expression k_lsd_spec's
+// add_angle evaluated per added pixel. NOTDEF pixels are never added.
+__device__ __forceinline__ uint64_t lsd_angle_terms(float d) {
+  if (d < 0.f) return 0;
+  float c, s;
+  cr_cos_sin((float)((double)d * (3.14159265358979323846 / 180)), &c, &s);
+  return ((uint64_t)__float_as_uint(s) << 32) | (uint64_t)__float_as_uint(c);
+}
+}  // namespace orbpl
+
+namespace orbpl {
 
 __device__ __forceinline__ int refl101(int i, int n) {
   if (n == 1) return 0;
@@ -132,8 +145,10 @@ __global__ void __launch_bounds__(256) k_lsd_grad(LsdGeom g, const uint8_t* __re
     deg[o] = d;
     q[o] = qq;
     // the speculative seed loop's pixel word: degrees + unclaimed stamp
-    sd[(long long)f * lsd_sd_words(sw, sh) + lsd_sd_index(x, y, lsd_sd_tw(sw))] =
-        (0xFFFFFFFFull << 32) | (uint64_t)__float_as_uint(d);
+    uint64_t* fsd = sd + (long long)f * lsd_sd_frame_words(sw, sh);
+    const int si = lsd_sd_index(x, y, lsd_sd_tw(sw));
+    fsd[si] = (0xFFFFFFFFull << 32) | (uint64_t)__float_as_uint(d);
+    fsd[lsd_sd_words(sw, sh) + si] = lsd_angle_terms(d);
   }
   // block max, one atomic per block
   __shared__ unsigned s_m[4];
@@ -262,7 +277,8 @@ __global__ void __launch_bounds__(256) k_lsd_prep(LsdGeom g, const int* __restri
   unsigned mq = 0;
   const int tw = lsd_sd_tw(sw);
   const long long fo = (long long)f * sw * sh;
-  uint64_t* fsd = sd + (long long)f * lsd_sd_words(sw, sh);
+  uint64_t* fsd = sd + (long long)f * lsd_sd_frame_words(sw, sh);
+  const long long csw = lsd_sd_words(sw, sh);
   for (int i = t; i < kPrTH * kPrTW; i += 256) {
     const int r = i / kPrTW, c = i - r * kPrTW;
     const int x = x0 + c, y = y0 + r;
@@ -284,7 +300,9 @@ __global__ void __launch_bounds__(256) k_lsd_prep(LsdGeom g, const int* __restri
     }
     deg[o] = d;
     q[o] = qq;
-    fsd[lsd_sd_index(x, y, tw)] = (0xFFFFFFFFull << 32) | (uint64_t)__float_as_uint(d);
+    const int si = lsd_sd_index(x, y, tw);
+    fsd[si] = (0xFFFFFFFFull << 32) | (uint64_t)__float_as_uint(d);
+    fsd[csw + si] = lsd_angle_terms(d);
   }
   unsigned m = mq;
   for (int o = 32; o >= 1; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o, 64));
