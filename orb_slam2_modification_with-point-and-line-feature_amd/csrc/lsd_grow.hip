@@ -660,6 +660,24 @@ __device__ __forceinline__ double entry_w(const uint4& e) {
 }
 __device__ __forceinline__ float entry_deg(const uint4& e) { return __uint_as_float(e.y); }
 
+// ORBPL_GROW_CS: the added pixels' cos / sin from the angle-term plane (1) or
+// evaluated per add (0); ORBPL_GROW_LOOP: first-aligned iteration (1) or the
+// in-order walk over the 9 positions (0). A/B build overrides.
+#ifndef ORBPL_GROW_CS
+#define ORBPL_GROW_CS 1
+#endif
+#ifndef ORBPL_GROW_LOOP
+#define ORBPL_GROW_LOOP 0
+#endif
+#if !ORBPL_GROW_CS
+__device__ __forceinline__ void add_angle(float d, float& sumdx, float& sumdy) {
+  float c, sn;
+  cr_cos_sin((float)((double)d * (3.14159265358979323846 / 180)), &c, &sn);
+  sumdx += c;
+  sumdy += sn;
+}
+#endif
+
 __device__ __forceinline__ int lane_grow(const Frame& F, uint64_t* sd, uint4* buf, int cap, int sx,
                                          int sy, double& reg_angle, double prec, uint32_t myval) {
   const uint32_t mytag = myval >> 1;
@@ -684,18 +702,72 @@ __device__ __forceinline__ int lane_grow(const Frame& F, uint64_t* sd, uint4* bu
     // all loads unconditional (clamped coordinates) so that they are in
     // flight together; out-of-image neighbours are masked afterwards
     const uint4 pref = buf[min(i + 1, n_start - 1)];
-    uint64_t v[9], cs[9];
+    uint64_t v[9];
+#if ORBPL_GROW_CS
+    uint64_t cs[9];
+#endif
     unsigned cand = 0;
 #pragma unroll
     for (int k = 0; k < 9; k++) {
       const int xx = x + (k % 3) - 1, yy = y + (k / 3) - 1;
       const int cx = min(max(xx, 0), sw - 1), cy = min(max(yy, 0), sh - 1);
       v[k] = ld_sd(sd + lsd_sd_index(cx, cy, tw));
+#if ORBPL_GROW_CS
       cs[k] = F.cs[lsd_sd_index(cx, cy, tw)];
+#endif
       const bool in = xx >= 0 && xx < sw && yy >= 0 && yy < sh;
       cand |= (in && (uint32_t)(v[k] >> 32) != 0u) ? (1u << k) : 0u;   // stamp 0 = USED
     }
     uint4 first_add = cur;
+#if ORBPL_GROW_LOOP
+    // Adds are rare (about one per step), so instead of walking the 9
+    // positions with the add code under each (executed wherever any lane
+    // adds), every iteration tests the remaining candidates against the
+    // current region angle and adds the first aligned one: the positions
+    // before it are not aligned under that angle, exactly as the in-order
+    // walk finds them, and the later ones are re-tested after the update.
+    unsigned rem = 0;
+#pragma unroll
+    for (int k = 0; k < 9; k++)
+      rem |= (((cand >> k) & 1u) && (uint32_t)(v[k] >> 32) != myval) ? (1u << k) : 0u;
+    while (rem) {
+      unsigned am = 0;
+#pragma unroll
+      for (int k = 0; k < 9; k++)
+        if ((rem >> k) & 1u)
+          am |= aligned_deg(__uint_as_float((uint32_t)v[k]), reg_angle, prec) ? (1u << k) : 0u;
+      if (!am) break;
+      const int k = __ffs(am) - 1;
+      rem &= ~((2u << k) - 1u);
+      uint64_t vk = v[0];
+#if ORBPL_GROW_CS
+      uint64_t ck = cs[0];
+#endif
+#pragma unroll
+      for (int j = 1; j < 9; j++) {
+        vk = (k == j) ? v[j] : vk;
+#if ORBPL_GROW_CS
+        ck = (k == j) ? cs[j] : ck;
+#endif
+      }
+      const uint32_t st = (uint32_t)(vk >> 32);
+      if ((st >> 1) < mytag) return kSpecConflict;      // an earlier seed's pixel
+      const int xx = x + (k % 3) - 1, yy = y + (k / 3) - 1;
+      atomicMin(reinterpret_cast<unsigned long long*>(sd + lsd_sd_index(xx, yy, tw)),
+                ((unsigned long long)myval << 32) | (uint32_t)vk);
+      if (n >= cap) return kSpecOverflow;
+      const uint4 e = make_uint4((uint32_t)xx | ((uint32_t)yy << 16), (uint32_t)vk, 0u, 0u);
+      if (n == n_start) first_add = e;
+      buf[n++] = e;
+#if ORBPL_GROW_CS
+      sumdx += __uint_as_float((uint32_t)ck);          // add_angle(d) terms
+      sumdy += __uint_as_float((uint32_t)(ck >> 32));
+#else
+      add_angle(__uint_as_float((uint32_t)vk), sumdx, sumdy);
+#endif
+      reg_angle = (double)fast_atan2_deg(sumdy, sumdx) * kDegToRad;
+    }
+#else
 #pragma unroll
     for (int k = 0; k < 9; k++) {
       const uint32_t st = (uint32_t)(v[k] >> 32);
@@ -710,10 +782,15 @@ __device__ __forceinline__ int lane_grow(const Frame& F, uint64_t* sd, uint4* bu
       const uint4 e = make_uint4((uint32_t)xx | ((uint32_t)yy << 16), (uint32_t)v[k], 0u, 0u);
       if (n == n_start) first_add = e;
       buf[n++] = e;
+#if ORBPL_GROW_CS
       sumdx += __uint_as_float((uint32_t)cs[k]);          // add_angle(d) terms
       sumdy += __uint_as_float((uint32_t)(cs[k] >> 32));
+#else
+      add_angle(d, sumdx, sumdy);
+#endif
       reg_angle = (double)fast_atan2_deg(sumdy, sumdx) * kDegToRad;
     }
+#endif
     cur = (i + 1 < n_start) ? pref : first_add;
   }
   return n;
