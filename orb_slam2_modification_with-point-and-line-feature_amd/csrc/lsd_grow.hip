@@ -711,9 +711,17 @@ __device__ __forceinline__ int lane_grow(const Frame& F, uint64_t* sd, uint4* bu
     for (int k = 0; k < 9; k++) {
       const int xx = x + (k % 3) - 1, yy = y + (k / 3) - 1;
       const int cx = min(max(xx, 0), sw - 1), cy = min(max(yy, 0), sh - 1);
+#if ORBPL_GROW_CS && ORBPL_SD_PAIRED
+      {   // word + terms in one 16-byte load (workgroup-scope plain load, as ld_sd)
+        const uint4 w = *reinterpret_cast<const uint4*>(sd + lsd_sd_index(cx, cy, tw));
+        v[k] = ((uint64_t)w.y << 32) | w.x;
+        cs[k] = ((uint64_t)w.w << 32) | w.z;
+      }
+#else
       v[k] = ld_sd(sd + lsd_sd_index(cx, cy, tw));
 #if ORBPL_GROW_CS
       cs[k] = F.cs[lsd_sd_index(cx, cy, tw)];
+#endif
 #endif
       const bool in = xx >= 0 && xx < sw && yy >= 0 && yy < sh;
       cand |= (in && (uint32_t)(v[k] >> 32) != 0u) ? (1u << k) : 0u;   // stamp 0 = USED
@@ -1344,7 +1352,7 @@ __global__ void __launch_bounds__(64, ORBPL_SPEC_MINW) k_lsd_spec(LsdGeom g, Lsd
   F.pf_cnt = 0;
   uint64_t* sd = sc.sd + (long long)f * lsd_sd_frame_words(sw, sh);   // stamps unclaimed at launch
   F.usd = sd;
-  F.cs = sd + lsd_sd_words(sw, sh);
+  F.cs = sd + lsd_cs_offset(sw, sh);
   F.tw = lsd_sd_tw(sw);
   (void)used_words;
   uint4* buf = sc.lbuf + ((long long)f * kSpecLanes + lane) * kLaneCap;

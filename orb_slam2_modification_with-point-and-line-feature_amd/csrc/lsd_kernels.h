@@ -50,8 +50,19 @@ __host__ __device__ inline long long lsd_sd_words(int sw, int sh) {
 __host__ __device__ inline long long lsd_sd_frame_words(int sw, int sh) {
   return 2 * lsd_sd_words(sw, sh);
 }
+// ORBPL_SD_PAIRED: a pixel's word and its angle terms side by side (one
+// 16-byte load per neighbour in the grow, 4x4-pixel tiles of 256 B) instead of
+// two planes of 128-B tiles (the terms at + lsd_sd_words).
+#ifndef ORBPL_SD_PAIRED
+#define ORBPL_SD_PAIRED 1
+#endif
 __host__ __device__ inline int lsd_sd_index(int x, int y, int tw) {
-  return ((((y >> 2) * tw) + (x >> 2)) << 4) | ((y & 3) << 2) | (x & 3);
+  const int i = ((((y >> 2) * tw) + (x >> 2)) << 4) | ((y & 3) << 2) | (x & 3);
+  return ORBPL_SD_PAIRED ? 2 * i : i;
+}
+// offset (u64 words) of a pixel's angle terms from its pixel word
+__host__ __device__ inline long long lsd_cs_offset(int sw, int sh) {
+  return ORBPL_SD_PAIRED ? 1 : lsd_sd_words(sw, sh);
 }
 
 struct LsdScratch {

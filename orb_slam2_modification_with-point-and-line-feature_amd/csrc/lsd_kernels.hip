@@ -148,7 +148,7 @@ __global__ void __launch_bounds__(256) k_lsd_grad(LsdGeom g, const uint8_t* __re
     uint64_t* fsd = sd + (long long)f * lsd_sd_frame_words(sw, sh);
     const int si = lsd_sd_index(x, y, lsd_sd_tw(sw));
     fsd[si] = (0xFFFFFFFFull << 32) | (uint64_t)__float_as_uint(d);
-    fsd[lsd_sd_words(sw, sh) + si] = lsd_angle_terms(d);
+    fsd[lsd_cs_offset(sw, sh) + si] = lsd_angle_terms(d);
   }
   // block max, one atomic per block
   __shared__ unsigned s_m[4];
@@ -278,7 +278,7 @@ __global__ void __launch_bounds__(256) k_lsd_prep(LsdGeom g, const int* __restri
   const int tw = lsd_sd_tw(sw);
   const long long fo = (long long)f * sw * sh;
   uint64_t* fsd = sd + (long long)f * lsd_sd_frame_words(sw, sh);
-  const long long csw = lsd_sd_words(sw, sh);
+  const long long csw = lsd_cs_offset(sw, sh);
   for (int i = t; i < kPrTH * kPrTW; i += 256) {
     const int r = i / kPrTW, c = i - r * kPrTW;
     const int x = x0 + c, y = y0 + r;

@@ -10,7 +10,13 @@ obj=$here/orb_slam2_modification_with-point-and-line-feature_amd/build_obj
 out=$here/variants/$name
 mkdir -p "$out"
 F="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -Wall -Wno-unused-function -Wno-unused-result"
-/opt/rocm/bin/hipcc $F "$@" -x hip -c "$csrc/$src" -o "$out/$src.o"
-objs=$(ls $obj/*.o | grep -v "/$src.o\$")
-/opt/rocm/bin/hipcc $F -shared -o "$out/liborbpl.so" $objs "$out/$src.o"
+# several sources: comma-separated (a layout shared by two kernels' files)
+objs=$(ls $obj/*.o)
+mine=""
+for s in ${src//,/ }; do
+  /opt/rocm/bin/hipcc $F "$@" -x hip -c "$csrc/$s" -o "$out/$s.o"
+  objs=$(echo "$objs" | grep -v "/$s.o\$")
+  mine="$mine $out/$s.o"
+done
+/opt/rocm/bin/hipcc $F -shared -o "$out/liborbpl.so" $objs $mine
 echo "$out/liborbpl.so"
