@@ -660,6 +660,31 @@ __device__ __forceinline__ double entry_w(const uint4& e) {
 }
 __device__ __forceinline__ float entry_deg(const uint4& e) { return __uint_as_float(e.y); }
 
+// A lane's region list: lbuf[frame][lane][i] (a lane's batch of 8 entries is
+// one cache line). ORBPL_LBUF_INTERLEAVED=1 (A/B build) puts entry i of lane l
+// at lbuf[frame][i][l], so that a wave's load of entry i (the lanes walk their
+// lists in step) reads 64 consecutive entries: measured slower (231 vs 222 ms
+// per 3072 frames) - the lane-major batch stays in one line per lane.
+#ifndef ORBPL_LBUF_INTERLEAVED
+#define ORBPL_LBUF_INTERLEAVED 0
+#endif
+struct LaneBuf {
+  uint4* p;
+  static constexpr long long kStride = ORBPL_LBUF_INTERLEAVED ? kSpecLanes : 1;
+  __device__ __forceinline__ uint4& operator[](int i) const { return p[(long long)i * kStride]; }
+  __device__ __forceinline__ LaneBuf operator+(int o) const { return LaneBuf{p + (long long)o * kStride}; }
+  __device__ __forceinline__ uint32_t pt(int i) const { return p[(long long)i * kStride].x; }
+  __device__ __forceinline__ void set_pt(int i, uint32_t v) const { p[(long long)i * kStride].x = v; }
+  __device__ __forceinline__ double w(int i) const {
+    const uint2 v = *reinterpret_cast<const uint2*>(&p[(long long)i * kStride].z);
+    return __hiloint2double((int)v.y, (int)v.x);
+  }
+  __device__ __forceinline__ void set_w(int i, double v) const {
+    *reinterpret_cast<uint2*>(&p[(long long)i * kStride].z) =
+        make_uint2((uint32_t)__double2loint(v), (uint32_t)__double2hiint(v));
+  }
+};
+
 // ORBPL_GROW_CS: the added pixels' cos / sin from the angle-term plane (1) or
 // evaluated per add (0); ORBPL_GROW_LOOP: first-aligned iteration (1) or the
 // in-order walk over the 9 positions (0). A/B build overrides.
@@ -678,7 +703,7 @@ __device__ __forceinline__ void add_angle(float d, float& sumdx, float& sumdy) {
 }
 #endif
 
-__device__ __forceinline__ int lane_grow(const Frame& F, uint64_t* sd, uint4* buf, int cap, int sx,
+__device__ __forceinline__ int lane_grow(const Frame& F, uint64_t* sd, LaneBuf buf, int cap, int sx,
                                          int sy, double& reg_angle, double prec, uint32_t myval) {
   const uint32_t mytag = myval >> 1;
   const int sw = F.sw, sh = F.sh, tw = F.tw;
@@ -810,11 +835,10 @@ __device__ __forceinline__ int lane_grow(const Frame& F, uint64_t* sd, uint4* bu
 // it loads give the q addresses, so the fill costs no pass of its own. Every
 // pass reads the list in batches of unconditional loads (indices clamped to
 // n - 1, contributions masked) so the loads overlap.
-__device__ __forceinline__ void lane_rect(uint4* buf, int n, double reg_angle, double prec,
+__device__ __forceinline__ void lane_rect(LaneBuf buf, int n, double reg_angle, double prec,
                                           double p, Rect& rec, const int* __restrict__ q = nullptr,
                                           int sw = 0) {
   constexpr int kB = 8, kB3 = 16;
-  const uint32_t* bx = reinterpret_cast<const uint32_t*>(buf);
   double x = 0, y = 0, sum = 0;
   for (int i0 = 0; i0 < n; i0 += kB) {
     uint32_t pt[kB];
@@ -822,15 +846,14 @@ __device__ __forceinline__ void lane_rect(uint4* buf, int n, double reg_angle, d
     if (q) {
       int qv[kB];
 #pragma unroll
-      for (int u = 0; u < kB; u++) pt[u] = bx[4 * min(i0 + u, n - 1)];
+      for (int u = 0; u < kB; u++) pt[u] = buf.pt(min(i0 + u, n - 1));
 #pragma unroll
       for (int u = 0; u < kB; u++) qv[u] = q[(int)(pt[u] >> 16) * sw + (int)(pt[u] & 0xFFFF)];
 #pragma unroll
       for (int u = 0; u < kB; u++) {
         w[u] = modgrad_q(qv[u]);
         if (i0 + u < n)
-          *reinterpret_cast<uint2*>(reinterpret_cast<uint32_t*>(buf + i0 + u) + 2) =
-              make_uint2((uint32_t)__double2loint(w[u]), (uint32_t)__double2hiint(w[u]));
+          buf.set_w(i0 + u, w[u]);
       }
     } else {
       uint4 e[kB];
@@ -882,7 +905,7 @@ __device__ __forceinline__ void lane_rect(uint4* buf, int n, double reg_angle, d
   for (int i0 = 0; i0 < n; i0 += kB3) {   // point words only
     uint32_t pt[kB3];
 #pragma unroll
-    for (int u = 0; u < kB3; u++) pt[u] = bx[4 * min(i0 + u, n - 1)];
+    for (int u = 0; u < kB3; u++) pt[u] = buf.pt(min(i0 + u, n - 1));
 #pragma unroll
     for (int u = 0; u < kB3; u++) {
       const double regdx = double(pt[u] & 0xFFFF) - x, regdy = double(pt[u] >> 16) - y;
@@ -925,15 +948,14 @@ __device__ __forceinline__ void lane_rect(uint4* buf, int n, double reg_angle, d
 __device__ __forceinline__ bool lane_far(uint32_t pt, double xc, double yc, double radSq) {
   return distSq(xc, yc, double(pt & 0xFFFF), double(pt >> 16)) > radSq;
 }
-__device__ __forceinline__ int lane_reduce_pass(uint4* g1, int n, double xc, double yc,
+__device__ __forceinline__ int lane_reduce_pass(LaneBuf g1, int n, double xc, double yc,
                                                 double radSq) {
   constexpr int kB = 8, kBb = 4;
-  const uint32_t* gx = reinterpret_cast<const uint32_t*>(g1);
   int nn = 0;
   for (int i0 = 0; i0 < n; i0 += kB) {
     uint32_t e[kB];
 #pragma unroll
-    for (int u = 0; u < kB; u++) e[u] = gx[4 * min(i0 + u, n - 1)];
+    for (int u = 0; u < kB; u++) e[u] = g1.pt(min(i0 + u, n - 1));
 #pragma unroll
     for (int u = 0; u < kB; u++) nn += (i0 + u < n && !lane_far(e[u], xc, yc, radSq)) ? 1 : 0;
   }
@@ -944,7 +966,7 @@ __device__ __forceinline__ int lane_reduce_pass(uint4* g1, int n, double xc, dou
   for (int fpos = 0; fpos < nn; fpos++) {
     if (fcnt == 0) {
 #pragma unroll
-      for (int u = 0; u < kB; u++) fw[u] = gx[4 * min(fpos + u, nn - 1)];
+      for (int u = 0; u < kB; u++) fw[u] = g1.pt(min(fpos + u, nn - 1));
       fcnt = kB;
     }
     const uint32_t e = fw[0];
@@ -966,7 +988,7 @@ __device__ __forceinline__ int lane_reduce_pass(uint4* g1, int n, double xc, dou
       bpos--;
     } while (lane_far(b.x, xc, yc, radSq));
     g1[fpos] = b;
-    reinterpret_cast<uint32_t*>(g1)[4 * (bpos + 1)] = e;
+    g1.set_pt(bpos + 1, e);
   }
   return nn;
 }
@@ -974,7 +996,7 @@ __device__ __forceinline__ int lane_reduce_pass(uint4* g1, int n, double xc, dou
 // refine + reduce_region_radius for a lane. The region [0, n) came from the
 // first grow; a second grow is appended after it. Returns the status; off /
 // len give the final region, touched the claimed prefix of the buffer.
-__device__ __forceinline__ int lane_refine(const Frame& F, uint64_t* sd, uint4* buf, int n,
+__device__ __forceinline__ int lane_refine(const Frame& F, uint64_t* sd, LaneBuf buf, int n,
                                            double reg_angle,
                                            double prec, double p, Rect& rec, uint32_t myval1,
                                            int& off, int& len, int& touched) {
@@ -1007,7 +1029,7 @@ __device__ __forceinline__ int lane_refine(const Frame& F, uint64_t* sd, uint4* 
   const double mean_angle = sum / double(cnt);
   const double tau =
       2.0 * sqrt((s_sum - 2.0 * mean_angle * sum) / double(cnt) + mean_angle * mean_angle);
-  uint4* g1 = buf + n;
+  LaneBuf g1 = buf + n;
   int n1 = lane_grow(F, sd, g1, kLaneCap - n, x0, y0, reg_angle, tau, myval1);
   if (n1 < 0) return n1;
   off = n;
@@ -1355,7 +1377,8 @@ __global__ void __launch_bounds__(64, ORBPL_SPEC_MINW) k_lsd_spec(LsdGeom g, Lsd
   F.cs = sd + lsd_cs_offset(sw, sh);
   F.tw = lsd_sd_tw(sw);
   (void)used_words;
-  uint4* buf = sc.lbuf + ((long long)f * kSpecLanes + lane) * kLaneCap;
+  LaneBuf buf{sc.lbuf + (long long)f * kSpecLanes * kLaneCap +
+              (ORBPL_LBUF_INTERLEAVED ? lane : (long long)lane * kLaneCap)};
   const uint32_t* A = sc.A + (long long)f * g.n;
   const int nlist = sc.sort_nge[f];   // later list entries are NOTDEF
   double* cand_out = sc.cand + (long long)f * kLsdMaxCand * 12;
