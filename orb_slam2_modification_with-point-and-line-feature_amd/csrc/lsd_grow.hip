@@ -1336,20 +1336,52 @@ __global__ void __launch_bounds__(64) k_lsd_grow(LsdGeom g, LsdScratch sc) {
 }
 
 
-// Speculative seed loop (see lane_grow): one wave per frame.
+// Speculative seed loop (see lane_grow): W waves per frame, 64 W seeds per
+// round. W = 1 from 1536 frames per batch on (every frame co-resident, one
+// wave each); mid-size batches take 2 or 4 waves per frame (lsd_spec_waves):
+// a round of 128 / 256 seeds needs 2.4x fewer rounds (388 -> 159 per frame),
+// but each round waits for the slowest of more lanes and wastes more
+// speculative regions (24.8k -> 40.5k per frame), so a lone frame gains
+// nothing; with the GPU partly empty the extra waves fill it (batch 256:
+// -5 %, 1024: -10 % per batch).
 // ORBPL_SPEC_MINW: waves per SIMD the register budget must allow (frames in
 // flight per CU = 4x; the loop is latency-bound, so more frames in flight
 // raise throughput until the memory system saturates)
 #ifndef ORBPL_SPEC_MINW
 #define ORBPL_SPEC_MINW 1
 #endif
-__global__ void __launch_bounds__(64, ORBPL_SPEC_MINW) k_lsd_spec(LsdGeom g, LsdScratch sc) {
+// the block's first index >= j whose bit is set in the per-wave masks, or n
+template <int W>
+__device__ __forceinline__ int next_set(const unsigned long long* m, int j, int n) {
+#pragma unroll
+  for (int w = 0; w < W; w++) {
+    if (j >= 64 * (w + 1)) continue;
+    const int b = j - 64 * w;
+    const unsigned long long r = b <= 0 ? m[w] : (m[w] & ~((1ull << b) - 1ull));
+    if (r) return min(n, 64 * w + __ffsll((long long)r) - 1);
+  }
+  return n;
+}
+template <int W>
+__device__ __forceinline__ void block_sync() {
+  if (W == 1) {
+    __builtin_amdgcn_wave_barrier();
+  } else {
+    __syncthreads();
+  }
+}
+
+template <int W>
+__global__ void __launch_bounds__(64 * W, ORBPL_SPEC_MINW) k_lsd_spec(LsdGeom g, LsdScratch sc) {
+  constexpr int SL = 64 * W;
   extern __shared__ uint32_t grow_smem[];
-  __shared__ uint32_t s_pt[kSpecLanes];
-  __shared__ int s_pos[kSpecLanes];
-  const int f = blockIdx.x, lane = threadIdx.x;
+  __shared__ uint32_t s_pt[SL];
+  __shared__ int s_pos[SL];
+  __shared__ int s_cnt[2][W];
+  __shared__ unsigned long long s_cm[W], s_km[W];
+  __shared__ int s_misc[2];   // next_pos, status of the stop seed / nl after a fallback
+  const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int sw = g.sw, sh = g.sh;
-  const int used_words = (sw * sh + 31) / 32;
   Frame F;
   F.sw = sw;
   F.sh = sh;
@@ -1358,7 +1390,8 @@ __global__ void __launch_bounds__(64, ORBPL_SPEC_MINW) k_lsd_spec(LsdGeom g, Lsd
   F.used = nullptr;
   // the cooperative fallback's region list head and prefetch ring live in
   // the (then idle) lane buffers, so LDS holds only the USED bits
-  uint32_t* coop = reinterpret_cast<uint32_t*>(sc.lbuf + (long long)f * kSpecLanes * kLaneCap);
+  uint4* fbuf = sc.lbuf + (long long)f * SL * kLaneCap;
+  uint32_t* coop = reinterpret_cast<uint32_t*>(fbuf);
   F.reg_l = coop;
   F.regq_l = reinterpret_cast<int*>(F.reg_l + kRegLds);
   F.regd_l = reinterpret_cast<float*>(F.regq_l + kRegLds);
@@ -1376,25 +1409,24 @@ __global__ void __launch_bounds__(64, ORBPL_SPEC_MINW) k_lsd_spec(LsdGeom g, Lsd
   F.usd = sd;
   F.cs = sd + lsd_cs_offset(sw, sh);
   F.tw = lsd_sd_tw(sw);
-  (void)used_words;
-  LaneBuf buf{sc.lbuf + (long long)f * kSpecLanes * kLaneCap +
-              (ORBPL_LBUF_INTERLEAVED ? lane : (long long)lane * kLaneCap)};
+  static_assert(!ORBPL_LBUF_INTERLEAVED || W == 1, "interleaved lane lists: one wave per frame");
+  LaneBuf buf{fbuf + (ORBPL_LBUF_INTERLEAVED ? t : (long long)t * kLaneCap)};
   const uint32_t* A = sc.A + (long long)f * g.n;
   const int nlist = sc.sort_nge[f];   // later list entries are NOTDEF
   double* cand_out = sc.cand + (long long)f * kLsdMaxCand * 12;
   const int w1 = sw - 1;
   const double prec = g.prec, p = g.p;
   const unsigned long long lt_mask = (1ull << lane) - 1ull;
-  int nl = 0, pos = 0;
+  int nl = 0, pos = 0, it = 0;
   uint32_t round = 0;
   long long n_spec = 0, n_rounds = 0, cyc_spec = 0, cyc_fit = 0, cyc_val = 0, max_steps = 0,
             n_coop = 0;
   const long long t_all = clock64();
   while (pos < nlist) {
-    // ---- the next 64 defined, NOTUSED seeds in list order ----
+    // ---- the next SL defined, NOTUSED seeds in list order ----
     int ncand = 0, scan = pos, next_pos = nlist;
-    while (ncand < kSpecLanes && scan < nlist) {
-      const int i = scan + lane;
+    while (ncand < SL && scan < nlist) {
+      const int i = scan + t;
       bool c = false;
       int px = 0, py = 0;
       if (i < nlist) {
@@ -1406,36 +1438,57 @@ __global__ void __launch_bounds__(64, ORBPL_SPEC_MINW) k_lsd_spec(LsdGeom g, Lsd
         c = __uint_as_float((uint32_t)v) >= 0.f && (uint32_t)(v >> 32) != 0u;
       }
       const unsigned long long m = __ballot(c);
-      const int before = __popcll(m & lt_mask);
-      if (c && ncand + before < kSpecLanes) {
+      int before = __popcll(m & lt_mask), cnt = __popcll(m);
+      if (W > 1) {
+        const int par = it++ & 1;   // double-buffered: no barrier before the next write
+        if (lane == 0) s_cnt[par][wv] = cnt;
+        __syncthreads();
+        int off = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < W; w++) {
+          const int v = s_cnt[par][w];
+          off += w < wv ? v : 0;
+          tot += v;
+        }
+        before += off;
+        cnt = tot;
+      }
+      if (c && ncand + before < SL) {
         s_pt[ncand + before] = (uint32_t)px | ((uint32_t)py << 16);
         s_pos[ncand + before] = i;
       }
-      const int cnt = __popcll(m);
-      if (ncand + cnt >= kSpecLanes) {
-        const unsigned long long mm = __ballot(c && before == kSpecLanes - ncand - 1);
-        next_pos = scan + __ffsll((long long)mm);
-        ncand = kSpecLanes;
+      if (ncand + cnt >= SL) {
+        if (W == 1) {
+          const unsigned long long mm = __ballot(c && before == SL - ncand - 1);
+          next_pos = scan + __ffsll((long long)mm);
+        } else {
+          if (c && before == SL - ncand - 1) s_misc[0] = i + 1;
+          __syncthreads();
+          next_pos = s_misc[0];
+        }
+        ncand = SL;
       } else {
         ncand += cnt;
-        scan += 64;
+        scan += SL;
       }
     }
     if (ncand == 0) break;
     __threadfence_block();
-    __builtin_amdgcn_wave_barrier();
+    block_sync<W>();
     n_rounds++;
     n_spec += ncand;
     // ---- speculative per-lane processing ----
     const long long t0 = clock64();
-    const uint32_t tag = ((0xFFFFFFu - round) << 7) | (uint32_t)lane;
+    // claim tags: a later round's are smaller (stale claims of uncommitted
+    // seeds lose to them), an earlier seed's of the same round smaller
+    const uint32_t tag = ((0x3FFFFFu - round) << 9) | (uint32_t)t;
     const uint32_t myval0 = (tag << 1) | 1u, myval1 = tag << 1;
     int status = kSpecConflict, off = 0, len = 0, touched = 0;
     Rect rec;
     double reg_angle = 0;
     int n = 0;
-    if (lane < ncand) {
-      const uint32_t pt = s_pt[lane];
+    if (t < ncand) {
+      const uint32_t pt = s_pt[t];
       n = lane_grow(F, sd, buf, kLaneCap, (int)(pt & 0xFFFF), (int)(pt >> 16), reg_angle, prec,
                     myval0);
     }
@@ -1447,7 +1500,7 @@ __global__ void __launch_bounds__(64, ORBPL_SPEC_MINW) k_lsd_spec(LsdGeom g, Lsd
       for (int o = 32; o >= 1; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
       max_steps += mx;
     }
-    if (lane < ncand) {
+    if (t < ncand) {
       if (n < 0) {
         status = n;
       } else if (n < g.min_reg_size) {
@@ -1460,13 +1513,13 @@ __global__ void __launch_bounds__(64, ORBPL_SPEC_MINW) k_lsd_spec(LsdGeom g, Lsd
       }
     }
     wg_fence();
-    __builtin_amdgcn_wave_barrier();
+    block_sync<W>();
     const long long t2 = clock64();
     cyc_spec += t1 - t0;
     cyc_fit += t2 - t1;
     // ---- re-read the claims: an earlier seed's smaller stamp = conflict ----
-    bool conflict = lane < ncand && status < 0;
-    if (lane < ncand && status >= 0) {
+    bool conflict = t < ncand && status < 0;
+    if (t < ncand && status >= 0) {
       for (int j0 = 0; j0 < touched && !conflict; j0 += 8) {
         uint32_t ev[8], sv[8];
 #pragma unroll
@@ -1478,14 +1531,24 @@ __global__ void __launch_bounds__(64, ORBPL_SPEC_MINW) k_lsd_spec(LsdGeom g, Lsd
         for (int u = 0; u < 8; u++) conflict |= (sv[u] >> 1) != tag;
       }
     }
-    // ---- commit in seed order ----
-    const unsigned long long cmask = __ballot(conflict);
-    int first = cmask ? __ffsll((long long)cmask) - 1 : ncand;
-    unsigned long long commit = (first >= 64 ? ~0ull : ((1ull << first) - 1ull)) &
-                                (ncand >= 64 ? ~0ull : ((1ull << ncand) - 1ull));
+    // ---- commit in seed order: seeds [lo, hi) ----
+    unsigned long long cmw[W];
+    {
+      const unsigned long long cm1 = __ballot(conflict);
+      if (W == 1) {
+        cmw[0] = cm1;
+      } else {
+        if (lane == 0) s_cm[wv] = cm1;
+        __syncthreads();
+#pragma unroll
+        for (int w = 0; w < W; w++) cmw[w] = s_cm[w];
+      }
+    }
+    int first = next_set<W>(cmw, 0, ncand);
+    int lo = 0, hi = first;
     int stop = ncand;
     while (true) {
-      const bool mine = (commit >> lane) & 1ull;
+      const bool mine = t >= lo && t < hi;
       if (mine && len > 0) {
         for (int j0 = off; j0 < off + len; j0 += 8) {
           uint32_t ev[8];
@@ -1498,9 +1561,22 @@ __global__ void __launch_bounds__(64, ORBPL_SPEC_MINW) k_lsd_spec(LsdGeom g, Lsd
           }
         }
       }
-      const unsigned long long cm = __ballot(mine && status == kSpecCand);
-      if (mine && status == kSpecCand) {
-        const int k = nl + __popcll(cm & lt_mask);
+      const bool is_cand = mine && status == kSpecCand;
+      const unsigned long long cm = __ballot(is_cand);
+      int kbefore = __popcll(cm & lt_mask), ktot = __popcll(cm);
+      if (W > 1) {
+        if (lane == 0) s_km[wv] = cm;
+        __syncthreads();
+        ktot = 0;
+#pragma unroll
+        for (int w = 0; w < W; w++) {
+          const int v = __popcll(s_km[w]);
+          kbefore += w < wv ? v : 0;
+          ktot += v;
+        }
+      }
+      if (is_cand) {
+        const int k = nl + kbefore;
         if (k < kLsdMaxCand) {
           double* o = cand_out + (long long)k * 12;
           o[0] = rec.x1; o[1] = rec.y1; o[2] = rec.x2; o[3] = rec.y2;
@@ -1508,18 +1584,18 @@ __global__ void __launch_bounds__(64, ORBPL_SPEC_MINW) k_lsd_spec(LsdGeom g, Lsd
           o[8] = rec.dx; o[9] = rec.dy; o[10] = rec.prec; o[11] = rec.p;
         }
       }
-      nl += __popcll(cm);
+      nl += ktot;
       __threadfence_block();
-      __builtin_amdgcn_wave_barrier();
+      block_sync<W>();
       if (first >= ncand) break;
       const uint32_t spt = s_pt[first];
       if (used_get(F, (int)(spt & 0xFFFF), (int)(spt >> 16))) {
         // covered by a committed region: the sequential loop skips it
-        const unsigned long long rest = first >= 63 ? 0ull : (cmask & ~((2ull << first) - 1ull));
-        const int nxt = rest ? __ffsll((long long)rest) - 1 : ncand;
-        commit = ((nxt >= 64 ? ~0ull : ((1ull << nxt) - 1ull)) & ~((2ull << first) - 1ull)) &
-                 (ncand >= 64 ? ~0ull : ((1ull << ncand) - 1ull));
+        const int nxt = next_set<W>(cmw, first + 1, ncand);
+        lo = first + 1;
+        hi = nxt;
         first = nxt;
+        if (W > 1) __syncthreads();   // every wave has read the USED bit before new stores
         continue;
       }
       stop = first;
@@ -1528,22 +1604,39 @@ __global__ void __launch_bounds__(64, ORBPL_SPEC_MINW) k_lsd_spec(LsdGeom g, Lsd
     cyc_val += clock64() - t2;
     if (stop < ncand) {
       pos = s_pos[stop];
-      if (__shfl(status, stop, 64) == kSpecOverflow) {
+      int st_stop;
+      if (W == 1) {
+        st_stop = __shfl(status, stop, 64);
+      } else {
+        if (t == stop) s_misc[1] = status;
+        __syncthreads();
+        st_stop = s_misc[1];
+      }
+      if (st_stop == kSpecOverflow) {
         // a region longer than a lane buffer: the wave-cooperative program
-        const uint32_t spt = s_pt[stop];
-        double reg_angle;
-        int n = region_grow(F, (int)(spt & 0xFFFF), (int)(spt >> 16), reg_angle, prec);
-        if (n >= g.min_reg_size) {
-          Rect& rc = *F.rect0;
-          fill_q(F, n);
-          region2rect(F, n, reg_angle, prec, p, rc);
-          if (refine(F, n, reg_angle, prec, p, rc, 0.7)) {
-            if (nl < kLsdMaxCand) {
-              const double* rv = reinterpret_cast<const double*>(F.rect0);
-              if (lane < 12) cand_out[(long long)nl * 12 + lane] = rv[lane];
+        // (wave 0; the lane lists it uses as scratch are idle)
+        if (wv == 0) {
+          const uint32_t spt = s_pt[stop];
+          double reg_angle;
+          int n = region_grow(F, (int)(spt & 0xFFFF), (int)(spt >> 16), reg_angle, prec);
+          if (n >= g.min_reg_size) {
+            Rect& rc = *F.rect0;
+            fill_q(F, n);
+            region2rect(F, n, reg_angle, prec, p, rc);
+            if (refine(F, n, reg_angle, prec, p, rc, 0.7)) {
+              if (nl < kLsdMaxCand) {
+                const double* rv = reinterpret_cast<const double*>(F.rect0);
+                if (lane < 12) cand_out[(long long)nl * 12 + lane] = rv[lane];
+              }
+              nl++;
             }
-            nl++;
           }
+          if (W > 1 && lane == 0) s_misc[1] = nl;
+        }
+        if (W > 1) {
+          __threadfence_block();
+          __syncthreads();
+          nl = s_misc[1];
         }
         n_coop++;
         pos++;
@@ -1552,12 +1645,13 @@ __global__ void __launch_bounds__(64, ORBPL_SPEC_MINW) k_lsd_spec(LsdGeom g, Lsd
       pos = next_pos;
     }
     round++;
+    if (W > 1) __syncthreads();   // s_pt / s_pos / s_misc reads done before the next round
   }
-  if (lane == 0) {
+  if (t == 0) {
     sc.ncand[f] = min(nl, kLsdMaxCand);
     if (nl > kLsdMaxCand) atomicOr(sc.err + f, 8);
   }
-  if (sc.prof && lane == 0) {
+  if (sc.prof && t == 0) {
     long long* pr = sc.prof + f * 8;
     pr[0] = cyc_spec;
     pr[1] = n_rounds;
@@ -1651,13 +1745,17 @@ size_t lsd_grow_smem(const LsdGeom& g) {
 void launch_lsd_grow(const LsdGeom& g, const LsdScratch& sc, int batch, hipStream_t s,
                      bool serial) {
   const size_t smem = serial ? lsd_grow_smem(g) : 2 * sizeof(Rect);
-  const void* k = serial ? (const void*)k_lsd_grow : (const void*)k_lsd_spec;
-  if (smem > 65536)
-    (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   if (serial) {
+    if (smem > 65536)
+      (void)hipFuncSetAttribute((const void*)k_lsd_grow, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)smem);
     hipLaunchKernelGGL(k_lsd_grow, dim3(batch), dim3(64), smem, s, g, sc);
-  } else {
-    hipLaunchKernelGGL(k_lsd_spec, dim3(batch), dim3(64), smem, s, g, sc);
+    return;
+  }
+  switch (lsd_spec_waves(batch)) {
+    case 4: hipLaunchKernelGGL(k_lsd_spec<4>, dim3(batch), dim3(256), smem, s, g, sc); break;
+    case 2: hipLaunchKernelGGL(k_lsd_spec<2>, dim3(batch), dim3(128), smem, s, g, sc); break;
+    default: hipLaunchKernelGGL(k_lsd_spec<1>, dim3(batch), dim3(64), smem, s, g, sc); break;
   }
 }
 

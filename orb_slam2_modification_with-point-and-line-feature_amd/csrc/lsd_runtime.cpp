@@ -256,7 +256,7 @@ int lsdx_create(int width, int height, int max_batch, int device, lsdx_ctx** out
   LA(s.cand_line, B * kLsdMaxCand * 4 * 4);
   LA(s.cand_ok, B * kLsdMaxCand * 4);
   LA(s.sd, B * (size_t)lsd_sd_frame_words(g.sw, g.sh) * 8);
-  LA(s.lbuf, B * kSpecLanes * kLaneCap * sizeof(uint4));
+  LA(s.lbuf, lsd_spec_lane_frames(B) * kSpecLanes * kLaneCap * sizeof(uint4));
   LA(s.sort_local, B * g.seg_cap * sizeof(int4));
   LA(s.sort_nlocal, B * 4);
   LA(s.sort_kt, B * 4);
