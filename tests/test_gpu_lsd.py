@@ -102,6 +102,20 @@ def test_lsd_batch_device_matches_single(orbpl, oracle, frames):
         assert np.array_equal(det.lines(f), oracle.lsd_detect(g))
 
 
+@pytest.mark.parametrize("B", [128, 800], ids=["4_waves_per_frame", "2_waves_per_frame"])
+def test_lsd_batch_multiwave_seed_loop(orbpl, oracle, frames, B):
+    """Mid-size batches run the seed loop with 4 (97-768 frames) or 2 (up to
+    1536) waves per frame (lsd_kernels.h lsd_spec_waves): sampled frames of
+    the batch equal the sequential oracle."""
+    det = orbpl.LineSegmentDetector(640, 480, max_batch=B)
+    buf = orbpl.DeviceBuffer.from_array(np.stack([frames[i % len(frames)] for i in range(B)]))
+    det.detect_batch_device(buf.ptr, B)
+    det.synchronize()
+    ref = [oracle.lsd_detect(g) for g in frames]
+    for f in (0, 1, 2, B // 2, B - 1):
+        assert np.array_equal(det.lines(f), ref[f % len(frames)])
+
+
 def test_lsd_kitti_geometry(orbpl, oracle):
     cfg, traj, fr = sequence(1, 4, cam_name="KITTI00", width=1241, height=376)
     g = fr[0][0]
@@ -165,6 +179,15 @@ def test_lsd_regions_longer_than_a_lane_buffer(orbpl, oracle):
         L = det.detect(img)
         assert np.array_equal(L, oracle.lsd_detect(img))
         assert det.debug_profile()["coop_regions"] > 0
+    # the same with 4 waves per frame (a batch of 128): wave 0 runs the
+    # cooperative program while the others wait
+    B = 128
+    det = orbpl.LineSegmentDetector(640, 480, max_batch=B)
+    buf = orbpl.DeviceBuffer.from_array(np.stack([imgs[i % 2] for i in range(B)]))
+    det.detect_batch_device(buf.ptr, B)
+    det.synchronize()
+    for f in (0, 1, B - 1):
+        assert np.array_equal(det.lines(f), oracle.lsd_detect(imgs[f % 2]))
 
 
 LINE_GOLDEN = sorted((Path(__file__).resolve().parent / "golden").glob("lines_*.npz"))
