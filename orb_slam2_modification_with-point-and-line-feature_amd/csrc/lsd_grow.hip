@@ -1344,11 +1344,14 @@ __global__ void __launch_bounds__(64) k_lsd_grow(LsdGeom g, LsdScratch sc) {
 // speculative regions (24.8k -> 40.5k per frame), so a lone frame gains
 // nothing; with the GPU partly empty the extra waves fill it (batch 256:
 // -5 %, 1024: -10 % per batch).
-// ORBPL_SPEC_MINW: waves per SIMD the register budget must allow (frames in
-// flight per CU = 4x; the loop is latency-bound, so more frames in flight
-// raise throughput until the memory system saturates)
+// ORBPL_SPEC_MINW: waves per SIMD the one-wave-per-frame variant's register
+// budget must allow. 4 (128 VGPRs, a few spills) although the batches that
+// use it hold 3 frames per SIMD: the free quarter of the register file lets
+// the concurrent ORB extraction / tracking waves in beside the seed loop.
+// LSD alone 222.9 -> 235 ms per 3072 frames, but the pipelined lines
+// workload 10.5k -> 11.4k frames/s (A/B on one box, tools/ab_lines_lib.sh).
 #ifndef ORBPL_SPEC_MINW
-#define ORBPL_SPEC_MINW 1
+#define ORBPL_SPEC_MINW 4
 #endif
 // the block's first index >= j whose bit is set in the per-wave masks, or n
 template <int W>
@@ -1372,7 +1375,7 @@ __device__ __forceinline__ void block_sync() {
 }
 
 template <int W>
-__global__ void __launch_bounds__(64 * W, ORBPL_SPEC_MINW) k_lsd_spec(LsdGeom g, LsdScratch sc) {
+__global__ void __launch_bounds__(64 * W, W == 1 ? ORBPL_SPEC_MINW : 1) k_lsd_spec(LsdGeom g, LsdScratch sc) {
   constexpr int SL = 64 * W;
   extern __shared__ uint32_t grow_smem[];
   __shared__ uint32_t s_pt[SL];
