@@ -1337,8 +1337,8 @@ __global__ void __launch_bounds__(64) k_lsd_grow(LsdGeom g, LsdScratch sc) {
 
 
 // Speculative seed loop (see lane_grow): W waves per frame, 64 W seeds per
-// round. W = 1 from 1536 frames per batch on (every frame co-resident, one
-// wave each); mid-size batches take 2 or 4 waves per frame (lsd_spec_waves):
+// round. W = 1 for large batches (every frame co-resident, one wave each);
+// mid-size batches take 4 waves per frame (lsd_spec_waves):
 // a round of 128 / 256 seeds needs 2.4x fewer rounds (388 -> 159 per frame),
 // but each round waits for the slowest of more lanes and wastes more
 // speculative regions (24.8k -> 40.5k per frame), so a lone frame gains

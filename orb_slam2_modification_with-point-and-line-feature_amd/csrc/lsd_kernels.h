@@ -13,23 +13,26 @@ constexpr int kLsdMaxCand = 4096;     // refined rectangles awaiting NFA validat
 constexpr int kSortLocalMax = 2048;   // introsort segments finished in LDS
 constexpr int kSpecLanes = 64;        // speculative regions per round (one wave)
 constexpr int kLaneCap = 2048;        // region points a lane can hold (both grows)
-// waves per frame of the speculative seed loop at a given batch: 4 / 2 while
-// the frames x waves fit the GPU's ~3072 co-resident seed-loop waves, else 1;
-// 1 for small batches too (LSD probe, ms per batch, 1 / 4 / 2 waves vs 1:
-// batch 64 89.8 vs 85.7, 256 86.9 vs 91.2, 1024 124.7 vs 138.0; batch 1 equal)
+// waves per frame of the speculative seed loop at a given batch: 4 for 97-384
+// frames (at most half the GPU's ~3072 co-resident seed-loop waves, so a
+// second LSD batch - the stereo right images - still fits beside it), else 1.
+// LSD probe (ms per batch, 4 / 2 waves vs 1): batch 64 89.8 vs 85.7, 256 86.9
+// vs 91.2, 1024 (2 waves) 124.7 vs 138.0, batch 1 equal; but the stereo
+// workload's two concurrent 1024-frame LSD batches at 2 waves each
+// oversubscribe the GPU (seed loop 128 -> 201 ms per step), so 2 waves are
+// not used by default.
 #ifndef ORBPL_SPEC_WAVES
 #define ORBPL_SPEC_WAVES 0   // 0 = by batch; 1, 2 or 4 forces it (A/B)
 #endif
 __host__ __device__ inline int lsd_spec_waves(int batch) {
   if (ORBPL_SPEC_WAVES) return ORBPL_SPEC_WAVES;
-  return batch <= 96 ? 1 : (batch <= 768 ? 4 : (batch <= 1536 ? 2 : 1));
+  return (batch > 96 && batch <= 384) ? 4 : 1;
 }
 // lane lists to allocate for batches up to B: the largest batch x waves
 __host__ __device__ inline long long lsd_spec_lane_frames(int B) {
-  long long m = 0;
-  for (int b : {B, B < 768 ? B : 768, B < 1536 ? B : 1536})
-    m = m > (long long)b * lsd_spec_waves(b) ? m : (long long)b * lsd_spec_waves(b);
-  return m;
+  const int b4 = B < 384 ? B : 384;
+  const long long m1 = (long long)B * lsd_spec_waves(B), m4 = (long long)b4 * lsd_spec_waves(b4);
+  return m1 > m4 ? m1 : m4;
 }
 constexpr int kLineKeep = 80;         // LineExtractor.cpp:24
 constexpr int kLsdSortChunk = 256;    // elements per partition chunk

@@ -102,11 +102,11 @@ def test_lsd_batch_device_matches_single(orbpl, oracle, frames):
         assert np.array_equal(det.lines(f), oracle.lsd_detect(g))
 
 
-@pytest.mark.parametrize("B", [128, 800], ids=["4_waves_per_frame", "2_waves_per_frame"])
+@pytest.mark.parametrize("B", [128, 800], ids=["4_waves_per_frame", "1_wave_per_frame"])
 def test_lsd_batch_multiwave_seed_loop(orbpl, oracle, frames, B):
-    """Mid-size batches run the seed loop with 4 (97-768 frames) or 2 (up to
-    1536) waves per frame (lsd_kernels.h lsd_spec_waves): sampled frames of
-    the batch equal the sequential oracle."""
+    """Batches of 97-384 frames run the seed loop with 4 waves per frame,
+    larger ones with one (lsd_kernels.h lsd_spec_waves): sampled frames of the
+    batch equal the sequential oracle."""
     det = orbpl.LineSegmentDetector(640, 480, max_batch=B)
     buf = orbpl.DeviceBuffer.from_array(np.stack([frames[i % len(frames)] for i in range(B)]))
     det.detect_batch_device(buf.ptr, B)
