@@ -61,21 +61,26 @@ def test_gpus_flag_builds_torchrun_command():
 def test_torchrun_two_ranks_env_contract():
     """torch.distributed.run with 2 ranks on CPU: each rank sees the env that
     bench.py reads and reaches the gloo barrier."""
+    tmp = Path(os.environ.get("TMPDIR", "/tmp"))
+    tag = f"orbpl_ws2_{os.getpid()}"
+    # each rank writes its own file (the ranks' shared stdout can interleave)
     code = ("import os, torch.distributed as d; d.init_process_group('gloo'); d.barrier(); "
-            "print('rank', os.environ['RANK'], os.environ['LOCAL_RANK'], os.environ['WORLD_SIZE'])")
-    script = Path(os.environ.get("TMPDIR", "/tmp")) / f"orbpl_ws2_{os.getpid()}.py"
+            f"open(os.path.join({str(tmp)!r}, '{tag}_' + os.environ['RANK'] + '.txt'), 'w').write("
+            "' '.join(['rank', os.environ['RANK'], os.environ['LOCAL_RANK'], os.environ['WORLD_SIZE']]))")
+    script = tmp / f"{tag}.py"
     script.write_text(code)
+    outs = [tmp / f"{tag}_{r}.txt" for r in range(2)]
     try:
         out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                               "--nproc-per-node=2", "--master-addr", "127.0.0.1", "--master-port",
                               str(_port()), str(script)], capture_output=True, text=True,
                              timeout=180)
+        assert out.returncode == 0, out.stderr[-2000:]
+        lines = [o.read_text() for o in outs]
     finally:
         script.unlink()
-    assert out.returncode == 0, out.stderr[-2000:]
-    # the two ranks share stdout: their lines may interleave
-    import re
-    lines = sorted(re.findall(r"rank \d \d \d", out.stdout))
+        for o in outs:
+            o.unlink(missing_ok=True)
     assert lines == ["rank 0 0 2", "rank 1 1 2"]
 
 
