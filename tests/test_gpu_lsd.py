@@ -116,6 +116,19 @@ def test_lsd_batch_multiwave_seed_loop(orbpl, oracle, frames, B):
         assert np.array_equal(det.lines(f), ref[f % len(frames)])
 
 
+def test_lsd_batch_multiwave_kitti(orbpl, oracle):
+    """4 waves per frame on the KITTI geometry (1241x376: ragged tiles)."""
+    kit = [sequence(1, s, cam_name="KITTI00", width=1241, height=376)[2][0][0] for s in (4, 5)]
+    B = 128
+    det = orbpl.LineSegmentDetector(1241, 376, max_batch=B)
+    buf = orbpl.DeviceBuffer.from_array(np.stack([kit[i % 2] for i in range(B)]))
+    det.detect_batch_device(buf.ptr, B)
+    det.synchronize()
+    ref = [oracle.lsd_detect(g) for g in kit]
+    for f in (0, 1, B - 2, B - 1):
+        assert np.array_equal(det.lines(f), ref[f % 2])
+
+
 def test_lsd_kitti_geometry(orbpl, oracle):
     cfg, traj, fr = sequence(1, 4, cam_name="KITTI00", width=1241, height=376)
     g = fr[0][0]
