@@ -162,6 +162,14 @@ def algorithmic_bytes(n_kp, w=W, h=H, orb=ORB, n_lines=80):
         "match": n_kp * (72 + 78),
         # per keypoint: kp 28 + ur 4 + match 4 + xyz 12 + outlier 2
         "pose": n_kp * 50,
+        # every k_pose launch of the step: TrackWithMotionModel's and
+        # TrackLocalMap's over all keypoints (TrackReferenceKeyFrame's runs
+        # only where the motion model failed: counted as 0 bytes)
+        "pose_all": n_kp * 50 * 2,
+        # SearchLocalPoints: the frame (kp 28 + desc 32 + ur 4 + nobs 4 + match
+        # out 4) and ~4 local map points per keypoint (desc 32, projection +
+        # level + view cos + in-view 25 B)
+        "match_local": n_kp * 72 + 4 * n_kp * 57,
         # LSD: read the image, write the scaled u8 image, the angle (f32) and
         # the gradient-norm key (i32) per scaled pixel
         "lsd_prep": A0 + sA * 9,
@@ -182,8 +190,24 @@ def algorithmic_bytes(n_kp, w=W, h=H, orb=ORB, n_lines=80):
     }
 
 
+def frame_bytes(n_kp, w=W, h=H, orb=ORB, lines=False, stereo=False):
+    """SURVEY.md §8(d) whole-frame algorithmic bytes: B_orb = 7 S - A_last +
+    60 N (read the input, write levels 1-7, read levels 0-6 for the resize,
+    FAST read, blur read + write, orientation read, descriptor read, 28 B
+    keypoint + 32 B descriptor out); lines add LSD A0 + 6 (0.64 A0) 4 +
+    2 (0.64 A0) and LBD A0 + 8 A0. Stereo extracts both images."""
+    areas, _ = level_areas(w, h, orb)
+    S = sum(areas)
+    A0 = w * h
+    b = 7 * S - areas[-1] + 60 * n_kp
+    if lines:
+        b += A0 + 6 * 0.64 * A0 * 4 + 2 * 0.64 * A0 + A0 + 8 * A0
+    return int(b * (2 if stereo else 1))
+
+
 KERNELS = {"pyramid": "k_pyramid", "fast": "k_fast_cells", "octree": "k_octree",
            "orient_desc": "k_orient_desc", "match": "k_match_last", "pose": "k_pose",
+           "pose_all": "k_pose", "match_local": "k_match_local",
            "lsd_prep": "k_lsd_blur+k_lsd_resize+k_lsd_grad", "lsd_sort": "k_lsd_sort+k_lsd_sort_local",
            "lsd_seed": "k_lsd_spec", "lsd_validate": "k_lsd_validate+k_lsd_compact",
            "keylines": "k_keylines", "lbd": "k_lsd_blur+k_sobel+k_lbd",
@@ -418,10 +442,9 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
     tr = pkg.Tracker(pkg.OrbParams(*wl["orb"]), cam, S, device=device, lines=lines, stereo=stereo,
                      local_map=bool(args.local_map), fixed_line_jac=bool(args.fixed_line_jacobian),
                      refkf=bool(args.refkf and voc is not None))
-    # pipelining overlaps extraction of step t+1 with tracking of step t; the
-    # LSD-bound line workloads gain nothing from it
-    # pipelined for every workload (lines too: the next batch's LSD overlaps
-    # this batch's matching and pose, 9.5k -> 9.8k frames/s at 3072 streams)
+    # pipelining overlaps extraction of step t+1 with tracking of step t, for
+    # every workload (lines too: the next batch's LSD overlaps this batch's
+    # matching and pose, 9.5k -> 9.8k frames/s at 3072 streams)
     pipelined = args.pipelined if args.pipelined >= 0 else 1
     tr.set_pipelined(bool(pipelined))
     if voc is not None:
@@ -454,10 +477,21 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
     t1 = time.perf_counter()
     elapsed = max_over_ranks(dist, t1 - t0)
     st = tr.state()
-    tim = tr.timings(steps)                            # (steps, 9) ms, in-stream hipEvents
+    tim = tr.timings(steps)                            # (steps, 11) ms, in-stream hipEvents
     avg = tim.mean(0)
     stages = dict(zip(tr.STAGES, [round(float(x), 4) for x in avg]))
     stage_avg = dict(zip(tr.STAGES, [float(x) for x in avg]))
+
+    def kernel_sums(kt):
+        """GPU time per step of the kernels that run in several stages:
+        k_pose summed over its launches, k_match_local alone."""
+        k = dict(zip(tr.KERNEL_STAGES, [float(x) for x in kt.mean(0)]))
+        return {"pose_all": k["pose_motion"] + k["pose_refkf"] + k["pose_local"],
+                "match_local": k["match_local"]}, k
+
+    ksum, kraw = kernel_sums(tr.kernel_timings(steps))
+    stage_avg.update(ksum)
+    stages.update({f"kernel_{k}": round(v, 4) for k, v in kraw.items()})
     tracking = {"mean_keypoints": float(st["nkeypoints"].mean()),
                 "mean_matches": float(st["nmatches"].mean()),
                 "mean_inliers": float(st["ninliers"].mean()),
@@ -491,7 +525,12 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
     # roofline of the dominant single-stage kernel
     n_kp = float(st["nkeypoints"].mean())
     ab = algorithmic_bytes(n_kp, fw, fh, wl["orb"])
-    cand = ["pyramid", "fast", "octree", "orient_desc", "match", "pose"]
+    # candidates: every kernel's GPU time per step, a kernel launched in
+    # several stages (k_pose: motion model, reference keyframe, local map)
+    # counted once with all its launches
+    cand = ["pyramid", "fast", "octree", "orient_desc", "match", "pose_all"]
+    if args.local_map:
+        cand.append("match_local")
     if lines:
         cand += list(tr.LSD_STAGES)
     iso = None
@@ -507,6 +546,7 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
             step(warmup + steps + k)
         tr.synchronize()
         iso = dict(zip(tr.STAGES, [float(x) for x in tr.timings(args.isolated_steps).mean(0)]))
+        iso.update(kernel_sums(tr.kernel_timings(args.isolated_steps))[0])
         if lines:
             iso.update(zip(tr.LSD_STAGES,
                            [float(x) for x in tr.lsd_timings(args.isolated_steps).mean(0)]))
@@ -516,7 +556,11 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
     bytes_launch = int(ab[dom] * S)
     achieved = bytes_launch / (dom_ms * 1e-3) / 1e9
     traffic, tsrc = pmc_traffic(KERNELS[dom], workload, S)
+    if traffic and dom == "pose_all":
+        traffic *= 2          # the PMC summary is per launch; two full launches per step
+    fbytes = frame_bytes(n_kp, fw, fh, wl["orb"], lines, stereo)
     roof = {"bound": "hbm", "kernel": KERNELS[dom], "stage": dom,
+            "dominance": "summed per-kernel GPU time per step (isolated steps when pipelined)",
             "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
             "traffic_source": tsrc,
@@ -524,6 +568,13 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
             "algorithmic_bytes_per_launch": bytes_launch, "avg_launch_ms": round(dom_ms, 4),
             "per_kernel_GBps": {k: round(ab[k] * S / (stage_avg[k] * 1e-3) / 1e9, 1)
                                 for k in cand if stage_avg[k] > 0}}
+    # whole pipeline: B_frame x frames/s against 8 TB/s
+    per_gpu = S * steps / elapsed
+    roof["pipeline"] = {"bytes_per_frame": fbytes, "frames_per_s_per_gpu": round(per_gpu, 1),
+                        "achieved": round(fbytes * per_gpu / 1e9, 2), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(fbytes * per_gpu / 1e9 / HBM_PEAK_GBS, 5),
+                        "formula": "SURVEY.md 8(d): 7 S - A_last + 60 N (+ LSD/LBD for lines; "
+                                   "x2 for stereo)"}
     if iso is not None:
         ims = iso[dom]
         roof["isolated"] = {
@@ -703,10 +754,12 @@ def cpu_baseline(seconds, threads, gray, depth, L, workload="points", flags=0):
     return sum(counts) / dt, sum(counts), dt
 
 
-def cpu_reference_faithful(seconds, gray, depth, L, workload, flags=0):
+def cpu_reference_faithful(gray, depth, L, workload, flags=0, warmup=20, frames=300):
     """BASELINE.md §2 mode 1: one stream as the reference runs it, ORB and
     the LineExtractor on two host threads per frame (Frame.cc:152-155),
-    matching and pose on the tracking thread; per-frame latency."""
+    matching and pose on the tracking thread; per-frame latency with
+    std::chrono-like perf_counter over `frames` frames after `warmup` untimed
+    ones (20 warm-up, >= 300 timed; the loop wraps)."""
     from _pkg import load_oracle
     import orbpl.synth as synth
     O = load_oracle()
@@ -718,23 +771,21 @@ def cpu_reference_faithful(seconds, gray, depth, L, workload, flags=0):
         vo.set_vocabulary(voc)
     vo.reset(np.linalg.inv(L.Twc(0, 0)).astype(np.float32).reshape(1, 16))
     lat = []
-    stop = time.time() + seconds
-    i = 0
-    while time.time() < stop or i < 3:
+    for i in range(warmup + frames):
         e = L.elem(0, i)
         t0 = time.perf_counter()
         if wl["stereo"]:
             vo.step_stereo(0, gray[e], depth[e])
         else:
             vo.step(0, gray[e], depth[e])
-        lat.append(time.perf_counter() - t0)
-        i += 1
-    lat = np.array(lat[2:]) * 1e3   # the first frames have no last frame
+        if i >= warmup:
+            lat.append(time.perf_counter() - t0)
+    lat = np.array(lat) * 1e3
     return {"value": round(1e3 / float(lat.mean()), 2), "unit": "frames/s",
             "threads_per_frame": 2 if wl["lines"] else 1,
             "median_ms_per_frame": round(float(np.median(lat)), 3),
             "mean_ms_per_frame": round(float(lat.mean()), 3), "frames": int(len(lat)),
-            "sample": f"one stream, {len(lat)} frames after 2 warm-up frames"}
+            "sample": f"one stream, {len(lat)} frames after {warmup} warm-up frames"}
 
 
 def _free_port():
@@ -755,6 +806,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the host's usable cores")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-ref-frames", type=int, default=300,
+                    help="timed frames of the reference-faithful one-stream CPU run (BASELINE.md "
+                         "§2: >= 300 after 20 warm-up)")
+    ap.add_argument("--cpu-ref-warmup", type=int, default=20)
     ap.add_argument("--workload", choices=tuple(WORKLOADS), default="points",
                     help="points = configs[1] (headline); lines = configs[2] ORB + LSD/LBD; "
                          "kitti = configs[3] stereo points+lines; rig = configs[4] 1280x720 rig")
@@ -881,9 +936,10 @@ def main():
                "build": f"oracle/_build ({oracle_build}: -O3 -march=x86-64-{oracle_build})"
                         if oracle_build != "O2" else "oracle/_build (-O2)",
                "host": host,
-               "reference_faithful": cpu_reference_faithful(args.cpu_seconds / 4, res["gray"],
-                                                            res["depth"], res["layout"],
-                                                            args.workload, ofl)}
+               "reference_faithful": cpu_reference_faithful(res["gray"], res["depth"],
+                                                            res["layout"], args.workload, ofl,
+                                                            args.cpu_ref_warmup,
+                                                            args.cpu_ref_frames)}
 
     if rank == 0:
         S = res["S"]
@@ -944,7 +1000,8 @@ def main():
                     "sample": f"{nfr} frames in {dt:.1f} s, oracle/ C++ restatement "
                               f"({o['wname']} workload), one stream per thread",
                     "reference_faithful": cpu_reference_faithful(
-                        args.cpu_seconds / 4, o["gray"], o["depth"], o["layout"], o["wname"], ofl)}
+                        o["gray"], o["depth"], o["layout"], o["wname"], ofl, args.cpu_ref_warmup,
+                        args.cpu_ref_frames)}
         print(json.dumps(out))
     if dist:
         dist.destroy_process_group()

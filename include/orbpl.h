@@ -64,7 +64,9 @@ typedef struct orbpl_orb_params {
 const char* orbpl_last_error(void);
 /* Number of visible HIP devices. */
 int orbpl_device_count(int* n);
-/* Library build tag (e.g. "orbpl gfx950 r1"). */
+/* Library build tag ("orbpl gfx950 r3"). r3: orbpl_tracker_timings writes 11
+ * floats per step, orbpl_tracker_stereo_timings 4 (r1: 9 and 2); size the
+ * buffers from orbpl_tracker_timing_counts. */
 const char* orbpl_version(void);
 
 /* Device memory plumbing for hosts without their own GPU allocator (the
@@ -444,6 +446,17 @@ int orbpl_tracker_stage_ms(orbpl_tracker* tr, float* ms5);
  * glue. */
 int orbpl_tracker_timings(orbpl_tracker* tr, int max_steps, float* ms, int* n_steps);
 int orbpl_tracker_timings_reset(orbpl_tracker* tr);
+/* Floats per step written by orbpl_tracker_timings, _line_timings,
+ * _lsd_timings, _stereo_timings and _kernel_timings (in that order): 11, 3, 7,
+ * 4, 4. A caller sizes its buffers max_steps x these. */
+int orbpl_tracker_timing_counts(int* counts5);
+/* Per-kernel device times (ms) of the last min(max_steps, 64) steps, 4 per
+ * step, each launch bracketed by its own hipEvents on the tracking stream:
+ * k_pose of TrackWithMotionModel, k_pose of TrackReferenceKeyFrame (0 without
+ * ORBPL_TRACK_REFKF), k_pose of TrackLocalMap and k_match_local (0 without
+ * ORBPL_TRACK_LOCAL_MAP). Summed per kernel they give a kernel's GPU time per
+ * step across the stages it runs in. */
+int orbpl_tracker_kernel_timings(orbpl_tracker* tr, int max_steps, float* ms, int* n_steps);
 /* Debug (ORBPL_POSE_PROFILE set): stream 0's PoseOptimization phase times of
  * the last step in ns (edges, linearize reduction, solve+exp, trial errors,
  * classify), the LM iteration / trial counts, the linearize edge loop (ns). */
@@ -506,7 +519,8 @@ int orbpl_tracker_get_local_stats(orbpl_tracker* tr, int* local_matches, int* lo
  * Sobel + LBD, UndistortKeyLines + line depths. */
 int orbpl_tracker_lsd_timings(orbpl_tracker* tr, int max_steps, float* ms, int* n_steps);
 /* Stereo stage device times (ms) of the last min(max_steps, 64) steps, 4 per
- * step: right-image ORB extraction, ComputeStereoMatches, and with
+ * step: right-image ORB extraction, ComputeStereoMatches (KeyFrame::ComputeBoW
+ * is the bow entry of orbpl_tracker_timings), and with
  * ORBPL_TRACK_LINES the right-image LineExtractor and the stereo line depths
  * (k_stereo_lines); 0 without lines. */
 int orbpl_tracker_stereo_timings(orbpl_tracker* tr, int max_steps, float* ms, int* n_steps);

@@ -21,7 +21,7 @@
 #include <thread>
 #include <vector>
 
-#include "../orb_slam2_modification_with-point-and-line-feature_amd/csrc/lsd_math.h"
+#include "pinned_math.h"
 #include "oracle_api.h"
 
 namespace line_track {
@@ -32,7 +32,7 @@ static int popcnt_dist(const uint8_t* a, const uint8_t* b) {
   return d;
 }
 
-static float atan2f_pinned(float y, float x) { return (float)lsdm::atan2_((double)y, (double)x); }
+static float atan2f_pinned(float y, float x) { return (float)pmath::atan2_((double)y, (double)x); }
 
 // fields recomputed from the end points (UpdateKeyLineData / UndistortKeyLines)
 static void refresh_keyline(orbpl_keyline& kl, int W, int H) {
@@ -614,7 +614,7 @@ static bool track_local_map(LVO* v, LStream& S, bool stereo, int n,
   std::vector<uint8_t> inview(nloc);
   std::vector<float> px(nloc), py(nloc), pxr(nloc), vcos(nloc);
   std::vector<int32_t> lev(nloc), mp_nobs(nloc, 1), lm(n, -1);
-  const float log_scale = (float)lsdm::log_((double)v->orb.scale_factor);   // P15
+  const float log_scale = (float)pmath::log_((double)v->orb.scale_factor);   // P15
   oracle_frame_is_in_frustum(&cam, log_scale, nlev, S.Tcw, nloc, Lx.data(), Ln.data(), Lmin.data(),
                              Lmax.data(), 0.5f, inview.data(), px.data(), py.data(), pxr.data(),
                              lev.data(), vcos.data());

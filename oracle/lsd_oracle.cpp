@@ -25,8 +25,9 @@
 // fixtures). Pinned semantic choices (DESIGN.md §Pinned semantics):
 //   P2  float cos/sin = correctly rounded, computed as (float)cos((double)x).
 //   P9  LSD resize = INTER_LINEAR_EXACT 8U (bit-exact resize, 8-bit coefficients).
-//   P10 double sin/cos/exp/log/log10/atan2 = the fdlibm algorithms of
-//       csrc/lsd_math.h (<= 1 ulp from glibc; identical on host and device).
+//   P10 double sin/cos/exp/log/log10/atan2 = the fdlibm algorithms, the
+//       oracle's own transcription in pinned_math.h (the product has its own
+//       in csrc/lsd_math.h; the oracle includes nothing from csrc/).
 //   P11 pow(x, integer) = binary exponentiation; sinh = odd Taylor series.
 //   P12 atan2f (KeyLine::angle) = (float)atan2((double)y, (double)x) (P10).
 //   P13 rect_nfa walks the rectangle with double-valued edge steps and the
@@ -41,7 +42,7 @@
 #include <cstring>
 #include <vector>
 
-#include "../orb_slam2_modification_with-point-and-line-feature_amd/csrc/lsd_math.h"
+#include "pinned_math.h"
 #include "oracle_api.h"
 
 namespace lsdo {
@@ -57,8 +58,8 @@ static inline int reflect101(int i, int n) {
   return i;
 }
 
-static inline float cosf_cr(float x) { return (float)std::cos((double)x); }
-static inline float sinf_cr(float x) { return (float)std::sin((double)x); }
+static inline float cosf_cr(float x) { return pmath::cosf_cr(x); }
+static inline float sinf_cr(float x) { return pmath::sinf_cr(x); }
 
 // ---------------------------------------------------------------------------
 // GaussianBlur, 8U fixed-point path (OpenCV >= 3.4.2 smooth.cpp): kernel in
@@ -70,7 +71,7 @@ void fixed_gauss_kernel(int n, double sigma, int* k) {
   std::vector<double> values(n2 + 1);
   double sum = 0;
   for (int i = 0, x = 1 - n; i < n2; i++, x += 2) {
-    values[i] = lsdm::exp_((double)(x * x) * scale2X);
+    values[i] = pmath::exp_((double)(x * x) * scale2X);
     sum += values[i];
   }
   sum *= 2;
@@ -214,19 +215,19 @@ static inline double distSq(double x1, double y1, double x2, double y2) {
 }
 
 static inline double log_gamma_windschitl(double x) {
-  return 0.918938533204673 + (x - 0.5) * lsdm::log_(x) - x +
-         0.5 * x * lsdm::log_(x * lsdm::sinh_(1 / x) + 1 / (810.0 * lsdm::powi_(x, 6.0)));
+  return 0.918938533204673 + (x - 0.5) * pmath::log_(x) - x +
+         0.5 * x * pmath::log_(x * pmath::sinh_(1 / x) + 1 / (810.0 * pmath::powi(x, 6.0)));
 }
 static inline double log_gamma_lanczos(double x) {
   static const double q[7] = {75122.6331530, 80916.6278952, 36308.2951477, 8687.24529705,
                               1168.92649479, 83.8676043424, 2.50662827511};
-  double a = (x + 0.5) * lsdm::log_(x + 5.5) - (x + 5.5);
+  double a = (x + 0.5) * pmath::log_(x + 5.5) - (x + 5.5);
   double b = 0;
   for (int n = 0; n < 7; ++n) {
-    a -= lsdm::log_(x + double(n));
-    b += q[n] * lsdm::powi_(x, double(n));
+    a -= pmath::log_(x + double(n));
+    b += q[n] * pmath::powi(x, double(n));
   }
-  return a + lsdm::log_(b);
+  return a + pmath::log_(b);
 }
 static inline double log_gamma(double x) {
   return x > 15.0 ? log_gamma_windschitl(x) : log_gamma_lanczos(x);
@@ -311,8 +312,8 @@ struct LSD {
     seed.angle = reg_angle;
     seed.modgrad = modgrad[(size_t)sy * W + sx];
     reg.push_back(seed);
-    float sumdx = float(lsdm::cos_(reg_angle));
-    float sumdy = float(lsdm::sin_(reg_angle));
+    float sumdx = float(pmath::cos_(reg_angle));
+    float sumdy = float(pmath::sin_(reg_angle));
     *seed.used = USED;
     for (size_t i = 0; i < reg.size(); i++) {
       const RegionPoint rpoint = reg[i];
@@ -371,7 +372,7 @@ struct LSD {
     x /= sum;
     y /= sum;
     const double theta = get_theta(reg, x, y, reg_angle, prec);
-    const double dx = lsdm::cos_(theta), dy = lsdm::sin_(theta);
+    const double dx = pmath::cos_(theta), dy = pmath::sin_(theta);
     double l_min = 0, l_max = 0, w_min = 0, w_max = 0;
     for (size_t i = 0; i < reg.size(); ++i) {
       const double regdx = double(reg[i].x) - x, regdy = double(reg[i].y) - y;
@@ -450,12 +451,12 @@ struct LSD {
 
   double nfa(int n, int k, double p) const {
     if (n == 0 || k == 0) return -LOG_NT;
-    if (n == k) return -LOG_NT - double(n) * lsdm::log10_(p);
+    if (n == k) return -LOG_NT - double(n) * pmath::log10_(p);
     const double p_term = p / (1 - p);
     const double log1term = log_gamma(double(n) + 1) - log_gamma(double(k) + 1) -
-                            log_gamma(double(n - k) + 1) + double(k) * lsdm::log_(p) +
-                            double(n - k) * lsdm::log_(1.0 - p);
-    double term = lsdm::exp_(log1term);
+                            log_gamma(double(n - k) + 1) + double(k) * pmath::log_(p) +
+                            double(n - k) * pmath::log_(1.0 - p);
+    double term = pmath::exp_(log1term);
     if (double_equal(term, 0)) {
       if (k > n * p) return -log1term / 2.30258509299404568402 - LOG_NT;
       return -LOG_NT;
@@ -469,11 +470,11 @@ struct LSD {
       bin_tail += term;
       if (bin_term < 1) {
         const double err =
-            term * ((1 - lsdm::powi_(mult_term, double(n - i + 1))) / (1 - mult_term) - 1);
-        if (err < tolerance * std::fabs(-lsdm::log10_(bin_tail) - LOG_NT) * bin_tail) break;
+            term * ((1 - pmath::powi(mult_term, double(n - i + 1))) / (1 - mult_term) - 1);
+        if (err < tolerance * std::fabs(-pmath::log10_(bin_tail) - LOG_NT) * bin_tail) break;
       }
     }
-    return -lsdm::log10_(bin_tail) - LOG_NT;
+    return -pmath::log10_(bin_tail) - LOG_NT;
   }
 
   double rect_nfa(const Rect& rec) const {
@@ -626,11 +627,11 @@ struct LSD {
     lines.clear();
     const double prec = kPi * ANG_TH / 180;
     const double p = ANG_TH / 180;
-    const double rho = QUANT / lsdm::sin_(prec);
+    const double rho = QUANT / pmath::sin_(prec);
     // Gaussian sub-sampling
     const double sigma = (SCALE < 1) ? (SIGMA_SCALE / SCALE) : SIGMA_SCALE;
     const double sprec = 3;
-    const unsigned h = (unsigned)std::ceil(sigma * std::sqrt(2 * sprec * lsdm::log_(10.0)));
+    const unsigned h = (unsigned)std::ceil(sigma * std::sqrt(2 * sprec * pmath::log_(10.0)));
     const int ksize = 1 + 2 * (int)h;
     std::vector<int> k(ksize);
     fixed_gauss_kernel(ksize, sigma, k.data());
@@ -641,9 +642,9 @@ struct LSD {
     scaled.assign((size_t)img_width * img_height, 0);
     resize_exact(g.data(), W, H, SCALE, scaled.data(), img_width, img_height);
     ll_angle(rho);
-    LOG_NT = 5 * (lsdm::log10_(double(img_width)) + lsdm::log10_(double(img_height))) / 2 +
-             lsdm::log10_(11.0);
-    const size_t min_reg_size = size_t(-LOG_NT / lsdm::log10_(p));
+    LOG_NT = 5 * (pmath::log10_(double(img_width)) + pmath::log10_(double(img_height))) / 2 +
+             pmath::log10_(11.0);
+    const size_t min_reg_size = size_t(-LOG_NT / pmath::log10_(p));
     used.assign((size_t)img_width * img_height, NOTUSED);
     std::vector<RegionPoint> reg;
     for (size_t i = 0; i < ordered.size(); ++i) {
@@ -742,14 +743,14 @@ void lbd_weights(float* gL /*21*/, float* gG /*63*/) {
   double invsigma2 = -1 / (2 * sigma * sigma);
   for (int i = 0; i < kBandW * 3; i++) {
     const double dis = i - u;
-    gL[i] = (float)lsdm::exp_(dis * dis * invsigma2);
+    gL[i] = (float)pmath::exp_(dis * dis * invsigma2);
   }
   u = (kBands * kBandW - 1) / 2;
   sigma = u;
   invsigma2 = -1 / (2 * sigma * sigma);
   for (int i = 0; i < kBands * kBandW; i++) {
     const double dis = i - u;
-    gG[i] = (float)lsdm::exp_(dis * dis * invsigma2);
+    gG[i] = (float)pmath::exp_(dis * dis * invsigma2);
   }
 }
 
@@ -913,9 +914,9 @@ int oracle_lsd_stages(const uint8_t* img, int W, int H, uint8_t* scaled, double*
                       uint32_t* order, int* sw, int* sh, int* n_order) {
   LSD lsd;
   const double prec = kPi * lsd.ANG_TH / 180;
-  const double rho = lsd.QUANT / lsdm::sin_(prec);
+  const double rho = lsd.QUANT / pmath::sin_(prec);
   const double sigma = lsd.SIGMA_SCALE / lsd.SCALE;
-  const unsigned h = (unsigned)std::ceil(sigma * std::sqrt(2 * 3.0 * lsdm::log_(10.0)));
+  const unsigned h = (unsigned)std::ceil(sigma * std::sqrt(2 * 3.0 * pmath::log_(10.0)));
   const int ksize = 1 + 2 * (int)h;
   std::vector<int> k(ksize);
   fixed_gauss_kernel(ksize, sigma, k.data());
@@ -960,7 +961,7 @@ int oracle_line_extract(const uint8_t* img, int W, int H, orbpl_keyline* kl_out,
     const double ddx = (double)(e[0] - e[2]), ddy = (double)(e[1] - e[3]);
     kl.lineLength = (float)std::sqrt(ddx * ddx + ddy * ddy);
     kl.numOfPixels = line_iterator_count(W, H, e[0], e[1], e[2], e[3]);
-    kl.angle = (float)lsdm::atan2_((double)(kl.endPointY - kl.startPointY),
+    kl.angle = (float)pmath::atan2_((double)(kl.endPointY - kl.startPointY),
                                    (double)(kl.endPointX - kl.startPointX));
     kl.class_id = k;
     kl.octave = 0;
@@ -1006,16 +1007,38 @@ int oracle_line_extract(const uint8_t* img, int W, int H, orbpl_keyline* kl_out,
 // pinned math, exported for the accuracy tests
 double oracle_lsdm(int fn, double x, double y) {
   switch (fn) {
-    case 0: return lsdm::exp_(x);
-    case 1: return lsdm::log_(x);
-    case 2: return lsdm::log10_(x);
-    case 3: return lsdm::sin_(x);
-    case 4: return lsdm::cos_(x);
-    case 5: return lsdm::atan2_(y, x);
-    case 6: return lsdm::sinh_(x);
-    case 7: return lsdm::powi_(x, y);
+    case 0: return pmath::exp_(x);
+    case 1: return pmath::log_(x);
+    case 2: return pmath::log10_(x);
+    case 3: return pmath::sin_(x);
+    case 4: return pmath::cos_(x);
+    case 5: return pmath::atan2_(y, x);
+    case 6: return pmath::sinh_(x);
+    case 7: return pmath::powi(x, y);
     default: return 0;
   }
+}
+
+// divergence probe (pinned_math.h): on != 0 starts counting (and resets the
+// counters), on == 0 stops; oracle_math_probe_read fills per function (exp,
+// log, log10, sin, cos, atan2, cosf, sinf) calls, results differing from
+// glibc, and the largest difference in ulps.
+int oracle_math_probe(int on) {
+  pmath::Probe& p = pmath::probe();
+  if (on)
+    for (int i = 0; i < pmath::kNumFn; i++) p.calls[i] = p.differ[i] = p.max_ulp[i] = 0;
+  p.on = on ? 1 : 0;
+  return 0;
+}
+
+int oracle_math_probe_read(long long* calls, long long* differ, long long* max_ulp) {
+  pmath::Probe& p = pmath::probe();
+  for (int i = 0; i < pmath::kNumFn; i++) {
+    calls[i] = p.calls[i];
+    differ[i] = p.differ[i];
+    max_ulp[i] = p.max_ulp[i];
+  }
+  return pmath::kNumFn;
 }
 
 int oracle_line_iterator_count(int W, int H, float x1, float y1, float x2, float y2) {

@@ -67,6 +67,8 @@ int oracle_lsd_stages(const uint8_t* img, int W, int H, uint8_t* scaled, double*
 int oracle_line_extract(const uint8_t* img, int W, int H, orbpl_keyline* kl_out, uint8_t* desc,
                         double* coef, int cap, int* n_out, int* n_detected);
 double oracle_lsdm(int fn, double x, double y);
+int oracle_math_probe(int on);
+int oracle_math_probe_read(long long* calls, long long* differ, long long* max_ulp);
 int oracle_line_iterator_count(int W, int H, float x1, float y1, float x2, float y2);
 int oracle_introsort_perm(const int* keys, int n, int* perm);
 /* line tracking (line_track_oracle.cpp) */

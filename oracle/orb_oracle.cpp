@@ -35,6 +35,7 @@
 #include <utility>
 
 #include "oracle_api.h"
+#include "pinned_math.h"
 
 namespace oracle {
 
@@ -560,7 +561,7 @@ static const float factorPI = (float)(M_PI / 180.f);
 
 static void orb_descriptor(float kx, float ky, float kangle, const Level& img, uint8_t* desc) {
     float angle = (float)kangle * factorPI;
-    float a = (float)cos((double)angle), b = (float)sin((double)angle);
+    float a = pmath::cosf_cr(angle), b = pmath::sinf_cr(angle);
     const uint8_t* center = img.at(cvRound_f(kx), cvRound_f(ky));
     const int step = img.pw;
     const int* pattern = bit_pattern_31_;

@@ -33,7 +33,7 @@
 #include <limits>
 #include <vector>
 
-#include "../orb_slam2_modification_with-point-and-line-feature_amd/csrc/lsd_math.h"
+#include "pinned_math.h"
 #include "oracle_api.h"
 
 namespace oracle_track {
@@ -1018,7 +1018,7 @@ int oracle_frame_is_in_frustum(const orbpl_camera* cam, float log_scale_factor, 
     const float vc = (float)(dot / (double)dist);
     if (vc < view_cos_limit) continue;
     const float ratio = max_dist[i] / dist;
-    int ns = (int)std::ceil((float)lsdm::log_((double)ratio) / log_scale_factor);
+    int ns = (int)std::ceil((float)pmath::log_((double)ratio) / log_scale_factor);
     if (ns < 0) ns = 0;
     else if (ns >= nlevels) ns = nlevels - 1;
     in_view[i] = 1;

@@ -378,6 +378,8 @@ def _declare_track(L):
     L.orbpl_tracker_kp_capacity.argtypes = [vp]
     L.orbpl_tracker_timings.argtypes = [vp, i, vp, ip]
     L.orbpl_tracker_timings_reset.argtypes = [vp]
+    L.orbpl_tracker_timing_counts.argtypes = [vp]
+    L.orbpl_tracker_kernel_timings.argtypes = [vp, i, vp, ip]
     L.orbpl_tracker_get_frame.argtypes = [vp, i, vp, vp, vp, vp, ip]
     L.orbpl_tracker_create_ex.argtypes = [vp, vp, i, i, i, C.POINTER(vp)]
     L.orbpl_line_frame_prepare.argtypes = [vp, vp, i, vp, vp, vp, vp, vp, vp]
@@ -775,9 +777,24 @@ class Tracker:
 
     LINE_STAGES = ("lsd", "keylines_lbd", "line_match")
 
+    @staticmethod
+    def timing_counts():
+        """Floats per step of timings / line_timings / lsd_timings /
+        stereo_timings as the library writes them (orbpl_tracker_timing_counts)."""
+        c = np.zeros(5, np.int32)
+        check(lib().orbpl_tracker_timing_counts(_ptr(c)), "orbpl_tracker_timing_counts")
+        return tuple(int(x) for x in c)
+
+    def _stage_buf(self, which, names, max_steps):
+        k = self.timing_counts()[which]
+        if k != len(names):
+            raise RuntimeError(f"liborbpl writes {k} timing entries per step, the mirror names "
+                               f"{len(names)}: library and package out of step")
+        return np.zeros((max_steps, k), np.float32)
+
     def line_timings(self, max_steps=64):
         """(n_steps, 3) line-stage ms of the last steps (hipEvents in-stream)."""
-        ms = np.zeros((max_steps, 3), np.float32)
+        ms = self._stage_buf(1, self.LINE_STAGES, max_steps)
         n = C.c_int(0)
         check(lib().orbpl_tracker_line_timings(self._h, max_steps, _ptr(ms), C.byref(n)),
               "orbpl_tracker_line_timings")
@@ -793,7 +810,7 @@ class Tracker:
 
     def lsd_timings(self, max_steps=64):
         """(n_steps, 7) LSD / LineExtractor kernel ms of the last steps."""
-        ms = np.zeros((max_steps, 7), np.float32)
+        ms = self._stage_buf(2, self.LSD_STAGES, max_steps)
         n = C.c_int(0)
         check(lib().orbpl_tracker_lsd_timings(self._h, max_steps, _ptr(ms), C.byref(n)),
               "orbpl_tracker_lsd_timings")
@@ -820,7 +837,7 @@ class Tracker:
     def stereo_timings(self, max_steps=64):
         """(n_steps, 4) stereo-stage ms of the last steps (hipEvents in-stream);
         the line stages are 0 without lines."""
-        ms = np.zeros((max_steps, 4), np.float32)
+        ms = self._stage_buf(3, self.STEREO_STAGES, max_steps)
         n = C.c_int(0)
         check(lib().orbpl_tracker_stereo_timings(self._h, max_steps, _ptr(ms), C.byref(n)),
               "orbpl_tracker_stereo_timings")
@@ -836,10 +853,21 @@ class Tracker:
 
     def timings(self, max_steps=64):
         """(n_steps, 11) per-kernel ms of the last steps (hipEvents in-stream)."""
-        ms = np.zeros((max_steps, 11), np.float32)
+        ms = self._stage_buf(0, self.STAGES, max_steps)
         n = C.c_int(0)
         check(lib().orbpl_tracker_timings(self._h, max_steps, _ptr(ms), C.byref(n)),
               "orbpl_tracker_timings")
+        return ms[:n.value]
+
+    KERNEL_STAGES = ("pose_motion", "pose_refkf", "pose_local", "match_local")
+
+    def kernel_timings(self, max_steps=64):
+        """(n_steps, 4) ms of every k_pose launch (motion model, reference
+        keyframe, local map) and of k_match_local, each launch alone."""
+        ms = self._stage_buf(4, self.KERNEL_STAGES, max_steps)
+        n = C.c_int(0)
+        check(lib().orbpl_tracker_kernel_timings(self._h, max_steps, _ptr(ms), C.byref(n)),
+              "orbpl_tracker_kernel_timings")
         return ms[:n.value]
 
     def timings_reset(self):

@@ -218,14 +218,10 @@ using namespace orbpl;
     if (e_ != hipSuccess) return orbpl::hip_fail(e_, #expr, __LINE__); \
   } while (0)
 
-struct orbv_vocab {
-  int k = 0, L = 0, scoring = 0, weighting = 0;
-  std::vector<int32_t> parent;   // -1 for the root
-  std::vector<uint8_t> leaf_flag, desc;
-  std::vector<double> weight;
-  std::vector<int32_t> word;
-  int n_words = 0;
-  std::vector<int32_t> child_start, child;
+// One device's copy of the tree (orbv_upload): trackers on different GPUs may
+// share one vocabulary, so every device keeps its own buffers until
+// orbv_destroy.
+struct VocCopy {
   int device = -1;
   int32_t *d_child_start = nullptr, *d_child = nullptr, *d_word = nullptr;
   uint8_t* d_desc = nullptr;
@@ -239,6 +235,22 @@ struct orbv_vocab {
   uint32_t* h_words = nullptr;
   int *h_bn = nullptr, *h_err = nullptr;
   hipStream_t stream = nullptr;
+};
+
+struct orbv_vocab {
+  int k = 0, L = 0, scoring = 0, weighting = 0;
+  std::vector<int32_t> parent;   // -1 for the root
+  std::vector<uint8_t> leaf_flag, desc;
+  std::vector<double> weight;
+  std::vector<int32_t> word;
+  int n_words = 0;
+  std::vector<int32_t> child_start, child;
+  std::vector<VocCopy> copies;   // one per device the tree was uploaded to
+  VocCopy* on(int device) {
+    for (auto& c : copies)
+      if (c.device == device) return &c;
+    return nullptr;
+  }
 };
 
 namespace {
@@ -264,23 +276,18 @@ int build_csr(orbv_vocab* v) {
   return ORBPL_OK;
 }
 
-void free_dev(orbv_vocab* v) {
-  if (v->device < 0) return;
-  (void)hipSetDevice(v->device);
-  (void)hipFree(v->d_child_start);
-  (void)hipFree(v->d_child);
-  (void)hipFree(v->d_word);
-  (void)hipFree(v->d_desc);
-  (void)hipFree(v->d_weight);
-  (void)hipFree(v->h_desc);
-  if (v->stream) (void)hipStreamDestroy(v->stream);
-  v->d_child_start = v->d_child = v->d_word = nullptr;
-  v->d_desc = nullptr;
-  v->d_weight = nullptr;
-  v->h_desc = nullptr;
-  v->stream = nullptr;
-  v->host_cap = 0;
-  v->device = -1;
+void free_copy(VocCopy* c) {
+  if (c->device < 0) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  (void)hipFree(c->d_child_start);
+  (void)hipFree(c->d_child);
+  (void)hipFree(c->d_word);
+  (void)hipFree(c->d_desc);
+  (void)hipFree(c->d_weight);
+  (void)hipFree(c->h_desc);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  *c = VocCopy{};
 }
 
 // one whitespace-separated token of [p, e) (stringstream >> semantics)
@@ -400,7 +407,7 @@ int orbv_load_text(const char* path, orbv_vocab** out) {
 
 int orbv_destroy(orbv_vocab* v) {
   if (!v) return ORBPL_OK;
-  free_dev(v);
+  for (auto& c : v->copies) free_copy(&c);
   delete v;
   return ORBPL_OK;
 }
@@ -428,23 +435,28 @@ int orbv_export(const orbv_vocab* v, int32_t* parent, uint8_t* leaf_flag, uint8_
 
 int orbv_upload(orbv_vocab* v, int device) {
   if (!v) return arg_fail("orbv_upload: NULL vocabulary");
-  if (v->device == device) return ORBPL_OK;
-  free_dev(v);
+  if (v->on(device)) return ORBPL_OK;
   HIP_CHECK(hipSetDevice(device));
   const size_t nn = v->parent.size();
-  HIP_CHECK(hipMalloc(&v->d_child_start, 4 * (nn + 1)));
-  HIP_CHECK(hipMalloc(&v->d_child, 4 * std::max<size_t>(1, v->child.size())));
-  HIP_CHECK(hipMalloc(&v->d_word, 4 * nn));
-  HIP_CHECK(hipMalloc(&v->d_desc, 32 * nn));
-  HIP_CHECK(hipMalloc(&v->d_weight, 8 * nn));
-  v->device = device;
-  HIP_CHECK(hipMemcpy(v->d_child_start, v->child_start.data(), 4 * (nn + 1), hipMemcpyHostToDevice));
-  if (!v->child.empty())
-    HIP_CHECK(hipMemcpy(v->d_child, v->child.data(), 4 * v->child.size(), hipMemcpyHostToDevice));
-  HIP_CHECK(hipMemcpy(v->d_word, v->word.data(), 4 * nn, hipMemcpyHostToDevice));
-  HIP_CHECK(hipMemcpy(v->d_desc, v->desc.data(), 32 * nn, hipMemcpyHostToDevice));
-  HIP_CHECK(hipMemcpy(v->d_weight, v->weight.data(), 8 * nn, hipMemcpyHostToDevice));
-  HIP_CHECK(hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking));
+  VocCopy c;
+  c.device = device;
+  hipError_t e = hipMalloc(&c.d_child_start, 4 * (nn + 1));
+  if (e == hipSuccess) e = hipMalloc(&c.d_child, 4 * std::max<size_t>(1, v->child.size()));
+  if (e == hipSuccess) e = hipMalloc(&c.d_word, 4 * nn);
+  if (e == hipSuccess) e = hipMalloc(&c.d_desc, 32 * nn);
+  if (e == hipSuccess) e = hipMalloc(&c.d_weight, 8 * nn);
+  if (e == hipSuccess) e = hipMemcpy(c.d_child_start, v->child_start.data(), 4 * (nn + 1), hipMemcpyHostToDevice);
+  if (e == hipSuccess && !v->child.empty())
+    e = hipMemcpy(c.d_child, v->child.data(), 4 * v->child.size(), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(c.d_word, v->word.data(), 4 * nn, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(c.d_desc, v->desc.data(), 32 * nn, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(c.d_weight, v->weight.data(), 8 * nn, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    free_copy(&c);
+    return hip_fail(e, "orbv_upload", __LINE__);
+  }
+  v->copies.push_back(c);
   return ORBPL_OK;
 }
 
@@ -456,14 +468,17 @@ int orbv_transform_batch_device(orbv_vocab* v, const uint8_t* d_desc, int64_t de
   if (!v || !d_desc || !d_n || !d_feat_node || !d_feat_word || !d_feat_weight || !d_bow_words ||
       !d_bow_vals || !d_bow_n || !d_err)
     return arg_fail("orbv_transform_batch_device: NULL argument");
-  if (v->device < 0) return arg_fail("orbv_transform_batch_device: vocabulary not uploaded");
+  // the copy of the calling thread's current device (the tracker sets it)
+  int dev = -1;
+  HIP_CHECK(hipGetDevice(&dev));
+  VocCopy* c = v->on(dev);
+  if (!c) return arg_fail("orbv_transform_batch_device: vocabulary not uploaded to this device");
   if (nframes <= 0 || max_n < 0) return ORBPL_OK;
   if (max_n > kBowMaxFeat || out_pitch < max_n || desc_pitch < max_n)
     return arg_fail("orbv_transform_batch_device: max_n > 4096 or pitch < max_n");
-  HIP_CHECK(hipSetDevice(v->device));
-  hipStream_t s = stream ? (hipStream_t)stream : v->stream;
-  VocDev vd{v->d_child_start, v->d_child, reinterpret_cast<const uint4*>(v->d_desc), v->d_word,
-            v->d_weight, v->L, norm_of(v->scoring), (v->weighting == 0 || v->weighting == 1) ? 1 : 0};
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  VocDev vd{c->d_child_start, c->d_child, reinterpret_cast<const uint4*>(c->d_desc), c->d_word,
+            c->d_weight, v->L, norm_of(v->scoring), (v->weighting == 0 || v->weighting == 1) ? 1 : 0};
   if (v->parent.size() <= 1) {   // empty(): nothing is added
     HIP_CHECK(hipMemsetAsync(d_bow_n, 0, 4 * (size_t)nframes, s));
     HIP_CHECK(hipMemsetAsync(d_feat_node, 0xFF, 4 * (size_t)(out_pitch * nframes), s));
@@ -488,44 +503,45 @@ int orbv_transform(orbv_vocab* v, int device, const uint8_t* desc, int n, int le
   if (n < 0 || n > kBowMaxFeat) return arg_fail("orbv_transform: n out of [0, 4096]");
   int rc = orbv_upload(v, device);
   if (rc) return rc;
-  HIP_CHECK(hipSetDevice(v->device));
-  if (!v->h_desc) {
+  HIP_CHECK(hipSetDevice(device));
+  VocCopy* c = v->on(device);
+  if (!c->h_desc) {
     // one device block: desc | n | node | word | weight | words | vals | bow_n | err
     const size_t cap = kBowMaxFeat;
     const size_t bytes = cap * 32 + 64 + cap * 4 * 3 + cap * 8 * 2 + cap * 4 + 64;
-    HIP_CHECK(hipMalloc(&v->h_desc, bytes));
-    char* q = reinterpret_cast<char*>(v->h_desc) + cap * 32;
-    v->h_n = reinterpret_cast<int*>(q);
-    v->h_bn = v->h_n + 1;
-    v->h_err = v->h_n + 2;
+    HIP_CHECK(hipMalloc(&c->h_desc, bytes));
+    char* q = reinterpret_cast<char*>(c->h_desc) + cap * 32;
+    c->h_n = reinterpret_cast<int*>(q);
+    c->h_bn = c->h_n + 1;
+    c->h_err = c->h_n + 2;
     q += 64;
-    v->h_node = reinterpret_cast<int32_t*>(q);
+    c->h_node = reinterpret_cast<int32_t*>(q);
     q += cap * 4;
-    v->h_word = reinterpret_cast<int32_t*>(q);
+    c->h_word = reinterpret_cast<int32_t*>(q);
     q += cap * 4;
-    v->h_words = reinterpret_cast<uint32_t*>(q);
+    c->h_words = reinterpret_cast<uint32_t*>(q);
     q += cap * 4;
-    v->h_wt = reinterpret_cast<double*>(q);
+    c->h_wt = reinterpret_cast<double*>(q);
     q += cap * 8;
-    v->h_vals = reinterpret_cast<double*>(q);
-    v->host_cap = (int)cap;
+    c->h_vals = reinterpret_cast<double*>(q);
+    c->host_cap = (int)cap;
   }
-  if (n > 0) HIP_CHECK(hipMemcpyAsync(v->h_desc, desc, 32 * (size_t)n, hipMemcpyHostToDevice, v->stream));
+  if (n > 0) HIP_CHECK(hipMemcpyAsync(c->h_desc, desc, 32 * (size_t)n, hipMemcpyHostToDevice, c->stream));
   int hdr[3] = {n, 0, 0};
-  HIP_CHECK(hipMemcpyAsync(v->h_n, hdr, sizeof(hdr), hipMemcpyHostToDevice, v->stream));
-  rc = orbv_transform_batch_device(v, v->h_desc, kBowMaxFeat, v->h_n, 1, n, levelsup, v->h_node,
-                                   v->h_word, v->h_wt, v->h_words, v->h_vals, v->h_bn, kBowMaxFeat,
-                                   v->h_err, v->stream);
+  HIP_CHECK(hipMemcpyAsync(c->h_n, hdr, sizeof(hdr), hipMemcpyHostToDevice, c->stream));
+  rc = orbv_transform_batch_device(v, c->h_desc, kBowMaxFeat, c->h_n, 1, n, levelsup, c->h_node,
+                                   c->h_word, c->h_wt, c->h_words, c->h_vals, c->h_bn, kBowMaxFeat,
+                                   c->h_err, c->stream);
   if (rc) return rc;
-  HIP_CHECK(hipMemcpyAsync(hdr, v->h_n, sizeof(hdr), hipMemcpyDeviceToHost, v->stream));
-  HIP_CHECK(hipStreamSynchronize(v->stream));
+  HIP_CHECK(hipMemcpyAsync(hdr, c->h_n, sizeof(hdr), hipMemcpyDeviceToHost, c->stream));
+  HIP_CHECK(hipStreamSynchronize(c->stream));
   const int k = hdr[1];
   *bow_n = k;
   if (k > 0) {
-    HIP_CHECK(hipMemcpy(bow_words, v->h_words, 4 * (size_t)k, hipMemcpyDeviceToHost));
-    HIP_CHECK(hipMemcpy(bow_vals, v->h_vals, 8 * (size_t)k, hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemcpy(bow_words, c->h_words, 4 * (size_t)k, hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemcpy(bow_vals, c->h_vals, 8 * (size_t)k, hipMemcpyDeviceToHost));
   }
-  if (n > 0) HIP_CHECK(hipMemcpy(feat_node, v->h_node, 4 * (size_t)n, hipMemcpyDeviceToHost));
+  if (n > 0) HIP_CHECK(hipMemcpy(feat_node, c->h_node, 4 * (size_t)n, hipMemcpyDeviceToHost));
   if (hdr[2]) return arg_fail("orbv_transform: feature capacity exceeded");
   return ORBPL_OK;
 }

@@ -4,9 +4,10 @@
 // The reference calls glibc's libm (exp, log, log10, pow, sinh, sin, cos,
 // atan2). Those are not bit-reproducible on the GPU, so the line path pins
 // them (pinned semantics P10-P12) to the fdlibm algorithms below,
-// written with plain IEEE-754 +,-,*,/ and bit manipulation only. Compiled with
-// -ffp-contract=off, the host (oracle) and device (kernels) results are
-// identical; against glibc they differ by at most 1 ulp (tests/test_lsd_math.py).
+// written with plain IEEE-754 +,-,*,/ and bit manipulation only, compiled with
+// -ffp-contract=off. The oracle has its own transcription (oracle/
+// pinned_math.h); tests/test_math_divergence.py compares the two bit for bit
+// and both against glibc (<= 1 ulp).
 #pragma once
 #include <stdint.h>
 
@@ -188,14 +189,18 @@ LSDM_HD double sinh_(double x) {
   return x < 0 ? -r : r;
 }
 
-// ---- sin / cos (fdlibm kernels with a two-part pi/2 reduction) ----
-LSDM_HD double ksin_(double x, double y) {
+// ---- sin / cos (fdlibm k_sin.c, k_cos.c, e_rem_pio2.c, s_sin.c, s_cos.c) ----
+// iy = 0: y is zero (the |x| <= pi/4 entry of sin); iy = 1: x + y is the
+// reduced argument (two formulas: they round differently)
+LSDM_HD double ksin_(double x, double y, int iy) {
   const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
                S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
                S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+  if ((hi_word(x) & 0x7fffffff) < 0x3e400000 && (int)x == 0) return x;   // |x| < 2^-27
   const double z = x * x;
   const double v = z * x;
   const double r = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+  if (iy == 0) return x + v * (S1 + z * r);
   return x - ((z * (0.5 * y - v * r) - y) - v * S1);
 }
 
@@ -204,6 +209,7 @@ LSDM_HD double kcos_(double x, double y) {
                C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
                C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
   const int32_t ix = hi_word(x) & 0x7fffffff;
+  if (ix < 0x3e400000 && (int)x == 0) return 1.0;
   const double z = x * x;
   const double r = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
   if (ix < 0x3FD33333) return 1.0 - (0.5 * z - (z * r - x * y));
@@ -215,27 +221,75 @@ LSDM_HD double kcos_(double x, double y) {
   return a - (hz - (z * r - x * y));
 }
 
-// |x| < 2^19 * pi/2. Returns the quadrant; *y0 + *y1 = x - n*pi/2.
+// high word of n * pi/2, n = 1..32 (e_rem_pio2.c's npio2_hw): equal high
+// words flag a cancellation that needs the second reduction round
+LSDM_HD int32_t npio2_hw_(int n) {
+  switch (n) {
+    case 1: return 0x3FF921FB; case 2: return 0x400921FB; case 3: return 0x4012D97C;
+    case 4: return 0x401921FB; case 5: return 0x401F6A7A; case 6: return 0x4022D97C;
+    case 7: return 0x4025FDBB; case 8: return 0x402921FB; case 9: return 0x402C463A;
+    case 10: return 0x402F6A7A; case 11: return 0x4031475C; case 12: return 0x4032D97C;
+    case 13: return 0x40346B9C; case 14: return 0x4035FDBB; case 15: return 0x40378FDB;
+    case 16: return 0x403921FB; case 17: return 0x403AB41B; case 18: return 0x403C463A;
+    case 19: return 0x403DD85A; case 20: return 0x403F6A7A; case 21: return 0x40407E4C;
+    case 22: return 0x4041475C; case 23: return 0x4042106C; case 24: return 0x4042D97C;
+    case 25: return 0x4043A28C; case 26: return 0x40446B9C; case 27: return 0x404534AC;
+    case 28: return 0x4045FDBB; case 29: return 0x4046C6CB; case 30: return 0x40478FDB;
+    case 31: return 0x404858EB; default: return 0x404921FB;
+  }
+}
+
+// |x| < 2^19 * pi/2 (the line path's angles are within a few pi). Returns the
+// quadrant; *y0 + *y1 = x - n*pi/2.
 LSDM_HD int rem_pio2_(double x, double* y0, double* y1) {
   const double invpio2 = 6.36619772367581382433e-01, pio2_1 = 1.57079632673412561417e+00,
                pio2_1t = 6.07710050650619224932e-11, pio2_2 = 6.07710050630396597660e-11,
-               pio2_2t = 2.02226624879595063154e-21;
-  const double t = fabs_(x);
-  if (t <= 7.85398163397448278999e-01) {  // |x| <= pi/4
+               pio2_2t = 2.02226624879595063154e-21, pio2_3 = 2.02226624871116645580e-21,
+               pio2_3t = 8.47842766036889956997e-32;
+  const int32_t hx = hi_word(x), ix = hx & 0x7fffffff;
+  if (ix <= 0x3fe921fb) {   // |x| <= pi/4
     *y0 = x;
     *y1 = 0.0;
     return 0;
   }
+  if (ix < 0x4002d97c) {    // |x| < 3pi/4: n = +-1, a 33+53-bit pi/2 suffices
+    const double sg = hx > 0 ? 1.0 : -1.0;
+    double z = x - sg * pio2_1;
+    if (ix != 0x3ff921fb) {
+      *y0 = z - sg * pio2_1t;
+      *y1 = (z - *y0) - sg * pio2_1t;
+    } else {                // near pi/2: 33+33+53 bits
+      z -= sg * pio2_2;
+      *y0 = z - sg * pio2_2t;
+      *y1 = (z - *y0) - sg * pio2_2t;
+    }
+    return hx > 0 ? 1 : -1;
+  }
+  const double t = fabs_(x);
   const int n = (int)(t * invpio2 + 0.5);
   const double fn = (double)n;
   double r = t - fn * pio2_1;
-  double w = fn * pio2_1t;
-  // second round (fdlibm "good to 118 bits")
-  const double tt = r;
-  w = fn * pio2_2;
-  r = tt - w;
-  w = fn * pio2_2t - ((tt - r) - w);
-  const double y = r - w;
+  double w = fn * pio2_1t;   // first round: 85 bits
+  double y = r - w;
+  if (!(n < 32 && ix != npio2_hw_(n))) {
+    const int j = ix >> 20;
+    int i = j - ((hi_word(y) >> 20) & 0x7ff);
+    if (i > 16) {            // second round: 118 bits
+      double tt = r;
+      w = fn * pio2_2;
+      r = tt - w;
+      w = fn * pio2_2t - ((tt - r) - w);
+      y = r - w;
+      i = j - ((hi_word(y) >> 20) & 0x7ff);
+      if (i > 49) {          // third round: 151 bits
+        tt = r;
+        w = fn * pio2_3;
+        r = tt - w;
+        w = fn * pio2_3t - ((tt - r) - w);
+        y = r - w;
+      }
+    }
+  }
   const double yt = (r - y) - w;
   if (x < 0) {
     *y0 = -y;
@@ -248,20 +302,27 @@ LSDM_HD int rem_pio2_(double x, double* y0, double* y1) {
 }
 
 LSDM_HD double sin_(double x) {
+  if ((hi_word(x) & 0x7fffffff) <= 0x3fe921fb) return ksin_(x, 0.0, 0);
   double a, b;
   const int n = rem_pio2_(x, &a, &b);
   switch (n & 3) {
-    case 0: return ksin_(a, b);
+    case 0: return ksin_(a, b, 1);
     case 1: return kcos_(a, b);
-    case 2: return -ksin_(a, b);
+    case 2: return -ksin_(a, b, 1);
     default: return -kcos_(a, b);
   }
 }
 
+// sin_(x) and cos_(x) together (the same results as the two calls)
 LSDM_HD void sincos_(double x, double* s, double* c) {
+  if ((hi_word(x) & 0x7fffffff) <= 0x3fe921fb) {
+    *s = ksin_(x, 0.0, 0);
+    *c = kcos_(x, 0.0);
+    return;
+  }
   double a, b;
   const int n = rem_pio2_(x, &a, &b);
-  const double ks = ksin_(a, b), kc = kcos_(a, b);
+  const double ks = ksin_(a, b, 1), kc = kcos_(a, b);
   switch (n & 3) {
     case 0: *s = ks; *c = kc; break;
     case 1: *s = kc; *c = -ks; break;
@@ -271,13 +332,14 @@ LSDM_HD void sincos_(double x, double* s, double* c) {
 }
 
 LSDM_HD double cos_(double x) {
+  if ((hi_word(x) & 0x7fffffff) <= 0x3fe921fb) return kcos_(x, 0.0);
   double a, b;
   const int n = rem_pio2_(x, &a, &b);
   switch (n & 3) {
     case 0: return kcos_(a, b);
-    case 1: return -ksin_(a, b);
+    case 1: return -ksin_(a, b, 1);
     case 2: return -kcos_(a, b);
-    default: return ksin_(a, b);
+    default: return ksin_(a, b, 1);
   }
 }
 

@@ -112,7 +112,7 @@ extern "C" {
 
 const char* orbpl_last_error(void) { return orbpl::g_last_error.c_str(); }
 
-const char* orbpl_version(void) { return "orbpl gfx950 r1"; }
+const char* orbpl_version(void) { return "orbpl gfx950 r3"; }
 
 int orbpl_device_count(int* n) {
   if (!n) return arg_fail("n is NULL");

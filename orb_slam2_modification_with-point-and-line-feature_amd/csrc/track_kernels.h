@@ -10,6 +10,13 @@
 namespace orbpl {
 
 constexpr int kMatchMaxKp = 2048;    // keypoints per frame the matcher handles
+// per-step entries of orbpl_tracker_timings / _line_timings / _lsd_timings /
+// _stereo_timings / _kernel_timings (orbpl_tracker_timing_counts reports them)
+constexpr int kTimingStages = 11;
+constexpr int kLineTimingStages = 3;
+constexpr int kLsdTimingStages = 7;
+constexpr int kStereoTimingStages = 4;
+constexpr int kKernelTimingStages = 4;   // orbpl_tracker_kernel_timings
 constexpr int kPoseMaxEdges = 2304;  // point + line edges per frame
 
 struct PoseEdge;

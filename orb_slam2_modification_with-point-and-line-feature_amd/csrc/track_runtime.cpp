@@ -802,7 +802,7 @@ struct orbpl_tracker {
   StreamState* d_state = nullptr;
   PoseEdge* d_edges = nullptr;
   static constexpr int kRing = 64;   // steps kept in the timing ring
-  static constexpr int kEv = 28;     // events per step
+  static constexpr int kEv = 36;     // events per step (28..35: kernel brackets)
   std::vector<hipEvent_t> ring;      // kRing * kEv events
   int ring_pos = 0, ring_count = 0;
   // TrackLocalMap (ORBPL_TRACK_LOCAL_MAP): ring of the last kLmK keyframes'
@@ -1360,7 +1360,11 @@ static int tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_
     p.lpitch = kLineKeep;
   }
   p.fixed_line_jac = t->fixed_line_jac;
+  HIP_CHECK(hipEventRecord(ev[28], ts));
   launch_pose(t->consts, p, S, ts);
+  HIP_CHECK(hipEventRecord(ev[29], ts));
+  HIP_CHECK(hipEventRecord(ev[30], ts));   // k_pose of TrackReferenceKeyFrame (0 without)
+  bool refkf_pose = false;
   if (t->refkf) {
     // ---- TrackReferenceKeyFrame where the motion model did not run or
     // failed (Tracking.cc:324-338, 942-1032; P22) ----
@@ -1417,9 +1421,16 @@ static int tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_
     launch_trk_merge(ta, S, ts);
     PoseLaunch pt = p;
     pt.gate_lm = 2;
+    HIP_CHECK(hipEventRecord(ev[30], ts));
     launch_pose(t->consts, pt, S, ts);
+    HIP_CHECK(hipEventRecord(ev[31], ts));
+    refkf_pose = true;
   }
+  if (!refkf_pose) HIP_CHECK(hipEventRecord(ev[31], ts));
   HIP_CHECK(hipEventRecord(ev[9], ts));
+  // TrackLocalMap's k_match_local / k_pose brackets (0 without it)
+  HIP_CHECK(hipEventRecord(ev[32], ts));
+  HIP_CHECK(hipEventRecord(ev[34], ts));
   LocalMapArgs lm{};
   if (t->local_map) {
     // ---- TrackLocalMap (Tracking.cc:1332-1420), defined local map P18 ----
@@ -1504,7 +1515,9 @@ static int tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_
     ma.kp_pitch = K;
     ma.mp_pitch = t->lp;
     ma.nm_stride = pstride;
+    HIP_CHECK(hipEventRecord(ev[32], ts));
     launch_match_local(t->consts, ma, ts, S);
+    HIP_CHECK(hipEventRecord(ev[33], ts));
     if (t->lines) {
       // SearchLocalLines: IsInFrustum(pML, 0.5), LineMatcher(0.8) local-map overload
       launch_line_in_frustum_batched(dTcw, pstride, t->ll_n, t->llp, t->ll_xyz, t->ll_valid, S, ts);
@@ -1542,8 +1555,14 @@ static int tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_
       p2.t_loutlier = t->loutlier2;
     }
     p2.gate_lm = 1;
+    HIP_CHECK(hipEventRecord(ev[34], ts));
     launch_pose(t->consts, p2, S, ts);
+    HIP_CHECK(hipEventRecord(ev[35], ts));
     launch_lm_count(lm, fid, S, ts);
+  }
+  if (!t->local_map) {
+    HIP_CHECK(hipEventRecord(ev[33], ts));
+    HIP_CHECK(hipEventRecord(ev[35], ts));
   }
   HIP_CHECK(hipEventRecord(ev[26], ts));
   LineFinish lf{};
@@ -1596,22 +1615,50 @@ int orbpl_tracker_step_host(orbpl_tracker* t, const uint8_t* h_gray, const uint1
   HIP_CHECK(hipSetDevice(t->device));
   const size_t npx = (size_t)t->S * t->W * t->H;
   if (!t->cstream) {
-    HIP_CHECK(hipStreamCreateWithFlags(&t->cstream, hipStreamNonBlocking));
+    // everything into locals first: a failed allocation leaves the tracker
+    // as it was (no half-initialised slots behind a non-null copy stream)
+    std::vector<void*> got;
+    auto fail = [&](hipError_t e, int line) {
+      for (void* p : got) (void)hipFree(p);
+      return hip_fail(e, "ingress slot allocation", line);
+    };
+    uint8_t* g[orbpl_tracker::kIn];
+    uint16_t* d16[orbpl_tracker::kIn];
+    float* df[orbpl_tracker::kIn];
     for (int k = 0; k < orbpl_tracker::kIn; k++) {
       void* p = nullptr;
-      HIP_CHECK(hipMalloc(&p, npx));
-      t->allocs.push_back(p);
-      t->in_gray[k] = (uint8_t*)p;
-      HIP_CHECK(hipMalloc(&p, npx * 2));
-      t->allocs.push_back(p);
-      t->in_d16[k] = (uint16_t*)p;
-      HIP_CHECK(hipMalloc(&p, npx * 4));
-      t->allocs.push_back(p);
-      t->in_depth[k] = (float*)p;
-      HIP_CHECK(hipEventCreateWithFlags(&t->in_copied[k], hipEventDisableTiming));
-      HIP_CHECK(hipEventCreateWithFlags(&t->in_done_s[k], hipEventDisableTiming));
-      HIP_CHECK(hipEventCreateWithFlags(&t->in_done_l[k], hipEventDisableTiming));
+      hipError_t e = hipMalloc(&p, npx);
+      if (e != hipSuccess) return fail(e, __LINE__);
+      got.push_back(p);
+      g[k] = (uint8_t*)p;
+      if ((e = hipMalloc(&p, npx * 2)) != hipSuccess) return fail(e, __LINE__);
+      got.push_back(p);
+      d16[k] = (uint16_t*)p;
+      if ((e = hipMalloc(&p, npx * 4)) != hipSuccess) return fail(e, __LINE__);
+      got.push_back(p);
+      df[k] = (float*)p;
     }
+    hipEvent_t evs[3 * orbpl_tracker::kIn] = {};
+    hipStream_t cs = nullptr;
+    hipError_t e = hipSuccess;
+    for (int i = 0; i < 3 * orbpl_tracker::kIn && e == hipSuccess; i++)
+      e = hipEventCreateWithFlags(&evs[i], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      for (hipEvent_t x : evs)
+        if (x) (void)hipEventDestroy(x);
+      return fail(e, __LINE__);
+    }
+    for (int k = 0; k < orbpl_tracker::kIn; k++) {
+      t->in_gray[k] = g[k];
+      t->in_d16[k] = d16[k];
+      t->in_depth[k] = df[k];
+      t->in_copied[k] = evs[3 * k];
+      t->in_done_s[k] = evs[3 * k + 1];
+      t->in_done_l[k] = evs[3 * k + 2];
+    }
+    t->allocs.insert(t->allocs.end(), got.begin(), got.end());
+    t->cstream = cs;
   }
   const int k = t->in_pos % orbpl_tracker::kIn;
   // the slot's previous frames must have been read (extraction + line stream)
@@ -1702,6 +1749,35 @@ int orbpl_tracker_get_state(orbpl_tracker* t, float* Tcw, int* nkps, int* nmatch
   return ORBPL_OK;
 }
 
+int orbpl_tracker_timing_counts(int* counts5) {
+  if (!counts5) return arg_fail("NULL argument");
+  counts5[0] = kTimingStages;
+  counts5[1] = kLineTimingStages;
+  counts5[2] = kLsdTimingStages;
+  counts5[3] = kStereoTimingStages;
+  counts5[4] = kKernelTimingStages;
+  return ORBPL_OK;
+}
+
+int orbpl_tracker_kernel_timings(orbpl_tracker* t, int max_steps, float* ms, int* n_steps) {
+  if (!t || !ms || !n_steps) return arg_fail("NULL argument");
+  HIP_CHECK(hipSetDevice(t->device));
+  HIP_CHECK(hipStreamSynchronize(t->stream));
+  HIP_CHECK(hipStreamSynchronize(t->tstream));
+  // every k_pose launch of the step (TrackWithMotionModel, TrackReferenceKeyFrame,
+  // TrackLocalMap) and TrackLocalMap's k_match_local, each bracketed alone
+  static const int kPair[kKernelTimingStages][2] = {{28, 29}, {30, 31}, {34, 35}, {32, 33}};
+  const int n = std::min(max_steps, t->ring_count);
+  for (int k = 0; k < n; k++) {
+    const int step = t->ring_pos - n + k;
+    hipEvent_t* ev = &t->ring[(size_t)(step % orbpl_tracker::kRing) * orbpl_tracker::kEv];
+    for (int i = 0; i < kKernelTimingStages; i++)
+      HIP_CHECK(hipEventElapsedTime(&ms[k * kKernelTimingStages + i], ev[kPair[i][0]], ev[kPair[i][1]]));
+  }
+  *n_steps = n;
+  return ORBPL_OK;
+}
+
 int orbpl_tracker_timings(orbpl_tracker* t, int max_steps, float* ms, int* n_steps) {
   if (!t || !ms || !n_steps) return arg_fail("NULL argument");
   HIP_CHECK(hipSetDevice(t->device));
@@ -1711,14 +1787,14 @@ int orbpl_tracker_timings(orbpl_tracker* t, int max_steps, float* ms, int* n_ste
   // match (incl. prediction), pose, finish (tracking stream)
   // (+ TrackLocalMap: gather, frustum, local matching, second pose, count)
   // (+ KeyFrame::ComputeBoW with a vocabulary; 0 without)
-  static const int kPair[11][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 27},
-                                   {7, 8}, {14, 9}, {26, 10}, {9, 26}, {27, 6}};
+  static const int kPair[kTimingStages][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 27},
+                                              {7, 8}, {14, 9}, {26, 10}, {9, 26}, {27, 6}};
   const int n = std::min(max_steps, t->ring_count);
   for (int k = 0; k < n; k++) {
     const int step = t->ring_pos - n + k;
     hipEvent_t* ev = &t->ring[(size_t)(step % orbpl_tracker::kRing) * orbpl_tracker::kEv];
-    for (int i = 0; i < 11; i++)
-      HIP_CHECK(hipEventElapsedTime(&ms[k * 11 + i], ev[kPair[i][0]], ev[kPair[i][1]]));
+    for (int i = 0; i < kTimingStages; i++)
+      HIP_CHECK(hipEventElapsedTime(&ms[k * kTimingStages + i], ev[kPair[i][0]], ev[kPair[i][1]]));
   }
   *n_steps = n;
   return ORBPL_OK;
@@ -1733,13 +1809,13 @@ int orbpl_tracker_line_timings(orbpl_tracker* t, int max_steps, float* ms, int* 
   HIP_CHECK(hipStreamSynchronize(t->lstream));
   // LSD (line stream), KeyLines + LBD + UndistortKeyLines (line stream),
   // LineMatcher::SearchByProjection (tracking stream)
-  static const int kPair[3][2] = {{11, 12}, {12, 13}, {8, 14}};
+  static const int kPair[kLineTimingStages][2] = {{11, 12}, {12, 13}, {8, 14}};
   const int n = std::min(max_steps, t->ring_count);
   for (int k = 0; k < n; k++) {
     const int step = t->ring_pos - n + k;
     hipEvent_t* ev = &t->ring[(size_t)(step % orbpl_tracker::kRing) * orbpl_tracker::kEv];
-    for (int i = 0; i < 3; i++)
-      HIP_CHECK(hipEventElapsedTime(&ms[k * 3 + i], ev[kPair[i][0]], ev[kPair[i][1]]));
+    for (int i = 0; i < kLineTimingStages; i++)
+      HIP_CHECK(hipEventElapsedTime(&ms[k * kLineTimingStages + i], ev[kPair[i][0]], ev[kPair[i][1]]));
   }
   *n_steps = n;
   return ORBPL_OK;
@@ -1802,13 +1878,14 @@ int orbpl_tracker_lsd_timings(orbpl_tracker* t, int max_steps, float* ms, int* n
   HIP_CHECK(hipStreamSynchronize(t->lstream));
   // line stream: blur+resize+grad, sort, seed loop, validate, KeyLines,
   // blur5+Sobel+LBD, UndistortKeyLines + line depths
-  static const int kPair[7][2] = {{11, 18}, {18, 19}, {19, 20}, {20, 12}, {12, 21}, {21, 22}, {22, 13}};
+  static const int kPair[kLsdTimingStages][2] = {{11, 18}, {18, 19}, {19, 20}, {20, 12},
+                                                 {12, 21}, {21, 22}, {22, 13}};
   const int n = std::min(max_steps, t->ring_count);
   for (int k = 0; k < n; k++) {
     const int step = t->ring_pos - n + k;
     hipEvent_t* ev = &t->ring[(size_t)(step % orbpl_tracker::kRing) * orbpl_tracker::kEv];
-    for (int i = 0; i < 7; i++)
-      HIP_CHECK(hipEventElapsedTime(&ms[k * 7 + i], ev[kPair[i][0]], ev[kPair[i][1]]));
+    for (int i = 0; i < kLsdTimingStages; i++)
+      HIP_CHECK(hipEventElapsedTime(&ms[k * kLsdTimingStages + i], ev[kPair[i][0]], ev[kPair[i][1]]));
   }
   *n_steps = n;
   return ORBPL_OK;
@@ -1824,17 +1901,17 @@ int orbpl_tracker_stereo_timings(orbpl_tracker* t, int max_steps, float* ms, int
   // right ORB extraction (right stream), ComputeStereoMatches (extraction
   // stream); with lines: right LineExtractor (right line stream),
   // k_stereo_lines (line stream); 0 without lines
-  static const int kPair[4][2] = {{15, 16}, {17, 6}, {23, 24}, {25, 13}};
+  static const int kPair[kStereoTimingStages][2] = {{15, 16}, {17, 27}, {23, 24}, {25, 13}};
   if (t->rlstream) HIP_CHECK(hipStreamSynchronize(t->rlstream));
   if (t->lstream) HIP_CHECK(hipStreamSynchronize(t->lstream));
   const int n = std::min(max_steps, t->ring_count);
   for (int k = 0; k < n; k++) {
     const int step = t->ring_pos - n + k;
     hipEvent_t* ev = &t->ring[(size_t)(step % orbpl_tracker::kRing) * orbpl_tracker::kEv];
-    for (int i = 0; i < 4; i++) {
-      ms[k * 4 + i] = 0.0f;
-      if (i < 2 || t->lines)
-        HIP_CHECK(hipEventElapsedTime(&ms[k * 4 + i], ev[kPair[i][0]], ev[kPair[i][1]]));
+    for (int i = 0; i < kStereoTimingStages; i++) {
+      float* o = &ms[k * kStereoTimingStages + i];
+      *o = 0.0f;
+      if (i < 2 || t->lines) HIP_CHECK(hipEventElapsedTime(o, ev[kPair[i][0]], ev[kPair[i][1]]));
     }
   }
   *n_steps = n;
@@ -1879,12 +1956,13 @@ int orbpl_tracker_timings_reset(orbpl_tracker* t) {
 int orbpl_tracker_stage_ms(orbpl_tracker* t, float* ms5) {
   if (!t || !ms5) return arg_fail("NULL argument");
   if (t->ring_count == 0) return arg_fail("no step recorded yet");
-  float m[10];
+  float m[kTimingStages];
   int n = 0;
   int rc = orbpl_tracker_timings(t, 1, m, &n);
   if (rc) return rc;
   ms5[0] = m[0] + m[1] + m[2] + m[3] + m[4];
   for (int i = 0; i < 4; i++) ms5[1 + i] = m[5 + i];
+  ms5[1] += m[10];  // glue: + KeyFrame::ComputeBoW
   ms5[3] += m[9];   // pose: both PoseOptimizations (+ the local map search)
   return ORBPL_OK;
 }

@@ -53,3 +53,12 @@ def test_descriptor_distance(orbpl):
     z = np.zeros(32, np.uint8)
     assert orbpl.DescriptorDistance(z, z) == 0
     assert orbpl.DescriptorDistance(z, np.full(32, 255, np.uint8)) == 256
+
+
+def test_timing_layout_and_version(orbpl):
+    """The timing buffers the mirror allocates match what the library writes
+    (orbpl_tracker_stage_ms wrote 11 floats into 10)."""
+    T = orbpl.Tracker
+    assert T.timing_counts() == (len(T.STAGES), len(T.LINE_STAGES), len(T.LSD_STAGES),
+                                 len(T.STEREO_STAGES), len(T.KERNEL_STAGES))
+    assert orbpl.lib().orbpl_version().decode() == "orbpl gfx950 r3"
