@@ -1,0 +1,152 @@
+// Drop-in ORB_SLAM2::Frame (see Frame.h).
+#include "Frame.h"
+
+#include <stdexcept>
+#include <thread>
+
+namespace ORB_SLAM2 {
+
+float Frame::fx, Frame::fy, Frame::cx, Frame::cy, Frame::invfx, Frame::invfy;
+float Frame::mnMinX, Frame::mnMaxX, Frame::mnMinY, Frame::mnMaxY;
+long unsigned int Frame::nNextId = 0;
+
+static void check(int rc) {
+  if (rc != ORBPL_OK) throw std::runtime_error(orbpl_last_error());
+}
+
+orbpl_camera Frame::Camera() const {
+  const float* d = mDistCoef.ptr<float>();
+  const int nd = mDistCoef.rows * mDistCoef.cols;
+  return orbpl_camera{fx, fy, cx, cy, d[0], d[1], d[2], d[3], nd > 4 ? d[4] : 0.0f, mbf,
+                      mThDepth, mnWidth, mnHeight};
+}
+
+Frame::Frame(const cv::Mat& imGray, const cv::Mat& imDepth, const double& timeStamp,
+             ORBextractor* extractor, void*, cv::Mat& K, cv::Mat& distCoef, const float& bf,
+             const float& thDepth, LineExtractor* lineExtractor)
+    : mTimeStamp(timeStamp), mK(K.clone()), mDistCoef(distCoef.clone()), mbf(bf),
+      mThDepth(thDepth) {
+  mnId = nNextId++;
+  mnScaleLevels = extractor->GetLevels();
+  mfScaleFactor = extractor->GetScaleFactor();
+  mvScaleFactors = extractor->GetScaleFactors();
+  mvInvScaleFactors = extractor->GetInverseScaleFactors();
+  mvLevelSigma2 = extractor->GetScaleSigmaSquares();
+  mvInvLevelSigma2 = extractor->GetInverseScaleSigmaSquares();
+  mnWidth = imGray.cols;
+  mnHeight = imGray.rows;
+  fx = K.at<float>(0, 0);
+  fy = K.at<float>(1, 1);
+  cx = K.at<float>(0, 2);
+  cy = K.at<float>(1, 2);
+  invfx = 1.0f / fx;
+  invfy = 1.0f / fy;
+  mb = mbf / fx;
+  // ORB || LineExtractor (Frame.cc:152-155)
+  thread_local LineExtractor own_lines;
+  LineExtractor* lx = lineExtractor ? lineExtractor : &own_lines;
+  std::exception_ptr lerr;
+  std::thread tl([&]() {
+    try {
+      lx->ExtractLineSegment(imGray, mvKeyLines, mLineDescriptors, mvKeyLineCoefficient);
+    } catch (...) {
+      lerr = std::current_exception();
+    }
+  });
+  (*extractor)(imGray, cv::Mat(), mvKeys, mDescriptors);
+  tl.join();
+  if (lerr) std::rethrow_exception(lerr);
+  N = (int)mvKeys.size();
+  NL = (int)mvKeyLines.size();
+  // UndistortKeyPoints + ComputeStereoFromRGBD + AssignFeaturesToGrid
+  // (Frame.cc:160-204) in one call
+  const orbpl_camera cam = Camera();
+  mvKeysUn.resize(N);
+  mvDepth.resize(N);
+  mvuRight.resize(N);
+  std::vector<int32_t> cell(N);
+  float bounds[4];
+  check(orbpl_frame_prepare(&cam, reinterpret_cast<const orbpl_keypoint*>(mvKeys.data()), N,
+                            imDepth.ptr<float>(), reinterpret_cast<orbpl_keypoint*>(mvKeysUn.data()),
+                            mvDepth.data(), mvuRight.data(), cell.data(), bounds));
+  mnMinX = bounds[0];
+  mnMaxX = bounds[1];
+  mnMinY = bounds[2];
+  mnMaxY = bounds[3];
+  for (int i = 0; i < N; i++)
+    if (cell[i] >= 0) mGrid[cell[i] % FRAME_GRID_COLS][cell[i] / FRAME_GRID_COLS].push_back(i);
+  mvpMapPoints.assign(N, nullptr);
+  mvbOutlier.assign(N, false);
+  // UndistortKeyLines + the line part of ComputeStereoFromRGBD
+  mvKeyLinesUn.resize(NL);
+  mvDepthLineStart.resize(NL);
+  mvDepthLineEnd.resize(NL);
+  mvuRightLineStart.resize(NL);
+  mvuRightLineEnd.resize(NL);
+  check(orbpl_line_frame_prepare(&cam, reinterpret_cast<const orbpl_keyline*>(mvKeyLines.data()),
+                                 NL, imDepth.ptr<float>(),
+                                 reinterpret_cast<orbpl_keyline*>(mvKeyLinesUn.data()),
+                                 mvDepthLineStart.data(), mvDepthLineEnd.data(),
+                                 mvuRightLineStart.data(), mvuRightLineEnd.data()));
+  mvpMapLines.assign(NL, nullptr);
+  mvbLineOutlier.assign(NL, false);
+}
+
+void Frame::SetPose(cv::Mat Tcw) {
+  mTcw = Tcw.clone();
+  UpdatePoseMatrices();
+}
+
+// Frame.cc:335-344: Rwc = Rcw^T, Ow = -Rcw^T tcw (float products summed in
+// double, one rounding: pinned P6)
+void Frame::UpdatePoseMatrices() {
+  mRcw.create(3, 3, cv::CV_32F);
+  mtcw.create(3, 1, cv::CV_32F);
+  mRwc.create(3, 3, cv::CV_32F);
+  mOw.create(3, 1, cv::CV_32F);
+  for (int r = 0; r < 3; r++) {
+    for (int c = 0; c < 3; c++) {
+      mRcw.at<float>(r, c) = mTcw.at<float>(r, c);
+      mRwc.at<float>(c, r) = mTcw.at<float>(r, c);
+    }
+    mtcw.at<float>(r, 0) = mTcw.at<float>(r, 3);
+  }
+  for (int r = 0; r < 3; r++) {
+    double s = 0;
+    for (int k = 0; k < 3; k++) s += (double)mRwc.at<float>(r, k) * mtcw.at<float>(k, 0);
+    mOw.at<float>(r, 0) = (float)(-s);
+  }
+}
+
+static cv::Mat unproject(const Frame& F, float u, float v, float z) {
+  const float x = (u - Frame::cx) * z * Frame::invfx;
+  const float y = (v - Frame::cy) * z * Frame::invfy;
+  const float xc[3] = {x, y, z};
+  cv::Mat w(3, 1, cv::CV_32F);
+  for (int r = 0; r < 3; r++) {
+    double s = 0;
+    for (int k = 0; k < 3; k++) s += (double)F.mRwc.at<float>(r, k) * xc[k];
+    w.at<float>(r, 0) = (float)(s + (double)F.mOw.at<float>(r, 0));
+  }
+  return w;
+}
+
+cv::Mat Frame::UnprojectStereo(const int& i) {
+  const float z = mvDepth[i];
+  if (z <= 0) return cv::Mat();
+  return unproject(*this, mvKeysUn[i].pt.x, mvKeysUn[i].pt.y, z);
+}
+
+cv::Mat Frame::UnprojectStereoLineStart(const int& i) {
+  const float z = mvDepthLineStart[i];
+  if (z <= 0) return cv::Mat();
+  return unproject(*this, mvKeyLinesUn[i].startPointX, mvKeyLinesUn[i].startPointY, z);
+}
+
+cv::Mat Frame::UnprojectStereoLineEnd(const int& i) {
+  const float z = mvDepthLineStart[i];   // Frame.cc:1192 reads the start depth
+  if (z <= 0) return cv::Mat();
+  return unproject(*this, mvKeyLinesUn[i].endPointX, mvKeyLinesUn[i].endPointY, z);
+}
+
+}  // namespace ORB_SLAM2

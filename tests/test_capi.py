@@ -62,3 +62,28 @@ def test_timing_layout_and_version(orbpl):
     assert T.timing_counts() == (len(T.STAGES), len(T.LINE_STAGES), len(T.LSD_STAGES),
                                  len(T.STEREO_STAGES), len(T.KERNEL_STAGES))
     assert orbpl.lib().orbpl_version().decode() == "orbpl gfx950 r3"
+
+
+def test_dropin_classes_build_with_the_reference_signatures():
+    """The g++-built drop-in library exports the reference's class methods
+    (ORBextractor.h:51-85, LineExtractor.h:25-30, ORBmatcher.h, LineMatcher.h,
+    Optimizer.h:121,234) and links against liborbpl.so."""
+    import subprocess
+    pkg = ROOT / "orb_slam2_modification_with-point-and-line-feature_amd"
+    subprocess.run(["make", "-s", "-C", str(pkg / "dropin")], check=True)
+    syms = subprocess.run(["nm", "-DC", "--defined-only", str(pkg / "liborbpl_dropin.so")],
+                          check=True, capture_output=True, text=True).stdout
+    for s in ("ORB_SLAM2::ORBextractor::ORBextractor(int, float, int, int, int)",
+              "ORB_SLAM2::ORBextractor::operator()(cv::InputArray, cv::InputArray, "
+              "std::vector<cv::KeyPoint, std::allocator<cv::KeyPoint> >&, cv::OutputArray)",
+              "ORB_SLAM2::LineExtractor::ExtractLineSegment(cv::Mat const&",
+              "ORB_SLAM2::ORBmatcher::SearchByProjection(ORB_SLAM2::Frame&, ORB_SLAM2::Frame const&, "
+              "float, bool)",
+              "ORB_SLAM2::ORBmatcher::DescriptorDistance(cv::Mat const&, cv::Mat const&)",
+              "ORB_SLAM2::LineMatcher::SearchByProjection(ORB_SLAM2::Frame&, ORB_SLAM2::Frame const&)",
+              "ORB_SLAM2::Optimizer::PoseOptimization(ORB_SLAM2::Frame*)",
+              "ORB_SLAM2::Optimizer::PoseOptimizationWithLines(ORB_SLAM2::Frame*)"):
+        assert s in syms, s
+    ldd = subprocess.run(["ldd", str(pkg / "dropin_driver")], check=True, capture_output=True,
+                         text=True).stdout
+    assert "liborbpl_dropin.so" in ldd and "liborbpl.so" in ldd and "not found" not in ldd
