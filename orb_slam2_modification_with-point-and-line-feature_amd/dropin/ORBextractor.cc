@@ -26,7 +26,7 @@ ORBextractor::ORBextractor(int _nfeatures, float _scaleFactor, int _nlevels, int
   int cap = 0;
   // a geometry large enough for every level; the scale tables and budgets do
   // not depend on it
-  check(orbx_describe(&params_, 4096, 4096, lw.data(), lh.data(), mnFeaturesPerLevel.data(),
+  check(orbx_describe(&params_, 2048, 2048, lw.data(), lh.data(), mnFeaturesPerLevel.data(),
                       mvScaleFactor.data(), &cap));
   mvInvScaleFactor.resize(nlevels);
   mvLevelSigma2.resize(nlevels);
