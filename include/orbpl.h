@@ -403,6 +403,24 @@ int orbpl_tracker_create(const orbpl_orb_params* orb, const orbpl_camera* cam, i
  * and the outlier discard; success = 10 map inliers (and, with lines, a
  * line count of 10 after the reference's outlier decrement). Pinned P22. */
 #define ORBPL_TRACK_REFKF 16
+/* ORBPL_TRACK_MAP: Tracking::Track with the reference's map model
+ * (Tracking.cc:283-599; RGB-D streams): StereoInitialization (> 500 keypoints:
+ * the first keyframe, a map point per keypoint with depth, a map line per line
+ * with both end-point depths), UpdateLastFrame's temporal VO points / lines,
+ * TrackWithMotionModel against the last frame's map points / lines,
+ * TrackReferenceKeyFrame against the reference keyframe (with
+ * ORBPL_TRACK_REFKF and a vocabulary), TrackLocalMap over the covisibility
+ * graph (UpdateLocalKeyFrames / UpdateLocalPoints / UpdateLocalLines,
+ * SearchLocalPoints / SearchLocalLines, the second pose), NeedNewKeyFrame,
+ * CreateNewKeyFrame and LocalMapping::ProcessNewKeyFrame (observations,
+ * distinctive descriptors, normals, UpdateConnections), the LOST state and the
+ * reset of a map with <= 5 keyframes. Per stream a keyframe table (32 by
+ * default; ORBPL_MAP_KF in the environment at creation, 2..64) and point / line
+ * pools of keyframes x keypoint capacity / x 80 in HBM. Pinned P23-P25
+ * (DESIGN.md): LocalMapping = its ProcessNewKeyFrame run synchronously,
+ * Relocalization fails; pointer-ordered containers in keyframe id order.
+ * Replaces ORBPL_TRACK_LOCAL_MAP (its P18 local map); not with STEREO. */
+#define ORBPL_TRACK_MAP 32
 int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam, int n_streams,
                             int device, int flags, orbpl_tracker** out);
 int orbpl_tracker_destroy(orbpl_tracker* tr);
@@ -496,6 +514,18 @@ int orbpl_tracker_line_timings(orbpl_tracker* tr, int max_steps, float* ms, int*
 int orbpl_tracker_set_history(orbpl_tracker* tr, int max_steps);
 int orbpl_tracker_get_history(orbpl_tracker* tr, int stream, int max_steps, float* Tcw,
                               int* counts12, int* n_steps);
+/* ORBPL_TRACK_MAP trackers: the recorded steps' 24 counts per step in the
+ * oracle's order (oracle_map_step): the 12 of get_history, then keyframe
+ * created (1, 2 = the initial one), keyframes, map points, map lines,
+ * temporal points, TrackReferenceKeyFrame ran, reference keyframe (-1 none),
+ * state (0 not initialised, 1 OK, 2 LOST), local keyframes, local map points
+ * searched, local map lines searched, temporal lines. */
+int orbpl_tracker_get_map_history(orbpl_tracker* tr, int stream, int max_steps, int* counts24,
+                                  int* n_steps);
+/* ORBPL_TRACK_MAP trackers: capacity flags of each stream's map since the last
+ * reset (1 keyframe table full: NeedNewKeyFrame declined; 2 point / line pool
+ * full; 4 local list full); 0 = the map matches the reference's. */
+int orbpl_tracker_get_map_errors(orbpl_tracker* tr, int* err);
 /* KeyFrame::ComputeBoW (KeyFrame.cc:67; every tracked frame is a keyframe,
  * P18) with `voc` (uploaded to the tracker's device; not owned, must outlive
  * the tracker or be unset with NULL): each step transforms the frame's

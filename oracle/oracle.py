@@ -694,3 +694,77 @@ class Vocabulary:
         if getattr(self, "h", None):
             lib().oracle_voc_destroy(self.h)
             self.h = None
+
+
+# ---- Tracking::Track with the map model (map_oracle.cpp) ----
+_setup_before_map = _setup
+
+
+def _setup(L):  # noqa: F811
+    _setup_before_map(L)
+    vp, i = C.c_void_p, C.c_int
+    L.oracle_map_create.argtypes = [vp, vp, i, i]
+    L.oracle_map_create.restype = vp
+    L.oracle_map_destroy.argtypes = [vp]
+    L.oracle_map_reset.argtypes = [vp, vp]
+    L.oracle_map_set_vocabulary.argtypes = [vp, vp]
+    L.oracle_map_step.argtypes = [vp, i, vp, vp, vp, vp]
+    L.oracle_map_keyframes.argtypes = [vp, i, vp, vp, i, vp]
+    L.oracle_map_points.argtypes = [vp, i, vp, vp, vp, i]
+
+
+MAP_COUNTS = ("nkeypoints", "nmatches", "ninliers", "nmatches_map", "ok", "nlines",
+              "line_matches", "line_nmatches_map", "local_matches", "local_inliers",
+              "local_line_matches", "local_line_inliers", "keyframe", "keyframes", "map_points",
+              "map_lines", "temporal_points", "trk", "ref_kf", "state", "local_keyframes",
+              "local_points", "local_lines", "temporal_lines")
+
+
+class MapVO:
+    """CPU oracle of Tracking::Track with the reference's map model
+    (UpdateLastFrame, NeedNewKeyFrame, CreateNewKeyFrame, observation counts,
+    covisibility local map; LocalMapping = ProcessNewKeyFrame, pinned P23).
+    flags: ORBPL_TRACK_LINES / ORBPL_TRACK_REFKF / ORBPL_TRACK_FIXED_LINE_JAC."""
+
+    def __init__(self, orb_params, cam, n_streams, use_lines=True, flags=0):
+        f = (TRACK_LINES if use_lines else 0) | flags
+        self.h = lib().oracle_map_create(C.byref(orb_params), C.byref(cam), n_streams, f)
+        self._voc = None
+
+    def reset(self, Tcw0=None):
+        T = None if Tcw0 is None else _c(Tcw0, np.float32)
+        lib().oracle_map_reset(self.h, None if T is None else _p(T))
+
+    def set_vocabulary(self, voc):
+        self._voc = voc
+        lib().oracle_map_set_vocabulary(self.h, voc.h if voc is not None else None)
+
+    def step(self, stream, gray, depth):
+        g = _c(gray, np.uint8)
+        d = _c(depth, np.float32)
+        T = np.zeros(16, np.float32)
+        o = np.zeros(24, np.int32)
+        rc = lib().oracle_map_step(self.h, stream, _p(g), _p(d), _p(T), _p(o))
+        assert rc == 0
+        return T.reshape(4, 4), dict(zip(MAP_COUNTS, (int(x) for x in o)))
+
+    def keyframes(self, stream, cap=64):
+        par = np.zeros(256, np.int32)
+        ord_ = np.zeros((256, cap), np.int32)
+        nord = np.zeros(256, np.int32)
+        n = lib().oracle_map_keyframes(self.h, stream, _p(par), _p(ord_), cap, _p(nord))
+        return par[:n], [ord_[k, :min(nord[k], cap)].copy() for k in range(n)]
+
+    def points(self, stream, cap=1 << 18):
+        nobs = np.zeros(cap, np.int32)
+        desc = np.zeros((cap, 32), np.uint8)
+        xyz = np.zeros((cap, 3), np.float32)
+        n = lib().oracle_map_points(self.h, stream, _p(nobs), _p(desc), _p(xyz), cap)
+        n = min(n, cap)
+        return nobs[:n], desc[:n], xyz[:n]
+
+    def __del__(self):
+        try:
+            lib().oracle_map_destroy(self.h)
+        except Exception:
+            pass

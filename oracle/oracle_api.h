@@ -104,6 +104,16 @@ int oracle_lvo_step(void* h, int stream, const uint8_t* gray, const float* depth
 int oracle_lvo_local_stats(void* h, int stream, int* out4);
 int oracle_lvo_step_stereo(void* h, int stream, const uint8_t* left, const uint8_t* right,
                            float* Tcw_out, int* out8);
+/* Tracking::Track with the map model (map_oracle.cpp) */
+void* oracle_map_create(const orbpl_orb_params* orb, const orbpl_camera* cam, int n_streams,
+                        int flags);
+void oracle_map_destroy(void* h);
+int oracle_map_reset(void* h, const float* Tcw0);
+int oracle_map_set_vocabulary(void* h, void* voc);
+int oracle_map_step(void* h, int stream, const uint8_t* gray, const float* depth, float* Tcw_out,
+                    int* out24);
+int oracle_map_keyframes(void* h, int stream, int* parent, int* ord, int cap, int* nord);
+int oracle_map_points(void* h, int stream, int* nobs, uint8_t* desc, float* xyz, int cap);
 #ifdef __cplusplus
 }
 #endif

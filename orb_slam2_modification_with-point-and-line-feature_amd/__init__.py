@@ -405,6 +405,8 @@ def _declare_track(L):
     L.orbpl_tracker_step_host.argtypes = [vp, vp, vp, C.c_float]
     L.orbpl_tracker_get_bow.argtypes = [vp, i, vp, vp, ip, vp, ip]
     L.orbpl_tracker_get_trk.argtypes = [vp, vp]
+    L.orbpl_tracker_get_map_history.argtypes = [vp, i, i, vp, ip]
+    L.orbpl_tracker_get_map_errors.argtypes = [vp, vp]
 
 
 _declare_orig = _declare
@@ -661,16 +663,18 @@ class Tracker:
     TRACK_LOCAL_MAP = 4
     TRACK_FIXED_LINE_JAC = 8
     TRACK_REFKF = 16
+    TRACK_MAP = 32
 
     def __init__(self, orb_params, camera, n_streams, device=0, lines=False, stereo=False,
-                 local_map=False, fixed_line_jac=False, refkf=False):
+                 local_map=False, fixed_line_jac=False, refkf=False, map=False):
         h = C.c_void_p()
         self.camera, self.S, self.device, self.use_lines = camera, n_streams, device, bool(lines)
         self.stereo = bool(stereo)
         flags = ((self.TRACK_LINES if lines else 0) | (self.TRACK_STEREO if stereo else 0) |
                  (self.TRACK_LOCAL_MAP if local_map else 0) |
                  (self.TRACK_FIXED_LINE_JAC if fixed_line_jac else 0) |
-                 (self.TRACK_REFKF if refkf else 0))
+                 (self.TRACK_REFKF if refkf else 0) | (self.TRACK_MAP if map else 0))
+        self.map = bool(map)
         check(lib().orbpl_tracker_create_ex(C.byref(orb_params), C.byref(camera), n_streams, device,
                                             flags, C.byref(h)),
               "orbpl_tracker_create_ex")
@@ -831,6 +835,28 @@ class Tracker:
         check(lib().orbpl_tracker_get_history(self._h, stream, max_steps, _ptr(T), _ptr(cnt),
                                               C.byref(n)), "orbpl_tracker_get_history")
         return T[:n.value], cnt[:n.value]
+
+    MAP_COUNTS = ("nkeypoints", "nmatches", "ninliers", "nmatches_map", "ok", "nlines",
+                  "line_matches", "line_nmatches_map", "local_matches", "local_inliers",
+                  "local_line_matches", "local_line_inliers", "keyframe", "keyframes",
+                  "map_points", "map_lines", "temporal_points", "trk", "ref_kf", "state",
+                  "local_keyframes", "local_points", "local_lines", "temporal_lines")
+
+    def map_history(self, stream, max_steps=4096):
+        """(n, 24) counts of one stream's recorded steps (map=True trackers), in
+        the order of MAP_COUNTS (the oracle's MapVO.step dictionary)."""
+        cnt = np.zeros((max_steps, 24), np.int32)
+        n = C.c_int(0)
+        check(lib().orbpl_tracker_get_map_history(self._h, stream, max_steps, _ptr(cnt),
+                                                  C.byref(n)), "orbpl_tracker_get_map_history")
+        return cnt[:n.value]
+
+    def map_errors(self):
+        """Per stream: capacity flags since the last reset (1 keyframe table
+        full, 2 point / line pool full, 4 local list full); 0 = exact."""
+        out = np.zeros(self.S, np.int32)
+        check(lib().orbpl_tracker_get_map_errors(self._h, _ptr(out)), "orbpl_tracker_get_map_errors")
+        return out
 
     STEREO_STAGES = ("right_extract", "stereo_match", "right_lines", "stereo_lines")
 

@@ -140,6 +140,11 @@ struct StreamState {
   int trk_go;          // enough BoW / line matches: the pose ran
   int trk_nlm;         // reference-keyframe line matches
   int trk_wiped;       // that line search's relaxed retry cleared the assignments
+  // map model (ORBPL_TRACK_MAP, map_kernels.h): keyframe created (1, 2 = the
+  // initial one), keyframes, map points, map lines, temporal points,
+  // TrackReferenceKeyFrame ran, reference keyframe, tracking state, local
+  // keyframes, local map points, local map lines, temporal lines
+  int map_out[12];
 };
 
 }  // namespace orbpl

@@ -17,6 +17,7 @@
 #include "track_kernels.h"
 #include "lsd_kernels.h"
 #include "lsd_math.h"
+#include "map_kernels.h"
 
 using namespace orbpl;
 
@@ -743,6 +744,13 @@ struct FrameBufs {
   uint8_t* loutlier = nullptr;
   uint8_t* has_ml = nullptr;
   float* ml_xyz = nullptr;
+  // map model (ORBPL_TRACK_MAP): the frame's map elements (pool id, -1, or a
+  // temporal element -2 - slot) and, as the last frame, the map point / line
+  // descriptors the matchers read
+  int* mpid = nullptr;
+  uint8_t* mp_desc = nullptr;
+  int* mlid = nullptr;
+  uint8_t* ml_desc = nullptr;
   // DBoW2 (orbpl_tracker_set_vocabulary): KeyFrame::ComputeBoW of the frame
   int32_t* feat_node = nullptr;   // FeatureVector: node per keypoint, -1 = stopped
   int32_t* feat_word = nullptr;
@@ -750,6 +758,19 @@ struct FrameBufs {
   uint32_t* bow_words = nullptr;  // BowVector (word order)
   double* bow_vals = nullptr;
   int* bow_n = nullptr;
+};
+
+// map-mode scratch of the matchers (local lists, reference-keyframe lines)
+struct MapExtra {
+  uint8_t* l_inview;
+  float *l_px, *l_py, *l_pxr, *l_vcos;
+  int* l_level;
+  int4* l_scratch;
+  uint8_t* ll_valid;
+  orbpl_keyline* ll_proj;
+  int* ll_src;
+  orbpl_keyline* trk_proj;
+  int* trk_src;
 };
 
 struct orbpl_tracker {
@@ -858,6 +879,14 @@ struct orbpl_tracker {
   StreamState* d_hist_state = nullptr;
   int* d_hist_n = nullptr;
   int* d_hist_nl = nullptr;
+  // map model (ORBPL_TRACK_MAP, map_kernels.hip): keyframe table and point /
+  // line pools per stream, the reference keyframe staged as a frame, the
+  // pose inputs in current-frame index space
+  int map = 0;
+  int map_kfc = 0;
+  MapArgs ma{};
+  MapExtra mx{};
+  std::vector<void*> map_allocs;
   std::vector<void*> allocs;
 };
 
@@ -872,12 +901,133 @@ static int tr_alloc(orbpl_tracker* t, void** p, size_t bytes) {
   return hipMemset(*p, 0, bytes ? bytes : 1) == hipSuccess ? ORBPL_OK : ORBPL_ERR_HIP;
 }
 
+// Map-model buffers for `kfc` keyframes per stream (pools of kfc x keypoint
+// capacity points and kfc x 80 lines, the local lists of the same sizes);
+// replaces earlier ones. Per-stream state is reset by the caller.
+
+static int map_alloc(orbpl_tracker* t, int kfc) {
+  MapExtra* x = &t->mx;
+  for (void* p : t->map_allocs) (void)hipFree(p);
+  t->map_allocs.clear();
+  const size_t S = t->S, K = t->kp_cap, L = kLineKeep, F = (size_t)kfc;
+  const size_t MPC = F * K, MLC = F * L;
+  auto A = [&](void** p, size_t bytes) -> int {
+    hipError_t e = hipMalloc(p, bytes ? bytes : 1);
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc (map model)", __LINE__);
+    t->map_allocs.push_back(*p);
+    return ORBPL_OK;
+  };
+#define MA(ptr, bytes)                                  \
+  do {                                                  \
+    int _r = A((void**)&(ptr), (bytes));                \
+    if (_r) return _r;                                  \
+  } while (0)
+  MapArgs& m = t->ma;
+  m.kfc = kfc;
+  m.kp_pitch = (int)K;
+  m.mpc = (long long)MPC;
+  m.mlc = (long long)MLC;
+  m.lines = t->lines;
+  m.lp = (long long)MPC;
+  m.llp = (long long)MLC;
+  MA(m.ms, S * sizeof(MapState));
+  MA(m.kf_T, S * F * 16 * 4);
+  MA(m.kf_Ow, S * F * 4 * 4);
+  MA(m.kf_N, S * F * 4);
+  MA(m.kf_NL, S * F * 4);
+  MA(m.kf_frame, S * F * 4);
+  MA(m.kf_mp, S * F * K * 4);
+  MA(m.kf_kp, S * F * K * sizeof(KeyPointD));
+  MA(m.kf_ur, S * F * K * 4);
+  MA(m.kf_desc, S * F * K * 32);
+  MA(m.kf_node, S * F * K * 4);
+  MA(m.kf_ml, S * F * L * 4);
+  MA(m.kf_ldesc, S * F * L * 32);
+  MA(m.kf_ds, S * F * L * 4);
+  MA(m.kf_de, S * F * L * 4);
+  MA(m.kf_w, S * F * F * 4);
+  MA(m.kf_ord, S * F * F);
+  MA(m.kf_nord, S * F * 4);
+  MA(m.kf_parent, S * F * 4);
+  MA(m.kf_first, S * F * 4);
+  MA(m.kf_child, S * F * 8);
+  MA(m.mp_pos, S * MPC * 16);
+  MA(m.mp_nrm, S * MPC * 16);
+  MA(m.mp_dist, S * MPC * 8);
+  MA(m.mp_desc, S * MPC * 32);
+  MA(m.mp_nobs, S * MPC * 4);
+  MA(m.mp_nob, S * MPC * 4);
+  MA(m.mp_obs, S * MPC * F * 4);
+  MA(m.mp_seen, S * MPC * 4);
+  MA(m.mp_tref, S * MPC * 4);
+  MA(m.ml_pos, S * MLC * 24);
+  MA(m.ml_desc, S * MLC * 32);
+  MA(m.ml_nobs, S * MLC * 4);
+  MA(m.ml_seen, S * MLC * 4);
+  MA(m.ml_tref, S * MLC * 4);
+  MA(m.r_n, S * 4);
+  MA(m.r_kps_un, S * K * sizeof(KeyPointD));
+  MA(m.r_desc, S * K * 32);
+  MA(m.r_has_mp, S * K);
+  MA(m.r_mp_xyz, S * K * 12);
+  MA(m.r_node, S * K * 4);
+  MA(m.r_mpid, S * K * 4);
+  MA(m.r_nl, S * 4);
+  MA(m.r_has_ml, S * L);
+  MA(m.r_ml_xyz, S * L * 24);
+  MA(m.r_ml_desc, S * L * 32);
+  MA(m.r_mlid, S * L * 4);
+  MA(m.trk_cur_nobs, S * L * 4);
+  MA(m.trk_lm, S * L * 4);
+  MA(m.trk_nml, S * 4);
+  MA(m.m2, S * K * 4);
+  MA(m.pxyz, S * K * 12);
+  MA(m.lm2, S * L * 4);
+  MA(m.lpxyz, S * L * 24);
+  MA(m.l_xyz, S * MPC * 12);
+  MA(m.l_nrm, S * MPC * 12);
+  MA(m.l_dmin, S * MPC * 4);
+  MA(m.l_dmax, S * MPC * 4);
+  MA(m.l_ldesc_pts, S * MPC * 32);
+  MA(m.l_count, S * 4);
+  MA(m.l_id, S * MPC * 4);
+  MA(m.ll_xyz, S * MLC * 24);
+  MA(m.ll_desc, S * MLC * 32);
+  MA(m.ll_count, S * 4);
+  MA(m.ll_id, S * MLC * 4);
+  MA(m.cur_nobs, S * K * 4);
+  MA(m.cur_nobs_l, S * L * 4);
+  MA(x->l_inview, S * MPC);
+  MA(x->l_px, S * MPC * 4);
+  MA(x->l_py, S * MPC * 4);
+  MA(x->l_pxr, S * MPC * 4);
+  MA(x->l_vcos, S * MPC * 4);
+  MA(x->l_level, S * MPC * 4);
+  MA(x->l_scratch, S * MPC * sizeof(int4));
+  MA(x->ll_valid, S * MLC);
+  MA(x->ll_proj, S * MLC * sizeof(orbpl_keyline));
+  MA(x->ll_src, S * MLC * 4);
+  MA(x->trk_proj, S * L * sizeof(orbpl_keyline));
+  MA(x->trk_src, S * L * 4);
+  int* lm_match = nullptr;
+  int* llm_match = nullptr;
+  MA(lm_match, S * K * 4);
+  MA(llm_match, S * L * 4);
+  m.lm_match = lm_match;
+  m.llm_match = llm_match;
+#undef MA
+  if (hipMemset(m.kf_w, 0, S * F * F * 4) != hipSuccess) return hip_fail(hipErrorUnknown, "hipMemset", __LINE__);
+  t->map_kfc = kfc;
+  return ORBPL_OK;
+}
+
 extern "C" {
 
 int orbpl_tracker_destroy(orbpl_tracker* t) {
   if (!t) return ORBPL_OK;
   (void)hipSetDevice(t->device);
   for (void* p : t->allocs) (void)hipFree(p);
+  for (void* p : t->map_allocs) (void)hipFree(p);
   if (t->tstream) (void)hipStreamSynchronize(t->tstream);
   for (auto& e : t->ring)
     if (e) (void)hipEventDestroy(e);
@@ -919,8 +1069,10 @@ int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam
                             int device, int flags, orbpl_tracker** out) {
   if (!orb || !cam || !out || n_streams <= 0) return arg_fail("bad argument");
   if (flags & ~(ORBPL_TRACK_LINES | ORBPL_TRACK_STEREO | ORBPL_TRACK_LOCAL_MAP |
-                ORBPL_TRACK_FIXED_LINE_JAC | ORBPL_TRACK_REFKF))
+                ORBPL_TRACK_FIXED_LINE_JAC | ORBPL_TRACK_REFKF | ORBPL_TRACK_MAP))
     return arg_fail("unknown tracker flag");
+  if ((flags & ORBPL_TRACK_MAP) && (flags & ORBPL_TRACK_STEREO))
+    return arg_fail("ORBPL_TRACK_MAP: RGB-D streams only");
   // ORBPL_TRACK_LINES | ORBPL_TRACK_STEREO: the defined stereo line mode (P17;
   // the reference's stereo Frame extracts no lines, Frame.cc:70-131)
   if ((flags & ORBPL_TRACK_STEREO) && cam->height > 1024)
@@ -933,6 +1085,8 @@ int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam
   t->fixed_line_jac = (flags & ORBPL_TRACK_FIXED_LINE_JAC) ? 1 : 0;
   t->local_map = (flags & ORBPL_TRACK_LOCAL_MAP) ? 1 : 0;
   t->refkf = (flags & ORBPL_TRACK_REFKF) ? 1 : 0;
+  t->map = (flags & ORBPL_TRACK_MAP) ? 1 : 0;
+  if (t->map) t->local_map = 0;   // the map model has its own TrackLocalMap
   t->scale_factor = orb->scale_factor;
   t->S = n_streams;
   t->W = cam->width;
@@ -976,6 +1130,12 @@ int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam
     TA(f.has_mp, S * K);
     TA(f.mp_xyz, S * K * 12);
     TA(f.nobs, S * K * 4);
+    if (t->map) {
+      TA(f.mpid, S * K * 4);
+      TA(f.mp_desc, S * K * 32);
+      TA(f.mlid, S * kLineKeep * 4);
+      TA(f.ml_desc, S * kLineKeep * 32);
+    }
     if (t->lines) {
       const size_t L = S * kLineKeep;
       TA(f.kl, L * sizeof(orbpl_keyline));
@@ -1073,6 +1233,19 @@ int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam
     }
   }
 #undef TA
+  if (t->map) {
+    int kfc = 32;
+    if (const char* e = getenv("ORBPL_MAP_KF")) kfc = atoi(e);
+    if (kfc < 2 || kfc > kMapMaxKF) {
+      orbpl_tracker_destroy(t);
+      return arg_fail("ORBPL_MAP_KF out of [2, 64]");
+    }
+    rc = map_alloc(t, kfc);
+    if (rc) {
+      orbpl_tracker_destroy(t);
+      return rc;
+    }
+  }
   t->ring.assign(orbpl_tracker::kRing * orbpl_tracker::kEv, nullptr);
   for (auto& e : t->ring)
     if (hipEventCreate(&e) != hipSuccess) {
@@ -1151,12 +1324,252 @@ int orbpl_tracker_reset(orbpl_tracker* t, const float* Tcw0) {
   if (t->rlstream) HIP_CHECK(hipStreamSynchronize(t->rlstream));
   HIP_CHECK(hipMemcpy(t->d_state, st.data(), sizeof(StreamState) * t->S, hipMemcpyHostToDevice));
   if (t->d_err) HIP_CHECK(hipMemset(t->d_err, 0, 4));
+  if (t->map) {
+    // every stream starts uninitialised; the first frame takes its Tcw0
+    float* dT0 = nullptr;
+    if (Tcw0) {
+      HIP_CHECK(hipMalloc(&dT0, (size_t)t->S * 64));
+      HIP_CHECK(hipMemcpy(dT0, Tcw0, (size_t)t->S * 64, hipMemcpyHostToDevice));
+    }
+    launch_map_reset(t->ma, dT0, t->S, nullptr);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipDeviceSynchronize());
+    if (dT0) HIP_CHECK(hipFree(dT0));
+  }
   t->hist_count = 0;
   t->lm_step = 0;
   return ORBPL_OK;
 }
 
 }  // extern "C"
+
+// Tracking::Track with the map model (ORBPL_TRACK_MAP) on the tracking stream:
+// the map kernels (map_kernels.hip) around the batched matchers and k_pose.
+// ev: the step's events (brackets as in the P18 path).
+static int map_track(orbpl_tracker* t, FrameBufs& C, FrameBufs& L, const LineTrackArgs& la0,
+                      hipEvent_t* ev, hipStream_t ts) {
+  const int S = t->S, K = t->kp_cap;
+  const int pstride = (int)(sizeof(StreamState) / sizeof(float));
+  char* stb = reinterpret_cast<char*>(t->d_state);
+  float* dTcw = reinterpret_cast<float*>(stb + offsetof(StreamState, Tcw));
+  float* dTlast = reinterpret_cast<float*>(stb + offsetof(StreamState, Tlast));
+  auto field = [&](size_t off) { return reinterpret_cast<int*>(stb + off); };
+  MapArgs a = t->ma;
+  a.st = t->d_state;
+  a.lines = t->lines;
+  a.refkf = t->refkf;
+  a.vocab = t->voc ? 1 : 0;
+  a.n = C.n; a.kps_un = C.kps_un; a.depth = C.depth; a.uright = C.uright; a.desc = C.desc;
+  a.feat_node = C.feat_node; a.match = C.match; a.outlier = C.outlier; a.mpid = C.mpid;
+  a.nl = C.nl; a.kl_un = C.kl_un; a.dstart = C.dstart; a.dend = C.dend; a.ldesc = C.ldesc;
+  a.lmatch = C.lmatch; a.loutlier = C.loutlier; a.mlid = C.mlid;
+  a.l_n = L.n; a.l_kps_un = L.kps_un; a.l_depth = L.depth; a.l_desc = L.desc; a.l_mpid = L.mpid;
+  a.l_has_mp = L.has_mp; a.l_mp_xyz = L.mp_xyz; a.l_mp_desc = L.mp_desc; a.l_nobs = L.nobs;
+  a.l_nl = L.nl; a.l_kl_un = L.kl_un; a.l_dstart = L.dstart; a.l_dend = L.dend; a.l_ldesc = L.ldesc;
+  a.l_mlid = L.mlid; a.l_has_ml = L.has_ml; a.l_ml_xyz = L.ml_xyz; a.l_ml_desc = L.ml_desc;
+  const MapExtra& x = t->mx;
+  // ---- frame id, path, UpdateLastFrame, the constant-velocity prediction ----
+  launch_map_begin(t->consts, a, S, ts);
+  // ---- TrackWithMotionModel (Tracking.cc:1212-1330) ----
+  MatchLaunch m{};
+  m.cur_kps_un = C.kps_un;
+  m.cur_desc = C.desc;
+  m.cur_uright = C.uright;
+  m.cur_gcell = C.gcell;
+  m.cur_n = C.n;
+  m.last_kps_un = L.kps_un;
+  m.last_has_mp = L.has_mp;
+  m.last_outlier = L.outlier;
+  m.last_xyz = L.mp_xyz;
+  m.last_desc = L.mp_desc;     // pMP->GetDescriptor()
+  m.last_nobs = L.nobs;
+  m.last_n = L.n;
+  m.kp_pitch = K;
+  m.Tcw = dTcw;
+  m.Tlw = dTlast;
+  m.pose_stride = pstride;
+  m.match = C.match;
+  m.nmatches = field(offsetof(StreamState, nmatches));
+  m.nm_stride = pstride;
+  m.th = 15.0f;
+  m.mono = 0;
+  m.check_ori = 1;
+  m.retry = 1;
+  m.active = t->d_state;
+  launch_match_last(t->consts, m, S, ts);
+  HIP_CHECK(hipEventRecord(ev[8], ts));
+  if (t->lines) {
+    LineTrackArgs la = la0;
+    la.last_desc = L.ml_desc;  // the map lines' descriptors
+    launch_line_match(t->consts, la, t->d_state, S, ts);
+  }
+  HIP_CHECK(hipEventRecord(ev[14], ts));
+  PoseLaunch p{};
+  p.kps_un = C.kps_un;
+  p.uright = C.uright;
+  p.match = C.match;
+  p.mp_xyz = L.mp_xyz;
+  p.n = C.n;
+  p.kp_pitch = K;
+  p.Tcw = dTcw;
+  p.pose_stride = pstride;
+  p.outlier = C.outlier;
+  p.ninliers = field(offsetof(StreamState, ninliers));
+  p.nm_stride = pstride;
+  p.active = t->d_state;
+  p.edges = t->d_edges;
+  if (t->lines) {
+    p.t_kl_un = C.kl_un;
+    p.t_lmatch = C.lmatch;
+    p.t_ml_xyz = L.ml_xyz;
+    p.t_nl = C.nl;
+    p.t_loutlier = C.loutlier;
+    p.lpitch = kLineKeep;
+  }
+  p.fixed_line_jac = t->fixed_line_jac;
+  HIP_CHECK(hipEventRecord(ev[28], ts));
+  launch_pose(t->consts, p, S, ts);
+  HIP_CHECK(hipEventRecord(ev[29], ts));
+  launch_map_resolve_motion(a, S, ts);
+  // the later poses read the frame's map elements in its own index space
+  PoseLaunch pm = p;
+  pm.match = a.m2;
+  pm.mp_xyz = a.pxyz;
+  if (t->lines) {
+    pm.t_lmatch = a.lm2;
+    pm.t_ml_xyz = a.lpxyz;
+  }
+  HIP_CHECK(hipEventRecord(ev[30], ts));
+  if (t->refkf) {
+    // ---- TrackReferenceKeyFrame (Tracking.cc:942-1032) ----
+    TrkArgs ta{};
+    ta.st = t->d_state;
+    ta.kp_pitch = K;
+    ta.lines = t->lines;
+    ta.n = C.n;
+    ta.match = C.match;
+    ta.kps_un = C.kps_un;
+    ta.desc = C.desc;
+    ta.feat_node = C.feat_node;
+    ta.last_n = a.r_n;
+    ta.last_kps_un = a.r_kps_un;
+    ta.last_desc = a.r_desc;
+    ta.last_has_mp = a.r_has_mp;
+    ta.last_feat_node = a.r_node;
+    launch_trk_bow(ta, S, ts);
+    if (t->lines) {
+      LineListArgs lr{};
+      lr.Tcw = dTcw;
+      lr.cur_kl_un = C.kl_un;
+      lr.cur_desc = C.ldesc;
+      lr.cur_nobs = a.trk_cur_nobs;
+      lr.valid = a.r_has_ml;
+      lr.ml_xyz6 = a.r_ml_xyz;
+      lr.ml_desc = a.r_ml_desc;
+      lr.proj_kl = x.trk_proj;
+      lr.proj_src = x.trk_src;
+      lr.match = a.trk_lm;
+      lr.nmatches = field(offsetof(StreamState, trk_nlm));
+      lr.wiped = field(offsetof(StreamState, trk_wiped));
+      lr.refkf = 1;
+      lr.ncur_arr = C.nl;
+      lr.nml_arr = a.trk_nml;
+      lr.cur_pitch = kLineKeep;
+      lr.ml_pitch = kLineKeep;
+      lr.pose_stride = pstride;
+      lr.nm_stride = pstride;
+      launch_line_match_list(t->consts, lr, ts, S);
+    }
+    launch_map_trk_merge(a, S, ts);
+    PoseLaunch pt = pm;
+    pt.gate_lm = 2;
+    launch_pose(t->consts, pt, S, ts);
+  }
+  HIP_CHECK(hipEventRecord(ev[31], ts));
+  launch_map_resolve_trk(a, S, ts);
+  HIP_CHECK(hipEventRecord(ev[9], ts));
+  // ---- TrackLocalMap (Tracking.cc:1332-1420) ----
+  launch_map_local(a, S, ts);
+  InFrustumArgs fa{};
+  fa.Tcw = dTcw;
+  fa.xyz = a.l_xyz;
+  fa.normal = a.l_nrm;
+  fa.min_dist = a.l_dmin;
+  fa.max_dist = a.l_dmax;
+  fa.view_cos_limit = 0.5f;
+  fa.in_view = x.l_inview;
+  fa.proj_x = x.l_px;
+  fa.proj_y = x.l_py;
+  fa.proj_xr = x.l_pxr;
+  fa.level = x.l_level;
+  fa.view_cos = x.l_vcos;
+  fa.n_arr = a.l_count;
+  fa.pitch = a.lp;
+  fa.pose_stride = pstride;
+  const float log_scale = (float)lsdm::log_((double)t->scale_factor);   // P15
+  launch_in_frustum(t->consts, log_scale, fa, ts, S);
+  LocalArgs ml{};
+  ml.kps_un = C.kps_un;
+  ml.desc = C.desc;
+  ml.uright = C.uright;
+  ml.cur_nobs = a.cur_nobs;
+  ml.in_view = x.l_inview;
+  ml.proj_x = x.l_px;
+  ml.proj_y = x.l_py;
+  ml.proj_xr = x.l_pxr;
+  ml.level = x.l_level;
+  ml.view_cos = x.l_vcos;
+  ml.mp_desc = a.l_ldesc_pts;
+  ml.mp_nobs = nullptr;        // every local map point is observed
+  ml.th = t->lm_step < 2 ? 5.0f : 3.0f;   // mnLastRelocFrameId + 2 (Tracking.cc:1731-1738)
+  ml.nnratio = 0.8f;
+  ml.match = const_cast<int*>(a.lm_match);
+  ml.nmatches = field(offsetof(StreamState, lm_nlocal));
+  ml.scratch = x.l_scratch;
+  ml.n_arr = C.n;
+  ml.nmp_arr = a.l_count;
+  ml.kp_pitch = K;
+  ml.mp_pitch = a.lp;
+  ml.nm_stride = pstride;
+  HIP_CHECK(hipEventRecord(ev[32], ts));
+  launch_match_local(t->consts, ml, ts, S);
+  HIP_CHECK(hipEventRecord(ev[33], ts));
+  if (t->lines) {
+    launch_line_in_frustum_batched(dTcw, pstride, a.ll_count, a.llp, a.ll_xyz, x.ll_valid, S, ts);
+    LineListArgs l3{};
+    l3.Tcw = dTcw;
+    l3.cur_kl_un = C.kl_un;
+    l3.cur_desc = C.ldesc;
+    l3.cur_nobs = a.cur_nobs_l;
+    l3.valid = x.ll_valid;
+    l3.ml_xyz6 = a.ll_xyz;
+    l3.ml_desc = a.ll_desc;
+    l3.proj_kl = x.ll_proj;
+    l3.proj_src = x.ll_src;
+    l3.match = const_cast<int*>(a.llm_match);
+    l3.nmatches = field(offsetof(StreamState, lm_nllocal));
+    l3.wiped = field(offsetof(StreamState, lm_wiped));
+    l3.ncur_arr = C.nl;
+    l3.nml_arr = a.ll_count;
+    l3.cur_pitch = kLineKeep;
+    l3.ml_pitch = a.llp;
+    l3.pose_stride = pstride;
+    l3.nm_stride = pstride;
+    launch_line_match_list(t->consts, l3, ts, S);
+  }
+  launch_map_assemble(a, S, ts);
+  PoseLaunch p2 = pm;
+  p2.ninliers = field(offsetof(StreamState, lm_ninl));
+  p2.gate_lm = 1;
+  HIP_CHECK(hipEventRecord(ev[34], ts));
+  launch_pose(t->consts, p2, S, ts);
+  HIP_CHECK(hipEventRecord(ev[35], ts));
+  HIP_CHECK(hipEventRecord(ev[26], ts));
+  // ---- decision, keyframe insertion, ProcessNewKeyFrame, relative pose ----
+  launch_map_finish(t->consts, a, S, ts);
+  t->lm_step++;
+  return ORBPL_OK;
+}
 
 // One TrackWithMotionModel step for every stream: RGB-D (d_depth) or stereo
 // (d_right, ORBPL_TRACK_STEREO trackers).
@@ -1304,6 +1717,10 @@ static int tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_
   HIP_CHECK(hipStreamWaitEvent(ts, ev[6], 0));
   if (t->lines) HIP_CHECK(hipStreamWaitEvent(ts, ev[13], 0));
   HIP_CHECK(hipEventRecord(ev[7], ts));
+  if (t->map) {
+    const int mrc = map_track(t, C, L, la, ev, ts);
+    if (mrc) return mrc;
+  } else {
   launch_predict(t->d_state, S, ts);
   MatchLaunch m{};
   m.cur_kps_un = C.kps_un;
@@ -1582,6 +1999,7 @@ static int tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_
     launch_lm_push(t->consts, lm, S, ts);   // the frame joins the local map
     t->lm_step++;
   }
+  }   // !t->map
   HIP_CHECK(hipEventRecord(ev[10], ts));
   if (t->hist_count < t->hist_cap) {
     const size_t k = (size_t)t->hist_count++ * S;
@@ -1863,11 +2281,42 @@ int orbpl_tracker_get_history(orbpl_tracker* t, int stream, int max_steps, float
       int* c = counts12 + 12 * k;
       c[0] = nk; c[1] = st.nmatches; c[2] = st.ninliers; c[3] = st.nmatches_map; c[4] = st.ok;
       c[5] = nl; c[6] = t->lines ? st.nlmatches : 0; c[7] = t->lines ? st.nlmatches_map : 0;
-      const bool lm = t->local_map && st.lm_active;
+      const bool lm = (t->local_map || t->map) && st.lm_active;
       c[8] = lm ? st.lm_nlocal : 0; c[9] = lm ? st.lm_inl : 0;
       c[10] = lm && t->lines ? st.lm_nllocal : 0; c[11] = lm && t->lines ? st.lm_linl : 0;
     }
   }
+  return ORBPL_OK;
+}
+
+int orbpl_tracker_get_map_history(orbpl_tracker* t, int stream, int max_steps, int* counts24,
+                                  int* n_steps) {
+  if (!t || !n_steps || !counts24 || stream < 0 || stream >= t->S || max_steps < 0)
+    return arg_fail("bad argument");
+  if (!t->map) return arg_fail("tracker created without ORBPL_TRACK_MAP");
+  std::vector<int> c12((size_t)std::max(max_steps, 1) * 12);
+  int rc = orbpl_tracker_get_history(t, stream, max_steps, nullptr, c12.data(), n_steps);
+  if (rc) return rc;
+  for (int k = 0; k < *n_steps; k++) {
+    StreamState st;
+    HIP_CHECK(hipMemcpy(&st, t->d_hist_state + (size_t)k * t->S + stream, sizeof(st),
+                        hipMemcpyDeviceToHost));
+    int* c = counts24 + 24 * k;
+    for (int q = 0; q < 12; q++) c[q] = c12[(size_t)k * 12 + q];
+    for (int q = 0; q < kMapOut; q++) c[12 + q] = st.map_out[q];
+  }
+  return ORBPL_OK;
+}
+
+int orbpl_tracker_get_map_errors(orbpl_tracker* t, int* err) {
+  if (!t || !err) return arg_fail("NULL argument");
+  if (!t->map) return arg_fail("tracker created without ORBPL_TRACK_MAP");
+  HIP_CHECK(hipSetDevice(t->device));
+  HIP_CHECK(hipStreamSynchronize(t->tstream));
+  HIP_CHECK(hipStreamSynchronize(t->stream));
+  std::vector<MapState> ms(t->S);
+  HIP_CHECK(hipMemcpy(ms.data(), t->ma.ms, sizeof(MapState) * t->S, hipMemcpyDeviceToHost));
+  for (int s = 0; s < t->S; s++) err[s] = ms[s].err;
   return ORBPL_OK;
 }
 
@@ -2087,7 +2536,7 @@ int orbpl_tracker_get_local_stats(orbpl_tracker* t, int* local_matches, int* loc
   std::vector<StreamState> st(t->S);
   HIP_CHECK(hipMemcpy(st.data(), t->d_state, sizeof(StreamState) * t->S, hipMemcpyDeviceToHost));
   for (int s = 0; s < t->S; s++) {
-    const bool lm = t->local_map && st[s].lm_active;
+    const bool lm = (t->local_map || t->map) && st[s].lm_active;
     if (local_matches) local_matches[s] = lm ? st[s].lm_nlocal : 0;
     if (local_inliers) local_inliers[s] = lm ? st[s].lm_inl : 0;
     if (local_line_matches) local_line_matches[s] = lm && t->lines ? st[s].lm_nllocal : 0;

@@ -1,0 +1,89 @@
+"""ORBPL_TRACK_MAP: Tracking::Track with the reference's map model on the
+device (map_kernels.hip) against the oracle's restatement (map_oracle.cpp,
+pinned P23-P25): every step's 24 counts identical (matches, inliers, the
+TrackLocalMap counts, keyframe decisions, map sizes, temporal points / lines,
+the TrackReferenceKeyFrame choice, the reference keyframe, the state and the
+local map sizes), poses within POSE_TOL."""
+import numpy as np
+import pytest
+
+from _scenes import sequence
+
+pytestmark = pytest.mark.gpu
+
+POSE_TOL = 1e-4   # north_star: pose within 1e-4 RMSE (max-abs used here: stricter)
+
+
+def _run(orbpl, oracle, lines, refkf, S, F, seed, turn=None, pipelined=False):
+    seqs = [sequence(F, seed + s, cam_name="TUM3" if lines else "TUM1") for s in range(S)]
+    frames = [[sq[2][f] for f in range(F)] for sq in seqs]
+    if turn is not None:
+        s, f0 = turn
+        for f in range(f0, F):
+            g, d = frames[s][f]
+            frames[s][f] = (np.ascontiguousarray(g[::-1, ::-1]), np.ascontiguousarray(d[::-1, ::-1]))
+    cfg = seqs[0][0]
+    flags = oracle.TRACK_REFKF if refkf else 0
+    mvo = oracle.MapVO(oracle.params(), oracle.camera(cfg), S, use_lines=lines, flags=flags)
+    tr = orbpl.Tracker(orbpl.OrbParams(1000, 1.2, 8, 20, 7), orbpl.make_camera(cfg), S, lines=lines,
+                       refkf=refkf, map=True)
+    if refkf:
+        from _vocab import vocabulary
+        path, _ = vocabulary(k=10, L=5, seed=3, n_frames=8)
+        voc = orbpl.ORBVocabulary(path)
+        mvo.set_vocabulary(oracle.Vocabulary(path))
+        tr.set_vocabulary(voc, 4)
+    tr.set_pipelined(pipelined)
+    T0 = np.stack([np.linalg.inv(sq[1][0]).astype(np.float32) for sq in seqs])
+    mvo.reset(T0.reshape(S, 16))
+    tr.reset(T0.reshape(S, 16))
+    tr.set_history(F)
+    fa, fb = S * 640 * 480, S * 640 * 480 * 4
+    a = orbpl.DeviceBuffer(F * fa)
+    b = orbpl.DeviceBuffer(F * fb)
+    for f in range(F):
+        a.upload(np.stack([frames[s][f][0] for s in range(S)]), offset=f * fa)
+        b.upload(np.stack([frames[s][f][1] for s in range(S)]), offset=f * fb)
+        tr.step_device(a.ptr + f * fa, b.ptr + f * fb)
+    tr.synchronize()
+    ref = [[mvo.step(s, *frames[s][f]) for f in range(F)] for s in range(S)]
+    keys = orbpl.Tracker.MAP_COUNTS
+    assert tuple(keys) == tuple(oracle.MAP_COUNTS)
+    out = []
+    for s in range(S):
+        Th, _ = tr.history(s)
+        Ch = tr.map_history(s)
+        assert len(Th) == F and len(Ch) == F
+        for f in range(F):
+            To, co = ref[s][f]
+            want = [co[k] for k in keys]
+            got = [int(x) for x in Ch[f]]
+            assert got == want, (s, f, [(k, g, w) for k, g, w in zip(keys, got, want) if g != w])
+            assert np.abs(Th[f] - To).max() < POSE_TOL, (s, f, np.abs(Th[f] - To).max())
+        out.append([r[1] for r in ref[s]])
+    assert (tr.map_errors() == 0).all()
+    return out
+
+
+@pytest.mark.parametrize("lines,refkf,pipelined", [(True, True, False), (False, True, True),
+                                                   (True, False, True)])
+def test_map_tracker_matches_oracle(orbpl, oracle, lines, refkf, pipelined):
+    """Initialisation, motion model / reference keyframe, covisibility local
+    map, keyframe insertion: 8 frames of 2 streams, every count identical."""
+    res = _run(orbpl, oracle, lines, refkf, S=2, F=8, seed=110, pipelined=pipelined)
+    for r in res:
+        assert r[0]["keyframe"] == 2 and r[0]["state"] == 1      # StereoInitialization
+        assert all(c["ok"] == 1 for c in r[1:])
+        assert r[-1]["local_points"] > 0                          # the covisibility local map
+    assert any(c["keyframe"] == 1 for r in res for c in r[1:])    # CreateNewKeyFrame ran
+    if refkf:
+        assert all(r[1]["trk"] == 1 for r in res)                 # no velocity yet
+
+
+def test_map_tracker_lost_and_reset(orbpl, oracle):
+    """A stream whose images turn by 180 degrees mid-sequence: the trackers
+    fail, go LOST and reset (<= 5 keyframes), then initialise again -- the same
+    states, counts and poses as the oracle."""
+    res = _run(orbpl, oracle, True, True, S=2, F=8, seed=130, turn=(1, 4))
+    st = [c["state"] for c in res[1]]
+    assert 2 in st or 0 in st[4:], st
