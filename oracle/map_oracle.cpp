@@ -41,6 +41,7 @@
 #include <cstring>
 #include <map>
 #include <set>
+#include <thread>
 #include <vector>
 
 #include "oracle_api.h"
@@ -396,14 +397,29 @@ static MapPoint new_point(const float* pos, int kf) {
 }
 
 // ---- frame helpers ----
+// Frame::Frame(RGB-D) (Frame.cc:135-205). flags & kTwoThreads: ORB and the
+// LineExtractor on two host threads as the reference (Frame.cc:152-155).
+constexpr int kTwoThreads = 1 << 16;
 static void extract(MapVO* v, const uint8_t* gray, const float* depth, Frame& F) {
   const orbpl_camera& cam = v->cam;
+  std::vector<orbpl_keyline> kl(kKeepLines);
+  std::vector<uint8_t> ld(kKeepLines * 32);
+  std::vector<double> coef(kKeepLines * 3);
+  int nl = 0, nd = 0;
+  auto lines = [&]() {
+    oracle_line_extract(gray, cam.width, cam.height, kl.data(), ld.data(), coef.data(), kKeepLines,
+                        &nl, &nd);
+  };
+  std::thread lt;
+  if (v->use_lines && (v->flags & kTwoThreads)) lt = std::thread(lines);
   const int cap = v->orb.nfeatures * 2 + 64;
   std::vector<orbpl_keypoint> kps(cap);
   std::vector<uint8_t> desc((size_t)cap * 32);
   int n = 0;
   oracle_orb_extract(&v->orb, gray, cam.width, cam.height, cam.width, kps.data(), desc.data(), cap,
                      &n, nullptr);
+  if (lt.joinable()) lt.join();
+  else if (v->use_lines) lines();
   kps.resize(n);
   desc.resize((size_t)n * 32);
   F.N = n;
@@ -429,12 +445,6 @@ static void extract(MapVO* v, const uint8_t* gray, const float* depth, Frame& F)
   F.outl.assign(n, 0);
   F.NL = 0;
   if (v->use_lines) {
-    std::vector<orbpl_keyline> kl(kKeepLines);
-    std::vector<uint8_t> ld(kKeepLines * 32);
-    std::vector<double> coef(kKeepLines * 3);
-    int nl = 0, nd = 0;
-    oracle_line_extract(gray, cam.width, cam.height, kl.data(), ld.data(), coef.data(), kKeepLines,
-                        &nl, &nd);
     F.NL = nl;
     F.kl_un.resize(nl);
     F.dstart.resize(nl);

@@ -724,7 +724,8 @@ class MapVO:
     """CPU oracle of Tracking::Track with the reference's map model
     (UpdateLastFrame, NeedNewKeyFrame, CreateNewKeyFrame, observation counts,
     covisibility local map; LocalMapping = ProcessNewKeyFrame, pinned P23).
-    flags: ORBPL_TRACK_LINES / ORBPL_TRACK_REFKF / ORBPL_TRACK_FIXED_LINE_JAC."""
+    flags: ORBPL_TRACK_LINES / ORBPL_TRACK_REFKF / ORBPL_TRACK_FIXED_LINE_JAC and
+    TWO_THREADS (ORB || LineExtractor on two host threads, Frame.cc:152-155)."""
 
     def __init__(self, orb_params, cam, n_streams, use_lines=True, flags=0):
         f = (TRACK_LINES if use_lines else 0) | flags

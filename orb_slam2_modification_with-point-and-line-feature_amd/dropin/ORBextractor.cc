@@ -24,9 +24,10 @@ ORBextractor::ORBextractor(int _nfeatures, float _scaleFactor, int _nlevels, int
   mnFeaturesPerLevel.assign(nlevels, 0);
   std::vector<int> lw(nlevels), lh(nlevels);
   int cap = 0;
-  // a geometry large enough for every level; the scale tables and budgets do
-  // not depend on it
-  check(orbx_describe(&params_, 2048, 2048, lw.data(), lh.data(), mnFeaturesPerLevel.data(),
+  // a geometry whose every level passes the library's bounds (<= 1024 FAST
+  // cells per level, coarse levels large enough); the scale tables and
+  // budgets do not depend on it
+  check(orbx_describe(&params_, 960, 960, lw.data(), lh.data(), mnFeaturesPerLevel.data(),
                       mvScaleFactor.data(), &cap));
   mvInvScaleFactor.resize(nlevels);
   mvLevelSigma2.resize(nlevels);
