@@ -256,12 +256,29 @@ def oracle_vocabulary(O):
     return VOCAB["oracle"]
 
 
-def oracle_vo(O, wl, flags=0):
+def map_mode(args, wl):
+    """Tracking::Track with the reference's map model (ORBPL_TRACK_MAP) for
+    the RGB-D workloads; the stereo ones keep the P18 local map."""
+    return bool(args.map) and not wl["stereo"]
+
+
+def map_capacity(total_steps):
+    """Keyframe slots per stream for a tracker that runs `total_steps` steps:
+    at most one keyframe per step, so the map never declines one (the
+    ORBPL_MAP_KF environment read at tracker creation; 64 at most)."""
+    os.environ["ORBPL_MAP_KF"] = str(max(2, min(64, total_steps + 1)))
+
+
+def oracle_vo(O, wl, flags=0, use_map=False):
     """The oracle's tracking loop for a workload (oracle/line_track_oracle.cpp
-    LVO with the tracker's flags and vocabulary); returns (vo, step(vo, a, b))."""
+    LVO, or map_oracle.cpp MapVO for the map model, with the tracker's flags
+    and vocabulary); returns (vo, step(vo, a, b))."""
     import orbpl.synth as synth
     cam = O.camera(getattr(synth, wl["cam"]))
-    vo = O.LVO(O.params(*wl["orb"]), cam, 1, use_lines=wl["lines"], flags=flags)
+    if use_map:
+        vo = O.MapVO(O.params(*wl["orb"]), cam, 1, use_lines=wl["lines"], flags=flags)
+    else:
+        vo = O.LVO(O.params(*wl["orb"]), cam, 1, use_lines=wl["lines"], flags=flags)
     voc = oracle_vocabulary(O)
     if voc is not None:
         vo.set_vocabulary(voc)
@@ -275,30 +292,34 @@ OUT8 = ("nkeypoints", "nmatches", "ninliers", "nmatches_map", "ok", "nlines", "l
         "local_line_inliers")
 
 
-def parity_check(T_gpu, C_gpu, streams, gray, depth, L, workload, flags=0):
+def parity_check(T_gpu, C_gpu, streams, gray, depth, L, workload, flags=0, use_map=False):
     """Replay `streams` of the timed tracker on the CPU oracle over the same
     frames (one host thread per stream) and compare every step: the 12 counts
-    exactly, the pose to POSE_TOL. T_gpu[k]: (n, 4, 4), C_gpu[k]: (n, 12)."""
+    (24 with the map model: + keyframe decisions, map sizes, temporal points /
+    lines, reference keyframe, state, local map sizes) exactly, the pose to
+    POSE_TOL. T_gpu[k]: (n, 4, 4), C_gpu[k]: (n, 12 | 24)."""
     from _pkg import load_oracle
     import orbpl.tum as tum
     O = load_oracle()
     wl = WORKLOADS[workload]
+    keys = O.MAP_COUNTS if use_map else OUT8
     n = min(len(T) for T in T_gpu)
     T_ref = np.zeros((len(streams), n, 4, 4), np.float32)
-    C_ref = np.zeros((len(streams), n, 12), np.int32)
+    C_ref = np.zeros((len(streams), n, len(keys)), np.int32)
 
     errors = []
 
     def worker(k, s):
         try:
-            vo, vstep = oracle_vo(O, wl, flags)
+            vo, vstep = oracle_vo(O, wl, flags, use_map)
             vo.reset(np.linalg.inv(L.Twc(s, 0)).astype(np.float32).reshape(1, 16))
             for t in range(n):
                 e = L.elem(s, t)
                 T, st = vstep(vo, gray[e], depth[e])
-                st.update(vo.local_stats(0))
+                if not use_map:
+                    st.update(vo.local_stats(0))
                 T_ref[k, t] = T
-                C_ref[k, t] = [st[key] for key in OUT8]
+                C_ref[k, t] = [st[key] for key in keys]
         except Exception as ex:  # surface, do not let a thread swallow it
             errors.append(ex)
 
@@ -311,18 +332,24 @@ def parity_check(T_gpu, C_gpu, streams, gray, depth, L, workload, flags=0):
         raise errors[0]
     Tg = np.stack([T[:n] for T in T_gpu])
     Cg = np.stack([c[:n] for c in C_gpu])
-    bad = [(int(streams[k]), int(t), OUT8[i]) for k, t, i in zip(*np.nonzero(Cg != C_ref))]
+    bad = [(int(streams[k]), int(t), keys[i]) for k, t, i in zip(*np.nonzero(Cg != C_ref))]
     dmax = float(np.abs(Tg - T_ref).max()) if n else 0.0
     gt = np.stack([np.linalg.inv(L.Twc(s, t)) for s in streams for t in range(n)])
     cg = tum.camera_centres(Tg.reshape(-1, 4, 4))
     cr = tum.camera_centres(T_ref.reshape(-1, 4, 4))
     cgt = tum.camera_centres(gt)
-    return {"source": "timed tracker (device-side per-step history)", "streams": [int(s) for s in streams],
+    out = {"source": "timed tracker (device-side per-step history)", "streams": [int(s) for s in streams],
             "steps_checked": n, "counts_equal": not bad, "count_mismatches": bad[:10],
             "max_abs_pose_diff_vs_ref": float(f"{dmax:.3e}"), "pose_tol": POSE_TOL,
             "pass": (not bad) and dmax < POSE_TOL,
             "ate_rmse_vs_gt_m": round(tum.ate(cg, cgt)["rmse"], 6) if n > 2 else None,
-            "ref_ate_rmse_vs_gt_m": round(tum.ate(cr, cgt)["rmse"], 6) if n > 2 else None}
+            "ref_ate_rmse_vs_gt_m": round(tum.ate(cr, cgt)["rmse"], 6) if n > 2 else None,
+            "oracle": "MapVO (map model)" if use_map else "LVO"}
+    if use_map and n:
+        kf = keys.index("keyframes")
+        out["keyframes_last_step"] = [int(c) for c in C_ref[:, n - 1, kf]]
+        out["keyframes_created"] = int((C_ref[:, :, keys.index("keyframe")] == 1).sum())
+    return out
 
 
 def max_over_ranks(dist, elapsed):
@@ -439,9 +466,12 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
     d_gray = pkg.DeviceBuffer.from_array(gray[rep], device=device)
     d_depth = pkg.DeviceBuffer.from_array(depth[rep], device=device)
     cam = pkg.make_camera(getattr(synth, cam_name))
+    use_map = map_mode(args, wl)
+    map_capacity(warmup + steps + (args.isolated_steps if args.isolated_steps > 0 else 0))
     tr = pkg.Tracker(pkg.OrbParams(*wl["orb"]), cam, S, device=device, lines=lines, stereo=stereo,
-                     local_map=bool(args.local_map), fixed_line_jac=bool(args.fixed_line_jacobian),
-                     refkf=bool(args.refkf and voc is not None))
+                     local_map=bool(args.local_map) and not use_map,
+                     fixed_line_jac=bool(args.fixed_line_jacobian),
+                     refkf=bool(args.refkf and voc is not None), map=use_map)
     # pipelining overlaps extraction of step t+1 with tracking of step t, for
     # every workload (lines too: the next batch's LSD overlaps this batch's
     # matching and pose, 9.5k -> 9.8k frames/s at 3072 streams)
@@ -496,7 +526,7 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
                 "mean_matches": float(st["nmatches"].mean()),
                 "mean_inliers": float(st["ninliers"].mean()),
                 "ok_frac": float(tr.status()["ok"].mean())}
-    if args.local_map:
+    if args.local_map or use_map:
         lst = tr.local_stats()
         tracking.update(mean_local_matches=float(lst["local_matches"].mean()),
                         mean_local_inliers=float(lst["local_inliers"].mean()))
@@ -520,7 +550,17 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
 
     # device-side history of the timed tracker: streams 0, S/2, S-1
     samp = sorted({0, S // 2, S - 1})
-    hist = [tr.history(s, warmup + steps) for s in samp]
+    hist = [(tr.history(s, warmup + steps)[0], tr.map_history(s, warmup + steps)) if use_map
+            else tr.history(s, warmup + steps) for s in samp]
+    if use_map:
+        mh = np.stack([h[1][-1] for h in hist])
+        ki = {k: i for i, k in enumerate(tr.MAP_COUNTS)}
+        tracking.update(
+            sampled_streams_keyframes=[int(x) for x in mh[:, ki["keyframes"]]],
+            sampled_streams_map_points=[int(x) for x in mh[:, ki["map_points"]]],
+            sampled_streams_map_lines=[int(x) for x in mh[:, ki["map_lines"]]],
+            keyframes_created_sampled=int(sum((h[1][:, ki["keyframe"]] == 1).sum() for h in hist)),
+            map_capacity_flags=int(tr.map_errors().max()))
 
     # roofline of the dominant single-stage kernel
     n_kp = float(st["nkeypoints"].mean())
@@ -529,7 +569,7 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
     # several stages (k_pose: motion model, reference keyframe, local map)
     # counted once with all its launches
     cand = ["pyramid", "fast", "octree", "orient_desc", "match", "pose_all"]
-    if args.local_map:
+    if args.local_map or use_map:
         cand.append("match_local")
     if lines:
         cand += list(tr.LSD_STAGES)
@@ -588,7 +628,7 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
     return dict(S=S, value=value, layout=L, elapsed=elapsed, stages=stages, tracking=tracking,
                 roof=roof, gray=gray, depth=depth, workload=wl["desc"], data=wl["data"],
                 image=f"{fw}x{fh}", nfeatures=wl["orb"][0], samp=samp, hist=hist, wname=workload,
-                pipelined=bool(pipelined))
+                pipelined=bool(pipelined), map=use_map)
 
 
 def run_ingress(pkg, synth, args, S, steps, warmup, rank, world, device, dist, voc=None):
@@ -609,8 +649,11 @@ def run_ingress(pkg, synth, args, S, steps, warmup, rank, world, device, dist, v
     hd = pkg.HostBuffer((len(rep), H, W), np.uint16)
     hg.array[:] = gray[rep]
     hd.array[:] = d16[rep]
+    use_map = map_mode(args, wl)
+    map_capacity(warmup + steps)
     tr = pkg.Tracker(pkg.OrbParams(*wl["orb"]), pkg.make_camera(synth.TUM1), S, device=device,
-                     local_map=bool(args.local_map), refkf=bool(args.refkf and voc is not None))
+                     local_map=bool(args.local_map) and not use_map,
+                     refkf=bool(args.refkf and voc is not None), map=use_map)
     tr.set_pipelined(True)
     if voc is not None:
         tr.set_vocabulary(voc, 4)
@@ -634,18 +677,20 @@ def run_ingress(pkg, synth, args, S, steps, warmup, rank, world, device, dist, v
         dist.barrier()
     elapsed = max_over_ranks(dist, time.perf_counter() - t0)
     samp = sorted({0, S // 2, S - 1})
-    hist = [tr.history(s, warmup + steps) for s in samp]
+    hist = [(tr.history(s, warmup + steps)[0], tr.map_history(s, warmup + steps)) if use_map
+            else tr.history(s, warmup + steps) for s in samp]
     tr.close()
     step_bytes = S * W * H * 3
     out = dict(S=S, value=S * steps * world / elapsed, elapsed=elapsed, nsteps=steps, samp=samp,
-               hist=hist, layout=L, gray=gray, depth=d32, wname="points",
+               hist=hist, layout=L, gray=gray, depth=d32, wname="points", map=use_map,
                h2d_GBps=round(step_bytes * steps / elapsed / 1e9, 2), bytes_per_step=step_bytes)
     hg.free()
     hd.free()
     return out
 
 
-def sweep(pkg, synth, workload, sizes, steps, device, local_map=True, voc=None, refkf=False):
+def sweep(pkg, synth, workload, sizes, steps, device, local_map=True, voc=None, refkf=False,
+          use_map=False):
     """Per-step latency and throughput at several batch sizes (untimed for the
     headline; each size gets its own tracker, 1 warm-up step)."""
     wl = WORKLOADS[workload]
@@ -660,9 +705,10 @@ def sweep(pkg, synth, workload, sizes, steps, device, local_map=True, voc=None, 
         rep = L.replicated(S)
         d_gray = pkg.DeviceBuffer.from_array(gray[rep], device=device)
         d_depth = pkg.DeviceBuffer.from_array(depth[rep], device=device)
+        map_capacity(1 + 2 * steps)
         tr = pkg.Tracker(pkg.OrbParams(*wl["orb"]), cam, S, device=device, lines=wl["lines"],
-                         stereo=wl["stereo"], local_map=local_map,
-                         refkf=bool(refkf and voc is not None))
+                         stereo=wl["stereo"], local_map=local_map and not use_map,
+                         refkf=bool(refkf and voc is not None), map=use_map)
         tr.set_pipelined(True)
         if voc is not None:
             tr.set_vocabulary(voc, 4)
@@ -726,7 +772,7 @@ def host_info():
             "usable_cores": usable}
 
 
-def cpu_baseline(seconds, threads, gray, depth, L, workload="points", flags=0):
+def cpu_baseline(seconds, threads, gray, depth, L, workload="points", flags=0, use_map=False):
     """Throughput mode (BASELINE.md §2 mode 2): the CPU oracle running the
     same per-frame step, one stream per host thread, for a bounded wall time."""
     from _pkg import load_oracle
@@ -736,7 +782,7 @@ def cpu_baseline(seconds, threads, gray, depth, L, workload="points", flags=0):
     stop = time.time() + seconds
 
     def worker(k):
-        vo, vstep = oracle_vo(O, wl, flags)
+        vo, vstep = oracle_vo(O, wl, flags, use_map)
         i = 0
         while time.time() < stop:   # worker k runs stream k of the layout
             e = L.elem(k, i)
@@ -754,7 +800,8 @@ def cpu_baseline(seconds, threads, gray, depth, L, workload="points", flags=0):
     return sum(counts) / dt, sum(counts), dt
 
 
-def cpu_reference_faithful(gray, depth, L, workload, flags=0, warmup=20, frames=300):
+def cpu_reference_faithful(gray, depth, L, workload, flags=0, warmup=20, frames=300,
+                           use_map=False):
     """BASELINE.md §2 mode 1: one stream as the reference runs it, ORB and
     the LineExtractor on two host threads per frame (Frame.cc:152-155),
     matching and pose on the tracking thread; per-frame latency with
@@ -765,7 +812,8 @@ def cpu_reference_faithful(gray, depth, L, workload, flags=0, warmup=20, frames=
     O = load_oracle()
     wl = WORKLOADS[workload]
     cam = O.camera(getattr(synth, wl["cam"]))
-    vo = O.LVO(O.params(*wl["orb"]), cam, 1, use_lines=wl["lines"], flags=O.TWO_THREADS | flags)
+    mk = O.MapVO if use_map else O.LVO
+    vo = mk(O.params(*wl["orb"]), cam, 1, use_lines=wl["lines"], flags=O.TWO_THREADS | flags)
     voc = oracle_vocabulary(O)
     if voc is not None:
         vo.set_vocabulary(voc)
@@ -842,6 +890,11 @@ def main():
                     help="1 = every step runs TrackWithMotionModel + TrackLocalMap (the "
                          "reference's per-frame Track, Tracking.cc:1332-1420; local map = the "
                          "last 4 frames, DESIGN.md P18); 0 = TrackWithMotionModel only")
+    ap.add_argument("--map", type=int, default=1,
+                    help="1 = Tracking::Track with the reference's map model (ORBPL_TRACK_MAP: "
+                         "UpdateLastFrame, covisibility local map, NeedNewKeyFrame, "
+                         "CreateNewKeyFrame; RGB-D workloads; the stereo leg keeps P18); "
+                         "0 = the P18 per-frame local map (--local-map)")
     ap.add_argument("--fixed-line-jacobian", type=int, default=0,
                     help="1 = the analytic line-edge Jacobian instead of the reference's "
                          "as-written one (pinned P7)")
@@ -913,15 +966,17 @@ def main():
             continue
         r["parity"] = gather_parity(dist, world, parity_check(
             [h[0] for h in r["hist"]], [h[1] for h in r["hist"]], r["samp"], r["gray"], r["depth"],
-            r["layout"], r["wname"], oracle_flags(O, args)))
+            r["layout"], r["wname"], oracle_flags(O, args), r.get("map", False)))
 
     sweeps = None
     if rank == 0 and world == 1 and args.sweep and args.workload == "points":
         lmf = bool(args.local_map)
         rk = bool(args.refkf)
+        mp = bool(args.map)
         sweeps = {"points": sweep(pkg, synth, "points", (1, 16, 64, 256, 1024), 5, device, lmf,
-                                  voc, rk),
-                  "lines": sweep(pkg, synth, "lines", (1, 16, 64, 256), 2, device, lmf, voc, rk)}
+                                  voc, rk, mp),
+                  "lines": sweep(pkg, synth, "lines", (1, 16, 64, 256), 2, device, lmf, voc, rk,
+                                 mp)}
 
     cpu = None
     host = host_info()
@@ -929,7 +984,7 @@ def main():
         thr = args.cpu_threads or host["usable_cores"]
         ofl = oracle_flags(O, args)
         fps, nfr, dt = cpu_baseline(args.cpu_seconds, thr, res["gray"], res["depth"],
-                                    res["layout"], args.workload, ofl)
+                                    res["layout"], args.workload, ofl, res["map"])
         cpu = {"value": round(fps, 2), "unit": "frames/s", "cores": thr, "kind": "port",
                "sample": f"{nfr} frames of the same {res['image']} loop in {dt:.1f} s, oracle/ "
                          f"C++ restatement ({args.workload} workload), one stream per thread",
@@ -939,7 +994,7 @@ def main():
                "reference_faithful": cpu_reference_faithful(res["gray"], res["depth"],
                                                             res["layout"], args.workload, ofl,
                                                             args.cpu_ref_warmup,
-                                                            args.cpu_ref_frames)}
+                                                            args.cpu_ref_frames, res["map"])}
 
     if rank == 0:
         S = res["S"]
@@ -959,7 +1014,9 @@ def main():
             "config": {"workload": res["workload"],
                        "image": res["image"], "nfeatures": res["nfeatures"], "streams_per_gpu": S,
                        "frames_per_step": S * world, "parallelism": f"streams sharded x{world}",
-                       "pipelined": res["pipelined"], "track_local_map": bool(args.local_map),
+                       "pipelined": res["pipelined"],
+                       "track_map": res["map"],
+                       "track_local_map": bool(args.local_map) or res["map"],
                        "fixed_line_jacobian": bool(args.fixed_line_jacobian),
                        "keyframe_bow": bool(args.bow),
                        "track_reference_keyframe": bool(args.bow and args.refkf)},
@@ -990,18 +1047,18 @@ def main():
                 "steps": o["nsteps"], "streams_per_gpu": o["S"],
                 "ms_per_step": round(o["elapsed"] / o["nsteps"] * 1e3, 3),
                 "stage_ms": o["stages"], "tracking": o["tracking"], "roofline": o["roof"],
-                "parity": o["parity"], "data": o["data"]}
+                "parity": o["parity"], "data": o["data"], "track_map": o["map"]}
             if cpu is not None:
                 thr = cpu["cores"]
                 fps, nfr, dt = cpu_baseline(args.cpu_seconds / 2, thr, o["gray"], o["depth"],
-                                            o["layout"], o["wname"], ofl)
+                                            o["layout"], o["wname"], ofl, o["map"])
                 out[key]["cpu_baseline"] = {
                     "value": round(fps, 2), "unit": "frames/s", "cores": thr, "kind": "port",
                     "sample": f"{nfr} frames in {dt:.1f} s, oracle/ C++ restatement "
                               f"({o['wname']} workload), one stream per thread",
                     "reference_faithful": cpu_reference_faithful(
                         o["gray"], o["depth"], o["layout"], o["wname"], ofl, args.cpu_ref_warmup,
-                        args.cpu_ref_frames)}
+                        args.cpu_ref_frames, o["map"])}
         print(json.dumps(out))
     if dist:
         dist.destroy_process_group()
