@@ -413,9 +413,8 @@ void launch_stereo_lines(const TrackConsts& c, const StereoLineArgs& a, int nstr
 // compacted in order into global scratch, then every (projected, current)
 // pair is tested; per current line the last passing projected line wins
 // (atomicMax), every pass counts.
-__global__ void __launch_bounds__(256) k_line_match_list(TrackConsts c, LineListArgs a) {
-  if (a.ncur_arr) {  // batched: stream blockIdx.x
-    const int b = blockIdx.x;
+__device__ __forceinline__ void line_list_stream(const TrackConsts& c, LineListArgs a, const int b) {
+  if (a.ncur_arr) {  // batched: stream b
     const long long co = (long long)b * a.cur_pitch, mo = (long long)b * a.ml_pitch;
     a.ncur = a.ncur_arr[b];
     a.nml = a.nml_arr[b];
@@ -511,6 +510,20 @@ __global__ void __launch_bounds__(256) k_line_match_list(TrackConsts c, LineList
   }
 }
 
+// batched: one workgroup per stream, or (a.list) a small grid looping over
+// the streams a list names
+__global__ void __launch_bounds__(256) k_line_match_list(TrackConsts c, LineListArgs a) {
+  if (a.list) {
+    const int n = *a.list_n;
+    for (int b = blockIdx.x; b < n; b += gridDim.x) {
+      line_list_stream(c, a, a.list[b]);
+      __syncthreads();
+    }
+  } else {
+    line_list_stream(c, a, blockIdx.x);
+  }
+}
+
 // Frame::IsInFrustum(MapLine*) (Frame.cc:403-430)
 __global__ void k_line_in_frustum(const float* __restrict__ Tcw, int n, const float* __restrict__ xyz6,
                                   uint8_t* __restrict__ in_view) {
@@ -530,7 +543,8 @@ __global__ void k_line_in_frustum(const float* __restrict__ Tcw, int n, const fl
 
 void launch_line_match_list(const TrackConsts& c, const LineListArgs& a, hipStream_t s,
                             int nstreams) {
-  hipLaunchKernelGGL(k_line_match_list, dim3(a.ncur_arr ? nstreams : 1), dim3(256), 0, s, c, a);
+  const int grid = !a.ncur_arr ? 1 : a.list ? (nstreams < kListGrid ? nstreams : kListGrid) : nstreams;
+  hipLaunchKernelGGL(k_line_match_list, dim3(grid), dim3(256), 0, s, c, a);
 }
 
 __global__ void k_line_in_frustum_b(const float* __restrict__ Tcw, int pose_stride,

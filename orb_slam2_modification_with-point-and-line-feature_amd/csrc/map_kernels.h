@@ -32,6 +32,8 @@ struct MapState {
   int n_local_kf;       // mvpLocalKeyFrames (persists across steps)
   int n_local_mp, n_local_ml;
   int err;              // capacity overflow (keyframes / points / lines)
+  int new_kf;           // keyframe inserted this step (-1 none): k_map_kf_points / k_map_connect
+  int kf_mp_base;       // its first new map point (the pool ids from here on are new)
   int local_kf[kMapMaxKF];
   float V[16];          // mVelocity
   float Tcr[16];        // mlRelativeFramePoses.back()
@@ -138,6 +140,8 @@ struct MapArgs {
   int* trk_cur_nobs;      // Observations() of each current line's map line
   int* trk_lm;            // its matches (reference keyframe line index)
   int* trk_nml;           // lines to search per stream (0: not tracked by it)
+  int* trk_list;          // the streams that run TrackReferenceKeyFrame this step
+  int* trk_count;         // (k_map_resolve_motion appends; k_map_begin clears)
   // pose inputs in current-frame index space
   int* m2;                // i when the keypoint has a map point, else -1
   float* pxyz;            // its position

@@ -151,12 +151,17 @@ __device__ void stl_move_median_to_first(LRec* r, LRec* a, LRec* b, LRec* c) {
   *r = *m;
   *m = t;
 }
-__device__ void stl_sort(LRec* f, int n) {
+// stk: 3 x 32 ints of LDS for the explicit stack (one thread sorts; an LDS
+// stack keeps the caller kernels' register and scratch budget)
+__device__ void stl_sort(LRec* f, int n, int* stk) {
   if (n < 2) return;
   int lg = 0;
   while ((1 << (lg + 1)) <= n) lg++;
   // explicit stack for the right-hand recursion of __introsort_loop
-  int st_lo[32], st_hi[32], st_d[32], sp = 0;
+  int* st_lo = stk;
+  int* st_hi = stk + 32;
+  int* st_d = stk + 64;
+  int sp = 0;
   st_lo[sp] = 0; st_hi[sp] = n; st_d[sp] = 2 * lg; sp++;
   while (sp > 0) {
     sp--;
@@ -298,67 +303,99 @@ __device__ void update_normal_depth(const TrackConsts& c, const MapArgs& a, cons
 
 // MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:256-321): the
 // observation descriptor with the least median distance to the others
-// (first on ties); dscr: this thread's kMapMaxKF distances
+// (first on ties); dscr: this thread's kMapMaxKF distances. With one or two
+// observations the median index is 0 (the distance to itself), so the first
+// observation's descriptor wins without a distance. The row's descriptors are
+// fetched four at a time (independent loads in flight together).
 __device__ void compute_distinctive(const MapArgs& a, const Pools& P, int p, uint16_t* dscr) {
   const long long g = P.mb + p;
   const int nob = a.mp_nob[g];
   if (nob == 0) return;
   const uint32_t* ob = a.mp_obs + g * a.kfc;
-  const int med = (int)(0.5 * (double)(nob - 1));
-  int best = 0x7fffffff, bi = 0;
-  for (int i = 0; i < nob; i++) {
-    const uint8_t* di = a.kf_desc + (P.kfb(ob[i] >> 16) * a.kp_pitch + (ob[i] & 0xffff)) * 32;
-    for (int j = 0; j < nob; j++) {
-      const uint8_t* dj = a.kf_desc + (P.kfb(ob[j] >> 16) * a.kp_pitch + (ob[j] & 0xffff)) * 32;
-      dscr[j] = (uint16_t)(i == j ? 0 : popc32(di, dj));
-    }
-    // insertion sort of the row, then its median entry
-    for (int x = 1; x < nob; x++) {
-      const uint16_t v = dscr[x];
-      int y = x - 1;
-      while (y >= 0 && dscr[y] > v) {
-        dscr[y + 1] = dscr[y];
-        y--;
+  auto dptr = [&](uint32_t o) {
+    return reinterpret_cast<const uint4*>(a.kf_desc +
+                                          (P.kfb(o >> 16) * a.kp_pitch + (o & 0xffff)) * 32);
+  };
+  int bi = 0;
+  if (nob > 2) {
+    const int med = (int)(0.5 * (double)(nob - 1));
+    int best = 0x7fffffff;
+    for (int i = 0; i < nob; i++) {
+      const uint4* di = dptr(ob[i]);
+      const uint4 x0 = di[0], x1 = di[1];
+      for (int j0 = 0; j0 < nob; j0 += 4) {
+        uint32_t o[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) o[q] = j0 + q < nob ? ob[j0 + q] : ob[0];
+        uint4 y[8];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const uint4* dj = dptr(o[q]);
+          y[2 * q] = dj[0];
+          y[2 * q + 1] = dj[1];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const int j = j0 + q;
+          if (j >= nob) break;
+          const uint4 u = y[2 * q], v = y[2 * q + 1];
+          const int d = __popc(x0.x ^ u.x) + __popc(x0.y ^ u.y) + __popc(x0.z ^ u.z) +
+                        __popc(x0.w ^ u.w) + __popc(x1.x ^ v.x) + __popc(x1.y ^ v.y) +
+                        __popc(x1.z ^ v.z) + __popc(x1.w ^ v.w);
+          dscr[j] = (uint16_t)(i == j ? 0 : d);
+        }
       }
-      dscr[y + 1] = v;
-    }
-    if ((int)dscr[med] < best) {
-      best = dscr[med];
-      bi = i;
+      // insertion sort of the row, then its median entry
+      for (int x = 1; x < nob; x++) {
+        const uint16_t v = dscr[x];
+        int y = x - 1;
+        while (y >= 0 && dscr[y] > v) {
+          dscr[y + 1] = dscr[y];
+          y--;
+        }
+        dscr[y + 1] = v;
+      }
+      if ((int)dscr[med] < best) {
+        best = dscr[med];
+        bi = i;
+      }
     }
   }
-  copy32(a.mp_desc + g * 32,
-         a.kf_desc + (P.kfb(ob[bi] >> 16) * a.kp_pitch + (ob[bi] & 0xffff)) * 32);
+  copy32(a.mp_desc + g * 32, reinterpret_cast<const uint8_t*>(dptr(ob[bi])));
 }
 
 // KeyFrame::UpdateBestCovisibles (KeyFrame.cc:139-158): every connection,
-// weight descending, ties by id descending (P24)
-__device__ void update_best_covisibles(const MapArgs& a, const Pools& P, int k) {
+// weight descending, ties by id descending (P24). wrow / ks: this thread's
+// LDS scratch (kfc ints / bytes) for the row and the sorted ids.
+__device__ void update_best_covisibles(const MapArgs& a, const Pools& P, int k, int* wrow,
+                                       uint8_t* ks) {
   const int* w = a.kf_w + P.kfb(k) * a.kfc;
   uint8_t* ord = a.kf_ord + P.kfb(k) * a.kfc;
+  for (int j = 0; j < a.kfc; j++) wrow[j] = w[j];
   int n = 0;
-  int ks[kMapMaxKF];
   for (int j = 0; j < a.kfc; j++)
-    if (w[j] > 0) ks[n++] = j;
+    if (wrow[j] > 0) ks[n++] = (uint8_t)j;
   // ascending (weight, id), then reversed
   for (int x = 1; x < n; x++) {
     const int v = ks[x];
     int y = x - 1;
-    while (y >= 0 && (w[ks[y]] > w[v] || (w[ks[y]] == w[v] && ks[y] > v))) {
+    while (y >= 0 && (wrow[ks[y]] > wrow[v] || (wrow[ks[y]] == wrow[v] && ks[y] > v))) {
       ks[y + 1] = ks[y];
       y--;
     }
-    ks[y + 1] = v;
+    ks[y + 1] = (uint8_t)v;
   }
-  for (int x = 0; x < n; x++) ord[x] = (uint8_t)ks[n - 1 - x];
+  for (int x = 0; x < n; x++) ord[x] = ks[n - 1 - x];
   a.kf_nord[P.kfb(k)] = n;
 }
 
-__device__ void add_connection(const MapArgs& a, const Pools& P, int k, int other, int w) {
+// KeyFrame::AddConnection (KeyFrame.cc:124-137)
+__device__ void add_connection(const MapArgs& a, const Pools& P, int k, int other, int w,
+                               int* wrow, uint8_t* ks) {
   int* wk = a.kf_w + P.kfb(k) * a.kfc;
   if (wk[other] == w) return;
   wk[other] = w;
-  update_best_covisibles(a, P, k);
+  update_best_covisibles(a, P, k, wrow, ks);
 }
 
 }  // namespace
@@ -378,6 +415,7 @@ __global__ void k_map_reset(MapArgs a, const float* T0, int nstreams) {
 __global__ void __launch_bounds__(kT) k_map_begin(TrackConsts c, MapArgs a) {
   __shared__ unsigned long long keys[kMatchMaxKp];
   __shared__ LRec lrec[kLineKeep];
+  __shared__ int sstk[96];
   __shared__ float sTl[16];
   __shared__ int s_flag[3];
   __shared__ int s_cut;
@@ -386,6 +424,7 @@ __global__ void __launch_bounds__(kT) k_map_begin(TrackConsts c, MapArgs a) {
   MapState& M = a.ms[s];
   StreamState& S = a.st[s];
   const Pools P(a, s);
+  if (s == 0 && t == 0) *a.trk_count = 0;
   if (t == 0) {
     const int fid = M.next_id++;
     M.frame_id = fid;
@@ -504,35 +543,45 @@ __global__ void __launch_bounds__(kT) k_map_begin(TrackConsts c, MapArgs a) {
   ntp = block_sum(ntp, wsum);
   if (t == 0) M.n_tp = ntp;
   if (!a.lines) return;
-  // ---- temporal lines: std::sort by max end-point depth ----
+  // ---- temporal lines: std::sort by max end-point depth (thread 0 decides
+  // from LDS, the lines are made in parallel) ----
+  __shared__ uint8_t lmake[kLineKeep];
+  if (t < kLineKeep) lmake[t] = 0;
+  if (t < lnl) {
+    const long long o = P.lb + t;
+    const float zs = a.l_dstart[o], ze = a.l_dend[o];
+    lrec[t] = LRec{(zs > 0 && ze > 0) ? fmaxf(zs, ze) : -1.f, a.l_mlid[o] == -1 ? t : -1 - t};
+  }
+  __syncthreads();
   if (t == 0) {
     int m = 0;
-    for (int j = 0; j < lnl; j++) {
-      const float zs = a.l_dstart[P.lb + j], ze = a.l_dend[P.lb + j];
-      if (zs > 0 && ze > 0) lrec[m++] = LRec{fmaxf(zs, ze), j};
-    }
-    stl_sort(lrec, m);
-    float Ow[3];
-    gemm_neg_Rt_t(sTl, Ow);
+    for (int j = 0; j < lnl; j++)
+      if (lrec[j].k >= 0) lrec[m++] = lrec[j];
+    stl_sort(lrec, m, sstk);
     int nlines = 0, ntl = 0;
     for (int q = 0; q < m; q++) {
-      const int j = lrec[q].i;
-      const long long o = P.lb + j;
-      if (a.l_mlid[o] == -1) {
-        const orbpl_keyline k = a.l_kl_un[o];
-        const float zs = a.l_dstart[o];
-        float* x = a.l_ml_xyz + o * 6;
-        unproject_f(c, sTl, Ow, k.startPointX, k.startPointY, zs, x);
-        unproject_f(c, sTl, Ow, k.endPointX, k.endPointY, zs, x + 3);   // Frame.cc:1192
-        copy32(a.l_ml_desc + o * 32, a.l_ldesc + o * 32);
-        a.l_mlid[o] = -2 - j;
-        a.l_has_ml[o] = 1;
+      if (lrec[q].i >= 0) {   // no map line at this line
+        lmake[lrec[q].i] = 1;
         ntl++;
       }
       nlines++;
       if (lrec[q].k > thd && nlines > 45) break;
     }
     M.n_tl = ntl;
+  }
+  __syncthreads();
+  if (t < lnl && lmake[t]) {
+    const long long o = P.lb + t;
+    float Ow[3];
+    gemm_neg_Rt_t(sTl, Ow);
+    const orbpl_keyline k = a.l_kl_un[o];
+    const float zs = a.l_dstart[o];
+    float* x = a.l_ml_xyz + o * 6;
+    unproject_f(c, sTl, Ow, k.startPointX, k.startPointY, zs, x);
+    unproject_f(c, sTl, Ow, k.endPointX, k.endPointY, zs, x + 3);   // Frame.cc:1192
+    copy32(a.l_ml_desc + o * 32, a.l_ldesc + o * 32);
+    a.l_mlid[o] = -2 - t;
+    a.l_has_ml[o] = 1;
   }
 }
 
@@ -602,6 +651,7 @@ __global__ void __launch_bounds__(kT) k_map_resolve_motion(MapArgs a) {
     s_trk = a.refkf && (M.trk_first || (M.motion && !motion_ok));
     S.trk = s_trk;
     a.trk_nml[s] = 0;
+    if (s_trk) a.trk_list[atomicAdd(a.trk_count, 1)] = s;
   }
   __syncthreads();
   if (!s_trk) return;
@@ -981,25 +1031,11 @@ __device__ static void write_keyframe(const MapArgs& a, const Pools& P, int kf, 
   }
 }
 
-// a new map point of keyframe kf at keypoint i (MapPoint ctor, AddObservation,
-// ComputeDistinctiveDescriptors / UpdateNormalAndDepth with one observation)
-__device__ static void new_point(const TrackConsts& c, const MapArgs& a, const Pools& P, int p,
-                                 int kf, int i, const float* T, float z, uint16_t* dscr) {
-  const long long g = P.mb + p, src = P.cb + i;
-  const KeyPointD kp = a.kps_un[src];
-  float Ow[3], w[3];
-  gemm_neg_Rt_t(T, Ow);
-  unproject_f(c, T, Ow, kp.x, kp.y, z, w);
-  a.mp_pos[g] = make_float4(w[0], w[1], w[2], 0.f);
-  a.mp_obs[g * a.kfc] = ((uint32_t)kf << 16) | (uint32_t)i;
-  a.mp_nob[g] = 1;
-  a.mp_nobs[g] = a.uright[src] >= 0 ? 2 : 1;
-  a.mp_seen[g] = -1;
-  a.mp_tref[g] = -1;
+// a new map point of keyframe kf at keypoint i: its pool id into the
+// keyframe and the frame (the point itself is built by k_map_kf_points)
+__device__ static void mark_new_point(const MapArgs& a, const Pools& P, int p, int kf, int i) {
   a.kf_mp[P.kfb(kf) * a.kp_pitch + i] = p;
-  compute_distinctive(a, P, p, dscr);
-  update_normal_depth(c, a, P, p);
-  a.mpid[src] = p;
+  a.mpid[P.cb + i] = p;
 }
 
 __device__ static void new_line(const TrackConsts& c, const MapArgs& a, const Pools& P, int l,
@@ -1022,9 +1058,9 @@ __device__ static void new_line(const TrackConsts& c, const MapArgs& a, const Po
 
 __global__ void __launch_bounds__(kT) k_map_finish(TrackConsts c, MapArgs a) {
   __shared__ unsigned long long keys[kMatchMaxKp];
-  __shared__ uint16_t dscr[kT][kMapMaxKF];
   __shared__ LRec lrec[kLineKeep];
-  __shared__ int cnt[kMapMaxKF];
+  __shared__ int lpool[kLineKeep];   // the pool slot a line's new map line takes, -1 none
+  __shared__ int sstk[96];
   __shared__ float sT[16];
   __shared__ int wsum[4];
   __shared__ int s_i[8];
@@ -1035,7 +1071,7 @@ __global__ void __launch_bounds__(kT) k_map_finish(TrackConsts c, MapArgs a) {
   const int fid = M.frame_id;
   const int n = a.n[s], nl = a.lines ? a.nl[s] : 0;
   const int state0 = M.state0;
-  uint16_t* my = dscr[t];
+  if (t == 0) M.new_kf = -1;
   // ================= not initialised: StereoInitialization ================
   if (state0 == kNotInit) {
     const bool init = n > 500;
@@ -1051,19 +1087,26 @@ __global__ void __launch_bounds__(kT) k_map_finish(TrackConsts c, MapArgs a) {
         const bool f = z > 0;
         int tot = 0;
         const int pos = base + block_prefix(f, wsum, &tot);
-        if (f && pos < a.mpc) new_point(c, a, P, pos, 0, i, sT, z, my);
+        if (f && pos < a.mpc) mark_new_point(a, P, pos, 0, i);
         base += tot;
       }
       __syncthreads();
+      // a map line per line with both end-point depths, in line order
+      {
+        const bool f = t < nl && a.dstart[P.lb + t] > 0 && a.dend[P.lb + t] > 0;
+        int tot = 0;
+        const int pos = block_prefix(f, wsum, &tot);
+        if (f && pos < a.mlc) new_line(c, a, P, pos, 0, t, sT);
+        if (t == 0) s_i[4] = (int)min((long long)tot, a.mlc);
+      }
+      __syncthreads();
       if (t == 0) {
-        int nml = 0;
-        for (int j = 0; j < nl; j++) {
-          const long long o = P.lb + j;
-          if (a.dstart[o] > 0 && a.dend[o] > 0 && nml < a.mlc) new_line(c, a, P, nml++, 0, j, sT);
-        }
+        const int nml = s_i[4];
         M.n_kf = 1;
         M.n_mp = (int)min((long long)base, a.mpc);
         M.n_ml = nml;
+        M.new_kf = 0;
+        M.kf_mp_base = 0;
         if (base > a.mpc) M.err |= 2;
         M.state = kOK;
         M.last_kf_frame = fid;
@@ -1222,27 +1265,33 @@ __global__ void __launch_bounds__(kT) k_map_finish(TrackConsts c, MapArgs a) {
           const bool f = i >= 0 && a.mpid[P.cb + i] == -1;
           int tot = 0;
           const int pos = base + block_prefix(f, wsum, &tot);
-          if (f && pos < a.mpc)
-            new_point(c, a, P, pos, kf, i, sT, __uint_as_float((unsigned)(keys[j] >> 32)), my);
+          if (f && pos < a.mpc) mark_new_point(a, P, pos, kf, i);
           base += tot;
+        }
+        __syncthreads();
+        // new lines: std::sort by the larger end-point depth, all close ones
+        // and at least 45 (Tracking.cc:1660-1730); thread 0 decides from LDS,
+        // the lines are created in parallel
+        if (t < kLineKeep) lpool[t] = -1;
+        if (t < nl) {
+          const long long o = P.lb + t;
+          const float zs = a.dstart[o], ze = a.dend[o];
+          lrec[t] = LRec{(zs > 0 && ze > 0) ? fmaxf(zs, ze) : -1.f, a.mlid[o] == -1 ? t : -1 - t};
         }
         __syncthreads();
         if (t == 0) {
           if (base > a.mpc) M.err |= 2;
+          M.kf_mp_base = M.n_mp;
+          M.new_kf = kf;
           M.n_mp = (int)min((long long)base, a.mpc);
-          // new lines: std::sort by the larger end-point depth, all close ones
-          // and at least 45 (Tracking.cc:1660-1730)
           int m = 0;
-          for (int j = 0; j < nl; j++) {
-            const float zs = a.dstart[P.lb + j], ze = a.dend[P.lb + j];
-            if (zs > 0 && ze > 0) lrec[m++] = LRec{fmaxf(zs, ze), j};
-          }
-          stl_sort(lrec, m);
+          for (int j = 0; j < nl; j++)
+            if (lrec[j].k >= 0) lrec[m++] = lrec[j];   // in line order, as the reference's vector
+          stl_sort(lrec, m, sstk);
           int nlines = 0, nml = M.n_ml;
           for (int q = 0; q < m; q++) {
-            const int j = lrec[q].i;
-            if (a.mlid[P.lb + j] == -1) {
-              if (nml < a.mlc) new_line(c, a, P, nml++, kf, j, sT);
+            if (lrec[q].i >= 0) {   // no map line at this line yet
+              if (nml < a.mlc) lpool[lrec[q].i] = nml++;
               else M.err |= 2;
             }
             nlines++;
@@ -1255,82 +1304,10 @@ __global__ void __launch_bounds__(kT) k_map_finish(TrackConsts c, MapArgs a) {
           S.map_out[0] = 1;
         }
         __syncthreads();
-        // ==== LocalMapping::ProcessNewKeyFrame (P23) ====
-        for (int i = t; i < n; i += kT) {
-          const int p = a.kf_mp[P.kfb(kf) * a.kp_pitch + i];
-          if (p < 0) continue;
-          const long long g = P.mb + p;
-          const int nob = a.mp_nob[g];
-          if (nob > 0 && (int)(a.mp_obs[g * a.kfc + nob - 1] >> 16) == kf) continue;  // IsInKeyFrame
-          a.mp_obs[g * a.kfc + nob] = ((uint32_t)kf << 16) | (uint32_t)i;
-          a.mp_nob[g] = nob + 1;
-          a.mp_nobs[g] += a.uright[P.cb + i] >= 0 ? 2 : 1;
-          update_normal_depth(c, a, P, p);
-          compute_distinctive(a, P, p, my);
-        }
-        if (t < kMapMaxKF) cnt[t] = 0;
+        if (t < nl && lpool[t] >= 0) new_line(c, a, P, lpool[t], kf, t, sT);
         __syncthreads();
-        // ==== KeyFrame::UpdateConnections (KeyFrame.cc:363-452) ====
-        for (int i = t; i < n; i += kT) {
-          const int p = a.kf_mp[P.kfb(kf) * a.kp_pitch + i];
-          if (p < 0) continue;
-          const long long g = P.mb + p;
-          const int nob = a.mp_nob[g];
-          for (int k = 0; k < nob; k++) {
-            const int o = a.mp_obs[g * a.kfc + k] >> 16;
-            if (o != kf) atomicAdd(&cnt[o], 1);
-          }
-        }
-        __syncthreads();
-        if (t == 0) {
-          int nmax = 0, kmax = -1, np = 0;
-          int pw[kMapMaxKF], pk[kMapMaxKF];
-          int* wk = a.kf_w + P.kfb(kf) * a.kfc;
-          bool any = false;
-          for (int k = 0; k < kf; k++) any |= cnt[k] > 0;
-          if (any) {
-            for (int k = 0; k < kf; k++) {
-              if (cnt[k] <= 0) continue;
-              if (cnt[k] > nmax) {
-                nmax = cnt[k];
-                kmax = k;
-              }
-              if (cnt[k] >= 15) {
-                pw[np] = cnt[k];
-                pk[np++] = k;
-                add_connection(a, P, k, kf, cnt[k]);
-              }
-            }
-            if (np == 0) {
-              pw[np] = nmax;
-              pk[np++] = kmax;
-              add_connection(a, P, kmax, kf, nmax);
-            }
-            // sort (weight, id) ascending, the ordered list is its reverse
-            for (int x = 1; x < np; x++) {
-              const int vw = pw[x], vk = pk[x];
-              int y = x - 1;
-              while (y >= 0 && (pw[y] > vw || (pw[y] == vw && pk[y] > vk))) {
-                pw[y + 1] = pw[y];
-                pk[y + 1] = pk[y];
-                y--;
-              }
-              pw[y + 1] = vw;
-              pk[y + 1] = vk;
-            }
-            for (int k = 0; k < kf; k++) wk[k] = cnt[k];
-            uint8_t* ord = a.kf_ord + P.kfb(kf) * a.kfc;
-            for (int x = 0; x < np; x++) ord[x] = (uint8_t)pk[np - 1 - x];
-            a.kf_nord[P.kfb(kf)] = np;
-            if (a.kf_first[P.kfb(kf)] && kf != 0) {
-              const int par = ord[0];
-              a.kf_parent[P.kfb(kf)] = par;
-              a.kf_child[P.kfb(par)] |= 1ull << kf;
-              a.kf_first[P.kfb(kf)] = 0;
-            }
-          }
-        }
-        __syncthreads();
+        // LocalMapping::ProcessNewKeyFrame and UpdateConnections follow in
+        // k_map_kf_points / k_map_connect
       }
       // ---- outliers leave the frame (Tracking.cc:548-555; lines by the
       // point flags, replicated) ----
@@ -1379,6 +1356,143 @@ __global__ void __launch_bounds__(kT) k_map_finish(TrackConsts c, MapArgs a) {
   }
 }
 
+// LocalMapping::ProcessNewKeyFrame's per-point work (LocalMapping.cc:186-240,
+// P23) for the keyframe k_map_finish inserted, and the construction of its new
+// map points (MapPoint(x3D, pKF, pMap) + AddObservation +
+// ComputeDistinctiveDescriptors + UpdateNormalAndDepth, Tracking.cc:1592-1655):
+// one thread per keypoint of the keyframe, grid (keypoints / 64, streams), so
+// the points' dependent gathers overlap across many waves.
+__global__ void __launch_bounds__(64) k_map_kf_points(TrackConsts c, MapArgs a) {
+  __shared__ uint16_t dscr[64][kMapMaxKF];
+  const int s = blockIdx.y;
+  const MapState& M = a.ms[s];
+  const int kf = M.new_kf;
+  if (kf < 0) return;
+  const Pools P(a, s);
+  const long long kb = P.kfb(kf);
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= a.kf_N[kb]) return;
+  const long long d = kb * a.kp_pitch + i;
+  const int p = a.kf_mp[d];
+  if (p < 0) return;
+  const long long g = P.mb + p;
+  if (p >= M.kf_mp_base) {
+    // a new point from the keyframe's depth
+    float T[16];
+    for (int q = 0; q < 16; q++) T[q] = a.kf_T[kb * 16 + q];
+    const float Ow[3] = {a.kf_Ow[kb * 4], a.kf_Ow[kb * 4 + 1], a.kf_Ow[kb * 4 + 2]};
+    const KeyPointD kp = a.kf_kp[d];
+    float w[3];
+    unproject_f(c, T, Ow, kp.x, kp.y, a.depth[P.cb + i], w);
+    a.mp_pos[g] = make_float4(w[0], w[1], w[2], 0.f);
+    a.mp_obs[g * a.kfc] = ((uint32_t)kf << 16) | (uint32_t)i;
+    a.mp_nob[g] = 1;
+    a.mp_nobs[g] = a.kf_ur[d] >= 0 ? 2 : 1;
+    a.mp_seen[g] = -1;
+    a.mp_tref[g] = -1;
+    copy32(a.mp_desc + g * 32, a.kf_desc + d * 32);   // one observation: its descriptor
+    update_normal_depth(c, a, P, p);
+    return;
+  }
+  // a tracked point: AddObservation, UpdateNormalAndDepth, ComputeDistinctiveDescriptors
+  const int nob = a.mp_nob[g];
+  if (nob > 0 && (int)(a.mp_obs[g * a.kfc + nob - 1] >> 16) == kf) return;   // IsInKeyFrame
+  a.mp_obs[g * a.kfc + nob] = ((uint32_t)kf << 16) | (uint32_t)i;
+  a.mp_nob[g] = nob + 1;
+  a.mp_nobs[g] += a.kf_ur[d] >= 0 ? 2 : 1;
+  update_normal_depth(c, a, P, p);
+  compute_distinctive(a, P, p, dscr[threadIdx.x]);
+}
+
+// KeyFrame::UpdateConnections (KeyFrame.cc:363-452) of the inserted keyframe:
+// covisibility counts over its points' observations, the connected keyframes'
+// ordered lists (thread k updates keyframe k), its own list and parent.
+// Dynamic LDS: 5 x kfc x kfc bytes of per-thread scratch.
+__global__ void __launch_bounds__(kT) k_map_connect(MapArgs a) {
+  extern __shared__ int cscr[];
+  __shared__ int cnt[kMapMaxKF];
+  __shared__ int pw[kMapMaxKF], pk[kMapMaxKF];
+  __shared__ int s_i[2];
+  const int s = blockIdx.x, t = threadIdx.x;
+  const MapState& M = a.ms[s];
+  const int kf = M.new_kf;
+  if (kf <= 0) return;   // the initial keyframe has no other keyframe to connect to
+  const Pools P(a, s);
+  const long long kb = P.kfb(kf);
+  const int N = a.kf_N[kb];
+  if (t < kMapMaxKF) cnt[t] = 0;
+  __syncthreads();
+  for (int i = t; i < N; i += kT) {
+    const int p = a.kf_mp[kb * a.kp_pitch + i];
+    if (p < 0) continue;
+    const long long g = P.mb + p;
+    const int nob = a.mp_nob[g];
+    for (int k = 0; k < nob; k++) {
+      const int o = a.mp_obs[g * a.kfc + k] >> 16;
+      if (o != kf) atomicAdd(&cnt[o], 1);
+    }
+  }
+  __syncthreads();
+  // the connection decision (thread 0), then every connected keyframe k
+  // updates its own list on thread k (independent rows)
+  if (t == 0) {
+    int nmax = 0, kmax = -1, np = 0;
+    for (int k = 0; k < kf; k++) {
+      if (cnt[k] <= 0) continue;
+      if (cnt[k] > nmax) {
+        nmax = cnt[k];
+        kmax = k;
+      }
+      np += cnt[k] >= 15;
+    }
+    s_i[0] = kmax;   // -1: no covisible keyframe (no connection at all)
+    s_i[1] = np;
+  }
+  __syncthreads();
+  const int kmax = s_i[0], npass = s_i[1];
+  if (kmax < 0) return;
+  if (t < kf && (cnt[t] >= 15 || (npass == 0 && t == kmax))) {
+    int* wrow = cscr + t * a.kfc;
+    uint8_t* ks = reinterpret_cast<uint8_t*>(cscr + a.kfc * a.kfc) + t * a.kfc;
+    add_connection(a, P, t, kf, cnt[t], wrow, ks);
+  }
+  if (t == 0) {
+    int np = 0;
+    for (int k = 0; k < kf; k++)
+      if (cnt[k] >= 15) {
+        pw[np] = cnt[k];
+        pk[np++] = k;
+      }
+    if (np == 0) {
+      pw[np] = cnt[kmax];
+      pk[np++] = kmax;
+    }
+    // sort (weight, id) ascending, the ordered list is its reverse
+    for (int x = 1; x < np; x++) {
+      const int vw = pw[x], vk = pk[x];
+      int y = x - 1;
+      while (y >= 0 && (pw[y] > vw || (pw[y] == vw && pk[y] > vk))) {
+        pw[y + 1] = pw[y];
+        pk[y + 1] = pk[y];
+        y--;
+      }
+      pw[y + 1] = vw;
+      pk[y + 1] = vk;
+    }
+    int* wk = a.kf_w + kb * a.kfc;
+    for (int k = 0; k < kf; k++) wk[k] = cnt[k];
+    uint8_t* ord = a.kf_ord + kb * a.kfc;
+    for (int x = 0; x < np; x++) ord[x] = (uint8_t)pk[np - 1 - x];
+    a.kf_nord[kb] = np;
+    if (a.kf_first[kb]) {
+      const int par = ord[0];
+      a.kf_parent[kb] = par;
+      a.kf_child[P.kfb(par)] |= 1ull << kf;
+      a.kf_first[kb] = 0;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 void launch_map_reset(const MapArgs& a, const float* T0, int nstreams, hipStream_t s) {
   hipLaunchKernelGGL(k_map_reset, dim3((nstreams + 255) / 256), dim3(256), 0, s, a, T0, nstreams);
@@ -1403,6 +1517,8 @@ void launch_map_assemble(const MapArgs& a, int nstreams, hipStream_t s) {
 }
 void launch_map_finish(const TrackConsts& c, const MapArgs& a, int nstreams, hipStream_t s) {
   hipLaunchKernelGGL(k_map_finish, dim3(nstreams), dim3(kT), 0, s, c, a);
+  hipLaunchKernelGGL(k_map_kf_points, dim3((a.kp_pitch + 63) / 64, nstreams), dim3(64), 0, s, c, a);
+  hipLaunchKernelGGL(k_map_connect, dim3(nstreams), dim3(kT), (size_t)5 * a.kfc * a.kfc, s, a);
 }
 
 }  // namespace orbpl

@@ -707,9 +707,7 @@ void launch_match_bow(const BowArgs& a, hipStream_t s) {
 // memory here: 32 KB more LDS on every workgroup of the launch made it slower
 // to place beside the next batch's extraction (a persistent grid with LDS
 // descriptors measured 2.2 ms per step against 0.3-0.8 ms this way).
-__global__ void __launch_bounds__(256) k_trk_bow(TrkArgs a) {
-  __shared__ BowShared B;
-  const int s = blockIdx.x;
+__device__ __forceinline__ void trk_bow_stream(const TrkArgs& a, BowShared& B, const int s) {
   StreamState& S = a.st[s];
   if (!S.trk) return;
   const long long cb = (long long)s * a.kp_pitch;
@@ -732,8 +730,24 @@ __global__ void __launch_bounds__(256) k_trk_bow(TrkArgs a) {
   match_bow_body(b, B, nullptr);
 }
 
+// one workgroup per stream, or (a.list) a small grid looping over the listed
+// streams (the map model's TrackReferenceKeyFrame streams)
+__global__ void __launch_bounds__(256) k_trk_bow(TrkArgs a) {
+  __shared__ BowShared B;
+  if (a.list) {
+    const int n = *a.list_n;
+    for (int b = blockIdx.x; b < n; b += gridDim.x) {
+      trk_bow_stream(a, B, a.list[b]);
+      __syncthreads();
+    }
+  } else {
+    trk_bow_stream(a, B, blockIdx.x);
+  }
+}
+
 void launch_trk_bow(const TrkArgs& a, int nstreams, hipStream_t s) {
-  hipLaunchKernelGGL(k_trk_bow, dim3(nstreams), dim3(256), 0, s, a);
+  const int grid = a.list ? (nstreams < kListGrid ? nstreams : kListGrid) : nstreams;
+  hipLaunchKernelGGL(k_trk_bow, dim3(grid), dim3(256), 0, s, a);
 }
 
 }  // namespace orbpl

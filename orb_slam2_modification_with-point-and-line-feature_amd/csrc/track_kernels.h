@@ -78,9 +78,16 @@ struct PoseLaunch {
   uint8_t* t_loutlier;
   int lpitch;
   int fixed_line_jac;           // ORBPL_POSE_FIXED_LINE_JAC (analytic line Jacobian)
+  const int* list = nullptr;    // optional device list of streams to run (list_n of them): a
+  const int* list_n = nullptr;  // grid of kListGrid workgroups loops over it
   int gate_lm;                  // 1: run only streams with active[s].lm_active (TrackLocalMap)
                                 // 2: only active[s].trk && trk_go (TrackReferenceKeyFrame)
 };
+
+// Workgroups of a launch over a device stream list (rare per-stream work such
+// as TrackReferenceKeyFrame): small enough to place quickly beside the
+// extraction kernels when the list is empty
+constexpr int kListGrid = 256;
 
 // Per-frame line buffers of the tracker (kLineKeep lines per stream).
 struct LineTrackArgs {
@@ -146,6 +153,8 @@ struct LineListArgs {
   long long ml_pitch;
   int pose_stride;
   int nm_stride;
+  const int* list = nullptr;     // optional (batched): the streams to run, list_n of them
+  const int* list_n = nullptr;
 };
 void launch_line_match_list(const TrackConsts& c, const LineListArgs& a, hipStream_t s,
                             int nstreams = 1);
@@ -242,6 +251,8 @@ struct TrkArgs {
   int* cur_nobs_l;  // Observations() of those (1 / 0)
   int* tlm;         // the reference-keyframe line search's matches
   int* nml;         // per stream: the keyframe's lines to search (0 = stream not tracked by it)
+  const int* list = nullptr;     // optional: the streams to run (k_trk_bow), list_n of them
+  const int* list_n = nullptr;
 };
 void launch_trk_prep(const TrkArgs& a, int nstreams, hipStream_t s);
 void launch_trk_bow(const TrkArgs& a, int nstreams, hipStream_t s);

@@ -1040,6 +1040,8 @@ struct PoseArgs {
   int prof;                   // debug: phase stamps of stream 0 into g_pose_prof
   int fixed_line_jac;         // ORBPL_POSE_FIXED_LINE_JAC
   int gate_lm;                // 1: only active[s].lm_active; 2: only trk && trk_go
+  const int* list;            // optional: the streams to run (list_n of them)
+  const int* list_n;
 };
 
 // debug (ORBPL_POSE_PROFILE): accumulated wall-clock ticks (100 MHz) of
@@ -1059,12 +1061,11 @@ __device__ void se3_from_T(const float* T, SE3d& s) {
 // kPoseThreads threads per stream (one workgroup per stream), kMinWaves waves
 // per SIMD the register budget must allow (1: ~300 VGPRs; 2: 256 and a few
 // spills); launch_pose picks both from the streams per CU
-template <int kPoseThreads, int kMinWaves>
-__global__ void __launch_bounds__(kPoseThreads, kMinWaves) k_pose(TrackConsts tc, PoseArgs a) {
+template <int kPoseThreads>
+__device__ __forceinline__ void pose_stream(const TrackConsts& tc, const PoseArgs& a,
+                                            PoseShared& S, const int s) {
   constexpr int kPoseWaves = kPoseThreads / 64;
-  extern __shared__ char smem_raw[];
-  PoseShared& S = *reinterpret_cast<PoseShared*>(smem_raw);
-  const int s = blockIdx.x, t = threadIdx.x;
+  const int t = threadIdx.x;
   // TrackWithMotionModel returns before optimising when no last frame exists
   // or nmatches < 20 after the retry (Tracking.cc:1255-1265).
   // (with lines: also when LineMatcher found < 15, Tracking.cc:1260-1265)
@@ -1438,6 +1439,25 @@ __global__ void __launch_bounds__(kPoseThreads, kMinWaves) k_pose(TrackConsts tc
   // (pt[7]: linearize edge loop only; pt[1]: its block reduction)
 }
 
+// One workgroup per stream, or (a.list) a small grid looping over the streams
+// a list names (the rarely used TrackReferenceKeyFrame pose: a launch of one
+// workgroup per stream costs its placement beside the extraction kernels even
+// when no stream has work)
+template <int kPoseThreads, int kMinWaves>
+__global__ void __launch_bounds__(kPoseThreads, kMinWaves) k_pose(TrackConsts tc, PoseArgs a) {
+  extern __shared__ char smem_raw[];
+  PoseShared& S = *reinterpret_cast<PoseShared*>(smem_raw);
+  if (a.list) {
+    const int n = *a.list_n;
+    for (int b = blockIdx.x; b < n; b += gridDim.x) {
+      pose_stream<kPoseThreads>(tc, a, S, a.list[b]);
+      __syncthreads();
+    }
+  } else {
+    pose_stream<kPoseThreads>(tc, a, S, blockIdx.x);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // After PoseOptimization: discard outliers (Tracking.cc:1273-1296), velocity
 // history, and the next frame's map points (all keypoints with depth,
@@ -1689,6 +1709,8 @@ void launch_pose(const TrackConsts& c, const PoseLaunch& p, int nstreams, hipStr
   a.lpitch = p.lpitch;
   a.fixed_line_jac = p.fixed_line_jac;
   a.gate_lm = p.gate_lm;
+  a.list = p.list;
+  a.list_n = p.list_n;
   static const int prof = getenv("ORBPL_POSE_PROFILE") ? 1 : 0;
   a.prof = prof;
   // threads per stream by streams per CU: the widest workgroup while every
@@ -1703,10 +1725,11 @@ void launch_pose(const TrackConsts& c, const PoseLaunch& p, int nstreams, hipStr
   if (nstreams > 2 * cus) nt = 64;   // (2 waves per SIMD measured slower at 512 / 1024)
   static const char* cfg = getenv("ORBPL_POSE_CFG");
   if (cfg) sscanf(cfg, "%d,%d", &nt, &mw);
+  const int grid = p.list ? (nstreams < kListGrid ? nstreams : kListGrid) : nstreams;
 #define ORBPL_POSE_LAUNCH(NT, MW)                                                            \
   if (nt == NT && mw == MW) {                                                                 \
     set_smem_attr((const void*)k_pose<NT, MW>, sizeof(PoseShared));                           \
-    hipLaunchKernelGGL((k_pose<NT, MW>), dim3(nstreams), dim3(NT), sizeof(PoseShared), s, c, a); \
+    hipLaunchKernelGGL((k_pose<NT, MW>), dim3(grid), dim3(NT), sizeof(PoseShared), s, c, a); \
     return;                                                                                   \
   }
   ORBPL_POSE_LAUNCH(256, 1)
@@ -1717,7 +1740,7 @@ void launch_pose(const TrackConsts& c, const PoseLaunch& p, int nstreams, hipStr
   ORBPL_POSE_LAUNCH(64, 2)
 #undef ORBPL_POSE_LAUNCH
   set_smem_attr((const void*)k_pose<64, 1>, sizeof(PoseShared));
-  hipLaunchKernelGGL((k_pose<64, 1>), dim3(nstreams), dim3(64), sizeof(PoseShared), s, c, a);
+  hipLaunchKernelGGL((k_pose<64, 1>), dim3(grid), dim3(64), sizeof(PoseShared), s, c, a);
 }
 
 void launch_finish(const TrackConsts& c, StreamState* st, const int* n, int kp_pitch,

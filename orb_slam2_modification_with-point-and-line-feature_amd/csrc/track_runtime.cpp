@@ -980,6 +980,8 @@ static int map_alloc(orbpl_tracker* t, int kfc) {
   MA(m.trk_cur_nobs, S * L * 4);
   MA(m.trk_lm, S * L * 4);
   MA(m.trk_nml, S * 4);
+  MA(m.trk_list, S * 4);
+  MA(m.trk_count, 4);
   MA(m.m2, S * K * 4);
   MA(m.pxyz, S * K * 12);
   MA(m.lm2, S * L * 4);
@@ -1456,6 +1458,8 @@ static int map_track(orbpl_tracker* t, FrameBufs& C, FrameBufs& L, const LineTra
     ta.last_desc = a.r_desc;
     ta.last_has_mp = a.r_has_mp;
     ta.last_feat_node = a.r_node;
+    ta.list = a.trk_list;      // only the streams k_map_resolve_motion listed
+    ta.list_n = a.trk_count;
     launch_trk_bow(ta, S, ts);
     if (t->lines) {
       LineListArgs lr{};
@@ -1478,11 +1482,15 @@ static int map_track(orbpl_tracker* t, FrameBufs& C, FrameBufs& L, const LineTra
       lr.ml_pitch = kLineKeep;
       lr.pose_stride = pstride;
       lr.nm_stride = pstride;
+      lr.list = a.trk_list;
+      lr.list_n = a.trk_count;
       launch_line_match_list(t->consts, lr, ts, S);
     }
     launch_map_trk_merge(a, S, ts);
     PoseLaunch pt = pm;
     pt.gate_lm = 2;
+    pt.list = a.trk_list;
+    pt.list_n = a.trk_count;
     launch_pose(t->consts, pt, S, ts);
   }
   HIP_CHECK(hipEventRecord(ev[31], ts));

@@ -1,23 +1,18 @@
 #!/bin/bash
-# Quick GPU iteration: selected parity tests (-k expression in $1, "" = all
-# GPU tests), then a kernel trace of a short headline bench run (extra
-# arguments go to bench.py). Every GPU step has its own time limit; the
-# script stops at the first failure.
+# Quick GPU check: map parity + the headline leg only (no secondary legs).
 set -o pipefail
-mkdir -p gpurun_out
-K=${1:-}
-shift
-if [ -n "$K" ]; then
-  timeout -k 10 500 python -u -m pytest tests -m gpu -x -v -k "$K" --timeout 300 --timeout-method thread > gpurun_out/quick_tests.log 2>&1
-else
-  timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/quick_tests.log 2>&1
-fi
-rc=$?; echo "pytest exit $rc"; tail -3 gpurun_out/quick_tests.log
-[ $rc -ne 0 ] && exit $rc
-cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-rm -rf $R/gpurun_out/prof_quick
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_quick -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --sweep 0 --secondary-steps 0 --stereo-steps 0 --rig-steps 0 --isolated-steps 0 --ingress-steps 0 "$@" > $R/gpurun_out/quick_bench.log 2>&1
-rc=$?; echo "trace exit $rc"; tail -c 300 $R/gpurun_out/quick_bench.log
-[ $rc -ne 0 ] && exit $rc
-cut -d, -f1-4 $R/gpurun_out/prof_quick/run_kernel_stats.csv | cut -c1-160 | head -16
+mkdir -p $R/gpurun_out
+cd $R
+timeout -k 10 600 python -u -m pytest tests/test_gpu_map.py -q --timeout 300 --timeout-method thread > gpurun_out/gpu_map_q.log 2>&1
+rc=$?
+echo "map tests rc=$rc"; tail -2 gpurun_out/gpu_map_q.log
+if [ $rc -ne 0 ]; then grep -E "assert|Error" gpurun_out/gpu_map_q.log | head -20; exit 1; fi
+timeout -k 10 600 python -u bench.py --secondary-steps 0 --stereo-steps 0 --rig-steps 0 --ingress-steps 0 --sweep 0 --no-cpu-baseline $QUICK_ARGS > gpurun_out/bench_q.json 2> gpurun_out/bench_q.err || { echo "bench failed"; tail -20 gpurun_out/bench_q.err; exit 1; }
+python3 - <<'PY'
+import json
+d = json.loads(open("gpurun_out/bench_q.json").read().strip().splitlines()[-1])
+print("value", d["value"], "ms", d["ms_per_step"], "parity", d["parity"]["pass"])
+print("stages", d["stage_ms"])
+print("isolated", d["roofline"].get("isolated", {}).get("stage_ms"))
+PY
