@@ -25,8 +25,7 @@ OUT = Path("/tmp/lsd_chain_stats")
 def build():
     OUT.mkdir(exist_ok=True)
     s = (ROOT / "oracle" / "lsd_oracle.cpp").read_text()
-    s = s.replace('#include "../orb_slam2_modification_with-point-and-line-feature_amd/csrc/lsd_math.h"',
-                  f'#include "{ROOT}/orb_slam2_modification_with-point-and-line-feature_amd/csrc/lsd_math.h"')
+    s = s.replace('#include "pinned_math.h"', f'#include "{ROOT}/oracle/pinned_math.h"')
     s = s.replace('#include "oracle_api.h"',
                   f'#include "{ROOT}/oracle/oracle_api.h"\n'
                   'static double C_grow = 0, C_fit = 0, C_red = 0;\n'
@@ -80,7 +79,9 @@ def main():
         r = pad.reshape(R, 64, 3)
         print(f"frame {f}: seeds {len(c)}, lines {no.value}, rounds {R}; per-round max "
               f"(load round trips): grow {r[:, :, 0].max(1).sum():.0f}, fit {r[:, :, 1].max(1).sum():.0f}, "
-              f"reduce scan {r[:, :, 2].max(1).sum():.0f}, whole lane {r.sum(2).max(1).sum():.0f}")
+              f"reduce scan {r[:, :, 2].max(1).sum():.0f}, whole lane {r.sum(2).max(1).sum():.0f}; "
+              f"balanced (sum / 64): grow {c[:, 0].sum() / 64:.0f}, whole lane {c.sum() / 64:.0f}; "
+              f"seeds >= min size {int((c[:, 1] > 0).sum())}, fit+reduce sum {c[:, 1:].sum():.0f}")
 
 
 if __name__ == "__main__":
