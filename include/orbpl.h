@@ -526,6 +526,19 @@ int orbpl_tracker_get_map_history(orbpl_tracker* tr, int stream, int max_steps, 
  * reset (1 keyframe table full: NeedNewKeyFrame declined; 2 point / line pool
  * full; 4 local list full); 0 = the map matches the reference's. */
 int orbpl_tracker_get_map_errors(orbpl_tracker* tr, int* err);
+/* ORBPL_TRACK_MAP trackers, one stream's map after the last step (host copies):
+ * keyframes (n_kf; per keyframe its spanning-tree parent (-1 none), the number
+ * of ordered connections and the first `cap` of them (GetVectorCovisibleKeyFrames
+ * order, -1 padded)); map points (n_mp; the first `cap`: Observations(),
+ * GetDescriptor(), world position, GetNormal(), [mfMinDistance,
+ * mfMaxDistance]); map lines (n_ml; Observations(), descriptor, end points).
+ * Any output pointer may be NULL. */
+int orbpl_tracker_get_map_keyframes(orbpl_tracker* tr, int stream, int* parent, int* ord, int cap,
+                                    int* nord, int* n_kf);
+int orbpl_tracker_get_map_points(orbpl_tracker* tr, int stream, int cap, int* nobs, uint8_t* desc,
+                                 float* xyz, float* normal, float* dist2, int* n_mp);
+int orbpl_tracker_get_map_lines(orbpl_tracker* tr, int stream, int cap, int* nobs, uint8_t* desc,
+                                float* pos6, int* n_ml);
 /* KeyFrame::ComputeBoW (KeyFrame.cc:67; every tracked frame is a keyframe,
  * P18) with `voc` (uploaded to the tracker's device; not owned, must outlive
  * the tracker or be unset with NULL): each step transforms the frame's

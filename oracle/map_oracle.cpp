@@ -1202,6 +1202,32 @@ int oracle_map_keyframes(void* h, int stream, int* parent, int* ord, int cap, in
   return n;
 }
 
+// per map point: mean viewing direction, mfMinDistance / mfMaxDistance
+int oracle_map_points_geom(void* h, int stream, float* nrm, float* dist2, int cap) {
+  const mapvo::Stream& S = static_cast<mapvo::MapVO*>(h)->st[stream];
+  const int n = (int)S.mps.size();
+  for (int p = 0; p < n && p < cap; p++) {
+    if (nrm) std::memcpy(nrm + 3 * (size_t)p, S.mps[p].normal, 12);
+    if (dist2) {
+      dist2[2 * p] = S.mps[p].min_dist;
+      dist2[2 * p + 1] = S.mps[p].max_dist;
+    }
+  }
+  return n;
+}
+
+// per map line: observation count, descriptor, end points; returns the count
+int oracle_map_lines(void* h, int stream, int* nobs, uint8_t* desc, float* pos6, int cap) {
+  const mapvo::Stream& S = static_cast<mapvo::MapVO*>(h)->st[stream];
+  const int n = (int)S.mls.size();
+  for (int l = 0; l < n && l < cap; l++) {
+    if (nobs) nobs[l] = S.mls[l].nobs;
+    if (desc) std::memcpy(desc + 32 * (size_t)l, S.mls[l].desc, 32);
+    if (pos6) std::memcpy(pos6 + 6 * (size_t)l, S.mls[l].pos, 24);
+  }
+  return n;
+}
+
 // per map point: observation count (nObs) and descriptor; returns the count
 int oracle_map_points(void* h, int stream, int* nobs, uint8_t* desc, float* xyz, int cap) {
   const mapvo::Stream& S = static_cast<mapvo::MapVO*>(h)->st[stream];

@@ -711,6 +711,8 @@ def _setup(L):  # noqa: F811
     L.oracle_map_step.argtypes = [vp, i, vp, vp, vp, vp]
     L.oracle_map_keyframes.argtypes = [vp, i, vp, vp, i, vp]
     L.oracle_map_points.argtypes = [vp, i, vp, vp, vp, i]
+    L.oracle_map_points_geom.argtypes = [vp, i, vp, vp, i]
+    L.oracle_map_lines.argtypes = [vp, i, vp, vp, vp, i]
 
 
 MAP_COUNTS = ("nkeypoints", "nmatches", "ninliers", "nmatches_map", "ok", "nlines",
@@ -763,6 +765,21 @@ class MapVO:
         n = lib().oracle_map_points(self.h, stream, _p(nobs), _p(desc), _p(xyz), cap)
         n = min(n, cap)
         return nobs[:n], desc[:n], xyz[:n]
+
+    def points_geom(self, stream, cap=1 << 18):
+        """(normal (n, 3), [min, max] distance (n, 2)) per map point."""
+        nrm = np.zeros((cap, 3), np.float32)
+        d2 = np.zeros((cap, 2), np.float32)
+        n = min(lib().oracle_map_points_geom(self.h, stream, _p(nrm), _p(d2), cap), cap)
+        return nrm[:n], d2[:n]
+
+    def lines(self, stream, cap=1 << 16):
+        """(nobs, descriptors, end points (n, 6)) per map line."""
+        nobs = np.zeros(cap, np.int32)
+        desc = np.zeros((cap, 32), np.uint8)
+        pos = np.zeros((cap, 6), np.float32)
+        n = min(lib().oracle_map_lines(self.h, stream, _p(nobs), _p(desc), _p(pos), cap), cap)
+        return nobs[:n], desc[:n], pos[:n]
 
     def __del__(self):
         try:

@@ -114,6 +114,8 @@ int oracle_map_step(void* h, int stream, const uint8_t* gray, const float* depth
                     int* out24);
 int oracle_map_keyframes(void* h, int stream, int* parent, int* ord, int cap, int* nord);
 int oracle_map_points(void* h, int stream, int* nobs, uint8_t* desc, float* xyz, int cap);
+int oracle_map_points_geom(void* h, int stream, float* nrm, float* dist2, int cap);
+int oracle_map_lines(void* h, int stream, int* nobs, uint8_t* desc, float* pos6, int cap);
 #ifdef __cplusplus
 }
 #endif

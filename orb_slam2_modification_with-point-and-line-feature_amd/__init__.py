@@ -407,6 +407,9 @@ def _declare_track(L):
     L.orbpl_tracker_get_trk.argtypes = [vp, vp]
     L.orbpl_tracker_get_map_history.argtypes = [vp, i, i, vp, ip]
     L.orbpl_tracker_get_map_errors.argtypes = [vp, vp]
+    L.orbpl_tracker_get_map_keyframes.argtypes = [vp, i, vp, vp, i, vp, ip]
+    L.orbpl_tracker_get_map_points.argtypes = [vp, i, i, vp, vp, vp, vp, vp, ip]
+    L.orbpl_tracker_get_map_lines.argtypes = [vp, i, i, vp, vp, vp, ip]
 
 
 _declare_orig = _declare
@@ -857,6 +860,43 @@ class Tracker:
         out = np.zeros(self.S, np.int32)
         check(lib().orbpl_tracker_get_map_errors(self._h, _ptr(out)), "orbpl_tracker_get_map_errors")
         return out
+
+    def map_keyframes(self, stream, cap=64):
+        """(parent (n,), [ordered connections per keyframe]) of one stream's map."""
+        par = np.zeros(64, np.int32)
+        ord_ = np.zeros((64, cap), np.int32)
+        nord = np.zeros(64, np.int32)
+        n = C.c_int(0)
+        check(lib().orbpl_tracker_get_map_keyframes(self._h, stream, _ptr(par), _ptr(ord_), cap,
+                                                    _ptr(nord), C.byref(n)),
+              "orbpl_tracker_get_map_keyframes")
+        k = n.value
+        return par[:k].copy(), [ord_[j, :min(nord[j], cap)].copy() for j in range(k)]
+
+    def map_points(self, stream, cap=1 << 17):
+        """dict(nobs, desc, xyz, normal, dist) of one stream's map points."""
+        nobs = np.zeros(cap, np.int32)
+        desc = np.zeros((cap, 32), np.uint8)
+        xyz = np.zeros((cap, 3), np.float32)
+        nrm = np.zeros((cap, 3), np.float32)
+        d2 = np.zeros((cap, 2), np.float32)
+        n = C.c_int(0)
+        check(lib().orbpl_tracker_get_map_points(self._h, stream, cap, _ptr(nobs), _ptr(desc),
+                                                 _ptr(xyz), _ptr(nrm), _ptr(d2), C.byref(n)),
+              "orbpl_tracker_get_map_points")
+        k = min(n.value, cap)
+        return dict(nobs=nobs[:k], desc=desc[:k], xyz=xyz[:k], normal=nrm[:k], dist=d2[:k])
+
+    def map_lines(self, stream, cap=1 << 14):
+        """dict(nobs, desc, pos) of one stream's map lines."""
+        nobs = np.zeros(cap, np.int32)
+        desc = np.zeros((cap, 32), np.uint8)
+        pos = np.zeros((cap, 6), np.float32)
+        n = C.c_int(0)
+        check(lib().orbpl_tracker_get_map_lines(self._h, stream, cap, _ptr(nobs), _ptr(desc),
+                                                _ptr(pos), C.byref(n)), "orbpl_tracker_get_map_lines")
+        k = min(n.value, cap)
+        return dict(nobs=nobs[:k], desc=desc[:k], pos=pos[:k])
 
     STEREO_STAGES = ("right_extract", "stereo_match", "right_lines", "stereo_lines")
 

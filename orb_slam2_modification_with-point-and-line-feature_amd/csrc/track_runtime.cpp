@@ -2316,6 +2316,82 @@ int orbpl_tracker_get_map_history(orbpl_tracker* t, int stream, int max_steps, i
   return ORBPL_OK;
 }
 
+// one stream's map (host copies; tests and inspection): keyframes with their
+// parent and covisibility order, map points, map lines
+static int map_stream_state(orbpl_tracker* t, int stream, MapState* ms) {
+  if (!t || stream < 0 || stream >= t->S) return arg_fail("bad argument");
+  if (!t->map) return arg_fail("tracker created without ORBPL_TRACK_MAP");
+  HIP_CHECK(hipSetDevice(t->device));
+  HIP_CHECK(hipStreamSynchronize(t->tstream));
+  HIP_CHECK(hipStreamSynchronize(t->stream));
+  HIP_CHECK(hipMemcpy(ms, t->ma.ms + stream, sizeof(MapState), hipMemcpyDeviceToHost));
+  return ORBPL_OK;
+}
+
+int orbpl_tracker_get_map_keyframes(orbpl_tracker* t, int stream, int* parent, int* ord, int cap,
+                                    int* nord, int* n_kf) {
+  MapState ms;
+  int rc = map_stream_state(t, stream, &ms);
+  if (rc) return rc;
+  if (!n_kf || cap < 0) return arg_fail("bad argument");
+  const int n = ms.n_kf, F = t->map_kfc;
+  *n_kf = n;
+  const size_t kb = (size_t)stream * F;
+  std::vector<int> par(F), no(F);
+  std::vector<uint8_t> o((size_t)F * F);
+  HIP_CHECK(hipMemcpy(par.data(), t->ma.kf_parent + kb, 4 * (size_t)F, hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(no.data(), t->ma.kf_nord + kb, 4 * (size_t)F, hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(o.data(), t->ma.kf_ord + kb * F, (size_t)F * F, hipMemcpyDeviceToHost));
+  for (int k = 0; k < n; k++) {
+    if (parent) parent[k] = par[k];
+    if (nord) nord[k] = no[k];
+    if (ord)
+      for (int j = 0; j < cap; j++) ord[(size_t)k * cap + j] = j < no[k] && j < F ? o[(size_t)k * F + j] : -1;
+  }
+  return ORBPL_OK;
+}
+
+int orbpl_tracker_get_map_points(orbpl_tracker* t, int stream, int cap, int* nobs, uint8_t* desc,
+                                 float* xyz, float* normal, float* dist2, int* n_mp) {
+  MapState ms;
+  int rc = map_stream_state(t, stream, &ms);
+  if (rc) return rc;
+  if (!n_mp || cap < 0) return arg_fail("bad argument");
+  *n_mp = ms.n_mp;
+  const int n = std::min(ms.n_mp, cap);
+  const size_t g = (size_t)stream * t->ma.mpc;
+  std::vector<float> f4((size_t)n * 4 + 1);
+  if (nobs && n) HIP_CHECK(hipMemcpy(nobs, t->ma.mp_nobs + g, 4 * (size_t)n, hipMemcpyDeviceToHost));
+  if (desc && n) HIP_CHECK(hipMemcpy(desc, t->ma.mp_desc + g * 32, 32 * (size_t)n, hipMemcpyDeviceToHost));
+  if (xyz && n) {
+    HIP_CHECK(hipMemcpy(f4.data(), t->ma.mp_pos + g, 16 * (size_t)n, hipMemcpyDeviceToHost));
+    for (int p = 0; p < n; p++)
+      for (int q = 0; q < 3; q++) xyz[3 * p + q] = f4[4 * p + q];
+  }
+  if (normal && n) {
+    HIP_CHECK(hipMemcpy(f4.data(), t->ma.mp_nrm + g, 16 * (size_t)n, hipMemcpyDeviceToHost));
+    for (int p = 0; p < n; p++)
+      for (int q = 0; q < 3; q++) normal[3 * p + q] = f4[4 * p + q];
+  }
+  if (dist2 && n) HIP_CHECK(hipMemcpy(dist2, t->ma.mp_dist + g, 8 * (size_t)n, hipMemcpyDeviceToHost));
+  return ORBPL_OK;
+}
+
+int orbpl_tracker_get_map_lines(orbpl_tracker* t, int stream, int cap, int* nobs, uint8_t* desc,
+                                float* pos6, int* n_ml) {
+  MapState ms;
+  int rc = map_stream_state(t, stream, &ms);
+  if (rc) return rc;
+  if (!n_ml || cap < 0) return arg_fail("bad argument");
+  *n_ml = ms.n_ml;
+  const int n = std::min(ms.n_ml, cap);
+  const size_t g = (size_t)stream * t->ma.mlc;
+  if (nobs && n) HIP_CHECK(hipMemcpy(nobs, t->ma.ml_nobs + g, 4 * (size_t)n, hipMemcpyDeviceToHost));
+  if (desc && n) HIP_CHECK(hipMemcpy(desc, t->ma.ml_desc + g * 32, 32 * (size_t)n, hipMemcpyDeviceToHost));
+  if (pos6 && n) HIP_CHECK(hipMemcpy(pos6, t->ma.ml_pos + g * 6, 24 * (size_t)n, hipMemcpyDeviceToHost));
+  return ORBPL_OK;
+}
+
 int orbpl_tracker_get_map_errors(orbpl_tracker* t, int* err) {
   if (!t || !err) return arg_fail("NULL argument");
   if (!t->map) return arg_fail("tracker created without ORBPL_TRACK_MAP");

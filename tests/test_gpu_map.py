@@ -61,8 +61,35 @@ def _run(orbpl, oracle, lines, refkf, S, F, seed, turn=None, pipelined=False):
             assert got == want, (s, f, [(k, g, w) for k, g, w in zip(keys, got, want) if g != w])
             assert np.abs(Th[f] - To).max() < POSE_TOL, (s, f, np.abs(Th[f] - To).max())
         out.append([r[1] for r in ref[s]])
+        _same_map(tr, mvo, s, lines)
     assert (tr.map_errors() == 0).all()
     return out
+
+
+def _same_map(tr, mvo, s, lines):
+    """The stream's map after the sequence equals the oracle's element by
+    element: keyframe parents and covisibility orders, and per map point /
+    line (same pool ids: both create them in the reference's order) nObs,
+    the distinctive descriptor, the position, the normal and the distance
+    bounds - bit for bit."""
+    par, ords = tr.map_keyframes(s)
+    opar, oords = mvo.keyframes(s)
+    assert np.array_equal(par, opar), (s, par, opar)
+    assert len(ords) == len(oords) and all(np.array_equal(a, b) for a, b in zip(ords, oords)), s
+    P = tr.map_points(s)
+    onobs, odesc, oxyz = mvo.points(s)
+    onrm, od2 = mvo.points_geom(s)
+    assert len(P["nobs"]) == len(onobs), s
+    assert np.array_equal(P["nobs"], onobs), s
+    assert np.array_equal(P["desc"], odesc), s
+    assert np.array_equal(P["xyz"].view(np.uint32), oxyz.view(np.uint32)), s
+    assert np.array_equal(P["normal"].view(np.uint32), onrm.view(np.uint32)), s
+    assert np.array_equal(P["dist"].view(np.uint32), od2.view(np.uint32)), s
+    if lines:
+        Lm = tr.map_lines(s)
+        lnobs, ldesc, lpos = mvo.lines(s)
+        assert np.array_equal(Lm["nobs"], lnobs) and np.array_equal(Lm["desc"], ldesc), s
+        assert np.array_equal(Lm["pos"].view(np.uint32), lpos.view(np.uint32)), s
 
 
 @pytest.mark.parametrize("lines,refkf,pipelined,seed", [(True, True, False, 110),
@@ -88,3 +115,37 @@ def test_map_tracker_lost_and_reset(orbpl, oracle):
     res = _run(orbpl, oracle, True, True, S=2, F=8, seed=130, turn=(1, 4))
     st = [c["state"] for c in res[1]]
     assert 2 in st or 0 in st[4:], st
+
+
+def test_map_tracker_long_sequence(orbpl, oracle):
+    """16 frames of 3 streams (points + lines, TrackReferenceKeyFrame,
+    pipelined): several keyframes per stream, covisibility orders and spanning
+    tree, the maps equal element by element."""
+    res = _run(orbpl, oracle, True, True, S=3, F=16, seed=150, pipelined=True)
+    for r in res:
+        assert all(c["ok"] == 1 for c in r)
+    assert max(r[-1]["keyframes"] for r in res) >= 4
+
+
+def test_map_capacity_flag(orbpl, oracle, monkeypatch):
+    """A keyframe table of 2 slots: NeedNewKeyFrame wants a third keyframe,
+    the tracker declines it and reports capacity flag 1 (the map no longer
+    matches the reference's)."""
+    monkeypatch.setenv("ORBPL_MAP_KF", "2")
+    S, F = 2, 8
+    seqs = [sequence(F, 130 + s, cam_name="TUM3") for s in range(S)]   # stream 0: 4 keyframes
+    cfg = seqs[0][0]
+    tr = orbpl.Tracker(orbpl.OrbParams(1000, 1.2, 8, 20, 7), orbpl.make_camera(cfg), S, lines=True,
+                       map=True)
+    tr.reset(np.stack([np.linalg.inv(sq[1][0]).astype(np.float32) for sq in seqs]).reshape(S, 16))
+    fa, fb = S * 640 * 480, S * 640 * 480 * 4
+    a = orbpl.DeviceBuffer(fa)
+    b = orbpl.DeviceBuffer(fb)
+    for f in range(F):
+        a.upload(np.stack([seqs[s][2][f][0] for s in range(S)]))
+        b.upload(np.stack([seqs[s][2][f][1] for s in range(S)]))
+        tr.step_device(a.ptr, b.ptr)
+        tr.synchronize()
+    err = tr.map_errors()
+    assert (err & 1).any(), err
+    assert all(tr.map_keyframes(s)[0].shape[0] <= 2 for s in range(S))
