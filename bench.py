@@ -452,7 +452,7 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
     wl = WORKLOADS[workload]
     lines, stereo, cam_name = wl["lines"], wl["stereo"], wl["cam"]
     cams = wl.get("cams", 1)
-    F = args.loop if cams == 1 else args.rig_loop
+    F = (args.loop if workload == args.workload else args.loop_other) if cams == 1 else args.rig_loop
     if S % cams:
         raise SystemExit(f"--streams must be a multiple of the rig's {cams} cameras")
     workers = min(16, os.cpu_count() or 4)
@@ -631,7 +631,8 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
                 pipelined=bool(pipelined), map=use_map)
 
 
-def run_ingress(pkg, synth, args, S, steps, warmup, rank, world, device, dist, voc=None):
+def run_ingress(pkg, synth, args, S, steps, warmup, rank, world, device, dist, voc=None,
+                loop=None):
     """The headline workload fed from host memory (GrabImageRGBD's inputs):
     u8 gray + 16-bit TUM depth (DepthMapFactor 5000) in page-locked host
     buffers, each step's batch copied host-to-device on the tracker's copy
@@ -639,7 +640,10 @@ def run_ingress(pkg, synth, args, S, steps, warmup, rank, world, device, dist, v
     depth converted on the device. The timed region includes the copies."""
     wl = WORKLOADS["points"]
     F = args.loop
-    gray, depth = render_loop(F, seed=1 + rank, workers=min(16, os.cpu_count() or 4))
+    if loop is not None:   # the headline's rendered loop (same camera, seed and length)
+        gray, depth = loop
+    else:
+        gray, depth = render_loop(F, seed=1 + rank, workers=min(16, os.cpu_count() or 4))
     d16 = np.clip(np.round(depth * 5000.0), 0, 65535).astype(np.uint16)
     d32 = d16.astype(np.float32) * (np.float32(1.0) / np.float32(5000.0))   # P21
     traj = synth.loop_trajectory(F, seed=1 + rank)
@@ -850,7 +854,11 @@ def main():
     ap.add_argument("--streams", type=int, default=1024,
                     help="streams (frames per step) per GPU; the sweep reports 1..1024 with the "
                          "per-step latency (8.5 ms at 1024: each stream still runs above 100 Hz)")
-    ap.add_argument("--loop", type=int, default=32, help="frames in the synthetic loop")
+    ap.add_argument("--loop", type=int, default=300,
+                    help="frames in the headline workload's synthetic closed loop (each stream "
+                         "starts at its own frame and walks along it)")
+    ap.add_argument("--loop-other", type=int, default=32,
+                    help="frames in the other single-camera legs' loops")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the host's usable cores")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -958,7 +966,8 @@ def main():
     ingress = None
     if args.workload == "points" and args.ingress_steps > 0:
         ingress = run_ingress(pkg, synth, args, args.streams, args.ingress_steps,
-                              args.warmup, rank, world, device, dist, voc)
+                              args.warmup, rank, world, device, dist, voc,
+                              loop=(res["gray"], res["depth"]))
     # parity of every timed tracker's sampled streams against the oracle
     for r in [res] + list(others.values()) + ([ingress] if ingress else []):
         if args.no_parity:

@@ -15,6 +15,8 @@
 // kRegLds points; longer regions continue in global scratch).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "lsd_kernels.h"
 #include "lsd_math.h"
 #include "orbpl_math.h"
@@ -1344,6 +1346,10 @@ __global__ void __launch_bounds__(64) k_lsd_grow(LsdGeom g, LsdScratch sc) {
 // speculative regions (24.8k -> 40.5k per frame), so a lone frame gains
 // nothing; with the GPU partly empty the extra waves fill it (batch 256:
 // -5 %, 1024: -10 % per batch).
+#ifndef ORBPL_SPEC_SMALL_BATCH
+#define ORBPL_SPEC_SMALL_BATCH 96
+#endif
+constexpr int kSpecSmallBatch = ORBPL_SPEC_SMALL_BATCH;
 // ORBPL_SPEC_MINW: waves per SIMD the one-wave-per-frame variant's register
 // budget must allow. 4 (128 VGPRs, a few spills) although the batches that
 // use it hold 3 frames per SIMD: the free quarter of the register file lets
@@ -1374,8 +1380,8 @@ __device__ __forceinline__ void block_sync() {
   }
 }
 
-template <int W>
-__global__ void __launch_bounds__(64 * W, W == 1 ? ORBPL_SPEC_MINW : 1) k_lsd_spec(LsdGeom g, LsdScratch sc) {
+template <int W, int MINW = (W == 1 ? ORBPL_SPEC_MINW : 1)>
+__global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch sc) {
   constexpr int SL = 64 * W;
   extern __shared__ uint32_t grow_smem[];
   __shared__ uint32_t s_pt[SL];
@@ -1758,7 +1764,16 @@ void launch_lsd_grow(const LsdGeom& g, const LsdScratch& sc, int batch, hipStrea
   switch (lsd_spec_waves(batch)) {
     case 4: hipLaunchKernelGGL(k_lsd_spec<4>, dim3(batch), dim3(256), smem, s, g, sc); break;
     case 2: hipLaunchKernelGGL(k_lsd_spec<2>, dim3(batch), dim3(128), smem, s, g, sc); break;
-    default: hipLaunchKernelGGL(k_lsd_spec<1>, dim3(batch), dim3(64), smem, s, g, sc); break;
+    default:
+      // few frames leave the GPU mostly idle: the register budget of one wave
+      // per SIMD (no spills on the seed chain) instead of the co-residence bound
+      static const char* sb_env = getenv("ORBPL_SPEC_SMALL");
+      static const int small_batch = sb_env ? atoi(sb_env) : kSpecSmallBatch;
+      if (batch <= small_batch)
+        hipLaunchKernelGGL((k_lsd_spec<1, 1>), dim3(batch), dim3(64), smem, s, g, sc);
+      else
+        hipLaunchKernelGGL(k_lsd_spec<1>, dim3(batch), dim3(64), smem, s, g, sc);
+      break;
   }
 }
 
