@@ -17,6 +17,7 @@
 //                     608-660 / Frame::UnprojectStereo)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <stdint.h>
@@ -730,7 +731,7 @@ __device__ SE3d se3_mul(const SE3d& a, const SE3d& b) {
   return r;
 }
 
-struct PoseEdge {
+struct alignas(16) PoseEdge {
   float obs[4];   // mono: u,v ; stereo: u,v,ur ; line: sx,sy,ex,ey
   float X[6];     // point: Xw ; line: world start, end
   float info;
@@ -739,16 +740,85 @@ struct PoseEdge {
   int pad;
 };
 
+// The fixed part of k_pose's LDS; launch_pose appends per-edge chi2 / level /
+// outlier flags for ecap edges and the on-chip edge records (PoseLds).
 struct PoseShared {
-  float chi2[kPoseMaxEdges];      // (float) chi2 of the last computed error (stale
-                                  // semantics; only its float is ever compared)
-  uint8_t level[kPoseMaxEdges];
-  uint8_t out_flag[kPoseMaxEdges];
   double red[4][32];
   double sys[1][28];              // reduced H (upper, row-major), b, robust chi2
   int wsum[8];
   int misc[8];
 };
+
+// Edge storage of one stream. Point edges are 32-byte records {u, v, ur,
+// invSigma2} {X, Y, Z, index} (kind = ur < 0 ? mono : stereo), line edges
+// PoseEdge records. The first pcap point edges and the first lcap line edges
+// live in LDS, read by every linearisation, trial and classification pass;
+// the rest (frames beyond the block's LDS budget) in the stream's global
+// scratch (pose_edge_bytes() per edge slot: points, then lines).
+struct PoseLds {
+  float* chi2;                    // (float) chi2 of the last computed error (stale
+                                  // semantics; only its float is ever compared)
+  uint8_t* level;
+  uint8_t* out_flag;
+  float4* prec;                   // pcap point records (2 float4 each)
+  PoseEdge* lrec;                 // lcap line records
+  float4* pg;                     // global: point records
+  PoseEdge* lg;                   // global: line records
+  int pcap, lcap, npts;
+};
+
+__device__ __forceinline__ PoseEdge fetch_edge(const PoseLds& V, int k) {
+  PoseEdge e;
+  if (k < V.npts) {
+    float4 A, B;
+    if (k < V.pcap) {
+      A = V.prec[2 * k];
+      B = V.prec[2 * k + 1];
+    } else {
+      A = V.pg[2 * k];
+      B = V.pg[2 * k + 1];
+    }
+    e.obs[0] = A.x; e.obs[1] = A.y; e.obs[2] = A.z; e.obs[3] = 0;
+    e.info = A.w;
+    e.X[0] = B.x; e.X[1] = B.y; e.X[2] = B.z;
+    e.X[3] = e.X[4] = e.X[5] = 0;
+    e.idx = __float_as_int(B.w);
+    e.kind = A.z < 0 ? 0 : 1;
+    e.pad = 0;
+  } else {
+    const int j = k - V.npts;
+    e = j < V.lcap ? V.lrec[j] : V.lg[j];
+  }
+  return e;
+}
+
+__device__ __forceinline__ PoseEdge fetch_point(const PoseLds& V, int k) {
+  float4 A, B;
+  if (k < V.pcap) {
+    A = V.prec[2 * k];
+    B = V.prec[2 * k + 1];
+  } else {
+    A = V.pg[2 * k];
+    B = V.pg[2 * k + 1];
+  }
+  PoseEdge e;
+  e.obs[0] = A.x; e.obs[1] = A.y; e.obs[2] = A.z; e.obs[3] = 0;
+  e.info = A.w;
+  e.X[0] = B.x; e.X[1] = B.y; e.X[2] = B.z;
+  e.X[3] = e.X[4] = e.X[5] = 0;
+  e.idx = __float_as_int(B.w);
+  e.kind = A.z < 0 ? 0 : 1;
+  e.pad = 0;
+  return e;
+}
+
+__device__ __forceinline__ void store_point(const PoseLds& V, int k, float u, float v, float ur,
+                                            float info, const float* X, int idx) {
+  const float4 A = make_float4(u, v, ur, info), B = make_float4(X[0], X[1], X[2], __int_as_float(idx));
+  float4* d = k < V.pcap ? V.prec : V.pg;
+  d[2 * k] = A;
+  d[2 * k + 1] = B;
+}
 
 struct PoseCam {
   double fx, fy, cx, cy, bf;
@@ -969,10 +1039,187 @@ __device__ __forceinline__ void huber(double chi, double delta, double dsqr, dou
   }
 }
 
+// A point edge's chi2 at T and its robust value: edge_error's arithmetic for
+// kinds 0 / 1 without branches (the mono projection's two divisions issued for
+// every edge, the stereo 1 / z taken from the first), so that the unrolled
+// trial pass overlaps several edges' dependent FP64 chains.
+__device__ __forceinline__ double point_chi2(const PoseEdge& e, const PoseCam& c, const SE3d& T,
+                                             bool robust, double dMono, double dsMono,
+                                             double dStereo, double dsStereo, double* rho0) {
+  const double X[3] = {e.X[0], e.X[1], e.X[2]};
+  double p[3];
+  quat_rotate(T.q, X, p);
+  p[0] += T.t[0]; p[1] += T.t[1]; p[2] += T.t[2];
+  const bool mono = e.kind == 0;
+  const double q0 = (mono ? p[0] : 1.0) / p[2];
+  const double q1 = p[1] / p[2];
+  const float invz = (float)q0;
+  const double u = mono ? q0 * c.fx + c.cx : p[0] * (double)invz * c.fx + c.cx;
+  const double v = mono ? q1 * c.fy + c.cy : p[1] * (double)invz * c.fy + c.cy;
+  const double e0 = (double)e.obs[0] - u, e1 = (double)e.obs[1] - v;
+  const double e2 = (double)e.obs[2] - (u - c.bf * (double)invz);
+  const double info = (double)e.info;
+  double x2 = e0 * info * e0;
+  x2 += e1 * info * e1;
+  const double x3 = x2 + e2 * info * e2;
+  x2 = mono ? x2 : x3;
+  double r = x2;
+  if (robust) {
+    const double delta = mono ? dMono : dStereo, dsqr = mono ? dsMono : dsStereo;
+    const double sq = sqrt(x2);
+    r = x2 <= dsqr ? x2 : 2 * sq * delta - dsqr;
+  }
+  *rho0 = r;
+  return x2;
+}
+
+// A point edge's linearisation (edge_error + edge_jacobian for kinds 0 / 1,
+// branch-free: 1 / z and the mono quotients all issued), its chi2 and robust
+// weight; the caller accumulates H / b in its edge order.
+struct PointLin {
+  double err[3], J[3][6], x2, w, r0, info;
+};
+__device__ __forceinline__ void point_lin(const PoseEdge& e, const PoseCam& c, const SE3d& T,
+                                          bool robust, double dMono, double dsMono, double dStereo,
+                                          double dsStereo, PointLin& o) {
+  const double X[3] = {e.X[0], e.X[1], e.X[2]};
+  double p[3];
+  quat_rotate(T.q, X, p);
+  p[0] += T.t[0]; p[1] += T.t[1]; p[2] += T.t[2];
+  const bool mono = e.kind == 0;
+  const double iz = 1.0 / p[2];
+  const double m0 = p[0] / p[2], m1 = p[1] / p[2];
+  const float invzf = (float)iz;
+  const double u = mono ? m0 * c.fx + c.cx : p[0] * (double)invzf * c.fx + c.cx;
+  const double v = mono ? m1 * c.fy + c.cy : p[1] * (double)invzf * c.fy + c.cy;
+  o.err[0] = (double)e.obs[0] - u;
+  o.err[1] = (double)e.obs[1] - v;
+  o.err[2] = mono ? 0.0 : (double)e.obs[2] - (u - c.bf * (double)invzf);
+  o.info = (double)e.info;
+  double x2 = o.err[0] * o.info * o.err[0];
+  x2 += o.err[1] * o.info * o.err[1];
+  x2 += o.err[2] * o.info * o.err[2];
+  o.x2 = x2;
+  o.w = 1.0;
+  o.r0 = x2;
+  if (robust) {
+    const double delta = mono ? dMono : dStereo, dsqr = mono ? dsMono : dsStereo;
+    const double sq = sqrt(x2);
+    const bool in = x2 <= dsqr;
+    o.r0 = in ? x2 : 2 * sq * delta - dsqr;
+    o.w = in ? 1.0 : delta / sq;
+  }
+  const double x = p[0], y = p[1], invz_2 = iz * iz;
+  double (&J)[3][6] = o.J;
+  J[0][0] = x * y * invz_2 * c.fx;
+  J[0][1] = -(1 + (x * x * invz_2)) * c.fx;
+  J[0][2] = y * iz * c.fx;
+  J[0][3] = -iz * c.fx;
+  J[0][4] = 0;
+  J[0][5] = x * invz_2 * c.fx;
+  J[1][0] = (1 + y * y * invz_2) * c.fy;
+  J[1][1] = -x * y * invz_2 * c.fy;
+  J[1][2] = -x * iz * c.fy;
+  J[1][3] = 0;
+  J[1][4] = -iz * c.fy;
+  J[1][5] = y * invz_2 * c.fy;
+  J[2][0] = mono ? 0.0 : J[0][0] - c.bf * y * invz_2;
+  J[2][1] = mono ? 0.0 : J[0][1] + c.bf * x * invz_2;
+  J[2][2] = mono ? 0.0 : J[0][2];
+  J[2][3] = mono ? 0.0 : J[0][3];
+  J[2][4] = 0;
+  J[2][5] = mono ? 0.0 : J[0][5] - c.bf * invz_2;
+}
+
+__device__ __forceinline__ void accumulate_lin(const PointLin& o, double* acc) {
+  acc[27] += o.r0;
+  const double wi = o.w * o.info;
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    double bi = o.J[0][i] * o.info * o.err[0];
+    bi += o.J[1][i] * o.info * o.err[1];
+    bi += o.J[2][i] * o.info * o.err[2];
+    acc[21 + i] -= o.w * bi;
+  }
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+#pragma unroll
+    for (int j = i; j < 6; j++) {
+      double h = o.J[0][i] * wi * o.J[0][j];
+      h += o.J[1][i] * wi * o.J[1][j];
+      h += o.J[2][i] * wi * o.J[2][j];
+      acc[6 * i - i * (i - 1) / 2 + (j - i)] += h;
+    }
+  }
+}
+
+// point_lin + accumulate_lin with the Jacobian built one row at a time into
+// the accumulators (6 doubles live instead of 18; H / b summed row by row, a
+// different order of the same products). Returns chi2; skips the
+// accumulation for inactive edges.
+template <int>
+__device__ __forceinline__ double point_lin_rows(const PoseEdge& e, const PoseCam& c, const SE3d& T,
+                                                 bool robust, double dMono, double dsMono,
+                                                 double dStereo, double dsStereo, bool on,
+                                                 double* acc) {
+  const double X[3] = {e.X[0], e.X[1], e.X[2]};
+  double p[3];
+  quat_rotate(T.q, X, p);
+  p[0] += T.t[0]; p[1] += T.t[1]; p[2] += T.t[2];
+  const bool mono = e.kind == 0;
+  const double iz = 1.0 / p[2];
+  const double m0 = p[0] / p[2], m1 = p[1] / p[2];
+  const float invzf = (float)iz;
+  const double u = mono ? m0 * c.fx + c.cx : p[0] * (double)invzf * c.fx + c.cx;
+  const double v = mono ? m1 * c.fy + c.cy : p[1] * (double)invzf * c.fy + c.cy;
+  const double e0 = (double)e.obs[0] - u, e1 = (double)e.obs[1] - v;
+  const double e2 = mono ? 0.0 : (double)e.obs[2] - (u - c.bf * (double)invzf);
+  const double info = (double)e.info;
+  double x2 = e0 * info * e0;
+  x2 += e1 * info * e1;
+  x2 += e2 * info * e2;
+  double w = 1.0, r0 = x2;
+  if (robust) {
+    const double delta = mono ? dMono : dStereo, dsqr = mono ? dsMono : dsStereo;
+    const double sq = sqrt(x2);
+    const bool in = x2 <= dsqr;
+    r0 = in ? x2 : 2 * sq * delta - dsqr;
+    w = in ? 1.0 : delta / sq;
+  }
+  if (!on) return x2;
+  acc[27] += r0;
+  const double wi = w * info;
+  const double x = p[0], y = p[1], invz_2 = iz * iz;
+  auto row = [&](const double (&j)[6], double er) {
+#pragma unroll
+    for (int i = 0; i < 6; i++) acc[21 + i] -= w * (j[i] * info * er);
+#pragma unroll
+    for (int i = 0; i < 6; i++)
+#pragma unroll
+      for (int q = i; q < 6; q++) acc[6 * i - i * (i - 1) / 2 + (q - i)] += j[i] * wi * j[q];
+  };
+  const double j0[6] = {x * y * invz_2 * c.fx, -(1 + (x * x * invz_2)) * c.fx, y * iz * c.fx,
+                        -iz * c.fx, 0.0, x * invz_2 * c.fx};
+  row(j0, e0);
+  {
+    const double j1[6] = {(1 + y * y * invz_2) * c.fy, -x * y * invz_2 * c.fy, -x * iz * c.fy, 0.0,
+                          -iz * c.fy, y * invz_2 * c.fy};
+    row(j1, e1);
+  }
+  if (!mono) {
+    const double j2[6] = {j0[0] - c.bf * y * invz_2, j0[1] + c.bf * x * invz_2, j0[2], j0[3], 0.0,
+                          j0[5] - c.bf * invz_2};
+    row(j2, e2);
+  }
+  return x2;
+}
+
 __device__ bool solve6(const double A[6][6], const double b[6], double x[6]) {
   // LDL^T without pivoting (pinned P8); fully unrolled so every array index
-  // is a compile-time constant (registers, no scratch)
-  double L[6][6], D[6];
+  // is a compile-time constant (registers, no scratch). One division per
+  // pivot (its reciprocal scales the column and the back substitution): the
+  // step differs from the oracle's quotients in the last bits only.
+  double L[6][6], D[6], rD[6];
   bool ok = true;
 #pragma unroll
   for (int j = 0; j < 6; j++) {
@@ -980,13 +1227,14 @@ __device__ bool solve6(const double A[6][6], const double b[6], double x[6]) {
 #pragma unroll
     for (int k = 0; k < j; k++) d -= L[j][k] * L[j][k] * D[k];
     D[j] = d;
+    rD[j] = 1.0 / d;
     ok = ok && (d > 0);
 #pragma unroll
     for (int i = j + 1; i < 6; i++) {
       double s = A[i][j];
 #pragma unroll
       for (int k = 0; k < j; k++) s -= L[i][k] * L[j][k] * D[k];
-      L[i][j] = s / d;
+      L[i][j] = s * rD[j];
     }
   }
   if (!ok) return false;
@@ -1000,7 +1248,7 @@ __device__ bool solve6(const double A[6][6], const double b[6], double x[6]) {
   }
 #pragma unroll
   for (int i = 5; i >= 0; i--) {
-    double s = y[i] / D[i];
+    double s = y[i] * rD[i];
 #pragma unroll
     for (int k = i + 1; k < 6; k++) s -= L[k][i] * x[k];
     x[i] = s;
@@ -1042,7 +1290,17 @@ struct PoseArgs {
   int gate_lm;                // 1: only active[s].lm_active; 2: only trk && trk_go
   const int* list;            // optional: the streams to run (list_n of them)
   const int* list_n;
+  int ecap;                   // edges per stream (chi2 / flags in LDS)
+  int pcap, lcap;             // point / line edge records in LDS (the rest global)
 };
+
+// k_pose's dynamic LDS: PoseShared, chi2 / level / outlier flag per edge,
+// pcap point records, lcap line records
+__host__ __device__ __forceinline__ size_t pose_lds_bytes(int ecap, int pcap, int lcap) {
+  const size_t h = (sizeof(PoseShared) + 15) & ~(size_t)15;
+  const size_t f = ((size_t)ecap * 6 + 15) & ~(size_t)15;
+  return h + f + (size_t)pcap * 32 + (size_t)lcap * sizeof(PoseEdge);
+}
 
 // debug (ORBPL_POSE_PROFILE): accumulated wall-clock ticks (100 MHz) of
 // stream 0's pose: [0] edges, [1] linearize+reduce, [2] solve+exp,
@@ -1063,7 +1321,7 @@ __device__ void se3_from_T(const float* T, SE3d& s) {
 // spills); launch_pose picks both from the streams per CU
 template <int kPoseThreads>
 __device__ __forceinline__ void pose_stream(const TrackConsts& tc, const PoseArgs& a,
-                                            PoseShared& S, const int s) {
+                                            PoseShared& S, PoseLds V, const int s) {
   constexpr int kPoseWaves = kPoseThreads / 64;
   const int t = threadIdx.x;
   // TrackWithMotionModel returns before optimising when no last frame exists
@@ -1095,7 +1353,11 @@ __device__ __forceinline__ void pose_stream(const TrackConsts& tc, const PoseArg
   const int n = a.n[s];
   uint8_t* outl = a.outlier + cb;
   // ---- edges (Optimizer.cc:2190-2283, 2285-2352), compacted in index order ----
-  PoseEdge* E = a.edges + (long long)s * kPoseMaxEdges;
+  {
+    char* G = reinterpret_cast<char*>(a.edges) + (long long)s * kPoseMaxEdges * (32 + sizeof(PoseEdge));
+    V.pg = reinterpret_cast<float4*>(G);
+    V.lg = reinterpret_cast<PoseEdge*>(G + kPoseMaxEdges * 32);
+  }
   const int wave = t >> 6, lane = t & 63;
   int npts = 0;
   for (int base = 0; base < n; base += kPoseThreads) {
@@ -1121,82 +1383,79 @@ __device__ __forceinline__ void pose_stream(const TrackConsts& tc, const PoseArg
       tot += S.wsum[w];
     }
     const int k = off + incl - flag;
-    if (flag && k < kPoseMaxEdges) {
-      PoseEdge e;
+    if (flag && k < a.ecap) {
       const KeyPointD kp = a.kps_un[cb + i];
       const float ur = a.uright[cb + i];
-      e.kind = ur < 0 ? 0 : 1;
-      e.idx = i;
-      e.obs[0] = kp.x;
-      e.obs[1] = kp.y;
-      e.obs[2] = ur;
-      e.obs[3] = 0;
-      e.info = tc.inv_sigma2[kp.octave];
-      const float* X = a.mp_xyz + (cb + j) * 3;
-      e.X[0] = X[0]; e.X[1] = X[1]; e.X[2] = X[2];
-      e.X[3] = e.X[4] = e.X[5] = 0;
-      e.pad = 0;
-      E[k] = e;
-      S.level[k] = 0;
-      S.out_flag[k] = 0;
+      store_point(V, k, kp.x, kp.y, ur, tc.inv_sigma2[kp.octave], a.mp_xyz + (cb + j) * 3, i);
+      V.level[k] = 0;
+      V.out_flag[k] = 0;
       outl[i] = 0;
     }
     npts += tot;
     __syncthreads();
   }
-  npts = min(npts, kPoseMaxEdges);
+  npts = min(npts, a.ecap);
+  V.npts = npts;
+  // line edges in line index order: a block-wide prefix over the matched lines
+  // (Optimizer.cc:2285-2352)
   int nlines = 0;
-  if (t == 0 && a.t_kl_un) {
-    // tracker mode: edges for the current lines matched to last-frame map lines
-    int ne = npts;
+  {
+    const bool trk = a.t_kl_un != nullptr;
     const long long lb = (long long)s * a.lpitch;
-    const int nlc = a.t_nl[s];
-    for (int i = 0; i < nlc; i++) {
-      const int m = a.t_lmatch[lb + i];
-      if (m < 0) continue;
-      if (ne >= kPoseMaxEdges) break;
-      if (i < n) outl[i] = 0;  // reference writes mvbOutlier here (Optimizer.cc:2308)
-      const orbpl_keyline kl = a.t_kl_un[lb + i];
-      PoseEdge e;
-      e.kind = 2;
-      e.idx = i;
-      e.obs[0] = kl.startPointX;
-      e.obs[1] = kl.startPointY;
-      e.obs[2] = kl.endPointX;
-      e.obs[3] = kl.endPointY;
-      e.info = tc.inv_sigma2[kl.octave];
-      const float* X = a.t_ml_xyz + (lb + m) * 6;
-      for (int q = 0; q < 6; q++) e.X[q] = X[q];
-      e.pad = 0;
-      E[ne] = e;
-      S.level[ne] = 0;
-      S.out_flag[ne] = a.t_loutlier[lb + i];
-      ne++;
-      nlines++;
+    const int nlc = trk ? a.t_nl[s] : a.nl;
+    for (int base = 0; base < nlc; base += kPoseThreads) {
+      const int i = base + t;
+      int m = -1;
+      if (i < nlc) m = trk ? a.t_lmatch[lb + i] : (a.has_ml[i] ? i : -1);
+      const int flag = m >= 0 ? 1 : 0;
+      int incl = flag;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        int u = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += u;
+      }
+      if (lane == 63) S.wsum[wave] = incl;
+      __syncthreads();
+      int off = npts + nlines;
+      int tot = 0;
+      for (int w = 0; w < kPoseWaves; w++) {
+        if (w < wave) off += S.wsum[w];
+        tot += S.wsum[w];
+      }
+      const int k = off + incl - flag;
+      if (flag && k < a.ecap) {
+        if (i < n) outl[i] = 0;  // reference writes mvbOutlier here (Optimizer.cc:2308)
+        PoseEdge e;
+        e.kind = 2;
+        e.idx = i;
+        if (trk) {
+          const orbpl_keyline kl = a.t_kl_un[lb + i];
+          e.obs[0] = kl.startPointX;
+          e.obs[1] = kl.startPointY;
+          e.obs[2] = kl.endPointX;
+          e.obs[3] = kl.endPointY;
+          e.info = tc.inv_sigma2[kl.octave];
+          const float* X = a.t_ml_xyz + (lb + m) * 6;
+          for (int q = 0; q < 6; q++) e.X[q] = X[q];
+          V.out_flag[k] = a.t_loutlier[lb + i];
+        } else {
+          for (int q = 0; q < 4; q++) e.obs[q] = a.kl_obs[4 * i + q];
+          e.info = tc.inv_sigma2[a.kl_octave[i]];
+          for (int q = 0; q < 6; q++) e.X[q] = a.ml_xyz[6 * i + q];
+          V.out_flag[k] = a.line_outlier[i];
+        }
+        e.pad = 0;
+        (k - npts < V.lcap ? V.lrec : V.lg)[k - npts] = e;
+        V.level[k] = 0;
+      }
+      nlines += tot;
+      __syncthreads();
     }
-    S.misc[0] = ne;
-    S.misc[2] = nlines;
-  } else if (t == 0) {
-    int ne = npts;
-    for (int i = 0; i < a.nl; i++) {
-      if (!a.has_ml[i]) continue;
-      if (ne >= kPoseMaxEdges) break;
-      if (i < n) outl[i] = 0;  // reference writes mvbOutlier here (Optimizer.cc:2308)
-      PoseEdge e;
-      e.kind = 2;
-      e.idx = i;
-      for (int q = 0; q < 4; q++) e.obs[q] = a.kl_obs[4 * i + q];
-      e.info = tc.inv_sigma2[a.kl_octave[i]];
-      for (int q = 0; q < 6; q++) e.X[q] = a.ml_xyz[6 * i + q];
-      e.pad = 0;
-      E[ne] = e;
-      S.level[ne] = 0;
-      S.out_flag[ne] = a.line_outlier[i];
-      ne++;
-      nlines++;
+    nlines = min(nlines, a.ecap - npts);
+    if (t == 0) {
+      S.misc[0] = npts + nlines;
+      S.misc[2] = nlines;
     }
-    S.misc[0] = ne;
-    S.misc[2] = nlines;
   }
   __syncthreads();
   lap(0);
@@ -1221,7 +1480,7 @@ __device__ __forceinline__ void pose_stream(const TrackConsts& tc, const PoseArg
     uni(T);
     // ---- optimizer.optimize(10) ----
     int nact = 0;
-    for (int k = t; k < ne; k += kPoseThreads) nact += S.level[k] == 0;
+    for (int k = t; k < ne; k += kPoseThreads) nact += V.level[k] == 0;
     {
       double v = nact;
       block_sum<1, kPoseWaves>(&v, S);
@@ -1238,13 +1497,36 @@ __device__ __forceinline__ void pose_stream(const TrackConsts& tc, const PoseArg
         uni(R);
         double acc[28];
         for (int k = 0; k < 28; k++) acc[k] = 0;
-        // the next edge's load is issued before this edge's arithmetic
-        PoseEdge e_next;
-        if (t < ne) e_next = E[t];
-        for (int k = t; k < ne; k += kPoseThreads) {
-          const PoseEdge e = e_next;
-          if (k + kPoseThreads < ne) e_next = E[k + kPoseThreads];
-          if (S.level[k]) continue;
+        int k = t;
+#if defined(ORBPL_POSE_ROWS)
+        for (; k < npts; k += kPoseThreads) {
+          const PoseEdge e = fetch_point(V, k);
+          const bool on = V.level[k] == 0;
+          const double x2 = point_lin_rows<0>(e, c, T, robust, deltaMono, dsqrMono, deltaStereo,
+                                              dsqrStereo, on, acc);
+          if (on) V.chi2[k] = (float)x2;
+        }
+#elif !defined(ORBPL_POSE_LIN1)
+        // point edges two at a time (branch-free, this thread's edge order kept)
+        for (; k + kPoseThreads < npts; k += 2 * kPoseThreads) {
+          PointLin o0, o1;
+          const PoseEdge e0 = fetch_point(V, k), e1 = fetch_point(V, k + kPoseThreads);
+          const bool on0 = V.level[k] == 0, on1 = V.level[k + kPoseThreads] == 0;
+          point_lin(e0, c, T, robust, deltaMono, dsqrMono, deltaStereo, dsqrStereo, o0);
+          point_lin(e1, c, T, robust, deltaMono, dsqrMono, deltaStereo, dsqrStereo, o1);
+          if (on0) {
+            V.chi2[k] = (float)o0.x2;
+            accumulate_lin(o0, acc);
+          }
+          if (on1) {
+            V.chi2[k + kPoseThreads] = (float)o1.x2;
+            accumulate_lin(o1, acc);
+          }
+        }
+#endif
+        for (; k < ne; k += kPoseThreads) {
+          const PoseEdge e = fetch_edge(V, k);
+          if (V.level[k]) continue;
           double err[3], J[3][6];
           edge_error(e, c, T, R, err);
           // rows beyond the edge's dimension are zero (err[2] = 0 and J row 2
@@ -1252,7 +1534,7 @@ __device__ __forceinline__ void pose_stream(const TrackConsts& tc, const PoseArg
           double x2 = err[0] * (double)e.info * err[0];
           x2 += err[1] * (double)e.info * err[1];
           x2 += err[2] * (double)e.info * err[2];
-          S.chi2[k] = (float)x2;
+          V.chi2[k] = (float)x2;
           double w = 1.0, r0 = x2;
           if (robust) {
             const bool isMono = e.kind == 0;
@@ -1323,18 +1605,36 @@ __device__ __forceinline__ void pose_stream(const TrackConsts& tc, const PoseArg
           quat_to_R(T.q, R2);
           uni(R2);
           double tc2 = 0;
-          PoseEdge e_next;
-          if (t < ne) e_next = E[t];
-          for (int k = t; k < ne; k += kPoseThreads) {
-            const PoseEdge e = e_next;
-            if (k + kPoseThreads < ne) e_next = E[k + kPoseThreads];
-            if (S.level[k]) continue;
+          // point edges four at a time (this thread's edge order kept)
+          int k = t;
+          for (; k + 3 * kPoseThreads < npts; k += 4 * kPoseThreads) {
+            PoseEdge e4[4];
+            bool on[4];
+            double x4[4], r4[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+              e4[u] = fetch_point(V, k + u * kPoseThreads);
+              on[u] = V.level[k + u * kPoseThreads] == 0;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+              x4[u] = point_chi2(e4[u], c, T, robust, deltaMono, dsqrMono, deltaStereo, dsqrStereo, &r4[u]);
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+              if (on[u]) {
+                V.chi2[k + u * kPoseThreads] = (float)x4[u];
+                tc2 += r4[u];
+              }
+          }
+          for (; k < ne; k += kPoseThreads) {
+            const PoseEdge e = fetch_edge(V, k);
+            if (V.level[k]) continue;
             double err[3];
             edge_error(e, c, T, R2, err);
-            const int dim = e.kind == 1 ? 3 : 2;
-            double x2 = 0;
-            for (int d = 0; d < dim; d++) x2 += err[d] * (double)e.info * err[d];
-            S.chi2[k] = (float)x2;
+            double x2 = err[0] * (double)e.info * err[0];
+            x2 += err[1] * (double)e.info * err[1];
+            if (e.kind == 1) x2 += err[2] * (double)e.info * err[2];
+            V.chi2[k] = (float)x2;
             double r0 = x2, w;
             if (robust) {
               const bool isMono = e.kind == 0;
@@ -1379,28 +1679,53 @@ __device__ __forceinline__ void pose_stream(const TrackConsts& tc, const PoseArg
     quat_to_R(T.q, R);
     uni(R);
     int nbad = 0;
-    for (int k = t; k < ne; k += kPoseThreads) {
-      const PoseEdge e = E[k];
-      const bool was_out = e.kind == 2 ? (S.out_flag[k] != 0) : (outl[e.idx] != 0);
-      float chi2 = S.chi2[k];
+    // point edges four at a time; an edge's outlier flag is kept in out_flag
+    // (for points it mirrors mvbOutlier[idx], written here only)
+    int k = t;
+    for (; k + 3 * kPoseThreads < npts; k += 4 * kPoseThreads) {
+      PoseEdge e4[4];
+      double x4[4], r4[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) e4[u] = fetch_point(V, k + u * kPoseThreads);
+#pragma unroll
+      for (int u = 0; u < 4; u++)
+        x4[u] = point_chi2(e4[u], c, T, false, deltaMono, dsqrMono, deltaStereo, dsqrStereo, &r4[u]);
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int kk = k + u * kPoseThreads;
+        float chi2 = V.chi2[kk];
+        if (V.out_flag[kk]) {
+          chi2 = (float)x4[u];
+          V.chi2[kk] = chi2;
+        }
+        const bool bad = chi2 > (e4[u].kind == 0 ? 5.991f : 7.815f);
+        V.out_flag[kk] = bad;
+        outl[e4[u].idx] = bad;
+        nbad += bad;
+        V.level[kk] = bad ? 1 : 0;
+      }
+    }
+    for (; k < ne; k += kPoseThreads) {
+      const PoseEdge e = fetch_edge(V, k);
+      const bool was_out = V.out_flag[k] != 0;
+      float chi2 = V.chi2[k];
       if (was_out) {
         double err[3];
         edge_error(e, c, T, R, err);
-        const int dim = e.kind == 1 ? 3 : 2;
-        double x2 = 0;
-        for (int d = 0; d < dim; d++) x2 += err[d] * (double)e.info * err[d];
+        double x2 = err[0] * (double)e.info * err[0];
+        x2 += err[1] * (double)e.info * err[1];
+        if (e.kind == 1) x2 += err[2] * (double)e.info * err[2];
         chi2 = (float)x2;
-        S.chi2[k] = chi2;
+        V.chi2[k] = chi2;
       }
       const float th = e.kind == 0 ? 5.991f : (e.kind == 1 ? 7.815f : 2 * 7.815f);
       const bool bad = chi2 > th;
-      if (e.kind == 2) {
-        S.out_flag[k] = bad;
-      } else {
+      V.out_flag[k] = bad;
+      if (e.kind != 2) {
         outl[e.idx] = bad;
         nbad += bad;
       }
-      S.level[k] = bad ? 1 : 0;
+      V.level[k] = bad ? 1 : 0;
     }
     {
       double v = nbad;
@@ -1427,10 +1752,10 @@ __device__ __forceinline__ void pose_stream(const TrackConsts& tc, const PoseArg
     __syncthreads();
   }
   for (int k = t; k < ne; k += kPoseThreads) {
-    const PoseEdge e = E[k];
+    const PoseEdge e = fetch_edge(V, k);
     if (e.kind == 2) {
-      if (a.t_kl_un) a.t_loutlier[(long long)s * a.lpitch + e.idx] = S.out_flag[k];
-      else a.line_outlier[e.idx] = S.out_flag[k];
+      if (a.t_kl_un) a.t_loutlier[(long long)s * a.lpitch + e.idx] = V.out_flag[k];
+      else a.line_outlier[e.idx] = V.out_flag[k];
     }
   }
   if (t == 0) a.ninliers[(long long)s * a.nm_stride] = npts - nBadOut;
@@ -1445,16 +1770,28 @@ __device__ __forceinline__ void pose_stream(const TrackConsts& tc, const PoseArg
 // when no stream has work)
 template <int kPoseThreads, int kMinWaves>
 __global__ void __launch_bounds__(kPoseThreads, kMinWaves) k_pose(TrackConsts tc, PoseArgs a) {
-  extern __shared__ char smem_raw[];
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   PoseShared& S = *reinterpret_cast<PoseShared*>(smem_raw);
+  PoseLds V;
+  {
+    char* q = smem_raw + ((sizeof(PoseShared) + 15) & ~(size_t)15);
+    V.chi2 = reinterpret_cast<float*>(q);
+    V.level = reinterpret_cast<uint8_t*>(q + (size_t)a.ecap * 4);
+    V.out_flag = V.level + a.ecap;
+    q += ((size_t)a.ecap * 6 + 15) & ~(size_t)15;
+    V.prec = reinterpret_cast<float4*>(q);
+    V.lrec = reinterpret_cast<PoseEdge*>(q + (size_t)a.pcap * 32);
+    V.pcap = a.pcap;
+    V.lcap = a.lcap;
+  }
   if (a.list) {
     const int n = *a.list_n;
     for (int b = blockIdx.x; b < n; b += gridDim.x) {
-      pose_stream<kPoseThreads>(tc, a, S, a.list[b]);
+      pose_stream<kPoseThreads>(tc, a, S, V, a.list[b]);
       __syncthreads();
     }
   } else {
-    pose_stream<kPoseThreads>(tc, a, S, blockIdx.x);
+    pose_stream<kPoseThreads>(tc, a, S, V, blockIdx.x);
   }
 }
 
@@ -1726,11 +2063,32 @@ void launch_pose(const TrackConsts& c, const PoseLaunch& p, int nstreams, hipStr
   static const char* cfg = getenv("ORBPL_POSE_CFG");
   if (cfg) sscanf(cfg, "%d,%d", &nt, &mw);
   const int grid = p.list ? (nstreams < kListGrid ? nstreams : kListGrid) : nstreams;
-#define ORBPL_POSE_LAUNCH(NT, MW)                                                            \
-  if (nt == NT && mw == MW) {                                                                 \
-    set_smem_attr((const void*)k_pose<NT, MW>, sizeof(PoseShared));                           \
-    hipLaunchKernelGGL((k_pose<NT, MW>), dim3(grid), dim3(NT), sizeof(PoseShared), s, c, a); \
-    return;                                                                                   \
+  // LDS: the CU's 160 KiB shared by the workgroups it holds at once (by the
+  // grid and the one-wave-per-SIMD register budget); within a workgroup's
+  // share every edge's chi2 / flags, the line records, then as many point
+  // records as fit. ORBPL_POSE_LDS=bytes overrides the share (A/B runs).
+  const int nlmax = p.t_kl_un ? p.lpitch : p.nl;
+  a.ecap = std::min(kPoseMaxEdges, p.kp_pitch + nlmax);
+  {
+    const int maxb = std::max(1, 4 * mw / std::max(1, nt / 64));
+    const int bpc = std::min(maxb, std::max(1, (grid + cus - 1) / cus));
+    // (capped at 16 KiB: in the pipelined tracker the pose workgroups are
+    // placed beside extraction workgroups, and a larger share delays them
+    // more than the on-chip records save: 40 KiB -4.5 %, 0 -2.5 % end to end)
+    long budget = std::min(163840L / bpc, 16384L);
+    static const char* lds_env = getenv("ORBPL_POSE_LDS");
+    if (lds_env) budget = std::min(163840L, atol(lds_env));
+    const long fixed = (long)pose_lds_bytes(a.ecap, 0, 0);
+    a.lcap = fixed + (long)nlmax * (long)sizeof(PoseEdge) <= budget ? nlmax : 0;
+    const long room = budget - fixed - (long)a.lcap * (long)sizeof(PoseEdge);
+    a.pcap = (int)std::max(0L, std::min((long)std::min(p.kp_pitch, a.ecap), room / 32));
+  }
+  const size_t smem = pose_lds_bytes(a.ecap, a.pcap, a.lcap);
+#define ORBPL_POSE_LAUNCH(NT, MW)                                                 \
+  if (nt == NT && mw == MW) {                                                      \
+    set_smem_attr((const void*)k_pose<NT, MW>, 163840);                           \
+    hipLaunchKernelGGL((k_pose<NT, MW>), dim3(grid), dim3(NT), smem, s, c, a);     \
+    return;                                                                        \
   }
   ORBPL_POSE_LAUNCH(256, 1)
   ORBPL_POSE_LAUNCH(128, 1)
@@ -1739,8 +2097,8 @@ void launch_pose(const TrackConsts& c, const PoseLaunch& p, int nstreams, hipStr
   ORBPL_POSE_LAUNCH(128, 2)
   ORBPL_POSE_LAUNCH(64, 2)
 #undef ORBPL_POSE_LAUNCH
-  set_smem_attr((const void*)k_pose<64, 1>, sizeof(PoseShared));
-  hipLaunchKernelGGL((k_pose<64, 1>), dim3(grid), dim3(64), sizeof(PoseShared), s, c, a);
+  set_smem_attr((const void*)k_pose<64, 1>, 163840);
+  hipLaunchKernelGGL((k_pose<64, 1>), dim3(grid), dim3(64), smem, s, c, a);
 }
 
 void launch_finish(const TrackConsts& c, StreamState* st, const int* n, int kp_pitch,
@@ -1754,5 +2112,5 @@ void launch_finish(const TrackConsts& c, StreamState* st, const int* n, int kp_p
 }  // namespace orbpl
 
 namespace orbpl {
-size_t pose_edge_bytes() { return sizeof(PoseEdge); }
+size_t pose_edge_bytes() { return 32 + sizeof(PoseEdge); }
 }  // namespace orbpl
