@@ -705,6 +705,123 @@ __device__ __forceinline__ void add_angle(float d, float& sumdx, float& sumdy) {
 }
 #endif
 
+// ORBPL_GROW_LEAN: the grow step as straight-line code (below); 0 = the
+// earlier step with the branchy aligned test (A/B build override).
+#ifndef ORBPL_GROW_LEAN
+#define ORBPL_GROW_LEAN 1
+#endif
+
+// cv::fastAtan2 with one division: both branches of fast_atan2_deg divide the
+// smaller of |x|, |y| by the larger + eps and evaluate the same polynomial, so
+// selecting the operands first gives the same float operations in the same
+// order (bit-identical) without executing both branches when lanes diverge.
+__device__ __forceinline__ float fast_atan2_deg_1div(float y, float x) {
+  const float k180pi = (float)(180.0 / 3.14159265358979323846);
+  const float p1 = 0.9997878412794807f * k180pi;
+  const float p3 = -0.3258083974640975f * k180pi;
+  const float p5 = 0.1555786518463281f * k180pi;
+  const float p7 = -0.04432655554792128f * k180pi;
+  const float eps = (float)2.220446049250313080847e-16;
+  const float ax = f_abs(x), ay = f_abs(y);
+  const bool ge = ax >= ay;
+  const float c = (ge ? ay : ax) / ((ge ? ax : ay) + eps);
+  const float c2 = c * c;
+  const float pc = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+  float a = ge ? pc : 90.f - pc;
+  a = x < 0 ? 180.f - a : a;
+  a = y < 0 ? 360.f - a : a;
+  return a;
+}
+
+#if ORBPL_GROW_LEAN && ORBPL_GROW_CS && ORBPL_SD_PAIRED
+// region_grow for one lane (same result as the step below). Per step the 8
+// neighbour addresses come from 3 row and 3 column terms of the tile index;
+// the neighbour's flags (in image, not USED, not already in this region,
+// defined) are computed for all 8 before the in-order walk, so the walk per
+// position is the aligned test (sub, abs, compare, a conditional 2 pi fold)
+// and the add body under one branch. The centre (the point being expanded)
+// is skipped: its stamp is this grow's own claim unless an earlier seed of
+// the round claimed it, and then the claim re-check after the round flags the
+// lane anyway (a conflict ends the lane's speculation whichever step finds
+// it).
+__device__ __forceinline__ int lane_grow(const Frame& F, uint64_t* sd, LaneBuf buf, int cap, int sx,
+                                         int sy, double& reg_angle, double prec, uint32_t myval) {
+  const uint32_t mytag = myval >> 1;
+  const int sw = F.sw, sh = F.sh, tw = F.tw;
+  const int si = lsd_sd_index(sx, sy, tw);
+  if (cap < 1) return kSpecOverflow;
+  const uint64_t v0 = ld_sd(sd + si);
+  if (((uint32_t)(v0 >> 32) >> 1) < mytag) return kSpecConflict;
+  atomicMin(reinterpret_cast<unsigned long long*>(sd + si),
+            ((unsigned long long)myval << 32) | (uint32_t)v0);
+  uint4 cur = make_uint4((uint32_t)sx | ((uint32_t)sy << 16), (uint32_t)v0, 0u, 0u);
+  buf[0] = cur;
+  reg_angle = deg2ang(entry_deg(cur));
+  double s0, c0;
+  lsdm::sincos_(reg_angle, &s0, &c0);
+  float sumdx = (float)c0;
+  float sumdy = (float)s0;
+  const double k3pi2 = (3 * kPi) / 2, k2pi = 2 * kPi;
+  int n = 1;
+  for (int i = 0; i < n; i++) {
+    const int x = pt_x(cur), y = pt_y(cur);
+    const int n_start = n;
+    const uint4 pref = buf[min(i + 1, n_start - 1)];
+    // tile index = row term + column term (disjoint bit fields), x2 for the
+    // paired 16-byte entries
+    int rterm[3], cterm[3];
+    bool rin[3], cin[3];
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+      const int yy = y + d - 1, xx = x + d - 1;
+      rin[d] = yy >= 0 && yy < sh;
+      cin[d] = xx >= 0 && xx < sw;
+      const int cy = min(max(yy, 0), sh - 1), cx = min(max(xx, 0), sw - 1);
+      rterm[d] = (((cy >> 2) * tw) << 5) | ((cy & 3) << 3);
+      cterm[d] = ((cx >> 2) << 5) | ((cx & 3) << 1);
+    }
+    uint4 w[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+      if (k == 4) continue;
+      w[k] = *reinterpret_cast<const uint4*>(sd + (rterm[k / 3] + cterm[k % 3]));
+    }
+    unsigned ok = 0;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+      if (k == 4) continue;
+      // bitwise, not short-circuit: no branch per neighbour
+      const unsigned f = (unsigned)(rin[k / 3] & cin[k % 3]) & (unsigned)(w[k].y != 0u) &
+                         (unsigned)(w[k].y != myval) & (unsigned)(__uint_as_float(w[k].x) >= 0.f);
+      ok |= f << k;
+    }
+    uint4 first_add = cur;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+      if (k == 4) continue;
+      // aligned_deg(d, reg_angle, prec) for a defined d
+      double nt = fabs(reg_angle - deg2ang(__uint_as_float(w[k].x)));
+      nt = nt > k3pi2 ? fabs(nt - k2pi) : nt;
+      if (((ok >> k) & 1u) && nt <= prec) {
+        if ((w[k].y >> 1) < mytag) return kSpecConflict;   // an earlier seed's pixel
+        const int id = rterm[k / 3] + cterm[k % 3];
+        atomicMin(reinterpret_cast<unsigned long long*>(sd + id),
+                  ((unsigned long long)myval << 32) | w[k].x);
+        if (n >= cap) return kSpecOverflow;
+        const int xx = x + (k % 3) - 1, yy = y + (k / 3) - 1;
+        const uint4 e = make_uint4((uint32_t)xx | ((uint32_t)yy << 16), w[k].x, 0u, 0u);
+        if (n == n_start) first_add = e;
+        buf[n++] = e;
+        sumdx += __uint_as_float(w[k].z);   // add_angle(d) terms
+        sumdy += __uint_as_float(w[k].w);
+        reg_angle = (double)fast_atan2_deg_1div(sumdy, sumdx) * kDegToRad;
+      }
+    }
+    cur = (i + 1 < n_start) ? pref : first_add;
+  }
+  return n;
+}
+#else
 __device__ __forceinline__ int lane_grow(const Frame& F, uint64_t* sd, LaneBuf buf, int cap, int sx,
                                          int sy, double& reg_angle, double prec, uint32_t myval) {
   const uint32_t mytag = myval >> 1;
@@ -830,6 +947,7 @@ __device__ __forceinline__ int lane_grow(const Frame& F, uint64_t* sd, LaneBuf b
   }
   return n;
 }
+#endif
 
 // region2rect over a lane's list (same operation order as region2rect).
 // With q given, the first pass also stores the weights modgrad = sqrt(q / 4)
