@@ -955,10 +955,12 @@ __device__ __forceinline__ int lane_grow(const Frame& F, uint64_t* sd, LaneBuf b
 // it loads give the q addresses, so the fill costs no pass of its own. Every
 // pass reads the list in batches of unconditional loads (indices clamped to
 // n - 1, contributions masked) so the loads overlap.
+__device__ __forceinline__ void lane_rect_tail(LaneBuf buf, int n, double x, double y, double sum,
+                                               double reg_angle, double prec, double p, Rect& rec);
 __device__ __forceinline__ void lane_rect(LaneBuf buf, int n, double reg_angle, double prec,
                                           double p, Rect& rec, const int* __restrict__ q = nullptr,
                                           int sw = 0) {
-  constexpr int kB = 8, kB3 = 16;
+  constexpr int kB = 8;
   double x = 0, y = 0, sum = 0;
   for (int i0 = 0; i0 < n; i0 += kB) {
     uint32_t pt[kB];
@@ -995,6 +997,13 @@ __device__ __forceinline__ void lane_rect(LaneBuf buf, int n, double reg_angle, 
       }
     }
   }
+  lane_rect_tail(buf, n, x, y, sum, reg_angle, prec, p, rec);
+}
+
+// region2rect after the weighted centroid sums (x, y, sum in list order)
+__device__ __forceinline__ void lane_rect_tail(LaneBuf buf, int n, double x, double y, double sum,
+                                               double reg_angle, double prec, double p, Rect& rec) {
+  constexpr int kB = 8, kB3 = 16;
   x /= sum;
   y /= sum;
   double Ixx = 0.0, Iyy = 0.0, Ixy = 0.0;
@@ -1065,11 +1074,15 @@ __device__ __forceinline__ void lane_rect(LaneBuf buf, int n, double reg_angle, 
 // far points stay in [nn, n) (their order is immaterial: the claim re-check
 // reads the touched prefix as a set), and only their point words: the scan
 // tests only point words, a near point moved forward carries all four.
-__device__ __forceinline__ bool lane_far(uint32_t pt, double xc, double yc, double radSq) {
-  return distSq(xc, yc, double(pt & 0xFFFF), double(pt >> 16)) > radSq;
+// distSq of two pixel positions is an integer below 2^21, exact in double
+// whichever way it is summed: the integer form gives the same comparison.
+__device__ __forceinline__ bool lane_far(uint32_t pt, int xc, int yc, double radSq) {
+  const int dx = (int)(pt & 0xFFFF) - xc, dy = (int)(pt >> 16) - yc;
+  return (double)(dx * dx + dy * dy) > radSq;
 }
-__device__ __forceinline__ int lane_reduce_pass(LaneBuf g1, int n, double xc, double yc,
-                                                double radSq) {
+__device__ __forceinline__ int lane_reduce_pass(LaneBuf g1, int n, int xc, int yc,
+                                                double radSq, double& cx, double& cy,
+                                                double& csum) {
   constexpr int kB = 8, kBb = 4;
   int nn = 0;
   for (int i0 = 0; i0 < n; i0 += kB) {
@@ -1080,38 +1093,68 @@ __device__ __forceinline__ int lane_reduce_pass(LaneBuf g1, int n, double xc, do
     for (int u = 0; u < kB; u++) nn += (i0 + u < n && !lane_far(e[u], xc, yc, radSq)) ? 1 : 0;
   }
   if (nn == n) return n;
-  uint32_t fw[kB];
+  // the merge visits the final list in order, so it also sums region2rect's
+  // weighted centroid terms (its first pass, same order and operations)
   uint4 bw[kBb];
-  int fcnt = 0, bcnt = 0, bpos = n - 1;
-  for (int fpos = 0; fpos < nn; fpos++) {
-    if (fcnt == 0) {
+  int bcnt = 0, bpos = n - 1;
+  double x = 0, y = 0, sum = 0;
+  for (int f0 = 0; f0 < nn; f0 += kB) {
+    uint4 fw[kB];
 #pragma unroll
-      for (int u = 0; u < kB; u++) fw[u] = g1.pt(min(fpos + u, nn - 1));
-      fcnt = kB;
-    }
-    const uint32_t e = fw[0];
+    for (int u = 0; u < kB; u++) fw[u] = g1[min(f0 + u, nn - 1)];
 #pragma unroll
-    for (int u = 0; u < kB - 1; u++) fw[u] = fw[u + 1];
-    fcnt--;
-    if (!lane_far(e, xc, yc, radSq)) continue;
-    uint4 b;
-    do {   // [nn, n) holds exactly as many near points as [0, nn) far ones
-      if (bcnt == 0) {
+    for (int u = 0; u < kB; u++) {
+      if (f0 + u >= nn) break;
+      uint4 e = fw[u];
+      if (lane_far(e.x, xc, yc, radSq)) {
+        uint4 b;
+        do {   // [nn, n) holds exactly as many near points as [0, nn) far ones
+          if (bcnt == 0) {
 #pragma unroll
-        for (int u = 0; u < kBb; u++) bw[u] = g1[max(bpos - u, nn)];
-        bcnt = kBb;
+            for (int v = 0; v < kBb; v++) bw[v] = g1[max(bpos - v, nn)];
+            bcnt = kBb;
+          }
+          b = bw[0];
+#pragma unroll
+          for (int v = 0; v < kBb - 1; v++) bw[v] = bw[v + 1];
+          bcnt--;
+          bpos--;
+        } while (lane_far(b.x, xc, yc, radSq));
+        g1[f0 + u] = b;
+        g1.set_pt(bpos + 1, e.x);
+        e = b;
       }
-      b = bw[0];
-#pragma unroll
-      for (int u = 0; u < kBb - 1; u++) bw[u] = bw[u + 1];
-      bcnt--;
-      bpos--;
-    } while (lane_far(b.x, xc, yc, radSq));
-    g1[fpos] = b;
-    g1.set_pt(bpos + 1, e);
+      const double weight = entry_w(e);
+      x += double(pt_x(e)) * weight;
+      y += double(pt_y(e)) * weight;
+      sum += weight;
+    }
   }
+  cx = x;
+  cy = y;
+  csum = sum;
   return nn;
 }
+
+// Profiling build (-DORBPL_FIT_PROF): wall time of the fit's phases per
+// round, as seen by the lanes in them, reduced to the wave maximum per round
+// and printed for frame 0 (0 first rect, 1 refine statistics, 2 second grow,
+// 3 second rect, 4 reduce_region_radius loop).
+struct FitProf {
+#ifdef ORBPL_FIT_PROF
+  long long d[5] = {0, 0, 0, 0, 0};
+  long long last = 0;
+  __device__ __forceinline__ void start() { last = clock64(); }
+  __device__ __forceinline__ void lap(int k) {
+    const long long c = clock64();
+    d[k] += c - last;
+    last = c;
+  }
+#else
+  __device__ __forceinline__ void start() {}
+  __device__ __forceinline__ void lap(int) {}
+#endif
+};
 
 // refine + reduce_region_radius for a lane. The region [0, n) came from the
 // first grow; a second grow is appended after it. Returns the status; off /
@@ -1119,7 +1162,7 @@ __device__ __forceinline__ int lane_reduce_pass(LaneBuf g1, int n, double xc, do
 __device__ __forceinline__ int lane_refine(const Frame& F, uint64_t* sd, LaneBuf buf, int n,
                                            double reg_angle,
                                            double prec, double p, Rect& rec, uint32_t myval1,
-                                           int& off, int& len, int& touched) {
+                                           int& off, int& len, int& touched, FitProf& fp) {
   const double density_th = 0.7;
   double density = double(n) / (dist(rec.x1, rec.y1, rec.x2, rec.y2) * rec.width);
   off = 0;
@@ -1150,7 +1193,9 @@ __device__ __forceinline__ int lane_refine(const Frame& F, uint64_t* sd, LaneBuf
   const double tau =
       2.0 * sqrt((s_sum - 2.0 * mean_angle * sum) / double(cnt) + mean_angle * mean_angle);
   LaneBuf g1 = buf + n;
+  fp.lap(1);
   int n1 = lane_grow(F, sd, g1, kLaneCap - n, x0, y0, reg_angle, tau, myval1);
+  fp.lap(2);
   if (n1 < 0) return n1;
   off = n;
   len = n1;
@@ -1158,6 +1203,7 @@ __device__ __forceinline__ int lane_refine(const Frame& F, uint64_t* sd, LaneBuf
   if (n1 < 2) return kSpecFail;
   lane_rect(g1, n1, reg_angle, prec, p, rec, F.q, F.sw);
   density = double(n1) / (dist(rec.x1, rec.y1, rec.x2, rec.y2) * rec.width);
+  fp.lap(3);
   if (density >= density_th) return kSpecCand;
   // reduce_region_radius
   const double radSq1 = distSq(xc, yc, rec.x1, rec.y1);
@@ -1165,12 +1211,18 @@ __device__ __forceinline__ int lane_refine(const Frame& F, uint64_t* sd, LaneBuf
   double radSq = radSq1 > radSq2 ? radSq1 : radSq2;
   while (density < density_th) {
     radSq *= 0.75 * 0.75;
-    n1 = lane_reduce_pass(g1, n1, xc, yc, radSq);
+    const int n_prev = n1;
+    double cx, cy, csum;
+    n1 = lane_reduce_pass(g1, n1, x0, y0, radSq, cx, cy, csum);
     len = n1;
     if (n1 < 2) return kSpecFail;
-    lane_rect(g1, n1, reg_angle, prec, p, rec);
+    // nothing removed: the list is untouched, so region2rect would return the
+    // same rectangle and density
+    if (n1 == n_prev) continue;
+    lane_rect_tail(g1, n1, cx, cy, csum, reg_angle, prec, p, rec);
     density = double(n1) / (dist(rec.x1, rec.y1, rec.x2, rec.y2) * rec.width);
   }
+  fp.lap(4);
   return kSpecCand;
 }
 
@@ -1546,6 +1598,9 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
   const unsigned long long lt_mask = (1ull << lane) - 1ull;
   int nl = 0, pos = 0, it = 0;
   uint32_t round = 0;
+#ifdef ORBPL_FIT_PROF
+  long long fpr[5] = {0, 0, 0, 0, 0}, fpt[5] = {0, 0, 0, 0, 0};
+#endif
   long long n_spec = 0, n_rounds = 0, cyc_spec = 0, cyc_fit = 0, cyc_val = 0, max_steps = 0,
             n_coop = 0;
   const long long t_all = clock64();
@@ -1635,10 +1690,25 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
         len = n;
         touched = n;
       } else {
+        FitProf fp;
+        fp.start();
         lane_rect(buf, n, reg_angle, prec, p, rec, F.q, sw);
-        status = lane_refine(F, sd, buf, n, reg_angle, prec, p, rec, myval1, off, len, touched);
+        fp.lap(0);
+        status = lane_refine(F, sd, buf, n, reg_angle, prec, p, rec, myval1, off, len, touched, fp);
+#ifdef ORBPL_FIT_PROF
+        for (int k = 0; k < 5; k++) fpr[k] = fp.d[k];
+#endif
       }
     }
+#ifdef ORBPL_FIT_PROF
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+      long long v = fpr[k];
+      for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+      fpt[k] += v;
+      fpr[k] = 0;
+    }
+#endif
     wg_fence();
     block_sync<W>();
     const long long t2 = clock64();
@@ -1778,6 +1848,11 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
     sc.ncand[f] = min(nl, kLsdMaxCand);
     if (nl > kLsdMaxCand) atomicOr(sc.err + f, 8);
   }
+#ifdef ORBPL_FIT_PROF
+  if (f == 0 && t == 0)
+    printf("fitprof rect1 %lld stats %lld grow2 %lld rect2 %lld reduce %lld (grow %lld fit %lld val %lld)\n",
+           fpt[0], fpt[1], fpt[2], fpt[3], fpt[4], cyc_spec, cyc_fit, cyc_val);
+#endif
   if (sc.prof && t == 0) {
     long long* pr = sc.prof + f * 8;
     pr[0] = cyc_spec;
