@@ -29,6 +29,10 @@ using namespace orbpl;
 
 namespace {
 
+// streams from which the RGB-D lines tracker splits its LSD batch in two
+// offset halves (ORBPL_LSD_SPLIT overrides)
+constexpr int kLsdSplitMin = 1024;
+
 // RAII device buffer for the synchronous host-pointer entry points.
 struct DBuf {
   void* p = nullptr;
@@ -795,6 +799,16 @@ struct orbpl_tracker {
   lsdx_ctx* lx = nullptr;
   hipStream_t lstream = nullptr;
   hipEvent_t ev_in = nullptr;      // step start on `stream`
+  // split LSD (ORBPL_LSD_SPLIT, RGB-D lines at >= kLsdSplitMin streams): the
+  // first lsplit frames on lstream_a (context lx), the rest on lstream_b
+  // (lx2) started once the first half's pseudo-ordering sort is done, so the
+  // halves' chains run offset: one half's latency-bound sort and validation
+  // beside the other's VALU-bound seed loop. The line glue then runs on
+  // lstream after both.
+  int lsplit = 0;
+  lsdx_ctx* lx2 = nullptr;
+  hipStream_t lstream_a = nullptr, lstream_b = nullptr;
+  hipEvent_t ev_la_sort = nullptr, ev_la_done = nullptr, ev_lb_done = nullptr;
   // stereo (ORBPL_TRACK_STEREO): the right image's ORB extraction runs on the
   // right extractor's stream, concurrently with the left one; the batched
   // ComputeStereoMatches then fills depth / uRight on the extraction stream
@@ -1055,8 +1069,15 @@ int orbpl_tracker_destroy(orbpl_tracker* t) {
     if (t->in_done_l[k]) (void)hipEventDestroy(t->in_done_l[k]);
   }
   if (t->tstream) (void)hipStreamDestroy(t->tstream);
+  if (t->lstream_a) (void)hipStreamSynchronize(t->lstream_a);
+  if (t->lstream_b) (void)hipStreamSynchronize(t->lstream_b);
   if (t->lstream) (void)hipStreamDestroy(t->lstream);
+  if (t->lstream_a) (void)hipStreamDestroy(t->lstream_a);
+  if (t->lstream_b) (void)hipStreamDestroy(t->lstream_b);
+  for (hipEvent_t e : {t->ev_la_sort, t->ev_la_done, t->ev_lb_done})
+    if (e) (void)hipEventDestroy(e);
   if (t->lx) lsdx_destroy(t->lx);
+  if (t->lx2) lsdx_destroy(t->lx2);
   if (t->ex) orbx_destroy(t->ex);
   delete t;
   return ORBPL_OK;
@@ -1264,13 +1285,30 @@ int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam
     return hip_fail(hipErrorUnknown, "hipStreamCreate", __LINE__);
   }
   if (t->lines) {
-    rc = lsdx_create(cam->width, cam->height, n_streams, device, &t->lx);
+    // "0" off, "1" on, else by size when the HIP runtime has the hardware
+    // queues for the extra streams (with the default 4, streams share queues
+    // and the halves serialise with the ORB stream: measured no gain)
+    const char* split_env = getenv("ORBPL_LSD_SPLIT");
+    const char* hwq = getenv("GPU_MAX_HW_QUEUES");
+    const bool split = !t->stereo && (split_env ? split_env[0] == '1'
+                                                : n_streams >= kLsdSplitMin && hwq && atoi(hwq) >= 8);
+    t->lsplit = split ? (n_streams + 1) / 2 : 0;
+    rc = lsdx_create(cam->width, cam->height, split ? t->lsplit : n_streams, device, &t->lx);
+    if (!rc && split) rc = lsdx_create(cam->width, cam->height, n_streams - t->lsplit, device, &t->lx2);
     if (rc) {
       orbpl_tracker_destroy(t);
       return rc;
     }
     if (hipStreamCreateWithFlags(&t->lstream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&t->ev_in, hipEventDisableTiming) != hipSuccess) {
+      orbpl_tracker_destroy(t);
+      return hip_fail(hipErrorUnknown, "hipStreamCreate", __LINE__);
+    }
+    if (split && (hipStreamCreateWithFlags(&t->lstream_a, hipStreamNonBlocking) != hipSuccess ||
+                  hipStreamCreateWithFlags(&t->lstream_b, hipStreamNonBlocking) != hipSuccess ||
+                  hipEventCreateWithFlags(&t->ev_la_sort, hipEventDisableTiming) != hipSuccess ||
+                  hipEventCreateWithFlags(&t->ev_la_done, hipEventDisableTiming) != hipSuccess ||
+                  hipEventCreateWithFlags(&t->ev_lb_done, hipEventDisableTiming) != hipSuccess)) {
       orbpl_tracker_destroy(t);
       return hip_fail(hipErrorUnknown, "hipStreamCreate", __LINE__);
     }
@@ -1632,16 +1670,39 @@ static int tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_
   if (t->lines) {
     // ---- line stream: LineExtractor + UndistortKeyLines + line depths
     HIP_CHECK(hipEventRecord(t->ev_in, s));
-    HIP_CHECK(hipStreamWaitEvent(t->lstream, t->ev_in, 0));
-    HIP_CHECK(hipEventRecord(ev[11], t->lstream));
     LineOut lo{};
     lo.kl = C.kl;
     lo.desc = C.ldesc;
     lo.coef = C.lcoef;
     lo.n = C.nl;
-    int lrc = lsdx_run(t->lx, d_gray, S, t->W, (int64_t)t->W * t->H, &lo, t->lstream, ev[12],
-                       &ev[18]);
-    if (lrc) return lrc;
+    if (t->lsplit) {
+      // first half on lstream_a (its stage events are the step's LSD
+      // timings), the second on lstream_b once the first half is sorted
+      const int S1 = t->lsplit, S2 = S - S1;
+      const int64_t fp = (int64_t)t->W * t->H;
+      HIP_CHECK(hipStreamWaitEvent(t->lstream_a, t->ev_in, 0));
+      HIP_CHECK(hipEventRecord(ev[11], t->lstream_a));
+      int lrc = lsdx_run(t->lx, d_gray, S1, t->W, fp, &lo, t->lstream_a, ev[12], &ev[18]);
+      if (lrc) return lrc;
+      HIP_CHECK(hipEventRecord(t->ev_la_done, t->lstream_a));
+      HIP_CHECK(hipStreamWaitEvent(t->lstream_b, ev[19], 0));   // ev_stage[1]: first half sorted
+      LineOut lo2 = lo;
+      lo2.kl = C.kl + (size_t)S1 * kLineKeep;
+      lo2.desc = C.ldesc + (size_t)S1 * kLineKeep * 32;
+      lo2.coef = C.lcoef + (size_t)S1 * kLineKeep * 3;
+      lo2.n = C.nl + S1;
+      lrc = lsdx_run(t->lx2, d_gray + (size_t)S1 * fp, S2, t->W, fp, &lo2, t->lstream_b, nullptr);
+      if (lrc) return lrc;
+      HIP_CHECK(hipEventRecord(t->ev_lb_done, t->lstream_b));
+      HIP_CHECK(hipStreamWaitEvent(t->lstream, t->ev_la_done, 0));
+      HIP_CHECK(hipStreamWaitEvent(t->lstream, t->ev_lb_done, 0));
+    } else {
+      HIP_CHECK(hipStreamWaitEvent(t->lstream, t->ev_in, 0));
+      HIP_CHECK(hipEventRecord(ev[11], t->lstream));
+      int lrc = lsdx_run(t->lx, d_gray, S, t->W, (int64_t)t->W * t->H, &lo, t->lstream, ev[12],
+                         &ev[18]);
+      if (lrc) return lrc;
+    }
     la.nl = C.nl;
     la.kl = C.kl;
     la.kl_un = C.kl_un;
@@ -2130,7 +2191,8 @@ int orbpl_tracker_synchronize(orbpl_tracker* t) {
   HIP_CHECK(hipStreamSynchronize(t->tstream));
   if (t->lines) {
     HIP_CHECK(hipStreamSynchronize(t->lstream));
-    int rc = lsdx_check(t->lx, t->S);
+    int rc = t->lsplit ? lsdx_check(t->lx, t->lsplit) : lsdx_check(t->lx, t->S);
+    if (!rc && t->lsplit) rc = lsdx_check(t->lx2, t->S - t->lsplit);
     if (rc) return rc;
   }
   if (t->stereo) {

@@ -185,11 +185,15 @@ def test_tracker_pipelined_matches_oracle_vo(orbpl, oracle):
         assert np.abs(st["Tcw"][s] - To).max() < POSE_TOL, s
 
 
-@pytest.mark.parametrize("pipelined,fixed", [(False, False), (True, False), (False, True)])
-def test_tracker_with_lines_matches_oracle_lvo(orbpl, oracle, pipelined, fixed):
+@pytest.mark.parametrize("pipelined,fixed,split", [(False, False, False), (True, False, False),
+                                                  (False, True, False), (True, False, True)])
+def test_tracker_with_lines_matches_oracle_lvo(orbpl, oracle, pipelined, fixed, split, monkeypatch):
     """Point+line tracker (ORBPL_TRACK_LINES) against the oracle LVO loop:
     identical point and line counts every frame, pose within POSE_TOL, and
-    the last frame's undistorted KeyLines / LBD rows bit-exact."""
+    the last frame's undistorted KeyLines / LBD rows bit-exact. split: the LSD
+    batch in two offset halves on two streams (ORBPL_LSD_SPLIT=1; frames 0-1
+    and 2 here)."""
+    monkeypatch.setenv("ORBPL_LSD_SPLIT", "1" if split else "0")
     S, F = 3, 5
     seqs = [sequence(F, 30 + s) for s in range(S)]
     cfg = seqs[0][0]
