@@ -46,12 +46,13 @@ from pathlib import Path
 import numpy as np
 
 # HIP hardware queues per process, read when the HIP runtime starts (nothing
-# above touches it): the tracker drives up to six streams at once (ORB
-# extraction, tracking, the LSD chain in two offset halves and its line glue,
-# host copies; the right image's ORB and LSD in stereo). With the runtime's
-# default of 4 queues, streams share a queue and their kernels serialise
-# (stereo 3.4k -> 4.7k, lines 13.0k -> 13.8k frames/s at 8).
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# above touches it): a tracker drives up to eight streams at once (ORB
+# extraction and LSD each in two offset halves, the line glue, tracking, host
+# copies; the right image's ORB and LSD in stereo), and the bench holds one
+# tracker per leg. With the runtime's default of 4 queues, streams share a
+# queue and their kernels serialise (at 16 queues vs 4 / 8,
+# stereo 3.4k / 3.2k -> 4.9k, lines 13.0k / 11.5k -> 13.1k frames/s).
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "tests"))

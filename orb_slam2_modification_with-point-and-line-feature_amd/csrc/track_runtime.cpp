@@ -32,6 +32,22 @@ namespace {
 // streams from which the RGB-D lines tracker splits its LSD batch in two
 // offset halves (ORBPL_LSD_SPLIT overrides)
 constexpr int kLsdSplitMin = 1024;
+// likewise the ORB extraction batch (ORBPL_ORB_SPLIT overrides): the second
+// half's pyramid beside the first half's FAST, and so on down the chain
+constexpr int kOrbSplitMin = 256;
+
+// the HIP runtime was started with >= 8 hardware queues (GPU_MAX_HW_QUEUES):
+// with the default 4, extra streams share queues and serialise
+bool enough_hw_queues() {
+  const char* q = getenv("GPU_MAX_HW_QUEUES");
+  return q && atoi(q) >= 8;
+}
+// a split switch: env "0" off, "1" on, else on from `min_streams` when the
+// runtime has the queues for it
+bool split_on(const char* env, int n_streams, int min_streams) {
+  const char* e = getenv(env);
+  return e ? e[0] == '1' : n_streams >= min_streams && enough_hw_queues();
+}
 
 // RAII device buffer for the synchronous host-pointer entry points.
 struct DBuf {
@@ -806,6 +822,13 @@ struct orbpl_tracker {
   // beside the other's VALU-bound seed loop. The line glue then runs on
   // lstream after both.
   int lsplit = 0;
+  // split ORB extraction (points / RGB-D lines at >= kOrbSplitMin streams):
+  // the first osplit frames on `stream` (context ex), the rest on stream2
+  // (ex2) once the first half's pyramid is done
+  int osplit = 0;
+  orbx_ctx* ex2 = nullptr;
+  hipStream_t stream2 = nullptr;   // owned by ex2
+  hipEvent_t ev_ob_done = nullptr;
   lsdx_ctx* lx2 = nullptr;
   hipStream_t lstream_a = nullptr, lstream_b = nullptr;
   hipEvent_t ev_la_sort = nullptr, ev_la_done = nullptr, ev_lb_done = nullptr;
@@ -1079,6 +1102,8 @@ int orbpl_tracker_destroy(orbpl_tracker* t) {
   if (t->lx) lsdx_destroy(t->lx);
   if (t->lx2) lsdx_destroy(t->lx2);
   if (t->ex) orbx_destroy(t->ex);
+  if (t->ex2) orbx_destroy(t->ex2);
+  if (t->ev_ob_done) (void)hipEventDestroy(t->ev_ob_done);
   delete t;
   return ORBPL_OK;
 }
@@ -1114,10 +1139,22 @@ int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam
   t->S = n_streams;
   t->W = cam->width;
   t->H = cam->height;
-  int rc = orbx_create(orb, cam->width, cam->height, n_streams, device, &t->ex);
+  const bool osplit = !(flags & ORBPL_TRACK_STEREO) && split_on("ORBPL_ORB_SPLIT", n_streams, kOrbSplitMin);
+  t->osplit = osplit ? (n_streams + 1) / 2 : 0;
+  int rc = orbx_create(orb, cam->width, cam->height, osplit ? t->osplit : n_streams, device, &t->ex);
   if (rc) {
     delete t;
     return rc;
+  }
+  if (osplit) {
+    rc = orbx_create(orb, cam->width, cam->height, n_streams - t->osplit, device, &t->ex2);
+    if (!rc && hipEventCreateWithFlags(&t->ev_ob_done, hipEventDisableTiming) != hipSuccess)
+      rc = hip_fail(hipErrorUnknown, "hipEventCreate", __LINE__);
+    if (rc) {
+      orbpl_tracker_destroy(t);
+      return rc;
+    }
+    t->stream2 = orbpl::orbx_stream(t->ex2);
   }
   t->kp_cap = orbx_max_keypoints(t->ex);
   if (t->kp_cap > kMatchMaxKp) {
@@ -1288,10 +1325,7 @@ int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam
     // "0" off, "1" on, else by size when the HIP runtime has the hardware
     // queues for the extra streams (with the default 4, streams share queues
     // and the halves serialise with the ORB stream: measured no gain)
-    const char* split_env = getenv("ORBPL_LSD_SPLIT");
-    const char* hwq = getenv("GPU_MAX_HW_QUEUES");
-    const bool split = !t->stereo && (split_env ? split_env[0] == '1'
-                                                : n_streams >= kLsdSplitMin && hwq && atoi(hwq) >= 8);
+    const bool split = !t->stereo && split_on("ORBPL_LSD_SPLIT", n_streams, kLsdSplitMin);
     t->lsplit = split ? (n_streams + 1) / 2 : 0;
     rc = lsdx_create(cam->width, cam->height, split ? t->lsplit : n_streams, device, &t->lx);
     if (!rc && split) rc = lsdx_create(cam->width, cam->height, n_streams - t->lsplit, device, &t->lx2);
@@ -1730,9 +1764,27 @@ static int tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_
     }
     HIP_CHECK(hipEventRecord(ev[13], t->lstream));
   }
-  int rc = orbx_run(t->ex, d_gray, S, t->W, (long long)t->W * t->H,
-                    reinterpret_cast<orbpl_keypoint_dev*>(C.kps), C.desc, K, C.n, ev);
-  if (rc) return rc;
+  int rc;
+  if (t->osplit) {
+    // first half on `s` (its stage events are the step's extraction
+    // timings), the second on stream2 after the first half's pyramid
+    const int S1 = t->osplit, S2 = S - S1;
+    const long long fp = (long long)t->W * t->H;
+    rc = orbx_run(t->ex, d_gray, S1, t->W, fp, reinterpret_cast<orbpl_keypoint_dev*>(C.kps),
+                  C.desc, K, C.n, ev);
+    if (rc) return rc;
+    HIP_CHECK(hipStreamWaitEvent(t->stream2, ev[1], 0));
+    rc = orbx_run(t->ex2, d_gray + (size_t)S1 * fp, S2, t->W, fp,
+                  reinterpret_cast<orbpl_keypoint_dev*>(C.kps + (size_t)S1 * K),
+                  C.desc + (size_t)S1 * K * 32, K, C.n + S1, nullptr);
+    if (rc) return rc;
+    HIP_CHECK(hipEventRecord(t->ev_ob_done, t->stream2));
+    HIP_CHECK(hipStreamWaitEvent(s, t->ev_ob_done, 0));
+  } else {
+    rc = orbx_run(t->ex, d_gray, S, t->W, (long long)t->W * t->H,
+                  reinterpret_cast<orbpl_keypoint_dev*>(C.kps), C.desc, K, C.n, ev);
+    if (rc) return rc;
+  }
   launch_frame_prepare(t->consts, C.kps, C.n, K, t->stereo ? nullptr : d_depth,
                        (long long)t->W * t->H, C.kps_un, C.depth, C.uright, C.gcell, S, s);
   if (t->stereo) {
@@ -2211,6 +2263,10 @@ int orbpl_tracker_synchronize(orbpl_tracker* t) {
       HIP_CHECK(hipMemset(t->d_err, 0, 4));
       return (arg_fail("stereo row band capacity exceeded"), ORBPL_ERR_OVERFLOW);
     }
+  }
+  if (t->ex2) {
+    const int rc = orbx_synchronize(t->ex2);
+    if (rc) return rc;
   }
   return orbx_synchronize(t->ex);
 }

@@ -148,9 +148,13 @@ def test_tracker_matches_oracle_vo(orbpl, oracle):
     assert np.all(ms >= 0)
 
 
-def test_tracker_pipelined_matches_oracle_vo(orbpl, oracle):
+@pytest.mark.parametrize("split", [False, True])
+def test_tracker_pipelined_matches_oracle_vo(orbpl, oracle, split, monkeypatch):
     """Two-stream pipelined tracker, steps issued back to back (no host sync
-    between steps): the final state equals the oracle VO after F frames."""
+    between steps): the final state equals the oracle VO after F frames.
+    split: the ORB extraction batch in two offset halves on two streams
+    (ORBPL_ORB_SPLIT=1; frames 0-1 and 2 here)."""
+    monkeypatch.setenv("ORBPL_ORB_SPLIT", "1" if split else "0")
     S, F = 3, 6
     seqs = [sequence(F, 20 + s) for s in range(S)]
     cfg = seqs[0][0]
@@ -191,9 +195,10 @@ def test_tracker_with_lines_matches_oracle_lvo(orbpl, oracle, pipelined, fixed, 
     """Point+line tracker (ORBPL_TRACK_LINES) against the oracle LVO loop:
     identical point and line counts every frame, pose within POSE_TOL, and
     the last frame's undistorted KeyLines / LBD rows bit-exact. split: the LSD
-    batch in two offset halves on two streams (ORBPL_LSD_SPLIT=1; frames 0-1
-    and 2 here)."""
+    batch and the ORB extraction batch in two offset halves on two streams
+    each (ORBPL_LSD_SPLIT=1, ORBPL_ORB_SPLIT=1; frames 0-1 and 2 here)."""
     monkeypatch.setenv("ORBPL_LSD_SPLIT", "1" if split else "0")
+    monkeypatch.setenv("ORBPL_ORB_SPLIT", "1" if split else "0")
     S, F = 3, 5
     seqs = [sequence(F, 30 + s) for s in range(S)]
     cfg = seqs[0][0]
