@@ -52,7 +52,9 @@ import numpy as np
 # tracker per leg. With the runtime's default of 4 queues, streams share a
 # queue and their kernels serialise (at 16 queues vs 4 / 8,
 # stereo 3.4k / 3.2k -> 4.9k, lines 13.0k / 11.5k -> 13.1k frames/s).
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+# (the GPU box exports the default 4 explicitly, so raise rather than default)
+if int(os.environ.get("GPU_MAX_HW_QUEUES") or 0) < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "tests"))
@@ -226,7 +228,8 @@ KERNELS = {"pyramid": "k_pyramid", "fast": "k_fast_cells", "octree": "k_octree",
 def pmc_traffic(kernel, workload, streams):
     """HBM bytes per launch of `kernel` from the committed PMC summary of the
     same workload (tools/prof.sh + tools/pmc_traffic.py: FETCH_SIZE x2 gfx950
-    correction + WRITE_SIZE), scaled to this run's stream count. PMC counters
+    correction + WRITE_SIZE), scaled to this run's frames per launch (the
+    kernel's "frames_per_launch" in the summary, else its stream count). PMC counters
     need their own rocprofv3 passes, so they cannot be read live. Stage
     kernels joined with '+' sum their parts."""
     for rnd in ("r03", "r02", "r01"):
@@ -240,9 +243,10 @@ def pmc_traffic(kernel, workload, streams):
         parts = kernel.split("+")
         es = [d.get(k) for k in parts]
         if all(e and e.get("traffic_bytes") for e in es) and meta.get("streams"):
+            per = es[0].get("frames_per_launch", meta["streams"])
             tb = sum(e["traffic_bytes"] for e in es)
-            return (int(tb * streams / meta["streams"]),
-                    f"{f.relative_to(ROOT)} ({meta['streams']} streams, scaled)")
+            return (int(tb * streams / per),
+                    f"{f.relative_to(ROOT)} ({per} frames per launch, scaled)")
     return None, None
 
 
@@ -602,9 +606,15 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
     sel = iso if iso is not None else stage_avg
     dom = max(cand, key=lambda k: sel.get(k, stage_avg[k]))
     dom_ms = stage_avg[dom]          # live: timed region, in-stream hipEvents
-    bytes_launch = int(ab[dom] * S)
+    # frames per launch: the extraction / LSD batches may be split in two
+    # offset halves on two streams; their stage events bracket the first half
+    orb_fr, lsd_fr = tr.launch_frames()
+    def launch_frames(k):
+        return (orb_fr if k in ("pyramid", "fast", "octree", "orient_desc") else
+                lsd_fr if k in tr.LSD_STAGES else S)
+    bytes_launch = int(ab[dom] * launch_frames(dom))
     achieved = bytes_launch / (dom_ms * 1e-3) / 1e9
-    traffic, tsrc = pmc_traffic(KERNELS[dom], workload, S)
+    traffic, tsrc = pmc_traffic(KERNELS[dom], workload, launch_frames(dom))
     if traffic and dom == "pose_all":
         traffic *= 2          # the PMC summary is per launch; two full launches per step
     fbytes = frame_bytes(n_kp, fw, fh, wl["orb"], lines, stereo)
@@ -615,7 +625,8 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
             "traffic_source": tsrc,
             "traffic_over_algorithmic": round(traffic / bytes_launch, 2) if traffic else None,
             "algorithmic_bytes_per_launch": bytes_launch, "avg_launch_ms": round(dom_ms, 4),
-            "per_kernel_GBps": {k: round(ab[k] * S / (stage_avg[k] * 1e-3) / 1e9, 1)
+            "frames_per_launch": launch_frames(dom),
+            "per_kernel_GBps": {k: round(ab[k] * launch_frames(k) / (stage_avg[k] * 1e-3) / 1e9, 1)
                                 for k in cand if stage_avg[k] > 0}}
     # whole pipeline: B_frame x frames/s against 8 TB/s
     per_gpu = S * steps / elapsed

@@ -468,6 +468,13 @@ int orbpl_tracker_timings_reset(orbpl_tracker* tr);
  * _lsd_timings, _stereo_timings and _kernel_timings (in that order): 11, 3, 7,
  * 4, 4. A caller sizes its buffers max_steps x these. */
 int orbpl_tracker_timing_counts(int* counts5);
+/* Frames one launch of the extraction kernels (pyramid, FAST, octree,
+ * orient+desc) and of the LSD kernels processes. Both equal the stream count
+ * unless the tracker splits that batch into two offset halves on two streams
+ * (ORBPL_ORB_SPLIT=1; ORBPL_LSD_SPLIT, by default from 1024 streams when the
+ * HIP runtime has GPU_MAX_HW_QUEUES >= 8): then the first half's, whose
+ * launches the stage timings above bracket. lsd_frames is 0 without lines. */
+int orbpl_tracker_launch_frames(const orbpl_tracker* tr, int* orb_frames, int* lsd_frames);
 /* Per-kernel device times (ms) of the last min(max_steps, 64) steps, 4 per
  * step, each launch bracketed by its own hipEvents on the tracking stream:
  * k_pose of TrackWithMotionModel, k_pose of TrackReferenceKeyFrame (0 without

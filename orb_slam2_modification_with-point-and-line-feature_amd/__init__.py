@@ -373,6 +373,7 @@ def _declare_track(L):
     L.orbpl_tracker_step.argtypes = [vp, vp, vp]
     L.orbpl_tracker_synchronize.argtypes = [vp]
     L.orbpl_tracker_set_pipelined.argtypes = [vp, C.c_int]
+    L.orbpl_tracker_launch_frames.argtypes = [vp, ip, ip]
     L.orbpl_tracker_get_state.argtypes = [vp, vp, vp, vp, vp, vp]
     L.orbpl_tracker_stage_ms.argtypes = [vp, vp]
     L.orbpl_tracker_kp_capacity.argtypes = [vp]
@@ -814,6 +815,14 @@ class Tracker:
                    "lsd_sort": "k_lsd_sort+k_lsd_sort_local", "lsd_seed": "k_lsd_spec",
                    "lsd_validate": "k_lsd_validate+k_lsd_compact", "keylines": "k_keylines",
                    "lbd": "k_lsd_blur+k_sobel+k_lbd", "line_prepare": "k_line_prepare"}
+
+    def launch_frames(self):
+        """(orb, lsd): frames one extraction / LSD stage launch processes (the
+        first half when the tracker splits that batch; lsd 0 without lines)."""
+        o, l = C.c_int(0), C.c_int(0)
+        check(lib().orbpl_tracker_launch_frames(self._h, C.byref(o), C.byref(l)),
+              "orbpl_tracker_launch_frames")
+        return o.value, l.value
 
     def lsd_timings(self, max_steps=64):
         """(n_steps, 7) LSD / LineExtractor kernel ms of the last steps."""

@@ -8,8 +8,10 @@ gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts half
 the bytes of wide coalesced reads, so fetch_bytes = 2 * FETCH_SIZE; WRITE_SIZE
 is taken as is. Both counters are in KiB.
 
-usage: python tools/pmc_traffic.py <tag> <round> [streams] [workload]
-(workload: points -> pmc_traffic_points.json, lines, kitti, ...)
+usage: python tools/pmc_traffic.py <tag> <round> [streams] [workload] [orb_frames,lsd_frames]
+(workload: points -> pmc_traffic_points.json, lines, kitti, ...; the last
+argument: frames per launch of the extraction / LSD kernels when the tracker
+split those batches in two halves, stored per kernel as "frames_per_launch")
 """
 import collections
 import csv
@@ -24,6 +26,11 @@ def short(name):
     n = name.split("(")[0]
     n = n.replace("void ", "").replace("orbpl::", "")
     return n.split("<")[0]
+
+
+ORB_KERNELS = ("k_pyramid", "k_fast_cells", "k_octree", "k_orient_desc")
+LSD_KERNELS = ("k_lsd_prep", "k_lsd_sort", "k_lsd_sort_local", "k_lsd_spec", "k_lsd_validate",
+               "k_lsd_compact", "k_keylines", "k_blur_sobel", "k_lbd")
 
 
 def main():
@@ -50,7 +57,11 @@ def main():
                   "fetch_bytes": fb, "write_bytes": wb,
                   "traffic_bytes": (fb + wb) if fb is not None and wb is not None else None}
     wl = sys.argv[4] if len(sys.argv) > 4 else "points"
-    out["_meta"] = {"streams": int(sys.argv[3]) if len(sys.argv) > 3 else 256, "workload": wl,
+    streams = int(sys.argv[3]) if len(sys.argv) > 3 else 256
+    of, lf = (int(x) for x in sys.argv[5].split(",")) if len(sys.argv) > 5 else (streams, streams)
+    for k, e in out.items():
+        e["frames_per_launch"] = of if k in ORB_KERNELS else lf if k in LSD_KERNELS else streams
+    out["_meta"] = {"streams": streams, "workload": wl,
                     "source": f"gpurun_out/prof_{tag}", "correction": "fetch x2 (gfx950)"}
     dst = ROOT / "profiles" / rnd / f"pmc_traffic_{wl}.json"
     dst.parent.mkdir(parents=True, exist_ok=True)

@@ -11,6 +11,8 @@ tag=${1:-run}
 out=gpurun_out/prof_$tag
 mkdir -p $out
 cd /tmp && export TMPDIR=/tmp
+# the bench's hardware queue count, set before rocprofv3 starts the runtime
+export GPU_MAX_HW_QUEUES=16
 R=$GRAFT_REPO_ROOT
 COMMON="--no-cpu-baseline --no-parity --sweep 0 --secondary-steps 0 --stereo-steps 0 --rig-steps 0 --isolated-steps 0 --ingress-steps 0"
 case "$MODE" in
