@@ -904,7 +904,7 @@ def main():
     ap.add_argument("--rig-steps", type=int, default=5,
                     help="steps of the configs[4] 8-camera rig workload reported under 'rig' "
                          "(points runs only; 0 = skip)")
-    ap.add_argument("--rig-streams", type=int, default=256, help="rig cameras per GPU (x8)")
+    ap.add_argument("--rig-streams", type=int, default=512, help="rig cameras per GPU (x8)")
     ap.add_argument("--isolated-steps", type=int, default=5,
                     help="untimed non-pipelined steps after the timed region: per-kernel "
                          "times without the other stream's interference (roofline.isolated)")
