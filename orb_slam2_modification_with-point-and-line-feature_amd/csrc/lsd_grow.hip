@@ -1233,13 +1233,34 @@ __device__ __forceinline__ int lane_refine(const Frame& F, uint64_t* sd, LaneBuf
 // dominate; a lane runs them for its own rectangle exactly as the reference
 // orders them, 64 rectangles per wave.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ double nfa_lane(int n, int k, double p, double log_nt) {
+// log(p) and log(1 - p) of the last p a lane's NFA saw (rect_improve changes
+// p only in its first and last phase)
+struct NfaLogs {
+  double p = -1, lp = 0, l1p = 0;
+  __device__ __forceinline__ void set(double q) {
+    if (q != p) {
+      p = q;
+      lp = lsdm::log_(q);
+      l1p = lsdm::log_(1.0 - q);
+    }
+  }
+};
+
+// nfa for one lane. The three log_gamma terms take integer arguments n + 1,
+// k + 1, n - k + 1: they come from a table the same log_gamma filled
+// (k_lgamma_table; Lanczos below 15, 8 logs and 7 powers, Windschitl above)
+// when n is inside it.
+__device__ __forceinline__ double nfa_lane(int n, int k, double p, double log_nt,
+                                           const double* __restrict__ lgam, int lgam_n,
+                                           NfaLogs& L) {
   if (n == 0 || k == 0) return -log_nt;
   if (n == k) return -log_nt - double(n) * lsdm::log10_(p);
   const double p_term = p / (1 - p);
-  const double log1term = log_gamma(double(n) + 1) - log_gamma(double(k) + 1) -
-                          log_gamma(double(n - k) + 1) + double(k) * lsdm::log_(p) +
-                          double(n - k) * lsdm::log_(1.0 - p);
+  L.set(p);
+  const double lgn = n < lgam_n ? lgam[n] : log_gamma(double(n) + 1);
+  const double lgk = n < lgam_n ? lgam[k] : log_gamma(double(k) + 1);
+  const double lgnk = n < lgam_n ? lgam[n - k] : log_gamma(double(n - k) + 1);
+  const double log1term = lgn - lgk - lgnk + double(k) * L.lp + double(n - k) * L.l1p;
   double term = lsdm::exp_(log1term);
   if (double_equal(term, 0)) {
     if (k > n * p) return -log1term / 2.30258509299404568402 - log_nt;
@@ -1264,7 +1285,9 @@ __device__ __forceinline__ double nfa_lane(int n, int k, double p, double log_nt
 // rect_nfa for one lane: the reference's row walk, pixels counted in
 // batches of 8 loads generated across rows.
 __device__ __forceinline__ double rect_nfa_lane(const float* __restrict__ deg, int sw, int sh,
-                                                const Rect& rec, double log_nt) {
+                                                const Rect& rec, double log_nt,
+                                                const double* __restrict__ lgam, int lgam_n,
+                                                NfaLogs& L) {
   const double half_width = rec.width / 2.0;
   const double dyhw = rec.dy * half_width;
   const double dxhw = rec.dx * half_width;
@@ -1368,13 +1391,15 @@ __device__ __forceinline__ double rect_nfa_lane(const float* __restrict__ deg, i
       }
     }
   }
-  return nfa_lane(total, alg, rec.p, log_nt);
+  return nfa_lane(total, alg, rec.p, log_nt, lgam, lgam_n, L);
 }
 
 __device__ __forceinline__ double rect_improve_lane(const float* __restrict__ deg, int sw, int sh,
-                                                    Rect& rec, double log_nt) {
+                                                    Rect& rec, double log_nt,
+                                                    const double* __restrict__ lgam, int lgam_n) {
   const double delta = 0.5, delta_2 = delta / 2.0;
-  double log_nfa = rect_nfa_lane(deg, sw, sh, rec, log_nt);
+  NfaLogs L;
+  double log_nfa = rect_nfa_lane(deg, sw, sh, rec, log_nt, lgam, lgam_n, L);
   if (log_nfa > 0) return log_nfa;
   for (int phase = 0; phase < 5; phase++) {
     Rect r = rec;
@@ -1406,7 +1431,7 @@ __device__ __forceinline__ double rect_improve_lane(const float* __restrict__ de
         eval = false;
       }
       if (eval) {
-        const double v = rect_nfa_lane(deg, sw, sh, r, log_nt);
+        const double v = rect_nfa_lane(deg, sw, sh, r, log_nt, lgam, lgam_n, L);
         if (v > log_nfa) {
           log_nfa = v;
           rec = r;
@@ -1898,7 +1923,7 @@ __global__ void __launch_bounds__(256, ORBPL_VAL_MINW) k_lsd_validate(LsdGeom g,
     rec.x1 = rv[0]; rec.y1 = rv[1]; rec.x2 = rv[2]; rec.y2 = rv[3];
     rec.width = rv[4]; rec.x = rv[5]; rec.y = rv[6]; rec.theta = rv[7];
     rec.dx = rv[8]; rec.dy = rv[9]; rec.prec = rv[10]; rec.p = rv[11];
-    const double log_nfa = rect_improve_lane(deg, g.sw, g.sh, rec, g.log_nt);
+    const double log_nfa = rect_improve_lane(deg, g.sw, g.sh, rec, g.log_nt, sc.lgam, sc.lgam_n);
     const bool ok = log_nfa > 0;
     sc.cand_ok[o] = ok;
     if (ok) {
@@ -1931,6 +1956,15 @@ __global__ void __launch_bounds__(64) k_lsd_compact(LsdScratch sc) {
     sc.nlines[f] = min(nl, kLsdMaxLines);
     if (nl > kLsdMaxLines) atomicOr(sc.err + f, 8);
   }
+}
+
+__global__ void __launch_bounds__(256) k_lgamma_table(double* t, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) t[i] = log_gamma(double(i) + 1);
+}
+
+void launch_lgamma_table(double* t, int n, hipStream_t s) {
+  hipLaunchKernelGGL(k_lgamma_table, dim3((n + 255) / 256), dim3(256), 0, s, t, n);
 }
 
 void launch_lsd_validate(const LsdGeom& g, const LsdScratch& sc, int batch, hipStream_t s) {

@@ -119,6 +119,8 @@ struct LsdScratch {
   int4* sort_local;    // seg_cap per frame: introsort segments finished in LDS
   int* sort_nlocal;    // 1 per frame
   int* sort_kt;        // 1 per frame: key bound, key < kt => NOTDEF pixel
+  const double* lgam;  // log_gamma(i + 1) for i < lgam_n (k_lgamma_table): the
+  int lgam_n;          // NFA's three log_gamma terms at integer arguments
   int* sort_nge;       // 1 per frame: elements with key >= kt (the list's
                        // exactly sorted prefix; every later pixel is NOTDEF)
 };
@@ -169,6 +171,8 @@ void launch_lsd_grow(const LsdGeom& g, const LsdScratch& sc, int batch, hipStrea
                      bool serial);
 size_t lsd_grow_smem(const LsdGeom& g);
 void launch_lsd_validate(const LsdGeom& g, const LsdScratch& sc, int batch, hipStream_t s);
+// t[i] = log_gamma(i + 1), i < n, with the NFA's own log_gamma (once per context)
+void launch_lgamma_table(double* t, int n, hipStream_t s);
 
 // Host runtime (lsd_runtime.cpp): LSD (+ LineExtractor when `out` is set) of
 // `batch` frames on stream `s`; lsdx_check reads the device capacity flags.

@@ -261,6 +261,8 @@ int lsdx_create(int width, int height, int max_batch, int device, lsdx_ctx** out
   LA(s.sort_nlocal, B * 4);
   LA(s.sort_kt, B * 4);
   LA(s.sort_nge, B * 4);
+  s.lgam_n = g.sw * g.sh + 1;   // a rectangle holds at most every pixel
+  LA(s.lgam, (size_t)s.lgam_n * 8);
   LA(c->d_tabs, (size_t)(2 * g.sw + 2 * g.sh) * 4);
   LA(c->blur5, B * width * height);
   LA(c->sdx, B * width * height * 2);
@@ -290,6 +292,7 @@ int lsdx_create(int width, int height, int max_batch, int device, lsdx_ctx** out
   lin_tab(0.8, width, g.sw, tabs.data(), tabs.data() + g.sw, &c->g.rx0, &c->g.rx1);
   lin_tab(0.8, height, g.sh, tabs.data() + 2 * g.sw, tabs.data() + 2 * g.sw + g.sh, &c->g.ry0,
           &c->g.ry1);
+  launch_lgamma_table(const_cast<double*>(s.lgam), s.lgam_n, nullptr);
   if (hipMemcpy(c->d_tabs, tabs.data(), tabs.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
     lsdx_destroy(c);
     return hip_fail(hipErrorUnknown, "hipMemcpy", __LINE__);
