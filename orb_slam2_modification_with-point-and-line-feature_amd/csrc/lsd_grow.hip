@@ -1554,6 +1554,21 @@ constexpr int kSpecSmallBatch = ORBPL_SPEC_SMALL_BATCH;
 #ifndef ORBPL_SPEC_MINW
 #define ORBPL_SPEC_MINW 4
 #endif
+// ORBPL_SPEC_KEEP (one wave per frame): a round ends at its first seed whose
+// region met an earlier seed's claim; the later seeds of the window whose
+// claim re-check passed keep their regions and fits for the next round
+// instead of growing them again. Their results are the reference's unless a
+// seed before them in the list (the stopping seed, regrown, or another
+// regrown one) now claims one of their pixels: at the next round's start
+// their touched pixels are re-stamped with that round's claim tag (ranks in
+// list order, so the regrown seeds before them win and the new seeds after
+// them lose), and the next re-check decides again. Lanes take the carried
+// seeds first, in list order, then new seeds from the scan; a lane's list
+// buffer travels with its seed (bufid). After a cooperative fallback nothing
+// is carried (the fallback uses buffer 0 as scratch).
+#ifndef ORBPL_SPEC_KEEP
+#define ORBPL_SPEC_KEEP 1
+#endif
 // the block's first index >= j whose bit is set in the per-wave masks, or n
 template <int W>
 __device__ __forceinline__ int next_set(const unsigned long long* m, int j, int n) {
@@ -1578,9 +1593,11 @@ __device__ __forceinline__ void block_sync() {
 template <int W, int MINW = (W == 1 ? ORBPL_SPEC_MINW : 1)>
 __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch sc) {
   constexpr int SL = 64 * W;
+  constexpr bool KEEP = W == 1 && ORBPL_SPEC_KEEP && !ORBPL_LBUF_INTERLEAVED;
   extern __shared__ uint32_t grow_smem[];
   __shared__ uint32_t s_pt[SL];
   __shared__ int s_pos[SL];
+  __shared__ int s_src[KEEP ? SL : 1];
   __shared__ int s_cnt[2][W];
   __shared__ unsigned long long s_cm[W], s_km[W];
   __shared__ int s_misc[2];   // next_pos, status of the stop seed / nl after a fallback
@@ -1614,7 +1631,11 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
   F.cs = sd + lsd_cs_offset(sw, sh);
   F.tw = lsd_sd_tw(sw);
   static_assert(!ORBPL_LBUF_INTERLEAVED || W == 1, "interleaved lane lists: one wave per frame");
-  LaneBuf buf{fbuf + (ORBPL_LBUF_INTERLEAVED ? t : (long long)t * kLaneCap)};
+  int bufid = t;       // this lane's list buffer (KEEP: travels with a carried seed)
+  bool keep = false;   // KEEP: the lane's seed, region and fit carried from the last round
+  int ncarry = 0;      // KEEP: lanes [0, ncarry) hold carried seeds
+  int status = kSpecConflict, off = 0, len = 0, touched = 0;
+  Rect rec;
   const uint32_t* A = sc.A + (long long)f * g.n;
   const int nlist = sc.sort_nge[f];   // later list entries are NOTDEF
   double* cand_out = sc.cand + (long long)f * kLsdMaxCand * 12;
@@ -1629,9 +1650,11 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
   long long n_spec = 0, n_rounds = 0, cyc_spec = 0, cyc_fit = 0, cyc_val = 0, max_steps = 0,
             n_coop = 0;
   const long long t_all = clock64();
-  while (pos < nlist) {
-    // ---- the next SL defined, NOTUSED seeds in list order ----
-    int ncand = 0, scan = pos, next_pos = nlist;
+  while (pos < nlist || ncarry > 0) {
+    const LaneBuf buf{fbuf + (ORBPL_LBUF_INTERLEAVED ? t : (long long)bufid * kLaneCap)};
+    // ---- the next SL defined, NOTUSED seeds in list order (after the
+    // carried ones) ----
+    int ncand = ncarry, scan = pos, next_pos = nlist;
     while (ncand < SL && scan < nlist) {
       const int i = scan + t;
       bool c = false;
@@ -1683,18 +1706,36 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
     __threadfence_block();
     block_sync<W>();
     n_rounds++;
-    n_spec += ncand;
+    n_spec += ncand - (KEEP ? __popcll(__ballot(keep)) : 0);
     // ---- speculative per-lane processing ----
     const long long t0 = clock64();
     // claim tags: a later round's are smaller (stale claims of uncommitted
     // seeds lose to them), an earlier seed's of the same round smaller
     const uint32_t tag = ((0x3FFFFFu - round) << 9) | (uint32_t)t;
     const uint32_t myval0 = (tag << 1) | 1u, myval1 = tag << 1;
-    int status = kSpecConflict, off = 0, len = 0, touched = 0;
-    Rect rec;
+    if (!keep) {
+      status = kSpecConflict;
+      off = 0;
+      len = 0;
+      touched = 0;
+    } else {
+      // a carried seed's touched pixels take this round's tag (a USED pixel
+      // keeps its 0 and fails the re-check)
+      for (int j0 = 0; j0 < touched; j0 += 8) {
+        uint32_t ev[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) ev[u] = buf[min(j0 + u, touched - 1)].x;
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+          atomicMin(sd_hi(sd, lsd_sd_index((int)(ev[u] & 0xFFFF), (int)(ev[u] >> 16), F.tw)),
+                    myval0);
+      }
+      wg_fence();
+    }
+    __builtin_amdgcn_wave_barrier();
     double reg_angle = 0;
     int n = 0;
-    if (t < ncand) {
+    if (t < ncand && !keep) {
       const uint32_t pt = s_pt[t];
       n = lane_grow(F, sd, buf, kLaneCap, (int)(pt & 0xFFFF), (int)(pt >> 16), reg_angle, prec,
                     myval0);
@@ -1707,7 +1748,7 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
       for (int o = 32; o >= 1; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
       max_steps += mx;
     }
-    if (t < ncand) {
+    if (t < ncand && !keep) {
       if (n < 0) {
         status = n;
       } else if (n < g.min_reg_size) {
@@ -1824,6 +1865,7 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
       break;
     }
     cyc_val += clock64() - t2;
+    bool carry = false;   // KEEP: this round's seeds from `stop` on go to the next one
     if (stop < ncand) {
       pos = s_pos[stop];
       int st_stop;
@@ -1862,9 +1904,51 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
         }
         n_coop++;
         pos++;
+      } else if (KEEP) {
+        carry = true;
+        pos = next_pos;
       }
     } else {
       pos = next_pos;
+    }
+    if constexpr (KEEP) {
+      // carry the seeds from `stop` on (the stopping seed and every later
+      // one, kept when its re-check passed; a conflicting one whose seed
+      // pixel a committed region now covers is dropped, as the sequential
+      // loop skips it) to lanes [0, ncarry) in list order; the other lanes'
+      // buffers go to the lanes the scan fills
+      bool car = carry && t >= stop && t < ncand;
+      const bool kp = car && t > stop && !conflict;
+      const uint32_t my_pt = s_pt[t];
+      const int my_pos = s_pos[t];
+      if (car && !kp && used_get(F, (int)(my_pt & 0xFFFF), (int)(my_pt >> 16))) car = false;
+      const unsigned long long cm = __ballot(car);
+      const int ncar = __popcll(cm);
+      s_src[car ? __popcll(cm & lt_mask) : ncar + __popcll(~cm & lt_mask)] = t;
+      __threadfence_block();
+      __builtin_amdgcn_wave_barrier();
+      const int src = s_src[t];
+      keep = __shfl((int)kp, src, 64) != 0 && t < ncar;
+      bufid = __shfl(bufid, src, 64);
+      status = __shfl(status, src, 64);
+      off = __shfl(off, src, 64);
+      len = __shfl(len, src, 64);
+      touched = __shfl(touched, src, 64);
+      rec.x1 = shfl_d(rec.x1, src); rec.y1 = shfl_d(rec.y1, src);
+      rec.x2 = shfl_d(rec.x2, src); rec.y2 = shfl_d(rec.y2, src);
+      rec.width = shfl_d(rec.width, src); rec.x = shfl_d(rec.x, src);
+      rec.y = shfl_d(rec.y, src); rec.theta = shfl_d(rec.theta, src);
+      rec.dx = shfl_d(rec.dx, src); rec.dy = shfl_d(rec.dy, src);
+      rec.prec = shfl_d(rec.prec, src); rec.p = shfl_d(rec.p, src);
+      const uint32_t npt = (uint32_t)__shfl((int)my_pt, src, 64);
+      const int npos = __shfl(my_pos, src, 64);
+      if (t < ncar) {
+        s_pt[t] = npt;
+        s_pos[t] = npos;
+      }
+      ncarry = ncar;
+      __threadfence_block();
+      __builtin_amdgcn_wave_barrier();
     }
     round++;
     if (W > 1) __syncthreads();   // s_pt / s_pos / s_misc reads done before the next round

@@ -346,7 +346,10 @@ struct SortPtrs {
 
 __device__ __forceinline__ int skey(uint32_t e) { return (int)(e >> 22); }
 
-constexpr int kSortThreads = 512;
+#ifndef ORBPL_SORT_THREADS
+#define ORBPL_SORT_THREADS 512
+#endif
+constexpr int kSortThreads = ORBPL_SORT_THREADS;   // k_lsd_sort's workgroup (A/B build override)
 
 // Exclusive scan of a[0..len) (global) in place by the whole block; returns
 // the total in every thread.
