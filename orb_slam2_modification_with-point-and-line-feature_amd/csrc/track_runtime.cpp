@@ -1721,7 +1721,11 @@ static int tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_
       int lrc = lsdx_run(t->lx, d_gray, S1, t->W, fp, &lo, t->lstream_a, ev[12], &ev[18]);
       if (lrc) return lrc;
       HIP_CHECK(hipEventRecord(t->ev_la_done, t->lstream_a));
-      HIP_CHECK(hipStreamWaitEvent(t->lstream_b, ev[19], 0));   // ev_stage[1]: first half sorted
+      // the second half starts once the first half is sorted (ev_stage[1]);
+      // ORBPL_LSD_STAGGER=0 / 2: at the step start / after its seed loop (A/B)
+      static const char* stg = getenv("ORBPL_LSD_STAGGER");
+      const int stagger = stg ? atoi(stg) : 1;
+      HIP_CHECK(hipStreamWaitEvent(t->lstream_b, stagger == 0 ? t->ev_in : ev[stagger == 2 ? 20 : 19], 0));
       LineOut lo2 = lo;
       lo2.kl = C.kl + (size_t)S1 * kLineKeep;
       lo2.desc = C.ldesc + (size_t)S1 * kLineKeep * 32;
