@@ -817,7 +817,7 @@ struct orbpl_tracker {
   lsdx_ctx* lx = nullptr;
   hipStream_t lstream = nullptr;
   hipEvent_t ev_in = nullptr;      // step start on `stream`
-  // split LSD (ORBPL_LSD_SPLIT, RGB-D lines at >= kLsdSplitMin streams): the
+  // split LSD (ORBPL_LSD_SPLIT, lines at >= kLsdSplitMin streams): the
   // first lsplit frames on lstream_a (context lx), the rest on lstream_b
   // (lx2) started once the first half's pseudo-ordering sort is done, so the
   // halves' chains run offset: one half's latency-bound sort and validation
@@ -1327,7 +1327,9 @@ int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam
     // "0" off, "1" on, else by size when the HIP runtime has the hardware
     // queues for the extra streams (with the default 4, streams share queues
     // and the halves serialise with the ORB stream: measured no gain)
-    const bool split = !t->stereo && split_on("ORBPL_LSD_SPLIT", n_streams, kLsdSplitMin);
+    // (stereo: the left image's batch; the right one has its own stream and
+    // context. KITTI leg, 1024 pairs: 4.9k -> 5.2k frames/s)
+    const bool split = split_on("ORBPL_LSD_SPLIT", n_streams, kLsdSplitMin);
     t->lsplit = split ? (n_streams + 1) / 2 : 0;
     rc = lsdx_create(cam->width, cam->height, split ? t->lsplit : n_streams, device, &t->lx);
     if (!rc && split) rc = lsdx_create(cam->width, cam->height, n_streams - t->lsplit, device, &t->lx2);
