@@ -4,7 +4,7 @@
 # combined with --pmc). Outputs under gpurun_out/prof_<tag>/.
 #   MODE=points (default): the headline configs[1] leg of the default bench
 #   MODE=lines: configs[2] at 3072 streams;  MODE=kitti: configs[3] at 1024
-#   MODE=rig: configs[4] at 256 cameras
+#   MODE=rig: configs[4] at 512 cameras
 #   SQ=1 adds an SQ counter pass (VALU / wait / LDS instruction counts)
 set -o pipefail
 tag=${1:-run}
@@ -18,7 +18,7 @@ COMMON="--no-cpu-baseline --no-parity --sweep 0 --secondary-steps 0 --stereo-ste
 case "$MODE" in
   lines) B="$R/bench.py --workload lines --streams 3072 --steps 3 --warmup 1 $COMMON" ;;
   kitti) B="$R/bench.py --workload kitti --streams 1024 --steps 3 --warmup 1 $COMMON" ;;
-  rig)   B="$R/bench.py --workload rig --streams 256 --steps 3 --warmup 1 $COMMON" ;;
+  rig)   B="$R/bench.py --workload rig --streams 512 --steps 3 --warmup 1 $COMMON" ;;
   *)     B="$R/bench.py --steps 20 --warmup 5 $COMMON" ;;
 esac
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/$out/trace -o run --output-format csv -- python3 $B > $R/$out/trace.log 2>&1 || { echo "trace failed"; tail -5 $R/$out/trace.log; exit 1; }
