@@ -275,10 +275,49 @@ def map_mode(args, wl):
     return bool(args.map) and not wl["stereo"]
 
 
+def leg_summary(out):
+    """A compact copy of every leg's headline figures (value, ms per step,
+    roofline fraction, parity), the batch-1 latencies and the reference-faithful
+    CPU per-frame times, emitted as the JSON line's last key so that a log cut
+    to its tail still carries the north-star (points + lines) numbers."""
+    def leg(o):
+        if not o:
+            return None
+        roof = o.get("roofline") or {}
+        par = o.get("parity") or {}
+        return {"value": o.get("value"), "ms_per_step": o.get("ms_per_step"),
+                "streams": o.get("streams_per_gpu", (o.get("config") or {}).get("streams_per_gpu")),
+                "frac": roof.get("frac"), "kernel": roof.get("kernel"),
+                "parity_pass": par.get("pass") if isinstance(par, dict) else None}
+    s = {"points": leg(out)}
+    for k in ("secondary", "stereo", "rig", "ingress"):
+        if k in out:
+            s[k] = leg(out[k])
+    sw = out.get("sweep") or {}
+    s["batch1_ms"] = {k: (v[0].get("latency_ms_per_step") if v else None) for k, v in sw.items()}
+    for k in ("trk_load",):
+        if k in out:
+            s[k] = out[k]
+    cpu = out.get("cpu_baseline") or {}
+    rf = {"points": (cpu.get("reference_faithful") or {}).get("median_ms_per_frame")}
+    if "secondary" in out:
+        rf["lines"] = ((out["secondary"].get("cpu_baseline") or {}).get("reference_faithful")
+                       or {}).get("median_ms_per_frame")
+    s["cpu_reference_faithful_ms"] = rf
+    return s
+
+
 def map_capacity(total_steps):
     """Keyframe slots per stream for a tracker that runs `total_steps` steps:
     at most one keyframe per step, so the map never declines one (the
-    ORBPL_MAP_KF environment read at tracker creation; 64 at most)."""
+    ORBPL_MAP_KF environment read at tracker creation; 64 at most). Beyond 63
+    steps a stream may run out of slots (capacity flag 1, a declined keyframe,
+    no longer the reference's map): say so loudly; the run's parity check and
+    `map_capacity_flags` then show whether it happened."""
+    if total_steps + 1 > 64:
+        print(f"bench: WARNING {total_steps} steps exceed the 63 keyframes the map model's "
+              f"64-slot table (ORBPL_MAP_KF) guarantees; a stream that inserts more declines "
+              f"keyframes (capacity flag 1)", file=sys.stderr, flush=True)
     os.environ["ORBPL_MAP_KF"] = str(max(2, min(64, total_steps + 1)))
 
 
@@ -1088,6 +1127,7 @@ def main():
                     "reference_faithful": cpu_reference_faithful(
                         o["gray"], o["depth"], o["layout"], o["wname"], ofl, args.cpu_ref_warmup,
                         args.cpu_ref_frames, o["map"])}
+        out["summary"] = leg_summary(out)   # last key: it survives a tail-cut log
         print(json.dumps(out))
     if dist:
         dist.destroy_process_group()

@@ -416,7 +416,13 @@ int orbpl_tracker_create(const orbpl_orb_params* orb, const orbpl_camera* cam, i
  * distinctive descriptors, normals, UpdateConnections), the LOST state and the
  * reset of a map with <= 5 keyframes. Per stream a keyframe table (32 by
  * default; ORBPL_MAP_KF in the environment at creation, 2..64) and point / line
- * pools of keyframes x keypoint capacity / x 80 in HBM. Pinned P23-P25
+ * pools of keyframes x keypoint capacity / x 80 in HBM: with F keyframe slots
+ * and K keypoints per frame about F*K*(160 + 4*F) + F*80*112 bytes per stream
+ * (the observation table grows with F^2: K = 1000 gives ~9.5 MB at F = 32,
+ * ~27 MB at F = 64, i.e. ~10 / ~28 GB for 1024 streams). A stream whose map
+ * needs a keyframe beyond its F slots declines it and raises capacity flag 1
+ * (orbpl_tracker_get_map_errors): size F above the keyframes a run inserts
+ * (at most one per step). Pinned P23-P25
  * (DESIGN.md): LocalMapping = its ProcessNewKeyFrame run synchronously,
  * Relocalization fails; pointer-ordered containers in keyframe id order.
  * Replaces ORBPL_TRACK_LOCAL_MAP (its P18 local map); not with STEREO. */

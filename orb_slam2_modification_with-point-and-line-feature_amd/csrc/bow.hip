@@ -23,6 +23,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -245,8 +247,13 @@ struct orbv_vocab {
   std::vector<int32_t> word;
   int n_words = 0;
   std::vector<int32_t> child_start, child;
-  std::vector<VocCopy> copies;   // one per device the tree was uploaded to
+  // one per device the tree was uploaded to; a deque keeps the handed-out
+  // pointers valid while another thread uploads to a further device, `mu`
+  // guards the list, `host_mu` the host-pointer transform's scratch
+  std::deque<VocCopy> copies;
+  std::mutex mu, host_mu;
   VocCopy* on(int device) {
+    std::lock_guard<std::mutex> g(mu);
     for (auto& c : copies)
       if (c.device == device) return &c;
     return nullptr;
@@ -435,7 +442,9 @@ int orbv_export(const orbv_vocab* v, int32_t* parent, uint8_t* leaf_flag, uint8_
 
 int orbv_upload(orbv_vocab* v, int device) {
   if (!v) return arg_fail("orbv_upload: NULL vocabulary");
-  if (v->on(device)) return ORBPL_OK;
+  std::lock_guard<std::mutex> g(v->mu);
+  for (auto& c : v->copies)
+    if (c.device == device) return ORBPL_OK;
   HIP_CHECK(hipSetDevice(device));
   const size_t nn = v->parent.size();
   VocCopy c;
@@ -504,6 +513,7 @@ int orbv_transform(orbv_vocab* v, int device, const uint8_t* desc, int n, int le
   int rc = orbv_upload(v, device);
   if (rc) return rc;
   HIP_CHECK(hipSetDevice(device));
+  std::lock_guard<std::mutex> g(v->host_mu);   // one host transform at a time
   VocCopy* c = v->on(device);
   if (!c->h_desc) {
     // one device block: desc | n | node | word | weight | words | vals | bow_n | err

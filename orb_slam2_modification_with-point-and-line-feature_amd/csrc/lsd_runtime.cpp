@@ -292,7 +292,17 @@ int lsdx_create(int width, int height, int max_batch, int device, lsdx_ctx** out
   lin_tab(0.8, width, g.sw, tabs.data(), tabs.data() + g.sw, &c->g.rx0, &c->g.rx1);
   lin_tab(0.8, height, g.sh, tabs.data() + 2 * g.sw, tabs.data() + 2 * g.sw + g.sh, &c->g.ry0,
           &c->g.ry1);
+  // the NFA's log_gamma table: filled and waited for here, so the first
+  // k_lsd_validate on the context's non-blocking streams reads a finished table
   launch_lgamma_table(const_cast<double*>(s.lgam), s.lgam_n, nullptr);
+  {
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+    if (e != hipSuccess) {
+      lsdx_destroy(c);
+      return hip_fail(e, "k_lgamma_table", __LINE__);
+    }
+  }
   if (hipMemcpy(c->d_tabs, tabs.data(), tabs.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
     lsdx_destroy(c);
     return hip_fail(hipErrorUnknown, "hipMemcpy", __LINE__);

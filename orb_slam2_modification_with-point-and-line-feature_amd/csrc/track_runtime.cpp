@@ -47,6 +47,7 @@ bool enough_hw_queues() {
 // a split switch: env "0" off, "1" on, else on from `min_streams` when the
 // runtime has the queues for it
 bool split_on(const char* env, int n_streams, int min_streams) {
+  if (n_streams < 2) return false;   // two halves need a frame each, even when forced
   const char* e = getenv(env);
   return e ? e[0] == '1' : n_streams >= min_streams && enough_hw_queues();
 }

@@ -45,7 +45,7 @@ Frame::Frame(const cv::Mat& imGray, const cv::Mat& imDepth, const double& timeSt
   // ORB || LineExtractor (Frame.cc:152-155)
   thread_local LineExtractor own_lines;
   LineExtractor* lx = lineExtractor ? lineExtractor : &own_lines;
-  std::exception_ptr lerr;
+  std::exception_ptr lerr, oerr;
   std::thread tl([&]() {
     try {
       lx->ExtractLineSegment(imGray, mvKeyLines, mLineDescriptors, mvKeyLineCoefficient);
@@ -53,8 +53,15 @@ Frame::Frame(const cv::Mat& imGray, const cv::Mat& imDepth, const double& timeSt
       lerr = std::current_exception();
     }
   });
-  (*extractor)(imGray, cv::Mat(), mvKeys, mDescriptors);
+  // the ORB call may throw (library error): the line thread is joined on
+  // every path before anything propagates
+  try {
+    (*extractor)(imGray, cv::Mat(), mvKeys, mDescriptors);
+  } catch (...) {
+    oerr = std::current_exception();
+  }
   tl.join();
+  if (oerr) std::rethrow_exception(oerr);
   if (lerr) std::rethrow_exception(lerr);
   N = (int)mvKeys.size();
   NL = (int)mvKeyLines.size();
