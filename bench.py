@@ -519,7 +519,8 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
     d_depth = pkg.DeviceBuffer.from_array(depth[rep], device=device)
     cam = pkg.make_camera(getattr(synth, cam_name))
     use_map = map_mode(args, wl)
-    map_capacity(warmup + steps + (args.isolated_steps if args.isolated_steps > 0 else 0))
+    map_capacity(warmup + steps + (args.isolated_steps if args.isolated_steps > 0 else 0)
+                 + (3 if args.trk_load else 0))
     tr = pkg.Tracker(pkg.OrbParams(*wl["orb"]), cam, S, device=device, lines=lines, stereo=stereo,
                      local_map=bool(args.local_map) and not use_map,
                      fixed_line_jac=bool(args.fixed_line_jacobian),
@@ -642,6 +643,39 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
         if lines:
             iso.update(zip(tr.LSD_STAGES,
                            [float(x) for x in tr.lsd_timings(args.isolated_steps).mean(0)]))
+    trk_load = None
+    if (args.trk_load and use_map and voc is not None and args.refkf
+            and workload == args.workload):
+        # untimed single steps after the timed region, serialised: a plain
+        # step, then steps where 10 % / 100 % of the streams lost their
+        # velocity (orbpl_tracker_clear_velocity: the state after
+        # initialisation or relocalisation) and so run TrackReferenceKeyFrame
+        # (SearchByBoW + the reference-keyframe pose) before TrackLocalMap.
+        # Parity of this path: test_map_tracker_reference_keyframe_under_load.
+        tr.set_pipelined(False)
+        k0 = warmup + steps + max(0, args.isolated_steps)
+
+        def one(k):
+            tr.synchronize()
+            tr.timings_reset()
+            t_a = time.perf_counter()
+            step(k)
+            tr.synchronize()
+            ms = (time.perf_counter() - t_a) * 1e3
+            kt = dict(zip(tr.KERNEL_STAGES, [float(x) for x in tr.kernel_timings(1)[-1]]))
+            return {"step_ms": round(ms, 3), "trk_section_ms": round(kt["pose_refkf"], 4),
+                    "ok_frac": round(float(tr.status()["ok"].mean()), 4)}
+        trk_load = {"streams": S, "plain": one(k0)}
+        for j, frac in enumerate((0.1, 1.0)):
+            every = int(round(1 / frac))
+            mask = (np.arange(S) % every) == 0
+            tr.clear_velocity(mask)
+            r = one(k0 + 1 + j)
+            r["streams_trk"] = int(mask.sum())
+            trk_load[f"{int(frac * 100)}%"] = r
+        trk_load["note"] = ("single non-pipelined steps after the timed region; trk_section_ms = "
+                            "hipEvents around TrackReferenceKeyFrame (k_trk_bow, line matcher, "
+                            "merge, pose) on the tracking stream")
     sel = iso if iso is not None else stage_avg
     dom = max(cand, key=lambda k: sel.get(k, stage_avg[k]))
     dom_ms = stage_avg[dom]          # live: timed region, in-stream hipEvents
@@ -687,7 +721,7 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
     return dict(S=S, value=value, layout=L, elapsed=elapsed, stages=stages, tracking=tracking,
                 roof=roof, gray=gray, depth=depth, workload=wl["desc"], data=wl["data"],
                 image=f"{fw}x{fh}", nfeatures=wl["orb"][0], samp=samp, hist=hist, wname=workload,
-                pipelined=bool(pipelined), map=use_map)
+                pipelined=bool(pipelined), map=use_map, trk_load=trk_load)
 
 
 def run_ingress(pkg, synth, args, S, steps, warmup, rank, world, device, dist, voc=None,
@@ -968,7 +1002,12 @@ def main():
     ap.add_argument("--bow", type=int, default=1,
                     help="1 = every frame's KeyFrame::ComputeBoW with a shared synthetic "
                          "vocabulary (broadcast + IDF all-reduce over ranks); 0 = off")
-    ap.add_argument("--vocab-levels", type=int, default=5, help="vocabulary depth L (k = 10)")
+    ap.add_argument("--vocab-levels", type=int, default=6,
+                    help="vocabulary depth L (k = 10; 6 = ORBvoc's shape: with levelsup 4 the "
+                         "FeatureVector nodes SearchByBoW walks sit at level 2)")
+    ap.add_argument("--trk-load", type=int, default=1,
+                    help="1 = after the timed region, time single steps in which 10 %% / 100 %% "
+                         "of the streams run TrackReferenceKeyFrame (headline, map model)")
     ap.add_argument("--refkf", type=int, default=1,
                     help="1 = Tracking::Track's TrackReferenceKeyFrame for the first tracked "
                          "frame and motion-model failures (needs --bow; DESIGN.md P22)")
@@ -1095,6 +1134,8 @@ def main():
             "parity": res["parity"],
             "cpu_baseline": cpu,
         }
+        if res.get("trk_load"):
+            out["trk_load"] = res["trk_load"]
         if sweeps:
             out["sweep"] = sweeps
         if ingress:

@@ -433,6 +433,14 @@ int orbpl_tracker_destroy(orbpl_tracker* tr);
 /* Forget all stream state; the next step initialises every stream with pose
  * Tcw0 (n_streams x 16 floats row-major, NULL = identity). */
 int orbpl_tracker_reset(orbpl_tracker* tr, const float* Tcw0);
+/* mVelocity = cv::Mat() for every stream s with mask[s] != 0 (n_streams
+ * bytes): the state Tracking holds after its initialisation or a
+ * relocalisation, so the stream's next step runs TrackReferenceKeyFrame
+ * instead of TrackWithMotionModel (Tracking.cc:324-338; with
+ * ORBPL_TRACK_REFKF and a vocabulary; without them the next prediction uses
+ * zero velocity). Waits for the tracker's queued steps. Used to time and test
+ * TrackReferenceKeyFrame under load. */
+int orbpl_tracker_clear_velocity(orbpl_tracker* tr, const uint8_t* mask);
 /* One step for all streams. d_gray: n_streams frames of width*height u8;
  * d_depth: n_streams frames of width*height float metres (device memory,
  * contiguous). Asynchronous on the tracker's stream. */

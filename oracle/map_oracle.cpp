@@ -1165,6 +1165,15 @@ int oracle_map_reset(void* h, const float* Tcw0) {
   return 0;
 }
 
+// mVelocity = cv::Mat() for one stream (after initialisation / relocalisation:
+// its next frame runs TrackReferenceKeyFrame, Tracking.cc:324-338)
+int oracle_map_clear_velocity(void* h, int stream) {
+  mapvo::MapVO* v = static_cast<mapvo::MapVO*>(h);
+  if (stream < 0 || stream >= (int)v->st.size()) return -1;
+  v->st[stream].has_velocity = false;
+  return 0;
+}
+
 int oracle_map_set_vocabulary(void* h, void* voc) {
   static_cast<mapvo::MapVO*>(h)->voc = voc;
   return 0;

@@ -707,6 +707,7 @@ def _setup(L):  # noqa: F811
     L.oracle_map_create.restype = vp
     L.oracle_map_destroy.argtypes = [vp]
     L.oracle_map_reset.argtypes = [vp, vp]
+    L.oracle_map_clear_velocity.argtypes = [vp, i]
     L.oracle_map_set_vocabulary.argtypes = [vp, vp]
     L.oracle_map_step.argtypes = [vp, i, vp, vp, vp, vp]
     L.oracle_map_keyframes.argtypes = [vp, i, vp, vp, i, vp]
@@ -737,6 +738,9 @@ class MapVO:
     def reset(self, Tcw0=None):
         T = None if Tcw0 is None else _c(Tcw0, np.float32)
         lib().oracle_map_reset(self.h, None if T is None else _p(T))
+
+    def clear_velocity(self, stream):
+        lib().oracle_map_clear_velocity(self.h, stream)
 
     def set_vocabulary(self, voc):
         self._voc = voc

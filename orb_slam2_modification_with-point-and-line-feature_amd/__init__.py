@@ -370,6 +370,7 @@ def _declare_track(L):
     L.orbpl_tracker_create.argtypes = [vp, vp, i, i, C.POINTER(vp)]
     L.orbpl_tracker_destroy.argtypes = [vp]
     L.orbpl_tracker_reset.argtypes = [vp, vp]
+    L.orbpl_tracker_clear_velocity.argtypes = [vp, vp]
     L.orbpl_tracker_step.argtypes = [vp, vp, vp]
     L.orbpl_tracker_synchronize.argtypes = [vp]
     L.orbpl_tracker_set_pipelined.argtypes = [vp, C.c_int]
@@ -699,6 +700,14 @@ class Tracker:
     def reset(self, Tcw0=None):
         T = None if Tcw0 is None else _c(Tcw0, np.float32)
         check(lib().orbpl_tracker_reset(self._h, None if T is None else _ptr(T)), "reset")
+
+    def clear_velocity(self, mask):
+        """mVelocity = cv::Mat() for the streams where mask != 0: their next
+        step runs TrackReferenceKeyFrame (orbpl_tracker_clear_velocity)."""
+        m = np.ascontiguousarray(np.asarray(mask).astype(np.uint8).reshape(-1))
+        if m.size != self.S:
+            raise ValueError("clear_velocity: one mask byte per stream")
+        check(lib().orbpl_tracker_clear_velocity(self._h, _ptr(m)), "orbpl_tracker_clear_velocity")
 
     def step_device(self, d_gray, d_depth):
         check(lib().orbpl_tracker_step(self._h, C.c_void_p(d_gray), C.c_void_p(d_depth)), "step")

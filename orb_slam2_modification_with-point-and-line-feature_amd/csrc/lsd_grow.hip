@@ -38,6 +38,7 @@ namespace {
 constexpr double kPi = 3.14159265358979323846;
 constexpr double kDegToRad = kPi / 180;
 constexpr int kRegLds = 512;
+constexpr int kRing = 64;   // point-word ring entries per lane of the prefetching grow (power of two)
 
 struct Rect {
   double x1, y1, x2, y2, width, x, y, theta, dx, dy, prec, p;
@@ -821,6 +822,161 @@ __device__ __forceinline__ int lane_grow(const Frame& F, uint64_t* sd, LaneBuf b
   }
   return n;
 }
+
+// ORBPL_GROW_PF: the small-batch seed loop (one wave per frame, batches of at
+// most kSpecSmallBatch frames) loads the next pixel's neighbourhood while it
+// tests / adds the current one, so a step no longer waits a memory round trip
+// before its tests (a lone wave on its SIMD hides no latency otherwise). The
+// point words of the grow's last 64 entries sit in a per-lane LDS ring, so
+// the next pixel to expand is known at the step's start. The prefetched words
+// predate the adds of the step in flight: those pixels (the only stamps that
+// step changes for this lane) are marked "in this region" from the step's
+// added mask, shifted to the next pixel's 3x3 (a 7x7 bit board). Claims other
+// lanes made meanwhile are caught by the claim re-check after the round, as
+// for any speculative read.
+#ifndef ORBPL_GROW_PF
+#define ORBPL_GROW_PF 1
+#endif
+
+__device__ __forceinline__ void nb_terms(int x, int y, int sw, int sh, int tw, int* rterm,
+                                         int* cterm, unsigned* inmask) {
+  bool rin[3], cin[3];
+#pragma unroll
+  for (int d = 0; d < 3; d++) {
+    const int yy = y + d - 1, xx = x + d - 1;
+    rin[d] = yy >= 0 && yy < sh;
+    cin[d] = xx >= 0 && xx < sw;
+    const int cy = min(max(yy, 0), sh - 1), cx = min(max(xx, 0), sw - 1);
+    rterm[d] = (((cy >> 2) * tw) << 5) | ((cy & 3) << 3);
+    cterm[d] = ((cx >> 2) << 5) | ((cx & 3) << 1);
+  }
+  unsigned m = 0;
+#pragma unroll
+  for (int k = 0; k < 9; k++) m |= (unsigned)(rin[k / 3] & cin[k % 3]) << k;
+  *inmask = m;
+}
+
+__device__ __forceinline__ int lane_grow_pf(const Frame& F, uint64_t* sd, LaneBuf buf, int cap,
+                                            int sx, int sy, double& reg_angle, double prec,
+                                            uint32_t myval, uint32_t* ring) {
+  const uint32_t mytag = myval >> 1;
+  const int sw = F.sw, sh = F.sh, tw = F.tw;
+  const int si = lsd_sd_index(sx, sy, tw);
+  if (cap < 1) return kSpecOverflow;
+  const uint64_t v0 = ld_sd(sd + si);
+  if (((uint32_t)(v0 >> 32) >> 1) < mytag) return kSpecConflict;
+  atomicMin(reinterpret_cast<unsigned long long*>(sd + si),
+            ((unsigned long long)myval << 32) | (uint32_t)v0);
+  uint32_t cur = (uint32_t)sx | ((uint32_t)sy << 16);
+  buf[0] = make_uint4(cur, (uint32_t)v0, 0u, 0u);
+  ring[0] = cur;
+  reg_angle = deg2ang(__uint_as_float((uint32_t)v0));
+  double s0, c0;
+  lsdm::sincos_(reg_angle, &s0, &c0);
+  float sumdx = (float)c0;
+  float sumdy = (float)s0;
+  const double k3pi2 = (3 * kPi) / 2, k2pi = 2 * kPi;
+  int n = 1;
+  // the current pixel's neighbourhood: terms, in-image mask and words
+  int rterm[3], cterm[3];
+  unsigned inm;
+  uint4 w[9];
+  nb_terms(sx, sy, sw, sh, tw, rterm, cterm, &inm);
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    if (k == 4) continue;
+    w[k] = *reinterpret_cast<const uint4*>(sd + (rterm[k / 3] + cterm[k % 3]));
+  }
+  unsigned own = 0;   // neighbours known to be in this region although their words predate it
+  for (int i = 0; i < n; i++) {
+    const int x = (int)(cur & 0xFFFF), y = (int)(cur >> 16);
+    const int n_start = n;
+    // the next pixel to expand, when already listed: its neighbourhood now
+    const bool pf = i + 1 < n_start;
+    uint32_t nxt = cur;
+    int nr[3], nc[3];
+    unsigned ninm = 0;
+    uint4 pw[9];
+    if (pf) {
+      nxt = n_start - (i + 1) <= kRing ? ring[(i + 1) & (kRing - 1)] : buf.pt(i + 1);
+      nb_terms((int)(nxt & 0xFFFF), (int)(nxt >> 16), sw, sh, tw, nr, nc, &ninm);
+#pragma unroll
+      for (int k = 0; k < 9; k++) {
+        if (k == 4) continue;
+        pw[k] = *reinterpret_cast<const uint4*>(sd + (nr[k / 3] + nc[k % 3]));
+      }
+    }
+    unsigned ok = 0;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+      if (k == 4) continue;
+      const unsigned f = ((inm >> k) & 1u) & ((~own >> k) & 1u) & (unsigned)(w[k].y != 0u) &
+                         (unsigned)(w[k].y != myval) & (unsigned)(__uint_as_float(w[k].x) >= 0.f);
+      ok |= f << k;
+    }
+    uint32_t first_add = cur;
+    unsigned added = 0;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+      if (k == 4) continue;
+      double nt = fabs(reg_angle - deg2ang(__uint_as_float(w[k].x)));
+      nt = nt > k3pi2 ? fabs(nt - k2pi) : nt;
+      if (((ok >> k) & 1u) && nt <= prec) {
+        if ((w[k].y >> 1) < mytag) return kSpecConflict;   // an earlier seed's pixel
+        const int id = rterm[k / 3] + cterm[k % 3];
+        atomicMin(reinterpret_cast<unsigned long long*>(sd + id),
+                  ((unsigned long long)myval << 32) | w[k].x);
+        if (n >= cap) return kSpecOverflow;
+        const int xx = x + (k % 3) - 1, yy = y + (k / 3) - 1;
+        const uint32_t pt = (uint32_t)xx | ((uint32_t)yy << 16);
+        if (n == n_start) first_add = pt;
+        buf[n] = make_uint4(pt, w[k].x, 0u, 0u);
+        ring[n & (kRing - 1)] = pt;
+        n++;
+        added |= 1u << k;
+        sumdx += __uint_as_float(w[k].z);   // add_angle(d) terms
+        sumdy += __uint_as_float(w[k].w);
+        reg_angle = (double)fast_atan2_deg_1div(sumdy, sumdx) * kDegToRad;
+      }
+    }
+    if (pf) {
+      // this step's adds, seen from the next pixel's 3x3: a 7x7 board with
+      // the current 3x3 at rows / columns 2..4
+      const int ddx = (int)(nxt & 0xFFFF) - x, ddy = (int)(nxt >> 16) - y;
+      unsigned nown = 0;
+      if (added && ddx >= -2 && ddx <= 2 && ddy >= -2 && ddy <= 2) {
+        const unsigned long long B = ((unsigned long long)(added & 7u) << 16) |
+                                     ((unsigned long long)((added >> 3) & 7u) << 23) |
+                                     ((unsigned long long)((added >> 6) & 7u) << 30);
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+          nown |= (unsigned)((B >> (7 * (2 + ddy + r) + 2 + ddx)) & 7ull) << (3 * r);
+      }
+      own = nown;
+      cur = nxt;
+      inm = ninm;
+#pragma unroll
+      for (int d = 0; d < 3; d++) {
+        rterm[d] = nr[d];
+        cterm[d] = nc[d];
+      }
+#pragma unroll
+      for (int k = 0; k < 9; k++) w[k] = pw[k];
+    } else if (i + 1 < n) {
+      // the next pixel is this step's first add: its words are loaded now
+      // (after this step's claims)
+      cur = first_add;
+      own = 0;
+      nb_terms((int)(cur & 0xFFFF), (int)(cur >> 16), sw, sh, tw, rterm, cterm, &inm);
+#pragma unroll
+      for (int k = 0; k < 9; k++) {
+        if (k == 4) continue;
+        w[k] = *reinterpret_cast<const uint4*>(sd + (rterm[k / 3] + cterm[k % 3]));
+      }
+    }
+  }
+  return n;
+}
 #else
 __device__ __forceinline__ int lane_grow(const Frame& F, uint64_t* sd, LaneBuf buf, int cap, int sx,
                                          int sy, double& reg_angle, double prec, uint32_t myval) {
@@ -1159,10 +1315,12 @@ struct FitProf {
 // refine + reduce_region_radius for a lane. The region [0, n) came from the
 // first grow; a second grow is appended after it. Returns the status; off /
 // len give the final region, touched the claimed prefix of the buffer.
+template <bool PF>
 __device__ __forceinline__ int lane_refine(const Frame& F, uint64_t* sd, LaneBuf buf, int n,
                                            double reg_angle,
                                            double prec, double p, Rect& rec, uint32_t myval1,
-                                           int& off, int& len, int& touched, FitProf& fp) {
+                                           int& off, int& len, int& touched, FitProf& fp,
+                                           uint32_t* ring) {
   const double density_th = 0.7;
   double density = double(n) / (dist(rec.x1, rec.y1, rec.x2, rec.y2) * rec.width);
   off = 0;
@@ -1194,7 +1352,12 @@ __device__ __forceinline__ int lane_refine(const Frame& F, uint64_t* sd, LaneBuf
       2.0 * sqrt((s_sum - 2.0 * mean_angle * sum) / double(cnt) + mean_angle * mean_angle);
   LaneBuf g1 = buf + n;
   fp.lap(1);
-  int n1 = lane_grow(F, sd, g1, kLaneCap - n, x0, y0, reg_angle, tau, myval1);
+  int n1;
+#if ORBPL_GROW_LEAN && ORBPL_GROW_CS && ORBPL_SD_PAIRED
+  if constexpr (PF) n1 = lane_grow_pf(F, sd, g1, kLaneCap - n, x0, y0, reg_angle, tau, myval1, ring);
+  else
+#endif
+  n1 = lane_grow(F, sd, g1, kLaneCap - n, x0, y0, reg_angle, tau, myval1);
   fp.lap(2);
   if (n1 < 0) return n1;
   off = n;
@@ -1601,6 +1764,12 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
   __shared__ int s_cnt[2][W];
   __shared__ unsigned long long s_cm[W], s_km[W];
   __shared__ int s_misc[2];   // next_pos, status of the stop seed / nl after a fallback
+#if ORBPL_GROW_LEAN && ORBPL_GROW_CS && ORBPL_SD_PAIRED
+  constexpr bool PF = ORBPL_GROW_PF && W == 1 && MINW == 1;   // the small-batch instance
+#else
+  constexpr bool PF = false;
+#endif
+  __shared__ uint32_t s_ring[PF ? 64 * kRing : 1];
   const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int sw = g.sw, sh = g.sh;
   Frame F;
@@ -1737,6 +1906,12 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
     int n = 0;
     if (t < ncand && !keep) {
       const uint32_t pt = s_pt[t];
+#if ORBPL_GROW_LEAN && ORBPL_GROW_CS && ORBPL_SD_PAIRED
+      if constexpr (PF)
+        n = lane_grow_pf(F, sd, buf, kLaneCap, (int)(pt & 0xFFFF), (int)(pt >> 16), reg_angle,
+                         prec, myval0, s_ring + lane * kRing);
+      else
+#endif
       n = lane_grow(F, sd, buf, kLaneCap, (int)(pt & 0xFFFF), (int)(pt >> 16), reg_angle, prec,
                     myval0);
     }
@@ -1760,7 +1935,8 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
         fp.start();
         lane_rect(buf, n, reg_angle, prec, p, rec, F.q, sw);
         fp.lap(0);
-        status = lane_refine(F, sd, buf, n, reg_angle, prec, p, rec, myval1, off, len, touched, fp);
+        status = lane_refine<PF>(F, sd, buf, n, reg_angle, prec, p, rec, myval1, off, len,
+                                 touched, fp, s_ring + lane * kRing);
 #ifdef ORBPL_FIT_PROF
         for (int k = 0; k < 5; k++) fpr[k] = fp.d[k];
 #endif

@@ -168,6 +168,8 @@ struct MapArgs {
 
 void launch_map_reset(const MapArgs& a, const float* T0, int nstreams, hipStream_t s);
 void launch_map_begin(const TrackConsts& c, const MapArgs& a, int nstreams, hipStream_t s);
+void launch_clear_velocity(MapState* ms, StreamState* st, const uint8_t* mask, int nstreams,
+                           hipStream_t s);
 void launch_map_resolve_motion(const MapArgs& a, int nstreams, hipStream_t s);
 void launch_map_trk_merge(const MapArgs& a, int nstreams, hipStream_t s);
 void launch_map_resolve_trk(const MapArgs& a, int nstreams, hipStream_t s);

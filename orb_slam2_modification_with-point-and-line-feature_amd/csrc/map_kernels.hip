@@ -1497,6 +1497,20 @@ __global__ void __launch_bounds__(kT) k_map_connect(MapArgs a) {
 void launch_map_reset(const MapArgs& a, const float* T0, int nstreams, hipStream_t s) {
   hipLaunchKernelGGL(k_map_reset, dim3((nstreams + 255) / 256), dim3(256), 0, s, a, T0, nstreams);
 }
+// mVelocity = cv::Mat() for the masked streams (what Tracking holds after its
+// initialisation or a relocalisation): their next frame runs
+// TrackReferenceKeyFrame (Tracking.cc:324-338). ms: map trackers, else st.
+__global__ void k_clear_velocity(MapState* ms, StreamState* st, const uint8_t* mask, int n) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n || !mask[s]) return;
+  if (ms) ms[s].has_velocity = 0;
+  else st[s].has_velocity = 0;
+}
+void launch_clear_velocity(MapState* ms, StreamState* st, const uint8_t* mask, int nstreams,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(k_clear_velocity, dim3((nstreams + 255) / 256), dim3(256), 0, s, ms, st, mask,
+                     nstreams);
+}
 void launch_map_begin(const TrackConsts& c, const MapArgs& a, int nstreams, hipStream_t s) {
   hipLaunchKernelGGL(k_map_begin, dim3(nstreams), dim3(kT), 0, s, c, a);
 }

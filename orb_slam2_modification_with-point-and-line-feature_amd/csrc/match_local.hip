@@ -546,116 +546,184 @@ __device__ void bitonic_sort(uint32_t* a, int n) {
 }
 }  // namespace
 
+// LDS of one SearchByBoW instance for frames of up to CAP features: both
+// sorted key lists, each keyframe feature's four best frame candidates, the
+// claims and rotation bins.
+template <int CAP>
 struct BowShared {
-  uint32_t skf[kBowMax], sf[kBowMax];
-  int smatch[kBowMax];
-  int sbin[kBowMax];
+  uint32_t skf[CAP], sf[CAP];
+  alignas(16) uint32_t cand[CAP][4];   // by sorted keyframe position: (dist << 11 | iF), ascending
+  int16_t smatch[CAP];     // frame feature -> claiming keyframe feature, -1
+  int8_t sbin[CAP];        // rotation bin of a claimed frame feature, -1
   int hist[32];
   int s_n, s_ind[3];
 };
 
-// fdl (LDS, 2 uint4 per feature, nf entries) stages the frame's descriptors:
-// the per-node loops compare against them from LDS instead of global memory.
-__device__ void match_bow_body(const BowArgs& a, BowShared& B, uint4* fdl) {
-  uint32_t* skf = B.skf;
-  uint32_t* sf = B.sf;
-  int* smatch = B.smatch;
-  int* sbin = B.sbin;
-  int* hist = B.hist;
-  int& s_n = B.s_n;
-  int* s_ind = B.s_ind;
+__device__ __forceinline__ int hamming32(const uint4 k0, const uint4 k1, const uint4 f0,
+                                         const uint4 f1) {
+  return __popc(k0.x ^ f0.x) + __popc(k0.y ^ f0.y) + __popc(k0.z ^ f0.z) + __popc(k0.w ^ f0.w) +
+         __popc(k1.x ^ f1.x) + __popc(k1.y ^ f1.y) + __popc(k1.z ^ f1.z) + __popc(k1.w ^ f1.w);
+}
+
+// [fb, fe) of the frame features of `node` in the sorted list sf (sentinels
+// 0xFFFFFFFF sort above every node: node ids are < 2^21 - 1)
+template <int CAP>
+__device__ __forceinline__ void frame_run(const uint32_t* sf, uint32_t node, int* fb, int* fe) {
+  int lo = 0, hi = CAP;
+  while (lo < hi) {
+    const int m = (lo + hi) >> 1;
+    if ((sf[m] >> 11) < node) lo = m + 1;
+    else hi = m;
+  }
+  int e = lo, h2 = CAP;
+  while (e < h2) {
+    const int m = (e + h2) >> 1;
+    if ((sf[m] >> 11) <= node) e = m + 1;
+    else h2 = m;
+  }
+  *fb = lo;
+  *fe = e;
+}
+
+// The body (ORBmatcher.cc:247-410). Nodes are independent (a frame feature is
+// claimed only by keyframe features of its own node); within a node the
+// reference walks the keyframe features in index order, each taking the best
+// (and second-best) distance over the node's frame features not yet claimed.
+//   1. both FeatureVectors sorted by (node, index) in LDS;
+//   2. every keyframe feature (all lanes) computes its four smallest
+//      (distance, frame index) keys over its node's frame run, the frame
+//      descriptors read from L2 in parallel;
+//   3. one lane per node replays the reference's in-order claims from those
+//      lists: the first two unclaimed entries are the best and second-best
+//      distances (ties keep index order, as the strict `<` of the reference);
+//      only when three of a truncated list are claimed does the lane rescan
+//      the run exactly;
+//   4. the rotation histogram and its top-3 cut.
+// fdl (LDS, 2 uint4 per feature) optionally stages the frame's descriptors.
+template <int CAP, int NT>
+__device__ void match_bow_body(const BowArgs& a, BowShared<CAP>& B, const uint4* fdl) {
   const int t = threadIdx.x;
-  const int nkf = min(a.nkf, kBowMax), nf = min(a.nf, kBowMax);
+  const int nkf = min(a.nkf, CAP), nf = min(a.nf, CAP);
   // key = node << 11 | index; features without a node sort last
-  for (int i = t; i < kBowMax; i += 256) {
-    skf[i] = (i < nkf && a.kf_node[i] >= 0) ? ((uint32_t)a.kf_node[i] << 11) | (uint32_t)i : 0xFFFFFFFFu;
-    sf[i] = (i < nf && a.f_node[i] >= 0) ? ((uint32_t)a.f_node[i] << 11) | (uint32_t)i : 0xFFFFFFFFu;
-    smatch[i] = -1;
-    sbin[i] = -1;
+  for (int i = t; i < CAP; i += NT) {
+    B.skf[i] = (i < nkf && a.kf_node[i] >= 0) ? ((uint32_t)a.kf_node[i] << 11) | (uint32_t)i : 0xFFFFFFFFu;
+    B.sf[i] = (i < nf && a.f_node[i] >= 0) ? ((uint32_t)a.f_node[i] << 11) | (uint32_t)i : 0xFFFFFFFFu;
+    B.smatch[i] = -1;
+    B.sbin[i] = -1;
   }
-  if (t < 32) hist[t] = 0;
-  if (t == 0) s_n = 0;
-  if (fdl) {
-    const uint4* d = reinterpret_cast<const uint4*>(a.f_desc);
-    for (int i = t; i < 2 * nf; i += 256) fdl[i] = d[i];
-  }
+  if (t < 32) B.hist[t] = 0;
+  if (t == 0) B.s_n = 0;
   __syncthreads();
   // the padding sorts last: sorting the next power of two above the counts
   // leaves the same runs
   int ns = 64;
   while (ns < nkf || ns < nf) ns <<= 1;
-  bitonic_sort(skf, ns);
-  bitonic_sort(sf, ns);
-  // one thread per keyframe node (first position of each node run)
+  bitonic_sort(B.skf, ns);
+  bitonic_sort(B.sf, ns);
+  const uint4* fd = reinterpret_cast<const uint4*>(a.f_desc);
+  const uint4* kd = reinterpret_cast<const uint4*>(a.kf_desc);
+  // 2. candidate lists, one keyframe feature per lane
+  for (int p = t; p < nkf; p += NT) {
+    const uint32_t key = B.skf[p];
+    uint32_t c0 = 0xFFFFFFFFu, c1 = c0, c2 = c0, c3 = c0;
+    if (key != 0xFFFFFFFFu && a.kf_valid[key & 0x7FF]) {
+      const int iKF = (int)(key & 0x7FF);
+      int fb, fe;
+      frame_run<CAP>(B.sf, key >> 11, &fb, &fe);
+      const uint4 k0 = kd[2 * iKF], k1 = kd[2 * iKF + 1];
+#pragma unroll 4
+      for (int r = fb; r < fe; r++) {
+        const uint32_t iF = B.sf[r] & 0x7FF;
+        const uint4 f0 = fdl ? fdl[2 * iF] : fd[2 * iF];
+        const uint4 f1 = fdl ? fdl[2 * iF + 1] : fd[2 * iF + 1];
+        const int d = hamming32(k0, k1, f0, f1);
+        // a distance of 256 never beats the reference's initial 256
+        const uint32_t k = d < 256 ? ((uint32_t)d << 11) | iF : 0xFFFFFFFFu;
+        // sorted insertion (frame indices ascend along the run: ties keep order)
+        c3 = min(c3, max(c2, k));
+        c2 = min(c2, max(c1, k));
+        c1 = min(c1, max(c0, k));
+        c0 = min(c0, k);
+      }
+    }
+    B.cand[p][0] = c0;
+    B.cand[p][1] = c1;
+    B.cand[p][2] = c2;
+    B.cand[p][3] = c3;
+  }
+  __syncthreads();
+  // 3. in-order claims, one lane per keyframe node run
   int nm = 0;
-  for (int p = t; p < kBowMax; p += 256) {
-    const uint32_t key = skf[p];
+  for (int p = t; p < nkf; p += NT) {
+    const uint32_t key = B.skf[p];
     if (key == 0xFFFFFFFFu) continue;
     const uint32_t node = key >> 11;
-    if (p > 0 && (skf[p - 1] >> 11) == node && skf[p - 1] != 0xFFFFFFFFu) continue;
-    // frame run of the same node
-    // node ids are < 2^21 - 1, so the 0xFFFFFFFF sentinels sort above every node
-    int lo = 0, hi = kBowMax;
-    while (lo < hi) {
-      const int m = (lo + hi) >> 1;
-      if ((sf[m] >> 11) < node) lo = m + 1;
-      else hi = m;
-    }
-    int fe = lo;
-    while (fe < kBowMax && sf[fe] != 0xFFFFFFFFu && (sf[fe] >> 11) == node) fe++;
-    const int fb = lo;
+    if (p > 0 && (B.skf[p - 1] >> 11) == node) continue;   // not the run's first
+    int fb, fe;
+    frame_run<CAP>(B.sf, node, &fb, &fe);
     if (fb == fe) continue;
-    for (int q = p; q < kBowMax && skf[q] != 0xFFFFFFFFu && (skf[q] >> 11) == node; q++) {
-      const int iKF = (int)(skf[q] & 0x7FF);
+    for (int q = p; q < nkf && B.skf[q] != 0xFFFFFFFFu && (B.skf[q] >> 11) == node; q++) {
+      const int iKF = (int)(B.skf[q] & 0x7FF);
       if (!a.kf_valid[iKF]) continue;
-      const uint4* kd = reinterpret_cast<const uint4*>(a.kf_desc + (long long)iKF * 32);
-      const uint4 k0 = kd[0], k1 = kd[1];
-      int bestDist1 = 256, bestIdxF = -1, bestDist2 = 256;
-      for (int r = fb; r < fe; r++) {
-        const int iF = (int)(sf[r] & 0x7FF);
-        if (smatch[iF] >= 0) continue;
-        uint4 f0, f1;
-        if (fdl) {
-          f0 = fdl[2 * iF];
-          f1 = fdl[2 * iF + 1];
-        } else {
-          const uint4* fd = reinterpret_cast<const uint4*>(a.f_desc + (long long)iF * 32);
-          f0 = fd[0];
-          f1 = fd[1];
-        }
-        const int dist = __popc(k0.x ^ f0.x) + __popc(k0.y ^ f0.y) + __popc(k0.z ^ f0.z) +
-                         __popc(k0.w ^ f0.w) + __popc(k1.x ^ f1.x) + __popc(k1.y ^ f1.y) +
-                         __popc(k1.z ^ f1.z) + __popc(k1.w ^ f1.w);
-        if (dist < bestDist1) {
-          bestDist2 = bestDist1;
-          bestDist1 = dist;
+      const uint4 cv = *reinterpret_cast<const uint4*>(B.cand[q]);
+      const uint32_t cl[4] = {cv.x, cv.y, cv.z, cv.w};
+      int bestDist1 = 256, bestIdxF = -1, bestDist2 = 256, found = 0;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        if (cl[k] == 0xFFFFFFFFu || found == 2) continue;
+        const int iF = (int)(cl[k] & 0x7FF);
+        if (B.smatch[iF] >= 0) continue;
+        if (found == 0) {
+          bestDist1 = (int)(cl[k] >> 11);
           bestIdxF = iF;
-        } else if (dist < bestDist2) {
-          bestDist2 = dist;
+        } else {
+          bestDist2 = (int)(cl[k] >> 11);
+        }
+        found++;
+      }
+      if (found < 2 && cl[3] != 0xFFFFFFFFu && fe - fb > 4) {
+        // the list was cut at four: the rest of the run decides, exactly
+        const uint4 k0 = kd[2 * iKF], k1 = kd[2 * iKF + 1];
+        bestDist1 = 256;
+        bestIdxF = -1;
+        bestDist2 = 256;
+        for (int r = fb; r < fe; r++) {
+          const int iF = (int)(B.sf[r] & 0x7FF);
+          if (B.smatch[iF] >= 0) continue;
+          const int dist = hamming32(k0, k1, fdl ? fdl[2 * iF] : fd[2 * iF],
+                                     fdl ? fdl[2 * iF + 1] : fd[2 * iF + 1]);
+          if (dist < bestDist1) {
+            bestDist2 = bestDist1;
+            bestDist1 = dist;
+            bestIdxF = iF;
+          } else if (dist < bestDist2) {
+            bestDist2 = dist;
+          }
         }
       }
       if (bestDist1 <= 50 && static_cast<float>(bestDist1) < a.nnratio * static_cast<float>(bestDist2)) {
-        smatch[bestIdxF] = iKF;
+        B.smatch[bestIdxF] = (int16_t)iKF;
         if (a.check_ori) {
           float rot = a.kf_angle[(long long)iKF * a.kf_angle_stride] -
-                    a.f_angle[(long long)bestIdxF * a.f_angle_stride];
+                      a.f_angle[(long long)bestIdxF * a.f_angle_stride];
           if (rot < 0.0f) rot += 360.0f;
           int bin = (int)roundf(rot * (30 / 360.0f));
           if (bin == 30) bin = 0;
-          sbin[bestIdxF] = bin;
-          atomicAdd(&hist[bin], 1);
+          B.sbin[bestIdxF] = (int8_t)bin;
+          atomicAdd(&B.hist[bin], 1);
         }
         nm++;
       }
     }
   }
-  if (nm) atomicAdd(&s_n, nm);
+  if (nm) atomicAdd(&B.s_n, nm);
   __syncthreads();
+  // 4. rotation consistency (ORBmatcher.cc:2035-2077, :386-404)
   if (a.check_ori) {
     if (t == 0) {
       int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
       for (int i = 0; i < 30; i++) {
-        const int sz = hist[i];
+        const int sz = B.hist[i];
         if (sz > max1) {
           max3 = max2; max2 = max1; max1 = sz; ind3 = ind2; ind2 = ind1; ind1 = i;
         } else if (sz > max2) {
@@ -669,45 +737,48 @@ __device__ void match_bow_body(const BowArgs& a, BowShared& B, uint4* fdl) {
       } else if (max3 < 0.1f * (float)max1) {
         ind3 = -1;
       }
-      s_ind[0] = ind1; s_ind[1] = ind2; s_ind[2] = ind3;
+      B.s_ind[0] = ind1; B.s_ind[1] = ind2; B.s_ind[2] = ind3;
     }
     __syncthreads();
     int rem = 0;
-    for (int j = t; j < nf; j += 256) {
-      const int b = sbin[j];
-      if (b >= 0 && b != s_ind[0] && b != s_ind[1] && b != s_ind[2]) {
-        smatch[j] = -1;
+    for (int j = t; j < nf; j += NT) {
+      const int b = B.sbin[j];
+      if (b >= 0 && b != B.s_ind[0] && b != B.s_ind[1] && b != B.s_ind[2]) {
+        B.smatch[j] = -1;
         rem++;
       }
     }
-    if (rem) atomicSub(&s_n, rem);
+    if (rem) atomicSub(&B.s_n, rem);
     __syncthreads();
   }
-  for (int j = t; j < nf; j += 256) a.match[j] = smatch[j];
-  if (t == 0) *a.nmatches = s_n;
+  for (int j = t; j < nf; j += NT) a.match[j] = B.smatch[j];
+  if (t == 0) *a.nmatches = B.s_n;
 }
 
 __global__ void __launch_bounds__(256) k_match_bow(BowArgs a) {
-  __shared__ BowShared B;
+  __shared__ BowShared<kBowMax> B;
   extern __shared__ uint4 bow_fdl[];
-  match_bow_body(a, B, bow_fdl);
+  const int nf = min(a.nf, kBowMax);
+  const uint4* d = reinterpret_cast<const uint4*>(a.f_desc);
+  for (int i = threadIdx.x; i < 2 * nf; i += 256) bow_fdl[i] = d[i];
+  // (the body's first barrier orders these stores before any read)
+  match_bow_body<kBowMax, 256>(a, B, bow_fdl);
 }
 
 void launch_match_bow(const BowArgs& a, hipStream_t s) {
   const size_t smem = (size_t)2 * sizeof(uint4) * (size_t)min(max(a.nf, 0), kBowMax);
-  set_smem_attr((const void*)k_match_bow, sizeof(BowShared) + (size_t)2 * sizeof(uint4) * kBowMax);
+  // the dynamic part only (static BowShared + this stay within the CU's 160 KiB)
+  set_smem_attr((const void*)k_match_bow, (size_t)2 * sizeof(uint4) * kBowMax);
   hipLaunchKernelGGL(k_match_bow, dim3(1), dim3(256), smem, s, a);
 }
 
 // TrackReferenceKeyFrame's ORBmatcher(0.7, true).SearchByBoW(pKF, F)
-// (Tracking.cc:947-952) for every stream with st[s].trk: the last frame's
-// FeatureVector / map points / descriptors against the current frame's
-// One workgroup per stream; only the streams whose motion model failed have
-// work (the rest return at once). The frame's descriptors stay in global
-// memory here: 32 KB more LDS on every workgroup of the launch made it slower
-// to place beside the next batch's extraction (a persistent grid with LDS
-// descriptors measured 2.2 ms per step against 0.3-0.8 ms this way).
-__device__ __forceinline__ void trk_bow_stream(const TrkArgs& a, BowShared& B, const int s) {
+// (Tracking.cc:947-952) for every stream with st[s].trk: the reference
+// keyframe's FeatureVector / map points / descriptors against the current
+// frame's. The frame's descriptors stay in global memory (L2): the launch runs
+// every step beside the next batch's extraction, so its LDS is kept small.
+template <int CAP>
+__device__ __forceinline__ void trk_bow_stream(const TrkArgs& a, BowShared<CAP>& B, const int s) {
   StreamState& S = a.st[s];
   if (!S.trk) return;
   const long long cb = (long long)s * a.kp_pitch;
@@ -727,27 +798,35 @@ __device__ __forceinline__ void trk_bow_stream(const TrkArgs& a, BowShared& B, c
   b.check_ori = 1;
   b.match = a.match + cb;
   b.nmatches = &S.nmatches;
-  match_bow_body(b, B, nullptr);
+  match_bow_body<CAP, 256>(b, B, nullptr);
 }
 
-// one workgroup per stream, or (a.list) a small grid looping over the listed
+// one workgroup per stream, or (a.list) a grid looping over the listed
 // streams (the map model's TrackReferenceKeyFrame streams)
+template <int CAP>
 __global__ void __launch_bounds__(256) k_trk_bow(TrkArgs a) {
-  __shared__ BowShared B;
+  __shared__ BowShared<CAP> B;
   if (a.list) {
     const int n = *a.list_n;
     for (int b = blockIdx.x; b < n; b += gridDim.x) {
-      trk_bow_stream(a, B, a.list[b]);
+      trk_bow_stream<CAP>(a, B, a.list[b]);
       __syncthreads();
     }
   } else {
-    trk_bow_stream(a, B, blockIdx.x);
+    trk_bow_stream<CAP>(a, B, blockIdx.x);
   }
 }
 
 void launch_trk_bow(const TrkArgs& a, int nstreams, hipStream_t s) {
-  const int grid = a.list ? (nstreams < kListGrid ? nstreams : kListGrid) : nstreams;
-  hipLaunchKernelGGL(k_trk_bow, dim3(grid), dim3(256), 0, s, a);
+  // a listed launch: one workgroup per stream up to kTrkGrid (the list is on
+  // the device; an empty list costs every workgroup one load)
+  static const int env_grid = getenv("ORBPL_TRK_GRID") ? atoi(getenv("ORBPL_TRK_GRID")) : 0;
+  const int cap_grid = env_grid > 0 ? env_grid : kTrkGrid;
+  const int grid = a.list ? (nstreams < cap_grid ? nstreams : cap_grid) : nstreams;
+  if (a.kp_pitch <= 1024)
+    hipLaunchKernelGGL(k_trk_bow<1024>, dim3(grid), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_trk_bow<kBowMax>, dim3(grid), dim3(256), 0, s, a);
 }
 
 }  // namespace orbpl

@@ -88,6 +88,8 @@ struct PoseLaunch {
 // as TrackReferenceKeyFrame): small enough to place quickly beside the
 // extraction kernels when the list is empty
 constexpr int kListGrid = 256;
+// k_trk_bow's listed launch: one workgroup per listed stream up to this many
+constexpr int kTrkGrid = 1024;
 
 // Per-frame line buffers of the tracker (kLineKeep lines per stream).
 struct LineTrackArgs {

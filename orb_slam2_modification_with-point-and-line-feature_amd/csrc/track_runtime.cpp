@@ -1420,6 +1420,21 @@ int orbpl_tracker_reset(orbpl_tracker* t, const float* Tcw0) {
   return ORBPL_OK;
 }
 
+int orbpl_tracker_clear_velocity(orbpl_tracker* t, const uint8_t* mask) {
+  if (!t || !mask) return arg_fail("orbpl_tracker_clear_velocity: NULL argument");
+  HIP_CHECK(hipSetDevice(t->device));
+  if (t->cstream) HIP_CHECK(hipStreamSynchronize(t->cstream));
+  HIP_CHECK(hipStreamSynchronize(t->stream));
+  if (t->tstream) HIP_CHECK(hipStreamSynchronize(t->tstream));
+  DBuf d;
+  HIP_CHECK(d.alloc((size_t)t->S));
+  HIP_CHECK(hipMemcpy(d.p, mask, (size_t)t->S, hipMemcpyHostToDevice));
+  launch_clear_velocity(t->map ? t->ma.ms : nullptr, t->d_state, d.as<uint8_t>(), t->S, nullptr);
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipDeviceSynchronize());
+  return ORBPL_OK;
+}
+
 }  // extern "C"
 
 // Tracking::Track with the map model (ORBPL_TRACK_MAP) on the tracking stream:

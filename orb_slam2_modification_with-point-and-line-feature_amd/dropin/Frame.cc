@@ -1,6 +1,8 @@
 // Drop-in ORB_SLAM2::Frame (see Frame.h).
 #include "Frame.h"
 
+#include "KeyFrame.h"
+
 #include <stdexcept>
 #include <thread>
 
@@ -9,6 +11,7 @@ namespace ORB_SLAM2 {
 float Frame::fx, Frame::fy, Frame::cx, Frame::cy, Frame::invfx, Frame::invfy;
 float Frame::mnMinX, Frame::mnMaxX, Frame::mnMinY, Frame::mnMaxY;
 long unsigned int Frame::nNextId = 0;
+long unsigned int KeyFrame::nNextId = 0;
 
 static void check(int rc) {
   if (rc != ORBPL_OK) throw std::runtime_error(orbpl_last_error());
@@ -22,10 +25,10 @@ orbpl_camera Frame::Camera() const {
 }
 
 Frame::Frame(const cv::Mat& imGray, const cv::Mat& imDepth, const double& timeStamp,
-             ORBextractor* extractor, void*, cv::Mat& K, cv::Mat& distCoef, const float& bf,
-             const float& thDepth, LineExtractor* lineExtractor)
+             ORBextractor* extractor, ORBVocabulary* voc, cv::Mat& K, cv::Mat& distCoef,
+             const float& bf, const float& thDepth, LineExtractor* lineExtractor)
     : mTimeStamp(timeStamp), mK(K.clone()), mDistCoef(distCoef.clone()), mbf(bf),
-      mThDepth(thDepth) {
+      mThDepth(thDepth), mpORBvocabulary(voc) {
   mnId = nNextId++;
   mnScaleLevels = extractor->GetLevels();
   mfScaleFactor = extractor->GetScaleFactor();
@@ -97,6 +100,63 @@ Frame::Frame(const cv::Mat& imGray, const cv::Mat& imDepth, const double& timeSt
                                  mvuRightLineStart.data(), mvuRightLineEnd.data()));
   mvpMapLines.assign(NL, nullptr);
   mvbLineOutlier.assign(NL, false);
+}
+
+void Frame::ComputeBoW() {
+  if (!mBowVec.empty()) return;
+  if (!mpORBvocabulary) throw std::runtime_error("Frame::ComputeBoW: no vocabulary");
+  mpORBvocabulary->transform(toDescriptorVector(mDescriptors), mBowVec, mFeatVec, 4);
+}
+
+int Frame::IsInFrustumBatch(const std::vector<MapPoint*>& vp, float viewingCosLimit,
+                            std::vector<uint8_t>* in_view) {
+  const int M = (int)vp.size();
+  std::vector<float> xyz(3 * (size_t)M), nrm(3 * (size_t)M), dmin(M), dmax(M);
+  std::vector<float> px(M), py(M), pxr(M), vcos(M);
+  std::vector<int32_t> level(M);
+  std::vector<uint8_t> iv(M);
+  for (int j = 0; j < M; j++) {
+    const cv::Mat X = vp[j]->GetWorldPos(), Nv = vp[j]->GetNormal();
+    for (int k = 0; k < 3; k++) {
+      xyz[3 * j + k] = X.at<float>(k, 0);
+      nrm[3 * j + k] = Nv.at<float>(k, 0);
+    }
+    dmin[j] = vp[j]->GetMinDistanceInvariance();
+    dmax[j] = vp[j]->GetMaxDistanceInvariance();
+  }
+  const orbpl_camera cam = Camera();
+  check(orbpl_frame_is_in_frustum(&cam, mfScaleFactor, mnScaleLevels, mTcw.ptr<float>(), M,
+                                  xyz.data(), nrm.data(), dmin.data(), dmax.data(),
+                                  viewingCosLimit, iv.data(), px.data(), py.data(), pxr.data(),
+                                  level.data(), vcos.data()));
+  int n = 0;
+  for (int j = 0; j < M; j++) {
+    MapPoint* p = vp[j];
+    p->mbTrackInView = iv[j] != 0;
+    if (!iv[j]) continue;   // the reference sets the projection only when in view
+    p->mTrackProjX = px[j];
+    p->mTrackProjY = py[j];
+    p->mTrackProjXR = pxr[j];
+    p->mnTrackScaleLevel = level[j];
+    p->mTrackViewCos = vcos[j];
+    n++;
+  }
+  if (in_view) in_view->assign(iv.begin(), iv.end());
+  return n;
+}
+
+bool Frame::IsInFrustum(MapPoint* pMP, float viewingCosLimit) {
+  return IsInFrustumBatch(std::vector<MapPoint*>{pMP}, viewingCosLimit) == 1;
+}
+
+bool Frame::IsInFrustum(MapLine* pML, float viewingCosLimit) {
+  const Eigen::Vector3d s = pML->GetWorldStartPos(), e = pML->GetWorldEndPos();
+  // the reference casts both end points to float (cv::Mat_<float>, Frame.cc:408-409)
+  const float xyz6[6] = {(float)s[0], (float)s[1], (float)s[2], (float)e[0], (float)e[1], (float)e[2]};
+  uint8_t iv = 0;
+  check(orbl_frame_is_in_frustum(mTcw.ptr<float>(), 1, xyz6, &iv));
+  pML->mbTrackInView = iv != 0;
+  return iv != 0;
 }
 
 void Frame::SetPose(cv::Mat Tcw) {

@@ -8,6 +8,7 @@
 
 #include "LineExtractor.h"
 #include "MapPoint.h"
+#include "ORBVocabulary.h"
 #include "ORBextractor.h"
 
 namespace ORB_SLAM2 {
@@ -19,10 +20,24 @@ class Frame {
  public:
   Frame() = default;
   Frame(const Frame&) = default;
-  // RGB-D (Frame.cc:135-205); voc is accepted for the signature and unused
+  // RGB-D (Frame.cc:135-205); voc is kept for ComputeBoW (may be NULL when
+  // the caller never computes a BoW)
   Frame(const cv::Mat& imGray, const cv::Mat& imDepth, const double& timeStamp,
-        ORBextractor* extractor, void* voc, cv::Mat& K, cv::Mat& distCoef, const float& bf,
-        const float& thDepth, LineExtractor* lineExtractor = nullptr);
+        ORBextractor* extractor, ORBVocabulary* voc, cv::Mat& K, cv::Mat& distCoef,
+        const float& bf, const float& thDepth, LineExtractor* lineExtractor = nullptr);
+
+  // Frame::ComputeBoW (Frame.cc:721-735): mBowVec / mFeatVec at levelsup 4
+  void ComputeBoW();
+  // Frame::IsInFrustum (Frame.cc:345-401, 403-430): the map point's / line's
+  // mbTrackInView and (points) mTrackProjX / Y / XR, mnTrackScaleLevel,
+  // mTrackViewCos, through orbpl_frame_is_in_frustum / orbl_frame_is_in_frustum
+  bool IsInFrustum(MapPoint* pMP, float viewingCosLimit);
+  bool IsInFrustum(MapLine* pML, float viewingCosLimit);
+  // Extension: the same for a whole local map in one call (Tracking::
+  // SearchLocalPoints' loop, Tracking.cc:1780-1795, without a device round
+  // trip per point); in_view[i] per point, returns the number in view
+  int IsInFrustumBatch(const std::vector<MapPoint*>& vpMapPoints, float viewingCosLimit,
+                       std::vector<uint8_t>* in_view = nullptr);
 
   void SetPose(cv::Mat Tcw);
   void UpdatePoseMatrices();
@@ -46,6 +61,9 @@ class Frame {
   std::vector<cv::KeyPoint> mvKeys, mvKeysUn;
   std::vector<float> mvuRight, mvDepth;
   cv::Mat mDescriptors;
+  ORBVocabulary* mpORBvocabulary = nullptr;
+  DBoW2::BowVector mBowVec;
+  DBoW2::FeatureVector mFeatVec;
   std::vector<MapPoint*> mvpMapPoints;
   std::vector<bool> mvbOutlier;
   std::vector<KeyLine> mvKeyLines, mvKeyLinesUn;

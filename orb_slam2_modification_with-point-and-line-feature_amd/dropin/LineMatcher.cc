@@ -1,6 +1,7 @@
 // Drop-in ORB_SLAM2::LineMatcher (see LineMatcher.h).
 #include "LineMatcher.h"
 
+#include <algorithm>
 #include <stdexcept>
 
 namespace ORB_SLAM2 {
@@ -39,6 +40,52 @@ int LineMatcher::SearchByProjection(Frame& Cur, const Frame& Last) {
   for (int j = 0; j < Cur.NL; j++)
     Cur.mvpMapLines[j] = match[j] >= 0 ? Last.mvpMapLines[match[j]] : nullptr;
   return n;
+}
+
+// both list overloads: projection + Liang-Barsky of the valid map lines, all
+// LineMatching pairs against the current lines whose map line has no
+// observations, the relaxed retry (which first clears F.mvpMapLines)
+static int search_list(Frame& F, const std::vector<MapLine*>& ml, const std::vector<uint8_t>& valid) {
+  const int M = (int)ml.size(), NLc = F.NL;
+  std::vector<float> xyz(6 * (size_t)(M > 0 ? M : 1), 0.f);
+  cv::Mat desc(M > 0 ? M : 1, 32, cv::CV_8U);
+  for (int i = 0; i < M; i++) {
+    const MapLine* l = ml[i];
+    if (!l) continue;
+    for (int k = 0; k < 3; k++) {
+      xyz[6 * i + k] = (float)l->mStart3d[k];
+      xyz[6 * i + 3 + k] = (float)l->mEnd3d[k];
+    }
+    std::memcpy(desc.ptr<uint8_t>(i), l->mLineDescriptor.data, 32);
+  }
+  std::vector<int32_t> curNobs(NLc > 0 ? NLc : 1, 0), match(NLc > 0 ? NLc : 1, -1);
+  for (int j = 0; j < NLc; j++)
+    if (F.mvpMapLines[j]) curNobs[j] = F.mvpMapLines[j]->Observations();
+  const orbpl_camera cam = F.Camera();
+  int n = 0, wiped = 0;
+  if (orbl_search_by_projection_list(&cam, F.mTcw.ptr<float>(), NLc,
+                                     reinterpret_cast<const orbpl_keyline*>(F.mvKeyLinesUn.data()),
+                                     F.mLineDescriptors.data, curNobs.data(), M, valid.data(),
+                                     xyz.data(), desc.data, match.data(), &n, &wiped) != ORBPL_OK)
+    throw std::runtime_error(orbpl_last_error());
+  if (wiped) std::fill(F.mvpMapLines.begin(), F.mvpMapLines.end(), nullptr);
+  for (int j = 0; j < NLc; j++)
+    if (match[j] >= 0) F.mvpMapLines[j] = ml[match[j]];
+  return n;
+}
+
+int LineMatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* RefFrame) {
+  const std::vector<MapLine*>& ml = RefFrame->mvpMapLines;
+  std::vector<uint8_t> valid(ml.size() > 0 ? ml.size() : 1, 0);
+  for (size_t i = 0; i < ml.size(); i++) valid[i] = ml[i] != nullptr;   // LineMatcher.cpp:562-564
+  return search_list(CurrentFrame, ml, valid);
+}
+
+int LineMatcher::SearchByProjection(Frame& F, const std::vector<MapLine*>& vpMapLines) {
+  std::vector<uint8_t> valid(vpMapLines.size() > 0 ? vpMapLines.size() : 1, 0);
+  for (size_t i = 0; i < vpMapLines.size(); i++)   // LineMatcher.cpp:788-793
+    valid[i] = vpMapLines[i]->mbTrackInView && !vpMapLines[i]->isBad();
+  return search_list(F, vpMapLines, valid);
 }
 
 }  // namespace ORB_SLAM2

@@ -46,31 +46,27 @@ int ORBmatcher::SearchByProjection(Frame& Cur, const Frame& Last, const float th
   return nmatches;
 }
 
-int ORBmatcher::SearchByProjection(Frame& F, const std::vector<LocalPoint>& vp, const float th) {
+int ORBmatcher::SearchByProjection(Frame& F, const std::vector<MapPoint*>& vp, const float th) {
   const int M = (int)vp.size(), N = F.N;
-  std::vector<float> xyz(3 * (size_t)M), nrm(3 * (size_t)M), dmin(M), dmax(M);
   std::vector<float> px(M), py(M), pxr(M), vcos(M);
   std::vector<int32_t> level(M), nobs(M), curNobs(N, 0), match(N, -1);
   std::vector<uint8_t> inView(M);
   cv::Mat desc(M > 0 ? M : 1, 32, cv::CV_8U);
   for (int j = 0; j < M; j++) {
-    cv::Mat X = vp[j].mp->GetWorldPos();
-    for (int k = 0; k < 3; k++) {
-      xyz[3 * j + k] = X.at<float>(k, 0);
-      nrm[3 * j + k] = vp[j].normal[k];
-    }
-    dmin[j] = vp[j].min_dist;
-    dmax[j] = vp[j].max_dist;
-    std::memcpy(desc.ptr<uint8_t>(j), vp[j].mp->GetDescriptor().data, 32);
-    nobs[j] = vp[j].mp->Observations();
+    const MapPoint* p = vp[j];
+    // ORBmatcher.cc:91-98: only points IsInFrustum put in view, and not bad
+    inView[j] = p->mbTrackInView && !p->isBad();
+    px[j] = p->mTrackProjX;
+    py[j] = p->mTrackProjY;
+    pxr[j] = p->mTrackProjXR;
+    level[j] = p->mnTrackScaleLevel;
+    vcos[j] = p->mTrackViewCos;
+    std::memcpy(desc.ptr<uint8_t>(j), p->GetDescriptor().data, 32);
+    nobs[j] = p->Observations();
   }
   for (int i = 0; i < N; i++)
     if (F.mvpMapPoints[i]) curNobs[i] = F.mvpMapPoints[i]->Observations();
   const orbpl_camera cam = F.Camera();
-  check(orbpl_frame_is_in_frustum(&cam, F.mfScaleFactor, F.mnScaleLevels, F.mTcw.ptr<float>(), M,
-                                  xyz.data(), nrm.data(), dmin.data(), dmax.data(), 0.5f,
-                                  inView.data(), px.data(), py.data(), pxr.data(), level.data(),
-                                  vcos.data()));
   const orbpl_match_current c{N, F.mTcw.ptr<float>(),
                               reinterpret_cast<const orbpl_keypoint*>(F.mvKeysUn.data()),
                               F.mDescriptors.data, F.mvuRight.data()};
@@ -79,9 +75,40 @@ int ORBmatcher::SearchByProjection(Frame& F, const std::vector<LocalPoint>& vp, 
                                         inView.data(), px.data(), py.data(), pxr.data(),
                                         level.data(), vcos.data(), desc.data, nobs.data(),
                                         curNobs.data(), th, mfNNratio, match.data(), &n));
-  for (int j = 0; j < M; j++) vp[j].mp->mbTrackInView = inView[j] != 0;
   for (int i = 0; i < N; i++)
-    if (match[i] >= 0) F.mvpMapPoints[i] = vp[match[i]].mp;
+    if (match[i] >= 0) F.mvpMapPoints[i] = vp[match[i]];
+  return n;
+}
+
+// the FeatureVector as one node id per feature (-1: none)
+static std::vector<int32_t> nodes_of(const DBoW2::FeatureVector& fv, int n) {
+  std::vector<int32_t> node(n > 0 ? n : 1, -1);
+  for (const auto& kv : fv)
+    for (unsigned i : kv.second)
+      if ((int)i < n) node[i] = (int32_t)kv.first;
+  return node;
+}
+
+int ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, std::vector<MapPoint*>& vpMapPointMatches) {
+  const std::vector<MapPoint*> vpMapPointsKF = pKF->GetMapPointMatches();
+  vpMapPointMatches.assign(F.N, nullptr);
+  const int nkf = pKF->N, nf = F.N;
+  const std::vector<int32_t> kf_node = nodes_of(pKF->mFeatVec, nkf), f_node = nodes_of(F.mFeatVec, nf);
+  std::vector<uint8_t> kf_valid(nkf > 0 ? nkf : 1, 0);
+  std::vector<float> kf_angle(nkf > 0 ? nkf : 1), f_angle(nf > 0 ? nf : 1);
+  for (int i = 0; i < nkf; i++) {
+    const MapPoint* p = vpMapPointsKF[i];
+    kf_valid[i] = p && !p->isBad();   // ORBmatcher.cc:298-303
+    kf_angle[i] = pKF->mvKeysUn[i].angle;
+  }
+  for (int j = 0; j < nf; j++) f_angle[j] = F.mvKeys[j].angle;
+  std::vector<int32_t> match(nf > 0 ? nf : 1, -1);
+  int n = 0;
+  check(orbm_search_by_bow(nkf, kf_node.data(), kf_valid.data(), pKF->mDescriptors.data,
+                           kf_angle.data(), nf, f_node.data(), F.mDescriptors.data, f_angle.data(),
+                           mfNNratio, mbCheckOrientation ? 1 : 0, match.data(), &n));
+  for (int j = 0; j < nf; j++)
+    if (match[j] >= 0) vpMapPointMatches[j] = vpMapPointsKF[match[j]];
   return n;
 }
 

@@ -1,9 +1,10 @@
-// Drop-in ORB_SLAM2::ORBmatcher, per-frame overloads (include/ORBmatcher.h:49-90,
-// src/ORBmatcher.cc:72-183, 1710-1879, 2083-2103) over orbm_*.
+// Drop-in ORB_SLAM2::ORBmatcher, the tracking overloads (include/ORBmatcher.h:
+// 49-140, src/ORBmatcher.cc:72-183, 247-410, 1710-1879, 2083-2103) over orbm_*.
 #pragma once
 #include <vector>
 
 #include "Frame.h"
+#include "KeyFrame.h"
 
 namespace ORB_SLAM2 {
 
@@ -19,14 +20,14 @@ class ORBmatcher {
                          const bool bMono);
 
   // Tracking::SearchLocalPoints (Tracking.cc:1812): the map points'
-  // IsInFrustum outputs are computed here from their world positions, normals
-  // and distance invariances (given per point by the caller's map)
-  struct LocalPoint {
-    MapPoint* mp;
-    float normal[3];
-    float min_dist, max_dist;   // GetMinDistanceInvariance / GetMaxDistanceInvariance
-  };
-  int SearchByProjection(Frame& F, const std::vector<LocalPoint>& vpMapPoints, const float th = 3);
+  // mbTrackInView / mTrackProj* / mnTrackScaleLevel / mTrackViewCos, as
+  // Frame::IsInFrustum left them (ORBmatcher.h:74, ORBmatcher.cc:72-183)
+  int SearchByProjection(Frame& F, const std::vector<MapPoint*>& vpMapPoints, const float th = 3);
+
+  // Tracking::TrackReferenceKeyFrame (Tracking.cc:958): the keyframe's and the
+  // frame's FeatureVectors (ComputeBoW first), ORBmatcher.h:140,
+  // ORBmatcher.cc:247-410
+  int SearchByBoW(KeyFrame* pKF, Frame& F, std::vector<MapPoint*>& vpMapPointMatches);
 
   float mfNNratio;
   bool mbCheckOrientation;

@@ -1,23 +1,49 @@
-// Exercises the drop-in classes the way Tracking uses them for the first two
-// RGB-D frames (StereoInitialization-style map from frame 0, then
-// TrackWithMotionModel's matching and pose for frame 1, Tracking.cc:608-690,
-// 1212-1271), and writes every output for tests/test_gpu_dropin.py to check
-// against the oracle.
+// Exercises the drop-in classes the way Tracking uses them on three RGB-D
+// frames and writes every output for tests/test_gpu_dropin.py to check
+// against the oracle:
+//   frame 0: StereoInitialization-style map (Tracking.cc:608-690): a map
+//            point per keypoint with depth, a map line per line with both
+//            end-point depths; the initial keyframe KF0 with its BoW;
+//   frame 1: TrackWithMotionModel's matching and pose with zero velocity
+//            (Tracking.cc:1228-1271);
+//   frame 2: TrackReferenceKeyFrame against KF0 (Tracking.cc:942-1032:
+//            ComputeBoW, ORBmatcher(0.7).SearchByBoW, the last frame's pose,
+//            LineMatcher(0.7).SearchByProjection(F, KF), the pose, the outlier
+//            discard), then TrackLocalMap with KF0 as the local map
+//            (Tracking.cc:1332-1420, 1746-1865: IsInFrustum,
+//            ORBmatcher(0.8).SearchByProjection(F, points, 3),
+//            LineMatcher(0.8).SearchByProjection(F, lines), the second pose).
 //   dropin_driver <in.bin> <out.bin>
 // in.bin : int32 W, H; float fx fy cx cy k1 k2 p1 p2 k3 bf thdepth;
 //          int32 nfeatures; float scale; int32 nlevels, iniTh, minTh;
-//          float Tcw0[16]; gray0 (W*H u8), depth0 (W*H f32), gray1, depth1
+//          float Tcw0[16]; 3 x (gray W*H u8, depth W*H f32);
+//          int32 len; vocabulary path (len bytes, DBoW2 text format)
 // out.bin: per frame: N, kps (N x 28 B), desc (N x 32), NL, keylines (NL x
 //          68 B), line desc (NL x 32), coef (NL x 3 f64), keysUn (N x 28 B),
 //          depth (N f32); frame 0's pyramid: nlevels x (w, h, w*h bytes);
-//          then nmatches, line matches, inliers, Tcw1[16], match[N1] (frame-0
-//          index or -1), outlier[N1] u8, line match[NL1], line outlier[NL1] u8
+//          frame 1: nmatches, line matches, inliers, Tcw1[16], match[N1]
+//          (frame-0 index or -1), outlier[N1] u8, line match[NL1], line
+//          outlier[NL1] u8;
+//          the map of frame 0: per keypoint has_mp u8, xyz f32x3, normal
+//          f32x3, min / max distance invariance f32x2; per line has_ml u8,
+//          xyz6 f32x6; the FeatureVector node of every frame-0 and frame-2
+//          feature (int32, -1 none);
+//          frame 2, TrackReferenceKeyFrame: nmatches, bow match[N2], line
+//          nmatches, line match[NL2], go, inliers, Tcw[16], outlier[N2] u8,
+//          line outlier[NL2] u8, nmatchesMap, line_nmatchesMap;
+//          TrackLocalMap: seen[N0] u8 (skipped: matched by frame 2), in_view
+//          [N0] u8, local nmatches, match[N2] after the search, line seen
+//          [NL0], line in_view[NL0], local line nmatches, line match[NL2],
+//          inliers, Tcw[16]
+#include <cmath>
 #include <cstdio>
 #include <map>
 #include <memory>
+#include <string>
 #include <vector>
 
 #include "Frame.h"
+#include "KeyFrame.h"
 #include "LineMatcher.h"
 #include "ORBmatcher.h"
 #include "Optimizer.h"
@@ -26,11 +52,15 @@ using namespace ORB_SLAM2;
 
 template <class T>
 static void rd(FILE* f, T* p, size_t n) {
-  if (fread(p, sizeof(T), n, f) != n) throw std::runtime_error("short input");
+  if (n && fread(p, sizeof(T), n, f) != n) throw std::runtime_error("short input");
 }
 template <class T>
 static void wr(FILE* f, const T* p, size_t n) {
   if (n && fwrite(p, sizeof(T), n, f) != n) throw std::runtime_error("short write");
+}
+template <class T>
+static void wr1(FILE* f, T v) {
+  wr(f, &v, 1);
 }
 
 static void write_frame(FILE* o, const Frame& F) {
@@ -43,6 +73,19 @@ static void write_frame(FILE* o, const Frame& F) {
   for (int i = 0; i < F.NL; i++) wr(o, F.mvKeyLineCoefficient[i].v, 3);
   wr(o, F.mvKeysUn.data(), F.N);
   wr(o, F.mvDepth.data(), F.N);
+}
+
+// index of a frame-0 map element in the frame-0 feature indexing (-1: NULL)
+template <class P>
+static void write_index(FILE* o, const std::vector<P*>& v, std::map<const P*, int>& idx) {
+  for (P* p : v) wr1<int32_t>(o, p ? idx.at(p) : -1);
+}
+
+static std::vector<int32_t> node_of(const DBoW2::FeatureVector& fv, int n) {
+  std::vector<int32_t> node(n, -1);
+  for (const auto& kv : fv)
+    for (unsigned i : kv.second) node[i] = (int32_t)kv.first;
+  return node;
 }
 
 int main(int argc, char** argv) {
@@ -66,13 +109,21 @@ int main(int argc, char** argv) {
     rd(in, &mn, 1);
     rd(in, Tcw0, 16);
     const int W = wh[0], H = wh[1];
-    cv::Mat g0(H, W, cv::CV_8U), d0(H, W, cv::CV_32F), g1(H, W, cv::CV_8U), d1(H, W, cv::CV_32F);
-    rd(in, g0.data, (size_t)W * H);
-    rd(in, d0.ptr<float>(), (size_t)W * H);
-    rd(in, g1.data, (size_t)W * H);
-    rd(in, d1.ptr<float>(), (size_t)W * H);
+    std::vector<cv::Mat> g(3), d(3);
+    for (int k = 0; k < 3; k++) {
+      g[k] = cv::Mat(H, W, cv::CV_8U);
+      d[k] = cv::Mat(H, W, cv::CV_32F);
+      rd(in, g[k].data, (size_t)W * H);
+      rd(in, d[k].ptr<float>(), (size_t)W * H);
+    }
+    int32_t plen = 0;
+    rd(in, &plen, 1);
+    std::string vpath(plen, '\0');
+    rd(in, &vpath[0], plen);
     fclose(in);
 
+    ORBVocabulary voc;
+    if (!voc.loadFromTextFile(vpath)) throw std::runtime_error("cannot load the vocabulary");
     // Tracking::Tracking: K, DistCoef, mbf, mThDepth = bf * ThDepth / fx
     // (Tracking.cc:54-138)
     cv::Mat K = cv::Mat::eye(3, 3, cv::CV_32F);
@@ -84,11 +135,11 @@ int main(int argc, char** argv) {
     for (int k = 0; k < 5; k++) dist.at<float>(k, 0) = camv[4 + k];
     const float bf = camv[9], thDepth = camv[10];
     ORBextractor ex(nf, sf, nl, ini, mn);
-    Frame F0(g0, d0, 0.0, &ex, nullptr, K, dist, bf, thDepth);
+    Frame F0(g[0], d[0], 0.0, &ex, &voc, K, dist, bf, thDepth);
     std::vector<cv::Mat> pyr = ex.mvImagePyramid;
-    Frame F1(g1, d1, 1.0, &ex, nullptr, K, dist, bf, thDepth);
+    Frame F1(g[1], d[1], 1.0, &ex, &voc, K, dist, bf, thDepth);
 
-    // frame 0: pose Tcw0, map points / lines from depth (Tracking.cc:633-692)
+    // ---- frame 0: pose Tcw0, map points / lines from depth (Tracking.cc:633-692)
     cv::Mat T0(4, 4, cv::CV_32F);
     std::memcpy(T0.data, Tcw0, 64);
     F0.SetPose(T0);
@@ -96,10 +147,22 @@ int main(int argc, char** argv) {
     std::vector<std::unique_ptr<MapLine>> mls;
     std::map<const MapPoint*, int> mp_index;
     std::map<const MapLine*, int> ml_index;
+    const cv::Mat Ow = F0.GetCameraCenter();
     for (int i = 0; i < F0.N; i++) {
       if (!(F0.mvDepth[i] > 0)) continue;
       cv::Mat X = F0.UnprojectStereo(i);
       mps.emplace_back(new MapPoint(X.ptr<float>(), F0.mDescriptors.ptr<uint8_t>(i)));
+      // MapPoint::UpdateNormalAndDepth with the one observation (MapPoint.cc:360-411)
+      float nrm[3];
+      double dd = 0;
+      for (int k = 0; k < 3; k++) {
+        nrm[k] = X.at<float>(k, 0) - Ow.at<float>(k, 0);
+        dd += (double)nrm[k] * nrm[k];
+      }
+      const float dn = (float)std::sqrt(dd);
+      for (int k = 0; k < 3; k++) nrm[k] = nrm[k] * (1.0f / dn);
+      const float maxd = dn * F0.mvScaleFactors[F0.mvKeysUn[i].octave];
+      mps.back()->SetNormalAndDistances(nrm, maxd / F0.mvScaleFactors[F0.mnScaleLevels - 1], maxd);
       F0.mvpMapPoints[i] = mps.back().get();
       mp_index[mps.back().get()] = i;
     }
@@ -112,8 +175,11 @@ int main(int argc, char** argv) {
       F0.mvpMapLines[j] = mls.back().get();
       ml_index[mls.back().get()] = j;
     }
+    // the initial keyframe (Tracking.cc:637-640: KeyFrame + ComputeBoW)
+    KeyFrame KF0(F0);
+    KF0.ComputeBoW();
 
-    // frame 1: TrackWithMotionModel with zero velocity (Tracking.cc:1228-1271)
+    // ---- frame 1: TrackWithMotionModel with zero velocity (Tracking.cc:1228-1271)
     F1.SetPose(F0.mTcw);
     ORBmatcher matcher(0.9f, true);
     LineMatcher line_matcher(0.9f, true);
@@ -141,25 +207,165 @@ int main(int argc, char** argv) {
     wr(o, &line_nmatches, 1);
     wr(o, &ninl, 1);
     wr(o, F1.mTcw.ptr<float>(), 16);
-    for (int i = 0; i < F1.N; i++) {
-      const int m = F1.mvpMapPoints[i] ? mp_index[F1.mvpMapPoints[i]] : -1;
-      wr(o, &m, 1);
+    write_index(o, F1.mvpMapPoints, mp_index);
+    for (int i = 0; i < F1.N; i++) wr1<uint8_t>(o, F1.mvbOutlier[i]);
+    write_index(o, F1.mvpMapLines, ml_index);
+    for (int j = 0; j < F1.NL; j++) wr1<uint8_t>(o, F1.mvbLineOutlier[j]);
+
+    // ---- the map of frame 0 and the FeatureVectors
+    for (int i = 0; i < F0.N; i++) {
+      const MapPoint* p = F0.mvpMapPoints[i];
+      wr1<uint8_t>(o, p != nullptr);
+      float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      if (p) {
+        const cv::Mat X = p->GetWorldPos(), Nv = p->GetNormal();
+        for (int k = 0; k < 3; k++) {
+          v[k] = X.at<float>(k, 0);
+          v[3 + k] = Nv.at<float>(k, 0);
+        }
+        v[6] = p->GetMinDistanceInvariance();
+        v[7] = p->GetMaxDistanceInvariance();
+      }
+      wr(o, v, 8);
     }
-    for (int i = 0; i < F1.N; i++) {
-      const uint8_t b = F1.mvbOutlier[i];
-      wr(o, &b, 1);
+    for (int j = 0; j < F0.NL; j++) {
+      const MapLine* l = F0.mvpMapLines[j];
+      wr1<uint8_t>(o, l != nullptr);
+      float v[6] = {0, 0, 0, 0, 0, 0};
+      if (l)
+        for (int k = 0; k < 3; k++) {
+          v[k] = (float)l->mStart3d[k];
+          v[3 + k] = (float)l->mEnd3d[k];
+        }
+      wr(o, v, 6);
     }
-    for (int j = 0; j < F1.NL; j++) {
-      const int m = F1.mvpMapLines[j] ? ml_index[F1.mvpMapLines[j]] : -1;
-      wr(o, &m, 1);
+
+    // ---- frame 2: TrackReferenceKeyFrame against KF0 (Tracking.cc:942-1032)
+    Frame F2(g[2], d[2], 2.0, &ex, &voc, K, dist, bf, thDepth);
+    F2.ComputeBoW();
+    const std::vector<int32_t> n0 = node_of(KF0.mFeatVec, KF0.N), n2 = node_of(F2.mFeatVec, F2.N);
+    wr(o, n0.data(), n0.size());
+    write_frame(o, F2);
+    wr(o, n2.data(), n2.size());
+    ORBmatcher matcher7(0.7f, true);
+    LineMatcher line_matcher7(0.7f, true);
+    std::vector<MapPoint*> vpMapPointMatches;
+    int nm2 = matcher7.SearchByBoW(&KF0, F2, vpMapPointMatches);
+    F2.SetPose(F1.mTcw);
+    const int nlm2 = line_matcher7.SearchByProjection(F2, &KF0);
+    wr(o, &nm2, 1);
+    write_index(o, vpMapPointMatches, mp_index);
+    wr(o, &nlm2, 1);
+    write_index(o, F2.mvpMapLines, ml_index);
+    const int go = nm2 >= 15 && nlm2 >= 10;
+    int ninl2 = 0, nmatchesMap = 0, line_nmatchesMap = 0;
+    if (go) {
+      F2.mvpMapPoints = vpMapPointMatches;
+      ninl2 = Optimizer::PoseOptimizationWithLines(&F2);
     }
-    for (int j = 0; j < F1.NL; j++) {
-      const uint8_t b = F1.mvbLineOutlier[j];
-      wr(o, &b, 1);
+    wr(o, &go, 1);
+    wr(o, &ninl2, 1);
+    wr(o, F2.mTcw.ptr<float>(), 16);
+    for (int i = 0; i < F2.N; i++) wr1<uint8_t>(o, F2.mvbOutlier[i]);
+    for (int j = 0; j < F2.NL; j++) wr1<uint8_t>(o, F2.mvbLineOutlier[j]);
+    if (go) {
+      // the discard (Tracking.cc:999-1029)
+      for (int i = 0; i < F2.N; i++) {
+        if (!F2.mvpMapPoints[i]) continue;
+        if (F2.mvbOutlier[i]) {
+          MapPoint* p = F2.mvpMapPoints[i];
+          F2.mvpMapPoints[i] = nullptr;
+          F2.mvbOutlier[i] = false;
+          p->mbTrackInView = false;
+          p->mnLastFrameSeen = F2.mnId;
+        } else if (F2.mvpMapPoints[i]->Observations() > 0) {
+          nmatchesMap++;
+        }
+      }
+      for (int j = 0; j < F2.NL; j++) {
+        if (!F2.mvpMapLines[j]) continue;
+        if (F2.mvbLineOutlier[j]) {
+          MapLine* l = F2.mvpMapLines[j];
+          F2.mvpMapLines[j] = nullptr;
+          F2.mvbLineOutlier[j] = false;
+          l->mbTrackInView = false;
+          l->mnLastFrameSeen = F2.mnId;
+          line_nmatchesMap--;
+        } else if (F2.mvpMapLines[j]->Observations() > 0) {
+          line_nmatchesMap++;
+        }
+      }
     }
+    wr(o, &nmatchesMap, 1);
+    wr(o, &line_nmatchesMap, 1);
+
+    // ---- TrackLocalMap with KF0 as the local map (Tracking.cc:1746-1865)
+    std::vector<MapPoint*> local_points;   // UpdateLocalPoints: KF0's, index order
+    for (MapPoint* p : KF0.GetMapPointMatches())
+      if (p) local_points.push_back(p);
+    std::vector<MapLine*> local_lines;
+    for (MapLine* l : KF0.mvpMapLines)
+      if (l) local_lines.push_back(l);
+    // SearchLocalPoints
+    for (MapPoint* p : F2.mvpMapPoints)
+      if (p) {
+        p->mnLastFrameSeen = F2.mnId;
+        p->mbTrackInView = false;
+      }
+    std::vector<uint8_t> seen(F0.N, 0), inview(F0.N, 0);
+    int nToMatch = 0;
+    for (MapPoint* p : local_points) {
+      const int i = mp_index.at(p);
+      if (p->mnLastFrameSeen == F2.mnId) {
+        seen[i] = 1;
+        continue;
+      }
+      if (p->isBad()) continue;
+      if (F2.IsInFrustum(p, 0.5f)) {
+        inview[i] = 1;
+        nToMatch++;
+      }
+    }
+    int nlocal = 0;
+    if (nToMatch > 0) nlocal = ORBmatcher(0.8f).SearchByProjection(F2, local_points, 3);
+    wr(o, seen.data(), seen.size());
+    wr(o, inview.data(), inview.size());
+    wr(o, &nlocal, 1);
+    write_index(o, F2.mvpMapPoints, mp_index);
+    // SearchLocalLines
+    for (MapLine* l : F2.mvpMapLines)
+      if (l) {
+        l->mnLastFrameSeen = F2.mnId;
+        l->mbTrackInView = false;
+      }
+    std::vector<uint8_t> lseen(F0.NL, 0), linview(F0.NL, 0);
+    int nlToMatch = 0;
+    for (MapLine* l : local_lines) {
+      const int j = ml_index.at(l);
+      if (l->mnLastFrameSeen == F2.mnId) {
+        lseen[j] = 1;
+        continue;
+      }
+      if (l->isBad()) continue;
+      if (F2.IsInFrustum(l, 0.5f)) {
+        linview[j] = 1;
+        nlToMatch++;
+      }
+    }
+    int nllocal = 0;
+    if (nlToMatch > 0) nllocal = LineMatcher(0.8f).SearchByProjection(F2, local_lines);
+    wr(o, lseen.data(), lseen.size());
+    wr(o, linview.data(), linview.size());
+    wr(o, &nllocal, 1);
+    write_index(o, F2.mvpMapLines, ml_index);
+    const int ninl3 = Optimizer::PoseOptimizationWithLines(&F2);
+    wr(o, &ninl3, 1);
+    wr(o, F2.mTcw.ptr<float>(), 16);
     fclose(o);
-    printf("dropin: N0 %d NL0 %d N1 %d NL1 %d matches %d line matches %d inliers %d\n", F0.N,
-           F0.NL, F1.N, F1.NL, nmatches, line_nmatches, ninl);
+    printf("dropin: N0 %d NL0 %d N1 %d NL1 %d matches %d line matches %d inliers %d | "
+           "TRK bow %d lines %d inliers %d | local %d lines %d inliers %d\n",
+           F0.N, F0.NL, F1.N, F1.NL, nmatches, line_nmatches, ninl, nm2, nlm2, ninl2, nlocal,
+           nllocal, ninl3);
   } catch (const std::exception& e) {
     fprintf(stderr, "dropin_driver: %s\n", e.what());
     return 1;

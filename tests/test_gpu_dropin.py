@@ -1,9 +1,13 @@
 """The compiled C++ drop-in classes (orb_slam2_..._amd/dropin: ORBextractor,
-LineExtractor, Frame, ORBmatcher, LineMatcher, Optimizer with the reference's
-signatures, g++-built, linked to liborbpl.so) against the oracle: two RGB-D
-frames through extraction, frame glue, the first frame's map, the second
-frame's SearchByProjection (points and lines) and PoseOptimizationWithLines.
-The driver binary reads / writes flat files (dropin_driver.cpp's header)."""
+LineExtractor, Frame, KeyFrame, ORBVocabulary, ORBmatcher, LineMatcher,
+Optimizer with the reference's signatures, g++-built, linked to liborbpl.so)
+against the oracle: three RGB-D frames through extraction, frame glue, the
+first frame's map and keyframe (ComputeBoW), the second frame's
+TrackWithMotionModel (SearchByProjection points / lines, the pose), the third
+frame's TrackReferenceKeyFrame (SearchByBoW, the reference-keyframe line
+overload, the pose, the discard) and TrackLocalMap (IsInFrustum,
+SearchByProjection over the local map points / lines, the second pose). The
+driver binary reads / writes flat files (dropin_driver.cpp's header)."""
 import struct
 import subprocess
 from pathlib import Path
@@ -32,14 +36,36 @@ def _frame(buf, off, KP, KL):
     return dict(kps=kps, desc=desc, kl=kl, ldesc=ld, coef=coef, kps_un=ku, depth=dep), off
 
 
+class _Reader:
+    def __init__(self, buf):
+        self.buf, self.off = buf, 0
+
+    def i32(self, n=None):
+        k = 1 if n is None else n
+        a = np.frombuffer(self.buf, np.int32, k, self.off)
+        self.off += 4 * k
+        return int(a[0]) if n is None else a
+
+    def arr(self, dt, n, shape=None):
+        a = np.frombuffer(self.buf, dt, n, self.off)
+        self.off += a.nbytes
+        return a.reshape(shape) if shape else a
+
+    def frame(self, KP, KL):
+        F, self.off = _frame(self.buf, self.off, KP, KL)
+        return F
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("cam_name,seed", [("TUM1", 5), ("TUM3", 8)])
 def test_dropin_classes_match_oracle(tmp_path, cam_name, seed):
     pkg = load_pkg()
     O = load_oracle()
     assert DRIVER.exists(), "build the drop-in first (make -C .../dropin)"
-    cfg, traj, frames = sequence(2, seed, cam_name=cam_name)
-    (g0, d0), (g1, d1) = frames
+    from _vocab import vocabulary
+    vpath, _ = vocabulary(k=10, L=5, seed=3, n_frames=8)
+    cfg, traj, frames = sequence(3, seed, cam_name=cam_name)
+    (g0, d0), (g1, d1), (g2, d2) = frames
     H, W = g0.shape
     orb = (1000, 1.2, 8, 20, 7)
     T0 = np.linalg.inv(traj[0]).astype(np.float32)
@@ -55,34 +81,44 @@ def test_dropin_classes_match_oracle(tmp_path, cam_name, seed):
         for g, d in frames:
             f.write(np.ascontiguousarray(g, np.uint8).tobytes())
             f.write(np.ascontiguousarray(d, np.float32).tobytes())
+        pb = str(vpath).encode()
+        f.write(struct.pack("<i", len(pb)) + pb)
     out = tmp_path / "out.bin"
     r = subprocess.run([str(DRIVER), str(inp), str(out)], capture_output=True, text=True,
-                       timeout=120)
+                       timeout=300)
     assert r.returncode == 0, r.stderr
-    buf = out.read_bytes()
+    R = _Reader(out.read_bytes())
     KP, KL = O.KP_DTYPE, O.KEYLINE_DTYPE
-    F0, off = _frame(buf, 0, KP, KL)
-    F1, off = _frame(buf, off, KP, KL)
+    F0 = R.frame(KP, KL)
+    F1 = R.frame(KP, KL)
     p = O.params(*orb)
-    for F, (g, d) in zip((F0, F1), frames):
+
+    def check_frame(F, g, d):
         okps, odesc, _ = O.extract(p, g)
         assert F["kps"].tobytes() == okps.tobytes()
         assert np.array_equal(F["desc"], odesc)
         okl, old, ocoef, _ = O.line_extract(g)
         assert F["kl"].tobytes() == okl.tobytes()
         assert np.array_equal(F["ldesc"], old) and np.array_equal(F["coef"], ocoef)
-        ku, dep, _, _, _ = O.frame_prepare(cam, okps, d)
+        ku, dep, ur, _, _ = O.frame_prepare(cam, okps, d)
         assert F["kps_un"].tobytes() == ku.tobytes() and np.array_equal(F["depth"], dep)
+        F["uright"] = ur
+        F["kl_un"] = O.line_frame_prepare(cam, okl, d)[0]
+
+    check_frame(F0, g0, d0)
+    check_frame(F1, g1, d1)
     # ORBextractor::mvImagePyramid of frame 0 = the oracle's level contents
-    (nlev,) = struct.unpack_from("<i", buf, off); off += 4
+    nlev = R.i32()
     opyr = O.pyramid(p, g0)
     for lv in range(nlev):
-        w, h = struct.unpack_from("<2i", buf, off); off += 8
-        img = np.frombuffer(buf, np.uint8, w * h, off).reshape(h, w); off += w * h
+        w, h = R.i32(2)
+        img = R.arr(np.uint8, w * h, (h, w))
         assert np.array_equal(img, opyr[lv][19:19 + h, 19:19 + w]), lv
-    nm, nlm, ninl = struct.unpack_from("<3i", buf, off); off += 12
-    T1 = np.frombuffer(buf, np.float32, 16, off).reshape(4, 4); off += 64
-    # the oracle's tracking loop over the same two frames (TrackWithMotionModel,
+    nm, nlm, ninl = R.i32(3)
+    T1 = R.arr(np.float32, 16, (4, 4))
+    R.i32(F1["kps"].size), R.arr(np.uint8, F1["kps"].size)
+    R.i32(F1["kl"].size), R.arr(np.uint8, F1["kl"].size)
+    # the oracle's tracking loop over the first two frames (TrackWithMotionModel,
     # no local map: the driver's sequence)
     lvo = O.LVO(p, cam, 1, use_lines=True)
     lvo.reset(T0.reshape(1, 16))
@@ -91,3 +127,118 @@ def test_dropin_classes_match_oracle(tmp_path, cam_name, seed):
     assert (nm, nlm, ninl) == (so["nmatches"], so["line_matches"], so["ninliers"])
     assert nm > 50 and nlm >= 15
     assert np.abs(T1 - To).max() < 1e-4
+
+    # frame 0's map and the FeatureVectors (Frame / KeyFrame::ComputeBoW)
+    N0, NL0 = len(F0["kps"]), len(F0["kl"])
+    mp = R.arr(np.dtype([("has", "u1"), ("v", "<f4", 8)]), N0)
+    ml = R.arr(np.dtype([("has", "u1"), ("v", "<f4", 6)]), NL0)
+    has_mp, has_ml = mp["has"].astype(np.uint8), ml["has"].astype(np.uint8)
+    assert np.array_equal(has_mp, (F0["depth"] > 0).astype(np.uint8))
+    node0 = R.i32(N0)
+    F2 = R.frame(KP, KL)
+    check_frame(F2, g2, d2)
+    N2, NL2 = len(F2["kps"]), len(F2["kl"])
+    node2 = R.i32(N2)
+    voc = O.Vocabulary(vpath)
+    assert np.array_equal(node0, voc.transform(F0["desc"], 4)[2])
+    assert np.array_equal(node2, voc.transform(F2["desc"], 4)[2])
+
+    # TrackReferenceKeyFrame: SearchByBoW(KF0, F2), LineMatcher(0.7)(F2, KF0)
+    nb = R.i32()
+    bow = R.i32(N2)
+    mb_o, nb_o = O.search_by_bow(node0, has_mp, F0["desc"], F0["kps_un"]["angle"], node2,
+                                 F2["desc"], F2["kps"]["angle"], 0.7, True)
+    assert nb == nb_o and np.array_equal(bow, mb_o), (nb, nb_o)
+    assert nb > 20
+    nlb = R.i32()
+    lbm = R.i32(NL2)
+    xyz6 = ml["v"]
+    ml_o, nl_o, _ = O.line_search_by_projection_list(cam, T1, F2["kl_un"], F2["ldesc"], None,
+                                                      has_ml, xyz6, F0["ldesc"])
+    assert nlb == nl_o and np.array_equal(lbm, ml_o)
+    go, ninl2 = R.i32(2)
+    T2 = R.arr(np.float32, 16, (4, 4))
+    out2, lout2 = R.arr(np.uint8, N2), R.arr(np.uint8, NL2)
+    nmap, lnmap = R.i32(2)
+    assert go == int(nb >= 15 and nlb >= 10)
+    lw, lh, nfl, scl, isc = O.level_sizes(p, W, H)
+    isg = (1.0 / (scl * scl)).astype(np.float32)
+
+    def pose(match, lmatch, T):
+        prob = dict(kps_un=F2["kps_un"], uright=F2["uright"], has_mp=(match >= 0).astype(np.uint8),
+                    mp_xyz=np.where((match >= 0)[:, None], mp["v"][np.maximum(match, 0), :3], 0),
+                    inv_sigma2=isg,
+                    kl_obs=np.stack([F2["kl_un"][k] for k in ("startPointX", "startPointY",
+                                                              "endPointX", "endPointY")], 1),
+                    kl_octave=F2["kl_un"]["octave"], has_ml=(lmatch >= 0).astype(np.uint8),
+                    ml_xyz=np.where((lmatch >= 0)[:, None], xyz6[np.maximum(lmatch, 0)], 0))
+        return O.pose_optimization(cam, prob, T, np.zeros(N2, np.uint8), np.zeros(NL2, np.uint8))
+
+    m2, l2 = bow.copy(), lbm.copy()
+    Tcur = T1
+    if go:
+        To2, oo, lo, no = pose(m2, l2, T1)
+        assert np.abs(T2 - To2).max() < 1e-4 and ninl2 == no
+        assert np.array_equal(out2, oo) and np.array_equal(lout2, lo)
+        m2[(m2 >= 0) & (oo == 1)] = -1
+        l2[(l2 >= 0) & (lo == 1)] = -1
+        assert nmap == int((m2 >= 0).sum())
+        Tcur = T2
+    else:
+        assert np.array_equal(T2, T1)
+        m2[:] = -1          # the matches stay in vpMapPointMatches (Tracking.cc:968-973)
+
+    # TrackLocalMap over KF0: SearchLocalPoints
+    seen, inview = R.arr(np.uint8, N0), R.arr(np.uint8, N0)
+    nloc = R.i32()
+    mloc = R.i32(N2)
+    want_seen = np.zeros(N0, np.uint8)
+    want_seen[m2[m2 >= 0]] = 1
+    if go:   # the discarded outliers are marked seen too (Tracking.cc:1006-1011)
+        want_seen[bow[(bow >= 0) & (oo == 1)]] = 1
+    assert np.array_equal(seen, want_seen)
+    loc = np.nonzero(has_mp)[0]          # UpdateLocalPoints: KF0's map points in index order
+    mps = dict(xyz=mp["v"][loc, :3], normal=mp["v"][loc, 3:6], min_dist=mp["v"][loc, 6],
+               max_dist=mp["v"][loc, 7])
+    tr = O.frame_is_in_frustum(cam, float(np.float32(O.lsdm(1, float(np.float32(1.2))))), 8,
+                               Tcur, mps, 0.5)
+    tr["in_view"] = tr["in_view"] & (seen[loc] == 0)
+    assert np.array_equal(inview[loc], tr["in_view"]) and not inview[has_mp == 0].any()
+    cur = dict(kps_un=F2["kps_un"], desc=F2["desc"], uright=F2["uright"])
+    if tr["in_view"].any():
+        mlo, nlo = O.search_by_projection_local(cam, scl, cur, tr, F0["desc"][loc],
+                                                np.ones(len(loc), np.int32),
+                                                (m2 >= 0).astype(np.int32), 3.0, 0.8)
+    else:
+        mlo, nlo = np.full(N2, -1, np.int32), 0
+    want = m2.copy()
+    want[mlo >= 0] = loc[mlo[mlo >= 0]]
+    assert nloc == nlo and np.array_equal(mloc, want), (nloc, nlo)
+    # SearchLocalLines
+    lseen, linview = R.arr(np.uint8, NL0), R.arr(np.uint8, NL0)
+    nlloc = R.i32()
+    lloc = R.i32(NL2)
+    want_ls = np.zeros(NL0, np.uint8)
+    want_ls[l2[l2 >= 0]] = 1
+    if go:
+        want_ls[lbm[(lbm >= 0) & (lo == 1)]] = 1
+    assert np.array_equal(lseen, want_ls)
+    lid = np.nonzero(has_ml)[0]
+    lv = O.line_is_in_frustum(Tcur, xyz6[lid]) & (lseen[lid] == 0)
+    assert np.array_equal(linview[lid], lv)
+    want_l = l2.copy()
+    if lv.any():
+        mll, nll, wiped = O.line_search_by_projection_list(
+            cam, Tcur, F2["kl_un"], F2["ldesc"], (l2 >= 0).astype(np.int32), lv, xyz6[lid],
+            F0["ldesc"][lid])
+        if wiped:
+            want_l[:] = -1
+        want_l[mll >= 0] = lid[mll[mll >= 0]]
+    else:
+        nll = 0
+    assert nlloc == nll and np.array_equal(lloc, want_l), (nlloc, nll)
+    ninl3 = R.i32()
+    T3 = R.arr(np.float32, 16, (4, 4))
+    To3, _, _, no3 = pose(mloc, lloc, Tcur)
+    assert np.abs(T3 - To3).max() < 1e-4 and ninl3 == no3
+    assert R.off == len(R.buf)

@@ -14,7 +14,21 @@ pytestmark = pytest.mark.gpu
 POSE_TOL = 1e-4   # north_star: pose within 1e-4 RMSE (max-abs used here: stricter)
 
 
-def _run(orbpl, oracle, lines, refkf, S, F, seed, turn=None, pipelined=False):
+def _vocab_arrays(L, seed=3):
+    """A seeded k = 10 vocabulary of depth L as arrays (no text round trip:
+    L = 6 has 1.1M nodes, ORB-SLAM2's ORBvoc shape)."""
+    import orbpl.synth as synth
+    from _vocab import training_descriptors
+    tree = synth.vocabulary_tree(training_descriptors(8), k=10, L=L, seed=seed)
+    return dict(parent=tree["parent"], leaf=tree["leaf"], desc=tree["desc"], weight=tree["weight"],
+                k=10, L=L, scoring=0, weighting=0)
+
+
+def _run(orbpl, oracle, lines, refkf, S, F, seed, turn=None, pipelined=False, clears=None,
+         vocab_levels=5):
+    """clears: {frame: [streams]} whose velocity is cleared before that
+    frame's step (orbpl_tracker_clear_velocity / MapVO.clear_velocity)."""
+    clears = clears or {}
     seqs = [sequence(F, seed + s, cam_name="TUM3" if lines else "TUM1") for s in range(S)]
     frames = [[sq[2][f] for f in range(F)] for sq in seqs]
     if turn is not None:
@@ -27,7 +41,12 @@ def _run(orbpl, oracle, lines, refkf, S, F, seed, turn=None, pipelined=False):
     mvo = oracle.MapVO(oracle.params(), oracle.camera(cfg), S, use_lines=lines, flags=flags)
     tr = orbpl.Tracker(orbpl.OrbParams(1000, 1.2, 8, 20, 7), orbpl.make_camera(cfg), S, lines=lines,
                        refkf=refkf, map=True)
-    if refkf:
+    if refkf and vocab_levels != 5:
+        arr = _vocab_arrays(vocab_levels)
+        voc = orbpl.ORBVocabulary(arrays=arr)
+        mvo.set_vocabulary(oracle.Vocabulary(arrays=arr))
+        tr.set_vocabulary(voc, 4)
+    elif refkf:
         from _vocab import vocabulary
         path, _ = vocabulary(k=10, L=5, seed=3, n_frames=8)
         voc = orbpl.ORBVocabulary(path)
@@ -44,9 +63,16 @@ def _run(orbpl, oracle, lines, refkf, S, F, seed, turn=None, pipelined=False):
     for f in range(F):
         a.upload(np.stack([frames[s][f][0] for s in range(S)]), offset=f * fa)
         b.upload(np.stack([frames[s][f][1] for s in range(S)]), offset=f * fb)
+        if f in clears:
+            tr.clear_velocity(np.isin(np.arange(S), clears[f]))
         tr.step_device(a.ptr + f * fa, b.ptr + f * fb)
     tr.synchronize()
-    ref = [[mvo.step(s, *frames[s][f]) for f in range(F)] for s in range(S)]
+    ref = [[None] * F for _ in range(S)]
+    for s in range(S):
+        for f in range(F):
+            if s in clears.get(f, ()):
+                mvo.clear_velocity(s)
+            ref[s][f] = mvo.step(s, *frames[s][f])
     keys = orbpl.Tracker.MAP_COUNTS
     assert tuple(keys) == tuple(oracle.MAP_COUNTS)
     out = []
@@ -149,3 +175,21 @@ def test_map_capacity_flag(orbpl, oracle, monkeypatch):
     err = tr.map_errors()
     assert (err & 1).any(), err
     assert all(tr.map_keyframes(s)[0].shape[0] <= 2 for s in range(S))
+
+
+@pytest.mark.parametrize("lines,vocab_levels,pipelined", [(False, 5, True), (True, 6, False),
+                                                          (False, 6, True)])
+def test_map_tracker_reference_keyframe_under_load(orbpl, oracle, lines, vocab_levels, pipelined):
+    """TrackReferenceKeyFrame for many streams at once: velocities cleared
+    for half the streams at frame 3 and for all at frame 5 (as after a
+    relocalisation), so those frames run SearchByBoW + the reference-keyframe
+    pose; with a 6-level vocabulary (ORBvoc's depth: FeatureVector nodes at
+    level 2) and a 5-level one. Every count, pose and the maps equal the
+    oracle's."""
+    S = 4
+    res = _run(orbpl, oracle, lines, True, S=S, F=7, seed=170, pipelined=pipelined,
+               clears={3: [1, 3], 5: list(range(S))}, vocab_levels=vocab_levels)
+    for s, r in enumerate(res):
+        assert r[5]["trk"] == 1
+        assert r[3]["trk"] == (1 if s in (1, 3) else r[3]["trk"])
+        assert r[5]["ok"] == 1 and r[5]["nmatches"] >= 15, r[5]
