@@ -72,13 +72,13 @@ WORKLOADS = {
     "lines": dict(cam="TUM3", orb=ORB, lines=True, stereo=False,
                   desc="TUM fr3_structure_texture_far-like RGB-D, ORB + LSD/LBD lines (configs[2])",
                   data="synthetic (seeded textured-room RGB-D loop, TUM3 intrinsics, no distortion)"),
-    "kitti": dict(cam="KITTI00", orb=(2000, 1.2, 8, 20, 7), lines=True, stereo=True,
+    "kitti": dict(cam="KITTI00", orb=(2000, 1.2, 8, 20, 7), lines=True, stereo=True, fps=10,
                   desc="KITTI 00-like stereo 1241x376, ORB 2000 + LSD/LBD on both images, "
                        "ComputeStereoMatches + stereo line depths (defined mode P17) + "
                        "PoseOptimizationWithLines (configs[3])",
                   data="synthetic (seeded textured-room rectified stereo loop, KITTI 00 intrinsics, "
                        "bf 386.1448)"),
-    "kitti_points": dict(cam="KITTI00", orb=(2000, 1.2, 8, 20, 7), lines=False, stereo=True,
+    "kitti_points": dict(cam="KITTI00", orb=(2000, 1.2, 8, 20, 7), lines=False, stereo=True, fps=10,
                          desc="KITTI 00-like stereo 1241x376, ORB 2000 both images + "
                               "ComputeStereoMatches + PoseOptimization (points only)",
                          data="synthetic (seeded textured-room rectified stereo loop, KITTI 00 "
@@ -271,8 +271,8 @@ def oracle_vocabulary(O):
 
 def map_mode(args, wl):
     """Tracking::Track with the reference's map model (ORBPL_TRACK_MAP) for
-    the RGB-D workloads; the stereo ones keep the P18 local map."""
-    return bool(args.map) and not wl["stereo"]
+    every workload (RGB-D and, through orbpl_tracker_step_stereo, stereo)."""
+    return bool(args.map)
 
 
 def leg_summary(out):
@@ -328,7 +328,9 @@ def oracle_vo(O, wl, flags=0, use_map=False):
     import orbpl.synth as synth
     cam = O.camera(getattr(synth, wl["cam"]))
     if use_map:
-        vo = O.MapVO(O.params(*wl["orb"]), cam, 1, use_lines=wl["lines"], flags=flags)
+        vo = O.MapVO(O.params(*wl["orb"]), cam, 1, use_lines=wl["lines"],
+                     flags=flags | (O.TRACK_STEREO if wl["stereo"] else 0))
+        vo.set_fps(wl.get("fps", 30))
     else:
         vo = O.LVO(O.params(*wl["orb"]), cam, 1, use_lines=wl["lines"], flags=flags)
     voc = oracle_vocabulary(O)
@@ -525,6 +527,8 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
                      local_map=bool(args.local_map) and not use_map,
                      fixed_line_jac=bool(args.fixed_line_jacobian),
                      refkf=bool(args.refkf and voc is not None), map=use_map)
+    if use_map:
+        tr.set_fps(wl.get("fps", 30))   # Camera.fps: mMaxFrames (KITTI 10, TUM 30)
     # pipelining overlaps extraction of step t+1 with tracking of step t, for
     # every workload (lines too: the next batch's LSD overlaps this batch's
     # matching and pose, 9.5k -> 9.8k frames/s at 3072 streams)
@@ -910,7 +914,10 @@ def cpu_reference_faithful(gray, depth, L, workload, flags=0, warmup=20, frames=
     wl = WORKLOADS[workload]
     cam = O.camera(getattr(synth, wl["cam"]))
     mk = O.MapVO if use_map else O.LVO
-    vo = mk(O.params(*wl["orb"]), cam, 1, use_lines=wl["lines"], flags=O.TWO_THREADS | flags)
+    st_flag = O.TRACK_STEREO if (use_map and wl["stereo"]) else 0
+    vo = mk(O.params(*wl["orb"]), cam, 1, use_lines=wl["lines"], flags=O.TWO_THREADS | flags | st_flag)
+    if use_map:
+        vo.set_fps(wl.get("fps", 30))
     voc = oracle_vocabulary(O)
     if voc is not None:
         vo.set_vocabulary(voc)

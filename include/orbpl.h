@@ -425,7 +425,11 @@ int orbpl_tracker_create(const orbpl_orb_params* orb, const orbpl_camera* cam, i
  * (at most one per step). Pinned P23-P25
  * (DESIGN.md): LocalMapping = its ProcessNewKeyFrame run synchronously,
  * Relocalization fails; pointer-ordered containers in keyframe id order.
- * Replaces ORBPL_TRACK_LOCAL_MAP (its P18 local map); not with STEREO. */
+ * Replaces ORBPL_TRACK_LOCAL_MAP (its P18 local map). With ORBPL_TRACK_STEREO
+ * the same Track() on stereo frames (orbpl_tracker_step_stereo: depths from
+ * ComputeStereoMatches, line depths P17) with the reference's STEREO branches:
+ * motion-model radius 7, local-map radius 1, outlier matches dropped after
+ * TrackLocalMap's pose (Tracking.cc:1238-1241, 1374-1401, 1801-1809). */
 #define ORBPL_TRACK_MAP 32
 int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam, int n_streams,
                             int device, int flags, orbpl_tracker** out);
@@ -441,6 +445,10 @@ int orbpl_tracker_reset(orbpl_tracker* tr, const float* Tcw0);
  * zero velocity). Waits for the tracker's queued steps. Used to time and test
  * TrackReferenceKeyFrame under load. */
 int orbpl_tracker_clear_velocity(orbpl_tracker* tr, const uint8_t* mask);
+/* Camera.fps of the settings (ORBPL_TRACK_MAP trackers): mMaxFrames = fps,
+ * 0 -> 30 (Tracking.cc:81-87), read by NeedNewKeyFrame and TrackLocalMap's
+ * recent-relocalisation test. Default 30 (TUM); KITTI's settings say 10. */
+int orbpl_tracker_set_fps(orbpl_tracker* tr, float fps);
 /* One step for all streams. d_gray: n_streams frames of width*height u8;
  * d_depth: n_streams frames of width*height float metres (device memory,
  * contiguous). Asynchronous on the tracker's stream. */

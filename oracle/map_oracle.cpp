@@ -50,7 +50,6 @@
 namespace mapvo {
 
 constexpr int kKeepLines = 80;
-constexpr int kMaxFrames = 30;   // mMaxFrames = Camera.fps (TUM1.yaml)
 constexpr int kMinFrames = 0;
 
 // ---- float matrix helpers (pinned P6: double accumulation, one rounding) ----
@@ -195,6 +194,8 @@ struct MapVO {
   orbpl_camera cam;
   int use_lines = 1;
   int flags = 0;
+  int stereo = 0;          // System::STEREO (ORBPL_TRACK_STEREO flag)
+  int max_frames = 30;     // mMaxFrames = Camera.fps (Tracking.cc:81-87)
   void* voc = nullptr;
   std::vector<float> scale, inv_sigma2;
   float log_scale;
@@ -400,8 +401,13 @@ static MapPoint new_point(const float* pos, int kf) {
 // Frame::Frame(RGB-D) (Frame.cc:135-205). flags & kTwoThreads: ORB and the
 // LineExtractor on two host threads as the reference (Frame.cc:152-155).
 constexpr int kTwoThreads = 1 << 16;
-static void extract(MapVO* v, const uint8_t* gray, const float* depth, Frame& F) {
+// right != NULL: Frame::Frame(stereo) (Frame.cc:70-131): ORB on both images,
+// ComputeStereoMatches on the two pyramids, and the defined stereo line mode
+// (P17: LineExtractor on the right image, end-point depths by line matching).
+static void extract(MapVO* v, const uint8_t* gray, const float* depth, Frame& F,
+                    const uint8_t* right = nullptr) {
   const orbpl_camera& cam = v->cam;
+  if (right) depth = nullptr;
   std::vector<orbpl_keyline> kl(kKeepLines);
   std::vector<uint8_t> ld(kKeepLines * 32);
   std::vector<double> coef(kKeepLines * 3);
@@ -429,6 +435,27 @@ static void extract(MapVO* v, const uint8_t* gray, const float* depth, Frame& F)
   std::vector<int32_t> gc(n);
   oracle_frame_prepare(&cam, kps.data(), n, depth, F.kps_un.data(), F.depth.data(), F.uright.data(),
                        gc.data(), nullptr);
+  if (right) {
+    const int cap2 = v->orb.nfeatures * 2 + 64;
+    std::vector<orbpl_keypoint> kr(cap2);
+    std::vector<uint8_t> dr((size_t)cap2 * 32);
+    int nr = 0;
+    oracle_orb_extract(&v->orb, right, cam.width, cam.height, cam.width, kr.data(), dr.data(), cap2,
+                       &nr, nullptr);
+    const int L = v->orb.nlevels;
+    std::vector<int32_t> lw(L), lh(L);
+    std::vector<float> sc(L), isc(L);
+    oracle_orb_level_sizes(&v->orb, cam.width, cam.height, lw.data(), lh.data(), nullptr, sc.data(),
+                           isc.data());
+    size_t tot = 0;
+    for (int l = 0; l < L; l++) tot += (size_t)(lw[l] + 38) * (lh[l] + 38);
+    std::vector<uint8_t> pl(tot), pr(tot);
+    oracle_orb_pyramid(&v->orb, gray, cam.width, cam.height, cam.width, pl.data(), 0);
+    oracle_orb_pyramid(&v->orb, right, cam.width, cam.height, cam.width, pr.data(), 0);
+    oracle_stereo_matches(&cam, sc.data(), isc.data(), L, lw.data(), lh.data(), pl.data(), pr.data(),
+                          kps.data(), desc.data(), n, kr.data(), dr.data(), nr, F.uright.data(),
+                          F.depth.data());
+  }
   F.desc = desc;
   F.angle.resize(n);
   for (int i = 0; i < n; i++) F.angle[i] = kps[i].angle;
@@ -453,6 +480,16 @@ static void extract(MapVO* v, const uint8_t* gray, const float* depth, Frame& F)
     oracle_line_frame_prepare(&cam, kl.data(), nl, depth, F.kl_un.data(), F.dstart.data(),
                               F.dend.data(), urs.data(), ure.data());
     F.ldesc.assign(ld.begin(), ld.begin() + (size_t)nl * 32);
+    if (right) {
+      std::vector<orbpl_keyline> klr(kKeepLines);
+      std::vector<uint8_t> ldr(kKeepLines * 32);
+      std::vector<double> coefr(kKeepLines * 3);
+      int nr = 0, ndr = 0;
+      oracle_line_extract(right, cam.width, cam.height, klr.data(), ldr.data(), coefr.data(),
+                          kKeepLines, &nr, &ndr);
+      oracle_stereo_line_depths(&cam, F.kl_un.data(), F.ldesc.data(), nl, klr.data(), ldr.data(), nr,
+                                F.dstart.data(), F.dend.data());
+    }
   }
   F.ml.assign(F.NL, -1);
   F.loutl.assign(F.NL, 0);
@@ -652,7 +689,7 @@ static bool track_motion(MapVO* v, Stream& S, Frame& F, TrackOut& o) {
   }
   std::fill(F.mp.begin(), F.mp.end(), -1);
   std::fill(F.ml.begin(), F.ml.end(), -1);
-  const float th = 15.0f;
+  const float th = v->stereo ? 7.0f : 15.0f;   // Tracking.cc:1238-1241
   o.nmatches = search_last(v, S, F, th);
   o.nlm = v->use_lines ? search_last_lines(v, S, F) : 0;
   if (o.nmatches < 20) {
@@ -823,7 +860,7 @@ static bool track_local_map(MapVO* v, Stream& S, Frame& F, LocalOut& o) {
   }
   for (int i = 0; i < F.N; i++) cur_nobs[i] = F.mp[i] != -1 ? mp_nobs(S, F.mp[i]) : 0;
   if (nto > 0) {
-    const float th = F.id < 2 ? 5.0f : 3.0f;
+    const float th = F.id < 2 ? 5.0f : (v->stereo ? 1.0f : 3.0f);   // Tracking.cc:1801-1809
     orbpl_match_current cur{F.N, F.Tcw, F.kps_un.data(), F.desc.data(), F.uright.data()};
     oracle_search_by_projection_local(&v->cam, v->scale.data(), (int)v->scale.size(), &cur, M,
                                       inview.data(), px.data(), py.data(), pxr.data(), lev.data(),
@@ -866,14 +903,20 @@ static bool track_local_map(MapVO* v, Stream& S, Frame& F, LocalOut& o) {
   o.linl = 0;
   for (int j = 0; j < F.NL; j++)
     if (F.ml[j] != -1 && !F.loutl[j] && ml_nobs(S, F.ml[j]) > 0) o.linl++;
-  if (F.id < 0 + kMaxFrames && o.inl + o.linl < 60) return false;
+  if (v->stereo) {   // an outlier's map point / line leaves the frame (Tracking.cc:1374-1401)
+    for (int i = 0; i < F.N; i++)
+      if (F.mp[i] != -1 && F.outl[i]) F.mp[i] = -1;
+    for (int j = 0; j < F.NL; j++)
+      if (F.ml[j] != -1 && F.loutl[j]) F.ml[j] = -1;
+  }
+  if (F.id < 0 + v->max_frames && o.inl + o.linl < 60) return false;
   return !(o.inl < 30 && o.linl < 20);
 }
 
 // Tracking::NeedNewKeyFrame (Tracking.cc:1423-1557) with the P23 stub
 static bool need_new_keyframe(MapVO* v, Stream& S, const Frame& F, int inliers) {
   const int nKFs = (int)S.kfs.size();
-  if (F.id < 0 + kMaxFrames && nKFs > kMaxFrames) return false;
+  if (F.id < 0 + v->max_frames && nKFs > v->max_frames) return false;
   const int nMinObs = nKFs <= 2 ? 2 : 3;
   const int nRefMatches = tracked_map_points(S, S.kfs[S.ref_kf], nMinObs);
   const bool idle = true;
@@ -886,7 +929,7 @@ static bool need_new_keyframe(MapVO* v, Stream& S, const Frame& F, int inliers) 
   const bool close = ntc < 100 && nntc > 70;
   float thRefRatio = 0.75f;
   if (nKFs < 2) thRefRatio = 0.4f;
-  const bool c1a = F.id >= S.last_kf_frame + kMaxFrames;
+  const bool c1a = F.id >= S.last_kf_frame + v->max_frames;
   const bool c1b = F.id >= S.last_kf_frame + kMinFrames && idle;
   const bool c1c = inliers < nRefMatches * 0.25 || close;
   const bool c2 = (inliers < nRefMatches * thRefRatio || close) && inliers > 15;
@@ -1010,10 +1053,11 @@ static void reset_stream(Stream& S) {
   std::memcpy(S.T0, T0, 64);
 }
 
-static int step(MapVO* v, int s, const uint8_t* gray, const float* depth, float* Tcw_out) {
+static int step(MapVO* v, int s, const uint8_t* gray, const float* depth, float* Tcw_out,
+                const uint8_t* right = nullptr) {
   Stream& S = v->st[s];
   Frame F;
-  extract(v, gray, depth, F);
+  extract(v, gray, depth, F, right);
   F.id = S.next_id++;
   int* out = S.out;
   std::memset(out, 0, sizeof(S.out));
@@ -1141,6 +1185,7 @@ void* oracle_map_create(const orbpl_orb_params* orb, const orbpl_camera* cam, in
   v->cam = *cam;
   v->flags = flags;
   v->use_lines = (flags & ORBPL_TRACK_LINES) ? 1 : 0;
+  v->stereo = (flags & ORBPL_TRACK_STEREO) ? 1 : 0;
   v->st.resize(n_streams);
   v->scale.resize(orb->nlevels);
   std::vector<float> isc(orb->nlevels);
@@ -1194,6 +1239,24 @@ int oracle_map_step(void* h, int stream, const uint8_t* gray, const float* depth
   if (Tcw_out) std::memcpy(Tcw_out, T, 64);
   if (out24) std::memcpy(out24, v->st[stream].out, sizeof(int) * 24);
   return rc;
+}
+
+// the stereo step: rectified left / right images (Tracking::GrabImageStereo)
+int oracle_map_step_stereo(void* h, int stream, const uint8_t* left, const uint8_t* right,
+                           float* Tcw_out, int* out24) {
+  mapvo::MapVO* v = static_cast<mapvo::MapVO*>(h);
+  if (stream < 0 || stream >= (int)v->st.size() || !right) return -1;
+  float T[16];
+  const int rc = mapvo::step(v, stream, left, nullptr, T, right);
+  if (Tcw_out) std::memcpy(Tcw_out, T, 64);
+  if (out24) std::memcpy(out24, v->st[stream].out, sizeof(int) * 24);
+  return rc;
+}
+
+// Camera.fps: mMaxFrames (0 -> 30, Tracking.cc:81-87)
+int oracle_map_set_fps(void* h, float fps) {
+  static_cast<mapvo::MapVO*>(h)->max_frames = (int)(fps == 0.0f ? 30.0f : fps);
+  return 0;
 }
 
 // the stream's map for tests: keyframe count; per keyframe its covisibility

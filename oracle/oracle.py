@@ -708,6 +708,8 @@ def _setup(L):  # noqa: F811
     L.oracle_map_destroy.argtypes = [vp]
     L.oracle_map_reset.argtypes = [vp, vp]
     L.oracle_map_clear_velocity.argtypes = [vp, i]
+    L.oracle_map_step_stereo.argtypes = [vp, i, vp, vp, vp, vp]
+    L.oracle_map_set_fps.argtypes = [vp, C.c_float]
     L.oracle_map_set_vocabulary.argtypes = [vp, vp]
     L.oracle_map_step.argtypes = [vp, i, vp, vp, vp, vp]
     L.oracle_map_keyframes.argtypes = [vp, i, vp, vp, i, vp]
@@ -754,6 +756,21 @@ class MapVO:
         rc = lib().oracle_map_step(self.h, stream, _p(g), _p(d), _p(T), _p(o))
         assert rc == 0
         return T.reshape(4, 4), dict(zip(MAP_COUNTS, (int(x) for x in o)))
+
+    def step_stereo(self, stream, left, right):
+        """Tracking::GrabImageStereo + Track() with the map model on a
+        rectified pair (ComputeStereoMatches, P17 line depths)."""
+        gl = _c(left, np.uint8)
+        gr = _c(right, np.uint8)
+        T = np.zeros(16, np.float32)
+        o = np.zeros(24, np.int32)
+        rc = lib().oracle_map_step_stereo(self.h, stream, _p(gl), _p(gr), _p(T), _p(o))
+        assert rc == 0
+        return T.reshape(4, 4), dict(zip(MAP_COUNTS, (int(x) for x in o)))
+
+    def set_fps(self, fps):
+        """Camera.fps: mMaxFrames (0 -> 30)."""
+        lib().oracle_map_set_fps(self.h, C.c_float(fps))
 
     def keyframes(self, stream, cap=64):
         par = np.zeros(256, np.int32)

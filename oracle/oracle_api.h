@@ -110,6 +110,9 @@ void* oracle_map_create(const orbpl_orb_params* orb, const orbpl_camera* cam, in
 void oracle_map_destroy(void* h);
 int oracle_map_reset(void* h, const float* Tcw0);
 int oracle_map_clear_velocity(void* h, int stream);
+int oracle_map_step_stereo(void* h, int stream, const uint8_t* left, const uint8_t* right,
+                           float* Tcw_out, int* out24);
+int oracle_map_set_fps(void* h, float fps);
 int oracle_map_set_vocabulary(void* h, void* voc);
 int oracle_map_step(void* h, int stream, const uint8_t* gray, const float* depth, float* Tcw_out,
                     int* out24);

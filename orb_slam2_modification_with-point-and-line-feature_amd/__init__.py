@@ -371,6 +371,7 @@ def _declare_track(L):
     L.orbpl_tracker_destroy.argtypes = [vp]
     L.orbpl_tracker_reset.argtypes = [vp, vp]
     L.orbpl_tracker_clear_velocity.argtypes = [vp, vp]
+    L.orbpl_tracker_set_fps.argtypes = [vp, C.c_float]
     L.orbpl_tracker_step.argtypes = [vp, vp, vp]
     L.orbpl_tracker_synchronize.argtypes = [vp]
     L.orbpl_tracker_set_pipelined.argtypes = [vp, C.c_int]
@@ -708,6 +709,10 @@ class Tracker:
         if m.size != self.S:
             raise ValueError("clear_velocity: one mask byte per stream")
         check(lib().orbpl_tracker_clear_velocity(self._h, _ptr(m)), "orbpl_tracker_clear_velocity")
+
+    def set_fps(self, fps):
+        """Camera.fps of the settings: mMaxFrames (map trackers; 0 -> 30)."""
+        check(lib().orbpl_tracker_set_fps(self._h, C.c_float(fps)), "orbpl_tracker_set_fps")
 
     def step_device(self, d_gray, d_depth):
         check(lib().orbpl_tracker_step(self._h, C.c_void_p(d_gray), C.c_void_p(d_depth)), "step")

@@ -49,6 +49,8 @@ struct MapArgs {
   int kfc, kp_pitch;
   long long mpc, mlc;
   int lines, refkf, vocab;
+  int stereo;              // System::STEREO: TrackLocalMap drops outlier matches (Tracking.cc:1374-1377)
+  int max_frames;          // mMaxFrames = Camera.fps (Tracking.cc:81-87; TUM 30, KITTI 10)
   // keyframes
   float* kf_T;            // [kfc][16]
   float* kf_Ow;           // [kfc][4]

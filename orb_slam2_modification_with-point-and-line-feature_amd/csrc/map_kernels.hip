@@ -36,7 +36,6 @@ namespace {
 
 constexpr int kT = 256;
 constexpr int kNotInit = 0, kOK = 1, kLost = 2;
-constexpr int kMaxFramesT = 30;   // mMaxFrames (Camera.fps 30, TUM)
 
 __device__ __forceinline__ int block_sum(int v, int* wsum) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -1142,15 +1141,18 @@ __global__ void __launch_bounds__(kT) k_map_finish(TrackConsts c, MapArgs a) {
         const long long o = P.cb + i;
         const int m = a.mpid[o];
         inl += m != -1 && !a.outlier[o] && P.mp_nobs(m) > 0;
+        // STEREO: an outlier's map point leaves the frame (Tracking.cc:1374-1377)
+        if (a.stereo && m != -1 && a.outlier[o]) a.mpid[o] = -1;
       }
       for (int j = t; j < nl; j += kT) {
         const long long o = P.lb + j;
         const int m = a.mlid[o];
         linl += m != -1 && !a.loutlier[o] && P.ml_nobs(m) > 0;
+        if (a.stereo && m != -1 && a.loutlier[o]) a.mlid[o] = -1;   // :1398-1401
       }
       inl = block_sum(inl, wsum);
       linl = block_sum(linl, wsum);
-      ok = !(fid < kMaxFramesT && inl + linl < 60) && !(inl < 30 && linl < 20);
+      ok = !(fid < a.max_frames && inl + linl < 60) && !(inl < 30 && linl < 20);
       if (t == 0) {
         S.lm_inl = inl;
         S.lm_linl = linl;
@@ -1214,11 +1216,11 @@ __global__ void __launch_bounds__(kT) k_map_finish(TrackConsts c, MapArgs a) {
       nntc = block_sum(nntc, wsum);
       const int inl = s_i[0];
       bool need = true;
-      if (fid < kMaxFramesT && nKFs > kMaxFramesT) need = false;
+      if (fid < a.max_frames && nKFs > a.max_frames) need = false;
       const bool close = ntc < 100 && nntc > 70;
       float thRefRatio = 0.75f;
       if (nKFs < 2) thRefRatio = 0.4f;
-      const bool c1a = fid >= M.last_kf_frame + kMaxFramesT;
+      const bool c1a = fid >= M.last_kf_frame + a.max_frames;
       const bool c1b = fid >= M.last_kf_frame + 0;   // && bLocalMappingIdle
       const bool c1c = inl < nref * 0.25 || close;
       const bool c2 = (inl < nref * thRefRatio || close) && inl > 15;

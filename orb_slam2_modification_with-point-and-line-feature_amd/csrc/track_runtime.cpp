@@ -968,6 +968,8 @@ static int map_alloc(orbpl_tracker* t, int kfc) {
   m.mpc = (long long)MPC;
   m.mlc = (long long)MLC;
   m.lines = t->lines;
+  m.stereo = t->stereo;
+  m.max_frames = 30;   // Camera.fps 30 (TUM); orbpl_tracker_set_fps
   m.lp = (long long)MPC;
   m.llp = (long long)MLC;
   MA(m.ms, S * sizeof(MapState));
@@ -1122,8 +1124,6 @@ int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam
   if (flags & ~(ORBPL_TRACK_LINES | ORBPL_TRACK_STEREO | ORBPL_TRACK_LOCAL_MAP |
                 ORBPL_TRACK_FIXED_LINE_JAC | ORBPL_TRACK_REFKF | ORBPL_TRACK_MAP))
     return arg_fail("unknown tracker flag");
-  if ((flags & ORBPL_TRACK_MAP) && (flags & ORBPL_TRACK_STEREO))
-    return arg_fail("ORBPL_TRACK_MAP: RGB-D streams only");
   // ORBPL_TRACK_LINES | ORBPL_TRACK_STEREO: the defined stereo line mode (P17;
   // the reference's stereo Frame extracts no lines, Frame.cc:70-131)
   if ((flags & ORBPL_TRACK_STEREO) && cam->height > 1024)
@@ -1420,6 +1420,15 @@ int orbpl_tracker_reset(orbpl_tracker* t, const float* Tcw0) {
   return ORBPL_OK;
 }
 
+int orbpl_tracker_set_fps(orbpl_tracker* t, float fps) {
+  if (!t) return arg_fail("NULL tracker");
+  if (!t->map) return arg_fail("tracker created without ORBPL_TRACK_MAP");
+  if (!(fps >= 0.0f) || fps > 1e6f) return arg_fail("orbpl_tracker_set_fps: fps out of range");
+  // Tracking::Tracking: if(fps==0) fps=30; mMaxFrames = fps (Tracking.cc:81-87)
+  t->ma.max_frames = (int)(fps == 0.0f ? 30.0f : fps);
+  return ORBPL_OK;
+}
+
 int orbpl_tracker_clear_velocity(orbpl_tracker* t, const uint8_t* mask) {
   if (!t || !mask) return arg_fail("orbpl_tracker_clear_velocity: NULL argument");
   HIP_CHECK(hipSetDevice(t->device));
@@ -1485,7 +1494,7 @@ static int map_track(orbpl_tracker* t, FrameBufs& C, FrameBufs& L, const LineTra
   m.match = C.match;
   m.nmatches = field(offsetof(StreamState, nmatches));
   m.nm_stride = pstride;
-  m.th = 15.0f;
+  m.th = t->stereo ? 7.0f : 15.0f;   // Tracking.cc:1238-1241
   m.mono = 0;
   m.check_ori = 1;
   m.retry = 1;
@@ -1621,7 +1630,8 @@ static int map_track(orbpl_tracker* t, FrameBufs& C, FrameBufs& L, const LineTra
   ml.view_cos = x.l_vcos;
   ml.mp_desc = a.l_ldesc_pts;
   ml.mp_nobs = nullptr;        // every local map point is observed
-  ml.th = t->lm_step < 2 ? 5.0f : 3.0f;   // mnLastRelocFrameId + 2 (Tracking.cc:1731-1738)
+  // RGB-D 3, stereo 1; 5 within mnLastRelocFrameId + 2 (Tracking.cc:1801-1809)
+  ml.th = t->lm_step < 2 ? 5.0f : (t->stereo ? 1.0f : 3.0f);
   ml.nnratio = 0.8f;
   ml.match = const_cast<int*>(a.lm_match);
   ml.nmatches = field(offsetof(StreamState, lm_nlocal));
