@@ -146,11 +146,42 @@ def level_areas(w=W, h=H, orb=ORB):
     return [int(a) * int(b) for a, b in zip(d["width"], d["height"])], d
 
 
-def algorithmic_bytes(n_kp, w=W, h=H, orb=ORB, n_lines=80):
+def lsd_touch_floor(counts):
+    """Per-frame bytes the sequential LSD touches in the kernels' layout, from
+    the oracle's element-access counts (oracle.lsd_traffic, averaged over
+    sampled frames of the workload): every access served once from memory.
+      pseudo-order sort: (compares + element writes) x 4 B packed key;
+      seed loop: seeds x (4 B key + 8 B pixel word) + neighbour reads x 16 B
+        (the paired word: angle, claim stamp, cos, sin) + adds x (8 B stamp +
+        16 B list entry) + expansions x 16 B + fit list reads / writes x 16 B;
+      NFA validation: rectangle pixels x 4 B angle + evaluations x 96 B
+        (the rectangle's 12 doubles)."""
+    c = counts
+    return {"lsd_sort": 4 * (c["sort_cmp"] + c["sort_moves"]),
+            "lsd_seed": (12 * c["seeds"] + 16 * c["grow_nb"] + 24 * c["grow_add"] +
+                         16 * c["grow_expand"] + 16 * (c["fit_reads"] + c["fit_writes"])),
+            "lsd_validate": 4 * c["nfa_px"] + 96 * c["nfa_evals"]}
+
+
+def lsd_counts(frames, k=8):
+    """oracle.lsd_traffic averaged over k frames spread over `frames`."""
+    from _pkg import load_oracle
+    O = load_oracle()
+    idx = np.linspace(0, len(frames) - 1, min(k, len(frames))).astype(int)
+    cs = [O.lsd_traffic(frames[i]) for i in idx]
+    out = {key: float(np.mean([c[key] for c in cs])) for key in cs[0]}
+    out["frames_sampled"] = len(idx)
+    return out
+
+
+def algorithmic_bytes(n_kp, w=W, h=H, orb=ORB, n_lines=80, lsd=None):
     """Per-frame algorithmic HBM bytes of each kernel: the
     bytes the kernel must move at minimum (each input read once, each output
     written once), with n_kp keypoints per frame. LSD works on the 0.8-scaled
-    image (sA pixels, LSD's `scale` of LineSegmentDetector)."""
+    image (sA pixels, LSD's `scale` of LineSegmentDetector); with `lsd` (the
+    oracle's element-access counts, lsd_counts) the sort, seed-loop and
+    validation kernels take the sequential algorithm's touch floor
+    (lsd_touch_floor) instead of the one-pass estimates."""
     areas, d = level_areas(w, h, orb)
     S = sum(areas)
     dims = list(zip((int(a) for a in d["width"]), (int(b) for b in d["height"])))
@@ -198,6 +229,7 @@ def algorithmic_bytes(n_kp, w=W, h=H, orb=ORB, n_lines=80):
         "lbd": A0 + 2 * A0 + 2 * 4 * A0 + n_lines * 32,
         # UndistortKeyLines + line depths: 80 KeyLines in and out, 160 depth reads
         "line_prepare": n_lines * (68 * 2 + 8 + 8),
+        **(lsd_touch_floor(lsd) if lsd else {}),
     }
 
 
@@ -621,7 +653,8 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
 
     # roofline of the dominant single-stage kernel
     n_kp = float(st["nkeypoints"].mean())
-    ab = algorithmic_bytes(n_kp, fw, fh, wl["orb"])
+    lsdc = lsd_counts(gray) if lines else None
+    ab = algorithmic_bytes(n_kp, fw, fh, wl["orb"], lsd=lsdc)
     # candidates: every kernel's GPU time per step, a kernel launched in
     # several stages (k_pose: motion model, reference keyframe, local map)
     # counted once with all its launches
@@ -705,6 +738,18 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
             "frames_per_launch": launch_frames(dom),
             "per_kernel_GBps": {k: round(ab[k] * launch_frames(k) / (stage_avg[k] * 1e-3) / 1e9, 1)
                                 for k in cand if stage_avg[k] > 0}}
+    if lsdc:
+        # the LSD kernels' algorithmic bytes are the sequential algorithm's
+        # touch floor (lsd_touch_floor); their committed PMC traffic over it
+        fl = lsd_touch_floor(lsdc)
+        ratios = {}
+        for k, b in fl.items():
+            tb, _ = pmc_traffic(KERNELS[k], workload, launch_frames(k))
+            ratios[k] = round(tb / (b * launch_frames(k)), 2) if tb else None
+        roof["lsd_floor"] = {"counts_per_frame": lsdc, "floor_bytes_per_frame": fl,
+                             "pmc_traffic_over_floor": ratios,
+                             "source": "oracle.lsd_traffic (oracle/lsd_oracle.cpp LsdTraffic) on "
+                                       "sampled frames of this workload"}
     # whole pipeline: B_frame x frames/s against 8 TB/s
     per_gpu = S * steps / elapsed
     roof["pipeline"] = {"bytes_per_frame": fbytes, "frames_per_s_per_gpu": round(per_gpu, 1),

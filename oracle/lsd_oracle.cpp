@@ -233,7 +233,21 @@ static inline double log_gamma(double x) {
   return x > 15.0 ? log_gamma_windschitl(x) : log_gamma_lanczos(x);
 }
 
+// Element accesses of the sequential algorithm, by stage (test / measurement
+// infrastructure: the algorithmic-traffic floor of the LSD kernels, see
+// oracle_lsd_traffic). Counted, not timed; the detection result is unchanged.
+struct LsdTraffic {
+  long long sort_cmp = 0, sort_moves = 0;    // pseudo-order std::sort: compares, element writes
+  long long seeds = 0;                       // ordered entries the seed loop visits
+  long long grow_nb = 0, grow_add = 0;       // region_grow: in-image neighbour reads, adds
+  long long grow_expand = 0;                 // region list reads (points expanded)
+  long long grows = 0;                       // region_grow calls (first + refine's second)
+  long long fit_reads = 0, fit_writes = 0;   // region list element reads / writes of the fit
+  long long nfa_evals = 0, nfa_px = 0;       // rect_nfa calls, rectangle pixels visited
+};
+
 struct LSD {
+  LsdTraffic* tr = nullptr;   // non-NULL: count element accesses
   // parameters (LSD_REFINE_ADV defaults)
   const double SCALE = 0.8, SIGMA_SCALE = 0.6, QUANT = 2.0, ANG_TH = 22.5, LOG_EPS = 0,
                DENSITY_TH = 0.7;
@@ -296,8 +310,35 @@ struct LSD {
         p.norm = int(modgrad[(size_t)y * W + x] * bin_coef);
         ordered.push_back(p);
       }
-    std::sort(ordered.begin(), ordered.end(),
-              [](const NormPoint& a, const NormPoint& b) { return a.norm > b.norm; });
+    if (!tr) {
+      std::sort(ordered.begin(), ordered.end(),
+                [](const NormPoint& a, const NormPoint& b) { return a.norm > b.norm; });
+    } else {
+      // the same std::sort over a counting element type: same comparisons,
+      // same permutation; compares and element writes counted
+      struct CP {
+        NormPoint v;
+        long long* mv;
+        CP(NormPoint a, long long* m) : v(a), mv(m) {}
+        CP(const CP& o) : v(o.v), mv(o.mv) { ++*mv; }
+        CP& operator=(const CP& o) {
+          v = o.v;
+          mv = o.mv;
+          ++*mv;
+          return *this;
+        }
+      };
+      std::vector<CP> c;
+      c.reserve(ordered.size());
+      for (const NormPoint& q : ordered) c.emplace_back(q, &tr->sort_moves);
+      tr->sort_moves = 0;
+      long long* nc = &tr->sort_cmp;
+      std::sort(c.begin(), c.end(), [nc](const CP& a, const CP& b) {
+        ++*nc;
+        return a.v.norm > b.v.norm;
+      });
+      for (size_t i = 0; i < c.size(); i++) ordered[i] = c[i].v;
+    }
   }
 
   void region_grow(int sx, int sy, std::vector<RegionPoint>& reg, double& reg_angle,
@@ -315,10 +356,18 @@ struct LSD {
     float sumdx = float(pmath::cos_(reg_angle));
     float sumdy = float(pmath::sin_(reg_angle));
     *seed.used = USED;
+    if (tr) {
+      tr->grows++;
+      tr->grow_add++;
+    }
     for (size_t i = 0; i < reg.size(); i++) {
       const RegionPoint rpoint = reg[i];
       const int xx_min = std::max(rpoint.x - 1, 0), xx_max = std::min(rpoint.x + 1, W - 1);
       const int yy_min = std::max(rpoint.y - 1, 0), yy_max = std::min(rpoint.y + 1, H - 1);
+      if (tr) {
+        tr->grow_expand++;
+        tr->grow_nb += (long long)(xx_max - xx_min + 1) * (yy_max - yy_min + 1) - 1;
+      }
       for (int yy = yy_min; yy <= yy_max; ++yy)
         for (int xx = xx_min; xx <= xx_max; ++xx) {
           uint8_t& is_used = used[(size_t)yy * W + xx];
@@ -335,6 +384,7 @@ struct LSD {
             sumdx += cosf_cr(float(angle));
             sumdy += sinf_cr(float(angle));
             reg_angle = oracle_fast_atan2(sumdy, sumdx) * DEG_TO_RADS;
+            if (tr) tr->grow_add++;
           }
         }
     }
@@ -362,6 +412,7 @@ struct LSD {
 
   void region2rect(const std::vector<RegionPoint>& reg, double reg_angle, double prec, double p,
                    Rect& rec) const {
+    if (tr) tr->fit_reads += 3 * (long long)reg.size();   // centroid, inertia, extents passes
     double x = 0, y = 0, sum = 0;
     for (size_t i = 0; i < reg.size(); ++i) {
       const double weight = reg[i].modgrad;
@@ -407,7 +458,9 @@ struct LSD {
     while (density < DENSITY_TH) {
       radSq *= 0.75 * 0.75;
       for (size_t i = 0; i < reg.size(); ++i) {
+        if (tr) tr->fit_reads++;
         if (distSq(xc, yc, double(reg[i].x), double(reg[i].y)) > radSq) {
+          if (tr) tr->fit_writes += 2;   // the USED flag, the swapped-in element
           *(reg[i].used) = NOTUSED;
           std::swap(reg[i], reg[reg.size() - 1]);
           reg.pop_back();
@@ -428,6 +481,10 @@ struct LSD {
     const double ang_c = reg[0].angle;
     double sum = 0, s_sum = 0;
     int n = 0;
+    if (tr) {
+      tr->fit_reads += (long long)reg.size();
+      tr->fit_writes += (long long)reg.size();   // USED flags released before the regrow
+    }
     for (size_t i = 0; i < reg.size(); ++i) {
       *(reg[i].used) = NOTUSED;
       if (dist(xc, yc, reg[i].x, reg[i].y) < rec.width) {
@@ -545,6 +602,10 @@ struct LSD {
       left_x += lstep;
       right_x += rstep;
     }
+    if (tr) {
+      tr->nfa_evals++;
+      tr->nfa_px += total_pts;
+    }
     return nfa(total_pts, alg_pts, rec.p);
   }
 
@@ -649,6 +710,7 @@ struct LSD {
     std::vector<RegionPoint> reg;
     for (size_t i = 0; i < ordered.size(); ++i) {
       const int px = ordered[i].x, py = ordered[i].y;
+      if (tr) tr->seeds++;
       if (used[(size_t)py * img_width + px] != NOTUSED || ang(px, py) == NOTDEF) continue;
       double reg_angle;
       region_grow(px, py, reg, reg_angle, prec);
@@ -906,6 +968,22 @@ int oracle_lsd_detect(const uint8_t* img, int W, int H, float* lines, int cap, i
   if (n > cap) return -2;
   std::memcpy(lines, L.data(), L.size() * sizeof(float));
   return 0;
+}
+
+// The element accesses of one detection (LsdTraffic, in declaration order:
+// sort_cmp, sort_moves, seeds, grow_nb, grow_add, grow_expand, grows,
+// fit_reads, fit_writes, nfa_evals, nfa_px); bench.py turns them into the LSD
+// kernels' algorithmic-byte floors. Returns the number of segments.
+int oracle_lsd_traffic(const uint8_t* img, int W, int H, long long* out11) {
+  LSD lsd;
+  LsdTraffic t;
+  lsd.tr = &t;
+  std::vector<float> L;
+  lsd.detect(img, W, H, L);
+  const long long v[11] = {t.sort_cmp, t.sort_moves, t.seeds, t.grow_nb, t.grow_add, t.grow_expand,
+                           t.grows, t.fit_reads, t.fit_writes, t.nfa_evals, t.nfa_px};
+  std::memcpy(out11, v, sizeof(v));
+  return (int)(L.size() / 4);
 }
 
 // Intermediate LSD stages for stage-wise parity: the 8-bit scaled image

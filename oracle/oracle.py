@@ -410,6 +410,7 @@ def _setup(L):  # noqa: F811
     _setup_track_orb(L)
     vp, i, f = C.c_void_p, C.c_int, C.c_float
     L.oracle_lsd_detect.argtypes = [vp, i, i, vp, i, vp]
+    L.oracle_lsd_traffic.argtypes = [vp, i, i, vp]
     L.oracle_lsd_stages.argtypes = [vp, i, i, vp, vp, vp, vp, vp, vp]
     L.oracle_line_extract.argtypes = [vp, i, i, vp, vp, vp, i, vp, vp]
     L.oracle_lsdm.argtypes = [i, C.c_double, C.c_double]
@@ -427,6 +428,24 @@ def lsd_detect(img, cap=4096):
     rc = lib().oracle_lsd_detect(_p(img), w, h, _p(out), cap, C.byref(n))
     assert rc == 0, rc
     return out[:n.value].copy()
+
+
+LSD_TRAFFIC_KEYS = ("sort_cmp", "sort_moves", "seeds", "grow_nb", "grow_add", "grow_expand",
+                    "grows", "fit_reads", "fit_writes", "nfa_evals", "nfa_px")
+
+
+def lsd_traffic(img):
+    """Element accesses of the sequential LSD on one image (the pseudo-order
+    sort's compares / element writes, the seed loop's seeds, neighbour reads,
+    adds, expansions and fit list accesses, the NFA's evaluations and
+    rectangle pixels): the algorithmic-traffic floor inputs of bench.py."""
+    img = _c(img, np.uint8)
+    h, w = img.shape
+    o = np.zeros(len(LSD_TRAFFIC_KEYS), np.int64)
+    n = lib().oracle_lsd_traffic(_p(img), w, h, _p(o))
+    out = dict(zip(LSD_TRAFFIC_KEYS, (int(x) for x in o)))
+    out["segments"] = int(n)
+    return out
 
 
 def lsd_stages(img):

@@ -834,8 +834,15 @@ __device__ __forceinline__ int lane_grow(const Frame& F, uint64_t* sd, LaneBuf b
 // added mask, shifted to the next pixel's 3x3 (a 7x7 bit board). Claims other
 // lanes made meanwhile are caught by the claim re-check after the round, as
 // for any speculative read.
+// Measured slower and off (A/B on one box, two rounds, tools/gpu_r04_b.sh:
+// LSD batch 1 / 16 / 64 = 54-55 / 63 / 67 ms with it, 49-52 / 55-57 / 59-60
+// ms without; the two-register-set form ORBPL_GROW_PF=2, which avoids copying
+// the prefetched words, 53-57 / 63-64 / 66 ms): the extra address work, the
+// LDS ring and the doubled neighbourhood registers cost more issue cycles
+// than the hidden load latency saves - the grow step is bound by its
+// instruction issue, not by the neighbourhood round trip.
 #ifndef ORBPL_GROW_PF
-#define ORBPL_GROW_PF 1
+#define ORBPL_GROW_PF 0
 #endif
 
 __device__ __forceinline__ void nb_terms(int x, int y, int sw, int sh, int tw, int* rterm,
@@ -888,6 +895,97 @@ __device__ __forceinline__ int lane_grow_pf(const Frame& F, uint64_t* sd, LaneBu
     w[k] = *reinterpret_cast<const uint4*>(sd + (rterm[k / 3] + cterm[k % 3]));
   }
   unsigned own = 0;   // neighbours known to be in this region although their words predate it
+#if ORBPL_GROW_PF == 2
+  // two register sets used in turn (the loop unrolled by two): the words
+  // prefetched for the next pixel are never copied, so nothing waits for them
+  // before that pixel's own tests
+  uint4 w2[9];
+  int rterm2[3], cterm2[3];
+  unsigned inm2 = 0;
+  int i = 0;
+  auto step = [&](uint4 (&wc)[9], int (&rc)[3], int (&cc)[3], unsigned& inc, uint4 (&wn)[9],
+                  int (&rn)[3], int (&cn)[3], unsigned& inn) -> int {
+    const int x = (int)(cur & 0xFFFF), y = (int)(cur >> 16);
+    const int n_start = n;
+    const bool pf = i + 1 < n_start;
+    uint32_t nxt = cur;
+    if (pf) {
+      nxt = n_start - (i + 1) <= kRing ? ring[(i + 1) & (kRing - 1)] : buf.pt(i + 1);
+      nb_terms((int)(nxt & 0xFFFF), (int)(nxt >> 16), sw, sh, tw, rn, cn, &inn);
+#pragma unroll
+      for (int k = 0; k < 9; k++) {
+        if (k == 4) continue;
+        wn[k] = *reinterpret_cast<const uint4*>(sd + (rn[k / 3] + cn[k % 3]));
+      }
+    }
+    unsigned ok = 0;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+      if (k == 4) continue;
+      const unsigned f = ((inc >> k) & 1u) & ((~own >> k) & 1u) & (unsigned)(wc[k].y != 0u) &
+                         (unsigned)(wc[k].y != myval) & (unsigned)(__uint_as_float(wc[k].x) >= 0.f);
+      ok |= f << k;
+    }
+    uint32_t first_add = cur;
+    unsigned added = 0;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+      if (k == 4) continue;
+      double nt = fabs(reg_angle - deg2ang(__uint_as_float(wc[k].x)));
+      nt = nt > k3pi2 ? fabs(nt - k2pi) : nt;
+      if (((ok >> k) & 1u) && nt <= prec) {
+        if ((wc[k].y >> 1) < mytag) return kSpecConflict;   // an earlier seed's pixel
+        const int id = rc[k / 3] + cc[k % 3];
+        atomicMin(reinterpret_cast<unsigned long long*>(sd + id),
+                  ((unsigned long long)myval << 32) | wc[k].x);
+        if (n >= cap) return kSpecOverflow;
+        const int xx = x + (k % 3) - 1, yy = y + (k / 3) - 1;
+        const uint32_t pt = (uint32_t)xx | ((uint32_t)yy << 16);
+        if (n == n_start) first_add = pt;
+        buf[n] = make_uint4(pt, wc[k].x, 0u, 0u);
+        ring[n & (kRing - 1)] = pt;
+        n++;
+        added |= 1u << k;
+        sumdx += __uint_as_float(wc[k].z);   // add_angle(d) terms
+        sumdy += __uint_as_float(wc[k].w);
+        reg_angle = (double)fast_atan2_deg_1div(sumdy, sumdx) * kDegToRad;
+      }
+    }
+    if (pf) {
+      const int ddx = (int)(nxt & 0xFFFF) - x, ddy = (int)(nxt >> 16) - y;
+      unsigned nown = 0;
+      if (added && ddx >= -2 && ddx <= 2 && ddy >= -2 && ddy <= 2) {
+        const unsigned long long B = ((unsigned long long)(added & 7u) << 16) |
+                                     ((unsigned long long)((added >> 3) & 7u) << 23) |
+                                     ((unsigned long long)((added >> 6) & 7u) << 30);
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+          nown |= (unsigned)((B >> (7 * (2 + ddy + r) + 2 + ddx)) & 7ull) << (3 * r);
+      }
+      own = nown;
+      cur = nxt;
+    } else if (i + 1 < n) {
+      // the next pixel is this step's first add: its words are loaded now
+      cur = first_add;
+      own = 0;
+      nb_terms((int)(cur & 0xFFFF), (int)(cur >> 16), sw, sh, tw, rn, cn, &inn);
+#pragma unroll
+      for (int k = 0; k < 9; k++) {
+        if (k == 4) continue;
+        wn[k] = *reinterpret_cast<const uint4*>(sd + (rn[k / 3] + cn[k % 3]));
+      }
+    }
+    i++;
+    return 0;
+  };
+  while (i < n) {
+    int r = step(w, rterm, cterm, inm, w2, rterm2, cterm2, inm2);
+    if (r) return r;
+    if (i >= n) break;
+    r = step(w2, rterm2, cterm2, inm2, w, rterm, cterm, inm);
+    if (r) return r;
+  }
+#else
   for (int i = 0; i < n; i++) {
     const int x = (int)(cur & 0xFFFF), y = (int)(cur >> 16);
     const int n_start = n;
@@ -975,6 +1073,7 @@ __device__ __forceinline__ int lane_grow_pf(const Frame& F, uint64_t* sd, LaneBu
       }
     }
   }
+#endif
   return n;
 }
 #else

@@ -98,3 +98,24 @@ def test_line_oracle_matches_golden(path, oracle, synth):
     assert kl.view(np.uint8).tobytes() == z["keylines"].tobytes()
     assert np.array_equal(desc, z["desc"]) and np.array_equal(coef, z["coef"])
     assert nd == int(z["n_detected"])
+
+
+def test_lsd_traffic_counts(oracle):
+    """The instrumented detection (oracle.lsd_traffic: the touch floors of the
+    LSD kernels in bench.py) finds the same segments and its counts hold the
+    algorithm's invariants: every added region point is expanded once, every
+    expansion reads at most 8 neighbours, the sort makes ~log2(n) compares
+    per element, every refined rectangle is NFA-evaluated at least once."""
+    from _scenes import sequence
+    cfg, traj, fr = sequence(1, 1)
+    img = fr[0][0]
+    t = oracle.lsd_traffic(img)
+    assert t["segments"] == len(oracle.lsd_detect(img)) > 100
+    assert t["grow_add"] == t["grow_expand"]
+    assert t["grow_expand"] < t["grow_nb"] <= 8 * t["grow_expand"]
+    sw, sh = 512, 384
+    n = (sw - 1) * (sh - 1)
+    assert t["seeds"] == n
+    assert 10 * n < t["sort_cmp"] < 30 * n and t["sort_moves"] > n
+    assert t["nfa_evals"] >= t["segments"] and t["nfa_px"] > t["nfa_evals"]
+    assert t["grows"] >= t["nfa_evals"] / 16

@@ -31,3 +31,7 @@ if [ -n "$SQ" ]; then
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES SQ_BUSY_CYCLES -d $R/$out/sq -o run --output-format csv -- python3 $B > $R/$out/sq.log 2>&1 || { echo "sq failed"; tail -5 $R/$out/sq.log; exit 1; }
 echo sq ok
 fi
+if [ -n "$SQ2" ]; then
+timeout -k 10 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_INSTS_SALU SQ_INSTS_VMEM_WR SQ_INST_CYCLES_VMEM_RD SQ_INSTS_VMEM_RD -d $R/$out/sq2 -o run --output-format csv -- python3 $B > $R/$out/sq2.log 2>&1 || { echo "sq2 failed"; tail -5 $R/$out/sq2.log; exit 1; }
+echo sq2 ok
+fi
