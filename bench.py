@@ -336,6 +336,8 @@ def leg_summary(out):
         rf["lines"] = ((out["secondary"].get("cpu_baseline") or {}).get("reference_faithful")
                        or {}).get("median_ms_per_frame")
     s["cpu_reference_faithful_ms"] = rf
+    if "secondary" in out and out["secondary"].get("dropin_frame"):
+        s["dropin_frame_ms"] = out["secondary"]["dropin_frame"].get("median_ms_per_frame")
     return s
 
 
@@ -946,6 +948,50 @@ def cpu_baseline(seconds, threads, gray, depth, L, workload="points", flags=0, u
     return sum(counts) / dt, sum(counts), dt
 
 
+def dropin_frame_latency(gray, depth, L, workload, reps=30):
+    """Single-frame latency of the compiled drop-in ORB_SLAM2::Frame (ORB ||
+    LineExtractor on two host threads + the frame glue, dropin/Frame.cc, one
+    frame at a time as the reference's Tracking builds it): dropin_driver
+    --time on three frames of the workload's loop; host buffers in and out,
+    so the PCIe copies are inside. Returns the driver's median / mean ms."""
+    import struct
+    import tempfile
+    import orbpl.synth as synth
+    drv = ROOT / "orb_slam2_modification_with-point-and-line-feature_amd" / "dropin_driver"
+    if not drv.exists():
+        return None
+    wl = WORKLOADS[workload]
+    cfg = getattr(synth, wl["cam"])
+    fh, fw = gray.shape[1:]
+    with tempfile.TemporaryDirectory() as td:
+        voc = Path(td) / "voc.txt"
+        voc.write_text("10 1 0 0\n")   # not read by the timing mode
+        inp = Path(td) / "in.bin"
+        with open(inp, "wb") as f:
+            f.write(struct.pack("<2i", fw, fh))
+            camv = [cfg["fx"], cfg["fy"], cfg["cx"], cfg["cy"], cfg["k1"], cfg["k2"], cfg["p1"],
+                    cfg["p2"], cfg["k3"], cfg["bf"], cfg["bf"] * cfg["thdepth"] / cfg["fx"]]
+            f.write(np.asarray(camv, np.float32).tobytes())
+            o = wl["orb"]
+            f.write(struct.pack("<ifiii", o[0], o[1], o[2], o[3], o[4]))
+            f.write(np.eye(4, dtype=np.float32).tobytes())
+            for t in range(3):
+                e = L.elem(0, t)
+                f.write(np.ascontiguousarray(gray[e], np.uint8).tobytes())
+                f.write(np.ascontiguousarray(depth[e], np.float32).tobytes())
+            pb = str(voc).encode()
+            f.write(struct.pack("<i", len(pb)) + pb)
+        r = subprocess.run([str(drv), "--time", str(inp), str(reps)], capture_output=True, text=True,
+                           timeout=300)
+    if r.returncode != 0 or "median" not in r.stdout:
+        return {"error": (r.stderr or r.stdout)[-200:]}
+    w = r.stdout.split()
+    return {"median_ms_per_frame": float(w[w.index("median") + 1]),
+            "mean_ms_per_frame": float(w[w.index("mean") + 1]), "frames": reps,
+            "what": "compiled drop-in ORB_SLAM2::Frame (ORB || LineExtractor threads + frame "
+                    "glue over the C ABI, host images in, host keypoints / lines out)"}
+
+
 def cpu_reference_faithful(gray, depth, L, workload, flags=0, warmup=20, frames=300,
                            use_map=False):
     """BASELINE.md §2 mode 1: one stream as the reference runs it, ORB and
@@ -1220,6 +1266,9 @@ def main():
                     "reference_faithful": cpu_reference_faithful(
                         o["gray"], o["depth"], o["layout"], o["wname"], ofl, args.cpu_ref_warmup,
                         args.cpu_ref_frames, o["map"])}
+                if key == "secondary":
+                    out[key]["dropin_frame"] = dropin_frame_latency(o["gray"], o["depth"],
+                                                                    o["layout"], o["wname"])
         out["summary"] = leg_summary(out)   # last key: it survives a tail-cut log
         print(json.dumps(out))
     if dist:

@@ -1828,6 +1828,9 @@ constexpr int kSpecSmallBatch = ORBPL_SPEC_SMALL_BATCH;
 // seeds first, in list order, then new seeds from the scan; a lane's list
 // buffer travels with its seed (bufid). After a cooperative fallback nothing
 // is carried (the fallback uses buffer 0 as scratch).
+#ifndef ORBPL_SPEC_WIN
+#define ORBPL_SPEC_WIN 64
+#endif
 #ifndef ORBPL_SPEC_KEEP
 #define ORBPL_SPEC_KEEP 1
 #endif
@@ -1855,6 +1858,8 @@ __device__ __forceinline__ void block_sync() {
 template <int W, int MINW = (W == 1 ? ORBPL_SPEC_MINW : 1)>
 __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch sc) {
   constexpr int SL = 64 * W;
+  // seeds per round (one-wave variant: ORBPL_SPEC_WIN, an A/B build override)
+  constexpr int WIN = W == 1 ? ORBPL_SPEC_WIN : SL;
   constexpr bool KEEP = W == 1 && ORBPL_SPEC_KEEP && !ORBPL_LBUF_INTERLEAVED;
   extern __shared__ uint32_t grow_smem[];
   __shared__ uint32_t s_pt[SL];
@@ -1923,7 +1928,7 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
     // ---- the next SL defined, NOTUSED seeds in list order (after the
     // carried ones) ----
     int ncand = ncarry, scan = pos, next_pos = nlist;
-    while (ncand < SL && scan < nlist) {
+    while (ncand < WIN && scan < nlist) {
       const int i = scan + t;
       bool c = false;
       int px = 0, py = 0;
@@ -1951,20 +1956,20 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
         before += off;
         cnt = tot;
       }
-      if (c && ncand + before < SL) {
+      if (c && ncand + before < WIN) {
         s_pt[ncand + before] = (uint32_t)px | ((uint32_t)py << 16);
         s_pos[ncand + before] = i;
       }
-      if (ncand + cnt >= SL) {
+      if (ncand + cnt >= WIN) {
         if (W == 1) {
-          const unsigned long long mm = __ballot(c && before == SL - ncand - 1);
+          const unsigned long long mm = __ballot(c && before == WIN - ncand - 1);
           next_pos = scan + __ffsll((long long)mm);
         } else {
-          if (c && before == SL - ncand - 1) s_misc[0] = i + 1;
+          if (c && before == WIN - ncand - 1) s_misc[0] = i + 1;
           __syncthreads();
           next_pos = s_misc[0];
         }
-        ncand = SL;
+        ncand = WIN;
       } else {
         ncand += cnt;
         scan += SL;

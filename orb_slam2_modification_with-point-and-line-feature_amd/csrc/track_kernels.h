@@ -88,8 +88,11 @@ struct PoseLaunch {
 // as TrackReferenceKeyFrame): small enough to place quickly beside the
 // extraction kernels when the list is empty
 constexpr int kListGrid = 256;
-// k_trk_bow's listed launch: one workgroup per listed stream up to this many
-constexpr int kTrkGrid = 1024;
+// k_trk_bow's listed launch: workgroups looping over the listed streams. The
+// launch runs every step beside the next batch's extraction, mostly with an
+// empty list: 1024 workgroups cost ~0.4 ms of placement per step there
+// (rocprof, 1024 streams), 256 keep the empty launch at a few us.
+constexpr int kTrkGrid = 256;
 
 // Per-frame line buffers of the tracker (kLineKeep lines per stream).
 struct LineTrackArgs {

@@ -14,6 +14,9 @@
 //            ORBmatcher(0.8).SearchByProjection(F, points, 3),
 //            LineMatcher(0.8).SearchByProjection(F, lines), the second pose).
 //   dropin_driver <in.bin> <out.bin>
+//   dropin_driver --time <in.bin> <K>: K Frame constructions of frame 0 (ORB ||
+//   LineExtractor on two host threads + the frame glue, one frame at a time as
+//   the reference's Tracking builds them), median / mean latency in ms
 // in.bin : int32 W, H; float fx fy cx cy k1 k2 p1 p2 k3 bf thdepth;
 //          int32 nfeatures; float scale; int32 nlevels, iniTh, minTh;
 //          float Tcw0[16]; 3 x (gray W*H u8, depth W*H f32);
@@ -35,6 +38,8 @@
 //          [N0] u8, local nmatches, match[N2] after the search, line seen
 //          [NL0], line in_view[NL0], local line nmatches, line match[NL2],
 //          inliers, Tcw[16]
+#include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <map>
@@ -89,12 +94,13 @@ static std::vector<int32_t> node_of(const DBoW2::FeatureVector& fv, int n) {
 }
 
 int main(int argc, char** argv) {
-  if (argc != 3) {
-    fprintf(stderr, "usage: dropin_driver in.bin out.bin\n");
+  const bool timing = argc == 4 && std::string(argv[1]) == "--time";
+  if (argc != 3 && !timing) {
+    fprintf(stderr, "usage: dropin_driver in.bin out.bin | dropin_driver --time in.bin K\n");
     return 2;
   }
   try {
-    FILE* in = fopen(argv[1], "rb");
+    FILE* in = fopen(argv[timing ? 2 : 1], "rb");
     if (!in) throw std::runtime_error("cannot open input");
     int32_t wh[2];
     float camv[11], Tcw0[16];
@@ -135,6 +141,21 @@ int main(int argc, char** argv) {
     for (int k = 0; k < 5; k++) dist.at<float>(k, 0) = camv[4 + k];
     const float bf = camv[9], thDepth = camv[10];
     ORBextractor ex(nf, sf, nl, ini, mn);
+    if (timing) {
+      const int reps = std::max(1, atoi(argv[3]));
+      std::vector<double> ms;
+      for (int r = 0; r < reps + 3; r++) {   // 3 warm-up constructions
+        const auto t0 = std::chrono::steady_clock::now();
+        Frame Ft(g[r % 3], d[r % 3], r, &ex, &voc, K, dist, bf, thDepth);
+        const auto t1 = std::chrono::steady_clock::now();
+        if (r >= 3) ms.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
+      }
+      std::sort(ms.begin(), ms.end());
+      double mean = 0;
+      for (double v : ms) mean += v / ms.size();
+      printf("time: median %.3f ms mean %.3f ms frames %d\n", ms[ms.size() / 2], mean, reps);
+      return 0;
+    }
     Frame F0(g[0], d[0], 0.0, &ex, &voc, K, dist, bf, thDepth);
     std::vector<cv::Mat> pyr = ex.mvImagePyramid;
     Frame F1(g[1], d[1], 1.0, &ex, &voc, K, dist, bf, thDepth);
