@@ -957,6 +957,8 @@ def dropin_frame_latency(gray, depth, L, workload, reps=30):
     import struct
     import tempfile
     import orbpl.synth as synth
+    from _pkg import load_pkg
+    pkg_th_depth = load_pkg().th_depth
     drv = ROOT / "orb_slam2_modification_with-point-and-line-feature_amd" / "dropin_driver"
     if not drv.exists():
         return None
@@ -970,7 +972,7 @@ def dropin_frame_latency(gray, depth, L, workload, reps=30):
         with open(inp, "wb") as f:
             f.write(struct.pack("<2i", fw, fh))
             camv = [cfg["fx"], cfg["fy"], cfg["cx"], cfg["cy"], cfg["k1"], cfg["k2"], cfg["p1"],
-                    cfg["p2"], cfg["k3"], cfg["bf"], cfg["bf"] * cfg["thdepth"] / cfg["fx"]]
+                    cfg["p2"], cfg["k3"], cfg["bf"], pkg_th_depth(cfg)]
             f.write(np.asarray(camv, np.float32).tobytes())
             o = wl["orb"]
             f.write(struct.pack("<ifiii", o[0], o[1], o[2], o[3], o[4]))

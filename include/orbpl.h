@@ -167,6 +167,28 @@ typedef struct orbpl_camera {
   int32_t width, height;
 } orbpl_camera;
 
+/* Tracking::Tracking's settings (Tracking.cc:53-147) read from the
+ * reference's OpenCV FileStorage YAML files (Examples/RGB-D/TUM1.yaml:8-55):
+ * the flat "Key.name: value" subset, with OpenCV 3.4's FileNode conversions
+ * (a missing key reads 0). sensor: System::eSensor. cam.th_depth = mbf *
+ * ThDepth / fx for stereo / RGB-D (0 monocular); fps 0 -> 30 and max_frames
+ * = mMaxFrames (orbpl_tracker_set_fps takes fps); depth_map_factor =
+ * mDepthMapFactor = 1 / DepthMapFactor (1 when |DepthMapFactor| < 1e-5 or
+ * not RGB-D); cam.width / height from Camera.width / height when present
+ * (the reference takes them from the images). */
+#define ORBPL_SENSOR_MONOCULAR 0
+#define ORBPL_SENSOR_STEREO 1
+#define ORBPL_SENSOR_RGBD 2
+typedef struct orbpl_settings {
+  orbpl_orb_params orb;
+  orbpl_camera cam;
+  float fps;
+  int32_t max_frames;
+  float depth_map_factor;
+  int32_t rgb;                 /* Camera.RGB */
+} orbpl_settings;
+int orbpl_settings_load(const char* path, int sensor, orbpl_settings* out);
+
 #define ORBPL_GRID_COLS 64     /* FRAME_GRID_COLS (Frame.h:41) */
 #define ORBPL_GRID_ROWS 48     /* FRAME_GRID_ROWS (Frame.h:40) */
 

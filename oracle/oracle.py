@@ -187,7 +187,8 @@ class PoseProblem(C.Structure):
 
 def camera(cfg):
     return Camera(cfg["fx"], cfg["fy"], cfg["cx"], cfg["cy"], cfg["k1"], cfg["k2"], cfg["p1"],
-                  cfg["p2"], cfg["k3"], cfg["bf"], cfg["bf"] * cfg["thdepth"] / cfg["fx"],
+                  cfg["p2"], cfg["k3"], cfg["bf"],
+                  float(np.float32(cfg["bf"]) * np.float32(cfg["thdepth"]) / np.float32(cfg["fx"])),
                   cfg["width"], cfg["height"])
 
 

@@ -335,11 +335,39 @@ class Camera(C.Structure):
                 ("width", C.c_int32), ("height", C.c_int32)]
 
 
+class Settings(C.Structure):
+    """orbpl_settings: Tracking::Tracking's settings (Tracking.cc:53-147)."""
+    _fields_ = [("orb", OrbParams), ("cam", Camera), ("fps", C.c_float),
+                ("max_frames", C.c_int32), ("depth_map_factor", C.c_float), ("rgb", C.c_int32)]
+
+
+SENSOR = {"monocular": 0, "stereo": 1, "rgbd": 2}
+
+
+def load_settings(path, sensor="rgbd"):
+    """The reference's OpenCV FileStorage YAML settings through the native
+    reader (orbpl_settings_load, OpenCV 3.4 FileNode semantics): (OrbParams,
+    Camera, dict(fps, max_frames, depth_map_factor, rgb))."""
+    out = Settings()
+    L = lib()
+    L.orbpl_settings_load.argtypes = [C.c_char_p, C.c_int, C.c_void_p]
+    check(L.orbpl_settings_load(str(path).encode(), SENSOR[sensor], C.byref(out)),
+          "orbpl_settings_load")
+    return out.orb, out.cam, dict(fps=out.fps, max_frames=out.max_frames,
+                                  depth_map_factor=out.depth_map_factor, rgb=out.rgb)
+
+
+def th_depth(cfg):
+    """mThDepth = mbf * (float)ThDepth / fx in float arithmetic, as
+    Tracking::Tracking computes it (Tracking.cc:136)."""
+    return float(np.float32(cfg["bf"]) * np.float32(cfg["thdepth"]) / np.float32(cfg["fx"]))
+
+
 def make_camera(cfg):
     """Camera from a settings dict (synth.TUM1 etc.); mThDepth = bf*ThDepth/fx
-    (Tracking.cc:134-138)."""
+    (Tracking.cc:134-138, th_depth)."""
     return Camera(cfg["fx"], cfg["fy"], cfg["cx"], cfg["cy"], cfg["k1"], cfg["k2"], cfg["p1"],
-                  cfg["p2"], cfg["k3"], cfg["bf"], cfg["bf"] * cfg["thdepth"] / cfg["fx"],
+                  cfg["p2"], cfg["k3"], cfg["bf"], th_depth(cfg),
                   cfg["width"], cfg["height"])
 
 

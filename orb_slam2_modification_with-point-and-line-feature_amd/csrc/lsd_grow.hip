@@ -2255,6 +2255,363 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
   }
 }
 
+// ---------------------------------------------------------------------------
+// The seed loop for small batches with its 64 speculative seeds per round
+// spread over 4 waves of 16 active lanes (one wave per SIMD): a round keeps the
+// one-wave loop's window (so its rounds and speculative regions), but each
+// wave's grow step executes the divergent add bodies of 16 regions instead of
+// 64 and the four waves issue on four SIMDs. Measured per round (one wave,
+// tools/gpu_r04_d.sh): 64 seeds 252k cycles, 32 seeds 190k, 16 seeds 119k.
+// Slot v = 16 * wave + lane (lanes 0-15) takes the v-th seed of the window;
+// claim tags rank by v, the commit walks the slots in order, and the kept
+// seeds of ORBPL_SPEC_KEEP are carried across waves through LDS. Only where
+// the GPU has spare SIMDs (batches of at most kSpecSparseBatch frames).
+// ---------------------------------------------------------------------------
+#ifndef ORBPL_SPEC_SPARSE_BATCH
+#define ORBPL_SPEC_SPARSE_BATCH 96
+#endif
+constexpr int kSpecSparseBatch = ORBPL_SPEC_SPARSE_BATCH;
+
+// the 64-bit slot mask of a per-thread predicate (false on lanes >= 16)
+__device__ __forceinline__ unsigned long long sp_vmask(bool pred, unsigned long long* s_vb, int wv,
+                                                       int lane) {
+  const unsigned long long b = __ballot(pred);
+  if (lane == 0) s_vb[wv] = (b & 0xFFFFull) << (16 * wv);
+  __syncthreads();
+  const unsigned long long m = s_vb[0] | s_vb[1] | s_vb[2] | s_vb[3];
+  __syncthreads();
+  return m;
+}
+__device__ __forceinline__ int sp_next(unsigned long long m, int j, int n) {
+  if (j >= 64) return n;
+  const unsigned long long r = m & ~((1ull << j) - 1ull);
+  return r ? min(n, __ffsll((long long)r) - 1) : n;
+}
+
+__global__ void __launch_bounds__(256, 1) k_lsd_spec_sparse(LsdGeom g, LsdScratch sc) {
+  constexpr int NS = 64;   // slots (seeds per round)
+  extern __shared__ uint32_t grow_smem[];
+  __shared__ uint32_t s_pt[NS], s_ptx[NS];
+  __shared__ int s_pos[NS], s_posx[NS], s_src[NS];
+  __shared__ int s_cnt[2][4];
+  __shared__ unsigned long long s_vb[4];
+  __shared__ int s_misc[2];
+  __shared__ int s_bufid[NS], s_status[NS], s_off[NS], s_len[NS], s_touched[NS], s_kp[NS];
+  __shared__ double s_rec[NS][12];
+  const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const bool act = lane < 16;
+  const int v = wv * 16 + (lane & 15);
+  const int sw = g.sw, sh = g.sh;
+  Frame F;
+  F.sw = sw;
+  F.sh = sh;
+  F.deg = sc.deg + (long long)f * sw * sh;
+  F.q = sc.q + (long long)f * sw * sh;
+  F.used = nullptr;
+  uint4* fbuf = sc.lbuf + (long long)f * NS * kLaneCap;
+  uint32_t* coop = reinterpret_cast<uint32_t*>(fbuf);
+  F.reg_l = coop;
+  F.regq_l = reinterpret_cast<int*>(F.reg_l + kRegLds);
+  F.regd_l = reinterpret_cast<float*>(F.regq_l + kRegLds);
+  F.ring = F.regd_l + kRegLds;
+  F.reg_g = sc.reg + (long long)f * 3 * sw * sh;
+  F.rows = reinterpret_cast<int4*>(grow_smem);
+  F.rect0 = reinterpret_cast<Rect*>(F.rows);
+  F.rect1 = F.rect0 + 1;
+  F.row_cap = 0;
+  F.log_nt = g.log_nt;
+  F.lane = lane;
+  F.pf_cyc = 0;
+  F.pf_cnt = 0;
+  uint64_t* sd = sc.sd + (long long)f * lsd_sd_frame_words(sw, sh);
+  F.usd = sd;
+  F.cs = sd + lsd_cs_offset(sw, sh);
+  F.tw = lsd_sd_tw(sw);
+  int bufid = v;       // the slot's list buffer (travels with a carried seed)
+  bool keep = false;   // the slot's seed, region and fit carried from the last round
+  int ncarry = 0;      // slots [0, ncarry) hold carried seeds
+  int status = kSpecConflict, off = 0, len = 0, touched = 0;
+  Rect rec;
+  const uint32_t* A = sc.A + (long long)f * g.n;
+  const int nlist = sc.sort_nge[f];
+  double* cand_out = sc.cand + (long long)f * kLsdMaxCand * 12;
+  const int w1 = sw - 1;
+  const double prec = g.prec, p = g.p;
+  const unsigned long long lt_mask = (1ull << lane) - 1ull;
+  const unsigned long long vlt = (1ull << v) - 1ull;
+  int nl = 0, pos = 0, it = 0;
+  uint32_t round = 0;
+  long long n_spec = 0, n_rounds = 0, cyc_spec = 0, cyc_fit = 0, cyc_val = 0, n_coop = 0;
+  const long long t_all = clock64();
+  while (pos < nlist || ncarry > 0) {
+    const LaneBuf buf{fbuf + (long long)bufid * kLaneCap};
+    // ---- the next NS defined, NOTUSED seeds (after the carried ones); all
+    // 256 threads scan ----
+    int ncand = ncarry, scan = pos, next_pos = nlist;
+    while (ncand < NS && scan < nlist) {
+      const int i = scan + t;
+      bool c = false;
+      int px = 0, py = 0;
+      if (i < nlist) {
+        const int idx = (int)(A[i] & 0x3FFFFFu);
+        py = idx / w1;
+        px = idx - py * w1;
+        const uint64_t vv = ld_sd(sd + lsd_sd_index(px, py, F.tw));
+        c = __uint_as_float((uint32_t)vv) >= 0.f && (uint32_t)(vv >> 32) != 0u;
+      }
+      const unsigned long long m = __ballot(c);
+      int before = __popcll(m & lt_mask), cnt = __popcll(m);
+      const int par = it++ & 1;
+      if (lane == 0) s_cnt[par][wv] = cnt;
+      __syncthreads();
+      int o = 0, tot = 0;
+#pragma unroll
+      for (int w = 0; w < 4; w++) {
+        const int x = s_cnt[par][w];
+        o += w < wv ? x : 0;
+        tot += x;
+      }
+      before += o;
+      cnt = tot;
+      if (c && ncand + before < NS) {
+        s_pt[ncand + before] = (uint32_t)px | ((uint32_t)py << 16);
+        s_pos[ncand + before] = i;
+      }
+      if (ncand + cnt >= NS) {
+        if (c && before == NS - ncand - 1) s_misc[0] = i + 1;
+        __syncthreads();
+        next_pos = s_misc[0];
+        ncand = NS;
+      } else {
+        ncand += cnt;
+        scan += 256;
+      }
+    }
+    if (ncand == 0) break;
+    __threadfence_block();
+    __syncthreads();
+    n_rounds++;
+    const long long t0 = clock64();
+    const uint32_t tag = ((0x3FFFFFu - round) << 9) | (uint32_t)v;
+    const uint32_t myval0 = (tag << 1) | 1u, myval1 = tag << 1;
+    if (act) {
+      if (!keep) {
+        status = kSpecConflict;
+        off = 0;
+        len = 0;
+        touched = 0;
+      } else {
+        for (int j0 = 0; j0 < touched; j0 += 8) {
+          uint32_t ev[8];
+#pragma unroll
+          for (int u = 0; u < 8; u++) ev[u] = buf[min(j0 + u, touched - 1)].x;
+#pragma unroll
+          for (int u = 0; u < 8; u++)
+            atomicMin(sd_hi(sd, lsd_sd_index((int)(ev[u] & 0xFFFF), (int)(ev[u] >> 16), F.tw)),
+                      myval0);
+        }
+        wg_fence();
+      }
+    }
+    __syncthreads();   // the carried re-stamps precede every grow of the round
+    double reg_angle = 0;
+    int n = 0;
+    const bool mine_seed = act && v < ncand && !keep;
+    if (mine_seed) {
+      n_spec++;
+      const uint32_t pt = s_pt[v];
+      n = lane_grow(F, sd, buf, kLaneCap, (int)(pt & 0xFFFF), (int)(pt >> 16), reg_angle, prec,
+                    myval0);
+    }
+    const long long t1 = clock64();
+    if (mine_seed) {
+      if (n < 0) {
+        status = n;
+      } else if (n < g.min_reg_size) {
+        status = kSpecSmall;
+        len = n;
+        touched = n;
+      } else {
+        FitProf fp;
+        lane_rect(buf, n, reg_angle, prec, p, rec, F.q, sw);
+        status = lane_refine<false>(F, sd, buf, n, reg_angle, prec, p, rec, myval1, off, len,
+                                    touched, fp, nullptr);
+      }
+    }
+    wg_fence();
+    __syncthreads();
+    const long long t2 = clock64();
+    cyc_spec += t1 - t0;
+    cyc_fit += t2 - t1;
+    // ---- re-read the claims: an earlier seed's smaller stamp = conflict ----
+    bool conflict = act && v < ncand && status < 0;
+    if (act && v < ncand && status >= 0) {
+      for (int j0 = 0; j0 < touched && !conflict; j0 += 8) {
+        uint32_t ev[8], sv[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) ev[u] = buf[min(j0 + u, touched - 1)].x;
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+          sv[u] = ld_stamp(sd, lsd_sd_index((int)(ev[u] & 0xFFFF), (int)(ev[u] >> 16), F.tw));
+#pragma unroll
+        for (int u = 0; u < 8; u++) conflict |= (sv[u] >> 1) != tag;
+      }
+    }
+    // ---- commit in seed order: slots [lo, hi) ----
+    const unsigned long long cm = sp_vmask(conflict, s_vb, wv, lane);
+    int first = sp_next(cm, 0, ncand);
+    int lo = 0, hi = first;
+    int stop = ncand;
+    while (true) {
+      const bool mine = act && v >= lo && v < hi;
+      if (mine && len > 0) {
+        for (int j0 = off; j0 < off + len; j0 += 8) {
+          uint32_t ev[8];
+#pragma unroll
+          for (int u = 0; u < 8; u++) ev[u] = buf[min(j0 + u, off + len - 1)].x;
+#pragma unroll
+          for (int u = 0; u < 8; u++) {
+            const int id = lsd_sd_index((int)(ev[u] & 0xFFFF), (int)(ev[u] >> 16), F.tw);
+            __hip_atomic_store(sd_hi(sd, id), 0u, __ATOMIC_RELAXED, ORBPL_LSD_SCOPE);
+          }
+        }
+      }
+      const bool is_cand = mine && status == kSpecCand;
+      const unsigned long long km = sp_vmask(is_cand, s_vb, wv, lane);
+      if (is_cand) {
+        const int k = nl + __popcll(km & vlt);
+        if (k < kLsdMaxCand) {
+          double* o = cand_out + (long long)k * 12;
+          o[0] = rec.x1; o[1] = rec.y1; o[2] = rec.x2; o[3] = rec.y2;
+          o[4] = rec.width; o[5] = rec.x; o[6] = rec.y; o[7] = rec.theta;
+          o[8] = rec.dx; o[9] = rec.dy; o[10] = rec.prec; o[11] = rec.p;
+        }
+      }
+      nl += __popcll(km);
+      __threadfence_block();
+      __syncthreads();
+      if (first >= ncand) break;
+      const uint32_t spt = s_pt[first];
+      if (used_get(F, (int)(spt & 0xFFFF), (int)(spt >> 16))) {
+        // covered by a committed region: the sequential loop skips it
+        const int nxt = sp_next(cm, first + 1, ncand);
+        lo = first + 1;
+        hi = nxt;
+        first = nxt;
+        __syncthreads();   // every wave has read the USED bit before new stores
+        continue;
+      }
+      stop = first;
+      break;
+    }
+    cyc_val += clock64() - t2;
+    bool carry = false;
+    if (stop < ncand) {
+      pos = s_pos[stop];
+      if (act && v == stop) s_misc[1] = status;
+      __syncthreads();
+      const int st_stop = s_misc[1];
+      __syncthreads();
+      if (st_stop == kSpecOverflow) {
+        // a region longer than a lane buffer: the wave-cooperative program
+        // (wave 0; the lane buffers it uses as scratch are idle)
+        if (wv == 0) {
+          const uint32_t spt = s_pt[stop];
+          double ra;
+          int nn = region_grow(F, (int)(spt & 0xFFFF), (int)(spt >> 16), ra, prec);
+          if (nn >= g.min_reg_size) {
+            Rect& rc = *F.rect0;
+            fill_q(F, nn);
+            region2rect(F, nn, ra, prec, p, rc);
+            if (refine(F, nn, ra, prec, p, rc, 0.7)) {
+              if (nl < kLsdMaxCand) {
+                const double* rv = reinterpret_cast<const double*>(F.rect0);
+                if (lane < 12) cand_out[(long long)nl * 12 + lane] = rv[lane];
+              }
+              nl++;
+            }
+          }
+          if (lane == 0) s_misc[1] = nl;
+        }
+        __threadfence_block();
+        __syncthreads();
+        nl = s_misc[1];
+        __syncthreads();
+        n_coop++;
+        pos++;
+      } else {
+        carry = true;
+        pos = next_pos;
+      }
+    } else {
+      pos = next_pos;
+    }
+    // ---- carry the seeds from `stop` on to slots [0, ncarry) in list order
+    // (kept when the re-check passed; a conflicting one whose seed pixel a
+    // committed region covers is dropped, as the sequential loop skips it)
+    {
+      bool car = act && carry && v >= stop && v < ncand;
+      const bool kp = car && v > stop && !conflict;
+      const uint32_t my_pt = s_pt[v];
+      const int my_pos = s_pos[v];
+      if (car && !kp && used_get(F, (int)(my_pt & 0xFFFF), (int)(my_pt >> 16))) car = false;
+      const unsigned long long cmc = sp_vmask(car, s_vb, wv, lane);
+      const int ncar = __popcll(cmc);
+      if (act) {
+        s_src[car ? __popcll(cmc & vlt) : ncar + __popcll(~cmc & vlt)] = v;
+        s_bufid[v] = bufid;
+        s_status[v] = status;
+        s_off[v] = off;
+        s_len[v] = len;
+        s_touched[v] = touched;
+        s_kp[v] = kp ? 1 : 0;
+        s_ptx[v] = my_pt;
+        s_posx[v] = my_pos;
+        s_rec[v][0] = rec.x1; s_rec[v][1] = rec.y1; s_rec[v][2] = rec.x2; s_rec[v][3] = rec.y2;
+        s_rec[v][4] = rec.width; s_rec[v][5] = rec.x; s_rec[v][6] = rec.y; s_rec[v][7] = rec.theta;
+        s_rec[v][8] = rec.dx; s_rec[v][9] = rec.dy; s_rec[v][10] = rec.prec; s_rec[v][11] = rec.p;
+      }
+      __syncthreads();
+      if (act) {
+        const int src = s_src[v];
+        keep = s_kp[src] != 0 && v < ncar;
+        bufid = s_bufid[src];
+        status = s_status[src];
+        off = s_off[src];
+        len = s_len[src];
+        touched = s_touched[src];
+        rec.x1 = s_rec[src][0]; rec.y1 = s_rec[src][1]; rec.x2 = s_rec[src][2];
+        rec.y2 = s_rec[src][3]; rec.width = s_rec[src][4]; rec.x = s_rec[src][5];
+        rec.y = s_rec[src][6]; rec.theta = s_rec[src][7]; rec.dx = s_rec[src][8];
+        rec.dy = s_rec[src][9]; rec.prec = s_rec[src][10]; rec.p = s_rec[src][11];
+        if (v < ncar) {
+          s_pt[v] = s_ptx[src];
+          s_pos[v] = s_posx[src];
+        }
+      }
+      ncarry = ncar;
+      __threadfence_block();
+      __syncthreads();
+    }
+    round++;
+  }
+  if (t == 0) {
+    sc.ncand[f] = min(nl, kLsdMaxCand);
+    if (nl > kLsdMaxCand) atomicOr(sc.err + f, 8);
+  }
+  if (sc.prof && t == 0) {
+    long long* pr = sc.prof + f * 8;
+    pr[0] = cyc_spec;
+    pr[1] = n_rounds;
+    pr[2] = n_spec;   // wave 0's slots only
+    pr[3] = clock64() - t_all;
+    pr[4] = cyc_fit;
+    pr[5] = cyc_val;
+    pr[6] = n_coop << 40;
+    pr[7] = nl;
+  }
+}
+
 // NFA validation of every refined rectangle (rect_improve), one lane per
 // rectangle; the accepted segments are compacted in seed order by
 // k_lsd_compact.
@@ -2360,7 +2717,11 @@ void launch_lsd_grow(const LsdGeom& g, const LsdScratch& sc, int batch, hipStrea
       // per SIMD (no spills on the seed chain) instead of the co-residence bound
       static const char* sb_env = getenv("ORBPL_SPEC_SMALL");
       static const int small_batch = sb_env ? atoi(sb_env) : kSpecSmallBatch;
-      if (batch <= small_batch)
+      static const char* sp_env = getenv("ORBPL_SPEC_SPARSE");
+      static const int sparse_batch = sp_env ? atoi(sp_env) : kSpecSparseBatch;
+      if (batch <= sparse_batch)
+        hipLaunchKernelGGL(k_lsd_spec_sparse, dim3(batch), dim3(256), smem, s, g, sc);
+      else if (batch <= small_batch)
         hipLaunchKernelGGL((k_lsd_spec<1, 1>), dim3(batch), dim3(64), smem, s, g, sc);
       else
         hipLaunchKernelGGL(k_lsd_spec<1>, dim3(batch), dim3(64), smem, s, g, sc);

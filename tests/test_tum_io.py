@@ -106,3 +106,47 @@ def test_ate_of_the_reference_result():
     assert r["n"] == 1352
     assert round(r["rmse"], 4) == 0.0540 and round(r["mean"], 4) == 0.0454
     assert round(r["median"], 4) == 0.0367 and round(r["max"], 4) == 0.1782
+
+
+TUM1_TEXT = ("%YAML:1.0\n\n# Camera calibration and distortion parameters (OpenCV)\n"
+             "Camera.fx: 517.306408\nCamera.fy: 516.469215\nCamera.cx: 318.643040\n"
+             "Camera.cy: 255.313989\n\nCamera.k1: 0.262383\nCamera.k2: -0.953104\n"
+             "Camera.p1: -0.005358\nCamera.p2: 0.002628\nCamera.k3: 1.163314\n\n"
+             "Camera.width: 640\nCamera.height: 480\n\n# Camera frames per second \n"
+             "Camera.fps: 30.0\n\nCamera.bf: 40.0\nCamera.RGB: 1\nThDepth: 40.0\n"
+             "DepthMapFactor: 5000.0\n\nORBextractor.nFeatures: 1000\n"
+             "ORBextractor.scaleFactor: 1.2\nORBextractor.nLevels: 8\n"
+             "ORBextractor.iniThFAST: 20\nORBextractor.minThFAST: 7\n"
+             "Viewer.KeyFrameSize: 0.05\nViewer.PointSize:2\n")
+
+
+def test_native_settings_loader(tmp_path, orbpl):
+    """orbpl_settings_load (the C++ reader of Tracking.cc:53-147) on the
+    reference's TUM1.yaml content (Examples/RGB-D/TUM1.yaml): every field as
+    Tracking::Tracking reads it, equal to the Python reader's camera; a
+    settings file without fps / ThDepth / DepthMapFactor takes the
+    reference's fallbacks (fps 30, depth factor 1)."""
+    p = tmp_path / "TUM1.yaml"
+    p.write_text(TUM1_TEXT)
+    orb, cam, extra = orbpl.load_settings(p, "rgbd")
+    _, pc, porb, pdmf = tum.load_settings(p)
+    ref = orbpl.make_camera(pc)
+    for f, _ in orbpl.Camera._fields_:
+        assert getattr(cam, f) == getattr(ref, f), f
+    assert (orb.nfeatures, orb.nlevels, orb.ini_th_fast, orb.min_th_fast) == (1000, 8, 20, 7)
+    assert orb.scale_factor == np.float32(1.2)
+    assert extra["fps"] == 30.0 and extra["max_frames"] == 30 and extra["rgb"] == 1
+    assert np.float32(extra["depth_map_factor"]) == pdmf
+    # stereo: no depth factor; monocular: no depth threshold
+    _, cs, es = orbpl.load_settings(p, "stereo")
+    assert es["depth_map_factor"] == 1.0 and cs.th_depth == ref.th_depth
+    _, cm, _ = orbpl.load_settings(p, "monocular")
+    assert cm.th_depth == 0.0
+    q = tmp_path / "bare.yaml"
+    q.write_text("%YAML:1.0\nCamera.fx: 700\nCamera.bf: 350.0\nORBextractor.nFeatures: 2000.4\n")
+    orb2, cam2, e2 = orbpl.load_settings(q, "rgbd")
+    assert e2["fps"] == 30.0 and e2["max_frames"] == 30 and e2["depth_map_factor"] == 1.0
+    assert orb2.nfeatures == 2000 and cam2.th_depth == 0.0 and cam2.k1 == 0.0
+    import pytest
+    with pytest.raises(orbpl.OrbplError):
+        orbpl.load_settings(tmp_path / "missing.yaml")
