@@ -2267,8 +2267,17 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
 // seeds of ORBPL_SPEC_KEEP are carried across waves through LDS. Only where
 // the GPU has spare SIMDs (batches of at most kSpecSparseBatch frames).
 // ---------------------------------------------------------------------------
+// Measured (tools/gpu_r04_e.sh, two rounds, bit-exact: 26 LSD tests): LSD
+// batch 1 / 16 / 64 / 96 = 48.8-52.7 / 68 / 69 / 69 ms against the one-wave
+// loop's 48.1-48.7 / 58 / 60 / 61 ms. Wave 0's grow phase fell 40-45M -> 28-33M
+// cycles per frame, but the round (grow + fit up to the last wave) rose
+// 252-280k -> 300k cycles: the four waves of a CU share its scalar unit and
+// instruction issue, and every wave runs the whole control flow (its exec-mask
+// SALU work, the per-round barriers), so their chains do not overlap as four
+// independent SIMDs would. Off (batch threshold 0); ORBPL_SPEC_SPARSE=<max
+// batch> turns it on for A/B runs.
 #ifndef ORBPL_SPEC_SPARSE_BATCH
-#define ORBPL_SPEC_SPARSE_BATCH 96
+#define ORBPL_SPEC_SPARSE_BATCH 0
 #endif
 constexpr int kSpecSparseBatch = ORBPL_SPEC_SPARSE_BATCH;
 
