@@ -184,7 +184,8 @@ typedef struct orbpl_settings {
   orbpl_camera cam;
   float fps;
   int32_t max_frames;
-  float depth_map_factor;
+  float depth_map_factor;      /* mDepthMapFactor (1 / DepthMapFactor)       */
+  float depth_map_factor_setting;  /* DepthMapFactor as read (orbpl_tracker_step_host) */
   int32_t rgb;                 /* Camera.RGB */
 } orbpl_settings;
 int orbpl_settings_load(const char* path, int sensor, orbpl_settings* out);

@@ -338,7 +338,8 @@ class Camera(C.Structure):
 class Settings(C.Structure):
     """orbpl_settings: Tracking::Tracking's settings (Tracking.cc:53-147)."""
     _fields_ = [("orb", OrbParams), ("cam", Camera), ("fps", C.c_float),
-                ("max_frames", C.c_int32), ("depth_map_factor", C.c_float), ("rgb", C.c_int32)]
+                ("max_frames", C.c_int32), ("depth_map_factor", C.c_float),
+                ("depth_map_factor_setting", C.c_float), ("rgb", C.c_int32)]
 
 
 SENSOR = {"monocular": 0, "stereo": 1, "rgbd": 2}
@@ -354,7 +355,9 @@ def load_settings(path, sensor="rgbd"):
     check(L.orbpl_settings_load(str(path).encode(), SENSOR[sensor], C.byref(out)),
           "orbpl_settings_load")
     return out.orb, out.cam, dict(fps=out.fps, max_frames=out.max_frames,
-                                  depth_map_factor=out.depth_map_factor, rgb=out.rgb)
+                                  depth_map_factor=out.depth_map_factor,
+                                  depth_map_factor_setting=out.depth_map_factor_setting,
+                                  rgb=out.rgb)
 
 
 def th_depth(cfg):

@@ -149,6 +149,7 @@ int orbpl_settings_load(const char* path, int sensor, orbpl_settings* out) {
   r.depth_map_factor = 1.0f;
   if (sensor == ORBPL_SENSOR_RGBD) {
     const float f = s.getf("DepthMapFactor");
+    r.depth_map_factor_setting = f;
     r.depth_map_factor = std::fabs(f) < 1e-5 ? 1.0f : 1.0f / f;
   }
   *out = r;

@@ -137,6 +137,7 @@ def test_native_settings_loader(tmp_path, orbpl):
     assert orb.scale_factor == np.float32(1.2)
     assert extra["fps"] == 30.0 and extra["max_frames"] == 30 and extra["rgb"] == 1
     assert np.float32(extra["depth_map_factor"]) == pdmf
+    assert extra["depth_map_factor_setting"] == 5000.0
     # stereo: no depth factor; monocular: no depth threshold
     _, cs, es = orbpl.load_settings(p, "stereo")
     assert es["depth_map_factor"] == 1.0 and cs.th_depth == ref.th_depth
