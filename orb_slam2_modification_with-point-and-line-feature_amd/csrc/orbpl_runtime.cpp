@@ -19,6 +19,27 @@
 
 namespace orbpl {
 
+// Hardware queues: the HIP runtime maps a process's streams onto
+// GPU_MAX_HW_QUEUES queues (4 by default, read when the runtime starts); a
+// tracker drives up to eight streams, which then share queues and serialise
+// (DESIGN.md §4 Tracker). At library load, before the runtime starts in a
+// process whose first HIP user is this library (the reference's process with
+// the drop-ins, the bench), the variable is raised to 16 unless it already
+// asks for at least 8; ORBPL_HW_QUEUES=<n> chooses n instead, 0 leaves the
+// process's setting alone. A runtime another library started earlier keeps
+// its queues: the split switches below then read the raised value, which
+// ORBPL_LSD_SPLIT=0 / ORBPL_ORB_SPLIT=0 override.
+__attribute__((constructor)) static void raise_hw_queues() {
+  const char* want = getenv("ORBPL_HW_QUEUES");
+  const int n = want ? atoi(want) : 16;
+  if (n <= 0) return;
+  const char* q = getenv("GPU_MAX_HW_QUEUES");
+  if (q && atoi(q) >= (want ? n : 8)) return;
+  char buf[16];
+  snprintf(buf, sizeof(buf), "%d", n > 32 ? 32 : n);
+  setenv("GPU_MAX_HW_QUEUES", buf, 1);
+}
+
 static thread_local std::string g_last_error;
 
 void set_error(const char* fmt, const char* a, int line) {
