@@ -46,7 +46,8 @@ struct Rect {
 
 struct Frame {
   int sw, sh;
-  const float* deg;
+  const float* deg;   // lsd_deg_index tiles
+  int dtw;
   const int* q;
   uint32_t* used;     // LDS bits (k_lsd_grow)
   uint64_t* usd;      // k_lsd_spec: USED lives in the claim stamps (high words, 0 = USED)
@@ -265,7 +266,7 @@ __device__ __forceinline__ void prefetch_ring(Frame& F, int i0, int i1) {
 #pragma unroll
     for (int k = 0; k < 9; k++) {
       const int xx = x + (k % 3) - 1, yy = y + (k / 3) - 1;
-      v[k] = (xx >= 0 && xx < F.sw && yy >= 0 && yy < F.sh) ? F.deg[yy * F.sw + xx] : kLsdNotdef;
+      v[k] = (xx >= 0 && xx < F.sw && yy >= 0 && yy < F.sh) ? F.deg[lsd_deg_index(xx, yy, F.dtw)] : kLsdNotdef;
     }
     float* r = F.ring + (j & 63) * 9;
 #pragma unroll
@@ -543,7 +544,7 @@ __device__ __forceinline__ double rect_nfa(Frame& F, const Rect& rec_lds) {
       if (k < total) {
         while (r + 1 < nrows && F.rows[r + 1].w <= k) r++;
         const int4 rw = F.rows[r];
-        dv[u] = F.deg[rw.x * F.sw + rw.y + (k - rw.w)];
+        dv[u] = F.deg[lsd_deg_index(rw.y + (k - rw.w), rw.x, F.dtw)];
       }
     }
 #pragma unroll
@@ -1617,6 +1618,7 @@ __device__ __forceinline__ double rect_nfa_lane(const float* __restrict__ deg, i
     xe = min((int)right_x, sw - 1);
   }
   int total = 0, alg = 0;
+  const int dtw = lsd_deg_tw(sw);
   const double theta = rec.theta, prec = rec.prec;
   while (y <= mxy) {
     int idx[8];
@@ -1637,7 +1639,7 @@ __device__ __forceinline__ double rect_nfa_lane(const float* __restrict__ deg, i
       }
       idx[u] = 0;
       if (y <= mxy) {
-        idx[u] = y * sw + x;
+        idx[u] = lsd_deg_index(x, y, dtw);
         valid |= 1u << u;
         x++;
       }
@@ -1715,7 +1717,8 @@ __global__ void __launch_bounds__(64) k_lsd_grow(LsdGeom g, LsdScratch sc) {
   Frame F;
   F.sw = sw;
   F.sh = sh;
-  F.deg = sc.deg + (long long)f * sw * sh;
+  F.deg = sc.deg + (long long)f * lsd_deg_words(sw, sh);
+  F.dtw = lsd_deg_tw(sw);
   F.q = sc.q + (long long)f * sw * sh;
   F.used = grow_smem;
   F.usd = nullptr;
@@ -1750,7 +1753,7 @@ __global__ void __launch_bounds__(64) k_lsd_grow(LsdGeom g, LsdScratch sc) {
       const int idx = (int)(A[i] & 0x3FFFFFu);
       py = idx / w1;
       px = idx - py * w1;
-      def = F.deg[py * sw + px] >= 0.f;
+      def = F.deg[lsd_deg_index(px, py, F.dtw)] >= 0.f;
     }
     unsigned long long mask = __ballot(def && !used_get(F, px, py));
     while (mask) {
@@ -1879,7 +1882,8 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
   Frame F;
   F.sw = sw;
   F.sh = sh;
-  F.deg = sc.deg + (long long)f * sw * sh;
+  F.deg = sc.deg + (long long)f * lsd_deg_words(sw, sh);
+  F.dtw = lsd_deg_tw(sw);
   F.q = sc.q + (long long)f * sw * sh;
   F.used = nullptr;
   // the cooperative fallback's region list head and prefetch ring live in
@@ -2314,7 +2318,8 @@ __global__ void __launch_bounds__(256, 1) k_lsd_spec_sparse(LsdGeom g, LsdScratc
   Frame F;
   F.sw = sw;
   F.sh = sh;
-  F.deg = sc.deg + (long long)f * sw * sh;
+  F.deg = sc.deg + (long long)f * lsd_deg_words(sw, sh);
+  F.dtw = lsd_deg_tw(sw);
   F.q = sc.q + (long long)f * sw * sh;
   F.used = nullptr;
   uint4* fbuf = sc.lbuf + (long long)f * NS * kLaneCap;
@@ -2641,7 +2646,7 @@ __global__ void __launch_bounds__(256, ORBPL_VAL_MINW) k_lsd_validate(LsdGeom g,
   __shared__ int s_next;
   const int f = blockIdx.y;
   const int nc = sc.ncand[f];
-  const float* deg = sc.deg + (long long)f * g.sw * g.sh;
+  const float* deg = sc.deg + (long long)f * lsd_deg_words(g.sw, g.sh);
   if (threadIdx.x == 0) s_next = 256;
   __syncthreads();
   for (int k = threadIdx.x;; k = atomicAdd(&s_next, 1)) {

@@ -81,6 +81,17 @@ __host__ __device__ inline int lsd_sd_index(int x, int y, int tw) {
   const int i = ((((y >> 2) * tw) + (x >> 2)) << 4) | ((y & 3) << 2) | (x & 3);
   return ORBPL_SD_PAIRED ? 2 * i : i;
 }
+// The degree plane (LsdScratch::deg) in 8x4-pixel tiles of 128 B: the NFA
+// walk of k_lsd_validate reads a rectangle row by row, and a thin oblique
+// rectangle's consecutive rows then share a line (row-major, every row of it
+// was a line of its own).
+__host__ __device__ inline int lsd_deg_tw(int sw) { return (sw + 7) >> 3; }
+__host__ __device__ inline long long lsd_deg_words(int sw, int sh) {
+  return (long long)lsd_deg_tw(sw) * ((sh + 3) >> 2) * 32;
+}
+__host__ __device__ inline int lsd_deg_index(int x, int y, int dtw) {
+  return ((((y >> 2) * dtw) + (x >> 3)) << 5) | ((y & 3) << 3) | (x & 7);
+}
 // offset (u64 words) of a pixel's angle terms from its pixel word
 __host__ __device__ inline long long lsd_cs_offset(int sw, int sh) {
   return ORBPL_SD_PAIRED ? 1 : lsd_sd_words(sw, sh);
@@ -89,7 +100,8 @@ __host__ __device__ inline long long lsd_cs_offset(int sw, int sh) {
 struct LsdScratch {
   uint8_t* blur;       // W*H
   uint8_t* scaled;     // sw*sh
-  float* deg;          // sw*sh, fastAtan2 degrees or kLsdNotdef
+  float* deg;          // lsd_deg_words per frame (lsd_deg_index tiles), fastAtan2
+                       // degrees or kLsdNotdef
   int* q;              // sw*sh, gx^2 + gy^2
   unsigned* maxq;      // 1 per frame
   uint32_t* A;         // n: key << 22 | raster index, sorted in place

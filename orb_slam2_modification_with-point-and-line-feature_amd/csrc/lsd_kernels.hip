@@ -142,7 +142,7 @@ __global__ void __launch_bounds__(256) k_lsd_grad(LsdGeom g, const uint8_t* __re
         mq = (unsigned)qq;
       }
     }
-    deg[o] = d;
+    deg[(long long)f * lsd_deg_words(sw, sh) + lsd_deg_index(x, y, lsd_deg_tw(sw))] = d;
     q[o] = qq;
     // the speculative seed loop's pixel word: degrees + unclaimed stamp
     uint64_t* fsd = sd + (long long)f * lsd_sd_frame_words(sw, sh);
@@ -277,6 +277,8 @@ __global__ void __launch_bounds__(256) k_lsd_prep(LsdGeom g, const int* __restri
   unsigned mq = 0;
   const int tw = lsd_sd_tw(sw);
   const long long fo = (long long)f * sw * sh;
+  const int dtw = lsd_deg_tw(sw);
+  const long long dfo = (long long)f * lsd_deg_words(sw, sh);
   uint64_t* fsd = sd + (long long)f * lsd_sd_frame_words(sw, sh);
   const long long csw = lsd_cs_offset(sw, sh);
   for (int i = t; i < kPrTH * kPrTW; i += 256) {
@@ -298,7 +300,7 @@ __global__ void __launch_bounds__(256) k_lsd_prep(LsdGeom g, const int* __restri
         mq = max(mq, (unsigned)qq);
       }
     }
-    deg[o] = d;
+    deg[dfo + lsd_deg_index(x, y, dtw)] = d;
     q[o] = qq;
     const int si = lsd_sd_index(x, y, tw);
     fsd[si] = (0xFFFFFFFFull << 32) | (uint64_t)__float_as_uint(d);

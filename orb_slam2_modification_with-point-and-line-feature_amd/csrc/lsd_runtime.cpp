@@ -234,7 +234,7 @@ int lsdx_create(int width, int height, int max_batch, int device, lsdx_ctx** out
   LA(c->d_in, B * width * height);
   LA(s.blur, B * width * height);
   LA(s.scaled, B * px);
-  LA(s.deg, B * px * 4);
+  LA(s.deg, B * (size_t)lsd_deg_words(g.sw, g.sh) * 4);
   LA(s.q, B * px * 4);
   LA(s.maxq, B * 4);
   LA(s.A, B * n * 4);
@@ -460,7 +460,15 @@ int lsdx_get_stages(lsdx_ctx* c, int frame, uint8_t* scaled, float* deg, uint32_
   if (sh) *sh = g.sh;
   if (n_order) *n_order = g.n;
   if (scaled) HIP_CHECK(hipMemcpy(scaled, c->sc.scaled + frame * px, px, hipMemcpyDeviceToHost));
-  if (deg) HIP_CHECK(hipMemcpy(deg, c->sc.deg + frame * px, px * 4, hipMemcpyDeviceToHost));
+  if (deg) {
+    // the plane is tiled on the device (lsd_deg_index); row-major here
+    const long long dw = lsd_deg_words(g.sw, g.sh);
+    std::vector<float> t((size_t)dw);
+    HIP_CHECK(hipMemcpy(t.data(), c->sc.deg + frame * dw, (size_t)dw * 4, hipMemcpyDeviceToHost));
+    const int dtw = lsd_deg_tw(g.sw);
+    for (int y = 0; y < g.sh; y++)
+      for (int x = 0; x < g.sw; x++) deg[(size_t)y * g.sw + x] = t[lsd_deg_index(x, y, dtw)];
+  }
   if (order) {
     std::vector<uint32_t> a(g.n);
     HIP_CHECK(hipMemcpy(a.data(), c->sc.A + (size_t)frame * g.n, (size_t)g.n * 4,

@@ -17,6 +17,9 @@
 //   dropin_driver --time <in.bin> <K>: K Frame constructions of frame 0 (ORB ||
 //   LineExtractor on two host threads + the frame glue, one frame at a time as
 //   the reference's Tracking builds them), median / mean latency in ms
+//   dropin_driver --fail: a Frame from an 8x8 image, which the library's
+//   extractors reject: the error must reach the caller as an exception (the
+//   line thread joined first), printed as "caught: <message>", exit 0
 // in.bin : int32 W, H; float fx fy cx cy k1 k2 p1 p2 k3 bf thdepth;
 //          int32 nfeatures; float scale; int32 nlevels, iniTh, minTh;
 //          float Tcw0[16]; 3 x (gray W*H u8, depth W*H f32);
@@ -93,7 +96,30 @@ static std::vector<int32_t> node_of(const DBoW2::FeatureVector& fv, int n) {
   return node;
 }
 
+static int fail_mode() {
+  ORBextractor ex(1000, 1.2f, 8, 20, 7);
+  cv::Mat K = cv::Mat::eye(3, 3, cv::CV_32F);
+  K.at<float>(0, 0) = K.at<float>(1, 1) = 500.f;
+  K.at<float>(0, 2) = K.at<float>(1, 2) = 4.f;
+  cv::Mat dist(5, 1, cv::CV_32F);
+  for (int k = 0; k < 5; k++) dist.at<float>(k, 0) = 0.f;
+  cv::Mat g(8, 8, cv::CV_8U), d(8, 8, cv::CV_32F);
+  for (int i = 0; i < 64; i++) {
+    g.data[i] = (uint8_t)(i * 37);
+    d.ptr<float>()[i] = 1.f;
+  }
+  try {
+    Frame F(g, d, 0.0, &ex, nullptr, K, dist, 40.f, 40.f);
+  } catch (const std::exception& e) {
+    printf("caught: %s\n", e.what());
+    return 0;
+  }
+  printf("no error\n");
+  return 1;
+}
+
 int main(int argc, char** argv) {
+  if (argc == 2 && std::string(argv[1]) == "--fail") return fail_mode();
   const bool timing = argc == 4 && std::string(argv[1]) == "--time";
   if (argc != 3 && !timing) {
     fprintf(stderr, "usage: dropin_driver in.bin out.bin | dropin_driver --time in.bin K\n");

@@ -242,3 +242,15 @@ def test_dropin_classes_match_oracle(tmp_path, cam_name, seed):
     To3, _, _, no3 = pose(mloc, lloc, Tcur)
     assert np.abs(T3 - To3).max() < 1e-4 and ninl3 == no3
     assert R.off == len(R.buf)
+
+
+def test_dropin_frame_error_reaches_caller():
+    """A library error inside the drop-in Frame constructor (an 8x8 image the
+    extractors reject on the GPU box; no HIP device here) reaches the caller
+    as a C++ exception after the line thread is joined, instead of
+    std::terminate (ADVICE r3: dropin/Frame.cc). No compute is launched."""
+    if not DRIVER.exists():
+        pytest.skip("dropin_driver not built (__graft_entry__.build())")
+    r = subprocess.run([str(DRIVER), "--fail"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
+    assert r.stdout.startswith("caught: "), r.stdout

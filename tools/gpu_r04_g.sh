@@ -1,0 +1,28 @@
+#!/bin/bash
+# Round-4 pass g: where the batch-1 lines step goes - kernel trace of the LSD
+# detector alone (1 and 16 frames) and of the lines tracker at 1 stream.
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r04g
+mkdir -p $O
+cd /tmp && export TMPDIR=/tmp
+export GPU_MAX_HW_QUEUES=16
+for B in 1 16; do
+  timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $O/lsd_$B -o run --output-format csv -- python3 $R/tools/time_lsd.py $B > $O/lsd_$B.log 2>&1 || { echo "lsd $B failed"; tail -5 $O/lsd_$B.log; exit 1; }
+  head -2 $O/lsd_$B.log
+done
+COMMON="--no-cpu-baseline --no-parity --sweep 0 --secondary-steps 0 --stereo-steps 0 --rig-steps 0 --isolated-steps 0 --ingress-steps 0 --trk-load 0"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/lines_1 -o run --output-format csv -- python3 $R/bench.py --workload lines --streams 1 --steps 10 --warmup 3 $COMMON > $O/lines_1.json 2> $O/lines_1.err || { echo "lines 1 failed"; tail -5 $O/lines_1.err; exit 1; }
+python3 - <<'PY'
+import csv, collections, os, glob
+O = os.environ["GRAFT_REPO_ROOT"] + "/gpurun_out/r04g"
+for d in ("lsd_1", "lsd_16", "lines_1"):
+    fs = glob.glob(f"{O}/{d}/**/run_kernel_stats.csv", recursive=True)
+    if not fs:
+        print(d, "no stats"); continue
+    rows = list(csv.DictReader(open(fs[0])))
+    print("==", d)
+    for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:14]:
+        print(f'{r["Name"][:60]:60s} calls {r["Calls"]:>5s} avg {float(r["AverageNs"])/1e6:8.3f} ms max {float(r["MaxNs"])/1e6:8.3f}')
+PY
+exit 0
