@@ -159,6 +159,74 @@ __device__ __forceinline__ fshort2 fast_m2_regs(const uint2* R) {
   return pmax(pmax(A, nB), zero);
 }
 
+// ORBPL_FAST_MM3 (default): the same selections on gfx950's packed 3-input
+// v_pk_maximum3_f16 / v_pk_minimum3_f16. A u16 lane holding a pixel value
+// 0 .. 255 read as f16 is a subnormal (value x 2^-24), ordered as the
+// integers, and IEEE maximum / minimum return one of their inputs bit for bit
+// (no NaN can occur, f16 denormals are preserved: the kernel descriptor's
+// float_denorm_mode_16_64 is 3), so a 3-input op selects exactly what two
+// v_pk_max_u16 / v_pk_min_u16 do. The window extrema fold into 3-input steps,
+// the 8-window max/min into the arc step (max3(suffix, prefix, min(p_k,
+// p_k+9))) and the arc reduction into 3-input trees: 68 packed ops for two
+// centres instead of 98.
+#ifndef ORBPL_FAST_MM3
+#define ORBPL_FAST_MM3 1
+#endif
+typedef _Float16 fhalf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ fhalf2 as_h2(uint32_t v) { return __builtin_bit_cast(fhalf2, v); }
+__device__ __forceinline__ fhalf2 hmax(fhalf2 a, fhalf2 b) { return __builtin_elementwise_maximum(a, b); }
+__device__ __forceinline__ fhalf2 hmin(fhalf2 a, fhalf2 b) { return __builtin_elementwise_minimum(a, b); }
+__device__ __forceinline__ fhalf2 hmax3(fhalf2 a, fhalf2 b, fhalf2 c) { return hmax(hmax(a, b), c); }
+__device__ __forceinline__ fhalf2 hmin3(fhalf2 a, fhalf2 b, fhalf2 c) { return hmin(hmin(a, b), c); }
+
+// suffixes from odd starts and prefixes to even ends of both ring halves
+// (fast_windows' s / pr) with 3-input ops: 6 per half
+template <bool kMax>
+__device__ __forceinline__ void fast_sp3(const fhalf2* p, fhalf2 (*s)[4], fhalf2 (*pr)[4]) {
+  auto op3 = [](fhalf2 a, fhalf2 b, fhalf2 c) { return kMax ? hmax3(a, b, c) : hmin3(a, b, c); };
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const fhalf2* d = p + 8 * h;
+    s[h][3] = d[7];
+    s[h][2] = op3(d[5], d[6], d[7]);
+    s[h][1] = op3(d[3], d[4], s[h][2]);
+    s[h][0] = op3(d[1], d[2], s[h][1]);
+    pr[h][0] = d[0];
+    pr[h][1] = op3(d[0], d[1], d[2]);
+    pr[h][2] = op3(pr[h][1], d[3], d[4]);
+    pr[h][3] = op3(pr[h][2], d[5], d[6]);
+  }
+}
+
+__device__ __forceinline__ fshort2 fast_m2_mm3(const uint2* R) {
+  const uint32_t v = ring_pair(R, 0, 0);
+  constexpr int kDy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+  constexpr int kDx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+  fhalf2 p[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) p[k] = as_h2(ring_pair(R, kDy[k], kDx[k]));
+  fhalf2 sx[2][4], px[2][4], sn[2][4], pn[2][4];
+  fast_sp3<true>(p, sx, px);
+  fast_sp3<false>(p, sn, pn);
+  // arc pair k = 2i, 2i + 1 over the 8-window from 2i + 1: suffix of one half
+  // from 2i + 1 (mod 8) and prefix of the other half
+  fhalf2 ux[8], un[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const int k = 2 * i, h = i < 4 ? 0 : 1, j = i & 3;
+    const fhalf2 a = p[k], b = p[(k + 9) & 15];
+    ux[i] = hmax3(sx[h][j], px[1 - h][j], hmin(a, b));
+    un[i] = hmin3(sn[h][j], pn[1 - h][j], hmax(a, b));
+  }
+  const fhalf2 Ap = hmin3(hmin3(ux[0], ux[1], ux[2]), hmin3(ux[3], ux[4], ux[5]), hmin(ux[6], ux[7]));
+  const fhalf2 Bp = hmax3(hmax3(un[0], un[1], un[2]), hmax3(un[3], un[4], un[5]), hmax(un[6], un[7]));
+  const fshort2 zero = {0, 0};
+  const fshort2 sv = as_s2(v);
+  const fshort2 A = sv - as_s2(__builtin_bit_cast(uint32_t, Ap));
+  const fshort2 nB = as_s2(__builtin_bit_cast(uint32_t, Bp)) - sv;
+  return pmax(pmax(A, nB), zero);
+}
+
 // 8 bytes x-3 .. x+4 of a row from the 3 aligned dwords at q (x-3 = 4 q + o)
 __device__ __forceinline__ uint2 load_ring_row(const uint32_t* q, uint32_t o) {
   const uint32_t w0 = q[0], w1 = q[1], w2 = q[2];
@@ -559,8 +627,10 @@ __device__ __forceinline__ void nms_pair(const uint32_t* M, int ps, int r, int q
 __device__ __forceinline__ int wave_incl_scan(int v);
 
 // minimum waves per SIMD for k_fast_cells (register budget); see DESIGN.md
+// (6: the MM3 score fits 80 VGPRs without spills, 6 waves per SIMD; unbounded
+// it takes 81 and 5)
 #ifndef ORBPL_FAST_MINW
-#define ORBPL_FAST_MINW 1
+#define ORBPL_FAST_MINW 6
 #endif
 __global__ void __launch_bounds__(256, ORBPL_FAST_MINW) k_fast_cells(const uint8_t* __restrict__ pyr,
                                                     const OrbGeom* __restrict__ g,
@@ -646,7 +716,11 @@ __global__ void __launch_bounds__(256, ORBPL_FAST_MINW) k_fast_cells(const uint8
 #pragma unroll
         for (int k = 0; k < 6; k++) R[k] = R[k + 1];
         R[6] = load_ring_row(col + (long long)(r + 6) * pdw, o);
+#if ORBPL_FAST_MM3
+        const fshort2 m2 = fast_m2_mm3(R);
+#else
         const fshort2 m2 = fast_m2_regs(R);
+#endif
         const int wr = r + 3;
         const uint32_t lo = (uint32_t)(uint16_t)m2.x;
         const uint32_t hi = has_hi ? (uint32_t)(uint16_t)m2.y : 0u;

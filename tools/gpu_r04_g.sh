@@ -13,6 +13,10 @@ for B in 1 16; do
 done
 COMMON="--no-cpu-baseline --no-parity --sweep 0 --secondary-steps 0 --stereo-steps 0 --rig-steps 0 --isolated-steps 0 --ingress-steps 0 --trk-load 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/lines_1 -o run --output-format csv -- python3 $R/bench.py --workload lines --streams 1 --steps 10 --warmup 3 $COMMON > $O/lines_1.json 2> $O/lines_1.err || { echo "lines 1 failed"; tail -5 $O/lines_1.err; exit 1; }
+# VALU lane utilisation of the LSD kernels (thread-cycles / (active VALU cycles x 64))
+for B in 1 1536; do
+  timeout -s KILL 180 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVES -d $O/lane_$B -o run --output-format csv -- python3 $R/tools/time_lsd.py $B > $O/lane_$B.log 2>&1 || { echo "lane $B failed"; tail -5 $O/lane_$B.log; exit 1; }
+done
 python3 - <<'PY'
 import csv, collections, os, glob
 O = os.environ["GRAFT_REPO_ROOT"] + "/gpurun_out/r04g"
@@ -24,5 +28,17 @@ for d in ("lsd_1", "lsd_16", "lines_1"):
     print("==", d)
     for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:14]:
         print(f'{r["Name"][:60]:60s} calls {r["Calls"]:>5s} avg {float(r["AverageNs"])/1e6:8.3f} ms max {float(r["MaxNs"])/1e6:8.3f}')
+for B in (1, 1536):
+    fs = glob.glob(f"{O}/lane_{B}/**/run_counter_collection.csv", recursive=True)
+    if not fs:
+        print("lane", B, "no counters"); continue
+    v = collections.defaultdict(lambda: collections.defaultdict(float))
+    for r in csv.DictReader(open(fs[0])):
+        k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+        v[k][r["Counter_Name"]] += float(r["Counter_Value"])
+    for k, c in v.items():
+        if "lsd" in k and c.get("SQ_ACTIVE_INST_VALU"):
+            print(f"lane util B={B} {k[:40]:40s} {100 * c['SQ_THREAD_CYCLES_VALU'] / (c['SQ_ACTIVE_INST_VALU'] * 64):6.1f} %  "
+                  f"valu {c['SQ_INSTS_VALU']:.3g} waves {c['SQ_WAVES']:.0f}")
 PY
 exit 0
