@@ -2642,15 +2642,30 @@ constexpr int kValBlocksSmall = 8, kValBlocksLarge = 2;
 // the next one instead of idling until the wave's costliest walk ends (the
 // improvement loop runs rect_nfa up to ~25 times on rejected rectangles).
 // gridDim.x = workgroups per frame.
+// ORBPL_VAL_XCD: the workgroups of one frame on one XCD (workgroups are dealt
+// round-robin over the 8 XCDs by linear id; the remap gives each XCD a
+// contiguous range of frames), so the frame's degree-plane lines one block
+// fetched into that XCD's L2 serve its other blocks' walks too.
+#ifndef ORBPL_VAL_XCD
+#define ORBPL_VAL_XCD 1
+#endif
 __global__ void __launch_bounds__(256, ORBPL_VAL_MINW) k_lsd_validate(LsdGeom g, LsdScratch sc) {
   __shared__ int s_next;
-  const int f = blockIdx.y;
+#if ORBPL_VAL_XCD
+  const int nx = gridDim.x, nwg = nx * gridDim.y;
+  const int orig = blockIdx.x + nx * blockIdx.y;
+  const int xcd = orig & 7, qq = nwg >> 3, rr = nwg & 7;
+  const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (orig >> 3);
+  const int f = wg / nx, bxv = wg - f * nx;
+#else
+  const int f = blockIdx.y, bxv = blockIdx.x;
+#endif
   const int nc = sc.ncand[f];
   const float* deg = sc.deg + (long long)f * lsd_deg_words(g.sw, g.sh);
   if (threadIdx.x == 0) s_next = 256;
   __syncthreads();
   for (int k = threadIdx.x;; k = atomicAdd(&s_next, 1)) {
-    const int c = blockIdx.x + k * (int)gridDim.x;
+    const int c = bxv + k * (int)gridDim.x;
     if (c >= nc) break;
     const long long o = (long long)f * kLsdMaxCand + c;
     const double* rv = sc.cand + o * 12;

@@ -498,6 +498,107 @@ __device__ __forceinline__ void pyr_blur_rows(const LevelGeom& L, const uint8_t*
   }
 }
 
+#ifndef ORBPL_PYR_MERGE
+#define ORBPL_PYR_MERGE 1
+#endif
+
+// level 0 content rows [na, nb): the input image, 16 bytes per task
+__device__ __forceinline__ void pyr_copy_level0(const LevelGeom& L, const uint8_t* src, int stride,
+                                                uint8_t* fp, int na, int nb) {
+  const int nv = (L.w + 15) >> 4;
+  const uint32_t inv_nv = div_inv(nv);
+  for (int i = threadIdx.x; i < (nb - na) * nv; i += kPyrThreads) {
+    const int rr = div_small(i, inv_nv);
+    const int r = na + rr, c = (i - rr * nv) * 16;
+    const uint8_t* s = src + (long long)r * stride + c;
+    uint8_t* d = fp + content_off(L, c, r);
+    if (c + 16 <= L.w && ((reinterpret_cast<uintptr_t>(s) & 15) == 0)) {
+      *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(s);
+    } else {
+      const int n = min(16, L.w - c);
+      for (int k = 0; k < n; k++) d[k] = s[k];
+    }
+  }
+}
+
+// copyMakeBorder(19, REFLECT_101) of level L for the content rows [na, nb)
+// and the top / bottom mirror rows whose source row lies in [na, nb), all
+// from content bytes only (no dependency on other border bytes): per (row,
+// side) the 19 mirrored side bytes, per mirror row its content bytes.
+__device__ __forceinline__ void pyr_borders(const LevelGeom& L, uint8_t* fp, int na, int nb) {
+  const int t = threadIdx.x;
+  const int t0 = max(na, 1), t1 = min(nb, kEdge + 1);               // y = -cy
+  const int b0 = max(na, L.h - 1 - kEdge), b1 = min(nb, L.h - 1);   // y = 2h-2-cy
+  const int nt = max(0, t1 - t0), nbm = max(0, b1 - b0);
+  const int nc = nb - na, nrow = nc + nt + nbm;
+  // row j of the task list: (source content row, destination padded row)
+  auto rows_of = [&](int j, int* cy, int* py) {
+    if (j < nc) {
+      *cy = na + j;
+      *py = *cy + kEdge;
+    } else if (j < nc + nt) {
+      *cy = t0 + (j - nc);
+      *py = kEdge - *cy;
+    } else {
+      *cy = b0 + (j - nc - nt);
+      *py = 2 * L.h - 2 - *cy + kEdge;
+    }
+  };
+  if (L.w >= kEdge + 2) {
+    for (int i = t; i < nrow * 2; i += kPyrThreads) {
+      int cy, py;
+      rows_of(i >> 1, &cy, &py);
+      const int side = i & 1;
+      const uint8_t* srow = fp + L.pyr_off + (long long)(cy + kEdge) * L.pitch;
+      uint8_t* drow = fp + L.pyr_off + (long long)py * L.pitch;
+      const int c0 = side ? L.w - kEdge - 1 : 0;        // first content byte used
+      const int a = kContent0 + c0;                     // its byte in the row
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(srow + (a & ~3));
+      const int o = a & 3;
+      uint32_t w[6];
+#pragma unroll
+      for (int k = 0; k < 6; k++) w[k] = src[k];
+      auto byte_at = [&](int j) -> uint8_t {
+        const int b = o + j;
+        uint32_t v = w[0];
+#pragma unroll
+        for (int k = 1; k < 6; k++) v = (b >> 2) == k ? w[k] : v;
+        return (uint8_t)(v >> (8 * (b & 3)));
+      };
+      if (side == 0) {
+#pragma unroll
+        for (int px = 0; px < kEdge; px++) drow[kLead + px] = byte_at(kEdge - px);
+      } else {
+#pragma unroll
+        for (int k = 0; k < kEdge; k++) drow[kLead + L.w + kEdge + k] = byte_at(kEdge - 1 - k);
+      }
+    }
+  } else {
+    for (int i = t; i < nrow * 2 * kEdge; i += kPyrThreads) {
+      const int j = i / (2 * kEdge), k = i - j * 2 * kEdge;
+      int cy, py;
+      rows_of(j, &cy, &py);
+      const int px = k < kEdge ? k : L.w + k;          // padded column
+      const int cx = reflect101_dev(px - kEdge, L.w);
+      fp[padded_off(L, px, py)] = fp[content_off(L, cx, cy)];
+    }
+  }
+  // content bytes of the mirror rows: 16-byte chunks, the tail byte by byte
+  const int nv = (L.w + 15) >> 4;
+  for (int i = t; i < (nt + nbm) * nv; i += kPyrThreads) {
+    const int j = i / nv, q = i - j * nv;
+    int cy, py;
+    rows_of(nc + j, &cy, &py);
+    const uint8_t* s = fp + content_off(L, 16 * q, cy);
+    uint8_t* d = fp + L.pyr_off + (long long)py * L.pitch + kContent0 + 16 * q;
+    if (16 * q + 16 <= L.w) {
+      *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(s);
+    } else {
+      for (int k = 0; k < L.w - 16 * q; k++) d[k] = s[k];
+    }
+  }
+}
+
 __global__ void __launch_bounds__(kPyrThreads) k_pyramid(const uint8_t* __restrict__ img, int stride,
                                                          long long frame_pitch, uint8_t* pyr,
                                                          uint8_t* __restrict__ blur,
@@ -514,6 +615,31 @@ __global__ void __launch_bounds__(kPyrThreads) k_pyramid(const uint8_t* __restri
   uint8_t* fp = pyr + (long long)f * g->pyr_bytes;
   uint8_t* bp = blur + (long long)f * g->blur_bytes;
   const int nl = g->nlevels;
+#if ORBPL_PYR_MERGE
+  // Two barriers per level: P(l) = level l's content rows (copy / resize of
+  // level l-1's content) beside the blur of level l-1 (its padded rows are
+  // complete), then Q(l) = level l's side borders and mirror rows, both
+  // computed from content (a mirror row's side bytes reflect its source row's
+  // content, as the copy of the finished padded row gave them).
+  for (int l = 0; l <= nl; l++) {
+    if (l < nl) {
+      const LevelGeom& L = g->lv[l];
+      const int na = B.na[l], nb = B.nb[l];
+      if (l == 0) {
+        pyr_copy_level0(L, img + (long long)f * frame_pitch, stride, fp, na, nb);
+      } else {
+        pyr_resize_rows(L, g->lv[l - 1], rs_all + L.rs_off, fp, na, nb);
+      }
+    }
+    if (l > 0) pyr_blur_rows(g->lv[l - 1], fp, bp, B.oa[l - 1], B.ob[l - 1]);
+    if (stamp) prof[1 + 4 * min(l, nl - 1)] = (long long)wall_clock64();
+    if (l == nl) break;
+    __syncthreads();
+    pyr_borders(g->lv[l], fp, B.na[l], B.nb[l]);
+    __syncthreads();
+    if (stamp) prof[2 + 4 * l] = (long long)wall_clock64();
+  }
+#else
   for (int l = 0; l < nl; l++) {
     const LevelGeom& L = g->lv[l];
     const int na = B.na[l], nb = B.nb[l];
@@ -609,6 +735,7 @@ __global__ void __launch_bounds__(kPyrThreads) k_pyramid(const uint8_t* __restri
     pyr_blur_rows(L, fp, bp, B.oa[l], B.ob[l]);
     if (stamp) prof[4 + 4 * l] = (long long)wall_clock64();
   }
+#endif
 }
 
 // NMS for the centre pair at M[r][q], M[r][q+1]: returns (m_lo, m_hi) in
