@@ -100,9 +100,15 @@ constexpr int kLevelCols = kMaxLevelsT * kGridCols;   // (octave, grid column) r
 // configurations). The keypoints in the grid are held as records sorted by
 // (octave, column, row, index): the candidates of one octave in one grid
 // column are one contiguous range, in the reference's scan order.
+// ORBPL_LOCAL_DESC_LDS: the current descriptors staged in LDS (1) or read
+// from global memory (0, L2-resident: 32 KB less LDS per workgroup at 1024
+// keypoints, A/B build)
+#ifndef ORBPL_LOCAL_DESC_LDS
+#define ORBPL_LOCAL_DESC_LDS 1
+#endif
 template <int kLocalKp>
 struct LocalShared {
-  uint4 desc[kLocalKp * 2];          // current descriptors (32 B rows), by keypoint
+  uint4 desc[ORBPL_LOCAL_DESC_LDS ? kLocalKp * 2 : 1];   // current descriptors (32 B rows)
   float4 rec[kLocalKp];              // sorted records: x, y, uRight, bits(column | row | index)
   int mw[kLocalKp];                  // last writer (map point index) per keypoint
   int own[kLocalKp];                 // phase B: (round << 6) | (63 - lane) of the round's
@@ -202,7 +208,12 @@ __device__ TopList local_scan(const LocalShared<KP>& S, const TrackConsts& c, co
       const int j = (int)(w & 2047);
       if (is_claimed(S, j)) continue;
       if (R.z > 0 && fabsf(xr - R.z) > rad) continue;
+#if ORBPL_LOCAL_DESC_LDS
       const uint4 c0 = S.desc[2 * j], c1 = S.desc[2 * j + 1];
+#else
+      const uint4* cd = reinterpret_cast<const uint4*>(a.desc + (long long)j * 32);
+      const uint4 c0 = cd[0], c1 = cd[1];
+#endif
       const uint32_t dist = __popc(m0.x ^ c0.x) + __popc(m0.y ^ c0.y) + __popc(m0.z ^ c0.z) +
                             __popc(m0.w ^ c0.w) + __popc(m1.x ^ c1.x) + __popc(m1.y ^ c1.y) +
                             __popc(m1.z ^ c1.z) + __popc(m1.w ^ c1.w);
@@ -291,10 +302,12 @@ __global__ void __launch_bounds__(NT) k_match_local(TrackConsts c, LocalArgs a) 
 #endif
   // ---- keypoint index (AssignFeaturesToGrid with PosInGrid, Frame.cc:265-287, 527-538) ----
   for (int i = t; i < kLocalKp / 32; i += NT) S.claimed[i] = 0;
+#if ORBPL_LOCAL_DESC_LDS
   {
     const uint4* d = reinterpret_cast<const uint4*>(a.desc);
     for (int i = t; i < 2 * n; i += NT) S.desc[i] = d[i];
   }
+#endif
   __syncthreads();
   for (int i = t; i < kLocalKp; i += NT) {
     uint32_t key = kEmpty;

@@ -498,8 +498,13 @@ __device__ __forceinline__ void pyr_blur_rows(const LevelGeom& L, const uint8_t*
   }
 }
 
+// ORBPL_PYR_MERGE=1: two barriers per level (level l's resize beside level
+// l-1's blur, borders and mirror rows both from content). Measured slower and
+// off (A/B on one box, two rounds: k_pyramid isolated 2.08 vs 2.03 ms with the
+// three-barrier order, tools/gpu_r04_f.sh): the phases are not what the
+// frame's chain waits on.
 #ifndef ORBPL_PYR_MERGE
-#define ORBPL_PYR_MERGE 1
+#define ORBPL_PYR_MERGE 0
 #endif
 
 // level 0 content rows [na, nb): the input image, 16 bytes per task

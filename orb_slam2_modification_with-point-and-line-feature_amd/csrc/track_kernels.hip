@@ -148,10 +148,15 @@ __device__ __forceinline__ int hamming_rl(uint4 a0, uint4 a1, const uint4* b) {
          __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
 }
 
-// Current-frame descriptors are staged in LDS when they fit (KMAX <= 1024:
-// 32 KB); the 2048-keypoint variant reads them from global memory.
+// Current-frame descriptors staged in LDS for KMAX <= ORBPL_MATCH_DESC_LDS_MAX
+// (32 KB at 1024 keypoints), else read from global memory (L2). Default 0:
+// from global memory for every KMAX - the smaller workgroup is placed sooner
+// beside the next batch's extraction kernels, and the scan's descriptor reads
+// hit L2 (A/B on one box, 1024 streams, two rounds: k_match_last isolated
+// 0.70 -> 0.50 ms, headline 124.3k / 125.6k -> 129.0k / 128.8k frames/s,
+// tools/gpu_r04_f.sh).
 #ifndef ORBPL_MATCH_DESC_LDS_MAX
-#define ORBPL_MATCH_DESC_LDS_MAX 1024
+#define ORBPL_MATCH_DESC_LDS_MAX 0
 #endif
 __host__ __device__ constexpr bool match_desc_lds(int kmax) { return kmax <= ORBPL_MATCH_DESC_LDS_MAX; }
 __host__ __device__ constexpr int match_desc_slots(int kmax) { return match_desc_lds(kmax) ? 2 * kmax : 1; }

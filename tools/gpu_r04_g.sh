@@ -66,4 +66,16 @@ for B in (1, 1536):
             print(f"lane util B={B} {k[:40]:40s} {100 * c['SQ_THREAD_CYCLES_VALU'] / (c['SQ_ACTIVE_INST_VALU'] * 64):6.1f} %  "
                   f"valu {c['SQ_INSTS_VALU']:.3g} waves {c['SQ_WAVES']:.0f}")
 PY
+
+# headline A/B: k_match_local descriptors in LDS (cur) or from global memory (locglob)
+cd $R
+A="--steps 20 --warmup 5 --secondary-steps 0 --stereo-steps 0 --rig-steps 0 --ingress-steps 0 --no-cpu-baseline --sweep 0 --trk-load 0 --isolated-steps 3 --no-parity"
+for r in 1 2; do
+  for v in cur locglob; do
+    L=""; [ "$v" != cur ] && L=$R/variants/$v/liborbpl.so
+    ORBPL_LIB=$L timeout -k 10 300 python bench.py $A > $O/b_${v}_$r.json 2> $O/b_${v}_$r.err || { echo "fail $v"; tail -3 $O/b_${v}_$r.err; exit 1; }
+    python3 -c "import json; d=json.load(open('$O/b_${v}_$r.json')); st=d['roofline']['isolated']['stage_ms']; print('$r $v', d['value'], d['ms_per_step'], 'isolated match_local', st.get('match_local'), 'local_map', st.get('local_map'), 'match', st.get('match'))"
+  done
+done
+
 exit 0
