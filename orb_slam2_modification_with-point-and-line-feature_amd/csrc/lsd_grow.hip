@@ -1707,6 +1707,68 @@ __device__ __forceinline__ double rect_improve_lane(const float* __restrict__ de
   return log_nfa;
 }
 
+// rect_improve with the best rectangle's changing fields (x1, y1, x2, y2,
+// width, prec, p) in a per-lane LDS slot instead of registers: the trial
+// rectangle is re-read from it at each phase start and written on an
+// improvement, so the 8-wave register budget holds the walk without scratch
+// spills (whose write-backs were most of the kernel's HBM writes).
+__device__ __forceinline__ double rect_improve_lds(const float* __restrict__ deg, int sw, int sh,
+                                                   Rect& rec, double* __restrict__ slot,
+                                                   double log_nt, const double* __restrict__ lgam,
+                                                   int lgam_n) {
+  const double delta = 0.5, delta_2 = delta / 2.0;
+  NfaLogs L;
+  double log_nfa = rect_nfa_lane(deg, sw, sh, rec, log_nt, lgam, lgam_n, L);
+  if (log_nfa > 0) return log_nfa;
+  slot[0] = rec.x1; slot[1] = rec.y1; slot[2] = rec.x2; slot[3] = rec.y2;
+  slot[4] = rec.width; slot[5] = rec.prec; slot[6] = rec.p;
+  Rect r = rec;
+  for (int phase = 0; phase < 5; phase++) {
+    r.x1 = slot[0]; r.y1 = slot[1]; r.x2 = slot[2]; r.y2 = slot[3];
+    r.width = slot[4]; r.prec = slot[5]; r.p = slot[6];
+    for (int n = 0; n < 5; ++n) {
+      bool eval = true;
+      if (phase == 0) {
+        r.p /= 2;
+        r.prec = r.p * kPi;
+      } else if ((r.width - delta) >= 0.5) {
+        if (phase == 1) {
+          r.width -= delta;
+        } else if (phase == 2) {
+          r.x1 += -r.dy * delta_2;
+          r.y1 += r.dx * delta_2;
+          r.x2 += -r.dy * delta_2;
+          r.y2 += r.dx * delta_2;
+          r.width -= delta;
+        } else if (phase == 3) {
+          r.x1 -= -r.dy * delta_2;
+          r.y1 -= r.dx * delta_2;
+          r.x2 -= -r.dy * delta_2;
+          r.y2 -= r.dx * delta_2;
+          r.width -= delta;
+        } else {
+          r.p /= 2;
+          r.prec = r.p * kPi;
+        }
+      } else {
+        eval = false;
+      }
+      if (eval) {
+        const double v = rect_nfa_lane(deg, sw, sh, r, log_nt, lgam, lgam_n, L);
+        if (v > log_nfa) {
+          log_nfa = v;
+          slot[0] = r.x1; slot[1] = r.y1; slot[2] = r.x2; slot[3] = r.y2;
+          slot[4] = r.width; slot[5] = r.prec; slot[6] = r.p;
+        }
+      }
+    }
+    if (log_nfa > 0) break;
+  }
+  rec.x1 = slot[0]; rec.y1 = slot[1]; rec.x2 = slot[2]; rec.y2 = slot[3];
+  rec.width = slot[4]; rec.prec = slot[5]; rec.p = slot[6];
+  return log_nfa;
+}
+
 }  // namespace
 
 __global__ void __launch_bounds__(64) k_lsd_grow(LsdGeom g, LsdScratch sc) {
@@ -2649,8 +2711,14 @@ constexpr int kValBlocksSmall = 8, kValBlocksLarge = 2;
 #ifndef ORBPL_VAL_XCD
 #define ORBPL_VAL_XCD 1
 #endif
+#ifndef ORBPL_VAL_RECLDS
+#define ORBPL_VAL_RECLDS 1
+#endif
 __global__ void __launch_bounds__(256, ORBPL_VAL_MINW) k_lsd_validate(LsdGeom g, LsdScratch sc) {
   __shared__ int s_next;
+#if ORBPL_VAL_RECLDS
+  __shared__ double s_rec[256][7];
+#endif
 #if ORBPL_VAL_XCD
   const int nx = gridDim.x, nwg = nx * gridDim.y;
   const int orig = blockIdx.x + nx * blockIdx.y;
@@ -2673,7 +2741,12 @@ __global__ void __launch_bounds__(256, ORBPL_VAL_MINW) k_lsd_validate(LsdGeom g,
     rec.x1 = rv[0]; rec.y1 = rv[1]; rec.x2 = rv[2]; rec.y2 = rv[3];
     rec.width = rv[4]; rec.x = rv[5]; rec.y = rv[6]; rec.theta = rv[7];
     rec.dx = rv[8]; rec.dy = rv[9]; rec.prec = rv[10]; rec.p = rv[11];
+#if ORBPL_VAL_RECLDS
+    const double log_nfa =
+        rect_improve_lds(deg, g.sw, g.sh, rec, s_rec[threadIdx.x], g.log_nt, sc.lgam, sc.lgam_n);
+#else
     const double log_nfa = rect_improve_lane(deg, g.sw, g.sh, rec, g.log_nt, sc.lgam, sc.lgam_n);
+#endif
     const bool ok = log_nfa > 0;
     sc.cand_ok[o] = ok;
     if (ok) {

@@ -101,10 +101,11 @@ constexpr int kLevelCols = kMaxLevelsT * kGridCols;   // (octave, grid column) r
 // (octave, column, row, index): the candidates of one octave in one grid
 // column are one contiguous range, in the reference's scan order.
 // ORBPL_LOCAL_DESC_LDS: the current descriptors staged in LDS (1) or read
-// from global memory (0, L2-resident: 32 KB less LDS per workgroup at 1024
-// keypoints, A/B build)
+// from global memory (0, the default: L2-resident, 32 KB less LDS per
+// workgroup at 1024 keypoints; A/B on one box, two rounds: k_match_local
+// isolated 0.228 -> 0.160 ms, headline within noise, tools/gpu_r04_g.sh)
 #ifndef ORBPL_LOCAL_DESC_LDS
-#define ORBPL_LOCAL_DESC_LDS 1
+#define ORBPL_LOCAL_DESC_LDS 0
 #endif
 template <int kLocalKp>
 struct LocalShared {
