@@ -2697,7 +2697,13 @@ __global__ void __launch_bounds__(256, 1) k_lsd_spec_sparse(LsdGeom g, LsdScratc
 constexpr int kValBlocksSmall = 8, kValBlocksLarge = 2;
 
 #ifndef ORBPL_VAL_MINW
-#define ORBPL_VAL_MINW 8   // 8 waves/SIMD (64 VGPRs, some scratch): 33.1 ms per 3072 frames; 6: 34.5; unbounded (111 VGPRs, 4 waves): 39.8
+// 6 waves/SIMD (80 VGPRs, the best rectangle in LDS): the same time as 8 (64
+// VGPRs) and a third less HBM traffic - 8 spilled doubles to scratch inside
+// the phase loop (A/B at 1536 frames, tools/gpu_r04_h.sh: 9.42 vs 9.44 ms,
+// 12.3 vs 16.8 MB per frame of FETCH x2 + WRITE; round 3, before the LDS
+// slot and the tiled degree plane: 8: 33.1 ms per 3072 frames, 6: 34.5,
+// unbounded (111 VGPRs, 4 waves): 39.8)
+#define ORBPL_VAL_MINW 6
 #endif
 // Lanes take rectangles from a workgroup-wide counter (block b owns the
 // rectangles c = b (mod gridDim.x)): a lane whose rectangle was cheap takes
