@@ -12,6 +12,7 @@
 //   k_lsd_grow    the greedy seed loop (region growing, rectangle fit,
 //                 refinement, NFA): one wave per frame, wave-uniform serial
 //                 control flow, parallel seed screening and NFA pixel counts
+#include <algorithm>
 #include <hip/hip_runtime.h>
 
 #include "lsd_kernels.h"
@@ -843,10 +844,18 @@ void launch_lsd_grad(const LsdGeom& g, const uint8_t* scaled, float* deg, int* q
                      scaled, deg, q, sd, maxq);
 }
 
+// workgroups per frame of k_lsd_sort_local: the LDS segments are independent,
+// so a small batch spreads a frame's ~50-100 segments over more CUs (batch 1:
+// 128 blocks instead of 4, the stage 2.0 ms -> one segment's sort); from 256
+// frames on the batch alone fills the GPU
+__host__ int lsd_sort_local_blocks(int batch) {
+  return std::max(kSortLocalBlocks, std::min(128, 1024 / std::max(batch, 1)));
+}
+
 void launch_lsd_sort(const LsdGeom& g, const LsdScratch& sc, int batch, hipStream_t s) {
   hipLaunchKernelGGL(k_lsd_sort, dim3(batch), dim3(kSortThreads), 0, s, g, sc);
-  hipLaunchKernelGGL(k_lsd_sort_local, dim3(kSortLocalBlocks, batch), dim3(kLocalThreads), 0, s,
-                     g, sc);
+  hipLaunchKernelGGL(k_lsd_sort_local, dim3(lsd_sort_local_blocks(batch), batch),
+                     dim3(kLocalThreads), 0, s, g, sc);
 }
 
 void launch_lsd_sort_keys(int n, const int* keys, const LsdScratch& sc, hipStream_t s) {
