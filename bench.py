@@ -1000,29 +1000,61 @@ def cpu_reference_faithful(gray, depth, L, workload, flags=0, warmup=20, frames=
     the LineExtractor on two host threads per frame (Frame.cc:152-155),
     matching and pose on the tracking thread; per-frame latency with
     std::chrono-like perf_counter over `frames` frames after `warmup` untimed
-    ones (20 warm-up, >= 300 timed; the loop wraps)."""
+    ones (20 warm-up, >= 300 timed; the loop wraps).
+    Measured in a child process of its own (tools/cpu_faithful.py) on the
+    stream's frames and the bench's vocabulary: inside the bench process,
+    after the GPU legs and the threaded CPU baseline, the same loop ran 2.6x
+    slower on the lines workload (81 vs 31 ms median on one box)."""
+    import tempfile
+    seq = [L.elem(0, i) for i in range(warmup + frames)]
+    uniq = sorted(set(seq))
+    pos = {e: k for k, e in enumerate(uniq)}
+    with tempfile.TemporaryDirectory() as td:
+        f = os.path.join(td, "faithful.npz")
+        extra = {}
+        if VOCAB["arrays"] is not None:
+            extra = {"voc_" + k: np.asarray(v) for k, v in VOCAB["arrays"].items()}
+        np.savez(f, gray=gray[uniq], depth=depth[uniq], order=np.array([pos[e] for e in seq]),
+                 Tcw0=np.linalg.inv(L.Twc(0, 0)).astype(np.float32).reshape(1, 16),
+                 workload=workload, flags=flags, warmup=warmup, use_map=use_map, **extra)
+        r = subprocess.run([sys.executable, str(ROOT / "tools" / "cpu_faithful.py"), "--npz", f],
+                           capture_output=True, text=True, timeout=900)
+    if r.returncode != 0:
+        raise RuntimeError(f"cpu_faithful failed: {r.stderr[-2000:]}")
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def faithful_run(npz):
+    """The child side of cpu_reference_faithful (tools/cpu_faithful.py --npz)."""
     from _pkg import load_oracle
     import orbpl.synth as synth
+    d = np.load(npz)
     O = load_oracle()
+    O.use_variant("best")
+    workload = str(d["workload"])
     wl = WORKLOADS[workload]
+    use_map = bool(d["use_map"])
+    warmup = int(d["warmup"])
     cam = O.camera(getattr(synth, wl["cam"]))
     mk = O.MapVO if use_map else O.LVO
     st_flag = O.TRACK_STEREO if (use_map and wl["stereo"]) else 0
-    vo = mk(O.params(*wl["orb"]), cam, 1, use_lines=wl["lines"], flags=O.TWO_THREADS | flags | st_flag)
+    vo = mk(O.params(*wl["orb"]), cam, 1, use_lines=wl["lines"],
+            flags=O.TWO_THREADS | int(d["flags"]) | st_flag)
     if use_map:
         vo.set_fps(wl.get("fps", 30))
-    voc = oracle_vocabulary(O)
-    if voc is not None:
-        vo.set_vocabulary(voc)
-    vo.reset(np.linalg.inv(L.Twc(0, 0)).astype(np.float32).reshape(1, 16))
+    if "voc_parent" in d.files:
+        arrays = {k[4:]: (d[k].item() if d[k].ndim == 0 else d[k]) for k in d.files
+                  if k.startswith("voc_")}
+        vo.set_vocabulary(O.Vocabulary(arrays=arrays))
+    vo.reset(d["Tcw0"])
+    gray, depth, order = d["gray"], d["depth"], d["order"]
     lat = []
-    for i in range(warmup + frames):
-        e = L.elem(0, i)
+    for i, k in enumerate(order):
         t0 = time.perf_counter()
         if wl["stereo"]:
-            vo.step_stereo(0, gray[e], depth[e])
+            vo.step_stereo(0, gray[k], depth[k])
         else:
-            vo.step(0, gray[e], depth[e])
+            vo.step(0, gray[k], depth[k])
         if i >= warmup:
             lat.append(time.perf_counter() - t0)
     lat = np.array(lat) * 1e3
@@ -1030,7 +1062,8 @@ def cpu_reference_faithful(gray, depth, L, workload, flags=0, warmup=20, frames=
             "threads_per_frame": 2 if wl["lines"] else 1,
             "median_ms_per_frame": round(float(np.median(lat)), 3),
             "mean_ms_per_frame": round(float(lat.mean()), 3), "frames": int(len(lat)),
-            "sample": f"one stream, {len(lat)} frames after {warmup} warm-up frames"}
+            "sample": f"one stream, {len(lat)} frames after {warmup} warm-up frames, "
+                      f"in a process of its own"}
 
 
 def _free_port():
