@@ -255,7 +255,23 @@ int orbx_create(const orbpl_orb_params* p, int width, int height, int max_batch,
     if (_e != hipSuccess) return fail(_e, #expr); \
   } while (0)
   CK(hipSetDevice(device));
-  CK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  // ORBPL_EXTRACT_CU_RESERVE=k (A/B): the extraction stream's kernels leave
+  // the last k CUs of every 32-CU group (an XCD) to the other streams, so a
+  // tracking workgroup that needs a whole SIMD's registers is placed at once
+  // instead of after the extraction kernel beside it drains
+  const char* resv = getenv("ORBPL_EXTRACT_CU_RESERVE");
+  const int reserve = resv ? atoi(resv) : 0;
+  int ncu = 0;
+  if (reserve > 0 && reserve < 32 &&
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
+      ncu >= 32) {
+    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+    for (int cu = 0; cu < ncu; cu++)
+      if ((cu & 31) < 32 - reserve) mask[cu >> 5] |= 1u << (cu & 31);
+    CK(hipExtStreamCreateWithCUMask(&c->stream, (uint32_t)mask.size(), mask.data()));
+  } else {
+    CK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  }
   for (auto& e : c->ev) CK(hipEventCreate(&e));
   const size_t B = (size_t)max_batch;
   CK(hipMalloc(&c->d_geom, sizeof(OrbGeom)));
