@@ -258,7 +258,8 @@ int orbx_create(const orbpl_orb_params* p, int width, int height, int max_batch,
   // ORBPL_EXTRACT_CU_RESERVE=k (A/B): the extraction stream's kernels leave
   // the last k CUs of every 32-CU group (an XCD) to the other streams, so a
   // tracking workgroup that needs a whole SIMD's registers is placed at once
-  // instead of after the extraction kernel beside it drains
+  // instead of after the extraction kernel beside it drains. Measured 18-20 %
+  // slower on the headline for k = 1, 2, 4 (tools/gpu_r04_l.sh): off
   const char* resv = getenv("ORBPL_EXTRACT_CU_RESERVE");
   const int reserve = resv ? atoi(resv) : 0;
   int ncu = 0;
