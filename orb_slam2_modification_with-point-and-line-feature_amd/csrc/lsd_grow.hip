@@ -1893,6 +1893,361 @@ constexpr int kSpecSmallBatch = ORBPL_SPEC_SMALL_BATCH;
 // seeds first, in list order, then new seeds from the scan; a lane's list
 // buffer travels with its seed (bufid). After a cooperative fallback nothing
 // is carried (the fallback uses buffer 0 as scratch).
+// ---------------------------------------------------------------------------
+// Wave-cooperative fit (ORBPL_COOP_FIT). After a round's grows, the fits of
+// the regions that reach min_reg_size (~4 per round) run one region at a time
+// across the whole wave instead of one lane per region while the other lanes
+// wait. A fit is a chain of passes over the region's list - region2rect's
+// centroid, inertia and extent passes, refine's angle statistics,
+// reduce_region_radius' count and merge - whose per-point work is independent
+// and whose sums are ordered double sums: the wave computes 64 points' terms
+// at once, then every lane adds them in list order from LDS, so each sum
+// rounds exactly as the sequential loop's (the extents and the counts are
+// order-free). refine's second region grow stays one lane per region (the
+// round's refining lanes at once, as before).
+// ---------------------------------------------------------------------------
+#ifndef ORBPL_COOP_FIT
+#define ORBPL_COOP_FIT 1
+#endif
+
+struct CoopScratch {
+  double a[64], b[64], c[64];
+  uint16_t farpos[kLaneCap / 2], nearpos[kLaneCap / 2];
+};
+
+// the wave's LDS operations so far are complete; no memory access moves across
+__device__ __forceinline__ void coop_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// A += a_k, B += b_k, C += c_k (C -= c_k with kSubC), k = 0 .. cnt-1 in order,
+// term k held by lane k; every lane ends with the same sums
+template <bool kSubC>
+__device__ __forceinline__ void coop_add3(CoopScratch& S, int lane, int cnt, double ta, double tb,
+                                          double tc, double& A, double& B, double& C) {
+  S.a[lane] = ta;
+  S.b[lane] = tb;
+  S.c[lane] = tc;
+  coop_lds_sync();
+  int k = 0;
+  for (; k + 4 <= cnt; k += 4) {
+    double xa[4], xb[4], xc[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      xa[u] = S.a[k + u];
+      xb[u] = S.b[k + u];
+      xc[u] = S.c[k + u];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      A += xa[u];
+      B += xb[u];
+      C = kSubC ? C - xc[u] : C + xc[u];
+    }
+  }
+  for (; k < cnt; k++) {
+    A += S.a[k];
+    B += S.b[k];
+    C = kSubC ? C - S.c[k] : C + S.c[k];
+  }
+  coop_lds_sync();   // every lane has read the terms before the next pass writes
+}
+
+__device__ __forceinline__ int coop_rl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ double coop_rl(double v, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                          __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+__device__ __forceinline__ double coop_max(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const double u = __shfl_xor(v, o, 64);
+    v = u > v ? u : v;
+  }
+  return v;
+}
+__device__ __forceinline__ double coop_min(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const double u = __shfl_xor(v, o, 64);
+    v = u < v ? u : v;
+  }
+  return v;
+}
+
+// region2rect's first pass (lane_rect): the weighted centroid sums over list
+// [0, n) in order; with q the weights are computed (modgrad) and stored into
+// the entries first
+__device__ __forceinline__ void coop_centroid(CoopScratch& S, int lane, LaneBuf bf, int n,
+                                              const int* __restrict__ q, int sw, double& x,
+                                              double& y, double& sum) {
+  x = 0;
+  y = 0;
+  sum = 0;
+  for (int i0 = 0; i0 < n; i0 += 64) {
+    const int i = i0 + lane;
+    double ta = 0, tb = 0, tc = 0;
+    if (i < n) {
+      uint32_t pt;
+      double w;
+      if (q) {
+        pt = bf.pt(i);
+        w = modgrad_q(q[(int)(pt >> 16) * sw + (int)(pt & 0xFFFF)]);
+        bf.set_w(i, w);
+      } else {
+        const uint4 e = bf[i];
+        pt = e.x;
+        w = entry_w(e);
+      }
+      ta = double(pt & 0xFFFF) * w;
+      tb = double(pt >> 16) * w;
+      tc = w;
+    }
+    coop_add3<false>(S, lane, min(64, n - i0), ta, tb, tc, x, y, sum);
+  }
+}
+
+// lane_rect_tail across the wave: inertia sums in order, theta, extents
+__device__ __forceinline__ void coop_rect_tail(CoopScratch& S, int lane, LaneBuf bf, int n,
+                                               double x, double y, double sum, double reg_angle,
+                                               double prec, double p, Rect& rec) {
+  x /= sum;
+  y /= sum;
+  double Ixx = 0.0, Iyy = 0.0, Ixy = 0.0;
+  for (int i0 = 0; i0 < n; i0 += 64) {
+    const int i = i0 + lane;
+    double ta = 0, tb = 0, tc = 0;
+    if (i < n) {
+      const uint4 e = bf[i];
+      const double weight = entry_w(e);
+      const double dx = double(pt_x(e)) - x, dy = double(pt_y(e)) - y;
+      ta = dy * dy * weight;
+      tb = dx * dx * weight;
+      tc = dx * dy * weight;
+    }
+    coop_add3<true>(S, lane, min(64, n - i0), ta, tb, tc, Ixx, Iyy, Ixy);
+  }
+  const double lambda = 0.5 * (Ixx + Iyy - sqrt((Ixx - Iyy) * (Ixx - Iyy) + 4.0 * Ixy * Ixy));
+  double theta = (fabs(Ixx) > fabs(Iyy)) ? double(fast_atan2_deg(float(lambda - Ixx), float(Ixy)))
+                                         : double(fast_atan2_deg(float(Ixy), float(lambda - Iyy)));
+  theta *= kDegToRad;
+  if (fabs(angle_diff_signed(theta, reg_angle)) > prec) theta += kPi;
+  const double dx = lsdm::cos_(theta), dy = lsdm::sin_(theta);
+  // l_max / l_min (and w) start at 0: independent max / min, any order
+  double l_min = 0, l_max = 0, w_min = 0, w_max = 0;
+  for (int i0 = 0; i0 < n; i0 += 64) {
+    const int i = i0 + lane;
+    if (i < n) {
+      const uint32_t pt = bf.pt(i);
+      const double regdx = double(pt & 0xFFFF) - x, regdy = double(pt >> 16) - y;
+      const double l = regdx * dx + regdy * dy;
+      const double w = -regdx * dy + regdy * dx;
+      l_max = l > l_max ? l : l_max;
+      l_min = l < l_min ? l : l_min;
+      w_max = w > w_max ? w : w_max;
+      w_min = w < w_min ? w : w_min;
+    }
+  }
+  l_max = coop_max(l_max);
+  l_min = coop_min(l_min);
+  w_max = coop_max(w_max);
+  w_min = coop_min(w_min);
+  rec.x1 = x + l_min * dx;
+  rec.y1 = y + l_min * dy;
+  rec.x2 = x + l_max * dx;
+  rec.y2 = y + l_max * dy;
+  rec.width = w_max - w_min;
+  rec.x = x;
+  rec.y = y;
+  rec.theta = theta;
+  rec.dx = dx;
+  rec.dy = dy;
+  rec.prec = prec;
+  rec.p = p;
+  if (rec.width < 1.0) rec.width = 1.0;
+}
+
+// refine's angle statistics over list [0, n) (lane_refine): tau
+__device__ __forceinline__ double coop_tau(CoopScratch& S, int lane, LaneBuf bf, int n,
+                                           const Rect& rec) {
+  const uint4 e0 = bf[0];
+  const double xc = double(pt_x(e0)), yc = double(pt_y(e0));
+  const double ang_c = deg2ang(entry_deg(e0));
+  double sum = 0, s_sum = 0, unused = 0;
+  int cnt = 0;
+  for (int i0 = 0; i0 < n; i0 += 64) {
+    const int i = i0 + lane;
+    double ta = 0, tb = 0;
+    bool in = false;
+    if (i < n) {
+      const uint4 e = bf[i];
+      if (dist(xc, yc, pt_x(e), pt_y(e)) < rec.width) {
+        const double ang_d = angle_diff_signed(deg2ang(entry_deg(e)), ang_c);
+        ta = ang_d;
+        tb = ang_d * ang_d;
+        in = true;
+      }
+    }
+    cnt += __popcll(__ballot(in));
+    // a point outside adds +0.0: the sums start at +0 and never become -0,
+    // so x + 0.0 == x, the same as skipping it
+    coop_add3<false>(S, lane, min(64, n - i0), ta, tb, 0.0, sum, s_sum, unused);
+  }
+  const double mean_angle = sum / double(cnt);
+  return 2.0 * sqrt((s_sum - 2.0 * mean_angle * sum) / double(cnt) + mean_angle * mean_angle);
+}
+
+// lane_reduce_pass across the wave: the near count, the merge (the k-th far
+// point of [0, nn) in index order takes the k-th near point of [nn, n)
+// counted from the end; that slot keeps the far point's word) and the
+// centroid sums of the final [0, nn) in order. Returns nn (n: nothing removed,
+// no sums).
+__device__ __forceinline__ int coop_reduce(CoopScratch& S, int lane, LaneBuf g1, int n, int xc,
+                                           int yc, double radSq, double& cx, double& cy,
+                                           double& csum) {
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  int nn = 0;
+  for (int i0 = 0; i0 < n; i0 += 64) {
+    const int i = i0 + lane;
+    const bool nr = i < n && !lane_far(g1.pt(i), xc, yc, radSq);
+    nn += __popcll(__ballot(nr));
+  }
+  if (nn == n) return n;
+  int m = 0;
+  for (int i0 = 0; i0 < nn; i0 += 64) {
+    const int i = i0 + lane;
+    const bool fr = i < nn && lane_far(g1.pt(i), xc, yc, radSq);
+    const unsigned long long mk = __ballot(fr);
+    if (fr) S.farpos[m + __popcll(mk & lt)] = (uint16_t)i;
+    m += __popcll(mk);
+  }
+  int m2 = 0;
+  for (int j0 = 0; j0 < n - nn; j0 += 64) {
+    const int j = n - 1 - (j0 + lane);
+    const bool nr = j >= nn && !lane_far(g1.pt(j), xc, yc, radSq);
+    const unsigned long long mk = __ballot(nr);
+    if (nr) S.nearpos[m2 + __popcll(mk & lt)] = (uint16_t)j;
+    m2 += __popcll(mk);
+  }
+  coop_lds_sync();
+  for (int k0 = 0; k0 < m; k0 += 64) {
+    const int k = k0 + lane;
+    if (k < m) {
+      const int i = S.farpos[k], j = S.nearpos[k];
+      const uint32_t farw = g1.pt(i);
+      const uint4 b = g1[j];
+      g1[i] = b;
+      g1.set_pt(j, farw);
+    }
+  }
+  wg_fence();
+  __builtin_amdgcn_wave_barrier();
+  coop_centroid(S, lane, g1, nn, nullptr, 0, cx, cy, csum);
+  return nn;
+}
+
+// The round's fits (lane_rect + lane_refine of every lane with n >=
+// min_reg_size), all lanes of the wave active. Per lane in: fitter, n,
+// reg_angle (the first grow's), buf; out: status, rec, off, len, touched
+// (fitters only).
+__device__ __forceinline__ void coop_fit(CoopScratch& S, int lane, bool fitter, int n,
+                                         double reg_angle, uint4* fbuf, int bufid, const Frame& F,
+                                         uint64_t* sd, double prec, double p, uint32_t myval1,
+                                         int& status, Rect& rec, int& off, int& len,
+                                         int& touched) {
+  bool need = false;
+  double tau = 0;
+  // the first region's rectangle and, where refine runs, its statistics
+  for (unsigned long long m = __ballot(fitter); m; m &= m - 1) {
+    const int f = __ffsll((long long)m) - 1;
+    const int nf = coop_rl(n, f);
+    const double ra = coop_rl(reg_angle, f);
+    const LaneBuf bf{fbuf + (long long)coop_rl(bufid, f) * kLaneCap};
+    double cx, cy, cs;
+    coop_centroid(S, lane, bf, nf, F.q, F.sw, cx, cy, cs);
+    wg_fence();
+    __builtin_amdgcn_wave_barrier();
+    Rect r;
+    coop_rect_tail(S, lane, bf, nf, cx, cy, cs, ra, prec, p, r);
+    const double density = double(nf) / (dist(r.x1, r.y1, r.x2, r.y2) * r.width);
+    const bool nd = density < 0.7;
+    const double tf = nd ? coop_tau(S, lane, bf, nf, r) : 0.0;
+    if (lane == f) {
+      rec = r;
+      off = 0;
+      len = nf;
+      touched = nf;
+      status = kSpecCand;
+      need = nd;
+      tau = tf;
+    }
+  }
+  // refine's second grow, one lane per refining region
+  const LaneBuf buf{fbuf + (long long)bufid * kLaneCap};
+  int n1 = 0;
+  double ra2 = reg_angle;
+  if (need) {
+    const uint4 e0 = buf[0];
+    n1 = lane_grow(F, sd, buf + n, kLaneCap - n, pt_x(e0), pt_y(e0), ra2, tau, myval1);
+    if (n1 < 0) {
+      status = n1;
+      need = false;
+    } else {
+      off = n;
+      len = n1;
+      touched = n + n1;
+      if (n1 < 2) {
+        status = kSpecFail;
+        need = false;
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  // the second region's rectangle and reduce_region_radius
+  for (unsigned long long m = __ballot(need); m; m &= m - 1) {
+    const int f = __ffsll((long long)m) - 1;
+    const int nf = coop_rl(n, f);
+    const int n1f = coop_rl(n1, f);
+    const double ra = coop_rl(ra2, f);
+    const LaneBuf b0{fbuf + (long long)coop_rl(bufid, f) * kLaneCap};
+    const LaneBuf g1 = b0 + nf;
+    const uint4 e0 = b0[0];
+    const int x0 = pt_x(e0), y0 = pt_y(e0);
+    double cx, cy, cs;
+    coop_centroid(S, lane, g1, n1f, F.q, F.sw, cx, cy, cs);
+    wg_fence();
+    __builtin_amdgcn_wave_barrier();
+    Rect r;
+    coop_rect_tail(S, lane, g1, n1f, cx, cy, cs, ra, prec, p, r);
+    double density = double(n1f) / (dist(r.x1, r.y1, r.x2, r.y2) * r.width);
+    int st = kSpecCand, lf = n1f;
+    if (density < 0.7) {
+      const double xc = double(x0), yc = double(y0);
+      const double radSq1 = distSq(xc, yc, r.x1, r.y1);
+      const double radSq2 = distSq(xc, yc, r.x2, r.y2);
+      double radSq = radSq1 > radSq2 ? radSq1 : radSq2;
+      while (density < 0.7) {
+        radSq *= 0.75 * 0.75;
+        const int n_prev = lf;
+        lf = coop_reduce(S, lane, g1, lf, x0, y0, radSq, cx, cy, cs);
+        if (lf < 2) {
+          st = kSpecFail;
+          break;
+        }
+        if (lf == n_prev) continue;
+        coop_rect_tail(S, lane, g1, lf, cx, cy, cs, ra, prec, p, r);
+        density = double(lf) / (dist(r.x1, r.y1, r.x2, r.y2) * r.width);
+      }
+    }
+    if (lane == f) {
+      rec = r;
+      status = st;
+      len = lf;
+    }
+  }
+}
+
 #ifndef ORBPL_SPEC_WIN
 #define ORBPL_SPEC_WIN 64
 #endif
@@ -1939,6 +2294,8 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
   constexpr bool PF = false;
 #endif
   __shared__ uint32_t s_ring[PF ? 64 * kRing : 1];
+  constexpr bool COOP = ORBPL_COOP_FIT && !PF && !ORBPL_LBUF_INTERLEAVED;
+  __shared__ CoopScratch s_coop[COOP ? W : 1];
   const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int sw = g.sw, sh = g.sh;
   Frame F;
@@ -2093,7 +2450,18 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
       for (int o = 32; o >= 1; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
       max_steps += mx;
     }
-    if (t < ncand && !keep) {
+    if constexpr (COOP) {
+      const bool mine = t < ncand && !keep;
+      if (mine && n < 0) {
+        status = n;
+      } else if (mine && n < g.min_reg_size) {
+        status = kSpecSmall;
+        len = n;
+        touched = n;
+      }
+      coop_fit(s_coop[wv], lane, mine && n >= g.min_reg_size, n, reg_angle, fbuf, bufid, F, sd,
+               prec, p, myval1, status, rec, off, len, touched);
+    } else if (t < ncand && !keep) {
       if (n < 0) {
         status = n;
       } else if (n < g.min_reg_size) {
