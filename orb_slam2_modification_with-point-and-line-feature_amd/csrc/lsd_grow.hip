@@ -1906,13 +1906,28 @@ constexpr int kSpecSmallBatch = ORBPL_SPEC_SMALL_BATCH;
 // order-free). refine's second region grow stays one lane per region (the
 // round's refining lanes at once, as before).
 // ---------------------------------------------------------------------------
+// 0: per lane; 1: one fitting region at a time across the wave (bit-exact,
+// measured no faster: the per-region fixed costs and the serialised regions
+// outweigh the parallel points); 2: per-lane fits with wave-wide passes
 #ifndef ORBPL_COOP_FIT
-#define ORBPL_COOP_FIT 1
+#define ORBPL_COOP_FIT 2
 #endif
 
+// fitters whose terms share LDS at once (ORBPL_COOP_FIT=2)
+constexpr int kCoopG = 4;
 struct CoopScratch {
-  double a[64], b[64], c[64];
-  uint16_t farpos[kLaneCap / 2], nearpos[kLaneCap / 2];
+  union {
+    struct {
+      double a[64], b[64], c[64];
+    };
+    struct {   // ORBPL_COOP_FIT=2: one row per fitter of a group, padded so that
+               // the lanes' rows start in different banks
+      double ga[kCoopG][65], gb[kCoopG][65], gc[kCoopG][65];
+    };
+    struct {
+      uint16_t farpos[kLaneCap / 2], nearpos[kLaneCap / 2];
+    };
+  };
 };
 
 // the wave's LDS operations so far are complete; no memory access moves across
@@ -2145,6 +2160,363 @@ __device__ __forceinline__ int coop_reduce(CoopScratch& S, int lane, LaneBuf g1,
   __builtin_amdgcn_wave_barrier();
   coop_centroid(S, lane, g1, nn, nullptr, 0, cx, cy, csum);
   return nn;
+}
+
+__device__ __forceinline__ uint4* coop_rl(uint4* v, int l) {
+  const uintptr_t u = reinterpret_cast<uintptr_t>(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+  return reinterpret_cast<uint4*>(((uintptr_t)hi << 32) | lo);
+}
+
+// ORBPL_COOP_FIT=2: the fits stay one lane per region (the round's fitting
+// lanes together, as the per-lane code), but every pass's per-point work is
+// spread over the whole wave: for a group of up to kCoopG fitting lanes and
+// a window of 64 points, the wave evaluates each lane's 64 terms in turn
+// (term(f, i, ...) with f the owning lane) into that lane's LDS row, then
+// every lane of the group adds its own row in point order. The sums round as
+// the sequential loop's; the serial part per point is three LDS reads and
+// three adds instead of the point's whole load / weight / product chain.
+template <bool kSubC, class Term>
+__device__ __forceinline__ void group_sums(CoopScratch& S, int lane, bool act, int n, double& A,
+                                           double& B, double& C, Term term) {
+  unsigned long long am = __ballot(act);
+  while (am) {
+    unsigned long long gm = 0;
+    int ng = 0;
+    for (unsigned long long r = am; r && ng < kCoopG; r &= r - 1, ng++) gm |= r & (~r + 1ull);
+    am &= ~gm;
+    const bool ing = (gm >> lane) & 1ull;
+    const int myslot = __popcll(gm & ((1ull << lane) - 1ull));
+    int nmax = ing ? n : 0;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) nmax = max(nmax, __shfl_xor(nmax, o, 64));
+    for (int k0 = 0; k0 < nmax; k0 += 64) {
+      int slot = 0;
+      for (unsigned long long r = gm; r; r &= r - 1, slot++) {
+        const int f = __ffsll((long long)r) - 1;
+        const int nf = coop_rl(n, f);
+        const int i = k0 + lane;
+        if (i < nf) {
+          double ta, tb, tc;
+          term(f, i, ta, tb, tc);
+          S.ga[slot][lane] = ta;
+          S.gb[slot][lane] = tb;
+          S.gc[slot][lane] = tc;
+        }
+      }
+      coop_lds_sync();
+      if (ing) {
+        const int cnt = min(64, n - k0);
+        const double* pa = S.ga[myslot];
+        const double* pb = S.gb[myslot];
+        const double* pc = S.gc[myslot];
+        int k = 0;
+        for (; k + 4 <= cnt; k += 4) {
+          double xa[4], xb[4], xc[4];
+#pragma unroll
+          for (int u = 0; u < 4; u++) {
+            xa[u] = pa[k + u];
+            xb[u] = pb[k + u];
+            xc[u] = pc[k + u];
+          }
+#pragma unroll
+          for (int u = 0; u < 4; u++) {
+            A += xa[u];
+            B += xb[u];
+            C = kSubC ? C - xc[u] : C + xc[u];
+          }
+        }
+        for (; k < cnt; k++) {
+          A += pa[k];
+          B += pb[k];
+          C = kSubC ? C - pc[k] : C + pc[k];
+        }
+      }
+      coop_lds_sync();
+    }
+  }
+}
+
+// region2rect's first pass for every act lane over its list bp[0, n) (with q:
+// the weights computed and stored into the entries first)
+__device__ __forceinline__ void group_centroid(CoopScratch& S, int lane, bool act, uint4* bp,
+                                               int n, const int* __restrict__ q, int sw,
+                                               double& x, double& y, double& sum) {
+  x = 0;
+  y = 0;
+  sum = 0;
+  group_sums<false>(S, lane, act, n, x, y, sum,
+                    [&](int f, int i, double& ta, double& tb, double& tc) {
+                      const LaneBuf bf{coop_rl(bp, f)};
+                      uint32_t pt;
+                      double w;
+                      if (q) {
+                        pt = bf.pt(i);
+                        w = modgrad_q(q[(int)(pt >> 16) * sw + (int)(pt & 0xFFFF)]);
+                        bf.set_w(i, w);
+                      } else {
+                        const uint4 e = bf[i];
+                        pt = e.x;
+                        w = entry_w(e);
+                      }
+                      ta = double(pt & 0xFFFF) * w;
+                      tb = double(pt >> 16) * w;
+                      tc = w;
+                    });
+}
+
+// lane_rect_tail for every act lane: inertia sums (group_sums), theta per
+// lane, the extents fitter by fitter over the whole wave
+__device__ __forceinline__ void group_rect_tail(CoopScratch& S, int lane, bool act, uint4* bp,
+                                                int n, double x, double y, double sum,
+                                                double reg_angle, double prec, double p,
+                                                Rect& rec) {
+  if (act) {
+    x /= sum;
+    y /= sum;
+  }
+  double Ixx = 0.0, Iyy = 0.0, Ixy = 0.0;
+  group_sums<true>(S, lane, act, n, Ixx, Iyy, Ixy,
+                   [&](int f, int i, double& ta, double& tb, double& tc) {
+                     const LaneBuf bf{coop_rl(bp, f)};
+                     const double xf = coop_rl(x, f), yf = coop_rl(y, f);
+                     const uint4 e = bf[i];
+                     const double weight = entry_w(e);
+                     const double dx = double(pt_x(e)) - xf, dy = double(pt_y(e)) - yf;
+                     ta = dy * dy * weight;
+                     tb = dx * dx * weight;
+                     tc = dx * dy * weight;
+                   });
+  double theta = 0, dx = 0, dy = 0;
+  if (act) {
+    const double lambda = 0.5 * (Ixx + Iyy - sqrt((Ixx - Iyy) * (Ixx - Iyy) + 4.0 * Ixy * Ixy));
+    theta = (fabs(Ixx) > fabs(Iyy)) ? double(fast_atan2_deg(float(lambda - Ixx), float(Ixy)))
+                                    : double(fast_atan2_deg(float(Ixy), float(lambda - Iyy)));
+    theta *= kDegToRad;
+    if (fabs(angle_diff_signed(theta, reg_angle)) > prec) theta += kPi;
+    dx = lsdm::cos_(theta);
+    dy = lsdm::sin_(theta);
+  }
+  double l_min = 0, l_max = 0, w_min = 0, w_max = 0;
+  for (unsigned long long m = __ballot(act); m; m &= m - 1) {
+    const int f = __ffsll((long long)m) - 1;
+    const int nf = coop_rl(n, f);
+    const LaneBuf bf{coop_rl(bp, f)};
+    const double xf = coop_rl(x, f), yf = coop_rl(y, f), dxf = coop_rl(dx, f),
+                 dyf = coop_rl(dy, f);
+    double a0 = 0, a1 = 0, b0 = 0, b1 = 0;   // l_min, l_max, w_min, w_max
+    for (int i0 = 0; i0 < nf; i0 += 64) {
+      const int i = i0 + lane;
+      if (i < nf) {
+        const uint32_t pt = bf.pt(i);
+        const double regdx = double(pt & 0xFFFF) - xf, regdy = double(pt >> 16) - yf;
+        const double l = regdx * dxf + regdy * dyf;
+        const double w = -regdx * dyf + regdy * dxf;
+        a1 = l > a1 ? l : a1;
+        a0 = l < a0 ? l : a0;
+        b1 = w > b1 ? w : b1;
+        b0 = w < b0 ? w : b0;
+      }
+    }
+    a0 = coop_min(a0);
+    a1 = coop_max(a1);
+    b0 = coop_min(b0);
+    b1 = coop_max(b1);
+    if (lane == f) {
+      l_min = a0;
+      l_max = a1;
+      w_min = b0;
+      w_max = b1;
+    }
+  }
+  if (act) {
+    rec.x1 = x + l_min * dx;
+    rec.y1 = y + l_min * dy;
+    rec.x2 = x + l_max * dx;
+    rec.y2 = y + l_max * dy;
+    rec.width = w_max - w_min;
+    rec.x = x;
+    rec.y = y;
+    rec.theta = theta;
+    rec.dx = dx;
+    rec.dy = dy;
+    rec.prec = prec;
+    rec.p = p;
+    if (rec.width < 1.0) rec.width = 1.0;
+  }
+}
+
+// refine's angle statistics for every act lane over bp[0, n) -> tau (the
+// count as a third sum: whole numbers, exact in double)
+__device__ __forceinline__ double group_tau(CoopScratch& S, int lane, bool act, uint4* bp, int n,
+                                           const Rect& rec) {
+  double sum = 0, s_sum = 0, cnt = 0;
+  const double width = rec.width;
+  group_sums<false>(S, lane, act, n, sum, s_sum, cnt,
+                    [&](int f, int i, double& ta, double& tb, double& tc) {
+                      const LaneBuf bf{coop_rl(bp, f)};
+                      const double wf = coop_rl(width, f);
+                      const uint4 e0 = bf[0];
+                      const double xc = double(pt_x(e0)), yc = double(pt_y(e0));
+                      const double ang_c = deg2ang(entry_deg(e0));
+                      const uint4 e = bf[i];
+                      ta = 0;
+                      tb = 0;
+                      tc = 0;
+                      // a point outside adds +0.0: the sums start at +0 and
+                      // never become -0, so x + 0.0 == x (skipping it)
+                      if (dist(xc, yc, pt_x(e), pt_y(e)) < wf) {
+                        const double ang_d = angle_diff_signed(deg2ang(entry_deg(e)), ang_c);
+                        ta = ang_d;
+                        tb = ang_d * ang_d;
+                        tc = 1.0;
+                      }
+                    });
+  if (!act) return 0.0;
+  const int c = (int)cnt;
+  const double mean_angle = sum / double(c);
+  return 2.0 * sqrt((s_sum - 2.0 * mean_angle * sum) / double(c) + mean_angle * mean_angle);
+}
+
+// lane_reduce_pass's merge for fitter f (count nn < n already known): the
+// k-th far point of [0, nn) in index order takes the k-th near point of
+// [nn, n) counted from the end; that slot keeps the far point's word
+__device__ __forceinline__ void group_merge(CoopScratch& S, int lane, LaneBuf g1, int n, int nn,
+                                            int xc, int yc, double radSq) {
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  int m = 0;
+  for (int i0 = 0; i0 < nn; i0 += 64) {
+    const int i = i0 + lane;
+    const bool fr = i < nn && lane_far(g1.pt(i), xc, yc, radSq);
+    const unsigned long long mk = __ballot(fr);
+    if (fr) S.farpos[m + __popcll(mk & lt)] = (uint16_t)i;
+    m += __popcll(mk);
+  }
+  int m2 = 0;
+  for (int j0 = 0; j0 < n - nn; j0 += 64) {
+    const int j = n - 1 - (j0 + lane);
+    const bool nr = j >= nn && !lane_far(g1.pt(j), xc, yc, radSq);
+    const unsigned long long mk = __ballot(nr);
+    if (nr) S.nearpos[m2 + __popcll(mk & lt)] = (uint16_t)j;
+    m2 += __popcll(mk);
+  }
+  coop_lds_sync();
+  for (int k0 = 0; k0 < m; k0 += 64) {
+    const int k = k0 + lane;
+    if (k < m) {
+      const int i = S.farpos[k], j = S.nearpos[k];
+      const uint32_t farw = g1.pt(i);
+      const uint4 b = g1[j];
+      g1[i] = b;
+      g1.set_pt(j, farw);
+    }
+  }
+  coop_lds_sync();
+}
+
+// ORBPL_COOP_FIT=2: the round's fits with the per-lane control flow of
+// lane_rect + lane_refine and the wave-wide passes above
+__device__ __forceinline__ void group_fit(CoopScratch& S, int lane, bool fitter, int n,
+                                          double reg_angle, uint4* fbuf, int bufid,
+                                          const Frame& F, uint64_t* sd, double prec, double p,
+                                          uint32_t myval1, int& status, Rect& rec, int& off,
+                                          int& len, int& touched) {
+  uint4* bp = fbuf + (long long)bufid * kLaneCap;
+  double cx, cy, cs;
+  group_centroid(S, lane, fitter, bp, n, F.q, F.sw, cx, cy, cs);
+  wg_fence();
+  __builtin_amdgcn_wave_barrier();
+  group_rect_tail(S, lane, fitter, bp, n, cx, cy, cs, reg_angle, prec, p, rec);
+  bool refine = false;
+  if (fitter) {
+    const double density = double(n) / (dist(rec.x1, rec.y1, rec.x2, rec.y2) * rec.width);
+    off = 0;
+    len = n;
+    touched = n;
+    status = kSpecCand;
+    refine = density < 0.7;
+  }
+  const double tau = group_tau(S, lane, refine, bp, n, rec);
+  // refine's second grow, one lane per region
+  const LaneBuf buf{bp};
+  int n1 = 0, x0 = 0, y0 = 0;
+  double ra2 = reg_angle;
+  if (refine) {
+    const uint4 e0 = buf[0];
+    x0 = pt_x(e0);
+    y0 = pt_y(e0);
+    n1 = lane_grow(F, sd, buf + n, kLaneCap - n, x0, y0, ra2, tau, myval1);
+    if (n1 < 0) {
+      status = n1;
+      refine = false;
+    } else {
+      off = n;
+      len = n1;
+      touched = n + n1;
+      if (n1 < 2) {
+        status = kSpecFail;
+        refine = false;
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  uint4* gp = bp + n;   // the second region's list
+  group_centroid(S, lane, refine, gp, n1, F.q, F.sw, cx, cy, cs);
+  wg_fence();
+  __builtin_amdgcn_wave_barrier();
+  group_rect_tail(S, lane, refine, gp, n1, cx, cy, cs, ra2, prec, p, rec);
+  bool red = false;
+  double radSq = 0;
+  if (refine) {
+    const double density = double(n1) / (dist(rec.x1, rec.y1, rec.x2, rec.y2) * rec.width);
+    if (density < 0.7) {
+      red = true;
+      const double xc = double(x0), yc = double(y0);
+      const double radSq1 = distSq(xc, yc, rec.x1, rec.y1);
+      const double radSq2 = distSq(xc, yc, rec.x2, rec.y2);
+      radSq = radSq1 > radSq2 ? radSq1 : radSq2;
+    }
+  }
+  // reduce_region_radius, one iteration of every reducing lane per pass
+  while (__ballot(red)) {
+    if (red) radSq *= 0.75 * 0.75;
+    int nn = n1;
+    for (unsigned long long m = __ballot(red); m; m &= m - 1) {
+      const int f = __ffsll((long long)m) - 1;
+      const int nf = coop_rl(n1, f), xf = coop_rl(x0, f), yf = coop_rl(y0, f);
+      const double rf = coop_rl(radSq, f);
+      const LaneBuf g1{coop_rl(gp, f)};
+      int c = 0;
+      for (int i0 = 0; i0 < nf; i0 += 64) {
+        const int i = i0 + lane;
+        c += __popcll(__ballot(i < nf && !lane_far(g1.pt(i), xf, yf, rf)));
+      }
+      if (c < nf) group_merge(S, lane, g1, nf, c, xf, yf, rf);
+      if (lane == f) nn = c;
+    }
+    wg_fence();
+    __builtin_amdgcn_wave_barrier();
+    const bool merged = red && nn < n1;
+    group_centroid(S, lane, merged, gp, nn, nullptr, 0, cx, cy, cs);
+    bool tail = false;
+    if (red) {
+      const int n_prev = n1;
+      n1 = nn;
+      len = n1;
+      if (n1 < 2) {
+        status = kSpecFail;
+        red = false;
+      } else if (n1 != n_prev) {
+        tail = true;
+      }
+    }
+    group_rect_tail(S, lane, tail, gp, n1, cx, cy, cs, ra2, prec, p, rec);
+    if (tail) {
+      const double density = double(n1) / (dist(rec.x1, rec.y1, rec.x2, rec.y2) * rec.width);
+      if (density >= 0.7) red = false;
+    }
+  }
 }
 
 // The round's fits (lane_rect + lane_refine of every lane with n >=
@@ -2459,8 +2831,12 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
         len = n;
         touched = n;
       }
-      coop_fit(s_coop[wv], lane, mine && n >= g.min_reg_size, n, reg_angle, fbuf, bufid, F, sd,
-               prec, p, myval1, status, rec, off, len, touched);
+      if constexpr (ORBPL_COOP_FIT == 2)
+        group_fit(s_coop[wv], lane, mine && n >= g.min_reg_size, n, reg_angle, fbuf, bufid, F,
+                  sd, prec, p, myval1, status, rec, off, len, touched);
+      else
+        coop_fit(s_coop[wv], lane, mine && n >= g.min_reg_size, n, reg_angle, fbuf, bufid, F,
+                 sd, prec, p, myval1, status, rec, off, len, touched);
     } else if (t < ncand && !keep) {
       if (n < 0) {
         status = n;
