@@ -2177,32 +2177,43 @@ __device__ __forceinline__ uint4* coop_rl(uint4* v, int l) {
 // every lane of the group adds its own row in point order. The sums round as
 // the sequential loop's; the serial part per point is three LDS reads and
 // three adds instead of the point's whole load / weight / product chain.
-template <bool kSubC, class Term>
+template <bool kSubC, class Load, class Term>
 __device__ __forceinline__ void group_sums(CoopScratch& S, int lane, bool act, int n, double& A,
-                                           double& B, double& C, Term term) {
+                                           double& B, double& C, Load load, Term term) {
   unsigned long long am = __ballot(act);
   while (am) {
+    // the group: the first kCoopG lanes of am, slot s = the s-th of them
+    int fs[kCoopG], nfs[kCoopG];
     unsigned long long gm = 0;
-    int ng = 0;
-    for (unsigned long long r = am; r && ng < kCoopG; r &= r - 1, ng++) gm |= r & (~r + 1ull);
-    am &= ~gm;
+#pragma unroll
+    for (int s = 0; s < kCoopG; s++) {
+      fs[s] = am ? __ffsll((long long)am) - 1 : -1;
+      nfs[s] = fs[s] >= 0 ? coop_rl(n, fs[s]) : 0;
+      if (am) {
+        gm |= am & (~am + 1ull);
+        am &= am - 1;
+      }
+    }
     const bool ing = (gm >> lane) & 1ull;
     const int myslot = __popcll(gm & ((1ull << lane) - 1ull));
     int nmax = ing ? n : 0;
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) nmax = max(nmax, __shfl_xor(nmax, o, 64));
     for (int k0 = 0; k0 < nmax; k0 += 64) {
-      int slot = 0;
-      for (unsigned long long r = gm; r; r &= r - 1, slot++) {
-        const int f = __ffsll((long long)r) - 1;
-        const int nf = coop_rl(n, f);
-        const int i = k0 + lane;
-        if (i < nf) {
+      const int i = k0 + lane;
+      // every slot's loads issue before any term is formed
+      uint4 v[kCoopG];
+#pragma unroll
+      for (int s = 0; s < kCoopG; s++)
+        v[s] = (i < nfs[s]) ? load(fs[s], i) : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+      for (int s = 0; s < kCoopG; s++) {
+        if (i < nfs[s]) {
           double ta, tb, tc;
-          term(f, i, ta, tb, tc);
-          S.ga[slot][lane] = ta;
-          S.gb[slot][lane] = tb;
-          S.gc[slot][lane] = tc;
+          term(fs[s], i, v[s], ta, tb, tc);
+          S.ga[s][lane] = ta;
+          S.gb[s][lane] = tb;
+          S.gc[s][lane] = tc;
         }
       }
       coop_lds_sync();
@@ -2246,24 +2257,30 @@ __device__ __forceinline__ void group_centroid(CoopScratch& S, int lane, bool ac
   x = 0;
   y = 0;
   sum = 0;
-  group_sums<false>(S, lane, act, n, x, y, sum,
-                    [&](int f, int i, double& ta, double& tb, double& tc) {
-                      const LaneBuf bf{coop_rl(bp, f)};
-                      uint32_t pt;
-                      double w;
-                      if (q) {
-                        pt = bf.pt(i);
-                        w = modgrad_q(q[(int)(pt >> 16) * sw + (int)(pt & 0xFFFF)]);
-                        bf.set_w(i, w);
-                      } else {
-                        const uint4 e = bf[i];
-                        pt = e.x;
-                        w = entry_w(e);
-                      }
-                      ta = double(pt & 0xFFFF) * w;
-                      tb = double(pt >> 16) * w;
-                      tc = w;
-                    });
+  if (q) {
+    group_sums<false>(
+        S, lane, act, n, x, y, sum,
+        [&](int f, int i) {
+          const uint32_t pt = LaneBuf{coop_rl(bp, f)}.pt(i);
+          return make_uint4(pt, (uint32_t)q[(int)(pt >> 16) * sw + (int)(pt & 0xFFFF)], 0u, 0u);
+        },
+        [&](int f, int i, const uint4& e, double& ta, double& tb, double& tc) {
+          const double w = modgrad_q((int)e.y);
+          LaneBuf{coop_rl(bp, f)}.set_w(i, w);
+          ta = double(e.x & 0xFFFF) * w;
+          tb = double(e.x >> 16) * w;
+          tc = w;
+        });
+  } else {
+    group_sums<false>(
+        S, lane, act, n, x, y, sum, [&](int f, int i) { return LaneBuf{coop_rl(bp, f)}[i]; },
+        [&](int f, int i, const uint4& e, double& ta, double& tb, double& tc) {
+          const double w = entry_w(e);
+          ta = double(e.x & 0xFFFF) * w;
+          tb = double(e.x >> 16) * w;
+          tc = w;
+        });
+  }
 }
 
 // lane_rect_tail for every act lane: inertia sums (group_sums), theta per
@@ -2277,17 +2294,16 @@ __device__ __forceinline__ void group_rect_tail(CoopScratch& S, int lane, bool a
     y /= sum;
   }
   double Ixx = 0.0, Iyy = 0.0, Ixy = 0.0;
-  group_sums<true>(S, lane, act, n, Ixx, Iyy, Ixy,
-                   [&](int f, int i, double& ta, double& tb, double& tc) {
-                     const LaneBuf bf{coop_rl(bp, f)};
-                     const double xf = coop_rl(x, f), yf = coop_rl(y, f);
-                     const uint4 e = bf[i];
-                     const double weight = entry_w(e);
-                     const double dx = double(pt_x(e)) - xf, dy = double(pt_y(e)) - yf;
-                     ta = dy * dy * weight;
-                     tb = dx * dx * weight;
-                     tc = dx * dy * weight;
-                   });
+  group_sums<true>(
+      S, lane, act, n, Ixx, Iyy, Ixy, [&](int f, int i) { return LaneBuf{coop_rl(bp, f)}[i]; },
+      [&](int f, int i, const uint4& e, double& ta, double& tb, double& tc) {
+        const double xf = coop_rl(x, f), yf = coop_rl(y, f);
+        const double weight = entry_w(e);
+        const double dx = double(pt_x(e)) - xf, dy = double(pt_y(e)) - yf;
+        ta = dy * dy * weight;
+        tb = dx * dx * weight;
+        tc = dx * dy * weight;
+      });
   double theta = 0, dx = 0, dy = 0;
   if (act) {
     const double lambda = 0.5 * (Ixx + Iyy - sqrt((Ixx - Iyy) * (Ixx - Iyy) + 4.0 * Ixy * Ixy));
@@ -2298,36 +2314,25 @@ __device__ __forceinline__ void group_rect_tail(CoopScratch& S, int lane, bool a
     dx = lsdm::cos_(theta);
     dy = lsdm::sin_(theta);
   }
+  // the extents: order-free max / min, one lane per region (lane_rect_tail)
   double l_min = 0, l_max = 0, w_min = 0, w_max = 0;
-  for (unsigned long long m = __ballot(act); m; m &= m - 1) {
-    const int f = __ffsll((long long)m) - 1;
-    const int nf = coop_rl(n, f);
-    const LaneBuf bf{coop_rl(bp, f)};
-    const double xf = coop_rl(x, f), yf = coop_rl(y, f), dxf = coop_rl(dx, f),
-                 dyf = coop_rl(dy, f);
-    double a0 = 0, a1 = 0, b0 = 0, b1 = 0;   // l_min, l_max, w_min, w_max
-    for (int i0 = 0; i0 < nf; i0 += 64) {
-      const int i = i0 + lane;
-      if (i < nf) {
-        const uint32_t pt = bf.pt(i);
-        const double regdx = double(pt & 0xFFFF) - xf, regdy = double(pt >> 16) - yf;
-        const double l = regdx * dxf + regdy * dyf;
-        const double w = -regdx * dyf + regdy * dxf;
-        a1 = l > a1 ? l : a1;
-        a0 = l < a0 ? l : a0;
-        b1 = w > b1 ? w : b1;
-        b0 = w < b0 ? w : b0;
+  if (act) {
+    const LaneBuf bf{bp};
+    constexpr int kB3 = 16;
+    for (int i0 = 0; i0 < n; i0 += kB3) {
+      uint32_t pt[kB3];
+#pragma unroll
+      for (int u = 0; u < kB3; u++) pt[u] = bf.pt(min(i0 + u, n - 1));
+#pragma unroll
+      for (int u = 0; u < kB3; u++) {
+        const double regdx = double(pt[u] & 0xFFFF) - x, regdy = double(pt[u] >> 16) - y;
+        const double l = regdx * dx + regdy * dy;
+        const double w = -regdx * dy + regdy * dx;
+        l_max = l > l_max ? l : l_max;
+        l_min = l < l_min ? l : l_min;
+        w_max = w > w_max ? w : w_max;
+        w_min = w < w_min ? w : w_min;
       }
-    }
-    a0 = coop_min(a0);
-    a1 = coop_max(a1);
-    b0 = coop_min(b0);
-    b1 = coop_max(b1);
-    if (lane == f) {
-      l_min = a0;
-      l_max = a1;
-      w_min = b0;
-      w_max = b1;
     }
   }
   if (act) {
@@ -2353,26 +2358,26 @@ __device__ __forceinline__ double group_tau(CoopScratch& S, int lane, bool act, 
                                            const Rect& rec) {
   double sum = 0, s_sum = 0, cnt = 0;
   const double width = rec.width;
-  group_sums<false>(S, lane, act, n, sum, s_sum, cnt,
-                    [&](int f, int i, double& ta, double& tb, double& tc) {
-                      const LaneBuf bf{coop_rl(bp, f)};
-                      const double wf = coop_rl(width, f);
-                      const uint4 e0 = bf[0];
-                      const double xc = double(pt_x(e0)), yc = double(pt_y(e0));
-                      const double ang_c = deg2ang(entry_deg(e0));
-                      const uint4 e = bf[i];
-                      ta = 0;
-                      tb = 0;
-                      tc = 0;
-                      // a point outside adds +0.0: the sums start at +0 and
-                      // never become -0, so x + 0.0 == x (skipping it)
-                      if (dist(xc, yc, pt_x(e), pt_y(e)) < wf) {
-                        const double ang_d = angle_diff_signed(deg2ang(entry_deg(e)), ang_c);
-                        ta = ang_d;
-                        tb = ang_d * ang_d;
-                        tc = 1.0;
-                      }
-                    });
+  group_sums<false>(
+      S, lane, act, n, sum, s_sum, cnt, [&](int f, int i) { return LaneBuf{coop_rl(bp, f)}[i]; },
+      [&](int f, int i, const uint4& e, double& ta, double& tb, double& tc) {
+        const LaneBuf bf{coop_rl(bp, f)};
+        const double wf = coop_rl(width, f);
+        const uint4 e0 = bf[0];
+        const double xc = double(pt_x(e0)), yc = double(pt_y(e0));
+        const double ang_c = deg2ang(entry_deg(e0));
+        ta = 0;
+        tb = 0;
+        tc = 0;
+        // a point outside adds +0.0: the sums start at +0 and never become
+        // -0, so x + 0.0 == x (skipping it)
+        if (dist(xc, yc, pt_x(e), pt_y(e)) < wf) {
+          const double ang_d = angle_diff_signed(deg2ang(entry_deg(e)), ang_c);
+          ta = ang_d;
+          tb = ang_d * ang_d;
+          tc = 1.0;
+        }
+      });
   if (!act) return 0.0;
   const int c = (int)cnt;
   const double mean_angle = sum / double(c);
