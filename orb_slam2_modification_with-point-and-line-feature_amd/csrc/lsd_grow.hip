@@ -2420,6 +2420,83 @@ __device__ __forceinline__ void group_merge(CoopScratch& S, int lane, LaneBuf g1
   coop_lds_sync();
 }
 
+// ORBPL_COOP_GROW2: refine's second region grow one region at a time on
+// the whole wave (the round's refining lanes one after another) instead of
+// one lane per region: per step the 8 neighbour words of the point being
+// expanded are loaded by 8 lanes at once and their flags and angles formed
+// in parallel; the in-order walk (the aligned test against the current
+// region angle, the claim, the add) runs on wave-uniform values, the same
+// operations in the same order as lane_grow.
+#ifndef ORBPL_COOP_GROW2
+#define ORBPL_COOP_GROW2 1
+#endif
+__device__ __forceinline__ uint32_t coop_rlu(uint32_t v, int l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+__device__ int wave_grow(const Frame& F, uint64_t* sd, LaneBuf buf, int cap, int sx, int sy,
+                         double& reg_angle, double prec, uint32_t myval, int lane) {
+  const uint32_t mytag = myval >> 1;
+  const int sw = F.sw, sh = F.sh, tw = F.tw;
+  const int si = lsd_sd_index(sx, sy, tw);
+  if (cap < 1) return kSpecOverflow;
+  const uint64_t v0 = ld_sd(sd + si);
+  const uint32_t v0lo = coop_rlu((uint32_t)v0, 0), v0hi = coop_rlu((uint32_t)(v0 >> 32), 0);
+  if ((v0hi >> 1) < mytag) return kSpecConflict;
+  if (lane == 0)
+    atomicMin(reinterpret_cast<unsigned long long*>(sd + si),
+              ((unsigned long long)myval << 32) | v0lo);
+  uint4 cur = make_uint4((uint32_t)sx | ((uint32_t)sy << 16), v0lo, 0u, 0u);
+  if (lane == 0) buf[0] = cur;
+  reg_angle = deg2ang(entry_deg(cur));
+  double s0, c0;
+  lsdm::sincos_(reg_angle, &s0, &c0);
+  float sumdx = (float)c0;
+  float sumdy = (float)s0;
+  const double k3pi2 = (3 * kPi) / 2, k2pi = 2 * kPi;
+  // lane k < 9 handles neighbour k = (dy + 1) * 3 + (dx + 1)
+  const int kdx = lane % 3 - 1, kdy = lane / 3 - 1;
+  const bool klane = lane < 9 && lane != 4;
+  int n = 1;
+  for (int i = 0; i < n; i++) {
+    const int x = pt_x(cur), y = pt_y(cur);
+    const int n_start = n;
+    const uint4 pref = buf[min(i + 1, n_start - 1)];
+    const int xx = x + kdx, yy = y + kdy;
+    const bool in = klane && xx >= 0 && xx < sw && yy >= 0 && yy < sh;
+    uint4 w = make_uint4(0u, 0u, 0u, 0u);
+    if (in) w = *reinterpret_cast<const uint4*>(sd + lsd_sd_index(xx, yy, tw));
+    const bool flag = in && w.y != 0u && w.y != myval && __uint_as_float(w.x) >= 0.f;
+    const double ang = deg2ang(__uint_as_float(w.x));
+    unsigned okm = (unsigned)__ballot(flag);
+    uint4 first_add = cur;
+    while (okm) {
+      const int k = __ffs((int)okm) - 1;
+      okm &= okm - 1;
+      // aligned_deg(d, reg_angle, prec) for a defined d (lane_grow's test)
+      double nt = fabs(reg_angle - coop_rl(ang, k));
+      nt = nt > k3pi2 ? fabs(nt - k2pi) : nt;
+      if (nt <= prec) {
+        const uint32_t wx = coop_rlu(w.x, k), wy = coop_rlu(w.y, k);
+        if ((wy >> 1) < mytag) return kSpecConflict;   // an earlier seed's pixel
+        const int ax = x + (k % 3) - 1, ay = y + (k / 3) - 1;
+        if (lane == 0)
+          atomicMin(reinterpret_cast<unsigned long long*>(sd + lsd_sd_index(ax, ay, tw)),
+                    ((unsigned long long)myval << 32) | wx);
+        if (n >= cap) return kSpecOverflow;
+        const uint4 e = make_uint4((uint32_t)ax | ((uint32_t)ay << 16), wx, 0u, 0u);
+        if (n == n_start) first_add = e;
+        if (lane == 0) buf[n] = e;
+        n++;
+        sumdx += __uint_as_float(coop_rlu(w.z, k));   // add_angle(d) terms
+        sumdy += __uint_as_float(coop_rlu(w.w, k));
+        reg_angle = (double)fast_atan2_deg_1div(sumdy, sumdx) * kDegToRad;
+      }
+    }
+    cur = (i + 1 < n_start) ? pref : first_add;
+  }
+  return n;
+}
+
 // ORBPL_COOP_FIT=2: the round's fits with the per-lane control flow of
 // lane_rect + lane_refine and the wave-wide passes above
 __device__ __forceinline__ void group_fit(CoopScratch& S, int lane, bool fitter, int n,
@@ -2451,7 +2528,25 @@ __device__ __forceinline__ void group_fit(CoopScratch& S, int lane, bool fitter,
     const uint4 e0 = buf[0];
     x0 = pt_x(e0);
     y0 = pt_y(e0);
+  }
+  if constexpr (ORBPL_COOP_GROW2) {
+    for (unsigned long long m = __ballot(refine); m; m &= m - 1) {
+      const int f = __ffsll((long long)m) - 1;
+      const int nf = coop_rl(n, f);
+      double ra = 0;
+      const int r = wave_grow(F, sd, LaneBuf{coop_rl(bp, f) + nf}, kLaneCap - nf, coop_rl(x0, f),
+                              coop_rl(y0, f), ra, coop_rl(tau, f), coop_rlu(myval1, f), lane);
+      if (lane == f) {
+        n1 = r;
+        ra2 = ra;
+      }
+    }
+    wg_fence();
+    __builtin_amdgcn_wave_barrier();
+  } else if (refine) {
     n1 = lane_grow(F, sd, buf + n, kLaneCap - n, x0, y0, ra2, tau, myval1);
+  }
+  if (refine) {
     if (n1 < 0) {
       status = n1;
       refine = false;
