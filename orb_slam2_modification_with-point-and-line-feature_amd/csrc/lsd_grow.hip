@@ -1910,7 +1910,7 @@ constexpr int kSpecSmallBatch = ORBPL_SPEC_SMALL_BATCH;
 // measured no faster: the per-region fixed costs and the serialised regions
 // outweigh the parallel points); 2: per-lane fits with wave-wide passes
 #ifndef ORBPL_COOP_FIT
-#define ORBPL_COOP_FIT 2
+#define ORBPL_COOP_FIT 0
 #endif
 
 // fitters whose terms share LDS at once (ORBPL_COOP_FIT=2)
@@ -2428,7 +2428,7 @@ __device__ __forceinline__ void group_merge(CoopScratch& S, int lane, LaneBuf g1
 // region angle, the claim, the add) runs on wave-uniform values, the same
 // operations in the same order as lane_grow.
 #ifndef ORBPL_COOP_GROW2
-#define ORBPL_COOP_GROW2 1
+#define ORBPL_COOP_GROW2 0
 #endif
 __device__ __forceinline__ uint32_t coop_rlu(uint32_t v, int l) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
