@@ -1908,9 +1908,13 @@ constexpr int kSpecSmallBatch = ORBPL_SPEC_SMALL_BATCH;
 // ---------------------------------------------------------------------------
 // 0: per lane; 1: one fitting region at a time across the wave (bit-exact,
 // measured no faster: the per-region fixed costs and the serialised regions
-// outweigh the parallel points); 2: per-lane fits with wave-wide passes
+// outweigh the parallel points); 2: per-lane fits with wave-wide passes, the
+// default: bit-exact (26 LSD tests, the -m gpu suite), measured on three boxes
+// (tools/gpu_r04_{m,o,p}.sh) LSD batch 1 44.0-47.4 vs 44.4-51.5 ms, batch 16
+// 51.8-53.1 vs 54.6-55.5 ms, batch 1536 115.3 vs 118.8 ms (the fit phase
+// 47-51M vs 49-60M cycles per frame)
 #ifndef ORBPL_COOP_FIT
-#define ORBPL_COOP_FIT 0
+#define ORBPL_COOP_FIT 2
 #endif
 
 // fitters whose terms share LDS at once (ORBPL_COOP_FIT=2)
