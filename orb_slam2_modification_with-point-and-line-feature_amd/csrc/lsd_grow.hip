@@ -735,6 +735,11 @@ __device__ __forceinline__ float fast_atan2_deg_1div(float y, float x) {
   return a;
 }
 
+// ORBPL_GROW_U32: 32-bit unsigned byte offsets for the grow's neighbour
+// loads and claims (A/B build override)
+#ifndef ORBPL_GROW_U32
+#define ORBPL_GROW_U32 1
+#endif
 #if ORBPL_GROW_LEAN && ORBPL_GROW_CS && ORBPL_SD_PAIRED
 // region_grow for one lane (same result as the step below). Per step the 8
 // neighbour addresses come from 3 row and 3 column terms of the tile index;
@@ -771,7 +776,14 @@ __device__ __forceinline__ int lane_grow(const Frame& F, uint64_t* sd, LaneBuf b
     const uint4 pref = buf[min(i + 1, n_start - 1)];
     // tile index = row term + column term (disjoint bit fields), x2 for the
     // paired 16-byte entries
+#if ORBPL_GROW_U32
+    // byte offsets from the frame's (wave-uniform) pixel-word base as 32-bit
+    // unsigned values: the loads and claims take the scalar-base + 32-bit
+    // vector-offset form (no 64-bit address arithmetic per neighbour)
+    uint32_t rterm[3], cterm[3];
+#else
     int rterm[3], cterm[3];
+#endif
     bool rin[3], cin[3];
 #pragma unroll
     for (int d = 0; d < 3; d++) {
@@ -779,14 +791,24 @@ __device__ __forceinline__ int lane_grow(const Frame& F, uint64_t* sd, LaneBuf b
       rin[d] = yy >= 0 && yy < sh;
       cin[d] = xx >= 0 && xx < sw;
       const int cy = min(max(yy, 0), sh - 1), cx = min(max(xx, 0), sw - 1);
+#if ORBPL_GROW_U32
+      rterm[d] = ((((uint32_t)(cy >> 2) * (uint32_t)tw) << 5) | ((uint32_t)(cy & 3) << 3)) << 3;
+      cterm[d] = (((uint32_t)(cx >> 2) << 5) | ((uint32_t)(cx & 3) << 1)) << 3;
+#else
       rterm[d] = (((cy >> 2) * tw) << 5) | ((cy & 3) << 3);
       cterm[d] = ((cx >> 2) << 5) | ((cx & 3) << 1);
+#endif
     }
     uint4 w[9];
 #pragma unroll
     for (int k = 0; k < 9; k++) {
       if (k == 4) continue;
+#if ORBPL_GROW_U32
+      w[k] = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(sd) +
+                                             (rterm[k / 3] + cterm[k % 3]));
+#else
       w[k] = *reinterpret_cast<const uint4*>(sd + (rterm[k / 3] + cterm[k % 3]));
+#endif
     }
     unsigned ok = 0;
 #pragma unroll
@@ -806,9 +828,15 @@ __device__ __forceinline__ int lane_grow(const Frame& F, uint64_t* sd, LaneBuf b
       nt = nt > k3pi2 ? fabs(nt - k2pi) : nt;
       if (((ok >> k) & 1u) && nt <= prec) {
         if ((w[k].y >> 1) < mytag) return kSpecConflict;   // an earlier seed's pixel
+#if ORBPL_GROW_U32
+        atomicMin(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(sd) +
+                                                        (rterm[k / 3] + cterm[k % 3])),
+                  ((unsigned long long)myval << 32) | w[k].x);
+#else
         const int id = rterm[k / 3] + cterm[k % 3];
         atomicMin(reinterpret_cast<unsigned long long*>(sd + id),
                   ((unsigned long long)myval << 32) | w[k].x);
+#endif
         if (n >= cap) return kSpecOverflow;
         const int xx = x + (k % 3) - 1, yy = y + (k / 3) - 1;
         const uint4 e = make_uint4((uint32_t)xx | ((uint32_t)yy << 16), w[k].x, 0u, 0u);
@@ -2181,6 +2209,11 @@ __device__ __forceinline__ uint4* coop_rl(uint4* v, int l) {
 // every lane of the group adds its own row in point order. The sums round as
 // the sequential loop's; the serial part per point is three LDS reads and
 // three adds instead of the point's whole load / weight / product chain.
+// ORBPL_COOP_CHAIN: the three sums of a slot on three lanes (1) or all on
+// the fitter's lane (0; A/B build override)
+#ifndef ORBPL_COOP_CHAIN
+#define ORBPL_COOP_CHAIN 1
+#endif
 template <bool kSubC, class Load, class Term>
 __device__ __forceinline__ void group_sums(CoopScratch& S, int lane, bool act, int n, double& A,
                                            double& B, double& C, Load load, Term term) {
@@ -2200,6 +2233,23 @@ __device__ __forceinline__ void group_sums(CoopScratch& S, int lane, bool act, i
     }
     const bool ing = (gm >> lane) & 1ull;
     const int myslot = __popcll(gm & ((1ull << lane) - 1ull));
+#if ORBPL_COOP_CHAIN
+    // chain lanes: lane c * kCoopG + s adds sum c (A, B, C) of slot s, so a
+    // point's three ordered adds run on three lanes at once; C's terms are
+    // stored negated where the sum subtracts (x - y == x + (-y) exactly)
+    const int cs = lane % kCoopG, cc = lane / kCoopG;
+    int myf = -1, mynf = 0;
+#pragma unroll
+    for (int s2 = 0; s2 < kCoopG; s2++) {
+      myf = cs == s2 ? fs[s2] : myf;
+      mynf = cs == s2 ? nfs[s2] : mynf;
+    }
+    const bool chain = cc < 3 && myf >= 0;
+    const double a0 = shfl_d(A, max(myf, 0)), b0 = shfl_d(B, max(myf, 0)),
+                 c0 = shfl_d(C, max(myf, 0));
+    double acc = cc == 0 ? a0 : (cc == 1 ? b0 : c0);
+    const double* prow = cc == 0 ? S.ga[cs] : (cc == 1 ? S.gb[cs] : S.gc[cs]);
+#endif
     int nmax = ing ? n : 0;
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) nmax = max(nmax, __shfl_xor(nmax, o, 64));
@@ -2217,10 +2267,24 @@ __device__ __forceinline__ void group_sums(CoopScratch& S, int lane, bool act, i
           term(fs[s], i, v[s], ta, tb, tc);
           S.ga[s][lane] = ta;
           S.gb[s][lane] = tb;
-          S.gc[s][lane] = tc;
+          S.gc[s][lane] = (ORBPL_COOP_CHAIN && kSubC) ? -tc : tc;
         }
       }
       coop_lds_sync();
+#if ORBPL_COOP_CHAIN
+      if (chain) {
+        const int cnt = min(64, mynf - k0);
+        int k = 0;
+        for (; k + 4 <= cnt; k += 4) {
+          double xv[4];
+#pragma unroll
+          for (int u = 0; u < 4; u++) xv[u] = prow[k + u];
+#pragma unroll
+          for (int u = 0; u < 4; u++) acc += xv[u];
+        }
+        for (; k < cnt; k++) acc += prow[k];
+      }
+#else
       if (ing) {
         const int cnt = min(64, n - k0);
         const double* pa = S.ga[myslot];
@@ -2248,8 +2312,19 @@ __device__ __forceinline__ void group_sums(CoopScratch& S, int lane, bool act, i
           C = kSubC ? C - pc[k] : C + pc[k];
         }
       }
+#endif
       coop_lds_sync();
     }
+#if ORBPL_COOP_CHAIN
+    // the chain lanes' sums back to their fitters
+    const double ra = shfl_d(acc, myslot), rb = shfl_d(acc, kCoopG + myslot),
+                 rc = shfl_d(acc, 2 * kCoopG + myslot);
+    if (ing) {
+      A = ra;
+      B = rb;
+      C = rc;
+    }
+#endif
   }
 }
 

@@ -769,7 +769,12 @@ __global__ void __launch_bounds__(kLocalThreads, 4) k_lsd_sort_local(LsdGeom g, 
   }
 }
 
-__global__ void __launch_bounds__(kSortThreads) k_lsd_sort(LsdGeom g, LsdScratch sc) {
+// waves per SIMD k_lsd_sort's register budget must allow (A/B build override;
+// 1 = unbounded: 63 VGPRs, 4 workgroups of 512 per CU)
+#ifndef ORBPL_SORT_MINW
+#define ORBPL_SORT_MINW 1
+#endif
+__global__ void __launch_bounds__(kSortThreads, ORBPL_SORT_MINW) k_lsd_sort(LsdGeom g, LsdScratch sc) {
   const int f = blockIdx.x;
   SortPtrs P = sort_ptrs(g, sc, f);
   // bins: int(norm * bin_coef), bin_coef = 1023 / max_grad (ll_angle)
