@@ -353,6 +353,16 @@ __device__ __forceinline__ int skey(uint32_t e) { return (int)(e >> 22); }
 #define ORBPL_SORT_THREADS 512
 #endif
 constexpr int kSortThreads = ORBPL_SORT_THREADS;   // k_lsd_sort's workgroup (A/B build override)
+// k_lsd_sort's partition chunk (elements; a multiple of 64, at least
+// kLsdSortChunk so that the chunk scratch sized for kLsdSortChunk suffices):
+// every lane keeps CH / 64 loads in flight per chunk
+#ifndef ORBPL_SORT_CHUNK_G
+#define ORBPL_SORT_CHUNK_G 1024
+#endif
+constexpr int kSortChunkG = ORBPL_SORT_CHUNK_G;
+static_assert(kSortChunkG % 64 == 0 && kSortChunkG >= kLsdSortChunk, "sort chunk");
+// segments of one level whose table k_lsd_sort keeps in LDS (more: global)
+constexpr int kSortTab = 1024;
 
 // Exclusive scan of a[0..len) (global) in place by the whole block; returns
 // the total in every thread.
@@ -445,8 +455,12 @@ __device__ void heap_sort_seg(uint32_t* A, int len) {
 }
 
 // Sorts A[first, last) whose introsort depth budget is depth0 (the top
-// level: 2 * floor(log2(n))). NT threads.
-template <int NT>
+// level: 2 * floor(log2(n))). NT threads, CH elements per partition chunk
+// (the decomposition only: any CH gives the same permutation). TAB: a level's
+// segment table (first, last, pivot key, first chunk) is copied to LDS so that
+// a chunk finds its segment by a binary search in LDS instead of a chain of
+// dependent global loads (the global-memory kernel; up to kSortTab segments).
+template <int NT, int CH = kLsdSortChunk, bool TAB = false>
 //
 // Segments carry an upper bound of their keys in .w: the right part of a
 // partition (keys <= pivot) gets min(bound, pivot key). A segment whose bound
@@ -458,6 +472,7 @@ __device__ __forceinline__ void sort_core(const SortPtrs& P, int first0, int las
                                           int ub0) {
   __shared__ int s_w[(NT / 64)];
   __shared__ int s_nseg, s_next, s_nheap, s_nleaf;
+  __shared__ int4 s_tab[TAB ? kSortTab : 1];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   uint32_t* A = P.A;
   int* piv = P.si;
@@ -500,7 +515,7 @@ __device__ __forceinline__ void sort_core(const SortPtrs& P, int first0, int las
       const int mid = first + (last - first) / 2;
       move_median_to_first(A, first, first + 1, mid, last - 1);
       piv[s] = skey(A[first]);
-      nch[s] = (last - first + kLsdSortChunk - 1) / kLsdSortChunk;
+      nch[s] = (last - first + CH - 1) / CH;
       choff[s] = nch[s];
     }
     __syncthreads();
@@ -509,21 +524,45 @@ __device__ __forceinline__ void sort_core(const SortPtrs& P, int first0, int las
       if (t == 0) *P.err |= 1;
       return;
     }
-    // R3: per chunk L / R stopper counts
-    for (int ch = wave; ch < nchunks; ch += (NT / 64)) {
+    const bool tab = TAB && nseg <= kSortTab;
+    if (tab) {
+      for (int s = t; s < nseg; s += NT) {
+        const int4 sg = cur[s];
+        s_tab[s] = make_int4(sg.x, sg.y, piv[s], choff[s]);
+      }
+      __syncthreads();
+    }
+    // the segment of chunk ch: (first, last, pivot key, first chunk) and its index
+    auto seg_of = [&](int ch, int& s) -> int4 {
       int lo = 0, hi = nseg;  // last segment with choff <= ch
+      if (tab) {
+        while (hi - lo > 1) {
+          const int m = (lo + hi) >> 1;
+          if (s_tab[m].w <= ch) lo = m;
+          else hi = m;
+        }
+        s = lo;
+        return s_tab[lo];
+      }
       while (hi - lo > 1) {
         const int m = (lo + hi) >> 1;
         if (choff[m] <= ch) lo = m;
         else hi = m;
       }
-      const int s = lo;
-      const int4 sg = cur[s];
-      const int first = sg.x, last = sg.y, p = piv[s];
-      const int b = first + (ch - choff[s]) * kLsdSortChunk;
-      const int e = min(b + kLsdSortChunk, last);
+      s = lo;
+      const int4 sg = cur[lo];
+      return make_int4(sg.x, sg.y, piv[lo], choff[lo]);
+    };
+    // R3: per chunk L / R stopper counts
+    for (int ch = wave; ch < nchunks; ch += (NT / 64)) {
+      int s;
+      const int4 sq = seg_of(ch, s);
+      const int first = sq.x, last = sq.y, p = sq.z;
+      const int b = first + (ch - sq.w) * CH;
+      const int e = min(b + CH, last);
       int cl = 0, cr = 0;
-      for (int j = 0; j < kLsdSortChunk / 64; j++) {
+#pragma unroll
+      for (int j = 0; j < CH / 64; j++) {
         const int i = b + j * 64 + lane;
         bool fl = false, fr = false;
         if (i < e) {
@@ -548,21 +587,15 @@ __device__ __forceinline__ void sort_core(const SortPtrs& P, int first0, int las
     __syncthreads();
     // R5: scatter stopper positions by rank
     for (int ch = wave; ch < nchunks; ch += (NT / 64)) {
-      int lo = 0, hi = nseg;
-      while (hi - lo > 1) {
-        const int m = (lo + hi) >> 1;
-        if (choff[m] <= ch) lo = m;
-        else hi = m;
-      }
-      const int s = lo;
-      const int4 sg = cur[s];
-      const int first = sg.x, last = sg.y, p = piv[s];
-      const int c0 = choff[s], c1 = c0 + nch[s] - 1;
-      const int b = first + (ch - c0) * kLsdSortChunk;
-      const int e = min(b + kLsdSortChunk, last);
-      unsigned long long mL[kLsdSortChunk / 64], mR[kLsdSortChunk / 64];
+      int s;
+      const int4 sq = seg_of(ch, s);
+      const int first = sq.x, last = sq.y, p = sq.z;
+      const int c0 = sq.w, c1 = c0 + (last - first + CH - 1) / CH - 1;
+      const int b = first + (ch - c0) * CH;
+      const int e = min(b + CH, last);
+      unsigned long long mL[CH / 64], mR[CH / 64];
 #pragma unroll
-      for (int j = 0; j < kLsdSortChunk / 64; j++) {
+      for (int j = 0; j < CH / 64; j++) {
         const int i = b + j * 64 + lane;
         bool fl = false, fr = false;
         if (i < e) {
@@ -576,7 +609,7 @@ __device__ __forceinline__ void sort_core(const SortPtrs& P, int first0, int las
       int runL = Lpre[ch] - Lpre[c0];
       int sufR = Rsuf[ch] - Rsuf[c1];
 #pragma unroll
-      for (int j = kLsdSortChunk / 64 - 1; j >= 0; j--) {
+      for (int j = CH / 64 - 1; j >= 0; j--) {
         const int i = b + j * 64 + lane;
         if ((mR[j] >> lane) & 1ull) {
           const int k = sufR + __popcll(mR[j] & ~(below | (1ull << lane)));
@@ -585,7 +618,7 @@ __device__ __forceinline__ void sort_core(const SortPtrs& P, int first0, int las
         sufR += __popcll(mR[j]);
       }
 #pragma unroll
-      for (int j = 0; j < kLsdSortChunk / 64; j++) {
+      for (int j = 0; j < CH / 64; j++) {
         const int i = b + j * 64 + lane;
         if ((mL[j] >> lane) & 1ull) P.Lpos[first + runL + __popcll(mL[j] & below)] = i;
         runL += __popcll(mL[j]);
@@ -615,15 +648,10 @@ __device__ __forceinline__ void sort_core(const SortPtrs& P, int first0, int las
     __syncthreads();
     // R7: swaps (disjoint pairs)
     for (int ch = wave; ch < nchunks; ch += (NT / 64)) {
-      int lo = 0, hi = nseg;
-      while (hi - lo > 1) {
-        const int m = (lo + hi) >> 1;
-        if (choff[m] <= ch) lo = m;
-        else hi = m;
-      }
-      const int s = lo;
-      const int first = cur[s].x;
-      const int kb = Lpre[ch] - Lpre[choff[s]];
+      int s;
+      const int4 sq = seg_of(ch, s);
+      const int first = sq.x;
+      const int kb = Lpre[ch] - Lpre[sq.w];
       const int ke = min(kb + Lc[ch], sK[s]);
       for (int k = kb + lane; k < ke; k += 64) {
         const int i = P.Lpos[first + k], j = P.Rpos[first + k];
@@ -769,10 +797,15 @@ __global__ void __launch_bounds__(kLocalThreads, 4) k_lsd_sort_local(LsdGeom g, 
   }
 }
 
-// waves per SIMD k_lsd_sort's register budget must allow (A/B build override;
-// 1 = unbounded: 63 VGPRs, 4 workgroups of 512 per CU)
+// waves per SIMD k_lsd_sort's register budget must allow (A/B build override):
+// 8 = 64 VGPRs, 4 workgroups of 512 per CU (unbounded, the 1024-element chunks
+// take 94). Measured with the LDS segment table (tools/gpu_r04_s.sh, kernel
+// time per launch, bit-exact): batch 1 2.39 ms (previous sort) -> 1.68 (1024,
+// unbounded) / 1.73 (1024, 8 waves) / 1.80 (512, 8 waves) / 2.06 (256, table
+// only); 1536 frames 18.1 -> 15.1 / 12.0 / 12.3 / 17.8 ms; LSD at 3072 frames
+// 187.4 -> 172.7 ms (512, 8 waves), lines leg 14.3-14.6k -> 15.2-15.8k frames/s
 #ifndef ORBPL_SORT_MINW
-#define ORBPL_SORT_MINW 1
+#define ORBPL_SORT_MINW 8
 #endif
 __global__ void __launch_bounds__(kSortThreads, ORBPL_SORT_MINW) k_lsd_sort(LsdGeom g, LsdScratch sc) {
   const int f = blockIdx.x;
@@ -805,7 +838,7 @@ __global__ void __launch_bounds__(kSortThreads, ORBPL_SORT_MINW) k_lsd_sort(LsdG
     sc.sort_kt[f] = kt;
     sc.sort_nge[f] = s_nge;
   }
-  sort_core<kSortThreads>(P, 0, g.n, g.n > 16 ? 2 * (31 - __clz(g.n)) : 0, 1023);
+  sort_core<kSortThreads, kSortChunkG, true>(P, 0, g.n, g.n > 16 ? 2 * (31 - __clz(g.n)) : 0, 1023);
 }
 
 // test hook: sort caller-provided keys (frame slot 0)
@@ -820,7 +853,8 @@ __global__ void __launch_bounds__(kSortThreads) k_lsd_sort_keys(LsdGeom g, LsdSc
     sc.sort_nge[0] = g.n;
   }
   __syncthreads();
-  sort_core<kSortThreads>(P, 0, g.n, g.n > 16 ? 2 * (31 - __clz(g.n)) : 0, 1 << 30);
+  sort_core<kSortThreads, kSortChunkG, true>(P, 0, g.n, g.n > 16 ? 2 * (31 - __clz(g.n)) : 0,
+                                            1 << 30);
 }
 
 void launch_lsd_blur(const LsdGeom& g, const uint8_t* img, int stride, long long frame_pitch,
