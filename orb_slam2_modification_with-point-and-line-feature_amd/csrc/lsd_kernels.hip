@@ -363,6 +363,11 @@ constexpr int kSortChunkG = ORBPL_SORT_CHUNK_G;
 static_assert(kSortChunkG % 64 == 0 && kSortChunkG >= kLsdSortChunk, "sort chunk");
 // segments of one level whose table k_lsd_sort keeps in LDS (more: global)
 constexpr int kSortTab = 1024;
+// batches up to this many frames sort with 1024-thread workgroups
+#ifndef ORBPL_SORT_WIDE_BATCH
+#define ORBPL_SORT_WIDE_BATCH 256
+#endif
+constexpr int kSortWideBatch = ORBPL_SORT_WIDE_BATCH;
 
 // Exclusive scan of a[0..len) (global) in place by the whole block; returns
 // the total in every thread.
@@ -807,7 +812,8 @@ __global__ void __launch_bounds__(kLocalThreads, 4) k_lsd_sort_local(LsdGeom g, 
 #ifndef ORBPL_SORT_MINW
 #define ORBPL_SORT_MINW 8
 #endif
-__global__ void __launch_bounds__(kSortThreads, ORBPL_SORT_MINW) k_lsd_sort(LsdGeom g, LsdScratch sc) {
+template <int NT>
+__global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : ORBPL_SORT_MINW) k_lsd_sort(LsdGeom g, LsdScratch sc) {
   const int f = blockIdx.x;
   SortPtrs P = sort_ptrs(g, sc, f);
   // bins: int(norm * bin_coef), bin_coef = 1023 / max_grad (ll_angle)
@@ -824,11 +830,25 @@ __global__ void __launch_bounds__(kSortThreads, ORBPL_SORT_MINW) k_lsd_sort(LsdG
   if (threadIdx.x == 0) s_nge = 0;
   __syncthreads();
   int nge = 0;
-  for (int i = threadIdx.x; i < g.n; i += kSortThreads) {
-    const int y = i / w1, x = i - y * w1;
-    const int key = (int)(sqrt(q[y * sw + x] / 4.0) * bin_coef);
-    P.A[i] = ((uint32_t)key << 22) | (uint32_t)i;
-    nge += key >= kt;
+  // the keys, kU gradient loads of a thread in flight at once
+  constexpr int kU = 4;
+  for (int i0 = threadIdx.x; i0 < g.n; i0 += NT * kU) {
+    int qv[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const int i = min(i0 + u * NT, g.n - 1);
+      const int y = i / w1, x = i - y * w1;
+      qv[u] = q[y * sw + x];
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const int i = i0 + u * NT;
+      if (i < g.n) {
+        const int key = (int)(sqrt(qv[u] / 4.0) * bin_coef);
+        P.A[i] = ((uint32_t)key << 22) | (uint32_t)i;
+        nge += key >= kt;
+      }
+    }
   }
   for (int o = 32; o >= 1; o >>= 1) nge += __shfl_xor(nge, o, 64);
   if ((threadIdx.x & 63) == 0 && nge) atomicAdd(&s_nge, nge);
@@ -838,7 +858,7 @@ __global__ void __launch_bounds__(kSortThreads, ORBPL_SORT_MINW) k_lsd_sort(LsdG
     sc.sort_kt[f] = kt;
     sc.sort_nge[f] = s_nge;
   }
-  sort_core<kSortThreads, kSortChunkG, true>(P, 0, g.n, g.n > 16 ? 2 * (31 - __clz(g.n)) : 0, 1023);
+  sort_core<NT, kSortChunkG, true>(P, 0, g.n, g.n > 16 ? 2 * (31 - __clz(g.n)) : 0, 1023);
 }
 
 // test hook: sort caller-provided keys (frame slot 0)
@@ -892,7 +912,14 @@ __host__ int lsd_sort_local_blocks(int batch) {
 }
 
 void launch_lsd_sort(const LsdGeom& g, const LsdScratch& sc, int batch, hipStream_t s) {
-  hipLaunchKernelGGL(k_lsd_sort, dim3(batch), dim3(kSortThreads), 0, s, g, sc);
+  // a batch that leaves CUs idle: 1024-thread workgroups (twice the chunks in
+  // flight per frame); ORBPL_SORT_WIDE_BATCH overrides the batch bound
+  static const char* wb_env = getenv("ORBPL_SORT_WIDE_BATCH");
+  static const int wide_batch = wb_env ? atoi(wb_env) : kSortWideBatch;
+  if (kSortThreads < 1024 && batch <= wide_batch)
+    hipLaunchKernelGGL(k_lsd_sort<1024>, dim3(batch), dim3(1024), 0, s, g, sc);
+  else
+    hipLaunchKernelGGL(k_lsd_sort<kSortThreads>, dim3(batch), dim3(kSortThreads), 0, s, g, sc);
   hipLaunchKernelGGL(k_lsd_sort_local, dim3(lsd_sort_local_blocks(batch), batch),
                      dim3(kLocalThreads), 0, s, g, sc);
 }
