@@ -794,7 +794,14 @@ __global__ void __launch_bounds__(kLocalThreads, 4) k_lsd_sort_local(LsdGeom g, 
   for (int k = blockIdx.x; k < nloc; k += gridDim.x) {
     const int4 sg = loc[k];
     const int m = sg.y - sg.x;
-    for (int i = t; i < m; i += kLocalThreads) sA[i] = A[sg.x + i];
+    // the segment's loads all in flight at once (m <= kSortLocalMax)
+    constexpr int kLU = kSortLocalMax / kLocalThreads;
+    uint32_t lv[kLU];
+#pragma unroll
+    for (int u = 0; u < kLU; u++) lv[u] = A[sg.x + min(t + u * kLocalThreads, m - 1)];
+#pragma unroll
+    for (int u = 0; u < kLU; u++)
+      if (t + u * kLocalThreads < m) sA[t + u * kLocalThreads] = lv[u];
     __syncthreads();
     sort_core<kLocalThreads>(L, 0, m, sg.z, sg.w);
     for (int i = t; i < m; i += kLocalThreads) A[sg.x + i] = sA[i];
