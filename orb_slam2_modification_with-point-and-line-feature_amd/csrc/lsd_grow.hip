@@ -3687,6 +3687,81 @@ __global__ void __launch_bounds__(256, ORBPL_VAL_MINW) k_lsd_validate(LsdGeom g,
   }
 }
 
+// Small batches: one WAVE per rectangle (rect_improve / rect_nfa / nfa, the
+// wave-cooperative restatement: the row walk on every lane, the pixels of the
+// rows counted 64 x 8 at a time, nfa's tail stopping test one iteration per
+// lane), waves fetching rectangles from a workgroup counter. With few frames
+// the per-lane kernel's time is its longest rectangle's serial walk; here a
+// rectangle's walk is spread over the wave. Same counts, same log_nfa.
+// Workgroups per frame: enough for ~1024 in all (at least 8).
+// Measured slower and off (bit-exact, 26 LSD tests; tools/gpu_r04_v.sh, kernel
+// time per launch): batch 1 1.10 vs 0.96 ms, 16 1.77 vs 1.10, 64 6.8 vs 1.26
+// ms - the per-lane kernel is not bound by its longest rectangle but by the
+// total walk work, which the wave version does not shrink (its row walk runs
+// on every lane); ORBPL_VAL_WAVE_BATCH=<max batch> turns it on for A/B runs.
+#ifndef ORBPL_VAL_WAVE_BATCH
+#define ORBPL_VAL_WAVE_BATCH 0
+#endif
+constexpr int kValWaveBatch = ORBPL_VAL_WAVE_BATCH;
+__global__ void __launch_bounds__(256) k_lsd_validate_wave(LsdGeom g, LsdScratch sc) {
+  extern __shared__ int4 vw_rows[];   // 4 waves x g.sh rows
+  __shared__ Rect s_r[4][2];
+  __shared__ int s_next;
+  const int f = blockIdx.y, bxv = blockIdx.x, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nc = sc.ncand[f];
+  Frame F;
+  F.sw = g.sw;
+  F.sh = g.sh;
+  F.deg = sc.deg + (long long)f * lsd_deg_words(g.sw, g.sh);
+  F.dtw = lsd_deg_tw(g.sw);
+  F.q = nullptr;
+  F.used = nullptr;
+  F.usd = nullptr;
+  F.cs = nullptr;
+  F.tw = 0;
+  F.reg_l = nullptr;
+  F.regq_l = nullptr;
+  F.regd_l = nullptr;
+  F.reg_g = nullptr;
+  F.ring = nullptr;
+  F.rows = vw_rows + wv * g.sh;
+  F.rect0 = &s_r[wv][0];
+  F.rect1 = &s_r[wv][1];
+  F.row_cap = g.sh;   // rect_nfa keeps only rows inside the image
+  F.log_nt = g.log_nt;
+  F.lane = lane;
+  F.pf_cyc = 0;
+  F.pf_cnt = 0;
+  F.seed_cyc = 0;
+  if (threadIdx.x == 0) s_next = 4;
+  __syncthreads();
+  int k = wv;
+  while (true) {
+    const int c = bxv + k * (int)gridDim.x;
+    if (c >= nc) break;
+    const long long o = (long long)f * kLsdMaxCand + c;
+    const double* rv = sc.cand + o * 12;
+    Rect& rec = *F.rect0;
+    if (lane < 12) reinterpret_cast<double*>(&rec)[lane] = rv[lane];
+    __builtin_amdgcn_wave_barrier();
+    const double log_nfa = rect_improve(F, rec);
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+      const bool ok = log_nfa > 0;
+      sc.cand_ok[o] = ok;
+      if (ok) {
+        sc.cand_line[o * 4 + 0] = float((rec.x1 + 0.5) / 0.8);
+        sc.cand_line[o * 4 + 1] = float((rec.y1 + 0.5) / 0.8);
+        sc.cand_line[o * 4 + 2] = float((rec.x2 + 0.5) / 0.8);
+        sc.cand_line[o * 4 + 3] = float((rec.y2 + 0.5) / 0.8);
+      }
+      k = atomicAdd(&s_next, 1);
+    }
+    k = __shfl(k, 0, 64);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 __global__ void __launch_bounds__(64) k_lsd_compact(LsdScratch sc) {
   const int f = blockIdx.x, lane = threadIdx.x;
   const int nc = sc.ncand[f];
@@ -3720,6 +3795,15 @@ void launch_lgamma_table(double* t, int n, hipStream_t s) {
 }
 
 void launch_lsd_validate(const LsdGeom& g, const LsdScratch& sc, int batch, hipStream_t s) {
+  static const char* vw_env = getenv("ORBPL_VAL_WAVE_BATCH");
+  static const int wave_batch = vw_env ? atoi(vw_env) : kValWaveBatch;
+  if (batch <= wave_batch) {
+    const int nblk = std::max(8, std::min(64, 1024 / std::max(batch, 1)));
+    const size_t smem = (size_t)4 * g.sh * sizeof(int4);
+    hipLaunchKernelGGL(k_lsd_validate_wave, dim3(nblk, batch), dim3(256), smem, s, g, sc);
+    hipLaunchKernelGGL(k_lsd_compact, dim3(batch), dim3(64), 0, s, sc);
+    return;
+  }
   const int nblk = batch >= 1024 ? kValBlocksLarge : kValBlocksSmall;
   hipLaunchKernelGGL(k_lsd_validate, dim3(nblk, batch), dim3(256), 0, s, g, sc);
   hipLaunchKernelGGL(k_lsd_compact, dim3(batch), dim3(64), 0, s, sc);
