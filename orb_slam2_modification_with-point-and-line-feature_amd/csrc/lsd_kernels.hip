@@ -361,8 +361,13 @@ constexpr int kSortThreads = ORBPL_SORT_THREADS;   // k_lsd_sort's workgroup (A/
 #endif
 constexpr int kSortChunkG = ORBPL_SORT_CHUNK_G;
 static_assert(kSortChunkG % 64 == 0 && kSortChunkG >= kLsdSortChunk, "sort chunk");
+#ifndef ORBPL_SORT_MAP_G
+#define ORBPL_SORT_MAP_G 4096
+#endif
 // segments of one level whose table k_lsd_sort keeps in LDS (more: global)
 constexpr int kSortTab = 1024;
+// k_lsd_sort's chunk -> segment map capacity (chunks of one level)
+constexpr int kSortMapG = ORBPL_SORT_MAP_G;
 // batches up to this many frames sort with 1024-thread workgroups
 #ifndef ORBPL_SORT_WIDE_BATCH
 #define ORBPL_SORT_WIDE_BATCH 256
@@ -465,7 +470,9 @@ __device__ void heap_sort_seg(uint32_t* A, int len) {
 // segment table (first, last, pivot key, first chunk) is copied to LDS so that
 // a chunk finds its segment by a binary search in LDS instead of a chain of
 // dependent global loads (the global-memory kernel; up to kSortTab segments).
-template <int NT, int CH = kLsdSortChunk, bool TAB = false>
+// MAPCAP > 0: a chunk -> segment map (one LDS read per chunk instead of the
+// binary search) for levels of at most MAPCAP chunks.
+template <int NT, int CH = kLsdSortChunk, bool TAB = false, int MAPCAP = 0>
 //
 // Segments carry an upper bound of their keys in .w: the right part of a
 // partition (keys <= pivot) gets min(bound, pivot key). A segment whose bound
@@ -478,6 +485,7 @@ __device__ __forceinline__ void sort_core(const SortPtrs& P, int first0, int las
   __shared__ int s_w[(NT / 64)];
   __shared__ int s_nseg, s_next, s_nheap, s_nleaf;
   __shared__ int4 s_tab[TAB ? kSortTab : 1];
+  __shared__ uint16_t s_map[MAPCAP > 0 ? MAPCAP : 1];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   uint32_t* A = P.A;
   int* piv = P.si;
@@ -530,16 +538,29 @@ __device__ __forceinline__ void sort_core(const SortPtrs& P, int first0, int las
       return;
     }
     const bool tab = TAB && nseg <= kSortTab;
-    if (tab) {
+    const bool map = MAPCAP > 0 && nchunks <= MAPCAP && nseg <= 65536;
+    if (tab || map) {
       for (int s = t; s < nseg; s += NT) {
         const int4 sg = cur[s];
-        s_tab[s] = make_int4(sg.x, sg.y, piv[s], choff[s]);
+        const int c0 = choff[s];
+        if (tab) s_tab[s] = make_int4(sg.x, sg.y, piv[s], c0);
+        if (map) {
+          const int c1 = c0 + (sg.y - sg.x + CH - 1) / CH;
+          for (int c = c0; c < c1; c++) s_map[c] = (uint16_t)s;
+        }
       }
       __syncthreads();
     }
     // the segment of chunk ch: (first, last, pivot key, first chunk) and its index
     auto seg_of = [&](int ch, int& s) -> int4 {
       int lo = 0, hi = nseg;  // last segment with choff <= ch
+      if (map) {
+        lo = s_map[ch];
+        s = lo;
+        if (tab) return s_tab[lo];
+        const int4 sg = cur[lo];
+        return make_int4(sg.x, sg.y, piv[lo], choff[lo]);
+      }
       if (tab) {
         while (hi - lo > 1) {
           const int m = (lo + hi) >> 1;
@@ -759,6 +780,12 @@ constexpr int kLocalThreads = 256;
 constexpr int kLSeg = kSortLocalMax / 17 + 2;
 constexpr int kLChunk = kSortLocalMax / kLsdSortChunk + kLSeg + 2;
 constexpr int kLLeaf = kSortLocalMax / 2 + 2;
+// the local sort's chunk -> segment map (ORBPL_SORT_MAP=0: binary search; the
+// map's 264 B fit the 4-blocks-per-CU LDS budget)
+#ifndef ORBPL_SORT_MAP
+#define ORBPL_SORT_MAP 1
+#endif
+constexpr int kLocalMap = ORBPL_SORT_MAP ? kLChunk : 0;
 constexpr int kSortLocalBlocks = 4;
 
 __global__ void __launch_bounds__(kLocalThreads, 4) k_lsd_sort_local(LsdGeom g, LsdScratch sc) {
@@ -803,7 +830,7 @@ __global__ void __launch_bounds__(kLocalThreads, 4) k_lsd_sort_local(LsdGeom g, 
     for (int u = 0; u < kLU; u++)
       if (t + u * kLocalThreads < m) sA[t + u * kLocalThreads] = lv[u];
     __syncthreads();
-    sort_core<kLocalThreads>(L, 0, m, sg.z, sg.w);
+    sort_core<kLocalThreads, kLsdSortChunk, false, kLocalMap>(L, 0, m, sg.z, sg.w);
     for (int i = t; i < m; i += kLocalThreads) A[sg.x + i] = sA[i];
     __syncthreads();
   }
@@ -865,7 +892,8 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : ORBPL_SORT_MINW) k_lsd_so
     sc.sort_kt[f] = kt;
     sc.sort_nge[f] = s_nge;
   }
-  sort_core<NT, kSortChunkG, true>(P, 0, g.n, g.n > 16 ? 2 * (31 - __clz(g.n)) : 0, 1023);
+  sort_core<NT, kSortChunkG, true, kSortMapG>(P, 0, g.n, g.n > 16 ? 2 * (31 - __clz(g.n)) : 0,
+                                              1023);
 }
 
 // test hook: sort caller-provided keys (frame slot 0)
