@@ -2582,13 +2582,15 @@ __device__ __forceinline__ void group_fit(CoopScratch& S, int lane, bool fitter,
                                           double reg_angle, uint4* fbuf, int bufid,
                                           const Frame& F, uint64_t* sd, double prec, double p,
                                           uint32_t myval1, int& status, Rect& rec, int& off,
-                                          int& len, int& touched) {
+                                          int& len, int& touched, FitProf& fp) {
   uint4* bp = fbuf + (long long)bufid * kLaneCap;
   double cx, cy, cs;
+  fp.start();
   group_centroid(S, lane, fitter, bp, n, F.q, F.sw, cx, cy, cs);
   wg_fence();
   __builtin_amdgcn_wave_barrier();
   group_rect_tail(S, lane, fitter, bp, n, cx, cy, cs, reg_angle, prec, p, rec);
+  fp.lap(0);
   bool refine = false;
   if (fitter) {
     const double density = double(n) / (dist(rec.x1, rec.y1, rec.x2, rec.y2) * rec.width);
@@ -2599,6 +2601,7 @@ __device__ __forceinline__ void group_fit(CoopScratch& S, int lane, bool fitter,
     refine = density < 0.7;
   }
   const double tau = group_tau(S, lane, refine, bp, n, rec);
+  fp.lap(1);
   // refine's second grow, one lane per region
   const LaneBuf buf{bp};
   int n1 = 0, x0 = 0, y0 = 0;
@@ -2640,11 +2643,13 @@ __device__ __forceinline__ void group_fit(CoopScratch& S, int lane, bool fitter,
     }
   }
   __builtin_amdgcn_wave_barrier();
+  fp.lap(2);
   uint4* gp = bp + n;   // the second region's list
   group_centroid(S, lane, refine, gp, n1, F.q, F.sw, cx, cy, cs);
   wg_fence();
   __builtin_amdgcn_wave_barrier();
   group_rect_tail(S, lane, refine, gp, n1, cx, cy, cs, ra2, prec, p, rec);
+  fp.lap(3);
   bool red = false;
   double radSq = 0;
   if (refine) {
@@ -2696,6 +2701,7 @@ __device__ __forceinline__ void group_fit(CoopScratch& S, int lane, bool fitter,
       if (density >= 0.7) red = false;
     }
   }
+  fp.lap(4);
 }
 
 // The round's fits (lane_rect + lane_refine of every lane with n >=
@@ -3010,10 +3016,14 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
         len = n;
         touched = n;
       }
-      if constexpr (ORBPL_COOP_FIT == 2)
+      if constexpr (ORBPL_COOP_FIT == 2) {
+        FitProf fp;
         group_fit(s_coop[wv], lane, mine && n >= g.min_reg_size, n, reg_angle, fbuf, bufid, F,
-                  sd, prec, p, myval1, status, rec, off, len, touched);
-      else
+                  sd, prec, p, myval1, status, rec, off, len, touched, fp);
+#ifdef ORBPL_FIT_PROF
+        for (int k = 0; k < 5; k++) fpr[k] = fp.d[k];
+#endif
+      } else
         coop_fit(s_coop[wv], lane, mine && n >= g.min_reg_size, n, reg_angle, fbuf, bufid, F,
                  sd, prec, p, myval1, status, rec, off, len, touched);
     } else if (t < ncand && !keep) {
