@@ -2808,6 +2808,13 @@ __device__ __forceinline__ void coop_fit(CoopScratch& S, int lane, bool fitter, 
 #ifndef ORBPL_SPEC_WIN
 #define ORBPL_SPEC_WIN 64
 #endif
+// ORBPL_SCAN2: the one-wave seed scan reads two list windows per iteration
+// (A/B build override). Measured (tools/gpu_r04_aa.sh, bit-exact): the scans
+// 3.3M -> 3.1M cycles per frame at batch 1 (~0.1 ms), but 1536 frames 106.5 ->
+// 108.9 ms (the 128-VGPR instance spills more), so off
+#ifndef ORBPL_SCAN2
+#define ORBPL_SCAN2 0
+#endif
 #ifndef ORBPL_SPEC_KEEP
 #define ORBPL_SPEC_KEEP 1
 #endif
@@ -2908,6 +2915,59 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
     // ---- the next SL defined, NOTUSED seeds in list order (after the
     // carried ones) ----
     int ncand = ncarry, scan = pos, next_pos = nlist;
+#if ORBPL_SCAN2
+    // one wave: two 64-entry windows per iteration, both windows' list and
+    // pixel-word loads in flight together (the stamps do not change during
+    // the scan, so window b read early equals window b read next iteration)
+    if constexpr (W == 1) {
+      while (ncand < WIN && scan < nlist) {
+        const int ia = scan + t, ib = scan + 64 + t;
+        const bool va = ia < nlist, vb = ib < nlist;
+        const uint32_t ea = va ? A[ia] : 0u, eb = vb ? A[ib] : 0u;
+        const int idxa = (int)(ea & 0x3FFFFFu), idxb = (int)(eb & 0x3FFFFFu);
+        const int pya = idxa / w1, pxa = idxa - pya * w1;
+        const int pyb = idxb / w1, pxb = idxb - pyb * w1;
+        uint64_t wa = 0, wb = 0;
+        if (va) wa = ld_sd(sd + lsd_sd_index(pxa, pya, F.tw));
+        if (vb) wb = ld_sd(sd + lsd_sd_index(pxb, pyb, F.tw));
+        const bool ca = va && __uint_as_float((uint32_t)wa) >= 0.f && (uint32_t)(wa >> 32) != 0u;
+        const bool cb = vb && __uint_as_float((uint32_t)wb) >= 0.f && (uint32_t)(wb >> 32) != 0u;
+        {
+          const unsigned long long m = __ballot(ca);
+          const int before = __popcll(m & lt_mask), cnt = __popcll(m);
+          if (ca && ncand + before < WIN) {
+            s_pt[ncand + before] = (uint32_t)pxa | ((uint32_t)pya << 16);
+            s_pos[ncand + before] = ia;
+          }
+          if (ncand + cnt >= WIN) {
+            const unsigned long long mm = __ballot(ca && before == WIN - ncand - 1);
+            next_pos = scan + __ffsll((long long)mm);
+            ncand = WIN;
+            break;
+          }
+          ncand += cnt;
+          scan += 64;
+        }
+        if (scan >= nlist) break;
+        {
+          const unsigned long long m = __ballot(cb);
+          const int before = __popcll(m & lt_mask), cnt = __popcll(m);
+          if (cb && ncand + before < WIN) {
+            s_pt[ncand + before] = (uint32_t)pxb | ((uint32_t)pyb << 16);
+            s_pos[ncand + before] = ib;
+          }
+          if (ncand + cnt >= WIN) {
+            const unsigned long long mm = __ballot(cb && before == WIN - ncand - 1);
+            next_pos = scan + __ffsll((long long)mm);
+            ncand = WIN;
+            break;
+          }
+          ncand += cnt;
+          scan += 64;
+        }
+      }
+    } else
+#endif
     while (ncand < WIN && scan < nlist) {
       const int i = scan + t;
       bool c = false;
