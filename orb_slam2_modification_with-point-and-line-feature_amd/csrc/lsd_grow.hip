@@ -1901,13 +1901,16 @@ __global__ void __launch_bounds__(64) k_lsd_grow(LsdGeom g, LsdScratch sc) {
 #endif
 constexpr int kSpecSmallBatch = ORBPL_SPEC_SMALL_BATCH;
 // ORBPL_SPEC_MINW: waves per SIMD the one-wave-per-frame variant's register
-// budget must allow. 4 (128 VGPRs, a few spills) although the batches that
-// use it hold 3 frames per SIMD: the free quarter of the register file lets
-// the concurrent ORB extraction / tracking waves in beside the seed loop.
-// LSD alone 222.9 -> 235 ms per 3072 frames, but the pipelined lines
-// workload 10.5k -> 11.4k frames/s (A/B on one box, tools/ab_lines_lib.sh).
+// budget must allow. Round 2 chose 4 (128 VGPRs) although the batches that
+// use it hold 3 frames per SIMD, so that the concurrent ORB extraction /
+// tracking waves fit beside the seed loop (LSD alone 222.9 -> 235 ms per 3072
+// frames, lines workload 10.5k -> 11.4k frames/s then). With the round-4 seed
+// loop the 128-VGPR build spills 77 registers; 3 (168 VGPRs) measured (two
+// rounds each, tools/ab_lines_lib.sh, tools/ab_kitti_lib.sh): LSD at 3072
+// frames 167.0 -> 156.6 ms, the lines leg's seed stage 86-90 -> 74 ms, the
+// lines leg equal (15.7-16.0k vs 15.9k), the stereo leg 5.4-5.8k -> 5.85-5.89k
 #ifndef ORBPL_SPEC_MINW
-#define ORBPL_SPEC_MINW 4
+#define ORBPL_SPEC_MINW 3
 #endif
 // ORBPL_SPEC_KEEP (one wave per frame): a round ends at its first seed whose
 // region met an earlier seed's claim; the later seeds of the window whose
