@@ -1535,6 +1535,154 @@ __global__ void __launch_bounds__(256, ORBPL_OD_MINW) k_orient_desc(const uint8_
     for (int k = 0; k < 6; k++) g_od_prof[k] = dt[k];
 }
 
+// Two keypoints per wave (ORBPL_OD_PAIR): each 32-lane half runs the kernel
+// above for its own slot - 9 IC and 12 BRIEF dword loads per lane, the
+// moments reduced within the half, 8 rounds of 32 tests whose ballot halves
+// are the two descriptors' dwords. The per-keypoint uniform work (level and
+// offset search, atan2, the correctly rounded cos / sin, address math) is
+// issued once for two keypoints. Same operations per keypoint: bit-exact.
+// Measured (tools/gpu_r04_ab.sh, 10 ORB tests green; isolated, 1024 frames):
+// 1.465-1.469 -> 1.403-1.409 ms (the kernel stays bound by its patch gathers).
+#ifndef ORBPL_OD_PAIR
+#define ORBPL_OD_PAIR 1
+#endif
+constexpr int kIcLoads2 = (kIcDw + 31) / 32;         // 9
+constexpr int kBriefLoads2 = (kBriefDw + 31) / 32;   // 12
+__global__ void __launch_bounds__(256, ORBPL_OD_MINW) k_orient_desc2(const uint8_t* __restrict__ pyr,
+                                                      const uint8_t* __restrict__ blur,
+                                                      const OrbGeom* __restrict__ g,
+                                                      const uint32_t* __restrict__ kp_list,
+                                                      const int* __restrict__ kp_count,
+                                                      orbpl_keypoint_dev* __restrict__ out_kps,
+                                                      uint8_t* __restrict__ out_desc,
+                                                      int kp_pitch, int* __restrict__ out_n) {
+  __shared__ uint32_t s_patch[8][kBriefDw];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int half = lane >> 5, l32 = lane & 31;
+  int bx, f;
+  xcd_block(&bx, &f);
+  const int slot = bx * 8 + wave * 2 + half;
+  const int nlev = g->nlevels;
+  bool act = slot < g->kp_cap_total;
+  int level = 0;
+  if (act)
+    while (level + 1 < nlev && slot >= g->lv[level + 1].kp_base) level++;
+  const LevelGeom& L = g->lv[level];
+  const int idx = slot - L.kp_base;
+  const int* cnts = kp_count + (long long)f * nlev;
+  int offset = 0, total = 0, mine = 0;
+  for (int l = 0; l < nlev; l++) {
+    const int c = cnts[l];
+    if (l < level) offset += c;
+    if (l == level) mine = c;
+    total += c;
+  }
+  if (slot == 0 && l32 == 0) out_n[f] = total < kp_pitch ? total : kp_pitch;
+  act = act && idx < mine && offset + idx < kp_pitch;
+  if (!__any(act)) return;
+  const int opos = offset + idx;
+  const uint32_t c = act ? kp_list[(long long)f * g->kp_cap_total + slot] : 0u;
+  const int kx = act ? cand_x(c) + kMinBorder : kIcR + kBriefR,
+            ky = act ? cand_y(c) + kMinBorder : kIcR + kBriefR;
+  // IC_Angle patch: rows ky-15 .. ky+15 as 9 aligned dwords each
+  const uint8_t* irow0 = pyr + (long long)f * g->pyr_bytes + content_off(L, kx - kIcR, ky - kIcR);
+  const int io = (int)(reinterpret_cast<uintptr_t>(irow0) & 3);
+  const uint32_t* irow = reinterpret_cast<const uint32_t*>(irow0 - io);
+  const int ipdw = L.pitch >> 2;
+  uint32_t iv[kIcLoads2];
+#pragma unroll
+  for (int j = 0; j < kIcLoads2; j++) {
+    const int i = l32 + 32 * j;
+    const int r = i / kIcRowDw, q = i - r * kIcRowDw;
+    iv[j] = (act && i < kIcDw) ? irow[r * ipdw + q] : 0u;
+  }
+  const int bx0 = kx - kBriefR;
+  const uint32_t* prow = reinterpret_cast<const uint32_t*>(
+      blur + (long long)f * g->blur_bytes + L.boff + (long long)(ky - kBriefR) * L.bpitch +
+      (bx0 & ~3));
+  const int pdw = L.bpitch >> 2;
+  uint32_t pv[kBriefLoads2];
+#pragma unroll
+  for (int j = 0; j < kBriefLoads2; j++) {
+    const int i = l32 + 32 * j;
+    const int r = i / kBriefRowDw, q = i - r * kBriefRowDw;
+    pv[j] = (act && i < kBriefDw) ? prow[r * pdw + q] : 0u;
+  }
+  int m01 = 0, m10 = 0;
+#pragma unroll
+  for (int j = 0; j < kIcLoads2; j++) {
+    const int i = l32 + 32 * j;
+    const int r = i / kIcRowDw, q = i - r * kIcRowDw;
+    const int v = r - kIcR;
+    const int um = i < kIcDw ? g->umax[v < 0 ? -v : v] : -1;
+    const int u0 = 4 * q - io - kIcR;
+    int s0 = 0, s1 = 0;
+#pragma unroll
+    for (int bq = 0; bq < 4; bq++) {
+      const int u = u0 + bq;
+      const int px = (int)((iv[j] >> (8 * bq)) & 0xFFu);
+      const int w = (u <= um && -u <= um) ? px : 0;
+      s0 += w;
+      s1 += u * w;
+    }
+    m10 += s1;
+    m01 += v * s0;
+  }
+#pragma unroll
+  for (int o = 16; o >= 1; o >>= 1) {   // within the half
+    m10 += __shfl_xor(m10, o, 64);
+    m01 += __shfl_xor(m01, o, 64);
+  }
+  const float angle = fast_atan2_deg((float)m01, (float)m10);
+  const float factorPI = (float)(3.14159265358979323846 / 180.f);
+  float a, b;
+  cr_cos_sin(angle * factorPI, &a, &b);
+  uint32_t* patch = s_patch[wave * 2 + half];
+#pragma unroll
+  for (int j = 0; j < kBriefLoads2; j++) {
+    const int i = l32 + 32 * j;
+    if (i < kBriefDw) patch[i] = pv[j];
+  }
+  __builtin_amdgcn_wave_barrier();
+  const uint8_t* bimg = reinterpret_cast<const uint8_t*>(patch) + kBriefR * 4 * kBriefRowDw +
+                        (bx0 & 3) + kBriefR;
+  const int step = 4 * kBriefRowDw;
+  uint32_t words[8];
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    const int tst = r * 32 + l32;
+    const int* p = &c_pattern[4 * tst];
+    const float x1 = (float)p[0], y1 = (float)p[1], x2 = (float)p[2], y2 = (float)p[3];
+    const int v1 = bimg[cv_round(x1 * b + y1 * a) * step + cv_round(x1 * a - y1 * b)];
+    const int v2 = bimg[cv_round(x2 * b + y2 * a) * step + cv_round(x2 * a - y2 * b)];
+    words[r] = (uint32_t)(__ballot(v1 < v2) >> (32 * half));
+  }
+  if (!act) return;
+  uint8_t* d = out_desc + ((long long)f * kp_pitch + opos) * 32;
+  if (l32 < 8) {
+    uint32_t w = words[0];
+#pragma unroll
+    for (int r = 1; r < 8; r++) w = l32 == r ? words[r] : w;
+    reinterpret_cast<uint32_t*>(d)[l32] = w;
+  }
+  if (l32 == 0) {
+    orbpl_keypoint_dev kp;
+    float sx = (float)kx, sy = (float)ky;
+    if (level != 0) {
+      sx = sx * L.scale;
+      sy = sy * L.scale;
+    }
+    kp.x = sx;
+    kp.y = sy;
+    kp.size = (float)L.scaled_patch;
+    kp.angle = angle;
+    kp.response = (float)cand_s(c);
+    kp.octave = level;
+    kp.class_id = -1;
+    out_kps[(long long)f * kp_pitch + opos] = kp;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Host-side launchers (called by the runtime in orbpl_runtime.cpp)
 // ---------------------------------------------------------------------------
@@ -1598,8 +1746,15 @@ void launch_orient_desc(const OrbGeom& hg, const OrbGeom* dg, const uint8_t* pyr
                         const uint8_t* blur, const uint32_t* kp_list, const int* kp_count,
                         orbpl_keypoint_dev* out_kps, uint8_t* out_desc, int kp_pitch, int* out_n,
                         int batch, hipStream_t s) {
-  hipLaunchKernelGGL(k_orient_desc, dim3((hg.kp_cap_total + 3) / 4, batch), dim3(256), 0, s, pyr,
-                     blur, dg, kp_list, kp_count, out_kps, out_desc, kp_pitch, out_n);
+  static const char* pe = getenv("ORBPL_OD_PAIR");
+  // the phase-stamp profile (ORBPL_OCT_PROFILE) lives in the one-per-wave kernel
+  static const bool pair = (pe ? atoi(pe) != 0 : ORBPL_OD_PAIR) && !getenv("ORBPL_OCT_PROFILE");
+  if (pair)
+    hipLaunchKernelGGL(k_orient_desc2, dim3((hg.kp_cap_total + 7) / 8, batch), dim3(256), 0, s,
+                       pyr, blur, dg, kp_list, kp_count, out_kps, out_desc, kp_pitch, out_n);
+  else
+    hipLaunchKernelGGL(k_orient_desc, dim3((hg.kp_cap_total + 3) / 4, batch), dim3(256), 0, s, pyr,
+                       blur, dg, kp_list, kp_count, out_kps, out_desc, kp_pitch, out_n);
 }
 
 }  // namespace orbpl
