@@ -25,7 +25,9 @@ ROOT = Path(__file__).resolve().parents[1]
 def short(name):
     n = name.split("(")[0]
     n = n.replace("void ", "").replace("orbpl::", "")
-    return n.split("<")[0]
+    n = n.split("<")[0]
+    # the paired variant of the orientation / descriptor kernel is the same stage
+    return "k_orient_desc" if n == "k_orient_desc2" else n
 
 
 ORB_KERNELS = ("k_pyramid", "k_fast_cells", "k_octree", "k_orient_desc")
