@@ -3690,7 +3690,10 @@ __global__ void __launch_bounds__(256, 1) k_lsd_spec_sparse(LsdGeom g, LsdScratc
 // workgroups per frame: 8 for small batches (one frame's rectangles spread
 // wide), 2 from 1024 frames on (each lane then takes ~3 rectangles from the
 // counter: 27.4 -> 24.2 ms per 3072 frames)
-constexpr int kValBlocksSmall = 8, kValBlocksLarge = 2;
+#ifndef ORBPL_VAL_BLOCKS_LARGE
+#define ORBPL_VAL_BLOCKS_LARGE 2
+#endif
+constexpr int kValBlocksSmall = 8, kValBlocksLarge = ORBPL_VAL_BLOCKS_LARGE;
 
 #ifndef ORBPL_VAL_MINW
 // 6 waves/SIMD (80 VGPRs, the best rectangle in LDS): the same time as 8 (64
