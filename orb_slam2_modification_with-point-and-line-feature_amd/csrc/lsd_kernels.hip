@@ -896,11 +896,13 @@ __global__ void __launch_bounds__(NT, NT >= 1024 ? 4 : ORBPL_SORT_MINW) k_lsd_so
                                               1023);
 }
 
-// test hook: sort caller-provided keys (frame slot 0)
-__global__ void __launch_bounds__(kSortThreads) k_lsd_sort_keys(LsdGeom g, LsdScratch sc,
-                                                                const int* __restrict__ keys) {
+// test hook: sort caller-provided keys (frame slot 0) with the configuration
+// a one-frame batch uses (NT = 1024 threads, LDS segment table and chunk map)
+template <int NT>
+__global__ void __launch_bounds__(NT) k_lsd_sort_keys(LsdGeom g, LsdScratch sc,
+                                                      const int* __restrict__ keys) {
   const SortPtrs P = sort_ptrs(g, sc, 0);
-  for (int i = threadIdx.x; i < g.n; i += kSortThreads)
+  for (int i = threadIdx.x; i < g.n; i += NT)
     P.A[i] = ((uint32_t)keys[i] << 22) | (uint32_t)i;
   if (threadIdx.x == 0) {
     *P.nlocal = 0;
@@ -908,8 +910,8 @@ __global__ void __launch_bounds__(kSortThreads) k_lsd_sort_keys(LsdGeom g, LsdSc
     sc.sort_nge[0] = g.n;
   }
   __syncthreads();
-  sort_core<kSortThreads, kSortChunkG, true>(P, 0, g.n, g.n > 16 ? 2 * (31 - __clz(g.n)) : 0,
-                                            1 << 30);
+  sort_core<NT, kSortChunkG, true, kSortMapG>(P, 0, g.n, g.n > 16 ? 2 * (31 - __clz(g.n)) : 0,
+                                              1 << 30);
 }
 
 void launch_lsd_blur(const LsdGeom& g, const uint8_t* img, int stride, long long frame_pitch,
@@ -965,7 +967,11 @@ void launch_lsd_sort_keys(int n, const int* keys, const LsdScratch& sc, hipStrea
   g.seg_cap = n / 17 + 2;
   g.chunk_cap = n / kLsdSortChunk + g.seg_cap + 2;
   g.leaf_cap = n / 2 + 2;
-  hipLaunchKernelGGL(k_lsd_sort_keys, dim3(1), dim3(kSortThreads), 0, s, g, sc, keys);
+  if (kSortThreads < 1024 && 1 <= kSortWideBatch)
+    hipLaunchKernelGGL(k_lsd_sort_keys<1024>, dim3(1), dim3(1024), 0, s, g, sc, keys);
+  else
+    hipLaunchKernelGGL(k_lsd_sort_keys<kSortThreads>, dim3(1), dim3(kSortThreads), 0, s, g, sc,
+                       keys);
   hipLaunchKernelGGL(k_lsd_sort_local, dim3(kSortLocalBlocks, 1), dim3(kLocalThreads), 0, s, g,
                      sc);
 }
