@@ -967,7 +967,7 @@ def dropin_frame_latency(gray, depth, L, workload, reps=30):
     fh, fw = gray.shape[1:]
     with tempfile.TemporaryDirectory() as td:
         voc = Path(td) / "voc.txt"
-        voc.write_text("10 1 0 0\n")   # not read by the timing mode
+        voc.write_text("10 1 0 0\n")   # never opened: the timing mode loads no vocabulary
         inp = Path(td) / "in.bin"
         with open(inp, "wb") as f:
             f.write(struct.pack("<2i", fw, fh))

@@ -64,6 +64,15 @@ typedef struct orbpl_orb_params {
 const char* orbpl_last_error(void);
 /* Number of visible HIP devices. */
 int orbpl_device_count(int* n);
+/* Hardware queues as recorded when the library was loaded (no HIP call):
+ * queues = GPU_MAX_HW_QUEUES the HIP runtime runs with; runtime_started = 1
+ * when the runtime was already up (another HIP user came first, so the
+ * library changed nothing); set_by_library = 1 when the library filled in
+ * the variable (it was unset, or ORBPL_HW_QUEUES asked). lsd_split_1024 = 1
+ * when a 1024-stream lines tracker would split its LSD batch (needs >= 8
+ * queues; ORBPL_LSD_SPLIT=0/1 overrides). Any pointer may be NULL. */
+int orbpl_hw_queue_state(int* queues, int* runtime_started, int* set_by_library,
+                         int* lsd_split_1024);
 /* Library build tag ("orbpl gfx950 r3"). r3: orbpl_tracker_timings writes 11
  * floats per step, orbpl_tracker_stereo_timings 4 (r1: 9 and 2); size the
  * buffers from orbpl_tracker_timing_counts. */
@@ -249,8 +258,10 @@ int orbpl_stereo_matches(const orbpl_camera* cam, orbx_ctx* left, orbx_ctx* righ
  * Tracking::SearchLocalPoints pieces (TrackLocalMap)
  * ---------------------------------------------------------------------- */
 /* Frame::IsInFrustum(MapPoint*, view_cos_limit) (Frame.cc:345-401) for n map
- * points (world xyz, normal, GetMin/MaxDistanceInvariance) with
- * MapPoint::PredictScale (MapPoint.cc:416-431); outputs the mTrack* fields:
+ * points (world xyz, normal, and the raw mfMinDistance / mfMaxDistance: the
+ * range test applies GetMin/MaxDistanceInvariance's 0.8f / 1.2f, MapPoint.cc:
+ * 387-397, and PredictScale's ratio is mfMaxDistance / dist, MapPoint.cc:
+ * 416-431); outputs the mTrack* fields:
  * in_view (mbTrackInView), proj_x/y, proj_xr (u - bf/z), level
  * (mnTrackScaleLevel, -1 when not in view), view_cos (mTrackViewCos).
  * scale_factor = ORBextractor scale factor (mfLogScaleFactor = logf of it). */

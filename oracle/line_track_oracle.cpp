@@ -710,8 +710,8 @@ static void push_local_kf(LVO* v, LStream& S, const float* Ow,
     const float dist = (float)nd;
     const float maxd = dist * v->scale[ku[i].octave];
     const float mind = maxd / v->scale[nlev - 1];
-    m.dmax[i] = 1.2f * maxd;
-    m.dmin[i] = 0.8f * mind;
+    m.dmax[i] = maxd;   // mfMaxDistance / mfMinDistance (the in-frustum test
+    m.dmin[i] = mind;   // applies GetMax/MinDistanceInvariance's 1.2f / 0.8f)
   }
   m.nl = (int)S.has_ml.size();
   m.lxyz = S.lxyz;

@@ -845,8 +845,8 @@ static bool track_local_map(MapVO* v, Stream& S, Frame& F, LocalOut& o) {
     const MapPoint& P = S.mps[lp[j]];
     std::memcpy(&x[3 * j], P.pos, 12);
     std::memcpy(&nr[3 * j], P.normal, 12);
-    dmn[j] = 0.8f * P.min_dist;
-    dmx[j] = 1.2f * P.max_dist;
+    dmn[j] = P.min_dist;   // raw mfMinDistance / mfMaxDistance: the in-frustum
+    dmx[j] = P.max_dist;   // test applies 0.8f / 1.2f, PredictScale the raw max
     std::memcpy(&ld[32 * (size_t)j], P.desc, 32);
     mpn[j] = P.nobs;
   }

@@ -1011,13 +1011,15 @@ int oracle_frame_is_in_frustum(const orbpl_camera* cam, float log_scale_factor, 
     const float PO[3] = {xyz[3 * i] - Ow[0], xyz[3 * i + 1] - Ow[1], xyz[3 * i + 2] - Ow[2]};
     const float dist = (float)std::sqrt((double)PO[0] * PO[0] + (double)PO[1] * PO[1] +
                                         (double)PO[2] * PO[2]);
-    if (dist < min_dist[i] || dist > max_dist[i]) continue;
+    // GetMin/MaxDistanceInvariance (MapPoint.cc:387-397) of the raw
+    // mfMinDistance / mfMaxDistance the arrays hold
+    if (dist < 0.8f * min_dist[i] || dist > 1.2f * max_dist[i]) continue;
     const float* Pn = normal + 3 * i;
     double dot = 0;
     for (int k = 0; k < 3; k++) dot += (double)(float)(PO[k] * Pn[k]);
     const float vc = (float)(dot / (double)dist);
     if (vc < view_cos_limit) continue;
-    const float ratio = max_dist[i] / dist;
+    const float ratio = max_dist[i] / dist;   // MapPoint::PredictScale: mfMaxDistance / dist (MapPoint.cc:421)
     int ns = (int)std::ceil((float)pmath::log_((double)ratio) / log_scale_factor);
     if (ns < 0) ns = 0;
     else if (ns >= nlevels) ns = nlevels - 1;

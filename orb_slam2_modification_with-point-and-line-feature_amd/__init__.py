@@ -568,7 +568,10 @@ def stereo_matches(camera, left, right, kl, dl, kr, dr, frame=0):
 
 def frame_is_in_frustum(camera, scale_factor, nlevels, Tcw, mps, view_cos_limit=0.5):
     """Frame::IsInFrustum(MapPoint*, limit) for the map points in ``mps`` (dict:
-    xyz, normal, min_dist, max_dist). Returns the mTrack* fields as a dict."""
+    xyz, normal, min_dist, max_dist = the raw mfMinDistance / mfMaxDistance; the
+    library applies GetMin/MaxDistanceInvariance's 0.8f / 1.2f to the range test
+    and PredictScale's mfMaxDistance / dist, MapPoint.cc:387-431). Returns the
+    mTrack* fields as a dict."""
     n = len(mps["xyz"])
     keep = [_c(Tcw, np.float32), _c(mps["xyz"], np.float32), _c(mps["normal"], np.float32),
             _c(mps["min_dist"], np.float32), _c(mps["max_dist"], np.float32)]

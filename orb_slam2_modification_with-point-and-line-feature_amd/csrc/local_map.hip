@@ -243,8 +243,8 @@ __global__ void __launch_bounds__(256) k_lm_push(TrackConsts c, LocalMapArgs a) 
       a.r_xyz[(rb + i) * 3 + q] = X[q];
       a.r_nrm[(rb + i) * 3 + q] = PO[q] * inv;
     }
-    a.r_dmax[rb + i] = 1.2f * maxd;
-    a.r_dmin[rb + i] = 0.8f * mind;
+    a.r_dmax[rb + i] = maxd;   // mfMaxDistance / mfMinDistance: k_in_frustum applies
+    a.r_dmin[rb + i] = mind;   // the 1.2f / 0.8f of GetMax/MinDistanceInvariance
   }
   if (t == 0) a.r_n[s * a.K + a.push_slot] = n;
   if (a.lines) {

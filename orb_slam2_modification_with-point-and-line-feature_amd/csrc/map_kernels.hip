@@ -924,8 +924,8 @@ __global__ void __launch_bounds__(kT) k_map_local(MapArgs a) {
         const float2 D = a.mp_dist[g];
         a.l_xyz[d * 3] = X.x; a.l_xyz[d * 3 + 1] = X.y; a.l_xyz[d * 3 + 2] = X.z;
         a.l_nrm[d * 3] = Nv.x; a.l_nrm[d * 3 + 1] = Nv.y; a.l_nrm[d * 3 + 2] = Nv.z;
-        a.l_dmin[d] = 0.8f * D.x;   // GetMinDistanceInvariance
-        a.l_dmax[d] = 1.2f * D.y;   // GetMaxDistanceInvariance
+        a.l_dmin[d] = D.x;   // mfMinDistance, mfMaxDistance: k_in_frustum applies
+        a.l_dmax[d] = D.y;   // GetMin/MaxDistanceInvariance's 0.8f / 1.2f itself
         copy32(a.l_ldesc_pts + d * 32, a.mp_desc + g * 32);
         a.l_id[d] = p;
       }

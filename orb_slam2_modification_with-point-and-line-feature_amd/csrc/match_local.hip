@@ -71,14 +71,16 @@ __global__ void __launch_bounds__(256) k_in_frustum(TrackConsts c, float log_sca
   // cv::norm (P16): double squares, one rounding
   const float dist =
       (float)sqrt((double)PO[0] * PO[0] + (double)PO[1] * PO[1] + (double)PO[2] * PO[2]);
-  if (dist < a.min_dist[i] || dist > a.max_dist[i]) return;
+  // GetMin/MaxDistanceInvariance (MapPoint.cc:387-397): 0.8f / 1.2f times the
+  // raw mfMinDistance / mfMaxDistance the arrays hold
+  if (dist < 0.8f * a.min_dist[i] || dist > 1.2f * a.max_dist[i]) return;
   // Mat::dot (P16): float products, double sum
   double dot = 0;
 #pragma unroll
   for (int k = 0; k < 3; k++) dot += (double)(float)(PO[k] * a.normal[3 * i + k]);
   const float vc = (float)(dot / (double)dist);
   if (vc < a.view_cos_limit) return;
-  const float ratio = a.max_dist[i] / dist;
+  const float ratio = a.max_dist[i] / dist;   // PredictScale: mfMaxDistance / dist (MapPoint.cc:421)
   int ns = (int)ceilf((float)lsdm::log_((double)ratio) / log_scale);  // P15
   if (ns < 0) ns = 0;
   else if (ns >= c.nlevels) ns = c.nlevels - 1;

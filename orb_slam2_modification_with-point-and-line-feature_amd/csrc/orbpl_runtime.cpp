@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <unistd.h>
 #include <mutex>
 #include <map>
 #include <set>
@@ -20,25 +21,59 @@
 namespace orbpl {
 
 // Hardware queues: the HIP runtime maps a process's streams onto
-// GPU_MAX_HW_QUEUES queues (4 by default, read when the runtime starts); a
-// tracker drives up to eight streams, which then share queues and serialise
-// (DESIGN.md §4 Tracker). At library load, before the runtime starts in a
-// process whose first HIP user is this library (the reference's process with
-// the drop-ins, the bench), the variable is raised to 16 unless it already
-// asks for at least 8; ORBPL_HW_QUEUES=<n> chooses n instead, 0 leaves the
-// process's setting alone. A runtime another library started earlier keeps
-// its queues: the split switches below then read the raised value, which
-// ORBPL_LSD_SPLIT=0 / ORBPL_ORB_SPLIT=0 override.
-__attribute__((constructor)) static void raise_hw_queues() {
-  const char* want = getenv("ORBPL_HW_QUEUES");
-  const int n = want ? atoi(want) : 16;
-  if (n <= 0) return;
-  const char* q = getenv("GPU_MAX_HW_QUEUES");
-  if (q && atoi(q) >= (want ? n : 8)) return;
-  char buf[16];
-  snprintf(buf, sizeof(buf), "%d", n > 32 ? 32 : n);
-  setenv("GPU_MAX_HW_QUEUES", buf, 1);
+// GPU_MAX_HW_QUEUES queues (4 by default, read once, when the runtime starts);
+// a tracker drives up to eight streams, which then share queues and serialise
+// (DESIGN.md §4 Tracker). At library load the constructor below records what
+// the runtime will really use and changes the environment only where that is
+// safe and wanted:
+//   * the runtime already started (the process holds /dev/kfd open: torch or
+//     another HIP library initialised first): nothing is changed, the queue
+//     count is the variable's value then (4 when unset);
+//   * ORBPL_HW_QUEUES=<n> (n > 0): the caller asks for n queues - set;
+//   * GPU_MAX_HW_QUEUES unset: filled in with 16 (a process whose first HIP
+//     user is this library: the reference's process with the drop-ins);
+//   * GPU_MAX_HW_QUEUES set by the user (the GPU box's 4, say): left alone.
+// The split switches (track_runtime.cpp) read the recorded count, never the
+// environment. ORBPL_ASSUME_RUNTIME_STARTED=1 makes the constructor treat the
+// runtime as started (the CPU test of the first case has no /dev/kfd).
+int g_hw_queues = 4;            // queues the runtime runs (or will run) with
+int g_runtime_started = 0;      // the runtime was up before this library loaded
+int g_queues_set_by_lib = 0;    // the constructor wrote GPU_MAX_HW_QUEUES
+
+static bool kfd_open() {
+  const char* force = getenv("ORBPL_ASSUME_RUNTIME_STARTED");
+  if (force) return force[0] == '1';
+  char path[64], target[256];
+  for (int fd = 0; fd < 4096; fd++) {
+    snprintf(path, sizeof(path), "/proc/self/fd/%d", fd);
+    const ssize_t n = readlink(path, target, sizeof(target) - 1);
+    if (n <= 0) continue;
+    target[n] = 0;
+    if (strcmp(target, "/dev/kfd") == 0) return true;
+  }
+  return false;
 }
+
+__attribute__((constructor)) static void record_hw_queues() {
+  const char* q = getenv("GPU_MAX_HW_QUEUES");
+  const int before = q && atoi(q) > 0 ? atoi(q) : 4;
+  g_hw_queues = before;
+  g_runtime_started = kfd_open() ? 1 : 0;
+  if (g_runtime_started) return;
+  const char* want = getenv("ORBPL_HW_QUEUES");
+  int n = 0;
+  if (want) n = atoi(want);     // an explicit request (0: leave the setting alone)
+  else if (!q) n = 16;          // unset: fill in
+  if (n <= 0) return;
+  if (n > 32) n = 32;
+  char buf[16];
+  snprintf(buf, sizeof(buf), "%d", n);
+  setenv("GPU_MAX_HW_QUEUES", buf, 1);
+  g_hw_queues = n;
+  g_queues_set_by_lib = 1;
+}
+
+int hw_queues() { return g_hw_queues; }
 
 static thread_local std::string g_last_error;
 
@@ -134,6 +169,15 @@ extern "C" {
 const char* orbpl_last_error(void) { return orbpl::g_last_error.c_str(); }
 
 const char* orbpl_version(void) { return "orbpl gfx950 r3"; }
+
+int orbpl_hw_queue_state(int* queues, int* runtime_started, int* set_by_library,
+                         int* lsd_split_1024) {
+  if (queues) *queues = orbpl::g_hw_queues;
+  if (runtime_started) *runtime_started = orbpl::g_runtime_started;
+  if (set_by_library) *set_by_library = orbpl::g_queues_set_by_lib;
+  if (lsd_split_1024) *lsd_split_1024 = orbpl::lsd_split_decision(1024) ? 1 : 0;
+  return ORBPL_OK;
+}
 
 int orbpl_device_count(int* n) {
   if (!n) return arg_fail("n is NULL");

@@ -15,6 +15,12 @@ int arg_fail(const char* msg);
 void set_smem_attr(const void* fn, size_t bytes);
 // compute units of the current device (cached per device)
 int device_cu_count();
+// hardware queues the HIP runtime runs with, as recorded at library load
+// (orbpl_runtime.cpp: not re-read from the environment)
+int hw_queues();
+extern int g_hw_queues, g_runtime_started, g_queues_set_by_lib;
+// would a lines tracker of n_streams split its LSD batch (track_runtime.cpp)
+bool lsd_split_decision(int n_streams);
 // Run `init` once per (key, device) (thread-safe); returns true the first time.
 bool once_per_device(const void* key);
 int orbx_run(orbx_ctx* c, const uint8_t* d_imgs, int batch, int stride, long long frame_pitch,

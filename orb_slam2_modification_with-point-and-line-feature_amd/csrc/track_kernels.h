@@ -181,8 +181,8 @@ struct InFrustumArgs {
   const float* Tcw;
   const float* xyz;        // n x 3 world positions
   const float* normal;     // n x 3 mean viewing directions
-  const float* min_dist;   // GetMinDistanceInvariance
-  const float* max_dist;   // GetMaxDistanceInvariance
+  const float* min_dist;   // mfMinDistance (the kernel applies GetMinDistanceInvariance's 0.8f)
+  const float* max_dist;   // mfMaxDistance (the kernel applies GetMaxDistanceInvariance's 1.2f)
   float view_cos_limit;
   uint8_t* in_view;        // mbTrackInView
   float* proj_x;           // mTrackProjX

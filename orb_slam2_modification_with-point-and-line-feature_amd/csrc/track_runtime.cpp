@@ -38,12 +38,10 @@ constexpr int kLsdSplitMin = 1024;
 // the run-to-run spread), lines -2 %
 constexpr int kOrbSplitMin = 1 << 30;
 
-// the HIP runtime was started with >= 8 hardware queues (GPU_MAX_HW_QUEUES):
-// with the default 4, extra streams share queues and serialise
-bool enough_hw_queues() {
-  const char* q = getenv("GPU_MAX_HW_QUEUES");
-  return q && atoi(q) >= 8;
-}
+// the HIP runtime runs with >= 8 hardware queues (recorded at library load,
+// orbpl_runtime.cpp): with the default 4, extra streams share queues and
+// serialise
+bool enough_hw_queues() { return hw_queues() >= 8; }
 // a split switch: env "0" off, "1" on, else on from `min_streams` when the
 // runtime has the queues for it
 bool split_on(const char* env, int n_streams, int min_streams) {
@@ -110,6 +108,10 @@ int make_consts(const orbpl_camera* cam, const float* scale, const float* inv_si
 hipStream_t scratch_stream() { return nullptr; }  // host-pointer APIs use the null stream
 
 }  // namespace
+
+bool orbpl::lsd_split_decision(int n_streams) {
+  return split_on("ORBPL_LSD_SPLIT", n_streams, kLsdSplitMin);
+}
 
 extern "C" {
 

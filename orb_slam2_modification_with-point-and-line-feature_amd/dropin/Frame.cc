@@ -121,8 +121,8 @@ int Frame::IsInFrustumBatch(const std::vector<MapPoint*>& vp, float viewingCosLi
       xyz[3 * j + k] = X.at<float>(k, 0);
       nrm[3 * j + k] = Nv.at<float>(k, 0);
     }
-    dmin[j] = vp[j]->GetMinDistanceInvariance();
-    dmax[j] = vp[j]->GetMaxDistanceInvariance();
+    dmin[j] = vp[j]->GetMinDistance();   // the library applies GetMin/MaxDistanceInvariance's
+    dmax[j] = vp[j]->GetMaxDistance();   // 0.8f / 1.2f and PredictScale's mfMaxDistance / dist
   }
   const orbpl_camera cam = Camera();
   check(orbpl_frame_is_in_frustum(&cam, mfScaleFactor, mnScaleLevels, mTcw.ptr<float>(), M,

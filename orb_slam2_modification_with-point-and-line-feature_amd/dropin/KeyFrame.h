@@ -7,6 +7,7 @@
 // from the Frame it is made of, as KeyFrame::KeyFrame(Frame&, ...) does. The
 // covisibility graph, spanning tree and map bookkeeping stay the caller's.
 #pragma once
+#include <stdexcept>
 #include <vector>
 
 #include "Frame.h"
@@ -28,6 +29,7 @@ class KeyFrame {
 
   // KeyFrame::ComputeBoW (KeyFrame.cc:67-80)
   void ComputeBoW() {
+    if (!mpORBvocabulary) throw std::runtime_error("KeyFrame::ComputeBoW: no vocabulary");
     if (mBowVec.empty() || mFeatVec.empty())
       mpORBvocabulary->transform(toDescriptorVector(mDescriptors), mBowVec, mFeatVec, 4);
   }

@@ -36,6 +36,10 @@ class MapPoint {
   // MapPoint.cc:413-423
   float GetMinDistanceInvariance() const { return 0.8f * mfMinDistance; }
   float GetMaxDistanceInvariance() const { return 1.2f * mfMaxDistance; }
+  // the raw distances: Frame::IsInFrustum hands these to the library, which
+  // applies the 0.8f / 1.2f above and PredictScale's mfMaxDistance / dist
+  float GetMinDistance() const { return mfMinDistance; }
+  float GetMaxDistance() const { return mfMaxDistance; }
 
   // Tracking variables (MapPoint.h:155-175), written by Frame::IsInFrustum
   float mTrackProjX = 0, mTrackProjY = 0, mTrackProjXR = 0;

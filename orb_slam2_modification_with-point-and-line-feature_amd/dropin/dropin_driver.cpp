@@ -154,8 +154,6 @@ int main(int argc, char** argv) {
     rd(in, &vpath[0], plen);
     fclose(in);
 
-    ORBVocabulary voc;
-    if (!voc.loadFromTextFile(vpath)) throw std::runtime_error("cannot load the vocabulary");
     // Tracking::Tracking: K, DistCoef, mbf, mThDepth = bf * ThDepth / fx
     // (Tracking.cc:54-138)
     cv::Mat K = cv::Mat::eye(3, 3, cv::CV_32F);
@@ -172,7 +170,8 @@ int main(int argc, char** argv) {
       std::vector<double> ms;
       for (int r = 0; r < reps + 3; r++) {   // 3 warm-up constructions
         const auto t0 = std::chrono::steady_clock::now();
-        Frame Ft(g[r % 3], d[r % 3], r, &ex, &voc, K, dist, bf, thDepth);
+        // the timed constructor reads no vocabulary (ComputeBoW is not part of it)
+        Frame Ft(g[r % 3], d[r % 3], r, &ex, nullptr, K, dist, bf, thDepth);
         const auto t1 = std::chrono::steady_clock::now();
         if (r >= 3) ms.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
       }
@@ -182,6 +181,8 @@ int main(int argc, char** argv) {
       printf("time: median %.3f ms mean %.3f ms frames %d\n", ms[ms.size() / 2], mean, reps);
       return 0;
     }
+    ORBVocabulary voc;
+    if (!voc.loadFromTextFile(vpath)) throw std::runtime_error("cannot load the vocabulary");
     Frame F0(g[0], d[0], 0.0, &ex, &voc, K, dist, bf, thDepth);
     std::vector<cv::Mat> pyr = ex.mvImagePyramid;
     Frame F1(g[1], d[1], 1.0, &ex, &voc, K, dist, bf, thDepth);
@@ -270,8 +271,8 @@ int main(int argc, char** argv) {
           v[k] = X.at<float>(k, 0);
           v[3 + k] = Nv.at<float>(k, 0);
         }
-        v[6] = p->GetMinDistanceInvariance();
-        v[7] = p->GetMaxDistanceInvariance();
+        v[6] = p->GetMinDistance();   // raw mfMinDistance / mfMaxDistance
+        v[7] = p->GetMaxDistance();
       }
       wr(o, v, 8);
     }

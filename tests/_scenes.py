@@ -198,3 +198,42 @@ def stereo_sequence(n=3, seed=0, cam_name="KITTI00"):
         right, _ = synth.render(cfg, T @ shift, room, seed=seed * 100 + i)
         pairs.append((left, right))
     return cfg, traj, pairs
+
+
+def predict_scale_problem():
+    """Map points straight ahead of an identity camera whose expected
+    mnTrackScaleLevel is known by hand: a point created at distance d0 from an
+    observation at octave k has mfMaxDistance = d0 * scale[k] and mfMinDistance
+    = mfMaxDistance / scale[7] (MapPoint::UpdateNormalAndDepth, MapPoint.cc:
+    376-382). Seen again from d0, MapPoint::PredictScale (MapPoint.cc:416-431)
+    gives ceil(log(scale[k]) / log(1.2)), which is k up to the float rounding of
+    the log ratio; octave 0 must give exactly 0 (ratio 1). Returns (cfg,
+    Tcw, mps, expected level, ratio) with the expected levels computed here in
+    numpy from the reference's formula, independently of the oracle."""
+    load_pkg()
+    import orbpl.synth as synth
+    cfg = dict(synth.TUM1)
+    sc = np.ones(8, np.float32)
+    for i in range(1, 8):
+        sc[i] = np.float32(sc[i - 1] * np.float32(1.2))
+    xyz, nrm, dmin, dmax, exp_level, ratio = [], [], [], [], [], []
+    for k in range(8):
+        for d0, dview in ((2.0, 2.0), (1.5, 1.5), (2.0, 2.0 * 1.1), (3.0, 3.0 / 1.1)):
+            # straight ahead: u = cx, v = cy, dist = z exactly
+            P = np.array([0, 0, dview], np.float32)
+            mx = np.float32(np.float32(d0) * sc[k])
+            mn = np.float32(mx / sc[7])
+            dist = np.float32(dview)
+            if not (dist >= np.float32(0.8) * mn and dist <= np.float32(1.2) * mx):
+                continue
+            r = np.float32(mx / dist)
+            lv = int(np.ceil(np.float32(np.log(np.float64(r))) / np.float32(np.log(np.float64(np.float32(1.2))))))
+            xyz.append(P)
+            nrm.append(np.array([0, 0, 1], np.float32))
+            dmin.append(mn)
+            dmax.append(mx)
+            exp_level.append(min(max(lv, 0), 7))
+            ratio.append(r)
+    mps = dict(xyz=np.array(xyz, np.float32), normal=np.array(nrm, np.float32),
+               min_dist=np.array(dmin, np.float32), max_dist=np.array(dmax, np.float32))
+    return cfg, np.eye(4, dtype=np.float32), mps, np.array(exp_level, np.int32), np.array(ratio)

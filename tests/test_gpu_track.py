@@ -469,6 +469,16 @@ def test_in_frustum_bit_exact(orbpl, oracle, seed):
     assert 0.2 * len(mps["xyz"]) < o["in_view"].sum() < len(mps["xyz"])
 
 
+def test_predict_scale_hand_computed_gpu(orbpl, oracle):
+    """k_in_frustum's mnTrackScaleLevel against hand-computed PredictScale
+    values (ratio = mfMaxDistance / dist, MapPoint.cc:421)."""
+    from _scenes import predict_scale_problem
+    cfg, T, mps, lev, ratio = predict_scale_problem()
+    g = orbpl.frame_is_in_frustum(orbpl.make_camera(cfg), 1.2, 8, T, mps, 0.5)
+    assert g["in_view"].all()
+    assert np.array_equal(g["level"], lev)
+
+
 @pytest.mark.parametrize("th,nnratio,claims", [(3.0, 0.8, True), (1.0, 0.6, False), (5.0, 0.8, True)])
 def test_search_by_projection_local_bit_exact(orbpl, oracle, th, nnratio, claims):
     from _scenes import local_map_problem

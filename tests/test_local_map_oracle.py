@@ -51,3 +51,20 @@ def test_search_by_bow_oracle_properties(oracle):
     assert d.max() <= 50
     # a keyframe feature is used at most once per node walk
     assert len(np.unique(m[j])) == len(j)
+
+
+def test_predict_scale_hand_computed(oracle):
+    """MapPoint::PredictScale's ratio is mfMaxDistance / dist (MapPoint.cc:421),
+    not GetMaxDistanceInvariance() / dist: a point seen from its creation
+    distance at octave k predicts octave k (0 exactly for octave 0)."""
+    from _scenes import predict_scale_problem
+    cfg, T, mps, lev, ratio = predict_scale_problem()
+    tr = oracle.frame_is_in_frustum(oracle.camera(cfg), _log_scale(oracle), 8, T, mps, 0.5)
+    assert tr["in_view"].all()
+    assert np.array_equal(tr["level"], lev)
+    # a point at its creation distance and octave: level == octave
+    same = np.isclose(ratio, mps["max_dist"] / mps["xyz"][:, 2]) & (
+        np.abs(np.log(ratio) / np.log(1.2) - np.round(np.log(ratio) / np.log(1.2))) < 1e-5)
+    k = np.round(np.log(ratio[same]) / np.log(1.2)).astype(int)
+    assert tr["level"][same][k == 0].tolist() == [0] * int((k == 0).sum()) and (k == 0).sum() >= 2
+    assert np.all(np.abs(tr["level"][same] - k) <= 1)
