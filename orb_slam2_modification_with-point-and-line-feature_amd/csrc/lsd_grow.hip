@@ -38,7 +38,6 @@ namespace {
 constexpr double kPi = 3.14159265358979323846;
 constexpr double kDegToRad = kPi / 180;
 constexpr int kRegLds = 512;
-constexpr int kRing = 64;   // point-word ring entries per lane of the prefetching grow (power of two)
 
 struct Rect {
   double x1, y1, x2, y2, width, x, y, theta, dx, dy, prec, p;
@@ -665,53 +664,23 @@ __device__ __forceinline__ double entry_w(const uint4& e) {
 __device__ __forceinline__ float entry_deg(const uint4& e) { return __uint_as_float(e.y); }
 
 // A lane's region list: lbuf[frame][lane][i] (a lane's batch of 8 entries is
-// one cache line). ORBPL_LBUF_INTERLEAVED=1 (A/B build) puts entry i of lane l
-// at lbuf[frame][i][l], so that a wave's load of entry i (the lanes walk their
-// lists in step) reads 64 consecutive entries: measured slower (231 vs 222 ms
-// per 3072 frames) - the lane-major batch stays in one line per lane.
-#ifndef ORBPL_LBUF_INTERLEAVED
-#define ORBPL_LBUF_INTERLEAVED 0
-#endif
+// one cache line; lane-interleaved lists measured slower, 231 vs 222 ms per
+// 3072 frames).
 struct LaneBuf {
   uint4* p;
-  static constexpr long long kStride = ORBPL_LBUF_INTERLEAVED ? kSpecLanes : 1;
-  __device__ __forceinline__ uint4& operator[](int i) const { return p[(long long)i * kStride]; }
-  __device__ __forceinline__ LaneBuf operator+(int o) const { return LaneBuf{p + (long long)o * kStride}; }
-  __device__ __forceinline__ uint32_t pt(int i) const { return p[(long long)i * kStride].x; }
-  __device__ __forceinline__ void set_pt(int i, uint32_t v) const { p[(long long)i * kStride].x = v; }
+  __device__ __forceinline__ uint4& operator[](int i) const { return p[i]; }
+  __device__ __forceinline__ LaneBuf operator+(int o) const { return LaneBuf{p + o}; }
+  __device__ __forceinline__ uint32_t pt(int i) const { return p[i].x; }
+  __device__ __forceinline__ void set_pt(int i, uint32_t v) const { p[i].x = v; }
   __device__ __forceinline__ double w(int i) const {
-    const uint2 v = *reinterpret_cast<const uint2*>(&p[(long long)i * kStride].z);
+    const uint2 v = *reinterpret_cast<const uint2*>(&p[i].z);
     return __hiloint2double((int)v.y, (int)v.x);
   }
   __device__ __forceinline__ void set_w(int i, double v) const {
-    *reinterpret_cast<uint2*>(&p[(long long)i * kStride].z) =
+    *reinterpret_cast<uint2*>(&p[i].z) =
         make_uint2((uint32_t)__double2loint(v), (uint32_t)__double2hiint(v));
   }
 };
-
-// ORBPL_GROW_CS: the added pixels' cos / sin from the angle-term plane (1) or
-// evaluated per add (0); ORBPL_GROW_LOOP: first-aligned iteration (1) or the
-// in-order walk over the 9 positions (0). A/B build overrides.
-#ifndef ORBPL_GROW_CS
-#define ORBPL_GROW_CS 1
-#endif
-#ifndef ORBPL_GROW_LOOP
-#define ORBPL_GROW_LOOP 0
-#endif
-#if !ORBPL_GROW_CS
-__device__ __forceinline__ void add_angle(float d, float& sumdx, float& sumdy) {
-  float c, sn;
-  cr_cos_sin((float)((double)d * (3.14159265358979323846 / 180)), &c, &sn);
-  sumdx += c;
-  sumdy += sn;
-}
-#endif
-
-// ORBPL_GROW_LEAN: the grow step as straight-line code (below); 0 = the
-// earlier step with the branchy aligned test (A/B build override).
-#ifndef ORBPL_GROW_LEAN
-#define ORBPL_GROW_LEAN 1
-#endif
 
 // cv::fastAtan2 with one division: both branches of fast_atan2_deg divide the
 // smaller of |x|, |y| by the larger + eps and evaluate the same polynomial, so
@@ -735,12 +704,6 @@ __device__ __forceinline__ float fast_atan2_deg_1div(float y, float x) {
   return a;
 }
 
-// ORBPL_GROW_U32: 32-bit unsigned byte offsets for the grow's neighbour
-// loads and claims (A/B build override)
-#ifndef ORBPL_GROW_U32
-#define ORBPL_GROW_U32 1
-#endif
-#if ORBPL_GROW_LEAN && ORBPL_GROW_CS && ORBPL_SD_PAIRED
 // region_grow for one lane (same result as the step below). Per step the 8
 // neighbour addresses come from 3 row and 3 column terms of the tile index;
 // the neighbour's flags (in image, not USED, not already in this region,
@@ -776,14 +739,10 @@ __device__ __forceinline__ int lane_grow(const Frame& F, uint64_t* sd, LaneBuf b
     const uint4 pref = buf[min(i + 1, n_start - 1)];
     // tile index = row term + column term (disjoint bit fields), x2 for the
     // paired 16-byte entries
-#if ORBPL_GROW_U32
     // byte offsets from the frame's (wave-uniform) pixel-word base as 32-bit
     // unsigned values: the loads and claims take the scalar-base + 32-bit
     // vector-offset form (no 64-bit address arithmetic per neighbour)
     uint32_t rterm[3], cterm[3];
-#else
-    int rterm[3], cterm[3];
-#endif
     bool rin[3], cin[3];
 #pragma unroll
     for (int d = 0; d < 3; d++) {
@@ -791,24 +750,15 @@ __device__ __forceinline__ int lane_grow(const Frame& F, uint64_t* sd, LaneBuf b
       rin[d] = yy >= 0 && yy < sh;
       cin[d] = xx >= 0 && xx < sw;
       const int cy = min(max(yy, 0), sh - 1), cx = min(max(xx, 0), sw - 1);
-#if ORBPL_GROW_U32
       rterm[d] = ((((uint32_t)(cy >> 2) * (uint32_t)tw) << 5) | ((uint32_t)(cy & 3) << 3)) << 3;
       cterm[d] = (((uint32_t)(cx >> 2) << 5) | ((uint32_t)(cx & 3) << 1)) << 3;
-#else
-      rterm[d] = (((cy >> 2) * tw) << 5) | ((cy & 3) << 3);
-      cterm[d] = ((cx >> 2) << 5) | ((cx & 3) << 1);
-#endif
     }
     uint4 w[9];
 #pragma unroll
     for (int k = 0; k < 9; k++) {
       if (k == 4) continue;
-#if ORBPL_GROW_U32
       w[k] = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(sd) +
                                              (rterm[k / 3] + cterm[k % 3]));
-#else
-      w[k] = *reinterpret_cast<const uint4*>(sd + (rterm[k / 3] + cterm[k % 3]));
-#endif
     }
     unsigned ok = 0;
 #pragma unroll
@@ -828,15 +778,9 @@ __device__ __forceinline__ int lane_grow(const Frame& F, uint64_t* sd, LaneBuf b
       nt = nt > k3pi2 ? fabs(nt - k2pi) : nt;
       if (((ok >> k) & 1u) && nt <= prec) {
         if ((w[k].y >> 1) < mytag) return kSpecConflict;   // an earlier seed's pixel
-#if ORBPL_GROW_U32
         atomicMin(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(sd) +
                                                         (rterm[k / 3] + cterm[k % 3])),
                   ((unsigned long long)myval << 32) | w[k].x);
-#else
-        const int id = rterm[k / 3] + cterm[k % 3];
-        atomicMin(reinterpret_cast<unsigned long long*>(sd + id),
-                  ((unsigned long long)myval << 32) | w[k].x);
-#endif
         if (n >= cap) return kSpecOverflow;
         const int xx = x + (k % 3) - 1, yy = y + (k / 3) - 1;
         const uint4 e = make_uint4((uint32_t)xx | ((uint32_t)yy << 16), w[k].x, 0u, 0u);
@@ -850,499 +794,6 @@ __device__ __forceinline__ int lane_grow(const Frame& F, uint64_t* sd, LaneBuf b
     cur = (i + 1 < n_start) ? pref : first_add;
   }
   return n;
-}
-
-// ORBPL_GROW_PF: the small-batch seed loop (one wave per frame, batches of at
-// most kSpecSmallBatch frames) loads the next pixel's neighbourhood while it
-// tests / adds the current one, so a step no longer waits a memory round trip
-// before its tests (a lone wave on its SIMD hides no latency otherwise). The
-// point words of the grow's last 64 entries sit in a per-lane LDS ring, so
-// the next pixel to expand is known at the step's start. The prefetched words
-// predate the adds of the step in flight: those pixels (the only stamps that
-// step changes for this lane) are marked "in this region" from the step's
-// added mask, shifted to the next pixel's 3x3 (a 7x7 bit board). Claims other
-// lanes made meanwhile are caught by the claim re-check after the round, as
-// for any speculative read.
-// Measured slower and off (A/B on one box, two rounds, tools/gpu_r04_b.sh:
-// LSD batch 1 / 16 / 64 = 54-55 / 63 / 67 ms with it, 49-52 / 55-57 / 59-60
-// ms without; the two-register-set form ORBPL_GROW_PF=2, which avoids copying
-// the prefetched words, 53-57 / 63-64 / 66 ms): the extra address work, the
-// LDS ring and the doubled neighbourhood registers cost more issue cycles
-// than the hidden load latency saves - the grow step is bound by its
-// instruction issue, not by the neighbourhood round trip.
-#ifndef ORBPL_GROW_PF
-#define ORBPL_GROW_PF 0
-#endif
-
-__device__ __forceinline__ void nb_terms(int x, int y, int sw, int sh, int tw, int* rterm,
-                                         int* cterm, unsigned* inmask) {
-  bool rin[3], cin[3];
-#pragma unroll
-  for (int d = 0; d < 3; d++) {
-    const int yy = y + d - 1, xx = x + d - 1;
-    rin[d] = yy >= 0 && yy < sh;
-    cin[d] = xx >= 0 && xx < sw;
-    const int cy = min(max(yy, 0), sh - 1), cx = min(max(xx, 0), sw - 1);
-    rterm[d] = (((cy >> 2) * tw) << 5) | ((cy & 3) << 3);
-    cterm[d] = ((cx >> 2) << 5) | ((cx & 3) << 1);
-  }
-  unsigned m = 0;
-#pragma unroll
-  for (int k = 0; k < 9; k++) m |= (unsigned)(rin[k / 3] & cin[k % 3]) << k;
-  *inmask = m;
-}
-
-__device__ __forceinline__ int lane_grow_pf(const Frame& F, uint64_t* sd, LaneBuf buf, int cap,
-                                            int sx, int sy, double& reg_angle, double prec,
-                                            uint32_t myval, uint32_t* ring) {
-  const uint32_t mytag = myval >> 1;
-  const int sw = F.sw, sh = F.sh, tw = F.tw;
-  const int si = lsd_sd_index(sx, sy, tw);
-  if (cap < 1) return kSpecOverflow;
-  const uint64_t v0 = ld_sd(sd + si);
-  if (((uint32_t)(v0 >> 32) >> 1) < mytag) return kSpecConflict;
-  atomicMin(reinterpret_cast<unsigned long long*>(sd + si),
-            ((unsigned long long)myval << 32) | (uint32_t)v0);
-  uint32_t cur = (uint32_t)sx | ((uint32_t)sy << 16);
-  buf[0] = make_uint4(cur, (uint32_t)v0, 0u, 0u);
-  ring[0] = cur;
-  reg_angle = deg2ang(__uint_as_float((uint32_t)v0));
-  double s0, c0;
-  lsdm::sincos_(reg_angle, &s0, &c0);
-  float sumdx = (float)c0;
-  float sumdy = (float)s0;
-  const double k3pi2 = (3 * kPi) / 2, k2pi = 2 * kPi;
-  int n = 1;
-  // the current pixel's neighbourhood: terms, in-image mask and words
-  int rterm[3], cterm[3];
-  unsigned inm;
-  uint4 w[9];
-  nb_terms(sx, sy, sw, sh, tw, rterm, cterm, &inm);
-#pragma unroll
-  for (int k = 0; k < 9; k++) {
-    if (k == 4) continue;
-    w[k] = *reinterpret_cast<const uint4*>(sd + (rterm[k / 3] + cterm[k % 3]));
-  }
-  unsigned own = 0;   // neighbours known to be in this region although their words predate it
-#if ORBPL_GROW_PF == 2
-  // two register sets used in turn (the loop unrolled by two): the words
-  // prefetched for the next pixel are never copied, so nothing waits for them
-  // before that pixel's own tests
-  uint4 w2[9];
-  int rterm2[3], cterm2[3];
-  unsigned inm2 = 0;
-  int i = 0;
-  auto step = [&](uint4 (&wc)[9], int (&rc)[3], int (&cc)[3], unsigned& inc, uint4 (&wn)[9],
-                  int (&rn)[3], int (&cn)[3], unsigned& inn) -> int {
-    const int x = (int)(cur & 0xFFFF), y = (int)(cur >> 16);
-    const int n_start = n;
-    const bool pf = i + 1 < n_start;
-    uint32_t nxt = cur;
-    if (pf) {
-      nxt = n_start - (i + 1) <= kRing ? ring[(i + 1) & (kRing - 1)] : buf.pt(i + 1);
-      nb_terms((int)(nxt & 0xFFFF), (int)(nxt >> 16), sw, sh, tw, rn, cn, &inn);
-#pragma unroll
-      for (int k = 0; k < 9; k++) {
-        if (k == 4) continue;
-        wn[k] = *reinterpret_cast<const uint4*>(sd + (rn[k / 3] + cn[k % 3]));
-      }
-    }
-    unsigned ok = 0;
-#pragma unroll
-    for (int k = 0; k < 9; k++) {
-      if (k == 4) continue;
-      const unsigned f = ((inc >> k) & 1u) & ((~own >> k) & 1u) & (unsigned)(wc[k].y != 0u) &
-                         (unsigned)(wc[k].y != myval) & (unsigned)(__uint_as_float(wc[k].x) >= 0.f);
-      ok |= f << k;
-    }
-    uint32_t first_add = cur;
-    unsigned added = 0;
-#pragma unroll
-    for (int k = 0; k < 9; k++) {
-      if (k == 4) continue;
-      double nt = fabs(reg_angle - deg2ang(__uint_as_float(wc[k].x)));
-      nt = nt > k3pi2 ? fabs(nt - k2pi) : nt;
-      if (((ok >> k) & 1u) && nt <= prec) {
-        if ((wc[k].y >> 1) < mytag) return kSpecConflict;   // an earlier seed's pixel
-        const int id = rc[k / 3] + cc[k % 3];
-        atomicMin(reinterpret_cast<unsigned long long*>(sd + id),
-                  ((unsigned long long)myval << 32) | wc[k].x);
-        if (n >= cap) return kSpecOverflow;
-        const int xx = x + (k % 3) - 1, yy = y + (k / 3) - 1;
-        const uint32_t pt = (uint32_t)xx | ((uint32_t)yy << 16);
-        if (n == n_start) first_add = pt;
-        buf[n] = make_uint4(pt, wc[k].x, 0u, 0u);
-        ring[n & (kRing - 1)] = pt;
-        n++;
-        added |= 1u << k;
-        sumdx += __uint_as_float(wc[k].z);   // add_angle(d) terms
-        sumdy += __uint_as_float(wc[k].w);
-        reg_angle = (double)fast_atan2_deg_1div(sumdy, sumdx) * kDegToRad;
-      }
-    }
-    if (pf) {
-      const int ddx = (int)(nxt & 0xFFFF) - x, ddy = (int)(nxt >> 16) - y;
-      unsigned nown = 0;
-      if (added && ddx >= -2 && ddx <= 2 && ddy >= -2 && ddy <= 2) {
-        const unsigned long long B = ((unsigned long long)(added & 7u) << 16) |
-                                     ((unsigned long long)((added >> 3) & 7u) << 23) |
-                                     ((unsigned long long)((added >> 6) & 7u) << 30);
-#pragma unroll
-        for (int r = 0; r < 3; r++)
-          nown |= (unsigned)((B >> (7 * (2 + ddy + r) + 2 + ddx)) & 7ull) << (3 * r);
-      }
-      own = nown;
-      cur = nxt;
-    } else if (i + 1 < n) {
-      // the next pixel is this step's first add: its words are loaded now
-      cur = first_add;
-      own = 0;
-      nb_terms((int)(cur & 0xFFFF), (int)(cur >> 16), sw, sh, tw, rn, cn, &inn);
-#pragma unroll
-      for (int k = 0; k < 9; k++) {
-        if (k == 4) continue;
-        wn[k] = *reinterpret_cast<const uint4*>(sd + (rn[k / 3] + cn[k % 3]));
-      }
-    }
-    i++;
-    return 0;
-  };
-  while (i < n) {
-    int r = step(w, rterm, cterm, inm, w2, rterm2, cterm2, inm2);
-    if (r) return r;
-    if (i >= n) break;
-    r = step(w2, rterm2, cterm2, inm2, w, rterm, cterm, inm);
-    if (r) return r;
-  }
-#else
-  for (int i = 0; i < n; i++) {
-    const int x = (int)(cur & 0xFFFF), y = (int)(cur >> 16);
-    const int n_start = n;
-    // the next pixel to expand, when already listed: its neighbourhood now
-    const bool pf = i + 1 < n_start;
-    uint32_t nxt = cur;
-    int nr[3], nc[3];
-    unsigned ninm = 0;
-    uint4 pw[9];
-    if (pf) {
-      nxt = n_start - (i + 1) <= kRing ? ring[(i + 1) & (kRing - 1)] : buf.pt(i + 1);
-      nb_terms((int)(nxt & 0xFFFF), (int)(nxt >> 16), sw, sh, tw, nr, nc, &ninm);
-#pragma unroll
-      for (int k = 0; k < 9; k++) {
-        if (k == 4) continue;
-        pw[k] = *reinterpret_cast<const uint4*>(sd + (nr[k / 3] + nc[k % 3]));
-      }
-    }
-    unsigned ok = 0;
-#pragma unroll
-    for (int k = 0; k < 9; k++) {
-      if (k == 4) continue;
-      const unsigned f = ((inm >> k) & 1u) & ((~own >> k) & 1u) & (unsigned)(w[k].y != 0u) &
-                         (unsigned)(w[k].y != myval) & (unsigned)(__uint_as_float(w[k].x) >= 0.f);
-      ok |= f << k;
-    }
-    uint32_t first_add = cur;
-    unsigned added = 0;
-#pragma unroll
-    for (int k = 0; k < 9; k++) {
-      if (k == 4) continue;
-      double nt = fabs(reg_angle - deg2ang(__uint_as_float(w[k].x)));
-      nt = nt > k3pi2 ? fabs(nt - k2pi) : nt;
-      if (((ok >> k) & 1u) && nt <= prec) {
-        if ((w[k].y >> 1) < mytag) return kSpecConflict;   // an earlier seed's pixel
-        const int id = rterm[k / 3] + cterm[k % 3];
-        atomicMin(reinterpret_cast<unsigned long long*>(sd + id),
-                  ((unsigned long long)myval << 32) | w[k].x);
-        if (n >= cap) return kSpecOverflow;
-        const int xx = x + (k % 3) - 1, yy = y + (k / 3) - 1;
-        const uint32_t pt = (uint32_t)xx | ((uint32_t)yy << 16);
-        if (n == n_start) first_add = pt;
-        buf[n] = make_uint4(pt, w[k].x, 0u, 0u);
-        ring[n & (kRing - 1)] = pt;
-        n++;
-        added |= 1u << k;
-        sumdx += __uint_as_float(w[k].z);   // add_angle(d) terms
-        sumdy += __uint_as_float(w[k].w);
-        reg_angle = (double)fast_atan2_deg_1div(sumdy, sumdx) * kDegToRad;
-      }
-    }
-    if (pf) {
-      // this step's adds, seen from the next pixel's 3x3: a 7x7 board with
-      // the current 3x3 at rows / columns 2..4
-      const int ddx = (int)(nxt & 0xFFFF) - x, ddy = (int)(nxt >> 16) - y;
-      unsigned nown = 0;
-      if (added && ddx >= -2 && ddx <= 2 && ddy >= -2 && ddy <= 2) {
-        const unsigned long long B = ((unsigned long long)(added & 7u) << 16) |
-                                     ((unsigned long long)((added >> 3) & 7u) << 23) |
-                                     ((unsigned long long)((added >> 6) & 7u) << 30);
-#pragma unroll
-        for (int r = 0; r < 3; r++)
-          nown |= (unsigned)((B >> (7 * (2 + ddy + r) + 2 + ddx)) & 7ull) << (3 * r);
-      }
-      own = nown;
-      cur = nxt;
-      inm = ninm;
-#pragma unroll
-      for (int d = 0; d < 3; d++) {
-        rterm[d] = nr[d];
-        cterm[d] = nc[d];
-      }
-#pragma unroll
-      for (int k = 0; k < 9; k++) w[k] = pw[k];
-    } else if (i + 1 < n) {
-      // the next pixel is this step's first add: its words are loaded now
-      // (after this step's claims)
-      cur = first_add;
-      own = 0;
-      nb_terms((int)(cur & 0xFFFF), (int)(cur >> 16), sw, sh, tw, rterm, cterm, &inm);
-#pragma unroll
-      for (int k = 0; k < 9; k++) {
-        if (k == 4) continue;
-        w[k] = *reinterpret_cast<const uint4*>(sd + (rterm[k / 3] + cterm[k % 3]));
-      }
-    }
-  }
-#endif
-  return n;
-}
-#else
-__device__ __forceinline__ int lane_grow(const Frame& F, uint64_t* sd, LaneBuf buf, int cap, int sx,
-                                         int sy, double& reg_angle, double prec, uint32_t myval) {
-  const uint32_t mytag = myval >> 1;
-  const int sw = F.sw, sh = F.sh, tw = F.tw;
-  const int si = lsd_sd_index(sx, sy, tw);
-  if (cap < 1) return kSpecOverflow;
-  const uint64_t v0 = ld_sd(sd + si);
-  if (((uint32_t)(v0 >> 32) >> 1) < mytag) return kSpecConflict;
-  atomicMin(reinterpret_cast<unsigned long long*>(sd + si),
-            ((unsigned long long)myval << 32) | (uint32_t)v0);
-  uint4 cur = make_uint4((uint32_t)sx | ((uint32_t)sy << 16), (uint32_t)v0, 0u, 0u);
-  buf[0] = cur;
-  reg_angle = deg2ang(entry_deg(cur));
-  double s0, c0;
-  lsdm::sincos_(reg_angle, &s0, &c0);
-  float sumdx = (float)c0;
-  float sumdy = (float)s0;
-  int n = 1;
-  for (int i = 0; i < n; i++) {
-    const int x = pt_x(cur), y = pt_y(cur);
-    const int n_start = n;
-    // all loads unconditional (clamped coordinates) so that they are in
-    // flight together; out-of-image neighbours are masked afterwards
-    const uint4 pref = buf[min(i + 1, n_start - 1)];
-    uint64_t v[9];
-#if ORBPL_GROW_CS
-    uint64_t cs[9];
-#endif
-    unsigned cand = 0;
-#pragma unroll
-    for (int k = 0; k < 9; k++) {
-      const int xx = x + (k % 3) - 1, yy = y + (k / 3) - 1;
-      const int cx = min(max(xx, 0), sw - 1), cy = min(max(yy, 0), sh - 1);
-#if ORBPL_GROW_CS && ORBPL_SD_PAIRED
-      {   // word + terms in one 16-byte load (workgroup-scope plain load, as ld_sd)
-        const uint4 w = *reinterpret_cast<const uint4*>(sd + lsd_sd_index(cx, cy, tw));
-        v[k] = ((uint64_t)w.y << 32) | w.x;
-        cs[k] = ((uint64_t)w.w << 32) | w.z;
-      }
-#else
-      v[k] = ld_sd(sd + lsd_sd_index(cx, cy, tw));
-#if ORBPL_GROW_CS
-      cs[k] = F.cs[lsd_sd_index(cx, cy, tw)];
-#endif
-#endif
-      const bool in = xx >= 0 && xx < sw && yy >= 0 && yy < sh;
-      cand |= (in && (uint32_t)(v[k] >> 32) != 0u) ? (1u << k) : 0u;   // stamp 0 = USED
-    }
-    uint4 first_add = cur;
-#if ORBPL_GROW_LOOP
-    // Adds are rare (about one per step), so instead of walking the 9
-    // positions with the add code under each (executed wherever any lane
-    // adds), every iteration tests the remaining candidates against the
-    // current region angle and adds the first aligned one: the positions
-    // before it are not aligned under that angle, exactly as the in-order
-    // walk finds them, and the later ones are re-tested after the update.
-    unsigned rem = 0;
-#pragma unroll
-    for (int k = 0; k < 9; k++)
-      rem |= (((cand >> k) & 1u) && (uint32_t)(v[k] >> 32) != myval) ? (1u << k) : 0u;
-    while (rem) {
-      unsigned am = 0;
-#pragma unroll
-      for (int k = 0; k < 9; k++)
-        if ((rem >> k) & 1u)
-          am |= aligned_deg(__uint_as_float((uint32_t)v[k]), reg_angle, prec) ? (1u << k) : 0u;
-      if (!am) break;
-      const int k = __ffs(am) - 1;
-      rem &= ~((2u << k) - 1u);
-      uint64_t vk = v[0];
-#if ORBPL_GROW_CS
-      uint64_t ck = cs[0];
-#endif
-#pragma unroll
-      for (int j = 1; j < 9; j++) {
-        vk = (k == j) ? v[j] : vk;
-#if ORBPL_GROW_CS
-        ck = (k == j) ? cs[j] : ck;
-#endif
-      }
-      const uint32_t st = (uint32_t)(vk >> 32);
-      if ((st >> 1) < mytag) return kSpecConflict;      // an earlier seed's pixel
-      const int xx = x + (k % 3) - 1, yy = y + (k / 3) - 1;
-      atomicMin(reinterpret_cast<unsigned long long*>(sd + lsd_sd_index(xx, yy, tw)),
-                ((unsigned long long)myval << 32) | (uint32_t)vk);
-      if (n >= cap) return kSpecOverflow;
-      const uint4 e = make_uint4((uint32_t)xx | ((uint32_t)yy << 16), (uint32_t)vk, 0u, 0u);
-      if (n == n_start) first_add = e;
-      buf[n++] = e;
-#if ORBPL_GROW_CS
-      sumdx += __uint_as_float((uint32_t)ck);          // add_angle(d) terms
-      sumdy += __uint_as_float((uint32_t)(ck >> 32));
-#else
-      add_angle(__uint_as_float((uint32_t)vk), sumdx, sumdy);
-#endif
-      reg_angle = (double)fast_atan2_deg(sumdy, sumdx) * kDegToRad;
-    }
-#else
-#pragma unroll
-    for (int k = 0; k < 9; k++) {
-      const uint32_t st = (uint32_t)(v[k] >> 32);
-      if (!((cand >> k) & 1u) || st == myval) continue;  // USED (committed or own)
-      const float d = __uint_as_float((uint32_t)v[k]);
-      if (!aligned_deg(d, reg_angle, prec)) continue;
-      if ((st >> 1) < mytag) return kSpecConflict;      // an earlier seed's pixel
-      const int xx = x + (k % 3) - 1, yy = y + (k / 3) - 1;
-      atomicMin(reinterpret_cast<unsigned long long*>(sd + lsd_sd_index(xx, yy, tw)),
-                ((unsigned long long)myval << 32) | (uint32_t)v[k]);
-      if (n >= cap) return kSpecOverflow;
-      const uint4 e = make_uint4((uint32_t)xx | ((uint32_t)yy << 16), (uint32_t)v[k], 0u, 0u);
-      if (n == n_start) first_add = e;
-      buf[n++] = e;
-#if ORBPL_GROW_CS
-      sumdx += __uint_as_float((uint32_t)cs[k]);          // add_angle(d) terms
-      sumdy += __uint_as_float((uint32_t)(cs[k] >> 32));
-#else
-      add_angle(d, sumdx, sumdy);
-#endif
-      reg_angle = (double)fast_atan2_deg(sumdy, sumdx) * kDegToRad;
-    }
-#endif
-    cur = (i + 1 < n_start) ? pref : first_add;
-  }
-  return n;
-}
-#endif
-
-// region2rect over a lane's list (same operation order as region2rect).
-// With q given, the first pass also stores the weights modgrad = sqrt(q / 4)
-// (ll_angle's modgrad, LSD's region weights) into the list: the point words
-// it loads give the q addresses, so the fill costs no pass of its own. Every
-// pass reads the list in batches of unconditional loads (indices clamped to
-// n - 1, contributions masked) so the loads overlap.
-__device__ __forceinline__ void lane_rect_tail(LaneBuf buf, int n, double x, double y, double sum,
-                                               double reg_angle, double prec, double p, Rect& rec);
-__device__ __forceinline__ void lane_rect(LaneBuf buf, int n, double reg_angle, double prec,
-                                          double p, Rect& rec, const int* __restrict__ q = nullptr,
-                                          int sw = 0) {
-  constexpr int kB = 8;
-  double x = 0, y = 0, sum = 0;
-  for (int i0 = 0; i0 < n; i0 += kB) {
-    uint32_t pt[kB];
-    double w[kB];
-    if (q) {
-      int qv[kB];
-#pragma unroll
-      for (int u = 0; u < kB; u++) pt[u] = buf.pt(min(i0 + u, n - 1));
-#pragma unroll
-      for (int u = 0; u < kB; u++) qv[u] = q[(int)(pt[u] >> 16) * sw + (int)(pt[u] & 0xFFFF)];
-#pragma unroll
-      for (int u = 0; u < kB; u++) {
-        w[u] = modgrad_q(qv[u]);
-        if (i0 + u < n)
-          buf.set_w(i0 + u, w[u]);
-      }
-    } else {
-      uint4 e[kB];
-#pragma unroll
-      for (int u = 0; u < kB; u++) e[u] = buf[min(i0 + u, n - 1)];
-#pragma unroll
-      for (int u = 0; u < kB; u++) {
-        pt[u] = e[u].x;
-        w[u] = entry_w(e[u]);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < kB; u++) {
-      if (i0 + u < n) {
-        const double weight = w[u];
-        x += double(pt[u] & 0xFFFF) * weight;
-        y += double(pt[u] >> 16) * weight;
-        sum += weight;
-      }
-    }
-  }
-  lane_rect_tail(buf, n, x, y, sum, reg_angle, prec, p, rec);
-}
-
-// region2rect after the weighted centroid sums (x, y, sum in list order)
-__device__ __forceinline__ void lane_rect_tail(LaneBuf buf, int n, double x, double y, double sum,
-                                               double reg_angle, double prec, double p, Rect& rec) {
-  constexpr int kB = 8, kB3 = 16;
-  x /= sum;
-  y /= sum;
-  double Ixx = 0.0, Iyy = 0.0, Ixy = 0.0;
-  for (int i0 = 0; i0 < n; i0 += kB) {
-    uint4 e[kB];
-#pragma unroll
-    for (int u = 0; u < kB; u++) e[u] = buf[min(i0 + u, n - 1)];
-#pragma unroll
-    for (int u = 0; u < kB; u++) {
-      if (i0 + u < n) {
-        const double weight = entry_w(e[u]);
-        const double dx = double(pt_x(e[u])) - x, dy = double(pt_y(e[u])) - y;
-        Ixx += dy * dy * weight;
-        Iyy += dx * dx * weight;
-        Ixy -= dx * dy * weight;
-      }
-    }
-  }
-  const double lambda = 0.5 * (Ixx + Iyy - sqrt((Ixx - Iyy) * (Ixx - Iyy) + 4.0 * Ixy * Ixy));
-  double theta = (fabs(Ixx) > fabs(Iyy)) ? double(fast_atan2_deg(float(lambda - Ixx), float(Ixy)))
-                                         : double(fast_atan2_deg(float(Ixy), float(lambda - Iyy)));
-  theta *= kDegToRad;
-  if (fabs(angle_diff_signed(theta, reg_angle)) > prec) theta += kPi;
-  const double dx = lsdm::cos_(theta), dy = lsdm::sin_(theta);
-  // l_max / l_min (and w) start at 0, so the reference's else-if is an
-  // independent max / min
-  double l_min = 0, l_max = 0, w_min = 0, w_max = 0;
-  for (int i0 = 0; i0 < n; i0 += kB3) {   // point words only
-    uint32_t pt[kB3];
-#pragma unroll
-    for (int u = 0; u < kB3; u++) pt[u] = buf.pt(min(i0 + u, n - 1));
-#pragma unroll
-    for (int u = 0; u < kB3; u++) {
-      const double regdx = double(pt[u] & 0xFFFF) - x, regdy = double(pt[u] >> 16) - y;
-      const double l = regdx * dx + regdy * dy;
-      const double w = -regdx * dy + regdy * dx;
-      l_max = l > l_max ? l : l_max;
-      l_min = l < l_min ? l : l_min;
-      w_max = w > w_max ? w : w_max;
-      w_min = w < w_min ? w : w_min;
-    }
-  }
-  rec.x1 = x + l_min * dx;
-  rec.y1 = y + l_min * dy;
-  rec.x2 = x + l_max * dx;
-  rec.y2 = y + l_max * dy;
-  rec.width = w_max - w_min;
-  rec.x = x;
-  rec.y = y;
-  rec.theta = theta;
-  rec.dx = dx;
-  rec.dy = dy;
-  rec.prec = prec;
-  rec.p = p;
-  if (rec.width < 1.0) rec.width = 1.0;
 }
 
 // One pass of reduce_region_radius's removal scan (lsd.cpp reduce_region_radius:
@@ -1364,62 +815,6 @@ __device__ __forceinline__ bool lane_far(uint32_t pt, int xc, int yc, double rad
   const int dx = (int)(pt & 0xFFFF) - xc, dy = (int)(pt >> 16) - yc;
   return (double)(dx * dx + dy * dy) > radSq;
 }
-__device__ __forceinline__ int lane_reduce_pass(LaneBuf g1, int n, int xc, int yc,
-                                                double radSq, double& cx, double& cy,
-                                                double& csum) {
-  constexpr int kB = 8, kBb = 4;
-  int nn = 0;
-  for (int i0 = 0; i0 < n; i0 += kB) {
-    uint32_t e[kB];
-#pragma unroll
-    for (int u = 0; u < kB; u++) e[u] = g1.pt(min(i0 + u, n - 1));
-#pragma unroll
-    for (int u = 0; u < kB; u++) nn += (i0 + u < n && !lane_far(e[u], xc, yc, radSq)) ? 1 : 0;
-  }
-  if (nn == n) return n;
-  // the merge visits the final list in order, so it also sums region2rect's
-  // weighted centroid terms (its first pass, same order and operations)
-  uint4 bw[kBb];
-  int bcnt = 0, bpos = n - 1;
-  double x = 0, y = 0, sum = 0;
-  for (int f0 = 0; f0 < nn; f0 += kB) {
-    uint4 fw[kB];
-#pragma unroll
-    for (int u = 0; u < kB; u++) fw[u] = g1[min(f0 + u, nn - 1)];
-#pragma unroll
-    for (int u = 0; u < kB; u++) {
-      if (f0 + u >= nn) break;
-      uint4 e = fw[u];
-      if (lane_far(e.x, xc, yc, radSq)) {
-        uint4 b;
-        do {   // [nn, n) holds exactly as many near points as [0, nn) far ones
-          if (bcnt == 0) {
-#pragma unroll
-            for (int v = 0; v < kBb; v++) bw[v] = g1[max(bpos - v, nn)];
-            bcnt = kBb;
-          }
-          b = bw[0];
-#pragma unroll
-          for (int v = 0; v < kBb - 1; v++) bw[v] = bw[v + 1];
-          bcnt--;
-          bpos--;
-        } while (lane_far(b.x, xc, yc, radSq));
-        g1[f0 + u] = b;
-        g1.set_pt(bpos + 1, e.x);
-        e = b;
-      }
-      const double weight = entry_w(e);
-      x += double(pt_x(e)) * weight;
-      y += double(pt_y(e)) * weight;
-      sum += weight;
-    }
-  }
-  cx = x;
-  cy = y;
-  csum = sum;
-  return nn;
-}
-
 // Profiling build (-DORBPL_FIT_PROF): wall time of the fit's phases per
 // round, as seen by the lanes in them, reduced to the wave maximum per round
 // and printed for frame 0 (0 first rect, 1 refine statistics, 2 second grow,
@@ -1439,83 +834,6 @@ struct FitProf {
   __device__ __forceinline__ void lap(int) {}
 #endif
 };
-
-// refine + reduce_region_radius for a lane. The region [0, n) came from the
-// first grow; a second grow is appended after it. Returns the status; off /
-// len give the final region, touched the claimed prefix of the buffer.
-template <bool PF>
-__device__ __forceinline__ int lane_refine(const Frame& F, uint64_t* sd, LaneBuf buf, int n,
-                                           double reg_angle,
-                                           double prec, double p, Rect& rec, uint32_t myval1,
-                                           int& off, int& len, int& touched, FitProf& fp,
-                                           uint32_t* ring) {
-  const double density_th = 0.7;
-  double density = double(n) / (dist(rec.x1, rec.y1, rec.x2, rec.y2) * rec.width);
-  off = 0;
-  len = n;
-  touched = n;
-  if (density >= density_th) return kSpecCand;
-  const uint4 e0 = buf[0];
-  const int x0 = pt_x(e0), y0 = pt_y(e0);
-  const double xc = double(x0), yc = double(y0);
-  const double ang_c = deg2ang(entry_deg(e0));
-  double sum = 0, s_sum = 0;
-  int cnt = 0;
-  for (int i0 = 0; i0 < n; i0 += 8) {
-    uint4 e[8];
-#pragma unroll
-    for (int u = 0; u < 8; u++) e[u] = buf[min(i0 + u, n - 1)];
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-      if (i0 + u < n && dist(xc, yc, pt_x(e[u]), pt_y(e[u])) < rec.width) {
-        const double ang_d = angle_diff_signed(deg2ang(entry_deg(e[u])), ang_c);
-        sum += ang_d;
-        s_sum += ang_d * ang_d;
-        ++cnt;
-      }
-    }
-  }
-  const double mean_angle = sum / double(cnt);
-  const double tau =
-      2.0 * sqrt((s_sum - 2.0 * mean_angle * sum) / double(cnt) + mean_angle * mean_angle);
-  LaneBuf g1 = buf + n;
-  fp.lap(1);
-  int n1;
-#if ORBPL_GROW_LEAN && ORBPL_GROW_CS && ORBPL_SD_PAIRED
-  if constexpr (PF) n1 = lane_grow_pf(F, sd, g1, kLaneCap - n, x0, y0, reg_angle, tau, myval1, ring);
-  else
-#endif
-  n1 = lane_grow(F, sd, g1, kLaneCap - n, x0, y0, reg_angle, tau, myval1);
-  fp.lap(2);
-  if (n1 < 0) return n1;
-  off = n;
-  len = n1;
-  touched = n + n1;
-  if (n1 < 2) return kSpecFail;
-  lane_rect(g1, n1, reg_angle, prec, p, rec, F.q, F.sw);
-  density = double(n1) / (dist(rec.x1, rec.y1, rec.x2, rec.y2) * rec.width);
-  fp.lap(3);
-  if (density >= density_th) return kSpecCand;
-  // reduce_region_radius
-  const double radSq1 = distSq(xc, yc, rec.x1, rec.y1);
-  const double radSq2 = distSq(xc, yc, rec.x2, rec.y2);
-  double radSq = radSq1 > radSq2 ? radSq1 : radSq2;
-  while (density < density_th) {
-    radSq *= 0.75 * 0.75;
-    const int n_prev = n1;
-    double cx, cy, csum;
-    n1 = lane_reduce_pass(g1, n1, x0, y0, radSq, cx, cy, csum);
-    len = n1;
-    if (n1 < 2) return kSpecFail;
-    // nothing removed: the list is untouched, so region2rect would return the
-    // same rectangle and density
-    if (n1 == n_prev) continue;
-    lane_rect_tail(g1, n1, cx, cy, csum, reg_angle, prec, p, rec);
-    density = double(n1) / (dist(rec.x1, rec.y1, rec.x2, rec.y2) * rec.width);
-  }
-  fp.lap(4);
-  return kSpecCand;
-}
 
 // ---------------------------------------------------------------------------
 // NFA validation with one lane per rectangle (k_lsd_validate): most
@@ -1912,7 +1230,7 @@ constexpr int kSpecSmallBatch = ORBPL_SPEC_SMALL_BATCH;
 #ifndef ORBPL_SPEC_MINW
 #define ORBPL_SPEC_MINW 3
 #endif
-// ORBPL_SPEC_KEEP (one wave per frame): a round ends at its first seed whose
+// Carried seeds (one wave per frame): a round ends at its first seed whose
 // region met an earlier seed's claim; the later seeds of the window whose
 // claim re-check passed keep their regions and fits for the next round
 // instead of growing them again. Their results are the reference's unless a
@@ -1925,38 +1243,27 @@ constexpr int kSpecSmallBatch = ORBPL_SPEC_SMALL_BATCH;
 // buffer travels with its seed (bufid). After a cooperative fallback nothing
 // is carried (the fallback uses buffer 0 as scratch).
 // ---------------------------------------------------------------------------
-// Wave-cooperative fit (ORBPL_COOP_FIT). After a round's grows, the fits of
-// the regions that reach min_reg_size (~4 per round) run one region at a time
-// across the whole wave instead of one lane per region while the other lanes
-// wait. A fit is a chain of passes over the region's list - region2rect's
-// centroid, inertia and extent passes, refine's angle statistics,
-// reduce_region_radius' count and merge - whose per-point work is independent
-// and whose sums are ordered double sums: the wave computes 64 points' terms
-// at once, then every lane adds them in list order from LDS, so each sum
-// rounds exactly as the sequential loop's (the extents and the counts are
-// order-free). refine's second region grow stays one lane per region (the
-// round's refining lanes at once, as before).
+// Wave-wide fits. After a round's grows, the fits of the regions that reach
+// min_reg_size (~4 per round) keep the per-lane control flow, but every pass
+// over a region's list - region2rect's centroid, inertia and extent passes,
+// refine's angle statistics, reduce_region_radius' count and merge - has
+// independent per-point work and ordered double sums: the wave computes 64
+// points' terms at once, then the sums are added in list order from LDS, so
+// each rounds exactly as the sequential loop's (the extents and the counts
+// are order-free). refine's second region grow stays one lane per region.
+// Measured on three boxes against per-lane fits (round 4, bit-exact): LSD
+// batch 1 44.0-47.4 vs 44.4-51.5 ms, batch 16 51.8-53.1 vs 54.6-55.5 ms,
+// batch 1536 115.3 vs 118.8 ms. One region at a time across the whole wave
+// measured no faster (the per-region fixed costs outweigh the parallel
+// points). The A/B records are under profiles/r04/.
 // ---------------------------------------------------------------------------
-// 0: per lane; 1: one fitting region at a time across the wave (bit-exact,
-// measured no faster: the per-region fixed costs and the serialised regions
-// outweigh the parallel points); 2: per-lane fits with wave-wide passes, the
-// default: bit-exact (26 LSD tests, the -m gpu suite), measured on three boxes
-// (tools/gpu_r04_{m,o,p}.sh) LSD batch 1 44.0-47.4 vs 44.4-51.5 ms, batch 16
-// 51.8-53.1 vs 54.6-55.5 ms, batch 1536 115.3 vs 118.8 ms (the fit phase
-// 47-51M vs 49-60M cycles per frame)
-#ifndef ORBPL_COOP_FIT
-#define ORBPL_COOP_FIT 2
-#endif
 
-// fitters whose terms share LDS at once (ORBPL_COOP_FIT=2)
+// fitters whose terms share LDS at once
 constexpr int kCoopG = 4;
 struct CoopScratch {
   union {
-    struct {
-      double a[64], b[64], c[64];
-    };
-    struct {   // ORBPL_COOP_FIT=2: one row per fitter of a group, padded so that
-               // the lanes' rows start in different banks
+    struct {   // one row per fitter of a group, padded so that the lanes'
+               // rows start in different banks
       double ga[kCoopG][65], gb[kCoopG][65], gc[kCoopG][65];
     };
     struct {
@@ -1971,232 +1278,11 @@ __device__ __forceinline__ void coop_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-// A += a_k, B += b_k, C += c_k (C -= c_k with kSubC), k = 0 .. cnt-1 in order,
-// term k held by lane k; every lane ends with the same sums
-template <bool kSubC>
-__device__ __forceinline__ void coop_add3(CoopScratch& S, int lane, int cnt, double ta, double tb,
-                                          double tc, double& A, double& B, double& C) {
-  S.a[lane] = ta;
-  S.b[lane] = tb;
-  S.c[lane] = tc;
-  coop_lds_sync();
-  int k = 0;
-  for (; k + 4 <= cnt; k += 4) {
-    double xa[4], xb[4], xc[4];
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      xa[u] = S.a[k + u];
-      xb[u] = S.b[k + u];
-      xc[u] = S.c[k + u];
-    }
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      A += xa[u];
-      B += xb[u];
-      C = kSubC ? C - xc[u] : C + xc[u];
-    }
-  }
-  for (; k < cnt; k++) {
-    A += S.a[k];
-    B += S.b[k];
-    C = kSubC ? C - S.c[k] : C + S.c[k];
-  }
-  coop_lds_sync();   // every lane has read the terms before the next pass writes
-}
-
 __device__ __forceinline__ int coop_rl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 __device__ __forceinline__ double coop_rl(double v, int l) {
   return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
                           __builtin_amdgcn_readlane(__double2loint(v), l));
 }
-__device__ __forceinline__ double coop_max(double v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    const double u = __shfl_xor(v, o, 64);
-    v = u > v ? u : v;
-  }
-  return v;
-}
-__device__ __forceinline__ double coop_min(double v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    const double u = __shfl_xor(v, o, 64);
-    v = u < v ? u : v;
-  }
-  return v;
-}
-
-// region2rect's first pass (lane_rect): the weighted centroid sums over list
-// [0, n) in order; with q the weights are computed (modgrad) and stored into
-// the entries first
-__device__ __forceinline__ void coop_centroid(CoopScratch& S, int lane, LaneBuf bf, int n,
-                                              const int* __restrict__ q, int sw, double& x,
-                                              double& y, double& sum) {
-  x = 0;
-  y = 0;
-  sum = 0;
-  for (int i0 = 0; i0 < n; i0 += 64) {
-    const int i = i0 + lane;
-    double ta = 0, tb = 0, tc = 0;
-    if (i < n) {
-      uint32_t pt;
-      double w;
-      if (q) {
-        pt = bf.pt(i);
-        w = modgrad_q(q[(int)(pt >> 16) * sw + (int)(pt & 0xFFFF)]);
-        bf.set_w(i, w);
-      } else {
-        const uint4 e = bf[i];
-        pt = e.x;
-        w = entry_w(e);
-      }
-      ta = double(pt & 0xFFFF) * w;
-      tb = double(pt >> 16) * w;
-      tc = w;
-    }
-    coop_add3<false>(S, lane, min(64, n - i0), ta, tb, tc, x, y, sum);
-  }
-}
-
-// lane_rect_tail across the wave: inertia sums in order, theta, extents
-__device__ __forceinline__ void coop_rect_tail(CoopScratch& S, int lane, LaneBuf bf, int n,
-                                               double x, double y, double sum, double reg_angle,
-                                               double prec, double p, Rect& rec) {
-  x /= sum;
-  y /= sum;
-  double Ixx = 0.0, Iyy = 0.0, Ixy = 0.0;
-  for (int i0 = 0; i0 < n; i0 += 64) {
-    const int i = i0 + lane;
-    double ta = 0, tb = 0, tc = 0;
-    if (i < n) {
-      const uint4 e = bf[i];
-      const double weight = entry_w(e);
-      const double dx = double(pt_x(e)) - x, dy = double(pt_y(e)) - y;
-      ta = dy * dy * weight;
-      tb = dx * dx * weight;
-      tc = dx * dy * weight;
-    }
-    coop_add3<true>(S, lane, min(64, n - i0), ta, tb, tc, Ixx, Iyy, Ixy);
-  }
-  const double lambda = 0.5 * (Ixx + Iyy - sqrt((Ixx - Iyy) * (Ixx - Iyy) + 4.0 * Ixy * Ixy));
-  double theta = (fabs(Ixx) > fabs(Iyy)) ? double(fast_atan2_deg(float(lambda - Ixx), float(Ixy)))
-                                         : double(fast_atan2_deg(float(Ixy), float(lambda - Iyy)));
-  theta *= kDegToRad;
-  if (fabs(angle_diff_signed(theta, reg_angle)) > prec) theta += kPi;
-  const double dx = lsdm::cos_(theta), dy = lsdm::sin_(theta);
-  // l_max / l_min (and w) start at 0: independent max / min, any order
-  double l_min = 0, l_max = 0, w_min = 0, w_max = 0;
-  for (int i0 = 0; i0 < n; i0 += 64) {
-    const int i = i0 + lane;
-    if (i < n) {
-      const uint32_t pt = bf.pt(i);
-      const double regdx = double(pt & 0xFFFF) - x, regdy = double(pt >> 16) - y;
-      const double l = regdx * dx + regdy * dy;
-      const double w = -regdx * dy + regdy * dx;
-      l_max = l > l_max ? l : l_max;
-      l_min = l < l_min ? l : l_min;
-      w_max = w > w_max ? w : w_max;
-      w_min = w < w_min ? w : w_min;
-    }
-  }
-  l_max = coop_max(l_max);
-  l_min = coop_min(l_min);
-  w_max = coop_max(w_max);
-  w_min = coop_min(w_min);
-  rec.x1 = x + l_min * dx;
-  rec.y1 = y + l_min * dy;
-  rec.x2 = x + l_max * dx;
-  rec.y2 = y + l_max * dy;
-  rec.width = w_max - w_min;
-  rec.x = x;
-  rec.y = y;
-  rec.theta = theta;
-  rec.dx = dx;
-  rec.dy = dy;
-  rec.prec = prec;
-  rec.p = p;
-  if (rec.width < 1.0) rec.width = 1.0;
-}
-
-// refine's angle statistics over list [0, n) (lane_refine): tau
-__device__ __forceinline__ double coop_tau(CoopScratch& S, int lane, LaneBuf bf, int n,
-                                           const Rect& rec) {
-  const uint4 e0 = bf[0];
-  const double xc = double(pt_x(e0)), yc = double(pt_y(e0));
-  const double ang_c = deg2ang(entry_deg(e0));
-  double sum = 0, s_sum = 0, unused = 0;
-  int cnt = 0;
-  for (int i0 = 0; i0 < n; i0 += 64) {
-    const int i = i0 + lane;
-    double ta = 0, tb = 0;
-    bool in = false;
-    if (i < n) {
-      const uint4 e = bf[i];
-      if (dist(xc, yc, pt_x(e), pt_y(e)) < rec.width) {
-        const double ang_d = angle_diff_signed(deg2ang(entry_deg(e)), ang_c);
-        ta = ang_d;
-        tb = ang_d * ang_d;
-        in = true;
-      }
-    }
-    cnt += __popcll(__ballot(in));
-    // a point outside adds +0.0: the sums start at +0 and never become -0,
-    // so x + 0.0 == x, the same as skipping it
-    coop_add3<false>(S, lane, min(64, n - i0), ta, tb, 0.0, sum, s_sum, unused);
-  }
-  const double mean_angle = sum / double(cnt);
-  return 2.0 * sqrt((s_sum - 2.0 * mean_angle * sum) / double(cnt) + mean_angle * mean_angle);
-}
-
-// lane_reduce_pass across the wave: the near count, the merge (the k-th far
-// point of [0, nn) in index order takes the k-th near point of [nn, n)
-// counted from the end; that slot keeps the far point's word) and the
-// centroid sums of the final [0, nn) in order. Returns nn (n: nothing removed,
-// no sums).
-__device__ __forceinline__ int coop_reduce(CoopScratch& S, int lane, LaneBuf g1, int n, int xc,
-                                           int yc, double radSq, double& cx, double& cy,
-                                           double& csum) {
-  const unsigned long long lt = (1ull << lane) - 1ull;
-  int nn = 0;
-  for (int i0 = 0; i0 < n; i0 += 64) {
-    const int i = i0 + lane;
-    const bool nr = i < n && !lane_far(g1.pt(i), xc, yc, radSq);
-    nn += __popcll(__ballot(nr));
-  }
-  if (nn == n) return n;
-  int m = 0;
-  for (int i0 = 0; i0 < nn; i0 += 64) {
-    const int i = i0 + lane;
-    const bool fr = i < nn && lane_far(g1.pt(i), xc, yc, radSq);
-    const unsigned long long mk = __ballot(fr);
-    if (fr) S.farpos[m + __popcll(mk & lt)] = (uint16_t)i;
-    m += __popcll(mk);
-  }
-  int m2 = 0;
-  for (int j0 = 0; j0 < n - nn; j0 += 64) {
-    const int j = n - 1 - (j0 + lane);
-    const bool nr = j >= nn && !lane_far(g1.pt(j), xc, yc, radSq);
-    const unsigned long long mk = __ballot(nr);
-    if (nr) S.nearpos[m2 + __popcll(mk & lt)] = (uint16_t)j;
-    m2 += __popcll(mk);
-  }
-  coop_lds_sync();
-  for (int k0 = 0; k0 < m; k0 += 64) {
-    const int k = k0 + lane;
-    if (k < m) {
-      const int i = S.farpos[k], j = S.nearpos[k];
-      const uint32_t farw = g1.pt(i);
-      const uint4 b = g1[j];
-      g1[i] = b;
-      g1.set_pt(j, farw);
-    }
-  }
-  wg_fence();
-  __builtin_amdgcn_wave_barrier();
-  coop_centroid(S, lane, g1, nn, nullptr, 0, cx, cy, csum);
-  return nn;
-}
-
 __device__ __forceinline__ uint4* coop_rl(uint4* v, int l) {
   const uintptr_t u = reinterpret_cast<uintptr_t>(v);
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
@@ -2204,19 +1290,15 @@ __device__ __forceinline__ uint4* coop_rl(uint4* v, int l) {
   return reinterpret_cast<uint4*>(((uintptr_t)hi << 32) | lo);
 }
 
-// ORBPL_COOP_FIT=2: the fits stay one lane per region (the round's fitting
-// lanes together, as the per-lane code), but every pass's per-point work is
+// The fits stay one lane per region (the round's fitting lanes together),
+// but every pass's per-point work is
 // spread over the whole wave: for a group of up to kCoopG fitting lanes and
 // a window of 64 points, the wave evaluates each lane's 64 terms in turn
 // (term(f, i, ...) with f the owning lane) into that lane's LDS row, then
 // every lane of the group adds its own row in point order. The sums round as
 // the sequential loop's; the serial part per point is three LDS reads and
 // three adds instead of the point's whole load / weight / product chain.
-// ORBPL_COOP_CHAIN: the three sums of a slot on three lanes (1) or all on
-// the fitter's lane (0; A/B build override)
-#ifndef ORBPL_COOP_CHAIN
-#define ORBPL_COOP_CHAIN 1
-#endif
+// The three sums of a slot run on three lanes.
 template <bool kSubC, class Load, class Term>
 __device__ __forceinline__ void group_sums(CoopScratch& S, int lane, bool act, int n, double& A,
                                            double& B, double& C, Load load, Term term) {
@@ -2236,7 +1318,6 @@ __device__ __forceinline__ void group_sums(CoopScratch& S, int lane, bool act, i
     }
     const bool ing = (gm >> lane) & 1ull;
     const int myslot = __popcll(gm & ((1ull << lane) - 1ull));
-#if ORBPL_COOP_CHAIN
     // chain lanes: lane c * kCoopG + s adds sum c (A, B, C) of slot s, so a
     // point's three ordered adds run on three lanes at once; C's terms are
     // stored negated where the sum subtracts (x - y == x + (-y) exactly)
@@ -2252,7 +1333,6 @@ __device__ __forceinline__ void group_sums(CoopScratch& S, int lane, bool act, i
                  c0 = shfl_d(C, max(myf, 0));
     double acc = cc == 0 ? a0 : (cc == 1 ? b0 : c0);
     const double* prow = cc == 0 ? S.ga[cs] : (cc == 1 ? S.gb[cs] : S.gc[cs]);
-#endif
     int nmax = ing ? n : 0;
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) nmax = max(nmax, __shfl_xor(nmax, o, 64));
@@ -2270,11 +1350,10 @@ __device__ __forceinline__ void group_sums(CoopScratch& S, int lane, bool act, i
           term(fs[s], i, v[s], ta, tb, tc);
           S.ga[s][lane] = ta;
           S.gb[s][lane] = tb;
-          S.gc[s][lane] = (ORBPL_COOP_CHAIN && kSubC) ? -tc : tc;
+          S.gc[s][lane] = kSubC ? -tc : tc;
         }
       }
       coop_lds_sync();
-#if ORBPL_COOP_CHAIN
       if (chain) {
         const int cnt = min(64, mynf - k0);
         int k = 0;
@@ -2287,38 +1366,8 @@ __device__ __forceinline__ void group_sums(CoopScratch& S, int lane, bool act, i
         }
         for (; k < cnt; k++) acc += prow[k];
       }
-#else
-      if (ing) {
-        const int cnt = min(64, n - k0);
-        const double* pa = S.ga[myslot];
-        const double* pb = S.gb[myslot];
-        const double* pc = S.gc[myslot];
-        int k = 0;
-        for (; k + 4 <= cnt; k += 4) {
-          double xa[4], xb[4], xc[4];
-#pragma unroll
-          for (int u = 0; u < 4; u++) {
-            xa[u] = pa[k + u];
-            xb[u] = pb[k + u];
-            xc[u] = pc[k + u];
-          }
-#pragma unroll
-          for (int u = 0; u < 4; u++) {
-            A += xa[u];
-            B += xb[u];
-            C = kSubC ? C - xc[u] : C + xc[u];
-          }
-        }
-        for (; k < cnt; k++) {
-          A += pa[k];
-          B += pb[k];
-          C = kSubC ? C - pc[k] : C + pc[k];
-        }
-      }
-#endif
       coop_lds_sync();
     }
-#if ORBPL_COOP_CHAIN
     // the chain lanes' sums back to their fitters
     const double ra = shfl_d(acc, myslot), rb = shfl_d(acc, kCoopG + myslot),
                  rc = shfl_d(acc, 2 * kCoopG + myslot);
@@ -2327,7 +1376,6 @@ __device__ __forceinline__ void group_sums(CoopScratch& S, int lane, bool act, i
       B = rb;
       C = rc;
     }
-#endif
   }
 }
 
@@ -2502,85 +1550,8 @@ __device__ __forceinline__ void group_merge(CoopScratch& S, int lane, LaneBuf g1
   coop_lds_sync();
 }
 
-// ORBPL_COOP_GROW2: refine's second region grow one region at a time on
-// the whole wave (the round's refining lanes one after another) instead of
-// one lane per region: per step the 8 neighbour words of the point being
-// expanded are loaded by 8 lanes at once and their flags and angles formed
-// in parallel; the in-order walk (the aligned test against the current
-// region angle, the claim, the add) runs on wave-uniform values, the same
-// operations in the same order as lane_grow.
-#ifndef ORBPL_COOP_GROW2
-#define ORBPL_COOP_GROW2 0
-#endif
-__device__ __forceinline__ uint32_t coop_rlu(uint32_t v, int l) {
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
-}
-__device__ int wave_grow(const Frame& F, uint64_t* sd, LaneBuf buf, int cap, int sx, int sy,
-                         double& reg_angle, double prec, uint32_t myval, int lane) {
-  const uint32_t mytag = myval >> 1;
-  const int sw = F.sw, sh = F.sh, tw = F.tw;
-  const int si = lsd_sd_index(sx, sy, tw);
-  if (cap < 1) return kSpecOverflow;
-  const uint64_t v0 = ld_sd(sd + si);
-  const uint32_t v0lo = coop_rlu((uint32_t)v0, 0), v0hi = coop_rlu((uint32_t)(v0 >> 32), 0);
-  if ((v0hi >> 1) < mytag) return kSpecConflict;
-  if (lane == 0)
-    atomicMin(reinterpret_cast<unsigned long long*>(sd + si),
-              ((unsigned long long)myval << 32) | v0lo);
-  uint4 cur = make_uint4((uint32_t)sx | ((uint32_t)sy << 16), v0lo, 0u, 0u);
-  if (lane == 0) buf[0] = cur;
-  reg_angle = deg2ang(entry_deg(cur));
-  double s0, c0;
-  lsdm::sincos_(reg_angle, &s0, &c0);
-  float sumdx = (float)c0;
-  float sumdy = (float)s0;
-  const double k3pi2 = (3 * kPi) / 2, k2pi = 2 * kPi;
-  // lane k < 9 handles neighbour k = (dy + 1) * 3 + (dx + 1)
-  const int kdx = lane % 3 - 1, kdy = lane / 3 - 1;
-  const bool klane = lane < 9 && lane != 4;
-  int n = 1;
-  for (int i = 0; i < n; i++) {
-    const int x = pt_x(cur), y = pt_y(cur);
-    const int n_start = n;
-    const uint4 pref = buf[min(i + 1, n_start - 1)];
-    const int xx = x + kdx, yy = y + kdy;
-    const bool in = klane && xx >= 0 && xx < sw && yy >= 0 && yy < sh;
-    uint4 w = make_uint4(0u, 0u, 0u, 0u);
-    if (in) w = *reinterpret_cast<const uint4*>(sd + lsd_sd_index(xx, yy, tw));
-    const bool flag = in && w.y != 0u && w.y != myval && __uint_as_float(w.x) >= 0.f;
-    const double ang = deg2ang(__uint_as_float(w.x));
-    unsigned okm = (unsigned)__ballot(flag);
-    uint4 first_add = cur;
-    while (okm) {
-      const int k = __ffs((int)okm) - 1;
-      okm &= okm - 1;
-      // aligned_deg(d, reg_angle, prec) for a defined d (lane_grow's test)
-      double nt = fabs(reg_angle - coop_rl(ang, k));
-      nt = nt > k3pi2 ? fabs(nt - k2pi) : nt;
-      if (nt <= prec) {
-        const uint32_t wx = coop_rlu(w.x, k), wy = coop_rlu(w.y, k);
-        if ((wy >> 1) < mytag) return kSpecConflict;   // an earlier seed's pixel
-        const int ax = x + (k % 3) - 1, ay = y + (k / 3) - 1;
-        if (lane == 0)
-          atomicMin(reinterpret_cast<unsigned long long*>(sd + lsd_sd_index(ax, ay, tw)),
-                    ((unsigned long long)myval << 32) | wx);
-        if (n >= cap) return kSpecOverflow;
-        const uint4 e = make_uint4((uint32_t)ax | ((uint32_t)ay << 16), wx, 0u, 0u);
-        if (n == n_start) first_add = e;
-        if (lane == 0) buf[n] = e;
-        n++;
-        sumdx += __uint_as_float(coop_rlu(w.z, k));   // add_angle(d) terms
-        sumdy += __uint_as_float(coop_rlu(w.w, k));
-        reg_angle = (double)fast_atan2_deg_1div(sumdy, sumdx) * kDegToRad;
-      }
-    }
-    cur = (i + 1 < n_start) ? pref : first_add;
-  }
-  return n;
-}
-
-// ORBPL_COOP_FIT=2: the round's fits with the per-lane control flow of
-// lane_rect + lane_refine and the wave-wide passes above
+// The round's fits: region2rect + refine + reduce_region_radius with the
+// per-lane control flow and the wave-wide passes above
 __device__ __forceinline__ void group_fit(CoopScratch& S, int lane, bool fitter, int n,
                                           double reg_angle, uint4* fbuf, int bufid,
                                           const Frame& F, uint64_t* sd, double prec, double p,
@@ -2614,21 +1585,7 @@ __device__ __forceinline__ void group_fit(CoopScratch& S, int lane, bool fitter,
     x0 = pt_x(e0);
     y0 = pt_y(e0);
   }
-  if constexpr (ORBPL_COOP_GROW2) {
-    for (unsigned long long m = __ballot(refine); m; m &= m - 1) {
-      const int f = __ffsll((long long)m) - 1;
-      const int nf = coop_rl(n, f);
-      double ra = 0;
-      const int r = wave_grow(F, sd, LaneBuf{coop_rl(bp, f) + nf}, kLaneCap - nf, coop_rl(x0, f),
-                              coop_rl(y0, f), ra, coop_rl(tau, f), coop_rlu(myval1, f), lane);
-      if (lane == f) {
-        n1 = r;
-        ra2 = ra;
-      }
-    }
-    wg_fence();
-    __builtin_amdgcn_wave_barrier();
-  } else if (refine) {
+  if (refine) {
     n1 = lane_grow(F, sd, buf + n, kLaneCap - n, x0, y0, ra2, tau, myval1);
   }
   if (refine) {
@@ -2707,119 +1664,9 @@ __device__ __forceinline__ void group_fit(CoopScratch& S, int lane, bool fitter,
   fp.lap(4);
 }
 
-// The round's fits (lane_rect + lane_refine of every lane with n >=
-// min_reg_size), all lanes of the wave active. Per lane in: fitter, n,
-// reg_angle (the first grow's), buf; out: status, rec, off, len, touched
-// (fitters only).
-__device__ __forceinline__ void coop_fit(CoopScratch& S, int lane, bool fitter, int n,
-                                         double reg_angle, uint4* fbuf, int bufid, const Frame& F,
-                                         uint64_t* sd, double prec, double p, uint32_t myval1,
-                                         int& status, Rect& rec, int& off, int& len,
-                                         int& touched) {
-  bool need = false;
-  double tau = 0;
-  // the first region's rectangle and, where refine runs, its statistics
-  for (unsigned long long m = __ballot(fitter); m; m &= m - 1) {
-    const int f = __ffsll((long long)m) - 1;
-    const int nf = coop_rl(n, f);
-    const double ra = coop_rl(reg_angle, f);
-    const LaneBuf bf{fbuf + (long long)coop_rl(bufid, f) * kLaneCap};
-    double cx, cy, cs;
-    coop_centroid(S, lane, bf, nf, F.q, F.sw, cx, cy, cs);
-    wg_fence();
-    __builtin_amdgcn_wave_barrier();
-    Rect r;
-    coop_rect_tail(S, lane, bf, nf, cx, cy, cs, ra, prec, p, r);
-    const double density = double(nf) / (dist(r.x1, r.y1, r.x2, r.y2) * r.width);
-    const bool nd = density < 0.7;
-    const double tf = nd ? coop_tau(S, lane, bf, nf, r) : 0.0;
-    if (lane == f) {
-      rec = r;
-      off = 0;
-      len = nf;
-      touched = nf;
-      status = kSpecCand;
-      need = nd;
-      tau = tf;
-    }
-  }
-  // refine's second grow, one lane per refining region
-  const LaneBuf buf{fbuf + (long long)bufid * kLaneCap};
-  int n1 = 0;
-  double ra2 = reg_angle;
-  if (need) {
-    const uint4 e0 = buf[0];
-    n1 = lane_grow(F, sd, buf + n, kLaneCap - n, pt_x(e0), pt_y(e0), ra2, tau, myval1);
-    if (n1 < 0) {
-      status = n1;
-      need = false;
-    } else {
-      off = n;
-      len = n1;
-      touched = n + n1;
-      if (n1 < 2) {
-        status = kSpecFail;
-        need = false;
-      }
-    }
-  }
-  __builtin_amdgcn_wave_barrier();
-  // the second region's rectangle and reduce_region_radius
-  for (unsigned long long m = __ballot(need); m; m &= m - 1) {
-    const int f = __ffsll((long long)m) - 1;
-    const int nf = coop_rl(n, f);
-    const int n1f = coop_rl(n1, f);
-    const double ra = coop_rl(ra2, f);
-    const LaneBuf b0{fbuf + (long long)coop_rl(bufid, f) * kLaneCap};
-    const LaneBuf g1 = b0 + nf;
-    const uint4 e0 = b0[0];
-    const int x0 = pt_x(e0), y0 = pt_y(e0);
-    double cx, cy, cs;
-    coop_centroid(S, lane, g1, n1f, F.q, F.sw, cx, cy, cs);
-    wg_fence();
-    __builtin_amdgcn_wave_barrier();
-    Rect r;
-    coop_rect_tail(S, lane, g1, n1f, cx, cy, cs, ra, prec, p, r);
-    double density = double(n1f) / (dist(r.x1, r.y1, r.x2, r.y2) * r.width);
-    int st = kSpecCand, lf = n1f;
-    if (density < 0.7) {
-      const double xc = double(x0), yc = double(y0);
-      const double radSq1 = distSq(xc, yc, r.x1, r.y1);
-      const double radSq2 = distSq(xc, yc, r.x2, r.y2);
-      double radSq = radSq1 > radSq2 ? radSq1 : radSq2;
-      while (density < 0.7) {
-        radSq *= 0.75 * 0.75;
-        const int n_prev = lf;
-        lf = coop_reduce(S, lane, g1, lf, x0, y0, radSq, cx, cy, cs);
-        if (lf < 2) {
-          st = kSpecFail;
-          break;
-        }
-        if (lf == n_prev) continue;
-        coop_rect_tail(S, lane, g1, lf, cx, cy, cs, ra, prec, p, r);
-        density = double(lf) / (dist(r.x1, r.y1, r.x2, r.y2) * r.width);
-      }
-    }
-    if (lane == f) {
-      rec = r;
-      status = st;
-      len = lf;
-    }
-  }
-}
 
 #ifndef ORBPL_SPEC_WIN
 #define ORBPL_SPEC_WIN 64
-#endif
-// ORBPL_SCAN2: the one-wave seed scan reads two list windows per iteration
-// (A/B build override). Measured (tools/gpu_r04_aa.sh, bit-exact): the scans
-// 3.3M -> 3.1M cycles per frame at batch 1 (~0.1 ms), but 1536 frames 106.5 ->
-// 108.9 ms (the 128-VGPR instance spills more), so off
-#ifndef ORBPL_SCAN2
-#define ORBPL_SCAN2 0
-#endif
-#ifndef ORBPL_SPEC_KEEP
-#define ORBPL_SPEC_KEEP 1
 #endif
 // the block's first index >= j whose bit is set in the per-wave masks, or n
 template <int W>
@@ -2847,7 +1694,7 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
   constexpr int SL = 64 * W;
   // seeds per round (one-wave variant: ORBPL_SPEC_WIN, an A/B build override)
   constexpr int WIN = W == 1 ? ORBPL_SPEC_WIN : SL;
-  constexpr bool KEEP = W == 1 && ORBPL_SPEC_KEEP && !ORBPL_LBUF_INTERLEAVED;
+  constexpr bool KEEP = W == 1;
   extern __shared__ uint32_t grow_smem[];
   __shared__ uint32_t s_pt[SL];
   __shared__ int s_pos[SL];
@@ -2855,14 +1702,7 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
   __shared__ int s_cnt[2][W];
   __shared__ unsigned long long s_cm[W], s_km[W];
   __shared__ int s_misc[2];   // next_pos, status of the stop seed / nl after a fallback
-#if ORBPL_GROW_LEAN && ORBPL_GROW_CS && ORBPL_SD_PAIRED
-  constexpr bool PF = ORBPL_GROW_PF && W == 1 && MINW == 1;   // the small-batch instance
-#else
-  constexpr bool PF = false;
-#endif
-  __shared__ uint32_t s_ring[PF ? 64 * kRing : 1];
-  constexpr bool COOP = ORBPL_COOP_FIT && !PF && !ORBPL_LBUF_INTERLEAVED;
-  __shared__ CoopScratch s_coop[COOP ? W : 1];
+  __shared__ CoopScratch s_coop[W];
   const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int sw = g.sw, sh = g.sh;
   Frame F;
@@ -2893,7 +1733,6 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
   F.usd = sd;
   F.cs = sd + lsd_cs_offset(sw, sh);
   F.tw = lsd_sd_tw(sw);
-  static_assert(!ORBPL_LBUF_INTERLEAVED || W == 1, "interleaved lane lists: one wave per frame");
   int bufid = t;       // this lane's list buffer (KEEP: travels with a carried seed)
   bool keep = false;   // KEEP: the lane's seed, region and fit carried from the last round
   int ncarry = 0;      // KEEP: lanes [0, ncarry) hold carried seeds
@@ -2914,63 +1753,10 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
             n_coop = 0;
   const long long t_all = clock64();
   while (pos < nlist || ncarry > 0) {
-    const LaneBuf buf{fbuf + (ORBPL_LBUF_INTERLEAVED ? t : (long long)bufid * kLaneCap)};
+    const LaneBuf buf{fbuf + (long long)bufid * kLaneCap};
     // ---- the next SL defined, NOTUSED seeds in list order (after the
     // carried ones) ----
     int ncand = ncarry, scan = pos, next_pos = nlist;
-#if ORBPL_SCAN2
-    // one wave: two 64-entry windows per iteration, both windows' list and
-    // pixel-word loads in flight together (the stamps do not change during
-    // the scan, so window b read early equals window b read next iteration)
-    if constexpr (W == 1) {
-      while (ncand < WIN && scan < nlist) {
-        const int ia = scan + t, ib = scan + 64 + t;
-        const bool va = ia < nlist, vb = ib < nlist;
-        const uint32_t ea = va ? A[ia] : 0u, eb = vb ? A[ib] : 0u;
-        const int idxa = (int)(ea & 0x3FFFFFu), idxb = (int)(eb & 0x3FFFFFu);
-        const int pya = idxa / w1, pxa = idxa - pya * w1;
-        const int pyb = idxb / w1, pxb = idxb - pyb * w1;
-        uint64_t wa = 0, wb = 0;
-        if (va) wa = ld_sd(sd + lsd_sd_index(pxa, pya, F.tw));
-        if (vb) wb = ld_sd(sd + lsd_sd_index(pxb, pyb, F.tw));
-        const bool ca = va && __uint_as_float((uint32_t)wa) >= 0.f && (uint32_t)(wa >> 32) != 0u;
-        const bool cb = vb && __uint_as_float((uint32_t)wb) >= 0.f && (uint32_t)(wb >> 32) != 0u;
-        {
-          const unsigned long long m = __ballot(ca);
-          const int before = __popcll(m & lt_mask), cnt = __popcll(m);
-          if (ca && ncand + before < WIN) {
-            s_pt[ncand + before] = (uint32_t)pxa | ((uint32_t)pya << 16);
-            s_pos[ncand + before] = ia;
-          }
-          if (ncand + cnt >= WIN) {
-            const unsigned long long mm = __ballot(ca && before == WIN - ncand - 1);
-            next_pos = scan + __ffsll((long long)mm);
-            ncand = WIN;
-            break;
-          }
-          ncand += cnt;
-          scan += 64;
-        }
-        if (scan >= nlist) break;
-        {
-          const unsigned long long m = __ballot(cb);
-          const int before = __popcll(m & lt_mask), cnt = __popcll(m);
-          if (cb && ncand + before < WIN) {
-            s_pt[ncand + before] = (uint32_t)pxb | ((uint32_t)pyb << 16);
-            s_pos[ncand + before] = ib;
-          }
-          if (ncand + cnt >= WIN) {
-            const unsigned long long mm = __ballot(cb && before == WIN - ncand - 1);
-            next_pos = scan + __ffsll((long long)mm);
-            ncand = WIN;
-            break;
-          }
-          ncand += cnt;
-          scan += 64;
-        }
-      }
-    } else
-#endif
     while (ncand < WIN && scan < nlist) {
       const int i = scan + t;
       bool c = false;
@@ -3053,12 +1839,6 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
     int n = 0;
     if (t < ncand && !keep) {
       const uint32_t pt = s_pt[t];
-#if ORBPL_GROW_LEAN && ORBPL_GROW_CS && ORBPL_SD_PAIRED
-      if constexpr (PF)
-        n = lane_grow_pf(F, sd, buf, kLaneCap, (int)(pt & 0xFFFF), (int)(pt >> 16), reg_angle,
-                         prec, myval0, s_ring + lane * kRing);
-      else
-#endif
       n = lane_grow(F, sd, buf, kLaneCap, (int)(pt & 0xFFFF), (int)(pt >> 16), reg_angle, prec,
                     myval0);
     }
@@ -3070,7 +1850,8 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
       for (int o = 32; o >= 1; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
       max_steps += mx;
     }
-    if constexpr (COOP) {
+    {
+      // the round's fits: per-lane control flow, wave-wide passes (group_fit)
       const bool mine = t < ncand && !keep;
       if (mine && n < 0) {
         status = n;
@@ -3079,34 +1860,12 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
         len = n;
         touched = n;
       }
-      if constexpr (ORBPL_COOP_FIT == 2) {
-        FitProf fp;
-        group_fit(s_coop[wv], lane, mine && n >= g.min_reg_size, n, reg_angle, fbuf, bufid, F,
-                  sd, prec, p, myval1, status, rec, off, len, touched, fp);
+      FitProf fp;
+      group_fit(s_coop[wv], lane, mine && n >= g.min_reg_size, n, reg_angle, fbuf, bufid, F, sd,
+                prec, p, myval1, status, rec, off, len, touched, fp);
 #ifdef ORBPL_FIT_PROF
-        for (int k = 0; k < 5; k++) fpr[k] = fp.d[k];
+      for (int k = 0; k < 5; k++) fpr[k] = fp.d[k];
 #endif
-      } else
-        coop_fit(s_coop[wv], lane, mine && n >= g.min_reg_size, n, reg_angle, fbuf, bufid, F,
-                 sd, prec, p, myval1, status, rec, off, len, touched);
-    } else if (t < ncand && !keep) {
-      if (n < 0) {
-        status = n;
-      } else if (n < g.min_reg_size) {
-        status = kSpecSmall;
-        len = n;
-        touched = n;
-      } else {
-        FitProf fp;
-        fp.start();
-        lane_rect(buf, n, reg_angle, prec, p, rec, F.q, sw);
-        fp.lap(0);
-        status = lane_refine<PF>(F, sd, buf, n, reg_angle, prec, p, rec, myval1, off, len,
-                                 touched, fp, s_ring + lane * kRing);
-#ifdef ORBPL_FIT_PROF
-        for (int k = 0; k < 5; k++) fpr[k] = fp.d[k];
-#endif
-      }
     }
 #ifdef ORBPL_FIT_PROF
 #pragma unroll
@@ -3317,373 +2076,6 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
   }
 }
 
-// ---------------------------------------------------------------------------
-// The seed loop for small batches with its 64 speculative seeds per round
-// spread over 4 waves of 16 active lanes (one wave per SIMD): a round keeps the
-// one-wave loop's window (so its rounds and speculative regions), but each
-// wave's grow step executes the divergent add bodies of 16 regions instead of
-// 64 and the four waves issue on four SIMDs. Measured per round (one wave,
-// tools/gpu_r04_d.sh): 64 seeds 252k cycles, 32 seeds 190k, 16 seeds 119k.
-// Slot v = 16 * wave + lane (lanes 0-15) takes the v-th seed of the window;
-// claim tags rank by v, the commit walks the slots in order, and the kept
-// seeds of ORBPL_SPEC_KEEP are carried across waves through LDS. Only where
-// the GPU has spare SIMDs (batches of at most kSpecSparseBatch frames).
-// ---------------------------------------------------------------------------
-// Measured (tools/gpu_r04_e.sh, two rounds, bit-exact: 26 LSD tests): LSD
-// batch 1 / 16 / 64 / 96 = 48.8-52.7 / 68 / 69 / 69 ms against the one-wave
-// loop's 48.1-48.7 / 58 / 60 / 61 ms. Wave 0's grow phase fell 40-45M -> 28-33M
-// cycles per frame, but the round (grow + fit up to the last wave) rose
-// 252-280k -> 300k cycles: the four waves of a CU share its scalar unit and
-// instruction issue, and every wave runs the whole control flow (its exec-mask
-// SALU work, the per-round barriers), so their chains do not overlap as four
-// independent SIMDs would. Off (batch threshold 0); ORBPL_SPEC_SPARSE=<max
-// batch> turns it on for A/B runs.
-#ifndef ORBPL_SPEC_SPARSE_BATCH
-#define ORBPL_SPEC_SPARSE_BATCH 0
-#endif
-constexpr int kSpecSparseBatch = ORBPL_SPEC_SPARSE_BATCH;
-
-// the 64-bit slot mask of a per-thread predicate (false on lanes >= 16)
-__device__ __forceinline__ unsigned long long sp_vmask(bool pred, unsigned long long* s_vb, int wv,
-                                                       int lane) {
-  const unsigned long long b = __ballot(pred);
-  if (lane == 0) s_vb[wv] = (b & 0xFFFFull) << (16 * wv);
-  __syncthreads();
-  const unsigned long long m = s_vb[0] | s_vb[1] | s_vb[2] | s_vb[3];
-  __syncthreads();
-  return m;
-}
-__device__ __forceinline__ int sp_next(unsigned long long m, int j, int n) {
-  if (j >= 64) return n;
-  const unsigned long long r = m & ~((1ull << j) - 1ull);
-  return r ? min(n, __ffsll((long long)r) - 1) : n;
-}
-
-__global__ void __launch_bounds__(256, 1) k_lsd_spec_sparse(LsdGeom g, LsdScratch sc) {
-  constexpr int NS = 64;   // slots (seeds per round)
-  extern __shared__ uint32_t grow_smem[];
-  __shared__ uint32_t s_pt[NS], s_ptx[NS];
-  __shared__ int s_pos[NS], s_posx[NS], s_src[NS];
-  __shared__ int s_cnt[2][4];
-  __shared__ unsigned long long s_vb[4];
-  __shared__ int s_misc[2];
-  __shared__ int s_bufid[NS], s_status[NS], s_off[NS], s_len[NS], s_touched[NS], s_kp[NS];
-  __shared__ double s_rec[NS][12];
-  const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const bool act = lane < 16;
-  const int v = wv * 16 + (lane & 15);
-  const int sw = g.sw, sh = g.sh;
-  Frame F;
-  F.sw = sw;
-  F.sh = sh;
-  F.deg = sc.deg + (long long)f * lsd_deg_words(sw, sh);
-  F.dtw = lsd_deg_tw(sw);
-  F.q = sc.q + (long long)f * sw * sh;
-  F.used = nullptr;
-  uint4* fbuf = sc.lbuf + (long long)f * NS * kLaneCap;
-  uint32_t* coop = reinterpret_cast<uint32_t*>(fbuf);
-  F.reg_l = coop;
-  F.regq_l = reinterpret_cast<int*>(F.reg_l + kRegLds);
-  F.regd_l = reinterpret_cast<float*>(F.regq_l + kRegLds);
-  F.ring = F.regd_l + kRegLds;
-  F.reg_g = sc.reg + (long long)f * 3 * sw * sh;
-  F.rows = reinterpret_cast<int4*>(grow_smem);
-  F.rect0 = reinterpret_cast<Rect*>(F.rows);
-  F.rect1 = F.rect0 + 1;
-  F.row_cap = 0;
-  F.log_nt = g.log_nt;
-  F.lane = lane;
-  F.pf_cyc = 0;
-  F.pf_cnt = 0;
-  uint64_t* sd = sc.sd + (long long)f * lsd_sd_frame_words(sw, sh);
-  F.usd = sd;
-  F.cs = sd + lsd_cs_offset(sw, sh);
-  F.tw = lsd_sd_tw(sw);
-  int bufid = v;       // the slot's list buffer (travels with a carried seed)
-  bool keep = false;   // the slot's seed, region and fit carried from the last round
-  int ncarry = 0;      // slots [0, ncarry) hold carried seeds
-  int status = kSpecConflict, off = 0, len = 0, touched = 0;
-  Rect rec;
-  const uint32_t* A = sc.A + (long long)f * g.n;
-  const int nlist = sc.sort_nge[f];
-  double* cand_out = sc.cand + (long long)f * kLsdMaxCand * 12;
-  const int w1 = sw - 1;
-  const double prec = g.prec, p = g.p;
-  const unsigned long long lt_mask = (1ull << lane) - 1ull;
-  const unsigned long long vlt = (1ull << v) - 1ull;
-  int nl = 0, pos = 0, it = 0;
-  uint32_t round = 0;
-  long long n_spec = 0, n_rounds = 0, cyc_spec = 0, cyc_fit = 0, cyc_val = 0, n_coop = 0;
-  const long long t_all = clock64();
-  while (pos < nlist || ncarry > 0) {
-    const LaneBuf buf{fbuf + (long long)bufid * kLaneCap};
-    // ---- the next NS defined, NOTUSED seeds (after the carried ones); all
-    // 256 threads scan ----
-    int ncand = ncarry, scan = pos, next_pos = nlist;
-    while (ncand < NS && scan < nlist) {
-      const int i = scan + t;
-      bool c = false;
-      int px = 0, py = 0;
-      if (i < nlist) {
-        const int idx = (int)(A[i] & 0x3FFFFFu);
-        py = idx / w1;
-        px = idx - py * w1;
-        const uint64_t vv = ld_sd(sd + lsd_sd_index(px, py, F.tw));
-        c = __uint_as_float((uint32_t)vv) >= 0.f && (uint32_t)(vv >> 32) != 0u;
-      }
-      const unsigned long long m = __ballot(c);
-      int before = __popcll(m & lt_mask), cnt = __popcll(m);
-      const int par = it++ & 1;
-      if (lane == 0) s_cnt[par][wv] = cnt;
-      __syncthreads();
-      int o = 0, tot = 0;
-#pragma unroll
-      for (int w = 0; w < 4; w++) {
-        const int x = s_cnt[par][w];
-        o += w < wv ? x : 0;
-        tot += x;
-      }
-      before += o;
-      cnt = tot;
-      if (c && ncand + before < NS) {
-        s_pt[ncand + before] = (uint32_t)px | ((uint32_t)py << 16);
-        s_pos[ncand + before] = i;
-      }
-      if (ncand + cnt >= NS) {
-        if (c && before == NS - ncand - 1) s_misc[0] = i + 1;
-        __syncthreads();
-        next_pos = s_misc[0];
-        ncand = NS;
-      } else {
-        ncand += cnt;
-        scan += 256;
-      }
-    }
-    if (ncand == 0) break;
-    __threadfence_block();
-    __syncthreads();
-    n_rounds++;
-    const long long t0 = clock64();
-    const uint32_t tag = ((0x3FFFFFu - round) << 9) | (uint32_t)v;
-    const uint32_t myval0 = (tag << 1) | 1u, myval1 = tag << 1;
-    if (act) {
-      if (!keep) {
-        status = kSpecConflict;
-        off = 0;
-        len = 0;
-        touched = 0;
-      } else {
-        for (int j0 = 0; j0 < touched; j0 += 8) {
-          uint32_t ev[8];
-#pragma unroll
-          for (int u = 0; u < 8; u++) ev[u] = buf[min(j0 + u, touched - 1)].x;
-#pragma unroll
-          for (int u = 0; u < 8; u++)
-            atomicMin(sd_hi(sd, lsd_sd_index((int)(ev[u] & 0xFFFF), (int)(ev[u] >> 16), F.tw)),
-                      myval0);
-        }
-        wg_fence();
-      }
-    }
-    __syncthreads();   // the carried re-stamps precede every grow of the round
-    double reg_angle = 0;
-    int n = 0;
-    const bool mine_seed = act && v < ncand && !keep;
-    if (mine_seed) {
-      n_spec++;
-      const uint32_t pt = s_pt[v];
-      n = lane_grow(F, sd, buf, kLaneCap, (int)(pt & 0xFFFF), (int)(pt >> 16), reg_angle, prec,
-                    myval0);
-    }
-    const long long t1 = clock64();
-    if (mine_seed) {
-      if (n < 0) {
-        status = n;
-      } else if (n < g.min_reg_size) {
-        status = kSpecSmall;
-        len = n;
-        touched = n;
-      } else {
-        FitProf fp;
-        lane_rect(buf, n, reg_angle, prec, p, rec, F.q, sw);
-        status = lane_refine<false>(F, sd, buf, n, reg_angle, prec, p, rec, myval1, off, len,
-                                    touched, fp, nullptr);
-      }
-    }
-    wg_fence();
-    __syncthreads();
-    const long long t2 = clock64();
-    cyc_spec += t1 - t0;
-    cyc_fit += t2 - t1;
-    // ---- re-read the claims: an earlier seed's smaller stamp = conflict ----
-    bool conflict = act && v < ncand && status < 0;
-    if (act && v < ncand && status >= 0) {
-      for (int j0 = 0; j0 < touched && !conflict; j0 += 8) {
-        uint32_t ev[8], sv[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++) ev[u] = buf[min(j0 + u, touched - 1)].x;
-#pragma unroll
-        for (int u = 0; u < 8; u++)
-          sv[u] = ld_stamp(sd, lsd_sd_index((int)(ev[u] & 0xFFFF), (int)(ev[u] >> 16), F.tw));
-#pragma unroll
-        for (int u = 0; u < 8; u++) conflict |= (sv[u] >> 1) != tag;
-      }
-    }
-    // ---- commit in seed order: slots [lo, hi) ----
-    const unsigned long long cm = sp_vmask(conflict, s_vb, wv, lane);
-    int first = sp_next(cm, 0, ncand);
-    int lo = 0, hi = first;
-    int stop = ncand;
-    while (true) {
-      const bool mine = act && v >= lo && v < hi;
-      if (mine && len > 0) {
-        for (int j0 = off; j0 < off + len; j0 += 8) {
-          uint32_t ev[8];
-#pragma unroll
-          for (int u = 0; u < 8; u++) ev[u] = buf[min(j0 + u, off + len - 1)].x;
-#pragma unroll
-          for (int u = 0; u < 8; u++) {
-            const int id = lsd_sd_index((int)(ev[u] & 0xFFFF), (int)(ev[u] >> 16), F.tw);
-            __hip_atomic_store(sd_hi(sd, id), 0u, __ATOMIC_RELAXED, ORBPL_LSD_SCOPE);
-          }
-        }
-      }
-      const bool is_cand = mine && status == kSpecCand;
-      const unsigned long long km = sp_vmask(is_cand, s_vb, wv, lane);
-      if (is_cand) {
-        const int k = nl + __popcll(km & vlt);
-        if (k < kLsdMaxCand) {
-          double* o = cand_out + (long long)k * 12;
-          o[0] = rec.x1; o[1] = rec.y1; o[2] = rec.x2; o[3] = rec.y2;
-          o[4] = rec.width; o[5] = rec.x; o[6] = rec.y; o[7] = rec.theta;
-          o[8] = rec.dx; o[9] = rec.dy; o[10] = rec.prec; o[11] = rec.p;
-        }
-      }
-      nl += __popcll(km);
-      __threadfence_block();
-      __syncthreads();
-      if (first >= ncand) break;
-      const uint32_t spt = s_pt[first];
-      if (used_get(F, (int)(spt & 0xFFFF), (int)(spt >> 16))) {
-        // covered by a committed region: the sequential loop skips it
-        const int nxt = sp_next(cm, first + 1, ncand);
-        lo = first + 1;
-        hi = nxt;
-        first = nxt;
-        __syncthreads();   // every wave has read the USED bit before new stores
-        continue;
-      }
-      stop = first;
-      break;
-    }
-    cyc_val += clock64() - t2;
-    bool carry = false;
-    if (stop < ncand) {
-      pos = s_pos[stop];
-      if (act && v == stop) s_misc[1] = status;
-      __syncthreads();
-      const int st_stop = s_misc[1];
-      __syncthreads();
-      if (st_stop == kSpecOverflow) {
-        // a region longer than a lane buffer: the wave-cooperative program
-        // (wave 0; the lane buffers it uses as scratch are idle)
-        if (wv == 0) {
-          const uint32_t spt = s_pt[stop];
-          double ra;
-          int nn = region_grow(F, (int)(spt & 0xFFFF), (int)(spt >> 16), ra, prec);
-          if (nn >= g.min_reg_size) {
-            Rect& rc = *F.rect0;
-            fill_q(F, nn);
-            region2rect(F, nn, ra, prec, p, rc);
-            if (refine(F, nn, ra, prec, p, rc, 0.7)) {
-              if (nl < kLsdMaxCand) {
-                const double* rv = reinterpret_cast<const double*>(F.rect0);
-                if (lane < 12) cand_out[(long long)nl * 12 + lane] = rv[lane];
-              }
-              nl++;
-            }
-          }
-          if (lane == 0) s_misc[1] = nl;
-        }
-        __threadfence_block();
-        __syncthreads();
-        nl = s_misc[1];
-        __syncthreads();
-        n_coop++;
-        pos++;
-      } else {
-        carry = true;
-        pos = next_pos;
-      }
-    } else {
-      pos = next_pos;
-    }
-    // ---- carry the seeds from `stop` on to slots [0, ncarry) in list order
-    // (kept when the re-check passed; a conflicting one whose seed pixel a
-    // committed region covers is dropped, as the sequential loop skips it)
-    {
-      bool car = act && carry && v >= stop && v < ncand;
-      const bool kp = car && v > stop && !conflict;
-      const uint32_t my_pt = s_pt[v];
-      const int my_pos = s_pos[v];
-      if (car && !kp && used_get(F, (int)(my_pt & 0xFFFF), (int)(my_pt >> 16))) car = false;
-      const unsigned long long cmc = sp_vmask(car, s_vb, wv, lane);
-      const int ncar = __popcll(cmc);
-      if (act) {
-        s_src[car ? __popcll(cmc & vlt) : ncar + __popcll(~cmc & vlt)] = v;
-        s_bufid[v] = bufid;
-        s_status[v] = status;
-        s_off[v] = off;
-        s_len[v] = len;
-        s_touched[v] = touched;
-        s_kp[v] = kp ? 1 : 0;
-        s_ptx[v] = my_pt;
-        s_posx[v] = my_pos;
-        s_rec[v][0] = rec.x1; s_rec[v][1] = rec.y1; s_rec[v][2] = rec.x2; s_rec[v][3] = rec.y2;
-        s_rec[v][4] = rec.width; s_rec[v][5] = rec.x; s_rec[v][6] = rec.y; s_rec[v][7] = rec.theta;
-        s_rec[v][8] = rec.dx; s_rec[v][9] = rec.dy; s_rec[v][10] = rec.prec; s_rec[v][11] = rec.p;
-      }
-      __syncthreads();
-      if (act) {
-        const int src = s_src[v];
-        keep = s_kp[src] != 0 && v < ncar;
-        bufid = s_bufid[src];
-        status = s_status[src];
-        off = s_off[src];
-        len = s_len[src];
-        touched = s_touched[src];
-        rec.x1 = s_rec[src][0]; rec.y1 = s_rec[src][1]; rec.x2 = s_rec[src][2];
-        rec.y2 = s_rec[src][3]; rec.width = s_rec[src][4]; rec.x = s_rec[src][5];
-        rec.y = s_rec[src][6]; rec.theta = s_rec[src][7]; rec.dx = s_rec[src][8];
-        rec.dy = s_rec[src][9]; rec.prec = s_rec[src][10]; rec.p = s_rec[src][11];
-        if (v < ncar) {
-          s_pt[v] = s_ptx[src];
-          s_pos[v] = s_posx[src];
-        }
-      }
-      ncarry = ncar;
-      __threadfence_block();
-      __syncthreads();
-    }
-    round++;
-  }
-  if (t == 0) {
-    sc.ncand[f] = min(nl, kLsdMaxCand);
-    if (nl > kLsdMaxCand) atomicOr(sc.err + f, 8);
-  }
-  if (sc.prof && t == 0) {
-    long long* pr = sc.prof + f * 8;
-    pr[0] = cyc_spec;
-    pr[1] = n_rounds;
-    pr[2] = n_spec;   // wave 0's slots only
-    pr[3] = clock64() - t_all;
-    pr[4] = cyc_fit;
-    pr[5] = cyc_val;
-    pr[6] = n_coop << 40;
-    pr[7] = nl;
-  }
-}
-
 // NFA validation of every refined rectangle (rect_improve), one lane per
 // rectangle; the accepted segments are compacted in seed order by
 // k_lsd_compact.
@@ -3709,30 +2101,18 @@ constexpr int kValBlocksSmall = 8, kValBlocksLarge = ORBPL_VAL_BLOCKS_LARGE;
 // the next one instead of idling until the wave's costliest walk ends (the
 // improvement loop runs rect_nfa up to ~25 times on rejected rectangles).
 // gridDim.x = workgroups per frame.
-// ORBPL_VAL_XCD: the workgroups of one frame on one XCD (workgroups are dealt
+// The workgroups of one frame run on one XCD (workgroups are dealt
 // round-robin over the 8 XCDs by linear id; the remap gives each XCD a
 // contiguous range of frames), so the frame's degree-plane lines one block
 // fetched into that XCD's L2 serve its other blocks' walks too.
-#ifndef ORBPL_VAL_XCD
-#define ORBPL_VAL_XCD 1
-#endif
-#ifndef ORBPL_VAL_RECLDS
-#define ORBPL_VAL_RECLDS 1
-#endif
 __global__ void __launch_bounds__(256, ORBPL_VAL_MINW) k_lsd_validate(LsdGeom g, LsdScratch sc) {
   __shared__ int s_next;
-#if ORBPL_VAL_RECLDS
   __shared__ double s_rec[256][7];
-#endif
-#if ORBPL_VAL_XCD
   const int nx = gridDim.x, nwg = nx * gridDim.y;
   const int orig = blockIdx.x + nx * blockIdx.y;
   const int xcd = orig & 7, qq = nwg >> 3, rr = nwg & 7;
   const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (orig >> 3);
   const int f = wg / nx, bxv = wg - f * nx;
-#else
-  const int f = blockIdx.y, bxv = blockIdx.x;
-#endif
   const int nc = sc.ncand[f];
   const float* deg = sc.deg + (long long)f * lsd_deg_words(g.sw, g.sh);
   if (threadIdx.x == 0) s_next = 256;
@@ -3746,12 +2126,8 @@ __global__ void __launch_bounds__(256, ORBPL_VAL_MINW) k_lsd_validate(LsdGeom g,
     rec.x1 = rv[0]; rec.y1 = rv[1]; rec.x2 = rv[2]; rec.y2 = rv[3];
     rec.width = rv[4]; rec.x = rv[5]; rec.y = rv[6]; rec.theta = rv[7];
     rec.dx = rv[8]; rec.dy = rv[9]; rec.prec = rv[10]; rec.p = rv[11];
-#if ORBPL_VAL_RECLDS
     const double log_nfa =
         rect_improve_lds(deg, g.sw, g.sh, rec, s_rec[threadIdx.x], g.log_nt, sc.lgam, sc.lgam_n);
-#else
-    const double log_nfa = rect_improve_lane(deg, g.sw, g.sh, rec, g.log_nt, sc.lgam, sc.lgam_n);
-#endif
     const bool ok = log_nfa > 0;
     sc.cand_ok[o] = ok;
     if (ok) {
@@ -3760,81 +2136,6 @@ __global__ void __launch_bounds__(256, ORBPL_VAL_MINW) k_lsd_validate(LsdGeom g,
       sc.cand_line[o * 4 + 2] = float((rec.x2 + 0.5) / 0.8);
       sc.cand_line[o * 4 + 3] = float((rec.y2 + 0.5) / 0.8);
     }
-  }
-}
-
-// Small batches: one WAVE per rectangle (rect_improve / rect_nfa / nfa, the
-// wave-cooperative restatement: the row walk on every lane, the pixels of the
-// rows counted 64 x 8 at a time, nfa's tail stopping test one iteration per
-// lane), waves fetching rectangles from a workgroup counter. With few frames
-// the per-lane kernel's time is its longest rectangle's serial walk; here a
-// rectangle's walk is spread over the wave. Same counts, same log_nfa.
-// Workgroups per frame: enough for ~1024 in all (at least 8).
-// Measured slower and off (bit-exact, 26 LSD tests; tools/gpu_r04_v.sh, kernel
-// time per launch): batch 1 1.10 vs 0.96 ms, 16 1.77 vs 1.10, 64 6.8 vs 1.26
-// ms - the per-lane kernel is not bound by its longest rectangle but by the
-// total walk work, which the wave version does not shrink (its row walk runs
-// on every lane); ORBPL_VAL_WAVE_BATCH=<max batch> turns it on for A/B runs.
-#ifndef ORBPL_VAL_WAVE_BATCH
-#define ORBPL_VAL_WAVE_BATCH 0
-#endif
-constexpr int kValWaveBatch = ORBPL_VAL_WAVE_BATCH;
-__global__ void __launch_bounds__(256) k_lsd_validate_wave(LsdGeom g, LsdScratch sc) {
-  extern __shared__ int4 vw_rows[];   // 4 waves x g.sh rows
-  __shared__ Rect s_r[4][2];
-  __shared__ int s_next;
-  const int f = blockIdx.y, bxv = blockIdx.x, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int nc = sc.ncand[f];
-  Frame F;
-  F.sw = g.sw;
-  F.sh = g.sh;
-  F.deg = sc.deg + (long long)f * lsd_deg_words(g.sw, g.sh);
-  F.dtw = lsd_deg_tw(g.sw);
-  F.q = nullptr;
-  F.used = nullptr;
-  F.usd = nullptr;
-  F.cs = nullptr;
-  F.tw = 0;
-  F.reg_l = nullptr;
-  F.regq_l = nullptr;
-  F.regd_l = nullptr;
-  F.reg_g = nullptr;
-  F.ring = nullptr;
-  F.rows = vw_rows + wv * g.sh;
-  F.rect0 = &s_r[wv][0];
-  F.rect1 = &s_r[wv][1];
-  F.row_cap = g.sh;   // rect_nfa keeps only rows inside the image
-  F.log_nt = g.log_nt;
-  F.lane = lane;
-  F.pf_cyc = 0;
-  F.pf_cnt = 0;
-  F.seed_cyc = 0;
-  if (threadIdx.x == 0) s_next = 4;
-  __syncthreads();
-  int k = wv;
-  while (true) {
-    const int c = bxv + k * (int)gridDim.x;
-    if (c >= nc) break;
-    const long long o = (long long)f * kLsdMaxCand + c;
-    const double* rv = sc.cand + o * 12;
-    Rect& rec = *F.rect0;
-    if (lane < 12) reinterpret_cast<double*>(&rec)[lane] = rv[lane];
-    __builtin_amdgcn_wave_barrier();
-    const double log_nfa = rect_improve(F, rec);
-    __builtin_amdgcn_wave_barrier();
-    if (lane == 0) {
-      const bool ok = log_nfa > 0;
-      sc.cand_ok[o] = ok;
-      if (ok) {
-        sc.cand_line[o * 4 + 0] = float((rec.x1 + 0.5) / 0.8);
-        sc.cand_line[o * 4 + 1] = float((rec.y1 + 0.5) / 0.8);
-        sc.cand_line[o * 4 + 2] = float((rec.x2 + 0.5) / 0.8);
-        sc.cand_line[o * 4 + 3] = float((rec.y2 + 0.5) / 0.8);
-      }
-      k = atomicAdd(&s_next, 1);
-    }
-    k = __shfl(k, 0, 64);
-    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -3871,15 +2172,6 @@ void launch_lgamma_table(double* t, int n, hipStream_t s) {
 }
 
 void launch_lsd_validate(const LsdGeom& g, const LsdScratch& sc, int batch, hipStream_t s) {
-  static const char* vw_env = getenv("ORBPL_VAL_WAVE_BATCH");
-  static const int wave_batch = vw_env ? atoi(vw_env) : kValWaveBatch;
-  if (batch <= wave_batch) {
-    const int nblk = std::max(8, std::min(64, 1024 / std::max(batch, 1)));
-    const size_t smem = (size_t)4 * g.sh * sizeof(int4);
-    hipLaunchKernelGGL(k_lsd_validate_wave, dim3(nblk, batch), dim3(256), smem, s, g, sc);
-    hipLaunchKernelGGL(k_lsd_compact, dim3(batch), dim3(64), 0, s, sc);
-    return;
-  }
   const int nblk = batch >= 1024 ? kValBlocksLarge : kValBlocksSmall;
   hipLaunchKernelGGL(k_lsd_validate, dim3(nblk, batch), dim3(256), 0, s, g, sc);
   hipLaunchKernelGGL(k_lsd_compact, dim3(batch), dim3(64), 0, s, sc);
@@ -3908,11 +2200,7 @@ void launch_lsd_grow(const LsdGeom& g, const LsdScratch& sc, int batch, hipStrea
       // per SIMD (no spills on the seed chain) instead of the co-residence bound
       static const char* sb_env = getenv("ORBPL_SPEC_SMALL");
       static const int small_batch = sb_env ? atoi(sb_env) : kSpecSmallBatch;
-      static const char* sp_env = getenv("ORBPL_SPEC_SPARSE");
-      static const int sparse_batch = sp_env ? atoi(sp_env) : kSpecSparseBatch;
-      if (batch <= sparse_batch)
-        hipLaunchKernelGGL(k_lsd_spec_sparse, dim3(batch), dim3(256), smem, s, g, sc);
-      else if (batch <= small_batch)
+      if (batch <= small_batch)
         hipLaunchKernelGGL((k_lsd_spec<1, 1>), dim3(batch), dim3(64), smem, s, g, sc);
       else
         hipLaunchKernelGGL(k_lsd_spec<1>, dim3(batch), dim3(64), smem, s, g, sc);

@@ -71,15 +71,11 @@ __host__ __device__ inline long long lsd_sd_words(int sw, int sh) {
 __host__ __device__ inline long long lsd_sd_frame_words(int sw, int sh) {
   return 2 * lsd_sd_words(sw, sh);
 }
-// ORBPL_SD_PAIRED: a pixel's word and its angle terms side by side (one
-// 16-byte load per neighbour in the grow, 4x4-pixel tiles of 256 B) instead of
-// two planes of 128-B tiles (the terms at + lsd_sd_words).
-#ifndef ORBPL_SD_PAIRED
-#define ORBPL_SD_PAIRED 1
-#endif
+// A pixel's word and its angle terms side by side: one 16-byte load per
+// neighbour in the grow, 4x4-pixel tiles of 256 B.
 __host__ __device__ inline int lsd_sd_index(int x, int y, int tw) {
   const int i = ((((y >> 2) * tw) + (x >> 2)) << 4) | ((y & 3) << 2) | (x & 3);
-  return ORBPL_SD_PAIRED ? 2 * i : i;
+  return 2 * i;
 }
 // The degree plane (LsdScratch::deg) in 8x4-pixel tiles of 128 B: the NFA
 // walk of k_lsd_validate reads a rectangle row by row, and a thin oblique
@@ -94,7 +90,7 @@ __host__ __device__ inline int lsd_deg_index(int x, int y, int dtw) {
 }
 // offset (u64 words) of a pixel's angle terms from its pixel word
 __host__ __device__ inline long long lsd_cs_offset(int sw, int sh) {
-  return ORBPL_SD_PAIRED ? 1 : lsd_sd_words(sw, sh);
+  return 1;
 }
 
 struct LsdScratch {
