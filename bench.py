@@ -146,10 +146,12 @@ def level_areas(w=W, h=H, orb=ORB):
     return [int(a) * int(b) for a, b in zip(d["width"], d["height"])], d
 
 
-def lsd_touch_floor(counts):
-    """Per-frame bytes the sequential LSD touches in the kernels' layout, from
-    the oracle's element-access counts (oracle.lsd_traffic, averaged over
-    sampled frames of the workload): every access served once from memory.
+def lsd_access_volume(counts):
+    """Per-frame ACCESS VOLUME of the sequential LSD in the kernels' layout,
+    from the oracle's element-access counts (oracle.lsd_traffic, averaged over
+    sampled frames of the workload): every access charged as if served from
+    memory with no reuse - the traffic of a cacheless machine, a ceiling on
+    what a kernel with any reuse should move, not a floor.
       pseudo-order sort: (compares + element writes) x 4 B packed key;
       seed loop: seeds x (4 B key + 8 B pixel word) + neighbour reads x 16 B
         (the paired word: angle, claim stamp, cos, sin) + adds x (8 B stamp +
@@ -163,6 +165,25 @@ def lsd_touch_floor(counts):
             "lsd_validate": 4 * c["nfa_px"] + 96 * c["nfa_evals"]}
 
 
+def lsd_unique_floor(counts):
+    """Per-frame UNIQUE-BYTES floor of the LSD kernels: the distinct addresses
+    the sequential algorithm touches (the oracle's touched-address bitmaps,
+    oracle/lsd_oracle.cpp LsdTraffic), each fetched or stored once in the
+    kernels' layout.
+      sort: every pseudo-ordered key read once and written once (2 x 4 B);
+      seed loop: the seed list's keys (4 B each), the distinct pixel words
+        read (16 B: angle, stamp, cos, sin), the distinct USED stamps written
+        (8 B), the distinct weights q read (4 B), the longest region list
+        written and read once (2 x 16 B per entry), the rectangles out (96 B);
+      NFA validation: the distinct rectangle pixels' angles (4 B), the
+        rectangles in (96 B) and their verdict + end points out (17 B)."""
+    c = counts
+    return {"lsd_sort": 8 * c["sort_n"],
+            "lsd_seed": (4 * c["seeds"] + 16 * c["u_seed_px"] + 8 * c["u_used_px"] +
+                         4 * c["u_q_px"] + 32 * c["max_reg"] + 96 * c["rects"]),
+            "lsd_validate": 4 * c["u_nfa_px"] + (96 + 17) * c["rects"]}
+
+
 def lsd_counts(frames, k=8):
     """oracle.lsd_traffic averaged over k frames spread over `frames`."""
     from _pkg import load_oracle
@@ -174,14 +195,14 @@ def lsd_counts(frames, k=8):
     return out
 
 
-def algorithmic_bytes(n_kp, w=W, h=H, orb=ORB, n_lines=80, lsd=None):
+def algorithmic_bytes(n_kp, w=W, h=H, orb=ORB, n_lines=80):
     """Per-frame algorithmic HBM bytes of each kernel: the
     bytes the kernel must move at minimum (each input read once, each output
-    written once), with n_kp keypoints per frame. LSD works on the 0.8-scaled
-    image (sA pixels, LSD's `scale` of LineSegmentDetector); with `lsd` (the
-    oracle's element-access counts, lsd_counts) the sort, seed-loop and
-    validation kernels take the sequential algorithm's touch floor
-    (lsd_touch_floor) instead of the one-pass estimates."""
+    written once, SURVEY §8(d)-style one-pass bytes), with n_kp keypoints per
+    frame. LSD works on the 0.8-scaled image (sA pixels, LSD's `scale` of
+    LineSegmentDetector). The LSD kernels' unique-bytes floor and access
+    volume (lsd_unique_floor, lsd_access_volume) are reported beside these in
+    roofline.lsd_floor, never in their place."""
     areas, d = level_areas(w, h, orb)
     S = sum(areas)
     dims = list(zip((int(a) for a in d["width"]), (int(b) for b in d["height"])))
@@ -229,7 +250,6 @@ def algorithmic_bytes(n_kp, w=W, h=H, orb=ORB, n_lines=80, lsd=None):
         "lbd": A0 + 2 * A0 + 2 * 4 * A0 + n_lines * 32,
         # UndistortKeyLines + line depths: 80 KeyLines in and out, 160 depth reads
         "line_prepare": n_lines * (68 * 2 + 8 + 8),
-        **(lsd_touch_floor(lsd) if lsd else {}),
     }
 
 
@@ -656,7 +676,7 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
     # roofline of the dominant single-stage kernel
     n_kp = float(st["nkeypoints"].mean())
     lsdc = lsd_counts(gray) if lines else None
-    ab = algorithmic_bytes(n_kp, fw, fh, wl["orb"], lsd=lsdc)
+    ab = algorithmic_bytes(n_kp, fw, fh, wl["orb"])
     # candidates: every kernel's GPU time per step, a kernel launched in
     # several stages (k_pose: motion model, reference keyframe, local map)
     # counted once with all its launches
@@ -741,17 +761,25 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
             "per_kernel_GBps": {k: round(ab[k] * launch_frames(k) / (stage_avg[k] * 1e-3) / 1e9, 1)
                                 for k in cand if stage_avg[k] > 0}}
     if lsdc:
-        # the LSD kernels' algorithmic bytes are the sequential algorithm's
-        # touch floor (lsd_touch_floor); their committed PMC traffic over it
-        fl = lsd_touch_floor(lsdc)
-        ratios = {}
-        for k, b in fl.items():
+        # each LSD kernel's committed PMC traffic against three byte counts per
+        # frame: the one-pass bytes (algorithmic_bytes), the
+        # unique-bytes floor (distinct addresses the sequential algorithm
+        # touches) and the access volume (every access with no reuse)
+        uf, av = lsd_unique_floor(lsdc), lsd_access_volume(lsdc)
+        per = {}
+        for k in uf:
             tb, _ = pmc_traffic(KERNELS[k], workload, launch_frames(k))
-            ratios[k] = round(tb / (b * launch_frames(k)), 2) if tb else None
-        roof["lsd_floor"] = {"counts_per_frame": lsdc, "floor_bytes_per_frame": fl,
-                             "pmc_traffic_over_floor": ratios,
-                             "source": "oracle.lsd_traffic (oracle/lsd_oracle.cpp LsdTraffic) on "
-                                       "sampled frames of this workload"}
+            pf = tb / launch_frames(k) if tb else None
+            per[k] = {"pmc_bytes_per_frame": int(pf) if pf else None,
+                      "one_pass_bytes": int(ab[k]), "unique_bytes": int(uf[k]),
+                      "access_volume_bytes": int(av[k]),
+                      "over_one_pass": round(pf / ab[k], 2) if pf else None,
+                      "over_unique": round(pf / uf[k], 2) if pf else None,
+                      "over_access_volume": round(pf / av[k], 2) if pf else None}
+        roof["lsd_floor"] = {"counts_per_frame": lsdc, "kernels": per,
+                             "source": "oracle.lsd_traffic (oracle/lsd_oracle.cpp LsdTraffic: "
+                                       "access counts and touched-address bitmaps) on sampled "
+                                       "frames of this workload"}
     # whole pipeline: B_frame x frames/s against 8 TB/s
     per_gpu = S * steps / elapsed
     roof["pipeline"] = {"bytes_per_frame": fbytes, "frames_per_s_per_gpu": round(per_gpu, 1),
@@ -1024,8 +1052,53 @@ def cpu_reference_faithful(gray, depth, L, workload, flags=0, warmup=20, frames=
     return json.loads(r.stdout.strip().splitlines()[-1])
 
 
-def faithful_run(npz):
-    """The child side of cpu_reference_faithful (tools/cpu_faithful.py --npz)."""
+def _cpu_list(text):
+    out = []
+    for part in text.strip().split(","):
+        if "-" in part:
+            a, b = part.split("-")
+            out += list(range(int(a), int(b) + 1))
+        elif part:
+            out.append(int(part))
+    return out
+
+
+def pin_one_ccd():
+    """Pin this process (before any thread starts) to the allowed CPUs of one
+    last-level-cache domain (a CCD on EPYC), one logical CPU per physical core
+    (no SMT sibling shares a core with another of our threads). Returns what
+    was done: the CPUs before / after and the LLC group."""
+    before = sorted(os.sched_getaffinity(0))
+    rec = {"allowed_before": before}
+    try:
+        groups = {}
+        for c in before:
+            llc = open(f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list").read()
+            groups.setdefault(llc.strip(), []).append(c)
+        llc, cpus = max(groups.items(), key=lambda kv: (len(kv[1]), -kv[1][0]))
+        cores, seen = [], set()
+        for c in cpus:
+            sib = _cpu_list(open(f"/sys/devices/system/cpu/cpu{c}/topology/"
+                                 "thread_siblings_list").read())
+            key = min(sib)
+            if key not in seen:
+                seen.add(key)
+                cores.append(c)
+        if len(cores) >= 2:
+            os.sched_setaffinity(0, cores)
+        rec.update(pinned=sorted(os.sched_getaffinity(0)), llc_group=llc,
+                   llc_groups=len(groups), physical_cores_in_group=len(cores))
+    except (OSError, ValueError) as e:
+        rec.update(pinned=None, note=f"not pinned: {e}")
+    return rec
+
+
+def faithful_run(npz, pin=True):
+    """The child side of cpu_reference_faithful (tools/cpu_faithful.py --npz):
+    pinned to one CCD's physical cores before the oracle starts any thread,
+    per-frame latency plus the per-thread stage times (ORB thread, LSD thread,
+    the ORB thread's join wait, tracking = the rest of the step)."""
+    affinity = pin_one_ccd() if pin else {"pinned": None, "note": "not pinned (--no-pin)"}
     from _pkg import load_oracle
     import orbpl.synth as synth
     d = np.load(npz)
@@ -1048,7 +1121,7 @@ def faithful_run(npz):
         vo.set_vocabulary(O.Vocabulary(arrays=arrays))
     vo.reset(d["Tcw0"])
     gray, depth, order = d["gray"], d["depth"], d["order"]
-    lat = []
+    lat, stages = [], []
     for i, k in enumerate(order):
         t0 = time.perf_counter()
         if wl["stereo"]:
@@ -1057,13 +1130,26 @@ def faithful_run(npz):
             vo.step(0, gray[k], depth[k])
         if i >= warmup:
             lat.append(time.perf_counter() - t0)
+            if use_map:
+                stages.append(vo.stage_times())
     lat = np.array(lat) * 1e3
-    return {"value": round(1e3 / float(lat.mean()), 2), "unit": "frames/s",
-            "threads_per_frame": 2 if wl["lines"] else 1,
-            "median_ms_per_frame": round(float(np.median(lat)), 3),
-            "mean_ms_per_frame": round(float(lat.mean()), 3), "frames": int(len(lat)),
-            "sample": f"one stream, {len(lat)} frames after {warmup} warm-up frames, "
-                      f"in a process of its own"}
+    out = {"value": round(1e3 / float(lat.mean()), 2), "unit": "frames/s",
+           "threads_per_frame": 2 if wl["lines"] else 1,
+           "median_ms_per_frame": round(float(np.median(lat)), 3),
+           "mean_ms_per_frame": round(float(lat.mean()), 3), "frames": int(len(lat)),
+           "p10_p90_ms": [round(float(np.percentile(lat, 10)), 3),
+                          round(float(np.percentile(lat, 90)), 3)],
+           "affinity": affinity,
+           "sample": f"one stream, {len(lat)} frames after {warmup} warm-up frames, "
+                     f"in a process of its own"}
+    if stages:
+        st = {k: np.array([x[k] for x in stages]) for k in stages[0]}
+        st["tracking"] = st["step"] - st["orb"] - st["join_wait"]
+        out["stage_median_ms"] = {k: round(float(np.median(v)), 3) for k, v in st.items()}
+        out["stage_note"] = ("orb = ORB extraction on the tracking thread; lines = LineExtractor "
+                             "on its own thread (Frame.cc:152-155); join_wait = the tracking "
+                             "thread's wait for it; tracking = step - orb - join_wait")
+    return out
 
 
 def _free_port():

@@ -244,6 +244,14 @@ struct LsdTraffic {
   long long grows = 0;                       // region_grow calls (first + refine's second)
   long long fit_reads = 0, fit_writes = 0;   // region list element reads / writes of the fit
   long long nfa_evals = 0, nfa_px = 0;       // rect_nfa calls, rectangle pixels visited
+  // distinct addresses (touched-address bitmaps over the scaled image): the
+  // unique-bytes floor of each stage, every element fetched or stored once
+  long long sort_n = 0;                      // pseudo-ordered entries (keys read + written)
+  long long max_reg = 0;                     // longest region list (list scratch slots)
+  long long rects = 0;                       // rectangles validated (rect_improve calls)
+  std::vector<uint8_t> px;                   // bit 0 seed-loop pixel read, 1 USED written,
+                                             // 2 q (weight) read, 3 NFA angle read
+  void mark(int W, int x, int y, uint8_t bit) { px[(size_t)y * W + x] |= bit; }
 };
 
 struct LSD {
@@ -332,6 +340,7 @@ struct LSD {
       c.reserve(ordered.size());
       for (const NormPoint& q : ordered) c.emplace_back(q, &tr->sort_moves);
       tr->sort_moves = 0;
+      tr->sort_n = (long long)ordered.size();
       long long* nc = &tr->sort_cmp;
       std::sort(c.begin(), c.end(), [nc](const CP& a, const CP& b) {
         ++*nc;
@@ -359,6 +368,7 @@ struct LSD {
     if (tr) {
       tr->grows++;
       tr->grow_add++;
+      tr->mark(W, sx, sy, 1 | 2);
     }
     for (size_t i = 0; i < reg.size(); i++) {
       const RegionPoint rpoint = reg[i];
@@ -367,6 +377,8 @@ struct LSD {
       if (tr) {
         tr->grow_expand++;
         tr->grow_nb += (long long)(xx_max - xx_min + 1) * (yy_max - yy_min + 1) - 1;
+        for (int yy = yy_min; yy <= yy_max; ++yy)
+          for (int xx = xx_min; xx <= xx_max; ++xx) tr->mark(W, xx, yy, 1);
       }
       for (int yy = yy_min; yy <= yy_max; ++yy)
         for (int xx = xx_min; xx <= xx_max; ++xx) {
@@ -384,7 +396,10 @@ struct LSD {
             sumdx += cosf_cr(float(angle));
             sumdy += sinf_cr(float(angle));
             reg_angle = oracle_fast_atan2(sumdy, sumdx) * DEG_TO_RADS;
-            if (tr) tr->grow_add++;
+            if (tr) {
+              tr->grow_add++;
+              tr->mark(W, xx, yy, 2);
+            }
           }
         }
     }
@@ -412,7 +427,11 @@ struct LSD {
 
   void region2rect(const std::vector<RegionPoint>& reg, double reg_angle, double prec, double p,
                    Rect& rec) const {
-    if (tr) tr->fit_reads += 3 * (long long)reg.size();   // centroid, inertia, extents passes
+    if (tr) {
+      tr->fit_reads += 3 * (long long)reg.size();   // centroid, inertia, extents passes
+      tr->max_reg = std::max(tr->max_reg, (long long)reg.size());
+      for (const RegionPoint& r : reg) tr->mark(img_width, r.x, r.y, 4);
+    }
     double x = 0, y = 0, sum = 0;
     for (size_t i = 0; i < reg.size(); ++i) {
       const double weight = reg[i].modgrad;
@@ -460,7 +479,10 @@ struct LSD {
       for (size_t i = 0; i < reg.size(); ++i) {
         if (tr) tr->fit_reads++;
         if (distSq(xc, yc, double(reg[i].x), double(reg[i].y)) > radSq) {
-          if (tr) tr->fit_writes += 2;   // the USED flag, the swapped-in element
+          if (tr) {
+            tr->fit_writes += 2;   // the USED flag, the swapped-in element
+            tr->mark(img_width, reg[i].x, reg[i].y, 2);
+          }
           *(reg[i].used) = NOTUSED;
           std::swap(reg[i], reg[reg.size() - 1]);
           reg.pop_back();
@@ -484,6 +506,7 @@ struct LSD {
     if (tr) {
       tr->fit_reads += (long long)reg.size();
       tr->fit_writes += (long long)reg.size();   // USED flags released before the regrow
+      for (const RegionPoint& r : reg) tr->mark(img_width, r.x, r.y, 2);
     }
     for (size_t i = 0; i < reg.size(); ++i) {
       *(reg[i].used) = NOTUSED;
@@ -595,6 +618,7 @@ struct LSD {
       for (int x = int(left_x); x <= int(right_x); ++x) {
         if (x < 0 || x >= img_width) continue;
         ++total_pts;
+        if (tr) tr->mark(img_width, x, y, 8);
         if (isAligned(x, y, rec.theta, rec.prec)) ++alg_pts;
       }
       if (y >= leftmost->y) lstep = slstep;
@@ -707,10 +731,14 @@ struct LSD {
              pmath::log10_(11.0);
     const size_t min_reg_size = size_t(-LOG_NT / pmath::log10_(p));
     used.assign((size_t)img_width * img_height, NOTUSED);
+    if (tr) tr->px.assign((size_t)img_width * img_height, 0);
     std::vector<RegionPoint> reg;
     for (size_t i = 0; i < ordered.size(); ++i) {
       const int px = ordered[i].x, py = ordered[i].y;
-      if (tr) tr->seeds++;
+      if (tr) {
+        tr->seeds++;
+        tr->mark(img_width, px, py, 1);
+      }
       if (used[(size_t)py * img_width + px] != NOTUSED || ang(px, py) == NOTDEF) continue;
       double reg_angle;
       region_grow(px, py, reg, reg_angle, prec);
@@ -718,6 +746,7 @@ struct LSD {
       Rect rec;
       region2rect(reg, reg_angle, prec, p, rec);
       if (!refine(reg, reg_angle, prec, p, rec)) continue;
+      if (tr) tr->rects++;
       const double log_nfa = rect_improve(rec);
       if (log_nfa <= LOG_EPS) continue;
       rec.x1 += 0.5;
@@ -972,17 +1001,24 @@ int oracle_lsd_detect(const uint8_t* img, int W, int H, float* lines, int cap, i
 
 // The element accesses of one detection (LsdTraffic, in declaration order:
 // sort_cmp, sort_moves, seeds, grow_nb, grow_add, grow_expand, grows,
-// fit_reads, fit_writes, nfa_evals, nfa_px); bench.py turns them into the LSD
-// kernels' algorithmic-byte floors. Returns the number of segments.
-int oracle_lsd_traffic(const uint8_t* img, int W, int H, long long* out11) {
+// fit_reads, fit_writes, nfa_evals, nfa_px), then the distinct-address counts
+// (sort_n, max_reg, rects, and the distinct scaled-image pixels the seed loop
+// reads, whose USED state it writes, whose weight q it reads, and whose angle
+// the NFA walks read); bench.py turns them into the LSD kernels' access
+// volume and unique-bytes floor. Returns the number of segments.
+int oracle_lsd_traffic(const uint8_t* img, int W, int H, long long* out18) {
   LSD lsd;
   LsdTraffic t;
   lsd.tr = &t;
   std::vector<float> L;
   lsd.detect(img, W, H, L);
-  const long long v[11] = {t.sort_cmp, t.sort_moves, t.seeds, t.grow_nb, t.grow_add, t.grow_expand,
-                           t.grows, t.fit_reads, t.fit_writes, t.nfa_evals, t.nfa_px};
-  std::memcpy(out11, v, sizeof(v));
+  long long u[4] = {0, 0, 0, 0};
+  for (uint8_t b : t.px)
+    for (int k = 0; k < 4; k++) u[k] += (b >> k) & 1;
+  const long long v[18] = {t.sort_cmp, t.sort_moves, t.seeds, t.grow_nb, t.grow_add, t.grow_expand,
+                           t.grows, t.fit_reads, t.fit_writes, t.nfa_evals, t.nfa_px,
+                           t.sort_n, t.max_reg, t.rects, u[0], u[1], u[2], u[3]};
+  std::memcpy(out18, v, sizeof(v));
   return (int)(L.size() / 4);
 }
 

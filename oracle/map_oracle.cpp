@@ -41,6 +41,7 @@
 #include <cstring>
 #include <map>
 #include <set>
+#include <chrono>
 #include <thread>
 #include <vector>
 
@@ -200,6 +201,10 @@ struct MapVO {
   std::vector<float> scale, inv_sigma2;
   float log_scale;
   std::vector<Stream> st;
+  // the last step's stage times (CPU baseline instrumentation, ms): the ORB
+  // extraction on the calling thread, the LineExtractor on its own thread,
+  // the calling thread's wait in join(), the whole step
+  double t_orb = 0, t_lines = 0, t_join = 0, t_step = 0;
 };
 
 // ---- MapPoint / MapLine methods ----
@@ -412,9 +417,16 @@ static void extract(MapVO* v, const uint8_t* gray, const float* depth, Frame& F,
   std::vector<uint8_t> ld(kKeepLines * 32);
   std::vector<double> coef(kKeepLines * 3);
   int nl = 0, nd = 0;
+  using clk = std::chrono::steady_clock;
+  auto ms = [](clk::time_point a, clk::time_point b) {
+    return std::chrono::duration<double, std::milli>(b - a).count();
+  };
+  double t_lines = 0;
   auto lines = [&]() {
+    const auto a = clk::now();
     oracle_line_extract(gray, cam.width, cam.height, kl.data(), ld.data(), coef.data(), kKeepLines,
                         &nl, &nd);
+    t_lines = ms(a, clk::now());
   };
   std::thread lt;
   if (v->use_lines && (v->flags & kTwoThreads)) lt = std::thread(lines);
@@ -422,10 +434,20 @@ static void extract(MapVO* v, const uint8_t* gray, const float* depth, Frame& F,
   std::vector<orbpl_keypoint> kps(cap);
   std::vector<uint8_t> desc((size_t)cap * 32);
   int n = 0;
+  const auto t0 = clk::now();
   oracle_orb_extract(&v->orb, gray, cam.width, cam.height, cam.width, kps.data(), desc.data(), cap,
                      &n, nullptr);
-  if (lt.joinable()) lt.join();
-  else if (v->use_lines) lines();
+  const auto t1 = clk::now();
+  double t_join = 0;
+  if (lt.joinable()) {
+    lt.join();
+    t_join = ms(t1, clk::now());
+  } else if (v->use_lines) {
+    lines();
+  }
+  v->t_orb = ms(t0, t1);
+  v->t_join = t_join;
+  v->t_lines = t_lines;
   kps.resize(n);
   desc.resize((size_t)n * 32);
   F.N = n;
@@ -1057,6 +1079,14 @@ static int step(MapVO* v, int s, const uint8_t* gray, const float* depth, float*
                 const uint8_t* right = nullptr) {
   Stream& S = v->st[s];
   Frame F;
+  const auto t_start = std::chrono::steady_clock::now();
+  struct StepClock {   // the whole step, however it returns
+    MapVO* v;
+    std::chrono::steady_clock::time_point a;
+    ~StepClock() {
+      v->t_step = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+    }
+  } step_clock{v, t_start};
   extract(v, gray, depth, F, right);
   F.id = S.next_id++;
   int* out = S.out;
@@ -1254,6 +1284,17 @@ int oracle_map_step_stereo(void* h, int stream, const uint8_t* left, const uint8
 }
 
 // Camera.fps: mMaxFrames (0 -> 30, Tracking.cc:81-87)
+// the last step's stage times in ms: ORB (calling thread), LineExtractor (its
+// own thread, or inline), the calling thread's join wait, the whole step
+int oracle_map_stage_times(void* h, double* out4) {
+  const mapvo::MapVO* v = static_cast<mapvo::MapVO*>(h);
+  out4[0] = v->t_orb;
+  out4[1] = v->t_lines;
+  out4[2] = v->t_join;
+  out4[3] = v->t_step;
+  return 0;
+}
+
 int oracle_map_set_fps(void* h, float fps) {
   static_cast<mapvo::MapVO*>(h)->max_frames = (int)(fps == 0.0f ? 30.0f : fps);
   return 0;

@@ -432,14 +432,20 @@ def lsd_detect(img, cap=4096):
 
 
 LSD_TRAFFIC_KEYS = ("sort_cmp", "sort_moves", "seeds", "grow_nb", "grow_add", "grow_expand",
-                    "grows", "fit_reads", "fit_writes", "nfa_evals", "nfa_px")
+                    "grows", "fit_reads", "fit_writes", "nfa_evals", "nfa_px",
+                    # distinct addresses (touched-address bitmap): entries sorted,
+                    # longest region list, rectangles validated, distinct pixels
+                    # the seed loop reads / marks USED / reads q of, NFA pixels
+                    "sort_n", "max_reg", "rects", "u_seed_px", "u_used_px", "u_q_px",
+                    "u_nfa_px")
 
 
 def lsd_traffic(img):
     """Element accesses of the sequential LSD on one image (the pseudo-order
     sort's compares / element writes, the seed loop's seeds, neighbour reads,
     adds, expansions and fit list accesses, the NFA's evaluations and
-    rectangle pixels): the algorithmic-traffic floor inputs of bench.py."""
+    rectangle pixels) and the distinct addresses each stage touches: the
+    access-volume and unique-bytes inputs of bench.py."""
     img = _c(img, np.uint8)
     h, w = img.shape
     o = np.zeros(len(LSD_TRAFFIC_KEYS), np.int64)
@@ -730,6 +736,7 @@ def _setup(L):  # noqa: F811
     L.oracle_map_clear_velocity.argtypes = [vp, i]
     L.oracle_map_step_stereo.argtypes = [vp, i, vp, vp, vp, vp]
     L.oracle_map_set_fps.argtypes = [vp, C.c_float]
+    L.oracle_map_stage_times.argtypes = [vp, vp]
     L.oracle_map_set_vocabulary.argtypes = [vp, vp]
     L.oracle_map_step.argtypes = [vp, i, vp, vp, vp, vp]
     L.oracle_map_keyframes.argtypes = [vp, i, vp, vp, i, vp]
@@ -791,6 +798,14 @@ class MapVO:
     def set_fps(self, fps):
         """Camera.fps: mMaxFrames (0 -> 30)."""
         lib().oracle_map_set_fps(self.h, C.c_float(fps))
+
+    def stage_times(self):
+        """The last step's stage times in ms: ORB on the calling thread, the
+        LineExtractor on its own thread (TWO_THREADS) or inline, the calling
+        thread's join wait, the whole step."""
+        o = np.zeros(4, np.float64)
+        lib().oracle_map_stage_times(self.h, _p(o))
+        return dict(orb=float(o[0]), lines=float(o[1]), join_wait=float(o[2]), step=float(o[3]))
 
     def keyframes(self, stream, cap=64):
         par = np.zeros(256, np.int32)

@@ -61,7 +61,7 @@ int oracle_vo_reset(void* h, const float* Tcw0);
 int oracle_vo_step(void* h, int stream, const uint8_t* gray, const float* depth, float* Tcw_out,
                    int* out5);
 /* line features (lsd_oracle.cpp) */
-int oracle_lsd_traffic(const uint8_t* img, int W, int H, long long* out11);
+int oracle_lsd_traffic(const uint8_t* img, int W, int H, long long* out18);
 int oracle_lsd_detect(const uint8_t* img, int W, int H, float* lines, int cap, int* n_out);
 int oracle_lsd_stages(const uint8_t* img, int W, int H, uint8_t* scaled, double* angles,
                       uint32_t* order, int* sw, int* sh, int* n_order);
@@ -114,6 +114,8 @@ int oracle_map_clear_velocity(void* h, int stream);
 int oracle_map_step_stereo(void* h, int stream, const uint8_t* left, const uint8_t* right,
                            float* Tcw_out, int* out24);
 int oracle_map_set_fps(void* h, float fps);
+/* the last step's stage times (ms): ORB, LineExtractor, join wait, whole step */
+int oracle_map_stage_times(void* h, double* out4);
 int oracle_map_set_vocabulary(void* h, void* voc);
 int oracle_map_step(void* h, int stream, const uint8_t* gray, const float* depth, float* Tcw_out,
                     int* out24);

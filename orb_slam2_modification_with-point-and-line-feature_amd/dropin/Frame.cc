@@ -3,6 +3,8 @@
 
 #include "KeyFrame.h"
 
+#include <algorithm>
+#include <cmath>
 #include <stdexcept>
 #include <thread>
 
@@ -10,6 +12,7 @@ namespace ORB_SLAM2 {
 
 float Frame::fx, Frame::fy, Frame::cx, Frame::cy, Frame::invfx, Frame::invfy;
 float Frame::mnMinX, Frame::mnMaxX, Frame::mnMinY, Frame::mnMaxY;
+float Frame::mfGridElementWidthInv, Frame::mfGridElementHeightInv;
 long unsigned int Frame::nNextId = 0;
 long unsigned int KeyFrame::nNextId = 0;
 
@@ -24,18 +27,49 @@ orbpl_camera Frame::Camera() const {
                       mThDepth, mnWidth, mnHeight};
 }
 
+// Frame.cc:78-85 / 141-148: the scale level info of the (left) extractor
+void Frame::ScaleInfo(ORBextractor* ex) {
+  mnScaleLevels = ex->GetLevels();
+  mfScaleFactor = ex->GetScaleFactor();
+  mvScaleFactors = ex->GetScaleFactors();
+  mvInvScaleFactors = ex->GetInverseScaleFactors();
+  mvLevelSigma2 = ex->GetScaleSigmaSquares();
+  mvInvLevelSigma2 = ex->GetInverseScaleSigmaSquares();
+}
+
+// UndistortKeyPoints, ComputeStereoFromRGBD (depth != NULL; stereo: NULL, the
+// stereo matcher fills mvuRight / mvDepth after), ComputeImageBounds and
+// AssignFeaturesToGrid (Frame.cc:98-131, 160-204) in one library call
+void Frame::PrepareKeys(const float* depth) {
+  const orbpl_camera cam = Camera();
+  mvKeysUn.resize(N);
+  mvDepth.resize(N);
+  mvuRight.resize(N);
+  std::vector<int32_t> cell(N);
+  float bounds[4];
+  check(orbpl_frame_prepare(&cam, reinterpret_cast<const orbpl_keypoint*>(mvKeys.data()), N, depth,
+                            reinterpret_cast<orbpl_keypoint*>(mvKeysUn.data()), mvDepth.data(),
+                            mvuRight.data(), cell.data(), bounds));
+  mnMinX = bounds[0];
+  mnMaxX = bounds[1];
+  mnMinY = bounds[2];
+  mnMaxY = bounds[3];
+  // Frame.cc:113-115
+  mfGridElementWidthInv = static_cast<float>(FRAME_GRID_COLS) / (mnMaxX - mnMinX);
+  mfGridElementHeightInv = static_cast<float>(FRAME_GRID_ROWS) / (mnMaxY - mnMinY);
+  for (int i = 0; i < N; i++)
+    if (cell[i] >= 0) mGrid[cell[i] % FRAME_GRID_COLS][cell[i] / FRAME_GRID_COLS].push_back(i);
+  mvpMapPoints.assign(N, nullptr);
+  mvbOutlier.assign(N, false);
+}
+
 Frame::Frame(const cv::Mat& imGray, const cv::Mat& imDepth, const double& timeStamp,
              ORBextractor* extractor, ORBVocabulary* voc, cv::Mat& K, cv::Mat& distCoef,
              const float& bf, const float& thDepth, LineExtractor* lineExtractor)
     : mTimeStamp(timeStamp), mK(K.clone()), mDistCoef(distCoef.clone()), mbf(bf),
-      mThDepth(thDepth), mpORBvocabulary(voc) {
+      mThDepth(thDepth), mpORBextractorLeft(extractor), mpORBvocabulary(voc) {
   mnId = nNextId++;
-  mnScaleLevels = extractor->GetLevels();
-  mfScaleFactor = extractor->GetScaleFactor();
-  mvScaleFactors = extractor->GetScaleFactors();
-  mvInvScaleFactors = extractor->GetInverseScaleFactors();
-  mvLevelSigma2 = extractor->GetScaleSigmaSquares();
-  mvInvLevelSigma2 = extractor->GetInverseScaleSigmaSquares();
+  ScaleInfo(extractor);
   mnWidth = imGray.cols;
   mnHeight = imGray.rows;
   fx = K.at<float>(0, 0);
@@ -70,23 +104,8 @@ Frame::Frame(const cv::Mat& imGray, const cv::Mat& imDepth, const double& timeSt
   NL = (int)mvKeyLines.size();
   // UndistortKeyPoints + ComputeStereoFromRGBD + AssignFeaturesToGrid
   // (Frame.cc:160-204) in one call
+  PrepareKeys(imDepth.ptr<float>());
   const orbpl_camera cam = Camera();
-  mvKeysUn.resize(N);
-  mvDepth.resize(N);
-  mvuRight.resize(N);
-  std::vector<int32_t> cell(N);
-  float bounds[4];
-  check(orbpl_frame_prepare(&cam, reinterpret_cast<const orbpl_keypoint*>(mvKeys.data()), N,
-                            imDepth.ptr<float>(), reinterpret_cast<orbpl_keypoint*>(mvKeysUn.data()),
-                            mvDepth.data(), mvuRight.data(), cell.data(), bounds));
-  mnMinX = bounds[0];
-  mnMaxX = bounds[1];
-  mnMinY = bounds[2];
-  mnMaxY = bounds[3];
-  for (int i = 0; i < N; i++)
-    if (cell[i] >= 0) mGrid[cell[i] % FRAME_GRID_COLS][cell[i] / FRAME_GRID_COLS].push_back(i);
-  mvpMapPoints.assign(N, nullptr);
-  mvbOutlier.assign(N, false);
   // UndistortKeyLines + the line part of ComputeStereoFromRGBD
   mvKeyLinesUn.resize(NL);
   mvDepthLineStart.resize(NL);
@@ -100,6 +119,100 @@ Frame::Frame(const cv::Mat& imGray, const cv::Mat& imDepth, const double& timeSt
                                  mvuRightLineStart.data(), mvuRightLineEnd.data()));
   mvpMapLines.assign(NL, nullptr);
   mvbLineOutlier.assign(NL, false);
+}
+
+Frame::Frame(const cv::Mat& imLeft, const cv::Mat& imRight, const double& timeStamp,
+             ORBextractor* extractorLeft, ORBextractor* extractorRight, ORBVocabulary* voc,
+             cv::Mat& K, cv::Mat& distCoef, const float& bf, const float& thDepth)
+    : mTimeStamp(timeStamp), mK(K.clone()), mDistCoef(distCoef.clone()), mbf(bf),
+      mThDepth(thDepth), mpORBextractorLeft(extractorLeft), mpORBextractorRight(extractorRight),
+      mpORBvocabulary(voc) {
+  mnId = nNextId++;
+  ScaleInfo(extractorLeft);
+  mnWidth = imLeft.cols;
+  mnHeight = imLeft.rows;
+  // ORB extraction, left || right (Frame.cc:88-91); each extractor owns its
+  // own device context, so the two host threads never share one
+  std::exception_ptr rerr, lerr;
+  std::thread tr([&]() {
+    try {
+      (*mpORBextractorRight)(imRight, cv::Mat(), mvKeysRight, mDescriptorsRight);
+    } catch (...) {
+      rerr = std::current_exception();
+    }
+  });
+  try {
+    (*mpORBextractorLeft)(imLeft, cv::Mat(), mvKeys, mDescriptors);
+  } catch (...) {
+    lerr = std::current_exception();
+  }
+  tr.join();
+  if (lerr) std::rethrow_exception(lerr);
+  if (rerr) std::rethrow_exception(rerr);
+  N = (int)mvKeys.size();
+  NL = 0;
+  if (mvKeys.empty()) return;   // Frame.cc:95-96
+  fx = K.at<float>(0, 0);
+  fy = K.at<float>(1, 1);
+  cx = K.at<float>(0, 2);
+  cy = K.at<float>(1, 2);
+  invfx = 1.0f / fx;
+  invfy = 1.0f / fy;
+  mb = mbf / fx;   // Frame.cc:128
+  // UndistortKeyPoints, then ComputeStereoMatches, the map point slots,
+  // ComputeImageBounds and the grid (Frame.cc:98-131): the glue runs first
+  // here (no depth image: mvuRight / mvDepth = -1), the stereo matcher
+  // then overwrites them - the same values in the reference's order
+  PrepareKeys(nullptr);
+  ComputeStereoMatches();
+}
+
+void Frame::ComputeStereoMatches() {
+  if (!mpORBextractorLeft || !mpORBextractorRight || !mpORBextractorLeft->ctx() ||
+      !mpORBextractorRight->ctx())
+    throw std::runtime_error("Frame::ComputeStereoMatches: no stereo extractors");
+  mvuRight.assign(N, -1.0f);
+  mvDepth.assign(N, -1.0f);
+  if (N == 0) return;
+  const orbpl_camera cam = Camera();
+  const int nr = (int)mvKeysRight.size();
+  check(orbpl_stereo_matches(&cam, mpORBextractorLeft->ctx(), mpORBextractorRight->ctx(), 0,
+                             reinterpret_cast<const orbpl_keypoint*>(mvKeys.data()),
+                             mDescriptors.data, N,
+                             reinterpret_cast<const orbpl_keypoint*>(mvKeysRight.data()),
+                             nr ? mDescriptorsRight.data : nullptr, nr, mvuRight.data(),
+                             mvDepth.data()));
+}
+
+std::vector<size_t> Frame::GetFeaturesInArea(const float& x, const float& y, const float& r,
+                                              const int minLevel, const int maxLevel) const {
+  std::vector<size_t> vIndices;
+  vIndices.reserve(N);
+  const int nMinCellX = std::max(0, (int)std::floor((x - mnMinX - r) * mfGridElementWidthInv));
+  if (nMinCellX >= FRAME_GRID_COLS) return vIndices;
+  const int nMaxCellX = std::min((int)FRAME_GRID_COLS - 1,
+                                 (int)std::ceil((x - mnMinX + r) * mfGridElementWidthInv));
+  if (nMaxCellX < 0) return vIndices;
+  const int nMinCellY = std::max(0, (int)std::floor((y - mnMinY - r) * mfGridElementHeightInv));
+  if (nMinCellY >= FRAME_GRID_ROWS) return vIndices;
+  const int nMaxCellY = std::min((int)FRAME_GRID_ROWS - 1,
+                                 (int)std::ceil((y - mnMinY + r) * mfGridElementHeightInv));
+  if (nMaxCellY < 0) return vIndices;
+  const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+  for (int ix = nMinCellX; ix <= nMaxCellX; ix++)
+    for (int iy = nMinCellY; iy <= nMaxCellY; iy++) {
+      for (size_t j : mGrid[ix][iy]) {
+        const cv::KeyPoint& kpUn = mvKeysUn[j];
+        if (bCheckLevels) {
+          if (kpUn.octave < minLevel) continue;
+          if (maxLevel >= 0 && kpUn.octave > maxLevel) continue;
+        }
+        const float distx = kpUn.pt.x - x;
+        const float disty = kpUn.pt.y - y;
+        if (std::fabs(distx) < r && std::fabs(disty) < r) vIndices.push_back(j);
+      }
+    }
+  return vIndices;
 }
 
 void Frame::ComputeBoW() {

@@ -17,6 +17,12 @@
 //   dropin_driver --time <in.bin> <K>: K Frame constructions of frame 0 (ORB ||
 //   LineExtractor on two host threads + the frame glue, one frame at a time as
 //   the reference's Tracking builds them), median / mean latency in ms
+//   dropin_driver --stereo <in.bin> <out.bin>: two rectified stereo pairs
+//   through the stereo Frame (Frame.cc:71-132: ORB left || right,
+//   ComputeStereoMatches), GetFeaturesInArea queries on frame 0, frame 0's
+//   map from the stereo depths and frame 1's TrackWithMotionModel with zero
+//   velocity and th = 7 (Tracking.cc:1228-1271, points only: the stereo Frame
+//   has no lines); formats at stereo_mode()
 //   dropin_driver --fail: a Frame from an 8x8 image, which the library's
 //   extractors reject: the error must reach the caller as an exception (the
 //   line thread joined first), printed as "caught: <message>", exit 0
@@ -96,6 +102,129 @@ static std::vector<int32_t> node_of(const DBoW2::FeatureVector& fv, int n) {
   return node;
 }
 
+// Tracking::StereoInitialization's map (Tracking.cc:633-660): a map point per
+// keypoint with depth, its normal and scale-invariance distances as
+// MapPoint::UpdateNormalAndDepth sets them with the one observation
+static void map_points_from_depth(Frame& F0, std::vector<std::unique_ptr<MapPoint>>& mps,
+                                  std::map<const MapPoint*, int>& mp_index) {
+  const cv::Mat Ow = F0.GetCameraCenter();
+  for (int i = 0; i < F0.N; i++) {
+    if (!(F0.mvDepth[i] > 0)) continue;
+    cv::Mat X = F0.UnprojectStereo(i);
+    mps.emplace_back(new MapPoint(X.ptr<float>(), F0.mDescriptors.ptr<uint8_t>(i)));
+    float nrm[3];
+    double dd = 0;
+    for (int k = 0; k < 3; k++) {
+      nrm[k] = X.at<float>(k, 0) - Ow.at<float>(k, 0);
+      dd += (double)nrm[k] * nrm[k];
+    }
+    const float dn = (float)std::sqrt(dd);
+    for (int k = 0; k < 3; k++) nrm[k] = nrm[k] * (1.0f / dn);
+    const float maxd = dn * F0.mvScaleFactors[F0.mvKeysUn[i].octave];
+    mps.back()->SetNormalAndDistances(nrm, maxd / F0.mvScaleFactors[F0.mnScaleLevels - 1], maxd);
+    F0.mvpMapPoints[i] = mps.back().get();
+    mp_index[mps.back().get()] = i;
+  }
+}
+
+// in.bin : int32 W, H; float fx fy cx cy k1 k2 p1 p2 k3 bf thdepth;
+//          int32 nfeatures; float scale; int32 nlevels, iniTh, minTh;
+//          float Tcw0[16]; 2 x (left W*H u8, right W*H u8);
+//          int32 Q; Q x (float x, y, r; int32 minLevel, maxLevel)
+// out.bin: per frame: N, kps (N x 28 B), desc (N x 32), Nr, right kps (Nr x
+//          28 B), keysUn (N x 28 B), uRight (N f32), depth (N f32);
+//          frame 0: per query the count and the indices (int32);
+//          frame 1: nmatches, inliers, Tcw1[16], match[N1] (frame-0 index or
+//          -1), outlier[N1] u8
+static int stereo_mode(const char* inp, const char* outp) {
+  FILE* in = fopen(inp, "rb");
+  if (!in) throw std::runtime_error("cannot open input");
+  int32_t wh[2];
+  float camv[11], Tcw0[16];
+  int32_t nf, nl, ini, mn;
+  float sf;
+  rd(in, wh, 2);
+  rd(in, camv, 11);
+  rd(in, &nf, 1);
+  rd(in, &sf, 1);
+  rd(in, &nl, 1);
+  rd(in, &ini, 1);
+  rd(in, &mn, 1);
+  rd(in, Tcw0, 16);
+  const int W = wh[0], H = wh[1];
+  std::vector<cv::Mat> L(2), R(2);
+  for (int k = 0; k < 2; k++) {
+    L[k] = cv::Mat(H, W, cv::CV_8U);
+    R[k] = cv::Mat(H, W, cv::CV_8U);
+    rd(in, L[k].data, (size_t)W * H);
+    rd(in, R[k].data, (size_t)W * H);
+  }
+  int32_t nq = 0;
+  rd(in, &nq, 1);
+  std::vector<float> qf(3 * (size_t)nq);
+  std::vector<int32_t> qi(2 * (size_t)nq);
+  for (int q = 0; q < nq; q++) {
+    rd(in, &qf[3 * q], 3);
+    rd(in, &qi[2 * q], 2);
+  }
+  fclose(in);
+  cv::Mat K = cv::Mat::eye(3, 3, cv::CV_32F);
+  K.at<float>(0, 0) = camv[0];
+  K.at<float>(1, 1) = camv[1];
+  K.at<float>(0, 2) = camv[2];
+  K.at<float>(1, 2) = camv[3];
+  cv::Mat dist(5, 1, cv::CV_32F);
+  for (int k = 0; k < 5; k++) dist.at<float>(k, 0) = camv[4 + k];
+  const float bf = camv[9], thDepth = camv[10];
+  // Tracking::Tracking: mpORBextractorLeft / Right (Tracking.cc:115-120)
+  ORBextractor exL(nf, sf, nl, ini, mn), exR(nf, sf, nl, ini, mn);
+  Frame F0(L[0], R[0], 0.0, &exL, &exR, nullptr, K, dist, bf, thDepth);
+  Frame F1(L[1], R[1], 1.0, &exL, &exR, nullptr, K, dist, bf, thDepth);
+  FILE* o = fopen(outp, "wb");
+  if (!o) throw std::runtime_error("cannot open output");
+  for (const Frame* F : {&F0, &F1}) {
+    wr(o, &F->N, 1);
+    wr(o, F->mvKeys.data(), F->N);
+    wr(o, F->mDescriptors.data, (size_t)F->N * 32);
+    const int32_t nr = (int32_t)F->mvKeysRight.size();
+    wr(o, &nr, 1);
+    wr(o, F->mvKeysRight.data(), nr);
+    wr(o, F->mvKeysUn.data(), F->N);
+    wr(o, F->mvuRight.data(), F->N);
+    wr(o, F->mvDepth.data(), F->N);
+  }
+  for (int q = 0; q < nq; q++) {
+    const std::vector<size_t> v =
+        F0.GetFeaturesInArea(qf[3 * q], qf[3 * q + 1], qf[3 * q + 2], qi[2 * q], qi[2 * q + 1]);
+    wr1<int32_t>(o, (int32_t)v.size());
+    for (size_t j : v) wr1<int32_t>(o, (int32_t)j);
+  }
+  // frame 0: pose Tcw0, its map; frame 1: TrackWithMotionModel, zero velocity
+  cv::Mat T0(4, 4, cv::CV_32F);
+  std::memcpy(T0.data, Tcw0, 64);
+  F0.SetPose(T0);
+  std::vector<std::unique_ptr<MapPoint>> mps;
+  std::map<const MapPoint*, int> mp_index;
+  map_points_from_depth(F0, mps, mp_index);
+  F1.SetPose(F0.mTcw);
+  ORBmatcher matcher(0.9f, true);
+  const int th = 7;   // STEREO (Tracking.cc:1238-1241)
+  int nmatches = matcher.SearchByProjection(F1, F0, th, false);
+  if (nmatches < 20) {
+    std::fill(F1.mvpMapPoints.begin(), F1.mvpMapPoints.end(), nullptr);
+    nmatches = matcher.SearchByProjection(F1, F0, 2 * th, false);
+  }
+  int ninl = 0;
+  if (nmatches >= 20) ninl = Optimizer::PoseOptimizationWithLines(&F1);   // NL = 0: points
+  wr(o, &nmatches, 1);
+  wr(o, &ninl, 1);
+  wr(o, F1.mTcw.ptr<float>(), 16);
+  write_index(o, F1.mvpMapPoints, mp_index);
+  for (int i = 0; i < F1.N; i++) wr1<uint8_t>(o, F1.mvbOutlier[i]);
+  fclose(o);
+  return 0;
+}
+
 static int fail_mode() {
   ORBextractor ex(1000, 1.2f, 8, 20, 7);
   cv::Mat K = cv::Mat::eye(3, 3, cv::CV_32F);
@@ -120,6 +249,14 @@ static int fail_mode() {
 
 int main(int argc, char** argv) {
   if (argc == 2 && std::string(argv[1]) == "--fail") return fail_mode();
+  if (argc == 4 && std::string(argv[1]) == "--stereo") {
+    try {
+      return stereo_mode(argv[2], argv[3]);
+    } catch (const std::exception& e) {
+      fprintf(stderr, "dropin_driver: %s\n", e.what());
+      return 1;
+    }
+  }
   const bool timing = argc == 4 && std::string(argv[1]) == "--time";
   if (argc != 3 && !timing) {
     fprintf(stderr, "usage: dropin_driver in.bin out.bin | dropin_driver --time in.bin K\n");
@@ -195,25 +332,7 @@ int main(int argc, char** argv) {
     std::vector<std::unique_ptr<MapLine>> mls;
     std::map<const MapPoint*, int> mp_index;
     std::map<const MapLine*, int> ml_index;
-    const cv::Mat Ow = F0.GetCameraCenter();
-    for (int i = 0; i < F0.N; i++) {
-      if (!(F0.mvDepth[i] > 0)) continue;
-      cv::Mat X = F0.UnprojectStereo(i);
-      mps.emplace_back(new MapPoint(X.ptr<float>(), F0.mDescriptors.ptr<uint8_t>(i)));
-      // MapPoint::UpdateNormalAndDepth with the one observation (MapPoint.cc:360-411)
-      float nrm[3];
-      double dd = 0;
-      for (int k = 0; k < 3; k++) {
-        nrm[k] = X.at<float>(k, 0) - Ow.at<float>(k, 0);
-        dd += (double)nrm[k] * nrm[k];
-      }
-      const float dn = (float)std::sqrt(dd);
-      for (int k = 0; k < 3; k++) nrm[k] = nrm[k] * (1.0f / dn);
-      const float maxd = dn * F0.mvScaleFactors[F0.mvKeysUn[i].octave];
-      mps.back()->SetNormalAndDistances(nrm, maxd / F0.mvScaleFactors[F0.mnScaleLevels - 1], maxd);
-      F0.mvpMapPoints[i] = mps.back().get();
-      mp_index[mps.back().get()] = i;
-    }
+    map_points_from_depth(F0, mps, mp_index);
     for (int j = 0; j < F0.NL; j++) {
       if (!(F0.mvDepthLineStart[j] > 0 && F0.mvDepthLineEnd[j] > 0)) continue;
       cv::Mat s = F0.UnprojectStereoLineStart(j), e = F0.UnprojectStereoLineEnd(j);

@@ -254,3 +254,121 @@ def test_dropin_frame_error_reaches_caller():
     r = subprocess.run([str(DRIVER), "--fail"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, (r.returncode, r.stdout, r.stderr)
     assert r.stdout.startswith("caught: "), r.stdout
+
+
+def _features_in_area(ku, gcell, bounds, x, y, r, min_level=-1, max_level=-1):
+    """Frame::GetFeaturesInArea (Frame.cc:432-485) restated in numpy float32
+    over the oracle's grid cells (gx + 64 gy per keypoint, index order within
+    a cell) and image bounds."""
+    f32 = np.float32
+    minx, maxx, miny, maxy = (f32(v) for v in bounds)
+    winv = f32(64) / f32(maxx - minx)
+    hinv = f32(48) / f32(maxy - miny)
+    x, y, r = f32(x), f32(y), f32(r)
+    x0 = max(0, int(np.floor(f32(f32(x - minx) - r) * winv)))
+    if x0 >= 64:
+        return []
+    x1 = min(63, int(np.ceil(f32(f32(x - minx) + r) * winv)))
+    if x1 < 0:
+        return []
+    y0 = max(0, int(np.floor(f32(f32(y - miny) - r) * hinv)))
+    if y0 >= 48:
+        return []
+    y1 = min(47, int(np.ceil(f32(f32(y - miny) + r) * hinv)))
+    if y1 < 0:
+        return []
+    check = min_level > 0 or max_level >= 0
+    out = []
+    for ix in range(x0, x1 + 1):
+        for iy in range(y0, y1 + 1):
+            for j in np.nonzero(gcell == ix + 64 * iy)[0]:
+                oc = int(ku["octave"][j])
+                if check and (oc < min_level or (max_level >= 0 and oc > max_level)):
+                    continue
+                if abs(f32(ku["x"][j] - x)) < r and abs(f32(ku["y"][j] - y)) < r:
+                    out.append(int(j))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [3, 4])
+def test_dropin_stereo_frame_matches_oracle(tmp_path, seed):
+    """The drop-in stereo Frame (Frame.cc:71-132: ORB left || right on two
+    host threads, ComputeStereoMatches on the two extractors' device
+    pyramids), GetFeaturesInArea, and frame 1's TrackWithMotionModel (th = 7,
+    zero velocity, PoseOptimizationWithLines with NL = 0) against the oracle:
+    keypoints, descriptors, right keypoints, mvKeysUn, mvuRight and mvDepth
+    bit-exact, the query results equal, the pose within 1e-4 of the oracle's
+    stereo VO loop (LVO.step_stereo) with identical match and inlier counts."""
+    load_pkg()
+    O = load_oracle()
+    assert DRIVER.exists(), "build the drop-in first (make -C .../dropin)"
+    from _scenes import stereo_sequence
+    cfg, traj, pairs = stereo_sequence(2, seed)
+    (l0, r0), (l1, r1) = pairs
+    H, W = l0.shape
+    orb = (2000, 1.2, 8, 20, 7)
+    p = O.params(*orb)
+    cam = O.camera(cfg)
+    T0 = np.linalg.inv(traj[0]).astype(np.float32)
+    camv = [cfg["fx"], cfg["fy"], cfg["cx"], cfg["cy"], cfg["k1"], cfg["k2"], cfg["p1"],
+            cfg["p2"], cfg["k3"], cam.bf, cam.th_depth]
+    queries = [(300.0, 150.0, 20.0, -1, -1), (620.5, 190.25, 7.0, -1, -1),
+               (900.0, 60.0, 40.0, 1, 3), (100.0, 300.0, 15.0, 0, 0), (5.0, 5.0, 3.0, -1, -1),
+               (-50.0, 100.0, 10.0, -1, -1), (1300.0, 100.0, 30.0, -1, -1),
+               (700.0, 200.0, 60.0, 2, -1)]
+    inp = tmp_path / "in.bin"
+    with open(inp, "wb") as f:
+        f.write(struct.pack("<2i", W, H))
+        f.write(np.asarray(camv, np.float32).tobytes())
+        f.write(struct.pack("<ifiii", orb[0], orb[1], orb[2], orb[3], orb[4]))
+        f.write(T0.tobytes())
+        for left, right in pairs:
+            f.write(np.ascontiguousarray(left, np.uint8).tobytes())
+            f.write(np.ascontiguousarray(right, np.uint8).tobytes())
+        f.write(struct.pack("<i", len(queries)))
+        for q in queries:
+            f.write(struct.pack("<3f2i", *q))
+    out = tmp_path / "out.bin"
+    r = subprocess.run([str(DRIVER), "--stereo", str(inp), str(out)], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    R = _Reader(out.read_bytes())
+    KP = O.KP_DTYPE
+    frames = []
+    for left, right in pairs:
+        n = R.i32()
+        kps = R.arr(KP, n)
+        desc = R.arr(np.uint8, n * 32, (n, 32))
+        nr = R.i32()
+        kpr = R.arr(KP, nr)
+        ku = R.arr(KP, n)
+        ur = R.arr(np.float32, n)
+        dep = R.arr(np.float32, n)
+        okps, odesc, _ = O.extract(p, left)
+        okr, odr, _ = O.extract(p, right)
+        assert kps.tobytes() == okps.tobytes() and np.array_equal(desc, odesc)
+        assert kpr.tobytes() == okr.tobytes()
+        oku, _, _, ogc, ob = O.frame_prepare(cam, okps, None)
+        assert ku.tobytes() == oku.tobytes()
+        our, odep = O.stereo_matches(cam, p, left, right, okps, odesc, okr, odr)
+        assert ur.view(np.uint32).tobytes() == our.view(np.uint32).tobytes()
+        assert dep.view(np.uint32).tobytes() == odep.view(np.uint32).tobytes()
+        assert (dep > 0).sum() > 0.3 * n
+        frames.append((oku, ogc, ob))
+    oku, ogc, ob = frames[0]
+    nonempty = 0
+    for q in queries:
+        k = R.i32()
+        got = R.arr(np.int32, k).tolist()
+        assert got == _features_in_area(oku, ogc, ob, *q), q
+        nonempty += k > 0
+    assert nonempty >= 4
+    nm, ninl = R.i32(2)
+    T1 = R.arr(np.float32, 16, (4, 4))
+    lvo = O.LVO(p, cam, 1, use_lines=False)
+    lvo.reset(T0.reshape(1, 16))
+    lvo.step_stereo(0, l0, r0)
+    To, so = lvo.step_stereo(0, l1, r1)
+    assert (nm, ninl) == (so["nmatches"], so["ninliers"]) and nm > 100
+    assert np.abs(T1 - To).max() < 1e-4

@@ -119,3 +119,9 @@ def test_lsd_traffic_counts(oracle):
     assert 10 * n < t["sort_cmp"] < 30 * n and t["sort_moves"] > n
     assert t["nfa_evals"] >= t["segments"] and t["nfa_px"] > t["nfa_evals"]
     assert t["grows"] >= t["nfa_evals"] / 16
+    # distinct addresses: bounded by the image and by the access counts
+    assert t["sort_n"] == n
+    assert t["u_used_px"] <= t["u_seed_px"] <= sw * sh
+    assert t["u_seed_px"] <= t["seeds"] + t["grow_nb"]
+    assert t["u_q_px"] <= t["u_used_px"] and t["u_nfa_px"] <= min(t["nfa_px"], sw * sh)
+    assert 0 < t["max_reg"] < sw * sh and t["segments"] <= t["rects"] <= t["nfa_evals"]

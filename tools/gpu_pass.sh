@@ -9,6 +9,8 @@
 #   smoke               __graft_entry__.smoke()
 #   bench[=<args>]      bench.py <args> (commas become spaces), JSON in bench_<n>.json
 #   prof=<MODE>         tools/prof.sh <tag> with MODE=points|lines|kitti|rig
+#   faithful=<workload> tools/cpu_faithful.py <workload> (no GPU): the reference-
+#                       faithful CPU loop, JSON appended to faithful.jsonl
 #   env=<NAME=VALUE>    exported for the steps after it
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
@@ -38,6 +40,9 @@ for step in "$@"; do
       tail -c 400 $O/bench_$n.json ;;
     prof)
       MODE=$arg bash tools/prof.sh ${tag}_$arg || exit 1 ;;
+    faithful)
+      timeout -k 10 600 python -u tools/cpu_faithful.py ${arg:-lines} 300 6 >> $O/faithful.jsonl 2> $O/faithful_$n.err || { echo "faithful failed"; tail -5 $O/faithful_$n.err; exit 1; }
+      tail -1 $O/faithful.jsonl | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('faithful', d['workload'], d['median_ms_per_frame'], d.get('stage_median_ms'), d['affinity'].get('pinned'))" ;;
     env)
       export "$arg"; echo "env $arg" ;;
     *) echo "unknown step $step"; exit 2 ;;
