@@ -2114,9 +2114,8 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
 // (identical candidates; ~0.6x the round loop's modelled cycles at batch 1).
 // ---------------------------------------------------------------------------
 constexpr int kStW = kStWSlots;   // window slots (power of two)
-constexpr int kStSteps = 4;       // lockstep grow steps per iteration
 constexpr int kStFitBatch = 16;   // queued fit phases that start a pass batch
-enum { kSlFree = 0, kSlActive = 1, kSlDone = 2, kSlConflict = 3, kSlOverflow = 4 };
+enum { kSlFree = 0, kSlActive = 1, kSlDone = 2, kSlConflict = 3, kSlOverflow = 4, kSlAbort = 5 };
 enum { kResSmall = 0, kResFail = 1, kResCand = 2, kResSkip = 3 };
 enum { kPhIdle = 0, kPhGrow1 = 1, kPhRect1 = 2, kPhGrow2 = 3, kPhRect2 = 4 };
 // s_info: state (3 bits) | result << 3 (2 bits) | lane << 5 (6 bits) | pinned << 11
@@ -2135,7 +2134,9 @@ struct GrowSt {
   float sumdx, sumdy;
   double reg_angle, prec;
   uint32_t myval;
+  bool lazy;   // the seed pixel's stamp is tested by the first step (gs_start_q)
 };
+constexpr int kSpecSkip = -3;   // gs_step: the seed pixel is USED (the seed is skipped)
 
 __device__ __forceinline__ int gs_start(GrowSt& s, uint64_t* sd, LaneBuf buf, int cap, int sx, int sy,
                                         double prec, uint32_t myval, int tw, uint32_t& blocker) {
@@ -2161,7 +2162,30 @@ __device__ __forceinline__ int gs_start(GrowSt& s, uint64_t* sd, LaneBuf buf, in
   s.myval = myval;
   s.i = 0;
   s.n = 1;
+  s.lazy = false;
   return 0;
+}
+
+// gs_start for a queued seed whose degrees the scan loaded: the claim is sent
+// without waiting for the stamp; the first step reads the seed pixel's stamp
+// with its neighbourhood (USED: kSpecSkip; an earlier seed's: conflict)
+__device__ __forceinline__ void gs_start_q(GrowSt& s, uint64_t* sd, LaneBuf buf, uint32_t pt,
+                                           uint32_t degbits, double prec, uint32_t myval, int tw) {
+  const int sx = (int)(pt & 0xFFFF), sy = (int)(pt >> 16);
+  atomicMin(reinterpret_cast<unsigned long long*>(sd + lsd_sd_index(sx, sy, tw)),
+            ((unsigned long long)myval << 32) | degbits);
+  s.cur = make_uint4(pt, degbits, 0u, 0u);
+  buf[0] = s.cur;
+  s.reg_angle = deg2ang(entry_deg(s.cur));
+  double s0, c0;
+  lsdm::sincos_(s.reg_angle, &s0, &c0);
+  s.sumdx = (float)c0;
+  s.sumdy = (float)s0;
+  s.prec = prec;
+  s.myval = myval;
+  s.i = 0;
+  s.n = 1;
+  s.lazy = true;
 }
 
 // one point expansion; 1 = the region is complete, 0 = continue, or
@@ -2186,11 +2210,20 @@ __device__ __forceinline__ int gs_step(GrowSt& s, const Frame& F, uint64_t* sd, 
     cterm[d] = (((uint32_t)(cx >> 2) << 5) | ((uint32_t)(cx & 3) << 1)) << 3;
   }
   uint4 w[9];
+  const bool centre = s.lazy && s.i == 0;
 #pragma unroll
   for (int k = 0; k < 9; k++) {
-    if (k == 4) continue;
+    if (k == 4 && !centre) continue;
     w[k] = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(sd) +
                                            (rterm[k / 3] + cterm[k % 3]));
+  }
+  if (centre) {
+    const uint32_t st = w[4].y;
+    if (st == 0u) return kSpecSkip;
+    if ((st >> 1) < mytag) {
+      blocker = st >> 1;
+      return kSpecConflict;
+    }
   }
   unsigned ok = 0;
 #pragma unroll
@@ -2236,19 +2269,51 @@ __device__ __forceinline__ int gs_step(GrowSt& s, const Frame& F, uint64_t* sd, 
 }
 
 // release the stamps a seed holds among list entries [0, n) (its own tag,
-// either grow): they become free again
+// either grow): they become free again. Runs while no lane grows (the wave
+// is in one phase), so a load and a conditional store cannot interleave with
+// another seed's claim; loads 8 entries / stamps at a time.
 __device__ __forceinline__ void st_release(uint64_t* sd, LaneBuf buf, int n, uint32_t tag, int tw) {
   for (int j0 = 0; j0 < n; j0 += 8) {
-    uint32_t ev[8];
+    uint32_t ev[8], sv[8];
+    int id[8];
 #pragma unroll
     for (int u = 0; u < 8; u++) ev[u] = buf.pt(min(j0 + u, n - 1));
 #pragma unroll
     for (int u = 0; u < 8; u++) {
-      if (j0 + u >= n) break;
-      const int id = lsd_sd_index((int)(ev[u] & 0xFFFF), (int)(ev[u] >> 16), tw);
-      atomicCAS(sd_hi(sd, id), (tag << 1) | 1u, 0xFFFFFFFFu);
-      atomicCAS(sd_hi(sd, id), tag << 1, 0xFFFFFFFFu);
+      id[u] = lsd_sd_index((int)(ev[u] & 0xFFFF), (int)(ev[u] >> 16), tw);
+      sv[u] = ld_stamp(sd, id[u]);
     }
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+      if (j0 + u < n && (sv[u] >> 1) == tag && sv[u] != 0u)
+        __hip_atomic_store(sd_hi(sd, id[u]), 0xFFFFFFFFu, __ATOMIC_RELAXED, ORBPL_LSD_SCOPE);
+  }
+}
+
+// the commit of a checked seed: every touched pixel (all carry the seed's own
+// tag) released, then the final region [off, off + len) USED; both stores go
+// to the same lane's addresses in order, so a pixel of both ends USED
+__device__ __forceinline__ void st_commit(uint64_t* sd, LaneBuf lb, int touched, int off, int len,
+                                          int tw) {
+  for (int j0 = 0; j0 < touched; j0 += 8) {
+    uint32_t ev[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) ev[u] = lb.pt(min(j0 + u, touched - 1));
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+      if (j0 + u < touched)
+        __hip_atomic_store(sd_hi(sd, lsd_sd_index((int)(ev[u] & 0xFFFF), (int)(ev[u] >> 16), tw)),
+                           0xFFFFFFFFu, __ATOMIC_RELAXED, ORBPL_LSD_SCOPE);
+  }
+  for (int j0 = off; j0 < off + len; j0 += 8) {
+    uint32_t ev[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) ev[u] = lb.pt(min(j0 + u, off + len - 1));
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+      if (j0 + u < off + len)
+        __hip_atomic_store(sd_hi(sd, lsd_sd_index((int)(ev[u] & 0xFFFF), (int)(ev[u] >> 16), tw)),
+                           0u, __ATOMIC_RELAXED, ORBPL_LSD_SCOPE);
   }
 }
 
@@ -2340,11 +2405,19 @@ __device__ __forceinline__ void st_rect2(CoopScratch& S, int lane, bool act, uin
   }
 }
 
-constexpr int kStSlotCap = kStSlotEntries;   // touched-list entries a slot holds (longer lists pin the lane)
+constexpr int kStSlotCap = kStSlotEntries;   // a seed's list (both grows) in its slot
+constexpr int kStQ = 256;                    // pre-scanned seeds queued in LDS (power of two)
+constexpr int kStInner = 8;                  // grow steps between the wave's bookkeeping phases
 
+// A seed's list lives in its slot (slist[slot][kStSlotCap]) from the first
+// grow to the commit, so a lane whose seed is finished takes the next one
+// without moving anything: inside kStInner lockstep grow steps a lane that
+// completes a small region (or aborts) takes the next queued seed at once;
+// between those runs the wave releases aborted seeds, refills the seed
+// queue, refetches conflicts, runs the queued fit phases and commits.
 __global__ void __launch_bounds__(64) k_lsd_stream(LsdGeom g, LsdScratch sc) {
   __shared__ uint32_t s_pt[kStW], s_info[kStW], s_blk[kStW], s_tl[kStW], s_fin[kStW];
-  __shared__ int s_work[64];
+  __shared__ uint2 s_q[kStQ];   // (x | y << 16, degree bits)
   __shared__ CoopScratch s_coop;
   extern __shared__ uint32_t grow_smem[];
   const int f = blockIdx.x, lane = threadIdx.x;
@@ -2375,8 +2448,6 @@ __global__ void __launch_bounds__(64) k_lsd_stream(LsdGeom g, LsdScratch sc) {
   F.cs = sd + lsd_cs_offset(sw, sh);
   F.tw = lsd_sd_tw(sw);
   const int tw = F.tw;
-  const LaneBuf buf{sc.lbuf + ((long long)f * kSpecLanes + lane) * kLaneCap};
-  uint4* const my_bp = sc.lbuf + ((long long)f * kSpecLanes + lane) * kLaneCap;
   uint4* const slist = sc.stlist + (long long)f * kStW * kStSlotCap;
   double* const srect = sc.strect + (long long)f * kStW * 12;
   const uint32_t* A = sc.A + (long long)f * g.n;
@@ -2390,302 +2461,281 @@ __global__ void __launch_bounds__(64) k_lsd_stream(LsdGeom g, LsdScratch sc) {
   // lane state
   int ph = kPhIdle;
   uint32_t my_t = 0;   // the slot tag this lane works on (0: none)
-  bool pinned = false;
   GrowSt gs;
   int n1 = 0, x0 = 0, y0 = 0;
   double ra1 = 0;
   Rect rec;
   // wave-uniform state
   uint32_t head_t = 1, next_t = 1;
-  int scan = 0, nl = 0;
-  long long n_iter = 0, n_gsteps = 0, n_batches = 0, n_conf = 0, n_fetch = 0, n_coop = 0;
+  int scan = 0, nl = 0, qh = 0, qt = 0;
+  long long n_iter = 0, n_coop = 0, n_fetch = 0;
+  long long c_book = 0, c_grow = 0, c_fit = 0, c_commit = 0;
   const long long t_all = clock64();
-  // a lane finishes its slot: result, final range, touched list to the slot
-  // (or the lane stays pinned to it)
-  auto finish = [&](bool act, int res, int off, int len, int touched) {
-    const int si = (int)(my_t & (kStW - 1));
-    bool pin = false;
-    if (act) {
-      pin = touched > kStSlotCap;
-      if (!pin)
-        for (int j = 0; j < touched; j++) slist[si * kStSlotCap + j] = buf[j];
-      if (res == kResCand) {
-        double* o = srect + si * 12;
-        o[0] = rec.x1; o[1] = rec.y1; o[2] = rec.x2; o[3] = rec.y2;
-        o[4] = rec.width; o[5] = rec.x; o[6] = rec.y; o[7] = rec.theta;
-        o[8] = rec.dx; o[9] = rec.dy; o[10] = rec.prec; o[11] = rec.p;
-      }
-      s_tl[si] = (uint32_t)touched;
-      s_fin[si] = (uint32_t)off | ((uint32_t)len << 16);
-      s_info[si] = sl_info(kSlDone, res, lane, pin ? 1 : 0);
-      pinned = pin;
-      ph = kPhIdle;
-      if (!pin) my_t = 0;
+  auto slot = [](uint32_t t) { return (int)(t & (kStW - 1)); };
+  auto lbuf_of = [&](uint32_t t) { return LaneBuf{slist + slot(t) * kStSlotCap}; };
+  // a lane's seed is final: result, final range, touched count (the list is
+  // already in the slot)
+  auto finish = [&](int res, int off, int len, int touched) {
+    const int si = slot(my_t);
+    if (res == kResCand) {
+      double* o = srect + si * 12;
+      o[0] = rec.x1; o[1] = rec.y1; o[2] = rec.x2; o[3] = rec.y2;
+      o[4] = rec.width; o[5] = rec.x; o[6] = rec.y; o[7] = rec.theta;
+      o[8] = rec.dx; o[9] = rec.dy; o[10] = rec.prec; o[11] = rec.p;
     }
+    s_tl[si] = (uint32_t)touched;
+    s_fin[si] = (uint32_t)off | ((uint32_t)len << 16);
+    s_info[si] = sl_info(kSlDone, res, lane, 0);
+    ph = kPhIdle;
+    my_t = 0;
   };
-  // a lane's seed aborts: release, conflict with its blocker
-  auto abort_seed = [&](bool act, int st, uint32_t blocker, int nlist_touched) {
-    if (act) {
-      st_release(sd, buf, nlist_touched, my_t, tw);
-      const int si = (int)(my_t & (kStW - 1));
-      s_blk[si] = st == kSpecOverflow ? 0u : blocker;
-      s_info[si] = sl_info(st == kSpecOverflow ? kSlOverflow : kSlConflict, 0, lane, 0);
-      ph = kPhIdle;
-      my_t = 0;
+  // a lane's seed aborts: its claims are released in the next bookkeeping
+  // phase (kSlAbort), then it waits for its blocker (conflict) or the head
+  // (overflow)
+  auto abort_seed = [&](int st, uint32_t blocker, int touched) {
+    const int si = slot(my_t);
+    s_tl[si] = (uint32_t)touched;
+    s_blk[si] = st == kSpecOverflow ? 0xFFFFFFFFu : blocker;
+    s_info[si] = sl_info(kSlAbort, 0, lane, 0);
+    ph = kPhIdle;
+    my_t = 0;
+  };
+  // idle lanes take queued seeds in list order (new slots), wave-wide
+  auto take_new = [&]() {
+    const bool idle = ph == kPhIdle;
+    const unsigned long long im = __ballot(idle);
+    const int take = min(min(__popcll(im), qt - qh), kStW - (int)(next_t - head_t));
+    if (take <= 0) return;
+    const int r = __popcll(im & lt_mask);
+    if (idle && r < take) {
+      my_t = next_t + (uint32_t)r;
+      const int si = slot(my_t);
+      const uint2 q = s_q[(qh + r) & (kStQ - 1)];
+      s_pt[si] = q.x;
+      s_info[si] = sl_info(kSlActive, 0, lane, 0);
+      gs_start_q(gs, sd, lbuf_of(my_t), q.x, q.y, prec, (my_t << 1) | 1u, tw);
+      ph = kPhGrow1;
     }
+    next_t += (uint32_t)take;
+    qh += take;
+    n_fetch += take;
   };
   while (true) {
     n_iter++;
-    // ---- 1. idle lanes take work: refetched conflicts, then new seeds ----
-    {
-      const bool idle = ph == kPhIdle && !pinned;
-      const unsigned long long im = __ballot(idle);
-      int nidle = __popcll(im);
-      int nwork = 0;
-      if (nidle > 0) {
-        // conflicted slots among the window's first 64 whose blocker committed
-        const uint32_t t = head_t + (uint32_t)lane;
-        bool ref = false;
-        if (t < next_t) {
-          const int si = (int)(t & (kStW - 1));
-          const uint32_t inf = s_info[si];
-          if (sl_state(inf) == kSlConflict && s_blk[si] < head_t) {
-            const uint32_t pt = s_pt[si];
-            if (ld_stamp(sd, lsd_sd_index((int)(pt & 0xFFFF), (int)(pt >> 16), tw)) == 0u) {
-              s_tl[si] = 0;
-              s_fin[si] = 0;
-              s_info[si] = sl_info(kSlDone, kResSkip, 0, 0);   // covered: skipped
-            } else {
-              ref = true;
-            }
-          }
-        }
-        const unsigned long long rm = __ballot(ref);
-        const int nref = min(__popcll(rm), nidle);
-        if (ref) {
-          const int r = __popcll(rm & lt_mask);
-          if (r < nref) {
-            s_work[r] = (int)t;
-            s_info[(int)(t & (kStW - 1))] = sl_info(kSlActive, 0, 0, 0);
-          }
-        }
-        nwork = nref;
-        // new seeds in list order while the window has room
-        while (nwork < nidle && scan < nlist && (int)(next_t - head_t) < kStW) {
-          const int i = scan + lane;
-          bool c = false;
-          int px = 0, py = 0;
-          if (i < nlist) {
-            const int idx = (int)(A[i] & 0x3FFFFFu);
-            py = idx / w1;
-            px = idx - py * w1;
-            const uint64_t v = ld_sd(sd + lsd_sd_index(px, py, tw));
-            c = __uint_as_float((uint32_t)v) >= 0.f && (uint32_t)(v >> 32) != 0u;
-          }
-          const unsigned long long m = __ballot(c);
-          const int room = min(nidle - nwork, kStW - (int)(next_t - head_t));
-          const int before = __popcll(m & lt_mask);
-          if (c && before < room) {
-            const uint32_t t2 = next_t + (uint32_t)before;
-            const int si = (int)(t2 & (kStW - 1));
-            s_pt[si] = (uint32_t)px | ((uint32_t)py << 16);
-            s_info[si] = sl_info(kSlActive, 0, 0, 0);
-            s_work[nwork + before] = (int)t2;
-          }
-          const int take = min(__popcll(m), room);
-          if (take == __popcll(m) || take == 0) {
-            scan += 64;
-            if (take == 0 && __popcll(m) > 0) break;
+    const long long tc0 = clock64();
+    // ---- kStInner lockstep grow steps, finished lanes refilled at once ----
+    for (int k = 0; k < kStInner; k++) {
+      const bool grow = ph == kPhGrow1 || ph == kPhGrow2;
+      if (!__ballot(grow)) break;
+      if (grow) {
+        const LaneBuf lb = lbuf_of(my_t);
+        const LaneBuf gb = ph == kPhGrow1 ? lb : lb + n1;
+        const int cap = ph == kPhGrow1 ? kStSlotCap : kStSlotCap - n1;
+        uint32_t blocker = 0;
+        const int r = gs_step(gs, F, sd, gb, cap, blocker);
+        if (r == kSpecSkip) {
+          finish(kResSkip, 0, 0, 0);   // USED since the scan: nothing of it was claimed
+        } else if (r < 0) {
+          abort_seed(r, blocker, ph == kPhGrow1 ? gs.n : n1 + gs.n);
+        } else if (r > 0) {
+          if (ph == kPhGrow1) {
+            n1 = gs.n;
+            ra1 = gs.reg_angle;
+            if (n1 < g.min_reg_size) finish(kResSmall, 0, n1, n1);
+            else ph = kPhRect1;
           } else {
-            // the list position after the last seed taken
-            const unsigned long long mm = __ballot(c && before == take - 1);
-            scan = scan + __ffsll((long long)mm);
-          }
-          next_t += (uint32_t)take;
-          nwork += take;
-          n_fetch += take;
-        }
-        if (scan > nlist) scan = nlist;
-        __threadfence_block();
-        __builtin_amdgcn_wave_barrier();
-        // the r-th idle lane takes work item r
-        const int r = __popcll(im & lt_mask);
-        if (idle && r < nwork) {
-          my_t = (uint32_t)s_work[r];
-          const int si = (int)(my_t & (kStW - 1));
-          s_info[si] = sl_info(kSlActive, 0, lane, 0);
-          const uint32_t pt = s_pt[si];
-          uint32_t blocker = 0;
-          const int st = gs_start(gs, sd, buf, kLaneCap, (int)(pt & 0xFFFF), (int)(pt >> 16), prec,
-                                  (my_t << 1) | 1u, tw, blocker);
-          ph = kPhGrow1;
-          if (st != 0) {
-            abort_seed(true, st, blocker, 0);
-            n_conf++;
-          }
-        }
-        __builtin_amdgcn_wave_barrier();
-      }
-    }
-    // ---- 2. lockstep grow steps (first grows and refine's second grows) ----
-    bool gdone = false;
-    int gst = 0;
-    uint32_t gblk = 0;
-    if (__ballot(ph == kPhGrow1 || ph == kPhGrow2)) {
-      n_gsteps++;
-#pragma unroll 1
-      for (int k = 0; k < kStSteps; k++) {
-        const bool grow = (ph == kPhGrow1 || ph == kPhGrow2) && !gdone;
-        if (!__ballot(grow)) break;
-        if (grow) {
-          const LaneBuf gb = ph == kPhGrow1 ? buf : buf + n1;
-          const int cap = ph == kPhGrow1 ? kLaneCap : kLaneCap - n1;
-          const int r = gs_step(gs, F, sd, gb, cap, gblk);
-          if (r != 0) {
-            gdone = true;
-            gst = r;
+            ph = kPhRect2;
           }
         }
       }
-      wg_fence();
+      __threadfence_block();
       __builtin_amdgcn_wave_barrier();
-      // classify the grows that ended
-      if (gdone) {
-        if (gst < 0) {
-          abort_seed(true, gst, gblk, ph == kPhGrow1 ? gs.n : n1 + gs.n);
-          n_conf++;
-        } else if (ph == kPhGrow1) {
-          n1 = gs.n;
-          ra1 = gs.reg_angle;
-          if (n1 < g.min_reg_size) finish(true, kResSmall, 0, n1, n1);
-          else ph = kPhRect1;
-        } else {
-          ph = kPhRect2;
+      take_new();
+    }
+    wg_fence();
+    __builtin_amdgcn_wave_barrier();
+    const long long tc1 = clock64();
+    c_grow += tc1 - tc0;
+    // ---- bookkeeping: release aborted seeds, refill the queue, refetch ----
+    {
+      for (int i0 = 0; i0 < kStW; i0 += 64) {
+        const uint32_t t = head_t + (uint32_t)(i0 + lane);
+        if (t < next_t) {
+          const int si = slot(t);
+          const uint32_t inf = s_info[si];
+          if (sl_state(inf) == kSlAbort) {
+            st_release(sd, lbuf_of(t), (int)s_tl[si], t, tw);
+            const bool ovf = s_blk[si] == 0xFFFFFFFFu;
+            s_blk[si] = ovf ? 0u : s_blk[si];
+            s_info[si] = sl_info(ovf ? kSlOverflow : kSlConflict, 0, 0, 0);
+          }
         }
       }
+      // the seed queue: defined, not USED list entries, 64 per load
+      while (qt - qh <= kStQ - 64 && scan < nlist) {
+        const int i = scan + lane;
+        bool c = false;
+        uint2 q = make_uint2(0u, 0u);
+        if (i < nlist) {
+          const int idx = (int)(A[i] & 0x3FFFFFu);
+          const int py = idx / w1, px = idx - py * w1;
+          const uint64_t v = ld_sd(sd + lsd_sd_index(px, py, tw));
+          c = __uint_as_float((uint32_t)v) >= 0.f && (uint32_t)(v >> 32) != 0u;
+          q = make_uint2((uint32_t)px | ((uint32_t)py << 16), (uint32_t)v);
+        }
+        const unsigned long long m = __ballot(c);
+        if (c) s_q[(qt + __popcll(m & lt_mask)) & (kStQ - 1)] = q;
+        qt += __popcll(m);
+        scan += 64;
+        if (qt - qh >= 128) break;   // enough for this run; loads stay off the chain
+      }
+      if (scan > nlist) scan = nlist;
+      // conflicted seeds among the window's first 64 whose blocker committed:
+      // skipped if covered, else taken by an idle lane (regrown)
+      const uint32_t t = head_t + (uint32_t)lane;
+      bool ref = false;
+      if (t < next_t) {
+        const int si = slot(t);
+        if (sl_state(s_info[si]) == kSlConflict && s_blk[si] < head_t) {
+          const uint32_t pt = s_pt[si];
+          if (ld_stamp(sd, lsd_sd_index((int)(pt & 0xFFFF), (int)(pt >> 16), tw)) == 0u) {
+            s_tl[si] = 0;
+            s_fin[si] = 0;
+            s_info[si] = sl_info(kSlDone, kResSkip, 0, 0);
+          } else {
+            ref = true;
+          }
+        }
+      }
+      __threadfence_block();
+      __builtin_amdgcn_wave_barrier();
+      const unsigned long long rm = __ballot(ref);
+      const bool idle = ph == kPhIdle;
+      const unsigned long long im = __ballot(idle);
+      const int nref = min(__popcll(rm), __popcll(im));
+      // the r-th refetch (window order) goes to the r-th idle lane
+      int* s_ref = reinterpret_cast<int*>(&s_coop);   // scratch: the pass batch is not running
+      if (ref) {
+        const int r = __popcll(rm & lt_mask);
+        if (r < nref) s_ref[r] = (int)t;
+      }
+      __threadfence_block();
+      __builtin_amdgcn_wave_barrier();
+      const int ri = __popcll(im & lt_mask);
+      if (idle && ri < nref) {
+        my_t = (uint32_t)s_ref[ri];
+        const int si = slot(my_t);
+        s_info[si] = sl_info(kSlActive, 0, lane, 0);
+        const uint32_t pt = s_pt[si];
+        uint32_t blocker = 0;
+        const int st = gs_start(gs, sd, lbuf_of(my_t), kStSlotCap, (int)(pt & 0xFFFF),
+                                (int)(pt >> 16), prec, (my_t << 1) | 1u, tw, blocker);
+        ph = kPhGrow1;
+        if (st != 0) abort_seed(st, blocker, 0);
+      }
+      __threadfence_block();
+      __builtin_amdgcn_wave_barrier();
+      take_new();
+      __threadfence_block();
+      __builtin_amdgcn_wave_barrier();
     }
-    // ---- 3. the fit's pass phases in a batch ----
+    const long long tc2 = clock64();
+    c_book += tc2 - tc1;
+    // ---- the fit's pass phases in a batch ----
     {
       const unsigned long long wm = __ballot(ph == kPhRect1 || ph == kPhRect2);
       const bool any_grow = __ballot(ph == kPhGrow1 || ph == kPhGrow2) != 0;
-      const uint32_t hinf = s_info[head_t & (kStW - 1)];
-      const int hl = sl_lane(hinf);
+      const uint32_t hinf = s_info[slot(head_t)];
       const bool head_waits = head_t < next_t && sl_state(hinf) == kSlActive &&
-                              (__shfl(ph, hl, 64) == kPhRect1 || __shfl(ph, hl, 64) == kPhRect2) &&
-                              __shfl((int)my_t, hl, 64) == (int)head_t;
+                              (__shfl(ph, sl_lane(hinf), 64) == kPhRect1 ||
+                               __shfl(ph, sl_lane(hinf), 64) == kPhRect2);
       if (wm && (__popcll(wm) >= kStFitBatch || head_waits || !any_grow)) {
-        n_batches++;
-        // phase 1: region2rect + refine's test / statistics
+        uint4* const my_bp = slist + slot(my_t) * kStSlotCap;
         const bool r1 = ph == kPhRect1;
         double tau = 0;
         if (r1) {
-          x0 = pt_x(buf[0]);
-          y0 = pt_y(buf[0]);
+          const uint4 e0 = my_bp[0];
+          x0 = pt_x(e0);
+          y0 = pt_y(e0);
         }
         const bool again = st_rect1(s_coop, lane, r1, my_bp, n1, F, ra1, prec, p, rec, tau);
-        if (r1 && !again) finish(true, kResCand, 0, n1, n1);
+        if (r1 && !again) finish(kResCand, 0, n1, n1);
         if (r1 && again) {
           uint32_t blocker = 0;
-          const int st = gs_start(gs, sd, buf + n1, kLaneCap - n1, x0, y0, tau, my_t << 1, tw,
-                                  blocker);
+          const int st = gs_start(gs, sd, LaneBuf{my_bp} + n1, kStSlotCap - n1, x0, y0, tau,
+                                  my_t << 1, tw, blocker);
           ph = kPhGrow2;
-          if (st != 0) {
-            abort_seed(true, st, blocker, n1);
-            n_conf++;
-          }
+          if (st != 0) abort_seed(st, blocker, n1);
         }
-        // phase 2: the second region's rectangle and reduce_region_radius
         const bool r2 = ph == kPhRect2;
         int res = kResFail, len = 0;
         const int n2 = r2 ? gs.n : 0;
         st_rect2(s_coop, lane, r2, my_bp + n1, n2, x0, y0, F, gs.reg_angle, prec, p, rec, res, len);
-        if (r2) finish(true, res, n1, len, n1 + n2);
+        if (r2) finish(res, n1, len, n1 + n2);
         wg_fence();
         __builtin_amdgcn_wave_barrier();
       }
     }
-    // ---- 4. commit from the head: up to 64 consecutive finished seeds ----
-    wg_fence();
-    __builtin_amdgcn_wave_barrier();
+    const long long tc3 = clock64();
+    c_fit += tc3 - tc2;
+    // ---- commit from the head: up to 64 consecutive finished seeds ----
     {
       const uint32_t t = head_t + (uint32_t)lane;
-      const int si = (int)(t & (kStW - 1));
+      const int si = slot(t);
       const uint32_t inf = t < next_t ? s_info[si] : 0u;
       const bool done = t < next_t && sl_state(inf) == kSlDone;
       const unsigned long long nd = __ballot(!done);
       const int run = nd ? __ffsll((long long)nd) - 1 : 64;
-      bool bad = false;
-      const int touched = (int)s_tl[si];
-      const bool pin = sl_pin(inf);
-      const int ol = sl_lane(inf);
-      const LaneBuf lb{pin ? sc.lbuf + ((long long)f * kSpecLanes + ol) * kLaneCap
-                           : slist + si * kStSlotCap};
-      if (lane < run && sl_res(inf) != kResSkip) {
-        for (int j0 = 0; j0 < touched && !bad; j0 += 8) {
-          uint32_t ev[8], sv[8];
+      if (run > 0) {
+        bool bad = false;
+        const int touched = (int)s_tl[si];
+        const LaneBuf lb = lbuf_of(t);
+        if (lane < run) {
+          for (int j0 = 0; j0 < touched && !bad; j0 += 8) {
+            uint32_t ev[8], sv[8];
 #pragma unroll
-          for (int u = 0; u < 8; u++) ev[u] = lb.pt(min(j0 + u, touched - 1));
+            for (int u = 0; u < 8; u++) ev[u] = lb.pt(min(j0 + u, touched - 1));
 #pragma unroll
-          for (int u = 0; u < 8; u++)
-            sv[u] = ld_stamp(sd, lsd_sd_index((int)(ev[u] & 0xFFFF), (int)(ev[u] >> 16), tw));
+            for (int u = 0; u < 8; u++)
+              sv[u] = ld_stamp(sd, lsd_sd_index((int)(ev[u] & 0xFFFF), (int)(ev[u] >> 16), tw));
 #pragma unroll
-          for (int u = 0; u < 8; u++) bad |= sv[u] == 0u || (sv[u] >> 1) != t;
+            for (int u = 0; u < 8; u++) bad |= sv[u] == 0u || (sv[u] >> 1) != t;
+          }
         }
-      }
-      const unsigned long long bm = __ballot(lane < run && bad);
-      const int ncom = bm ? __ffsll((long long)bm) - 1 : run;
-      const bool com = lane < ncom;
-      if (com && sl_res(inf) != kResSkip) {
-        // the final region USED, the other touched pixels released
-        const uint32_t fin = s_fin[si];
-        const int off = (int)(fin & 0xFFFF), len = (int)(fin >> 16);
-        for (int j = off; j < off + len; j++) {
-          const uint32_t e = lb.pt(j);
-          __hip_atomic_store(sd_hi(sd, lsd_sd_index((int)(e & 0xFFFF), (int)(e >> 16), tw)), 0u,
-                             __ATOMIC_RELAXED, ORBPL_LSD_SCOPE);
+        const unsigned long long bm = __ballot(lane < run && bad);
+        const int ncom = bm ? __ffsll((long long)bm) - 1 : run;
+        const bool com = lane < ncom;
+        if (com) {
+          const uint32_t fin = s_fin[si];
+          st_commit(sd, lb, touched, (int)(fin & 0xFFFF), (int)(fin >> 16), tw);
         }
-        st_release(sd, lb, touched, t, tw);
-      }
-      const bool is_cand = com && sl_res(inf) == kResCand;
-      const unsigned long long cm = __ballot(is_cand);
-      if (is_cand) {
-        const int k = nl + __popcll(cm & lt_mask);
-        if (k < kLsdMaxCand) {
-          const double* r = srect + si * 12;
-          double* o = cand_out + (long long)k * 12;
+        const bool is_cand = com && sl_res(inf) == kResCand;
+        const unsigned long long cm = __ballot(is_cand);
+        if (is_cand) {
+          const int k = nl + __popcll(cm & lt_mask);
+          if (k < kLsdMaxCand) {
+            const double* r = srect + si * 12;
+            double* o = cand_out + (long long)k * 12;
 #pragma unroll
-          for (int u = 0; u < 12; u++) o[u] = r[u];
+            for (int u = 0; u < 12; u++) o[u] = r[u];
+          }
         }
-      }
-      nl += __popcll(cm);
-      // the first failing seed: released, fetched again (exact: it is the head)
-      const bool fail = lane == ncom && ncom < run;
-      if (fail) {
-        st_release(sd, lb, touched, t, tw);
-        s_blk[si] = 0;
-        s_info[si] = sl_info(kSlConflict, 0, 0, 0);
-      }
-      // pinned lanes whose seed committed or failed are free again
-      const unsigned long long um = __ballot((com || fail) && pin);
-      for (unsigned long long m = um; m; m &= m - 1) {
-        const int src = __ffsll((long long)m) - 1;
-        const int ln = __shfl(ol, src, 64);
-        if (lane == ln) {
-          pinned = false;
-          my_t = 0;
+        nl += __popcll(cm);
+        // the first failing seed: released, fetched again (exact: the head)
+        if (lane == ncom && ncom < run) {
+          st_release(sd, lb, touched, t, tw);
+          s_blk[si] = 0;
+          s_info[si] = sl_info(kSlConflict, 0, 0, 0);
         }
+        if (com) s_info[si] = sl_info(kSlFree, 0, 0, 0);
+        wg_fence();
+        __builtin_amdgcn_wave_barrier();
+        head_t += (uint32_t)ncom;
       }
-      if (com) s_info[si] = sl_info(kSlFree, 0, 0, 0);
-      wg_fence();
-      __builtin_amdgcn_wave_barrier();
-      head_t += (uint32_t)ncom;
-      // a head longer than a lane buffer, or a conflicted head while every
-      // lane is pinned: the wave-cooperative serial program (exact at the head)
-      const uint32_t hinf = s_info[head_t & (kStW - 1)];
-      const bool no_idle = __ballot(ph == kPhIdle && !pinned) == 0;
-      if (head_t < next_t &&
-          (sl_state(hinf) == kSlOverflow || (sl_state(hinf) == kSlConflict && no_idle))) {
-        const uint32_t spt = s_pt[head_t & (kStW - 1)];
+      // a head longer than its slot: the wave-cooperative serial program
+      const uint32_t hinf = s_info[slot(head_t)];
+      if (head_t < next_t && sl_state(hinf) == kSlOverflow) {
+        const uint32_t spt = s_pt[slot(head_t)];
         double reg_angle;
         const bool covered = used_get(F, (int)(spt & 0xFFFF), (int)(spt >> 16));
         int n = covered ? 0 : region_grow(F, (int)(spt & 0xFFFF), (int)(spt >> 16), reg_angle, prec);
@@ -2701,18 +2751,18 @@ __global__ void __launch_bounds__(64) k_lsd_stream(LsdGeom g, LsdScratch sc) {
             nl++;
           }
         }
-        s_info[head_t & (kStW - 1)] = sl_info(kSlFree, 0, 0, 0);
+        s_info[slot(head_t)] = sl_info(kSlFree, 0, 0, 0);
         head_t++;
         n_coop++;
         wg_fence();
         __builtin_amdgcn_wave_barrier();
       }
     }
-    const bool busy = __ballot(ph != kPhIdle || pinned) != 0;
-    if (!busy && head_t == next_t && scan >= nlist) break;
-    // a loop that cannot finish is reported (err bit 16), never left running:
-    // every seed costs at most a few iterations per fetch and refetch
-    if (n_iter > 64LL * g.n + 100000) {
+    c_commit += clock64() - tc3;
+    const bool busy = __ballot(ph != kPhIdle) != 0;
+    if (!busy && head_t == next_t && scan >= nlist && qh == qt) break;
+    // a loop that cannot finish is reported (err bit 16), never left running
+    if (n_iter > 8LL * g.n + 100000) {
       if (lane == 0) atomicOr(sc.err + f, 16);
       break;
     }
@@ -2722,14 +2772,16 @@ __global__ void __launch_bounds__(64) k_lsd_stream(LsdGeom g, LsdScratch sc) {
     if (nl > kLsdMaxCand) atomicOr(sc.err + f, 8);
   }
   if (sc.prof && lane == 0) {
+    // the round loop's slots: grow, iterations, fetched seeds, total, fit,
+    // commit, bookkeeping (low 40 bits) | cooperative regions << 40, candidates
     long long* pr = sc.prof + f * 8;
-    pr[0] = n_gsteps;
+    pr[0] = c_grow;
     pr[1] = n_iter;
     pr[2] = n_fetch;
     pr[3] = clock64() - t_all;
-    pr[4] = n_batches;
-    pr[5] = n_conf;
-    pr[6] = n_coop << 40;
+    pr[4] = c_fit;
+    pr[5] = c_commit;
+    pr[6] = (c_book & ((1ll << 40) - 1)) | (n_coop << 40);
     pr[7] = nl;
   }
 }
@@ -2859,7 +2911,8 @@ void launch_lsd_grow(const LsdGeom& g, const LsdScratch& sc, int batch, hipStrea
       static const char* sb_env = getenv("ORBPL_SPEC_SMALL");
       static const int small_batch = sb_env ? atoi(sb_env) : kSpecSmallBatch;
       static const char* st_env = getenv("ORBPL_LSD_STREAM");
-      static const int stream_batch = st_env ? atoi(st_env) : kStreamBatch;
+      static const int stream_batch = std::min(st_env ? atoi(st_env) : kStreamBatch,
+                                               kStreamMaxBatch);   // its scratch's frames
       if (batch <= stream_batch)
         hipLaunchKernelGGL(k_lsd_stream, dim3(batch), dim3(64), smem, s, g, sc);
       else if (batch <= small_batch)

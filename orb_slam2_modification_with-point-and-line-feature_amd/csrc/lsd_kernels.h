@@ -138,7 +138,8 @@ struct LsdScratch {
   double* strect;
   uint32_t* stfb;
 };
-constexpr int kStWSlots = 512, kStSlotEntries = 32;   // = kStW, kStSlotCap (lsd_grow.hip)
+constexpr int kStWSlots = 256, kStSlotEntries = 512;   // = kStW, kStSlotCap (lsd_grow.hip)
+constexpr int kStreamMaxBatch = 96;   // batches that may run k_lsd_stream (its scratch is sized so)
 constexpr int kStFbWords = 2176;                      // 3 x 512 region words + 64 x 9 ring
 
 
