@@ -262,7 +262,7 @@ int lsdx_create(int width, int height, int max_batch, int device, lsdx_ctx** out
   LA(s.sort_kt, B * 4);
   LA(s.sort_nge, B * 4);
   {
-X
+    const size_t sf = (size_t)std::min<long long>((long long)B, kStreamMaxBatch);   // k_lsd_stream's frames
     LA(s.stlist, sf * kStWSlots * kStSlotEntries * sizeof(uint4));
     LA(s.strect, sf * kStWSlots * 12 * 8);
     LA(s.stfb, sf * kStFbWords * 4);
