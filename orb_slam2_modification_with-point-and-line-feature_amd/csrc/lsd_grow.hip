@@ -1218,12 +1218,6 @@ __global__ void __launch_bounds__(64) k_lsd_grow(LsdGeom g, LsdScratch sc) {
 #define ORBPL_SPEC_SMALL_BATCH 96
 #endif
 constexpr int kSpecSmallBatch = ORBPL_SPEC_SMALL_BATCH;
-// batches up to this run the round-free seed loop (k_lsd_stream);
-// ORBPL_LSD_STREAM=<max batch> overrides (0: the round loop everywhere)
-#ifndef ORBPL_STREAM_BATCH
-#define ORBPL_STREAM_BATCH 96
-#endif
-constexpr int kStreamBatch = ORBPL_STREAM_BATCH;
 // ORBPL_SPEC_MINW: waves per SIMD the one-wave-per-frame variant's register
 // budget must allow. Round 2 chose 4 (128 VGPRs) although the batches that
 // use it hold 3 frames per SIMD, so that the concurrent ORB extraction /
@@ -2082,710 +2076,6 @@ __global__ void __launch_bounds__(64 * W, MINW) k_lsd_spec(LsdGeom g, LsdScratch
   }
 }
 
-// ---------------------------------------------------------------------------
-// Round-free speculative seed loop (k_lsd_stream, one wave per frame).
-//
-// The round loop above waits, every round, for the slowest of its 64 lanes
-// (grow + fit), while the average lane works a twelfth of that. Here a lane
-// whose seed is finished takes the next one at once:
-//   * seeds are fetched in list order into a window of kStW slots; a seed's
-//     claim tag is its fetch number t (smaller = earlier), slot t & (kStW-1);
-//     stamps: 0 USED (committed), 0xFFFFFFFF free, t << 1 | g (g = 1 first
-//     grow, 0 refine's second grow) a claim;
-//   * growing lanes run kStSteps lockstep grow steps per iteration (the first
-//     and the second grows alike); an aligned, uncommitted neighbour claimed by
-//     an earlier seed aborts the seed (conflict): its claims are released and
-//     it is fetched again once that earlier seed has committed (then skipped
-//     if its seed pixel is USED, as the sequential loop skips it);
-//   * regions reaching min_reg_size queue for the fit's wave-wide pass phases
-//     (region2rect + refine's statistics; the second region's region2rect +
-//     reduce_region_radius), run in batches between grow steps;
-//   * a finished seed's touched list moves to its slot (or, when longer than
-//     kStSlotCap, pins its lane until the commit); seeds commit in fetch
-//     order from the head, up to 64 per pass: every touched pixel must still
-//     carry the seed's own tag (then its result is the sequential one: the
-//     region depends on the USED state of exactly the pixels it added), the
-//     final region becomes USED, the other touched pixels are released, the
-//     rectangle goes out in seed order; a failing head seed is refetched
-//     (exact: every earlier seed is committed);
-//   * a region longer than a lane buffer runs the wave-cooperative serial
-//     program once it is the head.
-// tools/lsd_stream_sim.cpp models this schedule on the CPU over the oracle
-// (identical candidates; ~0.6x the round loop's modelled cycles at batch 1).
-// ---------------------------------------------------------------------------
-constexpr int kStW = kStWSlots;   // window slots (power of two)
-constexpr int kStFitBatch = 16;   // queued fit phases that start a pass batch
-enum { kSlFree = 0, kSlActive = 1, kSlDone = 2, kSlConflict = 3, kSlOverflow = 4, kSlAbort = 5 };
-enum { kResSmall = 0, kResFail = 1, kResCand = 2, kResSkip = 3 };
-enum { kPhIdle = 0, kPhGrow1 = 1, kPhRect1 = 2, kPhGrow2 = 3, kPhRect2 = 4 };
-// s_info: state (3 bits) | result << 3 (2 bits) | lane << 5 (6 bits) | pinned << 11
-__device__ __forceinline__ uint32_t sl_info(int state, int res, int ln, int pin) {
-  return (uint32_t)state | ((uint32_t)res << 3) | ((uint32_t)ln << 5) | ((uint32_t)pin << 11);
-}
-__device__ __forceinline__ int sl_state(uint32_t v) { return (int)(v & 7u); }
-__device__ __forceinline__ int sl_res(uint32_t v) { return (int)((v >> 3) & 3u); }
-__device__ __forceinline__ int sl_lane(uint32_t v) { return (int)((v >> 5) & 63u); }
-__device__ __forceinline__ bool sl_pin(uint32_t v) { return ((v >> 11) & 1u) != 0; }
-
-// the resumable region grow of one lane (lane_grow's step, same operations)
-struct GrowSt {
-  uint4 cur;
-  int i, n;
-  float sumdx, sumdy;
-  double reg_angle, prec;
-  uint32_t myval;
-  bool lazy;   // the seed pixel's stamp is tested by the first step (gs_start_q)
-};
-constexpr int kSpecSkip = -3;   // gs_step: the seed pixel is USED (the seed is skipped)
-
-__device__ __forceinline__ int gs_start(GrowSt& s, uint64_t* sd, LaneBuf buf, int cap, int sx, int sy,
-                                        double prec, uint32_t myval, int tw, uint32_t& blocker) {
-  const uint32_t mytag = myval >> 1;
-  if (cap < 1) return kSpecOverflow;
-  const int si = lsd_sd_index(sx, sy, tw);
-  const uint64_t v0 = ld_sd(sd + si);
-  const uint32_t st = (uint32_t)(v0 >> 32);
-  if ((st >> 1) < mytag) {   // USED (0) or an earlier seed's claim
-    blocker = st >> 1;
-    return kSpecConflict;
-  }
-  atomicMin(reinterpret_cast<unsigned long long*>(sd + si),
-            ((unsigned long long)myval << 32) | (uint32_t)v0);
-  s.cur = make_uint4((uint32_t)sx | ((uint32_t)sy << 16), (uint32_t)v0, 0u, 0u);
-  buf[0] = s.cur;
-  s.reg_angle = deg2ang(entry_deg(s.cur));
-  double s0, c0;
-  lsdm::sincos_(s.reg_angle, &s0, &c0);
-  s.sumdx = (float)c0;
-  s.sumdy = (float)s0;
-  s.prec = prec;
-  s.myval = myval;
-  s.i = 0;
-  s.n = 1;
-  s.lazy = false;
-  return 0;
-}
-
-// gs_start for a queued seed whose degrees the scan loaded: the claim is sent
-// without waiting for the stamp; the first step reads the seed pixel's stamp
-// with its neighbourhood (USED: kSpecSkip; an earlier seed's: conflict)
-__device__ __forceinline__ void gs_start_q(GrowSt& s, uint64_t* sd, LaneBuf buf, uint32_t pt,
-                                           uint32_t degbits, double prec, uint32_t myval, int tw) {
-  const int sx = (int)(pt & 0xFFFF), sy = (int)(pt >> 16);
-  atomicMin(reinterpret_cast<unsigned long long*>(sd + lsd_sd_index(sx, sy, tw)),
-            ((unsigned long long)myval << 32) | degbits);
-  s.cur = make_uint4(pt, degbits, 0u, 0u);
-  buf[0] = s.cur;
-  s.reg_angle = deg2ang(entry_deg(s.cur));
-  double s0, c0;
-  lsdm::sincos_(s.reg_angle, &s0, &c0);
-  s.sumdx = (float)c0;
-  s.sumdy = (float)s0;
-  s.prec = prec;
-  s.myval = myval;
-  s.i = 0;
-  s.n = 1;
-  s.lazy = true;
-}
-
-// one point expansion; 1 = the region is complete, 0 = continue, or
-// kSpecConflict (blocker set) / kSpecOverflow
-__device__ __forceinline__ int gs_step(GrowSt& s, const Frame& F, uint64_t* sd, LaneBuf buf, int cap,
-                                       uint32_t& blocker) {
-  const uint32_t mytag = s.myval >> 1, myval = s.myval;
-  const int sw = F.sw, sh = F.sh, tw = F.tw;
-  const double k3pi2 = (3 * kPi) / 2, k2pi = 2 * kPi;
-  const int x = pt_x(s.cur), y = pt_y(s.cur);
-  const int n_start = s.n;
-  const uint4 pref = buf[min(s.i + 1, n_start - 1)];
-  uint32_t rterm[3], cterm[3];
-  bool rin[3], cin[3];
-#pragma unroll
-  for (int d = 0; d < 3; d++) {
-    const int yy = y + d - 1, xx = x + d - 1;
-    rin[d] = yy >= 0 && yy < sh;
-    cin[d] = xx >= 0 && xx < sw;
-    const int cy = min(max(yy, 0), sh - 1), cx = min(max(xx, 0), sw - 1);
-    rterm[d] = ((((uint32_t)(cy >> 2) * (uint32_t)tw) << 5) | ((uint32_t)(cy & 3) << 3)) << 3;
-    cterm[d] = (((uint32_t)(cx >> 2) << 5) | ((uint32_t)(cx & 3) << 1)) << 3;
-  }
-  uint4 w[9];
-  const bool centre = s.lazy && s.i == 0;
-#pragma unroll
-  for (int k = 0; k < 9; k++) {
-    if (k == 4 && !centre) continue;
-    w[k] = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(sd) +
-                                           (rterm[k / 3] + cterm[k % 3]));
-  }
-  if (centre) {
-    const uint32_t st = w[4].y;
-    if (st == 0u) return kSpecSkip;
-    if ((st >> 1) < mytag) {
-      blocker = st >> 1;
-      return kSpecConflict;
-    }
-  }
-  unsigned ok = 0;
-#pragma unroll
-  for (int k = 0; k < 9; k++) {
-    if (k == 4) continue;
-    const unsigned f = (unsigned)(rin[k / 3] & cin[k % 3]) & (unsigned)(w[k].y != 0u) &
-                       (unsigned)(w[k].y != myval) & (unsigned)(__uint_as_float(w[k].x) >= 0.f);
-    ok |= f << k;
-  }
-  uint4 first_add = s.cur;
-  int n = s.n;
-#pragma unroll
-  for (int k = 0; k < 9; k++) {
-    if (k == 4) continue;
-    double nt = fabs(s.reg_angle - deg2ang(__uint_as_float(w[k].x)));
-    nt = nt > k3pi2 ? fabs(nt - k2pi) : nt;
-    if (((ok >> k) & 1u) && nt <= s.prec) {
-      if ((w[k].y >> 1) < mytag) {   // an earlier seed's pixel
-        blocker = w[k].y >> 1;
-        s.n = n;
-        return kSpecConflict;
-      }
-      if (n >= cap) {   // before the claim: every claim is in the list (released on abort)
-        s.n = n;
-        return kSpecOverflow;
-      }
-      atomicMin(reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(sd) +
-                                                      (rterm[k / 3] + cterm[k % 3])),
-                ((unsigned long long)myval << 32) | w[k].x);
-      const int xx = x + (k % 3) - 1, yy = y + (k / 3) - 1;
-      const uint4 e = make_uint4((uint32_t)xx | ((uint32_t)yy << 16), w[k].x, 0u, 0u);
-      if (n == n_start) first_add = e;
-      buf[n++] = e;
-      s.sumdx += __uint_as_float(w[k].z);   // add_angle(d) terms
-      s.sumdy += __uint_as_float(w[k].w);
-      s.reg_angle = (double)fast_atan2_deg_1div(s.sumdy, s.sumdx) * kDegToRad;
-    }
-  }
-  s.n = n;
-  s.cur = (s.i + 1 < n_start) ? pref : first_add;
-  s.i++;
-  return s.i >= s.n ? 1 : 0;
-}
-
-// release the stamps a seed holds among list entries [0, n) (its own tag,
-// either grow): they become free again. Runs while no lane grows (the wave
-// is in one phase), so a load and a conditional store cannot interleave with
-// another seed's claim; loads 8 entries / stamps at a time.
-__device__ __forceinline__ void st_release(uint64_t* sd, LaneBuf buf, int n, uint32_t tag, int tw) {
-  for (int j0 = 0; j0 < n; j0 += 8) {
-    uint32_t ev[8], sv[8];
-    int id[8];
-#pragma unroll
-    for (int u = 0; u < 8; u++) ev[u] = buf.pt(min(j0 + u, n - 1));
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-      id[u] = lsd_sd_index((int)(ev[u] & 0xFFFF), (int)(ev[u] >> 16), tw);
-      sv[u] = ld_stamp(sd, id[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < 8; u++)
-      if (j0 + u < n && (sv[u] >> 1) == tag && sv[u] != 0u)
-        __hip_atomic_store(sd_hi(sd, id[u]), 0xFFFFFFFFu, __ATOMIC_RELAXED, ORBPL_LSD_SCOPE);
-  }
-}
-
-// the commit of a checked seed: every touched pixel (all carry the seed's own
-// tag) released, then the final region [off, off + len) USED; both stores go
-// to the same lane's addresses in order, so a pixel of both ends USED
-__device__ __forceinline__ void st_commit(uint64_t* sd, LaneBuf lb, int touched, int off, int len,
-                                          int tw) {
-  for (int j0 = 0; j0 < touched; j0 += 8) {
-    uint32_t ev[8];
-#pragma unroll
-    for (int u = 0; u < 8; u++) ev[u] = lb.pt(min(j0 + u, touched - 1));
-#pragma unroll
-    for (int u = 0; u < 8; u++)
-      if (j0 + u < touched)
-        __hip_atomic_store(sd_hi(sd, lsd_sd_index((int)(ev[u] & 0xFFFF), (int)(ev[u] >> 16), tw)),
-                           0xFFFFFFFFu, __ATOMIC_RELAXED, ORBPL_LSD_SCOPE);
-  }
-  for (int j0 = off; j0 < off + len; j0 += 8) {
-    uint32_t ev[8];
-#pragma unroll
-    for (int u = 0; u < 8; u++) ev[u] = lb.pt(min(j0 + u, off + len - 1));
-#pragma unroll
-    for (int u = 0; u < 8; u++)
-      if (j0 + u < off + len)
-        __hip_atomic_store(sd_hi(sd, lsd_sd_index((int)(ev[u] & 0xFFFF), (int)(ev[u] >> 16), tw)),
-                           0u, __ATOMIC_RELAXED, ORBPL_LSD_SCOPE);
-  }
-}
-
-// the fit's first pass phase for every act lane: region2rect of the first
-// region (weights filled from q) and refine's density test; returns whether
-// refine's second grow is needed (then tau), else the result is final (cand)
-__device__ __forceinline__ bool st_rect1(CoopScratch& S, int lane, bool act, uint4* bp, int n,
-                                         const Frame& F, double reg_angle, double prec, double p,
-                                         Rect& rec, double& tau) {
-  double cx, cy, cs;
-  group_centroid(S, lane, act, bp, n, F.q, F.sw, cx, cy, cs);
-  wg_fence();
-  __builtin_amdgcn_wave_barrier();
-  group_rect_tail(S, lane, act, bp, n, cx, cy, cs, reg_angle, prec, p, rec);
-  bool refine = false;
-  if (act) {
-    const double density = double(n) / (dist(rec.x1, rec.y1, rec.x2, rec.y2) * rec.width);
-    refine = density < 0.7;
-  }
-  tau = group_tau(S, lane, refine, bp, n, rec);
-  return refine;
-}
-
-// the fit's second pass phase: region2rect of the second region gp[0, n1)
-// and reduce_region_radius around (x0, y0); result kResCand / kResFail, the
-// final region gp[0, len)
-__device__ __forceinline__ void st_rect2(CoopScratch& S, int lane, bool act, uint4* gp, int n1,
-                                         int x0, int y0, const Frame& F, double ra2, double prec,
-                                         double p, Rect& rec, int& res, int& len) {
-  bool live = act && n1 >= 2;
-  if (act) {
-    len = n1;
-    res = n1 >= 2 ? kResCand : kResFail;
-  }
-  double cx, cy, cs;
-  group_centroid(S, lane, live, gp, n1, F.q, F.sw, cx, cy, cs);
-  wg_fence();
-  __builtin_amdgcn_wave_barrier();
-  group_rect_tail(S, lane, live, gp, n1, cx, cy, cs, ra2, prec, p, rec);
-  bool red = false;
-  double radSq = 0;
-  if (live) {
-    const double density = double(n1) / (dist(rec.x1, rec.y1, rec.x2, rec.y2) * rec.width);
-    if (density < 0.7) {
-      red = true;
-      const double xc = double(x0), yc = double(y0);
-      const double radSq1 = distSq(xc, yc, rec.x1, rec.y1);
-      const double radSq2 = distSq(xc, yc, rec.x2, rec.y2);
-      radSq = radSq1 > radSq2 ? radSq1 : radSq2;
-    }
-  }
-  while (__ballot(red)) {
-    if (red) radSq *= 0.75 * 0.75;
-    int nn = n1;
-    for (unsigned long long m = __ballot(red); m; m &= m - 1) {
-      const int f = __ffsll((long long)m) - 1;
-      const int nf = coop_rl(n1, f), xf = coop_rl(x0, f), yf = coop_rl(y0, f);
-      const double rf = coop_rl(radSq, f);
-      const LaneBuf g1{coop_rl(gp, f)};
-      int c = 0;
-      for (int i0 = 0; i0 < nf; i0 += 64) {
-        const int i = i0 + lane;
-        c += __popcll(__ballot(i < nf && !lane_far(g1.pt(i), xf, yf, rf)));
-      }
-      if (c < nf) group_merge(S, lane, g1, nf, c, xf, yf, rf);
-      if (lane == f) nn = c;
-    }
-    wg_fence();
-    __builtin_amdgcn_wave_barrier();
-    const bool merged = red && nn < n1;
-    group_centroid(S, lane, merged, gp, nn, nullptr, 0, cx, cy, cs);
-    bool tail = false;
-    if (red) {
-      const int n_prev = n1;
-      n1 = nn;
-      len = n1;
-      if (n1 < 2) {
-        res = kResFail;
-        red = false;
-      } else if (n1 != n_prev) {
-        tail = true;
-      }
-    }
-    group_rect_tail(S, lane, tail, gp, n1, cx, cy, cs, ra2, prec, p, rec);
-    if (tail) {
-      const double density = double(n1) / (dist(rec.x1, rec.y1, rec.x2, rec.y2) * rec.width);
-      if (density >= 0.7) red = false;
-    }
-  }
-}
-
-constexpr int kStSlotCap = kStSlotEntries;   // a seed's list (both grows) in its slot
-constexpr int kStQ = 256;                    // pre-scanned seeds queued in LDS (power of two)
-constexpr int kStInner = 8;                  // grow steps between the wave's bookkeeping phases
-
-// A seed's list lives in its slot (slist[slot][kStSlotCap]) from the first
-// grow to the commit, so a lane whose seed is finished takes the next one
-// without moving anything: inside kStInner lockstep grow steps a lane that
-// completes a small region (or aborts) takes the next queued seed at once;
-// between those runs the wave releases aborted seeds, refills the seed
-// queue, refetches conflicts, runs the queued fit phases and commits.
-__global__ void __launch_bounds__(64) k_lsd_stream(LsdGeom g, LsdScratch sc) {
-  __shared__ uint32_t s_pt[kStW], s_info[kStW], s_blk[kStW], s_tl[kStW], s_fin[kStW];
-  __shared__ uint2 s_q[kStQ];   // (x | y << 16, degree bits)
-  __shared__ CoopScratch s_coop;
-  extern __shared__ uint32_t grow_smem[];
-  const int f = blockIdx.x, lane = threadIdx.x;
-  const int sw = g.sw, sh = g.sh;
-  Frame F;
-  F.sw = sw;
-  F.sh = sh;
-  F.deg = sc.deg + (long long)f * lsd_deg_words(sw, sh);
-  F.dtw = lsd_deg_tw(sw);
-  F.q = sc.q + (long long)f * sw * sh;
-  F.used = nullptr;
-  uint32_t* fbk = sc.stfb + (long long)f * kStFbWords;   // the cooperative program's scratch
-  F.reg_l = fbk;
-  F.regq_l = reinterpret_cast<int*>(F.reg_l + kRegLds);
-  F.regd_l = reinterpret_cast<float*>(F.regq_l + kRegLds);
-  F.ring = F.regd_l + kRegLds;
-  F.reg_g = sc.reg + (long long)f * 3 * sw * sh;
-  F.rows = reinterpret_cast<int4*>(grow_smem);
-  F.rect0 = reinterpret_cast<Rect*>(F.rows);
-  F.rect1 = F.rect0 + 1;
-  F.row_cap = 0;
-  F.log_nt = g.log_nt;
-  F.lane = lane;
-  F.pf_cyc = 0;
-  F.pf_cnt = 0;
-  uint64_t* sd = sc.sd + (long long)f * lsd_sd_frame_words(sw, sh);
-  F.usd = sd;
-  F.cs = sd + lsd_cs_offset(sw, sh);
-  F.tw = lsd_sd_tw(sw);
-  const int tw = F.tw;
-  uint4* const slist = sc.stlist + (long long)f * kStW * kStSlotCap;
-  double* const srect = sc.strect + (long long)f * kStW * 12;
-  const uint32_t* A = sc.A + (long long)f * g.n;
-  const int nlist = sc.sort_nge[f];
-  double* cand_out = sc.cand + (long long)f * kLsdMaxCand * 12;
-  const int w1 = sw - 1;
-  const double prec = g.prec, p = g.p;
-  const unsigned long long lt_mask = (1ull << lane) - 1ull;
-  for (int i = lane; i < kStW; i += 64) s_info[i] = sl_info(kSlFree, 0, 0, 0);
-  __builtin_amdgcn_wave_barrier();
-  // lane state
-  int ph = kPhIdle;
-  uint32_t my_t = 0;   // the slot tag this lane works on (0: none)
-  GrowSt gs;
-  int n1 = 0, x0 = 0, y0 = 0;
-  double ra1 = 0;
-  Rect rec;
-  // wave-uniform state
-  uint32_t head_t = 1, next_t = 1;
-  int scan = 0, nl = 0, qh = 0, qt = 0;
-  long long n_iter = 0, n_coop = 0, n_fetch = 0;
-  long long c_book = 0, c_grow = 0, c_fit = 0, c_commit = 0;
-  const long long t_all = clock64();
-  auto slot = [](uint32_t t) { return (int)(t & (kStW - 1)); };
-  auto lbuf_of = [&](uint32_t t) { return LaneBuf{slist + slot(t) * kStSlotCap}; };
-  // a lane's seed is final: result, final range, touched count (the list is
-  // already in the slot)
-  auto finish = [&](int res, int off, int len, int touched) {
-    const int si = slot(my_t);
-    if (res == kResCand) {
-      double* o = srect + si * 12;
-      o[0] = rec.x1; o[1] = rec.y1; o[2] = rec.x2; o[3] = rec.y2;
-      o[4] = rec.width; o[5] = rec.x; o[6] = rec.y; o[7] = rec.theta;
-      o[8] = rec.dx; o[9] = rec.dy; o[10] = rec.prec; o[11] = rec.p;
-    }
-    s_tl[si] = (uint32_t)touched;
-    s_fin[si] = (uint32_t)off | ((uint32_t)len << 16);
-    s_info[si] = sl_info(kSlDone, res, lane, 0);
-    ph = kPhIdle;
-    my_t = 0;
-  };
-  // a lane's seed aborts: its claims are released in the next bookkeeping
-  // phase (kSlAbort), then it waits for its blocker (conflict) or the head
-  // (overflow)
-  auto abort_seed = [&](int st, uint32_t blocker, int touched) {
-    const int si = slot(my_t);
-    s_tl[si] = (uint32_t)touched;
-    s_blk[si] = st == kSpecOverflow ? 0xFFFFFFFFu : blocker;
-    s_info[si] = sl_info(kSlAbort, 0, lane, 0);
-    ph = kPhIdle;
-    my_t = 0;
-  };
-  // idle lanes take queued seeds in list order (new slots), wave-wide
-  auto take_new = [&]() {
-    const bool idle = ph == kPhIdle;
-    const unsigned long long im = __ballot(idle);
-    const int take = min(min(__popcll(im), qt - qh), kStW - (int)(next_t - head_t));
-    if (take <= 0) return;
-    const int r = __popcll(im & lt_mask);
-    if (idle && r < take) {
-      my_t = next_t + (uint32_t)r;
-      const int si = slot(my_t);
-      const uint2 q = s_q[(qh + r) & (kStQ - 1)];
-      s_pt[si] = q.x;
-      s_info[si] = sl_info(kSlActive, 0, lane, 0);
-      gs_start_q(gs, sd, lbuf_of(my_t), q.x, q.y, prec, (my_t << 1) | 1u, tw);
-      ph = kPhGrow1;
-    }
-    next_t += (uint32_t)take;
-    qh += take;
-    n_fetch += take;
-  };
-  while (true) {
-    n_iter++;
-    const long long tc0 = clock64();
-    // ---- kStInner lockstep grow steps, finished lanes refilled at once ----
-    for (int k = 0; k < kStInner; k++) {
-      const bool grow = ph == kPhGrow1 || ph == kPhGrow2;
-      if (!__ballot(grow)) break;
-      if (grow) {
-        const LaneBuf lb = lbuf_of(my_t);
-        const LaneBuf gb = ph == kPhGrow1 ? lb : lb + n1;
-        const int cap = ph == kPhGrow1 ? kStSlotCap : kStSlotCap - n1;
-        uint32_t blocker = 0;
-        const int r = gs_step(gs, F, sd, gb, cap, blocker);
-        if (r == kSpecSkip) {
-          finish(kResSkip, 0, 0, 0);   // USED since the scan: nothing of it was claimed
-        } else if (r < 0) {
-          abort_seed(r, blocker, ph == kPhGrow1 ? gs.n : n1 + gs.n);
-        } else if (r > 0) {
-          if (ph == kPhGrow1) {
-            n1 = gs.n;
-            ra1 = gs.reg_angle;
-            if (n1 < g.min_reg_size) finish(kResSmall, 0, n1, n1);
-            else ph = kPhRect1;
-          } else {
-            ph = kPhRect2;
-          }
-        }
-      }
-      __threadfence_block();
-      __builtin_amdgcn_wave_barrier();
-      take_new();
-    }
-    wg_fence();
-    __builtin_amdgcn_wave_barrier();
-    const long long tc1 = clock64();
-    c_grow += tc1 - tc0;
-    // ---- bookkeeping: release aborted seeds, refill the queue, refetch ----
-    {
-      for (int i0 = 0; i0 < kStW; i0 += 64) {
-        const uint32_t t = head_t + (uint32_t)(i0 + lane);
-        if (t < next_t) {
-          const int si = slot(t);
-          const uint32_t inf = s_info[si];
-          if (sl_state(inf) == kSlAbort) {
-            st_release(sd, lbuf_of(t), (int)s_tl[si], t, tw);
-            const bool ovf = s_blk[si] == 0xFFFFFFFFu;
-            s_blk[si] = ovf ? 0u : s_blk[si];
-            s_info[si] = sl_info(ovf ? kSlOverflow : kSlConflict, 0, 0, 0);
-          }
-        }
-      }
-      // the seed queue: defined, not USED list entries, 64 per load
-      while (qt - qh <= kStQ - 64 && scan < nlist) {
-        const int i = scan + lane;
-        bool c = false;
-        uint2 q = make_uint2(0u, 0u);
-        if (i < nlist) {
-          const int idx = (int)(A[i] & 0x3FFFFFu);
-          const int py = idx / w1, px = idx - py * w1;
-          const uint64_t v = ld_sd(sd + lsd_sd_index(px, py, tw));
-          c = __uint_as_float((uint32_t)v) >= 0.f && (uint32_t)(v >> 32) != 0u;
-          q = make_uint2((uint32_t)px | ((uint32_t)py << 16), (uint32_t)v);
-        }
-        const unsigned long long m = __ballot(c);
-        if (c) s_q[(qt + __popcll(m & lt_mask)) & (kStQ - 1)] = q;
-        qt += __popcll(m);
-        scan += 64;
-        if (qt - qh >= 128) break;   // enough for this run; loads stay off the chain
-      }
-      if (scan > nlist) scan = nlist;
-      // conflicted seeds among the window's first 64 whose blocker committed:
-      // skipped if covered, else taken by an idle lane (regrown)
-      const uint32_t t = head_t + (uint32_t)lane;
-      bool ref = false;
-      if (t < next_t) {
-        const int si = slot(t);
-        if (sl_state(s_info[si]) == kSlConflict && s_blk[si] < head_t) {
-          const uint32_t pt = s_pt[si];
-          if (ld_stamp(sd, lsd_sd_index((int)(pt & 0xFFFF), (int)(pt >> 16), tw)) == 0u) {
-            s_tl[si] = 0;
-            s_fin[si] = 0;
-            s_info[si] = sl_info(kSlDone, kResSkip, 0, 0);
-          } else {
-            ref = true;
-          }
-        }
-      }
-      __threadfence_block();
-      __builtin_amdgcn_wave_barrier();
-      const unsigned long long rm = __ballot(ref);
-      const bool idle = ph == kPhIdle;
-      const unsigned long long im = __ballot(idle);
-      const int nref = min(__popcll(rm), __popcll(im));
-      // the r-th refetch (window order) goes to the r-th idle lane
-      int* s_ref = reinterpret_cast<int*>(&s_coop);   // scratch: the pass batch is not running
-      if (ref) {
-        const int r = __popcll(rm & lt_mask);
-        if (r < nref) s_ref[r] = (int)t;
-      }
-      __threadfence_block();
-      __builtin_amdgcn_wave_barrier();
-      const int ri = __popcll(im & lt_mask);
-      if (idle && ri < nref) {
-        my_t = (uint32_t)s_ref[ri];
-        const int si = slot(my_t);
-        s_info[si] = sl_info(kSlActive, 0, lane, 0);
-        const uint32_t pt = s_pt[si];
-        uint32_t blocker = 0;
-        const int st = gs_start(gs, sd, lbuf_of(my_t), kStSlotCap, (int)(pt & 0xFFFF),
-                                (int)(pt >> 16), prec, (my_t << 1) | 1u, tw, blocker);
-        ph = kPhGrow1;
-        if (st != 0) abort_seed(st, blocker, 0);
-      }
-      __threadfence_block();
-      __builtin_amdgcn_wave_barrier();
-      take_new();
-      __threadfence_block();
-      __builtin_amdgcn_wave_barrier();
-    }
-    const long long tc2 = clock64();
-    c_book += tc2 - tc1;
-    // ---- the fit's pass phases in a batch ----
-    {
-      const unsigned long long wm = __ballot(ph == kPhRect1 || ph == kPhRect2);
-      const bool any_grow = __ballot(ph == kPhGrow1 || ph == kPhGrow2) != 0;
-      const uint32_t hinf = s_info[slot(head_t)];
-      const bool head_waits = head_t < next_t && sl_state(hinf) == kSlActive &&
-                              (__shfl(ph, sl_lane(hinf), 64) == kPhRect1 ||
-                               __shfl(ph, sl_lane(hinf), 64) == kPhRect2);
-      if (wm && (__popcll(wm) >= kStFitBatch || head_waits || !any_grow)) {
-        uint4* const my_bp = slist + slot(my_t) * kStSlotCap;
-        const bool r1 = ph == kPhRect1;
-        double tau = 0;
-        if (r1) {
-          const uint4 e0 = my_bp[0];
-          x0 = pt_x(e0);
-          y0 = pt_y(e0);
-        }
-        const bool again = st_rect1(s_coop, lane, r1, my_bp, n1, F, ra1, prec, p, rec, tau);
-        if (r1 && !again) finish(kResCand, 0, n1, n1);
-        if (r1 && again) {
-          uint32_t blocker = 0;
-          const int st = gs_start(gs, sd, LaneBuf{my_bp} + n1, kStSlotCap - n1, x0, y0, tau,
-                                  my_t << 1, tw, blocker);
-          ph = kPhGrow2;
-          if (st != 0) abort_seed(st, blocker, n1);
-        }
-        const bool r2 = ph == kPhRect2;
-        int res = kResFail, len = 0;
-        const int n2 = r2 ? gs.n : 0;
-        st_rect2(s_coop, lane, r2, my_bp + n1, n2, x0, y0, F, gs.reg_angle, prec, p, rec, res, len);
-        if (r2) finish(res, n1, len, n1 + n2);
-        wg_fence();
-        __builtin_amdgcn_wave_barrier();
-      }
-    }
-    const long long tc3 = clock64();
-    c_fit += tc3 - tc2;
-    // ---- commit from the head: up to 64 consecutive finished seeds ----
-    {
-      const uint32_t t = head_t + (uint32_t)lane;
-      const int si = slot(t);
-      const uint32_t inf = t < next_t ? s_info[si] : 0u;
-      const bool done = t < next_t && sl_state(inf) == kSlDone;
-      const unsigned long long nd = __ballot(!done);
-      const int run = nd ? __ffsll((long long)nd) - 1 : 64;
-      if (run > 0) {
-        bool bad = false;
-        const int touched = (int)s_tl[si];
-        const LaneBuf lb = lbuf_of(t);
-        if (lane < run) {
-          for (int j0 = 0; j0 < touched && !bad; j0 += 8) {
-            uint32_t ev[8], sv[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) ev[u] = lb.pt(min(j0 + u, touched - 1));
-#pragma unroll
-            for (int u = 0; u < 8; u++)
-              sv[u] = ld_stamp(sd, lsd_sd_index((int)(ev[u] & 0xFFFF), (int)(ev[u] >> 16), tw));
-#pragma unroll
-            for (int u = 0; u < 8; u++) bad |= sv[u] == 0u || (sv[u] >> 1) != t;
-          }
-        }
-        const unsigned long long bm = __ballot(lane < run && bad);
-        const int ncom = bm ? __ffsll((long long)bm) - 1 : run;
-        const bool com = lane < ncom;
-        if (com) {
-          const uint32_t fin = s_fin[si];
-          st_commit(sd, lb, touched, (int)(fin & 0xFFFF), (int)(fin >> 16), tw);
-        }
-        const bool is_cand = com && sl_res(inf) == kResCand;
-        const unsigned long long cm = __ballot(is_cand);
-        if (is_cand) {
-          const int k = nl + __popcll(cm & lt_mask);
-          if (k < kLsdMaxCand) {
-            const double* r = srect + si * 12;
-            double* o = cand_out + (long long)k * 12;
-#pragma unroll
-            for (int u = 0; u < 12; u++) o[u] = r[u];
-          }
-        }
-        nl += __popcll(cm);
-        // the first failing seed: released, fetched again (exact: the head)
-        if (lane == ncom && ncom < run) {
-          st_release(sd, lb, touched, t, tw);
-          s_blk[si] = 0;
-          s_info[si] = sl_info(kSlConflict, 0, 0, 0);
-        }
-        if (com) s_info[si] = sl_info(kSlFree, 0, 0, 0);
-        wg_fence();
-        __builtin_amdgcn_wave_barrier();
-        head_t += (uint32_t)ncom;
-      }
-      // a head longer than its slot: the wave-cooperative serial program
-      const uint32_t hinf = s_info[slot(head_t)];
-      if (head_t < next_t && sl_state(hinf) == kSlOverflow) {
-        const uint32_t spt = s_pt[slot(head_t)];
-        double reg_angle;
-        const bool covered = used_get(F, (int)(spt & 0xFFFF), (int)(spt >> 16));
-        int n = covered ? 0 : region_grow(F, (int)(spt & 0xFFFF), (int)(spt >> 16), reg_angle, prec);
-        if (n >= g.min_reg_size) {
-          Rect& rc = *F.rect0;
-          fill_q(F, n);
-          region2rect(F, n, reg_angle, prec, p, rc);
-          if (refine(F, n, reg_angle, prec, p, rc, 0.7)) {
-            if (nl < kLsdMaxCand) {
-              const double* rv = reinterpret_cast<const double*>(F.rect0);
-              if (lane < 12) cand_out[(long long)nl * 12 + lane] = rv[lane];
-            }
-            nl++;
-          }
-        }
-        s_info[slot(head_t)] = sl_info(kSlFree, 0, 0, 0);
-        head_t++;
-        n_coop++;
-        wg_fence();
-        __builtin_amdgcn_wave_barrier();
-      }
-    }
-    c_commit += clock64() - tc3;
-    const bool busy = __ballot(ph != kPhIdle) != 0;
-    if (!busy && head_t == next_t && scan >= nlist && qh == qt) break;
-    // a loop that cannot finish is reported (err bit 16), never left running
-    if (n_iter > 8LL * g.n + 100000) {
-      if (lane == 0) atomicOr(sc.err + f, 16);
-      break;
-    }
-  }
-  if (lane == 0) {
-    sc.ncand[f] = min(nl, kLsdMaxCand);
-    if (nl > kLsdMaxCand) atomicOr(sc.err + f, 8);
-  }
-  if (sc.prof && lane == 0) {
-    // the round loop's slots: grow, iterations, fetched seeds, total, fit,
-    // commit, bookkeeping (low 40 bits) | cooperative regions << 40, candidates
-    long long* pr = sc.prof + f * 8;
-    pr[0] = c_grow;
-    pr[1] = n_iter;
-    pr[2] = n_fetch;
-    pr[3] = clock64() - t_all;
-    pr[4] = c_fit;
-    pr[5] = c_commit;
-    pr[6] = (c_book & ((1ll << 40) - 1)) | (n_coop << 40);
-    pr[7] = nl;
-  }
-}
-
 // NFA validation of every refined rectangle (rect_improve), one lane per
 // rectangle; the accepted segments are compacted in seed order by
 // k_lsd_compact.
@@ -2910,12 +2200,7 @@ void launch_lsd_grow(const LsdGeom& g, const LsdScratch& sc, int batch, hipStrea
       // per SIMD (no spills on the seed chain) instead of the co-residence bound
       static const char* sb_env = getenv("ORBPL_SPEC_SMALL");
       static const int small_batch = sb_env ? atoi(sb_env) : kSpecSmallBatch;
-      static const char* st_env = getenv("ORBPL_LSD_STREAM");
-      static const int stream_batch = std::min(st_env ? atoi(st_env) : kStreamBatch,
-                                               kStreamMaxBatch);   // its scratch's frames
-      if (batch <= stream_batch)
-        hipLaunchKernelGGL(k_lsd_stream, dim3(batch), dim3(64), smem, s, g, sc);
-      else if (batch <= small_batch)
+      if (batch <= small_batch)
         hipLaunchKernelGGL((k_lsd_spec<1, 1>), dim3(batch), dim3(64), smem, s, g, sc);
       else
         hipLaunchKernelGGL(k_lsd_spec<1>, dim3(batch), dim3(64), smem, s, g, sc);

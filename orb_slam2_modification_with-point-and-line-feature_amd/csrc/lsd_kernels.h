@@ -131,17 +131,7 @@ struct LsdScratch {
   int lgam_n;          // NFA's three log_gamma terms at integer arguments
   int* sort_nge;       // 1 per frame: elements with key >= kt (the list's
                        // exactly sorted prefix; every later pixel is NOTDEF)
-  // k_lsd_stream (every frame of the context, so any batch may run it): per frame kStW slots of
-  // kStSlotCap list entries, kStW rectangles (12 doubles), the cooperative
-  // program's scratch (kStFbWords)
-  uint4* stlist;
-  double* strect;
-  uint32_t* stfb;
 };
-constexpr int kStWSlots = 256, kStSlotEntries = 512;   // = kStW, kStSlotCap (lsd_grow.hip)
-constexpr int kStreamMaxBatch = 96;   // batches that may run k_lsd_stream (its scratch is sized so)
-constexpr int kStFbWords = 2176;                      // 3 x 512 region words + 64 x 9 ring
-
 
 // Outputs of LineExtractor::ExtractLineSegment per frame.
 struct LineOut {

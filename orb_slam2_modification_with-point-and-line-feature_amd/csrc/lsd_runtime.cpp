@@ -261,12 +261,6 @@ int lsdx_create(int width, int height, int max_batch, int device, lsdx_ctx** out
   LA(s.sort_nlocal, B * 4);
   LA(s.sort_kt, B * 4);
   LA(s.sort_nge, B * 4);
-  {
-    const size_t sf = (size_t)std::min<long long>((long long)B, kStreamMaxBatch);   // k_lsd_stream's frames
-    LA(s.stlist, sf * kStWSlots * kStSlotEntries * sizeof(uint4));
-    LA(s.strect, sf * kStWSlots * 12 * 8);
-    LA(s.stfb, sf * kStFbWords * 4);
-  }
   s.lgam_n = g.sw * g.sh + 1;   // a rectangle holds at most every pixel
   LA(s.lgam, (size_t)s.lgam_n * 8);
   LA(c->d_tabs, (size_t)(2 * g.sw + 2 * g.sh) * 4);

@@ -24,6 +24,15 @@
 // its slowest lane) under the same cost constants.
 //
 // build + run: python tools/lsd_stream_sim.py [frames] [window] [fit_batch]
+//
+// Measured on MI355X in round 5 (k_lsd_stream, git history 5591b98..3bef507;
+// bit-exact: the 26 LSD parity tests passed with it at every step): at batch 1
+// 104-139M shader cycles per frame against the round loop's 99-105M on the
+// same boxes (profiles/r05/lsd_stream_ab.txt). Each lockstep iteration's
+// bookkeeping (seed queue, releases, refetches, the in-order commit's two
+// dependent loads per seed) and the lanes parked behind fit batches outweigh
+// the removed round barrier; a larger window (1024 slots) fetched 31.8k
+// instead of 27k seeds and ran slower still. Not kept.
 #include "../oracle/lsd_oracle.cpp"
 
 #include <cstdio>
