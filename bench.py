@@ -1063,19 +1063,39 @@ def _cpu_list(text):
     return out
 
 
-def pin_one_ccd():
+def _parent_cpus():
+    """The CPUs the parent process's threads last ran on (/proc stat field
+    39): the bench's own threads, HIP runtime threads included."""
+    out = set()
+    try:
+        ppid = os.getppid()
+        for tid in os.listdir(f"/proc/{ppid}/task"):
+            st = open(f"/proc/{ppid}/task/{tid}/stat").read()
+            out.add(int(st.rsplit(")", 1)[1].split()[36]))
+    except (OSError, ValueError, IndexError):
+        pass
+    return out
+
+
+def pin_one_ccd(avoid_parent=True):
     """Pin this process (before any thread starts) to the allowed CPUs of one
     last-level-cache domain (a CCD on EPYC), one logical CPU per physical core
-    (no SMT sibling shares a core with another of our threads). Returns what
-    was done: the CPUs before / after and the LLC group."""
+    (no SMT sibling shares a core with another of our threads), preferring a
+    domain none of the parent's threads ran on (the bench process and its HIP
+    runtime threads). Returns what was done: the CPUs before / after, the LLC
+    group and the parent's CPUs."""
     before = sorted(os.sched_getaffinity(0))
-    rec = {"allowed_before": before}
+    rec = {"allowed_before_count": len(before)}
     try:
         groups = {}
         for c in before:
             llc = open(f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list").read()
             groups.setdefault(llc.strip(), []).append(c)
-        llc, cpus = max(groups.items(), key=lambda kv: (len(kv[1]), -kv[1][0]))
+        par = _parent_cpus() if avoid_parent else set()
+        rec["parent_cpus"] = sorted(par)
+        free = {k: v for k, v in groups.items() if not (set(_cpu_list(k)) & par)}
+        pool = free if any(len(v) >= 2 for v in free.values()) else groups
+        llc, cpus = max(pool.items(), key=lambda kv: (len(kv[1]), -kv[1][0]))
         cores, seen = [], set()
         for c in cpus:
             sib = _cpu_list(open(f"/sys/devices/system/cpu/cpu{c}/topology/"
