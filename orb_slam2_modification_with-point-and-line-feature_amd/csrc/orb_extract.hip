@@ -293,7 +293,6 @@ constexpr int kPyrDepth = ORBPL_PYR_DEPTH;        // blur walk
 #define ORBPL_PYR_RS_DEPTH 4
 #endif
 constexpr int kPyrRsDepth = ORBPL_PYR_RS_DEPTH;   // resize walk (2 source rows per row)
-constexpr int kPyrCopyDepth = 8;   // level-0 input copy / mirror rows: loads in flight per thread
 
 // Row segments of a walk (tasks = groups x nseg, rps rows per segment): the
 // split with the fewest sequential rows per thread, counting `warm` extra
@@ -651,38 +650,19 @@ __global__ void __launch_bounds__(kPyrThreads) k_pyramid(const uint8_t* __restri
     const int na = B.na[l], nb = B.nb[l];
     // ---- 1. content rows [na, nb) ----
     if (l == 0) {
-      // the input rows, 16 bytes per item, kPyrCopyDepth items' loads issued
-      // before their stores (a thread's items were one load round trip each)
       const uint8_t* src = img + (long long)f * frame_pitch;
       const int nv = (L.w + 15) >> 4;
       const uint32_t inv_nv = div_inv(nv);
-      const int nitems = (nb - na) * nv;
-      for (int i0 = t; i0 < nitems; i0 += kPyrThreads * kPyrCopyDepth) {
-        uint4 v[kPyrCopyDepth];
-        bool fast[kPyrCopyDepth];
-#pragma unroll
-        for (int j = 0; j < kPyrCopyDepth; j++) {
-          const int i = i0 + j * kPyrThreads;
-          const int rr = div_small(min(i, nitems - 1), inv_nv);
-          const int r = na + rr, c = (min(i, nitems - 1) - rr * nv) * 16;
-          const uint8_t* s = src + (long long)r * stride + c;
-          fast[j] = i < nitems && c + 16 <= L.w && ((reinterpret_cast<uintptr_t>(s) & 15) == 0);
-          if (fast[j]) v[j] = *reinterpret_cast<const uint4*>(s);
-        }
-#pragma unroll
-        for (int j = 0; j < kPyrCopyDepth; j++) {
-          const int i = i0 + j * kPyrThreads;
-          if (i >= nitems) break;
-          const int rr = div_small(i, inv_nv);
-          const int r = na + rr, c = (i - rr * nv) * 16;
-          uint8_t* d = fp + content_off(L, c, r);
-          if (fast[j]) {
-            *reinterpret_cast<uint4*>(d) = v[j];
-          } else {
-            const uint8_t* s = src + (long long)r * stride + c;
-            const int n = min(16, L.w - c);
-            for (int k = 0; k < n; k++) d[k] = s[k];
-          }
+      for (int i = t; i < (nb - na) * nv; i += kPyrThreads) {
+        const int rr = div_small(i, inv_nv);
+        const int r = na + rr, c = (i - rr * nv) * 16;
+        const uint8_t* s = src + (long long)r * stride + c;
+        uint8_t* d = fp + content_off(L, c, r);
+        if (c + 16 <= L.w && ((reinterpret_cast<uintptr_t>(s) & 15) == 0)) {
+          *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(s);
+        } else {
+          const int n = min(16, L.w - c);
+          for (int k = 0; k < n; k++) d[k] = s[k];
         }
       }
     } else {
@@ -738,29 +718,20 @@ __global__ void __launch_bounds__(kPyrThreads) k_pyramid(const uint8_t* __restri
       const int b0 = max(na, L.h - 1 - kEdge), b1 = min(nb, L.h - 1);   // y = 2h-2-cy
       const int nt = max(0, t1 - t0), nbm = max(0, b1 - b0);
       const int nq = L.pitch >> 4;
-      const int nitems = (nt + nbm) * nq;
-      // kPyrCopyDepth 16-byte chunks' loads issued before their stores
-      for (int i0 = t; i0 < nitems; i0 += kPyrThreads * kPyrCopyDepth) {
-        uint4 v[kPyrCopyDepth];
-        uint4* dst[kPyrCopyDepth];
-#pragma unroll
-        for (int j = 0; j < kPyrCopyDepth; j++) {
-          const int i = min(i0 + j * kPyrThreads, nitems - 1);
-          const int k = i / nq, q = i - k * nq;
-          int cy, py;
-          if (k < nt) {
-            cy = t0 + k;
-            py = kEdge - cy;
-          } else {
-            cy = b0 + (k - nt);
-            py = 2 * L.h - 2 - cy + kEdge;
-          }
-          v[j] = reinterpret_cast<const uint4*>(fp + L.pyr_off + (long long)(cy + kEdge) * L.pitch)[q];
-          dst[j] = reinterpret_cast<uint4*>(fp + L.pyr_off + (long long)py * L.pitch) + q;
+      for (int i = t; i < (nt + nbm) * nq; i += kPyrThreads) {
+        const int k = i / nq, q = i - k * nq;
+        int cy, py;
+        if (k < nt) {
+          cy = t0 + k;
+          py = kEdge - cy;
+        } else {
+          cy = b0 + (k - nt);
+          py = 2 * L.h - 2 - cy + kEdge;
         }
-#pragma unroll
-        for (int j = 0; j < kPyrCopyDepth; j++)
-          if (i0 + j * kPyrThreads < nitems) *dst[j] = v[j];
+        const uint4* s =
+            reinterpret_cast<const uint4*>(fp + L.pyr_off + (long long)(cy + kEdge) * L.pitch) + q;
+        uint4* d = reinterpret_cast<uint4*>(fp + L.pyr_off + (long long)py * L.pitch) + q;
+        *d = *s;
       }
     }
     __syncthreads();
