@@ -284,7 +284,7 @@ def pmc_traffic(kernel, workload, streams):
     kernel's "frames_per_launch" in the summary, else its stream count). PMC counters
     need their own rocprofv3 passes, so they cannot be read live. Stage
     kernels joined with '+' sum their parts."""
-    for rnd in ("r04", "r03", "r02", "r01"):
+    for rnd in ("r05", "r04", "r03", "r02", "r01"):
         f = ROOT / "profiles" / rnd / f"pmc_traffic_{workload}.json"
         if not f.exists() and workload == "points":
             f = ROOT / "profiles" / rnd / "pmc_traffic.json"
