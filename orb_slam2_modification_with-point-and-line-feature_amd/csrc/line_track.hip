@@ -19,6 +19,7 @@
 namespace orbpl {
 
 __global__ void __launch_bounds__(64) k_line_prepare(TrackConsts c, LineTrackArgs a) {
+  trk_priority();
   const int s = blockIdx.x, lane = threadIdx.x;
   const int nl = a.nl[s];
   const long long lb = (long long)s * kLineKeep;
@@ -217,6 +218,7 @@ __device__ bool project_map_line(const TrackConsts& c, const double T[12], const
 // One 256-thread block per stream.
 __global__ void __launch_bounds__(256) k_line_match(TrackConsts c, LineTrackArgs a,
                                                      StreamState* st) {
+  trk_priority();
   __shared__ orbpl_keyline s_kl[kLineKeep];
   __shared__ int s_src[kLineKeep];
   __shared__ int s_np;
@@ -352,6 +354,7 @@ void launch_line_match(const TrackConsts& c, const LineTrackArgs& a, StreamState
 // thread i scans the right lines for left line i in index order with the
 // same double / float operation sequence as the oracle.
 __global__ void __launch_bounds__(128) k_stereo_lines(TrackConsts c, StereoLineArgs a) {
+  trk_priority();
   __shared__ orbpl_keyline s_kr[kLineKeep];
   __shared__ uint4 s_dr[kLineKeep * 2];
   const int s = blockIdx.x, t = threadIdx.x;
@@ -513,6 +516,7 @@ __device__ __forceinline__ void line_list_stream(const TrackConsts& c, LineListA
 // batched: one workgroup per stream, or (a.list) a small grid looping over
 // the streams a list names
 __global__ void __launch_bounds__(256) k_line_match_list(TrackConsts c, LineListArgs a) {
+  trk_priority();
   if (a.list) {
     const int n = *a.list_n;
     for (int b = blockIdx.x; b < n; b += gridDim.x) {
@@ -527,6 +531,7 @@ __global__ void __launch_bounds__(256) k_line_match_list(TrackConsts c, LineList
 // Frame::IsInFrustum(MapLine*) (Frame.cc:403-430)
 __global__ void k_line_in_frustum(const float* __restrict__ Tcw, int n, const float* __restrict__ xyz6,
                                   uint8_t* __restrict__ in_view) {
+  trk_priority();
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   float z[2];
@@ -550,6 +555,7 @@ void launch_line_match_list(const TrackConsts& c, const LineListArgs& a, hipStre
 __global__ void k_line_in_frustum_b(const float* __restrict__ Tcw, int pose_stride,
                                     const int* __restrict__ n_arr, long long pitch,
                                     const float* __restrict__ xyz6, uint8_t* __restrict__ in_view) {
+  trk_priority();
   const int b = blockIdx.y;
   const long long o = (long long)b * pitch;
   const float* T = Tcw + (long long)b * pose_stride;

@@ -59,6 +59,7 @@ __device__ __forceinline__ int block_sum(int v, int* wsum) {
 }  // namespace
 
 __global__ void __launch_bounds__(256) k_lm_gather(LocalMapArgs a) {
+  trk_priority();
   __shared__ uint32_t seen[kMatchMaxKp / 32];
   __shared__ uint32_t seen_l[(kLineKeep + 31) / 32];
   __shared__ int wsum[4];
@@ -161,6 +162,7 @@ __global__ void __launch_bounds__(256) k_lm_gather(LocalMapArgs a) {
 }
 
 __global__ void __launch_bounds__(256) k_lm_assemble(LocalMapArgs a) {
+  trk_priority();
   const int s = blockIdx.x, t = threadIdx.x;
   const StreamState& S = a.st[s];
   const int K = a.kp_pitch;
@@ -193,6 +195,7 @@ __global__ void __launch_bounds__(256) k_lm_assemble(LocalMapArgs a) {
 }
 
 __global__ void __launch_bounds__(256) k_lm_count(LocalMapArgs a, int frame_id) {
+  trk_priority();
   __shared__ int wsum[4];
   const int s = blockIdx.x, t = threadIdx.x;
   StreamState& S = a.st[s];
@@ -213,6 +216,7 @@ __global__ void __launch_bounds__(256) k_lm_count(LocalMapArgs a, int frame_id) 
 }
 
 __global__ void __launch_bounds__(256) k_lm_push(TrackConsts c, LocalMapArgs a) {
+  trk_priority();
   __shared__ float sT[16];
   const int s = blockIdx.x, t = threadIdx.x;
   const StreamState& S = a.st[s];
@@ -277,6 +281,7 @@ __global__ void __launch_bounds__(256) k_lm_push(TrackConsts c, LocalMapArgs a) 
 //                 15 / 10 match gates of the pose
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_trk_prep(TrkArgs a) {
+  trk_priority();
   __shared__ int wsum[4];
   const int s = blockIdx.x, t = threadIdx.x;
   StreamState& S = a.st[s];
@@ -321,6 +326,7 @@ __global__ void __launch_bounds__(256) k_trk_prep(TrkArgs a) {
 }
 
 __global__ void __launch_bounds__(256) k_trk_merge(TrkArgs a) {
+  trk_priority();
   const int s = blockIdx.x, t = threadIdx.x;
   StreamState& S = a.st[s];
   if (!S.trk) return;

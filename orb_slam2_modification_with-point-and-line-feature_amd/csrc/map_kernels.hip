@@ -412,6 +412,7 @@ __global__ void k_map_reset(MapArgs a, const float* T0, int nstreams) {
 }
 
 __global__ void __launch_bounds__(kT) k_map_begin(TrackConsts c, MapArgs a) {
+  trk_priority();
   __shared__ unsigned long long keys[kMatchMaxKp];
   __shared__ LRec lrec[kLineKeep];
   __shared__ int sstk[96];
@@ -586,6 +587,7 @@ __global__ void __launch_bounds__(kT) k_map_begin(TrackConsts c, MapArgs a) {
 
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(kT) k_map_resolve_motion(MapArgs a) {
+  trk_priority();
   __shared__ int wsum[4];
   __shared__ int s_trk;
   const int s = blockIdx.x, t = threadIdx.x;
@@ -718,6 +720,7 @@ __device__ static void pose_inputs(const MapArgs& a, const Pools& P, int n, int 
 }
 
 __global__ void __launch_bounds__(kT) k_map_trk_merge(MapArgs a) {
+  trk_priority();
   __shared__ int s_go;
   const int s = blockIdx.x, t = threadIdx.x;
   StreamState& S = a.st[s];
@@ -751,6 +754,7 @@ __global__ void __launch_bounds__(kT) k_map_trk_merge(MapArgs a) {
 }
 
 __global__ void __launch_bounds__(kT) k_map_resolve_trk(MapArgs a) {
+  trk_priority();
   __shared__ int wsum[4];
   const int s = blockIdx.x, t = threadIdx.x;
   MapState& M = a.ms[s];
@@ -807,6 +811,7 @@ __global__ void __launch_bounds__(kT) k_map_resolve_trk(MapArgs a) {
 
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(kT) k_map_local(MapArgs a) {
+  trk_priority();
   __shared__ int cnt[kMapMaxKF];
   __shared__ int wsum[4];
   const int s = blockIdx.x, t = threadIdx.x;
@@ -968,6 +973,7 @@ __global__ void __launch_bounds__(kT) k_map_local(MapArgs a) {
 }
 
 __global__ void __launch_bounds__(kT) k_map_assemble(MapArgs a) {
+  trk_priority();
   const int s = blockIdx.x, t = threadIdx.x;
   const StreamState& S = a.st[s];
   if (!S.lm_active) return;
@@ -1056,6 +1062,7 @@ __device__ static void new_line(const TrackConsts& c, const MapArgs& a, const Po
 }
 
 __global__ void __launch_bounds__(kT) k_map_finish(TrackConsts c, MapArgs a) {
+  trk_priority();
   __shared__ unsigned long long keys[kMatchMaxKp];
   __shared__ LRec lrec[kLineKeep];
   __shared__ int lpool[kLineKeep];   // the pool slot a line's new map line takes, -1 none
@@ -1365,6 +1372,7 @@ __global__ void __launch_bounds__(kT) k_map_finish(TrackConsts c, MapArgs a) {
 // one thread per keypoint of the keyframe, grid (keypoints / 64, streams), so
 // the points' dependent gathers overlap across many waves.
 __global__ void __launch_bounds__(64) k_map_kf_points(TrackConsts c, MapArgs a) {
+  trk_priority();
   __shared__ uint16_t dscr[64][kMapMaxKF];
   const int s = blockIdx.y;
   const MapState& M = a.ms[s];
@@ -1411,6 +1419,7 @@ __global__ void __launch_bounds__(64) k_map_kf_points(TrackConsts c, MapArgs a) 
 // ordered lists (thread k updates keyframe k), its own list and parent.
 // Dynamic LDS: 5 x kfc x kfc bytes of per-thread scratch.
 __global__ void __launch_bounds__(kT) k_map_connect(MapArgs a) {
+  trk_priority();
   extern __shared__ int cscr[];
   __shared__ int cnt[kMapMaxKF];
   __shared__ int pw[kMapMaxKF], pk[kMapMaxKF];

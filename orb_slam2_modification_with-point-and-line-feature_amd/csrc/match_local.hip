@@ -31,6 +31,7 @@
 namespace orbpl {
 
 __global__ void __launch_bounds__(256) k_in_frustum(TrackConsts c, float log_scale, InFrustumArgs a) {
+  trk_priority();
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (a.n_arr) {  // batched: stream blockIdx.y
     const int b = blockIdx.y;
@@ -275,6 +276,7 @@ __device__ __forceinline__ Top2 pick2(const LocalShared<KP>& S, const TopList& t
 
 template <int kLocalKp, int NT>
 __global__ void __launch_bounds__(NT) k_match_local(TrackConsts c, LocalArgs a) {
+  trk_priority();
   if (a.n_arr) {  // batched: stream blockIdx.x
     const int b = blockIdx.x;
     const long long ko = (long long)b * a.kp_pitch, mo = (long long)b * a.mp_pitch;
@@ -772,6 +774,7 @@ __device__ void match_bow_body(const BowArgs& a, BowShared<CAP>& B, const uint4*
 }
 
 __global__ void __launch_bounds__(256) k_match_bow(BowArgs a) {
+  trk_priority();
   __shared__ BowShared<kBowMax> B;
   extern __shared__ uint4 bow_fdl[];
   const int nf = min(a.nf, kBowMax);
@@ -821,6 +824,7 @@ __device__ __forceinline__ void trk_bow_stream(const TrkArgs& a, BowShared<CAP>&
 // streams (the map model's TrackReferenceKeyFrame streams)
 template <int CAP>
 __global__ void __launch_bounds__(256) k_trk_bow(TrkArgs a) {
+  trk_priority();
   __shared__ BowShared<CAP> B;
   if (a.list) {
     const int n = *a.list_n;

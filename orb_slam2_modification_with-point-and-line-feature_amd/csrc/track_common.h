@@ -6,6 +6,20 @@
 
 namespace orbpl {
 
+// Issue priority of the tracking-stream kernels' waves. In the pipelined step
+// they share SIMDs with the next frame's extraction waves (k_fast_cells is
+// VALU-bound), and the instruction arbiter picks by priority, then age: a
+// tracking wave that arrives while extraction waves hold the SIMD is the
+// youngest and gets the leftover issue slots, so its serial chain (k_pose's
+// LM iterations, the matchers' per-keypoint loops) stretches to the length
+// of the extraction kernel beside it. s_setprio raises it above them (0-3).
+#ifndef ORBPL_TRK_PRIO
+#define ORBPL_TRK_PRIO 3
+#endif
+__device__ __forceinline__ void trk_priority() {
+  if constexpr (ORBPL_TRK_PRIO > 0) __builtin_amdgcn_s_setprio(ORBPL_TRK_PRIO);
+}
+
 constexpr int kGridCols = 64;   // FRAME_GRID_COLS (Frame.h:41)
 constexpr int kGridRows = 48;   // FRAME_GRID_ROWS (Frame.h:40)
 constexpr int kMaxLevelsT = 16;

@@ -70,6 +70,7 @@ __global__ void __launch_bounds__(256) k_frame_prepare(TrackConsts c, const KeyP
 // Constant-velocity prediction (Tracking.cc:1228). One thread per stream.
 // ---------------------------------------------------------------------------
 __global__ void k_predict(StreamState* __restrict__ st, int nstreams) {
+  trk_priority();
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nstreams) return;
   StreamState& S = st[s];
@@ -287,6 +288,7 @@ static_assert(kMatchMaxKp * kTopK >= kGridCols * kGridRows, "top[] doubles as ce
 
 template <int KMAX, int NT>
 __global__ void __launch_bounds__(NT) k_match_last(TrackConsts c, MatchArgs a) {
+  trk_priority();
   static_assert((kGridCols * kGridRows) % NT == 0 && NT <= kMatchThreads, "cell scan split");
   extern __shared__ char smem_raw[];
   MatchShared<KMAX>& S = *reinterpret_cast<MatchShared<KMAX>*>(smem_raw);
@@ -1775,6 +1777,7 @@ __device__ __forceinline__ void pose_stream(const TrackConsts& tc, const PoseArg
 // when no stream has work)
 template <int kPoseThreads, int kMinWaves>
 __global__ void __launch_bounds__(kPoseThreads, kMinWaves) k_pose(TrackConsts tc, PoseArgs a) {
+  trk_priority();
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   PoseShared& S = *reinterpret_cast<PoseShared*>(smem_raw);
   PoseLds V;
@@ -1815,6 +1818,7 @@ __global__ void __launch_bounds__(256) k_finish(TrackConsts c, StreamState* __re
                                                 float* __restrict__ mp_xyz,
                                                 int* __restrict__ nobs, LineFinish lf,
                                                 int local_map) {
+  trk_priority();
   const int s = blockIdx.x, t = threadIdx.x;
   StreamState& S = st[s];
   const int n = n_in[s];

@@ -25,7 +25,7 @@ def _vocab_arrays(L, seed=3):
 
 
 def _run(orbpl, oracle, lines, refkf, S, F, seed, turn=None, pipelined=False, clears=None,
-         vocab_levels=5, stereo=False, fps=None):
+         vocab_levels=5, stereo=False, fps=None, thdepth=None):
     """clears: {frame: [streams]} whose velocity is cleared before that
     frame's step (orbpl_tracker_clear_velocity / MapVO.clear_velocity).
     stereo: KITTI 00 rectified pairs (2000 features) through
@@ -42,7 +42,9 @@ def _run(orbpl, oracle, lines, refkf, S, F, seed, turn=None, pipelined=False, cl
         for f in range(f0, F):
             g, d = frames[s][f]
             frames[s][f] = (np.ascontiguousarray(g[::-1, ::-1]), np.ascontiguousarray(d[::-1, ::-1]))
-    cfg = seqs[0][0]
+    cfg = dict(seqs[0][0])
+    if thdepth is not None:
+        cfg["thdepth"] = thdepth   # ThDepth: the close / far split of NeedNewKeyFrame
     flags = (oracle.TRACK_REFKF if refkf else 0) | (oracle.TRACK_STEREO if stereo else 0)
     nf = 2000 if stereo else 1000
     W, H = cfg.get("width", 640), cfg.get("height", 480)
@@ -226,3 +228,24 @@ def test_map_tracker_stereo_matches_oracle(orbpl, oracle, lines, refkf, pipeline
         assert r[0]["keyframe"] == 2 and r[0]["state"] == 1      # StereoInitialization
         assert all(c["ok"] == 1 for c in r[1:])
         assert r[-1]["local_points"] > 0 and r[-1]["temporal_points"] > 0   # UpdateLastFrame
+
+
+@pytest.mark.parametrize("lines,pipelined", [(False, True), (True, False)])
+def test_map_tracker_stereo_keyframe_after_outliers(orbpl, oracle, lines, pipelined):
+    """A stereo keyframe inserted on a frame whose TrackLocalMap found
+    outliers: CreateNewKeyFrame's close-point pass (Tracking.cc:1583-1660)
+    runs before Track() drops the outliers' map points (Tracking.cc:547-555),
+    and the next frames track against what it created. ThDepth 5 (2.7 m)
+    makes most of the room's points far, so frame 4 of stream 0 needs a
+    keyframe (nTrackedClose < 100 and nNonTrackedClose > 70,
+    Tracking.cc:1465-1480); the oracle inserts it there
+    (tests/_scenes.stereo_sequence, seed 60). Every count, pose and both maps
+    equal the oracle's."""
+    res = _run(orbpl, oracle, lines, True, S=2, F=6, seed=60, pipelined=pipelined, stereo=True,
+               fps=10, thdepth=5.0)
+    r = res[0]
+    kf = [f for f in range(1, 6) if r[f]["keyframe"] == 1]
+    assert kf, [c["keyframe"] for c in r]
+    assert any(r[f]["ninliers"] < r[f]["nmatches"] for f in range(1, kf[0] + 1)), r
+    assert r[kf[0]]["map_points"] > r[0]["map_points"]
+    assert all(c["ok"] == 1 for c in r[1:])
