@@ -498,119 +498,14 @@ __device__ __forceinline__ void pyr_blur_rows(const LevelGeom& L, const uint8_t*
   }
 }
 
-// ORBPL_PYR_MERGE=1: two barriers per level (level l's resize beside level
-// l-1's blur, borders and mirror rows both from content). Measured slower and
-// off (A/B on one box, two rounds: k_pyramid isolated 2.08 vs 2.03 ms with the
-// three-barrier order, tools/gpu_r04_f.sh): the phases are not what the
-// frame's chain waits on.
-#ifndef ORBPL_PYR_MERGE
-#define ORBPL_PYR_MERGE 0
-#endif
-
-// level 0 content rows [na, nb): the input image, 16 bytes per task
-__device__ __forceinline__ void pyr_copy_level0(const LevelGeom& L, const uint8_t* src, int stride,
-                                                uint8_t* fp, int na, int nb) {
-  const int nv = (L.w + 15) >> 4;
-  const uint32_t inv_nv = div_inv(nv);
-  for (int i = threadIdx.x; i < (nb - na) * nv; i += kPyrThreads) {
-    const int rr = div_small(i, inv_nv);
-    const int r = na + rr, c = (i - rr * nv) * 16;
-    const uint8_t* s = src + (long long)r * stride + c;
-    uint8_t* d = fp + content_off(L, c, r);
-    if (c + 16 <= L.w && ((reinterpret_cast<uintptr_t>(s) & 15) == 0)) {
-      *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(s);
-    } else {
-      const int n = min(16, L.w - c);
-      for (int k = 0; k < n; k++) d[k] = s[k];
-    }
-  }
-}
-
-// copyMakeBorder(19, REFLECT_101) of level L for the content rows [na, nb)
-// and the top / bottom mirror rows whose source row lies in [na, nb), all
-// from content bytes only (no dependency on other border bytes): per (row,
-// side) the 19 mirrored side bytes, per mirror row its content bytes.
-__device__ __forceinline__ void pyr_borders(const LevelGeom& L, uint8_t* fp, int na, int nb) {
-  const int t = threadIdx.x;
-  const int t0 = max(na, 1), t1 = min(nb, kEdge + 1);               // y = -cy
-  const int b0 = max(na, L.h - 1 - kEdge), b1 = min(nb, L.h - 1);   // y = 2h-2-cy
-  const int nt = max(0, t1 - t0), nbm = max(0, b1 - b0);
-  const int nc = nb - na, nrow = nc + nt + nbm;
-  // row j of the task list: (source content row, destination padded row)
-  auto rows_of = [&](int j, int* cy, int* py) {
-    if (j < nc) {
-      *cy = na + j;
-      *py = *cy + kEdge;
-    } else if (j < nc + nt) {
-      *cy = t0 + (j - nc);
-      *py = kEdge - *cy;
-    } else {
-      *cy = b0 + (j - nc - nt);
-      *py = 2 * L.h - 2 - *cy + kEdge;
-    }
-  };
-  if (L.w >= kEdge + 2) {
-    for (int i = t; i < nrow * 2; i += kPyrThreads) {
-      int cy, py;
-      rows_of(i >> 1, &cy, &py);
-      const int side = i & 1;
-      const uint8_t* srow = fp + L.pyr_off + (long long)(cy + kEdge) * L.pitch;
-      uint8_t* drow = fp + L.pyr_off + (long long)py * L.pitch;
-      const int c0 = side ? L.w - kEdge - 1 : 0;        // first content byte used
-      const int a = kContent0 + c0;                     // its byte in the row
-      const uint32_t* src = reinterpret_cast<const uint32_t*>(srow + (a & ~3));
-      const int o = a & 3;
-      uint32_t w[6];
-#pragma unroll
-      for (int k = 0; k < 6; k++) w[k] = src[k];
-      auto byte_at = [&](int j) -> uint8_t {
-        const int b = o + j;
-        uint32_t v = w[0];
-#pragma unroll
-        for (int k = 1; k < 6; k++) v = (b >> 2) == k ? w[k] : v;
-        return (uint8_t)(v >> (8 * (b & 3)));
-      };
-      if (side == 0) {
-#pragma unroll
-        for (int px = 0; px < kEdge; px++) drow[kLead + px] = byte_at(kEdge - px);
-      } else {
-#pragma unroll
-        for (int k = 0; k < kEdge; k++) drow[kLead + L.w + kEdge + k] = byte_at(kEdge - 1 - k);
-      }
-    }
-  } else {
-    for (int i = t; i < nrow * 2 * kEdge; i += kPyrThreads) {
-      const int j = i / (2 * kEdge), k = i - j * 2 * kEdge;
-      int cy, py;
-      rows_of(j, &cy, &py);
-      const int px = k < kEdge ? k : L.w + k;          // padded column
-      const int cx = reflect101_dev(px - kEdge, L.w);
-      fp[padded_off(L, px, py)] = fp[content_off(L, cx, cy)];
-    }
-  }
-  // content bytes of the mirror rows: 16-byte chunks, the tail byte by byte
-  const int nv = (L.w + 15) >> 4;
-  for (int i = t; i < (nt + nbm) * nv; i += kPyrThreads) {
-    const int j = i / nv, q = i - j * nv;
-    int cy, py;
-    rows_of(nc + j, &cy, &py);
-    const uint8_t* s = fp + content_off(L, 16 * q, cy);
-    uint8_t* d = fp + L.pyr_off + (long long)py * L.pitch + kContent0 + 16 * q;
-    if (16 * q + 16 <= L.w) {
-      *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(s);
-    } else {
-      for (int k = 0; k < L.w - 16 * q; k++) d[k] = s[k];
-    }
-  }
-}
-
 __global__ void __launch_bounds__(kPyrThreads) k_pyramid(const uint8_t* __restrict__ img, int stride,
                                                          long long frame_pitch, uint8_t* pyr,
                                                          uint8_t* __restrict__ blur,
                                                          const OrbGeom* __restrict__ g,
                                                          const int* __restrict__ rs_all,
                                                          const PyrBand* __restrict__ bands,
-                                                         long long* __restrict__ prof) {
+                                                         long long* __restrict__ prof, int l0,
+                                                         int l1) {
   const int t = threadIdx.x;
   const int f = blockIdx.y;
   // debug: phase time stamps of block (0, 0) (4 per level after the start)
@@ -619,33 +514,9 @@ __global__ void __launch_bounds__(kPyrThreads) k_pyramid(const uint8_t* __restri
   const PyrBand& B = bands[blockIdx.x];
   uint8_t* fp = pyr + (long long)f * g->pyr_bytes;
   uint8_t* bp = blur + (long long)f * g->blur_bytes;
-  const int nl = g->nlevels;
-#if ORBPL_PYR_MERGE
-  // Two barriers per level: P(l) = level l's content rows (copy / resize of
-  // level l-1's content) beside the blur of level l-1 (its padded rows are
-  // complete), then Q(l) = level l's side borders and mirror rows, both
-  // computed from content (a mirror row's side bytes reflect its source row's
-  // content, as the copy of the finished padded row gave them).
-  for (int l = 0; l <= nl; l++) {
-    if (l < nl) {
-      const LevelGeom& L = g->lv[l];
-      const int na = B.na[l], nb = B.nb[l];
-      if (l == 0) {
-        pyr_copy_level0(L, img + (long long)f * frame_pitch, stride, fp, na, nb);
-      } else {
-        pyr_resize_rows(L, g->lv[l - 1], rs_all + L.rs_off, fp, na, nb);
-      }
-    }
-    if (l > 0) pyr_blur_rows(g->lv[l - 1], fp, bp, B.oa[l - 1], B.ob[l - 1]);
-    if (stamp) prof[1 + 4 * min(l, nl - 1)] = (long long)wall_clock64();
-    if (l == nl) break;
-    __syncthreads();
-    pyr_borders(g->lv[l], fp, B.na[l], B.nb[l]);
-    __syncthreads();
-    if (stamp) prof[2 + 4 * l] = (long long)wall_clock64();
-  }
-#else
-  for (int l = 0; l < nl; l++) {
+  // levels [l0, l1) (one launch per group of levels: the FAST launches of a
+  // group's levels run on another stream beside the next group's launch)
+  for (int l = l0; l < l1; l++) {
     const LevelGeom& L = g->lv[l];
     const int na = B.na[l], nb = B.nb[l];
     // ---- 1. content rows [na, nb) ----
@@ -740,7 +611,6 @@ __global__ void __launch_bounds__(kPyrThreads) k_pyramid(const uint8_t* __restri
     pyr_blur_rows(L, fp, bp, B.oa[l], B.ob[l]);
     if (stamp) prof[4 + 4 * l] = (long long)wall_clock64();
   }
-#endif
 }
 
 // NMS for the centre pair at M[r][q], M[r][q+1]: returns (m_lo, m_hi) in
@@ -769,13 +639,13 @@ __global__ void __launch_bounds__(256, ORBPL_FAST_MINW) k_fast_cells(const uint8
                                                     const CellGeom* __restrict__ cells,
                                                     uint32_t* __restrict__ cell_cands,
                                                     int* __restrict__ cell_counts, int ini_th,
-                                                    int min_th) {
+                                                    int min_th, int cell0, int cell1) {
   extern __shared__ uint32_t fast_smem[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int bx, f;
   xcd_block(&bx, &f);
-  const int cell = bx * 4 + wave;
-  if (cell >= g->ncells_total) return;
+  const int cell = cell0 + bx * 4 + wave;   // cells [cell0, cell1): one group of levels
+  if (cell >= cell1) return;
   const CellGeom cg = cells[cell];
   const int slots = g->cell_slots;
   int* cnt_out = cell_counts + (long long)f * g->ncells_total + cell;
@@ -1703,18 +1573,21 @@ int read_octree_profile(long long* out128) {
 
 void launch_pyramid(const OrbGeom& hg, const OrbGeom* dg, const uint8_t* img, int stride,
                     long long frame_pitch, uint8_t* pyr, uint8_t* blur, const int* rs,
-                    const PyrBand* bands, int nbands, int batch, long long* prof,
+                    const PyrBand* bands, int nbands, int batch, long long* prof, int l0, int l1,
                     hipStream_t s) {
   hipLaunchKernelGGL(k_pyramid, dim3(nbands, batch), dim3(kPyrThreads), 0, s, img, stride,
-                     frame_pitch, pyr, blur, dg, rs, bands, prof);
+                     frame_pitch, pyr, blur, dg, rs, bands, prof, l0, l1);
 }
 
 void launch_fast(const OrbGeom& hg, const OrbGeom* dg, const CellGeom* cells, const uint8_t* pyr,
                  uint32_t* cell_cands, int* cell_counts, int ini_th, int min_th, int batch,
-                 hipStream_t s) {
+                 int l0, int l1, hipStream_t s) {
   const size_t smem = 4 * 4 * (size_t)fast_wave_words(hg.fast_win_w, hg.fast_win_h);
-  hipLaunchKernelGGL(k_fast_cells, dim3((hg.ncells_total + 3) / 4, batch), dim3(256), smem, s, pyr,
-                     dg, cells, cell_cands, cell_counts, ini_th, min_th);
+  const int c0 = hg.lv[l0].cell_base;
+  const int c1 = l1 < hg.nlevels ? hg.lv[l1].cell_base : hg.ncells_total;
+  if (c1 <= c0) return;
+  hipLaunchKernelGGL(k_fast_cells, dim3((c1 - c0 + 3) / 4, batch), dim3(256), smem, s, pyr, dg,
+                     cells, cell_cands, cell_counts, ini_th, min_th, c0, c1);
 }
 
 void launch_octree(const OrbGeom& hg, const OrbGeom* dg, const uint32_t* cell_cands,

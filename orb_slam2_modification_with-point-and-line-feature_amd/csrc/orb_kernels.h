@@ -20,15 +20,17 @@ hipError_t upload_pattern(hipStream_t s);
 int read_octree_profile(long long* out128);
 int read_od_profile(long long* out8);
 
-// Padded pyramid + borders + blurred levels of `batch` frames (k_pyramid);
+// Padded pyramid + borders + blurred levels [l0, l1) of `batch` frames
+// (k_pyramid; level l0 > 0 reads level l0 - 1 of an earlier launch);
 // bands = the nbands-band partition (pyr_band_base(nbands) in the table).
 void launch_pyramid(const OrbGeom& hg, const OrbGeom* dg, const uint8_t* img, int stride,
                     long long frame_pitch, uint8_t* pyr, uint8_t* blur, const int* rs,
-                    const PyrBand* bands, int nbands, int batch, long long* prof,
+                    const PyrBand* bands, int nbands, int batch, long long* prof, int l0, int l1,
                     hipStream_t s);
+// FAST cells of levels [l0, l1)
 void launch_fast(const OrbGeom& hg, const OrbGeom* dg, const CellGeom* cells, const uint8_t* pyr,
                  uint32_t* cell_cands, int* cell_counts, int ini_th, int min_th, int batch,
-                 hipStream_t s);
+                 int l0, int l1, hipStream_t s);
 void launch_octree(const OrbGeom& hg, const OrbGeom* dg, const uint32_t* cell_cands,
                    const int* cell_counts, uint32_t* kcand, int* knode, uint32_t* kp_list,
                    int* kp_count, int* err_flag, int batch, hipStream_t s);

@@ -10,6 +10,7 @@
 #include <mutex>
 #include <map>
 #include <set>
+#include <cctype>
 #include <string>
 #include <utility>
 #include <vector>
@@ -135,6 +136,17 @@ struct orbx_ctx {
   OrbHostGeom hg;
   hipStream_t stream = nullptr;
   hipEvent_t ev[6] = {};
+  // level pipeline (hardware queues >= 8, ORBPL_LEVEL_PIPE=0 turns it off):
+  // the pyramid runs as one launch per group of levels on `stream` and the
+  // FAST launch of each group on `fstream` once that group is written, so
+  // FAST of the early levels (2/3 of its work) runs beside the pyramid's
+  // chain of later levels instead of after it
+  hipStream_t fstream = nullptr;
+  hipEvent_t ev_group[kMaxLevels] = {};   // pyramid group g written (stream)
+  hipEvent_t ev_fjoin = nullptr;          // every FAST launch done (fstream)
+  hipEvent_t ev_fast[2] = {};             // FAST span, own timing
+  int ngroups = 1;
+  int group_end[kMaxLevels] = {};         // group g = levels [end[g-1], end[g])
   bool timed = false;
   OrbGeom* d_geom = nullptr;
   CellGeom* d_cells = nullptr;
@@ -262,6 +274,15 @@ static void free_ctx(orbx_ctx* c) {
     if (p) (void)hipFree(p);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
+  for (auto& e : c->ev_group)
+    if (e) (void)hipEventDestroy(e);
+  for (auto& e : c->ev_fast)
+    if (e) (void)hipEventDestroy(e);
+  if (c->ev_fjoin) (void)hipEventDestroy(c->ev_fjoin);
+  if (c->fstream) {
+    (void)hipStreamSynchronize(c->fstream);
+    (void)hipStreamDestroy(c->fstream);
+  }
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -318,6 +339,38 @@ int orbx_create(const orbpl_orb_params* p, int width, int height, int max_batch,
     CK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   }
   for (auto& e : c->ev) CK(hipEventCreate(&e));
+  for (auto& e : c->ev_fast) CK(hipEventCreate(&e));
+  {
+    // level groups: [0,1) [1,2) [2,3) [3,n) by default (FAST work per level
+    // ~ 1 / 1.44^l of level 0's: the first three groups hold 69 % of it);
+    // ORBPL_LEVEL_PIPE=0: one pyramid launch and one FAST launch (no fstream)
+    const char* lp = getenv("ORBPL_LEVEL_PIPE");
+    const bool pipe = lp ? lp[0] != '0' : orbpl::hw_queues() >= 8;
+    const int nl = c->hg.g.nlevels;
+    c->ngroups = 0;
+    if (pipe) {
+      // ORBPL_LEVEL_GROUPS="1/2/3": the group ends (ascending, < nlevels;
+      // any non-digit separates them)
+      const char* ge = getenv("ORBPL_LEVEL_GROUPS");
+      const std::string spec = ge ? ge : "1/2/3";
+      for (size_t pos = 0; pos < spec.size() && c->ngroups < kMaxLevels - 1;) {
+        if (!isdigit((unsigned char)spec[pos])) {
+          pos++;
+          continue;
+        }
+        const int e = atoi(spec.c_str() + pos);
+        while (pos < spec.size() && isdigit((unsigned char)spec[pos])) pos++;
+        if (e > (c->ngroups ? c->group_end[c->ngroups - 1] : 0) && e < nl) c->group_end[c->ngroups++] = e;
+      }
+    }
+    c->group_end[c->ngroups++] = nl;
+    if (c->ngroups > 1) {
+      CK(hipStreamCreateWithFlags(&c->fstream, hipStreamNonBlocking));
+      for (int i = 0; i < c->ngroups; i++)
+        CK(hipEventCreateWithFlags(&c->ev_group[i], hipEventDisableTiming));
+      CK(hipEventCreateWithFlags(&c->ev_fjoin, hipEventDisableTiming));
+    }
+  }
   const size_t B = (size_t)max_batch;
   CK(hipMalloc(&c->d_geom, sizeof(OrbGeom)));
   CK(hipMalloc(&c->d_cells, sizeof(CellGeom) * std::max<size_t>(1, c->hg.cells.size())));
@@ -450,11 +503,12 @@ hipStream_t orbx_stream(orbx_ctx* c) { return c->stream; }
 // Whole extraction pipeline on the ctx stream; images already in device memory.
 int orbx_run(orbx_ctx* c, const uint8_t* d_imgs, int batch, int stride, long long frame_pitch,
              orbpl_keypoint_dev* d_kps, uint8_t* d_desc, int kp_pitch, int* d_n,
-             hipEvent_t* ext_events) {
+             hipEvent_t* ext_events, hipEvent_t* ext_fast) {
   const OrbGeom& g = c->hg.g;
   hipStream_t s = c->stream;
   c->timed = ext_events == nullptr;
   hipEvent_t* ev = ext_events ? ext_events : c->ev;
+  hipEvent_t* evf = ext_fast ? ext_fast : (ext_events ? nullptr : c->ev_fast);
   HIP_CHECK(hipEventRecord(ev[0], s));
   // row bands per frame: enough blocks for ~4 per CU (256 CUs), at most 8
   int nb = c->pyr_bands;
@@ -462,14 +516,40 @@ int orbx_run(orbx_ctx* c, const uint8_t* d_imgs, int batch, int stride, long lon
     nb = 1;
     while (nb < kPyrMaxBands && nb * batch < 1024) nb *= 2;
   }
-  launch_pyramid(g, c->d_geom, d_imgs, stride, frame_pitch, c->d_pyr, c->d_blur, c->d_rs,
-                 c->d_bands + pyr_band_base(nb), nb, batch, c->d_pyr_prof, s);
-  HIP_CHECK(hipEventRecord(ev[1], s));
-  // the blur is fused into k_pyramid: the blur stage interval stays empty
-  HIP_CHECK(hipEventRecord(ev[2], s));
-  launch_fast(g, c->d_geom, c->d_cells, c->d_pyr, c->d_cell_cands, c->d_cell_counts,
-              c->params.ini_th_fast, c->params.min_th_fast, batch, s);
-  HIP_CHECK(hipEventRecord(ev[3], s));
+  if (c->ngroups == 1) {
+    launch_pyramid(g, c->d_geom, d_imgs, stride, frame_pitch, c->d_pyr, c->d_blur, c->d_rs,
+                   c->d_bands + pyr_band_base(nb), nb, batch, c->d_pyr_prof, 0, g.nlevels, s);
+    HIP_CHECK(hipEventRecord(ev[1], s));
+    // the blur is fused into k_pyramid: the blur stage interval stays empty
+    HIP_CHECK(hipEventRecord(ev[2], s));
+    if (evf) HIP_CHECK(hipEventRecord(evf[0], s));
+    launch_fast(g, c->d_geom, c->d_cells, c->d_pyr, c->d_cell_cands, c->d_cell_counts,
+                c->params.ini_th_fast, c->params.min_th_fast, batch, 0, g.nlevels, s);
+    if (evf) HIP_CHECK(hipEventRecord(evf[1], s));
+    HIP_CHECK(hipEventRecord(ev[3], s));
+  } else {
+    // group gi's FAST (fstream) waits for the group's pyramid launch; the
+    // next group's pyramid launch reads only pyramid levels, which FAST
+    // does not write. The FAST outputs are read by the octree after the join.
+    int l0 = 0;
+    for (int gi = 0; gi < c->ngroups; gi++) {
+      const int l1 = c->group_end[gi];
+      launch_pyramid(g, c->d_geom, d_imgs, stride, frame_pitch, c->d_pyr, c->d_blur, c->d_rs,
+                     c->d_bands + pyr_band_base(nb), nb, batch, c->d_pyr_prof, l0, l1, s);
+      HIP_CHECK(hipEventRecord(c->ev_group[gi], s));
+      HIP_CHECK(hipStreamWaitEvent(c->fstream, c->ev_group[gi], 0));
+      if (gi == 0 && evf) HIP_CHECK(hipEventRecord(evf[0], c->fstream));
+      launch_fast(g, c->d_geom, c->d_cells, c->d_pyr, c->d_cell_cands, c->d_cell_counts,
+                  c->params.ini_th_fast, c->params.min_th_fast, batch, l0, l1, c->fstream);
+      l0 = l1;
+    }
+    HIP_CHECK(hipEventRecord(ev[1], s));
+    HIP_CHECK(hipEventRecord(ev[2], s));
+    if (evf) HIP_CHECK(hipEventRecord(evf[1], c->fstream));
+    HIP_CHECK(hipEventRecord(c->ev_fjoin, c->fstream));
+    HIP_CHECK(hipStreamWaitEvent(s, c->ev_fjoin, 0));
+    HIP_CHECK(hipEventRecord(ev[3], s));
+  }
   launch_octree(g, c->d_geom, c->d_cell_cands, c->d_cell_counts, c->d_kcand, c->d_knode,
                 c->d_kp_list, c->d_kp_count, c->d_err, batch, s);
   HIP_CHECK(hipEventRecord(ev[4], s));
@@ -631,6 +711,9 @@ int orbx_last_stage_ms(const orbx_ctx* c, float* ms5) {
   HIP_CHECK(hipSetDevice(c->device));
   HIP_CHECK(hipEventSynchronize(c->ev[5]));
   for (int i = 0; i < 5; i++) HIP_CHECK(hipEventElapsedTime(&ms5[i], c->ev[i], c->ev[i + 1]));
+  // FAST: the span of its launches (beside the pyramid's later levels when
+  // the level pipeline is on)
+  HIP_CHECK(hipEventElapsedTime(&ms5[2], c->ev_fast[0], c->ev_fast[1]));
   return ORBPL_OK;
 }
 

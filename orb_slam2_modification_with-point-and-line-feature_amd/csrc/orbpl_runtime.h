@@ -25,7 +25,10 @@ bool lsd_split_decision(int n_streams);
 bool once_per_device(const void* key);
 int orbx_run(orbx_ctx* c, const uint8_t* d_imgs, int batch, int stride, long long frame_pitch,
              orbpl_keypoint_dev* d_kps, uint8_t* d_desc, int kp_pitch, int* d_n,
-             hipEvent_t* ext_events = nullptr);
+             hipEvent_t* ext_events = nullptr, hipEvent_t* ext_fast = nullptr);
+// ext_events[0..5]: start, pyramid done, (empty blur stage), FAST joined,
+// octree done, orientation + descriptors done (on the ctx stream);
+// ext_fast[0..1]: the FAST launches' span (first start, last end)
 hipStream_t orbx_stream(orbx_ctx* c);
 struct OrbGeom;
 int orbx_device_pyramid(orbx_ctx* c, int frame, const uint8_t** base, const OrbGeom** geom,

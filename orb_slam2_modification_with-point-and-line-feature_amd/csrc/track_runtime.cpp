@@ -865,7 +865,7 @@ struct orbpl_tracker {
   StreamState* d_state = nullptr;
   PoseEdge* d_edges = nullptr;
   static constexpr int kRing = 64;   // steps kept in the timing ring
-  static constexpr int kEv = 36;     // events per step (28..35: kernel brackets)
+  static constexpr int kEv = 38;     // events per step (28..35: kernel brackets, 36..37: FAST span)
   std::vector<hipEvent_t> ring;      // kRing * kEv events
   int ring_pos = 0, ring_count = 0;
   // TrackLocalMap (ORBPL_TRACK_LOCAL_MAP): ring of the last kLmK keyframes'
@@ -1807,7 +1807,7 @@ static int tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_
     const int S1 = t->osplit, S2 = S - S1;
     const long long fp = (long long)t->W * t->H;
     rc = orbx_run(t->ex, d_gray, S1, t->W, fp, reinterpret_cast<orbpl_keypoint_dev*>(C.kps),
-                  C.desc, K, C.n, ev);
+                  C.desc, K, C.n, ev, ev + 36);
     if (rc) return rc;
     HIP_CHECK(hipStreamWaitEvent(t->stream2, ev[1], 0));
     rc = orbx_run(t->ex2, d_gray + (size_t)S1 * fp, S2, t->W, fp,
@@ -1818,7 +1818,7 @@ static int tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_
     HIP_CHECK(hipStreamWaitEvent(s, t->ev_ob_done, 0));
   } else {
     rc = orbx_run(t->ex, d_gray, S, t->W, (long long)t->W * t->H,
-                  reinterpret_cast<orbpl_keypoint_dev*>(C.kps), C.desc, K, C.n, ev);
+                  reinterpret_cast<orbpl_keypoint_dev*>(C.kps), C.desc, K, C.n, ev, ev + 36);
     if (rc) return rc;
   }
   launch_frame_prepare(t->consts, C.kps, C.n, K, t->stereo ? nullptr : d_depth,
@@ -2374,7 +2374,9 @@ int orbpl_tracker_timings(orbpl_tracker* t, int max_steps, float* ms, int* n_ste
   // match (incl. prediction), pose, finish (tracking stream)
   // (+ TrackLocalMap: gather, frustum, local matching, second pose, count)
   // (+ KeyFrame::ComputeBoW with a vocabulary; 0 without)
-  static const int kPair[kTimingStages][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 27},
+  // (FAST: the span of its launches on the extractor's FAST stream, which
+  // overlaps the pyramid's later levels under the level pipeline)
+  static const int kPair[kTimingStages][2] = {{0, 1}, {1, 2}, {36, 37}, {3, 4}, {4, 5}, {5, 27},
                                               {7, 8}, {14, 9}, {26, 10}, {9, 26}, {27, 6}};
   const int n = std::min(max_steps, t->ring_count);
   for (int k = 0; k < n; k++) {

@@ -10,7 +10,7 @@ for r in $(seq 1 ${2:-2}); do
   for it in ${1:-cur}; do
     v=${it%%:*}; e=""; [ "$it" != "$v" ] && e=${it#*:}
     L=""; [ "$v" != cur ] && L=variants/$v/liborbpl.so
-    tag=$(echo "$it" | tr ':=,' '___')
+    tag=$(echo "$it" | tr ':=,/' '____')
     env ORBPL_LIB=$L ${e//,/ } timeout -k 10 120 python tools/time_lsd.py 3072 > gpurun_out/abl/t_$tag.log 2>&1 || { echo "fail probe $it"; exit 1; }
     echo "$r $it probe $(head -1 gpurun_out/abl/t_$tag.log)"
     env ORBPL_LIB=$L ${e//,/ } timeout -k 10 300 python bench.py --workload lines --streams 3072 --steps 4 --warmup 1 $C > gpurun_out/abl/b_$tag.log 2>&1 || { echo "fail bench $it"; exit 1; }
