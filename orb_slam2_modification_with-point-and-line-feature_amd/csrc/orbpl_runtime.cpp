@@ -144,7 +144,7 @@ struct orbx_ctx {
   hipStream_t fstream = nullptr;
   hipEvent_t ev_group[kMaxLevels] = {};   // pyramid group g written (stream)
   hipEvent_t ev_fjoin = nullptr;          // every FAST launch done (fstream)
-  hipEvent_t ev_fast[2] = {};             // FAST span, own timing
+  hipEvent_t ev_fast[2 * kFastGroups] = {};   // FAST launch brackets, own timing
   int ngroups = 1;
   int group_end[kMaxLevels] = {};         // group g = levels [end[g-1], end[g])
   bool timed = false;
@@ -353,7 +353,7 @@ int orbx_create(const orbpl_orb_params* p, int width, int height, int max_batch,
       // any non-digit separates them)
       const char* ge = getenv("ORBPL_LEVEL_GROUPS");
       const std::string spec = ge ? ge : "1/2/3";
-      for (size_t pos = 0; pos < spec.size() && c->ngroups < kMaxLevels - 1;) {
+      for (size_t pos = 0; pos < spec.size() && c->ngroups < kFastGroups - 1;) {
         if (!isdigit((unsigned char)spec[pos])) {
           pos++;
           continue;
@@ -525,7 +525,8 @@ int orbx_run(orbx_ctx* c, const uint8_t* d_imgs, int batch, int stride, long lon
     if (evf) HIP_CHECK(hipEventRecord(evf[0], s));
     launch_fast(g, c->d_geom, c->d_cells, c->d_pyr, c->d_cell_cands, c->d_cell_counts,
                 c->params.ini_th_fast, c->params.min_th_fast, batch, 0, g.nlevels, s);
-    if (evf) HIP_CHECK(hipEventRecord(evf[1], s));
+    if (evf)
+      for (int k = 1; k < 2 * kFastGroups; k++) HIP_CHECK(hipEventRecord(evf[k], s));
     HIP_CHECK(hipEventRecord(ev[3], s));
   } else {
     // group gi's FAST (fstream) waits for the group's pyramid launch; the
@@ -538,14 +539,17 @@ int orbx_run(orbx_ctx* c, const uint8_t* d_imgs, int batch, int stride, long lon
                      c->d_bands + pyr_band_base(nb), nb, batch, c->d_pyr_prof, l0, l1, s);
       HIP_CHECK(hipEventRecord(c->ev_group[gi], s));
       HIP_CHECK(hipStreamWaitEvent(c->fstream, c->ev_group[gi], 0));
-      if (gi == 0 && evf) HIP_CHECK(hipEventRecord(evf[0], c->fstream));
+      if (evf) HIP_CHECK(hipEventRecord(evf[2 * gi], c->fstream));
       launch_fast(g, c->d_geom, c->d_cells, c->d_pyr, c->d_cell_cands, c->d_cell_counts,
                   c->params.ini_th_fast, c->params.min_th_fast, batch, l0, l1, c->fstream);
+      if (evf) HIP_CHECK(hipEventRecord(evf[2 * gi + 1], c->fstream));
       l0 = l1;
     }
+    if (evf)
+      for (int k = 2 * c->ngroups; k < 2 * kFastGroups; k++)
+        HIP_CHECK(hipEventRecord(evf[k], c->fstream));
     HIP_CHECK(hipEventRecord(ev[1], s));
     HIP_CHECK(hipEventRecord(ev[2], s));
-    if (evf) HIP_CHECK(hipEventRecord(evf[1], c->fstream));
     HIP_CHECK(hipEventRecord(c->ev_fjoin, c->fstream));
     HIP_CHECK(hipStreamWaitEvent(s, c->ev_fjoin, 0));
     HIP_CHECK(hipEventRecord(ev[3], s));
@@ -711,9 +715,14 @@ int orbx_last_stage_ms(const orbx_ctx* c, float* ms5) {
   HIP_CHECK(hipSetDevice(c->device));
   HIP_CHECK(hipEventSynchronize(c->ev[5]));
   for (int i = 0; i < 5; i++) HIP_CHECK(hipEventElapsedTime(&ms5[i], c->ev[i], c->ev[i + 1]));
-  // FAST: the span of its launches (beside the pyramid's later levels when
-  // the level pipeline is on)
-  HIP_CHECK(hipEventElapsedTime(&ms5[2], c->ev_fast[0], c->ev_fast[1]));
+  // FAST: the kernel time of its launches (beside the pyramid's later levels
+  // when the level pipeline is on), without the waits between them
+  ms5[2] = 0.f;
+  for (int k = 0; k < kFastGroups; k++) {
+    float m = 0.f;
+    HIP_CHECK(hipEventElapsedTime(&m, c->ev_fast[2 * k], c->ev_fast[2 * k + 1]));
+    ms5[2] += m;
+  }
   return ORBPL_OK;
 }
 

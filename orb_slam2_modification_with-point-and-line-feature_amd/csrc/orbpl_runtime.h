@@ -28,7 +28,10 @@ int orbx_run(orbx_ctx* c, const uint8_t* d_imgs, int batch, int stride, long lon
              hipEvent_t* ext_events = nullptr, hipEvent_t* ext_fast = nullptr);
 // ext_events[0..5]: start, pyramid done, (empty blur stage), FAST joined,
 // octree done, orientation + descriptors done (on the ctx stream);
-// ext_fast[0..1]: the FAST launches' span (first start, last end)
+// ext_fast[2 g], [2 g + 1]: FAST launch g bracketed on its stream (g <
+// kFastGroups; unused pairs are recorded back to back): the FAST stage time
+// is the sum of the pairs, its kernel time without the waits between groups
+constexpr int kFastGroups = 4;
 hipStream_t orbx_stream(orbx_ctx* c);
 struct OrbGeom;
 int orbx_device_pyramid(orbx_ctx* c, int frame, const uint8_t** base, const OrbGeom** geom,

@@ -3,7 +3,9 @@
 Reads gpurun_out/prof_<tag>/{trace,fetch,write}/ (rocprofv3 csv) and writes
 profiles/<round>/pmc_traffic.json:
   {kernel: {"launches", "avg_ns", "fetch_bytes", "write_bytes", "traffic_bytes"}}
-per launch, averaged over the launches of the profiled bench command.
+per launch, averaged over the launches of the profiled bench command (per
+extraction step for k_pyramid / k_fast_cells, which the level pipeline
+launches once per group of levels: "group_launches" per step).
 gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts half
 the bytes of wide coalesced reads, so fetch_bytes = 2 * FETCH_SIZE; WRITE_SIZE
 is taken as is. Both counters are in KiB.
@@ -39,25 +41,56 @@ def main():
     tag, rnd = sys.argv[1], sys.argv[2]
     base = ROOT / "gpurun_out" / f"prof_{tag}"
     out = {}
-    dur = collections.defaultdict(list)
-    for r in csv.DictReader(open(base / "trace" / "run_kernel_trace.csv")):
-        dur[short(r["Kernel_Name"])].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    # per kernel, its launches in dispatch order: (duration, grid threads)
+    launches = collections.defaultdict(list)
+    for r in sorted(csv.DictReader(open(base / "trace" / "run_kernel_trace.csv")),
+                    key=lambda r: int(r["Dispatch_Id"])):
+        grid = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+        launches[short(r["Kernel_Name"])].append(
+            (int(r["End_Timestamp"]) - int(r["Start_Timestamp"]), grid))
     cnt = {}
     for part in ("fetch", "write"):
         vals = collections.defaultdict(list)
-        for r in csv.DictReader(open(base / part / "run_counter_collection.csv")):
+        for r in sorted(csv.DictReader(open(base / part / "run_counter_collection.csv")),
+                        key=lambda r: int(r["Dispatch_Id"])):
             vals[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
         cnt[part] = vals
-    for k, v in dur.items():
+    for k, v in launches.items():
         if "rocclr" in k:
             continue
+        # the bench workload's launches only: the runs dispatch the same
+        # sequence, so the i-th launch of a kernel is the same in every pass;
+        # the one-frame launches of the vocabulary training before the timed
+        # region (grids ~1/1000 of the batch's) are left out
+        gmax = max(g for _, g in v)
+        keep = [i for i, (_, g) in enumerate(v) if g >= gmax // 10]
         f = cnt["fetch"].get(k, [])
         w = cnt["write"].get(k, [])
+        if len(f) == len(v):
+            f = [f[i] for i in keep]
+        if len(w) == len(v):
+            w = [w[i] for i in keep]
+        d = [v[i][0] for i in keep]
         fb = 2.0 * 1024.0 * sum(f) / len(f) if f else None
         wb = 1024.0 * sum(w) / len(w) if w else None
-        out[k] = {"launches": len(v), "avg_ns": sum(v) / len(v),
+        out[k] = {"launches": len(d), "avg_ns": sum(d) / len(d),
                   "fetch_bytes": fb, "write_bytes": wb,
                   "traffic_bytes": (fb + wb) if fb is not None and wb is not None else None}
+    dur = {k: [0] * out[k]["launches"] for k in out}
+    # the ORB level pipeline launches k_pyramid and k_fast_cells once per group
+    # of levels: their entries are per step (the sum over a step's group
+    # launches, "group_launches" of them), k_octree runs once per step
+    steps = len(dur.get("k_octree", [])) or 0
+    for k in ("k_pyramid", "k_fast_cells"):
+        e = out.get(k)
+        if e and steps and e["launches"] > steps and e["launches"] % steps == 0:
+            m = e["launches"] // steps
+            e["group_launches"] = m
+            e["launches"] = steps
+            e["avg_ns"] *= m
+            for q in ("fetch_bytes", "write_bytes", "traffic_bytes"):
+                if e[q] is not None:
+                    e[q] *= m
     wl = sys.argv[4] if len(sys.argv) > 4 else "points"
     streams = int(sys.argv[3]) if len(sys.argv) > 3 else 256
     of, lf = (int(x) for x in sys.argv[5].split(",")) if len(sys.argv) > 5 else (streams, streams)
