@@ -26,6 +26,9 @@ namespace orbpl {
 
 #include "orb_pattern.inc"
 __constant__ int c_pattern[1024];
+// the same 256 point pairs as floats (x1, y1, x2, y2): the ints are small,
+// so the conversion is exact and the steered coordinates bit-identical
+__constant__ float4 c_pattern_f[256];
 
 __device__ __forceinline__ int reflect101_dev(int p, int len) {
   // BORDER_REFLECT_101 for |p| < 2*len (always true for the 19 px border on
@@ -1252,6 +1255,41 @@ constexpr int kBriefLoads = (kBriefDw + 63) / 64;    // 6
 #ifndef ORBPL_OD_MINW
 #define ORBPL_OD_MINW 1
 #endif
+
+// IC_Angle (ORBextractor.cc:77-108) over one dword of a patch row: pixels
+// u0 .. u0+3 of row v; the bytes inside the disc |u| <= um (bytes bq in
+// [lo, hi)) masked, then *s0 += their sum and *s1 += their u-weighted sum
+// = u0 * sum + sum(bq * pixel), both sums by v_dot4_u32_u8. Integer sums:
+// the same m01 / m10 in any order. um < 0 (a lane past the patch) masks all.
+// a * b for operands that fit 16 bits: the zero / sign extensions let the
+// compiler pick the full-rate v_mul_u32_u24 / v_mul_i32_i24 instead of the
+// quarter-rate v_mul_lo_u32
+__device__ __forceinline__ uint32_t umul24(uint32_t a, uint32_t b) {
+  return (uint32_t)(uint16_t)a * (uint32_t)(uint16_t)b;
+}
+// i / D for i < 2^16 / D (D = 9, 10: exact below 32768 / 16384)
+template <uint32_t D>
+__device__ __forceinline__ uint32_t div_c16(uint32_t i) {
+  return umul24(i, (65536u + D - 1) / D) >> 16;
+}
+__device__ __forceinline__ int imul24(int a, int b) {
+  return (int)(int16_t)a * (int)(int16_t)b;
+}
+// dword `dw` of a wave-uniform base: the scalar-base + 32-bit vector-offset
+// load form, no 64-bit address arithmetic per lane
+__device__ __forceinline__ uint32_t ld_dw(const uint32_t* base, uint32_t dw) {
+  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(base) + (dw << 2));
+}
+__device__ __forceinline__ void ic_dword(uint32_t px, int u0, int um, int* s0, int* s1) {
+  const int lo = min(max(-um - u0, 0), 4), hi = min(max(um - u0 + 1, 0), 4);
+  // hi > lo: 1 .. 4 bytes, the right shift is at most 24
+  const uint32_t m = hi > lo ? (0xFFFFFFFFu >> (8 * (4 - (hi - lo)))) << (8 * lo) : 0u;
+  const uint32_t pm = px & m;
+  const int a = (int)__builtin_amdgcn_udot4(pm, 0x01010101u, 0u, false);
+  const int b = (int)__builtin_amdgcn_udot4(pm, 0x03020100u, 0u, false);
+  *s0 += a;
+  *s1 += imul24(u0, a) + b;   // |u0| <= 18, a <= 1020
+}
 __global__ void __launch_bounds__(256, ORBPL_OD_MINW) k_orient_desc(const uint8_t* __restrict__ pyr,
                                                      const uint8_t* __restrict__ blur,
                                                      const OrbGeom* __restrict__ g,
@@ -1454,49 +1492,42 @@ __global__ void __launch_bounds__(256, ORBPL_OD_MINW) k_orient_desc2(const uint8
   const uint32_t c = act ? kp_list[(long long)f * g->kp_cap_total + slot] : 0u;
   const int kx = act ? cand_x(c) + kMinBorder : kIcR + kBriefR,
             ky = act ? cand_y(c) + kMinBorder : kIcR + kBriefR;
-  // IC_Angle patch: rows ky-15 .. ky+15 as 9 aligned dwords each
-  const uint8_t* irow0 = pyr + (long long)f * g->pyr_bytes + content_off(L, kx - kIcR, ky - kIcR);
-  const int io = (int)(reinterpret_cast<uintptr_t>(irow0) & 3);
-  const uint32_t* irow = reinterpret_cast<const uint32_t*>(irow0 - io);
-  const int ipdw = L.pitch >> 2;
+  // IC_Angle patch: rows ky-15 .. ky+15 as 9 aligned dwords each, loaded as
+  // 32-bit dword offsets from the frame's (uniform) pyramid base
+  const uint32_t* fpyr = reinterpret_cast<const uint32_t*>(pyr + (long long)f * g->pyr_bytes);
+  const int ioff = (int)content_off(L, kx - kIcR, ky - kIcR);   // < 2^31 within a frame
+  const int io = ioff & 3;                                      // pyr_bytes % 256 == 0
+  const uint32_t ibase = (uint32_t)ioff >> 2;
+  const uint32_t ipdw = (uint32_t)L.pitch >> 2;
   uint32_t iv[kIcLoads2];
 #pragma unroll
   for (int j = 0; j < kIcLoads2; j++) {
-    const int i = l32 + 32 * j;
-    const int r = i / kIcRowDw, q = i - r * kIcRowDw;
-    iv[j] = (act && i < kIcDw) ? irow[r * ipdw + q] : 0u;
+    const uint32_t i = (uint32_t)l32 + 32u * j;
+    const uint32_t r = div_c16<kIcRowDw>(i), q = i - umul24(r, kIcRowDw);
+    iv[j] = (act && i < (uint32_t)kIcDw) ? ld_dw(fpyr, ibase + umul24(r, ipdw) + q) : 0u;
   }
   const int bx0 = kx - kBriefR;
-  const uint32_t* prow = reinterpret_cast<const uint32_t*>(
-      blur + (long long)f * g->blur_bytes + L.boff + (long long)(ky - kBriefR) * L.bpitch +
-      (bx0 & ~3));
-  const int pdw = L.bpitch >> 2;
+  const uint32_t* fblur = reinterpret_cast<const uint32_t*>(blur + (long long)f * g->blur_bytes);
+  const uint32_t pdw = (uint32_t)L.bpitch >> 2;
+  const uint32_t pbase =
+      (uint32_t)((L.boff + (long long)(ky - kBriefR) * L.bpitch + (bx0 & ~3)) >> 2);
   uint32_t pv[kBriefLoads2];
 #pragma unroll
   for (int j = 0; j < kBriefLoads2; j++) {
-    const int i = l32 + 32 * j;
-    const int r = i / kBriefRowDw, q = i - r * kBriefRowDw;
-    pv[j] = (act && i < kBriefDw) ? prow[r * pdw + q] : 0u;
+    const uint32_t i = (uint32_t)l32 + 32u * j;
+    const uint32_t r = div_c16<kBriefRowDw>(i), q = i - umul24(r, kBriefRowDw);
+    pv[j] = (act && i < (uint32_t)kBriefDw) ? ld_dw(fblur, pbase + umul24(r, pdw) + q) : 0u;
   }
   int m01 = 0, m10 = 0;
 #pragma unroll
   for (int j = 0; j < kIcLoads2; j++) {
     const int i = l32 + 32 * j;
-    const int r = i / kIcRowDw, q = i - r * kIcRowDw;
+    const int r = (int)div_c16<kIcRowDw>((uint32_t)i), q = i - (int)umul24((uint32_t)r, kIcRowDw);
     const int v = r - kIcR;
     const int um = i < kIcDw ? g->umax[v < 0 ? -v : v] : -1;
-    const int u0 = 4 * q - io - kIcR;
-    int s0 = 0, s1 = 0;
-#pragma unroll
-    for (int bq = 0; bq < 4; bq++) {
-      const int u = u0 + bq;
-      const int px = (int)((iv[j] >> (8 * bq)) & 0xFFu);
-      const int w = (u <= um && -u <= um) ? px : 0;
-      s0 += w;
-      s1 += u * w;
-    }
-    m10 += s1;
-    m01 += v * s0;
+    int s0 = 0;
+    ic_dword(iv[j], 4 * q - io - kIcR, um, &s0, &m10);
+    m01 += imul24(v, s0);   // |v| <= 15, s0 <= 1020
   }
 #pragma unroll
   for (int o = 16; o >= 1; o >>= 1) {   // within the half
@@ -1520,11 +1551,13 @@ __global__ void __launch_bounds__(256, ORBPL_OD_MINW) k_orient_desc2(const uint8
   uint32_t words[8];
 #pragma unroll
   for (int r = 0; r < 8; r++) {
-    const int tst = r * 32 + l32;
-    const int* p = &c_pattern[4 * tst];
-    const float x1 = (float)p[0], y1 = (float)p[1], x2 = (float)p[2], y2 = (float)p[3];
-    const int v1 = bimg[cv_round(x1 * b + y1 * a) * step + cv_round(x1 * a - y1 * b)];
-    const int v2 = bimg[cv_round(x2 * b + y2 * a) * step + cv_round(x2 * a - y2 * b)];
+    const float4 P = c_pattern_f[r * 32 + l32];
+    const float x1 = P.x, y1 = P.y, x2 = P.z, y2 = P.w;
+    // cvRound(y) * step + cvRound(x): the rounded values are integers below
+    // 2^5, so the float multiply-add is exact and one conversion remains
+    const float fs = (float)step;
+    const int v1 = bimg[(int)(__builtin_rintf(x1 * b + y1 * a) * fs + __builtin_rintf(x1 * a - y1 * b))];
+    const int v2 = bimg[(int)(__builtin_rintf(x2 * b + y2 * a) * fs + __builtin_rintf(x2 * a - y2 * b))];
     words[r] = (uint32_t)(__ballot(v1 < v2) >> (32 * half));
   }
   if (!act) return;
@@ -1557,8 +1590,16 @@ __global__ void __launch_bounds__(256, ORBPL_OD_MINW) k_orient_desc2(const uint8
 // Host-side launchers (called by the runtime in orbpl_runtime.cpp)
 // ---------------------------------------------------------------------------
 hipError_t upload_pattern(hipStream_t s) {
-  return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_pattern), bit_pattern_31_, sizeof(bit_pattern_31_), 0,
-                                hipMemcpyHostToDevice, s);
+  static float pf[1024];
+  static const bool filled = [] {
+    for (int i = 0; i < 1024; i++) pf[i] = (float)bit_pattern_31_[i];
+    return true;
+  }();
+  (void)filled;
+  const hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(c_pattern), bit_pattern_31_,
+                                              sizeof(bit_pattern_31_), 0, hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) return e;
+  return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_pattern_f), pf, sizeof(pf), 0, hipMemcpyHostToDevice, s);
 }
 
 
