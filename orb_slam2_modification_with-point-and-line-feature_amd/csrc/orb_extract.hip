@@ -72,6 +72,43 @@ __host__ __device__ constexpr int fast_wave_words(int win_w, int win_h) {
 typedef short fshort2 __attribute__((ext_vector_type(2)));
 typedef unsigned short fushort2 __attribute__((ext_vector_type(2)));
 
+// Integer and address helpers for the per-lane index arithmetic.
+// a * b for operands that fit 16 bits: the zero / sign extensions let the
+// compiler pick the full-rate v_mul_u32_u24 / v_mul_i32_i24 instead of the
+// quarter-rate v_mul_lo_u32
+__device__ __forceinline__ uint32_t umul24(uint32_t a, uint32_t b) {
+  return (uint32_t)(uint16_t)a * (uint32_t)(uint16_t)b;
+}
+// i / D for i < 2^16 / D (D = 9, 10: exact below 32768 / 16384)
+template <uint32_t D>
+__device__ __forceinline__ uint32_t div_c16(uint32_t i) {
+  return umul24(i, (65536u + D - 1) / D) >> 16;
+}
+__device__ __forceinline__ int imul24(int a, int b) {
+  return (int)(int16_t)a * (int)(int16_t)b;
+}
+// dword `dw` of a wave-uniform base: the scalar-base + 32-bit vector-offset
+// load form, no 64-bit address arithmetic per lane
+__device__ __forceinline__ uint32_t ld_dw(const uint32_t* base, uint32_t dw) {
+  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(base) + (dw << 2));
+}
+// dwords dw, dw + 1, dw + 2 of a wave-uniform base: one 32-bit offset and
+// immediate offsets, so the three loads merge into one dwordx3
+__device__ __forceinline__ void ld_dw3(const uint32_t* base, uint32_t dw, uint32_t* a, uint32_t* b,
+                                       uint32_t* c) {
+  const char* p = reinterpret_cast<const char*>(base) + (dw << 2);
+  *a = *reinterpret_cast<const uint32_t*>(p);
+  *b = *reinterpret_cast<const uint32_t*>(p + 4);
+  *c = *reinterpret_cast<const uint32_t*>(p + 8);
+}
+// byte `off` of a wave-uniform base as a dword / for a dword store (same form)
+__device__ __forceinline__ uint32_t ld_b4(const uint8_t* base, uint32_t off) {
+  return *reinterpret_cast<const uint32_t*>(base + off);
+}
+__device__ __forceinline__ void st_b4(uint8_t* base, uint32_t off, uint32_t v) {
+  *reinterpret_cast<uint32_t*>(base + off) = v;
+}
+
 __device__ __forceinline__ fshort2 as_s2(uint32_t v) { return __builtin_bit_cast(fshort2, v); }
 __device__ __forceinline__ fushort2 as_u2(uint32_t v) { return __builtin_bit_cast(fushort2, v); }
 __device__ __forceinline__ fshort2 pmin(fshort2 a, fshort2 b) { return __builtin_elementwise_min(a, b); }
@@ -325,7 +362,11 @@ __device__ __forceinline__ void pyr_resize_rows(const LevelGeom& L, const LevelG
   const int groups = (L.w + 3) >> 2;
   int nseg, rps;
   walk_split(groups, nb - na, 2, &nseg, &rps);
+  // source dwords and destination bytes as 32-bit offsets from the block's
+  // (uniform) level bases
   const uint32_t* src0w = reinterpret_cast<const uint32_t*>(fp + content_off(S, 0, 0));
+  const uint32_t spdw = (uint32_t)S.pitch >> 2;
+  uint8_t* dst0 = fp + content_off(L, 0, 0);
   for (int task = threadIdx.x; task < groups * nseg; task += kPyrThreads) {
     const int seg = task / groups, gq = task - seg * groups;
     const int ra = na + seg * rps, rb = min(ra + rps, nb);
@@ -360,13 +401,10 @@ __device__ __forceinline__ void pyr_resize_rows(const LevelGeom& L, const LevelG
         const int sy0 = yofs[yy];
         bq[j] = beta[yy];
         // uniform base + 32-bit per-lane dword offsets (saddr loads)
-        const int q0 = min(max(sy0, 0), S.h - 1) * (S.pitch >> 2) + d0;
-        const int q1 = min(max(sy0 + 1, 0), S.h - 1) * (S.pitch >> 2) + d0;
-#pragma unroll
-        for (int e = 0; e < 3; e++) {
-          u[j][e] = src0w[q0 + e];
-          v[j][e] = src0w[q1 + e];
-        }
+        const uint32_t q0 = umul24((uint32_t)min(max(sy0, 0), S.h - 1), spdw) + (uint32_t)d0;
+        const uint32_t q1 = umul24((uint32_t)min(max(sy0 + 1, 0), S.h - 1), spdw) + (uint32_t)d0;
+        ld_dw3(src0w, q0, &u[j][0], &u[j][1], &u[j][2]);
+        ld_dw3(src0w, q1, &v[j][0], &v[j][1], &v[j][2]);
       }
 #pragma unroll
       for (int j = 0; j < kPyrRsDepth; j++) {
@@ -382,15 +420,16 @@ __device__ __forceinline__ void pyr_resize_rows(const LevelGeom& L, const LevelG
                                      : __builtin_amdgcn_perm(v[j][1], v[j][0], sel[k]);
           const int h0 = (int)__builtin_amdgcn_udot2(as_u2(tu), cf[k], 0u, false);
           const int h1 = (int)__builtin_amdgcn_udot2(as_u2(tv), cf[k], 0u, false);
-          const uint32_t o =
-              (uint32_t)((((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2);
+          // beta <= 2048, h >> 4 < 2^16: 24-bit products (v_mul_u32_u24)
+          const uint32_t o = (uint32_t)((((int)umul24((uint32_t)b0, (uint32_t)(h0 >> 4)) >> 16) +
+                                         ((int)umul24((uint32_t)b1, (uint32_t)(h1 >> 4)) >> 16) + 2) >> 2);
           packed |= o << (8 * k);
         }
-        uint8_t* dst = fp + content_off(L, x, y + j);
+        const uint32_t doff = umul24((uint32_t)(y + j), (uint32_t)L.pitch) + (uint32_t)x;
         if (x + 4 <= L.w) {
-          *reinterpret_cast<uint32_t*>(dst) = packed;
+          st_b4(dst0, doff, packed);
         } else {  // last partial group: the border bytes belong to step 2
-          for (int k = 0; k < L.w - x; k++) dst[k] = (uint8_t)(packed >> (8 * k));
+          for (int k = 0; k < L.w - x; k++) dst0[doff + k] = (uint8_t)(packed >> (8 * k));
         }
       }
     }
@@ -469,24 +508,25 @@ __device__ __forceinline__ void pyr_blur_rows(const LevelGeom& L, const uint8_t*
     // padded row py holds content column x-4 at byte kContent0 - 4 + x
     // uniform base + 32-bit per-lane offsets (saddr loads: one VGPR per row)
     const uint32_t* col = reinterpret_cast<const uint32_t*>(fp + L.pyr_off);
-    const int c0 = (kContent0 - 4) / 4 + gq;
-    const int pw = L.pitch >> 2;
+    const uint32_t c0 = (uint32_t)((kContent0 - 4) / 4 + gq);
+    const uint32_t pw = (uint32_t)L.pitch >> 2;
     uint2 h[7];
 #pragma unroll
     for (int v = 0; v < 6; v++) {
-      const int q = (ra - 3 + v + kEdge) * pw + c0;
-      h[v + 1] = blur_h4(col[q], col[q + 1], col[q + 2]);
+      const uint32_t q = umul24((uint32_t)(ra - 3 + v + kEdge), pw) + c0;
+      uint32_t a0, a1, a2;
+      ld_dw3(col, q, &a0, &a1, &a2);
+      h[v + 1] = blur_h4(a0, a1, a2);
     }
-    uint8_t* out = bp + L.boff + 4 * gq;
+    uint8_t* out = bp + L.boff;                 // uniform; the lane's column 4 gq
+    const uint32_t ocol = 4u * (uint32_t)gq;
     // kPyrDepth rows per iteration: the source dwords are loaded before any is used
     for (int y = ra; y < rb; y += kPyrDepth) {
       uint32_t w[kPyrDepth][3];
 #pragma unroll
       for (int j = 0; j < kPyrDepth; j++) {
-        const int q = (min(y + j, rb - 1) + 3 + kEdge) * pw + c0;
-        w[j][0] = col[q];
-        w[j][1] = col[q + 1];
-        w[j][2] = col[q + 2];
+        const uint32_t q = umul24((uint32_t)(min(y + j, rb - 1) + 3 + kEdge), pw) + c0;
+        ld_dw3(col, q, &w[j][0], &w[j][1], &w[j][2]);
       }
 #pragma unroll
       for (int j = 0; j < kPyrDepth; j++) {
@@ -495,7 +535,7 @@ __device__ __forceinline__ void pyr_blur_rows(const LevelGeom& L, const uint8_t*
         for (int v = 0; v < 6; v++) h[v] = h[v + 1];
         h[6] = blur_h4(w[j][0], w[j][1], w[j][2]);
         const uint32_t o = blur_v4(h);
-        *reinterpret_cast<uint32_t*>(out + (long long)(y + j) * L.bpitch) = o;
+        st_b4(out, umul24((uint32_t)(y + j), (uint32_t)L.bpitch) + ocol, o);
       }
     }
   }
@@ -1261,25 +1301,6 @@ constexpr int kBriefLoads = (kBriefDw + 63) / 64;    // 6
 // [lo, hi)) masked, then *s0 += their sum and *s1 += their u-weighted sum
 // = u0 * sum + sum(bq * pixel), both sums by v_dot4_u32_u8. Integer sums:
 // the same m01 / m10 in any order. um < 0 (a lane past the patch) masks all.
-// a * b for operands that fit 16 bits: the zero / sign extensions let the
-// compiler pick the full-rate v_mul_u32_u24 / v_mul_i32_i24 instead of the
-// quarter-rate v_mul_lo_u32
-__device__ __forceinline__ uint32_t umul24(uint32_t a, uint32_t b) {
-  return (uint32_t)(uint16_t)a * (uint32_t)(uint16_t)b;
-}
-// i / D for i < 2^16 / D (D = 9, 10: exact below 32768 / 16384)
-template <uint32_t D>
-__device__ __forceinline__ uint32_t div_c16(uint32_t i) {
-  return umul24(i, (65536u + D - 1) / D) >> 16;
-}
-__device__ __forceinline__ int imul24(int a, int b) {
-  return (int)(int16_t)a * (int)(int16_t)b;
-}
-// dword `dw` of a wave-uniform base: the scalar-base + 32-bit vector-offset
-// load form, no 64-bit address arithmetic per lane
-__device__ __forceinline__ uint32_t ld_dw(const uint32_t* base, uint32_t dw) {
-  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(base) + (dw << 2));
-}
 __device__ __forceinline__ void ic_dword(uint32_t px, int u0, int um, int* s0, int* s1) {
   const int lo = min(max(-um - u0, 0), 4), hi = min(max(um - u0 + 1, 0), 4);
   // hi > lo: 1 .. 4 bytes, the right shift is at most 24
