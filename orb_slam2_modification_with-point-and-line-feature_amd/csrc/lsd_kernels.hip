@@ -163,6 +163,19 @@ __global__ void __launch_bounds__(256) k_lsd_grad(LsdGeom g, const uint8_t* __re
   }
 }
 
+// element e of a wave-uniform array by a 32-bit byte offset (the scalar-base
+// + vector-offset addressing form; e * sizeof(T) < 2^32 for every array here)
+template <class T>
+__device__ __forceinline__ T& ix(T* base, int e) {
+  return *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + (uint32_t)e * (uint32_t)sizeof(T));
+}
+
+// a * b for operands that fit 16 bits (full-rate v_mul_u32_u24, not the
+// quarter-rate v_mul_lo_u32)
+__device__ __forceinline__ uint32_t umul16(uint32_t a, uint32_t b) {
+  return (uint32_t)(uint16_t)a * (uint32_t)(uint16_t)b;
+}
+
 // ---------------------------------------------------------------------------
 // k_lsd_prep: k_lsd_blur + k_lsd_resize + k_lsd_grad fused per tile of the
 // scaled image (the same integer arithmetic, in the same order): the block's
@@ -229,47 +242,55 @@ __global__ void __launch_bounds__(256) k_lsd_prep(LsdGeom g, const int* __restri
   __syncthreads();
   const int sx0 = s_span[0], sy0 = s_span[2];
   const int ncol = s_span[1] - sx0 + 1, nrow = s_span[3] - sy0 + 1;
-  // the source span with the blur halo (REFLECT_101 as k_lsd_blur)
+  // the source span with the blur halo (REFLECT_101 as k_lsd_blur). The
+  // passes below map a thread to column t % 128 and rows t / 128 + 2k (every
+  // span is at most kPrSC + 2 kPrR < 128 wide): no division per element, and
+  // 32-bit offsets from the frame's (uniform) base
+  static_assert(kPrSC + 2 * kPrR <= 128 && kPrTW + 1 <= 128, "prep column mapping");
   const uint8_t* src = img + (long long)f * frame_pitch;
   const int icols = ncol + 2 * kPrR, irows = nrow + 2 * kPrR;
-  for (int i = t; i < irows * icols; i += 256) {
-    const int r = i / icols, c = i - r * icols;
-    s_in[r][c] = src[(long long)refl101(sy0 + r - kPrR, H) * stride + refl101(sx0 + c - kPrR, W)];
+  const int tc = t & 127, tr = t >> 7;
+  if (tc < icols) {
+    const uint32_t sc = (uint32_t)refl101(sx0 + tc - kPrR, W);
+    for (int r = tr; r < irows; r += 2)
+      s_in[r][tc] = src[umul16((uint32_t)refl101(sy0 + r - kPrR, H), (uint32_t)stride) + sc];
   }
   __syncthreads();
-  for (int i = t; i < irows * ncol; i += 256) {
-    const int r = i / ncol, c = i - r * ncol;
-    int acc = 0;
+  if (tc < ncol)
+    for (int r = tr; r < irows; r += 2) {
+      uint32_t acc = 0;
 #pragma unroll
-    for (int j = 0; j < 2 * kPrR + 1; j++) acc += g.gk[j] * s_in[r][c + j];
-    s_h[r][c] = (uint16_t)acc;
-  }
+      for (int j = 0; j < 2 * kPrR + 1; j++) acc += umul16((uint32_t)g.gk[j], s_in[r][tc + j]);
+      s_h[r][tc] = (uint16_t)acc;
+    }
   __syncthreads();
-  for (int i = t; i < nrow * ncol; i += 256) {
-    const int r = i / ncol, c = i - r * ncol;
-    int acc = 0;
+  if (tc < ncol)
+    for (int r = tr; r < nrow; r += 2) {
+      int acc = 0;
 #pragma unroll
-    for (int j = 0; j < 2 * kPrR + 1; j++) acc += g.gk[j] * (int)s_h[r + j][c];
-    s_b[r][c] = (uint8_t)min(255, (acc + (1 << 15)) >> 16);
-  }
+      for (int j = 0; j < 2 * kPrR + 1; j++) acc += (int)umul16((uint32_t)g.gk[j], s_h[r + j][tc]);
+      s_b[r][tc] = (uint8_t)min(255, (acc + (1 << 15)) >> 16);
+    }
   __syncthreads();
   // resize (k_lsd_resize's arithmetic) of the scaled tile incl. the +1 halo
-  for (int i = t; i < ny * nx; i += 256) {
-    const int r = i / nx, c = i - r * nx;
+  for (int r = tr; tc < nx && r < ny; r += 2) {
+    const int c = tc;
     const int dx = x0 + c, dy = y0 + r;
     auto hval = [&](int sy) -> int {
       const uint8_t* row = s_b[sy - sy0];
       if (dx < g.rx0) return row[0 - sx0] << 8;
       if (dx >= g.rx1) return row[xlast - sx0] << 8;
       const int c1 = s_xc[c], o = s_xo[c] - sx0;
-      return (256 - c1) * row[o] + c1 * row[o + 1];
+      // coefficients <= 256, pixels <= 255: 16-bit operands
+      return (int)(umul16((uint32_t)(256 - c1), row[o]) + umul16((uint32_t)c1, row[o + 1]));
     };
     int v;
     if (dy < g.ry0 || dy >= g.ry1) {
       v = (hval(dy < g.ry0 ? 0 : H - 1) + 0x80) >> 8;
     } else {
       const int b1 = s_yc[r], b0 = 256 - b1, oy = s_yo[r];
-      v = (hval(oy) * b0 + hval(oy + 1) * b1 + 0x8000) >> 16;
+      v = (int)((umul16((uint32_t)hval(oy), (uint32_t)b0) + umul16((uint32_t)hval(oy + 1), (uint32_t)b1) +
+                 0x8000u) >> 16);
     }
     s_s[r][c] = (uint8_t)min(255, v);
   }
@@ -277,17 +298,19 @@ __global__ void __launch_bounds__(256) k_lsd_prep(LsdGeom g, const int* __restri
   // the scaled image and ll_angle (k_lsd_grad's arithmetic) of the core tile
   unsigned mq = 0;
   const int tw = lsd_sd_tw(sw);
-  const long long fo = (long long)f * sw * sh;
   const int dtw = lsd_deg_tw(sw);
-  const long long dfo = (long long)f * lsd_deg_words(sw, sh);
+  // the frame's planes (uniform bases) and 32-bit element offsets
+  uint8_t* fscaled = scaled + (long long)f * sw * sh;
+  int* fq = q + (long long)f * sw * sh;
+  float* fdeg = deg + (long long)f * lsd_deg_words(sw, sh);
   uint64_t* fsd = sd + (long long)f * lsd_sd_frame_words(sw, sh);
-  const long long csw = lsd_cs_offset(sw, sh);
+  const int csw = (int)lsd_cs_offset(sw, sh);
   for (int i = t; i < kPrTH * kPrTW; i += 256) {
     const int r = i / kPrTW, c = i - r * kPrTW;
     const int x = x0 + c, y = y0 + r;
     if (x >= sw || y >= sh) continue;
-    const long long o = fo + (long long)y * sw + x;
-    scaled[o] = s_s[r][c];
+    const int o = (int)umul16((uint32_t)y, (uint32_t)sw) + x;
+    ix(fscaled, o) = s_s[r][c];
     float d = kLsdNotdef;
     int qq = 0;
     if (x < sw - 1 && y < sh - 1) {
@@ -301,11 +324,11 @@ __global__ void __launch_bounds__(256) k_lsd_prep(LsdGeom g, const int* __restri
         mq = max(mq, (unsigned)qq);
       }
     }
-    deg[dfo + lsd_deg_index(x, y, dtw)] = d;
-    q[o] = qq;
+    ix(fdeg, lsd_deg_index(x, y, dtw)) = d;
+    ix(fq, o) = qq;
     const int si = lsd_sd_index(x, y, tw);
-    fsd[si] = (0xFFFFFFFFull << 32) | (uint64_t)__float_as_uint(d);
-    fsd[csw + si] = lsd_angle_terms(d);
+    ix(fsd, si) = (0xFFFFFFFFull << 32) | (uint64_t)__float_as_uint(d);
+    ix(fsd, csw + si) = lsd_angle_terms(d);
   }
   unsigned m = mq;
   for (int o = 32; o >= 1; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o, 64));
@@ -592,7 +615,7 @@ __device__ __forceinline__ void sort_core(const SortPtrs& P, int first0, int las
         const int i = b + j * 64 + lane;
         bool fl = false, fr = false;
         if (i < e) {
-          const int k = skey(A[i]);
+          const int k = skey(ix(A, i));
           fl = i > first && k <= p;
           fr = k >= p;
         }
@@ -625,7 +648,7 @@ __device__ __forceinline__ void sort_core(const SortPtrs& P, int first0, int las
         const int i = b + j * 64 + lane;
         bool fl = false, fr = false;
         if (i < e) {
-          const int k = skey(A[i]);
+          const int k = skey(ix(A, i));
           fl = i > first && k <= p;
           fr = k >= p;
         }
@@ -639,14 +662,14 @@ __device__ __forceinline__ void sort_core(const SortPtrs& P, int first0, int las
         const int i = b + j * 64 + lane;
         if ((mR[j] >> lane) & 1ull) {
           const int k = sufR + __popcll(mR[j] & ~(below | (1ull << lane)));
-          P.Rpos[first + k] = i;
+          ix(P.Rpos, first + k) = i;
         }
         sufR += __popcll(mR[j]);
       }
 #pragma unroll
       for (int j = 0; j < CH / 64; j++) {
         const int i = b + j * 64 + lane;
-        if ((mL[j] >> lane) & 1ull) P.Lpos[first + runL + __popcll(mL[j] & below)] = i;
+        if ((mL[j] >> lane) & 1ull) ix(P.Lpos, first + runL + __popcll(mL[j] & below)) = i;
         runL += __popcll(mL[j]);
       }
     }
@@ -661,7 +684,7 @@ __device__ __forceinline__ void sort_core(const SortPtrs& P, int first0, int las
       int lo = 0, hi = min(nL, nR);
       while (lo < hi) {
         const int m = (lo + hi) >> 1;
-        if (P.Lpos[first + m] < P.Rpos[first + m]) lo = m + 1;
+        if (ix(P.Lpos, first + m) < ix(P.Rpos, first + m)) lo = m + 1;
         else hi = m;
       }
       const int K = lo;
@@ -680,10 +703,10 @@ __device__ __forceinline__ void sort_core(const SortPtrs& P, int first0, int las
       const int kb = Lpre[ch] - Lpre[sq.w];
       const int ke = min(kb + Lc[ch], sK[s]);
       for (int k = kb + lane; k < ke; k += 64) {
-        const int i = P.Lpos[first + k], j = P.Rpos[first + k];
-        const uint32_t a = A[i], bb = A[j];
-        A[i] = bb;
-        A[j] = a;
+        const int i = ix(P.Lpos, first + k), j = ix(P.Rpos, first + k);
+        const uint32_t a = ix(A, i), bb = ix(A, j);
+        ix(A, i) = bb;
+        ix(A, j) = a;
       }
     }
     __syncthreads();
