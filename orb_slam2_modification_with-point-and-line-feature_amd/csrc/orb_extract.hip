@@ -996,10 +996,10 @@ __global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
                                                 int* __restrict__ knode,
                                                 uint32_t* __restrict__ kp_list,
                                                 int* __restrict__ kp_count,
-                                                int* __restrict__ err_flag) {
+                                                int* __restrict__ err_flag, int l0) {
   extern __shared__ char smem_raw[];
   OctShared<kCap>& S = *reinterpret_cast<OctShared<kCap>*>(smem_raw);
-  const int level = blockIdx.x, f = blockIdx.y, t = threadIdx.x;
+  const int level = l0 + blockIdx.x, f = blockIdx.y, t = threadIdx.x;   // levels l0 ..
   const LevelGeom& L = g->lv[level];
   const int N = L.nfeat;
   const bool stamp = g_oct_prof_on && f == 0 && t == 0;
@@ -1318,13 +1318,14 @@ __global__ void __launch_bounds__(256, ORBPL_OD_MINW) k_orient_desc(const uint8_
                                                      const int* __restrict__ kp_count,
                                                      orbpl_keypoint_dev* __restrict__ out_kps,
                                                      uint8_t* __restrict__ out_desc,
-                                                     int kp_pitch, int* __restrict__ out_n) {
+                                                     int kp_pitch, int* __restrict__ out_n,
+                                                      int slot0, int slot1, int write_n) {
   __shared__ uint32_t s_patch[4][kBriefDw];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int bx, f;
   xcd_block(&bx, &f);
-  const int slot = bx * 4 + wave;
-  if (slot >= g->kp_cap_total) return;
+  const int slot = slot0 + bx * 4 + wave;   // slots [slot0, slot1): one group of levels
+  if (slot >= slot1) return;
   const bool stamp = g_oct_prof_on && f == 0 && slot == 0 && lane == 0;
   long long dt[6] = {0, 0, 0, 0, 0, 0};
   long long d0 = stamp ? (long long)wall_clock64() : 0;
@@ -1346,7 +1347,9 @@ __global__ void __launch_bounds__(256, ORBPL_OD_MINW) k_orient_desc(const uint8_
     if (l < level) offset += c;
     total += c;
   }
-  if (slot == 0 && lane == 0) out_n[f] = total < kp_pitch ? total : kp_pitch;
+  // the frame's keypoint count, by the launch of the last level group (all
+  // levels' octrees are done by then)
+  if (write_n && slot == slot0 && lane == 0) out_n[f] = total < kp_pitch ? total : kp_pitch;
   if (idx >= cnts[level]) return;
   const int opos = offset + idx;
   if (opos >= kp_pitch) return;
@@ -1484,15 +1487,16 @@ __global__ void __launch_bounds__(256, ORBPL_OD_MINW) k_orient_desc2(const uint8
                                                       const int* __restrict__ kp_count,
                                                       orbpl_keypoint_dev* __restrict__ out_kps,
                                                       uint8_t* __restrict__ out_desc,
-                                                      int kp_pitch, int* __restrict__ out_n) {
+                                                      int kp_pitch, int* __restrict__ out_n,
+                                                      int slot0, int slot1, int write_n) {
   __shared__ uint32_t s_patch[8][kBriefDw];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int half = lane >> 5, l32 = lane & 31;
   int bx, f;
   xcd_block(&bx, &f);
-  const int slot = bx * 8 + wave * 2 + half;
+  const int slot = slot0 + bx * 8 + wave * 2 + half;   // slots [slot0, slot1)
   const int nlev = g->nlevels;
-  bool act = slot < g->kp_cap_total;
+  bool act = slot < slot1;
   int level = 0;
   if (act)
     while (level + 1 < nlev && slot >= g->lv[level + 1].kp_base) level++;
@@ -1506,7 +1510,7 @@ __global__ void __launch_bounds__(256, ORBPL_OD_MINW) k_orient_desc2(const uint8
     if (l == level) mine = c;
     total += c;
   }
-  if (slot == 0 && l32 == 0) out_n[f] = total < kp_pitch ? total : kp_pitch;
+  if (write_n && slot == slot0 && l32 == 0) out_n[f] = total < kp_pitch ? total : kp_pitch;
   act = act && idx < mine && offset + idx < kp_pitch;
   if (!__any(act)) return;
   const int opos = offset + idx;
@@ -1654,7 +1658,7 @@ void launch_fast(const OrbGeom& hg, const OrbGeom* dg, const CellGeom* cells, co
 
 void launch_octree(const OrbGeom& hg, const OrbGeom* dg, const uint32_t* cell_cands,
                    const int* cell_counts, uint32_t* kcand, int* knode, uint32_t* kp_list,
-                   int* kp_count, int* err_flag, int batch, hipStream_t s) {
+                   int* kp_count, int* err_flag, int batch, int l0, int l1, hipStream_t s) {
   set_smem_attr((const void*)k_octree<1024>, sizeof(OctShared<1024>));
   int cap = 0;
   for (int l = 0; l < hg.nlevels; l++) cap = std::max(cap, hg.lv[l].kp_cap);
@@ -1664,32 +1668,38 @@ void launch_octree(const OrbGeom& hg, const OrbGeom* dg, const uint32_t* cell_ca
                                  hipMemcpyHostToDevice, s);
   }
   if (cap <= 256)
-    hipLaunchKernelGGL(k_octree<256>, dim3(hg.nlevels, batch), dim3(256),
+    hipLaunchKernelGGL(k_octree<256>, dim3(l1 - l0, batch), dim3(256),
                        sizeof(OctShared<256>), s, dg, cell_cands, cell_counts, kcand, knode,
-                       kp_list, kp_count, err_flag);
+                       kp_list, kp_count, err_flag, l0);
   else if (cap <= 512)
-    hipLaunchKernelGGL(k_octree<512>, dim3(hg.nlevels, batch), dim3(256),
+    hipLaunchKernelGGL(k_octree<512>, dim3(l1 - l0, batch), dim3(256),
                        sizeof(OctShared<512>), s, dg, cell_cands, cell_counts, kcand, knode,
-                       kp_list, kp_count, err_flag);
+                       kp_list, kp_count, err_flag, l0);
   else
-    hipLaunchKernelGGL(k_octree<1024>, dim3(hg.nlevels, batch), dim3(256),
+    hipLaunchKernelGGL(k_octree<1024>, dim3(l1 - l0, batch), dim3(256),
                        sizeof(OctShared<1024>), s, dg, cell_cands, cell_counts, kcand, knode,
-                       kp_list, kp_count, err_flag);
+                       kp_list, kp_count, err_flag, l0);
 }
 
 void launch_orient_desc(const OrbGeom& hg, const OrbGeom* dg, const uint8_t* pyr,
                         const uint8_t* blur, const uint32_t* kp_list, const int* kp_count,
                         orbpl_keypoint_dev* out_kps, uint8_t* out_desc, int kp_pitch, int* out_n,
-                        int batch, hipStream_t s) {
+                        int batch, int l0, int l1, hipStream_t s) {
+  // keypoint slots of levels [l0, l1); the launch of the last level writes
+  // the frames' keypoint counts
+  const int s0 = hg.lv[l0].kp_base;
+  const int s1 = l1 < hg.nlevels ? hg.lv[l1].kp_base : hg.kp_cap_total;
+  const int wn = l1 == hg.nlevels ? 1 : 0;
+  if (s1 <= s0) return;
   static const char* pe = getenv("ORBPL_OD_PAIR");
   // the phase-stamp profile (ORBPL_OCT_PROFILE) lives in the one-per-wave kernel
   static const bool pair = (pe ? atoi(pe) != 0 : ORBPL_OD_PAIR) && !getenv("ORBPL_OCT_PROFILE");
   if (pair)
-    hipLaunchKernelGGL(k_orient_desc2, dim3((hg.kp_cap_total + 7) / 8, batch), dim3(256), 0, s,
-                       pyr, blur, dg, kp_list, kp_count, out_kps, out_desc, kp_pitch, out_n);
+    hipLaunchKernelGGL(k_orient_desc2, dim3((s1 - s0 + 7) / 8, batch), dim3(256), 0, s, pyr, blur,
+                       dg, kp_list, kp_count, out_kps, out_desc, kp_pitch, out_n, s0, s1, wn);
   else
-    hipLaunchKernelGGL(k_orient_desc, dim3((hg.kp_cap_total + 3) / 4, batch), dim3(256), 0, s, pyr,
-                       blur, dg, kp_list, kp_count, out_kps, out_desc, kp_pitch, out_n);
+    hipLaunchKernelGGL(k_orient_desc, dim3((s1 - s0 + 3) / 4, batch), dim3(256), 0, s, pyr, blur,
+                       dg, kp_list, kp_count, out_kps, out_desc, kp_pitch, out_n, s0, s1, wn);
 }
 
 }  // namespace orbpl

@@ -33,11 +33,11 @@ void launch_fast(const OrbGeom& hg, const OrbGeom* dg, const CellGeom* cells, co
                  int l0, int l1, hipStream_t s);
 void launch_octree(const OrbGeom& hg, const OrbGeom* dg, const uint32_t* cell_cands,
                    const int* cell_counts, uint32_t* kcand, int* knode, uint32_t* kp_list,
-                   int* kp_count, int* err_flag, int batch, hipStream_t s);
+                   int* kp_count, int* err_flag, int batch, int l0, int l1, hipStream_t s);
 void launch_orient_desc(const OrbGeom& hg, const OrbGeom* dg, const uint8_t* pyr,
                         const uint8_t* blur, const uint32_t* kp_list, const int* kp_count,
                         orbpl_keypoint_dev* out_kps, uint8_t* out_desc, int kp_pitch, int* out_n,
-                        int batch, hipStream_t s);
+                        int batch, int l0, int l1, hipStream_t s);
 
 // Host geometry (orb_geom.cpp). Returns 0 or an ORBPL_ERR_* code with a
 // message in *err.

@@ -144,7 +144,7 @@ struct orbx_ctx {
   hipStream_t fstream = nullptr;
   hipEvent_t ev_group[kMaxLevels] = {};   // pyramid group g written (stream)
   hipEvent_t ev_fjoin = nullptr;          // every FAST launch done (fstream)
-  hipEvent_t ev_fast[2 * kFastGroups] = {};   // FAST launch brackets, own timing
+  hipEvent_t ev_kern[kKernelBrackets] = {};   // FAST / octree / orientation launch brackets
   int ngroups = 1;
   int group_end[kMaxLevels] = {};         // group g = levels [end[g-1], end[g])
   bool timed = false;
@@ -276,7 +276,7 @@ static void free_ctx(orbx_ctx* c) {
     if (e) (void)hipEventDestroy(e);
   for (auto& e : c->ev_group)
     if (e) (void)hipEventDestroy(e);
-  for (auto& e : c->ev_fast)
+  for (auto& e : c->ev_kern)
     if (e) (void)hipEventDestroy(e);
   if (c->ev_fjoin) (void)hipEventDestroy(c->ev_fjoin);
   if (c->fstream) {
@@ -339,7 +339,7 @@ int orbx_create(const orbpl_orb_params* p, int width, int height, int max_batch,
     CK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   }
   for (auto& e : c->ev) CK(hipEventCreate(&e));
-  for (auto& e : c->ev_fast) CK(hipEventCreate(&e));
+  for (auto& e : c->ev_kern) CK(hipEventCreate(&e));
   {
     // level groups: [0,1) [1,2) [2,3) [3,n) by default (FAST work per level
     // ~ 1 / 1.44^l of level 0's: the first three groups hold 69 % of it);
@@ -503,12 +503,12 @@ hipStream_t orbx_stream(orbx_ctx* c) { return c->stream; }
 // Whole extraction pipeline on the ctx stream; images already in device memory.
 int orbx_run(orbx_ctx* c, const uint8_t* d_imgs, int batch, int stride, long long frame_pitch,
              orbpl_keypoint_dev* d_kps, uint8_t* d_desc, int kp_pitch, int* d_n,
-             hipEvent_t* ext_events, hipEvent_t* ext_fast) {
+             hipEvent_t* ext_events, hipEvent_t* ext_kernels) {
   const OrbGeom& g = c->hg.g;
   hipStream_t s = c->stream;
   c->timed = ext_events == nullptr;
   hipEvent_t* ev = ext_events ? ext_events : c->ev;
-  hipEvent_t* evf = ext_fast ? ext_fast : (ext_events ? nullptr : c->ev_fast);
+  hipEvent_t* evk = ext_kernels ? ext_kernels : (ext_events ? nullptr : c->ev_kern);
   HIP_CHECK(hipEventRecord(ev[0], s));
   // row bands per frame: enough blocks for ~4 per CU (256 CUs), at most 8
   int nb = c->pyr_bands;
@@ -516,49 +516,61 @@ int orbx_run(orbx_ctx* c, const uint8_t* d_imgs, int batch, int stride, long lon
     nb = 1;
     while (nb < kPyrMaxBands && nb * batch < 1024) nb *= 2;
   }
-  if (c->ngroups == 1) {
+  // kernel brackets: FAST / octree / orientation+descriptor launch of group gi
+  // at evk[2 (K G + gi)] .. + 1 (K = 0, 1, 2), unused pairs back to back
+  auto bracket = [&](int kind, int gi, int end, hipStream_t st) -> hipError_t {
+    return evk ? hipEventRecord(evk[2 * (kind * kFastGroups + gi) + end], st) : hipSuccess;
+  };
+  const bool pipe = c->ngroups > 1;
+  hipStream_t fs = pipe ? c->fstream : s;
+  // Level groups (one group without the pipeline): group gi's pyramid launch
+  // on `s`, then its FAST, octree and orientation + descriptor launches on the
+  // FAST stream - FAST reads only the group's levels, the octree of a level
+  // only its FAST cells, and the orientation of a level's keypoints the
+  // counts of that and the lower levels (in stream order). The next group's
+  // pyramid launch writes only its own levels.
+  int l0 = 0;
+  for (int gi = 0; gi < c->ngroups; gi++) {
+    const int l1 = c->group_end[gi];
     launch_pyramid(g, c->d_geom, d_imgs, stride, frame_pitch, c->d_pyr, c->d_blur, c->d_rs,
-                   c->d_bands + pyr_band_base(nb), nb, batch, c->d_pyr_prof, 0, g.nlevels, s);
-    HIP_CHECK(hipEventRecord(ev[1], s));
-    // the blur is fused into k_pyramid: the blur stage interval stays empty
-    HIP_CHECK(hipEventRecord(ev[2], s));
-    if (evf) HIP_CHECK(hipEventRecord(evf[0], s));
-    launch_fast(g, c->d_geom, c->d_cells, c->d_pyr, c->d_cell_cands, c->d_cell_counts,
-                c->params.ini_th_fast, c->params.min_th_fast, batch, 0, g.nlevels, s);
-    if (evf)
-      for (int k = 1; k < 2 * kFastGroups; k++) HIP_CHECK(hipEventRecord(evf[k], s));
-    HIP_CHECK(hipEventRecord(ev[3], s));
-  } else {
-    // group gi's FAST (fstream) waits for the group's pyramid launch; the
-    // next group's pyramid launch reads only pyramid levels, which FAST
-    // does not write. The FAST outputs are read by the octree after the join.
-    int l0 = 0;
-    for (int gi = 0; gi < c->ngroups; gi++) {
-      const int l1 = c->group_end[gi];
-      launch_pyramid(g, c->d_geom, d_imgs, stride, frame_pitch, c->d_pyr, c->d_blur, c->d_rs,
-                     c->d_bands + pyr_band_base(nb), nb, batch, c->d_pyr_prof, l0, l1, s);
+                   c->d_bands + pyr_band_base(nb), nb, batch, c->d_pyr_prof, l0, l1, s);
+    if (pipe) {
       HIP_CHECK(hipEventRecord(c->ev_group[gi], s));
-      HIP_CHECK(hipStreamWaitEvent(c->fstream, c->ev_group[gi], 0));
-      if (evf) HIP_CHECK(hipEventRecord(evf[2 * gi], c->fstream));
-      launch_fast(g, c->d_geom, c->d_cells, c->d_pyr, c->d_cell_cands, c->d_cell_counts,
-                  c->params.ini_th_fast, c->params.min_th_fast, batch, l0, l1, c->fstream);
-      if (evf) HIP_CHECK(hipEventRecord(evf[2 * gi + 1], c->fstream));
-      l0 = l1;
+      HIP_CHECK(hipStreamWaitEvent(fs, c->ev_group[gi], 0));
+    } else {
+      HIP_CHECK(hipEventRecord(ev[1], s));
+      // the blur is fused into k_pyramid: the blur stage interval stays empty
+      HIP_CHECK(hipEventRecord(ev[2], s));
     }
-    if (evf)
-      for (int k = 2 * c->ngroups; k < 2 * kFastGroups; k++)
-        HIP_CHECK(hipEventRecord(evf[k], c->fstream));
+    HIP_CHECK(bracket(0, gi, 0, fs));
+    launch_fast(g, c->d_geom, c->d_cells, c->d_pyr, c->d_cell_cands, c->d_cell_counts,
+                c->params.ini_th_fast, c->params.min_th_fast, batch, l0, l1, fs);
+    HIP_CHECK(bracket(0, gi, 1, fs));
+    if (!pipe) HIP_CHECK(hipEventRecord(ev[3], s));
+    HIP_CHECK(bracket(1, gi, 0, fs));
+    launch_octree(g, c->d_geom, c->d_cell_cands, c->d_cell_counts, c->d_kcand, c->d_knode,
+                  c->d_kp_list, c->d_kp_count, c->d_err, batch, l0, l1, fs);
+    HIP_CHECK(bracket(1, gi, 1, fs));
+    if (!pipe) HIP_CHECK(hipEventRecord(ev[4], s));
+    HIP_CHECK(bracket(2, gi, 0, fs));
+    launch_orient_desc(g, c->d_geom, c->d_pyr, c->d_blur, c->d_kp_list, c->d_kp_count, d_kps,
+                       d_desc, kp_pitch, d_n, batch, l0, l1, fs);
+    HIP_CHECK(bracket(2, gi, 1, fs));
+    l0 = l1;
+  }
+  for (int kind = 0; kind < 3; kind++)
+    for (int gi = c->ngroups; gi < kFastGroups; gi++) {
+      HIP_CHECK(bracket(kind, gi, 0, fs));
+      HIP_CHECK(bracket(kind, gi, 1, fs));
+    }
+  if (pipe) {
     HIP_CHECK(hipEventRecord(ev[1], s));
     HIP_CHECK(hipEventRecord(ev[2], s));
-    HIP_CHECK(hipEventRecord(c->ev_fjoin, c->fstream));
+    HIP_CHECK(hipEventRecord(c->ev_fjoin, fs));
     HIP_CHECK(hipStreamWaitEvent(s, c->ev_fjoin, 0));
     HIP_CHECK(hipEventRecord(ev[3], s));
+    HIP_CHECK(hipEventRecord(ev[4], s));
   }
-  launch_octree(g, c->d_geom, c->d_cell_cands, c->d_cell_counts, c->d_kcand, c->d_knode,
-                c->d_kp_list, c->d_kp_count, c->d_err, batch, s);
-  HIP_CHECK(hipEventRecord(ev[4], s));
-  launch_orient_desc(g, c->d_geom, c->d_pyr, c->d_blur, c->d_kp_list, c->d_kp_count, d_kps, d_desc,
-                     kp_pitch, d_n, batch, s);
   HIP_CHECK(hipEventRecord(ev[5], s));
   HIP_CHECK(hipGetLastError());
   c->last_batch = batch;
@@ -715,13 +727,17 @@ int orbx_last_stage_ms(const orbx_ctx* c, float* ms5) {
   HIP_CHECK(hipSetDevice(c->device));
   HIP_CHECK(hipEventSynchronize(c->ev[5]));
   for (int i = 0; i < 5; i++) HIP_CHECK(hipEventElapsedTime(&ms5[i], c->ev[i], c->ev[i + 1]));
-  // FAST: the kernel time of its launches (beside the pyramid's later levels
-  // when the level pipeline is on), without the waits between them
-  ms5[2] = 0.f;
-  for (int k = 0; k < kFastGroups; k++) {
-    float m = 0.f;
-    HIP_CHECK(hipEventElapsedTime(&m, c->ev_fast[2 * k], c->ev_fast[2 * k + 1]));
-    ms5[2] += m;
+  // FAST, octree, orientation + descriptors: the kernel time of their level
+  // group launches (beside the pyramid's later levels when the level
+  // pipeline is on), without the waits between them
+  for (int kind = 0; kind < 3; kind++) {
+    ms5[2 + kind] = 0.f;
+    for (int k = 0; k < kFastGroups; k++) {
+      float m = 0.f;
+      HIP_CHECK(hipEventElapsedTime(&m, c->ev_kern[2 * (kind * kFastGroups + k)],
+                                    c->ev_kern[2 * (kind * kFastGroups + k) + 1]));
+      ms5[2 + kind] += m;
+    }
   }
   return ORBPL_OK;
 }

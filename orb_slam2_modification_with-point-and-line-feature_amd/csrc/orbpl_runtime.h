@@ -25,13 +25,16 @@ bool lsd_split_decision(int n_streams);
 bool once_per_device(const void* key);
 int orbx_run(orbx_ctx* c, const uint8_t* d_imgs, int batch, int stride, long long frame_pitch,
              orbpl_keypoint_dev* d_kps, uint8_t* d_desc, int kp_pitch, int* d_n,
-             hipEvent_t* ext_events = nullptr, hipEvent_t* ext_fast = nullptr);
-// ext_events[0..5]: start, pyramid done, (empty blur stage), FAST joined,
-// octree done, orientation + descriptors done (on the ctx stream);
-// ext_fast[2 g], [2 g + 1]: FAST launch g bracketed on its stream (g <
-// kFastGroups; unused pairs are recorded back to back): the FAST stage time
-// is the sum of the pairs, its kernel time without the waits between groups
+             hipEvent_t* ext_events = nullptr, hipEvent_t* ext_kernels = nullptr);
+// ext_events[0..5]: start, pyramid done, (empty blur stage), FAST done,
+// octree done, orientation + descriptors done (on the ctx stream; with the
+// level pipeline 1..5 all mark the join of the FAST stream);
+// ext_kernels[2 (K kFastGroups + g)], [.. + 1]: the FAST (K = 0), octree (1)
+// and orientation + descriptor (2) launch of level group g bracketed on its
+// stream, unused pairs recorded back to back: a stage's time is the sum of
+// its pairs, its kernel time without the waits between groups
 constexpr int kFastGroups = 4;
+constexpr int kKernelBrackets = 6 * kFastGroups;
 hipStream_t orbx_stream(orbx_ctx* c);
 struct OrbGeom;
 int orbx_device_pyramid(orbx_ctx* c, int frame, const uint8_t** base, const OrbGeom** geom,

@@ -865,8 +865,8 @@ struct orbpl_tracker {
   StreamState* d_state = nullptr;
   PoseEdge* d_edges = nullptr;
   static constexpr int kRing = 64;   // steps kept in the timing ring
-  static constexpr int kEv = 36 + 2 * kFastGroups;   // events per step (28..35: kernel brackets,
-                                                     // 36..: FAST launch brackets)
+  static constexpr int kEv = 36 + kKernelBrackets;   // events per step (28..35: kernel brackets,
+                                                     // 36..: extraction launch brackets)
   std::vector<hipEvent_t> ring;      // kRing * kEv events
   int ring_pos = 0, ring_count = 0;
   // TrackLocalMap (ORBPL_TRACK_LOCAL_MAP): ring of the last kLmK keyframes'
@@ -2375,9 +2375,9 @@ int orbpl_tracker_timings(orbpl_tracker* t, int max_steps, float* ms, int* n_ste
   // match (incl. prediction), pose, finish (tracking stream)
   // (+ TrackLocalMap: gather, frustum, local matching, second pose, count)
   // (+ KeyFrame::ComputeBoW with a vocabulary; 0 without)
-  // (FAST, stage 2: the summed kernel time of its launches on the extractor's
-  // FAST stream, which overlap the pyramid's later levels under the level
-  // pipeline; pairs 36 + 2g, 37 + 2g)
+  // (FAST, octree, orientation + descriptors, stages 2-4: the summed kernel
+  // time of their level-group launches on the extractor's FAST stream, which
+  // overlap the pyramid's later levels under the level pipeline)
   static const int kPair[kTimingStages][2] = {{0, 1}, {1, 2}, {36, 37}, {3, 4}, {4, 5}, {5, 27},
                                               {7, 8}, {14, 9}, {26, 10}, {9, 26}, {27, 6}};
   const int n = std::min(max_steps, t->ring_count);
@@ -2386,10 +2386,16 @@ int orbpl_tracker_timings(orbpl_tracker* t, int max_steps, float* ms, int* n_ste
     hipEvent_t* ev = &t->ring[(size_t)(step % orbpl_tracker::kRing) * orbpl_tracker::kEv];
     for (int i = 0; i < kTimingStages; i++)
       HIP_CHECK(hipEventElapsedTime(&ms[k * kTimingStages + i], ev[kPair[i][0]], ev[kPair[i][1]]));
-    for (int gi = 1; gi < kFastGroups; gi++) {
-      float m = 0.f;
-      HIP_CHECK(hipEventElapsedTime(&m, ev[36 + 2 * gi], ev[37 + 2 * gi]));
-      ms[k * kTimingStages + 2] += m;
+    // FAST (2), octree (3), orientation + descriptors (4): summed launch brackets
+    for (int kind = 0; kind < 3; kind++) {
+      float sum = 0.f;
+      for (int gi = 0; gi < kFastGroups; gi++) {
+        float m = 0.f;
+        const int e = 36 + 2 * (kind * kFastGroups + gi);
+        HIP_CHECK(hipEventElapsedTime(&m, ev[e], ev[e + 1]));
+        sum += m;
+      }
+      ms[k * kTimingStages + 2 + kind] = sum;
     }
   }
   *n_steps = n;
