@@ -4,8 +4,9 @@ Reads gpurun_out/prof_<tag>/{trace,fetch,write}/ (rocprofv3 csv) and writes
 profiles/<round>/pmc_traffic.json:
   {kernel: {"launches", "avg_ns", "fetch_bytes", "write_bytes", "traffic_bytes"}}
 per launch, averaged over the launches of the profiled bench command (per
-extraction step for k_pyramid / k_fast_cells, which the level pipeline
-launches once per group of levels: "group_launches" per step).
+extraction step for k_pyramid / k_fast_cells / k_octree / k_orient_desc,
+which the level pipeline launches once per group of levels: "group_launches"
+per step).
 gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts half
 the bytes of wide coalesced reads, so fetch_bytes = 2 * FETCH_SIZE; WRITE_SIZE
 is taken as is. Both counters are in KiB.
@@ -77,11 +78,13 @@ def main():
                   "fetch_bytes": fb, "write_bytes": wb,
                   "traffic_bytes": (fb + wb) if fb is not None and wb is not None else None}
     dur = {k: [0] * out[k]["launches"] for k in out}
-    # the ORB level pipeline launches k_pyramid and k_fast_cells once per group
-    # of levels: their entries are per step (the sum over a step's group
-    # launches, "group_launches" of them), k_octree runs once per step
-    steps = len(dur.get("k_octree", [])) or 0
-    for k in ("k_pyramid", "k_fast_cells"):
+    # the ORB level pipeline launches k_pyramid, k_fast_cells, k_octree and
+    # k_orient_desc once per group of levels: their entries are per step (the
+    # sum over a step's group launches, "group_launches" of them)
+    # (k_frame_prepare runs once per step; the octree and orientation are
+    # group-launched too since round 5)
+    steps = out.get("k_frame_prepare", {}).get("launches", 0)
+    for k in ("k_pyramid", "k_fast_cells", "k_octree", "k_orient_desc"):
         e = out.get(k)
         if e and steps and e["launches"] > steps and e["launches"] % steps == 0:
             m = e["launches"] // steps
