@@ -501,6 +501,8 @@ namespace orbpl {
 hipStream_t orbx_stream(orbx_ctx* c) { return c->stream; }
 
 // Whole extraction pipeline on the ctx stream; images already in device memory.
+constexpr int kLevelPipeMinBatch = 64;
+
 int orbx_run(orbx_ctx* c, const uint8_t* d_imgs, int batch, int stride, long long frame_pitch,
              orbpl_keypoint_dev* d_kps, uint8_t* d_desc, int kp_pitch, int* d_n,
              hipEvent_t* ext_events, hipEvent_t* ext_kernels) {
@@ -521,7 +523,11 @@ int orbx_run(orbx_ctx* c, const uint8_t* d_imgs, int batch, int stride, long lon
   auto bracket = [&](int kind, int gi, int end, hipStream_t st) -> hipError_t {
     return evk ? hipEventRecord(evk[2 * (kind * kFastGroups + gi) + end], st) : hipSuccess;
   };
-  const bool pipe = c->ngroups > 1;
+  // small batches run the levels in one launch each: at batch 1 the 16
+  // launches and cross-stream events of the pipeline cost more latency than
+  // the overlap returns (points batch 1: 1.56 vs 1.51 ms)
+  const bool pipe = c->ngroups > 1 && batch >= kLevelPipeMinBatch;
+  const int ngroups = pipe ? c->ngroups : 1;
   hipStream_t fs = pipe ? c->fstream : s;
   // Level groups (one group without the pipeline): group gi's pyramid launch
   // on `s`, then its FAST, octree and orientation + descriptor launches on the
@@ -530,8 +536,8 @@ int orbx_run(orbx_ctx* c, const uint8_t* d_imgs, int batch, int stride, long lon
   // counts of that and the lower levels (in stream order). The next group's
   // pyramid launch writes only its own levels.
   int l0 = 0;
-  for (int gi = 0; gi < c->ngroups; gi++) {
-    const int l1 = c->group_end[gi];
+  for (int gi = 0; gi < ngroups; gi++) {
+    const int l1 = pipe ? c->group_end[gi] : g.nlevels;
     launch_pyramid(g, c->d_geom, d_imgs, stride, frame_pitch, c->d_pyr, c->d_blur, c->d_rs,
                    c->d_bands + pyr_band_base(nb), nb, batch, c->d_pyr_prof, l0, l1, s);
     if (pipe) {
@@ -559,7 +565,7 @@ int orbx_run(orbx_ctx* c, const uint8_t* d_imgs, int batch, int stride, long lon
     l0 = l1;
   }
   for (int kind = 0; kind < 3; kind++)
-    for (int gi = c->ngroups; gi < kFastGroups; gi++) {
+    for (int gi = ngroups; gi < kFastGroups; gi++) {
       HIP_CHECK(bracket(kind, gi, 0, fs));
       HIP_CHECK(bracket(kind, gi, 1, fs));
     }
