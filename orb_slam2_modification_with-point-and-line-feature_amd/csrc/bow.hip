@@ -66,11 +66,18 @@ struct BowBatch {
 
 }  // namespace
 
-__device__ __forceinline__ int dist256(const uint4& a0, const uint4& a1, const uint4* b) {
-  const uint4 b0 = b[0], b1 = b[1];
-  return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
-         __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+// the descriptor of node c: a 32-bit byte offset from the (uniform) node
+// descriptor base (n_nodes * 32 B < 2^32)
+__device__ __forceinline__ const uint4* node_desc(const uint4* base, int c) {
+  return reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(base) + ((uint32_t)c << 5));
 }
+
+// Children compared per level: up to kBowBatch of them have their ids and
+// descriptors loaded together before any distance is taken (the loads of a
+// level are then one dependent round instead of one per child); the
+// distances are compared in child order, so the first minimum wins as in
+// the reference loop.
+constexpr int kBowBatch = 10;   // the k of ORBvoc (and the bench vocabulary)
 
 __global__ void __launch_bounds__(256) k_bow_words(VocDev v, BowBatch b) {
   const int f = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
@@ -84,14 +91,32 @@ __global__ void __launch_bounds__(256) k_bow_words(VocDev v, BowBatch b) {
     const int cs = v.child_start[node], ce = v.child_start[node + 1];
     if (cs == ce) break;   // isLeaf(): children empty
     ++level;
-    int best = v.child[cs];
-    int bd = dist256(a0, a1, v.desc + 2 * (long long)best);
-    for (int q = cs + 1; q < ce; q++) {
-      const int c = v.child[q];
-      const int dd = dist256(a0, a1, v.desc + 2 * (long long)c);
-      if (dd < bd) {
-        bd = dd;
-        best = c;
+    int best = -1, bd = 0x7fffffff;
+    for (int q0 = cs; q0 < ce; q0 += kBowBatch) {
+      const int m = min(kBowBatch, ce - q0);
+      int c[kBowBatch];
+#pragma unroll
+      for (int k = 0; k < kBowBatch; k++) c[k] = k < m ? v.child[q0 + k] : 0;
+      uint4 e0[kBowBatch], e1[kBowBatch];
+#pragma unroll
+      for (int k = 0; k < kBowBatch; k++) {
+        if (k < m) {
+          const uint4* p = node_desc(v.desc, c[k]);
+          e0[k] = p[0];
+          e1[k] = p[1];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kBowBatch; k++) {
+        if (k < m) {
+          const int dd = __popc(a0.x ^ e0[k].x) + __popc(a0.y ^ e0[k].y) + __popc(a0.z ^ e0[k].z) +
+                         __popc(a0.w ^ e0[k].w) + __popc(a1.x ^ e1[k].x) + __popc(a1.y ^ e1[k].y) +
+                         __popc(a1.z ^ e1[k].z) + __popc(a1.w ^ e1[k].w);
+          if (best < 0 || dd < bd) {
+            bd = dd;
+            best = c[k];
+          }
+        }
       }
     }
     node = best;
