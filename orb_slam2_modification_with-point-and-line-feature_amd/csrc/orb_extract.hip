@@ -267,9 +267,13 @@ __device__ __forceinline__ fshort2 fast_m2_mm3(const uint2* R) {
   return pmax(pmax(A, nB), zero);
 }
 
-// 8 bytes x-3 .. x+4 of a row from the 3 aligned dwords at q (x-3 = 4 q + o)
-__device__ __forceinline__ uint2 load_ring_row(const uint32_t* q, uint32_t o) {
-  const uint32_t w0 = q[0], w1 = q[1], w2 = q[2];
+// 8 bytes x-3 .. x+4 of a row from the 3 aligned dwords at byte `off` of a
+// wave-uniform base (x-3 = off + o): one 32-bit offset, merged dwordx3 load
+__device__ __forceinline__ uint2 load_ring_row(const uint8_t* base, uint32_t off, uint32_t o) {
+  const uint8_t* q = base + off;
+  const uint32_t w0 = *reinterpret_cast<const uint32_t*>(q);
+  const uint32_t w1 = *reinterpret_cast<const uint32_t*>(q + 4);
+  const uint32_t w2 = *reinterpret_cast<const uint32_t*>(q + 8);
   return make_uint2(__builtin_amdgcn_alignbyte(w1, w0, o), __builtin_amdgcn_alignbyte(w2, w1, o));
 }
 
@@ -289,8 +293,9 @@ __device__ __forceinline__ void xcd_block(int* bx, int* by) {
 
 // floor(k / n) by multiply-high: inv = ceil(2^32 / n) for n >= 2 (exact for
 // k * n < 2^32), inv = 0 for n == 1.
+// (floor((2^32 - 1 + n) / n) = floor((2^32 - 1) / n) + 1: a 32-bit division)
 __device__ __forceinline__ uint32_t div_inv(int n) {
-  return n > 1 ? (uint32_t)((0xFFFFFFFFull + (unsigned)n) / (unsigned)n) : 0u;
+  return n > 1 ? 0xFFFFFFFFu / (unsigned)n + 1u : 0u;
 }
 __device__ __forceinline__ int div_small(int k, uint32_t inv) {
   return inv ? (int)__umulhi((uint32_t)k, inv) : k;
@@ -738,17 +743,18 @@ __global__ void __launch_bounds__(256, ORBPL_FAST_MINW) k_fast_cells(const uint8
     const int cx = cg.x0 + 3 + 2 * p;                    // content column of the left centre
     const int abase = (cx - 3) & ~3;
     const uint32_t o = (uint32_t)((cx - 3) - abase);
-    const int pdw = L.pitch >> 2;
-    // window row w = content row cg.y0 + w; detection row r = window row r + 3
-    const uint32_t* col = reinterpret_cast<const uint32_t*>(
-        pyr + (long long)f * g->pyr_bytes + content_off(L, abase, cg.y0));
+    const uint32_t pitch = (uint32_t)L.pitch;
+    // window row w = content row cg.y0 + w; detection row r = window row r + 3;
+    // rows as 32-bit byte offsets from the window's (uniform) first row
+    const uint8_t* wrow = pyr + (long long)f * g->pyr_bytes + content_off(L, 0, cg.y0);
+    const uint32_t acol = (uint32_t)abase;
     const bool has_hi = 2 * p + 1 < dc;
     const bool has_left = p > 0, has_right = p + 1 < np;
     const uint32_t pbit = 1u << p;
     uint2 R[7];
     if (in_seg) {
 #pragma unroll
-      for (int k = 0; k < 6; k++) R[k + 1] = load_ring_row(col + (long long)(ra + k) * pdw, o);
+      for (int k = 0; k < 6; k++) R[k + 1] = load_ring_row(wrow, umul24((uint32_t)(ra + k), pitch) + acol, o);
     }
     // rows r-1, r-2 of the walk: packed m, 3-wide row max, centre-excluded max
     uint32_t m1 = 0, rmax1 = 0, rmax2 = 0, cmax1 = 0;
@@ -760,7 +766,7 @@ __global__ void __launch_bounds__(256, ORBPL_FAST_MINW) k_fast_cells(const uint8
       if (act) {
 #pragma unroll
         for (int k = 0; k < 6; k++) R[k] = R[k + 1];
-        R[6] = load_ring_row(col + (long long)(r + 6) * pdw, o);
+        R[6] = load_ring_row(wrow, umul24((uint32_t)(r + 6), pitch) + acol, o);
 #if ORBPL_FAST_MM3
         const fshort2 m2 = fast_m2_mm3(R);
 #else
