@@ -558,14 +558,17 @@ int orbx_run(orbx_ctx* c, const uint8_t* d_imgs, int batch, int stride, long lon
                   c->d_kp_list, c->d_kp_count, c->d_err, batch, l0, l1, fs);
     HIP_CHECK(bracket(1, gi, 1, fs));
     if (!pipe) HIP_CHECK(hipEventRecord(ev[4], s));
-    HIP_CHECK(bracket(2, gi, 0, fs));
-    launch_orient_desc(g, c->d_geom, c->d_pyr, c->d_blur, c->d_kp_list, c->d_kp_count, d_kps,
-                       d_desc, kp_pitch, d_n, batch, l0, l1, fs);
-    HIP_CHECK(bracket(2, gi, 1, fs));
     l0 = l1;
   }
+  // orientation + descriptors of every level in one launch after the last
+  // group's octree (per-group launches measured 1.2 % slower: 148.3-149.0k
+  // vs 150.2-150.7k frames/s, `profiles/r05/pipeline_overlap_ab.txt` item 16)
+  HIP_CHECK(bracket(2, 0, 0, fs));
+  launch_orient_desc(g, c->d_geom, c->d_pyr, c->d_blur, c->d_kp_list, c->d_kp_count, d_kps, d_desc,
+                     kp_pitch, d_n, batch, 0, g.nlevels, fs);
+  HIP_CHECK(bracket(2, 0, 1, fs));
   for (int kind = 0; kind < 3; kind++)
-    for (int gi = ngroups; gi < kFastGroups; gi++) {
+    for (int gi = kind == 2 ? 1 : ngroups; gi < kFastGroups; gi++) {
       HIP_CHECK(bracket(kind, gi, 0, fs));
       HIP_CHECK(bracket(kind, gi, 1, fs));
     }
