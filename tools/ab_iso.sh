@@ -1,6 +1,6 @@
 #!/bin/bash
 # Headline A/B with the isolated extraction time: items as in tools/ab_lib.sh
-# ("<variant>[:NAME=VALUE[,NAME=VALUE]]"), $2 streams (1024), $3 rounds (2).
+# ("<variant>[:NAME=VALUE[+NAME=VALUE]]"), $2 streams (1024), $3 rounds (2).
 # Prints frames/s, ms per step and the isolated (non-pipelined) step's
 # pyramid + FAST span + octree + orientation/descriptor milliseconds.
 set -o pipefail
@@ -11,7 +11,7 @@ for r in $(seq 1 ${3:-2}); do
     v=${it%%:*}; e=""; [ "$it" != "$v" ] && e=${it#*:}
     L=""; [ "$v" != cur ] && L=variants/$v/liborbpl.so
     tag=$(echo "$it" | tr ':=,/' '____')
-    env ORBPL_LIB=$L ${e//,/ } timeout -k 10 200 python bench.py --streams ${2:-1024} --steps 10 --warmup 3 $B > gpurun_out/ab/iso_${tag}.log 2>&1 || { echo "fail $it"; tail -5 gpurun_out/ab/iso_${tag}.log; exit 1; }
+    env ORBPL_LIB=$L ${e//+/ } timeout -k 10 200 python bench.py --streams ${2:-1024} --steps 10 --warmup 3 $B > gpurun_out/ab/iso_${tag}.log 2>&1 || { echo "fail $it"; tail -5 gpurun_out/ab/iso_${tag}.log; exit 1; }
     grep '^{' gpurun_out/ab/iso_${tag}.log | python -c "
 import json,sys
 d=json.loads(sys.stdin.read()); i=d['roofline']['isolated']['stage_ms']

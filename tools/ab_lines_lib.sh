@@ -1,6 +1,6 @@
 #!/bin/bash
 # Lines A/B over library variants and settings: each item of $1 is
-# "<variant>[:NAME=VALUE[,NAME=VALUE]]" ("cur" = the in-tree library, else
+# "<variant>[:NAME=VALUE[+NAME=VALUE]]" ("cur" = the in-tree library, else
 # variants/<variant>/liborbpl.so): LSD probe at 3072 and the lines workload
 # at 3072 streams, $2 rounds alternating.
 set -o pipefail
@@ -11,9 +11,9 @@ for r in $(seq 1 ${2:-2}); do
     v=${it%%:*}; e=""; [ "$it" != "$v" ] && e=${it#*:}
     L=""; [ "$v" != cur ] && L=variants/$v/liborbpl.so
     tag=$(echo "$it" | tr ':=,/' '____')
-    env ORBPL_LIB=$L ${e//,/ } timeout -k 10 120 python tools/time_lsd.py 3072 > gpurun_out/abl/t_$tag.log 2>&1 || { echo "fail probe $it"; exit 1; }
+    env ORBPL_LIB=$L ${e//+/ } timeout -k 10 120 python tools/time_lsd.py 3072 > gpurun_out/abl/t_$tag.log 2>&1 || { echo "fail probe $it"; exit 1; }
     echo "$r $it probe $(head -1 gpurun_out/abl/t_$tag.log)"
-    env ORBPL_LIB=$L ${e//,/ } timeout -k 10 300 python bench.py --workload lines --streams 3072 --steps 4 --warmup 1 $C > gpurun_out/abl/b_$tag.log 2>&1 || { echo "fail bench $it"; exit 1; }
+    env ORBPL_LIB=$L ${e//+/ } timeout -k 10 300 python bench.py --workload lines --streams 3072 --steps 4 --warmup 1 $C > gpurun_out/abl/b_$tag.log 2>&1 || { echo "fail bench $it"; exit 1; }
     grep '^{' gpurun_out/abl/b_$tag.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$r $it lines', round(d['value']), d['ms_per_step'], round(d['stage_ms']['lsd_seed'],1))"
   done
 done
