@@ -328,14 +328,15 @@ __device__ __forceinline__ uint32_t byte_of(uint32_t w0, uint32_t w1, uint32_t w
   return (lo >> (8 * (p & 3))) & 0xFF;
 }
 
-// rows of a column walk whose loads are in flight together (registers allow
-// 8 for the blur at 4 waves per SIMD; 4 for the resize, 2 source rows each)
+// rows per batch of a column walk; each walk keeps two batches of loads in
+// flight (registers allow 8 for the blur and 3 for the resize, 2 source
+// rows each, within 128 VGPRs: 4 waves per SIMD)
 #ifndef ORBPL_PYR_DEPTH
 #define ORBPL_PYR_DEPTH 8
 #endif
 constexpr int kPyrDepth = ORBPL_PYR_DEPTH;        // blur walk
 #ifndef ORBPL_PYR_RS_DEPTH
-#define ORBPL_PYR_RS_DEPTH 4
+#define ORBPL_PYR_RS_DEPTH 3
 #endif
 constexpr int kPyrRsDepth = ORBPL_PYR_RS_DEPTH;   // resize walk (2 source rows per row)
 
@@ -396,23 +397,28 @@ __device__ __forceinline__ void pyr_resize_rows(const LevelGeom& L, const LevelG
         cf[k] = fushort2{2048, 0};               // sx + 1 >= src width: only sx
       }
     }
-    // kPyrRsDepth rows per iteration: all source dwords are loaded before any is used
-    for (int y = ra; y < rb; y += kPyrRsDepth) {
-      int bq[kPyrRsDepth];
-      uint32_t u[kPyrRsDepth][3], v[kPyrRsDepth][3];
+    // kPyrRsDepth rows per batch, two batches in flight: the source row
+    // indices (yofs) two batches ahead, the source dwords and beta of the next
+    // batch, then the current batch's math (rows past rb clamp to rb-1)
+    constexpr int D = kPyrRsDepth;
+    auto meta = [&](int* sy, int y) {
 #pragma unroll
-      for (int j = 0; j < kPyrRsDepth; j++) {
-        const int yy = min(y + j, rb - 1);
-        const int sy0 = yofs[yy];
-        bq[j] = beta[yy];
+      for (int j = 0; j < D; j++) sy[j] = yofs[min(y + j, rb - 1)];
+    };
+    auto load = [&](const int* sy, int* bq, uint32_t (*u)[3], uint32_t (*v)[3], int y) {
+#pragma unroll
+      for (int j = 0; j < D; j++) {
+        bq[j] = beta[min(y + j, rb - 1)];
         // uniform base + 32-bit per-lane dword offsets (saddr loads)
-        const uint32_t q0 = umul24((uint32_t)min(max(sy0, 0), S.h - 1), spdw) + (uint32_t)d0;
-        const uint32_t q1 = umul24((uint32_t)min(max(sy0 + 1, 0), S.h - 1), spdw) + (uint32_t)d0;
+        const uint32_t q0 = umul24((uint32_t)min(max(sy[j], 0), S.h - 1), spdw) + (uint32_t)d0;
+        const uint32_t q1 = umul24((uint32_t)min(max(sy[j] + 1, 0), S.h - 1), spdw) + (uint32_t)d0;
         ld_dw3(src0w, q0, &u[j][0], &u[j][1], &u[j][2]);
         ld_dw3(src0w, q1, &v[j][0], &v[j][1], &v[j][2]);
       }
+    };
+    auto work = [&](const int* bq, uint32_t (*u)[3], uint32_t (*v)[3], int y) {
 #pragma unroll
-      for (int j = 0; j < kPyrRsDepth; j++) {
+      for (int j = 0; j < D; j++) {
         if (y + j >= rb) break;
         const int b0 = (int)(short)(bq[j] & 0xFFFF), b1 = (int)(short)(bq[j] >> 16);
         uint32_t packed = 0;
@@ -437,6 +443,20 @@ __device__ __forceinline__ void pyr_resize_rows(const LevelGeom& L, const LevelG
           for (int k = 0; k < L.w - x; k++) dst0[doff + k] = (uint8_t)(packed >> (8 * k));
         }
       }
+    };
+    int sa[D], sb[D], ba[D], bb[D];
+    uint32_t ua[D][3], va[D][3], ub[D][3], vb[D][3];
+    meta(sa, ra);
+    meta(sb, ra + D);
+    load(sa, ba, ua, va, ra);
+    for (int y = ra; y < rb; y += 2 * D) {
+      meta(sa, y + 2 * D);
+      load(sb, bb, ub, vb, y + D);
+      work(ba, ua, va, y);
+      if (y + D >= rb) break;
+      meta(sb, y + 3 * D);
+      load(sa, ba, ua, va, y + 2 * D);
+      work(bb, ub, vb, y + D);
     }
   }
 }
@@ -525,14 +545,16 @@ __device__ __forceinline__ void pyr_blur_rows(const LevelGeom& L, const uint8_t*
     }
     uint8_t* out = bp + L.boff;                 // uniform; the lane's column 4 gq
     const uint32_t ocol = 4u * (uint32_t)gq;
-    // kPyrDepth rows per iteration: the source dwords are loaded before any is used
-    for (int y = ra; y < rb; y += kPyrDepth) {
-      uint32_t w[kPyrDepth][3];
+    // kPyrDepth rows per batch, two batches: the next batch's source dwords
+    // are loaded before the current batch's math (rows past rb clamp to rb-1)
+    auto load = [&](uint32_t (*w)[3], int y) {
 #pragma unroll
       for (int j = 0; j < kPyrDepth; j++) {
         const uint32_t q = umul24((uint32_t)(min(y + j, rb - 1) + 3 + kEdge), pw) + c0;
         ld_dw3(col, q, &w[j][0], &w[j][1], &w[j][2]);
       }
+    };
+    auto work = [&](uint32_t (*w)[3], int y) {
 #pragma unroll
       for (int j = 0; j < kPyrDepth; j++) {
         if (y + j >= rb) break;
@@ -542,11 +564,20 @@ __device__ __forceinline__ void pyr_blur_rows(const LevelGeom& L, const uint8_t*
         const uint32_t o = blur_v4(h);
         st_b4(out, umul24((uint32_t)(y + j), (uint32_t)L.bpitch) + ocol, o);
       }
+    };
+    uint32_t wa[kPyrDepth][3], wb[kPyrDepth][3];
+    load(wa, ra);
+    for (int y = ra; y < rb; y += 2 * kPyrDepth) {
+      load(wb, y + kPyrDepth);
+      work(wa, y);
+      if (y + kPyrDepth >= rb) break;
+      load(wa, y + 2 * kPyrDepth);
+      work(wb, y + kPyrDepth);
     }
   }
 }
 
-__global__ void __launch_bounds__(kPyrThreads) k_pyramid(const uint8_t* __restrict__ img, int stride,
+__global__ void __launch_bounds__(kPyrThreads, 4) k_pyramid(const uint8_t* __restrict__ img, int stride,
                                                          long long frame_pitch, uint8_t* pyr,
                                                          uint8_t* __restrict__ blur,
                                                          const OrbGeom* __restrict__ g,
@@ -572,16 +603,40 @@ __global__ void __launch_bounds__(kPyrThreads) k_pyramid(const uint8_t* __restri
       const uint8_t* src = img + (long long)f * frame_pitch;
       const int nv = (L.w + 15) >> 4;
       const uint32_t inv_nv = div_inv(nv);
-      for (int i = t; i < (nb - na) * nv; i += kPyrThreads) {
-        const int rr = div_small(i, inv_nv);
-        const int r = na + rr, c = (i - rr * nv) * 16;
-        const uint8_t* s = src + (long long)r * stride + c;
-        uint8_t* d = fp + content_off(L, c, r);
-        if (c + 16 <= L.w && ((reinterpret_cast<uintptr_t>(s) & 15) == 0)) {
-          *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(s);
-        } else {
-          const int n = min(16, L.w - c);
-          for (int k = 0; k < n; k++) d[k] = s[k];
+      const int total = (nb - na) * nv;
+      // kCopyBatch 16-byte loads in flight per thread before their stores
+      constexpr int kCopyBatch = 8;
+      for (int i0 = t; i0 < total; i0 += kPyrThreads * kCopyBatch) {
+        uint4 v[kCopyBatch];
+        bool whole[kCopyBatch];
+#pragma unroll
+        for (int b = 0; b < kCopyBatch; b++) {
+          const int i = i0 + b * kPyrThreads;
+          const int rr = div_small(i, inv_nv);
+          const int r = na + rr, c = (i - rr * nv) * 16;
+          const uint8_t* sp = src + (long long)r * stride + c;
+          whole[b] = i < total && c + 16 <= L.w && ((reinterpret_cast<uintptr_t>(sp) & 15) == 0);
+          v[b] = whole[b] ? *reinterpret_cast<const uint4*>(sp) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int b = 0; b < kCopyBatch; b++) {
+          const int i = i0 + b * kPyrThreads;
+          const int rr = div_small(i, inv_nv);
+          const int r = na + rr, c = (i - rr * nv) * 16;
+          if (whole[b]) *reinterpret_cast<uint4*>(fp + content_off(L, c, r)) = v[b];
+        }
+        // ragged row ends or an unaligned source: byte copies
+#pragma unroll
+        for (int b = 0; b < kCopyBatch; b++) {
+          const int i = i0 + b * kPyrThreads;
+          if (i < total && !whole[b]) {
+            const int rr = div_small(i, inv_nv);
+            const int r = na + rr, c = (i - rr * nv) * 16;
+            uint8_t* d = fp + content_off(L, c, r);
+            const uint8_t* sp = src + (long long)r * stride + c;
+            const int n = min(16, L.w - c);
+            for (int k = 0; k < n; k++) d[k] = sp[k];
+          }
         }
       }
     } else {
@@ -593,25 +648,40 @@ __global__ void __launch_bounds__(kPyrThreads) k_pyramid(const uint8_t* __restri
     // mirrored bytes (reflect-101: content 19..1 on the left, w-2..w-20 on the
     // right) from aligned dword loads issued together ----
     if (L.w >= kEdge + 2) {
-      for (int i = t; i < (nb - na) * 2; i += kPyrThreads) {
+      // row (i >> 1), side (i & 1): padded row and the aligned dword holding
+      // the first content byte used (o = its byte in that dword)
+      auto side_at = [&](int i, uint8_t** prow, int* o) __attribute__((always_inline)) -> const uint32_t* {
         const int r = na + (i >> 1), side = i & 1;
-        uint8_t* prow = fp + L.pyr_off + (long long)(r + kEdge) * L.pitch;   // padded row
+        *prow = fp + L.pyr_off + (long long)(r + kEdge) * L.pitch;
         const int c0 = side ? L.w - kEdge - 1 : 0;        // first content byte used
         const int a = kContent0 + c0;                     // its byte in the row
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(prow + (a & ~3));
-        const int o = a & 3;
-        uint32_t w[6];
+        *o = a & 3;
+        return reinterpret_cast<const uint32_t*>(*prow + (a & ~3));
+      };
+      const int ntask = (nb - na) * 2;
+      struct Run { uint32_t w[6]; };
+      auto side_load = [&](int i) __attribute__((always_inline)) -> Run {
+        uint8_t* prow;
+        int o;
+        const uint32_t* src = side_at(min(i, ntask - 1), &prow, &o);
+        Run R;
 #pragma unroll
-        for (int k = 0; k < 6; k++) w[k] = src[k];
-        // byte j of the 20-byte run c0 .. c0+19: w[(o + j) >> 2] >> 8 * ((o + j) & 3)
-        auto byte_at = [&](int j) -> uint8_t {
-          const int b = o + j;
-          uint32_t v = w[0];
+        for (int k = 0; k < 6; k++) R.w[k] = src[k];
+        return R;
+      };
+      auto side_store = [&](int i, Run R) __attribute__((always_inline)) {
+        if (i >= ntask) return;
+        uint8_t* prow;
+        int o;
+        side_at(i, &prow, &o);
+        // the 20-byte run c0 .. c0+19 realigned to byte 0 (v_alignbyte by o)
+        uint32_t A[5];
 #pragma unroll
-          for (int k = 1; k < 6; k++) v = (b >> 2) == k ? w[k] : v;
-          return (uint8_t)(v >> (8 * (b & 3)));
+        for (int k = 0; k < 5; k++) A[k] = __builtin_amdgcn_alignbyte(R.w[k + 1], R.w[k], (uint32_t)o);
+        auto byte_at = [&](int j) __attribute__((always_inline)) -> uint8_t {
+          return (uint8_t)(A[j >> 2] >> (8 * (j & 3)));
         };
-        if (side == 0) {
+        if ((i & 1) == 0) {
 #pragma unroll
           for (int px = 0; px < kEdge; px++) prow[kLead + px] = byte_at(kEdge - px);   // content 19 - px
         } else {
@@ -619,6 +689,16 @@ __global__ void __launch_bounds__(kPyrThreads) k_pyramid(const uint8_t* __restri
           for (int k = 0; k < kEdge; k++)                   // content w - 2 - k = c0 + 18 - k
             prow[kLead + L.w + kEdge + k] = byte_at(kEdge - 1 - k);
         }
+      };
+      // four tasks' loads in flight before their stores
+      constexpr int T = kPyrThreads;
+      for (int i0 = t; i0 < ntask; i0 += 4 * T) {
+        const Run r0 = side_load(i0), r1 = side_load(i0 + T);
+        const Run r2 = side_load(i0 + 2 * T), r3 = side_load(i0 + 3 * T);
+        side_store(i0, r0);
+        side_store(i0 + T, r1);
+        side_store(i0 + 2 * T, r2);
+        side_store(i0 + 3 * T, r3);
       }
     } else {
       for (int i = t; i < (nb - na) * 2 * kEdge; i += kPyrThreads) {
@@ -637,7 +717,9 @@ __global__ void __launch_bounds__(kPyrThreads) k_pyramid(const uint8_t* __restri
       const int b0 = max(na, L.h - 1 - kEdge), b1 = min(nb, L.h - 1);   // y = 2h-2-cy
       const int nt = max(0, t1 - t0), nbm = max(0, b1 - b0);
       const int nq = L.pitch >> 4;
-      for (int i = t; i < (nt + nbm) * nq; i += kPyrThreads) {
+      const int ncopy = (nt + nbm) * nq;
+      // 16-byte piece i: source (content) and destination (mirror) row offsets
+      auto mirror_at = [&](int i, long long* so, long long* dof) __attribute__((always_inline)) {
         const int k = i / nq, q = i - k * nq;
         int cy, py;
         if (k < nt) {
@@ -647,10 +729,29 @@ __global__ void __launch_bounds__(kPyrThreads) k_pyramid(const uint8_t* __restri
           cy = b0 + (k - nt);
           py = 2 * L.h - 2 - cy + kEdge;
         }
-        const uint4* s =
-            reinterpret_cast<const uint4*>(fp + L.pyr_off + (long long)(cy + kEdge) * L.pitch) + q;
-        uint4* d = reinterpret_cast<uint4*>(fp + L.pyr_off + (long long)py * L.pitch) + q;
-        *d = *s;
+        *so = L.pyr_off + (long long)(cy + kEdge) * L.pitch + 16 * q;
+        *dof = L.pyr_off + (long long)py * L.pitch + 16 * q;
+      };
+      auto mirror_load = [&](int i) __attribute__((always_inline)) -> uint4 {
+        long long so, dof;
+        mirror_at(min(i, ncopy - 1), &so, &dof);
+        return *reinterpret_cast<const uint4*>(fp + so);
+      };
+      auto mirror_store = [&](int i, uint4 v) __attribute__((always_inline)) {
+        if (i >= ncopy) return;
+        long long so, dof;
+        mirror_at(i, &so, &dof);
+        *reinterpret_cast<uint4*>(fp + dof) = v;
+      };
+      // four pieces' loads in flight before their stores
+      constexpr int T = kPyrThreads;
+      for (int i0 = t; i0 < ncopy; i0 += 4 * T) {
+        const uint4 v0 = mirror_load(i0), v1 = mirror_load(i0 + T);
+        const uint4 v2 = mirror_load(i0 + 2 * T), v3 = mirror_load(i0 + 3 * T);
+        mirror_store(i0, v0);
+        mirror_store(i0 + T, v1);
+        mirror_store(i0 + 2 * T, v2);
+        mirror_store(i0 + 3 * T, v3);
       }
     }
     __syncthreads();
