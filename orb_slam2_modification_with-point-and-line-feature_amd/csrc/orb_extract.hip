@@ -339,6 +339,10 @@ constexpr int kPyrDepth = ORBPL_PYR_DEPTH;        // blur walk
 #define ORBPL_PYR_RS_DEPTH 3
 #endif
 constexpr int kPyrRsDepth = ORBPL_PYR_RS_DEPTH;   // resize walk (2 source rows per row)
+// 16-byte loads in flight per thread in the level-0 input copy
+#ifndef ORBPL_PYR_COPY_BATCH
+#define ORBPL_PYR_COPY_BATCH 8
+#endif
 
 // Row segments of a walk (tasks = groups x nseg, rps rows per segment): the
 // split with the fewest sequential rows per thread, counting `warm` extra
@@ -605,7 +609,7 @@ __global__ void __launch_bounds__(kPyrThreads, 4) k_pyramid(const uint8_t* __res
       const uint32_t inv_nv = div_inv(nv);
       const int total = (nb - na) * nv;
       // kCopyBatch 16-byte loads in flight per thread before their stores
-      constexpr int kCopyBatch = 8;
+      constexpr int kCopyBatch = ORBPL_PYR_COPY_BATCH;
       for (int i0 = t; i0 < total; i0 += kPyrThreads * kCopyBatch) {
         uint4 v[kCopyBatch];
         bool whole[kCopyBatch];
