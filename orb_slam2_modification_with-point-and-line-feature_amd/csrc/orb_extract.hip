@@ -362,6 +362,11 @@ __device__ __forceinline__ void walk_split(int groups, int rows, int warm, int* 
   *rps = (rows + best - 1) / best;
 }
 
+template <bool B>
+struct BoolTag {
+  static constexpr bool value = B;
+};
+
 __device__ __forceinline__ void pyr_resize_rows(const LevelGeom& L, const LevelGeom& S,
                                                 const int* __restrict__ rs, uint8_t* fp, int na,
                                                 int nb) {
@@ -388,6 +393,13 @@ __device__ __forceinline__ void pyr_resize_rows(const LevelGeom& L, const LevelG
     uint32_t sel[4];
     bool hiw[4];
     fushort2 cf[4];
+    // narrow groups (all 4 pairs within 8 bytes from sx of column x, o = its
+    // byte in the first dword; every group at scale factors up to ~2): the
+    // window realigned by o (two v_alignbyte per source row) serves all four
+    // columns, with no per-column choice of half
+    const uint32_t o = (uint32_t)(xofs[x] & 3);
+    uint32_t seln[4];
+    bool lane_narrow = true;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const int cx = min(x + k, L.w - 1);
@@ -395,12 +407,16 @@ __device__ __forceinline__ void pyr_resize_rows(const LevelGeom& L, const LevelG
       hiw[k] = p0 > 6;
       const uint32_t pp = (uint32_t)(hiw[k] ? p0 - 4 : p0);
       sel[k] = pp | (0x0cu << 8) | ((pp + 1) << 16) | (0x0cu << 24);
+      const uint32_t pn = (uint32_t)p0 - o;
+      lane_narrow = lane_narrow && pn <= 6u;
+      seln[k] = pn | (0x0cu << 8) | ((pn + 1) << 16) | (0x0cu << 24);
       if (cx < L.xmax) {
         cf[k] = as_u2((uint32_t)alpha[cx]);      // (alpha0, alpha1), both in [0, 2048]
       } else {
         cf[k] = fushort2{2048, 0};               // sx + 1 >= src width: only sx
       }
     }
+    const bool narrow = __ballot(!lane_narrow) == 0ull;   // wave-uniform
     // kPyrRsDepth rows per batch, two batches in flight: the source row
     // indices (yofs) two batches ahead, the source dwords and beta of the next
     // batch, then the current batch's math (rows past rb clamp to rb-1)
@@ -420,19 +436,33 @@ __device__ __forceinline__ void pyr_resize_rows(const LevelGeom& L, const LevelG
         ld_dw3(src0w, q1, &v[j][0], &v[j][1], &v[j][2]);
       }
     };
-    auto work = [&](const int* bq, uint32_t (*u)[3], uint32_t (*v)[3], int y) {
+    auto work = [&](auto narrow_tag, const int* bq, uint32_t (*u)[3], uint32_t (*v)[3], int y) {
+      constexpr bool kNarrow = decltype(narrow_tag)::value;
 #pragma unroll
       for (int j = 0; j < D; j++) {
         if (y + j >= rb) break;
         const int b0 = (int)(short)(bq[j] & 0xFFFF), b1 = (int)(short)(bq[j] >> 16);
         uint32_t packed = 0;
+        uint32_t ua0 = 0, ua1 = 0, va0 = 0, va1 = 0;
+        if constexpr (kNarrow) {
+          ua0 = __builtin_amdgcn_alignbyte(u[j][1], u[j][0], o);
+          ua1 = __builtin_amdgcn_alignbyte(u[j][2], u[j][1], o);
+          va0 = __builtin_amdgcn_alignbyte(v[j][1], v[j][0], o);
+          va1 = __builtin_amdgcn_alignbyte(v[j][2], v[j][1], o);
+        }
 #pragma unroll
         for (int k = 0; k < 4; k++) {
           // alpha1 == 0 at the right edge: the (unused) sx + 1 byte may be border
-          const uint32_t tu = hiw[k] ? __builtin_amdgcn_perm(u[j][2], u[j][1], sel[k])
-                                     : __builtin_amdgcn_perm(u[j][1], u[j][0], sel[k]);
-          const uint32_t tv = hiw[k] ? __builtin_amdgcn_perm(v[j][2], v[j][1], sel[k])
-                                     : __builtin_amdgcn_perm(v[j][1], v[j][0], sel[k]);
+          uint32_t tu, tv;
+          if constexpr (kNarrow) {
+            tu = __builtin_amdgcn_perm(ua1, ua0, seln[k]);
+            tv = __builtin_amdgcn_perm(va1, va0, seln[k]);
+          } else {
+            tu = hiw[k] ? __builtin_amdgcn_perm(u[j][2], u[j][1], sel[k])
+                        : __builtin_amdgcn_perm(u[j][1], u[j][0], sel[k]);
+            tv = hiw[k] ? __builtin_amdgcn_perm(v[j][2], v[j][1], sel[k])
+                        : __builtin_amdgcn_perm(v[j][1], v[j][0], sel[k]);
+          }
           const int h0 = (int)__builtin_amdgcn_udot2(as_u2(tu), cf[k], 0u, false);
           const int h1 = (int)__builtin_amdgcn_udot2(as_u2(tv), cf[k], 0u, false);
           // beta <= 2048, h >> 4 < 2^16: 24-bit products (v_mul_u32_u24)
@@ -448,20 +478,26 @@ __device__ __forceinline__ void pyr_resize_rows(const LevelGeom& L, const LevelG
         }
       }
     };
-    int sa[D], sb[D], ba[D], bb[D];
-    uint32_t ua[D][3], va[D][3], ub[D][3], vb[D][3];
-    meta(sa, ra);
-    meta(sb, ra + D);
-    load(sa, ba, ua, va, ra);
-    for (int y = ra; y < rb; y += 2 * D) {
-      meta(sa, y + 2 * D);
-      load(sb, bb, ub, vb, y + D);
-      work(ba, ua, va, y);
-      if (y + D >= rb) break;
-      meta(sb, y + 3 * D);
-      load(sa, ba, ua, va, y + 2 * D);
-      work(bb, ub, vb, y + D);
-    }
+    auto walk = [&](auto narrow_tag) {
+      int sa[D], sb[D], ba[D], bb[D];
+      uint32_t ua[D][3], va[D][3], ub[D][3], vb[D][3];
+      meta(sa, ra);
+      meta(sb, ra + D);
+      load(sa, ba, ua, va, ra);
+      for (int y = ra; y < rb; y += 2 * D) {
+        meta(sa, y + 2 * D);
+        load(sb, bb, ub, vb, y + D);
+        work(narrow_tag, ba, ua, va, y);
+        if (y + D >= rb) break;
+        meta(sb, y + 3 * D);
+        load(sa, ba, ua, va, y + 2 * D);
+        work(narrow_tag, bb, ub, vb, y + D);
+      }
+    };
+    if (narrow)
+      walk(BoolTag<true>{});
+    else
+      walk(BoolTag<false>{});
   }
 }
 
