@@ -339,6 +339,10 @@ constexpr int kPyrDepth = ORBPL_PYR_DEPTH;        // blur walk
 #define ORBPL_PYR_RS_DEPTH 3
 #endif
 constexpr int kPyrRsDepth = ORBPL_PYR_RS_DEPTH;   // resize walk (2 source rows per row)
+// minimum waves per SIMD for k_pyramid (register budget: 4 = 128 VGPRs)
+#ifndef ORBPL_PYR_MINW
+#define ORBPL_PYR_MINW 4
+#endif
 // 16-byte loads in flight per thread in the level-0 input copy
 #ifndef ORBPL_PYR_COPY_BATCH
 #define ORBPL_PYR_COPY_BATCH 8
@@ -617,7 +621,7 @@ __device__ __forceinline__ void pyr_blur_rows(const LevelGeom& L, const uint8_t*
   }
 }
 
-__global__ void __launch_bounds__(kPyrThreads, 4) k_pyramid(const uint8_t* __restrict__ img, int stride,
+__global__ void __launch_bounds__(kPyrThreads, ORBPL_PYR_MINW) k_pyramid(const uint8_t* __restrict__ img, int stride,
                                                          long long frame_pitch, uint8_t* pyr,
                                                          uint8_t* __restrict__ blur,
                                                          const OrbGeom* __restrict__ g,
