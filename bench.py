@@ -284,7 +284,7 @@ def pmc_traffic(kernel, workload, streams):
     kernel's "frames_per_launch" in the summary, else its stream count). PMC counters
     need their own rocprofv3 passes, so they cannot be read live. Stage
     kernels joined with '+' sum their parts."""
-    for rnd in ("r05", "r04", "r03", "r02", "r01"):
+    for rnd in ("r06", "r05", "r04", "r03", "r02", "r01"):
         f = ROOT / "profiles" / rnd / f"pmc_traffic_{workload}.json"
         if not f.exists() and workload == "points":
             f = ROOT / "profiles" / rnd / "pmc_traffic.json"
@@ -359,6 +359,67 @@ def leg_summary(out):
     if "secondary" in out and out["secondary"].get("dropin_frame"):
         s["dropin_frame_ms"] = out["secondary"]["dropin_frame"].get("median_ms_per_frame")
     return s
+
+
+COMPACT_MAX = 6000   # bytes: the driver reads the line from an 8 KB tail
+
+
+def _roof_compact(r):
+    if not r:
+        return None
+    keep = ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic", "traffic_source",
+            "traffic_over_algorithmic", "algorithmic_bytes_per_launch", "avg_launch_ms",
+            "frames_per_launch")
+    c = {k: r.get(k) for k in keep}
+    iso = r.get("isolated_dominant")
+    if iso:
+        c["isolated_dominant"] = {k: iso.get(k) for k in ("kernel", "avg_launch_ms", "frac",
+                                                          "traffic", "traffic_source")}
+    if r.get("pipeline"):
+        c["pipeline_frac"] = r["pipeline"].get("frac")
+    return c
+
+
+def compact_line(out, detail):
+    """The one JSON line stdout ends with (<= COMPACT_MAX bytes): the
+    contract's keys, the dominant kernel's roofline, the CPU baseline, the
+    parity verdict and every leg's headline figures. Everything else (stage
+    times, sweeps, LSD floors, per-kernel GB/s, host facts) is in the side
+    file named by "detail"."""
+    cpu = out.get("cpu_baseline")
+    par = out.get("parity") or {}
+    c = {k: out.get(k) for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup",
+                                 "ms_per_step", "higher_is_better", "scaling", "vs_baseline",
+                                 "dtype", "data", "config")}
+    c["roofline"] = _roof_compact(out.get("roofline"))
+    c["cpu_baseline"] = None if cpu is None else {
+        "value": cpu.get("value"), "unit": cpu.get("unit"), "cores": cpu.get("cores"),
+        "kind": cpu.get("kind"), "sample": cpu.get("sample"),
+        "host": (cpu.get("host") or {}).get("model"),
+        "reference_faithful_ms": (cpu.get("reference_faithful") or {}).get("median_ms_per_frame"),
+        "reference_faithful_fps": (cpu.get("reference_faithful") or {}).get("value")}
+    legs = [par] + [(out.get(k) or {}).get("parity") or {} for k in
+                    ("secondary", "stereo", "rig", "ingress")]
+    c["parity"] = {"pass": all(p.get("pass", True) for p in legs if isinstance(p, dict)),
+                   "headline_pass": par.get("pass") if isinstance(par, dict) else None,
+                   "max_abs_pose_diff": par.get("max_abs_pose_diff_vs_ref"),
+                   "pose_tol": par.get("pose_tol"), "counts_equal": par.get("counts_equal"),
+                   "ate_rmse_vs_gt_m": par.get("ate_rmse_vs_gt_m"),
+                   "ref_ate_rmse_vs_gt_m": par.get("ref_ate_rmse_vs_gt_m")}
+    s = dict(out.get("summary") or {})
+    for k in ("secondary", "stereo", "rig"):
+        o = out.get(k)
+        if o and s.get(k):
+            s[k] = dict(s[k], roofline=_roof_compact(o.get("roofline")),
+                        cpu_fps=(o.get("cpu_baseline") or {}).get("value"))
+    s.pop("trk_load", None)
+    c["summary"] = s
+    c["detail"] = detail
+    if len(json.dumps(c)) > COMPACT_MAX:       # never print a line the driver cannot take
+        for k in ("secondary", "stereo", "rig"):
+            if s.get(k):
+                s[k].pop("roofline", None)
+    return c
 
 
 def map_capacity(total_steps):
@@ -684,7 +745,9 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
     if args.local_map or use_map:
         cand.append("match_local")
     if lines:
-        cand += list(tr.LSD_STAGES)
+        # (stereo: the line_prepare events also bracket the wait for the right
+        # image's lines and k_stereo_lines, not one kernel: left out)
+        cand += [k for k in tr.LSD_STAGES if not (stereo and k == "line_prepare")]
     iso = None
     if pipelined and args.isolated_steps > 0:
         # untimed: more steps with the two HIP streams serialised, so each
@@ -735,8 +798,11 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
         trk_load["note"] = ("single non-pipelined steps after the timed region; trk_section_ms = "
                             "hipEvents around TrackReferenceKeyFrame (k_trk_bow, line matcher, "
                             "merge, pose) on the tracking stream")
-    sel = iso if iso is not None else stage_avg
-    dom = max(cand, key=lambda k: sel.get(k, stage_avg[k]))
+    # the dominant kernel as rocprofv3 --stats ranks it: the most GPU time per
+    # step in the timed (pipelined) region; the isolated steps' dominant
+    # kernel is reported beside it (roofline.isolated_dominant)
+    dom = max(cand, key=lambda k: stage_avg[k])
+    dom_iso = max(cand, key=lambda k: iso.get(k, 0.0)) if iso is not None else dom
     dom_ms = stage_avg[dom]          # live: timed region, in-stream hipEvents
     # frames per launch: the extraction / LSD batches may be split in two
     # offset halves on two streams; their stage events bracket the first half
@@ -751,7 +817,8 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
         traffic *= 2          # the PMC summary is per launch; two full launches per step
     fbytes = frame_bytes(n_kp, fw, fh, wl["orb"], lines, stereo)
     roof = {"bound": "hbm", "kernel": KERNELS[dom], "stage": dom,
-            "dominance": "summed per-kernel GPU time per step (isolated steps when pipelined)",
+            "dominance": "summed per-kernel GPU time per step in the timed region (as "
+                         "rocprofv3 --stats ranks kernels)",
             "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
             "traffic_source": tsrc,
@@ -795,6 +862,19 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
             "achieved": round(bytes_launch / (ims * 1e-3) / 1e9, 2),
             "frac": round(bytes_launch / (ims * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
             "steps": args.isolated_steps}
+        # the kernel with the most GPU time when the two HIP streams are
+        # serialised (no CU sharing), at its isolated launch time
+        bl_iso = int(ab[dom_iso] * launch_frames(dom_iso))
+        t_iso = iso[dom_iso]
+        tr_iso, src_iso = pmc_traffic(KERNELS[dom_iso], workload, launch_frames(dom_iso))
+        if tr_iso and dom_iso == "pose_all":
+            tr_iso *= 2
+        roof["isolated_dominant"] = {
+            "kernel": KERNELS[dom_iso], "stage": dom_iso, "avg_launch_ms": round(t_iso, 4),
+            "algorithmic_bytes_per_launch": bl_iso,
+            "achieved": round(bl_iso / (t_iso * 1e-3) / 1e9, 2),
+            "frac": round(bl_iso / (t_iso * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+            "traffic": tr_iso, "traffic_source": src_iso}
     tr.close()
     del d_gray, d_depth
     return dict(S=S, value=value, layout=L, elapsed=elapsed, stages=stages, tracking=tracking,
@@ -1255,6 +1335,9 @@ def main():
                          "host-to-device inside the timed region; points runs only; 0 = skip)")
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the oracle replay of the timed trackers' sampled streams")
+    ap.add_argument("--detail", default="gpurun_out/bench_detail.json",
+                    help="side file for the full report (stage times, sweeps, LSD floors, "
+                         "per-kernel GB/s); stdout's last line is the compact record")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -1410,8 +1493,15 @@ def main():
                 if key == "secondary":
                     out[key]["dropin_frame"] = dropin_frame_latency(o["gray"], o["depth"],
                                                                     o["layout"], o["wname"])
-        out["summary"] = leg_summary(out)   # last key: it survives a tail-cut log
-        print(json.dumps(out))
+        out["summary"] = leg_summary(out)
+        detail = Path(args.detail)
+        if not detail.is_absolute():
+            detail = ROOT / detail
+        detail.parent.mkdir(parents=True, exist_ok=True)
+        detail.write_text(json.dumps(out) + "\n")
+        line = json.dumps(compact_line(out, str(detail.relative_to(ROOT))
+                                       if detail.is_relative_to(ROOT) else str(detail)))
+        print(line, flush=True)
     if dist:
         dist.destroy_process_group()
 

@@ -73,9 +73,14 @@ int orbpl_device_count(int* n);
  * queues; ORBPL_LSD_SPLIT=0/1 overrides). Any pointer may be NULL. */
 int orbpl_hw_queue_state(int* queues, int* runtime_started, int* set_by_library,
                          int* lsd_split_1024);
-/* Library build tag ("orbpl gfx950 r3"). r3: orbpl_tracker_timings writes 11
- * floats per step, orbpl_tracker_stereo_timings 4 (r1: 9 and 2); size the
- * buffers from orbpl_tracker_timing_counts. */
+/* Library build tag ("orbpl gfx950 r4").
+ * r4: orbpl_frame_is_in_frustum takes the RAW mfMinDistance / mfMaxDistance
+ *     (MapPoint::GetMinDistance / GetMaxDistance) and applies the 0.8f / 1.2f
+ *     of GetMin/MaxDistanceInvariance itself; r3 callers that pass the
+ *     pre-scaled invariance values must switch to the raw ones.
+ * r3: orbpl_tracker_timings writes 11 floats per step,
+ *     orbpl_tracker_stereo_timings 4 (r1: 9 and 2); size the buffers from
+ *     orbpl_tracker_timing_counts. */
 const char* orbpl_version(void);
 
 /* Device memory plumbing for hosts without their own GPU allocator (the

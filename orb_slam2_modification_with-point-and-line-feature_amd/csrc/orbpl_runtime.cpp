@@ -1,6 +1,7 @@
 // Host runtime and C-ABI (include/orbpl.h) of the ORB extraction path.
 // One orbx_ctx = one device + one HIP stream + device buffers sized for
 // max_batch frames of one image geometry.
+#include <dirent.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -44,15 +45,22 @@ int g_queues_set_by_lib = 0;    // the constructor wrote GPU_MAX_HW_QUEUES
 static bool kfd_open() {
   const char* force = getenv("ORBPL_ASSUME_RUNTIME_STARTED");
   if (force) return force[0] == '1';
-  char path[64], target[256];
-  for (int fd = 0; fd < 4096; fd++) {
-    snprintf(path, sizeof(path), "/proc/self/fd/%d", fd);
+  // every open descriptor, whatever its number
+  DIR* d = opendir("/proc/self/fd");
+  if (!d) return false;
+  const int self = dirfd(d);
+  char path[300], target[256];
+  bool found = false;
+  while (const dirent* e = readdir(d)) {
+    if (e->d_name[0] == '.' || atoi(e->d_name) == self) continue;
+    snprintf(path, sizeof(path), "/proc/self/fd/%s", e->d_name);
     const ssize_t n = readlink(path, target, sizeof(target) - 1);
     if (n <= 0) continue;
     target[n] = 0;
-    if (strcmp(target, "/dev/kfd") == 0) return true;
+    if (strcmp(target, "/dev/kfd") == 0) { found = true; break; }
   }
-  return false;
+  closedir(d);
+  return found;
 }
 
 __attribute__((constructor)) static void record_hw_queues() {
@@ -180,7 +188,7 @@ extern "C" {
 
 const char* orbpl_last_error(void) { return orbpl::g_last_error.c_str(); }
 
-const char* orbpl_version(void) { return "orbpl gfx950 r3"; }
+const char* orbpl_version(void) { return "orbpl gfx950 r4"; }
 
 int orbpl_hw_queue_state(int* queues, int* runtime_started, int* set_by_library,
                          int* lsd_split_1024) {

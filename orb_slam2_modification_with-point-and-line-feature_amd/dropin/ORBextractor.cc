@@ -69,7 +69,13 @@ void ORBextractor::operator()(cv::InputArray _image, cv::InputArray, std::vector
     std::memcpy(_descriptors.getMatRef().data, desc.data, (size_t)n * 32);
   }
   mvImagePyramid.clear();
-  if (!mbKeepPyramid) return;
+  pyr_valid_ = true;
+  if (mbKeepPyramid) FetchPyramid();
+}
+
+// the last call's level contents, device-to-host on request
+const std::vector<cv::Mat>& ORBextractor::FetchPyramid() {
+  if (!pyr_valid_ || (int)mvImagePyramid.size() == nlevels) return mvImagePyramid;
   mvImagePyramid.resize(nlevels);
   for (int l = 0; l < nlevels; l++) {
     int w = 0, h = 0;
@@ -77,6 +83,7 @@ void ORBextractor::operator()(cv::InputArray _image, cv::InputArray, std::vector
     mvImagePyramid[l].create(h, w, cv::CV_8U);
     check(orbx_get_pyramid(ctx_, 0, l, 0, 0, mvImagePyramid[l].data, w * h, &w, &h));
   }
+  return mvImagePyramid;
 }
 
 }  // namespace ORB_SLAM2

@@ -31,10 +31,15 @@ class ORBextractor {
   std::vector<float> GetInverseScaleSigmaSquares() { return mvInvLevelSigma2; }
 
   // the level images of the last call (content, w x h), as the public member
-  // the stereo matcher reads (Frame.cc:895-1002); filled after each call when
-  // mbKeepPyramid is set (device-to-host copies), else left empty
+  // the reference's stereo matcher reads (Frame.cc:895-1002). The pyramid
+  // stays on the device: the drop-in Frame's ComputeStereoMatches reads it
+  // there (orbpl_stereo_matches), so an RGB-D frame copies nothing back.
+  // FetchPyramid() fills mvImagePyramid from the last call on request (a host
+  // that keeps the reference's own ComputeStereoMatches calls it, or sets
+  // mbKeepPyramid to have every call fill it); otherwise it is left empty.
   std::vector<cv::Mat> mvImagePyramid;
-  bool mbKeepPyramid = true;
+  bool mbKeepPyramid = false;
+  const std::vector<cv::Mat>& FetchPyramid();
 
   // the device context (orbpl_stereo_matches reads the pyramid on the device)
   orbx_ctx* ctx() { return ctx_; }
@@ -53,6 +58,7 @@ class ORBextractor {
   orbpl_orb_params params_;
   orbx_ctx* ctx_ = nullptr;
   int ctx_w_ = 0, ctx_h_ = 0;
+  bool pyr_valid_ = false;   // the device holds a pyramid of the last call
 };
 
 }  // namespace ORB_SLAM2

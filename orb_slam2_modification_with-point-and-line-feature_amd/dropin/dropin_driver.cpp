@@ -321,7 +321,7 @@ int main(int argc, char** argv) {
     ORBVocabulary voc;
     if (!voc.loadFromTextFile(vpath)) throw std::runtime_error("cannot load the vocabulary");
     Frame F0(g[0], d[0], 0.0, &ex, &voc, K, dist, bf, thDepth);
-    std::vector<cv::Mat> pyr = ex.mvImagePyramid;
+    std::vector<cv::Mat> pyr = ex.FetchPyramid();   // lazy: only this check reads it
     Frame F1(g[1], d[1], 1.0, &ex, &voc, K, dist, bf, thDepth);
 
     // ---- frame 0: pose Tcw0, map points / lines from depth (Tracking.cc:633-692)

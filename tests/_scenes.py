@@ -112,6 +112,54 @@ def local_map_problem(seed=0, cam_name="TUM1", nobs_zero_frac=0.1, cur_claim_fra
     return cfg, cam, sc, mps, cur, cur_nobs, T3
 
 
+def frustum_reject_problem(seed=0, frac=0.05):
+    """local_map_problem's map points with disjoint subsets (each `frac` of
+    them) moved so that each Frame::IsInFrustum rejection (Frame.cc:345-401)
+    fires: behind the camera (Pc.z < 0), outside the image bounds, distance
+    above 1.2 mfMaxDistance, distance below 0.8 mfMinDistance, view cosine
+    below 0.5 (normal turned against the viewing ray). Returns
+    local_map_problem's tuple plus {branch: mask}."""
+    cfg, cam, sc, mps, cur, cur_nobs, T = local_map_problem(seed)
+    mps = {k: v.copy() for k, v in mps.items()}
+    n = len(mps["xyz"])
+    rng = np.random.default_rng(seed + 101)
+    order = rng.permutation(n)
+    m = int(frac * n)
+    names = ("behind", "outside", "far", "near", "view_cos")
+    sel = {b: order[i * m:(i + 1) * m] for i, b in enumerate(names)}
+    T64 = T.astype(np.float64)
+    R, t = T64[:3, :3], T64[:3, 3]
+    Ow = -R.T @ t
+    P = mps["xyz"].astype(np.float64)
+    Pc = P @ R.T + t
+    # behind the camera: mirror the camera-frame point through the image plane
+    i = sel["behind"]
+    Pb = Pc[i] * np.array([1.0, 1.0, -1.0])
+    mps["xyz"][i] = ((Pb - t) @ R).astype(np.float32)
+    # outside the image: shift along x by more than the image width at its depth
+    i = sel["outside"]
+    Po = Pc[i] + np.stack([np.abs(Pc[i, 2]) * (1.5 * cfg["width"] / cfg["fx"]),
+                           np.zeros(len(i)), np.zeros(len(i))], 1)
+    mps["xyz"][i] = ((Po - t) @ R).astype(np.float32)
+    dist = np.linalg.norm(P - Ow, axis=1)
+    # distance out of [0.8 min, 1.2 max]
+    i = sel["far"]
+    mps["max_dist"][i] = (dist[i] / 1.5).astype(np.float32)
+    mps["min_dist"][i] = (mps["max_dist"][i] / sc[-1]).astype(np.float32)
+    i = sel["near"]
+    mps["min_dist"][i] = (dist[i] / 0.6).astype(np.float32)
+    mps["max_dist"][i] = (mps["min_dist"][i] * sc[-1]).astype(np.float32)
+    # view cosine -1: the normal points along the ray from the camera
+    i = sel["view_cos"]
+    mps["normal"][i] = (-(P[i] - Ow) / dist[i, None]).astype(np.float32)
+    masks = {}
+    for b, i in sel.items():
+        mk = np.zeros(n, bool)
+        mk[i] = True
+        masks[b] = mk
+    return cfg, cam, sc, mps, cur, cur_nobs, T, masks
+
+
 def line_map_problem(seed=0, cam_name="TUM1", claim_frac=0.15):
     """Map lines from frames 0 and 1 (end points unprojected with their own
     depths at the true poses, LBD rows), the current frame 2's undistorted key

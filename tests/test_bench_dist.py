@@ -134,3 +134,25 @@ def test_shared_vocabulary_ws2():
     w, n, _ = bench.shared_idf(synth, tree, docs, None)
     assert n == 6 and np.array_equal(w, w0)
     assert (w0 > 0).sum() > 10
+
+
+def test_compact_line_fits_the_driver_tail():
+    """bench.py's last stdout line carries the contract's keys, the dominant
+    kernel's roofline, the CPU baseline, the parity verdict and the leg
+    summary within COMPACT_MAX bytes (round 5's 22.5 KB line was unparsed);
+    input: the full round-5 record committed under profiles/r05/."""
+    import json
+    import bench
+    full = json.loads((Path(__file__).resolve().parents[1] / "profiles" / "r05" /
+                       "bench_r05_h_default.json").read_text().strip().splitlines()[-1])
+    c = bench.compact_line(full, "gpurun_out/bench_detail.json")
+    s = json.dumps(c)
+    assert "\n" not in s and len(s) <= bench.COMPACT_MAX
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in c
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel"):
+        assert k in c["roofline"]
+    assert c["cpu_baseline"]["cores"] and c["cpu_baseline"]["reference_faithful_ms"]
+    assert c["parity"]["pass"] is True
+    assert {"points", "secondary", "stereo", "rig", "ingress", "batch1_ms"} <= set(c["summary"])

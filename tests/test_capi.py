@@ -61,7 +61,7 @@ def test_timing_layout_and_version(orbpl):
     T = orbpl.Tracker
     assert T.timing_counts() == (len(T.STAGES), len(T.LINE_STAGES), len(T.LSD_STAGES),
                                  len(T.STEREO_STAGES), len(T.KERNEL_STAGES))
-    assert orbpl.lib().orbpl_version().decode() == "orbpl gfx950 r3"
+    assert orbpl.lib().orbpl_version().decode() == "orbpl gfx950 r4"
 
 
 def test_dropin_classes_build_with_the_reference_signatures():

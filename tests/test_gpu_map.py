@@ -25,17 +25,18 @@ def _vocab_arrays(L, seed=3):
 
 
 def _run(orbpl, oracle, lines, refkf, S, F, seed, turn=None, pipelined=False, clears=None,
-         vocab_levels=5, stereo=False, fps=None, thdepth=None):
+         vocab_levels=5, stereo=False, fps=None, thdepth=None, nseq=None):
     """clears: {frame: [streams]} whose velocity is cleared before that
     frame's step (orbpl_tracker_clear_velocity / MapVO.clear_velocity).
     stereo: KITTI 00 rectified pairs (2000 features) through
     orbpl_tracker_step_stereo / MapVO.step_stereo."""
     clears = clears or {}
+    nseq = nseq or S    # stream s renders sequence seed + (s mod nseq)
     if stereo:
         from _scenes import stereo_sequence
-        seqs = [stereo_sequence(F, seed + s) for s in range(S)]
+        seqs = [stereo_sequence(F, seed + s % nseq) for s in range(S)]
     else:
-        seqs = [sequence(F, seed + s, cam_name="TUM3" if lines else "TUM1") for s in range(S)]
+        seqs = [sequence(F, seed + s % nseq, cam_name="TUM3" if lines else "TUM1") for s in range(S)]
     frames = [[sq[2][f] for f in range(F)] for sq in seqs]
     if turn is not None:
         s, f0 = turn
@@ -249,3 +250,15 @@ def test_map_tracker_stereo_keyframe_after_outliers(orbpl, oracle, lines, pipeli
     assert any(r[f]["ninliers"] < r[f]["nmatches"] for f in range(1, kf[0] + 1)), r
     assert r[kf[0]]["map_points"] > r[0]["map_points"]
     assert all(c["ok"] == 1 for c in r[1:])
+
+
+@pytest.mark.parametrize("groups", ["1/2/3", "1/3/5"])
+def test_map_tracker_level_pipeline_64_streams(orbpl, oracle, monkeypatch, groups):
+    """The ORB level pipeline (per-group pyramid / FAST / octree launches on a
+    second stream, orbpl_runtime.cpp; on for batches of >= 64 frames) forced
+    on (ORBPL_LEVEL_PIPE=1, whatever the box's queue count) in a 64-stream
+    tracker: every stream's counts, poses and map equal the oracle's."""
+    monkeypatch.setenv("ORBPL_LEVEL_PIPE", "1")
+    monkeypatch.setenv("ORBPL_LEVEL_GROUPS", groups)
+    res = _run(orbpl, oracle, False, False, S=64, F=3, seed=190, pipelined=True, nseq=8)
+    assert all(c["ok"] == 1 for r in res for c in r[1:])

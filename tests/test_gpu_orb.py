@@ -113,3 +113,42 @@ def test_batch_device_matches_single(orbpl, synth):
     for i in range(B):
         assert _kp_equal(kraw[i, :n[i]], singles[i][0])
         assert np.array_equal(dd[i, :n[i]], singles[i][1])
+
+
+@pytest.mark.parametrize("pipe,groups", [("1", "1/2/3"), ("1", "1/3/5"), ("1", "2/4/6"),
+                                         ("0", "")])
+def test_level_pipeline_batch_bit_exact(orbpl, synth, monkeypatch, pipe, groups):
+    """A 64-frame batch (the level pipeline's minimum, kLevelPipeMinBatch)
+    with the pipeline forced on (ORBPL_LEVEL_PIPE=1; several ORBPL_LEVEL_GROUPS
+    splits) or off: keypoints, descriptors and counts byte for byte equal to
+    single-frame extraction (itself bit-exact against the oracle above)."""
+    monkeypatch.setenv("ORBPL_LEVEL_PIPE", pipe)
+    if groups:
+        monkeypatch.setenv("ORBPL_LEVEL_GROUPS", groups)
+    B, U = 64, 8
+    uniq = [synth.textured_image(640, 480, seed=60 + i) for i in range(U)]
+    imgs = np.stack([uniq[i % U] if i % 3 else np.ascontiguousarray(uniq[i % U][::-1])
+                     for i in range(B)])
+    ex1 = _extractor(orbpl, (1000, 1.2, 8, 20, 7), 640, 480)
+    singles = {}
+    exb = _extractor(orbpl, (1000, 1.2, 8, 20, 7), 640, 480, batch=B)
+    cap = exb.max_keypoints
+    d_img = orbpl.DeviceBuffer.from_array(imgs)
+    d_kps = orbpl.DeviceBuffer(B * cap * 28)
+    d_desc = orbpl.DeviceBuffer(B * cap * 32)
+    d_n = orbpl.DeviceBuffer(B * 4)
+    for rep in range(2):   # twice: the second batch reuses the group events and streams
+        exb.extract_batch_device(d_img.ptr, B, 640, 640 * 480, d_kps.ptr, d_desc.ptr, cap,
+                                 d_n.ptr)
+        exb.synchronize()
+        n = d_n.download(np.int32, B)
+        kraw = d_kps.download(orbpl.KP_DTYPE, (B, cap))
+        dd = d_desc.download(np.uint8, (B, cap, 32))
+        for i in range(B):
+            key = (i % U, bool(i % 3))
+            if key not in singles:
+                singles[key] = ex1(imgs[i])
+            kp, de = singles[key]
+            assert n[i] == len(kp) > 0, (rep, i)
+            assert _kp_equal(kraw[i, :n[i]], kp), (rep, i)
+            assert np.array_equal(dd[i, :n[i]], de), (rep, i)

@@ -460,13 +460,23 @@ def _log_scale(oracle):
 
 @pytest.mark.parametrize("seed", [1, 2])
 def test_in_frustum_bit_exact(orbpl, oracle, seed):
-    from _scenes import local_map_problem
-    cfg, cam_o, sc, mps, cur, cur_nobs, T3 = local_map_problem(seed)
+    """k_in_frustum against the oracle on a local map in which >= 10 % of the
+    map points fail each IsInFrustum test (Frame.cc:345-401, MapPoint.cc:
+    387-431; _scenes.frustum_reject_problem): behind the camera, outside the
+    image, beyond 1.2 mfMaxDistance, inside 0.8 mfMinDistance, view cosine
+    < 0.5. in_view / level / projections / view cos bit-exact, every
+    branch's points rejected, the rest mostly in view."""
+    from _scenes import frustum_reject_problem
+    cfg, cam_o, sc, mps, cur, cur_nobs, T3, masks = frustum_reject_problem(seed)
     g = orbpl.frame_is_in_frustum(orbpl.make_camera(cfg), 1.2, 8, T3, mps, 0.5)
     o = oracle.frame_is_in_frustum(cam_o, _log_scale(oracle), 8, T3, mps, 0.5)
     for k in o:
         assert np.array_equal(g[k], o[k]), k
-    assert 0.2 * len(mps["xyz"]) < o["in_view"].sum() <= len(mps["xyz"])
+    n = len(mps["xyz"])
+    assert (~o["in_view"].astype(bool)).sum() >= 0.1 * n
+    for b, mk in masks.items():
+        assert mk.sum() > 0 and not o["in_view"][mk].any(), b
+    assert 0.2 * n < o["in_view"].sum() < n
 
 
 def test_predict_scale_hand_computed_gpu(orbpl, oracle):

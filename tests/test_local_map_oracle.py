@@ -68,3 +68,16 @@ def test_predict_scale_hand_computed(oracle):
     k = np.round(np.log(ratio[same]) / np.log(1.2)).astype(int)
     assert tr["level"][same][k == 0].tolist() == [0] * int((k == 0).sum()) and (k == 0).sum() >= 2
     assert np.all(np.abs(tr["level"][same] - k) <= 1)
+
+
+def test_in_frustum_reject_branches(oracle):
+    """The oracle's IsInFrustum rejects every point of each branch subset of
+    frustum_reject_problem (behind, outside, far, near, view cosine) and keeps
+    most of the others (the GPU parity test relies on this problem)."""
+    from _scenes import frustum_reject_problem
+    cfg, cam, sc, mps, cur, cur_nobs, T, masks = frustum_reject_problem(1)
+    iv = oracle.frame_is_in_frustum(cam, _log_scale(oracle), 8, T, mps, 0.5)["in_view"].astype(bool)
+    rest = ~np.any(np.stack(list(masks.values())), 0)
+    for b, mk in masks.items():
+        assert mk.sum() > 0 and not iv[mk].any(), b
+    assert iv[rest].mean() > 0.9

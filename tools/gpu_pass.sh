@@ -36,7 +36,7 @@ for step in "$@"; do
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
       tail -1 $O/smoke.log ;;
     bench)
-      timeout -k 10 1000 python -u bench.py ${arg//,/ } > $O/bench_$n.json 2> $O/bench_$n.err || { echo "bench failed"; tail -20 $O/bench_$n.err; exit 1; }
+      timeout -k 10 1000 python -u bench.py --detail gpurun_out/$tag/bench_detail_$n.json ${arg//,/ } > $O/bench_$n.json 2> $O/bench_$n.err || { echo "bench failed"; tail -20 $O/bench_$n.err; exit 1; }
       tail -c 400 $O/bench_$n.json ;;
     prof)
       MODE=$arg bash tools/prof.sh ${tag}_$arg || exit 1 ;;

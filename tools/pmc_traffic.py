@@ -44,11 +44,20 @@ def main():
     out = {}
     # per kernel, its launches in dispatch order: (duration, grid threads)
     launches = collections.defaultdict(list)
-    for r in sorted(csv.DictReader(open(base / "trace" / "run_kernel_trace.csv")),
-                    key=lambda r: int(r["Dispatch_Id"])):
+    rows = sorted(csv.DictReader(open(base / "trace" / "run_kernel_trace.csv")),
+                  key=lambda r: int(r["Dispatch_Id"]))
+    # the bench workload's window: from the tracker's reset (k_map_reset, the
+    # map model every bench leg runs) on; the vocabulary training's one-frame
+    # extractions before it are left out
+    starts = [int(r["Dispatch_Id"]) for r in rows if short(r["Kernel_Name"]) == "k_map_reset"]
+    d0 = starts[0] if starts else None
+    if d0 is None:
+        print("pmc_traffic: WARNING no k_map_reset launch: keeping launches with grids "
+              ">= 1/10 of the kernel's largest", file=sys.stderr)
+    for r in rows:
         grid = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
         launches[short(r["Kernel_Name"])].append(
-            (int(r["End_Timestamp"]) - int(r["Start_Timestamp"]), grid))
+            (int(r["End_Timestamp"]) - int(r["Start_Timestamp"]), grid, int(r["Dispatch_Id"])))
     cnt = {}
     for part in ("fetch", "write"):
         vals = collections.defaultdict(list)
@@ -60,11 +69,14 @@ def main():
         if "rocclr" in k:
             continue
         # the bench workload's launches only: the runs dispatch the same
-        # sequence, so the i-th launch of a kernel is the same in every pass;
-        # the one-frame launches of the vocabulary training before the timed
-        # region (grids ~1/1000 of the batch's) are left out
-        gmax = max(g for _, g in v)
-        keep = [i for i, (_, g) in enumerate(v) if g >= gmax // 10]
+        # sequence, so the i-th launch of a kernel is the same in every pass
+        if d0 is not None:
+            keep = [i for i, (_, _, di) in enumerate(v) if di >= d0]
+        else:
+            gmax = max(g for _, g, _ in v)
+            keep = [i for i, (_, g, _) in enumerate(v) if g >= gmax // 10]
+        if not keep:
+            continue
         f = cnt["fetch"].get(k, [])
         w = cnt["write"].get(k, [])
         if len(f) == len(v):
@@ -77,7 +89,6 @@ def main():
         out[k] = {"launches": len(d), "avg_ns": sum(d) / len(d),
                   "fetch_bytes": fb, "write_bytes": wb,
                   "traffic_bytes": (fb + wb) if fb is not None and wb is not None else None}
-    dur = {k: [0] * out[k]["launches"] for k in out}
     # the ORB level pipeline launches k_pyramid, k_fast_cells, k_octree and
     # k_orient_desc once per group of levels: their entries are per step (the
     # sum over a step's group launches, "group_launches" of them)
@@ -86,6 +97,9 @@ def main():
     steps = out.get("k_frame_prepare", {}).get("launches", 0)
     for k in ("k_pyramid", "k_fast_cells", "k_octree", "k_orient_desc"):
         e = out.get(k)
+        if e and steps and e["launches"] > steps and e["launches"] % steps != 0:
+            print(f"pmc_traffic: WARNING {k}: {e['launches']} launches is not a multiple of "
+                  f"the {steps} steps; left per launch", file=sys.stderr)
         if e and steps and e["launches"] > steps and e["launches"] % steps == 0:
             m = e["launches"] // steps
             e["group_launches"] = m

@@ -14,7 +14,7 @@ cd /tmp && export TMPDIR=/tmp
 # the bench's hardware queue count, set before rocprofv3 starts the runtime
 export GPU_MAX_HW_QUEUES=16
 R=$GRAFT_REPO_ROOT
-COMMON="--no-cpu-baseline --no-parity --sweep 0 --secondary-steps 0 --stereo-steps 0 --rig-steps 0 --isolated-steps 0 --ingress-steps 0"
+COMMON="--detail gpurun_out/prof_$tag/bench_detail.json --no-cpu-baseline --no-parity --sweep 0 --secondary-steps 0 --stereo-steps 0 --rig-steps 0 --isolated-steps 0 --ingress-steps 0"
 case "$MODE" in
   lines) B="$R/bench.py --workload lines --streams 3072 --steps 3 --warmup 1 $COMMON" ;;
   kitti) B="$R/bench.py --workload kitti --streams 1024 --steps 3 --warmup 1 $COMMON" ;;
