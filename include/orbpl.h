@@ -675,6 +675,43 @@ int orbl_search_by_projection_list(const orbpl_camera* cam, const float* Tcw, in
                                    const int32_t* cur_nobs, int nml, const uint8_t* valid,
                                    const float* ml_xyz6, const uint8_t* ml_desc, int32_t* match,
                                    int* nmatches, int* wiped);
+/* The reference's harness overloads, which also return new_kls (the
+ * projected, clipped KeyLines, appended by the caller) and match_indices
+ * (every passing (projected i, current j) pair; the relaxed retry clears
+ * them): mode 0 = SearchByProjection(Frame&, const Frame&, new_kls,
+ * match_indices) (include/LineMatcher.h:51, LineMatcher.cpp:272-487, called by
+ * Test/LastFrameProjection.cpp:293): projected KeyLines are copies of
+ * base_kl[i] (LastFrame.mvKeyLinesUn) rebuilt by UpdateKeyLineData,
+ * Observations() > 0 is tested per pair on the map line current line j holds
+ * at that moment (cur_nobs initially, ml_nobs of a map line a pass assigned),
+ * retry when matches * 1.0 / NL < 0.2; mode 1 = SearchByProjection(Frame&,
+ * const vector<MapLine*>&, new_kls, match_indices) (LineMatcher.h:66,
+ * LineMatcher.cpp:954-1170, Test/LocalMapProjectionTest.cpp:334): fresh
+ * (zeroed) KeyLines, the Observations() skip per current line, retry when
+ * matches <= 0.2 NL. valid = mvpMapLines[i] && !mvbLineOutlier[i] && !isBad()
+ * (mode 0) / mbTrackInView && !isBad() (mode 1). Outputs: proj_kl / proj_src
+ * (nml capacity; *nproj), pairs as int (i, j) (pair_cap capacity; *npairs =
+ * the full count), match[j] = map line assigned by the final pass or -1,
+ * *wiped = 1 when the retry ran (every assignment cleared first). cur_nobs,
+ * base_kl and ml_nobs may be NULL. (LineMatcher.h:59 declares a reference-
+ * keyframe variant the reference never defines.) */
+int orbl_search_by_projection_pairs(const orbpl_camera* cam, const float* Tcw, int mode, int ncur,
+                                    const orbpl_keyline* cur_kl_un, const uint8_t* cur_desc,
+                                    const int32_t* cur_nobs, int nml, const uint8_t* valid,
+                                    const orbpl_keyline* base_kl, const float* ml_xyz6,
+                                    const uint8_t* ml_desc, const int32_t* ml_nobs,
+                                    orbpl_keyline* proj_kl, int32_t* proj_src, int* nproj,
+                                    int32_t* pairs, int pair_cap, int* npairs, int32_t* match,
+                                    int* nmatches, int* wiped);
+/* SearchByProjection(Frame&, KeyFrame*, vector<MapLine*>& vpMapLineMatches)
+ * (LineMatcher.h:56, LineMatcher.cpp:492-525): cv::BFMatcher(NORM_HAMMING)
+ * knnMatch(keyframe line descriptors = queries, current line descriptors =
+ * train, k = 2) and best / second < 0.75 (float): out[j] = the last query
+ * whose best train line is j, or -1; *nmatches counts every passing query.
+ * Ties go to the lower train index; a query with fewer than two train lines
+ * has no match (pinned: the reference reads past the end). nq <= 256. */
+int orbl_match_bf_knn(int nq, const uint8_t* qdesc, int nt, const uint8_t* tdesc, int32_t* out,
+                      int* nmatches);
 
 /* ------------------------------------------------------------------------
  * Hamming distance — ORBmatcher::DescriptorDistance (ORBmatcher.cc:2083-2103)

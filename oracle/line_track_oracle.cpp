@@ -286,7 +286,189 @@ static int line_search_core(const orbpl_camera* cam, const float* Tcw, int ncur,
 }
 }  // namespace line_track
 
+namespace line_track {
+// The projection + clipping + KeyLine rebuild of line_search_core, alone
+// (projected KeyLines in map-line order and their map-line index).
+static void project_lines(const orbpl_camera* cam, const float* Tcw, int nml, const uint8_t* valid,
+                          const orbpl_keyline* base_kl, const float* ml_xyz6,
+                          std::vector<orbpl_keyline>& nk, std::vector<int>& nidx) {
+  const int W = cam->width, H = cam->height;
+  double T[12];
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 4; c++) T[r * 4 + c] = Tcw[r * 4 + c];
+  float b4[4];
+  oracle_image_bounds(cam, b4);
+  const float bounds[4] = {b4[0], b4[2], b4[1], b4[3]};
+  for (int i = 0; i < nml; i++) {
+    if (!valid[i]) continue;
+    double cs[3], ce[3];
+    for (int r = 0; r < 3; r++) {
+      cs[r] = (T[r * 4] * (double)ml_xyz6[6 * i] + T[r * 4 + 1] * (double)ml_xyz6[6 * i + 1] +
+               T[r * 4 + 2] * (double)ml_xyz6[6 * i + 2]) + T[r * 4 + 3];
+      ce[r] = (T[r * 4] * (double)ml_xyz6[6 * i + 3] + T[r * 4 + 1] * (double)ml_xyz6[6 * i + 4] +
+               T[r * 4 + 2] * (double)ml_xyz6[6 * i + 5]) + T[r * 4 + 3];
+    }
+    if (cs[2] < 0 && ce[2] < 0) continue;
+    double lp[4];
+    bool have = false;
+    if (cs[2] < 0.0 || ce[2] < 0.0) {
+      const double lambda = -1.0 * cs[2] / (cs[2] - ce[2]);
+      const double xc = cs[0] + lambda * (cs[0] - ce[0]);
+      const double yc = cs[1] + lambda * (cs[1] - ce[1]);
+      if (cs[2] < 0.0) {
+        const float u_end = cam->fx * ce[0] / ce[2] + cam->cx;
+        const float v_end = cam->fy * ce[1] / ce[2] + cam->cy;
+        lp[0] = xc; lp[1] = yc; lp[2] = u_end; lp[3] = v_end;
+      } else {
+        const float u_start = cam->fx * cs[0] / cs[2] + cam->cx;
+        const float v_start = cam->fy * cs[1] / cs[2] + cam->cy;
+        lp[0] = u_start; lp[1] = v_start; lp[2] = xc; lp[3] = yc;
+      }
+      have = true;
+    }
+    if (cs[2] > 0.0 && ce[2] > 0.0) {
+      const float u_start = cam->fx * cs[0] / cs[2] + cam->cx;
+      const float v_start = cam->fy * cs[1] / cs[2] + cam->cy;
+      const float u_end = cam->fx * ce[0] / ce[2] + cam->cx;
+      const float v_end = cam->fy * ce[1] / ce[2] + cam->cy;
+      lp[0] = u_start; lp[1] = v_start; lp[2] = u_end; lp[3] = v_end;
+      have = true;
+    }
+    if (!have) continue;
+    double nl4[4];
+    if (!liang_barsky(lp, nl4, bounds)) continue;
+    orbpl_keyline k{};
+    if (base_kl) k = base_kl[i];
+    k.startPointX = (float)nl4[0];
+    k.startPointY = (float)nl4[1];
+    k.endPointX = (float)nl4[2];
+    k.endPointY = (float)nl4[3];
+    k.sPointInOctaveX = (float)nl4[0];
+    k.sPointInOctaveY = (float)nl4[1];
+    k.ePointInOctaveX = (float)nl4[2];
+    k.ePointInOctaveY = (float)nl4[3];
+    refresh_keyline(k, W, H);
+    nk.push_back(k);
+    nidx.push_back(i);
+  }
+}
+}  // namespace line_track
+
 extern "C" {
+
+// The reference's two defined harness overloads of SearchByProjection (the
+// ones its Test/ demos call), which also return the projected KeyLines
+// (new_kls, appended) and every passing (projected index, current index) pair
+// (match_indices, cleared by the relaxed retry):
+//   mode 0: (Frame&, const Frame&, new_kls, match_indices), LineMatcher.cpp:
+//     272-487 (Test/LastFrameProjection.cpp:293): projected KeyLines are copies
+//     of the last frame's (base_kl) rebuilt by UpdateKeyLineData; the
+//     Observations() > 0 skip is tested per PAIR, on the map line the current
+//     line holds at that moment (cur_nobs initially, then ml_nobs of the map
+//     line a pass assigned); retry when matches * 1.0 / NL < 0.2;
+//   mode 1: (Frame&, const vector<MapLine*>&, new_kls, match_indices), :954-
+//     1170 (Test/LocalMapProjectionTest.cpp:334): fresh KeyLines (pinned to
+//     zero-initialised fields before UpdateKeyLineData, base_kl ignored); the
+//     skip is tested once per current line, before its pairs; retry when
+//     matches <= 0.2 * NL.
+// valid: mode 0 mvpMapLines[i] && !mvbLineOutlier[i] && !isBad(); mode 1
+// mbTrackInView && !isBad(). match[j] = map line assigned to current line j
+// by the final pass (-1: none; the caller keeps its line unless *wiped).
+// Outputs: proj_kl / proj_src (nml capacity, *nproj written), pairs as
+// (i, j) int pairs (pair_cap capacity, *npairs = the full count).
+int oracle_line_search_pairs(const orbpl_camera* cam, const float* Tcw, int mode, int ncur,
+                             const orbpl_keyline* cur_kl_un, const uint8_t* cur_desc,
+                             const int32_t* cur_nobs, int nml, const uint8_t* valid,
+                             const orbpl_keyline* base_kl, const float* ml_xyz6,
+                             const uint8_t* ml_desc, const int32_t* ml_nobs,
+                             orbpl_keyline* proj_kl, int32_t* proj_src, int* nproj,
+                             int32_t* pairs, int pair_cap, int* npairs, int32_t* match,
+                             int* nmatches_out, int* wiped) {
+  using namespace line_track;
+  std::vector<orbpl_keyline> nk;
+  std::vector<int> nidx;
+  project_lines(cam, Tcw, nml, valid, mode == 0 ? base_kl : nullptr, ml_xyz6, nk, nidx);
+  *nproj = (int)nk.size();
+  for (size_t i = 0; i < nk.size(); i++) {
+    proj_kl[i] = nk[i];
+    proj_src[i] = nidx[i];
+  }
+  std::vector<int> cnobs(ncur > 0 ? ncur : 1, 0);
+  for (int j = 0; j < ncur; j++) cnobs[j] = cur_nobs ? cur_nobs[j] : 0;
+  std::vector<int> pr;
+  auto run = [&](const double off[5]) {
+    int cnt = 0;
+    pr.clear();
+    for (int j = 0; j < ncur; j++) {
+      match[j] = -1;
+      if (mode == 1 && cnobs[j] > 0) continue;
+      for (size_t i = 0; i < nk.size(); i++) {
+        if (mode == 0 && cnobs[j] > 0) continue;
+        if (line_matching(nk[i], cur_kl_un[j], ml_desc + 32 * nidx[i], cur_desc + 32 * j, off)) {
+          match[j] = nidx[i];
+          cnobs[j] = ml_nobs ? ml_nobs[nidx[i]] : 0;
+          pr.push_back((int)i);
+          pr.push_back(j);
+          cnt++;
+        }
+      }
+    }
+    return cnt;
+  };
+  const double off0[5] = {0, 0, 0, 0, 0};
+  int n = run(off0);
+  *wiped = 0;
+  const bool retry = mode == 0 ? (n * 1.0 / ncur < 0.2) : (n <= 0.2 * ncur);
+  if (retry) {
+    const double off1[5] = {10.0, -0.1, -0.1, 5, 10};
+    std::fill(cnobs.begin(), cnobs.end(), 0);   // mvpMapLines wiped to NULL
+    n = run(off1);
+    *wiped = 1;
+  }
+  *nmatches_out = n;
+  *npairs = (int)pr.size() / 2;
+  for (int k = 0; k < std::min(*npairs, pair_cap); k++) {
+    pairs[2 * k] = pr[2 * k];
+    pairs[2 * k + 1] = pr[2 * k + 1];
+  }
+  return 0;
+}
+
+// LineMatcher::SearchByProjection(Frame&, KeyFrame*, vector<MapLine*>&)
+// (LineMatcher.cpp:492-525): cv::BFMatcher(NORM_HAMMING).knnMatch(keyframe
+// line descriptors, current line descriptors, k = 2); per query (keyframe
+// line q, in order) with a best and a second match, best.distance /
+// second.distance < 0.75 (float) assigns keyframe line q to the best train
+// line (a later query overwrites) and counts. knnMatch keeps the two smallest
+// distances in train order with ties to the lower train index (EXTERNAL:
+// OpenCV batchDistance insertion, strict <). A query with fewer than two train
+// descriptors has no second match (the reference reads past the end: pinned
+// to no match). out[j] = keyframe line assigned to current line j, or -1.
+int oracle_line_match_bf_knn(int nq, const uint8_t* qdesc, int nt, const uint8_t* tdesc,
+                             int32_t* out, int* nmatches_out) {
+  for (int j = 0; j < nt; j++) out[j] = -1;
+  int n = 0;
+  for (int q = 0; q < nq; q++) {
+    int b = -1, s = -1, db = 0, ds = 0;
+    for (int j = 0; j < nt; j++) {
+      const int d = line_track::popcnt_dist(qdesc + 32 * q, tdesc + 32 * j);
+      if (b < 0 || d < db) {
+        s = b; ds = db;
+        b = j; db = d;
+      } else if (s < 0 || d < ds) {
+        s = j; ds = d;
+      }
+    }
+    if (s < 0) continue;
+    const float ratio = (float)db / (float)ds;
+    if (ratio < 0.75f) {
+      out[b] = q;
+      n++;
+    }
+  }
+  *nmatches_out = n;
+  return 0;
+}
 
 // LineMatcher(0.9, true).SearchByProjection(CurrentFrame, LastFrame)
 // Tcw: current pose (16 floats). Last frame map lines: has_ml[i], outlier[i],

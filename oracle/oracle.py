@@ -512,6 +512,9 @@ def _setup(L):  # noqa: F811
     L.oracle_line_search_by_projection_list.argtypes = [vp, vp, i, vp, vp, vp, i, vp, vp, vp, vp,
                                                         ip, ip]
     L.oracle_line_is_in_frustum.argtypes = [vp, i, vp, vp]
+    L.oracle_line_search_pairs.argtypes = [vp, vp, i, i, vp, vp, vp, i, vp, vp, vp, vp, vp, vp, vp,
+                                           ip, vp, i, ip, vp, ip, ip]
+    L.oracle_line_match_bf_knn.argtypes = [i, vp, i, vp, vp, ip]
     L.oracle_stereo_line_depths.argtypes = [vp, vp, vp, i, vp, vp, i, vp, vp]
     L.oracle_lvo_create.argtypes = [vp, vp, i, i]
     L.oracle_lvo_create.restype = vp
@@ -573,6 +576,43 @@ def line_search_by_projection_last(cam, Tcw, cur_kl_un, cur_desc, last_kl_un, ha
                                                 _p(keep[5]), _p(keep[6]), _p(keep[7]), _p(match),
                                                 C.byref(nm))
     return match[:ncur].copy(), nm.value
+
+
+def line_search_pairs(cam, Tcw, mode, cur_kl_un, cur_desc, cur_nobs, valid, base_kl, ml_xyz6,
+                      ml_desc, ml_nobs):
+    """The harness overloads of LineMatcher::SearchByProjection that also
+    return new_kls and match_indices (oracle_line_search_pairs; mode 0 =
+    LineMatcher.cpp:272-487 last frame, 1 = :954-1170 local map). Returns
+    (match, nmatches, wiped, proj_kl, proj_src, pairs (npairs, 2))."""
+    keep = [_c(Tcw, np.float32), _c(cur_kl_un, KEYLINE_DTYPE), _c(cur_desc, np.uint8),
+            _c(valid, np.uint8), _c(ml_xyz6, np.float32), _c(ml_desc, np.uint8)]
+    cn = None if cur_nobs is None else _c(cur_nobs, np.int32)
+    mn = None if ml_nobs is None else _c(ml_nobs, np.int32)
+    bk = None if base_kl is None else _c(base_kl, KEYLINE_DTYPE)
+    ncur, nml = len(keep[1]), len(keep[3])
+    match = np.zeros(max(1, ncur), np.int32)
+    pk = np.zeros(max(1, nml), KEYLINE_DTYPE)
+    ps = np.zeros(max(1, nml), np.int32)
+    cap = max(1, ncur * nml)
+    pairs = np.zeros((cap, 2), np.int32)
+    nm, wiped, npj, npr = C.c_int(0), C.c_int(0), C.c_int(0), C.c_int(0)
+    lib().oracle_line_search_pairs(
+        C.byref(cam), _p(keep[0]), mode, ncur, _p(keep[1]), _p(keep[2]),
+        None if cn is None else _p(cn), nml, _p(keep[3]), None if bk is None else _p(bk),
+        _p(keep[4]), _p(keep[5]), None if mn is None else _p(mn), _p(pk), _p(ps), C.byref(npj),
+        _p(pairs), cap, C.byref(npr), _p(match), C.byref(nm), C.byref(wiped))
+    return (match[:ncur].copy(), nm.value, bool(wiped.value), pk[:npj.value].copy(),
+            ps[:npj.value].copy(), pairs[:npr.value].copy())
+
+
+def line_match_bf_knn(qdesc, tdesc):
+    """LineMatcher::SearchByProjection(Frame&, KeyFrame*, vector<MapLine*>&)'s
+    knnMatch(k = 2) + 0.75 ratio (LineMatcher.cpp:492-525): (out, n)."""
+    q, t = _c(qdesc, np.uint8), _c(tdesc, np.uint8)
+    out = np.zeros(max(1, len(t)), np.int32)
+    n = C.c_int(0)
+    lib().oracle_line_match_bf_knn(len(q), _p(q), len(t), _p(t), _p(out), C.byref(n))
+    return out[:len(t)].copy(), n.value
 
 
 TRACK_LINES, TRACK_STEREO, TRACK_LOCAL_MAP, TRACK_FIXED_LINE_JAC, TRACK_REFKF = 1, 2, 4, 8, 16

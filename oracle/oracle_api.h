@@ -89,6 +89,16 @@ int oracle_line_search_by_projection_list(const orbpl_camera* cam, const float* 
                                           const int32_t* cur_nobs, int nml, const uint8_t* valid,
                                           const float* ml_xyz6, const uint8_t* ml_desc,
                                           int32_t* match, int* nmatches_out, int* wiped);
+int oracle_line_search_pairs(const orbpl_camera* cam, const float* Tcw, int mode, int ncur,
+                             const orbpl_keyline* cur_kl_un, const uint8_t* cur_desc,
+                             const int32_t* cur_nobs, int nml, const uint8_t* valid,
+                             const orbpl_keyline* base_kl, const float* ml_xyz6,
+                             const uint8_t* ml_desc, const int32_t* ml_nobs,
+                             orbpl_keyline* proj_kl, int32_t* proj_src, int* nproj,
+                             int32_t* pairs, int pair_cap, int* npairs, int32_t* match,
+                             int* nmatches_out, int* wiped);
+int oracle_line_match_bf_knn(int nq, const uint8_t* qdesc, int nt, const uint8_t* tdesc,
+                             int32_t* out, int* nmatches_out);
 int oracle_stereo_line_depths(const orbpl_camera* cam, const orbpl_keyline* kl,
                               const uint8_t* desc, int nl, const orbpl_keyline* kr,
                               const uint8_t* desc_r, int nr, float* dstart, float* dend);

@@ -426,6 +426,9 @@ def _declare_track(L):
     L.orbm_search_by_projection_local.argtypes = [vp, vp, i, vp, i, vp, vp, vp, vp, vp, vp, vp, vp,
                                                   vp, C.c_float, C.c_float, vp, ip]
     L.orbl_search_by_projection_last.argtypes = [vp, vp, i, vp, vp, i, vp, vp, vp, vp, vp, vp, ip]
+    L.orbl_search_by_projection_pairs.argtypes = [vp, vp, i, i, vp, vp, vp, i, vp, vp, vp, vp, vp,
+                                                  vp, vp, ip, vp, i, ip, vp, ip, ip]
+    L.orbl_match_bf_knn.argtypes = [i, vp, i, vp, vp, ip]
     L.orbpl_tracker_get_status.argtypes = [vp, vp, vp, vp, vp]
     L.orbpl_tracker_get_lines.argtypes = [vp, i, vp, vp, vp, vp, ip]
     L.orbpl_tracker_line_timings.argtypes = [vp, i, vp, ip]
@@ -664,6 +667,48 @@ class LineMatcher:
             _ptr(keep[3]), _ptr(keep[4]), _ptr(keep[5]), _ptr(keep[6]), _ptr(keep[7]), _ptr(match),
             C.byref(nm)), "orbl_search_by_projection_last")
         return match[:ncur].copy(), nm.value
+
+
+    @staticmethod
+    def SearchByProjectionPairs(camera, Tcw, mode, cur_kl_un, cur_desc, cur_nobs, valid, base_kl,
+                                ml_xyz6, ml_desc, ml_nobs):
+        """The reference's harness overloads (orbl_search_by_projection_pairs;
+        mode 0 = (Frame&, const Frame&, new_kls, match_indices), 1 = (Frame&,
+        const vector<MapLine*>&, new_kls, match_indices)): (match, nmatches,
+        wiped, new_kls, their map-line index, match_indices (n, 2))."""
+        keep = [np.ascontiguousarray(Tcw, np.float32), np.ascontiguousarray(cur_kl_un, KEYLINE_DTYPE),
+                np.ascontiguousarray(cur_desc, np.uint8), np.ascontiguousarray(valid, np.uint8),
+                np.ascontiguousarray(ml_xyz6, np.float32), np.ascontiguousarray(ml_desc, np.uint8)]
+        cn = None if cur_nobs is None else np.ascontiguousarray(cur_nobs, np.int32)
+        mn = None if ml_nobs is None else np.ascontiguousarray(ml_nobs, np.int32)
+        bk = None if base_kl is None else np.ascontiguousarray(base_kl, KEYLINE_DTYPE)
+        ncur, nml = len(keep[1]), len(keep[3])
+        match = np.zeros(max(1, ncur), np.int32)
+        pk = np.zeros(max(1, nml), KEYLINE_DTYPE)
+        ps = np.zeros(max(1, nml), np.int32)
+        cap = max(1, ncur * nml)
+        pairs = np.zeros((cap, 2), np.int32)
+        nm, wiped, npj, npr = C.c_int(0), C.c_int(0), C.c_int(0), C.c_int(0)
+        check(lib().orbl_search_by_projection_pairs(
+            C.byref(camera), _ptr(keep[0]), mode, ncur, _ptr(keep[1]), _ptr(keep[2]),
+            None if cn is None else _ptr(cn), nml, _ptr(keep[3]), None if bk is None else _ptr(bk),
+            _ptr(keep[4]), _ptr(keep[5]), None if mn is None else _ptr(mn), _ptr(pk), _ptr(ps),
+            C.byref(npj), _ptr(pairs), cap, C.byref(npr), _ptr(match), C.byref(nm),
+            C.byref(wiped)), "orbl_search_by_projection_pairs")
+        return (match[:ncur].copy(), nm.value, bool(wiped.value), pk[:npj.value].copy(),
+                ps[:npj.value].copy(), pairs[:npr.value].copy())
+
+    @staticmethod
+    def MatchBFKnn(qdesc, tdesc):
+        """SearchByProjection(Frame&, KeyFrame*, vector<MapLine*>&)'s knnMatch
+        + 0.75 ratio (orbl_match_bf_knn): (out, nmatches)."""
+        q = np.ascontiguousarray(qdesc, np.uint8)
+        t = np.ascontiguousarray(tdesc, np.uint8)
+        out = np.zeros(max(1, len(t)), np.int32)
+        n = C.c_int(0)
+        check(lib().orbl_match_bf_knn(len(q), _ptr(q), len(t), _ptr(t), _ptr(out), C.byref(n)),
+              "orbl_match_bf_knn")
+        return out[:len(t)].copy(), n.value
 
 
 def line_is_in_frustum(Tcw, ml_xyz6):

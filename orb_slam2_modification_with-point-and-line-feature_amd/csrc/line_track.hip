@@ -528,6 +528,159 @@ __global__ void __launch_bounds__(256) k_line_match_list(TrackConsts c, LineList
   }
 }
 
+// The reference's harness overloads of SearchByProjection that also return
+// new_kls and match_indices (LineMatcher.cpp:272-487 = mode 0, last frame;
+// :954-1170 = mode 1, local map; restated in oracle_line_search_pairs). One
+// 256-thread block: the valid map lines are projected, clipped and rebuilt in
+// map-line order (mode 0 on a copy of base_kl[i], mode 1 on a zeroed KeyLine),
+// every (projected, current) pair's LineMatching verdict is a bit in global
+// scratch, then one thread walks the bits in the reference's loop order
+// (current j, projected i) with its Observations() bookkeeping: mode 0 skips a
+// pair once line j holds a map line with Observations() > 0 (tested per pair,
+// on the map line held at that moment), mode 1 skips line j when it starts
+// with one. Retry: mode 0 matches * 1.0 / NL < 0.2, mode 1 matches <= 0.2 NL;
+// the retry wipes every assignment (and the pairs) and walks the relaxed bits.
+__global__ void __launch_bounds__(256) k_line_pairs(TrackConsts c, LinePairArgs a) {
+  trk_priority();
+  __shared__ int s_wc[4];
+  __shared__ int s_np, s_retry;
+  __shared__ int s_cnobs[kLineKeep];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  double T[12];
+#pragma unroll
+  for (int q = 0; q < 12; q++) T[q] = a.Tcw[q];
+  if (t == 0) s_np = 0;
+  const int ncur = min(a.ncur, kLineKeep);
+  for (int j = t; j < ncur; j += 256) s_cnobs[j] = a.cur_nobs ? a.cur_nobs[j] : 0;
+  __syncthreads();
+  for (int base = 0; base < a.nml; base += 256) {
+    const int i = base + t;
+    orbpl_keyline k{};
+    if (i < a.nml && a.mode == 0 && a.base_kl) k = a.base_kl[i];
+    const bool ok = i < a.nml && a.valid[i] && project_map_line(c, T, a.ml_xyz6 + (long long)i * 6, k);
+    const unsigned long long m = __ballot(ok);
+    if (lane == 0) s_wc[wave] = __popcll(m);
+    __syncthreads();
+    int pos = s_np + __popcll(m & ((1ull << lane) - 1ull));
+    for (int w = 0; w < wave; w++) pos += s_wc[w];
+    if (ok) {
+      a.proj_kl[pos] = k;
+      a.proj_src[pos] = i;
+    }
+    __syncthreads();
+    if (t == 0) s_np += s_wc[0] + s_wc[1] + s_wc[2] + s_wc[3];
+    __syncthreads();
+  }
+  const int np = s_np, words = (np + 31) >> 5;
+  const uint4* cur_desc = reinterpret_cast<const uint4*>(a.cur_desc);
+  const uint4* ml_desc = reinterpret_cast<const uint4*>(a.ml_desc);
+  int npairs = 0;
+  for (int pass = 0; pass < 2; pass++) {
+    const double o0 = pass ? 10.0 : 0, o1 = pass ? -0.1 : 0, o2 = pass ? -0.1 : 0, o3 = pass ? 5 : 0;
+    for (int w = t; w < ncur * words; w += 256) a.okbits[w] = 0u;
+    __syncthreads();
+    for (long long pr = t; pr < (long long)ncur * np; pr += 256) {
+      const int j = (int)(pr / np), i = (int)(pr - (long long)j * np);
+      if (line_matching(a.proj_kl[i], a.cur_kl_un[j], ml_desc + 2 * a.proj_src[i], cur_desc + 2 * j,
+                        o0, o1, o2, o3))
+        atomicOr(a.okbits + (long long)j * words + (i >> 5), 1u << (i & 31));
+    }
+    __threadfence_block();
+    __syncthreads();
+    if (t == 0) {
+      if (pass) for (int j = 0; j < ncur; j++) s_cnobs[j] = 0;   // mvpMapLines wiped
+      int cnt = 0;
+      npairs = 0;
+      for (int j = 0; j < ncur; j++) {
+        a.match[j] = -1;
+        if (a.mode == 1 && s_cnobs[j] > 0) continue;
+        for (int w = 0; w < words; w++) {
+          unsigned b = a.okbits[(long long)j * words + w];
+          while (b) {
+            const int i = w * 32 + __builtin_ctz(b);
+            b &= b - 1u;
+            if (a.mode == 0 && s_cnobs[j] > 0) continue;
+            const int src = a.proj_src[i];
+            a.match[j] = src;
+            s_cnobs[j] = a.ml_nobs ? a.ml_nobs[src] : 0;
+            if (npairs < a.pair_cap) {
+              a.pairs[2 * npairs] = i;
+              a.pairs[2 * npairs + 1] = j;
+            }
+            npairs++;
+            cnt++;
+          }
+        }
+      }
+      s_retry = pass == 0 && (a.mode == 0 ? (cnt * 1.0 / ncur < 0.2) : (cnt <= 0.2 * ncur));
+      *a.nmatches = cnt;
+      *a.npairs = npairs;
+      *a.wiped = pass;
+      *a.nproj = np;
+    }
+    __syncthreads();
+    if (!s_retry) break;
+    __syncthreads();
+  }
+}
+
+void launch_line_pairs(const TrackConsts& c, const LinePairArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_line_pairs, dim3(1), dim3(256), 0, s, c, a);
+}
+
+// LineMatcher::SearchByProjection(Frame&, KeyFrame*, vector<MapLine*>&)
+// (LineMatcher.cpp:492-525; oracle_line_match_bf_knn): thread q finds query
+// q's two nearest train descriptors (knnMatch k = 2: the smaller distance
+// first, ties to the lower train index), then one thread assigns in query
+// order where best / second < 0.75 (float), a later query overwriting.
+__global__ void __launch_bounds__(256) k_line_bf_knn(int nq, const uint8_t* __restrict__ qdesc,
+                                                     int nt, const uint8_t* __restrict__ tdesc,
+                                                     int* __restrict__ out, int* __restrict__ nm) {
+  trk_priority();
+  __shared__ int s_best[256];
+  __shared__ unsigned char s_ok[256];
+  const int q = threadIdx.x;
+  for (int j = q; j < nt; j += 256) out[j] = -1;
+  if (q < nq) {
+    const uint4* a = reinterpret_cast<const uint4*>(qdesc) + 2 * q;
+    const uint4 a0 = a[0], a1 = a[1];
+    int b = -1, s = -1, db = 0, ds = 0;
+    for (int j = 0; j < nt; j++) {
+      const uint4* p = reinterpret_cast<const uint4*>(tdesc) + 2 * j;
+      const uint4 p0 = p[0], p1 = p[1];
+      const int d = __popc(a0.x ^ p0.x) + __popc(a0.y ^ p0.y) + __popc(a0.z ^ p0.z) +
+                    __popc(a0.w ^ p0.w) + __popc(a1.x ^ p1.x) + __popc(a1.y ^ p1.y) +
+                    __popc(a1.z ^ p1.z) + __popc(a1.w ^ p1.w);
+      if (b < 0 || d < db) {
+        s = b;
+        ds = db;
+        b = j;
+        db = d;
+      } else if (s < 0 || d < ds) {
+        s = j;
+        ds = d;
+      }
+    }
+    s_best[q] = b;
+    s_ok[q] = s >= 0 && (float)db / (float)ds < 0.75f;
+  }
+  __syncthreads();
+  if (q == 0) {
+    int n = 0;
+    for (int k = 0; k < nq; k++)
+      if (s_ok[k]) {
+        out[s_best[k]] = k;
+        n++;
+      }
+    *nm = n;
+  }
+}
+
+void launch_line_bf_knn(int nq, const uint8_t* qdesc, int nt, const uint8_t* tdesc, int* out,
+                        int* nm, hipStream_t s) {
+  hipLaunchKernelGGL(k_line_bf_knn, dim3(1), dim3(256), 0, s, nq, qdesc, nt, tdesc, out, nm);
+}
+
 // Frame::IsInFrustum(MapLine*) (Frame.cc:403-430)
 __global__ void k_line_in_frustum(const float* __restrict__ Tcw, int n, const float* __restrict__ xyz6,
                                   uint8_t* __restrict__ in_view) {

@@ -163,6 +163,34 @@ struct LineListArgs {
 };
 void launch_line_match_list(const TrackConsts& c, const LineListArgs& a, hipStream_t s,
                             int nstreams = 1);
+// the reference's harness overloads (k_line_pairs, line_track.hip): one frame
+struct LinePairArgs {
+  const float* Tcw;              // 16 floats
+  int mode;                      // 0: LineMatcher.cpp:272-487, 1: :954-1170
+  int ncur;
+  const orbpl_keyline* cur_kl_un;
+  const uint8_t* cur_desc;
+  const int* cur_nobs;           // optional
+  int nml;
+  const uint8_t* valid;
+  const orbpl_keyline* base_kl;  // mode 0: the last frame's KeyLines (optional)
+  const float* ml_xyz6;
+  const uint8_t* ml_desc;
+  const int* ml_nobs;            // optional: Observations() of each map line
+  orbpl_keyline* proj_kl;        // nml entries
+  int* proj_src;
+  int* nproj;
+  unsigned* okbits;              // ncur x ceil(nml / 32) words of scratch
+  int* pairs;                    // (i, j) pairs, pair_cap of them
+  int pair_cap;
+  int* npairs;
+  int* match;
+  int* nmatches;
+  int* wiped;
+};
+void launch_line_pairs(const TrackConsts& c, const LinePairArgs& a, hipStream_t s);
+void launch_line_bf_knn(int nq, const uint8_t* qdesc, int nt, const uint8_t* tdesc, int* out,
+                        int* nm, hipStream_t s);
 void launch_line_in_frustum(const float* Tcw, int n, const float* xyz6, uint8_t* in_view,
                             hipStream_t s);
 // batched: stream b = blockIdx.y tests n_arr[b] lines at xyz6 + b * pitch * 6

@@ -739,6 +739,121 @@ int orbl_search_by_projection_list(const orbpl_camera* cam, const float* Tcw, in
   return ORBPL_OK;
 }
 
+int orbl_search_by_projection_pairs(const orbpl_camera* cam, const float* Tcw, int mode, int ncur,
+                                    const orbpl_keyline* cur_kl_un, const uint8_t* cur_desc,
+                                    const int32_t* cur_nobs, int nml, const uint8_t* valid,
+                                    const orbpl_keyline* base_kl, const float* ml_xyz6,
+                                    const uint8_t* ml_desc, const int32_t* ml_nobs,
+                                    orbpl_keyline* proj_kl, int32_t* proj_src, int* nproj,
+                                    int32_t* pairs, int pair_cap, int* npairs, int32_t* match,
+                                    int* nmatches, int* wiped) {
+  if (!cam || !Tcw || !nmatches || !nproj || !npairs || !wiped || ncur < 0 || nml < 0 ||
+      pair_cap < 0 || (mode != 0 && mode != 1))
+    return arg_fail("bad argument");
+  if (ncur > kLineKeep) return arg_fail("more key lines than LineExtractor keeps (80)");
+  if ((ncur > 0 && (!cur_kl_un || !cur_desc || !match)) ||
+      (nml > 0 && (!valid || !ml_xyz6 || !ml_desc || !proj_kl || !proj_src)) ||
+      (pair_cap > 0 && !pairs))
+    return arg_fail("NULL line arrays");
+  TrackConsts c;
+  int rc = make_consts(cam, nullptr, nullptr, 1, &c);
+  if (rc) return rc;
+  const size_t L = kLineKeep, M = std::max(1, nml), words = (size_t)(nml + 31) / 32;
+  DBuf dT, dku, dde, dcn, dv, dbk, dx, dmd, dmn, dpk, dps, dnp, dok, dpr, dnpr, dm, dnm, dw;
+  HIP_CHECK(dT.alloc(64));
+  HIP_CHECK(dku.alloc(L * sizeof(orbpl_keyline)));
+  HIP_CHECK(dde.alloc(L * 32));
+  HIP_CHECK(dcn.alloc(L * 4));
+  HIP_CHECK(dv.alloc(M));
+  HIP_CHECK(dbk.alloc(M * sizeof(orbpl_keyline)));
+  HIP_CHECK(dx.alloc(M * 24));
+  HIP_CHECK(dmd.alloc(M * 32));
+  HIP_CHECK(dmn.alloc(M * 4));
+  HIP_CHECK(dpk.alloc(M * sizeof(orbpl_keyline)));
+  HIP_CHECK(dps.alloc(M * 4));
+  HIP_CHECK(dnp.alloc(4));
+  HIP_CHECK(dok.alloc(std::max<size_t>(1, L * words) * 4));
+  HIP_CHECK(dpr.alloc(std::max<size_t>(1, (size_t)pair_cap) * 8));
+  HIP_CHECK(dnpr.alloc(4));
+  HIP_CHECK(dm.alloc(L * 4));
+  HIP_CHECK(dnm.alloc(4));
+  HIP_CHECK(dw.alloc(4));
+  HIP_CHECK(hipMemcpy(dT.p, Tcw, 64, hipMemcpyHostToDevice));
+  if (ncur) {
+    HIP_CHECK(hipMemcpy(dku.p, cur_kl_un, ncur * sizeof(orbpl_keyline), hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dde.p, cur_desc, (size_t)ncur * 32, hipMemcpyHostToDevice));
+    if (cur_nobs) HIP_CHECK(hipMemcpy(dcn.p, cur_nobs, (size_t)ncur * 4, hipMemcpyHostToDevice));
+  }
+  if (nml) {
+    HIP_CHECK(hipMemcpy(dv.p, valid, nml, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dx.p, ml_xyz6, (size_t)nml * 24, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(dmd.p, ml_desc, (size_t)nml * 32, hipMemcpyHostToDevice));
+    if (base_kl)
+      HIP_CHECK(hipMemcpy(dbk.p, base_kl, (size_t)nml * sizeof(orbpl_keyline), hipMemcpyHostToDevice));
+    if (ml_nobs) HIP_CHECK(hipMemcpy(dmn.p, ml_nobs, (size_t)nml * 4, hipMemcpyHostToDevice));
+  }
+  LinePairArgs a{};
+  a.Tcw = dT.as<float>();
+  a.mode = mode;
+  a.ncur = ncur;
+  a.cur_kl_un = dku.as<orbpl_keyline>();
+  a.cur_desc = dde.as<uint8_t>();
+  a.cur_nobs = cur_nobs ? dcn.as<int>() : nullptr;
+  a.nml = nml;
+  a.valid = dv.as<uint8_t>();
+  a.base_kl = base_kl ? dbk.as<orbpl_keyline>() : nullptr;
+  a.ml_xyz6 = dx.as<float>();
+  a.ml_desc = dmd.as<uint8_t>();
+  a.ml_nobs = ml_nobs ? dmn.as<int>() : nullptr;
+  a.proj_kl = dpk.as<orbpl_keyline>();
+  a.proj_src = dps.as<int>();
+  a.nproj = dnp.as<int>();
+  a.okbits = dok.as<unsigned>();
+  a.pairs = dpr.as<int>();
+  a.pair_cap = pair_cap;
+  a.npairs = dnpr.as<int>();
+  a.match = dm.as<int>();
+  a.nmatches = dnm.as<int>();
+  a.wiped = dw.as<int>();
+  launch_line_pairs(c, a, scratch_stream());
+  HIP_CHECK(hipGetLastError());
+  int np = 0, npr = 0;
+  HIP_CHECK(hipMemcpy(&np, dnp.p, 4, hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(&npr, dnpr.p, 4, hipMemcpyDeviceToHost));
+  if (np) {
+    HIP_CHECK(hipMemcpy(proj_kl, dpk.p, (size_t)np * sizeof(orbpl_keyline), hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemcpy(proj_src, dps.p, (size_t)np * 4, hipMemcpyDeviceToHost));
+  }
+  if (std::min(npr, pair_cap) > 0)
+    HIP_CHECK(hipMemcpy(pairs, dpr.p, (size_t)std::min(npr, pair_cap) * 8, hipMemcpyDeviceToHost));
+  if (ncur) HIP_CHECK(hipMemcpy(match, dm.p, (size_t)ncur * 4, hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(nmatches, dnm.p, 4, hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(wiped, dw.p, 4, hipMemcpyDeviceToHost));
+  *nproj = np;
+  *npairs = npr;
+  return ORBPL_OK;
+}
+
+int orbl_match_bf_knn(int nq, const uint8_t* qdesc, int nt, const uint8_t* tdesc, int32_t* out,
+                      int* nmatches) {
+  if (nq < 0 || nt < 0 || !nmatches) return arg_fail("bad argument");
+  if (nq > 256) return arg_fail("more than 256 query descriptors");
+  if ((nq > 0 && !qdesc) || (nt > 0 && (!tdesc || !out))) return arg_fail("NULL descriptor arrays");
+  DBuf dq, dt, dout, dn;
+  HIP_CHECK(dq.alloc(std::max(1, nq) * 32));
+  HIP_CHECK(dt.alloc(std::max(1, nt) * 32));
+  HIP_CHECK(dout.alloc(std::max(1, nt) * 4));
+  HIP_CHECK(dn.alloc(4));
+  if (nq) HIP_CHECK(hipMemcpy(dq.p, qdesc, (size_t)nq * 32, hipMemcpyHostToDevice));
+  if (nt) HIP_CHECK(hipMemcpy(dt.p, tdesc, (size_t)nt * 32, hipMemcpyHostToDevice));
+  launch_line_bf_knn(nq, dq.as<uint8_t>(), nt, dt.as<uint8_t>(), dout.as<int>(), dn.as<int>(),
+                     scratch_stream());
+  HIP_CHECK(hipGetLastError());
+  if (nt) HIP_CHECK(hipMemcpy(out, dout.p, (size_t)nt * 4, hipMemcpyDeviceToHost));
+  HIP_CHECK(hipMemcpy(nmatches, dn.p, 4, hipMemcpyDeviceToHost));
+  return ORBPL_OK;
+}
+
 }  // extern "C"
 
 // ---------------------------------------------------------------------------

@@ -34,6 +34,7 @@ class KeyFrame {
       mpORBvocabulary->transform(toDescriptorVector(mDescriptors), mBowVec, mFeatVec, 4);
   }
   std::vector<MapPoint*> GetMapPointMatches() const { return mvpMapPoints; }
+  std::vector<MapLine*> GetMapLineMatches() const { return mvpMapLines; }
   MapPoint* GetMapPoint(const size_t& idx) const { return mvpMapPoints[idx]; }
   cv::Mat GetPose() const { return Tcw.clone(); }
 

@@ -23,6 +23,14 @@
 //   map from the stereo depths and frame 1's TrackWithMotionModel with zero
 //   velocity and th = 7 (Tracking.cc:1228-1271, points only: the stereo Frame
 //   has no lines); formats at stereo_mode()
+//   dropin_driver --harness <in.bin> <out.bin>: the reference's Test/ demos'
+//   calls (Test/LastFrameProjection.cpp:262-293, LocalMapProjectionTest.cpp:
+//   334): frame 0's map lines from both end-point depths (Observations() = 1
+//   for every third line, 0 otherwise: the fork's harness MapLines have none),
+//   LineMatcher::SearchByProjection(F1, F0, new_kls, match_indices) at frame
+//   0's pose, SearchByProjection(F2, frame 0's map lines with IsInFrustum,
+//   new_kls, match_indices) and SearchByProjection(F2, KF0, vpMapLineMatches);
+//   formats at harness_mode()
 //   dropin_driver --fail: a Frame from an 8x8 image, which the library's
 //   extractors reject: the error must reach the caller as an exception (the
 //   line thread joined first), printed as "caught: <message>", exit 0
@@ -225,6 +233,129 @@ static int stereo_mode(const char* inp, const char* outp) {
   return 0;
 }
 
+// out.bin: per frame 0..2: NL, kl_un (NL x 68 B), line desc (NL x 32);
+// frame 0's map lines: per line has u8, xyz6 f32x6, nobs i32; then
+// A (last frame): Tcw1[16], n, nnew, new_kls (nnew x 68 B), npairs, pairs
+//   (npairs x 2 i32), F1 line match[NL1] (frame-0 index or -1);
+// B (local map): Tcw2[16], in_view[NL0] u8, n, nnew, new_kls, npairs, pairs,
+//   F2 line match[NL2];
+// C (BFMatcher vs KF0): n, vpMapLineMatches[NL2] (frame-0 index or -1).
+static int harness_mode(const char* inp, const char* outp) {
+  FILE* in = fopen(inp, "rb");
+  if (!in) throw std::runtime_error("cannot open input");
+  int32_t wh[2];
+  float camv[11], Tcw0[16];
+  int32_t nf, nl, ini, mn;
+  float sf;
+  rd(in, wh, 2);
+  rd(in, camv, 11);
+  rd(in, &nf, 1);
+  rd(in, &sf, 1);
+  rd(in, &nl, 1);
+  rd(in, &ini, 1);
+  rd(in, &mn, 1);
+  rd(in, Tcw0, 16);
+  const int W = wh[0], H = wh[1];
+  std::vector<cv::Mat> g(3), d(3);
+  for (int k = 0; k < 3; k++) {
+    g[k] = cv::Mat(H, W, cv::CV_8U);
+    d[k] = cv::Mat(H, W, cv::CV_32F);
+    rd(in, g[k].data, (size_t)W * H);
+    rd(in, d[k].ptr<float>(), (size_t)W * H);
+  }
+  fclose(in);
+  cv::Mat K = cv::Mat::eye(3, 3, cv::CV_32F);
+  K.at<float>(0, 0) = camv[0];
+  K.at<float>(1, 1) = camv[1];
+  K.at<float>(0, 2) = camv[2];
+  K.at<float>(1, 2) = camv[3];
+  cv::Mat dist(5, 1, cv::CV_32F);
+  for (int k = 0; k < 5; k++) dist.at<float>(k, 0) = camv[4 + k];
+  ORBextractor ex(nf, sf, nl, ini, mn);
+  std::vector<std::unique_ptr<Frame>> F;
+  for (int k = 0; k < 3; k++)
+    F.emplace_back(new Frame(g[k], d[k], (double)k, &ex, nullptr, K, dist, camv[9], camv[10]));
+  cv::Mat T0(4, 4, cv::CV_32F);
+  std::memcpy(T0.data, Tcw0, 64);
+  for (auto& f : F) f->SetPose(T0);
+  FILE* o = fopen(outp, "wb");
+  if (!o) throw std::runtime_error("cannot open output");
+  for (auto& f : F) {
+    wr(o, &f->NL, 1);
+    wr(o, f->mvKeyLinesUn.data(), f->NL);
+    wr(o, f->mLineDescriptors.data, (size_t)f->NL * 32);
+  }
+  // Test/LastFrameProjection.cpp:262-284
+  Frame& F0 = *F[0];
+  std::vector<std::unique_ptr<MapLine>> mls;
+  std::map<const MapLine*, int> ml_index;
+  for (int j = 0; j < F0.NL; j++) {
+    float v[6] = {0, 0, 0, 0, 0, 0};
+    int32_t nobs = j % 3 == 0 ? 1 : 0;
+    const bool has = F0.mvDepthLineStart[j] > 0 && F0.mvDepthLineEnd[j] > 0;
+    if (has) {
+      cv::Mat s = F0.UnprojectStereoLineStart(j), e = F0.UnprojectStereoLineEnd(j);
+      for (int k = 0; k < 3; k++) {
+        v[k] = s.at<float>(k, 0);
+        v[3 + k] = e.at<float>(k, 0);
+      }
+      mls.emplace_back(new MapLine(v, F0.mLineDescriptors.ptr<uint8_t>(j), nobs));
+      F0.mvpMapLines[j] = mls.back().get();
+      ml_index[mls.back().get()] = j;
+    }
+    wr1<uint8_t>(o, has);
+    wr(o, v, 6);
+    wr1<int32_t>(o, has ? nobs : 0);
+  }
+  auto write_kls = [&](const std::vector<KeyLine>& kls,
+                       const std::vector<std::pair<int, int>>& mi) {
+    const int32_t nn = (int32_t)kls.size(), np = (int32_t)mi.size();
+    wr(o, &nn, 1);
+    wr(o, kls.data(), kls.size());
+    wr(o, &np, 1);
+    for (const auto& p : mi) {
+      wr1<int32_t>(o, p.first);
+      wr1<int32_t>(o, p.second);
+    }
+  };
+  // A: Test/LastFrameProjection.cpp:290-293
+  LineMatcher line_matcher(0.9f, true);
+  Frame& F1 = *F[1];
+  std::fill(F1.mvpMapLines.begin(), F1.mvpMapLines.end(), nullptr);
+  std::vector<KeyLine> new_kls;
+  std::vector<std::pair<int, int>> match_indices;
+  const int32_t nA = line_matcher.SearchByProjection(F1, F0, new_kls, match_indices);
+  wr(o, F1.mTcw.ptr<float>(), 16);
+  wr(o, &nA, 1);
+  write_kls(new_kls, match_indices);
+  write_index(o, F1.mvpMapLines, ml_index);
+  // B: Test/LocalMapProjectionTest.cpp:322-334 (local map = frame 0's lines)
+  Frame& F2 = *F[2];
+  std::vector<MapLine*> local;
+  for (int j = 0; j < F0.NL; j++)
+    if (F0.mvpMapLines[j]) local.push_back(F0.mvpMapLines[j]);
+  wr(o, F2.mTcw.ptr<float>(), 16);
+  std::vector<uint8_t> seen(F0.NL, 0);
+  for (int j = 0; j < F0.NL; j++)
+    if (F0.mvpMapLines[j]) seen[j] = F2.IsInFrustum(F0.mvpMapLines[j], 0.5f);
+  wr(o, seen.data(), seen.size());
+  std::fill(F2.mvpMapLines.begin(), F2.mvpMapLines.end(), nullptr);
+  std::vector<KeyLine> new_kls2;
+  std::vector<std::pair<int, int>> mi2;
+  const int32_t nB = line_matcher.SearchByProjection(F2, local, new_kls2, mi2);
+  wr(o, &nB, 1);
+  write_kls(new_kls2, mi2);
+  write_index(o, F2.mvpMapLines, ml_index);
+  // C: LineMatcher.cpp:492-525 against the keyframe of frame 0
+  KeyFrame KF0(F0);
+  std::vector<MapLine*> vpMapLineMatches;
+  const int32_t nC = line_matcher.SearchByProjection(F2, &KF0, vpMapLineMatches);
+  wr(o, &nC, 1);
+  write_index(o, vpMapLineMatches, ml_index);
+  fclose(o);
+  return 0;
+}
+
 static int fail_mode() {
   ORBextractor ex(1000, 1.2f, 8, 20, 7);
   cv::Mat K = cv::Mat::eye(3, 3, cv::CV_32F);
@@ -249,6 +380,14 @@ static int fail_mode() {
 
 int main(int argc, char** argv) {
   if (argc == 2 && std::string(argv[1]) == "--fail") return fail_mode();
+  if (argc == 4 && std::string(argv[1]) == "--harness") {
+    try {
+      return harness_mode(argv[2], argv[3]);
+    } catch (const std::exception& e) {
+      fprintf(stderr, "dropin_driver: %s\n", e.what());
+      return 1;
+    }
+  }
   if (argc == 4 && std::string(argv[1]) == "--stereo") {
     try {
       return stereo_mode(argv[2], argv[3]);

@@ -372,3 +372,96 @@ def test_dropin_stereo_frame_matches_oracle(tmp_path, seed):
     To, so = lvo.step_stereo(0, l1, r1)
     assert (nm, ninl) == (so["nmatches"], so["ninliers"]) and nm > 100
     assert np.abs(T1 - To).max() < 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cam_name,seed", [("TUM1", 5), ("TUM3", 8)])
+def test_dropin_harness_line_overloads_match_oracle(tmp_path, cam_name, seed):
+    """The reference's Test/ harness calls against the drop-in LineMatcher
+    (dropin_driver --harness): SearchByProjection(F1, F0, new_kls,
+    match_indices) (LineMatcher.cpp:272-487, Test/LastFrameProjection.cpp:293),
+    SearchByProjection(F2, local map lines, new_kls, match_indices) (:954-1170,
+    Test/LocalMapProjectionTest.cpp:334) and SearchByProjection(F2, KF0,
+    vpMapLineMatches) (:492-525): counts, new_kls bytes, match_indices and the
+    frames' map line assignments equal the oracle's (oracle_line_search_pairs,
+    oracle_line_match_bf_knn) on the same lines."""
+    load_pkg()
+    O = load_oracle()
+    assert DRIVER.exists(), "build the drop-in first (make -C .../dropin)"
+    cfg, traj, frames = sequence(3, seed, cam_name=cam_name)
+    H, W = frames[0][0].shape
+    orb = (1000, 1.2, 8, 20, 7)
+    T0 = np.linalg.inv(traj[0]).astype(np.float32)
+    cam = O.camera(cfg)
+    camv = [cfg["fx"], cfg["fy"], cfg["cx"], cfg["cy"], cfg["k1"], cfg["k2"], cfg["p1"],
+            cfg["p2"], cfg["k3"], cam.bf, cam.th_depth]
+    inp = tmp_path / "in.bin"
+    with open(inp, "wb") as f:
+        f.write(struct.pack("<2i", W, H))
+        f.write(np.asarray(camv, np.float32).tobytes())
+        f.write(struct.pack("<ifiii", orb[0], orb[1], orb[2], orb[3], orb[4]))
+        f.write(T0.tobytes())
+        for g, d in frames:
+            f.write(np.ascontiguousarray(g, np.uint8).tobytes())
+            f.write(np.ascontiguousarray(d, np.float32).tobytes())
+    out = tmp_path / "out.bin"
+    r = subprocess.run([str(DRIVER), "--harness", str(inp), str(out)], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    R = _Reader(out.read_bytes())
+    KL = O.KEYLINE_DTYPE
+    fr = []
+    for k in range(3):
+        nl = R.i32()
+        fr.append((R.arr(KL, nl).copy(), R.arr(np.uint8, nl * 32, (nl, 32)).copy()))
+    # the frames' lines are the oracle's (extraction + UndistortKeyLines)
+    for k, (g, d) in enumerate(frames):
+        okl, old, _, _ = O.line_extract(g)
+        oku = O.line_frame_prepare(cam, okl, d)[0]
+        assert fr[k][0].tobytes() == oku.tobytes() and np.array_equal(fr[k][1], old), k
+    nl0 = len(fr[0][0])
+    has = np.zeros(nl0, np.uint8)
+    xyz = np.zeros((nl0, 6), np.float32)
+    nobs = np.zeros(nl0, np.int32)
+    for j in range(nl0):
+        has[j] = R.arr(np.uint8, 1)[0]
+        xyz[j] = R.arr(np.float32, 6)
+        nobs[j] = R.i32()
+    assert has.sum() > 10 and (nobs[has == 1] > 0).any() and (nobs[has == 1] == 0).any()
+
+    def read_search():
+        n = R.i32()
+        nn = R.i32()
+        kls = R.arr(KL, nn).copy()
+        npr = R.i32()
+        pr = R.arr(np.int32, 2 * npr, (npr, 2)).copy() if npr else np.zeros((0, 2), np.int32)
+        return n, kls, pr
+
+    # A: the last-frame harness overload
+    T1 = R.arr(np.float32, 16, (4, 4)).copy()
+    nA, klsA, prA = read_search()
+    mA = R.i32(len(fr[1][0]))
+    m, n, w, pk, ps, pr = O.line_search_pairs(cam, T1, 0, fr[1][0], fr[1][1], None, has,
+                                              fr[0][0], xyz, fr[0][1], nobs)
+    assert nA == n and klsA.tobytes() == pk.tobytes() and np.array_equal(prA, pr)
+    assert np.array_equal(mA, m), (mA, m)
+    assert n > 5
+    # B: the local-map harness overload over frame 0's map lines (index order)
+    T2 = R.arr(np.float32, 16, (4, 4)).copy()
+    seen = R.arr(np.uint8, nl0).copy()
+    iv = O.line_is_in_frustum(T2, xyz)
+    assert np.array_equal(seen[has == 1], iv[has == 1])
+    loc = np.nonzero(has)[0]
+    nB, klsB, prB = read_search()
+    mB = R.i32(len(fr[2][0]))
+    m, n, w, pk, ps, pr = O.line_search_pairs(cam, T2, 1, fr[2][0], fr[2][1], None, iv[loc], None,
+                                              xyz[loc], fr[0][1][loc], nobs[loc])
+    assert nB == n and klsB.tobytes() == pk.tobytes() and np.array_equal(prB, pr)
+    assert np.array_equal(mB, np.where(m >= 0, loc[np.maximum(m, 0)], -1))
+    # C: BFMatcher knnMatch + ratio against the keyframe of frame 0
+    nC = R.i32()
+    mC = R.i32(len(fr[2][0]))
+    o, n = O.line_match_bf_knn(fr[0][1], fr[2][1])
+    assert nC == n > 0
+    assert np.array_equal(mC, np.where((o >= 0) & (has[np.maximum(o, 0)] == 1), o, -1))
+    assert R.off == len(R.buf)

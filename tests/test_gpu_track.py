@@ -784,3 +784,49 @@ def test_tracker_refkf_matches_oracle(orbpl, oracle, lines, local_map, pipelined
             assert [int(x) for x in Ch[f]] == ref, (s, f, list(Ch[f]), ref)
             assert np.abs(Th[f] - To).max() < POSE_TOL, (s, f)
     assert trk_seen >= S + 2    # every stream's first tracked frame, and the failures
+
+
+@pytest.mark.parametrize("mode,case", [(0, "plain"), (0, "observed"), (0, "retry"), (1, "plain"),
+                                       (1, "retry")])
+def test_line_search_pairs_bit_exact(orbpl, oracle, mode, case):
+    """orbl_search_by_projection_pairs (the reference's harness overloads,
+    LineMatcher.cpp:272-487 / 954-1170) against oracle_line_search_pairs:
+    match, count, wiped, the projected KeyLines (new_kls) and every pair
+    (match_indices) byte for byte; 'observed' gives map lines Observations()
+    so the last-frame variant's per-pair skip runs, 'retry' a pose far off."""
+    from _scenes import line_map_problem
+    cfg, cam_o, xyz, desc, ku, ld, cur_nobs, T2 = line_map_problem(5)
+    cam_g = orbpl.make_camera(cfg)
+    n = len(xyz)
+    rng = np.random.default_rng(3)
+    valid = (rng.random(n) < 0.9).astype(np.uint8)
+    base = np.zeros(n, ku.dtype) if mode == 0 else None
+    if mode == 0:
+        base = np.resize(ku, n).copy()
+    ml_nobs = (np.arange(n) % 3 == 0).astype(np.int32) if case == "observed" else None
+    if case == "retry":
+        T2 = T2.copy()
+        T2[:3, 3] += np.float32([0.4, 0.0, 0.2])
+    cn = cur_nobs if mode == 1 else None
+    o = oracle.line_search_pairs(cam_o, T2, mode, ku, ld, cn, valid, base, xyz, desc, ml_nobs)
+    g = orbpl.LineMatcher.SearchByProjectionPairs(cam_g, T2, mode, ku, ld, cn, valid, base, xyz,
+                                                  desc, ml_nobs)
+    assert g[1:3] == o[1:3]
+    assert np.array_equal(g[0], o[0])
+    assert g[3].tobytes() == o[3].tobytes() and np.array_equal(g[4], o[4])
+    assert np.array_equal(g[5], o[5])
+    assert len(o[3]) > 10
+    if case == "retry":
+        assert o[2] and o[1] > 5
+
+
+def test_line_bf_knn_bit_exact(orbpl, oracle):
+    """orbl_match_bf_knn (LineMatcher.cpp:492-525) against the oracle on two
+    frames' LBD rows, both directions."""
+    from _scenes import line_map_problem
+    cfg, cam_o, xyz, desc, ku, ld, cur_nobs, T2 = line_map_problem(5)
+    for q, t in ((desc[:80], ld), (ld, desc[:80])):
+        og, ng = orbpl.LineMatcher.MatchBFKnn(q, t)
+        oo, no = oracle.line_match_bf_knn(q, t)
+        assert ng == no and np.array_equal(og, oo)
+        assert no > 0

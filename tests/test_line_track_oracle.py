@@ -124,3 +124,82 @@ def test_line_in_frustum(oracle):
     T = np.eye(4, dtype=np.float32)
     X = np.array([[0, 0, 1, 0, 0, 2], [0, 0, -1, 0, 0, 2], [0, 0, -1, 0, 0, -2]], np.float32)
     assert oracle.line_is_in_frustum(T, X).tolist() == [1, 1, 0]
+
+
+def test_harness_pairs_overloads(oracle):
+    """The reference's harness overloads (LineMatcher.cpp:272-487 last frame,
+    :954-1170 local map; oracle_line_search_pairs) against the tracking
+    overloads: with no Observations() anywhere they assign the same map lines
+    and count the same matches; match_indices lists every passing pair in
+    (current j, projected i) order, so its last pair per j is the assignment;
+    new_kls are the projected lines in map-line order."""
+    from _scenes import line_map_problem
+    cfg, cam, xyz, desc, ku, ld, cur_nobs, T2 = line_map_problem(4)
+    n = len(xyz)
+    rng = np.random.default_rng(1)
+    has = (rng.random(n) < 0.9).astype(np.uint8)
+    out = (rng.random(n) < 0.1).astype(np.uint8)
+    base = np.zeros(n, ku.dtype)
+    valid = has & (1 - out)
+    m1, n1 = oracle.line_search_by_projection_last(cam, T2, ku, ld, base, has, out, xyz, desc)
+    m, nm, w, pk, ps, pr = oracle.line_search_pairs(cam, T2, 0, ku, ld, None, valid, base, xyz,
+                                                    desc, None)
+    assert nm == n1 > 10 and np.array_equal(m, m1) and len(pr) == nm
+    assert np.all(np.diff(ps) > 0) and np.all(valid[ps] == 1)
+    assert np.all(np.diff(pr[:, 1]) >= 0)                    # j-major
+    for j in np.unique(pr[:, 1]):
+        assert ps[pr[pr[:, 1] == j][-1, 0]] == m[j]           # the last pair wins
+    # local map: the list overload (away from the retry boundary)
+    m2, n2, w2 = oracle.line_search_by_projection_list(cam, T2, ku, ld, cur_nobs, valid, xyz, desc)
+    mb, nb, wb, pkb, psb, prb = oracle.line_search_pairs(cam, T2, 1, ku, ld, cur_nobs, valid, None,
+                                                         xyz, desc, None)
+    assert (nb, wb) == (n2, w2) and np.array_equal(mb, m2) and len(prb) == nb
+    assert np.array_equal(psb, ps)
+    for f in ("startPointX", "startPointY", "endPointX", "endPointY", "lineLength", "angle"):
+        assert np.array_equal(pkb[f], pk[f]), f
+
+
+def test_harness_last_frame_skips_observed_per_pair(oracle):
+    """LineMatcher.cpp:272-487 tests Observations() > 0 inside the pair loop:
+    once a current line holds an observed map line, its later pairs are
+    skipped, so each current line keeps its FIRST passing map line and at
+    most one pair (the tracking overload keeps the last and counts all)."""
+    from _scenes import line_map_problem
+    cfg, cam, xyz, desc, ku, ld, cur_nobs, T2 = line_map_problem(4)
+    n = len(xyz)
+    valid = np.ones(n, np.uint8)
+    base = np.zeros(n, ku.dtype)
+    r0 = oracle.line_search_pairs(cam, T2, 0, ku, ld, None, valid, base, xyz, desc, None)
+    r1 = oracle.line_search_pairs(cam, T2, 0, ku, ld, None, valid, base, xyz, desc,
+                                  np.ones(n, np.int32))
+    m0, n0, _, _, ps, pr0 = r0
+    m1, n1, _, _, _, pr1 = r1
+    assert n1 < n0 and len(pr1) == n1
+    assert len(np.unique(pr1[:, 1])) == len(pr1)              # one pair per current line
+    for j, i in ((j, pr0[pr0[:, 1] == j][0, 0]) for j in np.unique(pr0[:, 1])):
+        assert m1[j] == ps[i]                                 # the first passing map line
+
+
+def test_bf_knn_ratio_hand_computed(oracle):
+    """LineMatcher.cpp:492-525 (BFMatcher knnMatch k = 2, ratio 0.75) on
+    descriptors with hand-set Hamming distances to train lines t0 (no bits),
+    t1 (bits 100-139), t2 (bits 200-255):
+      q0 bits 0-1:      2 / 42 / 58  -> t0 (ratio 0.05)
+      q1 bits 100-121:  22 / 18 / 78 -> t1 18 vs t0 22 (0.82): none
+      q2 bits 100-119 + 200-219: 40 / 40 / 56 -> tie at the best: ratio 1, none
+      q3 bits 100-139:  40 / 0 / 96  -> t1 (zero best)
+      q4 bit 0:         1 / 41 / 57  -> t0 again (overwrites q0, both count)."""
+    def d(bits):
+        v = np.zeros(32, np.uint8)
+        for b in bits:
+            v[b // 8] |= 1 << (b % 8)
+        return v
+    t = np.stack([d([]), d(range(100, 140)), d(range(200, 256))])
+    q = np.stack([d(range(2)), d(range(100, 122)),
+                  d(list(range(100, 120)) + list(range(200, 220))), d(range(100, 140)),
+                  d(range(1))])
+    dist = np.array([[int(np.unpackbits(a ^ b).sum()) for b in t] for a in q])
+    assert dist.tolist() == [[2, 42, 58], [22, 18, 78], [40, 40, 56], [40, 0, 96], [1, 41, 57]]
+    out, n = oracle.line_match_bf_knn(q, t)
+    assert n == 3
+    assert list(out) == [4, 3, -1]

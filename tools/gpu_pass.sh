@@ -5,7 +5,7 @@
 # gpurun_out/<tag>/.
 #   usage: tools/gpu_pass.sh <tag> step [step ...]
 #   host                host facts (CPU model, cgroup quota, affinity)
-#   tests[=<expr>]      the -m gpu suite, or the -m gpu tests matching -k <expr>
+#   tests[=<expr>]      the -m gpu suite, or the -m gpu tests matching -k <expr> (commas = spaces)
 #   smoke               __graft_entry__.smoke()
 #   bench[=<args>]      bench.py <args> (commas become spaces), JSON in bench_<n>.json
 #   prof=<MODE>         tools/prof.sh <tag> with MODE=points|lines|kitti|rig
@@ -28,8 +28,8 @@ for step in "$@"; do
         python3 -c "import os; print('affinity', sorted(os.sched_getaffinity(0)))"; } > $O/host.txt 2>&1
       echo "host: $(grep 'Model name' $O/host.txt | head -1)" ;;
     tests)
-      K=""; [ -n "$arg" ] && K="-k $arg"
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread $K > $O/gpu_tests_$n.log 2>&1
+      K=(); [ -n "$arg" ] && K=(-k "${arg//,/ }")
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${K[@]}" > $O/gpu_tests_$n.log 2>&1
       rc=$?; echo "tests($arg) exit $rc: $(tail -1 $O/gpu_tests_$n.log)"
       [ $rc -ne 0 ] && { grep -E "FAILED|Error|assert" $O/gpu_tests_$n.log | head -20; exit $rc; } ;;
     smoke)
