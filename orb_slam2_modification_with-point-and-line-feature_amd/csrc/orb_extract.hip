@@ -1041,8 +1041,25 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
 }
 
 // Exclusive scan of vals[0..n) in place (n <= 256*kPer); returns the total.
-template <int kPer>
+// NT = 64 (a one-wave workgroup): element i in round i / 64 at lane i % 64,
+// one wave scan per round and a running offset, no LDS partials or barrier
+// (the caller's __syncthreads are then wave barriers).
+template <int kPer, int NT = 256>
 __device__ int block_excl_scan(int* vals, int n, int* s_wsum) {
+  if constexpr (NT == 64) {
+    const int lane = threadIdx.x;
+    int run = 0;
+    for (int base = 0; base < n; base += 64) {
+      const int i = base + lane;
+      const int v = i < n ? vals[i] : 0;
+      const int incl = wave_incl_scan(v);
+      if (i < n) vals[i] = run + incl - v;
+      run += __shfl(incl, 63, 64);
+    }
+    __builtin_amdgcn_wave_barrier();
+    return run;
+  }
+  static_assert(NT == 256 || NT == 64, "octree workgroups: 4 waves or 1");
   const int t = threadIdx.x;
   int local[kPer];
   int sum = 0;
@@ -1090,13 +1107,19 @@ __device__ int block_excl_scan(int* vals, int n, int* s_wsum) {
 // FAST candidates (every level of a 640x480 frame), else in global memory;
 // 8 KB keeps two blocks per CU.
 constexpr int kOctLdsCand = 4096;
+// first pyramid level whose octree launch runs one-wave workgroups (the
+// launch of a level group starting there; ORBPL_OCT_WAVE_FROM overrides)
+#ifndef ORBPL_OCT_WAVE_FROM
+#define ORBPL_OCT_WAVE_FROM 3
+#endif
+constexpr int kOctWaveFrom = ORBPL_OCT_WAVE_FROM;
 
 // The node list never exceeds the level's kp_cap = max(N + 3, 4 nIni) (a
 // phase-1 pass starts only while size + 3 nexp <= N, phase 2 stops at the
 // first size >= N), so the list arrays are sized by kCap = the smallest of
 // 256 / 512 / 1024 that holds every level's kp_cap: at 1000 features 27 KB
 // of LDS per workgroup (5 per CU) instead of 74 KB (2 per CU).
-template <int kCap>
+template <int kCap, int kKn = kOctLdsCand>
 struct OctShared {
   uint2 rect[2][kCap];              // (x0 | y0<<16, x1 | y1<<16)
   int cnt[2][kCap];
@@ -1109,7 +1132,7 @@ struct OctShared {
   int scan[kOctMaxList];            // also the cell-count scan (<= 1024 cells)
   int wsum[8];
   int misc[8];
-  uint16_t kn[kOctLdsCand];         // node of each key when total <= kOctLdsCand
+  uint16_t kn[kKn];                 // node of each key when total <= kKn
 };
 
 __device__ __forceinline__ uint2 mk_rect(int x0, int y0, int x1, int y1) {
@@ -1139,8 +1162,11 @@ __device__ __forceinline__ uint2 child_rect(uint2 r, int c) {
 __device__ long long g_oct_prof[8 * 16];
 __device__ int g_oct_prof_on;
 
-template <int kCap>
-__global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
+// NT = 256 (4 waves) or 64: the levels with few candidates run as one wave,
+// whose block scans are wave scans and whose barriers are wave barriers (a
+// pass's fixed cost was its ~16 block barriers and scans)
+template <int kCap, int NT = 256>
+__global__ void __launch_bounds__(NT) k_octree(const OrbGeom* __restrict__ g,
                                                 const uint32_t* __restrict__ cell_cands,
                                                 const int* __restrict__ cell_counts,
                                                 uint32_t* __restrict__ kcand,
@@ -1149,7 +1175,10 @@ __global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
                                                 int* __restrict__ kp_count,
                                                 int* __restrict__ err_flag, int l0) {
   extern __shared__ char smem_raw[];
-  OctShared<kCap>& S = *reinterpret_cast<OctShared<kCap>*>(smem_raw);
+  // one-wave workgroups keep the key nodes of up to 2048 candidates in LDS
+  // (23 instead of 27 KB at kCap 256: 6 workgroups per CU)
+  constexpr int kKn = NT == 64 ? 2048 : kOctLdsCand;
+  OctShared<kCap, kKn>& S = *reinterpret_cast<OctShared<kCap, kKn>*>(smem_raw);
   const int level = l0 + blockIdx.x, f = blockIdx.y, t = threadIdx.x;   // levels l0 ..
   const LevelGeom& L = g->lv[level];
   const int N = L.nfeat;
@@ -1172,14 +1201,14 @@ __global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
   // ---- 1. gather candidates in cell order (vToDistributeKeys order) ----
   const int ncells = L.ncells;
   const int* ccnt = cell_counts + (long long)f * g->ncells_total + L.cell_base;
-  for (int i = t; i < ncells; i += 256) S.scan[i] = ccnt[i];
+  for (int i = t; i < ncells; i += NT) S.scan[i] = ccnt[i];
   __syncthreads();
-  const int total = block_excl_scan<4>(S.scan, ncells, S.wsum);
+  const int total = block_excl_scan<4, NT>(S.scan, ncells, S.wsum);
   if (total == 0) {
     if (t == 0) *out_count = 0;
     return;
   }
-  const bool kn_lds = total <= kOctLdsCand;   // block-uniform
+  const bool kn_lds = total <= kKn;   // block-uniform
   auto kn_get = [&](int k) -> int { return kn_lds ? (int)S.kn[k] : KN[k]; };
   auto kn_set = [&](int k, int v) {
     if (kn_lds) S.kn[k] = (uint16_t)v;
@@ -1190,11 +1219,11 @@ __global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
   const int nIni = L.n_ini;
   const float hX = L.hx;
   const int H = L.max_border_y - kMinBorder;
-  for (int i = t; i < nIni; i += 256) S.child[i] = 0;
+  for (int i = t; i < nIni; i += NT) S.child[i] = 0;
   __syncthreads();
   {
     const uint32_t* cc = cell_cands + ((long long)f * g->ncells_total + L.cell_base) * slots;
-    for (int k = t; k < total; k += 256) {
+    for (int k = t; k < total; k += NT) {
       int lo = 0, hi = ncells - 1;
       while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
@@ -1211,11 +1240,11 @@ __global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
   }
   __syncthreads();
   // list = nonempty initial nodes in order
-  for (int i = t; i < nIni; i += 256) S.scan[i] = S.child[i] > 0 ? 1 : 0;
+  for (int i = t; i < nIni; i += NT) S.scan[i] = S.child[i] > 0 ? 1 : 0;
   __syncthreads();
-  int size = block_excl_scan<4>(S.scan, nIni, S.wsum);
+  int size = block_excl_scan<4, NT>(S.scan, nIni, S.wsum);
   int cur = 0;
-  for (int i = t; i < nIni; i += 256) {
+  for (int i = t; i < nIni; i += NT) {
     if (S.child[i] > 0) {
       int p = S.scan[i];
       S.rect[0][p] = mk_rect((int)(hX * (float)i), 0, (int)(hX * (float)(i + 1)), H);
@@ -1224,7 +1253,7 @@ __global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
     }
   }
   __syncthreads();
-  for (int k = t; k < total; k += 256) kn_set(k, S.upos[kn_get(k)]);
+  for (int k = t; k < total; k += NT) kn_set(k, S.upos[kn_get(k)]);
   // expandable list (for phase 2): empty until a pass creates children
   int nexp = 0;
   bool finish = false;
@@ -1238,10 +1267,10 @@ __global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
     // ---- choose the nodes to divide and their processing rank ----
     int nproc;  // number of candidate nodes (speculative in phase 2)
     if (!phase2) {
-      for (int i = t; i < size; i += 256) S.scan[i] = S.cnt[cur][i] > 1 ? 1 : 0;
+      for (int i = t; i < size; i += NT) S.scan[i] = S.cnt[cur][i] > 1 ? 1 : 0;
       __syncthreads();
-      nproc = block_excl_scan<4>(S.scan, size, S.wsum);
-      for (int i = t; i < size; i += 256) {
+      nproc = block_excl_scan<4, NT>(S.scan, size, S.wsum);
+      for (int i = t; i < size; i += NT) {
         bool d = S.cnt[cur][i] > 1;
         S.rank[i] = d ? S.scan[i] : -1;
         if (d) S.proc[S.scan[i]] = i;
@@ -1249,9 +1278,9 @@ __global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
     } else {
       // sort expandable nodes by (count, seq) descending; seq = creation index
       nproc = nexp;
-      for (int i = t; i < size; i += 256) S.rank[i] = -1;
+      for (int i = t; i < size; i += NT) S.rank[i] = -1;
       __syncthreads();
-      for (int i = t; i < nexp; i += 256) {
+      for (int i = t; i < nexp; i += NT) {
         int ci = S.exp_cnt[i];
         int r = 0;
         for (int j = 0; j < nexp; j++) {
@@ -1268,10 +1297,10 @@ __global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
       if (t == 0) atomicOr(err_flag, 1);
       break;
     }
-    for (int i = t; i < 4 * nproc; i += 256) S.child[i] = 0;
+    for (int i = t; i < 4 * nproc; i += NT) S.child[i] = 0;
     __syncthreads();
     // ---- sweep 1: child counts ----
-    for (int k = t; k < total; k += 256) {
+    for (int k = t; k < total; k += NT) {
       int e = kn_get(k);
       int r = S.rank[e];
       if (r >= 0) {
@@ -1281,33 +1310,33 @@ __global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
     }
     __syncthreads();
     // nonempty children per processed node
-    for (int r = t; r < nproc; r += 256) {
+    for (int r = t; r < nproc; r += NT) {
       int ne = (S.child[4 * r] > 0) + (S.child[4 * r + 1] > 0) + (S.child[4 * r + 2] > 0) +
                (S.child[4 * r + 3] > 0);
       S.scan[r] = ne;
     }
     __syncthreads();
-    int nchild_all = block_excl_scan<4>(S.scan, nproc, S.wsum);  // S.scan = prefix (excl)
+    int nchild_all = block_excl_scan<4, NT>(S.scan, nproc, S.wsum);  // S.scan = prefix (excl)
     int kproc = nproc;
     if (phase2) {
       // first r with prevSize + sum_{q<=r}(ne_q - 1) >= N
       if (t == 0) S.misc[0] = nproc;
       __syncthreads();
-      for (int r = t; r < nproc; r += 256) {
+      for (int r = t; r < nproc; r += NT) {
         int ne = (r + 1 < nproc ? S.scan[r + 1] : nchild_all) - S.scan[r];
         int sz = prevSize + (S.scan[r] + ne) - (r + 1);
         if (sz >= N) atomicMin(&S.misc[0], r + 1);
       }
       __syncthreads();
       kproc = S.misc[0];
-      for (int i = t; i < size; i += 256)
+      for (int i = t; i < size; i += NT)
         if (S.rank[i] >= kproc) S.rank[i] = -1;
       __syncthreads();
     }
     const int nchild = kproc < nproc ? S.scan[kproc] : nchild_all;
     // ---- new positions: children blocks in reverse processing order ----
     const int nxt = cur ^ 1;
-    for (int r = t; r < kproc; r += 256) {
+    for (int r = t; r < kproc; r += NT) {
       const int pre = S.scan[r];
       const int ne = (r + 1 < nproc ? S.scan[r + 1] : nchild_all) - pre;
       const int off = nchild - pre - ne;
@@ -1328,10 +1357,10 @@ __global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
       }
     }
     // untouched entries keep relative order after the children
-    for (int i = t; i < size; i += 256) S.upos[i] = S.rank[i] < 0 ? 1 : 0;
+    for (int i = t; i < size; i += NT) S.upos[i] = S.rank[i] < 0 ? 1 : 0;
     __syncthreads();
-    const int nunt = block_excl_scan<4>(S.upos, size, S.wsum);
-    for (int i = t; i < size; i += 256) {
+    const int nunt = block_excl_scan<4, NT>(S.upos, size, S.wsum);
+    for (int i = t; i < size; i += NT) {
       if (S.rank[i] < 0) {
         int p = nchild + S.upos[i];
         S.rect[nxt][p] = S.rect[cur][i];
@@ -1346,7 +1375,7 @@ __global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
     }
     __syncthreads();
     // ---- sweep 2: re-index keys ----
-    for (int k = t; k < total; k += 256) {
+    for (int k = t; k < total; k += NT) {
       int e = kn_get(k);
       int r = S.rank[e];
       int ne;
@@ -1359,7 +1388,7 @@ __global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
       kn_set(k, ne);
     }
     // ---- expandable children in creation order (rank asc, child asc) ----
-    for (int r = t; r < kproc; r += 256) {
+    for (int r = t; r < kproc; r += NT) {
       int ne = 0;
 #pragma unroll
       for (int c = 0; c < 4; c++) {
@@ -1369,8 +1398,8 @@ __global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
       S.scan[r] = ne;
     }
     __syncthreads();
-    nexp = block_excl_scan<4>(S.scan, kproc, S.wsum);
-    for (int r = t; r < kproc; r += 256) {
+    nexp = block_excl_scan<4, NT>(S.scan, kproc, S.wsum);
+    for (int r = t; r < kproc; r += NT) {
       int o = S.scan[r];
 #pragma unroll
       for (int c = 0; c < 4; c++) {
@@ -1393,16 +1422,16 @@ __global__ void __launch_bounds__(256) k_octree(const OrbGeom* __restrict__ g,
   }
   lap(1);
   // ---- retain the best key per node (strict >, first in candidate order) ----
-  for (int i = t; i < size; i += 256) S.child[i] = 0;
+  for (int i = t; i < size; i += NT) S.child[i] = 0;
   __syncthreads();
-  for (int k = t; k < total; k += 256) {
+  for (int k = t; k < total; k += NT) {
     uint32_t c = K[k];
     int key = (cand_s(c) << 20) | (kMaxCandPerLevel - k);
     atomicMax(&S.child[kn_get(k)], key);
   }
   __syncthreads();
   const int cap = L.kp_cap;
-  for (int i = t; i < size && i < cap; i += 256) {
+  for (int i = t; i < size && i < cap; i += NT) {
     int k = kMaxCandPerLevel - (S.child[i] & kMaxCandPerLevel);
     out_list[i] = K[k];
   }
@@ -1810,7 +1839,7 @@ void launch_fast(const OrbGeom& hg, const OrbGeom* dg, const CellGeom* cells, co
 void launch_octree(const OrbGeom& hg, const OrbGeom* dg, const uint32_t* cell_cands,
                    const int* cell_counts, uint32_t* kcand, int* knode, uint32_t* kp_list,
                    int* kp_count, int* err_flag, int batch, int l0, int l1, hipStream_t s) {
-  set_smem_attr((const void*)k_octree<1024>, sizeof(OctShared<1024>));
+  set_smem_attr((const void*)k_octree<1024, 256>, sizeof(OctShared<1024>));
   int cap = 0;
   for (int l = 0; l < hg.nlevels; l++) cap = std::max(cap, hg.lv[l].kp_cap);
   if (once_per_device((const void*)&g_oct_prof_on)) {
@@ -1818,18 +1847,30 @@ void launch_octree(const OrbGeom& hg, const OrbGeom* dg, const uint32_t* cell_ca
     (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_oct_prof_on), &on, sizeof(int), 0,
                                  hipMemcpyHostToDevice, s);
   }
-  if (cap <= 256)
-    hipLaunchKernelGGL(k_octree<256>, dim3(l1 - l0, batch), dim3(256),
-                       sizeof(OctShared<256>), s, dg, cell_cands, cell_counts, kcand, knode,
+  // levels from ORBPL_OCT_WAVE_FROM on (default 3: the coarse levels, a few
+  // hundred candidates each) as one-wave workgroups; 0 = all, nlevels = none
+  const char* wf = getenv("ORBPL_OCT_WAVE_FROM");   // read per launch: tests vary it
+  const int wave_from = wf ? atoi(wf) : kOctWaveFrom;
+  const bool one_wave = l0 >= wave_from;
+#define ORBPL_OCT_LAUNCH(CAP)                                                                   \
+  if (one_wave)                                                                                 \
+    hipLaunchKernelGGL((k_octree<CAP, 64>), dim3(l1 - l0, batch), dim3(64),                    \
+                       sizeof(OctShared<CAP, 2048>), s, dg, cell_cands, cell_counts, kcand,     \
+                       knode,                                                                   \
+                       kp_list, kp_count, err_flag, l0);                                        \
+  else                                                                                          \
+    hipLaunchKernelGGL((k_octree<CAP, 256>), dim3(l1 - l0, batch), dim3(256),                  \
+                       sizeof(OctShared<CAP>), s, dg, cell_cands, cell_counts, kcand, knode,    \
                        kp_list, kp_count, err_flag, l0);
-  else if (cap <= 512)
-    hipLaunchKernelGGL(k_octree<512>, dim3(l1 - l0, batch), dim3(256),
-                       sizeof(OctShared<512>), s, dg, cell_cands, cell_counts, kcand, knode,
-                       kp_list, kp_count, err_flag, l0);
-  else
-    hipLaunchKernelGGL(k_octree<1024>, dim3(l1 - l0, batch), dim3(256),
-                       sizeof(OctShared<1024>), s, dg, cell_cands, cell_counts, kcand, knode,
-                       kp_list, kp_count, err_flag, l0);
+  if (cap <= 256) {
+    ORBPL_OCT_LAUNCH(256)
+  } else if (cap <= 512) {
+    ORBPL_OCT_LAUNCH(512)
+  } else {
+    if (one_wave) set_smem_attr((const void*)k_octree<1024, 64>, sizeof(OctShared<1024, 2048>));
+    ORBPL_OCT_LAUNCH(1024)
+  }
+#undef ORBPL_OCT_LAUNCH
 }
 
 void launch_orient_desc(const OrbGeom& hg, const OrbGeom* dg, const uint8_t* pyr,

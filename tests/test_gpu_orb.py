@@ -152,3 +152,4 @@ def test_level_pipeline_batch_bit_exact(orbpl, synth, monkeypatch, pipe, groups)
             assert n[i] == len(kp) > 0, (rep, i)
             assert _kp_equal(kraw[i, :n[i]], kp), (rep, i)
             assert np.array_equal(dd[i, :n[i]], de), (rep, i)
+

@@ -11,10 +11,10 @@ for s in $SS; do
   for e in $ES; do
     tag=$(echo "$e" | tr '=' '_')
     if [ "$e" = "-" ]; then
-      timeout -k 10 200 python bench.py --streams $s --steps 10 --warmup 3 $B > gpurun_out/ab/env_${tag}_$s.log 2>&1 || exit 1
+      timeout -k 10 200 python bench.py --streams $s --steps 10 --warmup 3 $B --detail gpurun_out/ab/env_${tag}_$s.detail.json > gpurun_out/ab/env_${tag}_$s.log 2>&1 || exit 1
     else
-      env "$e" timeout -k 10 200 python bench.py --streams $s --steps 10 --warmup 3 $B > gpurun_out/ab/env_${tag}_$s.log 2>&1 || exit 1
+      env "$e" timeout -k 10 200 python bench.py --streams $s --steps 10 --warmup 3 $B --detail gpurun_out/ab/env_${tag}_$s.detail.json > gpurun_out/ab/env_${tag}_$s.log 2>&1 || exit 1
     fi
-    grep '^{' gpurun_out/ab/env_${tag}_$s.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$e', $s, round(d['value']), d['ms_per_step'])"
+    python -c "import json; d=json.load(open('gpurun_out/ab/env_${tag}_$s.detail.json')); st=d['stage_ms']; print('$e', $s, round(d['value']), d['ms_per_step'], 'stages', {k: st[k] for k in ('pyramid', 'fast', 'octree', 'orient_desc', 'match', 'pose', 'local_map')})"
   done
 done

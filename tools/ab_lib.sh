@@ -14,8 +14,9 @@ for r in $(seq 1 $RN); do
       v=${it%%:*}; e=""; [ "$it" != "$v" ] && e=${it#*:}
       L=""; [ "$v" != cur ] && L=variants/$v/liborbpl.so
       tag=$(echo "$it" | tr ':=,/' '____')
-      env ORBPL_LIB=$L ${e//+/ } timeout -k 10 200 python bench.py --streams $s --steps 10 --warmup 3 $B > gpurun_out/ab/lib_${tag}_$s.log 2>&1 || { echo "fail $it $s"; tail -5 gpurun_out/ab/lib_${tag}_$s.log; exit 1; }
-      grep '^{' gpurun_out/ab/lib_${tag}_$s.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$it', $s, round(d['value']), d['ms_per_step'])"
+      D=gpurun_out/ab/lib_${tag}_$s.detail.json
+      env ORBPL_LIB=$L ${e//+/ } timeout -k 10 200 python bench.py --streams $s --steps 10 --warmup 3 $B --detail $D > gpurun_out/ab/lib_${tag}_$s.log 2>&1 || { echo "fail $it $s"; tail -5 gpurun_out/ab/lib_${tag}_$s.log; exit 1; }
+      python -c "import json; d=json.load(open('$D')); st=d['stage_ms']; print('$it', $s, round(d['value']), d['ms_per_step'], {k: st.get(k) for k in ('pyramid', 'fast', 'octree', 'orient_desc', 'match', 'pose', 'local_map')})"
     done
   done
 done

@@ -31,7 +31,7 @@ for step in "$@"; do
       K=(); [ -n "$arg" ] && K=(-k "${arg//,/ }")
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${K[@]}" > $O/gpu_tests_$n.log 2>&1
       rc=$?; echo "tests($arg) exit $rc: $(tail -1 $O/gpu_tests_$n.log)"
-      [ $rc -ne 0 ] && { grep -E "FAILED|Error|assert" $O/gpu_tests_$n.log | head -20; exit $rc; } ;;
+      if [ $rc -ne 0 ]; then grep -E "FAILED|Error|assert" $O/gpu_tests_$n.log | head -20; exit $rc; fi ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
       tail -1 $O/smoke.log ;;
