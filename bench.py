@@ -8,7 +8,7 @@ TUM1.yaml camera + distortion, ORB 1000 features / 1.2 / 8 levels / FAST 20,7.
 A step = one pass of the reference's per-frame Tracking::Track() (ORB
 extraction, Frame glue, KeyFrame::ComputeBoW, TrackWithMotionModel or
 TrackReferenceKeyFrame, TrackLocalMap, the keyframe push) over a batch of
-`--streams` independent synthetic 640x480 RGB-D streams (default 1024), all
+`--streams` independent synthetic 640x480 RGB-D streams (default 2048), all
 inputs resident in HBM before the timed region. The other BASELINE configs are timed
 the same way and reported in the same JSON line: configs[2] (TUM3, ORB +
 LSD/LBD LineExtractor, LineMatcher::SearchByProjection, line edges) under
@@ -1263,9 +1263,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--streams", type=int, default=1024,
+    ap.add_argument("--streams", type=int, default=2048,
                     help="streams (frames per step) per GPU; the sweep reports 1..1024 with the "
-                         "per-step latency (8.5 ms at 1024: each stream still runs above 100 Hz)")
+                         "per-step latency (12.6 ms at 2048: each stream still runs at ~79 Hz, "
+                         "above a TUM camera's 30 Hz; 1024: 155.7k, 2048: 162.2k, 3072: 163.1k "
+                         "frames/s, profiles/r06/ab/streams_ab.txt)")
     ap.add_argument("--loop", type=int, default=300,
                     help="frames in the headline workload's synthetic closed loop (each stream "
                          "starts at its own frame and walks along it)")
@@ -1308,7 +1310,7 @@ def main():
                     help="1 = overlap extraction of step t+1 with tracking of step t; 0 = no; "
                          "-1 = per workload (on, except for the LSD-bound line workloads)")
     ap.add_argument("--sweep", type=int, default=1,
-                    help="1 = per-step latency / fps at batch 1..1024 (points) and 1..256 "
+                    help="1 = per-step latency / fps at batch 1..2048 (points) and 1..256 "
                          "(lines) after the timed runs (points runs, rank 0 only)")
     ap.add_argument("--local-map", type=int, default=1,
                     help="1 = every step runs TrackWithMotionModel + TrackLocalMap (the "
@@ -1406,7 +1408,7 @@ def main():
         lmf = bool(args.local_map)
         rk = bool(args.refkf)
         mp = bool(args.map)
-        sweeps = {"points": sweep(pkg, synth, "points", (1, 16, 64, 256, 1024), 5, device, lmf,
+        sweeps = {"points": sweep(pkg, synth, "points", (1, 16, 64, 256, 1024, 2048), 5, device, lmf,
                                   voc, rk, mp),
                   "lines": sweep(pkg, synth, "lines", (1, 16, 64, 256), 2, device, lmf, voc, rk,
                                  mp)}

@@ -162,6 +162,7 @@ struct orbx_ctx {
   PyrBand* d_bands = nullptr;
   long long* d_pyr_prof = nullptr;   // ORBPL_PYR_PROFILE: k_pyramid phase stamps
   int pyr_bands = 0;           // 0 = choose per batch (ORBPL_PYR_BANDS overrides)
+  int group_bands[kFastGroups] = {0, 0, 0, 0};   // per level group (0 = nb above)
   uint8_t* d_in = nullptr;
   uint8_t* d_pyr = nullptr;
   uint8_t* d_blur = nullptr;
@@ -412,6 +413,21 @@ int orbx_create(const orbpl_orb_params* p, int width, int height, int max_batch,
     const int b = atoi(e);
     if (b == 1 || b == 2 || b == 4 || b == 8) c->pyr_bands = b;
   }
+  // ORBPL_PYR_GROUP_BANDS="1/1/1/4": row bands of each level group's
+  // pyramid launch (A/B; a group's launch only reads complete lower levels,
+  // so its bands need not match the other groups')
+  if (const char* e = getenv("ORBPL_PYR_GROUP_BANDS")) {
+    int gi = 0;
+    for (const char* q = e; *q && gi < kFastGroups;) {
+      if (!isdigit((unsigned char)*q)) {
+        q++;
+        continue;
+      }
+      const int b = atoi(q);
+      while (isdigit((unsigned char)*q)) q++;
+      c->group_bands[gi++] = (b == 1 || b == 2 || b == 4 || b == 8) ? b : 0;
+    }
+  }
   if (getenv("ORBPL_PYR_PROFILE")) {
     CK(hipMalloc(&c->d_pyr_prof, 8 * (1 + 4 * kMaxLevels)));
     CK(hipMemsetAsync(c->d_pyr_prof, 0, 8 * (1 + 4 * kMaxLevels), c->stream));
@@ -546,8 +562,9 @@ int orbx_run(orbx_ctx* c, const uint8_t* d_imgs, int batch, int stride, long lon
   int l0 = 0;
   for (int gi = 0; gi < ngroups; gi++) {
     const int l1 = pipe ? c->group_end[gi] : g.nlevels;
+    const int nbg = pipe && c->group_bands[gi] ? c->group_bands[gi] : nb;
     launch_pyramid(g, c->d_geom, d_imgs, stride, frame_pitch, c->d_pyr, c->d_blur, c->d_rs,
-                   c->d_bands + pyr_band_base(nb), nb, batch, c->d_pyr_prof, l0, l1, s);
+                   c->d_bands + pyr_band_base(nbg), nbg, batch, c->d_pyr_prof, l0, l1, s);
     if (pipe) {
       HIP_CHECK(hipEventRecord(c->ev_group[gi], s));
       HIP_CHECK(hipStreamWaitEvent(fs, c->ev_group[gi], 0));

@@ -9,7 +9,7 @@ SS=${2:-256 1024}
 B="--no-cpu-baseline --no-parity --sweep 0 --secondary-steps 0 --stereo-steps 0 --rig-steps 0 --ingress-steps 0 --isolated-steps 0"
 for s in $SS; do
   for e in $ES; do
-    tag=$(echo "$e" | tr '=' '_')
+    tag=$(echo "$e" | tr '=/,' '___')
     if [ "$e" = "-" ]; then
       timeout -k 10 200 python bench.py --streams $s --steps 10 --warmup 3 $B --detail gpurun_out/ab/env_${tag}_$s.detail.json > gpurun_out/ab/env_${tag}_$s.log 2>&1 || exit 1
     else
