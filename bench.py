@@ -400,8 +400,13 @@ def compact_line(out, detail):
         "reference_faithful_fps": (cpu.get("reference_faithful") or {}).get("value")}
     legs = [par] + [(out.get(k) or {}).get("parity") or {} for k in
                     ("secondary", "stereo", "rig", "ingress")]
-    c["parity"] = {"pass": all(p.get("pass", True) for p in legs if isinstance(p, dict)),
-                   "headline_pass": par.get("pass") if isinstance(par, dict) else None,
+
+    def passed(p):   # one rank's report, or the gathered {"all_ranks_pass", "by_rank"}
+        return p.get("all_ranks_pass", p.get("pass")) if isinstance(p, dict) and p else None
+    if isinstance(par, dict) and "by_rank" in par:
+        par = dict((par["by_rank"] or [None])[0] or {}, all_ranks_pass=par.get("all_ranks_pass"))
+    c["parity"] = {"pass": all(passed(p) is not False for p in legs),
+                   "headline_pass": passed(par),
                    "max_abs_pose_diff": par.get("max_abs_pose_diff_vs_ref"),
                    "pose_tol": par.get("pose_tol"), "counts_equal": par.get("counts_equal"),
                    "ate_rmse_vs_gt_m": par.get("ate_rmse_vs_gt_m"),

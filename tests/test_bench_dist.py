@@ -156,3 +156,20 @@ def test_compact_line_fits_the_driver_tail():
     assert c["cpu_baseline"]["cores"] and c["cpu_baseline"]["reference_faithful_ms"]
     assert c["parity"]["pass"] is True
     assert {"points", "secondary", "stereo", "rig", "ingress", "batch1_ms"} <= set(c["summary"])
+
+
+def test_compact_line_gathered_parity():
+    """With ranks > 1 the headline parity is the gathered {all_ranks_pass,
+    by_rank} report: the compact line's verdict follows all_ranks_pass."""
+    import bench
+    base = {"metric": "m", "value": 1.0, "unit": "frames/s", "n_gpus": 2, "steps": 1, "warmup": 1,
+            "ms_per_step": 1.0, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "u8", "data": "synthetic", "config": {}, "roofline": None,
+            "cpu_baseline": None, "summary": {}}
+    for ok in (True, False):
+        out = dict(base, parity={"all_ranks_pass": ok,
+                                 "by_rank": [{"pass": True, "pose_tol": 1e-4},
+                                             {"pass": ok, "pose_tol": 1e-4}]})
+        c = bench.compact_line(out, "d.json")
+        assert c["parity"]["pass"] is ok and c["parity"]["headline_pass"] is ok
+        assert c["parity"]["pose_tol"] == 1e-4
