@@ -523,7 +523,29 @@ __device__ __forceinline__ fushort2 blur_pair(uint32_t w0, uint32_t w1, uint32_t
 // horizontal 7-tap sums of content columns x .. x+3 from the padded row's
 // dwords w0 | w1 | w2 = content columns x-4 .. x+7, packed as 4 x u16
 // (packed u16 arithmetic: two columns per instruction)
+#ifndef ORBPL_BLUR_DOT4
+#define ORBPL_BLUR_DOT4 1
+#endif
 __device__ __forceinline__ uint2 blur_h4(uint32_t w0, uint32_t w1, uint32_t w2) {
+#if ORBPL_BLUR_DOT4
+  // one v_dot4_u32_u8 per source dword and output column: column x + j sums
+  // bytes j + 1 .. j + 7 of the window with the taps placed at their byte
+  // lanes (integer sums: the same values as the packed u16 form below, which
+  // needs 9 byte-pair permutes and 14 packed ops per 4 columns, here 10 dot4
+  // + 2 packs)
+  constexpr uint32_t k0_a = 0x31221200u, k0_b = 0x12223136u;   // j = 0: w0 (-, 18, 34, 49), w1 (54, 49, 34, 18)
+  constexpr uint32_t k1_a = 0x22120000u, k1_b = 0x22313631u, k1_c = 0x00000012u;
+  constexpr uint32_t k2_a = 0x12000000u, k2_b = 0x31363122u, k2_c = 0x00001222u;
+  constexpr uint32_t k3_b = 0x36312212u, k3_c = 0x00122231u;
+  const uint32_t h0 = __builtin_amdgcn_udot4(w1, k0_b, __builtin_amdgcn_udot4(w0, k0_a, 0u, false), false);
+  const uint32_t h1 = __builtin_amdgcn_udot4(
+      w2, k1_c, __builtin_amdgcn_udot4(w1, k1_b, __builtin_amdgcn_udot4(w0, k1_a, 0u, false), false), false);
+  const uint32_t h2 = __builtin_amdgcn_udot4(
+      w2, k2_c, __builtin_amdgcn_udot4(w1, k2_b, __builtin_amdgcn_udot4(w0, k2_a, 0u, false), false), false);
+  const uint32_t h3 = __builtin_amdgcn_udot4(w2, k3_c, __builtin_amdgcn_udot4(w1, k3_b, 0u, false), false);
+  // sums <= 255 * 256 < 2^16: pack column pairs as u16x2
+  return make_uint2(__builtin_amdgcn_perm(h1, h0, 0x05040100u), __builtin_amdgcn_perm(h3, h2, 0x05040100u));
+#else
   const fushort2 P0 = blur_pair<0>(w0, w1, w2), P1 = blur_pair<1>(w0, w1, w2);
   const fushort2 P2 = blur_pair<2>(w0, w1, w2), P3 = blur_pair<3>(w0, w1, w2);
   const fushort2 P4 = blur_pair<4>(w0, w1, w2), P5 = blur_pair<5>(w0, w1, w2);
@@ -533,6 +555,7 @@ __device__ __forceinline__ uint2 blur_h4(uint32_t w0, uint32_t w1, uint32_t w2) 
   const fushort2 h01 = k0 * (P0 + P6) + k1 * (P1 + P5) + k2 * (P2 + P4) + k3 * P3;
   const fushort2 h23 = k0 * (P2 + P8) + k1 * (P3 + P7) + k2 * (P4 + P6) + k3 * P5;
   return make_uint2(__builtin_bit_cast(uint32_t, h01), __builtin_bit_cast(uint32_t, h23));
+#endif
 }
 
 // vertical 7-tap of one packed word (2 columns) of the ring h[0..6]: rows v
