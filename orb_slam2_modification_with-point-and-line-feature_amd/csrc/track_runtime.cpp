@@ -980,8 +980,10 @@ struct orbpl_tracker {
   StreamState* d_state = nullptr;
   PoseEdge* d_edges = nullptr;
   static constexpr int kRing = 64;   // steps kept in the timing ring
-  static constexpr int kEv = 36 + kKernelBrackets;   // events per step (28..35: kernel brackets,
-                                                     // 36..: extraction launch brackets)
+  static constexpr int kEvGlue = 36 + kKernelBrackets;   // glue start (frame_prepare)
+  static constexpr int kEvXdone = kEvGlue + 1;            // extraction done (glue on ts)
+  static constexpr int kEv = kEvXdone + 1;   // events per step (28..35: kernel brackets,
+                                             // 36..: extraction launch brackets)
   std::vector<hipEvent_t> ring;      // kRing * kEv events
   int ring_pos = 0, ring_count = 0;
   // TrackLocalMap (ORBPL_TRACK_LOCAL_MAP): ring of the last kLmK keyframes'
@@ -989,6 +991,7 @@ struct orbpl_tracker {
   static constexpr int kLmK = 4;
   int local_map = 0;
   int refkf = 0;                   // ORBPL_TRACK_REFKF (needs a vocabulary)
+  int glue_on_ts = 0;              // pipelined RGB-D: glue + BoW on the tracking stream
   int *trk_lcur = nullptr, *trk_nobs = nullptr, *trk_lm = nullptr, *trk_nml = nullptr;
   orbpl_keyline* trk_proj = nullptr;
   int* trk_src = nullptr;
@@ -1414,6 +1417,7 @@ int orbpl_tracker_create_ex(const orbpl_orb_params* orb, const orbpl_camera* cam
     }
   }
 #undef TA
+  if (const char* e = getenv("ORBPL_GLUE_ON_TRACK")) t->glue_on_ts = e[0] != '0';
   if (t->map) {
     int kfc = 32;
     if (const char* e = getenv("ORBPL_MAP_KF")) kfc = atoi(e);
@@ -1937,8 +1941,23 @@ static int tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_
                   reinterpret_cast<orbpl_keypoint_dev*>(C.kps), C.desc, K, C.n, ev, ev + 36);
     if (rc) return rc;
   }
+  // The frame glue and KeyFrame::ComputeBoW read only this step's frame
+  // buffers (and the depth input), so a pipelined RGB-D tracker can run them
+  // at the head of the tracking stream (ORBPL_GLUE_ON_TRACK=1): the next
+  // step's extraction on `s` then follows this step's orientation launch
+  // directly. Measured 1-3 % slower at 2048 streams (the tracking chain
+  // becomes the longer one; profiles/r06/ab/glue_on_track_ab.txt), so off by
+  // default. Stereo keeps them on `s` regardless: ComputeStereoMatches reads
+  // the extractors' device pyramids, which the next extraction overwrites.
+  hipStream_t gs = s;
+  if (t->glue_on_ts && ts != s && !t->stereo) {
+    gs = ts;
+    HIP_CHECK(hipEventRecord(ev[orbpl_tracker::kEvXdone], s));
+    HIP_CHECK(hipStreamWaitEvent(ts, ev[orbpl_tracker::kEvXdone], 0));
+  }
+  HIP_CHECK(hipEventRecord(ev[orbpl_tracker::kEvGlue], gs));
   launch_frame_prepare(t->consts, C.kps, C.n, K, t->stereo ? nullptr : d_depth,
-                       (long long)t->W * t->H, C.kps_un, C.depth, C.uright, C.gcell, S, s);
+                       (long long)t->W * t->H, C.kps_un, C.depth, C.uright, C.gcell, S, gs);
   if (t->stereo) {
     // ComputeStereoMatches (Frame.cc:886-1063) for the whole batch
     HIP_CHECK(hipStreamWaitEvent(s, ev[16], 0));
@@ -1976,16 +1995,16 @@ static int tracker_step(orbpl_tracker* t, const uint8_t* d_gray, const float* d_
     a.err = t->d_err;
     launch_stereo(a, S, s);
   }
-  HIP_CHECK(hipEventRecord(ev[27], s));
+  HIP_CHECK(hipEventRecord(ev[27], gs));
   if (t->voc) {
     // every tracked frame is a keyframe (P18): KeyFrame::ComputeBoW
-    // (KeyFrame.cc:67, Frame.cc:730) on the extraction stream
+    // (KeyFrame.cc:67, Frame.cc:730) after the glue
     rc = orbv_transform_batch_device(t->voc, C.desc, K, C.n, S, K, t->voc_levelsup, C.feat_node,
                                      C.feat_word, C.feat_weight, C.bow_words, C.bow_vals, C.bow_n,
-                                     K, t->d_bow_err, (void*)s);
+                                     K, t->d_bow_err, (void*)gs);
     if (rc) return rc;
   }
-  HIP_CHECK(hipEventRecord(ev[6], s));
+  HIP_CHECK(hipEventRecord(ev[6], gs));
   // ---- tracking stream
   HIP_CHECK(hipStreamWaitEvent(ts, ev[6], 0));
   if (t->lines) HIP_CHECK(hipStreamWaitEvent(ts, ev[13], 0));
@@ -2366,7 +2385,9 @@ int orbpl_tracker_step_host(orbpl_tracker* t, const uint8_t* h_gray, const uint1
                    t->stream);
   const int rc = tracker_step(t, t->in_gray[k], t->in_depth[k], nullptr);
   if (rc) return rc;
-  HIP_CHECK(hipEventRecord(t->in_done_s[k], t->stream));
+  // the depth slot is read by the frame glue, on the tracking stream when the
+  // glue runs there (which follows the extraction stream's reads of the slot)
+  HIP_CHECK(hipEventRecord(t->in_done_s[k], t->glue_on_ts && t->pipelined ? t->tstream : t->stream));
   if (t->lines) HIP_CHECK(hipEventRecord(t->in_done_l[k], t->lstream));
   t->in_used[k] = true;
   t->in_pos++;
@@ -2493,7 +2514,8 @@ int orbpl_tracker_timings(orbpl_tracker* t, int max_steps, float* ms, int* n_ste
   // (FAST, octree, orientation + descriptors, stages 2-4: the summed kernel
   // time of their level-group launches on the extractor's FAST stream, which
   // overlap the pyramid's later levels under the level pipeline)
-  static const int kPair[kTimingStages][2] = {{0, 1}, {1, 2}, {36, 37}, {3, 4}, {4, 5}, {5, 27},
+  static const int kPair[kTimingStages][2] = {{0, 1}, {1, 2}, {36, 37}, {3, 4}, {4, 5},
+                                              {orbpl_tracker::kEvGlue, 27},
                                               {7, 8}, {14, 9}, {26, 10}, {9, 26}, {27, 6}};
   const int n = std::min(max_steps, t->ring_count);
   for (int k = 0; k < n; k++) {

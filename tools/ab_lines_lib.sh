@@ -13,7 +13,8 @@ for r in $(seq 1 ${2:-2}); do
     tag=$(echo "$it" | tr ':=,/' '____')
     env ORBPL_LIB=$L ${e//+/ } timeout -k 10 120 python tools/time_lsd.py 3072 > gpurun_out/abl/t_$tag.log 2>&1 || { echo "fail probe $it"; exit 1; }
     echo "$r $it probe $(head -1 gpurun_out/abl/t_$tag.log)"
-    env ORBPL_LIB=$L ${e//+/ } timeout -k 10 300 python bench.py --workload lines --streams 3072 --steps 4 --warmup 1 $C > gpurun_out/abl/b_$tag.log 2>&1 || { echo "fail bench $it"; exit 1; }
-    grep '^{' gpurun_out/abl/b_$tag.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$r $it lines', round(d['value']), d['ms_per_step'], round(d['stage_ms']['lsd_seed'],1))"
+    D=gpurun_out/abl/b_$tag.detail.json
+    env ORBPL_LIB=$L ${e//+/ } timeout -k 10 300 python bench.py --workload lines --streams 3072 --steps 4 --warmup 1 $C --detail $D > gpurun_out/abl/b_$tag.log 2>&1 || { echo "fail bench $it"; exit 1; }
+    python -c "import json; d=json.load(open('$D')); st=d['stage_ms']; print('$r $it lines', round(d['value']), d['ms_per_step'], {k: round(st[k], 1) for k in ('lsd_sort', 'lsd_seed', 'lsd_validate', 'lsd') if k in st})"
   done
 done
