@@ -10,7 +10,14 @@ namespace orbpl {
 
 constexpr int kLsdMaxLines = 4096;    // raw LSD segments kept per frame
 constexpr int kLsdMaxCand = 4096;     // refined rectangles awaiting NFA validation per frame
-constexpr int kSortLocalMax = 2048;   // introsort segments finished in LDS
+// introsort segments of at most this many elements are finished in LDS, one
+// wave each (k_lsd_sort_wave); the global kernel partitions down to it.
+// Lines leg at 3072 streams, 2 rounds (profiles/r06/ab/lsd_sort_wave_ab.txt):
+// 2048 17.2k / 17.0k, 1024 17.4k / 17.6k, 512 16.9k / 16.6k frames/s
+#ifndef ORBPL_SORT_LOCAL_MAX
+#define ORBPL_SORT_LOCAL_MAX 1024
+#endif
+constexpr int kSortLocalMax = ORBPL_SORT_LOCAL_MAX;
 constexpr int kSpecLanes = 64;        // speculative regions per round (one wave)
 constexpr int kLaneCap = 2048;        // region points a lane can hold (both grows)
 // waves per frame of the speculative seed loop at a given batch: 4 for 97-384

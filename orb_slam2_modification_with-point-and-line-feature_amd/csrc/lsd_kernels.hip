@@ -859,6 +859,322 @@ __global__ void __launch_bounds__(kLocalThreads, 4) k_lsd_sort_local(LsdGeom g, 
   }
 }
 
+// ---------------------------------------------------------------------------
+// k_lsd_sort_wave: the deferred segments (<= kSortLocalMax elements) finished
+// by ONE wave each, in its own LDS, with no block barriers. The same replay
+// of libstdc++'s introsort as sort_core (median of three into first, the
+// closed-form Hoare partition, depth budget -> heap sort, <= 16 -> insertion
+// sort of the leaf), organised for a single wave:
+//   * a segment of more than 64 elements is scanned in 64-element chunks (all
+//     keys loaded at once): one ballot per chunk gives the L stoppers' ranks
+//     (bottom-up, the running count in a scalar register), a second pass in
+//     reverse chunk order the R stoppers' (top-down); ranks 0 .. n/2 go to two
+//     position tables in LDS (K <= n/2), K is the first rank whose L_k >= R_k
+//     (64 ranks per ballot), and the K swaps are table-driven; the pending
+//     segments are a depth-first stack in LDS (at most one more per level);
+//   * a segment of at most 64 elements is sorted entirely in registers, one
+//     element per lane (ws_small_sort): every active sub-segment is
+//     partitioned in the same pass, and the leaves are ranked stably.
+// The level-synchronous sort_core paid ~10 block barriers per level per
+// segment for its 256 threads. Exactness: the same permutation
+// (tests/test_gpu_lsd.py test_introsort_replica_matches_std_sort, every LSD
+// parity test).
+// ---------------------------------------------------------------------------
+constexpr int kWsStack = 64;    // pending segments (depth-first: <= depth budget + 1)
+struct WaveSortLds {
+  uint32_t a[kSortLocalMax];
+  // L / R stopper position by rank, ranks 0 .. n / 2 (K <= n / 2: the K swap
+  // pairs are 2K distinct positions)
+  uint16_t lp[kSortLocalMax / 2 + 2], rp[kSortLocalMax / 2 + 2];
+  int4 stack[kWsStack];
+  uint8_t tl[64], tr[64];   // in-register sort: stopper lane by (segment start + rank)
+};
+
+// __unguarded_partition_pivot on S.a[f, l) (l - f > 64): returns the cut;
+// *pkey = the pivot key. Every lane returns the same values.
+__device__ int ws_partition(WaveSortLds& S, int f, int l, int* pkey, int lane) {
+  uint32_t* A = S.a;
+  const int n = l - f;
+  {
+    // std::__move_median_to_first(first, first + 1, mid, last - 1)
+    const int a = f + 1, b = f + n / 2, c = l - 1;
+    const int ka = skey(A[a]), kb = skey(A[b]), kc = skey(A[c]);
+    int m;
+    if (ka > kb) {
+      if (kb > kc) m = b;
+      else if (ka > kc) m = c;
+      else m = a;
+    } else if (ka > kc) {
+      m = a;
+    } else if (kb > kc) {
+      m = c;
+    } else {
+      m = b;
+    }
+    const uint32_t vf = A[f], vm = A[m];
+    __syncthreads();
+    if (lane == 0) {
+      A[f] = vm;
+      A[m] = vf;
+    }
+    *pkey = skey(vm);
+    __syncthreads();
+  }
+  const int p = *pkey;
+  const unsigned long long bl = (1ull << lane) - 1ull;
+  const unsigned long long ab = ~bl & ~(1ull << lane);   // bits above the lane
+  // 64-element chunks, four chunks' key loads in flight per group: L
+  // stoppers ranked bottom-up in chunk order, R stoppers top-down in reverse
+  // chunk order (a second read of the keys), the running counts in scalar
+  // registers; ranks 0 .. lim (positions relative to f) go to the tables
+  const int nc = (n + 63) >> 6;
+  const int lim = n >> 1;
+  int nL = 0, nR = 0;
+  for (int c0 = 0; c0 < nc; c0 += 4) {
+    int kk[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int j = f + 64 * (c0 + u) + lane;
+      kk[u] = (j < l) ? skey(A[j]) : -1;   // keys are >= 0
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int c = c0 + u;
+      if (c < nc) {
+        const int j = f + 64 * c + lane;
+        const bool isl = kk[u] >= 0 && j > f && kk[u] <= p;
+        const unsigned long long lm = __ballot(isl);
+        const int kl = nL + __popcll(lm & bl);
+        if (isl && kl <= lim) S.lp[kl] = (uint16_t)(64 * c + lane);
+        nL += __popcll(lm);
+      }
+    }
+  }
+  for (int c1 = nc - 1; c1 >= 0; c1 -= 4) {
+    int kk[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int j = f + 64 * (c1 - u) + lane;
+      kk[u] = (c1 - u >= 0 && j < l) ? skey(A[j]) : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int c = c1 - u;
+      if (c >= 0) {
+        const bool isr = kk[u] >= p;
+        const unsigned long long rm = __ballot(isr);
+        const int kr = nR + __popcll(rm & ab);
+        if (isr && kr <= lim) S.rp[kr] = (uint16_t)(64 * c + lane);
+        nR += __popcll(rm);
+      }
+    }
+  }
+  const int mn = min(nL, nR);
+  __syncthreads();
+  // K: the first k with L_k >= R_k (k < mn; it exists below lim + 1 when
+  // mn > lim), else mn
+  const int kend = min(mn, lim + 1);
+  int K = mn;
+  for (int k0 = 0; k0 < kend; k0 += 128) {
+    const int ka = k0 + lane, kb2 = k0 + 64 + lane;
+    const bool fa = ka < kend && S.lp[ka] >= S.rp[ka];
+    const bool fb = kb2 < kend && S.lp[kb2] >= S.rp[kb2];
+    const unsigned long long Fa = __ballot(fa), Fb = __ballot(fb);
+    if (Fa | Fb) {
+      K = Fa ? k0 + __builtin_ctzll(Fa) : k0 + 64 + __builtin_ctzll(Fb);
+      break;
+    }
+  }
+  int cut = n;
+  if (K < nL) cut = min(cut, (int)S.lp[K]);
+  if (K > 0) cut = min(cut, (int)S.rp[K - 1]);
+  for (int k0 = 0; k0 < K; k0 += 4 * 64) {   // 4 x 64 pairs per round, loads first
+    int pi[4], pj[4];
+    uint32_t vi[4], vj[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int k = min(k0 + u * 64 + lane, K - 1);
+      pi[u] = f + S.lp[k];
+      pj[u] = f + S.rp[k];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      vi[u] = A[pi[u]];
+      vj[u] = A[pj[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+      if (k0 + u * 64 + lane < K) {
+        A[pi[u]] = vj[u];
+        A[pj[u]] = vi[u];
+      }
+  }
+  __syncthreads();
+  return f + cut;
+}
+
+// S.a[b, b + n) (n <= 64) sorted entirely in registers, one element per
+// lane: every lane carries the bounds [sa, sb) of its current segment, so one
+// pass partitions every active segment at once (median of three by three
+// lane reads, the pivot swap and the Hoare swaps as lane permutations, the
+// stopper ranks by popcounts of the segment-masked ballots, the k-th stopper's
+// lane from a rank table in LDS). Leaves (2 .. 16 elements) are then ranked stably in registers
+// (the final insertion sort's order); a depth-exhausted segment is heap-sorted
+// in LDS by lane 0 afterwards (libstdc++'s partial_sort).
+__device__ void ws_small_sort(WaveSortLds& S, int b, int n, int d, int ub, int kt, int lane) {
+  const bool in = lane < n;
+  uint32_t x = in ? S.a[b + lane] : 0u;
+  int sa = 0, sb = n, sd = d, su = ub;
+  auto part_of = [&]() { return in && su >= kt && sb - sa > 16 && sd > 0; };
+  bool part = part_of();
+  while (__ballot(part)) {
+    const int nn = sb - sa;
+    const int p1 = min(sa + 1, 63), p2 = min(sa + nn / 2, 63), p3 = max(min(sb - 1, 63), 0);
+    const int k0 = skey(x);
+    const int ka = __shfl(k0, p1, 64), kb = __shfl(k0, p2, 64), kc = __shfl(k0, p3, 64);
+    int m, km;
+    if (ka > kb) {
+      if (kb > kc) { m = p2; km = kb; }
+      else if (ka > kc) { m = p3; km = kc; }
+      else { m = p1; km = ka; }
+    } else if (ka > kc) {
+      m = p1; km = ka;
+    } else if (kb > kc) {
+      m = p3; km = kc;
+    } else {
+      m = p2; km = kb;
+    }
+    int src = lane;
+    if (part) src = lane == sa ? m : (lane == m ? sa : lane);
+    x = (uint32_t)__shfl((int)x, src, 64);
+    const int k = skey(x);
+    const unsigned long long segm =
+        part ? (((nn >= 64 ? ~0ull : ((1ull << nn) - 1ull))) << sa) : 0ull;
+    const unsigned long long Ls = __ballot(part && lane > sa && k <= km) & segm;
+    const unsigned long long Rs = __ballot(part && k >= km) & segm;
+    const unsigned long long bl = (1ull << lane) - 1ull;
+    const int nL = __popcll(Ls), nR = __popcll(Rs), mn = min(nL, nR);
+    const bool isL = (Ls >> lane) & 1ull, isR = (Rs >> lane) & 1ull;
+    const int rkl = __popcll(Ls & bl), rkr = __popcll(Rs & ~bl & ~(1ull << lane));
+    // stopper lane by rank: S.tl / S.tr[sa + rank] (segments are disjoint lane ranges)
+    if (isL) S.tl[sa + rkl] = (uint8_t)lane;
+    if (isR) S.tr[sa + rkr] = (uint8_t)lane;
+    __syncthreads();
+    const bool hasp = isL && rkl < mn;
+    const int partner = hasp ? (int)S.tr[sa + rkl] : 64;   // R_rkl
+    const int partL = (isR && rkr < nL) ? (int)S.tl[sa + rkr] : lane;   // L_rkr
+    const unsigned long long F = __ballot(hasp && lane >= partner) & segm;
+    const int K = F ? __popcll(Ls & ((1ull << __builtin_ctzll(F)) - 1ull)) : mn;
+    int cut = sb;
+    if (part) {
+      if (K < nL) cut = min(cut, (int)S.tl[sa + K]);
+      if (K > 0) cut = min(cut, (int)S.tr[sa + K - 1]);
+    }
+    src = lane;
+    if (isL && rkl < K) src = partner;
+    if (isR && rkr < K) src = partL;
+    __syncthreads();
+    x = (uint32_t)__shfl((int)x, src, 64);
+    if (part) {
+      if (lane >= cut) {
+        sa = cut;
+        su = min(su, km);   // [cut, last): keys <= pivot
+      } else {
+        sb = cut;
+      }
+      sd--;
+      part = part_of();
+    }
+  }
+  // leaves: stable rank by key (descending) within [sa, sb)
+  const int len = sb - sa;
+  const bool leaf = in && su >= kt && len > 1 && len <= 16;
+  int dst = lane;
+  if (__ballot(leaf)) {
+    const int k = skey(x);
+    int rank = 0;
+    // as many steps as the longest leaf (<= 16), two lane reads per step
+    for (int t = 0; __ballot(leaf && t < len); t += 2) {
+      const int o0 = min(sa + t, 63), o1 = min(sa + t + 1, 63);
+      const int k0 = __shfl(k, o0, 64), k1 = __shfl(k, o1, 64);
+      if (leaf && t < len && o0 != lane) rank += (k0 > k) || (k0 == k && o0 < lane);
+      if (leaf && t + 1 < len && o1 != lane) rank += (k1 > k) || (k1 == k && o1 < lane);
+    }
+    if (leaf) dst = sa + rank;
+  }
+  __syncthreads();
+  if (in) S.a[b + dst] = x;
+  // depth-exhausted segments (> 16 elements, budget 0): heap sort in LDS
+  const unsigned long long H = __ballot(in && su >= kt && len > 16 && sd <= 0 && lane == sa);
+  __syncthreads();
+  for (unsigned long long h = H; h; h &= h - 1ull) {
+    const int a0 = __builtin_ctzll(h);
+    const int e0 = __builtin_amdgcn_readlane(sb, a0);
+    if (lane == 0) heap_sort_seg(S.a + b + a0, e0 - a0);
+  }
+  __syncthreads();
+}
+
+// Sorts S.a[0, m) as __introsort_loop with depth budget d0 and key bound ub0
+// (segments whose bound is below kt hold only NOTDEF pixels: left as they are).
+__device__ void ws_sort_segment(WaveSortLds& S, int m, int d0, int ub0, int kt, int lane,
+                                int* err) {
+  int sp = 0;
+  auto add = [&](int b, int e, int d, int ub) {   // uniform
+    const int sz = e - b;
+    if (ub < kt || sz < 2) return;
+    if (sz <= 64) {
+      ws_small_sort(S, b, sz, d, ub, kt, lane);
+    } else if (d > 0) {
+      if (sp < kWsStack) {
+        if (lane == 0) S.stack[sp] = make_int4(b, e, d, ub);
+        sp++;
+      } else if (lane == 0) {
+        atomicOr(err, 8);
+      }
+    } else {
+      __syncthreads();
+      if (lane == 0) heap_sort_seg(S.a + b, sz);
+      __syncthreads();
+    }
+  };
+  add(0, m, d0, ub0);
+  while (sp > 0) {
+    __syncthreads();
+    const int4 e = S.stack[--sp];
+    int p;
+    const int cut = ws_partition(S, e.x, e.y, &p, lane);
+    add(cut, e.y, e.z - 1, min(e.w, p));   // [cut, last): keys <= pivot
+    add(e.x, cut, e.z - 1, e.w);
+  }
+}
+
+__global__ void __launch_bounds__(64) k_lsd_sort_wave(LsdGeom g, LsdScratch sc) {
+  __shared__ WaveSortLds S;
+  const int f = blockIdx.y, lane = threadIdx.x;
+  uint32_t* A = sc.A + (long long)f * g.n;
+  const int nloc = min(sc.sort_nlocal[f], g.seg_cap);
+  const int4* loc = sc.sort_local + (long long)f * g.seg_cap;
+  const int kt = sc.sort_kt[f];
+  for (int k = blockIdx.x; k < nloc; k += gridDim.x) {
+    const int4 sg = loc[k];
+    const int m = sg.y - sg.x;
+    for (int i0 = 0; i0 < m; i0 += 8 * 64) {
+      uint32_t lv[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) lv[u] = A[sg.x + min(i0 + lane + u * 64, m - 1)];
+#pragma unroll
+      for (int u = 0; u < 8; u++)
+        if (i0 + lane + u * 64 < m) S.a[i0 + lane + u * 64] = lv[u];
+    }
+    __syncthreads();
+    ws_sort_segment(S, m, sg.z, sg.w, kt, lane, sc.err + f);
+    __syncthreads();
+    for (int i = lane; i < m; i += 64) A[sg.x + i] = S.a[i];
+    __syncthreads();
+  }
+}
+
 // waves per SIMD k_lsd_sort's register budget must allow (A/B build override):
 // 8 = 64 VGPRs, 4 workgroups of 512 per CU (unbounded, the 1024-element chunks
 // take 94). Measured with the LDS segment table (tools/gpu_r04_s.sh, kernel
@@ -970,6 +1286,25 @@ void launch_lsd_grad(const LsdGeom& g, const uint8_t* scaled, float* deg, int* q
 __host__ int lsd_sort_local_blocks(int batch) {
   return std::max(kSortLocalBlocks, std::min(128, 1024 / std::max(batch, 1)));
 }
+// one-wave workgroups per frame of k_lsd_sort_wave (a frame has ~50-100
+// deferred segments): 16 from 512 frames on, up to 128 for small batches
+__host__ int lsd_sort_wave_blocks(int batch) {
+  return std::max(16, std::min(128, 8192 / std::max(batch, 1)));
+}
+
+// the deferred segments: one wave per segment (k_lsd_sort_wave), or the
+// 256-thread level-synchronous replay (ORBPL_SORT_WAVE=0, k_lsd_sort_local)
+static void launch_lsd_sort_local(const LsdGeom& g, const LsdScratch& sc, int batch,
+                                  hipStream_t s) {
+  static const char* we = getenv("ORBPL_SORT_WAVE");
+  static const bool wave = !(we && we[0] == '0');
+  if (wave)
+    hipLaunchKernelGGL(k_lsd_sort_wave, dim3(lsd_sort_wave_blocks(batch), batch), dim3(64), 0, s, g,
+                       sc);
+  else
+    hipLaunchKernelGGL(k_lsd_sort_local, dim3(lsd_sort_local_blocks(batch), batch),
+                       dim3(kLocalThreads), 0, s, g, sc);
+}
 
 void launch_lsd_sort(const LsdGeom& g, const LsdScratch& sc, int batch, hipStream_t s) {
   // a batch that leaves CUs idle: 1024-thread workgroups (twice the chunks in
@@ -980,8 +1315,7 @@ void launch_lsd_sort(const LsdGeom& g, const LsdScratch& sc, int batch, hipStrea
     hipLaunchKernelGGL(k_lsd_sort<1024>, dim3(batch), dim3(1024), 0, s, g, sc);
   else
     hipLaunchKernelGGL(k_lsd_sort<kSortThreads>, dim3(batch), dim3(kSortThreads), 0, s, g, sc);
-  hipLaunchKernelGGL(k_lsd_sort_local, dim3(lsd_sort_local_blocks(batch), batch),
-                     dim3(kLocalThreads), 0, s, g, sc);
+  launch_lsd_sort_local(g, sc, batch, s);
 }
 
 void launch_lsd_sort_keys(int n, const int* keys, const LsdScratch& sc, hipStream_t s) {
@@ -995,8 +1329,7 @@ void launch_lsd_sort_keys(int n, const int* keys, const LsdScratch& sc, hipStrea
   else
     hipLaunchKernelGGL(k_lsd_sort_keys<kSortThreads>, dim3(1), dim3(kSortThreads), 0, s, g, sc,
                        keys);
-  hipLaunchKernelGGL(k_lsd_sort_local, dim3(kSortLocalBlocks, 1), dim3(kLocalThreads), 0, s, g,
-                     sc);
+  launch_lsd_sort_local(g, sc, 1, s);
 }
 
 }  // namespace orbpl
