@@ -258,22 +258,38 @@ __global__ void __launch_bounds__(256) k_lbd(int W, int H, const int16_t* __rest
       sCorX0 -= dL1;
       sCorY0 += dL0;
     }
+    // the row's walk along the line, kLbdU steps per round: the positions
+    // (the reference's running sCorX / sCorY sums, in order) and all their
+    // dx / dy loads first, then the accumulation in step order (each step's
+    // loads used to wait for the previous step's)
+    constexpr int kLbdU = 8;
     float sCorX = sCorX0, sCorY = sCorY0;
     float pLr = 0, nLr = 0, pOr = 0, nOr = 0;
-    for (short wID = 0; wID < lengthOfLSP; wID++) {
-      short t = (short)roundf(sCorX);
-      const short xCor = (t < 0) ? 0 : (t > imageWidth) ? imageWidth : t;
-      t = (short)roundf(sCorY);
-      const short yCor = (t < 0) ? 0 : (t > imageHeight) ? imageHeight : t;
-      const short dx = pdx[yCor * W + xCor], dy = pdy[yCor * W + xCor];
-      const float gDL = dx * dL0 + dy * dL1;
-      const float gDO = dx * dO0 + dy * dO1;
-      if (gDL > 0) pLr += gDL;
-      else nLr -= gDL;
-      if (gDO > 0) pOr += gDO;
-      else nOr -= gDO;
-      sCorX += dL0;
-      sCorY += dL1;
+    for (int w0 = 0; w0 < lengthOfLSP; w0 += kLbdU) {
+      short dxs[kLbdU], dys[kLbdU];
+#pragma unroll
+      for (int u = 0; u < kLbdU; u++) {
+        short t = (short)roundf(sCorX);
+        const short xCor = (t < 0) ? 0 : (t > imageWidth) ? imageWidth : t;
+        t = (short)roundf(sCorY);
+        const short yCor = (t < 0) ? 0 : (t > imageHeight) ? imageHeight : t;
+        dxs[u] = pdx[yCor * W + xCor];
+        dys[u] = pdy[yCor * W + xCor];
+        sCorX += dL0;
+        sCorY += dL1;
+      }
+#pragma unroll
+      for (int u = 0; u < kLbdU; u++) {
+        if (w0 + u < lengthOfLSP) {
+          const short dx = dxs[u], dy = dys[u];
+          const float gDL = dx * dL0 + dy * dL1;
+          const float gDO = dx * dO0 + dy * dO1;
+          if (gDL > 0) pLr += gDL;
+          else nLr -= gDL;
+          if (gDO > 0) pOr += gDO;
+          else nOr -= gDO;
+        }
+      }
     }
     const float c = wts.gG[lane];
     s_row[wave][lane][0] = c * pLr;
