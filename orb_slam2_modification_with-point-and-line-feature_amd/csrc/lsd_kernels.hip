@@ -657,19 +657,23 @@ __device__ __forceinline__ void sort_core(const SortPtrs& P, int first0, int las
       }
       int runL = Lpre[ch] - Lpre[c0];
       int sufR = Rsuf[ch] - Rsuf[c1];
+      // only ranks 0 .. (last - first) / 2 are ever read: K <= n / 2 (the K
+      // swap pairs are 2K distinct positions), R6 reads L_K and R_{K-1}
+      const int lim = (last - first) >> 1;
 #pragma unroll
       for (int j = CH / 64 - 1; j >= 0; j--) {
         const int i = b + j * 64 + lane;
         if ((mR[j] >> lane) & 1ull) {
           const int k = sufR + __popcll(mR[j] & ~(below | (1ull << lane)));
-          ix(P.Rpos, first + k) = i;
+          if (k <= lim) ix(P.Rpos, first + k) = i;
         }
         sufR += __popcll(mR[j]);
       }
 #pragma unroll
       for (int j = 0; j < CH / 64; j++) {
         const int i = b + j * 64 + lane;
-        if ((mL[j] >> lane) & 1ull) ix(P.Lpos, first + runL + __popcll(mL[j] & below)) = i;
+        const int k = runL + __popcll(mL[j] & below);
+        if (((mL[j] >> lane) & 1ull) && k <= lim) ix(P.Lpos, first + k) = i;
         runL += __popcll(mL[j]);
       }
     }
@@ -681,13 +685,16 @@ __device__ __forceinline__ void sort_core(const SortPtrs& P, int first0, int las
       const int c0 = choff[s], c1 = c0 + nch[s] - 1;
       const int nL = Lpre[c1] + Lc[c1] - Lpre[c0];
       const int nR = Rsuf[c0] + Rc[c0] - Rsuf[c1];
-      int lo = 0, hi = min(nL, nR);
+      // the first k with L_k >= R_k lies at or below (last - first) / 2 when
+      // min(nL, nR) exceeds it (ranks beyond it were not written)
+      const int mn = min(nL, nR);
+      int lo = 0, hi = min(mn, ((last - first) >> 1) + 1);
       while (lo < hi) {
         const int m = (lo + hi) >> 1;
         if (ix(P.Lpos, first + m) < ix(P.Rpos, first + m)) lo = m + 1;
         else hi = m;
       }
-      const int K = lo;
+      const int K = lo < min(mn, ((last - first) >> 1) + 1) ? lo : mn;
       int cut = last;
       if (K < nL) cut = min(cut, P.Lpos[first + K]);
       if (K > 0) cut = min(cut, P.Rpos[first + K - 1]);
