@@ -60,6 +60,7 @@ struct LsdGeom {
   int rx0, rx1, ry0, ry1;
   // sort scratch capacities
   int seg_cap, chunk_cap, leaf_cap;
+  int mask_cap;   // k_lsd_sort's chunks per level whose stopper masks are kept (sort_masks)
 };
 
 // Device scratch of one frame slot (all pointers are per-batch bases; the
@@ -115,6 +116,7 @@ struct LsdScratch {
   int4* heap;          // seg_cap
   int* seg_i;          // 8 * seg_cap: pivot, choff, nL, nR, K, cut, nch, -
   int* chunk_i;        // 4 * chunk_cap: Lc, Rc, Lpre, Rsuf
+  unsigned long long* sort_masks;   // mask_cap * 32 per frame: a level's chunk stopper ballots
   int2* leaves;        // leaf_cap
   uint32_t* reg;       // 3*sw*sh region overflow (point, q, degrees)
   float* lines;        // kLsdMaxLines * 4

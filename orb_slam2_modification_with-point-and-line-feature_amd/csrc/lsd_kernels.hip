@@ -368,6 +368,11 @@ struct SortPtrs {
   int* nlocal;
   int local_max;   // 0: partition everything here
   int kt;          // segments whose key bound is < kt hold only NOTDEF pixels
+  // the level's stopper ballots by chunk (CH / 64 L then CH / 64 R words per
+  // chunk), kept from the count sweep for the scatter sweep so that it does
+  // not read the keys again; null or a level above mask_cap chunks: re-read
+  unsigned long long* masks;
+  int mask_cap;
 };
 
 __device__ __forceinline__ int skey(uint32_t e) { return (int)(e >> 22); }
@@ -561,6 +566,7 @@ __device__ __forceinline__ void sort_core(const SortPtrs& P, int first0, int las
       return;
     }
     const bool tab = TAB && nseg <= kSortTab;
+    const bool use_masks = P.masks != nullptr && nchunks <= P.mask_cap && 2 * CH / 64 <= 64;
     const bool map = MAPCAP > 0 && nchunks <= MAPCAP && nseg <= 65536;
     if (tab || map) {
       for (int s = t; s < nseg; s += NT) {
@@ -610,6 +616,7 @@ __device__ __forceinline__ void sort_core(const SortPtrs& P, int first0, int las
       const int b = first + (ch - sq.w) * CH;
       const int e = min(b + CH, last);
       int cl = 0, cr = 0;
+      unsigned long long myL = 0ull, myR = 0ull;   // lane j: chunk word j's ballots
 #pragma unroll
       for (int j = 0; j < CH / 64; j++) {
         const int i = b + j * 64 + lane;
@@ -619,8 +626,17 @@ __device__ __forceinline__ void sort_core(const SortPtrs& P, int first0, int las
           fl = i > first && k <= p;
           fr = k >= p;
         }
-        cl += __popcll(__ballot(fl));
-        cr += __popcll(__ballot(fr));
+        const unsigned long long bL = __ballot(fl), bR = __ballot(fr);
+        cl += __popcll(bL);
+        cr += __popcll(bR);
+        if (lane == j) {
+          myL = bL;
+          myR = bR;
+        }
+      }
+      if (use_masks && lane < CH / 64) {
+        P.masks[(size_t)ch * (2 * CH / 64) + lane] = myL;
+        P.masks[(size_t)ch * (2 * CH / 64) + CH / 64 + lane] = myR;
       }
       if (lane == 0) {
         Lc[ch] = cl;
@@ -642,39 +658,58 @@ __device__ __forceinline__ void sort_core(const SortPtrs& P, int first0, int las
       const int c0 = sq.w, c1 = c0 + (last - first + CH - 1) / CH - 1;
       const int b = first + (ch - c0) * CH;
       const int e = min(b + CH, last);
-      unsigned long long mL[CH / 64], mR[CH / 64];
-#pragma unroll
-      for (int j = 0; j < CH / 64; j++) {
-        const int i = b + j * 64 + lane;
-        bool fl = false, fr = false;
-        if (i < e) {
-          const int k = skey(ix(A, i));
-          fl = i > first && k <= p;
-          fr = k >= p;
-        }
-        mL[j] = __ballot(fl);
-        mR[j] = __ballot(fr);
-      }
       int runL = Lpre[ch] - Lpre[c0];
       int sufR = Rsuf[ch] - Rsuf[c1];
       // only ranks 0 .. (last - first) / 2 are ever read: K <= n / 2 (the K
       // swap pairs are 2K distinct positions), R6 reads L_K and R_{K-1}
       const int lim = (last - first) >> 1;
-#pragma unroll
-      for (int j = CH / 64 - 1; j >= 0; j--) {
+      auto scatter_r = [&](unsigned long long m, int j) {
         const int i = b + j * 64 + lane;
-        if ((mR[j] >> lane) & 1ull) {
-          const int k = sufR + __popcll(mR[j] & ~(below | (1ull << lane)));
+        if ((m >> lane) & 1ull) {
+          const int k = sufR + __popcll(m & ~(below | (1ull << lane)));
           if (k <= lim) ix(P.Rpos, first + k) = i;
         }
-        sufR += __popcll(mR[j]);
-      }
-#pragma unroll
-      for (int j = 0; j < CH / 64; j++) {
+        sufR += __popcll(m);
+      };
+      auto scatter_l = [&](unsigned long long m, int j) {
         const int i = b + j * 64 + lane;
-        const int k = runL + __popcll(mL[j] & below);
-        if (((mL[j] >> lane) & 1ull) && k <= lim) ix(P.Lpos, first + k) = i;
-        runL += __popcll(mL[j]);
+        const int k = runL + __popcll(m & below);
+        if (((m >> lane) & 1ull) && k <= lim) ix(P.Lpos, first + k) = i;
+        runL += __popcll(m);
+      };
+      if (use_masks) {
+        // the count sweep's ballots (vector loads: the words are rewritten
+        // every level), one word per lane, each broadcast by v_readlane where
+        // it is used
+        const unsigned long long v =
+            lane < 2 * CH / 64 ? P.masks[(size_t)ch * (2 * CH / 64) + lane] : 0ull;
+        const int vlo = (int)(uint32_t)v, vhi = (int)(uint32_t)(v >> 32);
+        auto word = [&](int w) {
+          return (unsigned long long)(uint32_t)__builtin_amdgcn_readlane(vlo, w) |
+                 ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane(vhi, w) << 32);
+        };
+#pragma unroll
+        for (int j = CH / 64 - 1; j >= 0; j--) scatter_r(word(CH / 64 + j), j);
+#pragma unroll
+        for (int j = 0; j < CH / 64; j++) scatter_l(word(j), j);
+      } else {
+        unsigned long long mL[CH / 64], mR[CH / 64];
+#pragma unroll
+        for (int j = 0; j < CH / 64; j++) {
+          const int i = b + j * 64 + lane;
+          bool fl = false, fr = false;
+          if (i < e) {
+            const int k = skey(ix(A, i));
+            fl = i > first && k <= p;
+            fr = k >= p;
+          }
+          mL[j] = __ballot(fl);
+          mR[j] = __ballot(fr);
+        }
+#pragma unroll
+        for (int j = CH / 64 - 1; j >= 0; j--) scatter_r(mR[j], j);
+#pragma unroll
+        for (int j = 0; j < CH / 64; j++) scatter_l(mL[j], j);
       }
     }
     __syncthreads();
@@ -800,6 +835,8 @@ __device__ SortPtrs sort_ptrs(const LsdGeom& g, const LsdScratch& sc, int f) {
   P.nlocal = sc.sort_nlocal + f;
   P.local_max = kSortLocalMax;
   P.kt = -(1 << 30);
+  P.masks = sc.sort_masks + (long long)f * g.mask_cap * 32;
+  P.mask_cap = kSortChunkG == 1024 ? g.mask_cap : 0;
   return P;
 }
 
@@ -847,6 +884,8 @@ __global__ void __launch_bounds__(kLocalThreads, 4) k_lsd_sort_local(LsdGeom g, 
   L.local = nullptr;
   L.nlocal = nullptr;
   L.local_max = 0;
+  L.masks = nullptr;
+  L.mask_cap = 0;
   L.kt = sc.sort_kt[f];
   for (int k = blockIdx.x; k < nloc; k += gridDim.x) {
     const int4 sg = loc[k];
@@ -1331,6 +1370,7 @@ void launch_lsd_sort_keys(int n, const int* keys, const LsdScratch& sc, hipStrea
   g.seg_cap = n / 17 + 2;
   g.chunk_cap = n / kLsdSortChunk + g.seg_cap + 2;
   g.leaf_cap = n / 2 + 2;
+  g.mask_cap = 2 * (n / 1024) + 8;
   if (kSortThreads < 1024 && 1 <= kSortWideBatch)
     hipLaunchKernelGGL(k_lsd_sort_keys<1024>, dim3(1), dim3(1024), 0, s, g, sc, keys);
   else

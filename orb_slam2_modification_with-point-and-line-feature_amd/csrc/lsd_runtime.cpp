@@ -124,6 +124,9 @@ int lsd_geometry(int W, int H, LsdGeom* out) {
   g.seg_cap = g.n / 17 + 2;
   g.chunk_cap = g.n / kLsdSortChunk + g.seg_cap + 2;
   g.leaf_cap = g.n / 2 + 2;
+  // the global levels only partition segments above the deferral bound
+  // (>= 1024 elements): at most 2 n / 1024 chunks of 1024 per level
+  g.mask_cap = 2 * (g.n / 1024) + 8;
   *out = g;
   return ORBPL_OK;
 }
@@ -246,6 +249,7 @@ int lsdx_create(int width, int height, int max_batch, int device, lsdx_ctx** out
   LA(s.seg_i, B * 8 * g.seg_cap * 4);
   LA(s.chunk_i, B * 4 * g.chunk_cap * 4);
   LA(s.leaves, B * g.leaf_cap * sizeof(int2));
+  LA(s.sort_masks, B * (size_t)g.mask_cap * 32 * 8);
   LA(s.reg, B * px * 3 * 4);
   LA(s.lines, B * kLsdMaxLines * 4 * 4);
   LA(s.nlines, B * 4);
@@ -529,6 +533,7 @@ int orbpl_test_introsort(const int* keys, int n, int* perm) {
   e = e ? e : A((void**)&sc.seg_i, (size_t)8 * seg_cap * 4);
   e = e ? e : A((void**)&sc.chunk_i, (size_t)4 * chunk_cap * 4);
   e = e ? e : A((void**)&sc.leaves, (size_t)leaf_cap * sizeof(int2));
+  e = e ? e : A((void**)&sc.sort_masks, (size_t)(2 * (n / 1024) + 8) * 32 * 8);
   e = e ? e : A((void**)&sc.err, 4);
   e = e ? e : A((void**)&sc.sort_local, (size_t)seg_cap * sizeof(int4));
   e = e ? e : A((void**)&sc.sort_nlocal, 4);
