@@ -744,11 +744,29 @@ __device__ __forceinline__ void sort_core(const SortPtrs& P, int first0, int las
       const int first = sq.x;
       const int kb = Lpre[ch] - Lpre[sq.w];
       const int ke = min(kb + Lc[ch], sK[s]);
-      for (int k = kb + lane; k < ke; k += 64) {
-        const int i = ix(P.Lpos, first + k), j = ix(P.Rpos, first + k);
-        const uint32_t a = ix(A, i), bb = ix(A, j);
-        ix(A, i) = bb;
-        ix(A, j) = a;
+      // kSwapU x 64 pairs per round: positions, then elements, then stores
+      // (one round trip each instead of two per 64 pairs)
+      constexpr int kSwapU = 4;
+      for (int k0 = kb; k0 < ke; k0 += kSwapU * 64) {
+        int pi[kSwapU], pj[kSwapU];
+        uint32_t va[kSwapU], vb[kSwapU];
+#pragma unroll
+        for (int u = 0; u < kSwapU; u++) {
+          const int k = min(k0 + u * 64 + lane, ke - 1);
+          pi[u] = ix(P.Lpos, first + k);
+          pj[u] = ix(P.Rpos, first + k);
+        }
+#pragma unroll
+        for (int u = 0; u < kSwapU; u++) {
+          va[u] = ix(A, pi[u]);
+          vb[u] = ix(A, pj[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < kSwapU; u++)
+          if (k0 + u * 64 + lane < ke) {
+            ix(A, pi[u]) = vb[u];
+            ix(A, pj[u]) = va[u];
+          }
       }
     }
     __syncthreads();
