@@ -566,7 +566,9 @@ __device__ __forceinline__ void sort_core(const SortPtrs& P, int first0, int las
       return;
     }
     const bool tab = TAB && nseg <= kSortTab;
-    const bool use_masks = P.masks != nullptr && nchunks <= P.mask_cap && 2 * CH / 64 <= 64;
+    const bool use_masks =
+        P.masks != nullptr && (long long)nchunks * (2 * CH / 64) <= (long long)P.mask_cap * 32 &&
+        2 * CH / 64 <= 64;
     const bool map = MAPCAP > 0 && nchunks <= MAPCAP && nseg <= 65536;
     if (tab || map) {
       for (int s = t; s < nseg; s += NT) {
@@ -854,7 +856,7 @@ __device__ SortPtrs sort_ptrs(const LsdGeom& g, const LsdScratch& sc, int f) {
   P.local_max = kSortLocalMax;
   P.kt = -(1 << 30);
   P.masks = sc.sort_masks + (long long)f * g.mask_cap * 32;
-  P.mask_cap = kSortChunkG == 1024 ? g.mask_cap : 0;
+  P.mask_cap = g.mask_cap;   // in 1024-element chunks (32 words each)
   return P;
 }
 
