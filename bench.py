@@ -1295,9 +1295,11 @@ def main():
     ap.add_argument("--secondary-steps", type=int, default=5,
                     help="steps of the configs[2] lines workload reported under 'secondary' "
                          "(points runs only; 0 = skip)")
-    ap.add_argument("--lines-streams", type=int, default=3072,
+    ap.add_argument("--lines-streams", type=int, default=4096,
                     help="streams of the lines workload: the LSD seed loop is one wave per "
-                         "frame, latency-bound, so it needs many frames in flight")
+                         "frame, latency-bound, so it needs many frames in flight (round 6, "
+                         "after the one-wave LDS sort: 3072 17.6-18.3k, 4096 18.3-18.7k, "
+                         "5120 19.5k frames/s, profiles/r06/ab/streams_ab.txt)")
     ap.add_argument("--stereo-steps", type=int, default=5,
                     help="steps of the configs[3] stereo workload reported under 'stereo' "
                          "(points runs only; 0 = skip)")
