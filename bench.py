@@ -752,9 +752,11 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
     if args.local_map or use_map:
         cand.append("match_local")
     if lines:
-        # (stereo: the line_prepare events also bracket the wait for the right
-        # image's lines and k_stereo_lines, not one kernel: left out)
-        cand += [k for k in tr.LSD_STAGES if not (stereo and k == "line_prepare")]
+        # (line_prepare: its events run from the first LSD half's LBD to the end
+        # of k_line_prepare on the line stream, so they bracket the wait for the
+        # second half's chain (and, stereo, the right image's lines and
+        # k_stereo_lines), not one kernel: left out)
+        cand += [k for k in tr.LSD_STAGES if k != "line_prepare"]
     iso = None
     if pipelined and args.isolated_steps > 0:
         # untimed: more steps with the two HIP streams serialised, so each
