@@ -271,9 +271,9 @@ def frame_bytes(n_kp, w=W, h=H, orb=ORB, lines=False, stereo=False):
 KERNELS = {"pyramid": "k_pyramid", "fast": "k_fast_cells", "octree": "k_octree",
            "orient_desc": "k_orient_desc", "match": "k_match_last", "pose": "k_pose",
            "pose_all": "k_pose", "match_local": "k_match_local",
-           "lsd_prep": "k_lsd_blur+k_lsd_resize+k_lsd_grad", "lsd_sort": "k_lsd_sort+k_lsd_sort_local",
+           "lsd_prep": "k_lsd_prep", "lsd_sort": "k_lsd_sort+k_lsd_sort_wave",
            "lsd_seed": "k_lsd_spec", "lsd_validate": "k_lsd_validate+k_lsd_compact",
-           "keylines": "k_keylines", "lbd": "k_lsd_blur+k_sobel+k_lbd",
+           "keylines": "k_keylines", "lbd": "k_blur_sobel+k_lbd",
            "line_prepare": "k_line_prepare"}
 
 

@@ -34,7 +34,8 @@ def short(name):
 
 
 ORB_KERNELS = ("k_pyramid", "k_fast_cells", "k_octree", "k_orient_desc")
-LSD_KERNELS = ("k_lsd_prep", "k_lsd_sort", "k_lsd_sort_local", "k_lsd_spec", "k_lsd_validate",
+LSD_KERNELS = ("k_lsd_prep", "k_lsd_sort", "k_lsd_sort_local", "k_lsd_sort_wave", "k_lsd_fill",
+               "k_lsd_spec", "k_lsd_validate",
                "k_lsd_compact", "k_keylines", "k_blur_sobel", "k_lbd")
 
 
