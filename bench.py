@@ -1305,11 +1305,11 @@ def main():
     ap.add_argument("--stereo-steps", type=int, default=5,
                     help="steps of the configs[3] stereo workload reported under 'stereo' "
                          "(points runs only; 0 = skip)")
-    ap.add_argument("--stereo-streams", type=int, default=2048,
+    ap.add_argument("--stereo-streams", type=int, default=3072,
                     help="stereo pairs per GPU: the leg is bound by the two images' LSD "
-                         "chains and gains up to 2048 pairs (1024: 6.03k, 1536: 6.67k, "
-                         "2048: 6.75-6.80k, 2560: 6.74k frames/s, profiles/r06/ab/"
-                         "streams_ab.txt)")
+                         "chains (before the round-6 LDS sort: 1024: 6.03k, 1536: 6.67k, "
+                         "2048: 6.75-6.80k, 2560: 6.74k; after it: 2048: 7.35-7.50k, 3072: "
+                         "7.65-7.72k frames/s, profiles/r06/ab/streams_ab.txt)")
     ap.add_argument("--rig-steps", type=int, default=5,
                     help="steps of the configs[4] 8-camera rig workload reported under 'rig' "
                          "(points runs only; 0 = skip)")

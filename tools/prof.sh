@@ -3,7 +3,7 @@
 # then PMC passes, each counter group in its own run (no tracing domains
 # combined with --pmc). Outputs under gpurun_out/prof_<tag>/.
 #   MODE=points (default): the headline configs[1] leg of the default bench
-#   MODE=lines: configs[2] at 4096 streams;  MODE=kitti: configs[3] at 2048
+#   MODE=lines: configs[2] at 4096 streams;  MODE=kitti: configs[3] at 3072
 #   MODE=rig: configs[4] at 512 cameras
 #   SQ=1 adds an SQ counter pass (VALU / wait / LDS instruction counts)
 set -o pipefail
@@ -17,7 +17,7 @@ R=$GRAFT_REPO_ROOT
 COMMON="--detail gpurun_out/prof_$tag/bench_detail.json --no-cpu-baseline --no-parity --sweep 0 --secondary-steps 0 --stereo-steps 0 --rig-steps 0 --isolated-steps 0 --ingress-steps 0"
 case "$MODE" in
   lines) B="$R/bench.py --workload lines --streams 4096 --steps 3 --warmup 1 $COMMON" ;;
-  kitti) B="$R/bench.py --workload kitti --streams 2048 --steps 3 --warmup 1 $COMMON" ;;
+  kitti) B="$R/bench.py --workload kitti --streams 3072 --steps 3 --warmup 1 $COMMON" ;;
   rig)   B="$R/bench.py --workload rig --streams 512 --steps 3 --warmup 1 $COMMON" ;;
   *)     B="$R/bench.py --steps 20 --warmup 5 $COMMON" ;;
 esac
