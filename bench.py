@@ -369,7 +369,7 @@ def _roof_compact(r):
         return None
     keep = ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic", "traffic_source",
             "traffic_over_algorithmic", "algorithmic_bytes_per_launch", "avg_launch_ms",
-            "frames_per_launch")
+            "frames_per_launch", "launches_per_step")
     c = {k: r.get(k) for k in keep}
     iso = r.get("isolated_dominant")
     if iso:
@@ -810,15 +810,22 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
     # the dominant kernel as rocprofv3 --stats ranks it: the most GPU time per
     # step in the timed (pipelined) region; the isolated steps' dominant
     # kernel is reported beside it (roofline.isolated_dominant)
-    dom = max(cand, key=lambda k: stage_avg[k])
-    dom_iso = max(cand, key=lambda k: iso.get(k, 0.0)) if iso is not None else dom
-    dom_ms = stage_avg[dom]          # live: timed region, in-stream hipEvents
     # frames per launch: the extraction / LSD batches may be split in two
     # offset halves on two streams; their stage events bracket the first half
     orb_fr, lsd_fr = tr.launch_frames()
     def launch_frames(k):
         return (orb_fr if k in ("pyramid", "fast", "octree", "orient_desc") else
                 lsd_fr if k in tr.LSD_STAGES else S)
+    # launches per step of a stage's kernel: the timed stage is one launch of
+    # launch_frames(k) frames; the step runs S frames through the extraction
+    # and S (2 S with the right images, stereo) through the LSD chain
+    def per_step(k):
+        if k in tr.LSD_STAGES:
+            return (2 if stereo else 1) * S / lsd_fr
+        return S / launch_frames(k) if k in ("pyramid", "fast", "octree", "orient_desc") else 1
+    dom = max(cand, key=lambda k: stage_avg[k] * per_step(k))
+    dom_iso = max(cand, key=lambda k: iso.get(k, 0.0)) if iso is not None else dom
+    dom_ms = stage_avg[dom]          # live: timed region, in-stream hipEvents (one launch)
     bytes_launch = int(ab[dom] * launch_frames(dom))
     achieved = bytes_launch / (dom_ms * 1e-3) / 1e9
     traffic, tsrc = pmc_traffic(KERNELS[dom], workload, launch_frames(dom))
@@ -827,7 +834,9 @@ def run_workload(pkg, synth, args, workload, S, steps, warmup, rank, world, devi
     fbytes = frame_bytes(n_kp, fw, fh, wl["orb"], lines, stereo)
     roof = {"bound": "hbm", "kernel": KERNELS[dom], "stage": dom,
             "dominance": "summed per-kernel GPU time per step in the timed region (as "
-                         "rocprofv3 --stats ranks kernels)",
+                         "rocprofv3 --stats ranks kernels): one launch's in-stream time x "
+                         "the kernel's launches per step",
+            "launches_per_step": round(per_step(dom), 3),
             "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
             "traffic_source": tsrc,
