@@ -558,6 +558,62 @@ __device__ __forceinline__ uint2 blur_h4(uint32_t w0, uint32_t w1, uint32_t w2) 
 #endif
 }
 
+// ORBPL_BLUR_VPAIR (default): the vertical taps over ADJACENT-row pairs. The
+// horizontal sums of rows r, r+1 of a column packed as u16x2, P_r = (h_r,
+// h_r+1), serve three output rows (r+3, r+1, r-1 with tap pairs (18, 34),
+// (49, 54), (49, 34)), so each source row costs one v_perm per column
+// (P_r+1 from P_r's high half and the new row) and each output row 3
+// v_dot2 + 1 v_mad per column: 20 ops per 4 columns instead of the
+// symmetric pairing's 12 v_perm + 16 v_dot2 (rows v and 6-v are a new pair for
+// every output row). Integer sums, the same values.
+#ifndef ORBPL_BLUR_VPAIR
+#define ORBPL_BLUR_VPAIR 1
+#endif
+// horizontal 7-tap sums of content columns x .. x+3, one u32 each (<= 65280)
+__device__ __forceinline__ uint4 blur_h4u(uint32_t w0, uint32_t w1, uint32_t w2) {
+  constexpr uint32_t k0_a = 0x31221200u, k0_b = 0x12223136u;
+  constexpr uint32_t k1_a = 0x22120000u, k1_b = 0x22313631u, k1_c = 0x00000012u;
+  constexpr uint32_t k2_a = 0x12000000u, k2_b = 0x31363122u, k2_c = 0x00001222u;
+  constexpr uint32_t k3_b = 0x36312212u, k3_c = 0x00122231u;
+  uint4 h;
+  h.x = __builtin_amdgcn_udot4(w1, k0_b, __builtin_amdgcn_udot4(w0, k0_a, 0u, false), false);
+  h.y = __builtin_amdgcn_udot4(w2, k1_c,
+                               __builtin_amdgcn_udot4(w1, k1_b, __builtin_amdgcn_udot4(w0, k1_a, 0u, false), false),
+                               false);
+  h.z = __builtin_amdgcn_udot4(w2, k2_c,
+                               __builtin_amdgcn_udot4(w1, k2_b, __builtin_amdgcn_udot4(w0, k2_a, 0u, false), false),
+                               false);
+  h.w = __builtin_amdgcn_udot4(w2, k3_c, __builtin_amdgcn_udot4(w1, k3_b, 0u, false), false);
+  return h;
+}
+// (h_r, h_r+1) of 4 columns from two rows' sums
+__device__ __forceinline__ uint4 blur_pair_rows(uint4 a, uint4 b) {
+  constexpr uint32_t kLo = 0x05040100u;   // (a.lo16, b.lo16)
+  return make_uint4(__builtin_amdgcn_perm(b.x, a.x, kLo), __builtin_amdgcn_perm(b.y, a.y, kLo),
+                    __builtin_amdgcn_perm(b.z, a.z, kLo), __builtin_amdgcn_perm(b.w, a.w, kLo));
+}
+// P_r+1 from P_r = (h_r, h_r+1) and row r+2's sums
+__device__ __forceinline__ uint4 blur_pair_next(uint4 p, uint4 b) {
+  constexpr uint32_t kHiLo = 0x05040302u;   // (p.hi16, b.lo16)
+  return make_uint4(__builtin_amdgcn_perm(b.x, p.x, kHiLo), __builtin_amdgcn_perm(b.y, p.y, kHiLo),
+                    __builtin_amdgcn_perm(b.z, p.z, kHiLo), __builtin_amdgcn_perm(b.w, p.w, kHiLo));
+}
+// the 4 blurred bytes of output row y from P_y-3, P_y-1, P_y+1 and h_y+3
+__device__ __forceinline__ uint32_t blur_vpair4(uint4 pa, uint4 pb, uint4 pc, uint4 h3) {
+  const fushort2 ka = {18, 34}, kb = {49, 54}, kc = {49, 34};
+  auto col = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t h) __attribute__((always_inline)) {
+    uint32_t s = __builtin_amdgcn_udot2(as_u2(a), ka, 1u << 15, false);
+    s = __builtin_amdgcn_udot2(as_u2(b), kb, s, false);
+    s = __builtin_amdgcn_udot2(as_u2(c), kc, s, false);
+    return s + umul24(h, 18u);
+  };
+  const uint32_t a0 = col(pa.x, pb.x, pc.x, h3.x), a1 = col(pa.y, pb.y, pc.y, h3.y);
+  const uint32_t a2 = col(pa.z, pb.z, pc.z, h3.z), a3 = col(pa.w, pb.w, pc.w, h3.w);
+  const uint32_t p01 = __builtin_amdgcn_perm(a1, a0, 0x0c0c0602u);   // a0.b2 | a1.b2 << 8
+  const uint32_t p23 = __builtin_amdgcn_perm(a3, a2, 0x06020c0cu);   // a2.b2 << 16 | a3.b2 << 24
+  return p01 | p23;
+}
+
 // vertical 7-tap of one packed word (2 columns) of the ring h[0..6]: rows v
 // and 6-v paired into u16x2 (v_perm) and summed with v_dot2_u32_u16
 __device__ __forceinline__ void blur_v2(uint32_t h0, uint32_t h1, uint32_t h2, uint32_t h3,
@@ -602,6 +658,22 @@ __device__ __forceinline__ void pyr_blur_rows(const LevelGeom& L, const uint8_t*
     const uint32_t* col = reinterpret_cast<const uint32_t*>(fp + L.pyr_off);
     const uint32_t c0 = (uint32_t)((kContent0 - 4) / 4 + gq);
     const uint32_t pw = (uint32_t)L.pitch >> 2;
+#if ORBPL_BLUR_VPAIR
+    // P[k] = P_y-3+k (rows y-3+k, y-2+k) for the next output row y
+    uint4 P[5];
+    {
+      uint4 hp;
+#pragma unroll
+      for (int v = 0; v < 6; v++) {
+        const uint32_t q = umul24((uint32_t)(ra - 3 + v + kEdge), pw) + c0;
+        uint32_t a0, a1, a2;
+        ld_dw3(col, q, &a0, &a1, &a2);
+        const uint4 hv = blur_h4u(a0, a1, a2);
+        if (v > 0) P[v - 1] = blur_pair_rows(hp, hv);
+        hp = hv;
+      }
+    }
+#else
     uint2 h[7];
 #pragma unroll
     for (int v = 0; v < 6; v++) {
@@ -610,6 +682,7 @@ __device__ __forceinline__ void pyr_blur_rows(const LevelGeom& L, const uint8_t*
       ld_dw3(col, q, &a0, &a1, &a2);
       h[v + 1] = blur_h4(a0, a1, a2);
     }
+#endif
     uint8_t* out = bp + L.boff;                 // uniform; the lane's column 4 gq
     const uint32_t ocol = 4u * (uint32_t)gq;
     // kPyrDepth rows per batch, two batches: the next batch's source dwords
@@ -625,10 +698,19 @@ __device__ __forceinline__ void pyr_blur_rows(const LevelGeom& L, const uint8_t*
 #pragma unroll
       for (int j = 0; j < kPyrDepth; j++) {
         if (y + j >= rb) break;
+#if ORBPL_BLUR_VPAIR
+        const uint4 h3 = blur_h4u(w[j][0], w[j][1], w[j][2]);   // row y+j+3
+        const uint32_t o = blur_vpair4(P[0], P[2], P[4], h3);
+        const uint4 pn = blur_pair_next(P[4], h3);
+#pragma unroll
+        for (int v = 0; v < 4; v++) P[v] = P[v + 1];
+        P[4] = pn;
+#else
 #pragma unroll
         for (int v = 0; v < 6; v++) h[v] = h[v + 1];
         h[6] = blur_h4(w[j][0], w[j][1], w[j][2]);
         const uint32_t o = blur_v4(h);
+#endif
         st_b4(out, umul24((uint32_t)(y + j), (uint32_t)L.bpitch) + ocol, o);
       }
     };
