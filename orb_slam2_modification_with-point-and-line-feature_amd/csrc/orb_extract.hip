@@ -932,6 +932,15 @@ __device__ __forceinline__ int wave_incl_scan(int v);
 #ifndef ORBPL_FAST_MINW
 #define ORBPL_FAST_MINW 6
 #endif
+// neighbour pixels of the walk's row from the adjacent lanes by DPP wave
+// shifts (1 VALU each) instead of ds_bpermute with per-row lane arithmetic
+#ifndef ORBPL_FAST_DPP
+#define ORBPL_FAST_DPP 1
+#endif
+// the ring's next row loaded one row ahead of its use
+#ifndef ORBPL_FAST_PREFETCH
+#define ORBPL_FAST_PREFETCH 1
+#endif
 __global__ void __launch_bounds__(256, ORBPL_FAST_MINW) k_fast_cells(const uint8_t* __restrict__ pyr,
                                                     const OrbGeom* __restrict__ g,
                                                     const CellGeom* __restrict__ cells,
@@ -939,7 +948,9 @@ __global__ void __launch_bounds__(256, ORBPL_FAST_MINW) k_fast_cells(const uint8
                                                     int* __restrict__ cell_counts, int ini_th,
                                                     int min_th, int cell0, int cell1) {
   extern __shared__ uint32_t fast_smem[];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // the wave index as a scalar: the cell, its geometry and the window's row
+  // base are then wave-uniform (scalar loads, saddr row loads)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   int bx, f;
   xcd_block(&bx, &f);
   const int cell = cell0 + bx * 4 + wave;   // cells [cell0, cell1): one group of levels
@@ -1009,6 +1020,17 @@ __global__ void __launch_bounds__(256, ORBPL_FAST_MINW) k_fast_cells(const uint8
     // rows r-1, r-2 of the walk: packed m, 3-wide row max, centre-excluded max
     uint32_t m1 = 0, rmax1 = 0, rmax2 = 0, cmax1 = 0;
     const int nit = __builtin_amdgcn_readfirstlane(rps);   // the longest segment
+#if ORBPL_FAST_PREFETCH
+    // the next ring row's dwords are loaded one row ahead
+    uint32_t nw0 = 0, nw1 = 0, nw2 = 0;
+    auto ring_raw = [&](int row) __attribute__((always_inline)) {
+      const uint8_t* q = wrow + (umul24((uint32_t)row, pitch) + acol);
+      nw0 = *reinterpret_cast<const uint32_t*>(q);
+      nw1 = *reinterpret_cast<const uint32_t*>(q + 4);
+      nw2 = *reinterpret_cast<const uint32_t*>(q + 8);
+    };
+    if (in_seg && ra < rb) ring_raw(ra + 6);
+#endif
     for (int i = 0; i < nit; i++) {
       const int r = ra + i;
       const bool act = r < rb;
@@ -1016,7 +1038,12 @@ __global__ void __launch_bounds__(256, ORBPL_FAST_MINW) k_fast_cells(const uint8
       if (act) {
 #pragma unroll
         for (int k = 0; k < 6; k++) R[k] = R[k + 1];
+#if ORBPL_FAST_PREFETCH
+        R[6] = make_uint2(__builtin_amdgcn_alignbyte(nw1, nw0, o), __builtin_amdgcn_alignbyte(nw2, nw1, o));
+        if (r + 1 < rb) ring_raw(r + 7);
+#else
         R[6] = load_ring_row(wrow, umul24((uint32_t)(r + 6), pitch) + acol, o);
+#endif
 #if ORBPL_FAST_MM3
         const fshort2 m2 = fast_m2_mm3(R);
 #else
@@ -1026,12 +1053,19 @@ __global__ void __launch_bounds__(256, ORBPL_FAST_MINW) k_fast_cells(const uint8
         const uint32_t lo = (uint32_t)(uint16_t)m2.x;
         const uint32_t hi = has_hi ? (uint32_t)(uint16_t)m2.y : 0u;
         m = lo | (hi << 16);
-        M16[wr * pw + 3 + 2 * p] = (uint16_t)lo;   // window column x = 3 + 2p
-        M16[wr * pw + 4 + 2 * p] = (uint16_t)hi;
+        const uint32_t mo = umul24((uint32_t)wr, (uint32_t)pw) + 3 + 2 * p;
+        M16[mo] = (uint16_t)lo;   // window column x = 3 + 2p
+        M16[mo + 1] = (uint16_t)hi;
       }
       // all lanes: neighbour pixels of the same row from the adjacent lanes
+#if ORBPL_FAST_DPP
+      // DPP wave shifts (lane i <- lane i - 1 / i + 1; lane 0 / 63 read 0)
+      const uint32_t lhi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(m >> 16), 0x138, 0xf, 0xf, false);
+      const uint32_t rlo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(m & 0xFFFFu), 0x130, 0xf, 0xf, false);
+#else
       const uint32_t lhi = (uint32_t)__shfl_up((int)(m >> 16), 1, 64);
       const uint32_t rlo = (uint32_t)__shfl_down((int)(m & 0xFFFFu), 1, 64);
+#endif
       if (act) {
         const uint32_t Pl = (has_left ? lhi : 0u) | (m << 16);        // (x-1, x)
         const uint32_t Pr = (m >> 16) | ((has_right ? rlo : 0u) << 16);  // (x+1, x+2)
