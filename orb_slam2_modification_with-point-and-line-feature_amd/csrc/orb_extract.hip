@@ -927,8 +927,9 @@ __device__ __forceinline__ void nms_pair(const uint32_t* M, int ps, int r, int q
 __device__ __forceinline__ int wave_incl_scan(int v);
 
 // minimum waves per SIMD for k_fast_cells (register budget); see DESIGN.md
-// (6: the MM3 score fits 80 VGPRs without spills, 6 waves per SIMD; unbounded
-// it takes 81 and 5)
+// (6: the MM3 score fit 80 VGPRs without spills; since the DPP neighbours and
+// the scalar wave index it takes 71 = 7 waves; 8 fits 63 without spills but
+// gains nothing on the headline, profiles/r06/ab/occupancy_fast_pyr_ab.txt)
 #ifndef ORBPL_FAST_MINW
 #define ORBPL_FAST_MINW 6
 #endif
