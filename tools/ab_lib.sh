@@ -9,8 +9,12 @@ SS=${2:-256}
 RN=${3:-2}
 B="--no-cpu-baseline --no-parity --sweep 0 --secondary-steps 0 --stereo-steps 0 --rig-steps 0 --ingress-steps 0 --isolated-steps 0"
 for r in $(seq 1 $RN); do
+  # rotate the order every round: the first run of a round is ~0.6 % slow
+  # (profiles/r06/ab/trk_prio_ab.txt)
+  set -- $IT
+  k=$(( (r - 1) % $# )); ORD="${@:k+1} ${@:1:k}"
   for s in $SS; do
-    for it in $IT; do
+    for it in $ORD; do
       v=${it%%:*}; e=""; [ "$it" != "$v" ] && e=${it#*:}
       L=""; [ "$v" != cur ] && L=variants/$v/liborbpl.so
       tag=$(echo "$it" | tr ':=,/' '____')

@@ -6,8 +6,12 @@
 set -o pipefail
 mkdir -p gpurun_out/abl
 C="--no-cpu-baseline --no-parity --sweep 0 --secondary-steps 0 --stereo-steps 0 --rig-steps 0 --ingress-steps 0 --isolated-steps 0"
+IT=${1:-cur}
 for r in $(seq 1 ${2:-2}); do
-  for it in ${1:-cur}; do
+  # rotate the order every round (the first run of a round is slow)
+  set -- $IT
+  k=$(( (r - 1) % $# )); ORD="${@:k+1} ${@:1:k}"
+  for it in $ORD; do
     v=${it%%:*}; e=""; [ "$it" != "$v" ] && e=${it#*:}
     L=""; [ "$v" != cur ] && L=variants/$v/liborbpl.so
     tag=$(echo "$it" | tr ':=,/' '____')
